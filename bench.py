@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: LogisticRegression mini-batch SGD, 10M × 1K dense, bf16 features.
+
+Config (BASELINE.json north star #2; reference ``logisticregression-benchmark.json`` widened to
+1K features): maxIter/lr 0.1/tol 1e-6/reg 0, global batch 100,000 rows per GPU, synthetic
+``LabeledPointWithWeightGenerator``-shaped data (features U[0,1), labels {0,1}) generated on
+device, random-init-equivalent zero model (the reference's init).
+
+One *step* = one full SGD round of the reference (``SGD.java:246-285``): fused loss+gradient
+over the rank's 100k-row minibatch (HIP kernel), deterministic reduction, RCCL all-reduce of
+the (d+2) feedback when N > 1, device-side termination check, model update + regularisation.
+Nothing is skipped inside the timed region.
+
+Scaling is *weak*: every GPU keeps a 100k-row local batch (global batch = 100k·N) over its
+1/N shard of the 10M-row dataset. ``value`` = total samples/s over all GPUs.
+
+Launch: ``python bench.py`` (1 GPU) or
+``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N``.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--rows", type=int, default=10_000_000, help="total dataset rows (sharded over GPUs)")
+    ap.add_argument("--dim", type=int, default=1000)
+    ap.add_argument("--batch", type=int, default=100_000, help="per-GPU minibatch rows")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp64"])
+    ap.add_argument("--no-graph", action="store_true")
+    args = ap.parse_args()
+
+    from flink_ml_amd.parallel.context import init_distributed
+    from flink_ml_amd.parallel import comm
+
+    ctx = init_distributed()
+    world, rank = ctx.world_size, ctx.rank
+    if ctx.device.type != "cuda":
+        raise SystemExit("bench.py needs a GPU (torch.cuda.is_available() is False)")
+    dev = ctx.device
+
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer
+
+    dt = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp64": torch.float64}[args.dtype]
+    n_local = args.rows // world + (1 if args.rows % world > rank else 0)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + rank)
+    # synthetic LabeledPointWithWeight data, generated directly in HBM in the compute dtype
+    X = torch.empty((n_local, args.dim), dtype=dt, device=dev)
+    chunk = 1 << 20
+    for s in range(0, n_local, chunk):
+        e = min(s + chunk, n_local)
+        X[s:e] = torch.rand((e - s, args.dim), generator=gen, device=dev, dtype=torch.float32).to(dt)
+    y = torch.randint(0, 2, (n_local,), generator=gen, device=dev).to(torch.float32)
+    torch.cuda.synchronize()
+
+    total_rounds = args.warmup + args.steps + 1
+    sgd = SGD(max_iter=total_rounds, learning_rate=0.1, global_batch_size=args.batch * world, tol=1e-6)
+    import numpy as np
+
+    trainer = DeviceGlmTrainer(sgd, np.zeros(args.dim), X, y, None, "logistic", use_graph=not args.no_graph)
+
+    for _ in range(args.warmup):
+        trainer.step()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        trainer.step()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    elapsed = comm.all_reduce_scalar(elapsed, "max")
+    executed = trainer.rounds_executed()
+    if executed < args.warmup + args.steps:
+        raise SystemExit("SGD terminated early (%d rounds): timing would skip work" % executed)
+
+    ms = elapsed / args.steps * 1e3
+    samples = args.batch * world * args.steps
+    value = samples / elapsed
+    if rank == 0:
+        rec = {
+            "metric": "samples/sec (whole node), LogisticRegression 10M×1K dense",
+            "value": round(value, 1),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (device-generated U[0,1) features, Bernoulli labels; LabeledPointWithWeightGenerator shape)",
+            "config": {
+                "model": "LogisticRegression (SGD, binary logistic loss)",
+                "global_batch": args.batch * world,
+                "seq_len": None,
+                "parallelism": "dp%d" % world,
+                "rows": args.rows,
+                "dim": args.dim,
+                "per_gpu_batch": args.batch,
+                "hipgraph": not args.no_graph,
+                "hbm_gb_per_s": round(args.batch * args.dim * X.element_size() / (ms * 1e-3) / 1e9, 1),
+            },
+        }
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()

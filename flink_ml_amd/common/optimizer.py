@@ -1,0 +1,249 @@
+"""Mini-batch SGD as an SPMD round loop (reference ``LIB/common/optimizer/SGD.java:67-390``).
+
+Semantics reproduced exactly:
+* local batch = globalBatchSize / P, remainder to the low ranks (``SGD.java:206-213``);
+* round e trains on rows ``[off_e, min(off_e + B, n))`` of the rank's cached partition with
+  ``off`` advancing by B and resetting to 0 once it passes the end (``SGD.java:263-268``);
+* feedback = all-reduced [Σ mult·x | Σ weight | Σ loss] (``SGD.java:252,271-283``);
+* termination: after round e the iteration continues iff ``e+1 < maxIter`` and
+  ``Σloss/Σweight > tol`` (``TerminateOnMaxIterOrTol.java:62-68``); the final feedback is
+  applied once more when the iteration terminates (``SGD.java:288-294``) — so every computed
+  feedback is applied exactly once;
+* update: ``w -= lr/Σw · Σg`` then elastic-net regularisation, skipped when Σw = 0.
+
+MI355X execution (see ``ops/csrc/glm.hip``): the data partition stays resident in HBM, the
+round is 2 (1 GPU) or 3 + one RCCL all-reduce (N GPUs) kernel launches with all control
+state on the device, captured once into a hipGraph and replayed; the host only polls the
+device "running" flag every ``check_every`` rounds for early termination.
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..ops import glm as gk
+from ..parallel import comm
+from ..parallel.context import get_context
+from ..table import SparseColumn
+from ..utils import tracing
+
+
+def local_batch_size(global_batch: int, rank: int, world: int) -> int:
+    b = global_batch // world
+    if global_batch % world > rank:
+        b += 1
+    return b
+
+
+class SGD:
+    def __init__(self, max_iter: int = 20, learning_rate: float = 0.1, global_batch_size: int = 32,
+                 tol: float = 1e-6, reg: float = 0.0, elastic_net: float = 0.0):
+        self.max_iter = int(max_iter)
+        self.learning_rate = float(learning_rate)
+        self.global_batch_size = int(global_batch_size)
+        self.tol = float(tol)
+        self.reg = float(reg)
+        self.elastic_net = float(elastic_net)
+
+    def optimize(self, init_coef: np.ndarray, X, y: torch.Tensor, weight: Optional[torch.Tensor],
+                 loss: str) -> np.ndarray:
+        trainer = make_trainer(self, init_coef, X, y, weight, loss)
+        return trainer.fit()
+
+
+def make_trainer(sgd: SGD, init_coef, X, y, weight, loss, use_graph: Optional[bool] = None):
+    dev = X.device if isinstance(X, (torch.Tensor, SparseColumn)) else torch.device("cpu")
+    if dev.type == "cuda":
+        return DeviceGlmTrainer(sgd, init_coef, X, y, weight, loss, use_graph=use_graph)
+    return TorchGlmTrainer(sgd, init_coef, X, y, weight, loss)
+
+
+class TorchGlmTrainer:
+    """Host reference implementation (fp64), used on CPU-only hosts and by the test-suite."""
+
+    def __init__(self, sgd: SGD, init_coef, X, y, weight, loss: str):
+        ctx = get_context()
+        self.sgd = sgd
+        self.loss = gk.LOSS_CODES[loss]
+        self.sparse = isinstance(X, SparseColumn)
+        if self.sparse:
+            self.X = X
+            self.n = len(X)
+            self.d = X.size
+        else:
+            self.X = X.to(torch.float64)
+            self.n, self.d = (int(X.shape[0]), int(X.shape[1]))
+        self.y = y.to(torch.float64).reshape(-1)
+        self.w = weight.to(torch.float64).reshape(-1) if weight is not None else torch.ones(self.n, dtype=torch.float64)
+        self.coef = torch.as_tensor(np.asarray(init_coef, dtype=np.float64)).clone()
+        self.B = local_batch_size(sgd.global_batch_size, ctx.rank, ctx.world_size)
+        self.offset = 0
+        self.rounds = 0
+
+    def _batch(self):
+        s = self.offset
+        e = min(s + self.B, self.n)
+        self.offset += self.B
+        if self.offset >= self.n:
+            self.offset = 0
+        return s, e
+
+    def _feedback(self) -> torch.Tensor:
+        fb = torch.zeros(self.d + 2, dtype=torch.float64)
+        if self.n > 0:
+            s, e = self._batch()
+            if self.sparse:
+                sub = self.X
+                ip = sub.indptr[s:e + 1]
+                idx = sub.indices[ip[0]:ip[-1]].long()
+                val = sub.values[ip[0]:ip[-1]].to(torch.float64)
+                rows = torch.repeat_interleave(torch.arange(e - s), ip[1:] - ip[:-1])
+                dot = torch.zeros(e - s, dtype=torch.float64).index_add_(0, rows, val * self.coef[idx])
+                l, m = gk.torch_loss_and_mult(self.loss, dot, self.y[s:e], self.w[s:e])
+                fb[: self.d].index_add_(0, idx, m[rows] * val)
+            else:
+                xb = self.X[s:e]
+                dot = xb @ self.coef
+                l, m = gk.torch_loss_and_mult(self.loss, dot, self.y[s:e], self.w[s:e])
+                fb[: self.d] = m @ xb
+            fb[self.d] = self.w[s:e].sum()
+            fb[self.d + 1] = l.sum()
+        return comm.all_reduce_sum(fb)
+
+    def _apply(self, fb: torch.Tensor) -> None:
+        W = float(fb[self.d])
+        if W > 0:
+            self.coef -= self.sgd.learning_rate / W * fb[: self.d]
+            gk.torch_regularize(self.coef, self.sgd.reg, self.sgd.elastic_net, self.sgd.learning_rate)
+
+    def fit(self) -> np.ndarray:
+        for e in range(self.sgd.max_iter):
+            fb = self._feedback()
+            self.rounds += 1
+            self._apply(fb)
+            W, L = float(fb[self.d]), float(fb[self.d + 1])
+            crit = L / W if W != 0 else float("nan")
+            if not (e + 1 < self.sgd.max_iter and crit > self.sgd.tol):
+                break
+        return self.coef.numpy().copy()
+
+
+class DeviceGlmTrainer:
+    """HBM-resident SGD on MI355X via the fused HIP kernels (one process per GPU)."""
+
+    def __init__(self, sgd: SGD, init_coef, X, y, weight, loss: str, use_graph: Optional[bool] = None,
+                 check_every: int = 8):
+        ctx = get_context()
+        self.ctx = ctx
+        self.sgd = sgd
+        self.loss = gk.LOSS_CODES[loss]
+        self.sparse = isinstance(X, SparseColumn)
+        dev = X.device
+        self.device = dev
+        if self.sparse:
+            self.n, self.d = len(X), X.size
+            acc = torch.float64 if X.values.dtype == torch.float64 else torch.float32
+            self.indptr = X.indptr.to(device=dev, dtype=torch.int64).contiguous()
+            self.indices = X.indices.to(device=dev, dtype=torch.int32).contiguous()
+            self.values = X.values.to(device=dev, dtype=acc).contiguous()
+        else:
+            if X.dtype not in (torch.float32, torch.float64, torch.bfloat16):
+                X = X.to(torch.float32)
+            X = X.contiguous() if X.stride(-1) != 1 else X
+            self.layout = gk.pick_layout(X)
+            if self.layout is None:
+                # too wide for the register-resident path: keep the data, densify rows per round in torch
+                raise NotImplementedError("dense d=%d exceeds the register-resident GLM kernel; use a sparse column"
+                                          % X.shape[1])
+            self.X = X
+            self.n, self.d = int(X.shape[0]), int(X.shape[1])
+            acc = torch.float64 if X.dtype == torch.float64 else torch.float32
+        self.acc = acc
+        self.y = y.to(device=dev, dtype=acc).reshape(-1).contiguous()
+        self.w = weight.to(device=dev, dtype=acc).reshape(-1).contiguous() if weight is not None else None
+        self.coef = torch.as_tensor(np.asarray(init_coef, dtype=np.float64)).to(device=dev, dtype=acc).contiguous()
+        self.B = local_batch_size(sgd.global_batch_size, ctx.rank, ctx.world_size)
+        self.state = torch.zeros(8, dtype=torch.int32, device=dev)
+        self.state[1] = 1  # running[0]
+        self.feedback = torch.zeros(self.d + 2, dtype=acc, device=dev)
+        if self.sparse:
+            self.partials = None
+            self.nparts = 0
+        else:
+            self.nparts = max(1, min(512, math.ceil(max(self.B, 1) / (gk.WPB * 16))))
+            self.partials = torch.zeros((self.nparts, self.d + 2), dtype=acc, device=dev)
+        self.distributed = ctx.is_distributed
+        if use_graph is None:
+            use_graph = os.environ.get("FMLX_HIPGRAPH", "1") == "1"
+        self.use_graph = use_graph
+        self.graph = None
+        self.check_every = max(1, int(check_every))
+
+    # -- one round as a fixed launch sequence (capturable) -------------------------------------
+    def _launch_round(self) -> None:
+        s = self.sgd
+        if self.sparse:
+            self.feedback.zero_()
+            if self.n > 0:
+                gk.grad_csr(self.indptr, self.indices, self.values, self.y, self.w, self.coef, self.n, self.d, self.B,
+                            self.loss, self.state, self.feedback)
+            if self.distributed:
+                comm.all_reduce_sum(self.feedback)
+            gk.update(self.feedback, self.d, self.coef, self.state, s.max_iter, s.tol, s.learning_rate, s.reg,
+                      s.elastic_net)
+            return
+        if self.n > 0:
+            gk.grad_partials(self.X, self.y, self.w, self.coef, self.B, self.loss, self.state, self.partials,
+                             self.nparts)
+        if self.distributed:
+            gk.reduce_only(self.partials, self.nparts, self.d, self.feedback, self.state)
+            comm.all_reduce_sum(self.feedback)
+            gk.update(self.feedback, self.d, self.coef, self.state, s.max_iter, s.tol, s.learning_rate, s.reg,
+                      s.elastic_net)
+        else:
+            gk.reduce_update(self.partials, self.nparts, self.d, self.coef, self.feedback, self.state, s.max_iter,
+                             s.tol, s.learning_rate, s.reg, s.elastic_net)
+
+    def _capture(self) -> None:
+        # warm up on a side stream (required before capture), then capture one round
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        snapshot = (self.state.clone(), self.coef.clone())
+        with torch.cuda.stream(side):
+            self._launch_round()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        self.state.copy_(snapshot[0])
+        self.coef.copy_(snapshot[1])
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._launch_round()
+        self.graph = g
+
+    def step(self) -> None:
+        """Runs one SGD round (predicated on the device running flag)."""
+        if self.use_graph:
+            if self.graph is None:
+                self._capture()
+            self.graph.replay()
+        else:
+            self._launch_round()
+
+    def running(self) -> bool:
+        st = self.state.cpu()
+        e = int(st[0])
+        return bool(st[1 + (e & 1)])
+
+    def rounds_executed(self) -> int:
+        return int(self.state[4].item())
+
+    def fit(self) -> np.ndarray:
+        with tracing.range("sgd.fit"):
+            for e in range(self.sgd.max_iter):
+                self.step()
+                if (e + 1) % self.check_every == 0 and not self.running():
+                    break
+        return self.coef.to(torch.float64).cpu().numpy()

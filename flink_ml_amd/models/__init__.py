@@ -1,0 +1,4 @@
+"""Algorithm library (reference flink-ml-lib): importing this package registers every stage."""
+from . import linear  # noqa: F401
+from .linear import (LinearRegression, LinearRegressionModel, LinearSVC, LinearSVCModel,  # noqa: F401
+                     LogisticRegression, LogisticRegressionModel)

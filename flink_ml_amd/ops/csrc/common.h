@@ -1,0 +1,91 @@
+// Shared device helpers for the flink_ml_amd CDNA4 (gfx950) kernels.
+//
+// Conventions
+//  * wave64 everywhere: lane = threadIdx.x & 63, wave = threadIdx.x >> 6.
+//  * bf16 is carried as raw uint16 and widened with a shift (exact); narrowing uses the
+//    compiler's cast (v_cvt_pk_bf16_f32 keeps NaN a NaN, see MI355X_MICROARCH correctness).
+//  * Every launcher is `extern "C"` taking raw device pointers + a hipStream_t so Python
+//    (ctypes) can launch onto torch's current stream, and a stream capture (hipGraph) of a
+//    whole training round works unchanged.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define FMLX_API extern "C" __attribute__((visibility("default")))
+
+typedef uint16_t bf16_t;
+
+// dtype codes shared with Python (flink_ml_amd/ops/native.py)
+enum FmlxDType { DT_F32 = 0, DT_F64 = 1, DT_BF16 = 2, DT_F16 = 3, DT_I32 = 4, DT_I64 = 5 };
+
+__device__ __forceinline__ float bf16_to_f32(bf16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+
+__device__ __forceinline__ bf16_t f32_to_bf16(float f) {
+  // round-to-nearest-even; NaN preserved by forcing a quiet-NaN mantissa bit
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (bf16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+template <typename T> struct Ld;
+template <> struct Ld<float> {
+  static __device__ __forceinline__ float f(float v) { return v; }
+};
+template <> struct Ld<double> {
+  static __device__ __forceinline__ double f(double v) { return v; }
+};
+template <> struct Ld<bf16_t> {
+  static __device__ __forceinline__ float f(bf16_t v) { return bf16_to_f32(v); }
+};
+
+// Accumulator type per storage type: fp32 for bf16/fp32 inputs, fp64 for fp64 (parity mode).
+template <typename T> struct AccOf { typedef float type; };
+template <> struct AccOf<double> { typedef double type; };
+
+// --- wave64 reductions (butterfly over __shfl_xor lowers to DPP / ds_swizzle) ------------------
+template <typename A>
+__device__ __forceinline__ A wave_sum(A v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+template <typename A>
+__device__ __forceinline__ A wave_max(A v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) { A o = __shfl_xor(v, off, 64); v = o > v ? o : v; }
+  return v;
+}
+template <typename A>
+__device__ __forceinline__ A wave_min(A v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) { A o = __shfl_xor(v, off, 64); v = o < v ? o : v; }
+  return v;
+}
+
+// Vector chunk of EPC elements of T loaded with one instruction (EPC*sizeof(T) in {2,4,8,16}).
+template <typename T, int EPC>
+struct Chunk {
+  T v[EPC];
+};
+
+template <typename T, int EPC>
+__device__ __forceinline__ void load_chunk(const T* __restrict__ p, Chunk<T, EPC>& c) {
+  constexpr int BYTES = EPC * (int)sizeof(T);
+  if constexpr (BYTES == 16) {
+    *reinterpret_cast<uint4*>(c.v) = *reinterpret_cast<const uint4*>(p);
+  } else if constexpr (BYTES == 8) {
+    *reinterpret_cast<uint2*>(c.v) = *reinterpret_cast<const uint2*>(p);
+  } else if constexpr (BYTES == 4) {
+    *reinterpret_cast<uint32_t*>(c.v) = *reinterpret_cast<const uint32_t*>(p);
+  } else {
+#pragma unroll
+    for (int i = 0; i < EPC; ++i) c.v[i] = p[i];
+  }
+}
+
+static inline int fmlx_ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+
+#define FMLX_CHECK_LAUNCH() return (int)hipGetLastError()

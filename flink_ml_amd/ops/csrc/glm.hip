@@ -1,0 +1,591 @@
+// Fused generalized-linear-model kernels for SGD training and prediction (SURVEY §2.1 K4–K7).
+//
+// Reference hot loop (per row, fp64, Java): LIB/common/optimizer/SGD.java:275-279 calling
+// LIB/common/lossfunc/{BinaryLogisticLoss,HingeLoss,LeastSquareLoss}.java — dot(x, w), loss,
+// then axpy(mult, x, grad). Update + regularisation: SGD.java:231-243 and
+// RegularizationUtils.java:47-91.
+//
+// MI355X design
+//  * glm_grad_partials: ONE pass over the minibatch rows in HBM. A wave owns a row at a
+//    time (two rows in flight for ILP when registers allow); each lane owns a fixed set of
+//    EPC-element chunks (16-byte loads), so the coefficient slice AND the gradient
+//    accumulator for those columns live in that lane's registers for the whole kernel: the
+//    row is read exactly once, dot → wave butterfly → loss/multiplier → axpy, no LDS, no
+//    atomics. Waves of a block combine by a fixed-order LDS tree, each block writes one
+//    partial row [grad(d) | Σweight | Σloss] → deterministic, bit-reproducible.
+//  * glm_reduce_update (1 GPU): sums the block partials per 64-column tile in a fixed
+//    order, evaluates TerminateOnMaxIterOrTol on device, applies w -= lr/Σw·g plus
+//    elastic-net regularisation, and advances the device-resident round state. No host
+//    synchronisation per round: the whole round is capturable in a hipGraph.
+//  * glm_reduce (N GPUs) → RCCL all-reduce of the (d+2) feedback → glm_update.
+//  * Device round state (int32[8]): [0] round e, [1..2] running flag ping-pong
+//    (running[e&1] gates round e), [3] arrival ticket, [4] rounds executed.
+//    The batch of round e is rows [(e mod P)·B, min(+B, n)), P = ceil(n/B): exactly the
+//    reference's sequential slicing with reset-to-0 (SGD.java:263-268).
+#include "common.h"
+
+namespace {
+
+enum { LOSS_LOGISTIC = 0, LOSS_HINGE = 1, LOSS_LSQ = 2 };
+enum { ST_ROUND = 0, ST_RUN0 = 1, ST_ARRIVE = 3, ST_EXECUTED = 4 };
+
+template <typename A>
+__device__ __forceinline__ void loss_and_mult(int loss, A dot, A y, A wt, A& l, A& m) {
+  if (loss == LOSS_LOGISTIC) {
+    A ys = (A)2 * y - (A)1;
+    A z = -dot * ys;
+    // wt*log(1+exp(z)), stable softplus
+    A sp = z > (A)0 ? z + log1p(exp(-z)) : log1p(exp(z));
+    l = wt * sp;
+    m = wt * (-ys / (exp(dot * ys) + (A)1));
+  } else if (loss == LOSS_HINGE) {
+    A ys = (A)2 * y - (A)1;
+    A h = (A)1 - ys * dot;
+    if (h > (A)0) { l = wt * h; m = -ys * wt; } else { l = (A)0; m = (A)0; }
+  } else {
+    A r = dot - y;
+    l = wt * (A)0.5 * r * r;
+    m = r * wt;
+  }
+}
+
+__device__ __forceinline__ bool round_running(const int* st, int& e) {
+  e = st[ST_ROUND];
+  return st[ST_RUN0 + (e & 1)] != 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// K4/K5/K6 — fused minibatch loss + gradient partials
+// ------------------------------------------------------------------------------------------
+template <typename T, int EPC, int CPL, int U, int WPB>
+__global__ __launch_bounds__(WPB * 64) void glm_grad_partials_kernel(
+    const T* __restrict__ X, long ld, const typename AccOf<T>::type* __restrict__ y,
+    const typename AccOf<T>::type* __restrict__ wt, const typename AccOf<T>::type* __restrict__ coef,
+    long n, int d, long B, int loss, const int* __restrict__ state,
+    typename AccOf<T>::type* __restrict__ partials) {
+  typedef typename AccOf<T>::type A;
+  int e;
+  if (!round_running(state, e)) return;
+  const long P = (n + B - 1) / B;
+  const long start = (long)(e % P) * B;
+  const long end = start + B < n ? start + B : n;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nch = d / EPC;
+  const long W = (long)gridDim.x * WPB;
+  const long gw = (long)blockIdx.x * WPB + wave;
+
+  A w[CPL][EPC];
+  A acc[CPL][EPC];
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) {
+    const int c = lane + 64 * k;
+#pragma unroll
+    for (int i = 0; i < EPC; ++i) {
+      w[k][i] = c < nch ? coef[c * EPC + i] : (A)0;
+      acc[k][i] = (A)0;
+    }
+  }
+  A wsum = 0, lsum = 0;
+
+  for (long r = start + gw; r < end; r += U * W) {
+    Chunk<T, EPC> xa[U][CPL];
+    bool valid[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long ru = r + u * W;
+      valid[u] = ru < end;
+      const T* row = X + ru * ld;
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const int c = lane + 64 * k;
+        if (valid[u] && c < nch) {
+          load_chunk<T, EPC>(row + c * EPC, xa[u][k]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < EPC; ++i) xa[u][k].v[i] = (T)0;
+        }
+      }
+    }
+    A dot[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      A s = 0;
+#pragma unroll
+      for (int k = 0; k < CPL; ++k)
+#pragma unroll
+        for (int i = 0; i < EPC; ++i) s += (A)Ld<T>::f(xa[u][k].v[i]) * w[k][i];
+      dot[u] = s;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) dot[u] = wave_sum(dot[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!valid[u]) continue;
+      const long ru = r + u * W;
+      const A yy = y[ru];
+      const A ww = wt ? wt[ru] : (A)1;
+      A l, m;
+      loss_and_mult<A>(loss, dot[u], yy, ww, l, m);
+      wsum += ww;
+      lsum += l;
+#pragma unroll
+      for (int k = 0; k < CPL; ++k)
+#pragma unroll
+        for (int i = 0; i < EPC; ++i) acc[k][i] += m * (A)Ld<T>::f(xa[u][k].v[i]);
+    }
+  }
+
+  // fixed-order tree across the block's waves through LDS
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  A* buf = reinterpret_cast<A*>(smem_raw);         // [WPB/2][d]
+  A* lw = buf + (WPB / 2) * (long)d;                // [WPB][2]
+  if (lane == 0) { lw[wave * 2] = wsum; lw[wave * 2 + 1] = lsum; }
+#pragma unroll
+  for (int half = WPB / 2; half >= 1; half >>= 1) {
+    if (wave >= half && wave < 2 * half) {
+      A* dst = buf + (long)(wave - half) * d;
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const int c = lane + 64 * k;
+        if (c < nch)
+#pragma unroll
+          for (int i = 0; i < EPC; ++i) dst[c * EPC + i] = acc[k][i];
+      }
+    }
+    __syncthreads();
+    if (wave < half) {
+      const A* src = buf + (long)wave * d;
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const int c = lane + 64 * k;
+        if (c < nch)
+#pragma unroll
+          for (int i = 0; i < EPC; ++i) acc[k][i] += src[c * EPC + i];
+      }
+    }
+    __syncthreads();
+  }
+  if (wave == 0) {
+    A* out = partials + (long)blockIdx.x * (d + 2);
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      const int c = lane + 64 * k;
+      if (c < nch)
+#pragma unroll
+        for (int i = 0; i < EPC; ++i) out[c * EPC + i] = acc[k][i];
+    }
+    if (lane == 0) {
+      A ws = 0, ls = 0;
+      for (int q = 0; q < WPB; ++q) { ws += lw[q * 2]; ls += lw[q * 2 + 1]; }
+      out[d] = ws;
+      out[d + 1] = ls;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// fixed-order reduction of the block partials for one 64-column tile (+ the 2 scalar cols)
+// ------------------------------------------------------------------------------------------
+template <typename A>
+__device__ __forceinline__ void reduce_tile(const A* __restrict__ partials, int nparts, int d, int col,
+                                            A& g, A& W, A& L, A* sm /*[16][66]*/) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  const long stride = d + 2;
+  A s = 0, sw = 0, sl = 0;
+  for (int p = wave; p < nparts; p += nw) {
+    const A* row = partials + (long)p * stride;
+    if (col < d) s += row[col];
+    if (lane == 0) { sw += row[d]; sl += row[d + 1]; }
+  }
+  sm[wave * 66 + lane] = s;
+  if (lane == 0) { sm[wave * 66 + 64] = sw; sm[wave * 66 + 65] = sl; }
+  __syncthreads();
+  if (wave == 0) {
+    A a = 0, b = 0, c = 0;
+    for (int q = 0; q < nw; ++q) {
+      a += sm[q * 66 + lane];
+      b += sm[q * 66 + 64];
+      c += sm[q * 66 + 65];
+    }
+    g = a; W = b; L = c;
+  }
+}
+
+// apply the SGD step + elastic-net regularisation to one coefficient (SGD.java:231-243,
+// RegularizationUtils.java:47-91). The reg loss only feeds the discarded totalLoss slot in the
+// reference, so it is not materialised here.
+template <typename A>
+__device__ __forceinline__ A sgd_apply(A w, A g, A W, A lr, A reg, A en) {
+  if (!(W > (A)0)) return w;
+  w = w - lr / W * g;
+  if (reg == (A)0) return w;
+  if (en == (A)0) return w * ((A)1 - lr * reg);
+  A sg = w > (A)0 ? (A)1 : (w < (A)0 ? (A)-1 : (A)0);
+  if (en == (A)1) return w - lr * en * reg * sg;
+  return w - lr * (en * reg * sg + ((A)1 - en) * reg * w);
+}
+
+// last-arriving block advances the round state (Guideline 16 counter form).
+__device__ __forceinline__ void arrive_and_advance(int* state, int e, bool cont, int executed_inc) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int t = __hip_atomic_fetch_add(&state[ST_ARRIVE], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == (int)gridDim.x - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      state[ST_RUN0 + ((e + 1) & 1)] = cont ? 1 : 0;
+      state[ST_EXECUTED] += executed_inc;
+      state[ST_ROUND] = e + 1;
+      state[ST_ARRIVE] = 0;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    }
+  }
+}
+
+template <typename A>
+__global__ __launch_bounds__(1024) void glm_reduce_update_kernel(
+    const A* __restrict__ partials, int nparts, int d, A* __restrict__ coef, A* __restrict__ feedback,
+    int* __restrict__ state, int max_iter, A tol, A lr, A reg, A en) {
+  __shared__ A sm[16 * 66];
+  __shared__ A bc[3];
+  int e;
+  const bool run = round_running(state, e);
+  if (!run) {
+    arrive_and_advance(state, e, false, 0);
+    return;
+  }
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  A g = 0, W = 0, L = 0;
+  reduce_tile<A>(partials, nparts, d, col, g, W, L, sm);
+  if (threadIdx.x < 64) {
+    if (threadIdx.x == 0) { bc[0] = W; bc[1] = L; }
+  }
+  __syncthreads();
+  W = bc[0];
+  L = bc[1];
+  const bool cont = (e + 1 < max_iter) && (L / W > tol);
+  if (threadIdx.x < 64 && col < d) {
+    coef[col] = sgd_apply<A>(coef[col], g, W, lr, reg, en);
+    if (feedback) feedback[col] = g;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && feedback) { feedback[d] = W; feedback[d + 1] = L; }
+  arrive_and_advance(state, e, cont, 1);
+}
+
+template <typename A>
+__global__ __launch_bounds__(1024) void glm_reduce_kernel(const A* __restrict__ partials, int nparts, int d,
+                                                          A* __restrict__ feedback, const int* __restrict__ state) {
+  __shared__ A sm[16 * 66];
+  int e;
+  if (!round_running(state, e)) return;
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  A g = 0, W = 0, L = 0;
+  reduce_tile<A>(partials, nparts, d, col, g, W, L, sm);
+  if (threadIdx.x < 64) {
+    if (col < d) feedback[col] = g;
+    if (blockIdx.x == 0 && threadIdx.x == 0) { feedback[d] = W; feedback[d + 1] = L; }
+  }
+}
+
+template <typename A>
+__global__ __launch_bounds__(256) void glm_update_kernel(const A* __restrict__ feedback, int d, A* __restrict__ coef,
+                                                         int* __restrict__ state, int max_iter, A tol, A lr, A reg,
+                                                         A en) {
+  int e;
+  const bool run = round_running(state, e);
+  if (!run) {
+    arrive_and_advance(state, e, false, 0);
+    return;
+  }
+  const A W = feedback[d];
+  const A L = feedback[d + 1];
+  const bool cont = (e + 1 < max_iter) && (L / W > tol);
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < d; c += gridDim.x * blockDim.x)
+    coef[c] = sgd_apply<A>(coef[c], feedback[c], W, lr, reg, en);
+  arrive_and_advance(state, e, cont, 1);
+}
+
+// ------------------------------------------------------------------------------------------
+// prediction: dot + model-specific epilogue (LogisticRegressionModel.java:165-169,
+// LinearSVCModel.java:170-174, LinearRegressionModel.java:158-160)
+// mode 0: LR   pred = dot>=0, raw = [1-p, p], p = 1-1/(1+e^dot)
+// mode 1: SVC  pred = dot>=thr, raw = [dot, -dot]
+// mode 2: LinReg pred = dot (raw unused)
+// ------------------------------------------------------------------------------------------
+template <typename T, int EPC, int CPL>
+__global__ __launch_bounds__(256) void glm_predict_kernel(const T* __restrict__ X, long ld, long n, int d,
+                                                          const typename AccOf<T>::type* __restrict__ coef, int mode,
+                                                          double thr, double* __restrict__ pred,
+                                                          double* __restrict__ raw) {
+  typedef typename AccOf<T>::type A;
+  const int lane = threadIdx.x & 63;
+  const long gw = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long W = ((long)gridDim.x * blockDim.x) >> 6;
+  const int nch = d / EPC;
+  A w[CPL][EPC];
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) {
+    const int c = lane + 64 * k;
+#pragma unroll
+    for (int i = 0; i < EPC; ++i) w[k][i] = c < nch ? coef[c * EPC + i] : (A)0;
+  }
+  for (long r = gw; r < n; r += W) {
+    const T* row = X + r * ld;
+    A s = 0;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      const int c = lane + 64 * k;
+      if (c < nch) {
+        Chunk<T, EPC> x;
+        load_chunk<T, EPC>(row + c * EPC, x);
+#pragma unroll
+        for (int i = 0; i < EPC; ++i) s += (A)Ld<T>::f(x.v[i]) * w[k][i];
+      }
+    }
+    s = wave_sum(s);
+    if (lane == 0) {
+      const double dot = (double)s;
+      if (mode == 0) {
+        const double p = 1.0 - 1.0 / (1.0 + exp(dot));
+        pred[r] = dot >= 0 ? 1.0 : 0.0;
+        raw[2 * r] = 1.0 - p;
+        raw[2 * r + 1] = p;
+      } else if (mode == 1) {
+        pred[r] = dot >= thr ? 1.0 : 0.0;
+        raw[2 * r] = dot;
+        raw[2 * r + 1] = -dot;
+      } else {
+        pred[r] = dot;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// CSR (sparse features) gradient — a wave per row, gather dot, atomic scatter of mult·x into
+// a dense gradient (K5 sparse path, for the 1M-feature LinearSVC config).
+// ------------------------------------------------------------------------------------------
+template <typename A>
+__global__ __launch_bounds__(256) void glm_grad_csr_kernel(const long* __restrict__ indptr, const int* __restrict__ idx,
+                                                           const A* __restrict__ val, const A* __restrict__ y,
+                                                           const A* __restrict__ wt, const A* __restrict__ coef, long n,
+                                                           int d, long B, int loss, const int* __restrict__ state,
+                                                           A* __restrict__ grad /* d+2, zeroed */) {
+  int e;
+  if (!round_running(state, e)) return;
+  const long P = (n + B - 1) / B;
+  const long start = (long)(e % P) * B;
+  const long end = start + B < n ? start + B : n;
+  const int lane = threadIdx.x & 63;
+  const long gw = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long W = ((long)gridDim.x * blockDim.x) >> 6;
+  A wsum = 0, lsum = 0;
+  for (long r = start + gw; r < end; r += W) {
+    const long s0 = indptr[r], s1 = indptr[r + 1];
+    A s = 0;
+    for (long j = s0 + lane; j < s1; j += 64) s += val[j] * coef[idx[j]];
+    s = wave_sum(s);
+    const A yy = y[r];
+    const A ww = wt ? wt[r] : (A)1;
+    A l, m;
+    loss_and_mult<A>(loss, s, yy, ww, l, m);
+    wsum += ww;
+    lsum += l;
+    if (m != (A)0)
+      for (long j = s0 + lane; j < s1; j += 64) atomicAdd(&grad[idx[j]], m * val[j]);
+  }
+  if (lane == 0) {
+    atomicAdd(&grad[d], wsum);
+    atomicAdd(&grad[d + 1], lsum);
+  }
+}
+
+template <typename A>
+__global__ void glm_csr_predict_kernel(const long* __restrict__ indptr, const int* __restrict__ idx,
+                                       const A* __restrict__ val, const A* __restrict__ coef, long n,
+                                       double* __restrict__ dots) {
+  const int lane = threadIdx.x & 63;
+  const long gw = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long W = ((long)gridDim.x * blockDim.x) >> 6;
+  for (long r = gw; r < n; r += W) {
+    A s = 0;
+    for (long j = indptr[r] + lane; j < indptr[r + 1]; j += 64) s += val[j] * coef[idx[j]];
+    s = wave_sum(s);
+    if (lane == 0) dots[r] = (double)s;
+  }
+}
+
+// ---------------------------- host-side dispatch ------------------------------------------
+constexpr int WPB = 8;
+
+template <typename T, int EPC, int CPL>
+int launch_grad(const void* X, long ld, const void* y, const void* wt, const void* coef, long n, int d, long B,
+                int loss, const int* state, void* partials, int nblocks, hipStream_t s) {
+  typedef typename AccOf<T>::type A;
+  constexpr int U = (CPL * EPC <= 16) ? 2 : 1;
+  size_t shmem = (size_t)(WPB / 2) * d * sizeof(A) + WPB * 2 * sizeof(A);
+  hipLaunchKernelGGL((glm_grad_partials_kernel<T, EPC, CPL, U, WPB>), dim3(nblocks), dim3(WPB * 64), shmem, s,
+                     (const T*)X, ld, (const A*)y, (const A*)wt, (const A*)coef, n, d, B, loss, state, (A*)partials);
+  return (int)hipGetLastError();
+}
+
+template <typename T, int EPC>
+int launch_grad_cpl(int cpl, const void* X, long ld, const void* y, const void* wt, const void* coef, long n, int d,
+                    long B, int loss, const int* state, void* partials, int nblocks, hipStream_t s) {
+  switch (cpl) {
+    case 1: return launch_grad<T, EPC, 1>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    case 2: return launch_grad<T, EPC, 2>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    case 4: return launch_grad<T, EPC, 4>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    case 8: return launch_grad<T, EPC, 8>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+  }
+  return -1;
+}
+
+template <typename T, int EPC, int CPL>
+int launch_pred(const void* X, long ld, long n, int d, const void* coef, int mode, double thr, double* pred,
+                double* raw, hipStream_t s) {
+  long waves = n;
+  int blocks = (int)((waves + 3) / 4);
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL((glm_predict_kernel<T, EPC, CPL>), dim3(blocks), dim3(256), 0, s, (const T*)X, ld, n, d,
+                     (const typename AccOf<T>::type*)coef, mode, thr, pred, raw);
+  return (int)hipGetLastError();
+}
+
+template <typename T, int EPC>
+int launch_pred_cpl(int cpl, const void* X, long ld, long n, int d, const void* coef, int mode, double thr,
+                    double* pred, double* raw, hipStream_t s) {
+  switch (cpl) {
+    case 1: return launch_pred<T, EPC, 1>(X, ld, n, d, coef, mode, thr, pred, raw, s);
+    case 2: return launch_pred<T, EPC, 2>(X, ld, n, d, coef, mode, thr, pred, raw, s);
+    case 4: return launch_pred<T, EPC, 4>(X, ld, n, d, coef, mode, thr, pred, raw, s);
+    case 8: return launch_pred<T, EPC, 8>(X, ld, n, d, coef, mode, thr, pred, raw, s);
+  }
+  return -1;
+}
+
+}  // namespace
+
+// epc = elements per 16/8/4/2-byte chunk chosen by the host so that d % epc == 0 and rows are
+// aligned; cpl = chunks per lane (power of two, 64*cpl*epc >= d).
+FMLX_API int fmlx_glm_grad_partials(int dtype, int epc, int cpl, const void* X, long ld, const void* y, const void* wt,
+                                    const void* coef, long n, int d, long B, int loss, const int* state,
+                                    void* partials, int nblocks, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == DT_BF16) {
+    if (epc == 8) return launch_grad_cpl<bf16_t, 8>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    if (epc == 4) return launch_grad_cpl<bf16_t, 4>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    if (epc == 2) return launch_grad_cpl<bf16_t, 2>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    if (epc == 1) return launch_grad_cpl<bf16_t, 1>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+  } else if (dtype == DT_F32) {
+    if (epc == 4) return launch_grad_cpl<float, 4>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    if (epc == 2) return launch_grad_cpl<float, 2>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    if (epc == 1) return launch_grad_cpl<float, 1>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+  } else if (dtype == DT_F64) {
+    if (epc == 2) return launch_grad_cpl<double, 2>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    if (epc == 1) return launch_grad_cpl<double, 1>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+  }
+  return -1;
+}
+
+FMLX_API int fmlx_glm_reduce_update(int acc_f64, const void* partials, int nparts, int d, void* coef, void* feedback,
+                                    int* state, int max_iter, double tol, double lr, double reg, double en,
+                                    void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int blocks = (d + 63) / 64;
+  int threads = nparts >= 16 ? 1024 : 64 * (nparts < 1 ? 1 : nparts);
+  if (acc_f64)
+    hipLaunchKernelGGL(glm_reduce_update_kernel<double>, dim3(blocks), dim3(threads), 0, s, (const double*)partials,
+                       nparts, d, (double*)coef, (double*)feedback, state, max_iter, tol, lr, reg, en);
+  else
+    hipLaunchKernelGGL(glm_reduce_update_kernel<float>, dim3(blocks), dim3(threads), 0, s, (const float*)partials,
+                       nparts, d, (float*)coef, (float*)feedback, state, max_iter, (float)tol, (float)lr, (float)reg,
+                       (float)en);
+  return (int)hipGetLastError();
+}
+
+FMLX_API int fmlx_glm_reduce(int acc_f64, const void* partials, int nparts, int d, void* feedback, const int* state,
+                             void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int blocks = (d + 63) / 64;
+  int threads = nparts >= 16 ? 1024 : 64 * (nparts < 1 ? 1 : nparts);
+  if (acc_f64)
+    hipLaunchKernelGGL(glm_reduce_kernel<double>, dim3(blocks), dim3(threads), 0, s, (const double*)partials, nparts,
+                       d, (double*)feedback, state);
+  else
+    hipLaunchKernelGGL(glm_reduce_kernel<float>, dim3(blocks), dim3(threads), 0, s, (const float*)partials, nparts, d,
+                       (float*)feedback, state);
+  return (int)hipGetLastError();
+}
+
+FMLX_API int fmlx_glm_update(int acc_f64, const void* feedback, int d, void* coef, int* state, int max_iter,
+                             double tol, double lr, double reg, double en, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int blocks = (d + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  if (acc_f64)
+    hipLaunchKernelGGL(glm_update_kernel<double>, dim3(blocks), dim3(256), 0, s, (const double*)feedback, d,
+                       (double*)coef, state, max_iter, tol, lr, reg, en);
+  else
+    hipLaunchKernelGGL(glm_update_kernel<float>, dim3(blocks), dim3(256), 0, s, (const float*)feedback, d,
+                       (float*)coef, state, max_iter, (float)tol, (float)lr, (float)reg, (float)en);
+  return (int)hipGetLastError();
+}
+
+FMLX_API int fmlx_glm_predict(int dtype, int epc, int cpl, const void* X, long ld, long n, int d, const void* coef,
+                              int mode, double thr, double* pred, double* raw, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) return 0;
+  if (dtype == DT_BF16) {
+    if (epc == 8) return launch_pred_cpl<bf16_t, 8>(cpl, X, ld, n, d, coef, mode, thr, pred, raw, s);
+    if (epc == 4) return launch_pred_cpl<bf16_t, 4>(cpl, X, ld, n, d, coef, mode, thr, pred, raw, s);
+    if (epc == 2) return launch_pred_cpl<bf16_t, 2>(cpl, X, ld, n, d, coef, mode, thr, pred, raw, s);
+    if (epc == 1) return launch_pred_cpl<bf16_t, 1>(cpl, X, ld, n, d, coef, mode, thr, pred, raw, s);
+  } else if (dtype == DT_F32) {
+    if (epc == 4) return launch_pred_cpl<float, 4>(cpl, X, ld, n, d, coef, mode, thr, pred, raw, s);
+    if (epc == 2) return launch_pred_cpl<float, 2>(cpl, X, ld, n, d, coef, mode, thr, pred, raw, s);
+    if (epc == 1) return launch_pred_cpl<float, 1>(cpl, X, ld, n, d, coef, mode, thr, pred, raw, s);
+  } else if (dtype == DT_F64) {
+    if (epc == 2) return launch_pred_cpl<double, 2>(cpl, X, ld, n, d, coef, mode, thr, pred, raw, s);
+    if (epc == 1) return launch_pred_cpl<double, 1>(cpl, X, ld, n, d, coef, mode, thr, pred, raw, s);
+  }
+  return -1;
+}
+
+FMLX_API int fmlx_glm_grad_csr(int acc_f64, const long* indptr, const int* idx, const void* val, const void* y,
+                               const void* wt, const void* coef, long n, int d, long B, int loss, const int* state,
+                               void* grad, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  long waves = B < n ? B : n;
+  int blocks = (int)((waves + 3) / 4);
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  if (acc_f64)
+    hipLaunchKernelGGL(glm_grad_csr_kernel<double>, dim3(blocks), dim3(256), 0, s, indptr, idx, (const double*)val,
+                       (const double*)y, (const double*)wt, (const double*)coef, n, d, B, loss, state, (double*)grad);
+  else
+    hipLaunchKernelGGL(glm_grad_csr_kernel<float>, dim3(blocks), dim3(256), 0, s, indptr, idx, (const float*)val,
+                       (const float*)y, (const float*)wt, (const float*)coef, n, d, B, loss, state, (float*)grad);
+  return (int)hipGetLastError();
+}
+
+FMLX_API int fmlx_glm_csr_predict(int acc_f64, const long* indptr, const int* idx, const void* val, const void* coef,
+                                  long n, double* dots, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) return 0;
+  int blocks = (int)((n + 3) / 4);
+  if (blocks > 4096) blocks = 4096;
+  if (acc_f64)
+    hipLaunchKernelGGL(glm_csr_predict_kernel<double>, dim3(blocks), dim3(256), 0, s, indptr, idx, (const double*)val,
+                       (const double*)coef, n, dots);
+  else
+    hipLaunchKernelGGL(glm_csr_predict_kernel<float>, dim3(blocks), dim3(256), 0, s, indptr, idx, (const float*)val,
+                       (const float*)coef, n, dots);
+  return (int)hipGetLastError();
+}

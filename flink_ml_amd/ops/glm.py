@@ -1,0 +1,157 @@
+"""Python bindings for the GLM kernels (``csrc/glm.hip``) plus torch reference versions.
+
+The reference versions define the semantics and run on CPU (tests, parity mode); on a GPU
+the HIP launchers are used and there is no fallback.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+
+from . import native
+
+LOSS_CODES = {"logistic": 0, "hinge": 1, "leastsquare": 2}
+MAX_CPL = 8
+WPB = 8
+
+
+def pick_layout(X: torch.Tensor) -> Optional[Tuple[int, int]]:
+    """(epc, cpl) for the register-resident path, or None if d is too wide / misaligned."""
+    if X.dim() != 2:
+        return None
+    n, d = X.shape
+    es = X.element_size()
+    ld = X.stride(0)
+    if X.stride(1) != 1:
+        return None
+    base = X.data_ptr()
+    for vb in (16, 8, 4, 2):
+        epc = vb // es
+        if epc < 1:
+            continue
+        if d % epc == 0 and (ld * es) % vb == 0 and base % vb == 0:
+            break
+    else:
+        return None
+    nch = d // epc
+    cpl = 1
+    while cpl * 64 < nch:
+        cpl *= 2
+    if cpl > MAX_CPL:
+        return None
+    return epc, cpl
+
+
+def grad_partials(X, y, wt, coef, B: int, loss: int, state, partials, nblocks: int) -> None:
+    epc, cpl = pick_layout(X)
+    native.call("fmlx_glm_grad_partials", native.dtype_code(X.dtype), epc, cpl, native.ptr(X), X.stride(0),
+                native.ptr(y), native.ptr(wt), native.ptr(coef), X.shape[0], X.shape[1], B, loss,
+                native.ptr(state), native.ptr(partials), nblocks, native.stream_ptr(X.device))
+
+
+def reduce_update(partials, nparts: int, d: int, coef, feedback, state, max_iter, tol, lr, reg, en) -> None:
+    native.call("fmlx_glm_reduce_update", int(coef.dtype == torch.float64), native.ptr(partials), nparts, d,
+                native.ptr(coef), native.ptr(feedback), native.ptr(state), max_iter, tol, lr, reg, en,
+                native.stream_ptr(coef.device))
+
+
+def reduce_only(partials, nparts: int, d: int, feedback, state) -> None:
+    native.call("fmlx_glm_reduce", int(feedback.dtype == torch.float64), native.ptr(partials), nparts, d,
+                native.ptr(feedback), native.ptr(state), native.stream_ptr(feedback.device))
+
+
+def update(feedback, d: int, coef, state, max_iter, tol, lr, reg, en) -> None:
+    native.call("fmlx_glm_update", int(coef.dtype == torch.float64), native.ptr(feedback), d, native.ptr(coef),
+                native.ptr(state), max_iter, tol, lr, reg, en, native.stream_ptr(coef.device))
+
+
+def grad_csr(indptr, idx, val, y, wt, coef, n, d, B, loss, state, grad) -> None:
+    native.call("fmlx_glm_grad_csr", int(val.dtype == torch.float64), native.ptr(indptr), native.ptr(idx),
+                native.ptr(val), native.ptr(y), native.ptr(wt), native.ptr(coef), n, d, B, loss,
+                native.ptr(state), native.ptr(grad), native.stream_ptr(val.device))
+
+
+# ---------------------------------------------------------------------------------------------
+# prediction
+# ---------------------------------------------------------------------------------------------
+MODE_LR, MODE_SVC, MODE_LINREG = 0, 1, 2
+
+
+def predict_dense(X: torch.Tensor, coef: torch.Tensor, mode: int, threshold: float = 0.0):
+    """Returns (prediction[n] f64, raw[n,2] f64 or None)."""
+    n = X.shape[0]
+    if X.device.type == "cuda":
+        lay = pick_layout(X)
+        if lay is not None and X.dtype in (torch.float32, torch.float64, torch.bfloat16):
+            acc = torch.float64 if X.dtype == torch.float64 else torch.float32
+            c = coef.to(device=X.device, dtype=acc).contiguous()
+            pred = torch.empty(n, dtype=torch.float64, device=X.device)
+            raw = torch.empty((n, 2), dtype=torch.float64, device=X.device)
+            native.call("fmlx_glm_predict", native.dtype_code(X.dtype), lay[0], lay[1], native.ptr(X), X.stride(0),
+                        n, X.shape[1], native.ptr(c), mode, float(threshold), native.ptr(pred), native.ptr(raw),
+                        native.stream_ptr(X.device))
+            return pred, (raw if mode != MODE_LINREG else None)
+        dot = (X.to(torch.float64) @ coef.to(device=X.device, dtype=torch.float64))
+    else:
+        dot = X.to(torch.float64) @ coef.to(dtype=torch.float64, device=X.device)
+    return dots_to_outputs(dot, mode, threshold)
+
+
+def predict_csr(indptr, idx, val, coef, n, mode: int, threshold: float = 0.0):
+    if val.device.type == "cuda":
+        acc = torch.float64 if val.dtype == torch.float64 else torch.float32
+        c = coef.to(device=val.device, dtype=acc).contiguous()
+        dots = torch.empty(n, dtype=torch.float64, device=val.device)
+        native.call("fmlx_glm_csr_predict", int(acc == torch.float64), native.ptr(indptr), native.ptr(idx),
+                    native.ptr(val.to(acc)), native.ptr(c), n, native.ptr(dots), native.stream_ptr(val.device))
+    else:
+        counts = indptr[1:] - indptr[:-1]
+        rows = torch.repeat_interleave(torch.arange(n), counts)
+        dots = torch.zeros(n, dtype=torch.float64)
+        dots.index_add_(0, rows, val.to(torch.float64) * coef.to(torch.float64)[idx.long()])
+    return dots_to_outputs(dots, mode, threshold)
+
+
+def dots_to_outputs(dot: torch.Tensor, mode: int, threshold: float):
+    dot = dot.to(torch.float64)
+    if mode == MODE_LR:
+        p = 1.0 - 1.0 / (1.0 + torch.exp(dot))
+        return (dot >= 0).to(torch.float64), torch.stack([1.0 - p, p], dim=1)
+    if mode == MODE_SVC:
+        return (dot >= threshold).to(torch.float64), torch.stack([dot, -dot], dim=1)
+    return dot, None
+
+
+# ---------------------------------------------------------------------------------------------
+# torch reference of the per-row loss / multiplier (LIB/common/lossfunc/*.java)
+# ---------------------------------------------------------------------------------------------
+def torch_loss_and_mult(loss: int, dot, y, wt):
+    if loss == 0:
+        ys = 2 * y - 1
+        z = -dot * ys
+        l = wt * torch.nn.functional.softplus(z)
+        m = wt * (-ys / (torch.exp(dot * ys) + 1))
+    elif loss == 1:
+        ys = 2 * y - 1
+        h = 1 - ys * dot
+        pos = h > 0
+        l = torch.where(pos, wt * h, torch.zeros_like(h))
+        m = torch.where(pos, -ys * wt, torch.zeros_like(h))
+    else:
+        r = dot - y
+        l = wt * 0.5 * r * r
+        m = r * wt
+    return l, m
+
+
+def torch_regularize(coef: torch.Tensor, reg: float, en: float, lr: float) -> None:
+    if reg == 0:
+        return
+    if en == 0:
+        coef.mul_(1 - lr * reg)
+    elif en == 1:
+        coef.sub_(lr * en * reg * torch.sign(coef))
+    else:
+        coef.sub_(lr * (en * reg * torch.sign(coef) + (1 - en) * reg * coef))

@@ -1,0 +1,153 @@
+"""Loader for the in-tree native libraries (ctypes, flat C ABI).
+
+The HIP kernels are plain ``extern "C"`` launchers that take device pointers and a
+``hipStream_t``; we launch them onto torch's *current* HIP stream, so they order correctly
+with torch ops and RCCL collectives and can be captured into a hipGraph
+(``torch.cuda.CUDAGraph``) together with them.
+
+Policy: on a GPU host the native library is REQUIRED — ``kernels()`` raises if it is
+missing (no silent eager fallback). On CPU-only hosts the ops layer runs its torch reference
+implementation (same semantics, fp64), which is what the CPU test-suite exercises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must be imported first: our .so binds to torch's libamdhip64.so.7)
+
+from . import build as _build
+
+_LOCK = threading.Lock()
+_KLIB = None
+_HLIB = None
+
+DT_F32, DT_F64, DT_BF16, DT_F16, DT_I32, DT_I64 = 0, 1, 2, 3, 4, 5
+
+_TORCH2DT = {
+    torch.float32: DT_F32,
+    torch.float64: DT_F64,
+    torch.bfloat16: DT_BF16,
+    torch.float16: DT_F16,
+    torch.int32: DT_I32,
+    torch.int64: DT_I64,
+}
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_long = ctypes.c_long
+c_double = ctypes.c_double
+c_float = ctypes.c_float
+
+# name -> argtypes (restype is always int: hipError_t, 0 == success)
+_KERNEL_SIGS = {
+    # glm.hip
+    "fmlx_glm_grad_partials": [c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_long, c_int,
+                               c_long, c_int, c_void_p, c_void_p, c_int, c_void_p],
+    "fmlx_glm_reduce_update": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_double,
+                               c_double, c_double, c_double, c_void_p],
+    "fmlx_glm_reduce": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "fmlx_glm_update": [c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_double, c_double, c_double, c_double,
+                        c_void_p],
+    "fmlx_glm_predict": [c_int, c_int, c_int, c_void_p, c_long, c_long, c_int, c_void_p, c_int, c_double, c_void_p,
+                         c_void_p, c_void_p],
+    "fmlx_glm_grad_csr": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_long,
+                          c_int, c_void_p, c_void_p, c_void_p],
+    "fmlx_glm_csr_predict": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p],
+}
+
+_HOST_SIGS = {}
+
+
+def register_kernel_sigs(sigs: dict) -> None:
+    _KERNEL_SIGS.update(sigs)
+    if _KLIB is not None:
+        _apply_sigs(_KLIB, sigs)
+
+
+def register_host_sigs(sigs: dict) -> None:
+    _HOST_SIGS.update(sigs)
+    if _HLIB is not None:
+        _apply_sigs(_HLIB, sigs, restype=None)
+
+
+def _apply_sigs(lib, sigs, restype=c_int):
+    for name, spec in sigs.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        if isinstance(spec, tuple):
+            fn.argtypes, fn.restype = spec
+        else:
+            fn.argtypes = spec
+            fn.restype = restype
+
+
+def gpu_available() -> bool:
+    from ..parallel.context import get_context
+
+    return get_context().device.type == "cuda"
+
+
+def kernel_lib_path() -> str:
+    return _build.KERNEL_LIB
+
+
+def kernels():
+    """The HIP kernel library (raises if missing: never a silent fallback on GPU)."""
+    global _KLIB
+    if _KLIB is not None:
+        return _KLIB
+    with _LOCK:
+        if _KLIB is None:
+            path = _build.KERNEL_LIB
+            if not os.path.exists(path):
+                if os.environ.get("FMLX_AUTOBUILD", "1") == "1":
+                    _build.build_kernels()
+                else:
+                    raise RuntimeError("native kernel library missing: %s (run python -m flink_ml_amd.ops.build)" % path)
+            lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+            _apply_sigs(lib, _KERNEL_SIGS)
+            _KLIB = lib
+    return _KLIB
+
+
+def host():
+    """The host-side C++ runtime library (hashing, caches, sketches)."""
+    global _HLIB
+    if _HLIB is not None:
+        return _HLIB
+    with _LOCK:
+        if _HLIB is None:
+            path = _build.HOST_LIB
+            if not os.path.exists(path):
+                _build.build_host()
+            lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+            _apply_sigs(lib, _HOST_SIGS, restype=None)
+            _HLIB = lib
+    return _HLIB
+
+
+def ptr(t) -> int:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def dtype_code(dtype: torch.dtype) -> int:
+    return _TORCH2DT[dtype]
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError("HIP launch %s failed with error %d" % (what, rc))
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(kernels(), name)(*args)
+    check(rc, name)

@@ -1,0 +1,121 @@
+"""SPMD execution context: one process per GPU.
+
+Replaces Flink's JobManager/TaskManager/subtask model: every rank runs the
+same driver program over its own data partition, in lockstep; there is no dataflow graph and
+no coordinator. Rank/world come from ``torch.distributed`` (env:// rendezvous — RANK,
+WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT, as set by ``torch.distributed.run``). The
+collective backend is ``nccl`` (= RCCL on ROCm, over xGMI) when GPUs are present and ``gloo``
+on CPU-only hosts (tests).
+"""
+from __future__ import annotations
+
+import os
+import threading
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class SPMDContext:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: Optional[str] = None
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world_size > 1 and dist.is_available() and dist.is_initialized()
+
+    @property
+    def is_gpu(self) -> bool:
+        return self.device.type == "cuda"
+
+    def barrier(self) -> None:
+        if self.is_distributed:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index or 0])
+            else:
+                dist.barrier()
+
+
+_CTX: Optional[SPMDContext] = None
+_LOCK = threading.Lock()
+
+
+def _gpu_available() -> bool:
+    if os.environ.get("FMLX_DEVICE", "").lower() == "cpu":
+        return False
+    try:
+        return torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        return False
+
+
+def default_device(local_rank: int = 0) -> torch.device:
+    forced = os.environ.get("FMLX_DEVICE")
+    if forced and forced.lower() != "cpu" and forced.lower() != "cuda":
+        return torch.device(forced)
+    if _gpu_available():
+        n = torch.cuda.device_count()
+        return torch.device("cuda", local_rank % max(n, 1))
+    return torch.device("cpu")
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> SPMDContext:
+    """Initialises the process group from the environment (idempotent)."""
+    global _CTX
+    with _LOCK:
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+        device = default_device(local_rank)
+        if device.type == "cuda":
+            torch.cuda.set_device(device)
+        if world > 1 and not dist.is_initialized():
+            import datetime
+
+            if backend is None:
+                backend = "nccl" if device.type == "cuda" else "gloo"
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            kwargs = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+            if backend == "nccl":
+                kwargs["device_id"] = device
+            dist.init_process_group(**kwargs)
+        if dist.is_initialized():
+            backend = dist.get_backend()
+            world = dist.get_world_size()
+            rank = dist.get_rank()
+        _CTX = SPMDContext(rank=rank, world_size=world, local_rank=local_rank, device=device, backend=backend)
+        return _CTX
+
+
+def get_context() -> SPMDContext:
+    global _CTX
+    if _CTX is None:
+        if dist.is_available() and dist.is_initialized():
+            return init_distributed()
+        with _LOCK:
+            if _CTX is None:
+                _CTX = SPMDContext(device=default_device(0))
+    return _CTX
+
+
+def set_context(ctx: SPMDContext) -> None:
+    global _CTX
+    _CTX = ctx
+
+
+def reset_context() -> None:
+    global _CTX
+    _CTX = None
+
+
+def shutdown() -> None:
+    global _CTX
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+    _CTX = None

@@ -1,0 +1,322 @@
+"""Columnar, device-resident tables.
+
+Replaces the reference's Flink ``Table``/``DataStream<Row>``: instead of a
+stream of boxed ``Row`` objects, a ``Table`` is an ordered set of named columns, each one of
+
+* ``torch.Tensor`` of rank 1 — a numeric scalar column (double/long/int/bool),
+* ``torch.Tensor`` of rank 2 — a *dense vector* column, row i = vector i (this is the form
+  the HIP kernels consume; it stays in HBM between pipeline stages),
+* ``SparseColumn`` — a CSR batch of sparse vectors (indptr/indices/values tensors),
+* ``list`` — host objects (strings, string arrays, mixed vectors, anything else).
+
+In an SPMD job every rank holds *its own partition* of each table (the analogue of a
+Flink subtask's slice of a stream); collectives in ``flink_ml_amd.parallel`` combine them.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, Iterable, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .linalg.vectors import DenseVector, SparseVector, Vector
+
+
+class SparseColumn:
+    """CSR batch of sparse vectors of a common logical size."""
+
+    __slots__ = ("indptr", "indices", "values", "size")
+
+    def __init__(self, indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, size: int):
+        self.indptr = indptr
+        self.indices = indices
+        self.values = values
+        self.size = int(size)
+
+    def __len__(self):
+        return int(self.indptr.shape[0]) - 1
+
+    @property
+    def device(self):
+        return self.values.device
+
+    def to(self, device=None, dtype=None) -> "SparseColumn":
+        return SparseColumn(
+            self.indptr.to(device) if device is not None else self.indptr,
+            self.indices.to(device) if device is not None else self.indices,
+            self.values.to(device=device, dtype=dtype) if (device is not None or dtype is not None) else self.values,
+            self.size,
+        )
+
+    @staticmethod
+    def from_vectors(vectors: Sequence[Vector], size: int = None) -> "SparseColumn":
+        n = len(vectors)
+        if size is None:
+            size = max((v.size() for v in vectors), default=0)
+        lens = np.zeros(n + 1, dtype=np.int64)
+        idx_parts, val_parts = [], []
+        for i, v in enumerate(vectors):
+            if isinstance(v, SparseVector):
+                ii, vv = v.indices, v.values
+            else:
+                arr = v.to_array()
+                ii = np.nonzero(arr)[0].astype(np.int32)
+                vv = arr[ii]
+            lens[i + 1] = ii.shape[0]
+            idx_parts.append(ii)
+            val_parts.append(vv)
+        indptr = np.cumsum(lens)
+        indices = np.concatenate(idx_parts).astype(np.int32) if idx_parts else np.zeros(0, np.int32)
+        values = np.concatenate(val_parts).astype(np.float64) if val_parts else np.zeros(0, np.float64)
+        return SparseColumn(torch.from_numpy(indptr), torch.from_numpy(indices), torch.from_numpy(values), size)
+
+    def row(self, i: int) -> SparseVector:
+        s, e = int(self.indptr[i]), int(self.indptr[i + 1])
+        return SparseVector(self.size, self.indices[s:e].cpu().numpy(), self.values[s:e].double().cpu().numpy())
+
+    def to_dense(self, dtype=torch.float64, device=None) -> torch.Tensor:
+        n = len(self)
+        device = device if device is not None else self.values.device
+        out = torch.zeros((n, self.size), dtype=dtype, device=device)
+        if self.values.numel():
+            counts = (self.indptr[1:] - self.indptr[:-1]).to(device)
+            rows = torch.repeat_interleave(torch.arange(n, device=device), counts)
+            out[rows, self.indices.to(device).long()] = self.values.to(device=device, dtype=dtype)
+        return out
+
+    def take(self, idx: torch.Tensor) -> "SparseColumn":
+        idx = idx.cpu().long()
+        vecs = [self.row(int(i)) for i in idx]
+        return SparseColumn.from_vectors(vecs, self.size)
+
+
+Column = Any  # torch.Tensor | SparseColumn | list
+
+
+def _col_len(col) -> int:
+    if isinstance(col, torch.Tensor):
+        return int(col.shape[0])
+    return len(col)
+
+
+def compact_column(values: List[Any]) -> Column:
+    """Chooses the columnar representation for a list of row values."""
+    if len(values) == 0:
+        return values
+    first = values[0]
+    if all(isinstance(v, DenseVector) for v in values):
+        d = first.size()
+        if all(v.size() == d for v in values):
+            return torch.from_numpy(np.stack([v.values for v in values]).astype(np.float64)) if d > 0 else values
+        return list(values)
+    if all(isinstance(v, SparseVector) for v in values):
+        d = first.size()
+        if all(v.size() == d for v in values):
+            return SparseColumn.from_vectors(values, d)
+        return list(values)
+    if all(isinstance(v, (bool, np.bool_)) for v in values):
+        return torch.tensor([bool(v) for v in values], dtype=torch.bool)
+    if all(isinstance(v, (int, np.integer)) and not isinstance(v, (bool, np.bool_)) for v in values):
+        return torch.tensor([int(v) for v in values], dtype=torch.int64)
+    if all(isinstance(v, (int, float, np.integer, np.floating)) and not isinstance(v, (bool, np.bool_)) for v in values):
+        return torch.tensor([float(v) for v in values], dtype=torch.float64)
+    return list(values)
+
+
+def _row_value(col, i: int):
+    if isinstance(col, torch.Tensor):
+        if col.dim() == 2:
+            return DenseVector(col[i].double().cpu().numpy())
+        v = col[i].item()
+        return v
+    if isinstance(col, SparseColumn):
+        return col.row(i)
+    return col[i]
+
+
+class Table:
+    """An ordered mapping of column name → column (see module docstring)."""
+
+    def __init__(self, columns: Optional[Dict[str, Column]] = None, num_rows: Optional[int] = None):
+        self._cols: Dict[str, Column] = dict(columns or {})
+        if num_rows is None:
+            num_rows = _col_len(next(iter(self._cols.values()))) if self._cols else 0
+        self._n = int(num_rows)
+        for name, c in self._cols.items():
+            if _col_len(c) != self._n:
+                raise ValueError("Column %s has %d rows, expected %d" % (name, _col_len(c), self._n))
+
+    # -- construction ------------------------------------------------------------------------
+    @staticmethod
+    def from_rows(rows: Iterable[Sequence[Any]], names: Sequence[str]) -> "Table":
+        rows = [tuple(r) for r in rows]
+        cols = {}
+        for j, name in enumerate(names):
+            cols[name] = compact_column([r[j] for r in rows])
+        return Table(cols, num_rows=len(rows))
+
+    @staticmethod
+    def from_columns(**cols) -> "Table":
+        return Table(cols)
+
+    @staticmethod
+    def concat(tables: Sequence["Table"]) -> "Table":
+        tables = [t for t in tables if t is not None]
+        if not tables:
+            return Table()
+        names = tables[0].column_names
+        out = {}
+        for name in names:
+            parts = [t.column(name) for t in tables]
+            if all(isinstance(p, torch.Tensor) for p in parts) and len({(p.dim(), tuple(p.shape[1:])) for p in parts}) == 1:
+                dev = parts[0].device
+                out[name] = torch.cat([p.to(dev) for p in parts], dim=0)
+            else:
+                rows = []
+                for t in tables:
+                    rows.extend(t.get_list(name))
+                out[name] = compact_column(rows)
+        return Table(out, num_rows=sum(t.num_rows for t in tables))
+
+    # -- introspection -----------------------------------------------------------------------
+    @property
+    def column_names(self) -> List[str]:
+        return list(self._cols.keys())
+
+    def get_column_names(self) -> List[str]:
+        return self.column_names
+
+    @property
+    def num_rows(self) -> int:
+        return self._n
+
+    def __len__(self) -> int:
+        return self._n
+
+    def has_column(self, name: str) -> bool:
+        return name in self._cols
+
+    def column(self, name: str) -> Column:
+        if name not in self._cols:
+            raise KeyError("Column %s not found in table with columns %s" % (name, self.column_names))
+        return self._cols[name]
+
+    def __getitem__(self, name: str) -> Column:
+        return self.column(name)
+
+    # -- row-level access --------------------------------------------------------------------
+    def get_list(self, name: str) -> List[Any]:
+        col = self.column(name)
+        if isinstance(col, list):
+            return col
+        return [_row_value(col, i) for i in range(self._n)]
+
+    def rows(self) -> List[tuple]:
+        lists = [self.get_list(n) for n in self.column_names]
+        return [tuple(l[i] for l in lists) for i in range(self._n)]
+
+    to_rows = rows
+
+    # -- typed column accessors used by kernels ---------------------------------------------
+    def vectors_as_matrix(self, name: str, dtype=torch.float64, device=None) -> torch.Tensor:
+        """Dense [n, d] tensor for a vector column (dense, sparse or list-of-vectors)."""
+        col = self.column(name)
+        if isinstance(col, torch.Tensor):
+            if col.dim() == 1:
+                col = col.reshape(-1, 1)
+            return col.to(device=device if device is not None else col.device, dtype=dtype)
+        if isinstance(col, SparseColumn):
+            return col.to_dense(dtype=dtype, device=device)
+        if self._n == 0:
+            return torch.zeros((0, 0), dtype=dtype, device=device)
+        vecs = [v if isinstance(v, Vector) else DenseVector(v) for v in col]
+        d = max(v.size() for v in vecs)
+        arr = np.zeros((len(vecs), d), dtype=np.float64)
+        for i, v in enumerate(vecs):
+            if isinstance(v, SparseVector):
+                arr[i, v.indices] = v.values
+            else:
+                arr[i, : v.size()] = v.values
+        return torch.from_numpy(arr).to(device=device, dtype=dtype)
+
+    def scalars(self, name: str, dtype=torch.float64, device=None) -> torch.Tensor:
+        col = self.column(name)
+        if isinstance(col, torch.Tensor):
+            if col.dim() != 1:
+                raise ValueError("Column %s is not a scalar column" % name)
+            return col.to(device=device if device is not None else col.device, dtype=dtype)
+        return torch.tensor([float(v) for v in col], dtype=dtype, device=device)
+
+    def vector_size(self, name: str) -> int:
+        col = self.column(name)
+        if isinstance(col, torch.Tensor):
+            return int(col.shape[1]) if col.dim() == 2 else 1
+        if isinstance(col, SparseColumn):
+            return col.size
+        return max((v.size() for v in col), default=0)
+
+    def is_sparse(self, name: str) -> bool:
+        col = self.column(name)
+        if isinstance(col, SparseColumn):
+            return True
+        if isinstance(col, list):
+            return any(isinstance(v, SparseVector) for v in col)
+        return False
+
+    # -- transformations (all return new tables; columns are shared, not copied) -------------
+    def with_column(self, name: str, col: Column) -> "Table":
+        cols = dict(self._cols)
+        cols[name] = col
+        return Table(cols, num_rows=self._n)
+
+    def with_columns(self, mapping: Dict[str, Column]) -> "Table":
+        cols = dict(self._cols)
+        cols.update(mapping)
+        return Table(cols, num_rows=self._n)
+
+    def select(self, *names: str) -> "Table":
+        if len(names) == 1 and isinstance(names[0], (list, tuple)):
+            names = tuple(names[0])
+        return Table({n: self.column(n) for n in names}, num_rows=self._n)
+
+    def drop(self, *names: str) -> "Table":
+        return Table({k: v for k, v in self._cols.items() if k not in names}, num_rows=self._n)
+
+    def rename(self, mapping: Dict[str, str]) -> "Table":
+        return Table({mapping.get(k, k): v for k, v in self._cols.items()}, num_rows=self._n)
+
+    def take(self, idx) -> "Table":
+        if isinstance(idx, torch.Tensor) and idx.dtype == torch.bool:
+            idx = torch.nonzero(idx.cpu(), as_tuple=False).reshape(-1)
+        idx_t = torch.as_tensor(idx, dtype=torch.long).cpu()
+        cols = {}
+        for k, c in self._cols.items():
+            if isinstance(c, torch.Tensor):
+                cols[k] = c[idx_t.to(c.device)]
+            elif isinstance(c, SparseColumn):
+                cols[k] = c.take(idx_t)
+            else:
+                cols[k] = [c[int(i)] for i in idx_t]
+        return Table(cols, num_rows=int(idx_t.shape[0]))
+
+    def slice(self, start: int, end: int) -> "Table":
+        return self.take(torch.arange(start, min(end, self._n)))
+
+    def filter(self, mask) -> "Table":
+        return self.take(torch.as_tensor(mask, dtype=torch.bool))
+
+    def to(self, device) -> "Table":
+        cols = {}
+        for k, c in self._cols.items():
+            if isinstance(c, (torch.Tensor, SparseColumn)):
+                cols[k] = c.to(device)
+            else:
+                cols[k] = c
+        return Table(cols, num_rows=self._n)
+
+    def partition(self, rank: int, world: int) -> "Table":
+        """Round-robin partition, the analogue of Flink's ``rebalance()``."""
+        return self.take(torch.arange(rank, self._n, world))
+
+    def __repr__(self):
+        return "Table(rows=%d, columns=%s)" % (self._n, self.column_names)
