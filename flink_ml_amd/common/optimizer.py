@@ -174,8 +174,9 @@ class DeviceGlmTrainer:
             self.partials = None
             self.nparts = 0
         else:
-            self.nparts = max(1, min(512, math.ceil(max(self.B, 1) / (gk.WPB * 16))))
+            self.nparts = max(1, min(gk.GRAD_BLOCKS, 512, math.ceil(max(self.B, 1) / (gk.WPB * 16))))
             self.partials = torch.zeros((self.nparts, self.d + 2), dtype=acc, device=dev)
+            self.stage1 = torch.zeros((gk.stage1_rows(self.nparts), self.d + 2), dtype=acc, device=dev)
         self.distributed = ctx.is_distributed
         if use_graph is None:
             use_graph = os.environ.get("FMLX_HIPGRAPH", "1") == "1"
@@ -200,12 +201,12 @@ class DeviceGlmTrainer:
             gk.grad_partials(self.X, self.y, self.w, self.coef, self.B, self.loss, self.state, self.partials,
                              self.nparts)
         if self.distributed:
-            gk.reduce_only(self.partials, self.nparts, self.d, self.feedback, self.state)
+            gk.reduce_only(self.partials, self.nparts, self.d, self.stage1, self.feedback, self.state)
             comm.all_reduce_sum(self.feedback)
             gk.update(self.feedback, self.d, self.coef, self.state, s.max_iter, s.tol, s.learning_rate, s.reg,
                       s.elastic_net)
         else:
-            gk.reduce_update(self.partials, self.nparts, self.d, self.coef, self.feedback, self.state, s.max_iter,
+            gk.reduce_update(self.partials, self.nparts, self.d, self.stage1, self.coef, self.feedback, self.state, s.max_iter,
                              s.tol, s.learning_rate, s.reg, s.elastic_net)
 
     def _capture(self) -> None:

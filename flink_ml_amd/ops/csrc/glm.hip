@@ -71,7 +71,9 @@ __global__ __launch_bounds__(WPB * 64) void glm_grad_partials_kernel(
   const long end = start + B < n ? start + B : n;
 
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  // wave id made provably wave-uniform so row indices / label loads become scalar (SMEM, lgkmcnt)
+  // and do not serialize behind the vector row loads on vmcnt
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nch = d / EPC;
   const long W = (long)gridDim.x * WPB;
   const long gw = (long)blockIdx.x * WPB + wave;
@@ -89,25 +91,32 @@ __global__ __launch_bounds__(WPB * 64) void glm_grad_partials_kernel(
   }
   A wsum = 0, lsum = 0;
 
-  for (long r = start + gw; r < end; r += U * W) {
-    Chunk<T, EPC> xa[U][CPL];
-    bool valid[U];
+  // Software pipeline, manually unrolled by two so the compiler can keep the next batch's loads
+  // in flight with counted vmcnt waits (a loop-carried register copy would force vmcnt(0)):
+  // while batch A (U rows) is reduced and accumulated, batch B's U rows are already loading.
+  Chunk<T, EPC> xa[U][CPL], xb[U][CPL];
+  A ya[U], wa[U], yb[U], wb[U];
+  auto load_rows = [&](long r0, Chunk<T, EPC> (&dst)[U][CPL], A (&yy)[U], A (&ww)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const long ru = r + u * W;
-      valid[u] = ru < end;
+      const long ru = r0 + u * W;
+      const bool ok = ru < end;
+      yy[u] = ok ? y[ru] : (A)0;
+      ww[u] = ok ? (wt ? wt[ru] : (A)1) : (A)0;
       const T* row = X + ru * ld;
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
         const int c = lane + 64 * k;
-        if (valid[u] && c < nch) {
-          load_chunk<T, EPC>(row + c * EPC, xa[u][k]);
+        if (ok && c < nch) {
+          load_chunk<T, EPC>(row + c * EPC, dst[u][k]);
         } else {
 #pragma unroll
-          for (int i = 0; i < EPC; ++i) xa[u][k].v[i] = (T)0;
+          for (int i = 0; i < EPC; ++i) dst[u][k].v[i] = (T)0;
         }
       }
     }
+  };
+  auto process = [&](long r0, Chunk<T, EPC> (&x)[U][CPL], A (&yy)[U], A (&ww)[U]) {
     A dot[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -115,26 +124,35 @@ __global__ __launch_bounds__(WPB * 64) void glm_grad_partials_kernel(
 #pragma unroll
       for (int k = 0; k < CPL; ++k)
 #pragma unroll
-        for (int i = 0; i < EPC; ++i) s += (A)Ld<T>::f(xa[u][k].v[i]) * w[k][i];
+        for (int i = 0; i < EPC; ++i) s += (A)Ld<T>::f(x[u][k].v[i]) * w[k][i];
       dot[u] = s;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) dot[u] = wave_sum(dot[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (!valid[u]) continue;
-      const long ru = r + u * W;
-      const A yy = y[ru];
-      const A ww = wt ? wt[ru] : (A)1;
+      if (r0 + u * W >= end) continue;
       A l, m;
-      loss_and_mult<A>(loss, dot[u], yy, ww, l, m);
-      wsum += ww;
+      loss_and_mult<A>(loss, dot[u], yy[u], ww[u], l, m);
+      wsum += ww[u];
       lsum += l;
 #pragma unroll
       for (int k = 0; k < CPL; ++k)
 #pragma unroll
-        for (int i = 0; i < EPC; ++i) acc[k][i] += m * (A)Ld<T>::f(xa[u][k].v[i]);
+        for (int i = 0; i < EPC; ++i) acc[k][i] += m * (A)Ld<T>::f(x[u][k].v[i]);
     }
+  };
+  const long step = (long)U * W;
+  long r = start + gw;
+  if (r < end) load_rows(r, xa, ya, wa);
+  while (r < end) {
+    if (r + step < end) load_rows(r + step, xb, yb, wb);
+    process(r, xa, ya, wa);
+    r += step;
+    if (r >= end) break;
+    if (r + step < end) load_rows(r + step, xa, ya, wa);
+    process(r, xb, yb, wb);
+    r += step;
   }
 
   // fixed-order tree across the block's waves through LDS
@@ -186,33 +204,40 @@ __global__ __launch_bounds__(WPB * 64) void glm_grad_partials_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
-// fixed-order reduction of the block partials for one 64-column tile (+ the 2 scalar cols)
+// Deterministic two-stage reduction of the block partials [nparts][d+2]:
+//  stage 1 (many blocks): column c of row-group g = Σ_{p in group g, fixed order} partials[p][c]
+//  stage 2 (fused with the update): Σ_g stage1[g][c] in fixed order.
+// Every load in a stage is independent (fully unrolled) so each stage costs ~one memory latency.
 // ------------------------------------------------------------------------------------------
+constexpr int RED_G = 16;  // partial rows per stage-1 group
+
 template <typename A>
-__device__ __forceinline__ void reduce_tile(const A* __restrict__ partials, int nparts, int d, int col,
-                                            A& g, A& W, A& L, A* sm /*[16][66]*/) {
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int nw = blockDim.x >> 6;
+__global__ __launch_bounds__(256) void glm_reduce_stage1_kernel(const A* __restrict__ partials, int nparts, int d,
+                                                                A* __restrict__ stage1, const int* __restrict__ state) {
+  int e;
+  if (!round_running(state, e)) return;
   const long stride = d + 2;
-  A s = 0, sw = 0, sl = 0;
-  for (int p = wave; p < nparts; p += nw) {
-    const A* row = partials + (long)p * stride;
-    if (col < d) s += row[col];
-    if (lane == 0) { sw += row[d]; sl += row[d + 1]; }
-  }
-  sm[wave * 66 + lane] = s;
-  if (lane == 0) { sm[wave * 66 + 64] = sw; sm[wave * 66 + 65] = sl; }
-  __syncthreads();
-  if (wave == 0) {
-    A a = 0, b = 0, c = 0;
-    for (int q = 0; q < nw; ++q) {
-      a += sm[q * 66 + lane];
-      b += sm[q * 66 + 64];
-      c += sm[q * 66 + 65];
-    }
-    g = a; W = b; L = c;
-  }
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= stride) return;
+  const int p0 = blockIdx.y * RED_G;
+  A v[RED_G];
+#pragma unroll
+  for (int q = 0; q < RED_G; ++q) v[q] = (p0 + q < nparts) ? partials[(long)(p0 + q) * stride + c] : (A)0;
+  A s = 0;
+#pragma unroll
+  for (int q = 0; q < RED_G; ++q) s += v[q];
+  stage1[(long)blockIdx.y * stride + c] = s;
+}
+
+template <typename A>
+__device__ __forceinline__ A sum_groups(const A* __restrict__ stage1, int ngroups, long stride, long c) {
+  A v[32];
+#pragma unroll
+  for (int q = 0; q < 32; ++q) v[q] = q < ngroups ? stage1[(long)q * stride + c] : (A)0;
+  A s = 0;
+#pragma unroll
+  for (int q = 0; q < 32; ++q) s += v[q];
+  return s;
 }
 
 // apply the SGD step + elastic-net regularisation to one coefficient (SGD.java:231-243,
@@ -232,64 +257,54 @@ __device__ __forceinline__ A sgd_apply(A w, A g, A W, A lr, A reg, A en) {
 // last-arriving block advances the round state (Guideline 16 counter form).
 __device__ __forceinline__ void arrive_and_advance(int* state, int e, bool cont, int executed_inc) {
   __syncthreads();
+  // No data is handed between blocks here: every block has already consumed its read of the
+  // state words (its control flow depended on them) before its ticket add, so the last arriver
+  // may overwrite them; the next kernel sees the writes through the kernel boundary.
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int nblocks = (int)(gridDim.x * gridDim.y);
     int t = __hip_atomic_fetch_add(&state[ST_ARRIVE], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == (int)gridDim.x - 1) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (t == nblocks - 1) {
       state[ST_RUN0 + ((e + 1) & 1)] = cont ? 1 : 0;
       state[ST_EXECUTED] += executed_inc;
       state[ST_ROUND] = e + 1;
       state[ST_ARRIVE] = 0;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     }
   }
 }
 
 template <typename A>
-__global__ __launch_bounds__(1024) void glm_reduce_update_kernel(
-    const A* __restrict__ partials, int nparts, int d, A* __restrict__ coef, A* __restrict__ feedback,
+__global__ __launch_bounds__(256) void glm_reduce_update_kernel(
+    const A* __restrict__ stage1, int ngroups, int d, A* __restrict__ coef, A* __restrict__ feedback,
     int* __restrict__ state, int max_iter, A tol, A lr, A reg, A en) {
-  __shared__ A sm[16 * 66];
-  __shared__ A bc[3];
   int e;
   const bool run = round_running(state, e);
   if (!run) {
     arrive_and_advance(state, e, false, 0);
     return;
   }
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
-  A g = 0, W = 0, L = 0;
-  reduce_tile<A>(partials, nparts, d, col, g, W, L, sm);
-  if (threadIdx.x < 64) {
-    if (threadIdx.x == 0) { bc[0] = W; bc[1] = L; }
-  }
-  __syncthreads();
-  W = bc[0];
-  L = bc[1];
+  const long stride = d + 2;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  // every thread derives Σweight / Σloss itself (same fixed order → identical values)
+  const A W = sum_groups(stage1, ngroups, stride, d);
+  const A L = sum_groups(stage1, ngroups, stride, d + 1);
   const bool cont = (e + 1 < max_iter) && (L / W > tol);
-  if (threadIdx.x < 64 && col < d) {
-    coef[col] = sgd_apply<A>(coef[col], g, W, lr, reg, en);
-    if (feedback) feedback[col] = g;
+  if (c < d) {
+    const A g = sum_groups(stage1, ngroups, stride, c);
+    coef[c] = sgd_apply<A>(coef[c], g, W, lr, reg, en);
+    if (feedback) feedback[c] = g;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && feedback) { feedback[d] = W; feedback[d + 1] = L; }
+  if (feedback && blockIdx.x == 0 && threadIdx.x == 0) { feedback[d] = W; feedback[d + 1] = L; }
   arrive_and_advance(state, e, cont, 1);
 }
 
 template <typename A>
-__global__ __launch_bounds__(1024) void glm_reduce_kernel(const A* __restrict__ partials, int nparts, int d,
-                                                          A* __restrict__ feedback, const int* __restrict__ state) {
-  __shared__ A sm[16 * 66];
+__global__ __launch_bounds__(256) void glm_reduce_kernel(const A* __restrict__ stage1, int ngroups, int d,
+                                                         A* __restrict__ feedback, const int* __restrict__ state) {
   int e;
   if (!round_running(state, e)) return;
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
-  A g = 0, W = 0, L = 0;
-  reduce_tile<A>(partials, nparts, d, col, g, W, L, sm);
-  if (threadIdx.x < 64) {
-    if (col < d) feedback[col] = g;
-    if (blockIdx.x == 0 && threadIdx.x == 0) { feedback[d] = W; feedback[d + 1] = L; }
-  }
+  const long stride = d + 2;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c < stride) feedback[c] = sum_groups(stage1, ngroups, stride, c);
 }
 
 template <typename A>
@@ -423,25 +438,37 @@ __global__ void glm_csr_predict_kernel(const long* __restrict__ indptr, const in
 // ---------------------------- host-side dispatch ------------------------------------------
 constexpr int WPB = 8;
 
-template <typename T, int EPC, int CPL>
-int launch_grad(const void* X, long ld, const void* y, const void* wt, const void* coef, long n, int d, long B,
-                int loss, const int* state, void* partials, int nblocks, hipStream_t s) {
+template <typename T, int EPC, int CPL, int U>
+int launch_grad_u(const void* X, long ld, const void* y, const void* wt, const void* coef, long n, int d, long B,
+                  int loss, const int* state, void* partials, int nblocks, hipStream_t s) {
   typedef typename AccOf<T>::type A;
-  constexpr int U = (CPL * EPC <= 16) ? 2 : 1;
   size_t shmem = (size_t)(WPB / 2) * d * sizeof(A) + WPB * 2 * sizeof(A);
   hipLaunchKernelGGL((glm_grad_partials_kernel<T, EPC, CPL, U, WPB>), dim3(nblocks), dim3(WPB * 64), shmem, s,
                      (const T*)X, ld, (const A*)y, (const A*)wt, (const A*)coef, n, d, B, loss, state, (A*)partials);
   return (int)hipGetLastError();
 }
 
+// rows in flight per wave = 2·U (software pipeline); u == 0 picks the default for the shape
+template <typename T, int EPC, int CPL>
+int launch_grad(int u, const void* X, long ld, const void* y, const void* wt, const void* coef, long n, int d, long B,
+                int loss, const int* state, void* partials, int nblocks, hipStream_t s) {
+  constexpr int BYTES = CPL * EPC * (int)sizeof(T);
+  if (u == 0) u = BYTES <= 32 ? 4 : (BYTES <= 64 ? 2 : 1);
+  if (u >= 4 && BYTES <= 32)
+    return launch_grad_u<T, EPC, CPL, 4>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+  if (u >= 2 && BYTES <= 64)
+    return launch_grad_u<T, EPC, CPL, 2>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+  return launch_grad_u<T, EPC, CPL, 1>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+}
+
 template <typename T, int EPC>
-int launch_grad_cpl(int cpl, const void* X, long ld, const void* y, const void* wt, const void* coef, long n, int d,
-                    long B, int loss, const int* state, void* partials, int nblocks, hipStream_t s) {
+int launch_grad_cpl(int cpl, int u, const void* X, long ld, const void* y, const void* wt, const void* coef, long n,
+                    int d, long B, int loss, const int* state, void* partials, int nblocks, hipStream_t s) {
   switch (cpl) {
-    case 1: return launch_grad<T, EPC, 1>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-    case 2: return launch_grad<T, EPC, 2>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-    case 4: return launch_grad<T, EPC, 4>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-    case 8: return launch_grad<T, EPC, 8>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    case 1: return launch_grad<T, EPC, 1>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    case 2: return launch_grad<T, EPC, 2>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    case 4: return launch_grad<T, EPC, 4>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    case 8: return launch_grad<T, EPC, 8>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
   }
   return -1;
 }
@@ -474,52 +501,69 @@ int launch_pred_cpl(int cpl, const void* X, long ld, long n, int d, const void* 
 
 // epc = elements per 16/8/4/2-byte chunk chosen by the host so that d % epc == 0 and rows are
 // aligned; cpl = chunks per lane (power of two, 64*cpl*epc >= d).
-FMLX_API int fmlx_glm_grad_partials(int dtype, int epc, int cpl, const void* X, long ld, const void* y, const void* wt,
+FMLX_API int fmlx_glm_grad_partials(int dtype, int epc, int cpl, int u, const void* X, long ld, const void* y, const void* wt,
                                     const void* coef, long n, int d, long B, int loss, const int* state,
                                     void* partials, int nblocks, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (dtype == DT_BF16) {
-    if (epc == 8) return launch_grad_cpl<bf16_t, 8>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-    if (epc == 4) return launch_grad_cpl<bf16_t, 4>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-    if (epc == 2) return launch_grad_cpl<bf16_t, 2>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-    if (epc == 1) return launch_grad_cpl<bf16_t, 1>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    if (epc == 8) return launch_grad_cpl<bf16_t, 8>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    if (epc == 4) return launch_grad_cpl<bf16_t, 4>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    if (epc == 2) return launch_grad_cpl<bf16_t, 2>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    if (epc == 1) return launch_grad_cpl<bf16_t, 1>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
   } else if (dtype == DT_F32) {
-    if (epc == 4) return launch_grad_cpl<float, 4>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-    if (epc == 2) return launch_grad_cpl<float, 2>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-    if (epc == 1) return launch_grad_cpl<float, 1>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    if (epc == 4) return launch_grad_cpl<float, 4>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    if (epc == 2) return launch_grad_cpl<float, 2>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    if (epc == 1) return launch_grad_cpl<float, 1>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
   } else if (dtype == DT_F64) {
-    if (epc == 2) return launch_grad_cpl<double, 2>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-    if (epc == 1) return launch_grad_cpl<double, 1>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    if (epc == 2) return launch_grad_cpl<double, 2>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    if (epc == 1) return launch_grad_cpl<double, 1>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
   }
   return -1;
 }
 
-FMLX_API int fmlx_glm_reduce_update(int acc_f64, const void* partials, int nparts, int d, void* coef, void* feedback,
-                                    int* state, int max_iter, double tol, double lr, double reg, double en,
-                                    void* stream) {
+// stage1 scratch: [ceil(nparts/16)][d+2] of the accumulator type (nparts <= 512)
+template <typename A>
+static int launch_stage1(const void* partials, int nparts, int d, void* stage1, const int* state, hipStream_t s) {
+  dim3 grid((d + 2 + 255) / 256, (nparts + RED_G - 1) / RED_G);
+  hipLaunchKernelGGL(glm_reduce_stage1_kernel<A>, grid, dim3(256), 0, s, (const A*)partials, nparts, d, (A*)stage1,
+                     state);
+  return (int)hipGetLastError();
+}
+
+FMLX_API int fmlx_glm_reduce_update(int acc_f64, const void* partials, int nparts, int d, void* stage1, void* coef,
+                                    void* feedback, int* state, int max_iter, double tol, double lr, double reg,
+                                    double en, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  int blocks = (d + 63) / 64;
-  int threads = nparts >= 16 ? 1024 : 64 * (nparts < 1 ? 1 : nparts);
+  const int ngroups = (nparts + RED_G - 1) / RED_G;
+  if (ngroups > 32) return -2;
+  int rc = acc_f64 ? launch_stage1<double>(partials, nparts, d, stage1, state, s)
+                   : launch_stage1<float>(partials, nparts, d, stage1, state, s);
+  if (rc) return rc;
+  int blocks = (d + 255) / 256;
   if (acc_f64)
-    hipLaunchKernelGGL(glm_reduce_update_kernel<double>, dim3(blocks), dim3(threads), 0, s, (const double*)partials,
-                       nparts, d, (double*)coef, (double*)feedback, state, max_iter, tol, lr, reg, en);
+    hipLaunchKernelGGL(glm_reduce_update_kernel<double>, dim3(blocks), dim3(256), 0, s, (const double*)stage1,
+                       ngroups, d, (double*)coef, (double*)feedback, state, max_iter, tol, lr, reg, en);
   else
-    hipLaunchKernelGGL(glm_reduce_update_kernel<float>, dim3(blocks), dim3(threads), 0, s, (const float*)partials,
-                       nparts, d, (float*)coef, (float*)feedback, state, max_iter, (float)tol, (float)lr, (float)reg,
+    hipLaunchKernelGGL(glm_reduce_update_kernel<float>, dim3(blocks), dim3(256), 0, s, (const float*)stage1, ngroups,
+                       d, (float*)coef, (float*)feedback, state, max_iter, (float)tol, (float)lr, (float)reg,
                        (float)en);
   return (int)hipGetLastError();
 }
 
-FMLX_API int fmlx_glm_reduce(int acc_f64, const void* partials, int nparts, int d, void* feedback, const int* state,
-                             void* stream) {
+FMLX_API int fmlx_glm_reduce(int acc_f64, const void* partials, int nparts, int d, void* stage1, void* feedback,
+                             const int* state, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  int blocks = (d + 63) / 64;
-  int threads = nparts >= 16 ? 1024 : 64 * (nparts < 1 ? 1 : nparts);
+  const int ngroups = (nparts + RED_G - 1) / RED_G;
+  if (ngroups > 32) return -2;
+  int rc = acc_f64 ? launch_stage1<double>(partials, nparts, d, stage1, state, s)
+                   : launch_stage1<float>(partials, nparts, d, stage1, state, s);
+  if (rc) return rc;
+  int blocks = (d + 2 + 255) / 256;
   if (acc_f64)
-    hipLaunchKernelGGL(glm_reduce_kernel<double>, dim3(blocks), dim3(threads), 0, s, (const double*)partials, nparts,
-                       d, (double*)feedback, state);
+    hipLaunchKernelGGL(glm_reduce_kernel<double>, dim3(blocks), dim3(256), 0, s, (const double*)stage1, ngroups, d,
+                       (double*)feedback, state);
   else
-    hipLaunchKernelGGL(glm_reduce_kernel<float>, dim3(blocks), dim3(threads), 0, s, (const float*)partials, nparts, d,
+    hipLaunchKernelGGL(glm_reduce_kernel<float>, dim3(blocks), dim3(256), 0, s, (const float*)stage1, ngroups, d,
                        (float*)feedback, state);
   return (int)hipGetLastError();
 }

@@ -6,6 +6,7 @@ the HIP launchers are used and there is no fallback.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -15,6 +16,9 @@ from . import native
 LOSS_CODES = {"logistic": 0, "hinge": 1, "leastsquare": 2}
 MAX_CPL = 8
 WPB = 8
+# rows in flight per wave = 2*GRAD_UNROLL (0 = kernel default for the shape); tunable for A/B runs
+GRAD_UNROLL = int(os.environ.get("FMLX_GLM_UNROLL", "0"))
+GRAD_BLOCKS = int(os.environ.get("FMLX_GLM_BLOCKS", "256"))
 
 
 def pick_layout(X: torch.Tensor) -> Optional[Tuple[int, int]]:
@@ -46,20 +50,24 @@ def pick_layout(X: torch.Tensor) -> Optional[Tuple[int, int]]:
 
 def grad_partials(X, y, wt, coef, B: int, loss: int, state, partials, nblocks: int) -> None:
     epc, cpl = pick_layout(X)
-    native.call("fmlx_glm_grad_partials", native.dtype_code(X.dtype), epc, cpl, native.ptr(X), X.stride(0),
+    native.call("fmlx_glm_grad_partials", native.dtype_code(X.dtype), epc, cpl, GRAD_UNROLL, native.ptr(X), X.stride(0),
                 native.ptr(y), native.ptr(wt), native.ptr(coef), X.shape[0], X.shape[1], B, loss,
                 native.ptr(state), native.ptr(partials), nblocks, native.stream_ptr(X.device))
 
 
-def reduce_update(partials, nparts: int, d: int, coef, feedback, state, max_iter, tol, lr, reg, en) -> None:
+def stage1_rows(nparts: int) -> int:
+    return (nparts + 15) // 16
+
+
+def reduce_update(partials, nparts: int, d: int, stage1, coef, feedback, state, max_iter, tol, lr, reg, en) -> None:
     native.call("fmlx_glm_reduce_update", int(coef.dtype == torch.float64), native.ptr(partials), nparts, d,
-                native.ptr(coef), native.ptr(feedback), native.ptr(state), max_iter, tol, lr, reg, en,
+                native.ptr(stage1), native.ptr(coef), native.ptr(feedback), native.ptr(state), max_iter, tol, lr, reg, en,
                 native.stream_ptr(coef.device))
 
 
-def reduce_only(partials, nparts: int, d: int, feedback, state) -> None:
+def reduce_only(partials, nparts: int, d: int, stage1, feedback, state) -> None:
     native.call("fmlx_glm_reduce", int(feedback.dtype == torch.float64), native.ptr(partials), nparts, d,
-                native.ptr(feedback), native.ptr(state), native.stream_ptr(feedback.device))
+                native.ptr(stage1), native.ptr(feedback), native.ptr(state), native.stream_ptr(feedback.device))
 
 
 def update(feedback, d: int, coef, state, max_iter, tol, lr, reg, en) -> None:

@@ -43,11 +43,11 @@ c_float = ctypes.c_float
 # name -> argtypes (restype is always int: hipError_t, 0 == success)
 _KERNEL_SIGS = {
     # glm.hip
-    "fmlx_glm_grad_partials": [c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_long, c_int,
+    "fmlx_glm_grad_partials": [c_int, c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_long, c_int,
                                c_long, c_int, c_void_p, c_void_p, c_int, c_void_p],
-    "fmlx_glm_reduce_update": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_double,
-                               c_double, c_double, c_double, c_void_p],
-    "fmlx_glm_reduce": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "fmlx_glm_reduce_update": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                               c_double, c_double, c_double, c_double, c_void_p],
+    "fmlx_glm_reduce": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "fmlx_glm_update": [c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_double, c_double, c_double, c_double,
                         c_void_p],
     "fmlx_glm_predict": [c_int, c_int, c_int, c_void_p, c_long, c_long, c_int, c_void_p, c_int, c_double, c_void_p,
