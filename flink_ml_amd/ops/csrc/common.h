@@ -52,6 +52,24 @@ __device__ __forceinline__ A wave_sum(A v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
 }
+// Full wave64 sum with DPP row ops (no LDS round trips, unlike ds_bpermute-based shuffles):
+// quad xor1/xor2 → half-row mirror → row mirror → row_bcast:15 → row_bcast:31; lane 63 holds the
+// total, broadcast with v_readlane into a (wave-uniform) scalar.
+template <int CTRL, int ROW_MASK = 0xF, bool BOUND = true>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xF, BOUND));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_mov<0xB1>(v);          // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);          // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);         // row_half_mirror
+  v += dpp_mov<0x140>(v);         // row_mirror
+  v += dpp_mov<0x142, 0xA, false>(v);  // row_bcast:15 → rows 1,3
+  v += dpp_mov<0x143, 0xC, false>(v);  // row_bcast:31 → rows 2,3
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ double wave_sum_dpp(double v) { return wave_sum(v); }
+
 template <typename A>
 __device__ __forceinline__ A wave_max(A v) {
 #pragma unroll

@@ -91,32 +91,33 @@ __global__ __launch_bounds__(WPB * 64) void glm_grad_partials_kernel(
   }
   A wsum = 0, lsum = 0;
 
-  // Software pipeline, manually unrolled by two so the compiler can keep the next batch's loads
-  // in flight with counted vmcnt waits (a loop-carried register copy would force vmcnt(0)):
-  // while batch A (U rows) is reduced and accumulated, batch B's U rows are already loading.
+  // Software pipeline, manually unrolled by two so the compiler keeps the next batch's loads in
+  // flight under counted vmcnt waits (a loop-carried register copy, or a conditional load, would
+  // force vmcnt(0)). All loads are unconditional: rows past the batch end are clamped to the
+  // wave's current (just-read, L2-hot) row and masked by a zero weight; lanes past the last
+  // chunk read an in-row chunk and meet a zero coefficient / are never written back.
   Chunk<T, EPC> xa[U][CPL], xb[U][CPL];
   A ya[U], wa[U], yb[U], wb[U];
-  auto load_rows = [&](long r0, Chunk<T, EPC> (&dst)[U][CPL], A (&yy)[U], A (&ww)[U]) {
+  bool va[U], vb[U];
+  auto load_rows = [&](long r0, long rsafe, Chunk<T, EPC> (&dst)[U][CPL], A (&yy)[U], A (&ww)[U],
+                       bool (&vv)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const long ru = r0 + u * W;
-      const bool ok = ru < end;
-      yy[u] = ok ? y[ru] : (A)0;
-      ww[u] = ok ? (wt ? wt[ru] : (A)1) : (A)0;
+      const long ru0 = r0 + u * W;
+      const bool ok = ru0 < end;
+      const long ru = ok ? ru0 : rsafe;
+      vv[u] = ok;
+      yy[u] = y[ru];
+      ww[u] = wt ? wt[ru] : (A)1;
       const T* row = X + ru * ld;
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
         const int c = lane + 64 * k;
-        if (ok && c < nch) {
-          load_chunk<T, EPC>(row + c * EPC, dst[u][k]);
-        } else {
-#pragma unroll
-          for (int i = 0; i < EPC; ++i) dst[u][k].v[i] = (T)0;
-        }
+        load_chunk<T, EPC>(row + (c < nch ? c : nch - 1) * EPC, dst[u][k]);
       }
     }
   };
-  auto process = [&](long r0, Chunk<T, EPC> (&x)[U][CPL], A (&yy)[U], A (&ww)[U]) {
+  auto process = [&](Chunk<T, EPC> (&x)[U][CPL], A (&yy)[U], A (&ww)[U], bool (&vv)[U]) {
     A dot[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -128,13 +129,13 @@ __global__ __launch_bounds__(WPB * 64) void glm_grad_partials_kernel(
       dot[u] = s;
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) dot[u] = wave_sum(dot[u]);
+    for (int u = 0; u < U; ++u) dot[u] = wave_sum_dpp(dot[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (r0 + u * W >= end) continue;
       A l, m;
       loss_and_mult<A>(loss, dot[u], yy[u], ww[u], l, m);
-      wsum += ww[u];
+      if (!vv[u]) { l = (A)0; m = (A)0; }
+      wsum += vv[u] ? ww[u] : (A)0;
       lsum += l;
 #pragma unroll
       for (int k = 0; k < CPL; ++k)
@@ -144,15 +145,18 @@ __global__ __launch_bounds__(WPB * 64) void glm_grad_partials_kernel(
   };
   const long step = (long)U * W;
   long r = start + gw;
-  if (r < end) load_rows(r, xa, ya, wa);
-  while (r < end) {
-    if (r + step < end) load_rows(r + step, xb, yb, wb);
-    process(r, xa, ya, wa);
-    r += step;
-    if (r >= end) break;
-    if (r + step < end) load_rows(r + step, xa, ya, wa);
-    process(r, xb, yb, wb);
-    r += step;
+  if (r < end) {
+    load_rows(r, r, xa, ya, wa, va);
+    while (true) {
+      load_rows(r + step, r, xb, yb, wb, vb);
+      process(xa, ya, wa, va);
+      r += step;
+      if (r >= end) break;
+      load_rows(r + step, r, xa, ya, wa, va);
+      process(xb, yb, wb, vb);
+      r += step;
+      if (r >= end) break;
+    }
   }
 
   // fixed-order tree across the block's waves through LDS
