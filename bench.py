@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--batch", type=int, default=100_000, help="per-GPU minibatch rows")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp64"])
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--graph-rounds", type=int, default=10, help="SGD rounds captured per hipGraph replay")
     args = ap.parse_args()
 
     from flink_ml_amd.parallel.context import init_distributed
@@ -72,14 +73,13 @@ def main():
 
     trainer = DeviceGlmTrainer(sgd, np.zeros(args.dim), X, y, None, "logistic", use_graph=not args.no_graph)
 
-    for _ in range(args.warmup):
-        trainer.step()
+    trainer.rounds_per_graph = args.graph_rounds
+    trainer.run_rounds(args.warmup)
     torch.cuda.synchronize()
     ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        trainer.step()
+    trainer.run_rounds(args.steps)
     torch.cuda.synchronize()
     ctx.barrier()
     torch.cuda.synchronize()

@@ -181,8 +181,9 @@ class DeviceGlmTrainer:
         if use_graph is None:
             use_graph = os.environ.get("FMLX_HIPGRAPH", "1") == "1"
         self.use_graph = use_graph
-        self.graph = None
+        self.graphs = {}
         self.check_every = max(1, int(check_every))
+        self.rounds_per_graph = self.check_every
 
     # -- one round as a fixed launch sequence (capturable) -------------------------------------
     def _launch_round(self) -> None:
@@ -209,29 +210,44 @@ class DeviceGlmTrainer:
             gk.reduce_update(self.partials, self.nparts, self.d, self.stage1, self.coef, self.feedback, self.state, s.max_iter,
                              s.tol, s.learning_rate, s.reg, s.elastic_net)
 
-    def _capture(self) -> None:
-        # warm up on a side stream (required before capture), then capture one round
+    def _capture(self, rounds: int):
+        """Captures ``rounds`` consecutive SGD rounds into one hipGraph (state lives on device, so
+        the same launch sequence repeats); replaying it costs one host submission per ``rounds``."""
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         snapshot = (self.state.clone(), self.coef.clone())
         with torch.cuda.stream(side):
-            self._launch_round()
+            self._launch_round()  # warm-up outside capture (allocator / RCCL lazy init)
         torch.cuda.current_stream(self.device).wait_stream(side)
         self.state.copy_(snapshot[0])
         self.coef.copy_(snapshot[1])
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._launch_round()
-        self.graph = g
+            for _ in range(rounds):
+                self._launch_round()
+        self.graphs[rounds] = g
+        return g
+
+    def run_rounds(self, k: int) -> None:
+        """Runs ``k`` SGD rounds (each predicated on the device running flag), no host sync."""
+        if not self.use_graph:
+            for _ in range(k):
+                self._launch_round()
+            return
+        R = self.rounds_per_graph
+        full, rem = divmod(k, R)
+        if full:
+            g = self.graphs.get(R) or self._capture(R)
+            for _ in range(full):
+                g.replay()
+        if rem:
+            g1 = self.graphs.get(1) or self._capture(1)
+            for _ in range(rem):
+                g1.replay()
 
     def step(self) -> None:
         """Runs one SGD round (predicated on the device running flag)."""
-        if self.use_graph:
-            if self.graph is None:
-                self._capture()
-            self.graph.replay()
-        else:
-            self._launch_round()
+        self.run_rounds(1)
 
     def running(self) -> bool:
         st = self.state.cpu()
@@ -243,8 +259,11 @@ class DeviceGlmTrainer:
 
     def fit(self) -> np.ndarray:
         with tracing.range("sgd.fit"):
-            for e in range(self.sgd.max_iter):
-                self.step()
-                if (e + 1) % self.check_every == 0 and not self.running():
+            done = 0
+            while done < self.sgd.max_iter:
+                k = min(self.check_every, self.sgd.max_iter - done)
+                self.run_rounds(k)
+                done += k
+                if done < self.sgd.max_iter and not self.running():
                     break
         return self.coef.to(torch.float64).cpu().numpy()

@@ -2,3 +2,5 @@
 from . import linear  # noqa: F401
 from .linear import (LinearRegression, LinearRegressionModel, LinearSVC, LinearSVCModel,  # noqa: F401
                      LogisticRegression, LogisticRegressionModel)
+from . import kmeans  # noqa: F401,E402
+from .kmeans import KMeans, KMeansModel  # noqa: F401,E402

@@ -213,7 +213,7 @@ __global__ __launch_bounds__(WPB * 64) void glm_grad_partials_kernel(
 //  stage 2 (fused with the update): Σ_g stage1[g][c] in fixed order.
 // Every load in a stage is independent (fully unrolled) so each stage costs ~one memory latency.
 // ------------------------------------------------------------------------------------------
-constexpr int RED_G = 16;  // partial rows per stage-1 group
+constexpr int RED_G = 32;  // partial rows per stage-1 group (<= 512 partials -> <= 16 groups)
 
 template <typename A>
 __global__ __launch_bounds__(256) void glm_reduce_stage1_kernel(const A* __restrict__ partials, int nparts, int d,
@@ -235,12 +235,12 @@ __global__ __launch_bounds__(256) void glm_reduce_stage1_kernel(const A* __restr
 
 template <typename A>
 __device__ __forceinline__ A sum_groups(const A* __restrict__ stage1, int ngroups, long stride, long c) {
-  A v[32];
+  A v[16];
 #pragma unroll
-  for (int q = 0; q < 32; ++q) v[q] = q < ngroups ? stage1[(long)q * stride + c] : (A)0;
+  for (int q = 0; q < 16; ++q) v[q] = q < ngroups ? stage1[(long)q * stride + c] : (A)0;
   A s = 0;
 #pragma unroll
-  for (int q = 0; q < 32; ++q) s += v[q];
+  for (int q = 0; q < 16; ++q) s += v[q];
   return s;
 }
 
@@ -288,12 +288,16 @@ __global__ __launch_bounds__(256) void glm_reduce_update_kernel(
   }
   const long stride = d + 2;
   const int c = blockIdx.x * 256 + threadIdx.x;
-  // every thread derives Σweight / Σloss itself (same fixed order → identical values)
-  const A W = sum_groups(stage1, ngroups, stride, d);
-  const A L = sum_groups(stage1, ngroups, stride, d + 1);
+  // Σweight / Σloss: two lanes of wave 0 reduce them (fixed order) while every thread reduces its
+  // own column; broadcast through LDS
+  __shared__ A wl[2];
+  if (threadIdx.x < 2) wl[threadIdx.x] = sum_groups(stage1, ngroups, stride, d + threadIdx.x);
+  const A g = c < d ? sum_groups(stage1, ngroups, stride, c) : (A)0;
+  __syncthreads();
+  const A W = wl[0];
+  const A L = wl[1];
   const bool cont = (e + 1 < max_iter) && (L / W > tol);
   if (c < d) {
-    const A g = sum_groups(stage1, ngroups, stride, c);
     coef[c] = sgd_apply<A>(coef[c], g, W, lr, reg, en);
     if (feedback) feedback[c] = g;
   }
@@ -457,7 +461,7 @@ template <typename T, int EPC, int CPL>
 int launch_grad(int u, const void* X, long ld, const void* y, const void* wt, const void* coef, long n, int d, long B,
                 int loss, const int* state, void* partials, int nblocks, hipStream_t s) {
   constexpr int BYTES = CPL * EPC * (int)sizeof(T);
-  if (u == 0) u = BYTES <= 32 ? 4 : (BYTES <= 64 ? 2 : 1);
+  if (u == 0) u = BYTES <= 64 ? 2 : 1;
   if (u >= 4 && BYTES <= 32)
     return launch_grad_u<T, EPC, CPL, 4>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
   if (u >= 2 && BYTES <= 64)
@@ -539,7 +543,7 @@ FMLX_API int fmlx_glm_reduce_update(int acc_f64, const void* partials, int npart
                                     double en, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int ngroups = (nparts + RED_G - 1) / RED_G;
-  if (ngroups > 32) return -2;
+  if (ngroups > 16) return -2;
   int rc = acc_f64 ? launch_stage1<double>(partials, nparts, d, stage1, state, s)
                    : launch_stage1<float>(partials, nparts, d, stage1, state, s);
   if (rc) return rc;
@@ -558,7 +562,7 @@ FMLX_API int fmlx_glm_reduce(int acc_f64, const void* partials, int nparts, int 
                              const int* state, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int ngroups = (nparts + RED_G - 1) / RED_G;
-  if (ngroups > 32) return -2;
+  if (ngroups > 16) return -2;
   int rc = acc_f64 ? launch_stage1<double>(partials, nparts, d, stage1, state, s)
                    : launch_stage1<float>(partials, nparts, d, stage1, state, s);
   if (rc) return rc;

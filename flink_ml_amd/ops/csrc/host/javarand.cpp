@@ -1,0 +1,76 @@
+// Host-side Java-compatible random utilities (bit-exact with java.util.Random), used where the
+// reference's results depend on the JVM RNG stream (SURVEY §7.4 "RNG compatibility"):
+//   * reservoir sampling of DataStreamUtils.SamplingOperator (DataStreamUtils.java:633-704)
+//   * bulk nextDouble / nextInt / nextGaussian streams (data generators, RandomSplitter, MinHash)
+#include <cmath>
+#include <cstdint>
+
+namespace {
+struct JRandom {
+  uint64_t seed;
+  bool have_gauss = false;
+  double next_gauss = 0;
+  explicit JRandom(int64_t s) : seed(((uint64_t)s ^ 0x5DEECE66DULL) & ((1ULL << 48) - 1)) {}
+  int32_t next(int bits) {
+    seed = (seed * 0x5DEECE66DULL + 0xBULL) & ((1ULL << 48) - 1);
+    return (int32_t)(int64_t)(seed >> (48 - bits));
+  }
+  int32_t next_int(int32_t bound) {
+    int32_t r = next(31);
+    int32_t m = bound - 1;
+    if ((bound & m) == 0) return (int32_t)(((int64_t)bound * (int64_t)r) >> 31);
+    for (int32_t u = r; u - (r = u % bound) + m < 0; u = next(31)) {
+    }
+    return r;
+  }
+  double next_double() { return (double)(((int64_t)next(26) << 27) + next(27)) * (1.0 / (double)(1LL << 53)); }
+  double next_gaussian() {
+    if (have_gauss) { have_gauss = false; return next_gauss; }
+    double v1, v2, s;
+    do {
+      v1 = 2 * next_double() - 1;
+      v2 = 2 * next_double() - 1;
+      s = v1 * v1 + v2 * v2;
+    } while (s >= 1 || s == 0);
+    double mul = std::sqrt(-2 * std::log(s) / s);
+    next_gauss = v2 * mul;
+    have_gauss = true;
+    return v1 * mul;
+  }
+};
+}  // namespace
+
+extern "C" {
+
+// Reservoir sample of k positions out of n (SamplingOperator.processElement semantics).
+// Writes the chosen positions (in reservoir slot order) to out[0..min(n,k)); returns that count.
+int fmlx_reservoir_sample(int64_t n, int32_t k, int64_t seed, int64_t* out) {
+  JRandom rnd(seed);
+  int64_t filled = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const int32_t count = (int32_t)(i + 1);
+    if (filled < k) {
+      out[filled++] = i;
+    } else {
+      int32_t idx = rnd.next_int(count);
+      if (idx < k) out[idx] = i;
+    }
+  }
+  return (int)filled;
+}
+
+void fmlx_java_next_doubles(int64_t seed, int64_t n, double* out) {
+  JRandom rnd(seed);
+  for (int64_t i = 0; i < n; ++i) out[i] = rnd.next_double();
+}
+
+void fmlx_java_next_gaussians(int64_t seed, int64_t n, double* out) {
+  JRandom rnd(seed);
+  for (int64_t i = 0; i < n; ++i) out[i] = rnd.next_gaussian();
+}
+
+void fmlx_java_next_ints(int64_t seed, int64_t n, int32_t bound, int32_t* out) {
+  JRandom rnd(seed);
+  for (int64_t i = 0; i < n; ++i) out[i] = rnd.next_int(bound);
+}
+}

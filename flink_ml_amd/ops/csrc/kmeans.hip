@@ -1,0 +1,425 @@
+// KMeans kernels (SURVEY §2.1 K8–K10).
+//
+// Reference: LIB/clustering/kmeans/KMeans.java:269-300 (per point findClosest + axpy + count),
+// :200-212 (divide by counts), CORE/common/distance/EuclideanDistanceMeasure.java:53-73
+// (norm-based distance with lower-bound pruning, strict '<' → lowest index wins ties),
+// Cosine/ManhattanDistanceMeasure.java.
+//
+// MI355X design
+//  * kmeans_assign_bf16: the distance "GEMM" X·Cᵀ on MFMA (v_mfma_f32_32x32x16_bf16) with the
+//    argmin fused into the epilogue — the n×k distance matrix is never written. Each wave owns
+//    MT·32 rows whose A fragments (16-byte row chunks) stay in registers for the whole kernel;
+//    centroid tiles of 32 are register-staged into a double-buffered, padded (bank-conflict-free)
+//    LDS image shared by the block's 4 waves, so every centroid byte is read once per block
+//    (from L2: C is tiny) while the block streams its 128–256 rows from HBM exactly once.
+//    Epilogue: v = ‖c‖² − 2·x·c (‖x‖² is row-constant), running (v, idx) per accumulator
+//    register, then a 32-lane butterfly (ties → lower index) per row.
+//  * kmeans_assign_generic<T>: fp32/fp64 (parity) path, one thread per row, centroids in LDS,
+//    exact reference semantics for euclidean (incl. pruning), manhattan and cosine.
+//  * Centroid update without atomics, deterministic: rows are ordered by label (stable sort),
+//    cut into ≤CH-row chunks that never straddle clusters; kmeans_chunk_sum gathers each chunk's
+//    rows (fixed order) into a partial; kmeans_cluster_sum adds a cluster's chunk partials in
+//    order → [k·D sums ‖ k counts], the exact payload of the cross-GPU all-reduce (C3 → RCCL).
+//  * kmeans_finalize: c = sum·(1/count) (KMeans.java:205), weights = counts, and the padded bf16
+//    copy + ‖c‖² used by the next round's MFMA assign.
+#include "common.h"
+
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+constexpr int KM_CH = 256;  // rows per gather chunk
+
+// ------------------------------------------------------------------------------------------
+// MFMA assign (euclidean, bf16)
+// ------------------------------------------------------------------------------------------
+template <int KS>
+__global__ __launch_bounds__(256) void kmeans_assign_bf16_kernel(const bf16_t* __restrict__ X, long ld, long n,
+                                                                 int D, const bf16_t* __restrict__ Cb,
+                                                                 const float* __restrict__ cnorm, int kpad,
+                                                                 int* __restrict__ labels) {
+  constexpr int MT = KS <= 8 ? 2 : 1;     // 32-row m-tiles per wave
+  constexpr int DP = KS * 16;             // padded feature dim
+  constexpr int ROWB = DP * 2 + 16;       // padded LDS row stride (bytes): conflict-free b128 reads
+  constexpr int CHUNKS = 32 * DP / 8;     // 16-byte chunks per 32-centroid tile
+  constexpr int CPT = (CHUNKS + 255) / 256;
+  __shared__ __align__(16) unsigned char lds[2 * 32 * ROWB];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+  const long rowbase = (long)blockIdx.x * (4 * 32 * MT) + (long)wave * 32 * MT;
+
+  // ---- A fragments: this wave's MT x 32 rows, whole padded K, in registers
+  bf16x8_t a[MT][KS];
+  const bool aligned16 = (ld & 7) == 0;
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const long row = rowbase + m * 32 + r32;
+    const bf16_t* xr = X + (row < n ? row : 0) * ld;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k0 = 16 * s + 8 * h;
+      union { uint4 u; bf16x8_t v; uint16_t e[8]; } t;
+      t.u = make_uint4(0, 0, 0, 0);
+      if (row < n) {
+        if (k0 + 8 <= D) {
+          if (aligned16) {
+            t.u = *reinterpret_cast<const uint4*>(xr + k0);
+          } else {
+            const uint32_t* p = reinterpret_cast<const uint32_t*>(xr + k0);
+            t.u = make_uint4(p[0], p[1], p[2], p[3]);
+          }
+        } else {
+          for (int j = 0; j < 8; ++j) t.e[j] = (k0 + j < D) ? xr[k0 + j] : (uint16_t)0;
+        }
+      }
+      a[m][s] = t.v;
+    }
+  }
+
+  float best[MT][16];
+  int bidx[MT][16];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { best[m][r] = __builtin_huge_valf(); bidx[m][r] = 0; }
+
+  const int ntiles = kpad / 32;
+  // register-staged tile loader: chunk q of the tile = (row q / (DP/8), 16B piece q % (DP/8))
+  uint4 stage[CPT];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int q = threadIdx.x + 256 * i;
+      if (q < CHUNKS) stage[i] = reinterpret_cast<const uint4*>(Cb + (long)t * 32 * DP)[q];
+    }
+  };
+  auto swrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int q = threadIdx.x + 256 * i;
+      if (q < CHUNKS) {
+        const int rr = q / (DP / 8), cc = q % (DP / 8);
+        *reinterpret_cast<uint4*>(lds + buf * 32 * ROWB + rr * ROWB + cc * 16) = stage[i];
+      }
+    }
+  };
+
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < ntiles) gload(t + 1);  // in flight during the MFMAs
+    f32x16_t acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+    const unsigned char* tb = lds + cur * 32 * ROWB + r32 * ROWB + h * 16;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(tb + s * 32);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m][s], b, acc[m], 0, 0, 0);
+    }
+    const int col = t * 32 + r32;
+    const float cn = cnorm[col];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = cn - 2.f * acc[m][r];
+        if (v < best[m][r]) { best[m][r] = v; bidx[m][r] = col; }
+      }
+    if (t + 1 < ntiles) swrite(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- row argmin across the 32 lanes of each half (ties → lower index)
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    int mine = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float v = best[m][r];
+      int id = bidx[m][r];
+#pragma unroll
+      for (int off = 1; off < 32; off <<= 1) {
+        const float ov = __shfl_xor(v, off, 64);
+        const int oi = __shfl_xor(id, off, 64);
+        if (ov < v || (ov == v && oi < id)) { v = ov; id = oi; }
+      }
+      if (r32 == r) mine = id;
+    }
+    if (r32 < 16) {
+      const long row = rowbase + m * 32 + (r32 & 3) + 8 * (r32 >> 2) + 4 * h;
+      if (row < n) labels[row] = mine;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// generic assign (fp32 / fp64): exact reference semantics
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void kmeans_assign_generic_kernel(const T* __restrict__ X, long ld, long n, int D,
+                                                                    const T* __restrict__ C, const T* __restrict__ cnrm,
+                                                                    int k, int metric, int use_lds,
+                                                                    int* __restrict__ labels) {
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  T* Cs = reinterpret_cast<T*>(smem_raw);
+  if (use_lds) {
+    for (int i = threadIdx.x; i < k * D; i += blockDim.x) Cs[i] = C[i];
+    __syncthreads();
+  }
+  const T* Cp = use_lds ? Cs : C;
+  const long row = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= n) return;
+  const T* x = X + row * ld;
+  T pn2 = 0;
+  for (int j = 0; j < D; ++j) pn2 += x[j] * x[j];
+  const T pn = sqrt(pn2);
+  int bi = metric == 0 ? 0 : -1;
+  T best = metric == 0 ? (T)__builtin_huge_val() : (T)1.7976931348623157e308;
+  for (int i = 0; i < k; ++i) {
+    const T* c = Cp + (long)i * D;
+    const T cn = cnrm[i];
+    if (metric == 0) {
+      const T lb = pn - cn;
+      if (lb * lb >= best) continue;
+      T dot = 0;
+      for (int j = 0; j < D; ++j) dot += x[j] * c[j];
+      T d2 = pn * pn + cn * cn - (T)2 * dot;
+      d2 = d2 > (T)0 ? d2 : (T)0;
+      if (d2 < best) { best = d2; bi = i; }
+    } else if (metric == 1) {
+      T s = 0;
+      for (int j = 0; j < D; ++j) s += fabs(x[j] - c[j]);
+      if (s < best) { best = s; bi = i; }
+    } else {
+      T dot = 0;
+      for (int j = 0; j < D; ++j) dot += x[j] * c[j];
+      const T dist = (T)1 - dot / pn / cn;
+      if (dist < best) { best = dist; bi = i; }
+    }
+  }
+  labels[row] = bi;
+}
+
+// ------------------------------------------------------------------------------------------
+// deterministic centroid accumulation: chunk gather-sum then per-cluster chunk reduction
+// ------------------------------------------------------------------------------------------
+template <typename T, int VPL>
+__global__ __launch_bounds__(256) void kmeans_chunk_sum_kernel(const T* __restrict__ X, long ld, int D,
+                                                               const long* __restrict__ order,
+                                                               const long* __restrict__ offsets,  // [k+1]
+                                                               const long* __restrict__ chunk_off,  // [k+1]
+                                                               int k, typename AccOf<T>::type* __restrict__ partial) {
+  typedef typename AccOf<T>::type A;
+  const long b = blockIdx.x;
+  if (b >= chunk_off[k]) return;
+  // cluster j with chunk_off[j] <= b < chunk_off[j+1]
+  int lo = 0, hi = k;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (chunk_off[mid] <= b) lo = mid; else hi = mid;
+  }
+  const int j = lo;
+  const long q = b - chunk_off[j];
+  const long p0 = offsets[j] + q * KM_CH;
+  long p1 = p0 + KM_CH;
+  if (p1 > offsets[j + 1]) p1 = offsets[j + 1];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  A acc[VPL];
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) acc[v] = 0;
+  for (long p = p0 + wave; p < p1; p += 4) {
+    const T* xr = X + order[p] * ld;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int c = lane + 64 * v;
+      if (c < D) acc[v] += (A)Ld<T>::f(xr[c]);
+    }
+  }
+  __shared__ A sm[4][64 * VPL];
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) sm[wave][lane + 64 * v] = acc[v];
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256) partial[b * D + c] = ((sm[0][c] + sm[1][c]) + sm[2][c]) + sm[3][c];
+}
+
+template <typename A>
+__global__ __launch_bounds__(256) void kmeans_cluster_sum_kernel(const A* __restrict__ partial, int D,
+                                                                 const long* __restrict__ offsets,
+                                                                 const long* __restrict__ chunk_off, int k,
+                                                                 A* __restrict__ out /* [k*D sums | k counts] */) {
+  const int j = blockIdx.x;
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  const long q0 = chunk_off[j], q1 = chunk_off[j + 1];
+  if (c < D) {
+    A s8[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s8[i] = 0;
+    long q = q0;
+    for (; q + 8 <= q1; q += 8)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s8[i] += partial[(q + i) * D + c];
+    for (int i = 0; q < q1; ++q, ++i) s8[i] += partial[q * D + c];
+    A s = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += s8[i];
+    out[(long)j * D + c] = s;
+  }
+  if (blockIdx.y == 0 && threadIdx.x == 0) out[(long)k * D + j] = (A)(offsets[j + 1] - offsets[j]);
+}
+
+// centroids = sums * (1/count); padded bf16 copy + squared norms (of the bf16 values) for MFMA
+template <typename A>
+__global__ __launch_bounds__(256) void kmeans_finalize_kernel(const A* __restrict__ red, int D, int k,
+                                                              A* __restrict__ cent, double* __restrict__ weights,
+                                                              bf16_t* __restrict__ Cb, int DP,
+                                                              float* __restrict__ cnorm_bf16,
+                                                              A* __restrict__ cnorm_acc) {
+  const int j = blockIdx.x;
+  const A cnt = red[(long)k * D + j];
+  const A inv = (A)1 / cnt;
+  float nb = 0.f;
+  A na = 0;
+  for (int c = threadIdx.x; c < DP; c += blockDim.x) {
+    A v = c < D ? red[(long)j * D + c] * inv : (A)0;
+    if (c < D) cent[(long)j * D + c] = v;
+    if (Cb) {
+      const bf16_t bv = f32_to_bf16((float)v);
+      Cb[(long)j * DP + c] = bv;
+      const float fb = bf16_to_f32(bv);
+      nb += fb * fb;
+    }
+    na += v * v;
+  }
+  __shared__ float smb[256];
+  __shared__ A sma[256];
+  smb[threadIdx.x] = nb;
+  sma[threadIdx.x] = na;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float tb = 0.f;
+    A ta = 0;
+    for (int i = 0; i < (int)blockDim.x; ++i) { tb += smb[i]; ta += sma[i]; }
+    if (cnorm_bf16) cnorm_bf16[j] = tb;
+    if (cnorm_acc) cnorm_acc[j] = sqrt(ta);
+    if (weights) weights[j] = (double)cnt;
+  }
+}
+
+template <int KS>
+int launch_assign_bf16(const void* X, long ld, long n, int D, const void* Cb, const float* cnorm, int kpad, int* labels,
+                       hipStream_t s) {
+  constexpr int MT = KS <= 8 ? 2 : 1;
+  const long rows_per_block = 4 * 32 * MT;
+  const int blocks = (int)((n + rows_per_block - 1) / rows_per_block);
+  if (blocks == 0) return 0;
+  hipLaunchKernelGGL(kmeans_assign_bf16_kernel<KS>, dim3(blocks), dim3(256), 0, s, (const bf16_t*)X, ld, n, D,
+                     (const bf16_t*)Cb, cnorm, kpad, labels);
+  return (int)hipGetLastError();
+}
+
+template <typename T, int VPL>
+int launch_chunk_sum(const void* X, long ld, int D, const long* order, const long* offsets, const long* chunk_off,
+                     int k, long max_chunks, void* partial, hipStream_t s) {
+  if (max_chunks <= 0) return 0;
+  hipLaunchKernelGGL((kmeans_chunk_sum_kernel<T, VPL>), dim3((unsigned)max_chunks), dim3(256), 0, s, (const T*)X, ld,
+                     D, order, offsets, chunk_off, k, (typename AccOf<T>::type*)partial);
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+int chunk_sum_vpl(const void* X, long ld, int D, const long* order, const long* offsets, const long* chunk_off, int k,
+                  long max_chunks, void* partial, hipStream_t s) {
+  if (D <= 64) return launch_chunk_sum<T, 1>(X, ld, D, order, offsets, chunk_off, k, max_chunks, partial, s);
+  if (D <= 128) return launch_chunk_sum<T, 2>(X, ld, D, order, offsets, chunk_off, k, max_chunks, partial, s);
+  if (D <= 256) return launch_chunk_sum<T, 4>(X, ld, D, order, offsets, chunk_off, k, max_chunks, partial, s);
+  if (D <= 512) return launch_chunk_sum<T, 8>(X, ld, D, order, offsets, chunk_off, k, max_chunks, partial, s);
+  if (D <= 1024) return launch_chunk_sum<T, 16>(X, ld, D, order, offsets, chunk_off, k, max_chunks, partial, s);
+  return -3;
+}
+
+}  // namespace
+
+FMLX_API int fmlx_kmeans_assign_bf16(const void* X, long ld, long n, int D, const void* Cb, const float* cnorm,
+                                     int kpad, int* labels, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int KS = (D + 15) / 16;
+  switch (KS) {
+    case 1: return launch_assign_bf16<1>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
+    case 2: return launch_assign_bf16<2>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
+    case 3: return launch_assign_bf16<3>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
+    case 4: return launch_assign_bf16<4>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
+    case 5: return launch_assign_bf16<5>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
+    case 6: return launch_assign_bf16<6>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
+    case 7: return launch_assign_bf16<7>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
+    case 8: return launch_assign_bf16<8>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
+    case 10: return launch_assign_bf16<10>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
+    case 12: return launch_assign_bf16<12>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
+    case 16: return launch_assign_bf16<16>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
+  }
+  return -2;  // unsupported D for the MFMA path
+}
+
+FMLX_API int fmlx_kmeans_assign_generic(int dtype, const void* X, long ld, long n, int D, const void* C,
+                                        const void* cnrm, int k, int metric, int* labels, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) return 0;
+  const int blocks = (int)((n + 255) / 256);
+  const size_t es = dtype == DT_F64 ? 8 : 4;
+  const size_t need = (size_t)k * D * es;
+  const int use_lds = need <= 64 * 1024;
+  const size_t sh = use_lds ? need : 0;
+  if (dtype == DT_F64)
+    hipLaunchKernelGGL(kmeans_assign_generic_kernel<double>, dim3(blocks), dim3(256), sh, s, (const double*)X, ld, n,
+                       D, (const double*)C, (const double*)cnrm, k, metric, use_lds, labels);
+  else if (dtype == DT_F32)
+    hipLaunchKernelGGL(kmeans_assign_generic_kernel<float>, dim3(blocks), dim3(256), sh, s, (const float*)X, ld, n, D,
+                       (const float*)C, (const float*)cnrm, k, metric, use_lds, labels);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+FMLX_API int fmlx_kmeans_chunk_sum(int dtype, const void* X, long ld, int D, const long* order, const long* offsets,
+                                   const long* chunk_off, int k, long max_chunks, void* partial, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == DT_BF16) return chunk_sum_vpl<bf16_t>(X, ld, D, order, offsets, chunk_off, k, max_chunks, partial, s);
+  if (dtype == DT_F32) return chunk_sum_vpl<float>(X, ld, D, order, offsets, chunk_off, k, max_chunks, partial, s);
+  if (dtype == DT_F64) return chunk_sum_vpl<double>(X, ld, D, order, offsets, chunk_off, k, max_chunks, partial, s);
+  return -1;
+}
+
+FMLX_API int fmlx_kmeans_cluster_sum(int acc_f64, const void* partial, int D, const long* offsets,
+                                     const long* chunk_off, int k, void* out, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(k, (D + 255) / 256);
+  if (acc_f64)
+    hipLaunchKernelGGL(kmeans_cluster_sum_kernel<double>, grid, dim3(256), 0, s, (const double*)partial, D, offsets,
+                       chunk_off, k, (double*)out);
+  else
+    hipLaunchKernelGGL(kmeans_cluster_sum_kernel<float>, grid, dim3(256), 0, s, (const float*)partial, D, offsets,
+                       chunk_off, k, (float*)out);
+  return (int)hipGetLastError();
+}
+
+FMLX_API int fmlx_kmeans_finalize(int acc_f64, const void* red, int D, int k, void* cent, double* weights, void* Cb,
+                                  int DP, float* cnorm_bf16, void* cnorm_acc, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (acc_f64)
+    hipLaunchKernelGGL(kmeans_finalize_kernel<double>, dim3(k), dim3(256), 0, s, (const double*)red, D, k,
+                       (double*)cent, weights, (bf16_t*)Cb, DP, cnorm_bf16, (double*)cnorm_acc);
+  else
+    hipLaunchKernelGGL(kmeans_finalize_kernel<float>, dim3(k), dim3(256), 0, s, (const float*)red, D, k, (float*)cent,
+                       weights, (bf16_t*)Cb, DP, cnorm_bf16, (float*)cnorm_acc);
+  return (int)hipGetLastError();
+}

@@ -18,7 +18,7 @@ MAX_CPL = 8
 WPB = 8
 # rows in flight per wave = 2*GRAD_UNROLL (0 = kernel default for the shape); tunable for A/B runs
 GRAD_UNROLL = int(os.environ.get("FMLX_GLM_UNROLL", "0"))
-GRAD_BLOCKS = int(os.environ.get("FMLX_GLM_BLOCKS", "256"))
+GRAD_BLOCKS = int(os.environ.get("FMLX_GLM_BLOCKS", "512"))
 
 
 def pick_layout(X: torch.Tensor) -> Optional[Tuple[int, int]]:
@@ -56,7 +56,7 @@ def grad_partials(X, y, wt, coef, B: int, loss: int, state, partials, nblocks: i
 
 
 def stage1_rows(nparts: int) -> int:
-    return (nparts + 15) // 16
+    return (nparts + 31) // 32
 
 
 def reduce_update(partials, nparts: int, d: int, stage1, coef, feedback, state, max_iter, tol, lr, reg, en) -> None:

@@ -1,0 +1,166 @@
+"""Bindings for ``csrc/kmeans.hip`` plus the host reference (exact reference semantics, fp64).
+
+``assign`` = findClosest for every row (K8); ``KMeansRound`` = one Lloyd step on the rank's
+partition producing the all-reduce payload ``[k·D sums | k counts]`` (K9), deterministic.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import native
+from .native import c_int, c_long, c_void_p
+
+native.register_kernel_sigs({
+    "fmlx_kmeans_assign_bf16": [c_void_p, c_long, c_long, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
+    "fmlx_kmeans_assign_generic": [c_int, c_void_p, c_long, c_long, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                                   c_void_p],
+    "fmlx_kmeans_chunk_sum": [c_int, c_void_p, c_long, c_int, c_void_p, c_void_p, c_void_p, c_int, c_long, c_void_p,
+                              c_void_p],
+    "fmlx_kmeans_cluster_sum": [c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
+    "fmlx_kmeans_finalize": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                             c_void_p],
+})
+
+METRICS = {"euclidean": 0, "manhattan": 1, "cosine": 2}
+CHUNK = 256
+MFMA_KS = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16}
+
+
+def mfma_ok(X: torch.Tensor, metric: str) -> bool:
+    D = X.shape[1]
+    return (X.device.type == "cuda" and X.dtype == torch.bfloat16 and metric == "euclidean"
+            and X.stride(1) == 1 and X.stride(0) % 2 == 0 and X.data_ptr() % 4 == 0
+            and ((D + 15) // 16) in MFMA_KS)
+
+
+class CentroidBuffers:
+    """Device-side centroid representations consumed by the assign kernels."""
+
+    def __init__(self, k: int, D: int, device, acc_dtype):
+        self.k, self.D = k, D
+        self.kpad = max(32, (k + 31) // 32 * 32)
+        self.DP = (D + 15) // 16 * 16
+        self.cent = torch.zeros((k, D), dtype=acc_dtype, device=device)
+        self.cnorm = torch.zeros(k, dtype=acc_dtype, device=device)          # ‖c‖ (acc dtype)
+        self.Cb = torch.zeros((self.kpad, self.DP), dtype=torch.bfloat16, device=device)
+        self.cnorm_b = torch.full((self.kpad,), float("inf"), dtype=torch.float32, device=device)  # ‖c_bf16‖²
+        self.weights = torch.zeros(k, dtype=torch.float64, device=device)
+
+    def set(self, centroids: torch.Tensor) -> None:
+        c = centroids.to(device=self.cent.device, dtype=self.cent.dtype)
+        self.cent.copy_(c)
+        self.cnorm.copy_(torch.linalg.vector_norm(c.to(torch.float64), dim=1).to(self.cent.dtype))
+        cb = c.to(torch.bfloat16)
+        self.Cb.zero_()
+        self.Cb[: self.k, : self.D] = cb
+        self.cnorm_b.fill_(float("inf"))
+        self.cnorm_b[: self.k] = (cb.float() ** 2).sum(1)
+
+
+def assign(X: torch.Tensor, cb: CentroidBuffers, metric: str, out: torch.Tensor = None) -> torch.Tensor:
+    """Index of the closest centroid for every row (reference ``DistanceMeasure.findClosest``)."""
+    n, D = X.shape
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=X.device)
+    if n == 0:
+        return out
+    if X.device.type != "cuda":
+        return torch_assign(X, cb.cent, metric).to(torch.int32)
+    if mfma_ok(X, metric):
+        native.call("fmlx_kmeans_assign_bf16", native.ptr(X), X.stride(0), n, D, native.ptr(cb.Cb),
+                    native.ptr(cb.cnorm_b), cb.kpad, native.ptr(out), native.stream_ptr(X.device))
+        return out
+    if X.dtype not in (torch.float32, torch.float64):
+        X = X.to(torch.float32)
+    X = X if X.stride(1) == 1 else X.contiguous()
+    C = cb.cent.to(X.dtype).contiguous()
+    cn = cb.cnorm.to(X.dtype).contiguous()
+    native.call("fmlx_kmeans_assign_generic", native.dtype_code(X.dtype), native.ptr(X), X.stride(0), n, D,
+                native.ptr(C), native.ptr(cn), cb.k, METRICS[metric], native.ptr(out), native.stream_ptr(X.device))
+    return out
+
+
+def torch_assign(X: torch.Tensor, C: torch.Tensor, metric: str) -> torch.Tensor:
+    """Host reference of findClosest (EuclideanDistanceMeasure.java:53-73 incl. pruning order)."""
+    X = X.to(torch.float64)
+    C = C.to(device=X.device, dtype=torch.float64)
+    if X.shape[0] == 0:
+        return torch.zeros(0, dtype=torch.int64)
+    if metric == "euclidean":
+        pn = torch.linalg.vector_norm(X, dim=1)
+        cn = torch.linalg.vector_norm(C, dim=1)
+        d2 = torch.clamp(pn[:, None] * pn[:, None] + (cn * cn)[None, :] - 2.0 * (X @ C.T), min=0.0)
+        d2 = torch.where(torch.isnan(d2), torch.full_like(d2, float("inf")), d2)
+        return torch.argmin(d2, dim=1)  # argmin returns the first minimum: lowest index on ties
+    if metric == "manhattan":
+        d = torch.cdist(X, C, p=1)
+    else:
+        d = 1.0 - (X @ C.T) / torch.linalg.vector_norm(X, dim=1)[:, None] / torch.linalg.vector_norm(C, dim=1)[None, :]
+    return torch.argmin(d, dim=1)
+
+
+class KMeansRound:
+    """One Lloyd iteration on a device-resident partition: assign → ordered chunk sums →
+    per-cluster sums/counts. ``payload`` is the fixed-size all-reduce buffer."""
+
+    def __init__(self, X: torch.Tensor, k: int, metric: str):
+        self.X = X
+        self.n, self.D = X.shape
+        self.k = k
+        self.metric = metric
+        dev = X.device
+        self.acc = torch.float64 if X.dtype == torch.float64 else torch.float32
+        self.labels = torch.empty(self.n, dtype=torch.int32, device=dev)
+        self.max_chunks = (self.n + CHUNK - 1) // CHUNK + k
+        self.partial = torch.zeros((self.max_chunks, self.D), dtype=self.acc, device=dev)
+        self.payload = torch.zeros(k * self.D + k, dtype=self.acc, device=dev)
+        self.zero_i64 = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def run(self, cb: CentroidBuffers) -> torch.Tensor:
+        X = self.X
+        if self.n == 0:
+            self.payload.zero_()
+            return self.payload
+        assign(X, cb, self.metric, self.labels)
+        lab = self.labels.to(torch.int64)
+        order = torch.argsort(lab, stable=True)
+        counts = torch.bincount(lab, minlength=self.k)
+        offsets = torch.cat([self.zero_i64, torch.cumsum(counts, 0)])
+        chunk_off = torch.cat([self.zero_i64, torch.cumsum((counts + CHUNK - 1) // CHUNK, 0)])
+        Xs = X if X.dtype in (torch.bfloat16, torch.float32, torch.float64) else X.to(torch.float32)
+        native.call("fmlx_kmeans_chunk_sum", native.dtype_code(Xs.dtype), native.ptr(Xs), Xs.stride(0), self.D,
+                    native.ptr(order), native.ptr(offsets), native.ptr(chunk_off), self.k, self.max_chunks,
+                    native.ptr(self.partial), native.stream_ptr(X.device))
+        native.call("fmlx_kmeans_cluster_sum", int(self.acc == torch.float64), native.ptr(self.partial), self.D,
+                    native.ptr(offsets), native.ptr(chunk_off), self.k, native.ptr(self.payload),
+                    native.stream_ptr(X.device))
+        return self.payload
+
+    def finalize(self, cb: CentroidBuffers, payload: torch.Tensor) -> None:
+        native.call("fmlx_kmeans_finalize", int(self.acc == torch.float64), native.ptr(payload), self.D, self.k,
+                    native.ptr(cb.cent), native.ptr(cb.weights), native.ptr(cb.Cb), cb.DP, native.ptr(cb.cnorm_b),
+                    native.ptr(cb.cnorm), native.stream_ptr(self.X.device))
+
+
+def torch_round_payload(X: torch.Tensor, C: torch.Tensor, metric: str) -> torch.Tensor:
+    """Host reference for one round's [sums | counts] (CentroidsUpdateAccumulator, KMeans.java:269-300)."""
+    k, D = C.shape
+    X = X.to(torch.float64)
+    out = torch.zeros(k * D + k, dtype=torch.float64)
+    if X.shape[0] == 0:
+        return out
+    lab = torch_assign(X, C, metric)
+    sums = torch.zeros((k, D), dtype=torch.float64).index_add_(0, lab, X)
+    out[: k * D] = sums.reshape(-1)
+    out[k * D:] = torch.bincount(lab, minlength=k).to(torch.float64)
+    return out
+
+
+def torch_finalize(payload: torch.Tensor, k: int, D: int):
+    sums = payload[: k * D].reshape(k, D)
+    counts = payload[k * D:]
+    cent = sums * (1.0 / counts)[:, None]  # scal(1/count): 0 rows → NaN like the reference
+    return cent, counts

@@ -1,0 +1,204 @@
+"""KMeans / KMeansModel (reference LIBT/clustering/KMeansTest.java) on CPU incl. 4 gloo ranks,
+plus GPU numerics of the MFMA assign and the deterministic centroid update."""
+import numpy as np
+import pytest
+import torch
+
+from flink_ml_amd import Table, Vectors
+from flink_ml_amd.models import KMeans, KMeansModel
+from flink_ml_amd.models.kmeans import reservoir_sample_indices
+from tests.spmd import run_spmd
+
+DATA = [Vectors.dense(0.0, 0.0), Vectors.dense(0.0, 0.3), Vectors.dense(0.3, 0.0),
+        Vectors.dense(9.0, 0.0), Vectors.dense(9.0, 0.6), Vectors.dense(9.6, 0.0)]
+GROUPS = [{(0.0, 0.0), (0.0, 0.3), (0.3, 0.0)}, {(9.0, 0.0), (9.0, 0.6), (9.6, 0.0)}]
+
+
+def _table(rows=DATA):
+    return Table.from_rows([(v,) for v in rows], ["features"])
+
+
+def _groups(out):
+    g = {}
+    for feat, pred in out.rows():
+        g.setdefault(pred, set()).add(tuple(feat.values.tolist()))
+    return sorted(g.values(), key=lambda s: min(s))
+
+
+def test_params():
+    km = KMeans()
+    assert km.get_k() == 2 and km.get_max_iter() == 20 and km.get_distance_measure() == "euclidean"
+    assert km.get_init_mode() == "random" and km.get_seed() == km.get_seed()
+    from flink_ml_amd.utils.java import java_string_hash
+
+    assert km.get_seed() == java_string_hash("org.apache.flink.ml.clustering.kmeans.KMeans")
+    with pytest.raises(ValueError):
+        km.set_k(1)
+
+
+def test_fit_predict_golden():
+    model = KMeans().set_max_iter(2).set_k(2).fit(_table())
+    out = model.transform(_table())[0]
+    assert out.column_names == ["features", "prediction"]
+    assert _groups(out) == sorted(GROUPS, key=lambda s: min(s))
+
+
+@pytest.mark.parametrize("metric", ["manhattan", "cosine"])
+def test_other_metrics(metric):
+    rows = DATA if metric == "manhattan" else [Vectors.dense(1.0, 0.01), Vectors.dense(1.0, 0.02),
+                                               Vectors.dense(0.01, 1.0), Vectors.dense(0.02, 1.0)]
+    model = KMeans().set_distance_measure(metric).set_seed(7).fit(_table(rows))
+    out = model.transform(_table(rows))[0]
+    assert len({p for _, p in out.rows()}) == 2
+
+
+def test_save_load_and_model_data(tmp_path):
+    model = KMeans().set_max_iter(5).fit(_table())
+    p = str(tmp_path / "km")
+    model.save(p)
+    loaded = KMeansModel.load(p)
+    assert np.allclose(loaded.centroids(), model.centroids())
+    assert _groups(loaded.transform(_table())[0]) == sorted(GROUPS, key=lambda s: min(s))
+    md = loaded.get_model_data()[0].rows()[0]
+    assert sorted(md[1].values.tolist()) == [3.0, 3.0]
+    # byte layout: int32 k + k*(int32 2 + 2 doubles) + weights(int32 2 + 2 doubles)
+    import os
+
+    data = open(os.path.join(p, "data", "part-0-0"), "rb").read()
+    assert len(data) == 4 + 2 * (4 + 16) + (4 + 16)
+
+
+def test_reservoir_matches_java_random():
+    from flink_ml_amd.utils.java import JavaRandom
+
+    got = reservoir_sample_indices(500, 7, 1234)
+    r = JavaRandom(1234)
+    ref = list(range(7))
+    for i in range(7, 500):
+        j = r.next_int(i + 1)
+        if j < 7:
+            ref[j] = i
+    assert got.tolist() == ref
+
+
+def test_fewer_points_than_k():
+    model = KMeans().set_k(10).fit(_table(DATA[:3]))
+    assert len(model.get_model_data()[0].rows()[0][0]) == 3
+
+
+def _spmd_kmeans(rank, world):
+    t = _table().partition(rank, world)
+    model = KMeans().set_max_iter(3).fit(t)
+    return model.centroids().tolist()
+
+
+def test_kmeans_four_ranks():
+    res = run_spmd(_spmd_kmeans, 4)
+    for r in res:
+        assert np.allclose(r, res[0], equal_nan=True)
+    cents = sorted(map(tuple, np.round(np.array(res[0]), 6)))
+    assert np.allclose(cents, [(0.1, 0.1), (9.2, 0.2)])
+
+
+def _spmd_plumbing(rank, world):
+    # north-star config 1: KMeans k=2 on 100 synthetic 2-D vectors across local ranks
+    g = np.random.default_rng(5)
+    pts = np.concatenate([g.normal(0, 0.1, (50, 2)), g.normal(5, 0.1, (50, 2))])
+    t = Table({"features": torch.as_tensor(pts)}).partition(rank, world)
+    model = KMeans().set_k(2).fit(t)
+    out = model.transform(t)[0]
+    return sorted(map(tuple, np.round(model.centroids(), 3))), out.column("prediction").tolist(), out.column(
+        "features")[:, 0].tolist()
+
+
+def test_config1_plumbing_100_points_4_ranks():
+    res = run_spmd(_spmd_plumbing, 4)
+    assert all(r[0] == res[0][0] for r in res)
+    for _, preds, xs in res:
+        for p, x in zip(preds, xs):
+            assert (x > 2.5) == (p == (1 if res[0][0][1][0] > 2.5 else 0))
+
+
+# ------------------------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("D", [2, 10, 100, 128, 200])
+@pytest.mark.parametrize("k", [2, 10, 33, 257])
+def test_gpu_assign_bf16_matches_torch(D, k):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from flink_ml_amd.ops import kmeans as kk
+
+    g = torch.Generator().manual_seed(D * 1000 + k)
+    X = torch.randn((3000, D), generator=g).to(torch.bfloat16)
+    C = torch.randn((k, D), generator=g, dtype=torch.float64)
+    cb = kk.CentroidBuffers(k, D, torch.device("cuda"), torch.float32)
+    cb.set(C)
+    lab = kk.assign(X.cuda(), cb, "euclidean").cpu().long()
+    # reference on the same bf16-rounded operands, fp32 distance
+    Xf, Cf = X.float(), C.to(torch.bfloat16).float()
+    d = (Cf ** 2).sum(1)[None, :] - 2 * Xf @ Cf.T
+    ref = torch.argmin(d, 1)
+    dsel = d.gather(1, lab[:, None]).squeeze(1)
+    dref = d.gather(1, ref[:, None]).squeeze(1)
+    # identical except near-ties within fp32 accumulation-order noise
+    assert torch.all((lab == ref) | ((dsel - dref).abs() <= 1e-3 * (1 + dref.abs())))
+    assert (lab == ref).float().mean() > 0.99
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("metric", ["euclidean", "manhattan", "cosine"])
+def test_gpu_assign_generic(dtype, metric):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from flink_ml_amd.ops import kmeans as kk
+
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn((2000, 37), generator=g, dtype=torch.float64)
+    C = torch.randn((9, 37), generator=g, dtype=torch.float64)
+    cb = kk.CentroidBuffers(9, 37, torch.device("cuda"), torch.float64 if dtype == torch.float64 else torch.float32)
+    cb.set(C)
+    lab = kk.assign(X.to(dtype).cuda(), cb, metric).cpu().long()
+    ref = kk.torch_assign(X.to(dtype), C.to(dtype), metric)
+    assert (lab == ref).float().mean() > 0.999
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32, torch.float64])
+def test_gpu_round_payload_matches_torch(dtype):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from flink_ml_amd.ops import kmeans as kk
+
+    g = torch.Generator().manual_seed(2)
+    n, D, k = 20000, 100, 10
+    X = torch.rand((n, D), generator=g, dtype=torch.float64).to(dtype)
+    C = X[:k].to(torch.float64)
+    acc = torch.float64 if dtype == torch.float64 else torch.float32
+    cb = kk.CentroidBuffers(k, D, torch.device("cuda"), acc)
+    cb.set(C)
+    rnd = kk.KMeansRound(X.cuda(), k, "euclidean")
+    p1 = rnd.run(cb).clone()
+    p2 = rnd.run(cb).clone()
+    assert torch.equal(p1, p2)  # deterministic
+    lab = rnd.labels.cpu().long()
+    ref_sums = torch.zeros((k, D), dtype=torch.float64).index_add_(0, lab, X.to(torch.float64))
+    ref_cnt = torch.bincount(lab, minlength=k).double()
+    got = p1.cpu().double()
+    assert torch.allclose(got[: k * D].reshape(k, D), ref_sums, rtol=1e-5, atol=1e-3)
+    assert torch.equal(got[k * D:], ref_cnt)
+    rnd.finalize(cb, p1)
+    assert torch.allclose(cb.cent.cpu().double(), ref_sums / ref_cnt[:, None], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_gpu_kmeans_fit_golden():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    for dt in ("fp64", "bf16", "fp32"):
+        from flink_ml_amd.config import dtype_policy
+
+        with dtype_policy(dt):
+            model = KMeans().set_max_iter(2).fit(_table())
+            out = model.transform(_table())[0]
+        assert _groups(out) == sorted(GROUPS, key=lambda s: min(s)), dt
