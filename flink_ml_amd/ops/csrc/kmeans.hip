@@ -350,10 +350,11 @@ int chunk_sum_vpl(const void* X, long ld, int D, const long* order, const long* 
 
 }  // namespace
 
-FMLX_API int fmlx_kmeans_assign_bf16(const void* X, long ld, long n, int D, const void* Cb, const float* cnorm,
+// KS = padded K-steps of 16 (one of 1..8,10,12,16; >= ceil(D/16)); Cb is [kpad][16*KS] zero-padded
+FMLX_API int fmlx_kmeans_assign_bf16(const void* X, long ld, long n, int D, int KS, const void* Cb, const float* cnorm,
                                      int kpad, int* labels, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  const int KS = (D + 15) / 16;
+  if (KS * 16 < D) return -2;
   switch (KS) {
     case 1: return launch_assign_bf16<1>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
     case 2: return launch_assign_bf16<2>(X, ld, n, D, Cb, cnorm, kpad, labels, s);

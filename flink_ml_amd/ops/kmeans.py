@@ -14,7 +14,8 @@ from . import native
 from .native import c_int, c_long, c_void_p
 
 native.register_kernel_sigs({
-    "fmlx_kmeans_assign_bf16": [c_void_p, c_long, c_long, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
+    "fmlx_kmeans_assign_bf16": [c_void_p, c_long, c_long, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                c_void_p],
     "fmlx_kmeans_assign_generic": [c_int, c_void_p, c_long, c_long, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p,
                                    c_void_p],
     "fmlx_kmeans_chunk_sum": [c_int, c_void_p, c_long, c_int, c_void_p, c_void_p, c_void_p, c_int, c_long, c_void_p,
@@ -26,14 +27,21 @@ native.register_kernel_sigs({
 
 METRICS = {"euclidean": 0, "manhattan": 1, "cosine": 2}
 CHUNK = 256
-MFMA_KS = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16}
+MFMA_KS = (1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16)
+
+
+def mfma_ks(D: int) -> int:
+    """Padded number of 16-wide K steps for the MFMA assign kernel (0 if D is too wide)."""
+    need = (D + 15) // 16
+    for ks in MFMA_KS:
+        if ks >= need:
+            return ks
+    return 0
 
 
 def mfma_ok(X: torch.Tensor, metric: str) -> bool:
-    D = X.shape[1]
     return (X.device.type == "cuda" and X.dtype == torch.bfloat16 and metric == "euclidean"
-            and X.stride(1) == 1 and X.stride(0) % 2 == 0 and X.data_ptr() % 4 == 0
-            and ((D + 15) // 16) in MFMA_KS)
+            and X.stride(1) == 1 and X.stride(0) % 2 == 0 and X.data_ptr() % 4 == 0 and mfma_ks(X.shape[1]) > 0)
 
 
 class CentroidBuffers:
@@ -42,7 +50,8 @@ class CentroidBuffers:
     def __init__(self, k: int, D: int, device, acc_dtype):
         self.k, self.D = k, D
         self.kpad = max(32, (k + 31) // 32 * 32)
-        self.DP = (D + 15) // 16 * 16
+        self.KS = mfma_ks(D) or (D + 15) // 16
+        self.DP = self.KS * 16
         self.cent = torch.zeros((k, D), dtype=acc_dtype, device=device)
         self.cnorm = torch.zeros(k, dtype=acc_dtype, device=device)          # ‖c‖ (acc dtype)
         self.Cb = torch.zeros((self.kpad, self.DP), dtype=torch.bfloat16, device=device)
@@ -70,7 +79,7 @@ def assign(X: torch.Tensor, cb: CentroidBuffers, metric: str, out: torch.Tensor 
     if X.device.type != "cuda":
         return torch_assign(X, cb.cent, metric).to(torch.int32)
     if mfma_ok(X, metric):
-        native.call("fmlx_kmeans_assign_bf16", native.ptr(X), X.stride(0), n, D, native.ptr(cb.Cb),
+        native.call("fmlx_kmeans_assign_bf16", native.ptr(X), X.stride(0), n, D, cb.KS, native.ptr(cb.Cb),
                     native.ptr(cb.cnorm_b), cb.kpad, native.ptr(out), native.stream_ptr(X.device))
         return out
     if X.dtype not in (torch.float32, torch.float64):

@@ -1,0 +1,151 @@
+"""SPMD equivalents of ``DataStreamUtils`` (reference ``CORE/common/datastream/DataStreamUtils.java``).
+
+In the reference each helper is a small dataflow sub-graph (partial operator per subtask, then
+a parallelism-1 operator, network shuffles in between). Here each is a local computation on the
+rank's partition plus at most one collective:
+
+==========================  ============================================================
+reference                   here
+==========================  ============================================================
+``allReduceSum`` (:102)     ``all_reduce_sum`` — RCCL all-reduce of a device tensor
+``mapPartition`` (:115)     ``map_partition`` — apply fn to the whole local partition
+``reduce`` (:132-155)       ``reduce`` — local fold, all-gather, fold in rank order
+``aggregate`` (:182-199)    ``aggregate`` — local accumulator, all-gather, merge in rank order
+``sample`` (:212-227)       ``sample`` — reservoir per rank (java.util.Random), gather, again
+``generateBatchData``       ``generate_batch_data`` — deterministic per-rank split of a global
+  (:571-628)                  mini-batch from the rank's stream shard
+``windowAllAndProcess``     ``window_all_and_process`` — cut the partition into windows and
+  (:262-303)                  process each window on rank 0's gathered data
+==========================  ============================================================
+"""
+from __future__ import annotations
+
+from typing import Any, Callable, Iterable, Iterator, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..common.window import CountTumblingWindows, GlobalWindows, Windows
+from ..table import Table
+from . import comm
+from .context import get_context
+
+
+def all_reduce_sum(t: torch.Tensor) -> torch.Tensor:
+    """``DataStreamUtils.allReduceSum``: element-wise sum of one array per rank (equal lengths)."""
+    comm.check_equal_across_ranks(int(t.numel()), "all-reduce array length")
+    return comm.all_reduce_sum(t)
+
+
+def map_partition(partition, fn: Callable):
+    return fn(partition)
+
+
+def reduce(value: Any, fn: Callable[[Any, Any], Any]):
+    """Folds one value per rank with ``fn`` in rank order; every rank gets the result.
+    ``value=None`` marks an empty partition."""
+    vals = [v for v in comm.all_gather_object(value) if v is not None]
+    if not vals:
+        return None
+    acc = vals[0]
+    for v in vals[1:]:
+        acc = fn(acc, v)
+    return acc
+
+
+class AggregateFunction:
+    """``org.apache.flink.api.common.functions.AggregateFunction`` shape."""
+
+    def create_accumulator(self):
+        raise NotImplementedError
+
+    def add(self, value, acc):
+        raise NotImplementedError
+
+    def get_result(self, acc):
+        return acc
+
+    def merge(self, a, b):
+        raise NotImplementedError
+
+
+def aggregate(values: Iterable, fn: AggregateFunction, local_acc=None):
+    """Local accumulation then merge of the per-rank accumulators in rank order."""
+    if local_acc is None:
+        local_acc = fn.create_accumulator()
+        for v in values:
+            local_acc = fn.add(v, local_acc)
+    accs = comm.all_gather_object(local_acc)
+    acc = accs[0]
+    for a in accs[1:]:
+        acc = fn.merge(acc, a)
+    return fn.get_result(acc)
+
+
+def sample(rows: Sequence, k: int, seed: int) -> list:
+    """``DataStreamUtils.sample``: reservoir with ``java.util.Random(seed)`` per rank, then again
+    over the rank-ordered union (``SamplingOperator``, DataStreamUtils.java:633-704)."""
+    from ..models.kmeans import reservoir_sample_indices
+
+    local = [rows[i] for i in reservoir_sample_indices(len(rows), k, seed)]
+    union = [r for part in comm.all_gather_object(local) for r in part]
+    return [union[i] for i in reservoir_sample_indices(len(union), k, seed)]
+
+
+def generate_batch_data(stream: Iterable, global_batch_size: int) -> Iterator:
+    """Yields this rank's share of each global mini-batch: ``globalBatch/P`` items, the remainder
+    going to the low ranks (``DataStreamUtils.generateBatchData`` splits a countWindowAll batch
+    the same way). A trailing partial batch is dropped, like the count window."""
+    ctx = get_context()
+    b = global_batch_size // ctx.world_size + (1 if global_batch_size % ctx.world_size > ctx.rank else 0)
+    if isinstance(stream, Table):
+        for s in range(0, stream.num_rows - b + 1, max(b, 1)):
+            yield stream.slice(s, s + b)
+        return
+    buf = []
+    for item in stream:
+        if isinstance(item, Table):
+            yield item
+            continue
+        buf.append(item)
+        if len(buf) == b:
+            yield buf
+            buf = []
+
+
+def window_all_and_process(table: Table, windows: Windows, fn: Callable[[Table], Table],
+                           time_col: Optional[str] = None) -> Table:
+    """Applies ``fn`` to every window of the (globally gathered) input; the result is produced on
+    rank 0 (parallelism-1 semantics of ``windowAll``) and is empty on other ranks."""
+    ctx = get_context()
+    parts = comm.all_gather_object(table.to("cpu")) if ctx.is_distributed else [table]
+    full = Table.concat(parts) if len(parts) > 1 else parts[0]
+    if ctx.rank != 0:
+        return None
+    outs = []
+    if isinstance(windows, GlobalWindows) or windows is None:
+        outs.append(fn(full))
+    elif isinstance(windows, CountTumblingWindows):
+        n = windows.size
+        for s in range(0, full.num_rows - n + 1, n):
+            outs.append(fn(full.slice(s, s + n)))
+    else:
+        # time windows: tumbling by a timestamp column (ms), sessions by gaps
+        if time_col is None:
+            outs.append(fn(full))
+        else:
+            ts = np.asarray(full.scalars(time_col, dtype=torch.float64).cpu().numpy())
+            order = np.argsort(ts, kind="stable")
+            full = full.take(torch.as_tensor(order))
+            ts = ts[order]
+            if hasattr(windows, "size"):
+                keys = np.floor(ts / windows.size)
+                bounds = np.nonzero(np.diff(keys))[0] + 1
+            else:
+                bounds = np.nonzero(np.diff(ts) >= windows.gap)[0] + 1
+            starts = np.concatenate([[0], bounds])
+            ends = np.concatenate([bounds, [len(ts)]])
+            for s, e in zip(starts, ends):
+                outs.append(fn(full.slice(int(s), int(e))))
+    outs = [o for o in outs if o is not None]
+    return Table.concat(outs) if outs else None

@@ -20,7 +20,7 @@ for step in $STEPS; do
       timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
       rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log; [ $rc -eq 0 ] || exit $rc ;;
     prof)
-      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 50 --warmup 5 ${PROF_ARGS:-}) > gpurun_out/prof.log 2>&1
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/${PROF_SCRIPT:-bench.py}" ${PROF_ARGS:---steps 50 --warmup 5}) > gpurun_out/prof.log 2>&1
       rc=$?; echo "prof rc=$rc"; tail -3 gpurun_out/prof.log; [ $rc -eq 0 ] || exit $rc ;;
     extra)
       timeout -k 10 900 bash -c "${EXTRA_CMD}" > gpurun_out/extra.log 2>&1
