@@ -4,3 +4,6 @@ from .linear import (LinearRegression, LinearRegressionModel, LinearSVC, LinearS
                      LogisticRegression, LogisticRegressionModel)
 from . import kmeans  # noqa: F401,E402
 from .kmeans import KMeans, KMeansModel  # noqa: F401,E402
+from . import online  # noqa: F401,E402
+from .online import (OnlineKMeans, OnlineKMeansModel, OnlineLogisticRegression,  # noqa: F401,E402
+                     OnlineLogisticRegressionModel)

@@ -1,0 +1,524 @@
+"""Online (unbounded-stream) models: OnlineLogisticRegression (FTRL) and OnlineKMeans.
+
+Reference: ``LIB/classification/logisticregression/OnlineLogisticRegression{,Model}.java``
+ and ``LIB/clustering/kmeans/OnlineKMeans{,Model}.java``.
+
+Execution model (SURVEY §7.1 "unbounded streams"): each rank ingests its own stream shard,
+re-batched to ``globalBatchSize / P`` rows (remainder to low ranks) with async H2D prefetch;
+one training round per global mini-batch = fused local-gradient kernel (``glm.hip`` loss code 3)
+→ ONE RCCL all-reduce of ``[grad | weightSum]`` → fused FTRL kernel (``ftrl.hip``). Every rank
+holds the FTRL state (z, n) replicated, so no model broadcast is needed (C1/C3 disappear).
+Models produced by training form a *versioned model-data stream*; a ``transform`` predicts each
+input batch with the latest version available at that moment (pulling training batches that are
+already queued, blocking only until the first version exists — the reference buffers points
+until the first model arrives) and reports the ``modelDataVersion`` gauge.
+"""
+from __future__ import annotations
+
+import math
+from typing import Iterable, List, Optional
+
+import numpy as np
+import torch
+
+from .. import config
+from ..api.stage import Estimator
+from ..common.param import (HasBatchStrategy, HasDecayFactor, HasDistanceMeasure, HasElasticNet, HasFeaturesCol,
+                            HasGlobalBatchSize, HasLabelCol, HasPredictionCol, HasRawPredictionCol, HasReg, HasSeed,
+                            HasWeightCol)
+from ..io import read_write as rw
+from ..linalg.vectors import DenseVector
+from ..ops import glm as gk
+from ..ops import kmeans as kk
+from ..ops import native
+from ..ops.native import c_double, c_int, c_long, c_void_p
+from ..param.param import FloatParam, IntParam, ParamValidators, StringParam
+from ..parallel import comm
+from ..stream import InMemorySource, StreamTable
+from ..table import SparseColumn, Table
+from ..utils.java import JavaRandom
+from ..utils.tracing import MetricGroup
+from .base import ModelWithData
+from .kmeans import KMeansModel, _decode_kmeans, _encode_kmeans
+from .linear import LogisticRegressionModel, rw_update
+
+native.register_kernel_sigs({
+    "fmlx_ftrl_update": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_double, c_double,
+                         c_double, c_double, c_void_p],
+})
+
+
+def _as_stream(inp, batch_rows: Optional[int] = None) -> Iterable[Table]:
+    if isinstance(inp, StreamTable):
+        return inp
+    if isinstance(inp, InMemorySource):
+        return StreamTable.from_source(inp)
+    if isinstance(inp, Table):
+        return StreamTable.from_table(inp, max(1, batch_rows or inp.num_rows))
+    return StreamTable(inp)
+
+
+class VersionedModelStream:
+    """Lazily-trained sequence of model versions shared by the estimator's output model.
+
+    ``pull(block)`` trains on the next mini-batch (collectively across ranks) and appends the
+    resulting version. With an ``InMemorySource`` the non-blocking pull only consumes batches
+    that every rank has already received.
+    """
+
+    def __init__(self, source, rebatch: int, step_fn, initial_versions: List = ()):
+        self.versions: List = list(initial_versions)
+        self._source = source
+        self._step = step_fn
+        self._iter = None
+        self._pending = None
+        self._done = False
+        self._rebatch = rebatch
+
+    def _next_local(self, block: bool):
+        if self._pending is not None:
+            return self._pending
+        if isinstance(self._source, InMemorySource) and not block:
+            item = self._source.poll(timeout=0)
+            if item is None:
+                return None
+            from ..stream import END
+
+            if item is END:
+                self._done = True
+                return None
+            self._pending = _BatchBuf.feed(self, item)
+            return self._pending
+        if self._iter is None:
+            src = self._source
+            stream = _as_stream(src)
+            self._iter = iter(stream.rebatch(self._rebatch).to_device() if isinstance(stream, StreamTable)
+                              else stream)
+        try:
+            self._pending = next(self._iter)
+        except StopIteration:
+            self._done = True
+            return None
+        return self._pending
+
+    def pull(self, block: bool = True) -> bool:
+        if self._done and self._pending is None:
+            return False
+        got = self._next_local(block) is not None
+        if comm.all_reduce_scalar(1.0 if got else 0.0, "min") == 0.0:
+            return False
+        batch = self._pending
+        self._pending = None
+        self.versions.append(self._step(batch))
+        return True
+
+    def drain_available(self) -> None:
+        if isinstance(self._source, InMemorySource):
+            while self.pull(block=False):
+                pass
+        else:
+            while self.pull(block=True):
+                pass
+
+    def latest(self, block_until_first: bool = True):
+        if not self.versions and block_until_first:
+            self.pull(block=True)
+        return self.versions[-1] if self.versions else None
+
+
+class _BatchBuf:
+    """Regroups non-blocking InMemorySource arrivals into local mini-batches."""
+
+    @staticmethod
+    def feed(stream: VersionedModelStream, table: Table):
+        from ..parallel.context import get_context
+
+        ctx = get_context()
+        g = stream._rebatch
+        b = g // ctx.world_size + (1 if g % ctx.world_size > ctx.rank else 0)
+        buf = getattr(stream, "_buf", None)
+        buf = Table.concat([buf, table]) if buf is not None and buf.num_rows else table
+        if buf.num_rows >= b:
+            stream._buf = buf.slice(b, buf.num_rows)
+            return buf.slice(0, b).to(config.compute_device())
+        stream._buf = buf
+        return None
+
+
+# ==============================================================================================
+# OnlineLogisticRegression
+# ==============================================================================================
+class OnlineLogisticRegressionModelParams(HasFeaturesCol, HasPredictionCol, HasRawPredictionCol):
+    MODEL_VERSION_COL = StringParam("modelVersionCol", "Model version column name.", "modelVersion",
+                                    ParamValidators.not_null())
+
+
+class OnlineLogisticRegressionParams(HasLabelCol, HasWeightCol, HasBatchStrategy, HasGlobalBatchSize, HasReg,
+                                     HasElasticNet, OnlineLogisticRegressionModelParams):
+    ALPHA = FloatParam("alpha", "The alpha parameter of ftrl.", 0.1, ParamValidators.gt(0.0))
+    BETA = FloatParam("beta", "The beta parameter of ftrl.", 0.1, ParamValidators.gt(0.0))
+
+
+class FtrlTrainer:
+    """Replicated FTRL state on the device + one round per mini-batch."""
+
+    def __init__(self, coef0: np.ndarray, alpha, beta, l1, l2, features_col, label_col, weight_col):
+        self.dev = config.compute_device()
+        self.acc = config.acc_dtype() if self.dev.type == "cuda" else torch.float64
+        d = coef0.shape[0]
+        self.d = d
+        self.coef = torch.as_tensor(coef0, dtype=self.acc, device=self.dev).clone()
+        self.z = torch.zeros(d, dtype=self.acc, device=self.dev)
+        self.n = torch.zeros(d, dtype=self.acc, device=self.dev)
+        self.alpha, self.beta, self.l1, self.l2 = alpha, beta, l1, l2
+        self.fcol, self.lcol, self.wcol = features_col, label_col, weight_col
+        self.version = 0
+
+    def local_gradient(self, batch: Table):
+        X = config.features_for_compute(batch, self.fcol)
+        y = batch.scalars(self.lcol, dtype=self.acc, device=self.dev)
+        payload = torch.zeros(2 * self.d, dtype=self.acc, device=self.dev)
+        if isinstance(X, SparseColumn):
+            w = batch.scalars(self.wcol, dtype=self.acc, device=self.dev) if self.wcol and batch.has_column(
+                self.wcol) else torch.ones(len(X), dtype=self.acc, device=self.dev)
+            counts = X.indptr[1:] - X.indptr[:-1]
+            rows = torch.repeat_interleave(torch.arange(len(X), device=self.dev), counts.to(self.dev))
+            idx = X.indices.to(self.dev).long()
+            vals = X.values.to(self.dev, self.acc)
+            dot = torch.zeros(len(X), dtype=self.acc, device=self.dev).index_add_(0, rows, vals * self.coef[idx])
+            mult = torch.sigmoid(dot) - y
+            payload[: self.d].index_add_(0, idx, mult[rows] * vals)
+            payload[self.d:].index_add_(0, idx, w[rows])
+            return payload
+        n = X.shape[0]
+        if n == 0:
+            return payload
+        if self.dev.type == "cuda" and gk.pick_layout(X) is not None:
+            Xk = X if X.dtype in (torch.float32, torch.float64, torch.bfloat16) else X.to(self.acc)
+            kacc = torch.float64 if Xk.dtype == torch.float64 else torch.float32
+            nparts = max(1, min(512, math.ceil(n / (gk.WPB * 16))))
+            partials = torch.zeros((nparts, self.d + 2), dtype=kacc, device=self.dev)
+            stage1 = torch.zeros((gk.stage1_rows(nparts), self.d + 2), dtype=kacc, device=self.dev)
+            fb = torch.zeros(self.d + 2, dtype=kacc, device=self.dev)
+            state = torch.tensor([0, 1, 1, 0, 0, 0, 0, 0], dtype=torch.int32, device=self.dev)
+            coef = self.coef.to(kacc).contiguous()
+            gk.grad_partials(Xk, y.to(kacc).contiguous(), None, coef, n, gk.LOSS_CODES["ftrl"], state, partials,
+                             nparts)
+            gk.reduce_only(partials, nparts, self.d, stage1, fb, state)
+            payload[: self.d] = fb[: self.d].to(self.acc)
+            payload[self.d:] = fb[self.d].to(self.acc)
+            return payload
+        Xf = X.to(self.acc)
+        mult = torch.sigmoid(Xf @ self.coef) - y
+        payload[: self.d] = mult @ Xf
+        payload[self.d:] = float(n)
+        return payload
+
+    def step(self, batch: Table):
+        payload = comm.all_reduce_sum(self.local_gradient(batch))
+        grad, wsum = payload[: self.d], payload[self.d:]
+        if self.dev.type == "cuda":
+            native.call("fmlx_ftrl_update", int(self.acc == torch.float64), native.ptr(grad), native.ptr(wsum),
+                        native.ptr(self.coef), native.ptr(self.z), native.ptr(self.n), self.d, self.alpha,
+                        self.beta, self.l1, self.l2, native.stream_ptr(self.dev))
+        else:
+            ftrl_update_torch(grad, wsum, self.coef, self.z, self.n, self.alpha, self.beta, self.l1, self.l2)
+        self.version += 1
+        return (DenseVector(self.coef.to(torch.float64).cpu().numpy()), self.version)
+
+
+def ftrl_update_torch(grad, wsum, coef, z, n, alpha, beta, l1, l2):
+    g = torch.where(wsum != 0, grad / torch.where(wsum != 0, wsum, torch.ones_like(wsum)), grad)
+    sigma = (torch.sqrt(n + g * g) - torch.sqrt(n)) / alpha
+    z += g - sigma * coef
+    n += g * g
+    new = (torch.where(z < 0, -torch.ones_like(z), torch.ones_like(z)) * l1 - z) / ((beta + torch.sqrt(n)) / alpha + l2)
+    coef.copy_(torch.where(z.abs() <= l1, torch.zeros_like(z), new))
+
+
+class _OnlineModelMixin:
+    """Prediction against a versioned model stream, with the modelDataVersion gauge."""
+
+    _GAUGE_SCOPE = "OnlineModel"
+
+    def _init_online(self):
+        self._stream: Optional[VersionedModelStream] = None
+        self._static_version = None
+        MetricGroup(self._GAUGE_SCOPE + "@%x" % id(self)).gauge("modelDataVersion", self.model_data_version)
+
+    def model_data_version(self) -> int:
+        v = self._current(block=False)
+        return 0 if v is None else self._version_of(v)
+
+    def _current(self, block=True):
+        if self._stream is not None:
+            self._stream.drain_available()
+            return self._stream.latest(block_until_first=block)
+        return self._static_version
+
+    def transform(self, *inputs):
+        inp = inputs[0]
+        if isinstance(inp, (StreamTable, InMemorySource)):
+            return [StreamTable(self._predict_batch(t) for t in _as_stream(inp))]
+        return [self._predict_batch(inp)]
+
+
+@rw.register_stage
+class OnlineLogisticRegressionModel(_OnlineModelMixin, ModelWithData, OnlineLogisticRegressionModelParams):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.classification.logisticregression.OnlineLogisticRegressionModel"
+    MODEL_DATA_COLUMNS = ("coefficient", "modelVersion")
+    encode_record = staticmethod(LogisticRegressionModel.encode_record)
+    decode_record = staticmethod(LogisticRegressionModel.decode_record)
+    _GAUGE_SCOPE = "OnlineLogisticRegressionModel"
+
+    def __init__(self):
+        super().__init__()
+        self._init_online()
+
+    @staticmethod
+    def _version_of(v):
+        return int(v[1])
+
+    def set_model_data(self, *inputs):
+        inp = inputs[0]
+        if isinstance(inp, VersionedModelStream):
+            self._stream = inp
+            self._md_table = None
+        else:
+            super().set_model_data(inp)
+            rows = inp.rows()
+            self._static_version = rows[-1] if rows else None
+        return self
+
+    def get_model_data(self):
+        if self._stream is not None:
+            s = self._stream
+
+            def gen():
+                i = 0
+                while True:
+                    while i >= len(s.versions):
+                        if not s.pull(block=True):
+                            return
+                    yield Table.from_rows([s.versions[i]], list(self.MODEL_DATA_COLUMNS))
+                    i += 1
+            return [StreamTable(gen())]
+        return super().get_model_data()
+
+    def model_data_rows(self):
+        if self._stream is not None:
+            self._stream.drain_available()
+            return [self._stream.latest()]
+        return super().model_data_rows()
+
+    def _predict_batch(self, t: Table) -> Table:
+        ver = self._current(block=True)
+        coef = torch.as_tensor(ver[0].values, dtype=torch.float64)
+        X = config.features_for_compute(t, self.get(self.FEATURES_COL))
+        if isinstance(X, SparseColumn):
+            pred, raw = gk.predict_csr(X.indptr, X.indices, X.values, coef, len(X), gk.MODE_LR)
+        else:
+            pred, raw = gk.predict_dense(X, coef, gk.MODE_LR)
+        return t.with_columns({self.get(self.PREDICTION_COL): pred, self.get(self.RAW_PREDICTION_COL): raw,
+                               self.get(self.MODEL_VERSION_COL): torch.full((t.num_rows,), int(ver[1]),
+                                                                             dtype=torch.int64)})
+
+
+@rw.register_stage
+class OnlineLogisticRegression(Estimator, OnlineLogisticRegressionParams):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.classification.logisticregression.OnlineLogisticRegression"
+
+    def __init__(self):
+        super().__init__()
+        self._init_md = None
+
+    def set_initial_model_data(self, table: Table):
+        self._init_md = table
+        return self
+
+    setInitialModelData = set_initial_model_data
+
+    def fit(self, *inputs) -> OnlineLogisticRegressionModel:
+        if self._init_md is None:
+            raise ValueError("OnlineLogisticRegression needs set_initial_model_data(...)")
+        from ..parallel.context import get_context
+
+        if get_context().world_size > self.get(self.GLOBAL_BATCH_SIZE):
+            raise ValueError("There are more subtasks in the training process than the number of elements in "
+                             "each batch. Some subtasks might be idling forever.")
+        coef0 = self._init_md.rows()[0][0].to_dense().values
+        reg, en = self.get(self.REG), self.get(self.ELASTIC_NET)
+        trainer = FtrlTrainer(coef0, self.get(self.ALPHA), self.get(self.BETA), en * reg, (1 - en) * reg,
+                              self.get(self.FEATURES_COL), self.get(self.LABEL_COL), self.get(self.WEIGHT_COL))
+        src = inputs[0]
+        stream = VersionedModelStream(src if not isinstance(src, Table) else StreamTable.from_table(src, 1 << 30),
+                                      self.get(self.GLOBAL_BATCH_SIZE), trainer.step)
+        model = OnlineLogisticRegressionModel().set_model_data(stream)
+        rw_update(model, self)
+        return model
+
+    def save(self, path: str) -> None:
+        rw.save_metadata(self, path)
+        if self._init_md is not None:
+            rw.save_model_data(path, self._init_md.rows(), LogisticRegressionModel.encode_record)
+
+    @classmethod
+    def load(cls, path: str):
+        est = rw.load_stage_param(path)
+        import os
+
+        if os.path.isdir(rw.data_path(path)):
+            rows = rw.load_model_data(path, LogisticRegressionModel.decode_record)
+            est.set_initial_model_data(Table.from_rows(rows, ["coefficient", "modelVersion"]))
+        return est
+
+
+# ==============================================================================================
+# OnlineKMeans
+# ==============================================================================================
+class OnlineKMeansModelParams(HasDistanceMeasure, HasFeaturesCol, HasPredictionCol):
+    K = IntParam("k", "The max number of clusters to create.", 2, ParamValidators.gt(1))
+
+
+class OnlineKMeansParams(HasBatchStrategy, HasGlobalBatchSize, HasDecayFactor, HasSeed, OnlineKMeansModelParams):
+    pass
+
+
+def generate_random_kmeans_model_data(k: int, dim: int, weight: float, seed: int) -> Table:
+    """``KMeansModelData.generateRandomModelData`` (java.util.Random(seed).nextDouble per value)."""
+    r = JavaRandom(seed)
+    cents = [DenseVector([r.next_double() for _ in range(dim)]) for _ in range(k)]
+    return KMeansModel.make_model_data_table([(cents, DenseVector(np.full(k, weight)))])
+
+
+class OnlineKMeansTrainer:
+    def __init__(self, cents: np.ndarray, weights: np.ndarray, k: int, metric: str, decay: float, fcol: str):
+        self.k, self.metric, self.decay, self.fcol = k, metric, decay, fcol
+        self.C = torch.as_tensor(cents, dtype=torch.float64)
+        self.W = torch.as_tensor(weights, dtype=torch.float64)
+
+    def step(self, batch: Table):
+        """Local decayed update (OnlineKMeans.java:292-321) then weight-averaged global merge (:188-211)
+        as one all-reduce of [Σ c·w | Σ w]."""
+        from ..parallel.context import get_context
+
+        P = get_context().world_size
+        X = config.features_for_compute(batch, self.fcol, allow_sparse=False)
+        kc, D = self.C.shape
+        if X.device.type == "cuda" and X.shape[0] > 0:
+            acc = torch.float64 if X.dtype == torch.float64 else torch.float32
+            cb = kk.CentroidBuffers(kc, D, X.device, acc)
+            cb.set(self.C)
+            rnd = kk.KMeansRound(X, kc, self.metric)
+            payload = rnd.run(cb).to(torch.float64).cpu()
+        else:
+            payload = kk.torch_round_payload(X.cpu() if X.shape[0] else X.cpu(), self.C, self.metric)
+        sums = payload[: kc * D].reshape(kc, D)
+        counts = payload[kc * D:]
+        C = self.C.clone()
+        W = self.W * (self.decay / P)
+        nz = counts > 0
+        W = torch.where(nz, W + counts, W)
+        lam = torch.where(nz, counts / torch.where(nz, W, torch.ones_like(W)), torch.zeros_like(W))
+        C = torch.where(nz[:, None], C * (1.0 - lam)[:, None] + sums * (lam / torch.where(nz, counts, torch.ones_like(
+            counts)))[:, None], C)
+        merged = comm.all_reduce_sum(torch.cat([(C * W[:, None]).reshape(-1), W]))
+        Wt = merged[kc * D:]
+        self.C = merged[: kc * D].reshape(kc, D) / torch.clamp(Wt, min=1e-16)[:, None]
+        self.W = Wt
+        return ([DenseVector(c) for c in self.C.numpy()], DenseVector(self.W.numpy()))
+
+
+@rw.register_stage
+class OnlineKMeansModel(_OnlineModelMixin, ModelWithData, OnlineKMeansModelParams):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.clustering.kmeans.OnlineKMeansModel"
+    MODEL_DATA_COLUMNS = ("centroids", "weights")
+    encode_record = staticmethod(_encode_kmeans)
+    decode_record = staticmethod(_decode_kmeans)
+    _GAUGE_SCOPE = "OnlineKMeansModel"
+    make_model_data_table = KMeansModel.make_model_data_table
+
+    def __init__(self):
+        super().__init__()
+        self._init_online()
+
+    def _version_of(self, v):
+        if self._stream is not None:
+            return len(self._stream.versions)
+        return 1
+
+    def set_model_data(self, *inputs):
+        inp = inputs[0]
+        if isinstance(inp, VersionedModelStream):
+            self._stream = inp
+        else:
+            super().set_model_data(inp)
+            self._static_version = inp.rows()[-1]
+        return self
+
+    def model_data_rows(self):
+        if self._stream is not None:
+            self._stream.drain_available()
+            return [self._stream.latest()]
+        return super().model_data_rows()
+
+    def _predict_batch(self, t: Table) -> Table:
+        ver = self._current(block=True)
+        C = torch.as_tensor(np.stack([c.to_array() for c in ver[0]]), dtype=torch.float64)
+        X = config.features_for_compute(t, self.get(self.FEATURES_COL), allow_sparse=False)
+        metric = self.get(self.DISTANCE_MEASURE)
+        if X.device.type == "cuda":
+            cb = kk.CentroidBuffers(C.shape[0], C.shape[1], X.device,
+                                    torch.float64 if X.dtype == torch.float64 else torch.float32)
+            cb.set(C)
+            pred = kk.assign(X, cb, metric).to(torch.int64)
+        else:
+            pred = kk.torch_assign(X, C, metric)
+        return t.with_column(self.get(self.PREDICTION_COL), pred)
+
+
+@rw.register_stage
+class OnlineKMeans(Estimator, OnlineKMeansParams):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.clustering.kmeans.OnlineKMeans"
+
+    def __init__(self):
+        super().__init__()
+        self._init_md = None
+
+    def set_initial_model_data(self, table: Table):
+        self._init_md = table
+        return self
+
+    setInitialModelData = set_initial_model_data
+
+    def fit(self, *inputs) -> OnlineKMeansModel:
+        if self._init_md is None:
+            raise ValueError("OnlineKMeans needs set_initial_model_data(...)")
+        cents, weights = self._init_md.rows()[0]
+        C = np.stack([c.to_array() for c in cents])
+        if C.shape[0] != self.get(self.K):
+            raise ValueError("initial model data must have k centroids")
+        tr = OnlineKMeansTrainer(C, weights.to_array(), self.get(self.K), self.get(self.DISTANCE_MEASURE),
+                                 self.get(self.DECAY_FACTOR), self.get(self.FEATURES_COL))
+        src = inputs[0]
+        stream = VersionedModelStream(src if not isinstance(src, Table) else StreamTable.from_table(src, 1 << 30),
+                                      self.get(self.GLOBAL_BATCH_SIZE), tr.step,
+                                      initial_versions=[(list(cents), weights)])
+        model = OnlineKMeansModel().set_model_data(stream)
+        rw_update(model, self)
+        return model
+
+    def save(self, path: str) -> None:
+        rw.save_metadata(self, path)
+        if self._init_md is not None:
+            rw.save_model_data(path, self._init_md.rows(), _encode_kmeans)
+
+    @classmethod
+    def load(cls, path: str):
+        import os
+
+        est = rw.load_stage_param(path)
+        if os.path.isdir(rw.data_path(path)):
+            rows = rw.load_model_data(path, _decode_kmeans)
+            est.set_initial_model_data(KMeansModel.make_model_data_table(rows))
+        return est

@@ -26,7 +26,7 @@
 
 namespace {
 
-enum { LOSS_LOGISTIC = 0, LOSS_HINGE = 1, LOSS_LSQ = 2 };
+enum { LOSS_LOGISTIC = 0, LOSS_HINGE = 1, LOSS_LSQ = 2, LOSS_FTRL = 3 };
 enum { ST_ROUND = 0, ST_RUN0 = 1, ST_ARRIVE = 3, ST_EXECUTED = 4 };
 
 template <typename A>
@@ -42,6 +42,11 @@ __device__ __forceinline__ void loss_and_mult(int loss, A dot, A y, A wt, A& l, 
     A ys = (A)2 * y - (A)1;
     A h = (A)1 - ys * dot;
     if (h > (A)0) { l = wt * h; m = -ys * wt; } else { l = (A)0; m = (A)0; }
+  } else if (loss == LOSS_FTRL) {
+    // OnlineLogisticRegression local gradient (OnlineLogisticRegression.java:344-368, dense
+    // branch): (sigmoid(dot) - label) · x, weight ignored; the weight slot counts rows.
+    m = (A)1 / ((A)1 + exp(-dot)) - y;
+    l = (A)0;
   } else {
     A r = dot - y;
     l = wt * (A)0.5 * r * r;

@@ -13,7 +13,7 @@ import torch
 
 from . import native
 
-LOSS_CODES = {"logistic": 0, "hinge": 1, "leastsquare": 2}
+LOSS_CODES = {"logistic": 0, "hinge": 1, "leastsquare": 2, "ftrl": 3}
 MAX_CPL = 8
 WPB = 8
 # rows in flight per wave = 2*GRAD_UNROLL (0 = kernel default for the shape); tunable for A/B runs
