@@ -7,3 +7,5 @@ from .kmeans import KMeans, KMeansModel  # noqa: F401,E402
 from . import online  # noqa: F401,E402
 from .online import (OnlineKMeans, OnlineKMeansModel, OnlineLogisticRegression,  # noqa: F401,E402
                      OnlineLogisticRegressionModel)
+from . import feature  # noqa: F401,E402
+from .feature import *  # noqa: F401,F403,E402

@@ -1,0 +1,9 @@
+"""Feature engineering stages (reference flink-ml-lib ``org.apache.flink.ml.feature``)."""
+from . import scalers, text, vector_ops  # noqa: F401
+from .scalers import (MaxAbsScaler, MaxAbsScalerModel, MinMaxScaler, MinMaxScalerModel,  # noqa: F401
+                      RobustScaler, RobustScalerModel, StandardScaler, StandardScalerModel,
+                      VarianceThresholdSelector, VarianceThresholdSelectorModel)
+from .text import (IDF, CountVectorizer, CountVectorizerModel, FeatureHasher, HashingTF,  # noqa: F401
+                   IDFModel, NGram, RegexTokenizer, StopWordsRemover, Tokenizer)
+from .vector_ops import (DCT, Binarizer, Bucketizer, ElementwiseProduct, Interaction,  # noqa: F401
+                         Normalizer, PolynomialExpansion, VectorAssembler, VectorSlicer)

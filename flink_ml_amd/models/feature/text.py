@@ -1,0 +1,430 @@
+"""Text / hashing feature stages (reference ``LIB/feature/{tokenizer,regextokenizer,ngram,
+stopwordsremover,hashingtf,featurehasher,countvectorizer,idf}``).
+
+String handling is host-side (columns of Python lists); the hashing (Guava murmur3_32, K18) runs in
+the native host library or, for large batches, in the device kernel (``hash.hip``). Numeric
+outputs (term-frequency vectors, IDF weighting) are device-resident sparse/dense columns.
+"""
+from __future__ import annotations
+
+import functools
+import json
+import math
+import os
+import re
+from collections import Counter
+from typing import Dict, List, Sequence
+
+import numpy as np
+import torch
+
+from ...api.stage import Estimator, Transformer
+from ...common.param import (HasCategoricalCols, HasInputCol, HasInputCols, HasNumFeatures, HasOutputCol,
+                             HasOutputCols)
+from ...io import read_write as rw
+from ...io import serialization as ser
+from ...linalg.vectors import DenseVector, SparseVector, Vector
+from ...ops import hashing
+from ...param.param import (BooleanParam, FloatParam, IntParam, ParamValidators, StringArrayParam, StringParam)
+from ...parallel import comm
+from ...table import SparseColumn, Table
+from ...utils.java import java_string_hash
+from ..base import ModelWithData
+from ..linear import rw_update
+from .common import dec_dense, enc_dense, vector_input
+
+ENGLISH_STOP_WORDS = (
+    'a', 'about', 'above', 'after', 'again', 'against', 'all', 'am', 'an', 'and', 'any', 'are', "aren't",
+    'as', 'at', 'be', 'because', 'been', 'before', 'being', 'below', 'between', 'both', 'but', 'by', 'can',
+    "can't", 'cannot', 'could', "couldn't", 'did', "didn't", 'do', 'does', "doesn't", 'doing', 'don',
+    "don't", 'down', 'during', 'each', 'few', 'for', 'from', 'further', 'had', "hadn't", 'has', "hasn't",
+    'have', "haven't", 'having', 'he', "he'd", "he'll", "he's", 'her', 'here', "here's", 'hers', 'herself',
+    'him', 'himself', 'his', 'how', "how's", 'i', "i'd", "i'll", "i'm", "i've", 'if', 'in', 'into', 'is',
+    "isn't", 'it', "it's", 'its', 'itself', 'just', "let's", 'me', 'more', 'most', "mustn't", 'my', 'myself',
+    'no', 'nor', 'not', 'now', 'of', 'off', 'on', 'once', 'only', 'or', 'other', 'ought', 'our', 'ours',
+    'ourselves', 'out', 'over', 'own', 's', 'same', "shan't", 'she', "she'd", "she'll", "she's", 'should',
+    "shouldn't", 'so', 'some', 'such', 't', 'than', 'that', "that's", 'the', 'their', 'theirs', 'them',
+    'themselves', 'then', 'there', "there's", 'these', 'they', "they'd", "they'll", "they're", "they've",
+    'this', 'those', 'through', 'to', 'too', 'under', 'until', 'up', 'very', 'was', "wasn't", 'we', "we'd",
+    "we'll", "we're", "we've", 'were', "weren't", 'what', "what's", 'when', "when's", 'where', "where's",
+    'which', 'while', 'who', "who's", 'whom', 'why', "why's", 'will', 'with', "won't", 'would', "wouldn't",
+    'you', "you'd", "you'll", "you're", "you've", 'your', 'yours', 'yourself', 'yourselves',
+)
+
+
+def java_split(pattern: str, s: str) -> List[str]:
+    """``String.split(regex)``: trailing empty strings removed, no leading empty string for a
+    zero-width match at position 0, ``"".split(x) == [""]``."""
+    if s == "":
+        return [""]
+    parts = re.split(pattern, s)
+    m = re.match(pattern, s)
+    if m is not None and m.end() == 0 and parts and parts[0] == "":
+        parts = parts[1:]
+    while parts and parts[-1] == "":
+        parts.pop()
+    return parts
+
+
+def java_hashmap_order(keys: Sequence[str]) -> List[str]:
+    """Iteration order of a ``java.util.HashMap<String, _>`` filled in ``keys`` order (no
+    treeified bins): by bucket index of the final table, then insertion order."""
+    cap, size = 16, 0
+    for _ in keys:
+        size += 1
+        if size > cap * 0.75:
+            cap *= 2
+
+    def bucket(k):
+        h = java_string_hash(k) & 0xFFFFFFFF
+        return (h ^ (h >> 16)) & (cap - 1)
+
+    return [k for _, _, k in sorted((bucket(k), i, k) for i, k in enumerate(keys))]
+
+
+def _strings_col(t: Table, col: str) -> list:
+    return t.get_list(col)
+
+
+# ------------------------------------------------------------------------------------ Tokenizer
+@rw.register_stage
+class Tokenizer(Transformer, HasInputCol, HasOutputCol):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.tokenizer.Tokenizer"
+
+    def transform(self, *inputs):
+        t = inputs[0]
+        out = [java_split(r"\s", s.lower()) for s in _strings_col(t, self.get(self.INPUT_COL))]
+        return [t.with_column(self.get(self.OUTPUT_COL), out)]
+
+
+@rw.register_stage
+class RegexTokenizer(Transformer, HasInputCol, HasOutputCol):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.regextokenizer.RegexTokenizer"
+    MIN_TOKEN_LENGTH = IntParam("minTokenLength", "Minimum token length", 1, ParamValidators.gt_eq(0))
+    GAPS = BooleanParam("gaps", "Set regex to match gaps or tokens", True)
+    PATTERN = StringParam("pattern", "Regex pattern used for tokenizing", "\\s+")
+    TO_LOWERCASE = BooleanParam("toLowercase", "Whether to convert all characters to lowercase before tokenizing",
+                                True)
+
+    def transform(self, *inputs):
+        t = inputs[0]
+        pat = re.compile(self.get(self.PATTERN))
+        gaps, low, mn = self.get(self.GAPS), self.get(self.TO_LOWERCASE), self.get(self.MIN_TOKEN_LENGTH)
+        out = []
+        for s in _strings_col(t, self.get(self.INPUT_COL)):
+            s = s.lower() if low else s
+            toks = java_split(pat.pattern, s) if gaps else [m.group(0) for m in pat.finditer(s)]
+            out.append([x for x in toks if len(x) >= mn])
+        return [t.with_column(self.get(self.OUTPUT_COL), out)]
+
+
+@rw.register_stage
+class NGram(Transformer, HasInputCol, HasOutputCol):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.ngram.NGram"
+    N = IntParam("n", "Number of elements per n-gram (>=1).", 2, ParamValidators.gt_eq(1))
+
+    def transform(self, *inputs):
+        t = inputs[0]
+        n = self.get(self.N)
+        out = [[" ".join(toks[i:i + n]) for i in range(len(toks) - n + 1)]
+               for toks in _strings_col(t, self.get(self.INPUT_COL))]
+        return [t.with_column(self.get(self.OUTPUT_COL), out)]
+
+
+# ------------------------------------------------------------------------------------ StopWordsRemover
+_AVAILABLE_LOCALES = ("en_US", "en", "en_GB", "fr_FR", "de_DE", "es_ES", "it_IT", "pt_PT", "nl_NL", "sv_SE",
+                      "da_DK", "fi_FI", "hu_HU", "nb_NO", "ru_RU", "tr_TR", "zh_CN", "ja_JP")
+
+
+def _default_locale() -> str:
+    return "en_US"
+
+
+@functools.lru_cache(maxsize=1)
+def _stopword_corpus() -> dict:
+    path = os.path.join(os.path.dirname(__file__), "..", "..", "resources", "stopwords.json")
+    with open(path, encoding="utf-8") as f:
+        return json.load(f)["languages"]
+
+
+@rw.register_stage
+class StopWordsRemover(Transformer, HasInputCols, HasOutputCols):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.stopwordsremover.StopWordsRemover"
+    STOP_WORDS = StringArrayParam("stopWords", "The words to be filtered out.", ENGLISH_STOP_WORDS,
+                                  ParamValidators.non_empty_array())
+    CASE_SENSITIVE = BooleanParam("caseSensitive", "Whether to do a case-sensitive comparison over the stop words.",
+                                  False)
+    LOCALE = StringParam("locale", "Locale of the input for case insensitive matching. Ignored when caseSensitive is "
+                         "true.", _default_locale(), ParamValidators.in_array(_AVAILABLE_LOCALES))
+    SUPPORTED_LANGUAGES = ("danish", "dutch", "english", "finnish", "french", "german", "hungarian", "italian",
+                           "norwegian", "portuguese", "russian", "spanish", "swedish", "turkish")
+
+    @staticmethod
+    def load_default_stop_words(language: str):
+        """Default stop words of ``language`` (StopWordsRemover.java loadDefaultStopWords); the
+        lists are the Snowball corpus bundled in ``resources/stopwords.json``."""
+        lang = language.lower()
+        if lang not in StopWordsRemover.SUPPORTED_LANGUAGES:
+            raise ValueError("%s is not in the supported language list: %s."
+                             % (language, list(StopWordsRemover.SUPPORTED_LANGUAGES)))
+        if lang == "english":
+            return list(ENGLISH_STOP_WORDS)
+        return list(_stopword_corpus()[lang])
+
+    @staticmethod
+    def get_default_or_us() -> str:
+        return _default_locale()
+
+    @staticmethod
+    def get_available_locales():
+        return set(_AVAILABLE_LOCALES)
+
+    @staticmethod
+    def load_stop_words_file(path: str):
+        with open(path, encoding="utf-8") as f:
+            return [l.strip() for l in f if l.strip()]
+
+    def transform(self, *inputs):
+        t = inputs[0]
+        ins, outs = self.get(self.INPUT_COLS), self.get(self.OUTPUT_COLS)
+        if len(ins) != len(outs):
+            raise ValueError("The number of input columns and output columns must be equal.")
+        cs = self.get(self.CASE_SENSITIVE)
+        sw = set(self.get(self.STOP_WORDS)) if cs else {w.lower() for w in self.get(self.STOP_WORDS)}
+        res = {}
+        for c, o in zip(ins, outs):
+            res[o] = [[w for w in toks if (w if cs else (w.lower() if w is not None else w)) not in sw]
+                      for toks in _strings_col(t, c)]
+        return [t.with_columns(res)]
+
+
+# ------------------------------------------------------------------------------------ HashingTF
+@rw.register_stage
+class HashingTF(Transformer, HasInputCol, HasOutputCol, HasNumFeatures):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.hashingtf.HashingTF"
+    BINARY = BooleanParam("binary", "Whether each dimension of the output vector is binary or not.", False)
+
+    def transform(self, *inputs):
+        t = inputs[0]
+        nf, binary = self.get(self.NUM_FEATURES), self.get(self.BINARY)
+        docs = _strings_col(t, self.get(self.INPUT_COL))
+        flat, lens = [], []
+        for d in docs:
+            if isinstance(d, str) or not hasattr(d, "__iter__"):
+                raise ValueError("Input format %s is not supported for input column %s. Supported options are "
+                                 "Array and Iterable." % (type(d).__name__, self.get(self.INPUT_COL)))
+            d = list(d)
+            flat.extend(d)
+            lens.append(len(d))
+        if flat and all(isinstance(x, str) for x in flat):
+            h = hashing.hash_strings(flat)
+        else:
+            h = np.array([hashing.hash_object(x) for x in flat], dtype=np.int32)
+        idx = hashing.non_negative_mod(h, nf)
+        out, pos = [], 0
+        for L in lens:
+            cnt = Counter(idx[pos:pos + L].tolist())
+            pos += L
+            keys = sorted(cnt)
+            out.append(SparseVector(nf, keys, [1.0 if binary else float(cnt[k]) for k in keys]))
+        col = SparseColumn.from_vectors(out, nf) if out else out
+        return [t.with_column(self.get(self.OUTPUT_COL), col)]
+
+
+# ------------------------------------------------------------------------------------ FeatureHasher
+@rw.register_stage
+class FeatureHasher(Transformer, HasInputCols, HasOutputCol, HasCategoricalCols, HasNumFeatures):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.featurehasher.FeatureHasher"
+
+    def transform(self, *inputs):
+        t = inputs[0]
+        nf = self.get(self.NUM_FEATURES)
+        ins = list(self.get(self.INPUT_COLS))
+        cats = list(self.get(self.CATEGORICAL_COLS))
+        if cats and not set(cats) <= set(ins):
+            raise ValueError("CategoricalCols must be included in inputCols!")
+        lists = {c: t.get_list(c) for c in ins}
+
+        def is_cat(c):
+            if c in cats:
+                return True
+            vals = [v for v in lists[c] if v is not None]
+            return bool(vals) and all(isinstance(v, (str, bool, np.bool_)) for v in vals)
+
+        cat_cols = [c for c in ins if is_cat(c)]
+        num_cols = [c for c in ins if c not in cat_cols]
+        keys, vals, owners = [], [], []
+        for r in range(t.num_rows):
+            for c in num_cols:
+                v = lists[c][r]
+                if v is not None:
+                    keys.append(c)
+                    vals.append(float(v))
+                    owners.append(r)
+            for c in cat_cols:
+                v = lists[c][r]
+                if v is not None:
+                    sv = ("true" if v else "false") if isinstance(v, (bool, np.bool_)) else str(v)
+                    keys.append(c + "=" + sv)
+                    vals.append(1.0)
+                    owners.append(r)
+        h = hashing.hash_strings(keys).astype(np.int64)
+        h = np.where(h == -(1 << 31), h, np.abs(h))  # Math.abs(Integer.MIN_VALUE) stays negative
+        idx = np.mod(h, nf)
+        per_row: List[Dict[int, float]] = [dict() for _ in range(t.num_rows)]
+        for r, i, v in zip(owners, idx.tolist(), vals):
+            per_row[r][i] = per_row[r].get(i, 0.0) + v
+        out = [SparseVector(nf, sorted(m), [m[k] for k in sorted(m)]) for m in per_row]
+        return [t.with_column(self.get(self.OUTPUT_COL), SparseColumn.from_vectors(out, nf) if out else out)]
+
+
+# ------------------------------------------------------------------------------------ CountVectorizer
+class CountVectorizerModelParams(HasInputCol, HasOutputCol):
+    MIN_TF = FloatParam("minTF", "Filter to ignore rare words in a document.", 1.0, ParamValidators.gt_eq(0.0))
+    BINARY = BooleanParam("binary", "Binary toggle to control the output vector values.", False)
+
+
+class CountVectorizerParams(CountVectorizerModelParams):
+    VOCABULARY_SIZE = IntParam("vocabularySize", "Max size of the vocabulary.", 1 << 18, ParamValidators.gt(0))
+    MIN_DF = FloatParam("minDF", "Minimum number of different documents a term must appear in.", 1.0,
+                        ParamValidators.gt_eq(0.0))
+    MAX_DF = FloatParam("maxDF", "Maximum number of different documents a term could appear in.", float(2 ** 63 - 1),
+                        ParamValidators.gt_eq(0.0))
+
+
+@rw.register_stage
+class CountVectorizerModel(ModelWithData, CountVectorizerModelParams):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.countvectorizer.CountVectorizerModel"
+    MODEL_DATA_COLUMNS = ("vocabulary",)
+
+    @staticmethod
+    def encode_record(out, row):
+        ser.write_string_array(out, list(row[0]))
+
+    @staticmethod
+    def decode_record(inp):
+        return (ser.read_string_array(inp),)
+
+    @classmethod
+    def make_model_data_table(cls, rows):
+        return Table({"vocabulary": [list(r[0]) for r in rows]}, num_rows=len(rows))
+
+    def transform(self, *inputs):
+        t = inputs[0]
+        vocab = self.model_data_rows()[0][0]
+        index = {w: i for i, w in enumerate(vocab)}
+        min_tf, binary = self.get(self.MIN_TF), self.get(self.BINARY)
+        out = []
+        for doc in _strings_col(t, self.get(self.INPUT_COL)):
+            cnt = Counter(index[w] for w in doc if w in index)
+            thr = min_tf if min_tf >= 1.0 else len(doc) * min_tf
+            keys = sorted(k for k, c in cnt.items() if c >= thr)
+            out.append(SparseVector(len(vocab), keys, [1.0 if binary else float(cnt[k]) for k in keys]))
+        return [t.with_column(self.get(self.OUTPUT_COL), SparseColumn.from_vectors(out, len(vocab)) if out else out)]
+
+
+@rw.register_stage
+class CountVectorizer(Estimator, CountVectorizerParams):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.countvectorizer.CountVectorizer"
+
+    def fit(self, *inputs):
+        docs = _strings_col(inputs[0], self.get(self.INPUT_COL))
+        order, tf, df = [], {}, {}
+        for doc in docs:
+            for w, c in Counter(doc).items():
+                if w not in tf:
+                    order.append(w)
+                    tf[w], df[w] = 0, 0
+                tf[w] += c
+                df[w] += 1
+        parts = comm.all_gather_object((len(docs), order, tf, df))
+        rows = sum(p[0] for p in parts)
+        if rows == 0:
+            raise RuntimeError("The training set is empty.")
+        g_order, g_df = [], {}
+        for _, o, _tf, d in parts:
+            for w in o:
+                if w not in g_df:
+                    g_order.append(w)
+                    g_df[w] = 0
+                g_df[w] += d[w]
+        min_df, max_df = self.get(self.MIN_DF), self.get(self.MAX_DF)
+        keys = java_hashmap_order(g_order)
+        if min_df != self.MIN_DF.default_value or max_df != self.MAX_DF.default_value:
+            amin = min_df if min_df >= 1.0 else min_df * rows
+            amax = max_df if max_df >= 1.0 else max_df * rows
+            if amax < amin:
+                raise RuntimeError("maxDF must be >= minDF.")
+            keys = java_hashmap_order([k for k in keys if amin <= g_df[k] <= amax])
+        keys = sorted(keys, key=lambda k: -g_df[k])  # stable, like List.sort
+        vocab = keys[: self.get(self.VOCABULARY_SIZE)]
+        m = CountVectorizerModel().set_model_data(CountVectorizerModel.make_model_data_table([(vocab,)]))
+        rw_update(m, self)
+        return m
+
+
+# ------------------------------------------------------------------------------------ IDF
+class IDFModelParams(HasInputCol, HasOutputCol):
+    pass
+
+
+@rw.register_stage
+class IDFModel(ModelWithData, IDFModelParams):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.idf.IDFModel"
+    MODEL_DATA_COLUMNS = ("idf", "docFreq", "numDocs")
+
+    @staticmethod
+    def encode_record(out, row):
+        enc_dense(out, row[0])
+        ser.write_long_array(out, row[1])
+        out.write_long(int(row[2]))
+
+    @staticmethod
+    def decode_record(inp):
+        return (dec_dense(inp), list(ser.read_long_array(inp)), inp.read_long())
+
+    @classmethod
+    def make_model_data_table(cls, rows):
+        return Table({"idf": [r[0] for r in rows], "docFreq": [list(r[1]) for r in rows],
+                      "numDocs": torch.tensor([int(r[2]) for r in rows])}, num_rows=len(rows))
+
+    def transform(self, *inputs):
+        t = inputs[0]
+        idf = self.model_data_rows()[0][0]
+        X = vector_input(t, self.get(self.INPUT_COL))
+        if isinstance(X, SparseColumn):
+            w = torch.as_tensor(idf.values, dtype=torch.float64, device=X.values.device)
+            out = SparseColumn(X.indptr, X.indices, X.values.to(torch.float64) * w[X.indices.long()], X.size)
+        else:
+            w = torch.as_tensor(idf.values, dtype=torch.float64, device=X.device)
+            out = X.to(torch.float64) * w if X.device.type == "cpu" else X.float() * w.float()
+        return [t.with_column(self.get(self.OUTPUT_COL), out)]
+
+
+@rw.register_stage
+class IDF(Estimator, IDFModelParams):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.idf.IDF"
+    MIN_DOC_FREQ = IntParam("minDocFreq", "Minimum number of documents that a term should appear for filtering.", 0,
+                            ParamValidators.gt_eq(0))
+
+    def fit(self, *inputs):
+        t = inputs[0]
+        X = vector_input(t, self.get(self.INPUT_COL))
+        if isinstance(X, SparseColumn):
+            n = len(X)
+            df = torch.zeros(X.size, dtype=torch.float64, device=X.values.device)
+            df.index_add_(0, X.indices.long(), (X.values > 0).to(torch.float64))
+        else:
+            n = X.shape[0]
+            df = (X > 0).to(torch.float64).sum(0)
+        df = comm.all_reduce_sum(df)
+        n = int(comm.all_reduce_scalar(float(n), "sum"))
+        if n == 0:
+            raise RuntimeError("The training set is empty.")
+        keep = df >= self.get(self.MIN_DOC_FREQ)
+        idf = torch.where(keep, torch.log((n + 1) / (df + 1)), torch.zeros_like(df))
+        dfl = torch.where(keep, df, torch.zeros_like(df)).to(torch.int64)
+        m = IDFModel().set_model_data(IDFModel.make_model_data_table(
+            [(DenseVector(idf.cpu().numpy()), dfl.cpu().tolist(), n)]))
+        rw_update(m, self)
+        return m

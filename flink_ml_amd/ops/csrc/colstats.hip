@@ -1,0 +1,134 @@
+// Column statistics and per-column affine transforms.
+//
+// Reference hot loops: StandardScaler ComputeMetaOperator (sum, Σx², n — StandardScaler.java:75-140),
+// MinMaxScaler min/max (MinMaxScaler.java:88-98), MaxAbsScaler max|x| (MaxAbsScaler.java:78-82),
+// VarianceThresholdSelector (sum, Σx², n — VarianceThresholdSelector.java:73), and the per-row
+// Model.map functions that scale/offset each coordinate (StandardScalerModel, MinMaxScalerModel,
+// MaxAbsScalerModel, RobustScalerModel, ElementwiseProduct).
+//
+// MI355X design: one pass over the row-major [n, d] matrix; a block owns a contiguous row range
+// and each thread owns columns (c = tid, tid + 256, ...), so every row is read as one coalesced
+// segment. Accumulation in fp64 registers (exact enough for 10M-row sums); one fp64 partial
+// record [sum | sumsq | min | max] per block, combined in block order (deterministic) by a
+// second tiny kernel. The affine kernel fuses (x - sub) * mul + add per column.
+#include "common.h"
+
+namespace {
+
+template <typename T>
+__global__ __launch_bounds__(256) void colstats_partial_kernel(const T* __restrict__ X, long ld, long n, int d,
+                                                               long rows_per_block, double* __restrict__ part) {
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  long r1 = r0 + rows_per_block;
+  if (r1 > n) r1 = n;
+  double* out = part + (long)blockIdx.x * 4 * d;
+  for (int c = threadIdx.x; c < d; c += blockDim.x) {
+    double s = 0, q = 0, mn = __builtin_huge_val(), mx = -__builtin_huge_val();
+    long r = r0;
+    for (; r + 4 <= r1; r += 4) {
+      double v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = (double)Ld<T>::f(X[(r + u) * ld + c]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s += v[u];
+        q += v[u] * v[u];
+        mn = v[u] < mn ? v[u] : mn;
+        mx = v[u] > mx ? v[u] : mx;
+      }
+    }
+    for (; r < r1; ++r) {
+      const double v = (double)Ld<T>::f(X[r * ld + c]);
+      s += v;
+      q += v * v;
+      mn = v < mn ? v : mn;
+      mx = v > mx ? v : mx;
+    }
+    out[c] = s;
+    out[d + c] = q;
+    out[2 * d + c] = mn;
+    out[3 * d + c] = mx;
+  }
+}
+
+__global__ __launch_bounds__(256) void colstats_combine_kernel(const double* __restrict__ part, int nb, int d,
+                                                               double* __restrict__ res) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= d) return;
+  double s = 0, q = 0, mn = __builtin_huge_val(), mx = -__builtin_huge_val();
+  for (int b = 0; b < nb; ++b) {
+    const double* p = part + (long)b * 4 * d;
+    s += p[c];
+    q += p[d + c];
+    mn = p[2 * d + c] < mn ? p[2 * d + c] : mn;
+    mx = p[3 * d + c] > mx ? p[3 * d + c] : mx;
+  }
+  res[c] = s;
+  res[d + c] = q;
+  res[2 * d + c] = mn;
+  res[3 * d + c] = mx;
+}
+
+template <typename T, typename O>
+__global__ __launch_bounds__(256) void affine_cols_kernel(const T* __restrict__ X, long ld, long n, int d,
+                                                          const double* __restrict__ sub,
+                                                          const double* __restrict__ mul,
+                                                          const double* __restrict__ add, O* __restrict__ out) {
+  const long total = n * (long)d;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / d;
+    const int c = (int)(i - r * d);
+    double v = (double)Ld<T>::f(X[r * ld + c]);
+    if (sub) v -= sub[c];
+    if (mul) v *= mul[c];
+    if (add) v += add[c];
+    out[i] = (O)v;
+  }
+}
+
+template <typename T>
+int launch_stats(const void* X, long ld, long n, int d, double* part, int nb, double* res, hipStream_t s) {
+  const long rpb = (n + nb - 1) / nb;
+  hipLaunchKernelGGL(colstats_partial_kernel<T>, dim3(nb), dim3(256), 0, s, (const T*)X, ld, n, d, rpb, part);
+  hipLaunchKernelGGL(colstats_combine_kernel, dim3((d + 255) / 256), dim3(256), 0, s, part, nb, d, res);
+  return (int)hipGetLastError();
+}
+
+template <typename T, typename O>
+int launch_affine(const void* X, long ld, long n, int d, const double* sub, const double* mul, const double* add,
+                  void* out, hipStream_t s) {
+  long total = n * (long)d;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) return 0;
+  hipLaunchKernelGGL((affine_cols_kernel<T, O>), dim3(blocks), dim3(256), 0, s, (const T*)X, ld, n, d, sub, mul, add,
+                     (O*)out);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// part: scratch [nb][4][d] fp64; res: [4][d] fp64 = sum | sumsq | min | max
+FMLX_API int fmlx_colstats(int dtype, const void* X, long ld, long n, int d, double* part, int nb, double* res,
+                           void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (nb < 1) return -1;
+  if (dtype == DT_F32) return launch_stats<float>(X, ld, n, d, part, nb, res, s);
+  if (dtype == DT_F64) return launch_stats<double>(X, ld, n, d, part, nb, res, s);
+  if (dtype == DT_BF16) return launch_stats<bf16_t>(X, ld, n, d, part, nb, res, s);
+  return -1;
+}
+
+// out[r, c] = ((x - sub[c]) * mul[c]) + add[c]   (any of sub/mul/add may be null); out is dense [n, d]
+FMLX_API int fmlx_affine_cols(int dtype, int out_dtype, const void* X, long ld, long n, int d, const double* sub,
+                              const double* mul, const double* add, void* out, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == DT_F32 && out_dtype == DT_F32) return launch_affine<float, float>(X, ld, n, d, sub, mul, add, out, s);
+  if (dtype == DT_F64 && out_dtype == DT_F64)
+    return launch_affine<double, double>(X, ld, n, d, sub, mul, add, out, s);
+  if (dtype == DT_BF16 && out_dtype == DT_F32)
+    return launch_affine<bf16_t, float>(X, ld, n, d, sub, mul, add, out, s);
+  if (dtype == DT_F32 && out_dtype == DT_F64)
+    return launch_affine<float, double>(X, ld, n, d, sub, mul, add, out, s);
+  return -1;
+}

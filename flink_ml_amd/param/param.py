@@ -426,18 +426,37 @@ class WithParams:
                     if not rest[0].isupper():
                         continue
                     pname = rest[0].lower() + rest[1:]
-                p = params.get(pname)
+                p = _lookup_param(params, pname)
                 if p is None:
                     continue
                 if is_set:
+                    if isinstance(p, _ArrayParam):
+                        # variadic like the reference Python API: set_input_cols('a', 'b')
+                        def _set_arr(*values, _p=p):
+                            if len(values) == 1 and (values[0] is None or isinstance(
+                                    values[0], (list, tuple, np.ndarray))):
+                                return self.set(_p, values[0])
+                            return self.set(_p, values)
+                        return _set_arr
                     return lambda value, _p=p: self.set(_p, value)
                 return lambda _p=p: self.get(_p)
         # property-style access: obj.features_col
         pname = snake_to_camel(item)
-        p = params.get(pname)
+        p = _lookup_param(params, pname)
         if p is not None:
             return self.get(p)
         raise AttributeError("%s has no attribute %s" % (type(self).__name__, item))
+
+
+def _lookup_param(params: Dict[str, Param], name: str) -> Optional[Param]:
+    """Exact name first, then case-insensitive (``get_min_df`` -> ``minDF``)."""
+    p = params.get(name)
+    if p is None:
+        low = name.lower()
+        for k, v in params.items():
+            if k.lower() == low:
+                return v
+    return p
 
 
 def update_existing_params(target: WithParams, param_map: Dict[Param, Any]) -> None:
