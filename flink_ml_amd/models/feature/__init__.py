@@ -7,3 +7,7 @@ from .text import (IDF, CountVectorizer, CountVectorizerModel, FeatureHasher, Ha
                    IDFModel, NGram, RegexTokenizer, StopWordsRemover, Tokenizer)
 from .vector_ops import (DCT, Binarizer, Bucketizer, ElementwiseProduct, Interaction,  # noqa: F401
                          Normalizer, PolynomialExpansion, VectorAssembler, VectorSlicer)
+from . import encoders  # noqa: F401,E402
+from .encoders import (Imputer, ImputerModel, IndexToStringModel, KBinsDiscretizer,  # noqa: F401,E402
+                       KBinsDiscretizerModel, OneHotEncoder, OneHotEncoderModel, StringIndexer, StringIndexerModel,
+                       VectorIndexer, VectorIndexerModel)

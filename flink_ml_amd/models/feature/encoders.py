@@ -1,0 +1,727 @@
+"""Categorical / discretising encoders (reference ``LIB/feature/{onehotencoder,stringindexer,
+vectorindexer,kbinsdiscretizer,imputer}``).
+
+Numeric work stays on the rank's device and only fixed-size statistics cross ranks:
+
+* OneHotEncoder: per-column max index is a device ``max`` + all-reduce; the transform builds the
+  one-hot SparseColumn (indptr = cumsum(valid)) with no per-row host loop.
+* StringIndexer on numeric columns maps unique values (device ``unique``) to strings once and
+  then indexes rows with a device ``searchsorted`` lookup table; string columns use a host dict.
+* VectorIndexer counts distinct values per column with a single column-wise device sort.
+* KBinsDiscretizer bins every column with one batched ``searchsorted`` over padded edges.
+* Imputer computes mean / median / most-frequent surrogates from device-side reductions.
+
+Model-data records use the reference encoders so saved models are interchangeable:
+OneHotEncoder (Kryo ``writeInt`` pairs), StringIndexer (``IntSerializer`` + ``StringArraySerializer``),
+VectorIndexer (``MapSerializer<Integer, Map<Double, Integer>>``), KBinsDiscretizer (``double[][]``),
+Imputer (``MapSerializer<String, Double>``); map entries are written in Java ``HashMap`` order.
+"""
+from __future__ import annotations
+
+import math
+from collections import Counter
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ... import config
+from ...api.stage import Estimator
+from ...common.param import HasHandleInvalid, HasInputCol, HasInputCols, HasOutputCol, HasOutputCols, HasRelativeError
+from ...io import read_write as rw
+from ...io import serialization as ser
+from ...linalg.vectors import DenseVector, SparseVector, Vector
+from ...ops import features as fo
+from ...param.param import BooleanParam, FloatParam, IntParam, ParamValidators, StringParam
+from ...parallel import comm
+from ...table import SparseColumn, Table
+from ...utils.java import (java_double_hash, java_hashmap_order, java_int_hash, java_number_to_string,
+                           java_string_hash)
+from ..base import ModelWithData
+from ..linear import rw_update
+from .common import get_world_distributed
+from .scalers import exact_quantiles
+
+
+def _dev():
+    return config.compute_device()
+
+
+def _numeric_col(t: Table, col: str) -> torch.Tensor:
+    c = t.column(col)
+    if isinstance(c, torch.Tensor):
+        if c.dim() != 1:
+            raise ValueError("Column %s is not a scalar column" % col)
+        return c
+    vals = [float("nan") if v is None else float(v) for v in c]
+    return torch.tensor(vals, dtype=torch.float64)
+
+
+def _ordered_map(m: Dict, hash_fn) -> Dict:
+    """Re-inserts ``m`` in Java ``HashMap`` iteration order (insertion order = current order)."""
+    return {k: m[k] for k in java_hashmap_order(list(m.keys()), hash_fn)}
+
+
+# ================================================================================ OneHotEncoder
+class OneHotEncoderParams(HasInputCols, HasOutputCols, HasHandleInvalid):
+    DROP_LAST = BooleanParam("dropLast", "Whether to drop the last category.", True)
+
+
+@rw.register_stage
+class OneHotEncoderModel(ModelWithData, OneHotEncoderParams):
+    """``OneHotEncoderModel.java``: column i value v -> SparseVector(size_i, [v], [1.0]); with
+    dropLast the last category (v == size_i) maps to the empty vector."""
+
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.onehotencoder.OneHotEncoderModel"
+    MODEL_DATA_COLUMNS = ("f0", "f1")
+
+    @staticmethod
+    def encode_record(out, row):
+        out.write_int(int(row[0]))  # Kryo Output.writeInt is big-endian
+        out.write_int(int(row[1]))
+
+    @staticmethod
+    def decode_record(inp):
+        return (inp.read_int(), inp.read_int())
+
+    def _build_state(self, rows):
+        sizes = [0] * len(rows)
+        off = 0 if self.get(self.DROP_LAST) else 1
+        for ci, mx in rows:
+            sizes[int(ci)] = int(mx) + off
+        return sizes
+
+    def transform(self, *inputs):
+        if self.get(self.HANDLE_INVALID) != self.ERROR_INVALID:
+            raise ValueError("OneHotEncoderModel only supports handleInvalid = 'error'.")
+        t = inputs[0]
+        ins, outs = self.get(self.INPUT_COLS), self.get(self.OUTPUT_COLS)
+        if len(ins) != len(outs):
+            raise ValueError("The number of input columns and output columns must be equal.")
+        sizes = self._model_state()
+        res = {}
+        for i, (c, o) in enumerate(zip(ins, outs)):
+            x = _numeric_col(t, c)
+            xi = x.to(torch.int64)
+            if bool((xi.to(x.dtype) != x).any()):
+                bad = x[xi.to(x.dtype) != x][0].item()
+                raise ValueError("Value %s cannot be parsed as indexed integer." % bad)
+            size = sizes[i]
+            if bool(((xi < 0) | (xi > size)).any()):
+                raise IndexError("Index out of bounds for one-hot vector of size %d." % size)
+            valid = xi < size
+            indptr = torch.zeros(len(xi) + 1, dtype=torch.int64, device=xi.device)
+            indptr[1:] = torch.cumsum(valid.to(torch.int64), 0)
+            idx = xi[valid].to(torch.int32)
+            res[o] = SparseColumn(indptr, idx, torch.ones(idx.numel(), dtype=torch.float64, device=xi.device), size)
+        return [t.with_columns(res)]
+
+
+@rw.register_stage
+class OneHotEncoder(Estimator, OneHotEncoderParams):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.onehotencoder.OneHotEncoder"
+
+    def fit(self, *inputs):
+        if self.get(self.HANDLE_INVALID) != self.ERROR_INVALID:
+            raise ValueError("OneHotEncoder only supports handleInvalid = 'error'.")
+        t = inputs[0]
+        cols = self.get(self.INPUT_COLS)
+        maxes = []
+        for c in cols:
+            x = _numeric_col(t, c)
+            xi = x.to(torch.int64)
+            if x.numel() and bool((xi.to(x.dtype) != x).any()):
+                bad = x[xi.to(x.dtype) != x][0].item()
+                raise ValueError("Value %s cannot be parsed as indexed integer." % bad)
+            if x.numel() and bool((xi < 0).any()):
+                raise ValueError("Negative value not supported.")
+            maxes.append(int(xi.max().item()) if xi.numel() else -(1 << 31))
+        mx = torch.tensor(maxes, dtype=torch.int64)
+        if get_world_distributed():
+            mx = comm.all_reduce(mx, "max")
+        rows = [(i, int(v)) for i, v in enumerate(mx.tolist())]
+        m = OneHotEncoderModel().set_model_data(OneHotEncoderModel.make_model_data_table(rows))
+        rw_update(m, self)
+        return m
+
+
+# ================================================================================ StringIndexer
+ARBITRARY_ORDER = "arbitrary"
+FREQUENCY_DESC_ORDER = "frequencyDesc"
+FREQUENCY_ASC_ORDER = "frequencyAsc"
+ALPHABET_DESC_ORDER = "alphabetDesc"
+ALPHABET_ASC_ORDER = "alphabetAsc"
+
+
+class StringIndexerModelParams(HasInputCols, HasOutputCols, HasHandleInvalid):
+    pass
+
+
+class StringIndexerParams(StringIndexerModelParams):
+    ARBITRARY_ORDER = ARBITRARY_ORDER
+    FREQUENCY_DESC_ORDER = FREQUENCY_DESC_ORDER
+    FREQUENCY_ASC_ORDER = FREQUENCY_ASC_ORDER
+    ALPHABET_DESC_ORDER = ALPHABET_DESC_ORDER
+    ALPHABET_ASC_ORDER = ALPHABET_ASC_ORDER
+    STRING_ORDER_TYPE = StringParam("stringOrderType", "How to order strings of each column.", ARBITRARY_ORDER,
+                                    ParamValidators.in_array(ARBITRARY_ORDER, FREQUENCY_DESC_ORDER,
+                                                             FREQUENCY_ASC_ORDER, ALPHABET_DESC_ORDER,
+                                                             ALPHABET_ASC_ORDER))
+
+
+def _java_str_key(s: str) -> bytes:
+    # String.compareTo compares UTF-16 code units
+    return s.encode("utf-16-be")
+
+
+def _string_counts(t: Table, col: str) -> Dict[str, int]:
+    """Per-rank ``Map<String, Long>`` of a column in first-seen order (numbers via String.valueOf)."""
+    c = t.column(col)
+    if isinstance(c, torch.Tensor):
+        if c.dim() != 1:
+            raise RuntimeError("The input column only supports string and numeric type.")
+        # device: unique + counts; first-seen order is recovered from the first occurrence index
+        u, inv, cnt = torch.unique(c, return_inverse=True, return_counts=True)
+        first = torch.full((u.numel(),), c.numel(), dtype=torch.int64, device=c.device)
+        first.scatter_reduce_(0, inv, torch.arange(c.numel(), device=c.device), "amin")
+        order = torch.argsort(first).tolist()
+        uvals, ucnt = u.tolist(), cnt.tolist()
+        is_int = not c.dtype.is_floating_point
+        return {(str(int(uvals[i])) if is_int else java_number_to_string(uvals[i])): int(ucnt[i]) for i in order}
+    out: Dict[str, int] = {}
+    for v in c:
+        if isinstance(v, str):
+            s = v
+        elif isinstance(v, (int, float, np.integer, np.floating)) and not isinstance(v, bool):
+            s = java_number_to_string(v.item() if hasattr(v, "item") else v)
+        else:
+            raise RuntimeError("The input column only supports string and numeric type.")
+        out[s] = out.get(s, 0) + 1
+    return out
+
+
+def _order_strings(counts: Dict[str, int], order: str) -> List[str]:
+    items = [(k, counts[k]) for k in java_hashmap_order(list(counts.keys()), java_string_hash)]
+    if order == ALPHABET_ASC_ORDER:
+        items.sort(key=lambda kv: _java_str_key(kv[0]))
+    elif order == ALPHABET_DESC_ORDER:
+        items.sort(key=lambda kv: _java_str_key(kv[0]), reverse=True)
+    elif order == FREQUENCY_ASC_ORDER:
+        items.sort(key=lambda kv: kv[1])
+    elif order == FREQUENCY_DESC_ORDER:
+        items.sort(key=lambda kv: -kv[1])
+    elif order != ARBITRARY_ORDER:
+        raise ValueError("Unsupported stringOrderType type: %s." % order)
+    return [k for k, _ in items]
+
+
+class _StringArraysModel(ModelWithData):
+    MODEL_DATA_COLUMNS = ("stringArrays",)
+
+    @staticmethod
+    def encode_record(out, row):
+        arrays = row[0]
+        out.write_int(len(arrays))
+        for a in arrays:
+            ser.write_string_array(out, list(a))
+
+    @staticmethod
+    def decode_record(inp):
+        return ([ser.read_string_array(inp) for _ in range(inp.read_int())],)
+
+    @classmethod
+    def make_model_data_table(cls, rows):
+        def as_str(v):
+            return v if isinstance(v, str) else java_number_to_string(v)
+
+        return Table({"stringArrays": [[[as_str(v) for v in a] for a in r[0]] for r in rows]}, num_rows=len(rows))
+
+
+@rw.register_stage
+class StringIndexerModel(_StringArraysModel, StringIndexerModelParams):
+    """``StringIndexerModel.java``: string (or String.valueOf(number)) -> double index;
+    unseen values follow handleInvalid (error / skip the row / keep -> numLabels)."""
+
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.stringindexer.StringIndexerModel"
+
+    def _build_state(self, rows):
+        return [{s: float(i) for i, s in enumerate(arr)} for arr in rows[0][0]]
+
+    def transform(self, *inputs):
+        t = inputs[0]
+        ins, outs = self.get(self.INPUT_COLS), self.get(self.OUTPUT_COLS)
+        hi = self.get(self.HANDLE_INVALID)
+        maps = self._model_state()
+        keep_rows = torch.ones(t.num_rows, dtype=torch.bool)
+        res = {}
+        for i, (c, o) in enumerate(zip(ins, outs)):
+            m = maps[i]
+            col = t.column(c)
+            if isinstance(col, torch.Tensor) and col.dim() == 1:
+                u, inv = torch.unique(col, return_inverse=True)
+                is_int = not col.dtype.is_floating_point
+                keys = [str(int(v)) if is_int else java_number_to_string(v) for v in u.tolist()]
+                lut = torch.tensor([m.get(k, -1.0) for k in keys], dtype=torch.float64, device=col.device)
+                idx = lut[inv]
+                bad = idx < 0
+                if bool(bad.any()):
+                    if hi == self.ERROR_INVALID:
+                        k = keys[int(inv[bad][0])]
+                        raise RuntimeError("The input contains unseen string: %s. See handleInvalid parameter for "
+                                           "more options." % k)
+                    if hi == self.SKIP_INVALID:
+                        keep_rows &= ~bad.cpu()
+                    idx = torch.where(bad, torch.full_like(idx, float(len(m))), idx)
+                res[o] = idx
+            else:
+                vals = []
+                for r, v in enumerate(col):
+                    if isinstance(v, str):
+                        s = v
+                    elif isinstance(v, (int, float, np.integer, np.floating)) and not isinstance(v, bool):
+                        s = java_number_to_string(v.item() if hasattr(v, "item") else v)
+                    else:
+                        raise RuntimeError("The input column only supports string and numeric type.")
+                    if s in m:
+                        vals.append(m[s])
+                    elif hi == self.ERROR_INVALID:
+                        raise RuntimeError("The input contains unseen string: %s. See handleInvalid parameter for "
+                                           "more options." % s)
+                    elif hi == self.SKIP_INVALID:
+                        keep_rows[r] = False
+                        vals.append(-1.0)
+                    else:
+                        vals.append(float(len(m)))
+                res[o] = torch.tensor(vals, dtype=torch.float64)
+        out = t.with_columns(res)
+        if not bool(keep_rows.all()):
+            out = out.filter(keep_rows)
+        return [out]
+
+
+@rw.register_stage
+class StringIndexer(Estimator, StringIndexerParams):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.stringindexer.StringIndexer"
+
+    def fit(self, *inputs):
+        t = inputs[0]
+        cols = self.get(self.INPUT_COLS)
+        if len(cols) != len(self.get(self.OUTPUT_COLS)):
+            raise ValueError("The number of input columns and output columns must be equal.")
+        local = [_string_counts(t, c) for c in cols]
+        parts = comm.all_gather_object(local) if get_world_distributed() else [local]
+        arrays = []
+        for ci in range(len(cols)):
+            merged: Dict[str, int] = {}
+            for p in parts:
+                for k, v in p[ci].items():
+                    merged[k] = merged.get(k, 0) + v
+            arrays.append(_order_strings(merged, self.get(self.STRING_ORDER_TYPE)))
+        m = StringIndexerModel().set_model_data(StringIndexerModel.make_model_data_table([(arrays,)]))
+        rw_update(m, self)
+        return m
+
+
+@rw.register_stage
+class IndexToStringModel(_StringArraysModel, HasInputCols, HasOutputCols):
+    """``IndexToStringModel.java``: integer index -> string of the StringIndexerModel data."""
+
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.stringindexer.IndexToStringModel"
+
+    def transform(self, *inputs):
+        t = inputs[0]
+        arrays = self.model_data_rows()[0][0]
+        res = {}
+        for i, (c, o) in enumerate(zip(self.get(self.INPUT_COLS), self.get(self.OUTPUT_COLS))):
+            ids = _numeric_col(t, c).to(torch.int64).tolist()
+            arr = arrays[i]
+            out = []
+            for sid in ids:
+                if 0 <= sid < len(arr):
+                    out.append(arr[sid])
+                else:
+                    raise RuntimeError("The input contains unseen index: %d." % sid)
+            res[o] = out
+        return [t.with_columns(res)]
+
+
+# ================================================================================ VectorIndexer
+class VectorIndexerModelParams(HasInputCol, HasOutputCol, HasHandleInvalid):
+    pass
+
+
+class VectorIndexerParams(VectorIndexerModelParams):
+    MAX_CATEGORIES = IntParam("maxCategories", "Threshold for the number of values a categorical feature can take "
+                              "(>= 2). If a feature is found to have > maxCategories values, then it is declared "
+                              "continuous.", 20, ParamValidators.gt_eq(2))
+
+
+def _dense_matrix(t: Table, col: str) -> torch.Tensor:
+    c = t.column(col)
+    if isinstance(c, SparseColumn):
+        return c.to_dense(torch.float64)
+    return config.features_for_compute(t, col, allow_sparse=False)
+
+
+def _category_map(values: Sequence[float]) -> Dict[float, int]:
+    """``VectorIndexer.ModelGenerator``: sorted distinct values with 0.0 (if present) moved to index 0."""
+    vals = sorted(values)
+    if 0.0 in vals:
+        vals.remove(0.0)
+        vals = [0.0] + vals
+    return {v: i for i, v in enumerate(vals)}
+
+
+@rw.register_stage
+class VectorIndexerModel(ModelWithData, VectorIndexerModelParams):
+    """``VectorIndexerModel.java``: categorical columns' values -> category indices."""
+
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.vectorindexer.VectorIndexerModel"
+    MODEL_DATA_COLUMNS = ("categoryMaps",)
+
+    @staticmethod
+    def encode_record(out, row):
+        maps = _ordered_map({int(k): v for k, v in row[0].items()}, java_int_hash)
+        ser.write_map(out, maps, lambda o, k: o.write_int(k),
+                      lambda o, m: ser.write_map(o, _ordered_map(m, java_double_hash), lambda o2, x: o2.write_double(x),
+                                                 lambda o2, x: o2.write_int(int(x))))
+
+    @staticmethod
+    def decode_record(inp):
+        return (ser.read_map(inp, lambda i: i.read_int(),
+                             lambda i: ser.read_map(i, lambda i2: i2.read_double(), lambda i2: i2.read_int())),)
+
+    @classmethod
+    def make_model_data_table(cls, rows):
+        return Table({"categoryMaps": [r[0] for r in rows]}, num_rows=len(rows))
+
+    def _build_state(self, rows):
+        maps = rows[0][0]
+        state = []
+        for ci in sorted(maps.keys()):
+            m = maps[ci]
+            keys = sorted(m.keys())
+            state.append((int(ci), torch.tensor(keys, dtype=torch.float64),
+                          torch.tensor([float(m[k]) for k in keys], dtype=torch.float64), len(m)))
+        return state
+
+    def transform(self, *inputs):
+        t = inputs[0]
+        col = t.column(self.get(self.INPUT_COL))
+        was_sparse = isinstance(col, SparseColumn) or (isinstance(col, list) and col and isinstance(col[0],
+                                                                                                     SparseVector))
+        X = _dense_matrix(t, self.get(self.INPUT_COL)).to(torch.float64)
+        out = X.clone()
+        hi = self.get(self.HANDLE_INVALID)
+        keep = torch.ones(X.shape[0], dtype=torch.bool, device=X.device)
+        for ci, keys, vals, size in self._model_state():
+            keys, vals = keys.to(X.device), vals.to(X.device)
+            x = X[:, ci].contiguous()
+            pos = torch.clamp(torch.searchsorted(keys, x), max=keys.numel() - 1)
+            hit = keys[pos] == x
+            if not bool(hit.all()):
+                if hi == self.ERROR_INVALID:
+                    raise RuntimeError("The input contains unseen double: %s. See handleInvalid parameter for more "
+                                       "options." % java_number_to_string(float(x[~hit][0])))
+                if hi == self.SKIP_INVALID:
+                    keep &= hit
+            out[:, ci] = torch.where(hit, vals[pos], torch.full_like(x, float(size)))
+        if was_sparse:
+            res_col = SparseColumn.from_vectors([DenseVector(r).to_sparse() for r in out.cpu().numpy()],
+                                                X.shape[1])
+        else:
+            res_col = out
+        res = t.with_column(self.get(self.OUTPUT_COL), res_col)
+        if not bool(keep.all()):
+            res = res.filter(keep.cpu())
+        return [res]
+
+
+@rw.register_stage
+class VectorIndexer(Estimator, VectorIndexerParams):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.vectorindexer.VectorIndexer"
+
+    def fit(self, *inputs):
+        t = inputs[0]
+        max_cat = self.get(self.MAX_CATEGORIES)
+        X = _dense_matrix(t, self.get(self.INPUT_COL)).to(torch.float64)
+        local: List[Optional[List[float]]] = []
+        if X.shape[0]:
+            S, _ = torch.sort(X, dim=0)
+            distinct = 1 + (S[1:] != S[:-1]).sum(0)
+            ok = (distinct <= max_cat).tolist()
+            for c in range(X.shape[1]):
+                local.append(torch.unique(S[:, c]).tolist() if ok[c] else None)
+        parts = comm.all_gather_object(local) if get_world_distributed() else [local]
+        parts = [p for p in parts if p]
+        if not parts:
+            raise RuntimeError("The training set is empty.")
+        d = len(parts[0])
+        maps = {}
+        for c in range(d):
+            vals = set()
+            for p in parts:
+                if p[c] is None:
+                    vals = None
+                    break
+                vals.update(p[c])
+            if vals is not None and len(vals) <= max_cat:
+                maps[c] = _category_map(vals)
+        m = VectorIndexerModel().set_model_data(VectorIndexerModel.make_model_data_table([(maps,)]))
+        rw_update(m, self)
+        return m
+
+
+# ================================================================================ KBinsDiscretizer
+class KBinsDiscretizerModelParams(HasInputCol, HasOutputCol):
+    pass
+
+
+class KBinsDiscretizerParams(KBinsDiscretizerModelParams):
+    UNIFORM = "uniform"
+    QUANTILE = "quantile"
+    KMEANS = "kmeans"
+    STRATEGY = StringParam("strategy", "Strategy used to define the width of the bin.", "quantile",
+                           ParamValidators.in_array("uniform", "quantile", "kmeans"))
+    NUM_BINS = IntParam("numBins", "Number of bins to produce.", 5, ParamValidators.gt_eq(2))
+    SUB_SAMPLES = IntParam("subSamples", "Maximum number of samples used to fit the model.", 200000,
+                           ParamValidators.gt_eq(2))
+
+
+_JAVA_DOUBLE_MIN = 4.9e-324
+_JAVA_DOUBLE_MAX = 1.7976931348623157e308
+
+
+def _uniform_edges(mn: float, mx: float, k: int) -> np.ndarray:
+    width = (mx - mn) / k
+    e = np.empty(k + 1)
+    e[0] = mn
+    for i in range(1, k + 1):  # sequential accumulation like the reference
+        e[i] = e[i - 1] + width
+    return e
+
+
+def _quantile_edges(f: np.ndarray, k: int) -> np.ndarray:
+    n = f.shape[0]
+    width = 1.0 * n / k
+    tmp = [f[int(i * width)] for i in range(k)] + [f[n - 1]]
+    return np.array(sorted(set(tmp)))
+
+
+def _kmeans_edges(f: np.ndarray, k: int) -> np.ndarray:
+    n = f.shape[0]
+    distinct = np.unique(f)
+    if distinct.shape[0] <= k:
+        return _uniform_edges(f[0], f[-1], k)
+    width = 1.0 * n / k
+    cent = np.array([f[int(i * width)] for i in range(k)], dtype=np.float64)
+    old, rel, it = _JAVA_DOUBLE_MAX, _JAVA_DOUBLE_MAX, 0
+    while it < 300 and rel > 1e-4:
+        dist = np.abs(cent[None, :] - f[:, None])
+        cid = np.argmin(dist, axis=1)  # first minimum == the reference's strict '<' scan
+        loss = dist[np.arange(n), cid].sum()
+        with np.errstate(invalid="ignore", divide="ignore"):
+            cent = np.bincount(cid, weights=f, minlength=k) / np.bincount(cid, minlength=k)
+        loss /= n
+        rel = abs(loss - old)
+        old = loss
+        it += 1
+    cent = np.sort(cent)
+    e = np.empty(k + 1)
+    e[0], e[k] = f[0], f[-1]
+    e[1:k] = (cent[:-1] + cent[1:]) / 2
+    return e
+
+
+@rw.register_stage
+class KBinsDiscretizerModel(ModelWithData, KBinsDiscretizerModelParams):
+    """``KBinsDiscretizerModel.java``: value -> bin id (binary search, clamped to [0, #edges-2])."""
+
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.kbinsdiscretizer.KBinsDiscretizerModel"
+    MODEL_DATA_COLUMNS = ("binEdges",)
+
+    @staticmethod
+    def encode_record(out, row):
+        out.write_int(len(row[0]))
+        for e in row[0]:
+            ser.write_double_array(out, np.asarray(e, dtype=np.float64))
+
+    @staticmethod
+    def decode_record(inp):
+        return ([ser.read_double_array(inp) for _ in range(inp.read_int())],)
+
+    @classmethod
+    def make_model_data_table(cls, rows):
+        return Table({"binEdges": [[np.asarray(e, dtype=np.float64) for e in r[0]] for r in rows]},
+                     num_rows=len(rows))
+
+    def _build_state(self, rows):
+        edges = rows[0][0]
+        L = max(len(e) for e in edges)
+        E = torch.full((len(edges), L), float("inf"), dtype=torch.float64)
+        for i, e in enumerate(edges):
+            E[i, :len(e)] = torch.as_tensor(np.asarray(e, dtype=np.float64))
+        lens = torch.tensor([len(e) for e in edges], dtype=torch.int64)
+        return E, lens
+
+    def transform(self, *inputs):
+        t = inputs[0]
+        X = _dense_matrix(t, self.get(self.INPUT_COL)).to(torch.float64)
+        E, lens = self._model_state()
+        E, lens = E.to(X.device), lens.to(X.device)
+        if X.shape[1] != E.shape[0]:
+            raise ValueError("Input vector size %d does not match the model's %d columns." % (X.shape[1], E.shape[0]))
+        # batched binary search: idx = #edges <= x minus one, clamped to the last bin
+        idx = torch.searchsorted(E, X.t().contiguous(), right=True) - 1
+        idx = torch.minimum(idx, (lens - 2)[:, None])
+        idx = torch.clamp(idx, min=0)
+        return [t.with_column(self.get(self.OUTPUT_COL), idx.t().to(torch.float64).contiguous())]
+
+
+@rw.register_stage
+class KBinsDiscretizer(Estimator, KBinsDiscretizerParams):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.kbinsdiscretizer.KBinsDiscretizer"
+
+    def fit(self, *inputs):
+        from ..kmeans import sample_rows
+
+        t = inputs[0]
+        X = _dense_matrix(t, self.get(self.INPUT_COL))
+        strategy, k = self.get(self.STRATEGY), self.get(self.NUM_BINS)
+        d = X.shape[1] if X.dim() == 2 else 0
+        if strategy == self.UNIFORM:
+            st = fo.column_stats(X) if X.shape[0] else None
+            mn = st["min"] if st else torch.full((d,), float("inf"), dtype=torch.float64)
+            mx = st["max"] if st else torch.full((d,), float("-inf"), dtype=torch.float64)
+            if get_world_distributed():
+                mn, mx = comm.all_reduce(mn.clone(), "min"), comm.all_reduce(mx.clone(), "max")
+                n = int(comm.all_reduce_scalar(float(X.shape[0]), "sum"))
+            else:
+                n = X.shape[0]
+            if n == 0:
+                raise RuntimeError("The training set is empty.")
+            mn, mx = mn.cpu().numpy(), mx.cpu().numpy()
+            edges = [np.array([_JAVA_DOUBLE_MIN, _JAVA_DOUBLE_MAX]) if mn[c] == mx[c] else
+                     _uniform_edges(mn[c], mx[c], k) for c in range(len(mn))]
+        else:
+            seed = java_string_hash(self.JAVA_CLASS_NAME)
+            S = sample_rows(X, self.get(self.SUB_SAMPLES), seed)
+            if S.shape[0] == 0:
+                raise RuntimeError("The training set is empty.")
+            edges = []
+            for c in range(S.shape[1]):
+                f = np.sort(S[:, c])
+                if f[0] == f[-1]:
+                    edges.append(np.array([_JAVA_DOUBLE_MIN, _JAVA_DOUBLE_MAX]))
+                elif strategy == self.QUANTILE:
+                    edges.append(_quantile_edges(f, k))
+                else:
+                    edges.append(_kmeans_edges(f, k))
+        m = KBinsDiscretizerModel().set_model_data(KBinsDiscretizerModel.make_model_data_table([(edges,)]))
+        rw_update(m, self)
+        return m
+
+
+# ================================================================================ Imputer
+class ImputerModelParams(HasInputCols, HasOutputCols, HasRelativeError):
+    MISSING_VALUE = FloatParam("missingValue", "The placeholder for the missing values. All occurrences of "
+                               "missingValue will be imputed.", float("nan"))
+
+
+class ImputerParams(ImputerModelParams):
+    MEAN = "mean"
+    MEDIAN = "median"
+    MOST_FREQUENT = "most_frequent"
+    STRATEGY = StringParam("strategy", "The imputation strategy.", "mean",
+                           ParamValidators.in_array("mean", "median", "most_frequent"))
+
+
+def _is_missing(x: torch.Tensor, missing: float) -> torch.Tensor:
+    return torch.isnan(x) if math.isnan(missing) else (x == missing)
+
+
+@rw.register_stage
+class ImputerModel(ModelWithData, ImputerModelParams):
+    """``ImputerModel.java``: null / missingValue entries -> per-column surrogate (output double).
+    Columns are read by name (the reference reads the i-th field of the row)."""
+
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.imputer.ImputerModel"
+    MODEL_DATA_COLUMNS = ("surrogates",)
+
+    @staticmethod
+    def encode_record(out, row):
+        ser.write_map(out, _ordered_map(dict(row[0]), java_string_hash), lambda o, k: o.write_string(k),
+                      lambda o, v: o.write_double(float(v)))
+
+    @staticmethod
+    def decode_record(inp):
+        return (ser.read_map(inp, lambda i: i.read_string(), lambda i: i.read_double()),)
+
+    @classmethod
+    def make_model_data_table(cls, rows):
+        return Table({"surrogates": [dict(r[0]) for r in rows]}, num_rows=len(rows))
+
+    def transform(self, *inputs):
+        t = inputs[0]
+        sur = self.model_data_rows()[0][0]
+        missing = self.get(self.MISSING_VALUE)
+        res = {}
+        for c, o in zip(self.get(self.INPUT_COLS), self.get(self.OUTPUT_COLS)):
+            if c not in sur:
+                raise ValueError("Column %s is unacceptable for the Imputer model." % c)
+            x = _numeric_col(t, c).to(torch.float64)
+            null = torch.isnan(x) if not isinstance(t.column(c), torch.Tensor) else torch.zeros_like(x, dtype=torch.bool)
+            res[o] = torch.where(null | _is_missing(x, missing), torch.full_like(x, float(sur[c])), x)
+        return [t.with_columns(res)]
+
+
+@rw.register_stage
+class Imputer(Estimator, ImputerParams):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.imputer.Imputer"
+
+    def fit(self, *inputs):
+        t = inputs[0]
+        cols, outs = self.get(self.INPUT_COLS), self.get(self.OUTPUT_COLS)
+        if len(cols) != len(outs):
+            raise ValueError("Num of input columns and output columns are inconsistent.")
+        missing, strategy = self.get(self.MISSING_VALUE), self.get(self.STRATEGY)
+        dist = get_world_distributed()
+        xs = []
+        for c in cols:
+            x = _numeric_col(t, c).to(torch.float64)
+            xs.append(x[~(torch.isnan(x) | _is_missing(x, missing))])
+        sur: Dict[str, float] = {}
+        if strategy == self.MEAN:
+            st = torch.tensor([[float(x.sum()), float(x.numel())] for x in xs], dtype=torch.float64)
+            if dist:
+                st = comm.all_reduce_sum(st)
+            if st[0, 1] <= 0:
+                raise RuntimeError("The training set is empty or does not contains valid data.")
+            for i, c in enumerate(cols):
+                sur[c] = float(st[i, 0] / st[i, 1])
+        elif strategy == self.MEDIAN:
+            for c, x in zip(cols, xs):
+                n = int(comm.all_reduce_scalar(float(x.numel()), "sum")) if dist else x.numel()
+                if n == 0:
+                    raise RuntimeError("Surrogate cannot be computed. All the values in column [%s] are null, NaN or "
+                                       "missingValue." % c)
+                sur[c] = float(exact_quantiles(x[:, None], [0.5], self.get(self.RELATIVE_ERROR))[0, 0])
+        else:
+            for c, x in zip(cols, xs):
+                u, cnt = torch.unique(x, return_counts=True)
+                local = list(zip(u.tolist(), cnt.tolist()))
+                parts = comm.all_gather_object(local) if dist else [local]
+                counts: Counter = Counter()
+                for p in parts:
+                    for v, n in p:
+                        counts[v] += n
+                if not counts:
+                    sur[c] = float("nan")
+                    continue
+                best = max(counts.values())
+                sur[c] = min(v for v, n in counts.items() if n == best)
+            if all(math.isnan(v) for v in sur.values()):
+                raise RuntimeError("The training set is empty or does not contains valid data.")
+        m = ImputerModel().set_model_data(ImputerModel.make_model_data_table([(sur,)]))
+        rw_update(m, self)
+        return m

@@ -18,6 +18,7 @@ from typing import Dict, List, Sequence
 import numpy as np
 import torch
 
+from ... import config
 from ...api.stage import Estimator, Transformer
 from ...common.param import (HasCategoricalCols, HasInputCol, HasInputCols, HasNumFeatures, HasOutputCol,
                              HasOutputCols)
@@ -28,6 +29,7 @@ from ...ops import hashing
 from ...param.param import (BooleanParam, FloatParam, IntParam, ParamValidators, StringArrayParam, StringParam)
 from ...parallel import comm
 from ...table import SparseColumn, Table
+from ...utils.java import java_hashmap_order as _java_hashmap_order
 from ...utils.java import java_string_hash
 from ..base import ModelWithData
 from ..linear import rw_update
@@ -67,19 +69,8 @@ def java_split(pattern: str, s: str) -> List[str]:
 
 
 def java_hashmap_order(keys: Sequence[str]) -> List[str]:
-    """Iteration order of a ``java.util.HashMap<String, _>`` filled in ``keys`` order (no
-    treeified bins): by bucket index of the final table, then insertion order."""
-    cap, size = 16, 0
-    for _ in keys:
-        size += 1
-        if size > cap * 0.75:
-            cap *= 2
-
-    def bucket(k):
-        h = java_string_hash(k) & 0xFFFFFFFF
-        return (h ^ (h >> 16)) & (cap - 1)
-
-    return [k for _, _, k in sorted((bucket(k), i, k) for i, k in enumerate(keys))]
+    """Iteration order of a ``java.util.HashMap<String, _>`` filled in ``keys`` order."""
+    return _java_hashmap_order(keys, java_string_hash)
 
 
 def _strings_col(t: Table, col: str) -> list:
@@ -216,18 +207,23 @@ class HashingTF(Transformer, HasInputCol, HasOutputCol, HasNumFeatures):
             d = list(d)
             flat.extend(d)
             lens.append(len(d))
-        if flat and all(isinstance(x, str) for x in flat):
-            h = hashing.hash_strings(flat)
+        dev = config.compute_device()
+        all_str = bool(flat) and all(isinstance(x, str) for x in flat)
+        if all_str and dev.type == "cuda":
+            idx = hashing.hash_strings_device(flat, nf, 0, dev).to(torch.int64)
         else:
-            h = np.array([hashing.hash_object(x) for x in flat], dtype=np.int32)
-        idx = hashing.non_negative_mod(h, nf)
-        out, pos = [], 0
-        for L in lens:
-            cnt = Counter(idx[pos:pos + L].tolist())
-            pos += L
-            keys = sorted(cnt)
-            out.append(SparseVector(nf, keys, [1.0 if binary else float(cnt[k]) for k in keys]))
-        col = SparseColumn.from_vectors(out, nf) if out else out
+            h = hashing.hash_strings(flat) if all_str else np.array([hashing.hash_object(x) for x in flat],
+                                                                    dtype=np.int32)
+            idx = torch.from_numpy(hashing.non_negative_mod(h, nf).astype(np.int64)).to(dev)
+        # term counts per document as one sort-unique over (doc, bucket) keys -> CSR column
+        n = len(lens)
+        doc = torch.repeat_interleave(torch.arange(n, device=dev), torch.tensor(lens, dtype=torch.int64, device=dev))
+        keys, cnt = torch.unique(doc * nf + idx, return_counts=True)
+        rows = torch.div(keys, nf, rounding_mode="floor")
+        indptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        indptr[1:] = torch.cumsum(torch.bincount(rows, minlength=n), 0)
+        vals = torch.ones_like(cnt, dtype=torch.float64) if binary else cnt.to(torch.float64)
+        col = SparseColumn(indptr, (keys - rows * nf).to(torch.int32), vals, nf)
         return [t.with_column(self.get(self.OUTPUT_COL), col)]
 
 

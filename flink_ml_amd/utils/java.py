@@ -65,6 +65,78 @@ def java_hash(obj) -> int:
     raise TypeError("no Java hash for %r" % type(obj))
 
 
+def _table_size_for(n: int) -> int:
+    cap = 1
+    while cap < n:
+        cap <<= 1
+    return max(cap, 1)
+
+
+def java_hashmap_order(keys, hash_fn=java_hash, initial_capacity: int = 16):
+    """Iteration order of a ``java.util.HashMap`` / ``HashSet`` filled with ``keys`` in that order
+    (no treeified bins): by bucket of the final table, then insertion order (Java's resize split
+    keeps the relative order inside a bucket). ``initial_capacity`` mirrors ``new HashMap<>(n)``."""
+    keys = list(keys)
+    cap = _table_size_for(initial_capacity)
+    size = 0
+    for _ in keys:
+        size += 1
+        if size > cap * 0.75:
+            cap *= 2
+
+    def bucket(k):
+        h = hash_fn(k) & 0xFFFFFFFF
+        return (h ^ (h >> 16)) & (cap - 1)
+
+    return [k for _, _, k in sorted(((bucket(k), i, k) for i, k in enumerate(keys)), key=lambda x: (x[0], x[1]))]
+
+
+def java_double_to_string(d: float) -> str:
+    """``Double.toString``: plain notation for 1e-3 <= |d| < 1e7, else ``d.dddE±n``; shortest
+    round-trip digits (same digit selection as Python's ``repr``)."""
+    if d != d:
+        return "NaN"
+    if d in (float("inf"), float("-inf")):
+        return "Infinity" if d > 0 else "-Infinity"
+    if d == 0:
+        return "-0.0" if math.copysign(1.0, d) < 0 else "0.0"
+    a = abs(d)
+    if 1e-3 <= a < 1e7:
+        r = repr(d)
+        if "e" in r or "E" in r:
+            r = "%.17f" % d
+            r = r.rstrip("0")
+        if "." not in r:
+            r += ".0"
+        if r.endswith("."):
+            r += "0"
+        return r
+    mant, exp = ("%r" % a).lower().split("e") if "e" in repr(a) else (repr(a), "0")
+    if "e" not in repr(a):
+        # repr printed a plain number (e.g. 12345678.0): normalise to scientific
+        digits = repr(a).replace(".", "").lstrip("0").rstrip("0") or "0"
+        ip = repr(a).split(".")[0]
+        e = len(ip.lstrip("0")) - 1 if ip.strip("0") else -(len(repr(a).split(".")[1]) - len(
+            repr(a).split(".")[1].lstrip("0")) + 1)
+        mant = digits[0] + "." + (digits[1:] or "0")
+        exp = str(e)
+    else:
+        if "." not in mant:
+            mant += ".0"
+        e = int(exp)
+        exp = str(e)
+    return ("-" if d < 0 else "") + mant + "E" + exp
+
+
+def java_number_to_string(v) -> str:
+    """``String.valueOf(Number)`` for the boxed types the reference accepts."""
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, int):
+        return str(v)
+    return java_double_to_string(float(v))
+
+
 def tuple2_hash(a, b) -> int:
     """``org.apache.flink.api.java.tuple.Tuple2.hashCode``: 31*hash(f0) + hash(f1)."""
     return _i32(31 * java_hash(a) + java_hash(b))

@@ -1,0 +1,83 @@
+"""GPU numerics of the feature kernels (colstats.hip, hash.hip) against fp64 torch references, and
+device-resident fit/transform of the scalers/encoders matching the CPU results."""
+import numpy as np
+import pytest
+import torch
+
+from flink_ml_amd import Table, Vectors
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(1, 3), (1000, 37), (70000, 300)])
+def test_colstats_kernel(dtype, shape):
+    from flink_ml_amd.ops import features as fo
+
+    g = torch.Generator().manual_seed(3)
+    X = (torch.randn(shape, generator=g, dtype=torch.float64) * 3 + 1).to(dtype).cuda()
+    st = fo.column_stats(X)
+    Xd = X.double()
+    tol = dict(rtol=1e-9, atol=1e-6)
+    torch.testing.assert_close(st["sum"], Xd.sum(0), **tol)
+    torch.testing.assert_close(st["sumsq"], (Xd * Xd).sum(0), **tol)
+    torch.testing.assert_close(st["min"], Xd.min(0).values, rtol=0, atol=0)
+    torch.testing.assert_close(st["max"], Xd.max(0).values, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_affine_kernel(dtype):
+    from flink_ml_amd.ops import features as fo
+
+    X = torch.randn(5000, 129, dtype=torch.float64).to(dtype).cuda()
+    sub = torch.randn(129, dtype=torch.float64).cuda()
+    mul = torch.rand(129, dtype=torch.float64).cuda()
+    add = torch.randn(129, dtype=torch.float64).cuda()
+    out = fo.affine_cols(X, sub, mul, add)
+    ref = (X.double() - sub) * mul + add
+    torch.testing.assert_close(out.double(), ref, rtol=1e-6, atol=1e-5)
+    out2 = fo.affine_cols(X, None, mul, None)
+    torch.testing.assert_close(out2.double(), X.double() * mul, rtol=1e-6, atol=1e-5)
+
+
+def test_murmur3_device_matches_host():
+    from flink_ml_amd.ops import hashing
+
+    words = ["HashingTFTest", "Hashing", "Term", "Frequency", "Test", "", "ünïcødé", "a" * 37] * 50
+    for mode, mod in ((0, 262144), (1, 1000)):
+        dev = hashing.hash_strings_device(words, mod, mode, torch.device("cuda")).cpu().numpy()
+        h = hashing.hash_strings(words)
+        host = hashing.non_negative_mod(h, mod) if mode == 0 else np.fmod(np.abs(h.astype(np.int64)), mod)
+        np.testing.assert_array_equal(dev, host)
+
+
+def test_scalers_on_device_match_cpu():
+    from flink_ml_amd.models import KBinsDiscretizer, MinMaxScaler, StandardScaler
+
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(4096, 16))
+    tc = Table({"input": torch.from_numpy(X)}, num_rows=4096)
+    tg = Table({"input": torch.from_numpy(X).cuda()}, num_rows=4096)
+    for est in (StandardScaler().set_with_mean(True), MinMaxScaler()):
+        oc = est.fit(tc).transform(tc)[0].column("output")
+        og = est.fit(tg).transform(tg)[0].column("output")
+        assert og.is_cuda
+        torch.testing.assert_close(og.double().cpu(), oc.double(), rtol=1e-5, atol=1e-5)
+    kb = KBinsDiscretizer().set_strategy("uniform").set_num_bins(7)
+    bc = kb.fit(tc).transform(tc)[0].column("output")
+    bg = kb.fit(tg).transform(tg)[0].column("output")
+    assert torch.equal(bg.cpu(), bc)
+
+
+def test_hashing_tf_device():
+    from flink_ml_amd.models import HashingTF
+
+    t = Table.from_rows([(["HashingTFTest", "Hashing", "Term", "Frequency", "Test"],)] * 3000, ["input"])
+    out = HashingTF().transform(t)[0].get_list("output")
+    assert out[0] == Vectors.sparse(262144, [67564, 89917, 113827, 131486, 228971], [1.0] * 5)
