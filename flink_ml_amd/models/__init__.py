@@ -9,3 +9,5 @@ from .online import (OnlineKMeans, OnlineKMeansModel, OnlineLogisticRegression, 
                      OnlineLogisticRegressionModel)
 from . import feature  # noqa: F401,E402
 from .feature import *  # noqa: F401,F403,E402
+from . import stats  # noqa: F401,E402
+from .stats import ANOVATest, ChiSqTest, FValueTest  # noqa: F401,E402

@@ -11,3 +11,5 @@ from . import encoders  # noqa: F401,E402
 from .encoders import (Imputer, ImputerModel, IndexToStringModel, KBinsDiscretizer,  # noqa: F401,E402
                        KBinsDiscretizerModel, OneHotEncoder, OneHotEncoderModel, StringIndexer, StringIndexerModel,
                        VectorIndexer, VectorIndexerModel)
+from . import selectors  # noqa: F401,E402
+from .selectors import UnivariateFeatureSelector, UnivariateFeatureSelectorModel  # noqa: F401,E402

@@ -86,3 +86,21 @@ class VectorTransformerBase(Transformer, HasInputCol, HasOutputCol):
         t = inputs[0]
         X = vector_input(t, self.get(self.INPUT_COL))
         return [t.with_column(self.get(self.OUTPUT_COL), self._apply(X))]
+
+
+def select_by_indices(X, sorted_idx: Sequence[int]):
+    """``VectorUtils.selectByIndices``: dense columns are gathered; a SparseColumn stays sparse
+    (entries at unselected positions dropped, kept ones renumbered)."""
+    if isinstance(X, SparseColumn):
+        dev = X.values.device
+        remap = torch.full((X.size,), -1, dtype=torch.int64, device=dev)
+        if len(sorted_idx):
+            remap[torch.as_tensor(sorted_idx, dtype=torch.int64, device=dev)] = torch.arange(len(sorted_idx),
+                                                                                          device=dev)
+        new = remap[X.indices.long()]
+        keep = new >= 0
+        rows = row_ids(X)[keep]
+        indptr = torch.zeros(len(X) + 1, dtype=torch.int64, device=dev)
+        indptr[1:] = torch.cumsum(torch.bincount(rows, minlength=len(X)), 0)
+        return SparseColumn(indptr, new[keep].to(torch.int32), X.values[keep].to(torch.float64), len(sorted_idx))
+    return X[:, torch.as_tensor(list(sorted_idx), dtype=torch.long, device=X.device)].to(torch.float64)

@@ -21,8 +21,8 @@ from ...parallel import comm
 from ...table import SparseColumn, Table
 from ..base import ModelWithData
 from ..linear import rw_update
-from .common import (all_reduce_stats, dec_dense, dense_input, dense_vec, enc_dense, sparse_map_values,
-                     vector_input)
+from .common import (all_reduce_stats, dec_dense, dense_input, dense_vec, enc_dense, select_by_indices,
+                     sparse_map_values, vector_input)
 
 
 def _stats(table: Table, col: str) -> dict:
@@ -310,10 +310,7 @@ class VarianceThresholdSelectorModel(ModelWithData, HasInputCol, HasOutputCol):
         if t.num_rows and d != nf:
             raise ValueError("%s has %d features, but VarianceThresholdSelector is expecting %d features as input."
                              % (self.get(self.INPUT_COL), d, nf))
-        if isinstance(X, SparseColumn):
-            X = X.to_dense(torch.float64)
-        out = X[:, torch.as_tensor(idx, dtype=torch.long, device=X.device)].to(torch.float64)
-        return [t.with_column(self.get(self.OUTPUT_COL), out)]
+        return [t.with_column(self.get(self.OUTPUT_COL), select_by_indices(X, idx))]
 
 
 @rw.register_stage

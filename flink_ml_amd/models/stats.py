@@ -1,0 +1,199 @@
+"""Statistical hypothesis tests (reference ``LIB/stats/{anovatest,chisqtest,fvaluetest}``).
+
+Each test reduces the rank's partition to fixed-size sufficient statistics on the device, then
+one all-reduce combines them:
+
+* ANOVATest — per-class feature sums as a one-hot GEMM (fp64, deterministic, no atomics) plus
+  column sum / Σx²; F = MSB / MSW, p = 1 - F_cdf(F; C-1, N-C)  (``ANOVATest.java:120-200``).
+* FValueTest — label/feature moments, then the centred cross-moment (y - ȳ)ᵀ(X - x̄) as one GEMV;
+  corr² → F with (1, N-2) dof (``FValueTest.java:150-260``).
+* ChiSqTest — per-feature contingency tables [#values, #labels] counted with one ``bincount``
+  per column; Pearson statistic, dof = (V-1)(L-1), p-value and statistic rounded HALF_UP to 11
+  decimals like ``ChiSqTest.java:440-455``.
+
+Distribution CDFs come from scipy (commons-math3 in the reference).
+"""
+from __future__ import annotations
+
+from decimal import ROUND_HALF_UP, Decimal
+from typing import List, Tuple
+
+import numpy as np
+import torch
+from scipy import stats as sps
+
+from .. import config
+from ..api.stage import AlgoOperator
+from ..common.param import HasFeaturesCol, HasFlatten, HasLabelCol
+from ..io import read_write as rw
+from ..linalg.vectors import DenseVector
+from ..parallel import comm
+from ..table import SparseColumn, Table
+from .feature.common import get_world_distributed
+
+
+def features_and_labels(t: Table, features_col: str, label_col: str) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Dense fp64 features [n, d] and fp64 labels on the compute device."""
+    c = t.column(features_col)
+    if isinstance(c, SparseColumn):
+        X = c.to_dense(torch.float64, device=config.compute_device())
+    else:
+        X = config.features_for_compute(t, features_col, allow_sparse=False).to(torch.float64)
+    lab = t.column(label_col)
+    if isinstance(lab, list) and any(v is None for v in lab):
+        raise ValueError("Input data must contain label value.")
+    y = t.scalars(label_col, dtype=torch.float64, device=X.device)
+    return X, y
+
+
+def global_sorted_unique(v: torch.Tensor) -> torch.Tensor:
+    """Sorted union of the ranks' distinct values (small: labels / categories)."""
+    u = torch.unique(v)
+    if get_world_distributed():
+        parts = comm.all_gather_object(u.cpu().tolist())
+        u = torch.tensor(sorted(set(x for p in parts for x in p)), dtype=v.dtype, device=v.device)
+    return u
+
+
+def class_sums(X: torch.Tensor, ci: torch.Tensor, C: int, chunk: int = 1 << 20) -> torch.Tensor:
+    """Σ rows of X per class as onehotᵀ·X in fp64 row chunks (deterministic, MFMA/BLAS path)."""
+    out = torch.zeros((C, X.shape[1]), dtype=torch.float64, device=X.device)
+    ar = torch.arange(C, device=X.device)
+    for s in range(0, X.shape[0], chunk):
+        oh = (ci[s:s + chunk, None] == ar[None, :]).to(torch.float64)
+        out += oh.t() @ X[s:s + chunk]
+    return out
+
+
+def _reduce(t: torch.Tensor) -> torch.Tensor:
+    return comm.all_reduce_sum(t) if get_world_distributed() else t
+
+
+def _result_table(idx_name: str, stat_name: str, flat_names, p, dof, stat, flatten: bool, dof_kind=int) -> Table:
+    d = len(p)
+    if flatten:
+        return Table({flat_names[0]: torch.arange(d, dtype=torch.int64), flat_names[1]: torch.tensor(p, dtype=torch.float64),
+                      flat_names[2]: torch.tensor(dof, dtype=torch.int64), flat_names[3]: torch.tensor(stat, dtype=torch.float64)},
+                     num_rows=d)
+    return Table({idx_name: [DenseVector(np.asarray(p, dtype=np.float64))],
+                  "degreesOfFreedom": [[dof_kind(x) for x in dof]],
+                  stat_name: [DenseVector(np.asarray(stat, dtype=np.float64))]}, num_rows=1)
+
+
+class _TestParams(HasFeaturesCol, HasLabelCol, HasFlatten):
+    pass
+
+
+@rw.register_stage
+class ANOVATest(AlgoOperator, _TestParams):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.stats.anovatest.ANOVATest"
+
+    def compute(self, t: Table):
+        X, y = features_and_labels(t, self.get(self.FEATURES_COL), self.get(self.LABEL_COL))
+        cls = global_sorted_unique(y)
+        C, d = cls.numel(), X.shape[1]
+        ci = torch.searchsorted(cls, y)
+        packed = torch.cat([class_sums(X, ci, C).reshape(-1), torch.bincount(ci, minlength=C).to(torch.float64),
+                            X.sum(0), (X * X).sum(0)])
+        packed = _reduce(packed).cpu().numpy()
+        S = packed[:C * d].reshape(C, d)
+        cnt = packed[C * d:C * d + C]
+        tot, totsq = packed[C * d + C:C * d + C + d], packed[C * d + C + d:]
+        n = cnt.sum()
+        dfb, dfw = C - 1, int(n) - C
+        if dfb <= 0:
+            raise ValueError("Num of classes should be positive.")
+        if dfw <= 0:
+            raise ValueError("Num of samples should be greater than num of classes.")
+        with np.errstate(invalid="ignore", divide="ignore"):
+            sq = tot * tot
+            ss_tot = totsq - sq / n
+            between = (S * S / cnt[:, None]).sum(0) - sq / n
+            within = ss_tot - between
+            f = (between / dfb) / (within / dfw)
+            p = 1.0 - sps.f.cdf(f, dfb, dfw)
+        return p, [dfb + dfw] * d, f
+
+    def transform(self, *inputs):
+        p, dof, f = self.compute(inputs[0])
+        return [_result_table("pValues", "fValues", ("featureIndex", "pValue", "degreeOfFreedom", "fValue"), p, dof, f,
+                              self.get(self.FLATTEN))]
+
+
+@rw.register_stage
+class FValueTest(AlgoOperator, _TestParams):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.stats.fvaluetest.FValueTest"
+
+    def compute(self, t: Table):
+        X, y = features_and_labels(t, self.get(self.FEATURES_COL), self.get(self.LABEL_COL))
+        d = X.shape[1]
+        mom = _reduce(torch.cat([torch.tensor([float(y.numel())], dtype=torch.float64, device=X.device),
+                                 y.sum()[None], (y * y).sum()[None], X.sum(0), (X * X).sum(0)]))
+        n = float(mom[0])
+        my = mom[1] / n
+        sy = torch.sqrt((mom[2] / n - my * my) * n / (n - 1))
+        mx = mom[3:3 + d] / n
+        sx = torch.sqrt((mom[3 + d:] / n - mx * mx) * n / (n - 1))
+        cov = _reduce(((y - my)[None, :] @ (X - mx))[0] / (n - 1))
+        dof = int(n) - 2
+        corr = cov / (sy * sx)
+        f = (corr * corr / (1 - corr * corr) * dof).cpu().numpy()
+        with np.errstate(invalid="ignore"):
+            p = 1.0 - sps.f.cdf(f, 1, dof)
+        return p, [dof] * d, f
+
+    def transform(self, *inputs):
+        p, dof, f = self.compute(inputs[0])
+        return [_result_table("pValues", "fValues", ("featureIndex", "pValue", "degreeOfFreedom", "fValue"), p, dof, f,
+                              self.get(self.FLATTEN))]
+
+
+def _round11(v: float) -> float:
+    if v != v or v in (float("inf"), float("-inf")):
+        return v
+    return float(Decimal(v).quantize(Decimal("1e-11"), rounding=ROUND_HALF_UP))
+
+
+@rw.register_stage
+class ChiSqTest(AlgoOperator, _TestParams):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.stats.chisqtest.ChiSqTest"
+
+    def compute(self, t: Table):
+        X, y = features_and_labels(t, self.get(self.FEATURES_COL), self.get(self.LABEL_COL))
+        labels = global_sorted_unique(y)
+        L, d = labels.numel(), X.shape[1]
+        li = torch.searchsorted(labels, y)
+        local_vals = [torch.unique(X[:, j]) for j in range(d)]
+        if get_world_distributed():
+            parts = comm.all_gather_object([v.cpu().tolist() for v in local_vals])
+            vals = [torch.tensor(sorted(set(x for p in parts for x in p[j])), dtype=torch.float64, device=X.device)
+                    for j in range(d)]
+        else:
+            vals = local_vals
+        tables = []
+        for j in range(d):
+            vi = torch.searchsorted(vals[j], X[:, j].contiguous())
+            tables.append(torch.bincount(vi * L + li, minlength=vals[j].numel() * L).to(torch.float64))
+        flat = _reduce(torch.cat(tables)).cpu().numpy() if tables else np.zeros(0)
+        p_out, dof_out, stat_out, off = [], [], [], 0
+        for j in range(d):
+            V = vals[j].numel()
+            obs = flat[off:off + V * L].reshape(V, L)
+            off += V * L
+            n = obs.sum()
+            exp = np.outer(obs.sum(1), obs.sum(0)) / n
+            stat = float(((obs - exp) ** 2 / exp).sum())
+            dof = (V - 1) * (L - 1)
+            if dof == 0:
+                stat, p = 0.0, 1.0
+            else:
+                p = 1.0 - float(sps.chi2.cdf(stat, dof))
+            p_out.append(_round11(p))
+            dof_out.append(dof)
+            stat_out.append(_round11(stat))
+        return p_out, dof_out, stat_out
+
+    def transform(self, *inputs):
+        p, dof, s = self.compute(inputs[0])
+        return [_result_table("pValues", "statistics", ("featureIndex", "pValue", "degreeOfFreedom", "statistic"), p,
+                              dof, s, self.get(self.FLATTEN))]
