@@ -13,3 +13,7 @@ from .encoders import (Imputer, ImputerModel, IndexToStringModel, KBinsDiscretiz
                        VectorIndexer, VectorIndexerModel)
 from . import selectors  # noqa: F401,E402
 from .selectors import UnivariateFeatureSelector, UnivariateFeatureSelectorModel  # noqa: F401,E402
+from . import lsh  # noqa: F401,E402
+from .lsh import MinHashLSH, MinHashLSHModel  # noqa: F401,E402
+from . import misc  # noqa: F401,E402
+from .misc import RandomSplitter, SQLTransformer  # noqa: F401,E402

@@ -1,0 +1,236 @@
+"""MinHashLSH / MinHashLSHModel (reference ``LIB/feature/lsh/{LSH,LSHModel,MinHashLSH,
+MinHashLSHModel,MinHashLSHModelData}.java``).
+
+* fit: the input dimension (all vector sizes must agree) and ``java.util.Random(seed)``
+  coefficients a_k = 1 + nextInt(P-1), b_k = nextInt(P-1) exactly like ``generateModelData``.
+* transform: one ``minhash.hip`` launch over the CSR nonzero pattern → a [n, tables, funcs]
+  fp64 tensor column (each row reads back as ``DenseVector[]``).
+* approx_nearest_neighbors: bucket filter (any table whose signature equals the key's), device
+  Jaccard distances from sorted-key membership, per-rank top-k then a global top-k; each rank
+  returns its own rows of the global answer.
+* approx_similarity_join: broadcast join — dataset B's signatures and sets are all-gathered, each
+  rank joins its partition of A on (table, signature) via ``unique(dim=0)`` group ids, dedupes the
+  candidate pairs and keeps those with Jaccard distance <= threshold.
+"""
+from __future__ import annotations
+
+from typing import List, Tuple
+
+import numpy as np
+import torch
+
+from ... import config
+from ...api.stage import Estimator
+from ...common.param import HasInputCol, HasOutputCol, HasSeed
+from ...io import read_write as rw
+from ...io import serialization as ser
+from ...linalg.vectors import Vector
+from ...ops import lsh as lsh_ops
+from ...param.param import IntParam, ParamValidators
+from ...parallel import comm
+from ...table import SparseColumn, Table
+from ...utils.java import JavaRandom
+from ..base import ModelWithData
+from ..linear import rw_update
+from .common import get_world_distributed, vector_input
+
+HASH_PRIME = lsh_ops.HASH_PRIME
+
+
+class LSHModelParams(HasInputCol, HasOutputCol):
+    pass
+
+
+class LSHParams(LSHModelParams):
+    NUM_HASH_TABLES = IntParam("numHashTables", "Number of hash tables.", 1, ParamValidators.gt_eq(1))
+    NUM_HASH_FUNCTIONS_PER_TABLE = IntParam("numHashFunctionsPerTable", "Number of hash functions per table.", 1,
+                                            ParamValidators.gt_eq(1))
+
+
+def generate_model_data(num_tables: int, num_funcs: int, dim: int, seed: int):
+    if dim > HASH_PRIME:
+        raise ValueError("The input vector dimension %d exceeds the threshold %d." % (dim, HASH_PRIME))
+    rnd = JavaRandom(seed)
+    a, b = [], []
+    for _ in range(num_tables * num_funcs):
+        a.append(1 + rnd.next_int(HASH_PRIME - 1))
+        b.append(rnd.next_int(HASH_PRIME - 1))
+    return (num_tables, num_funcs, a, b)
+
+
+def _sets(X) -> SparseColumn:
+    return lsh_ops.to_csr_sets(X)
+
+
+def _row_keys(sets: SparseColumn) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(row id per nnz, sorted key row*d + col) for membership tests."""
+    dev = sets.values.device
+    rows = torch.repeat_interleave(torch.arange(len(sets), device=dev), (sets.indptr[1:] - sets.indptr[:-1]).to(dev))
+    return rows, rows * sets.size + sets.indices.to(dev).long()
+
+
+def _pair_jaccard(sa: SparseColumn, sb: SparseColumn, ia: torch.Tensor, ib: torch.Tensor) -> torch.Tensor:
+    """Jaccard distance of set pairs (sa[ia[p]], sb[ib[p]]), vectorised over all nnz of the A side."""
+    dev = ia.device
+    if ia.numel() == 0:
+        return torch.zeros(0, dtype=torch.float64, device=dev)
+    a_ptr, b_ptr = sa.indptr.to(dev), sb.indptr.to(dev)
+    la = (a_ptr[ia + 1] - a_ptr[ia])
+    lb = (b_ptr[ib + 1] - b_ptr[ib])
+    # expand every pair by its A-side nnz, look the column up in B's row-keyed sorted index
+    pid = torch.repeat_interleave(torch.arange(ia.numel(), device=dev), la)
+    off = torch.arange(pid.numel(), device=dev) - torch.repeat_interleave(torch.cumsum(la, 0) - la, la)
+    cols = sa.indices.to(dev).long()[a_ptr[ia][pid] + off]
+    d = max(sa.size, sb.size)
+    _, bkeys = _row_keys(SparseColumn(sb.indptr, sb.indices, sb.values, d))
+    bkeys_sorted, _ = torch.sort(bkeys)
+    q = ib[pid] * d + cols
+    pos = torch.clamp(torch.searchsorted(bkeys_sorted, q), max=max(bkeys_sorted.numel() - 1, 0))
+    hit = (bkeys_sorted[pos] == q) if bkeys_sorted.numel() else torch.zeros_like(q, dtype=torch.bool)
+    inter = torch.zeros(ia.numel(), dtype=torch.float64, device=dev).index_add_(0, pid, hit.to(torch.float64))
+    union = (la + lb).to(torch.float64) - inter
+    if bool((union <= 0).any()):
+        raise ValueError("The union of two input sets must have at least 1 elements")
+    return 1.0 - inter / union
+
+
+@rw.register_stage
+class MinHashLSHModel(ModelWithData, LSHModelParams):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.lsh.MinHashLSHModel"
+    MODEL_DATA_COLUMNS = ("numHashTables", "numHashFunctionsPerTable", "randCoefficientA", "randCoefficientB")
+
+    @staticmethod
+    def encode_record(out, row):
+        out.write_int(int(row[0]))
+        out.write_int(int(row[1]))
+        ser.write_int_array(out, np.asarray(row[2], dtype=np.int32))
+        ser.write_int_array(out, np.asarray(row[3], dtype=np.int32))
+
+    @staticmethod
+    def decode_record(inp):
+        return (inp.read_int(), inp.read_int(), [int(x) for x in ser.read_int_array(inp)],
+                [int(x) for x in ser.read_int_array(inp)])
+
+    @classmethod
+    def make_model_data_table(cls, rows):
+        return Table({"numHashTables": torch.tensor([int(r[0]) for r in rows], dtype=torch.int64),
+                      "numHashFunctionsPerTable": torch.tensor([int(r[1]) for r in rows], dtype=torch.int64),
+                      "randCoefficientA": [list(r[2]) for r in rows], "randCoefficientB": [list(r[3]) for r in rows]},
+                     num_rows=len(rows))
+
+    def _params(self):
+        nt, nf, a, b = self.model_data_rows()[0]
+        return int(nt), int(nf), list(a), list(b)
+
+    def hash_function(self, X) -> torch.Tensor:
+        """Signatures [n, tables, funcs] (fp64) of a dense tensor or SparseColumn."""
+        nt, nf, a, b = self._params()
+        return lsh_ops.minhash(X, a, b).reshape(-1, nt, nf)
+
+    def _hashes_of(self, t: Table) -> torch.Tensor:
+        oc = self.get(self.OUTPUT_COL)
+        if t.has_column(oc) and isinstance(t.column(oc), torch.Tensor) and t.column(oc).dim() == 3:
+            return t.column(oc)
+        return self.hash_function(vector_input(t, self.get(self.INPUT_COL)))
+
+    def transform(self, *inputs):
+        t = inputs[0]
+        return [t.with_column(self.get(self.OUTPUT_COL), self._hashes_of(t))]
+
+    # ------------------------------------------------------------------------ similarity search
+    def approx_nearest_neighbors(self, dataset: Table, key: Vector, k: int, dist_col: str = "distCol") -> Table:
+        dev = config.compute_device()
+        H = self._hashes_of(dataset).to(dev)
+        sets = _sets(vector_input(dataset, self.get(self.INPUT_COL))).to(dev)
+        ks = key.to_sparse() if hasattr(key, "to_sparse") else key
+        kset = SparseColumn(torch.tensor([0, len(ks.indices)], dtype=torch.int64, device=dev),
+                            torch.as_tensor(np.asarray(ks.indices, dtype=np.int32), device=dev),
+                            torch.ones(len(ks.indices), dtype=torch.float64, device=dev), ks.size())
+        kh = self.hash_function(kset.to(dev))[0]
+        cand = (H == kh[None]).all(dim=2).any(dim=1)
+        idx = torch.nonzero(cand, as_tuple=True)[0]
+        dist = _pair_jaccard(kset, sets, torch.zeros_like(idx), idx)
+        order = torch.argsort(dist, stable=True)[:k]
+        loc_idx, loc_dist = idx[order].cpu().tolist(), dist[order].cpu().tolist()
+        if get_world_distributed():
+            from ...parallel.context import get_context
+
+            me = get_context().rank
+            allc = [(d, r, i) for r, part in enumerate(comm.all_gather_object(list(zip(loc_dist, loc_idx))))
+                    for d, i in part]
+            allc.sort(key=lambda x: (x[0], x[1], x[2]))
+            chosen = [(i, d) for d, r, i in allc[:k] if r == me]
+        else:
+            chosen = list(zip(loc_idx, loc_dist))
+        rows = [i for i, _ in chosen]
+        out = dataset.with_column(self.get(self.OUTPUT_COL), H).take(rows)
+        return out.with_column(dist_col, torch.tensor([d for _, d in chosen], dtype=torch.float64))
+
+    approxNearestNeighbors = approx_nearest_neighbors
+
+    def approx_similarity_join(self, dataset_a: Table, dataset_b: Table, threshold: float, id_col: str,
+                               dist_col: str = "distCol") -> Table:
+        dev = config.compute_device()
+        ha = self._hashes_of(dataset_a).to(dev)
+        hb = self._hashes_of(dataset_b).to(dev)
+        sa = _sets(vector_input(dataset_a, self.get(self.INPUT_COL))).to(dev)
+        sb = _sets(vector_input(dataset_b, self.get(self.INPUT_COL))).to(dev)
+        ids_b = dataset_b.get_list(id_col)
+        if get_world_distributed():
+            # broadcast join: every rank sees all of B
+            parts = comm.all_gather_object((hb.cpu(), sb.to("cpu"), ids_b))
+            hb = torch.cat([p[0] for p in parts]).to(dev)
+            sb = SparseColumn.concat([p[1] for p in parts]).to(dev)
+            ids_b = [x for p in parts for x in p[2]]
+        na, nb = ha.shape[0], hb.shape[0]
+        pairs = []
+        for tb in range(ha.shape[1]):
+            allk = torch.cat([ha[:, tb], hb[:, tb]])
+            _, g = torch.unique(allk, dim=0, return_inverse=True)
+            ga, gb = g[:na], g[na:]
+            ob = torch.argsort(gb, stable=True)
+            gbs = gb[ob]
+            lo = torch.searchsorted(gbs, ga)
+            hi = torch.searchsorted(gbs, ga, right=True)
+            cnt = hi - lo
+            ia = torch.repeat_interleave(torch.arange(na, device=dev), cnt)
+            off = torch.arange(ia.numel(), device=dev) - torch.repeat_interleave(torch.cumsum(cnt, 0) - cnt, cnt)
+            ib = ob[lo[ia] + off]
+            pairs.append(ia * nb + ib)
+        keys = torch.unique(torch.cat(pairs)) if pairs else torch.zeros(0, dtype=torch.int64, device=dev)
+        ia, ib = torch.div(keys, nb, rounding_mode="floor"), keys % nb if nb else keys
+        dist = _pair_jaccard(sa, sb, ia, ib)
+        keep = dist <= threshold
+        ia, ib, dist = ia[keep].cpu().tolist(), ib[keep].cpu().tolist(), dist[keep].cpu()
+        ids_a = dataset_a.get_list(id_col)
+        return Table({"datasetA.id": [ids_a[i] for i in ia], "datasetB.id": [ids_b[j] for j in ib], dist_col: dist},
+                     num_rows=len(ia))
+
+    approxSimilarityJoin = approx_similarity_join
+
+
+@rw.register_stage
+class MinHashLSH(Estimator, LSHParams, HasSeed):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.lsh.MinHashLSH"
+
+    def fit(self, *inputs):
+        t = inputs[0]
+        col = t.column(self.get(self.INPUT_COL))
+        if isinstance(col, torch.Tensor):
+            sizes = {int(col.shape[1])} if t.num_rows else set()
+        elif isinstance(col, SparseColumn):
+            sizes = {col.size} if t.num_rows else set()
+        else:
+            sizes = {v.size() for v in col}
+        if get_world_distributed():
+            sizes = set(x for p in comm.all_gather_object(sorted(sizes)) for x in p)
+        if len(sizes) > 1:
+            s = sorted(sizes)
+            raise RuntimeError("Vector sizes are not the same: %d %d." % (s[0], s[1]))
+        if not sizes:
+            raise RuntimeError("The training set is empty.")
+        md = generate_model_data(self.get(self.NUM_HASH_TABLES), self.get(self.NUM_HASH_FUNCTIONS_PER_TABLE),
+                                 sizes.pop(), self.get_seed())
+        m = MinHashLSHModel().set_model_data(MinHashLSHModel.make_model_data_table([md]))
+        rw_update(m, self)
+        return m

@@ -1,0 +1,151 @@
+"""RandomSplitter and SQLTransformer (reference ``LIB/feature/{randomsplitter,sqltransformer}``).
+
+* RandomSplitter: each rank draws ``java.util.Random(Tuple2.of(seed, rank).hashCode())``
+  doubles (native host loop, bit-identical to ``SplitterOperator``) and routes row i to split
+  ``#{cumulative fractions < r_i}`` — one searchsorted and one gather per output.
+* SQLTransformer: the statement (``__THIS__`` = the input) runs on SQLite (stdlib) with the
+  input's scalar columns; vector/object columns pass through as opaque references. Row-wise
+  statements run per rank; statements that aggregate, sort, join or de-duplicate are evaluated
+  over the gathered table and the result is re-partitioned round-robin.
+"""
+from __future__ import annotations
+
+import math
+import re
+import sqlite3
+from typing import List
+
+import numpy as np
+import torch
+
+from ...api.stage import AlgoOperator
+from ...common.param import HasSeed
+from ...io import read_write as rw
+from ...param.param import FloatArrayParam, ParamValidator, StringParam
+from ...parallel import comm
+from ...table import Table, compact_column
+from ...utils.java import _i32, java_long_hash, java_random_doubles
+from .common import get_world_distributed
+
+
+def _weights_ok(w) -> bool:
+    return w is not None and len(w) > 1 and all(x > 0.0 for x in w)
+
+
+@rw.register_stage
+class RandomSplitter(AlgoOperator, HasSeed):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.randomsplitter.RandomSplitter"
+    WEIGHTS = FloatArrayParam("weights", "The weights of data splitting.", (1.0, 1.0),
+                              ParamValidator(_weights_ok, "weightsValidator"))
+
+    def transform(self, *inputs) -> List[Table]:
+        from ...parallel.context import get_context
+
+        t = inputs[0]
+        w = np.asarray(self.get(self.WEIGHTS), dtype=np.float64)
+        # the reference accumulates currentSum / weightSum element by element
+        acc, fr = 0.0, []
+        for x in w:
+            acc += x
+            fr.append(acc / w.sum())
+        fractions = np.asarray(fr)
+        rank = get_context().rank
+        # Tuple2.of(Long seed, Integer subtask).hashCode()
+        r = java_random_doubles(_i32(31 * java_long_hash(int(self.get_seed())) + rank), t.num_rows)
+        split = np.searchsorted(fractions, r, side="left")
+        return [t.take(torch.from_numpy(np.nonzero(split == i)[0])) for i in range(len(w))]
+
+
+_GLOBAL_SQL = re.compile(r"\b(GROUP\s+BY|ORDER\s+BY|DISTINCT|JOIN|LIMIT|OFFSET|UNION|INTERSECT|EXCEPT|HAVING|OVER|"
+                         r"COUNT|SUM|AVG|MIN|MAX|STDDEV\w*|VAR\w*|COLLECT|LISTAGG)\b", re.IGNORECASE)
+_REF = "\x00fmlx-ref:"
+
+
+def _statement_ok(s) -> bool:
+    return s is not None and "__THIS__" in s
+
+
+def _register_functions(con: sqlite3.Connection) -> None:
+    def f1(fn):
+        return lambda x: None if x is None else fn(x)
+
+    for name, fn in (("SQRT", math.sqrt), ("LN", math.log), ("LOG10", math.log10), ("EXP", math.exp),
+                     ("ABS", abs), ("CEIL", math.ceil), ("FLOOR", math.floor), ("SIN", math.sin), ("COS", math.cos),
+                     ("TAN", math.tan), ("SIGN", lambda x: (x > 0) - (x < 0))):
+        con.create_function(name, 1, f1(fn), deterministic=True)
+    con.create_function("POWER", 2, lambda a, b: None if a is None or b is None else math.pow(a, b),
+                        deterministic=True)
+    con.create_function("MOD", 2, lambda a, b: None if a is None or b is None else math.fmod(a, b),
+                        deterministic=True)
+
+
+def _sql_value(v):
+    if v is None or isinstance(v, (int, float, str, bytes)):
+        return v
+    if isinstance(v, (np.integer,)):
+        return int(v)
+    if isinstance(v, (np.floating,)):
+        return float(v)
+    if isinstance(v, (bool, np.bool_)):
+        return int(v)
+    return None  # replaced by a reference token below
+
+
+def run_sql(statement: str, t: Table) -> Table:
+    names = t.column_names
+    cols = [t.get_list(n) for n in names]
+    objects = []
+    rows = []
+    for i in range(t.num_rows):
+        row = []
+        for j, c in enumerate(cols):
+            v = c[i]
+            sv = _sql_value(v)
+            if sv is None and v is not None:
+                sv = "%s%d" % (_REF, len(objects))
+                objects.append(v)
+            row.append(sv)
+        rows.append(row)
+    con = sqlite3.connect(":memory:")
+    try:
+        _register_functions(con)
+        qn = ", ".join('"%s"' % n for n in names)
+        con.execute('CREATE TABLE __fmlx_this (%s)' % qn)
+        if rows:
+            con.executemany('INSERT INTO __fmlx_this VALUES (%s)' % ", ".join("?" * len(names)), rows)
+        cur = con.execute(statement.replace("__THIS__", "__fmlx_this"))
+        out_names = [d[0] for d in cur.description]
+        data = cur.fetchall()
+    finally:
+        con.close()
+
+    def unref(v):
+        if isinstance(v, str) and v.startswith(_REF):
+            return objects[int(v[len(_REF):])]
+        return v
+
+    out_cols = {}
+    for j, n in enumerate(out_names):
+        vals = [unref(r[j]) for r in data]
+        if vals and all(isinstance(v, float) or isinstance(v, int) for v in vals) and any(
+                isinstance(v, float) for v in vals):
+            vals = [float(v) for v in vals]
+        out_cols[n] = compact_column(vals)
+    return Table(out_cols, num_rows=len(data))
+
+
+@rw.register_stage
+class SQLTransformer(AlgoOperator):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.feature.sqltransformer.SQLTransformer"
+    STATEMENT = StringParam("statement", "SQL statement.", None, ParamValidator(_statement_ok, "statement"))
+
+    def transform(self, *inputs) -> List[Table]:
+        t = inputs[0]
+        stmt = self.get(self.STATEMENT)
+        if get_world_distributed() and _GLOBAL_SQL.search(stmt):
+            from ...parallel.context import get_context
+
+            ctx = get_context()
+            full = Table.concat(comm.all_gather_object(t.to("cpu")))
+            return [run_sql(stmt, full).partition(ctx.rank, ctx.world_size)]
+        return [run_sql(stmt, t.to("cpu"))]

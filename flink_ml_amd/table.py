@@ -84,6 +84,18 @@ class SparseColumn:
             out[rows, self.indices.to(device).long()] = self.values.to(device=device, dtype=dtype)
         return out
 
+    @staticmethod
+    def concat(parts: Sequence["SparseColumn"]) -> "SparseColumn":
+        """Row-wise concatenation (sizes must agree); result on the first part's device."""
+        parts = list(parts)
+        dev = parts[0].values.device
+        ptrs, off = [torch.zeros(1, dtype=torch.int64, device=dev)], 0
+        for p in parts:
+            ptrs.append(p.indptr[1:].to(dev).long() + off)
+            off += int(p.indptr[-1])
+        return SparseColumn(torch.cat(ptrs), torch.cat([p.indices.to(dev) for p in parts]),
+                            torch.cat([p.values.to(dev) for p in parts]), max(p.size for p in parts))
+
     def take(self, idx: torch.Tensor) -> "SparseColumn":
         idx = idx.cpu().long()
         vecs = [self.row(int(i)) for i in idx]
@@ -127,6 +139,8 @@ def _row_value(col, i: int):
     if isinstance(col, torch.Tensor):
         if col.dim() == 2:
             return DenseVector(col[i].double().cpu().numpy())
+        if col.dim() == 3:  # DenseVector[] per row (e.g. LSH hash signatures)
+            return [DenseVector(r) for r in col[i].double().cpu().numpy()]
         v = col[i].item()
         return v
     if isinstance(col, SparseColumn):
@@ -171,6 +185,8 @@ class Table:
             if all(isinstance(p, torch.Tensor) for p in parts) and len({(p.dim(), tuple(p.shape[1:])) for p in parts}) == 1:
                 dev = parts[0].device
                 out[name] = torch.cat([p.to(dev) for p in parts], dim=0)
+            elif all(isinstance(p, SparseColumn) for p in parts) and len({p.size for p in parts}) == 1:
+                out[name] = SparseColumn.concat(parts)
             else:
                 rows = []
                 for t in tables:

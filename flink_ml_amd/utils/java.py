@@ -208,3 +208,20 @@ class JavaRandom:
     nextLong = next_long
     nextDouble = next_double
     nextGaussian = next_gaussian
+
+
+def java_random_doubles(seed: int, n: int):
+    """``n`` successive ``new Random(seed).nextDouble()`` values (native host loop)."""
+    import ctypes
+
+    import numpy as np
+
+    from ..ops import native
+
+    out = np.empty(n, dtype=np.float64)
+    if n:
+        lib = native.host()
+        fn = lib.fmlx_java_next_doubles
+        fn.argtypes, fn.restype = [ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p], None
+        fn(int(seed), int(n), out.ctypes.data)
+    return out

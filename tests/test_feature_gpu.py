@@ -68,11 +68,11 @@ def test_scalers_on_device_match_cpu():
         oc = est.fit(tc).transform(tc)[0].column("output")
         og = est.fit(tg).transform(tg)[0].column("output")
         assert og.is_cuda
-        torch.testing.assert_close(og.double().cpu(), oc.double(), rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(og.double().cpu(), oc.double().cpu(), rtol=1e-5, atol=1e-5)
     kb = KBinsDiscretizer().set_strategy("uniform").set_num_bins(7)
     bc = kb.fit(tc).transform(tc)[0].column("output")
     bg = kb.fit(tg).transform(tg)[0].column("output")
-    assert torch.equal(bg.cpu(), bc)
+    assert torch.equal(bg.cpu(), bc.cpu())
 
 
 def test_hashing_tf_device():
