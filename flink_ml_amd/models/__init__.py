@@ -11,3 +11,6 @@ from . import feature  # noqa: F401,E402
 from .feature import *  # noqa: F401,F403,E402
 from . import stats  # noqa: F401,E402
 from .stats import ANOVATest, ChiSqTest, FValueTest  # noqa: F401,E402
+from . import knn, naive_bayes  # noqa: F401,E402
+from .knn import Knn, KnnModel  # noqa: F401,E402
+from .naive_bayes import NaiveBayes, NaiveBayesModel  # noqa: F401,E402

@@ -1,0 +1,178 @@
+"""NaiveBayes / NaiveBayesModel, multinomial over categorical feature values
+(reference ``LIB/classification/naivebayes/{NaiveBayes,NaiveBayesModel,NaiveBayesModelData}.java``).
+
+fit: the per-(label, feature, value) counts the reference builds with two keyed mapPartitions
+(C11/K22) are, per feature column, one ``bincount`` over (value-index, label-index) on the device;
+the tables of all columns are all-reduced in one call. Then, as in ``GenerateModelFunction``:
+
+    theta[l][j][v] = log(count(l, j, v) + s) − log(n_l + s·|V_j|)
+    pi[l]          = log(n_l·d + s) − log(n·d + L·s)
+
+predict: every feature value becomes a column index into one flattened [L, ΣV_j] log-probability
+table, so a block of rows is a single gather + sum over features; argmax with the reference's
+first-max rule. An unseen feature value raises (the reference fails with an NPE).
+"""
+from __future__ import annotations
+
+from typing import Dict, List
+
+import numpy as np
+import torch
+
+from .. import config
+from ..api.stage import Estimator
+from ..common.param import HasFeaturesCol, HasLabelCol, HasPredictionCol
+from ..io import read_write as rw
+from ..io import serialization as ser
+from ..linalg.vectors import DenseVector
+from ..param.param import FloatParam, ParamValidators, StringParam
+from ..parallel import comm
+from ..table import SparseColumn, Table
+from ..utils.java import java_double_hash, java_hashmap_order
+from .base import ModelWithData
+from .feature.common import get_world_distributed
+from .linear import rw_update
+from .stats import features_and_labels, global_sorted_unique
+
+
+class NaiveBayesModelParams(HasFeaturesCol, HasPredictionCol):
+    MODEL_TYPE = StringParam("modelType", "The model type.", "multinomial", ParamValidators.in_array("multinomial"))
+
+
+class NaiveBayesParams(NaiveBayesModelParams, HasLabelCol):
+    SMOOTHING = FloatParam("smoothing", "The smoothing parameter.", 1.0, ParamValidators.gt_eq(0.0))
+
+
+def _ordered(m: Dict[float, float]) -> Dict[float, float]:
+    return {k: m[k] for k in java_hashmap_order(list(m.keys()), java_double_hash)}
+
+
+@rw.register_stage
+class NaiveBayesModel(ModelWithData, NaiveBayesModelParams):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.classification.naivebayes.NaiveBayesModel"
+    MODEL_DATA_COLUMNS = ("theta", "piArray", "labels")
+
+    @staticmethod
+    def encode_record(out, row):
+        theta, pi, labels = row
+        ser.write_dense_vector(out, labels)
+        ser.write_dense_vector(out, pi)
+        out.write_int(len(theta))
+        out.write_int(len(theta[0]))
+        for maps in theta:
+            for m in maps:
+                ser.write_map(out, _ordered(m), lambda o, k: o.write_double(k), lambda o, v: o.write_double(v))
+
+    @staticmethod
+    def decode_record(inp):
+        labels = ser.read_dense_vector(inp)
+        pi = ser.read_dense_vector(inp)
+        nl, nf = inp.read_int(), inp.read_int()
+        theta = [[ser.read_map(inp, lambda i: i.read_double(), lambda i: i.read_double()) for _ in range(nf)]
+                 for _ in range(nl)]
+        return (theta, pi, labels)
+
+    @classmethod
+    def make_model_data_table(cls, rows):
+        return Table({"theta": [r[0] for r in rows], "piArray": [r[1] for r in rows], "labels": [r[2] for r in rows]},
+                     num_rows=len(rows))
+
+    def _build_state(self, rows):
+        theta, pi, labels = rows[0]
+        dev = config.compute_device()
+        nl, nf = len(theta), len(theta[0])
+        vals, offs, flat_cols = [], [0], []
+        for j in range(nf):
+            v = sorted(theta[0][j].keys())
+            vals.append(torch.tensor(v, dtype=torch.float64, device=dev))
+            flat_cols.append(np.array([[theta[i][j].get(x, np.nan) for x in v] for i in range(nl)]).reshape(nl, -1))
+            offs.append(offs[-1] + len(v))
+        table = torch.from_numpy(np.concatenate(flat_cols, axis=1) if flat_cols else np.zeros((nl, 0))).to(dev)
+        return (vals, torch.tensor(offs[:-1], dtype=torch.int64, device=dev), table,
+                torch.as_tensor(np.asarray(pi.values), device=dev), torch.as_tensor(np.asarray(labels.values),
+                                                                                   device=dev))
+
+    def transform(self, *inputs):
+        t = inputs[0]
+        vals, offs, table, pi, labels = self._model_state()
+        c = t.column(self.get(self.FEATURES_COL))
+        X = c.to_dense(torch.float64, device=table.device) if isinstance(c, SparseColumn) else \
+            config.features_for_compute(t, self.get(self.FEATURES_COL), allow_sparse=False).to(table.device,
+                                                                                                torch.float64)
+        n, d = X.shape
+        if d > len(vals):
+            raise ValueError("The input vector has %d features, the model has %d." % (d, len(vals)))
+        cols = torch.empty((n, d), dtype=torch.int64, device=X.device)
+        for j in range(d):
+            pos = torch.clamp(torch.searchsorted(vals[j], X[:, j].contiguous()), max=vals[j].numel() - 1)
+            if not bool((vals[j][pos] == X[:, j]).all()):
+                raise RuntimeError("Feature %d of the input contains a value unseen in training." % j)
+            cols[:, j] = offs[j] + pos
+        probs = table[:, cols].sum(dim=2).t() + pi[None, :] if d else pi[None, :].expand(n, -1)
+        pred = labels[torch.argmax(probs, dim=1)]  # first max, like findMaxProbLabel
+        return [t.with_column(self.get(self.PREDICTION_COL), pred.to(torch.float64))]
+
+
+@rw.register_stage
+class NaiveBayes(Estimator, NaiveBayesParams):
+    JAVA_CLASS_NAME = "org.apache.flink.ml.classification.naivebayes.NaiveBayes"
+
+    def fit(self, *inputs):
+        t = inputs[0]
+        lab = t.column(self.get(self.LABEL_COL))
+        if isinstance(lab, list) and any(v is None for v in lab):
+            raise ValueError("Input data should contain label value.")
+        fc = t.column(self.get(self.FEATURES_COL))
+        if isinstance(fc, list) and len({v.size() for v in fc}) > 1:
+            raise ValueError("Feature vectors should be of equal length.")
+        X, y = features_and_labels(t, self.get(self.FEATURES_COL), self.get(self.LABEL_COL))
+        if bool((y != torch.round(y)).any()):
+            raise ValueError("Label value should be indexed number.")
+        s = self.get(self.SMOOTHING)
+        dist = get_world_distributed()
+        dims = comm.all_gather_object(int(X.shape[1])) if dist else [int(X.shape[1])]
+        if len(set(d for d, r in zip(dims, range(len(dims))))) > 1:
+            raise ValueError("Feature vectors should be of equal length.")
+        labels = global_sorted_unique(y)
+        L, d = labels.numel(), X.shape[1]
+        li = torch.searchsorted(labels, y)
+        local_vals = [torch.unique(X[:, j]) for j in range(d)]
+        if dist:
+            parts = comm.all_gather_object([v.cpu().tolist() for v in local_vals])
+            vals = [torch.tensor(sorted(set(x for p in parts for x in p[j])), dtype=torch.float64, device=X.device)
+                    for j in range(d)]
+        else:
+            vals = local_vals
+        tables = [torch.bincount(li * vals[j].numel() + torch.searchsorted(vals[j], X[:, j].contiguous()),
+                                 minlength=L * vals[j].numel()).to(torch.float64) for j in range(d)]
+        tables.append(torch.bincount(li, minlength=L).to(torch.float64))
+        flat = torch.cat(tables)
+        if dist:
+            flat = comm.all_reduce_sum(flat)
+        flat = flat.cpu().numpy()
+        n_l = flat[-L:]
+        labels_np = labels.cpu().numpy()
+        # the reference's model lists labels in HashMap<Double, _> order
+        order = [int(np.searchsorted(labels_np, v)) for v in java_hashmap_order(labels_np.tolist(), java_double_hash)]
+        n_total = n_l.sum()
+        pi_log = np.log(n_total * d + L * s)
+        theta: List[List[Dict[float, float]]] = []
+        off = 0
+        counts = []
+        for j in range(d):
+            V = vals[j].numel()
+            counts.append(flat[off:off + L * V].reshape(L, V))
+            off += L * V
+        for li_ in order:
+            row = []
+            for j in range(d):
+                V = vals[j].numel()
+                tlog = np.log(n_l[li_] + s * V)
+                vv = vals[j].cpu().numpy()
+                row.append({float(vv[c]): float(np.log(counts[j][li_, c] + s) - tlog) for c in range(V)})
+            theta.append(row)
+        pi = DenseVector(np.array([np.log(n_l[i] * d + s) - pi_log for i in order]))
+        md = (theta, pi, DenseVector(labels_np[order].astype(np.float64)))
+        m = NaiveBayesModel().set_model_data(NaiveBayesModel.make_model_data_table([md]))
+        rw_update(m, self)
+        return m

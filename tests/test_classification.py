@@ -1,0 +1,135 @@
+"""Knn and NaiveBayes against LIBT/classification/{KnnTest,NaiveBayesTest}.java and the Python
+tests' expectations; distributed fits over gloo ranks; GPU path of the Knn GEMM/top-k."""
+import numpy as np
+import pytest
+import torch
+
+from flink_ml_amd import Table, Vectors
+from flink_ml_amd.models import Knn, KnnModel, NaiveBayes, NaiveBayesModel
+from tests.spmd import run_spmd
+
+KNN_TRAIN = [([2.0, 3.0], 1.0), ([2.1, 3.1], 1.0), ([200.1, 300.1], 2.0), ([200.2, 300.2], 2.0), ([200.3, 300.3], 2.0),
+             ([200.4, 300.4], 2.0), ([200.4, 300.4], 2.0), ([200.6, 300.6], 2.0), ([2.1, 3.1], 1.0), ([2.1, 3.1], 1.0),
+             ([2.1, 3.1], 1.0), ([2.1, 3.1], 1.0), ([2.3, 3.2], 1.0), ([2.3, 3.2], 1.0), ([2.8, 3.2], 3.0),
+             ([300., 3.2], 4.0), ([2.2, 3.2], 1.0), ([2.4, 3.2], 5.0), ([2.5, 3.2], 5.0), ([2.5, 3.2], 5.0),
+             ([2.1, 3.1], 1.0)]
+KNN_PRED = [([4.0, 4.1], 5.0), ([300, 42], 2.0)]
+
+
+def _t(rows, sparse=False):
+    return Table.from_rows([((Vectors.dense(*f).to_sparse() if sparse else Vectors.dense(*f)), l) for f, l in rows],
+                           ["features", "label"])
+
+
+def _check_pred(out):
+    for label, pred in zip(out.get_list("label"), out.get_list("prediction")):
+        assert label == pred
+
+
+def test_knn(tmp_path):
+    knn = Knn()
+    assert knn.get_k() == 5 and knn.get_features_col() == "features" and knn.get_prediction_col() == "prediction"
+    model = knn.fit(_t(KNN_TRAIN))
+    out = model.transform(_t(KNN_PRED))[0]
+    assert out.column_names == ["features", "label", "prediction"]
+    _check_pred(out)
+    _check_pred(Knn().fit(_t(KNN_PRED)).transform(_t(KNN_PRED))[0])  # fewer points than k
+    _check_pred(Knn().fit(_t(KNN_TRAIN, True)).transform(_t(KNN_PRED, True))[0])
+    p = str(tmp_path / "knn")
+    model.save(p)
+    loaded = KnnModel.load(p)
+    _check_pred(loaded.transform(_t(KNN_PRED))[0])
+    md = model.get_model_data()[0]
+    assert md.column_names == ["packedFeatures", "featureNormSquares", "labels"]
+    m, norms, labels = md.rows()[0]
+    assert (m.num_rows, m.num_cols) == (2, 21)
+    np.testing.assert_allclose(norms.values[:2], [13.0, 2.1 ** 2 + 3.1 ** 2])
+    m2 = KnnModel().set_model_data(md)
+    _check_pred(m2.transform(_t(KNN_PRED))[0])
+
+
+def _spmd_knn(rank, world):
+    model = Knn().fit(_t(KNN_TRAIN).partition(rank, world))
+    out = model.transform(_t(KNN_PRED).partition(rank, world))[0]
+    return list(zip(out.get_list("label"), out.get_list("prediction"))), model.get_model_data()[0].rows()[0][0].num_cols
+
+
+def test_knn_distributed():
+    res = run_spmd(_spmd_knn, 2)
+    assert all(n == 21 for _, n in res)
+    assert sorted(x for r, _ in res for x in r) == [(2.0, 2.0), (5.0, 5.0)]
+
+
+NB_TRAIN = [([0, 0.], 11.), ([1, 0], 10.), ([1, 1.], 10.)]
+NB_PRED = [[0, 1.], [0, 0.], [1, 0], [1, 1.]]
+NB_EXPECTED = [11., 11., 10., 10.]
+
+
+def _nb_pred():
+    return Table.from_rows([(Vectors.dense(*f),) for f in NB_PRED], ["features"])
+
+
+def test_naive_bayes(tmp_path):
+    est = NaiveBayes()
+    assert est.get_smoothing() == 1.0 and est.get_model_type() == "multinomial"
+    est.set_smoothing(2.0)
+    assert est.get_smoothing() == 2.0
+    model = NaiveBayes().fit(_t(NB_TRAIN))
+    assert model.transform(_nb_pred())[0].get_list("prediction") == NB_EXPECTED
+    p = str(tmp_path / "nb")
+    model.save(p)
+    assert NaiveBayesModel.load(p).transform(_nb_pred())[0].get_list("prediction") == NB_EXPECTED
+    assert NaiveBayesModel().set_model_data(*model.get_model_data()).transform(_nb_pred())[0].get_list(
+        "prediction") == NB_EXPECTED
+    sp = Table.from_rows([(Vectors.dense(*f).to_sparse(),) for f in NB_PRED], ["features"])
+    assert model.transform(sp)[0].get_list("prediction") == NB_EXPECTED
+
+
+def test_naive_bayes_model_data_and_errors():
+    md = NaiveBayes().fit(_t([([1, 1.], 11.), ([2, 1], 11.)])).get_model_data()[0]
+    assert md.column_names == ["theta", "piArray", "labels"]
+    theta, pi, labels = md.rows()[0]
+    assert list(labels.values) == [11.0] and abs(pi.values[0]) < 1e-9
+    assert abs(theta[0][0][1.0] + 0.6931471805599453) < 1e-9 and abs(theta[0][0][2.0] + 0.6931471805599453) < 1e-9
+    assert abs(theta[0][1][1.0]) < 1e-9
+    model = NaiveBayes().fit(_t(NB_TRAIN))
+    with pytest.raises(RuntimeError, match="unseen"):
+        model.transform(Table.from_rows([(Vectors.dense(2, 1.),)], ["features"]))
+    with pytest.raises(ValueError, match="equal length"):
+        NaiveBayes().fit(Table.from_rows([(Vectors.dense(0, 0.), 11.0), (Vectors.dense(1), 10.0)],
+                                         ["features", "label"]))
+    with pytest.raises(ValueError, match="indexed number"):
+        NaiveBayes().fit(_t([([0, 0.], 1.5)]))
+
+
+def _spmd_nb(rank, world):
+    m = NaiveBayes().fit(_t(NB_TRAIN).partition(rank, world))
+    theta, pi, labels = m.get_model_data()[0].rows()[0]
+    return m.transform(_nb_pred())[0].get_list("prediction"), list(pi.values), list(labels.values)
+
+
+def test_naive_bayes_distributed():
+    single = NaiveBayes().fit(_t(NB_TRAIN)).get_model_data()[0].rows()[0]
+    for pred, pi, labels in run_spmd(_spmd_nb, 2):
+        assert pred == NB_EXPECTED
+        np.testing.assert_allclose(pi, single[1].values)
+        assert labels == list(single[2].values)
+
+
+@pytest.mark.gpu
+def test_knn_gpu_matches_cpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from flink_ml_amd.models.knn import knn_predict
+
+    g = torch.Generator().manual_seed(0)
+    centers = torch.randn(8, 32, generator=g, dtype=torch.float64) * 10
+    lab = torch.randint(0, 8, (20000,), generator=g)
+    T = centers[lab] + torch.randn(20000, 32, generator=g, dtype=torch.float64)
+    ql = torch.randint(0, 8, (3000,), generator=g)
+    Q = centers[ql] + torch.randn(3000, 32, generator=g, dtype=torch.float64)
+    tn = (T * T).sum(1)
+    cpu = knn_predict(Q, T, tn, lab.double(), 5)
+    gpu = knn_predict(Q.cuda(), T.cuda(), tn.cuda(), lab.double().cuda(), 5)
+    assert (gpu.cpu() == cpu).double().mean() > 0.999
+    assert (cpu == ql.double()).double().mean() > 0.99
