@@ -14,3 +14,5 @@ from .stats import ANOVATest, ChiSqTest, FValueTest  # noqa: F401,E402
 from . import knn, naive_bayes  # noqa: F401,E402
 from .knn import Knn, KnnModel  # noqa: F401,E402
 from .naive_bayes import NaiveBayes, NaiveBayesModel  # noqa: F401,E402
+from . import evaluation  # noqa: F401,E402
+from .evaluation import BinaryClassificationEvaluator  # noqa: F401,E402
