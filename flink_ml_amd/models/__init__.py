@@ -16,3 +16,5 @@ from .knn import Knn, KnnModel  # noqa: F401,E402
 from .naive_bayes import NaiveBayes, NaiveBayesModel  # noqa: F401,E402
 from . import evaluation  # noqa: F401,E402
 from .evaluation import BinaryClassificationEvaluator  # noqa: F401,E402
+from . import agglomerative  # noqa: F401,E402
+from .agglomerative import AgglomerativeClustering  # noqa: F401,E402

@@ -118,6 +118,8 @@ def window_all_and_process(table: Table, windows: Windows, fn: Callable[[Table],
     """Applies ``fn`` to every window of the (globally gathered) input; the result is produced on
     rank 0 (parallelism-1 semantics of ``windowAll``) and is empty on other ranks."""
     ctx = get_context()
+    if time_col is None:
+        time_col = getattr(table, "time_col", None)
     parts = comm.all_gather_object(table.to("cpu")) if ctx.is_distributed else [table]
     full = Table.concat(parts) if len(parts) > 1 else parts[0]
     if ctx.rank != 0:

@@ -151,8 +151,12 @@ def _row_value(col, i: int):
 class Table:
     """An ordered mapping of column name → column (see module docstring)."""
 
-    def __init__(self, columns: Optional[Dict[str, Column]] = None, num_rows: Optional[int] = None):
+    def __init__(self, columns: Optional[Dict[str, Column]] = None, num_rows: Optional[int] = None,
+                 time_col: Optional[str] = None):
         self._cols: Dict[str, Column] = dict(columns or {})
+        # event-time attribute (the analogue of a Flink rowtime column with a watermark): time
+        # windows cut on it; it survives column-preserving transformations
+        self.time_col = time_col if time_col in self._cols else None
         if num_rows is None:
             num_rows = _col_len(next(iter(self._cols.values()))) if self._cols else 0
         self._n = int(num_rows)
@@ -192,7 +196,7 @@ class Table:
                 for t in tables:
                     rows.extend(t.get_list(name))
                 out[name] = compact_column(rows)
-        return Table(out, num_rows=sum(t.num_rows for t in tables))
+        return Table(out, num_rows=sum(t.num_rows for t in tables), time_col=tables[0].time_col)
 
     # -- introspection -----------------------------------------------------------------------
     @property
@@ -283,23 +287,30 @@ class Table:
     def with_column(self, name: str, col: Column) -> "Table":
         cols = dict(self._cols)
         cols[name] = col
-        return Table(cols, num_rows=self._n)
+        return Table(cols, num_rows=self._n, time_col=self.time_col)
 
     def with_columns(self, mapping: Dict[str, Column]) -> "Table":
         cols = dict(self._cols)
         cols.update(mapping)
-        return Table(cols, num_rows=self._n)
+        return Table(cols, num_rows=self._n, time_col=self.time_col)
 
     def select(self, *names: str) -> "Table":
         if len(names) == 1 and isinstance(names[0], (list, tuple)):
             names = tuple(names[0])
-        return Table({n: self.column(n) for n in names}, num_rows=self._n)
+        return Table({n: self.column(n) for n in names}, num_rows=self._n, time_col=self.time_col)
 
     def drop(self, *names: str) -> "Table":
-        return Table({k: v for k, v in self._cols.items() if k not in names}, num_rows=self._n)
+        return Table({k: v for k, v in self._cols.items() if k not in names}, num_rows=self._n, time_col=self.time_col)
 
     def rename(self, mapping: Dict[str, str]) -> "Table":
-        return Table({mapping.get(k, k): v for k, v in self._cols.items()}, num_rows=self._n)
+        return Table({mapping.get(k, k): v for k, v in self._cols.items()}, num_rows=self._n,
+                     time_col=mapping.get(self.time_col, self.time_col))
+
+    def with_time_column(self, name: str) -> "Table":
+        """Marks ``name`` (epoch milliseconds) as the event-time attribute for time windows."""
+        if name not in self._cols:
+            raise KeyError(name)
+        return Table(dict(self._cols), num_rows=self._n, time_col=name)
 
     def take(self, idx) -> "Table":
         if isinstance(idx, torch.Tensor) and idx.dtype == torch.bool:
@@ -313,7 +324,7 @@ class Table:
                 cols[k] = c.take(idx_t)
             else:
                 cols[k] = [c[int(i)] for i in idx_t]
-        return Table(cols, num_rows=int(idx_t.shape[0]))
+        return Table(cols, num_rows=int(idx_t.shape[0]), time_col=self.time_col)
 
     def slice(self, start: int, end: int) -> "Table":
         return self.take(torch.arange(start, min(end, self._n)))
@@ -328,7 +339,7 @@ class Table:
                 cols[k] = c.to(device)
             else:
                 cols[k] = c
-        return Table(cols, num_rows=self._n)
+        return Table(cols, num_rows=self._n, time_col=self.time_col)
 
     def partition(self, rank: int, world: int) -> "Table":
         """Round-robin partition, the analogue of Flink's ``rebalance()``."""
