@@ -1,0 +1,133 @@
+"""Benchmark runner (reference ``flink-ml-benchmark/.../Benchmark.java`` + ``BenchmarkUtils.java``).
+
+Reads a JSON v1 config (``"version": 1`` plus named benchmarks of ``stage`` / ``inputData`` /
+optional ``modelData``, each a ``className`` + ``paramMap``; ``//`` comment lines allowed) and, for
+every benchmark, on every rank:
+
+1. instantiates the stage and generators (unknown params fail like the reference);
+2. times — between barrier + device synchronisation on both sides, max over ranks — the data
+   generation plus ``fit(...).get_model_data()`` for Estimators or ``transform(...)`` for
+   AlgoOperators (the reference's ``netRuntime`` also covers its source operators);
+3. reports ``totalTimeMs, inputRecordNum, inputThroughput, outputRecordNum, outputThroughput``
+   (+ ``stageTimeMs``/``generateTimeMs`` splits), or ``{"exception": ...}`` on failure.
+
+Results are written (rank 0) in the reference's result-file shape: the config entry plus a
+``results`` object, keyed by benchmark name.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+import traceback
+from typing import Dict, Optional
+
+import torch
+
+from .. import config
+from ..api.stage import AlgoOperator, Estimator, Model
+from ..io import read_write as rw
+from ..parallel import comm
+from ..parallel.context import get_context, init_distributed
+from . import generators  # noqa: F401  (registers the generator classes)
+
+
+def load_config(path: str) -> Dict:
+    with open(path, encoding="utf-8") as f:
+        text = "\n".join(l for l in f.read().split("\n") if not l.strip().startswith("//"))
+    conf = json.loads(text)
+    if conf.get("version") != 1:
+        raise ValueError("Unsupported benchmark config version %s" % conf.get("version"))
+    return conf
+
+
+def _sync():
+    if torch.cuda.is_available() and config.compute_device().type == "cuda":
+        torch.cuda.synchronize()
+    if get_context().is_distributed:
+        comm.barrier()
+
+
+def _count_rows(tables) -> int:
+    """Rows the reference's counting sink would see: partitioned tables are summed over ranks,
+    replicated ones (model data, statistics) counted once."""
+    ctx = get_context()
+    part = sum(int(t.num_rows) for t in tables if t is not None and not t.replicated)
+    rep = sum(int(t.num_rows) for t in tables if t is not None and t.replicated)
+    if ctx.is_distributed:
+        part = int(comm.all_reduce_scalar(float(part), "sum"))
+    return part + rep
+
+
+def run_benchmark(name: str, spec: Dict) -> Dict:
+    stage = rw.instantiate_with_params(spec["stage"])
+    in_gen = rw.instantiate_with_params(spec["inputData"])
+    md_gen = rw.instantiate_with_params(spec["modelData"]) if "modelData" in spec else None
+    _sync()
+    t0 = time.perf_counter()
+    inputs = in_gen.get_data()
+    if md_gen is not None:
+        if not isinstance(stage, Model):
+            raise ValueError("modelData given for a non-Model stage %s" % type(stage).__name__)
+        stage.set_model_data(*md_gen.get_data())
+    _sync()
+    t1 = time.perf_counter()
+    if isinstance(stage, Estimator):
+        outputs = stage.fit(*inputs).get_model_data()
+    elif isinstance(stage, AlgoOperator):
+        outputs = stage.transform(*inputs)
+    else:
+        raise ValueError("Unsupported Stage class %s" % type(stage).__name__)
+    _sync()
+    t2 = time.perf_counter()
+    times = torch.tensor([t2 - t0, t1 - t0, t2 - t1], dtype=torch.float64)
+    if get_context().is_distributed:
+        times = comm.all_reduce(times, "max")
+    total_ms, gen_ms, stage_ms = (float(x) * 1000.0 for x in times)
+    n_in = int(in_gen.get(in_gen.NUM_VALUES))
+    n_out = _count_rows(outputs)
+    return {"totalTimeMs": total_ms, "inputRecordNum": n_in, "inputThroughput": n_in * 1000.0 / total_ms,
+            "outputRecordNum": n_out, "outputThroughput": n_out * 1000.0 / total_ms, "generateTimeMs": gen_ms,
+            "stageTimeMs": stage_ms, "stageInputThroughput": n_in * 1000.0 / stage_ms if stage_ms > 0 else None}
+
+
+def run_config(conf: Dict, pattern: Optional[str] = None, verbose: bool = True) -> Dict:
+    import re
+
+    out = {}
+    rx = re.compile(pattern) if pattern else None
+    for name, spec in conf.items():
+        if name == "version" or (rx and not rx.match(name)):
+            continue
+        entry = dict(spec)
+        try:
+            entry["results"] = run_benchmark(name, spec)
+        except Exception as e:  # noqa: BLE001 - recorded like the reference's exception results
+            entry["results"] = {"exception": "%s: %s" % (type(e).__name__, e)}
+            if verbose and get_context().rank == 0:
+                traceback.print_exc()
+        out[name] = entry
+        if verbose and get_context().rank == 0:
+            print("%s: %s" % (name, json.dumps(entry["results"])), flush=True)
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="Runs the benchmarks of a JSON v1 config file.")
+    ap.add_argument("config", help="Benchmark JSON config")
+    ap.add_argument("--output-file", help="Where to write the results JSON")
+    ap.add_argument("--pattern", help="Regex of benchmark names to run", default=None)
+    args = ap.parse_args(argv)
+    if "RANK" in os.environ and "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) > 1:
+        init_distributed()
+    res = run_config(load_config(args.config), args.pattern)
+    if get_context().rank == 0 and args.output_file:
+        with open(args.output_file, "w", encoding="utf-8") as f:
+            json.dump(res, f, indent=2)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

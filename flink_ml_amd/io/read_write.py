@@ -131,19 +131,24 @@ def load_metadata(path: str, expected_class_name: str = "") -> Dict[str, Any]:
     return meta
 
 
-def instantiate_with_params(meta: Dict[str, Any]):
+def instantiate_with_params(meta: Dict[str, Any], strict: bool = True):
     cls = lookup_stage_class(meta["className"])
     stage = cls()
-    pm = meta.get("paramMap", {})
-    for p in list(stage.get_param_map().keys()):
-        if p.name in pm:
-            stage.set(p, p.json_decode(pm[p.name]))
+    pm = meta.get("paramMap", {}) or {}
+    by_name = {p.name: p for p in stage.get_param_map().keys()}
+    for name, value in pm.items():
+        p = by_name.get(name)
+        if p is None and not strict:
+            continue
+        if p is None:  # the reference dereferences a null Param here (NPE)
+            raise ValueError("Parameter %s is not defined on the class %s" % (name, cls.__name__))
+        stage.set(p, p.json_decode(value))
     return stage
 
 
 def load_stage_param(path: str):
     """Instantiates the stage recorded in ``<path>/metadata`` and restores its params."""
-    return instantiate_with_params(load_metadata(path))
+    return instantiate_with_params(load_metadata(path), strict=False)
 
 
 def load_stage(path: str):

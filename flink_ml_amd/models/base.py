@@ -33,6 +33,8 @@ class ModelWithData(Model):
         return self
 
     def get_model_data(self) -> List[Table]:
+        if self._md_table is not None:
+            self._md_table.replicated = True  # every rank holds the full model data
         return [self._md_table]
 
     def model_data_rows(self) -> List[tuple]:

@@ -150,4 +150,4 @@ class BinaryClassificationEvaluator(AlgoOperator, HasLabelCol, HasRawPredictionC
                                       self.get(self.WEIGHT_COL))
         m = compute_metrics(score, pos, w)
         names = self.get(self.METRICS_NAMES)
-        return [Table({k: torch.tensor([m[k]], dtype=torch.float64) for k in names}, num_rows=1)]
+        return [Table({k: torch.tensor([m[k]], dtype=torch.float64) for k in names}, num_rows=1).as_replicated()]

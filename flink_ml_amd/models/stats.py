@@ -74,10 +74,10 @@ def _result_table(idx_name: str, stat_name: str, flat_names, p, dof, stat, flatt
     if flatten:
         return Table({flat_names[0]: torch.arange(d, dtype=torch.int64), flat_names[1]: torch.tensor(p, dtype=torch.float64),
                       flat_names[2]: torch.tensor(dof, dtype=torch.int64), flat_names[3]: torch.tensor(stat, dtype=torch.float64)},
-                     num_rows=d)
+                     num_rows=d).as_replicated()
     return Table({idx_name: [DenseVector(np.asarray(p, dtype=np.float64))],
                   "degreesOfFreedom": [[dof_kind(x) for x in dof]],
-                  stat_name: [DenseVector(np.asarray(stat, dtype=np.float64))]}, num_rows=1)
+                  stat_name: [DenseVector(np.asarray(stat, dtype=np.float64))]}, num_rows=1).as_replicated()
 
 
 class _TestParams(HasFeaturesCol, HasLabelCol, HasFlatten):

@@ -1,0 +1,120 @@
+// Bit-exact java.util.Random streams on the GPU for the benchmark data generators
+// (reference flink-ml-benchmark/.../datagenerator/common/*Generator.java; RowGenerator seeds each
+// task with new Random(Tuple2.of(seed, taskIdx).hashCode()) and draws row after row).
+//
+// java.util.Random is a 48-bit LCG, so the state after k draws is an affine map of the seed:
+// x_k = A_k x + C_k (mod 2^48). Every thread jumps straight to its row's first draw with
+// (A_k, C_k) computed by binary powering (the low 48 bits of 64-bit products are exact), then
+// runs the row's "program" sequentially: nextDouble (2 draws) or nextInt(bound) (1 draw;
+// power-of-two bounds never reject). For other bounds Java's nextInt rejects u with
+// u - u % bound + bound - 1 >= 2^31 and draws again (probability ~ bound / 2^31 per draw);
+// the kernel reports the first row that would reject and the host replays that row
+// sequentially and relaunches for the remaining rows at the shifted offset, so the output is
+// exactly the reference stream.
+//
+// Outputs: the first `nvec` program slots go to a dense [n, nvec] buffer in the requested dtype
+// (the features column, written coalesced); the remaining slots go to an fp64 [n, nscalar] buffer
+// (label / weight / scalar columns).
+#include "common.h"
+
+namespace {
+constexpr unsigned long long kMult = 0x5DEECE66DULL;
+constexpr unsigned long long kAdd = 0xBULL;
+constexpr unsigned long long kMask = (1ULL << 48) - 1;
+
+__device__ __forceinline__ unsigned long long jump(unsigned long long x, unsigned long long k) {
+  unsigned long long A = 1, C = 0;  // accumulated map
+  unsigned long long a = kMult, c = kAdd;  // map for 2^i steps
+  while (k) {
+    if (k & 1) {
+      A = (A * a) & kMask;
+      C = (C * a + c) & kMask;
+    }
+    c = (c * a + c) & kMask;
+    a = (a * a) & kMask;
+    k >>= 1;
+  }
+  return (A * x + C) & kMask;
+}
+
+__device__ __forceinline__ int next_bits(unsigned long long& s, int bits) {
+  s = (s * kMult + kAdd) & kMask;
+  return (int)(long long)(s >> (48 - bits));
+}
+
+template <typename T>
+__device__ __forceinline__ void store(T* p, double v) {
+  *p = (T)v;
+}
+template <>
+__device__ __forceinline__ void store<bf16_t>(bf16_t* p, double v) {
+  *p = f32_to_bf16((float)v);
+}
+
+// ops: per slot, 0 = nextDouble, >0 = nextInt(bound). draws_per_row = sum(op == 0 ? 2 : 1).
+template <typename T>
+__global__ __launch_bounds__(256) void java_rows_kernel(unsigned long long seed, unsigned long long start_draw,
+                                                        long row0, long nrows, const int* __restrict__ ops, int nslots,
+                                                        int nvec, int draws_per_row, T* __restrict__ vec,
+                                                        double* __restrict__ scal, unsigned long long* first_reject) {
+  for (long r = (long)blockIdx.x * blockDim.x + threadIdx.x; r < nrows; r += (long)gridDim.x * blockDim.x) {
+    unsigned long long s = jump(seed, start_draw + (unsigned long long)r * draws_per_row);
+    const long row = row0 + r;
+    for (int j = 0; j < nslots; ++j) {
+      const int op = ops[j];
+      double v;
+      if (op == 0) {
+        const long long hi = next_bits(s, 26);
+        const long long lo = next_bits(s, 27);
+        v = (double)((hi << 27) + lo) * (1.0 / (double)(1ULL << 53));
+      } else {
+        const int u = next_bits(s, 31);
+        if ((op & (op - 1)) == 0) {
+          v = (double)(int)(((long long)op * (long long)u) >> 31);
+        } else {
+          const int rr = u % op;
+          if ((long long)u - rr + (op - 1) >= (1LL << 31)) {
+            atomicMin(first_reject, (unsigned long long)r);
+            v = 0.0;
+          } else {
+            v = (double)rr;
+          }
+        }
+      }
+      if (j < nvec)
+        store(vec + row * (long)nvec + j, v);
+      else
+        scal[row * (long)(nslots - nvec) + (j - nvec)] = v;
+    }
+  }
+}
+
+template <typename T>
+int launch(unsigned long long seed, unsigned long long start_draw, long row0, long nrows, const int* ops, int nslots,
+           int nvec, int draws_per_row, void* vec, double* scal, unsigned long long* first_reject, hipStream_t st) {
+  if (nrows <= 0) return 0;
+  long blocks = (nrows + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL((java_rows_kernel<T>), dim3((unsigned)blocks), dim3(256), 0, st, seed, start_draw, row0, nrows,
+                     ops, nslots, nvec, draws_per_row, (T*)vec, scal, first_reject);
+  return (int)hipGetLastError();
+}
+}  // namespace
+
+// seed: the already scrambled LCG state ((seed ^ 0x5DEECE66D) & mask); start_draw: draws consumed
+// before row0. first_reject must be preset to ULLONG_MAX; it receives the smallest local row index
+// (relative to row0) whose nextInt would have rejected.
+FMLX_API int fmlx_java_rows(int vec_dtype, unsigned long long seed, unsigned long long start_draw, long row0,
+                            long nrows, const int* ops, int nslots, int nvec, int draws_per_row, void* vec,
+                            double* scal, unsigned long long* first_reject, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (vec_dtype == DT_F64)
+    return launch<double>(seed, start_draw, row0, nrows, ops, nslots, nvec, draws_per_row, vec, scal, first_reject,
+                          st);
+  if (vec_dtype == DT_F32)
+    return launch<float>(seed, start_draw, row0, nrows, ops, nslots, nvec, draws_per_row, vec, scal, first_reject, st);
+  if (vec_dtype == DT_BF16)
+    return launch<bf16_t>(seed, start_draw, row0, nrows, ops, nslots, nvec, draws_per_row, vec, scal, first_reject,
+                          st);
+  return -1;
+}

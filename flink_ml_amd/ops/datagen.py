@@ -1,0 +1,162 @@
+"""Bit-exact ``java.util.Random`` row streams for the benchmark data generators.
+
+``java_rows(seed, n, ops, nvec)`` reproduces, for one task, the values a reference
+``RowGenerator`` subclass draws: ``ops[j] == 0`` is ``nextDouble()`` and ``ops[j] == b > 0`` is
+``nextInt(b)``. On the GPU every row jumps to its first draw (``csrc/datagen.hip``); on the CPU the
+same jump-ahead runs vectorised in numpy (uint64 arithmetic keeps the low 48 bits exact).
+Rejected ``nextInt`` draws (non power-of-two bounds, ~1e-9 per draw) are detected, the offending
+row is replayed sequentially on the host and the rest of the rows are regenerated at the shifted
+offset — the result is always the exact reference stream.
+"""
+from __future__ import annotations
+
+from typing import Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import native
+from .native import c_int, c_long, c_void_p
+
+_MULT = 0x5DEECE66D
+_ADD = 0xB
+_MASK = (1 << 48) - 1
+
+native.register_kernel_sigs({
+    "fmlx_java_rows": [c_int, native.c_ulonglong, native.c_ulonglong, c_long, c_long, c_void_p, c_int, c_int, c_int,
+                       c_void_p, c_void_p, c_void_p, c_void_p],
+})
+
+
+def scramble(seed: int) -> int:
+    return (int(seed) ^ _MULT) & _MASK
+
+
+def _jump_host(x: int, k: int) -> int:
+    A, C, a, c = 1, 0, _MULT, _ADD
+    while k:
+        if k & 1:
+            A, C = (A * a) & _MASK, (C * a + c) & _MASK
+        c, a = (c * a + c) & _MASK, (a * a) & _MASK
+        k >>= 1
+    return (A * x + C) & _MASK
+
+
+def _draws_per_row(ops: Sequence[int]) -> int:
+    return sum(2 if o == 0 else 1 for o in ops)
+
+
+def _replay_row(state: int, ops: Sequence[int]) -> Tuple[list, int]:
+    """Sequential reference draws for one row from LCG ``state``; returns (values, draws used)."""
+    used = 0
+    vals = []
+
+    def nxt(bits):
+        nonlocal state, used
+        state = (state * _MULT + _ADD) & _MASK
+        used += 1
+        v = state >> (48 - bits)
+        return v - (1 << bits) if v >= (1 << (bits - 1)) and bits == 32 else v
+
+    for op in ops:
+        if op == 0:
+            vals.append(((nxt(26) << 27) + nxt(27)) * (1.0 / (1 << 53)))
+        elif op & (op - 1) == 0:
+            vals.append(float((op * nxt(31)) >> 31))
+        else:
+            while True:
+                u = nxt(31)
+                r = u % op
+                if u - r + op - 1 < (1 << 31):
+                    vals.append(float(r))
+                    break
+    return vals, used
+
+
+def _cpu_rows(x0: int, start: int, n: int, ops, nvec, vec: np.ndarray, scal: np.ndarray, row0: int) -> int:
+    """numpy jump-ahead generation of rows [row0, row0+n); returns first rejecting row or -1."""
+    dpr = _draws_per_row(ops)
+    M, MASK = np.uint64(_MULT), np.uint64(_MASK)
+    k = np.uint64(start) + np.arange(n, dtype=np.uint64) * np.uint64(dpr)
+    A = np.ones(n, dtype=np.uint64)
+    C = np.zeros(n, dtype=np.uint64)
+    a, c = _MULT, _ADD
+    kk = k.copy()
+    with np.errstate(over="ignore"):
+        while kk.any():
+            bit = (kk & np.uint64(1)).astype(bool)
+            A = np.where(bit, (A * np.uint64(a)) & MASK, A)
+            C = np.where(bit, (C * np.uint64(a) + np.uint64(c)) & MASK, C)
+            c, a = (c * a + c) & _MASK, (a * a) & _MASK
+            kk >>= np.uint64(1)
+        s = (A * np.uint64(x0) + C) & MASK
+        reject = np.full(n, False)
+
+        def nxt(bits):
+            nonlocal s
+            s = (s * M + np.uint64(_ADD)) & MASK
+            return (s >> np.uint64(48 - bits)).astype(np.int64)
+
+        nv = nvec
+        for j, op in enumerate(ops):
+            if op == 0:
+                v = ((nxt(26) << 27) + nxt(27)).astype(np.float64) * (1.0 / (1 << 53))
+            else:
+                u = nxt(31)
+                if op & (op - 1) == 0:
+                    v = ((op * u) >> 31).astype(np.float64)
+                else:
+                    r = u % op
+                    reject |= (u - r + op - 1) >= (1 << 31)
+                    v = r.astype(np.float64)
+            if j < nv:
+                vec[row0:row0 + n, j] = v
+            else:
+                scal[row0:row0 + n, j - nv] = v
+    bad = np.nonzero(reject)[0]
+    return int(bad[0]) if bad.size else -1
+
+
+def java_rows(seed: int, n: int, ops: Sequence[int], nvec: int, device=None, vec_dtype=torch.float64):
+    """Rows of one generator task: (vec [n, nvec] in ``vec_dtype``, scalars [n, len(ops)-nvec] fp64)."""
+    device = torch.device(device) if device is not None else torch.device("cpu")
+    ops = [int(o) for o in ops]
+    ns = len(ops) - nvec
+    dpr = _draws_per_row(ops)
+    x0 = scramble(seed)
+    start, row0 = 0, 0
+    if device.type == "cuda":
+        vec = torch.empty((n, nvec), dtype=vec_dtype, device=device)
+        scal = torch.empty((n, max(ns, 0)), dtype=torch.float64, device=device)
+        ops_t = torch.tensor(ops, dtype=torch.int32, device=device)
+        flag = torch.empty(1, dtype=torch.int64, device=device)
+        while row0 < n:
+            flag.fill_(-1)  # 0xFFFF... as unsigned
+            native.call("fmlx_java_rows", native.dtype_code(vec_dtype), x0, start, row0, n - row0, native.ptr(ops_t),
+                        len(ops), nvec, dpr, native.ptr(vec), native.ptr(scal) if ns else None, native.ptr(flag),
+                        native.stream_ptr(device))
+            bad = int(flag.item())
+            if bad < 0:
+                break
+            r = row0 + bad
+            vals, used = _replay_row(_jump_host(x0, start + bad * dpr), ops)
+            if nvec:
+                vec[r] = torch.tensor(vals[:nvec], dtype=torch.float64, device=device).to(vec_dtype)
+            if ns:
+                scal[r] = torch.tensor(vals[nvec:], dtype=torch.float64, device=device)
+            start += bad * dpr + used
+            row0 = r + 1
+        return vec, scal
+    vec_np = np.empty((n, nvec), dtype=np.float64)
+    scal_np = np.empty((n, max(ns, 0)), dtype=np.float64)
+    while row0 < n:
+        bad = _cpu_rows(x0, start, n - row0, ops, nvec, vec_np, scal_np, row0)
+        if bad < 0:
+            break
+        r = row0 + bad
+        vals, used = _replay_row(_jump_host(x0, start + bad * dpr), ops)
+        vec_np[r, :nvec] = vals[:nvec]
+        scal_np[r, :] = vals[nvec:]
+        start += bad * dpr + used
+        row0 = r + 1
+    return torch.from_numpy(vec_np).to(vec_dtype), torch.from_numpy(scal_np)

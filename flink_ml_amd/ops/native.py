@@ -37,6 +37,7 @@ _TORCH2DT = {
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int
 c_long = ctypes.c_long
+c_ulonglong = ctypes.c_ulonglong
 c_double = ctypes.c_double
 c_float = ctypes.c_float
 

@@ -163,3 +163,9 @@ def check_equal_across_ranks(value: int, what: str) -> None:
     hi = all_reduce_scalar(float(value), "max")
     if lo != hi:
         raise ValueError("%s differs across ranks: min %s, max %s" % (what, lo, hi))
+
+
+def barrier() -> None:
+    ctx = get_context()
+    if ctx.is_distributed:
+        dist.barrier()

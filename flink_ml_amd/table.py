@@ -157,6 +157,9 @@ class Table:
         # event-time attribute (the analogue of a Flink rowtime column with a watermark): time
         # windows cut on it; it survives column-preserving transformations
         self.time_col = time_col if time_col in self._cols else None
+        # True when every rank holds the same rows (model data, test statistics, metrics) rather
+        # than its own partition
+        self.replicated = False
         if num_rows is None:
             num_rows = _col_len(next(iter(self._cols.values()))) if self._cols else 0
         self._n = int(num_rows)
@@ -305,6 +308,10 @@ class Table:
     def rename(self, mapping: Dict[str, str]) -> "Table":
         return Table({mapping.get(k, k): v for k, v in self._cols.items()}, num_rows=self._n,
                      time_col=mapping.get(self.time_col, self.time_col))
+
+    def as_replicated(self) -> "Table":
+        self.replicated = True
+        return self
 
     def with_time_column(self, name: str) -> "Table":
         """Marks ``name`` (epoch milliseconds) as the event-time attribute for time windows."""

@@ -1,0 +1,123 @@
+"""Benchmark framework: bit-exact generators (vs java.util.Random semantics of RowGenerator), the
+JSON v1 runner on the reference demo config and the whole reference suite (scaled down), and a
+2-rank run."""
+import copy
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from flink_ml_amd.bench.generators import (DenseVectorGenerator, DoubleGenerator, KMeansModelDataGenerator,
+                                           LabeledPointWithWeightGenerator, RandomStringGenerator, task_rows, task_seed)
+from flink_ml_amd.bench.runner import load_config, run_config
+from flink_ml_amd.ops.datagen import java_rows
+from flink_ml_amd.utils.java import JavaRandom, java_string_hash
+from tests.spmd import run_spmd
+
+CONF = os.path.join(os.path.dirname(__file__), "..", "flink_ml_amd", "bench", "conf")
+
+
+def _java_rows(seed, n, ops):
+    r = JavaRandom(seed)
+    return np.array([[r.next_double() if o == 0 else float(r.next_int(o)) for o in ops] for _ in range(n)])
+
+
+def test_task_seed_and_split():
+    # Tuple2.of(2L, 0).hashCode() = 31 * Long.hashCode(2) + 0
+    assert task_seed(2, 0) == 62 and task_seed(2, 3) == 65
+    assert task_seed(-1, 1) == 1  # Long.hashCode(-1) == 0
+    assert [task_rows(10, t, 4) for t in range(4)] == [3, 3, 2, 2]
+
+
+def test_dense_vector_generator_exact():
+    g = DenseVectorGenerator().set_seed(2).set_col_names([["features"]]).set_num_values(50).set_vector_dim(7)
+    t = g.get_data()[0]
+    np.testing.assert_array_equal(t.column("features").numpy(), _java_rows(task_seed(2, 0), 50, [0] * 7))
+    assert DenseVectorGenerator().get_seed() == java_string_hash(
+        "org.apache.flink.ml.benchmark.datagenerator.common.DenseVectorGenerator")
+
+
+def test_labeled_point_and_double_generators_exact():
+    g = LabeledPointWithWeightGenerator().set_seed(5).set_col_names([["f", "l", "w"]]).set_num_values(40) \
+        .set_vector_dim(4).set_feature_arity(20).set_label_arity(10)
+    t = g.get_data()[0]
+    ref = _java_rows(task_seed(5, 0), 40, [20] * 4 + [10, 0])
+    np.testing.assert_array_equal(t.column("f").numpy(), ref[:, :4])
+    np.testing.assert_array_equal(t.column("l").numpy(), ref[:, 4])
+    np.testing.assert_array_equal(t.column("w").numpy(), ref[:, 5])
+    d = DoubleGenerator().set_seed(1).set_col_names([["a", "b"]]).set_num_values(30).set_arity(3).get_data()[0]
+    ref = _java_rows(task_seed(1, 0), 30, [3, 3])
+    np.testing.assert_array_equal(np.stack([d.column("a").numpy(), d.column("b").numpy()], 1), ref)
+    s = RandomStringGenerator().set_seed(9).set_col_names([["s"]]).set_num_values(20).set_num_distinct_values(7)
+    ref = _java_rows(task_seed(9, 0), 20, [7])
+    assert s.get_data()[0].get_list("s") == [str(int(x)) for x in ref[:, 0]]
+
+
+def test_rejection_replay_is_exact():
+    ops = [0, (1 << 30) + 3, 0]
+    vec, sc = java_rows(11, 500, ops, 1)
+    ref = _java_rows(11, 500, ops)
+    np.testing.assert_array_equal(np.concatenate([vec.numpy(), sc.numpy()], 1), ref)
+
+
+def test_kmeans_model_data_generator():
+    md = KMeansModelDataGenerator().set_seed(1).set_array_size(2).set_vector_dim(10).get_data()[0]
+    cents, weights = md.rows()[0]
+    assert len(cents) == 2 and list(weights.values) == [0.0, 0.0]
+    ref = _java_rows(task_seed(1, 0), 1, [0] * 20).reshape(2, 10)
+    np.testing.assert_array_equal(np.stack([c.values for c in cents]), ref)
+
+
+def test_runner_demo(tmp_path):
+    conf = load_config(os.path.join(CONF, "demo.json"))
+    res = run_config(conf, verbose=False)
+    assert set(res) == {k for k in conf if k != "version"}
+    r = res["KMeans-1"]["results"]
+    assert r["inputRecordNum"] == 10000 and r["outputRecordNum"] == 1
+    assert abs(r["inputThroughput"] - 10000 * 1000.0 / r["totalTimeMs"]) < 1e-6
+    assert res["KMeansModel-3"]["results"]["outputRecordNum"] == 30000
+    assert "exception" in res["Undefined-Parameter"]["results"]
+    assert "exception" in res["Unmatch-Input"]["results"]
+    from flink_ml_amd.bench.runner import main
+
+    out = tmp_path / "r.json"
+    main([os.path.join(CONF, "demo.json"), "--output-file", str(out), "--pattern", "^KMeansModel-1$"])
+    saved = json.load(open(out))
+    assert list(saved) == ["KMeansModel-1"] and "results" in saved["KMeansModel-1"]
+
+
+def _small_suite(n=300):
+    conf = load_config(os.path.join(CONF, "reference-suite.json"))
+    small = {"version": 1}
+    for k, v in conf.items():
+        if k == "version":
+            continue
+        v = copy.deepcopy(v)
+        v["inputData"]["paramMap"]["numValues"] = min(v["inputData"]["paramMap"].get("numValues", 10), n)
+        small[k] = v
+    return small
+
+
+def test_reference_suite_scaled_down():
+    res = run_config(_small_suite(), verbose=False)
+    failed = {k: v["results"]["exception"] for k, v in res.items() if "exception" in v["results"]}
+    assert not failed, failed
+    assert len(res) == 35
+
+
+def _spmd_bench(rank, world):
+    conf = load_config(os.path.join(CONF, "demo.json"))
+    res = run_config({"version": 1, "KMeans-1": conf["KMeans-1"], "KMeansModel-2": conf["KMeansModel-2"]},
+                     verbose=False)
+    g = DenseVectorGenerator().set_seed(2).set_col_names([["f"]]).set_num_values(11).set_vector_dim(3)
+    return res["KMeans-1"]["results"]["outputRecordNum"], res["KMeansModel-2"]["results"]["outputRecordNum"], \
+        g.get_data()[0].column("f").numpy().tolist()
+
+
+def test_runner_distributed():
+    res = run_spmd(_spmd_bench, 2)
+    for i, (a, b, rows) in enumerate(res):
+        assert a == 1 and b == 20000
+        np.testing.assert_array_equal(np.array(rows), _java_rows(task_seed(2, i), task_rows(11, i, 2), [0] * 3))
