@@ -102,6 +102,8 @@ def run_config(conf: Dict, pattern: Optional[str] = None, verbose: bool = True) 
         if name == "version" or (rx and not rx.match(name)):
             continue
         entry = dict(spec)
+        if verbose and get_context().rank == 0:
+            print("running %s ..." % name, flush=True)
         try:
             entry["results"] = run_benchmark(name, spec)
         except Exception as e:  # noqa: BLE001 - recorded like the reference's exception results

@@ -427,8 +427,7 @@ class VectorIndexerModel(ModelWithData, VectorIndexerModelParams):
                     keep &= hit
             out[:, ci] = torch.where(hit, vals[pos], torch.full_like(x, float(size)))
         if was_sparse:
-            res_col = SparseColumn.from_vectors([DenseVector(r).to_sparse() for r in out.cpu().numpy()],
-                                                X.shape[1])
+            res_col = SparseColumn.from_dense(out)
         else:
             res_col = out
         res = t.with_column(self.get(self.OUTPUT_COL), res_col)

@@ -30,7 +30,7 @@ from ...param.param import (BooleanParam, FloatParam, IntParam, ParamValidators,
 from ...parallel import comm
 from ...table import SparseColumn, Table
 from ...utils.java import java_hashmap_order as _java_hashmap_order
-from ...utils.java import java_string_hash
+from ...utils.java import java_number_to_string, java_string_hash
 from ..base import ModelWithData
 from ..linear import rw_update
 from .common import dec_dense, enc_dense, vector_input
@@ -239,39 +239,69 @@ class FeatureHasher(Transformer, HasInputCols, HasOutputCol, HasCategoricalCols,
         cats = list(self.get(self.CATEGORICAL_COLS))
         if cats and not set(cats) <= set(ins):
             raise ValueError("CategoricalCols must be included in inputCols!")
-        lists = {c: t.get_list(c) for c in ins}
+        dev = config.compute_device()
 
         def is_cat(c):
             if c in cats:
                 return True
-            vals = [v for v in lists[c] if v is not None]
+            col = t.column(c)
+            if isinstance(col, torch.Tensor):
+                return col.dtype == torch.bool
+            vals = [v for v in col if v is not None]
             return bool(vals) and all(isinstance(v, (str, bool, np.bool_)) for v in vals)
 
-        cat_cols = [c for c in ins if is_cat(c)]
-        num_cols = [c for c in ins if c not in cat_cols]
-        keys, vals, owners = [], [], []
-        for r in range(t.num_rows):
-            for c in num_cols:
-                v = lists[c][r]
-                if v is not None:
-                    keys.append(c)
-                    vals.append(float(v))
-                    owners.append(r)
-            for c in cat_cols:
-                v = lists[c][r]
-                if v is not None:
-                    sv = ("true" if v else "false") if isinstance(v, (bool, np.bool_)) else str(v)
-                    keys.append(c + "=" + sv)
-                    vals.append(1.0)
-                    owners.append(r)
-        h = hashing.hash_strings(keys).astype(np.int64)
-        h = np.where(h == -(1 << 31), h, np.abs(h))  # Math.abs(Integer.MIN_VALUE) stays negative
-        idx = np.mod(h, nf)
-        per_row: List[Dict[int, float]] = [dict() for _ in range(t.num_rows)]
-        for r, i, v in zip(owners, idx.tolist(), vals):
-            per_row[r][i] = per_row[r].get(i, 0.0) + v
-        out = [SparseVector(nf, sorted(m), [m[k] for k in sorted(m)]) for m in per_row]
-        return [t.with_column(self.get(self.OUTPUT_COL), SparseColumn.from_vectors(out, nf) if out else out)]
+        def bucket(strings):
+            h = hashing.hash_strings(list(strings)).astype(np.int64)
+            h = np.where(h == -(1 << 31), h, np.abs(h))  # Math.abs(Integer.MIN_VALUE) stays negative
+            return np.mod(h, nf)
+
+        n = t.num_rows
+        rows_l, idx_l, val_l = [], [], []
+        ar = torch.arange(n, device=dev)
+        for c in [c for c in ins if not is_cat(c)]:
+            col = t.column(c)
+            if isinstance(col, torch.Tensor):
+                x, ok = col.to(dev, torch.float64), None
+            else:
+                ok = torch.tensor([v is not None for v in col], device=dev)
+                x = torch.tensor([float(v) if v is not None else 0.0 for v in col], dtype=torch.float64, device=dev)
+            i = torch.full((n,), int(bucket([c])[0]), dtype=torch.int64, device=dev)
+            rows_l.append(ar if ok is None else ar[ok])
+            idx_l.append(i if ok is None else i[ok])
+            val_l.append(x if ok is None else x[ok])
+        for c in [c for c in ins if is_cat(c)]:
+            col = t.column(c)
+            if isinstance(col, torch.Tensor):
+                u, inv = torch.unique(col, return_inverse=True)
+                if col.dtype == torch.bool:
+                    names = ["true" if v else "false" for v in u.tolist()]
+                elif col.dtype.is_floating_point:
+                    names = [java_number_to_string(v) for v in u.tolist()]
+                else:
+                    names = [str(int(v)) for v in u.tolist()]
+                lut = torch.from_numpy(bucket(c + "=" + x for x in names)).to(dev)
+                rows_l.append(ar)
+                idx_l.append(lut[inv.to(dev)])
+                val_l.append(torch.ones(n, dtype=torch.float64, device=dev))
+            else:
+                keep = [r for r, v in enumerate(col) if v is not None]
+                strs = [c + "=" + (("true" if col[r] else "false") if isinstance(col[r], (bool, np.bool_)) else
+                                   (col[r] if isinstance(col[r], str) else java_number_to_string(col[r])))
+                        for r in keep]
+                rows_l.append(torch.tensor(keep, dtype=torch.int64, device=dev))
+                idx_l.append(torch.from_numpy(bucket(strs)).to(dev))
+                val_l.append(torch.ones(len(keep), dtype=torch.float64, device=dev))
+        # TreeMap<Integer, Double> per row: sum duplicates, ascending indices -> one sort-unique
+        rows = torch.cat(rows_l) if rows_l else torch.zeros(0, dtype=torch.int64, device=dev)
+        keys = rows * nf + (torch.cat(idx_l) if idx_l else rows)
+        vals = torch.cat(val_l) if val_l else torch.zeros(0, dtype=torch.float64, device=dev)
+        ukeys, inv = torch.unique(keys, return_inverse=True)
+        sums = torch.zeros(ukeys.numel(), dtype=torch.float64, device=dev).index_add_(0, inv, vals)
+        urows = torch.div(ukeys, nf, rounding_mode="floor")
+        indptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        indptr[1:] = torch.cumsum(torch.bincount(urows, minlength=n), 0)
+        col_out = SparseColumn(indptr, (ukeys - urows * nf).to(torch.int32), sums, nf)
+        return [t.with_column(self.get(self.OUTPUT_COL), col_out)]
 
 
 # ------------------------------------------------------------------------------------ CountVectorizer

@@ -75,11 +75,13 @@ class Bucketizer(Transformer, HasInputCols, HasOutputCols, HasHandleInvalid):
         t = inputs[0]
         ins, outs, splits = self.get(self.INPUT_COLS), self.get(self.OUTPUT_COLS), self.get(self.SPLITS_ARRAY)
         hi = self.get(self.HANDLE_INVALID)
-        keep_rows = torch.ones(t.num_rows, dtype=torch.bool)
+        keep_rows = None
         res = {}
         for c, o, sp in zip(ins, outs, splits):
-            x = t.scalars(c, dtype=torch.float64).cpu()
-            s = torch.tensor(sp, dtype=torch.float64)
+            col = t.column(c)
+            dev = col.device if isinstance(col, torch.Tensor) else torch.device("cpu")
+            x = t.scalars(c, dtype=torch.float64, device=dev)
+            s = torch.tensor(sp, dtype=torch.float64, device=dev)
             pos = torch.searchsorted(s, x, right=False)  # first index with s[idx] >= x
             exact = (pos < len(s)) & (s[torch.clamp(pos, max=len(s) - 1)] == x)
             idx = torch.where(exact, torch.where(pos == len(s) - 1, pos - 1, pos), pos - 1).to(torch.float64)
@@ -88,12 +90,13 @@ class Bucketizer(Transformer, HasInputCols, HasOutputCols, HasHandleInvalid):
                 if hi == self.ERROR_INVALID:
                     raise RuntimeError("The input contains invalid value. See handleInvalid parameter for more options.")
                 if hi == self.SKIP_INVALID:
-                    keep_rows &= ~invalid
+                    inv_cpu = invalid.cpu()
+                    keep_rows = ~inv_cpu if keep_rows is None else keep_rows & ~inv_cpu
                 else:
                     idx = torch.where(invalid, torch.full_like(idx, float(len(s) - 1)), idx)
             res[o] = idx
         out = t.with_columns(res)
-        if not bool(keep_rows.all()):
+        if keep_rows is not None and not bool(keep_rows.all()):
             out = out.filter(keep_rows)
         return [out]
 
@@ -226,7 +229,7 @@ class PolynomialExpansion(Transformer, HasInputCol, HasOutputCol):
         Xp = torch.cat([Xd, torch.ones((Xd.shape[0], 1), dtype=Xd.dtype, device=Xd.device)], dim=1)
         out = Xp[:, terms].prod(dim=2)
         if sparse_in:
-            out = SparseColumn.from_vectors([DenseVector(r).to_sparse() for r in out.cpu().numpy()], out.shape[1])
+            out = SparseColumn.from_dense(out)
         return [t.with_column(self.get(self.OUTPUT_COL), out)]
 
 
@@ -250,7 +253,7 @@ class Interaction(Transformer, HasInputCols, HasOutputCol):
         for m in mats[1:]:
             out = (out[:, :, None] * m.to(out.device)[:, None, :]).reshape(out.shape[0], -1)
         if sparse:
-            out = SparseColumn.from_vectors([DenseVector(r).to_sparse() for r in out.cpu().numpy()], out.shape[1])
+            out = SparseColumn.from_dense(out)
         return [t.with_column(self.get(self.OUTPUT_COL), out)]
 
 
@@ -347,7 +350,7 @@ class VectorSlicer(Transformer, HasInputCol, HasOutputCol):
         if isinstance(X, SparseColumn):
             dense = X.to_dense(torch.float64)
             sel = dense[:, torch.as_tensor(idx, device=dense.device)]
-            out = SparseColumn.from_vectors([DenseVector(r).to_sparse() for r in sel.cpu().numpy()], len(idx))
+            out = SparseColumn.from_dense(sel)
         else:
             out = X[:, torch.as_tensor(idx, device=X.device)]
         return [t.with_column(self.get(self.OUTPUT_COL), out)]

@@ -85,6 +85,14 @@ class SparseColumn:
         return out
 
     @staticmethod
+    def from_dense(X: torch.Tensor) -> "SparseColumn":
+        """Nonzero entries of a dense [n, d] tensor as CSR, on X's device (``DenseVector.toSparse``)."""
+        nzr, nzc = torch.nonzero(X, as_tuple=True)
+        indptr = torch.zeros(X.shape[0] + 1, dtype=torch.int64, device=X.device)
+        indptr[1:] = torch.cumsum(torch.bincount(nzr, minlength=X.shape[0]), 0)
+        return SparseColumn(indptr, nzc.to(torch.int32), X[nzr, nzc].to(torch.float64), int(X.shape[1]))
+
+    @staticmethod
     def concat(parts: Sequence["SparseColumn"]) -> "SparseColumn":
         """Row-wise concatenation (sizes must agree); result on the first part's device."""
         parts = list(parts)
