@@ -93,7 +93,7 @@ def run_benchmark(name: str, spec: Dict) -> Dict:
             "stageTimeMs": stage_ms, "stageInputThroughput": n_in * 1000.0 / stage_ms if stage_ms > 0 else None}
 
 
-def run_config(conf: Dict, pattern: Optional[str] = None, verbose: bool = True) -> Dict:
+def run_config(conf: Dict, pattern: Optional[str] = None, verbose: bool = True, warmup: int = 0) -> Dict:
     import re
 
     out = {}
@@ -105,6 +105,8 @@ def run_config(conf: Dict, pattern: Optional[str] = None, verbose: bool = True) 
         if verbose and get_context().rank == 0:
             print("running %s ..." % name, flush=True)
         try:
+            for _ in range(warmup):  # untimed: first-touch costs (library handles, allocator, caches)
+                run_benchmark(name, spec)
             entry["results"] = run_benchmark(name, spec)
         except Exception as e:  # noqa: BLE001 - recorded like the reference's exception results
             entry["results"] = {"exception": "%s: %s" % (type(e).__name__, e)}
@@ -121,10 +123,11 @@ def main(argv=None):
     ap.add_argument("config", help="Benchmark JSON config")
     ap.add_argument("--output-file", help="Where to write the results JSON")
     ap.add_argument("--pattern", help="Regex of benchmark names to run", default=None)
+    ap.add_argument("--warmup", type=int, default=0, help="untimed runs of each benchmark before the timed one")
     args = ap.parse_args(argv)
     if "RANK" in os.environ and "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) > 1:
         init_distributed()
-    res = run_config(load_config(args.config), args.pattern)
+    res = run_config(load_config(args.config), args.pattern, warmup=args.warmup)
     if get_context().rank == 0 and args.output_file:
         with open(args.output_file, "w", encoding="utf-8") as f:
             json.dump(res, f, indent=2)

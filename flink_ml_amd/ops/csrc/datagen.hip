@@ -51,16 +51,26 @@ __device__ __forceinline__ void store<bf16_t>(bf16_t* p, double v) {
   *p = f32_to_bf16((float)v);
 }
 
-// ops: per slot, 0 = nextDouble, >0 = nextInt(bound). draws_per_row = sum(op == 0 ? 2 : 1).
+// ops: per slot, 0 = nextDouble, >0 = nextInt(bound); slot_off[j] = draws before slot j within a row.
+// One thread per (row, chunk of CHUNK slots): consecutive threads cover consecutive chunks of a
+// row, so a wave writes one contiguous span of the output and each thread jumps only once.
+constexpr int CHUNK = 16;
+
 template <typename T>
 __global__ __launch_bounds__(256) void java_rows_kernel(unsigned long long seed, unsigned long long start_draw,
-                                                        long row0, long nrows, const int* __restrict__ ops, int nslots,
-                                                        int nvec, int draws_per_row, T* __restrict__ vec,
+                                                        long row0, long nrows, const int* __restrict__ ops,
+                                                        const int* __restrict__ slot_off, int nslots, int nvec,
+                                                        int draws_per_row, T* __restrict__ vec,
                                                         double* __restrict__ scal, unsigned long long* first_reject) {
-  for (long r = (long)blockIdx.x * blockDim.x + threadIdx.x; r < nrows; r += (long)gridDim.x * blockDim.x) {
-    unsigned long long s = jump(seed, start_draw + (unsigned long long)r * draws_per_row);
+  const int nchunks = (nslots + CHUNK - 1) / CHUNK;
+  const long total = nrows * (long)nchunks;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const long r = t / nchunks;
+    const int j0 = (int)(t - r * nchunks) * CHUNK;
+    const int j1 = j0 + CHUNK < nslots ? j0 + CHUNK : nslots;
+    unsigned long long s = jump(seed, start_draw + (unsigned long long)r * draws_per_row + (unsigned)slot_off[j0]);
     const long row = row0 + r;
-    for (int j = 0; j < nslots; ++j) {
+    for (int j = j0; j < j1; ++j) {
       const int op = ops[j];
       double v;
       if (op == 0) {
@@ -90,13 +100,15 @@ __global__ __launch_bounds__(256) void java_rows_kernel(unsigned long long seed,
 }
 
 template <typename T>
-int launch(unsigned long long seed, unsigned long long start_draw, long row0, long nrows, const int* ops, int nslots,
-           int nvec, int draws_per_row, void* vec, double* scal, unsigned long long* first_reject, hipStream_t st) {
+int launch(unsigned long long seed, unsigned long long start_draw, long row0, long nrows, const int* ops,
+           const int* slot_off, int nslots, int nvec, int draws_per_row, void* vec, double* scal,
+           unsigned long long* first_reject, hipStream_t st) {
   if (nrows <= 0) return 0;
-  long blocks = (nrows + 255) / 256;
-  if (blocks > 16384) blocks = 16384;
+  const long work = nrows * (long)((nslots + CHUNK - 1) / CHUNK);
+  long blocks = (work + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
   hipLaunchKernelGGL((java_rows_kernel<T>), dim3((unsigned)blocks), dim3(256), 0, st, seed, start_draw, row0, nrows,
-                     ops, nslots, nvec, draws_per_row, (T*)vec, scal, first_reject);
+                     ops, slot_off, nslots, nvec, draws_per_row, (T*)vec, scal, first_reject);
   return (int)hipGetLastError();
 }
 }  // namespace
@@ -105,16 +117,17 @@ int launch(unsigned long long seed, unsigned long long start_draw, long row0, lo
 // before row0. first_reject must be preset to ULLONG_MAX; it receives the smallest local row index
 // (relative to row0) whose nextInt would have rejected.
 FMLX_API int fmlx_java_rows(int vec_dtype, unsigned long long seed, unsigned long long start_draw, long row0,
-                            long nrows, const int* ops, int nslots, int nvec, int draws_per_row, void* vec,
-                            double* scal, unsigned long long* first_reject, void* stream) {
+                            long nrows, const int* ops, const int* slot_off, int nslots, int nvec, int draws_per_row,
+                            void* vec, double* scal, unsigned long long* first_reject, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (vec_dtype == DT_F64)
-    return launch<double>(seed, start_draw, row0, nrows, ops, nslots, nvec, draws_per_row, vec, scal, first_reject,
-                          st);
+    return launch<double>(seed, start_draw, row0, nrows, ops, slot_off, nslots, nvec, draws_per_row, vec, scal,
+                          first_reject, st);
   if (vec_dtype == DT_F32)
-    return launch<float>(seed, start_draw, row0, nrows, ops, nslots, nvec, draws_per_row, vec, scal, first_reject, st);
+    return launch<float>(seed, start_draw, row0, nrows, ops, slot_off, nslots, nvec, draws_per_row, vec, scal,
+                         first_reject, st);
   if (vec_dtype == DT_BF16)
-    return launch<bf16_t>(seed, start_draw, row0, nrows, ops, nslots, nvec, draws_per_row, vec, scal, first_reject,
-                          st);
+    return launch<bf16_t>(seed, start_draw, row0, nrows, ops, slot_off, nslots, nvec, draws_per_row, vec, scal,
+                          first_reject, st);
   return -1;
 }

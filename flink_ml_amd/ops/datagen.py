@@ -23,8 +23,8 @@ _ADD = 0xB
 _MASK = (1 << 48) - 1
 
 native.register_kernel_sigs({
-    "fmlx_java_rows": [c_int, native.c_ulonglong, native.c_ulonglong, c_long, c_long, c_void_p, c_int, c_int, c_int,
-                       c_void_p, c_void_p, c_void_p, c_void_p],
+    "fmlx_java_rows": [c_int, native.c_ulonglong, native.c_ulonglong, c_long, c_long, c_void_p, c_void_p, c_int, c_int,
+                       c_int, c_void_p, c_void_p, c_void_p, c_void_p],
 })
 
 
@@ -129,11 +129,13 @@ def java_rows(seed: int, n: int, ops: Sequence[int], nvec: int, device=None, vec
         vec = torch.empty((n, nvec), dtype=vec_dtype, device=device)
         scal = torch.empty((n, max(ns, 0)), dtype=torch.float64, device=device)
         ops_t = torch.tensor(ops, dtype=torch.int32, device=device)
+        offs = np.concatenate([[0], np.cumsum([2 if o == 0 else 1 for o in ops])[:-1]]).astype(np.int32)
+        off_t = torch.from_numpy(offs).to(device)
         flag = torch.empty(1, dtype=torch.int64, device=device)
         while row0 < n:
             flag.fill_(-1)  # 0xFFFF... as unsigned
             native.call("fmlx_java_rows", native.dtype_code(vec_dtype), x0, start, row0, n - row0, native.ptr(ops_t),
-                        len(ops), nvec, dpr, native.ptr(vec), native.ptr(scal) if ns else None, native.ptr(flag),
+                        native.ptr(off_t), len(ops), nvec, dpr, native.ptr(vec), native.ptr(scal) if ns else None, native.ptr(flag),
                         native.stream_ptr(device))
             bad = int(flag.item())
             if bad < 0:

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 PATTERN="${PATTERN:-^(?!(countvectorizer|hashingtf|ngram|regextokenizer|stopwordsremover|stringindexer|tokenizer|sqltransformer)).*}"
 OUT="${OUT:-gpurun_out/suite.json}"
 timeout -k 10 "${SUITE_TIMEOUT:-900}" python -m flink_ml_amd.bench.run flink_ml_amd/bench/conf/reference-suite.json \
-  --pattern "$PATTERN" --output-file "$OUT" > gpurun_out/suite.log 2>&1
+  --pattern "$PATTERN" --warmup "${WARMUP:-1}" --output-file "$OUT" > gpurun_out/suite.log 2>&1
 rc=$?
 echo "suite rc=$rc"
 tail -40 gpurun_out/suite.log

@@ -121,3 +121,16 @@ def test_runner_distributed():
     for i, (a, b, rows) in enumerate(res):
         assert a == 1 and b == 20000
         np.testing.assert_array_equal(np.array(rows), _java_rows(task_seed(2, i), task_rows(11, i, 2), [0] * 3))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ops,nvec,n", [([0] * 37, 37, 20000), ([20] * 5 + [10, 0], 5, 20000),
+                                        ([0, (1 << 30) + 3, 0, 7], 1, 400)])
+def test_java_rows_gpu_matches_cpu(ops, nvec, n):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cv, cs = java_rows(77, n, ops, nvec)
+    gv, gs = java_rows(77, n, ops, nvec, device="cuda", vec_dtype=torch.float64)
+    assert torch.equal(gv.cpu(), cv) and torch.equal(gs.cpu(), cs)
+    g32, _ = java_rows(77, n, ops, nvec, device="cuda", vec_dtype=torch.float32)
+    assert torch.equal(g32.cpu(), cv.float())
