@@ -191,26 +191,12 @@ class MaxAbsScaler(Estimator, HasInputCol, HasOutputCol):
 # ------------------------------------------------------------------------------- RobustScaler
 def exact_quantiles(X: torch.Tensor, ps, rel_err: float) -> torch.Tensor:
     """Per-column quantiles with the reference QuantileSummary query semantics on exact data
-    (``QuantileSummary.java:237-364``): p <= relErr → min, p >= 1-relErr → max, otherwise the
-    element of 1-based rank ceil(p·n). NaNs are ignored. Exact ranks satisfy the GK ε bound."""
-    Xg = comm.all_gather_cat(X.to(torch.float64)) if get_distributed() else X.to(torch.float64)
-    res = torch.empty((len(ps), Xg.shape[1]), dtype=torch.float64, device=Xg.device)
-    for c in range(Xg.shape[1]):
-        col = Xg[:, c]
-        col = col[~torch.isnan(col)]
-        if col.numel() == 0:
-            raise RuntimeError("Cannot query percentiles without any records inserted.")
-        s, _ = torch.sort(col)
-        n = s.numel()
-        for i, p in enumerate(ps):
-            if p <= rel_err:
-                res[i, c] = s[0]
-            elif p >= 1 - rel_err:
-                res[i, c] = s[-1]
-            else:
-                r = int(np.ceil(p * n))
-                res[i, c] = s[max(r, 1) - 1]
-    return res
+    (``QuantileSummary.java:237-364``): p <= relErr -> min, p >= 1-relErr -> max, otherwise the
+    element of 1-based rank ceil(p·n); NaNs ignored. Exact ranks satisfy the GK ε bound. Computed by
+    a distributed radix select (``ops/quantile.py``) — the shards never leave their ranks."""
+    from ...ops.quantile import column_quantiles
+
+    return column_quantiles(X, ps, rel_err, distributed=get_distributed())
 
 
 def get_distributed():

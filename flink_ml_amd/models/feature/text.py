@@ -271,7 +271,14 @@ class FeatureHasher(Transformer, HasInputCols, HasOutputCol, HasCategoricalCols,
             val_l.append(x if ok is None else x[ok])
         for c in [c for c in ins if is_cat(c)]:
             col = t.column(c)
-            if isinstance(col, torch.Tensor):
+            if isinstance(col, torch.Tensor) and col.dtype.is_floating_point:
+                # Double.toString + murmur3 of every value in native multi-threaded host code
+                h = hashing.hash_prefixed_doubles(c + "=", col.detach().to("cpu", torch.float64).numpy())
+                h = np.where(h == -(1 << 31), h.astype(np.int64), np.abs(h.astype(np.int64)))
+                rows_l.append(ar)
+                idx_l.append(torch.from_numpy(np.mod(h, nf)).to(dev))
+                val_l.append(torch.ones(n, dtype=torch.float64, device=dev))
+            elif isinstance(col, torch.Tensor):
                 u, inv = torch.unique(col, return_inverse=True)
                 if col.dtype == torch.bool:
                     names = ["true" if v else "false" for v in u.tolist()]

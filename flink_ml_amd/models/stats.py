@@ -27,18 +27,23 @@ from ..api.stage import AlgoOperator
 from ..common.param import HasFeaturesCol, HasFlatten, HasLabelCol
 from ..io import read_write as rw
 from ..linalg.vectors import DenseVector
+from ..ops import features as fo
 from ..parallel import comm
 from ..table import SparseColumn, Table
 from .feature.common import get_world_distributed
 
 
-def features_and_labels(t: Table, features_col: str, label_col: str) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Dense fp64 features [n, d] and fp64 labels on the compute device."""
+def features_and_labels(t: Table, features_col: str, label_col: str,
+                        keep_dtype: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Dense features [n, d] (fp64, or the stored dtype on the GPU with ``keep_dtype`` — the
+    reduction kernels accumulate in fp64 themselves) and fp64 labels on the compute device."""
     c = t.column(features_col)
     if isinstance(c, SparseColumn):
         X = c.to_dense(torch.float64, device=config.compute_device())
     else:
-        X = config.features_for_compute(t, features_col, allow_sparse=False).to(torch.float64)
+        X = config.features_for_compute(t, features_col, allow_sparse=False)
+        if not (keep_dtype and X.device.type == "cuda"):
+            X = X.to(torch.float64)
     lab = t.column(label_col)
     if isinstance(lab, list) and any(v is None for v in lab):
         raise ValueError("Input data must contain label value.")
@@ -89,12 +94,16 @@ class ANOVATest(AlgoOperator, _TestParams):
     JAVA_CLASS_NAME = "org.apache.flink.ml.stats.anovatest.ANOVATest"
 
     def compute(self, t: Table):
-        X, y = features_and_labels(t, self.get(self.FEATURES_COL), self.get(self.LABEL_COL))
+        X, y = features_and_labels(t, self.get(self.FEATURES_COL), self.get(self.LABEL_COL), keep_dtype=True)
         cls = global_sorted_unique(y)
         C, d = cls.numel(), X.shape[1]
         ci = torch.searchsorted(cls, y)
-        packed = torch.cat([class_sums(X, ci, C).reshape(-1), torch.bincount(ci, minlength=C).to(torch.float64),
-                            X.sum(0), (X * X).sum(0)])
+        if C <= fo.MAX_GROUPS:
+            S, tot, totsq = fo.group_colstats(X, ci, C)
+        else:
+            Xd = X.to(torch.float64)
+            S, tot, totsq = class_sums(Xd, ci, C), Xd.sum(0), (Xd * Xd).sum(0)
+        packed = torch.cat([S.reshape(-1), torch.bincount(ci, minlength=C).to(torch.float64), tot, totsq])
         packed = _reduce(packed).cpu().numpy()
         S = packed[:C * d].reshape(C, d)
         cnt = packed[C * d:C * d + C]
@@ -125,16 +134,20 @@ class FValueTest(AlgoOperator, _TestParams):
     JAVA_CLASS_NAME = "org.apache.flink.ml.stats.fvaluetest.FValueTest"
 
     def compute(self, t: Table):
-        X, y = features_and_labels(t, self.get(self.FEATURES_COL), self.get(self.LABEL_COL))
+        X, y = features_and_labels(t, self.get(self.FEATURES_COL), self.get(self.LABEL_COL), keep_dtype=True)
         d = X.shape[1]
-        mom = _reduce(torch.cat([torch.tensor([float(y.numel())], dtype=torch.float64, device=X.device),
-                                 y.sum()[None], (y * y).sum()[None], X.sum(0), (X * X).sum(0)]))
-        n = float(mom[0])
-        my = mom[1] / n
-        sy = torch.sqrt((mom[2] / n - my * my) * n / (n - 1))
-        mx = mom[3:3 + d] / n
-        sx = torch.sqrt((mom[3 + d:] / n - mx * mx) * n / (n - 1))
-        cov = _reduce(((y - my)[None, :] @ (X - mx))[0] / (n - 1))
+        ym = _reduce(torch.stack([torch.tensor(float(y.numel()), dtype=torch.float64, device=y.device), y.sum(),
+                                  (y * y).sum()]))
+        n = float(ym[0])
+        my = ym[1] / n
+        sy = torch.sqrt((ym[2] / n - my * my) * n / (n - 1))
+        yc = y - my
+        S, sx_, sxx = fo.group_colstats(X, None, 1, yc)
+        mom = _reduce(torch.cat([S[0], yc.sum()[None], sx_, sxx]))
+        mx = mom[d + 1:2 * d + 1] / n
+        sx = torch.sqrt((mom[2 * d + 1:] / n - mx * mx) * n / (n - 1))
+        # Σ (y-ȳ)(x-x̄) = Σ (y-ȳ)x − x̄ Σ (y-ȳ)
+        cov = (mom[:d] - mx * mom[d]) / (n - 1)
         dof = int(n) - 2
         corr = cov / (sy * sx)
         f = (corr * corr / (1 - corr * corr) * dof).cpu().numpy()

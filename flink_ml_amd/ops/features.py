@@ -65,3 +65,36 @@ def affine_cols(X: torch.Tensor, sub: Optional[torch.Tensor] = None, mul: Option
     if add is not None:
         out = out + add
     return out
+
+
+native.register_kernel_sigs({
+    "fmlx_group_colstats": [c_int, c_void_p, c_long, c_long, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                            c_void_p, c_void_p],
+})
+
+MAX_GROUPS = 32
+
+
+def group_colstats(X: torch.Tensor, gidx: Optional[torch.Tensor] = None, G: int = 1,
+                   w: Optional[torch.Tensor] = None):
+    """Per-group weighted column sums S[G, d] = Σ_{group(r)=g} w_r·x_r, plus Σx and Σx² (all fp64)
+    in one pass (``csrc/groupstats.hip`` on the GPU, G <= 32)."""
+    n, d = X.shape
+    dev = X.device
+    if (dev.type == "cuda" and 1 <= G <= MAX_GROUPS and X.dtype in (torch.float32, torch.float64, torch.bfloat16)
+            and X.stride(1) == 1 and n > 0):
+        nb = max(1, min(1024, (n + 2047) // 2048))
+        part = torch.empty((nb, (G + 2) * d), dtype=torch.float64, device=dev)
+        res = torch.empty(((G + 2) * d,), dtype=torch.float64, device=dev)
+        g = gidx.to(device=dev, dtype=torch.int32).contiguous() if gidx is not None else None
+        ww = w.to(device=dev, dtype=torch.float64).contiguous() if w is not None else None
+        native.call("fmlx_group_colstats", native.dtype_code(X.dtype), native.ptr(X), X.stride(0), n, d, native.ptr(g),
+                    G, native.ptr(ww), native.ptr(part), nb, native.ptr(res), native.stream_ptr(dev))
+        return res[:G * d].reshape(G, d), res[G * d:(G + 1) * d], res[(G + 1) * d:]
+    Xd = X.to(torch.float64)
+    wx = Xd * w.to(dev, torch.float64)[:, None] if w is not None else Xd
+    if gidx is None:
+        S = wx.sum(0, keepdim=True).expand(G, d).clone() if G == 1 else None
+    else:
+        S = torch.zeros((G, d), dtype=torch.float64, device=dev).index_add_(0, gidx.to(dev).long(), wx)
+    return S, Xd.sum(0), (Xd * Xd).sum(0)

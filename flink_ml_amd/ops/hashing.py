@@ -89,3 +89,40 @@ def hash_strings_device(strings: Sequence[str], mod: int, mode: int, device) -> 
 def non_negative_mod(h: np.ndarray, mod: int) -> np.ndarray:
     r = np.fmod(h.astype(np.int64), mod)
     return np.where(r < 0, r + mod, r)
+
+
+native.register_host_sigs({
+    "fmlx_hash_prefixed_doubles": [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                   ctypes.c_int32],
+    "fmlx_java_double_strings": [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p],
+})
+
+
+def hash_prefixed_doubles(prefix: str, vals: np.ndarray, nthreads: int = 0) -> np.ndarray:
+    """murmur3_32(prefix + Double.toString(v)) for every value (native, multi-threaded)."""
+    import os
+
+    vals = np.ascontiguousarray(vals, dtype=np.float64)
+    units = np.frombuffer(prefix.encode("utf-16-le"), dtype=np.uint16).copy()
+    out = np.empty(vals.shape[0], dtype=np.int32)
+    if vals.shape[0]:
+        nt = nthreads or min(16, os.cpu_count() or 1)
+        native.host().fmlx_hash_prefixed_doubles(units.ctypes.data if units.size else None, int(units.size),
+                                                 vals.ctypes.data, int(vals.shape[0]), out.ctypes.data, int(nt))
+    return out
+
+
+def java_double_strings(vals) -> list:
+    """``Double.toString`` of every value (native)."""
+    vals = np.ascontiguousarray(vals, dtype=np.float64)
+    n = vals.shape[0]
+    chars = np.empty(max(n, 1) * 32, dtype=np.uint8)
+    ends = np.empty(n, dtype=np.int64)
+    if n:
+        native.host().fmlx_java_double_strings(vals.ctypes.data, n, chars.ctypes.data, ends.ctypes.data)
+    b = chars.tobytes()
+    out, s = [], 0
+    for e in ends.tolist():
+        out.append(b[s:e].decode("ascii"))
+        s = e
+    return out

@@ -81,3 +81,35 @@ def test_hashing_tf_device():
     t = Table.from_rows([(["HashingTFTest", "Hashing", "Term", "Frequency", "Test"],)] * 3000, ["input"])
     out = HashingTF().transform(t)[0].get_list("output")
     assert out[0] == Vectors.sparse(262144, [67564, 89917, 113827, 131486, 228971], [1.0] * 5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.bfloat16])
+@pytest.mark.parametrize("shape,G", [((100000, 100), 10), ((3000, 300), 1), ((777, 5), 32)])
+def test_group_colstats_kernel(dtype, shape, G):
+    from flink_ml_amd.ops import features as fo
+
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(shape, generator=g, dtype=torch.float64).to(dtype)
+    gi = torch.randint(0, G, (shape[0],), generator=g)
+    w = torch.randn(shape[0], generator=g, dtype=torch.float64)
+    S, s, q = fo.group_colstats(X.cuda(), gi.cuda(), G, w.cuda())
+    Xd = X.double()
+    ref = torch.zeros(G, shape[1], dtype=torch.float64).index_add_(0, gi, Xd * w[:, None])
+    torch.testing.assert_close(S.cpu(), ref, rtol=1e-9, atol=1e-8)
+    torch.testing.assert_close(s.cpu(), Xd.sum(0), rtol=1e-9, atol=1e-8)
+    torch.testing.assert_close(q.cpu(), (Xd * Xd).sum(0), rtol=1e-9, atol=1e-8)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_radix_select_gpu(dtype):
+    from flink_ml_amd.ops.quantile import kth_smallest
+
+    X = (torch.randn(200000, 6, dtype=torch.float64) * 100).to(dtype)
+    X[::7, 2] = float("nan")
+    k = torch.tensor([1, 1000, 100000, 150000, 199999, 200000])
+    k[2] = 100
+    got = kth_smallest(X.cuda(), k.cuda()).cpu()
+    for j in range(6):
+        col = X[:, j][~torch.isnan(X[:, j])]
+        kj = min(int(k[j]), col.numel())
+        assert got[j] == torch.sort(col).values[kj - 1]
