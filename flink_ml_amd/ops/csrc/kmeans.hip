@@ -211,6 +211,93 @@ __global__ __launch_bounds__(256) void kmeans_assign_generic_kernel(const T* __r
 }
 
 // ------------------------------------------------------------------------------------------
+// generic assign v2 (fp32 / fp64): one wave per row, lanes split the feature dimension
+// ------------------------------------------------------------------------------------------
+// Each lane holds VPL = ceil(D/64) coalesced row elements in registers; for every group of KG
+// centroids the lanes accumulate partial dot products / L1 sums and a wave butterfly (DPP for
+// fp32) turns them into wave-uniform distances, so the argmin runs on uniform values (ties keep
+// the lower index, strict '<' like DistanceMeasure.findClosest). X is read exactly once,
+// coalesced; centroids come from LDS when k·D fits.
+template <typename T>
+__device__ __forceinline__ T wave_allsum(T v) {
+  return wave_sum_dpp(v);
+}
+
+template <typename T, int VPL>
+__global__ __launch_bounds__(256) void kmeans_assign_wave_kernel(const T* __restrict__ X, long ld, long n, int D,
+                                                                 const T* __restrict__ C, const T* __restrict__ cnrm,
+                                                                 int k, int metric, int use_lds,
+                                                                 int* __restrict__ labels) {
+  constexpr int KG = 8;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  T* Cs = reinterpret_cast<T*>(smem_raw);
+  if (use_lds) {
+    for (int i = threadIdx.x; i < k * D; i += blockDim.x) Cs[i] = C[i];
+    __syncthreads();
+  }
+  const T* Cp = use_lds ? Cs : C;
+  const int lane = threadIdx.x & 63;
+  const long wave = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const long nwaves = (long)gridDim.x * (blockDim.x >> 6);
+  for (long row = wave; row < n; row += nwaves) {
+    const T* x = X + row * ld;
+    T xv[VPL];
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int c = lane + 64 * v;
+      xv[v] = c < D ? x[c] : (T)0;
+    }
+    T pn2 = 0;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) pn2 += xv[v] * xv[v];
+    pn2 = wave_allsum(pn2);
+    const T pn = sqrt(pn2);
+    int bi = metric == 0 ? 0 : -1;
+    T best = metric == 0 ? (T)__builtin_huge_val() : (T)1.7976931348623157e308;
+    for (int i0 = 0; i0 < k; i0 += KG) {
+      T acc[KG];
+#pragma unroll
+      for (int g = 0; g < KG; ++g) {
+        acc[g] = 0;
+        const int i = i0 + g;
+        if (i < k) {
+          const T* c = Cp + (long)i * D;
+#pragma unroll
+          for (int v = 0; v < VPL; ++v) {
+            const int cc = lane + 64 * v;
+            const T cv = cc < D ? c[cc] : (T)0;
+            if (metric == 1) acc[g] += cc < D ? (T)fabs(xv[v] - cv) : (T)0;
+            else acc[g] += xv[v] * cv;
+          }
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < KG; ++g) acc[g] = wave_allsum(acc[g]);
+#pragma unroll
+      for (int g = 0; g < KG; ++g) {
+        const int i = i0 + g;
+        if (i >= k) break;
+        T dist;
+        if (metric == 0) {
+          const T cn = cnrm[i];
+          dist = pn * pn + cn * cn - (T)2 * acc[g];
+          dist = dist > (T)0 ? dist : (T)0;
+        } else if (metric == 1) {
+          dist = acc[g];
+        } else {
+          dist = (T)1 - acc[g] / pn / cnrm[i];
+        }
+        if (dist < best) {
+          best = dist;
+          bi = i;
+        }
+      }
+    }
+    if (lane == 0) labels[row] = bi;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // deterministic centroid accumulation: chunk gather-sum then per-cluster chunk reduction
 // ------------------------------------------------------------------------------------------
 template <typename T, int VPL>
@@ -371,10 +458,39 @@ FMLX_API int fmlx_kmeans_assign_bf16(const void* X, long ld, long n, int D, int 
   return -2;  // unsupported D for the MFMA path
 }
 
+template <typename T, int VPL>
+int launch_assign_wave(const void* X, long ld, long n, int D, const void* C, const void* cnrm, int k, int metric,
+                       int* labels, hipStream_t s) {
+  const size_t need = (size_t)k * D * sizeof(T);
+  const int use_lds = need <= 64 * 1024;
+  const size_t sh = use_lds ? need : 0;
+  long waves = n;
+  long blocks = (waves + 3) / 4;
+  if (blocks > 2048) blocks = 2048;  // ≫ 256 CUs; each wave then loops over rows
+  hipLaunchKernelGGL((kmeans_assign_wave_kernel<T, VPL>), dim3((unsigned)blocks), dim3(256), sh, s, (const T*)X, ld,
+                     n, D, (const T*)C, (const T*)cnrm, k, metric, use_lds, labels);
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+int assign_wave_vpl(const void* X, long ld, long n, int D, const void* C, const void* cnrm, int k, int metric,
+                    int* labels, hipStream_t s) {
+  if (D <= 64) return launch_assign_wave<T, 1>(X, ld, n, D, C, cnrm, k, metric, labels, s);
+  if (D <= 128) return launch_assign_wave<T, 2>(X, ld, n, D, C, cnrm, k, metric, labels, s);
+  if (D <= 256) return launch_assign_wave<T, 4>(X, ld, n, D, C, cnrm, k, metric, labels, s);
+  if (D <= 512) return launch_assign_wave<T, 8>(X, ld, n, D, C, cnrm, k, metric, labels, s);
+  return launch_assign_wave<T, 16>(X, ld, n, D, C, cnrm, k, metric, labels, s);
+}
+
 FMLX_API int fmlx_kmeans_assign_generic(int dtype, const void* X, long ld, long n, int D, const void* C,
                                         const void* cnrm, int k, int metric, int* labels, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) return 0;
+  if (D <= 1024) {
+    if (dtype == DT_F64) return assign_wave_vpl<double>(X, ld, n, D, C, cnrm, k, metric, labels, s);
+    if (dtype == DT_F32) return assign_wave_vpl<float>(X, ld, n, D, C, cnrm, k, metric, labels, s);
+    return -1;
+  }
   const int blocks = (int)((n + 255) / 256);
   const size_t es = dtype == DT_F64 ? 8 : 4;
   const size_t need = (size_t)k * D * es;
