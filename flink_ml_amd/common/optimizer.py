@@ -27,6 +27,7 @@ import torch
 
 from ..ops import glm as gk
 from ..parallel import comm
+from ..parallel.checkpoint import AlgorithmCheckpoint, fault_point
 from ..parallel.context import get_context
 from ..table import SparseColumn
 from ..utils import tracing
@@ -121,13 +122,26 @@ class TorchGlmTrainer:
             gk.torch_regularize(self.coef, self.sgd.reg, self.sgd.elastic_net, self.sgd.learning_rate)
 
     def fit(self) -> np.ndarray:
-        for e in range(self.sgd.max_iter):
+        ck = AlgorithmCheckpoint("sgd")
+        start = 0
+        restored = ck.restore()
+        if restored is not None:
+            start, st = restored
+            self.coef = st["coef"].to(torch.float64).clone()
+            self.offset, self.rounds = int(st["offset"]), int(st["rounds"])
+            if st["done"]:
+                return self.coef.numpy().copy()
+        for e in range(start, self.sgd.max_iter):
+            fault_point(e)
             fb = self._feedback()
             self.rounds += 1
             self._apply(fb)
             W, L = float(fb[self.d]), float(fb[self.d + 1])
             crit = L / W if W != 0 else float("nan")
-            if not (e + 1 < self.sgd.max_iter and crit > self.sgd.tol):
+            cont = e + 1 < self.sgd.max_iter and crit > self.sgd.tol
+            ck.maybe_save(e + 1, lambda: {"coef": self.coef, "offset": self.offset, "rounds": self.rounds,
+                                          "done": not cont})
+            if not cont:
                 break
         return self.coef.numpy().copy()
 
@@ -258,12 +272,25 @@ class DeviceGlmTrainer:
         return int(self.state[4].item())
 
     def fit(self) -> np.ndarray:
+        ck = AlgorithmCheckpoint("sgd")
+        done = 0
+        restored = ck.restore()
+        if restored is not None:
+            done, st = restored
+            self.coef.copy_(st["coef"].to(self.coef.dtype))
+            self.state.copy_(st["state"])
+            if st["done"]:
+                return self.coef.to(torch.float64).cpu().numpy()
+        step = ck.interval if ck.interval else self.check_every
         with tracing.range("sgd.fit"):
-            done = 0
             while done < self.sgd.max_iter:
-                k = min(self.check_every, self.sgd.max_iter - done)
+                fault_point(done)
+                k = min(step, self.sgd.max_iter - done)
                 self.run_rounds(k)
                 done += k
-                if done < self.sgd.max_iter and not self.running():
+                stop = done < self.sgd.max_iter and not self.running()
+                ck.maybe_save(done, lambda: {"coef": self.coef, "state": self.state,
+                                             "done": stop or done >= self.sgd.max_iter})
+                if stop:
                     break
         return self.coef.to(torch.float64).cpu().numpy()

@@ -141,22 +141,34 @@ class KMeans(Estimator, KMeansParams):
 
 def kmeans_lloyd(X: torch.Tensor, init: np.ndarray, max_iter: int, metric: str):
     """``maxIter`` Lloyd rounds; returns (centroids [k,D] f64, weights [k] f64)."""
-    ctx = get_context()
+    from ..parallel.checkpoint import AlgorithmCheckpoint, fault_point
+
     kc, D = init.shape
+    ck = AlgorithmCheckpoint("kmeans")
+    start, restored = 0, ck.restore()
+    if restored is not None:
+        start, st = restored
+        init, counts0 = st["centroids"].numpy(), st["weights"]
     if X.device.type == "cuda":
         acc = torch.float64 if X.dtype == torch.float64 else torch.float32
         cb = kk.CentroidBuffers(kc, D, X.device, acc)
         cb.set(torch.as_tensor(init))
+        if restored is not None:
+            cb.weights.copy_(counts0.to(cb.weights.dtype))
         rnd = kk.KMeansRound(X, kc, metric)
         with tracing.range("kmeans.fit"):
-            for _ in range(max_iter):
+            for e in range(start, max_iter):
+                fault_point(e)
                 payload = rnd.run(cb)
                 comm.all_reduce_sum(payload)
                 rnd.finalize(cb, payload)
+                ck.maybe_save(e + 1, lambda: {"centroids": cb.cent.to(torch.float64), "weights": cb.weights})
         return cb.cent.to(torch.float64).cpu().numpy(), cb.weights.cpu().numpy()
     C = torch.as_tensor(init, dtype=torch.float64)
-    counts = torch.zeros(kc, dtype=torch.float64)
-    for _ in range(max_iter):
+    counts = counts0.to(torch.float64) if restored is not None else torch.zeros(kc, dtype=torch.float64)
+    for e in range(start, max_iter):
+        fault_point(e)
         payload = comm.all_reduce_sum(kk.torch_round_payload(X, C, metric))
         C, counts = kk.torch_finalize(payload, kc, D)
+        ck.maybe_save(e + 1, lambda: {"centroids": C, "weights": counts})
     return C.numpy(), counts.numpy()

@@ -208,6 +208,9 @@ def _run_bounded(init_variables, data, config, body_or_factory, max_rounds, chec
     while True:
         if config.operator_life_cycle == OperatorLifeCycle.PER_ROUND:
             body = _make_body(body_or_factory, config, epoch)
+        from .checkpoint import fault_point
+
+        fault_point(epoch)
         ctx = IterationContext(epoch)
         streams = DataStreamList(list(data.replayed) + (list(data.non_replayed) if epoch == 0 else
                                                         [None] * len(data.non_replayed)))
@@ -310,10 +313,21 @@ class ForwardInputsOfLastRound(IterationListener):
 
 
 class RoundCheckpointer:
-    """Round-level checkpoint hook (see ``parallel.checkpoint``)."""
+    """Round-level checkpoint of an iteration: the variables fed back into the next round and the
+    outputs collected so far are saved through ``parallel.checkpoint`` every ``interval`` rounds
+    and restored on restart (the analogue of the head operator's checkpointed feedback)."""
+
+    def __init__(self, name: str = "iteration"):
+        from .checkpoint import AlgorithmCheckpoint
+
+        self._ck = AlgorithmCheckpoint(name)
 
     def restore(self):
-        return None
+        r = self._ck.restore()
+        if r is None:
+            return None
+        epoch, st = r
+        return {"epoch": epoch, "variables": st["variables"], "outputs": st["outputs"]}
 
     def maybe_save(self, epoch: int, variables, outputs) -> None:
-        pass
+        self._ck.maybe_save(epoch, lambda: {"variables": list(variables), "outputs": [list(o) for o in outputs]})
