@@ -18,3 +18,5 @@ from . import evaluation  # noqa: F401,E402
 from .evaluation import BinaryClassificationEvaluator  # noqa: F401,E402
 from . import agglomerative  # noqa: F401,E402
 from .agglomerative import AgglomerativeClustering  # noqa: F401,E402
+# reference Python API spellings (pyflink.ml.lib.classification.knn)
+KNN, KNNModel = Knn, KnnModel  # noqa: E305
