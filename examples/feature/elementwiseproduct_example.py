@@ -1,0 +1,16 @@
+"""Multiplies every vector element-wise by a scaling vector.
+
+Run: python examples/feature/elementwiseproduct_example.py
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+
+from flink_ml_amd import Table, Vectors  # noqa: E402,F401
+from flink_ml_amd.lib.feature import ElementwiseProduct  # noqa: E402
+data = Table.from_rows([(1, Vectors.dense(2.1, 3.1)), (2, Vectors.dense(1.1, 3.3))], ["id", "vec"])
+stage = ElementwiseProduct().set_input_col("vec").set_output_col("outputVec").set_scaling_vec(Vectors.dense(1.1, 1.1))
+out = stage.transform(data)[0]
+for i, o in zip(out.get_list("vec"), out.get_list("outputVec")):
+    print("Input Value: %s \tOutput Value: %s" % (i, o))

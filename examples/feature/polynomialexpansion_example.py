@@ -1,0 +1,15 @@
+"""Expands vectors into their polynomial features of a given degree.
+
+Run: python examples/feature/polynomialexpansion_example.py
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+
+from flink_ml_amd import Table, Vectors  # noqa: E402,F401
+from flink_ml_amd.lib.feature import PolynomialExpansion  # noqa: E402
+data = Table.from_rows([(1, Vectors.dense(2.1, 3.1, 1.2)), (2, Vectors.dense(1.2, 3.1, 4.6))], ["id", "vec"])
+out = PolynomialExpansion().set_degree(2).set_input_col("vec").set_output_col("outputVec").transform(data)[0]
+for i, o in zip(out.get_list("vec"), out.get_list("outputVec")):
+    print("Input Value: %s \tOutput Value: %s" % (i, o))
