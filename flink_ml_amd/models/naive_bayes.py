@@ -136,40 +136,55 @@ class NaiveBayes(Estimator, NaiveBayesParams):
         labels = global_sorted_unique(y)
         L, d = labels.numel(), X.shape[1]
         li = torch.searchsorted(labels, y)
-        local_vals = [torch.unique(X[:, j]) for j in range(d)]
+        # distinct values of every column at once: column-wise sort of X^T, run starts, padded
+        # [d, Vmax] value table (+inf padding), then one batched searchsorted + one bincount
+        Xt = X.t().contiguous()
+        S = torch.sort(Xt, dim=1).values if Xt.shape[1] else Xt
         if dist:
-            parts = comm.all_gather_object([v.cpu().tolist() for v in local_vals])
-            vals = [torch.tensor(sorted(set(x for p in parts for x in p[j])), dtype=torch.float64, device=X.device)
-                    for j in range(d)]
+            local = [S[j][torch.cat([S.new_ones(1, dtype=torch.bool), S[j, 1:] != S[j, :-1]])].cpu().tolist()
+                     if S.shape[1] else [] for j in range(d)]
+            parts = comm.all_gather_object(local)
+            vals_list = [sorted(set(x for p in parts for x in p[j])) for j in range(d)]
+            Vn = torch.tensor([len(v) for v in vals_list], dtype=torch.int64)
+            Vmax = max(1, int(Vn.max()) if d else 1)
+            table = torch.full((d, Vmax), float("inf"), dtype=torch.float64)
+            for j, v in enumerate(vals_list):
+                table[j, :len(v)] = torch.tensor(v, dtype=torch.float64)
+            table = table.to(X.device)
         else:
-            vals = local_vals
-        tables = [torch.bincount(li * vals[j].numel() + torch.searchsorted(vals[j], X[:, j].contiguous()),
-                                 minlength=L * vals[j].numel()).to(torch.float64) for j in range(d)]
-        tables.append(torch.bincount(li, minlength=L).to(torch.float64))
-        flat = torch.cat(tables)
+            start = torch.ones_like(S, dtype=torch.bool)
+            if S.shape[1] > 1:
+                start[:, 1:] = S[:, 1:] != S[:, :-1]
+            pos = torch.cumsum(start.to(torch.int64), dim=1) - 1
+            Vn = (pos[:, -1] + 1).cpu() if S.shape[1] else torch.zeros(d, dtype=torch.int64)
+            Vmax = max(1, int(Vn.max()) if d else 1)
+            table = torch.full((d, Vmax), float("inf"), dtype=torch.float64, device=X.device)
+            # every element of a run writes the same value to its slot; padding stays +inf
+            table.scatter_(1, pos, S.to(torch.float64))
+        codes = torch.searchsorted(table, Xt.to(torch.float64))
+        jj = torch.arange(d, device=X.device, dtype=torch.int64)[:, None]
+        key = (jj * L + li[None, :]) * Vmax + codes
+        cnt = torch.bincount(key.reshape(-1), minlength=d * L * Vmax).to(torch.float64)
+        n_lab = torch.bincount(li, minlength=L).to(torch.float64)
         if dist:
-            flat = comm.all_reduce_sum(flat)
-        flat = flat.cpu().numpy()
-        n_l = flat[-L:]
+            both = comm.all_reduce_sum(torch.cat([cnt, n_lab]))
+            cnt, n_lab = both[:-L], both[-L:]
+        counts = cnt.reshape(d, L, Vmax).cpu().numpy()
+        n_l = n_lab.cpu().numpy()
+        table_np = table.cpu().numpy()
+        Vn = Vn.numpy()
         labels_np = labels.cpu().numpy()
         # the reference's model lists labels in HashMap<Double, _> order
         order = [int(np.searchsorted(labels_np, v)) for v in java_hashmap_order(labels_np.tolist(), java_double_hash)]
         n_total = n_l.sum()
         pi_log = np.log(n_total * d + L * s)
         theta: List[List[Dict[float, float]]] = []
-        off = 0
-        counts = []
-        for j in range(d):
-            V = vals[j].numel()
-            counts.append(flat[off:off + L * V].reshape(L, V))
-            off += L * V
         for li_ in order:
             row = []
             for j in range(d):
-                V = vals[j].numel()
-                tlog = np.log(n_l[li_] + s * V)
-                vv = vals[j].cpu().numpy()
-                row.append({float(vv[c]): float(np.log(counts[j][li_, c] + s) - tlog) for c in range(V)})
+                V = int(Vn[j])
+                logs = np.log(counts[j, li_, :V] + s) - np.log(n_l[li_] + s * V)
+                row.append(dict(zip(table_np[j, :V].tolist(), logs.tolist())))
             theta.append(row)
         pi = DenseVector(np.array([np.log(n_l[i] * d + s) - pi_log for i in order]))
         md = (theta, pi, DenseVector(labels_np[order].astype(np.float64)))

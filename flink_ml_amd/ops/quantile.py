@@ -16,8 +16,16 @@ from typing import Sequence
 import torch
 
 from ..parallel import comm
+from . import native
+from .native import c_int, c_long, c_void_p
+
+native.register_kernel_sigs({
+    "fmlx_radix_hist": [c_int, c_void_p, c_long, c_long, c_int, c_void_p, c_int, c_int, c_int, c_long, c_void_p,
+                        c_void_p, c_void_p],
+})
 
 _BITS = 11
+_MAXQ = 4  # quantiles per kernel pass (LDS histogram [Q][16][256])
 _M63 = 0x7FFFFFFFFFFFFFFF
 
 
@@ -87,6 +95,52 @@ def quantile_ranks(counts: torch.Tensor, ps: Sequence[float], rel_err: float):
     return out
 
 
+def _unsigned_to_value(u: torch.Tensor, nbits: int) -> torch.Tensor:
+    """Inverse of the kernel's order-preserving unsigned key (held as an int64 bit pattern)."""
+    if nbits == 64:
+        bits = torch.where(u < 0, u ^ torch.iinfo(torch.int64).min, ~u)
+        return bits.view(torch.float64)
+    top = u >= (1 << 31)
+    bits = torch.where(top, u - (1 << 31), (~u) & 0xFFFFFFFF)
+    bits = torch.where(bits >= (1 << 31), bits - (1 << 32), bits)
+    return bits.to(torch.int32).view(torch.float32)
+
+
+def kth_smallest_device(X: torch.Tensor, ks: torch.Tensor, distributed: bool = False) -> torch.Tensor:
+    """k-th smallest (1-based ``ks`` [Q, d], Q <= 4) of every column of a GPU matrix, NaNs skipped,
+    by the ``radixselect.hip`` histogram kernel: 4 (fp32) / 8 (fp64) passes of 8-bit digits for
+    all Q ranks at once; per pass only the [Q, d, 256] histogram is all-reduced."""
+    if X.dtype not in (torch.float32, torch.float64):
+        X = X.to(torch.float32)
+    if X.stride(1) != 1:
+        X = X.contiguous()
+    n, d = X.shape
+    Q = ks.shape[0]
+    assert 1 <= Q <= _MAXQ and ks.shape[1] == d
+    nbits = 64 if X.dtype == torch.float64 else 32
+    dev = X.device
+    groups = (d + 15) // 16
+    chunks = int(max(1, min(256, (2048 + groups - 1) // groups, (n + 255) // 256)))
+    while chunks > 1 and chunks * Q * d * 256 * 4 > (256 << 20):
+        chunks //= 2
+    part = torch.empty(chunks * Q * d * 256, dtype=torch.int32, device=dev)
+    hist = torch.empty((Q, d, 256), dtype=torch.int64, device=dev)
+    prefix = torch.zeros((Q, d), dtype=torch.int64, device=dev)
+    kk = ks.to(device=dev, dtype=torch.int64).clone()
+    for i, shift in enumerate(range(nbits - 8, -1, -8)):
+        native.call("fmlx_radix_hist", native.dtype_code(X.dtype), native.ptr(X), X.stride(0), n, d,
+                    native.ptr(prefix), Q, shift, int(i == 0), chunks, native.ptr(part), native.ptr(hist),
+                    native.stream_ptr(dev))
+        h = comm.all_reduce_sum(hist) if distributed else hist
+        cum = torch.cumsum(h, dim=2)
+        sel = torch.clamp(torch.searchsorted(cum, kk[..., None]).squeeze(-1), max=255)
+        before = torch.where(sel > 0, cum.gather(2, torch.clamp(sel - 1, min=0)[..., None]).squeeze(-1),
+                             torch.zeros_like(kk))
+        kk = kk - before
+        prefix = (prefix << 8) | sel
+    return _unsigned_to_value(prefix, nbits)
+
+
 def column_quantiles(X: torch.Tensor, ps: Sequence[float], rel_err: float, distributed: bool = False) -> torch.Tensor:
     """[len(ps), d] quantiles of every column (NaNs ignored), exact and rank-local."""
     valid = ~torch.isnan(X)
@@ -95,5 +149,10 @@ def column_quantiles(X: torch.Tensor, ps: Sequence[float], rel_err: float, distr
         counts = comm.all_reduce_sum(counts)
     if bool((counts == 0).any()):
         raise RuntimeError("Cannot query percentiles without any records inserted.")
-    return torch.stack([kth_smallest(X, r, valid, distributed).to(torch.float64)
-                        for r in quantile_ranks(counts, ps, rel_err)])
+    ranks = quantile_ranks(counts, ps, rel_err)
+    if X.device.type == "cuda":
+        out = []
+        for j in range(0, len(ranks), _MAXQ):
+            out.append(kth_smallest_device(X, torch.stack(ranks[j:j + _MAXQ]), distributed).to(torch.float64))
+        return torch.cat(out)
+    return torch.stack([kth_smallest(X, r, valid, distributed).to(torch.float64) for r in ranks])

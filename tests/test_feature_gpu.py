@@ -113,3 +113,27 @@ def test_radix_select_gpu(dtype):
         col = X[:, j][~torch.isnan(X[:, j])]
         kj = min(int(k[j]), col.numel())
         assert got[j] == torch.sort(col).values[kj - 1]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("d", [3, 37])
+def test_radix_hist_kernel_multi_quantile(dtype, d):
+    from flink_ml_amd.ops.quantile import column_quantiles, kth_smallest_device
+
+    g = torch.Generator().manual_seed(d)
+    X = (torch.randn(100003, d, generator=g, dtype=torch.float64) * 50).to(dtype)
+    X[::5, 0] = float("nan")
+    X[:, -1] = torch.round(X[:, -1] / 20)  # many duplicates
+    X[:1000, 1] = -0.0
+    n_valid = (~torch.isnan(X)).sum(0)
+    ks = torch.stack([torch.ones(d, dtype=torch.int64), n_valid // 3, n_valid // 2 + 1, n_valid])
+    got = kth_smallest_device(X.cuda(), ks.cuda()).cpu()
+    for j in range(d):
+        col = torch.sort(X[:, j][~torch.isnan(X[:, j])]).values
+        for q in range(4):
+            assert got[q, j] == col[int(ks[q, j]) - 1], (q, j)
+    # through the public entry point (device path) vs the host radix select
+    ps = [0.25, 0.5, 0.75]
+    dev = column_quantiles(X.cuda(), ps, 0.001).cpu()
+    host = column_quantiles(X, ps, 0.001)
+    assert torch.equal(dev, host)
