@@ -114,6 +114,71 @@ class NaiveBayesModel(ModelWithData, NaiveBayesModelParams):
 
 
 @rw.register_stage
+def _label_value_counts(X: torch.Tensor, li: torch.Tensor, L: int, dist: bool):
+    """Per (feature, label, distinct value) counts (NaiveBayes.java:97-200's three keyed
+    aggregations) as one device histogram. Returns counts [d, L, Vmax] (numpy), per-feature sorted
+    distinct values and their slots in the last axis, and per-label row counts.
+
+    Small non-negative integer features (the categorical case) index the histogram directly;
+    anything else goes through one column-wise sort + batched searchsorted."""
+    n, d = X.shape
+    dev = X.device
+    n_lab = torch.bincount(li, minlength=L).to(torch.float64)
+    if n:
+        flags = torch.stack([-X.min(), X.max(), (X != torch.round(X)).any().to(X.dtype)]).to(torch.float64)
+    else:
+        flags = torch.tensor([-0.0, -1.0, 0.0], dtype=torch.float64, device=dev)
+    if dist:
+        flags = comm.all_reduce(flags, "max")
+    neg_min, vmax_f, non_int = flags.tolist()
+    if non_int == 0 and -neg_min >= 0 and (vmax_f + 1) * L * d <= (1 << 27):
+        Vmax = int(vmax_f) + 1
+        jj = torch.arange(d, device=dev, dtype=torch.int64)[None, :]
+        key = (jj * L + li[:, None]) * Vmax + X.to(torch.int64)
+        cnt = torch.bincount(key.reshape(-1), minlength=d * L * Vmax).to(torch.float64)
+        if dist:
+            both = comm.all_reduce_sum(torch.cat([cnt, n_lab]))
+            cnt, n_lab = both[:-L], both[-L:]
+        counts = cnt.reshape(d, L, Vmax).cpu().numpy()
+        present = counts.sum(1) > 0
+        slots = [np.nonzero(present[j])[0] for j in range(d)]
+        return counts, [sl.astype(np.float64) for sl in slots], slots, n_lab.cpu().numpy()
+    Xt = X.t().contiguous()
+    S = torch.sort(Xt, dim=1).values if n else Xt
+    if dist:
+        local = [S[j][torch.cat([S.new_ones(1, dtype=torch.bool), S[j, 1:] != S[j, :-1]])].cpu().tolist()
+                 if n else [] for j in range(d)]
+        parts = comm.all_gather_object(local)
+        vals_list = [sorted(set(x for p in parts for x in p[j])) for j in range(d)]
+        Vn = np.array([len(v) for v in vals_list], dtype=np.int64)
+        Vmax = max(1, int(Vn.max()) if d else 1)
+        table = torch.full((d, Vmax), float("inf"), dtype=torch.float64)
+        for j, v in enumerate(vals_list):
+            table[j, :len(v)] = torch.tensor(v, dtype=torch.float64)
+        table = table.to(dev)
+    else:
+        start = torch.ones_like(S, dtype=torch.bool)
+        if n > 1:
+            start[:, 1:] = S[:, 1:] != S[:, :-1]
+        pos = torch.cumsum(start.to(torch.int64), dim=1) - 1
+        Vn = (pos[:, -1] + 1).cpu().numpy() if n else np.zeros(d, dtype=np.int64)
+        Vmax = max(1, int(Vn.max()) if d else 1)
+        table = torch.full((d, Vmax), float("inf"), dtype=torch.float64, device=dev)
+        # every element of a run writes the same value to its slot; padding stays +inf
+        table.scatter_(1, pos, S.to(torch.float64))
+    codes = torch.searchsorted(table, Xt.to(torch.float64))
+    jj = torch.arange(d, device=dev, dtype=torch.int64)[:, None]
+    key = (jj * L + li[None, :]) * Vmax + codes
+    cnt = torch.bincount(key.reshape(-1), minlength=d * L * Vmax).to(torch.float64)
+    if dist:
+        both = comm.all_reduce_sum(torch.cat([cnt, n_lab]))
+        cnt, n_lab = both[:-L], both[-L:]
+    table_np = table.cpu().numpy()
+    slots = [np.arange(int(Vn[j])) for j in range(d)]
+    return (cnt.reshape(d, L, Vmax).cpu().numpy(), [table_np[j, :int(Vn[j])] for j in range(d)], slots,
+            n_lab.cpu().numpy())
+
+
 class NaiveBayes(Estimator, NaiveBayesParams):
     JAVA_CLASS_NAME = "org.apache.flink.ml.classification.naivebayes.NaiveBayes"
 
@@ -136,43 +201,7 @@ class NaiveBayes(Estimator, NaiveBayesParams):
         labels = global_sorted_unique(y)
         L, d = labels.numel(), X.shape[1]
         li = torch.searchsorted(labels, y)
-        # distinct values of every column at once: column-wise sort of X^T, run starts, padded
-        # [d, Vmax] value table (+inf padding), then one batched searchsorted + one bincount
-        Xt = X.t().contiguous()
-        S = torch.sort(Xt, dim=1).values if Xt.shape[1] else Xt
-        if dist:
-            local = [S[j][torch.cat([S.new_ones(1, dtype=torch.bool), S[j, 1:] != S[j, :-1]])].cpu().tolist()
-                     if S.shape[1] else [] for j in range(d)]
-            parts = comm.all_gather_object(local)
-            vals_list = [sorted(set(x for p in parts for x in p[j])) for j in range(d)]
-            Vn = torch.tensor([len(v) for v in vals_list], dtype=torch.int64)
-            Vmax = max(1, int(Vn.max()) if d else 1)
-            table = torch.full((d, Vmax), float("inf"), dtype=torch.float64)
-            for j, v in enumerate(vals_list):
-                table[j, :len(v)] = torch.tensor(v, dtype=torch.float64)
-            table = table.to(X.device)
-        else:
-            start = torch.ones_like(S, dtype=torch.bool)
-            if S.shape[1] > 1:
-                start[:, 1:] = S[:, 1:] != S[:, :-1]
-            pos = torch.cumsum(start.to(torch.int64), dim=1) - 1
-            Vn = (pos[:, -1] + 1).cpu() if S.shape[1] else torch.zeros(d, dtype=torch.int64)
-            Vmax = max(1, int(Vn.max()) if d else 1)
-            table = torch.full((d, Vmax), float("inf"), dtype=torch.float64, device=X.device)
-            # every element of a run writes the same value to its slot; padding stays +inf
-            table.scatter_(1, pos, S.to(torch.float64))
-        codes = torch.searchsorted(table, Xt.to(torch.float64))
-        jj = torch.arange(d, device=X.device, dtype=torch.int64)[:, None]
-        key = (jj * L + li[None, :]) * Vmax + codes
-        cnt = torch.bincount(key.reshape(-1), minlength=d * L * Vmax).to(torch.float64)
-        n_lab = torch.bincount(li, minlength=L).to(torch.float64)
-        if dist:
-            both = comm.all_reduce_sum(torch.cat([cnt, n_lab]))
-            cnt, n_lab = both[:-L], both[-L:]
-        counts = cnt.reshape(d, L, Vmax).cpu().numpy()
-        n_l = n_lab.cpu().numpy()
-        table_np = table.cpu().numpy()
-        Vn = Vn.numpy()
+        counts, vals, slots, n_l = _label_value_counts(X, li, L, dist)
         labels_np = labels.cpu().numpy()
         # the reference's model lists labels in HashMap<Double, _> order
         order = [int(np.searchsorted(labels_np, v)) for v in java_hashmap_order(labels_np.tolist(), java_double_hash)]
@@ -182,9 +211,9 @@ class NaiveBayes(Estimator, NaiveBayesParams):
         for li_ in order:
             row = []
             for j in range(d):
-                V = int(Vn[j])
-                logs = np.log(counts[j, li_, :V] + s) - np.log(n_l[li_] + s * V)
-                row.append(dict(zip(table_np[j, :V].tolist(), logs.tolist())))
+                V = vals[j].size
+                logs = np.log(counts[j, li_, slots[j]] + s) - np.log(n_l[li_] + s * V)
+                row.append(dict(zip(vals[j].tolist(), logs.tolist())))
             theta.append(row)
         pi = DenseVector(np.array([np.log(n_l[i] * d + s) - pi_log for i in order]))
         md = (theta, pi, DenseVector(labels_np[order].astype(np.float64)))

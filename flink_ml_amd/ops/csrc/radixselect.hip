@@ -20,11 +20,13 @@ constexpr int kCols = 16;
 constexpr int kRows = 16;
 constexpr int kBins = 256;
 constexpr int kMaxQ = 4;
+constexpr int kUnroll = 8;
 
 template <typename T> struct Key;
 template <> struct Key<float> {
   typedef uint32_t U;
   static __device__ __forceinline__ bool ok(float v) { return v == v; }
+  static __device__ __forceinline__ float nan() { return __builtin_nanf(""); }
   static __device__ __forceinline__ U get(float v) {
     const uint32_t b = __float_as_uint(v);
     return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
@@ -33,6 +35,7 @@ template <> struct Key<float> {
 template <> struct Key<double> {
   typedef unsigned long long U;
   static __device__ __forceinline__ bool ok(double v) { return v == v; }
+  static __device__ __forceinline__ double nan() { return __builtin_nan(""); }
   static __device__ __forceinline__ U get(double v) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(v);
     return (b & 0x8000000000000000ull) ? ~b : (b | 0x8000000000000000ull);
@@ -60,15 +63,24 @@ __global__ __launch_bounds__(256) void radix_hist_kernel(const T* __restrict__ X
     const long r0 = chunk * rows_per_chunk;
     long r1 = r0 + rows_per_chunk;
     if (r1 > n) r1 = n;
-    for (long r = r0 + lr; r < r1; r += kRows) {
-      const T v = X[r * ld + c];
-      if (!Key<T>::ok(v)) continue;
-      const U u = Key<T>::get(v);
-      const int dig = (int)((u >> shift) & 0xFF);
-      const U hi = match_all ? (U)0 : (u >> hs);
+    // kUnroll independent loads in flight per thread before the LDS atomics that consume them
+    for (long r = r0 + lr; r < r1; r += (long)kRows * kUnroll) {
+      T v[kUnroll];
 #pragma unroll
-      for (int q = 0; q < kMaxQ; ++q)
-        if (q < Q && (match_all || hi == pre[q])) atomicAdd(&h[(q * kCols + lc) * kBins + dig], 1u);
+      for (int u = 0; u < kUnroll; ++u) {
+        const long rr = r + (long)u * kRows;
+        v[u] = rr < r1 ? X[rr * ld + c] : Key<T>::nan();
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        if (!Key<T>::ok(v[u])) continue;
+        const U key = Key<T>::get(v[u]);
+        const int dig = (int)((key >> shift) & 0xFF);
+        const U hi = match_all ? (U)0 : (key >> hs);
+#pragma unroll
+        for (int q = 0; q < kMaxQ; ++q)
+          if (q < Q && (match_all || hi == pre[q])) atomicAdd(&h[(q * kCols + lc) * kBins + dig], 1u);
+      }
     }
   }
   __syncthreads();

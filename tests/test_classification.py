@@ -133,3 +133,18 @@ def test_knn_gpu_matches_cpu():
     gpu = knn_predict(Q.cuda(), T.cuda(), tn.cuda(), lab.double().cuda(), 5)
     assert (gpu.cpu() == cpu).double().mean() > 0.999
     assert (cpu == ql.double()).double().mean() > 0.99
+
+
+def test_naive_bayes_integer_and_general_paths_agree():
+    from flink_ml_amd.models import NaiveBayes
+
+    g = torch.Generator().manual_seed(1)
+    X = torch.randint(0, 5, (300, 4), generator=g).to(torch.float64)
+    X[:, 2] *= 3  # sparse value set {0, 3, 6, 9, 12}
+    y = torch.randint(0, 3, (300,), generator=g).to(torch.float64)
+    a = NaiveBayes().fit(Table({"features": X, "label": y}, num_rows=300)).get_model_data()[0].rows()[0]
+    b = NaiveBayes().fit(Table({"features": X + 0.5, "label": y}, num_rows=300)).get_model_data()[0].rows()[0]
+    for ra, rb in zip(a[0], b[0]):
+        for ma, mb in zip(ra, rb):
+            assert [k + 0.5 for k in ma] == list(mb) and list(ma.values()) == list(mb.values())
+    assert np.array_equal(a[1].values, b[1].values)
