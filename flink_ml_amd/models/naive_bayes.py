@@ -113,7 +113,6 @@ class NaiveBayesModel(ModelWithData, NaiveBayesModelParams):
         return [t.with_column(self.get(self.PREDICTION_COL), pred.to(torch.float64))]
 
 
-@rw.register_stage
 def _label_value_counts(X: torch.Tensor, li: torch.Tensor, L: int, dist: bool):
     """Per (feature, label, distinct value) counts (NaiveBayes.java:97-200's three keyed
     aggregations) as one device histogram. Returns counts [d, L, Vmax] (numpy), per-feature sorted
@@ -179,6 +178,7 @@ def _label_value_counts(X: torch.Tensor, li: torch.Tensor, L: int, dist: bool):
             n_lab.cpu().numpy())
 
 
+@rw.register_stage
 class NaiveBayes(Estimator, NaiveBayesParams):
     JAVA_CLASS_NAME = "org.apache.flink.ml.classification.naivebayes.NaiveBayes"
 

@@ -51,50 +51,66 @@ __device__ __forceinline__ void store<bf16_t>(bf16_t* p, double v) {
   *p = f32_to_bf16((float)v);
 }
 
-// ops: per slot, 0 = nextDouble, >0 = nextInt(bound); slot_off[j] = draws before slot j within a row.
-// One thread per (row, chunk of CHUNK slots): consecutive threads cover consecutive chunks of a
-// row, so a wave writes one contiguous span of the output and each thread jumps only once.
+// ops: per slot, 0 = nextDouble, >0 = nextInt(bound).
 constexpr int CHUNK = 16;
+constexpr int kRowsPerBlock = 256;
 
+// One thread per row, generating the row's program sequentially (the jump-ahead is paid once per
+// row: a wave-uniform jump to the block's first row plus a short per-lane jump of at most
+// 256·draws_per_row). Vector slots are staged through an LDS tile [256][CHUNK+1] and stored
+// cooperatively so each store instruction writes whole 16-element row segments.
 template <typename T>
 __global__ __launch_bounds__(256) void java_rows_kernel(unsigned long long seed, unsigned long long start_draw,
                                                         long row0, long nrows, const int* __restrict__ ops,
-                                                        const int* __restrict__ slot_off, int nslots, int nvec,
-                                                        int draws_per_row, T* __restrict__ vec,
-                                                        double* __restrict__ scal, unsigned long long* first_reject) {
-  const int nchunks = (nslots + CHUNK - 1) / CHUNK;
-  const long total = nrows * (long)nchunks;
-  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const long r = t / nchunks;
-    const int j0 = (int)(t - r * nchunks) * CHUNK;
+                                                        int nslots, int nvec, int draws_per_row,
+                                                        T* __restrict__ vec, double* __restrict__ scal,
+                                                        unsigned long long* first_reject) {
+  __shared__ T tile[kRowsPerBlock][CHUNK + 1];
+  const int tid = threadIdx.x;
+  const long rbase = (long)blockIdx.x * kRowsPerBlock;
+  const long r = rbase + tid;
+  const bool live = r < nrows;
+  const unsigned long long base = jump(seed, start_draw + (unsigned long long)rbase * draws_per_row);
+  unsigned long long s = jump(base, (unsigned long long)tid * draws_per_row);
+  const int nsc = nslots - nvec;
+  for (int j0 = 0; j0 < nslots; j0 += CHUNK) {
     const int j1 = j0 + CHUNK < nslots ? j0 + CHUNK : nslots;
-    unsigned long long s = jump(seed, start_draw + (unsigned long long)r * draws_per_row + (unsigned)slot_off[j0]);
-    const long row = row0 + r;
-    for (int j = j0; j < j1; ++j) {
-      const int op = ops[j];
-      double v;
-      if (op == 0) {
-        const long long hi = next_bits(s, 26);
-        const long long lo = next_bits(s, 27);
-        v = (double)((hi << 27) + lo) * (1.0 / (double)(1ULL << 53));
-      } else {
-        const int u = next_bits(s, 31);
-        if ((op & (op - 1)) == 0) {
-          v = (double)(int)(((long long)op * (long long)u) >> 31);
+    if (live) {
+      for (int j = j0; j < j1; ++j) {
+        const int op = ops[j];
+        double v;
+        if (op == 0) {
+          const long long hi = next_bits(s, 26);
+          const long long lo = next_bits(s, 27);
+          v = (double)((hi << 27) + lo) * (1.0 / (double)(1ULL << 53));
         } else {
-          const int rr = u % op;
-          if ((long long)u - rr + (op - 1) >= (1LL << 31)) {
-            atomicMin(first_reject, (unsigned long long)r);
-            v = 0.0;
+          const int u = next_bits(s, 31);
+          if ((op & (op - 1)) == 0) {
+            v = (double)(int)(((long long)op * (long long)u) >> 31);
           } else {
-            v = (double)rr;
+            const int rr = u % op;
+            if ((long long)u - rr + (op - 1) >= (1LL << 31)) {
+              atomicMin(first_reject, (unsigned long long)r);
+              v = 0.0;
+            } else {
+              v = (double)rr;
+            }
           }
         }
+        if (j < nvec)
+          store(&tile[tid][j - j0], v);
+        else
+          scal[(row0 + r) * (long)nsc + (j - nvec)] = v;
       }
-      if (j < nvec)
-        store(vec + row * (long)nvec + j, v);
-      else
-        scal[row * (long)(nslots - nvec) + (j - nvec)] = v;
+    }
+    if (j0 < nvec) {
+      const int w = (nvec < j1 ? nvec : j1) - j0;
+      __syncthreads();
+      for (int idx = tid; idx < kRowsPerBlock * w; idx += kRowsPerBlock) {
+        const int rr = idx / w, jj = idx - rr * w;
+        if (rbase + rr < nrows) vec[(row0 + rbase + rr) * (long)nvec + j0 + jj] = tile[rr][jj];
+      }
+      __syncthreads();
     }
   }
 }
@@ -104,11 +120,10 @@ int launch(unsigned long long seed, unsigned long long start_draw, long row0, lo
            const int* slot_off, int nslots, int nvec, int draws_per_row, void* vec, double* scal,
            unsigned long long* first_reject, hipStream_t st) {
   if (nrows <= 0) return 0;
-  const long work = nrows * (long)((nslots + CHUNK - 1) / CHUNK);
-  long blocks = (work + 255) / 256;
-  if (blocks > 65536) blocks = 65536;
-  hipLaunchKernelGGL((java_rows_kernel<T>), dim3((unsigned)blocks), dim3(256), 0, st, seed, start_draw, row0, nrows,
-                     ops, slot_off, nslots, nvec, draws_per_row, (T*)vec, scal, first_reject);
+  (void)slot_off;
+  const long blocks = (nrows + kRowsPerBlock - 1) / kRowsPerBlock;
+  hipLaunchKernelGGL((java_rows_kernel<T>), dim3((unsigned)blocks), dim3(kRowsPerBlock), 0, st, seed, start_draw,
+                     row0, nrows, ops, nslots, nvec, draws_per_row, (T*)vec, scal, first_reject);
   return (int)hipGetLastError();
 }
 }  // namespace

@@ -128,10 +128,13 @@ def kth_smallest_device(X: torch.Tensor, ks: torch.Tensor, distributed: bool = F
     prefix = torch.zeros((Q, d), dtype=torch.int64, device=dev)
     kk = ks.to(device=dev, dtype=torch.int64).clone()
     for i, shift in enumerate(range(nbits - 8, -1, -8)):
+        # the top digit's histogram is the same for every rank target: count it once
+        q_eff = 1 if i == 0 else Q
         native.call("fmlx_radix_hist", native.dtype_code(X.dtype), native.ptr(X), X.stride(0), n, d,
-                    native.ptr(prefix), Q, shift, int(i == 0), chunks, native.ptr(part), native.ptr(hist),
+                    native.ptr(prefix), q_eff, shift, int(i == 0), chunks, native.ptr(part), native.ptr(hist),
                     native.stream_ptr(dev))
-        h = comm.all_reduce_sum(hist) if distributed else hist
+        h = hist[:1].expand(Q, d, 256) if i == 0 else hist
+        h = comm.all_reduce_sum(h.contiguous()) if distributed else h
         cum = torch.cumsum(h, dim=2)
         sel = torch.clamp(torch.searchsorted(cum, kk[..., None]).squeeze(-1), max=255)
         before = torch.where(sel > 0, cum.gather(2, torch.clamp(sel - 1, min=0)[..., None]).squeeze(-1),
