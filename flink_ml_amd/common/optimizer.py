@@ -11,10 +11,13 @@ Semantics reproduced exactly:
   feedback is applied exactly once;
 * update: ``w -= lr/Σw · Σg`` then elastic-net regularisation, skipped when Σw = 0.
 
-MI355X execution (see ``ops/csrc/glm.hip``): the data partition stays resident in HBM, the
-round is 2 (1 GPU) or 3 + one RCCL all-reduce (N GPUs) kernel launches with all control
-state on the device, captured once into a hipGraph and replayed; the host only polls the
-device "running" flag every ``check_every`` rounds for early termination.
+MI355X execution (see ``ops/csrc/glm.hip``): the data partition stays resident in HBM and a
+dense round is ONE kernel launch — loss+gradient over the batch, fixed-order in-kernel
+reduction, then (1 GPU) the update, or (N GPUs) the feedback exchange with every peer over
+xGMI (``parallel/xgmi.py``) followed by the same update on every rank. Without the xGMI
+exchange the kernel ends with the feedback, RCCL all-reduces it and an update kernel follows.
+All control state is on the device; rounds are captured once into a hipGraph and replayed; the
+host only polls the device "running" flag every ``check_every`` rounds for early termination.
 """
 from __future__ import annotations
 
@@ -184,14 +187,24 @@ class DeviceGlmTrainer:
         self.state = torch.zeros(8, dtype=torch.int32, device=dev)
         self.state[1] = 1  # running[0]
         self.feedback = torch.zeros(self.d + 2, dtype=acc, device=dev)
+        self.distributed = ctx.is_distributed
+        self.xg = None
         if self.sparse:
-            self.partials = None
+            self.scratch = None
             self.nparts = 0
         else:
-            self.nparts = max(1, min(gk.GRAD_BLOCKS, 512, math.ceil(max(self.B, 1) / (gk.WPB * 16))))
-            self.partials = torch.zeros((self.nparts, self.d + 2), dtype=acc, device=dev)
-            self.stage1 = torch.zeros((gk.stage1_rows(self.nparts), self.d + 2), dtype=acc, device=dev)
-        self.distributed = ctx.is_distributed
+            self.nparts = max(1, min(gk.GRAD_BLOCKS, gk.TAIL_MAX_BLOCKS, math.ceil(max(self.B, 1) / (gk.WPB * 16))))
+            self.scratch = gk.RoundScratch(self.nparts, self.d, acc, dev)
+            if self.distributed:
+                from ..parallel import xgmi
+
+                self.xg = xgmi.get()
+                if self.xg is not None and self.d + 2 > self.xg.glm_max:
+                    self.xg = None
+        if self.sparse or self.distributed and self.xg is None:
+            self.mode = gk.TAIL_FEEDBACK  # feedback → RCCL all-reduce → update kernel
+        else:
+            self.mode = gk.TAIL_XGMI if self.distributed else gk.TAIL_UPDATE
         if use_graph is None:
             use_graph = os.environ.get("FMLX_HIPGRAPH", "1") == "1"
         self.use_graph = use_graph
@@ -212,17 +225,13 @@ class DeviceGlmTrainer:
             gk.update(self.feedback, self.d, self.coef, self.state, s.max_iter, s.tol, s.learning_rate, s.reg,
                       s.elastic_net)
             return
-        if self.n > 0:
-            gk.grad_partials(self.X, self.y, self.w, self.coef, self.B, self.loss, self.state, self.partials,
-                             self.nparts)
-        if self.distributed:
-            gk.reduce_only(self.partials, self.nparts, self.d, self.stage1, self.feedback, self.state)
+        # every rank launches the round, also one without rows: it still joins the reduction tail
+        gk.glm_round(self.X, self.y, self.w, self.coef, self.B, self.loss, self.state, self.scratch, self.mode,
+                     self.feedback, s.max_iter, s.tol, s.learning_rate, s.reg, s.elastic_net, xg=self.xg)
+        if self.mode == gk.TAIL_FEEDBACK:
             comm.all_reduce_sum(self.feedback)
             gk.update(self.feedback, self.d, self.coef, self.state, s.max_iter, s.tol, s.learning_rate, s.reg,
                       s.elastic_net)
-        else:
-            gk.reduce_update(self.partials, self.nparts, self.d, self.stage1, self.coef, self.feedback, self.state, s.max_iter,
-                             s.tol, s.learning_rate, s.reg, s.elastic_net)
 
     def _capture(self, rounds: int):
         """Captures ``rounds`` consecutive SGD rounds into one hipGraph (state lives on device, so
@@ -271,6 +280,12 @@ class DeviceGlmTrainer:
     def rounds_executed(self) -> int:
         return int(self.state[4].item())
 
+    def check_exchange(self) -> None:
+        """Raises if a bounded xGMI wait gave up (a peer never arrived): the rounds since then
+        used a partial feedback and must not be reported."""
+        if self.xg is not None and not self.xg.healthy():
+            raise RuntimeError("xGMI feedback exchange timed out on rank %d" % self.ctx.rank)
+
     def fit(self) -> np.ndarray:
         ck = AlgorithmCheckpoint("sgd")
         done = 0
@@ -293,4 +308,5 @@ class DeviceGlmTrainer:
                                              "done": stop or done >= self.sgd.max_iter})
                 if stop:
                     break
+        self.check_exchange()
         return self.coef.to(torch.float64).cpu().numpy()

@@ -196,15 +196,14 @@ class FtrlTrainer:
         if self.dev.type == "cuda" and gk.pick_layout(X) is not None:
             Xk = X if X.dtype in (torch.float32, torch.float64, torch.bfloat16) else X.to(self.acc)
             kacc = torch.float64 if Xk.dtype == torch.float64 else torch.float32
-            nparts = max(1, min(512, math.ceil(n / (gk.WPB * 16))))
-            partials = torch.zeros((nparts, self.d + 2), dtype=kacc, device=self.dev)
-            stage1 = torch.zeros((gk.stage1_rows(nparts), self.d + 2), dtype=kacc, device=self.dev)
+            nparts = max(1, min(gk.TAIL_MAX_BLOCKS, math.ceil(n / (gk.WPB * 16))))
+            scratch = gk.RoundScratch(nparts, self.d, kacc, self.dev)
             fb = torch.zeros(self.d + 2, dtype=kacc, device=self.dev)
             state = torch.tensor([0, 1, 1, 0, 0, 0, 0, 0], dtype=torch.int32, device=self.dev)
             coef = self.coef.to(kacc).contiguous()
-            gk.grad_partials(Xk, y.to(kacc).contiguous(), None, coef, n, gk.LOSS_CODES["ftrl"], state, partials,
-                             nparts)
-            gk.reduce_only(partials, nparts, self.d, stage1, fb, state)
+            # one launch: local gradient + fixed-order reduction → [Σ mult·x | rows | 0]
+            gk.glm_round(Xk, y.to(kacc).contiguous(), None, coef, n, gk.LOSS_CODES["ftrl"], state, scratch,
+                         gk.TAIL_FEEDBACK, fb)
             payload[: self.d] = fb[: self.d].to(self.acc)
             payload[self.d:] = fb[self.d].to(self.acc)
             return payload

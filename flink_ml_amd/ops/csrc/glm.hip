@@ -13,21 +13,34 @@
 //    row is read exactly once, dot → wave butterfly → loss/multiplier → axpy, no LDS, no
 //    atomics. Waves of a block combine by a fixed-order LDS tree, each block writes one
 //    partial row [grad(d) | Σweight | Σloss] → deterministic, bit-reproducible.
-//  * glm_reduce_update (1 GPU): sums the block partials per 64-column tile in a fixed
-//    order, evaluates TerminateOnMaxIterOrTol on device, applies w -= lr/Σw·g plus
-//    elastic-net regularisation, and advances the device-resident round state. No host
-//    synchronisation per round: the whole round is capturable in a hipGraph.
-//  * glm_reduce (N GPUs) → RCCL all-reduce of the (d+2) feedback → glm_update.
+//  * The round's reduction is fused into the same launch (glm_round_tail): each block publishes
+//    its partial row and draws an arrival ticket (agent-scope release/acquire, Guideline 16);
+//    the last block of every group of 32 sums the group's partials in fixed order, the last
+//    group finisher sums the ≤16 group rows in fixed order and then, by mode,
+//      TAIL_FEEDBACK  writes the (d+2) feedback (N GPUs over RCCL: all-reduce → glm_update),
+//      TAIL_UPDATE    (1 GPU) evaluates TerminateOnMaxIterOrTol, applies w -= lr/Σw·g plus
+//                     elastic-net regularisation and advances the device round state,
+//      TAIL_XGMI      (N GPUs) exchanges the feedback with every peer over xGMI (xgmi.h: one
+//                     record per rank, bounded tag waits, rank-order sum → bit-identical on all
+//                     ranks) and then updates like TAIL_UPDATE.
+//    So one SGD round is ONE kernel launch on 1 GPU and on N GPUs: no host synchronisation,
+//    no separate reduce kernels, the whole round capturable in a hipGraph.
+//  * Legacy split path (glm_reduce_stage1 → glm_reduce_update / glm_reduce) kept for the FTRL
+//    local-gradient call and A/B measurements.
 //  * Device round state (int32[8]): [0] round e, [1..2] running flag ping-pong
 //    (running[e&1] gates round e), [3] arrival ticket, [4] rounds executed.
 //    The batch of round e is rows [(e mod P)·B, min(+B, n)), P = ceil(n/B): exactly the
 //    reference's sequential slicing with reset-to-0 (SGD.java:263-268).
 #include "common.h"
+#include "xgmi.h"
 
 namespace {
 
 enum { LOSS_LOGISTIC = 0, LOSS_HINGE = 1, LOSS_LSQ = 2, LOSS_FTRL = 3 };
 enum { ST_ROUND = 0, ST_RUN0 = 1, ST_ARRIVE = 3, ST_EXECUTED = 4 };
+enum { TAIL_PARTIALS = 0, TAIL_FEEDBACK = 1, TAIL_UPDATE = 2, TAIL_XGMI = 3 };
+constexpr int TAIL_GROUP = 32;  // block partials summed per group finisher
+constexpr int TAIL_MAXG = 16;   // groups (=> at most 512 blocks per fused round)
 
 template <typename A>
 __device__ __forceinline__ void loss_and_mult(int loss, A dot, A y, A wt, A& l, A& m) {
@@ -59,21 +72,146 @@ __device__ __forceinline__ bool round_running(const int* st, int& e) {
   return st[ST_RUN0 + (e & 1)] != 0;
 }
 
+// apply the SGD step + elastic-net regularisation to one coefficient (SGD.java:231-243,
+// RegularizationUtils.java:47-91). The reg loss only feeds the discarded totalLoss slot in the
+// reference, so it is not materialised here.
+template <typename A>
+__device__ __forceinline__ A sgd_apply(A w, A g, A W, A lr, A reg, A en) {
+  if (!(W > (A)0)) return w;
+  w = w - lr / W * g;
+  if (reg == (A)0) return w;
+  if (en == (A)0) return w * ((A)1 - lr * reg);
+  A sg = w > (A)0 ? (A)1 : (w < (A)0 ? (A)-1 : (A)0);
+  if (en == (A)1) return w - lr * en * reg * sg;
+  return w - lr * (en * reg * sg + ((A)1 - en) * reg * w);
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused round tail (after every block wrote its partial row)
+// ------------------------------------------------------------------------------------------
+struct GlmTail {
+  int mode;        // TAIL_*
+  int max_iter;
+  int* cnt;        // int32[TAIL_MAXG + 1] arrival tickets: zero-initialised once, re-armed by the
+                   // last arrivers, so every launch (and hipGraph replay) starts from zero
+  void* stage1;    // [ngroups][d+2] accumulator rows
+  void* feedback;  // [d+2]: output of TAIL_FEEDBACK, a copy of the global feedback otherwise
+  double tol, lr, reg, en;
+  xgmi::Ctx x;     // TAIL_XGMI only
+};
+
+// Split-K style hand-off (cdna_hip_programming.md Guideline 16 / "Projection GEMM" item 2):
+// every wave drains its stores, lane 0 releases at agent scope and draws a ticket; the block
+// drawing the last ticket acquires and proceeds. Returns true in that block only.
+__device__ __forceinline__ bool arrive_last(int* cnt, int expected, int* sflag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == expected - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *sflag = last;
+  }
+  __syncthreads();
+  return *sflag != 0;
+}
+
+// Replaces this rank's feedback fb[0..stride) (in LDS) by the rank-order sum over all ranks.
+template <typename A>
+__device__ void glm_xgmi_exchange(const xgmi::Ctx& x, A* fb, long stride) {
+  using namespace xgmi;
+  const int g = x.gen[GEN_GLM];
+  const int slot = g & 1;
+  const long rec = GLM_DATA + (long)slot * GLM_MAX * (long)sizeof(A);
+  A* mine = at<A>(x.peers[x.rank], rec);
+  for (long c = threadIdx.x; c < stride; c += blockDim.x) st_sys(mine + c, fb[c]);
+  signal_and_wait(x, GLM_FLAGS, slot, g + 1);
+  for (long c = threadIdx.x; c < stride; c += blockDim.x) fb[c] = sum_ranks<A>(x, rec, c);
+  __syncthreads();
+  if (threadIdx.x == 0) x.gen[GEN_GLM] = g + 1;
+}
+
+template <typename A>
+__device__ void glm_round_tail(const GlmTail& tl, const A* partials, int d, A* coef, int* state, int e, A* sbuf,
+                               int* sflag) {
+  const long stride = d + 2;
+  const int nb = gridDim.x;
+  const int ngroups = (nb + TAIL_GROUP - 1) / TAIL_GROUP;
+  const int g = blockIdx.x / TAIL_GROUP;
+  const int g0 = g * TAIL_GROUP;
+  const int gs = nb - g0 < TAIL_GROUP ? nb - g0 : TAIL_GROUP;
+  A* st1 = (A*)tl.stage1;
+  // ---- ticket 1: the group's last block sums its partial rows (fixed order)
+  if (!arrive_last(&tl.cnt[g], gs, sflag)) return;
+  for (long c = threadIdx.x; c < stride; c += blockDim.x) {
+    A v[TAIL_GROUP];
+#pragma unroll
+    for (int q = 0; q < TAIL_GROUP; ++q) v[q] = partials[(long)(g0 + (q < gs ? q : 0)) * stride + c];
+    A sum = (A)0;
+#pragma unroll
+    for (int q = 0; q < TAIL_GROUP; ++q) sum += q < gs ? v[q] : (A)0;
+    st1[(long)g * stride + c] = sum;
+  }
+  if (threadIdx.x == 0) tl.cnt[g] = 0;  // all gs arrivals of this launch are in: re-arm
+  // ---- ticket 2: the last group finisher sums the group rows and completes the round
+  if (!arrive_last(&tl.cnt[TAIL_MAXG], ngroups, sflag)) return;
+  if (threadIdx.x == 0) tl.cnt[TAIL_MAXG] = 0;
+  for (long c = threadIdx.x; c < stride; c += blockDim.x) {
+    A v[TAIL_MAXG];
+#pragma unroll
+    for (int q = 0; q < TAIL_MAXG; ++q) v[q] = st1[(long)(q < ngroups ? q : 0) * stride + c];
+    A sum = (A)0;
+#pragma unroll
+    for (int q = 0; q < TAIL_MAXG; ++q) sum += q < ngroups ? v[q] : (A)0;
+    sbuf[c] = sum;
+  }
+  __syncthreads();
+  if (tl.mode == TAIL_XGMI) glm_xgmi_exchange<A>(tl.x, sbuf, stride);
+  A* fb = (A*)tl.feedback;
+  if (tl.mode == TAIL_FEEDBACK) {
+    for (long c = threadIdx.x; c < stride; c += blockDim.x) fb[c] = sbuf[c];
+    return;
+  }
+  const A W = sbuf[d], L = sbuf[d + 1];
+  const bool cont = (e + 1 < tl.max_iter) && (L / W > (A)tl.tol);
+  for (long c = threadIdx.x; c < d; c += blockDim.x) {
+    coef[c] = sgd_apply<A>(coef[c], sbuf[c], W, (A)tl.lr, (A)tl.reg, (A)tl.en);
+    if (fb) fb[c] = sbuf[c];
+  }
+  if (threadIdx.x == 0) {
+    if (fb) {
+      fb[d] = W;
+      fb[d + 1] = L;
+    }
+    // every block of this launch read the state words before its first ticket
+    state[ST_RUN0 + ((e + 1) & 1)] = cont ? 1 : 0;
+    state[ST_EXECUTED] += 1;
+    state[ST_ROUND] = e + 1;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // K4/K5/K6 — fused minibatch loss + gradient partials
 // ------------------------------------------------------------------------------------------
 template <typename T, int EPC, int CPL, int U, int WPB>
-__global__ __launch_bounds__(WPB * 64) void glm_grad_partials_kernel(
+__global__ __launch_bounds__(WPB * 64) void glm_round_kernel(
     const T* __restrict__ X, long ld, const typename AccOf<T>::type* __restrict__ y,
-    const typename AccOf<T>::type* __restrict__ wt, const typename AccOf<T>::type* __restrict__ coef,
-    long n, int d, long B, int loss, const int* __restrict__ state,
-    typename AccOf<T>::type* __restrict__ partials) {
+    const typename AccOf<T>::type* __restrict__ wt, typename AccOf<T>::type* coef,
+    long n, int d, long B, int loss, int* state, typename AccOf<T>::type* partials, GlmTail tl) {
   typedef typename AccOf<T>::type A;
   int e;
   if (!round_running(state, e)) return;
-  const long P = (n + B - 1) / B;
-  const long start = (long)(e % P) * B;
-  const long end = start + B < n ? start + B : n;
+  long start = 0, end = 0;  // a rank with no rows (or a zero local batch) still joins the tail
+  if (n > 0 && B > 0) {
+    const long P = (n + B - 1) / B;
+    start = (long)(e % P) * B;
+    end = start + B < n ? start + B : n;
+  }
 
   const int lane = threadIdx.x & 63;
   // wave id made provably wave-uniform so row indices / label loads become scalar (SMEM, lgkmcnt)
@@ -210,6 +348,8 @@ __global__ __launch_bounds__(WPB * 64) void glm_grad_partials_kernel(
       out[d + 1] = ls;
     }
   }
+  if (tl.mode == TAIL_PARTIALS) return;
+  glm_round_tail<A>(tl, partials, d, coef, state, e, buf, reinterpret_cast<int*>(lw + WPB * 2));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -247,20 +387,6 @@ __device__ __forceinline__ A sum_groups(const A* __restrict__ stage1, int ngroup
 #pragma unroll
   for (int q = 0; q < 16; ++q) s += v[q];
   return s;
-}
-
-// apply the SGD step + elastic-net regularisation to one coefficient (SGD.java:231-243,
-// RegularizationUtils.java:47-91). The reg loss only feeds the discarded totalLoss slot in the
-// reference, so it is not materialised here.
-template <typename A>
-__device__ __forceinline__ A sgd_apply(A w, A g, A W, A lr, A reg, A en) {
-  if (!(W > (A)0)) return w;
-  w = w - lr / W * g;
-  if (reg == (A)0) return w;
-  if (en == (A)0) return w * ((A)1 - lr * reg);
-  A sg = w > (A)0 ? (A)1 : (w < (A)0 ? (A)-1 : (A)0);
-  if (en == (A)1) return w - lr * en * reg * sg;
-  return w - lr * (en * reg * sg + ((A)1 - en) * reg * w);
 }
 
 // last-arriving block advances the round state (Guideline 16 counter form).
@@ -452,36 +578,56 @@ __global__ void glm_csr_predict_kernel(const long* __restrict__ indptr, const in
 constexpr int WPB = 8;
 
 template <typename T, int EPC, int CPL, int U>
-int launch_grad_u(const void* X, long ld, const void* y, const void* wt, const void* coef, long n, int d, long B,
-                  int loss, const int* state, void* partials, int nblocks, hipStream_t s) {
+int launch_grad_u(const void* X, long ld, const void* y, const void* wt, void* coef, long n, int d, long B, int loss,
+                  int* state, void* partials, int nblocks, const GlmTail& tl, hipStream_t s) {
   typedef typename AccOf<T>::type A;
-  size_t shmem = (size_t)(WPB / 2) * d * sizeof(A) + WPB * 2 * sizeof(A);
-  hipLaunchKernelGGL((glm_grad_partials_kernel<T, EPC, CPL, U, WPB>), dim3(nblocks), dim3(WPB * 64), shmem, s,
-                     (const T*)X, ld, (const A*)y, (const A*)wt, (const A*)coef, n, d, B, loss, state, (A*)partials);
+  // [WPB/2][d] tree buffer (reused as the final block's feedback row) | [WPB][2] | ticket flag
+  size_t shmem = (size_t)(WPB / 2) * d * sizeof(A) + WPB * 2 * sizeof(A) + 16;
+  hipLaunchKernelGGL((glm_round_kernel<T, EPC, CPL, U, WPB>), dim3(nblocks), dim3(WPB * 64), shmem, s, (const T*)X,
+                     ld, (const A*)y, (const A*)wt, (A*)coef, n, d, B, loss, state, (A*)partials, tl);
   return (int)hipGetLastError();
 }
 
 // rows in flight per wave = 2·U (software pipeline); u == 0 picks the default for the shape
 template <typename T, int EPC, int CPL>
-int launch_grad(int u, const void* X, long ld, const void* y, const void* wt, const void* coef, long n, int d, long B,
-                int loss, const int* state, void* partials, int nblocks, hipStream_t s) {
+int launch_grad(int u, const void* X, long ld, const void* y, const void* wt, void* coef, long n, int d, long B,
+                int loss, int* state, void* partials, int nblocks, const GlmTail& tl, hipStream_t s) {
   constexpr int BYTES = CPL * EPC * (int)sizeof(T);
   if (u == 0) u = BYTES <= 64 ? 2 : 1;
   if (u >= 4 && BYTES <= 32)
-    return launch_grad_u<T, EPC, CPL, 4>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    return launch_grad_u<T, EPC, CPL, 4>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
   if (u >= 2 && BYTES <= 64)
-    return launch_grad_u<T, EPC, CPL, 2>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-  return launch_grad_u<T, EPC, CPL, 1>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    return launch_grad_u<T, EPC, CPL, 2>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
+  return launch_grad_u<T, EPC, CPL, 1>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
 }
 
 template <typename T, int EPC>
-int launch_grad_cpl(int cpl, int u, const void* X, long ld, const void* y, const void* wt, const void* coef, long n,
-                    int d, long B, int loss, const int* state, void* partials, int nblocks, hipStream_t s) {
+int launch_grad_cpl(int cpl, int u, const void* X, long ld, const void* y, const void* wt, void* coef, long n, int d,
+                    long B, int loss, int* state, void* partials, int nblocks, const GlmTail& tl, hipStream_t s) {
   switch (cpl) {
-    case 1: return launch_grad<T, EPC, 1>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-    case 2: return launch_grad<T, EPC, 2>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-    case 4: return launch_grad<T, EPC, 4>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-    case 8: return launch_grad<T, EPC, 8>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
+    case 1: return launch_grad<T, EPC, 1>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
+    case 2: return launch_grad<T, EPC, 2>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
+    case 4: return launch_grad<T, EPC, 4>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
+    case 8: return launch_grad<T, EPC, 8>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
+  }
+  return -1;
+}
+
+int launch_round(int dtype, int epc, int cpl, int u, const void* X, long ld, const void* y, const void* wt, void* coef,
+                 long n, int d, long B, int loss, int* state, void* partials, int nblocks, const GlmTail& tl,
+                 hipStream_t s) {
+  if (dtype == DT_BF16) {
+    if (epc == 8) return launch_grad_cpl<bf16_t, 8>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
+    if (epc == 4) return launch_grad_cpl<bf16_t, 4>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
+    if (epc == 2) return launch_grad_cpl<bf16_t, 2>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
+    if (epc == 1) return launch_grad_cpl<bf16_t, 1>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
+  } else if (dtype == DT_F32) {
+    if (epc == 4) return launch_grad_cpl<float, 4>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
+    if (epc == 2) return launch_grad_cpl<float, 2>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
+    if (epc == 1) return launch_grad_cpl<float, 1>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
+  } else if (dtype == DT_F64) {
+    if (epc == 2) return launch_grad_cpl<double, 2>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
+    if (epc == 1) return launch_grad_cpl<double, 1>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
   }
   return -1;
 }
@@ -514,24 +660,39 @@ int launch_pred_cpl(int cpl, const void* X, long ld, long n, int d, const void* 
 
 // epc = elements per 16/8/4/2-byte chunk chosen by the host so that d % epc == 0 and rows are
 // aligned; cpl = chunks per lane (power of two, 64*cpl*epc >= d).
-FMLX_API int fmlx_glm_grad_partials(int dtype, int epc, int cpl, int u, const void* X, long ld, const void* y, const void* wt,
-                                    const void* coef, long n, int d, long B, int loss, const int* state,
+FMLX_API int fmlx_glm_grad_partials(int dtype, int epc, int cpl, int u, const void* X, long ld, const void* y,
+                                    const void* wt, const void* coef, long n, int d, long B, int loss, const int* state,
                                     void* partials, int nblocks, void* stream) {
-  hipStream_t s = (hipStream_t)stream;
-  if (dtype == DT_BF16) {
-    if (epc == 8) return launch_grad_cpl<bf16_t, 8>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-    if (epc == 4) return launch_grad_cpl<bf16_t, 4>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-    if (epc == 2) return launch_grad_cpl<bf16_t, 2>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-    if (epc == 1) return launch_grad_cpl<bf16_t, 1>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-  } else if (dtype == DT_F32) {
-    if (epc == 4) return launch_grad_cpl<float, 4>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-    if (epc == 2) return launch_grad_cpl<float, 2>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-    if (epc == 1) return launch_grad_cpl<float, 1>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-  } else if (dtype == DT_F64) {
-    if (epc == 2) return launch_grad_cpl<double, 2>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-    if (epc == 1) return launch_grad_cpl<double, 1>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, s);
-  }
-  return -1;
+  GlmTail tl{};
+  tl.mode = TAIL_PARTIALS;
+  return launch_round(dtype, epc, cpl, u, X, ld, y, wt, const_cast<void*>(coef), n, d, B, loss,
+                      const_cast<int*>(state), partials, nblocks, tl, (hipStream_t)stream);
+}
+
+// One whole SGD round in one launch (see the header comment). cnt: int32[17] zero-initialised;
+// stage1: [ceil(nblocks/32)][d+2]; feedback: [d+2] (may be null for TAIL_UPDATE / TAIL_XGMI).
+// peers/gen/err/spin_limit: the xGMI exchange (TAIL_XGMI only, see parallel/xgmi.py).
+FMLX_API int fmlx_glm_round(int dtype, int epc, int cpl, int u, const void* X, long ld, const void* y, const void* wt,
+                            void* coef, long n, int d, long B, int loss, int* state, void* partials, int nblocks,
+                            int mode, int* cnt, void* stage1, void* feedback, int max_iter, double tol, double lr,
+                            double reg, double en, void* const* peers, int world, int rank, int* gen, int* err,
+                            long spin_limit, void* stream) {
+  if (mode != TAIL_PARTIALS && (nblocks > TAIL_GROUP * TAIL_MAXG || cnt == nullptr || stage1 == nullptr)) return -4;
+  if (mode == TAIL_FEEDBACK && feedback == nullptr) return -5;
+  if (mode == TAIL_XGMI && (d + 2 > xgmi::GLM_MAX || peers == nullptr || world > xgmi::MAX_RANKS)) return -6;
+  GlmTail tl{};
+  tl.mode = mode;
+  tl.max_iter = max_iter;
+  tl.cnt = cnt;
+  tl.stage1 = stage1;
+  tl.feedback = feedback;
+  tl.tol = tol;
+  tl.lr = lr;
+  tl.reg = reg;
+  tl.en = en;
+  tl.x = xgmi::Ctx{peers, world, rank, gen, err, spin_limit};
+  return launch_round(dtype, epc, cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl,
+                      (hipStream_t)stream);
 }
 
 // stage1 scratch: [ceil(nparts/16)][d+2] of the accumulator type (nparts <= 512)

@@ -1,0 +1,108 @@
+// Layout and device helpers of the one-shot xGMI exchange (xgmi_allreduce.hip, glm.hip).
+//
+// Every rank owns ONE exchange buffer allocated uncached (fine-grained) and exported through a
+// dmabuf IPC handle; every rank maps every peer's buffer (flink_ml_amd/parallel/xgmi.py). A
+// payload is published with system-scope stores into the owner's own buffer, then a tag word is
+// raised; consumers poll the peers' tag words over xGMI (one lane per peer, relaxed, bounded,
+// s_sleep between polls) and read the peers' payloads with system-scope loads.
+//
+// Byte layout of one rank's buffer:
+//   FLAGS      int32 [2][MAX_BLOCKS]             generic all-reduce, one tag per (slot, chunk)
+//   GLM_FLAGS  int32 [2] (256-B block)           fused GLM round feedback exchange
+//   DATA       [2][MAX_BLOCKS][CHUNK] x 8 B      generic records (f32 or f64 elements)
+//   GLM_DATA   [2][GLM_MAX] x 8 B                fused GLM feedback record [grad | Σw | Σloss]
+// Slot = tag parity; tags are per-channel counters kept in LOCAL memory (gen[]), advanced by the
+// consuming block itself, so every rank — issuing the same call sequence — uses the same tags and
+// hipGraph replays keep advancing them (they are read from memory, never frozen arguments).
+// Two slots make reuse safe: a block that writes slot s in call k+2 has seen every peer publish
+// call k+1, which that peer issued only after its call k (stream order) finished reading slot s.
+#pragma once
+#include "common.h"
+
+namespace xgmi {
+
+constexpr int THREADS = 256;
+constexpr int VEC = 4;
+constexpr int CHUNK = THREADS * VEC;  // elements per generic record / block
+constexpr int MAX_RANKS = 8;          // one node: 8 GPUs, fully connected by xGMI
+constexpr int MAX_BLOCKS = 1024;      // => up to 1M elements per generic all-reduce
+constexpr int GLM_MAX = 4104;         // d + 2 for the register-resident GLM path (d <= 4096)
+
+constexpr long FLAGS = 0;
+constexpr long GLM_FLAGS = FLAGS + 2L * MAX_BLOCKS * 4;
+constexpr long DATA = GLM_FLAGS + 256;
+constexpr long GLM_DATA = DATA + 2L * MAX_BLOCKS * CHUNK * 8;
+constexpr long TOTAL = GLM_DATA + 2L * GLM_MAX * 8;
+constexpr int GEN_GLM = MAX_BLOCKS;   // index of the fused-GLM counter in gen[]
+constexpr int GEN_SIZE = MAX_BLOCKS + 1;
+
+// Kernel-argument bundle. `peers` is a DEVICE array of `world` buffer pointers (mine at `rank`).
+struct Ctx {
+  void* const* peers;
+  int world, rank;
+  int* gen;         // int32[GEN_SIZE], local memory
+  int* err;         // int32[1], local: set to 1 when a peer never arrived
+  long spin_limit;  // polls before giving up
+};
+
+__device__ __forceinline__ int ld_sys(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename A>
+__device__ __forceinline__ A ld_sys(const A* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename A>
+__device__ __forceinline__ void st_sys(A* p, A v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <typename T>
+__device__ __forceinline__ T* at(void* buf, long byte_off) {
+  return reinterpret_cast<T*>(reinterpret_cast<char*>(buf) + byte_off);
+}
+
+// Called by EVERY thread of the block after it stored its share of this rank's record with
+// st_sys: drain every wave's stores, raise my tag, then wait until every peer raised the same
+// tag (one polling lane per peer, bounded). On return the peers' records are readable.
+__device__ __forceinline__ void signal_and_wait(const Ctx& x, long flag_off, int idx, int tag) {
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) st_sys(at<int>(x.peers[x.rank], flag_off) + idx, tag);
+  if ((int)threadIdx.x < x.world && (int)threadIdx.x != x.rank) {
+    const int* f = at<int>(x.peers[threadIdx.x], flag_off) + idx;
+    long it = 0;
+    while (ld_sys(f) != tag) {
+      if (++it > x.spin_limit) {
+        atomicOr(x.err, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+}
+
+// Σ over ranks 0..world-1, in rank order, of element `i` of the records at byte offset `off`
+// (element type A): identical bits on every rank. All MAX_RANKS loads are issued
+// unconditionally (ranks past `world` re-read my own record and are masked out of the sum) so
+// they are in flight together instead of one xGMI round trip per rank.
+template <typename A>
+__device__ __forceinline__ A sum_ranks(const Ctx& x, long off, long i) {
+  A v[MAX_RANKS];
+#pragma unroll
+  for (int r = 0; r < MAX_RANKS; ++r) {
+    const int rr = r < x.world ? r : x.rank;
+    v[r] = ld_sys(at<A>(x.peers[rr], off) + i);
+  }
+  A s = (A)0;
+#pragma unroll
+  for (int r = 0; r < MAX_RANKS; ++r) s += r < x.world ? v[r] : (A)0;
+  return s;
+}
+
+}  // namespace xgmi

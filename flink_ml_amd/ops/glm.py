@@ -59,6 +59,38 @@ def stage1_rows(nparts: int) -> int:
     return (nparts + 31) // 32
 
 
+# fused-round tails (csrc/glm.hip): what the last block of the round does after the reduction
+TAIL_PARTIALS, TAIL_FEEDBACK, TAIL_UPDATE, TAIL_XGMI = 0, 1, 2, 3
+TAIL_MAX_BLOCKS = 512
+
+
+class RoundScratch:
+    """Device scratch of one fused round: block partials, group rows, arrival tickets."""
+
+    def __init__(self, nparts: int, d: int, acc: torch.dtype, device):
+        self.nparts = nparts
+        self.partials = torch.zeros((nparts, d + 2), dtype=acc, device=device)
+        self.stage1 = torch.zeros((stage1_rows(nparts), d + 2), dtype=acc, device=device)
+        self.cnt = torch.zeros(32, dtype=torch.int32, device=device)  # >= 17 tickets, zero-initialised
+
+
+def glm_round(X, y, wt, coef, B: int, loss: int, state, scratch: RoundScratch, mode: int, feedback=None,
+              max_iter: int = 1, tol: float = 0.0, lr: float = 0.0, reg: float = 0.0, en: float = 0.0,
+              xg=None) -> None:
+    """One SGD round (loss+gradient over the round's batch, fixed-order reduction and — by mode —
+    feedback output, update, or xGMI exchange + update) as ONE kernel launch."""
+    epc, cpl = pick_layout(X)
+    if xg is not None:
+        peers, world, rank, gen, err, spin = xg.kernel_args()
+    else:
+        peers, world, rank, gen, err, spin = None, 1, 0, None, None, 0
+    native.call("fmlx_glm_round", native.dtype_code(X.dtype), epc, cpl, GRAD_UNROLL, native.ptr(X), X.stride(0),
+                native.ptr(y), native.ptr(wt), native.ptr(coef), X.shape[0], X.shape[1], B, loss, native.ptr(state),
+                native.ptr(scratch.partials), scratch.nparts, mode, native.ptr(scratch.cnt),
+                native.ptr(scratch.stage1), native.ptr(feedback), int(max_iter), float(tol), float(lr), float(reg),
+                float(en), peers, world, rank, gen, err, int(spin), native.stream_ptr(X.device))
+
+
 def reduce_update(partials, nparts: int, d: int, stage1, coef, feedback, state, max_iter, tol, lr, reg, en) -> None:
     native.call("fmlx_glm_reduce_update", int(coef.dtype == torch.float64), native.ptr(partials), nparts, d,
                 native.ptr(stage1), native.ptr(coef), native.ptr(feedback), native.ptr(state), max_iter, tol, lr, reg, en,

@@ -6,7 +6,8 @@ collectives:
 =========================================  ==============================================
 reference                                  here
 =========================================  ==============================================
-``AllReduceImpl.allReduceSum`` (C2)        ``all_reduce_sum`` (one RCCL all-reduce)
+``AllReduceImpl.allReduceSum`` (C2)        ``all_reduce_sum``: one-shot xGMI kernel for device
+                                           tensors up to 1M elements (``xgmi.py``), else RCCL
 gather-to-one ``countWindowAll(P).reduce``  ``all_reduce_sum`` (result replicated, no bcast)
   + broadcast (C3)
 ``DataStreamUtils.reduce/aggregate`` (C4)  ``all_reduce_*`` for fixed-size accumulators,
@@ -47,6 +48,12 @@ def all_reduce(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
     ctx = get_context()
     if not ctx.is_distributed:
         return t
+    if op == "sum" and t.is_cuda:
+        from . import xgmi
+
+        x = xgmi.get()
+        if x is not None and x.accepts(t):
+            return x.all_reduce_(t)  # one-shot xGMI kernel (small payloads, bit-identical on all ranks)
     rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN,
            "prod": dist.ReduceOp.PRODUCT}[op]
     work, moved = _to_backend(t, ctx)

@@ -90,7 +90,11 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> SPM
             world = dist.get_world_size()
             rank = dist.get_rank()
         _CTX = SPMDContext(rank=rank, world_size=world, local_rank=local_rank, device=device, backend=backend)
-        return _CTX
+    if _CTX.is_distributed and _CTX.is_gpu and backend == "nccl":
+        from . import xgmi
+
+        xgmi.get()  # collective set-up of the one-shot xGMI exchange, at a point every rank reaches
+    return _CTX
 
 
 def get_context() -> SPMDContext:
@@ -116,6 +120,9 @@ def reset_context() -> None:
 
 def shutdown() -> None:
     global _CTX
+    from . import xgmi
+
+    xgmi.reset()
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
     _CTX = None

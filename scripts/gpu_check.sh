@@ -10,7 +10,7 @@ STEPS="${STEPS:-tests bench prof}"
 for step in $STEPS; do
   case "$step" in
     tests)
-      timeout -k 10 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
       rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
       ok_or_testfail $rc || exit $rc ;;
     smoke)

@@ -16,9 +16,10 @@ def _free_port() -> int:
     return port
 
 
-def _worker(rank, world, port, fn, args, q):
+def _worker(rank, world, port, fn, args, q, env=None):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "FMLX_DEVICE": "cpu"})
+    os.environ.update(env or {})
     try:
         import torch
 
@@ -33,11 +34,13 @@ def _worker(rank, world, port, fn, args, q):
         q.put((rank, "err", traceback.format_exc()))
 
 
-def run_spmd(fn, world: int, *args, timeout: float = 180):
+def run_spmd(fn, world: int, *args, timeout: float = 180, env=None):
+    """``env``: extra environment for every rank (e.g. ``{"FMLX_DEVICE": "cuda:0"}`` to put all
+    ranks on one GPU with a gloo group)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, q, env)) for r in range(world)]
     for p in procs:
         p.start()
     results = {}
