@@ -193,7 +193,7 @@ class DeviceGlmTrainer:
             self.scratch = None
             self.nparts = 0
         else:
-            self.nparts = max(1, min(gk.GRAD_BLOCKS, gk.TAIL_MAX_BLOCKS, math.ceil(max(self.B, 1) / (gk.WPB * 16))))
+            self.nparts = max(1, min(gk.GRAD_BLOCKS, gk.max_round_blocks(), math.ceil(max(self.B, 1) / (gk.WPB * 16))))
             self.scratch = gk.RoundScratch(self.nparts, self.d, acc, dev)
             if self.distributed:
                 from ..parallel import xgmi

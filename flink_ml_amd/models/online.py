@@ -196,7 +196,7 @@ class FtrlTrainer:
         if self.dev.type == "cuda" and gk.pick_layout(X) is not None:
             Xk = X if X.dtype in (torch.float32, torch.float64, torch.bfloat16) else X.to(self.acc)
             kacc = torch.float64 if Xk.dtype == torch.float64 else torch.float32
-            nparts = max(1, min(gk.TAIL_MAX_BLOCKS, math.ceil(n / (gk.WPB * 16))))
+            nparts = max(1, min(gk.max_round_blocks(), math.ceil(n / (gk.WPB * 16))))
             scratch = gk.RoundScratch(nparts, self.d, kacc, self.dev)
             fb = torch.zeros(self.d + 2, dtype=kacc, device=self.dev)
             state = torch.tensor([0, 1, 1, 0, 0, 0, 0, 0], dtype=torch.int32, device=self.dev)

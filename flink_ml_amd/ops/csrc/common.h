@@ -104,6 +104,19 @@ __device__ __forceinline__ void load_chunk(const T* __restrict__ p, Chunk<T, EPC
   }
 }
 
+// Same, with the non-temporal hint (global_load … nt) for rows streamed exactly once.
+template <typename T, int EPC>
+__device__ __forceinline__ void load_chunk_nt(const T* __restrict__ p, Chunk<T, EPC>& c) {
+  constexpr int BYTES = EPC * (int)sizeof(T);
+  if constexpr (BYTES == 16) {
+    typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    __builtin_memcpy(c.v, &v, 16);
+  } else {
+    load_chunk<T, EPC>(p, c);
+  }
+}
+
 static inline int fmlx_ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
 #define FMLX_CHECK_LAUNCH() return (int)hipGetLastError()

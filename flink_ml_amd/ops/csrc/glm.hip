@@ -40,7 +40,37 @@ enum { LOSS_LOGISTIC = 0, LOSS_HINGE = 1, LOSS_LSQ = 2, LOSS_FTRL = 3 };
 enum { ST_ROUND = 0, ST_RUN0 = 1, ST_ARRIVE = 3, ST_EXECUTED = 4 };
 enum { TAIL_PARTIALS = 0, TAIL_FEEDBACK = 1, TAIL_UPDATE = 2, TAIL_XGMI = 3 };
 constexpr int TAIL_GROUP = 32;  // block partials summed per group finisher
-constexpr int TAIL_MAXG = 16;   // groups (=> at most 512 blocks per fused round)
+constexpr int TAIL_MAXG = 16;   // groups of the deterministic tail (=> at most 512 blocks)
+constexpr int TAIL_TOP = 64;    // index of the top-level ticket (atomic tail: up to 64 groups)
+
+// fp32 (bf16/fp32 data): one v_exp, one v_log, one v_rcp per row instead of the accurate libm
+// expf/log1pf/division sequences (~100 VALU instructions per row, wave-uniform work that cost
+// 6 µs of the 200 MB round body, measured); fp64 parity mode keeps the accurate path below.
+//   logistic, z = −dot·ys, t = e^(−|z|) ∈ (0, 1]:  softplus(z) = max(z, 0) + log(1 + t),
+//   mult = −ys / (e^(−z) + 1) = −ys · (z > 0 ? 1 : t) / (1 + t)
+__device__ __forceinline__ void loss_and_mult(int loss, float dot, float y, float wt, float& l, float& m) {
+  if (loss == LOSS_LOGISTIC) {
+    const float ys = 2.f * y - 1.f;
+    const float z = -dot * ys;
+    const float t = __expf(-fabsf(z));
+    const float r = __frcp_rn(1.f + t);
+    l = wt * (fmaxf(z, 0.f) + __logf(1.f + t));
+    m = wt * (-ys) * (z > 0.f ? r : t * r);
+  } else if (loss == LOSS_HINGE) {
+    const float ys = 2.f * y - 1.f;
+    const float h = 1.f - ys * dot;
+    const bool pos = h > 0.f;
+    l = pos ? wt * h : 0.f;
+    m = pos ? -ys * wt : 0.f;
+  } else if (loss == LOSS_FTRL) {
+    m = __frcp_rn(1.f + __expf(-dot)) - y;
+    l = 0.f;
+  } else {
+    const float r = dot - y;
+    l = wt * 0.5f * r * r;
+    m = r * wt;
+  }
+}
 
 template <typename A>
 __device__ __forceinline__ void loss_and_mult(int loss, A dot, A y, A wt, A& l, A& m) {
@@ -92,32 +122,41 @@ __device__ __forceinline__ A sgd_apply(A w, A g, A W, A lr, A reg, A en) {
 struct GlmTail {
   int mode;        // TAIL_*
   int max_iter;
-  int* cnt;        // int32[TAIL_MAXG + 1] arrival tickets: zero-initialised once, re-armed by the
+  int det;         // 1: deterministic fixed-order group tree; 0: float atomics into `acc`
+  int* cnt;        // int32[TAIL_TOP + 1] arrival tickets: zero-initialised once, re-armed by the
                    // last arrivers, so every launch (and hipGraph replay) starts from zero
+  void* acc;       // [d+2] zero-initialised accumulator of the atomic tail (re-zeroed by it)
   void* stage1;    // [ngroups][d+2] accumulator rows
   void* feedback;  // [d+2]: output of TAIL_FEEDBACK, a copy of the global feedback otherwise
   double tol, lr, reg, en;
   xgmi::Ctx x;     // TAIL_XGMI only
 };
 
-// Split-K style hand-off (cdna_hip_programming.md Guideline 16 / "Projection GEMM" item 2):
-// every wave drains its stores, lane 0 releases at agent scope and draws a ticket; the block
-// drawing the last ticket acquires and proceeds. Returns true in that block only.
+// Write-through (sc1) hand-off of the partial rows (cdna_hip_programming.md Guideline 16, the
+// sc1 form of the split-K combine): every handed-off value is stored with an agent-scope store
+// (global_store … sc1) and loaded with an agent-scope load (global_load … sc1), so no release
+// fence (an L2 write-back per block: ~20 µs over 512 blocks, measured) and no acquire fence
+// are needed — only the drain before the ticket.
+template <typename A>
+__device__ __forceinline__ void st_agent(A* p, A v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename A>
+__device__ __forceinline__ A ld_agent(const A* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Every wave drains its sc1 stores, lane 0 draws a ticket; the block drawing the last one
+// proceeds (returns true there only).
 __device__ __forceinline__ bool arrive_last(int* cnt, int expected, int* sflag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = t == expected - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *sflag = last;
+    *sflag = t == expected - 1;
   }
   __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the ticket
   return *sflag != 0;
 }
 
@@ -136,58 +175,33 @@ __device__ void glm_xgmi_exchange(const xgmi::Ctx& x, A* fb, long stride) {
   if (threadIdx.x == 0) x.gen[GEN_GLM] = g + 1;
 }
 
+// Completes the round once sbuf[0..d+2) holds this rank's reduced feedback. In one-pass layouts
+// (d + 2 <= 2·blockDim) the caller has prefetched coef[tid], coef[tid + blockDim] into wa, wb.
 template <typename A>
-__device__ void glm_round_tail(const GlmTail& tl, const A* partials, int d, A* coef, int* state, int e, A* sbuf,
-                               int* sflag) {
+__device__ void glm_round_finish(const GlmTail& tl, A* sbuf, int d, A* coef, int* state, int e, bool one_pass, A wa,
+                                 A wb) {
   const long stride = d + 2;
-  const int nb = gridDim.x;
-  const int ngroups = (nb + TAIL_GROUP - 1) / TAIL_GROUP;
-  const int g = blockIdx.x / TAIL_GROUP;
-  const int g0 = g * TAIL_GROUP;
-  const int gs = nb - g0 < TAIL_GROUP ? nb - g0 : TAIL_GROUP;
-  A* st1 = (A*)tl.stage1;
-  // ---- ticket 1: the group's last block sums its partial rows (fixed order)
-  if (!arrive_last(&tl.cnt[g], gs, sflag)) return;
-  for (long c = threadIdx.x; c < stride; c += blockDim.x) {
-    A v[TAIL_GROUP];
-#pragma unroll
-    for (int q = 0; q < TAIL_GROUP; ++q) v[q] = partials[(long)(g0 + (q < gs ? q : 0)) * stride + c];
-    A sum = (A)0;
-#pragma unroll
-    for (int q = 0; q < TAIL_GROUP; ++q) sum += q < gs ? v[q] : (A)0;
-    st1[(long)g * stride + c] = sum;
-  }
-  if (threadIdx.x == 0) tl.cnt[g] = 0;  // all gs arrivals of this launch are in: re-arm
-  // ---- ticket 2: the last group finisher sums the group rows and completes the round
-  if (!arrive_last(&tl.cnt[TAIL_MAXG], ngroups, sflag)) return;
-  if (threadIdx.x == 0) tl.cnt[TAIL_MAXG] = 0;
-  for (long c = threadIdx.x; c < stride; c += blockDim.x) {
-    A v[TAIL_MAXG];
-#pragma unroll
-    for (int q = 0; q < TAIL_MAXG; ++q) v[q] = st1[(long)(q < ngroups ? q : 0) * stride + c];
-    A sum = (A)0;
-#pragma unroll
-    for (int q = 0; q < TAIL_MAXG; ++q) sum += q < ngroups ? v[q] : (A)0;
-    sbuf[c] = sum;
-  }
+  const int nt = blockDim.x;
   __syncthreads();
   if (tl.mode == TAIL_XGMI) glm_xgmi_exchange<A>(tl.x, sbuf, stride);
   A* fb = (A*)tl.feedback;
   if (tl.mode == TAIL_FEEDBACK) {
-    for (long c = threadIdx.x; c < stride; c += blockDim.x) fb[c] = sbuf[c];
+    for (long c = threadIdx.x; c < stride; c += nt) fb[c] = sbuf[c];
     return;
   }
   const A W = sbuf[d], L = sbuf[d + 1];
   const bool cont = (e + 1 < tl.max_iter) && (L / W > (A)tl.tol);
-  for (long c = threadIdx.x; c < d; c += blockDim.x) {
-    coef[c] = sgd_apply<A>(coef[c], sbuf[c], W, (A)tl.lr, (A)tl.reg, (A)tl.en);
-    if (fb) fb[c] = sbuf[c];
+  const A lr = (A)tl.lr, reg = (A)tl.reg, en = (A)tl.en;
+  const long ca = threadIdx.x, cb = threadIdx.x + nt;
+  if (one_pass) {
+    if (ca < d) coef[ca] = sgd_apply<A>(wa, sbuf[ca], W, lr, reg, en);
+    if (cb < d) coef[cb] = sgd_apply<A>(wb, sbuf[cb], W, lr, reg, en);
+  } else {
+    for (long c = threadIdx.x; c < d; c += nt) coef[c] = sgd_apply<A>(coef[c], sbuf[c], W, lr, reg, en);
   }
+  if (fb)
+    for (long c = threadIdx.x; c < stride; c += nt) fb[c] = sbuf[c];
   if (threadIdx.x == 0) {
-    if (fb) {
-      fb[d] = W;
-      fb[d + 1] = L;
-    }
     // every block of this launch read the state words before its first ticket
     state[ST_RUN0 + ((e + 1) & 1)] = cont ? 1 : 0;
     state[ST_EXECUTED] += 1;
@@ -195,13 +209,125 @@ __device__ void glm_round_tail(const GlmTail& tl, const A* partials, int d, A* c
   }
 }
 
+// Deterministic tail: block partial rows → per-group fixed-order sums → fixed-order total.
+template <typename A>
+__device__ void glm_round_tail_det(const GlmTail& tl, const A* partials, int d, A* coef, int* state, int e, A* sbuf,
+                                   int* sflag) {
+  const long stride = d + 2;
+  const int nb = gridDim.x;
+  const int nt = blockDim.x;
+  const int ngroups = (nb + TAIL_GROUP - 1) / TAIL_GROUP;
+  const int g = blockIdx.x / TAIL_GROUP;
+  const int g0 = g * TAIL_GROUP;
+  const int gs = nb - g0 < TAIL_GROUP ? nb - g0 : TAIL_GROUP;
+  A* st1 = (A*)tl.stage1;
+  // ---- ticket 1: the group's last block sums its partial rows (fixed order). Two columns per
+  // thread per pass with all their loads in flight together: one memory latency per pass.
+  if (!arrive_last(&tl.cnt[g], gs, sflag)) return;
+  for (long c0 = threadIdx.x; c0 < stride; c0 += 2 * nt) {
+    const long c1 = c0 + nt < stride ? c0 + nt : c0;
+    A v0[TAIL_GROUP], v1[TAIL_GROUP];
+#pragma unroll
+    for (int q = 0; q < TAIL_GROUP; ++q) {
+      const A* row = partials + (long)(g0 + (q < gs ? q : 0)) * stride;
+      v0[q] = ld_agent(row + c0);
+      v1[q] = ld_agent(row + c1);
+    }
+    A s0 = (A)0, s1 = (A)0;
+#pragma unroll
+    for (int q = 0; q < TAIL_GROUP; ++q) {
+      s0 += q < gs ? v0[q] : (A)0;
+      s1 += q < gs ? v1[q] : (A)0;
+    }
+    st_agent(st1 + (long)g * stride + c0, s0);
+    if (c1 != c0) st_agent(st1 + (long)g * stride + c1, s1);
+  }
+  if (threadIdx.x == 0) tl.cnt[g] = 0;  // all gs arrivals of this launch are in: re-arm
+  // ---- ticket 2: the last group finisher sums the group rows and completes the round
+  if (!arrive_last(&tl.cnt[TAIL_TOP], ngroups, sflag)) return;
+  if (threadIdx.x == 0) tl.cnt[TAIL_TOP] = 0;
+  const bool one_pass = stride <= 2L * nt && tl.mode != TAIL_FEEDBACK;
+  A wa = (A)0, wb = (A)0;
+  for (long c0 = threadIdx.x; c0 < stride; c0 += 2 * nt) {
+    const long c1 = c0 + nt < stride ? c0 + nt : c0;
+    A v0[TAIL_MAXG], v1[TAIL_MAXG];
+#pragma unroll
+    for (int q = 0; q < TAIL_MAXG; ++q) {
+      const A* row = st1 + (long)(q < ngroups ? q : 0) * stride;
+      v0[q] = ld_agent(row + c0);
+      v1[q] = ld_agent(row + c1);
+    }
+    if (one_pass) {  // the coefficients come in the same memory latency
+      wa = coef[threadIdx.x < d ? threadIdx.x : 0];
+      wb = coef[threadIdx.x + nt < d ? threadIdx.x + nt : 0];
+    }
+    A s0 = (A)0, s1 = (A)0;
+#pragma unroll
+    for (int q = 0; q < TAIL_MAXG; ++q) {
+      s0 += q < ngroups ? v0[q] : (A)0;
+      s1 += q < ngroups ? v1[q] : (A)0;
+    }
+    sbuf[c0] = s0;
+    sbuf[c1] = s1;
+  }
+  glm_round_finish<A>(tl, sbuf, d, coef, state, e, one_pass, wa, wb);
+}
+
+// Atomic tail: every block adds its row (LDS, 256 contiguous bytes per wave-instruction) into
+// `acc` with no-return float atomics, drains, and draws a ticket (per group of 32, then a top
+// ticket: no single counter takes all arrivals). The last block reads `acc` once, re-zeroes it
+// for the next launch and completes the round. Summation order varies run to run (last bits);
+// every rank of a multi-GPU job still ends identical (xGMI sums the published values in rank
+// order).
+template <typename A>
+__device__ void glm_round_tail_atomic(const GlmTail& tl, int d, A* coef, int* state, int e, A* sbuf, int* sflag) {
+  const long stride = d + 2;
+  const int nb = gridDim.x;
+  const int nt = blockDim.x;
+  A* acc = (A*)tl.acc;
+  for (long c = threadIdx.x; c < stride; c += nt) atomicAdd(acc + c, sbuf[c]);
+  const int ngroups = (nb + TAIL_GROUP - 1) / TAIL_GROUP;
+  const int g = blockIdx.x / TAIL_GROUP;
+  const int gs = nb - g * TAIL_GROUP < TAIL_GROUP ? nb - g * TAIL_GROUP : TAIL_GROUP;
+  if (!arrive_last(&tl.cnt[g], gs, sflag)) return;
+  if (threadIdx.x == 0) tl.cnt[g] = 0;
+  if (!arrive_last(&tl.cnt[TAIL_TOP], ngroups, sflag)) return;
+  if (threadIdx.x == 0) tl.cnt[TAIL_TOP] = 0;
+  const bool one_pass = stride <= 2L * nt && tl.mode != TAIL_FEEDBACK;
+  A wa = (A)0, wb = (A)0;
+  if (one_pass) {
+    const long ca = threadIdx.x, cb = threadIdx.x + nt;
+    const A a0 = ld_agent(acc + ca);
+    const A a1 = ld_agent(acc + (cb < stride ? cb : ca));
+    wa = coef[ca < d ? ca : 0];
+    wb = coef[cb < d ? cb : 0];
+    if (ca < stride) { sbuf[ca] = a0; st_agent(acc + ca, (A)0); }
+    if (cb < stride) { sbuf[cb] = a1; st_agent(acc + cb, (A)0); }
+  } else {
+    for (long c = threadIdx.x; c < stride; c += nt) {
+      sbuf[c] = ld_agent(acc + c);
+      st_agent(acc + c, (A)0);
+    }
+  }
+  glm_round_finish<A>(tl, sbuf, d, coef, state, e, one_pass, wa, wb);
+}
+
 // ------------------------------------------------------------------------------------------
 // K4/K5/K6 — fused minibatch loss + gradient partials
 // ------------------------------------------------------------------------------------------
-template <typename T, int EPC, int CPL, int U, int WPB>
-__global__ __launch_bounds__(WPB * 64) void glm_round_kernel(
-    const T* __restrict__ X, long ld, const typename AccOf<T>::type* __restrict__ y,
-    const typename AccOf<T>::type* __restrict__ wt, typename AccOf<T>::type* coef,
+// register-light shapes are capped at 128 VGPRs (4 waves per SIMD) so that two 8-wave blocks
+// share a CU; heavier ones (which would spill under the cap) keep the compiler's choice
+template <typename T, int EPC, int CPL, int U>
+constexpr int glm_min_waves() {
+  return CPL * EPC * (int)sizeof(T) * U <= 64 ? 4 : 1;
+}
+
+// X / y / wt are deliberately NOT __restrict__: with restrict the compiler may move the row
+// prefetch loads below the compiler fence that pins them ahead of the math (see the row loop).
+template <typename T, int EPC, int CPL, int U, int WPB, bool NT>
+__global__ __launch_bounds__(WPB * 64, (glm_min_waves<T, EPC, CPL, U>())) void glm_round_kernel(
+    const T* X, long ld, const typename AccOf<T>::type* y,
+    const typename AccOf<T>::type* wt, typename AccOf<T>::type* coef,
     long n, int d, long B, int loss, int* state, typename AccOf<T>::type* partials, GlmTail tl) {
   typedef typename AccOf<T>::type A;
   int e;
@@ -214,8 +340,7 @@ __global__ __launch_bounds__(WPB * 64) void glm_round_kernel(
   }
 
   const int lane = threadIdx.x & 63;
-  // wave id made provably wave-uniform so row indices / label loads become scalar (SMEM, lgkmcnt)
-  // and do not serialize behind the vector row loads on vmcnt
+  // wave id made provably wave-uniform so row indices are scalar
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nch = d / EPC;
   const long W = (long)gridDim.x * WPB;
@@ -242,22 +367,54 @@ __global__ __launch_bounds__(WPB * 64) void glm_round_kernel(
   Chunk<T, EPC> xa[U][CPL], xb[U][CPL];
   A ya[U], wa[U], yb[U], wb[U];
   bool va[U], vb[U];
-  auto load_rows = [&](long r0, long rsafe, Chunk<T, EPC> (&dst)[U][CPL], A (&yy)[U], A (&ww)[U],
+  const bool has_wt = wt != nullptr;
+  const A* wsrc = has_wt ? wt : y;
+  // Labels and weights of this wave's rows j = 0, 1, ... (row r_first + j·W) arrive 64 at a
+  // time, one per lane, by ONE vector load each, and are read out with readlane. Scalar loads
+  // per row would put every label behind an lgkmcnt(0) drain (SMEM returns out of order), i.e.
+  // a full memory latency per row pair; the vector loads are ordered with the row loads.
+  const long r_first = start + gw;
+  A ylab = (A)0, wlab = (A)1;
+  auto load_labels = [&](long j0) {
+    long rr = r_first + (j0 + lane) * W;
+    rr = rr < end ? rr : (end > 0 ? end - 1 : 0);
+    ylab = y[rr];
+    wlab = wsrc[rr];  // wsrc = wt, or y as a harmless stand-in (replaced by 1 in process)
+  };
+  auto lane_val = [&](A v, int l) -> A {
+    if constexpr (sizeof(A) == 4) {
+      return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+    } else {
+      const long long b = __double_as_longlong(v);
+      const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), l);
+      const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+      return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+    }
+  };
+  // rows r0 + u·W (u < U) are rows j0 + u of this wave; U divides 64, so a batch never
+  // straddles a label refill
+  auto load_rows = [&](long r0, long j0, long rsafe, Chunk<T, EPC> (&dst)[U][CPL], A (&yy)[U], A (&ww)[U],
                        bool (&vv)[U]) {
+    if ((j0 & 63) == 0 && j0 > 0) load_labels(j0);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long ru0 = r0 + u * W;
       const bool ok = ru0 < end;
       const long ru = ok ? ru0 : rsafe;
       vv[u] = ok;
-      yy[u] = y[ru];
-      ww[u] = wt ? wt[ru] : (A)1;
       const T* row = X + ru * ld;
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
         const int c = lane + 64 * k;
-        load_chunk<T, EPC>(row + (c < nch ? c : nch - 1) * EPC, dst[u][k]);
+        if constexpr (NT) load_chunk_nt<T, EPC>(row + (c < nch ? c : nch - 1) * EPC, dst[u][k]);
+        else load_chunk<T, EPC>(row + (c < nch ? c : nch - 1) * EPC, dst[u][k]);
       }
+    }
+    // after the row loads: reading the labels waits only for the (older) label load
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      yy[u] = lane_val(ylab, (int)((j0 + u) & 63));
+      ww[u] = lane_val(wlab, (int)((j0 + u) & 63));
     }
   };
   auto process = [&](Chunk<T, EPC> (&x)[U][CPL], A (&yy)[U], A (&ww)[U], bool (&vv)[U]) {
@@ -276,9 +433,10 @@ __global__ __launch_bounds__(WPB * 64) void glm_round_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       A l, m;
-      loss_and_mult<A>(loss, dot[u], yy[u], ww[u], l, m);
+      const A wu = has_wt ? ww[u] : (A)1;
+      loss_and_mult(loss, dot[u], yy[u], wu, l, m);
       if (!vv[u]) { l = (A)0; m = (A)0; }
-      wsum += vv[u] ? ww[u] : (A)0;
+      wsum += vv[u] ? wu : (A)0;
       lsum += l;
 #pragma unroll
       for (int k = 0; k < CPL; ++k)
@@ -288,16 +446,28 @@ __global__ __launch_bounds__(WPB * 64) void glm_round_kernel(
   };
   const long step = (long)U * W;
   long r = start + gw;
+  long j = 0;
   if (r < end) {
-    load_rows(r, r, xa, ya, wa, va);
+    load_labels(0);
+    load_rows(r, 0, r, xa, ya, wa, va);
     while (true) {
-      load_rows(r + step, r, xb, yb, wb, vb);
+      load_rows(r + step, j + U, r, xb, yb, wb, vb);
+      // pin the next batch's loads ahead of this batch's math: without the fences the compiler
+      // sinks them into the math (IR code motion, then the scheduler) to recycle registers and
+      // only ~1 row stays in flight per wave (measured: 47 µs vs a 33 µs streaming floor for
+      // the 200 MB batch). The asm is a compiler-only memory fence (no instruction, no wait).
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
       process(xa, ya, wa, va);
       r += step;
+      j += U;
       if (r >= end) break;
-      load_rows(r + step, r, xa, ya, wa, va);
+      load_rows(r + step, j + U, r, xa, ya, wa, va);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
       process(xb, yb, wb, vb);
       r += step;
+      j += U;
       if (r >= end) break;
     }
   }
@@ -332,24 +502,56 @@ __global__ __launch_bounds__(WPB * 64) void glm_round_kernel(
     }
     __syncthreads();
   }
+  int* sflag = reinterpret_cast<int*>(lw + WPB * 2);
+  if (tl.mode != TAIL_PARTIALS && !tl.det) {
+    // atomic tail: the block's row goes to LDS (row 0 of the tree buffer), then to `acc`
+    if (wave == 0) {
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const int c = lane + 64 * k;
+        if (c < nch)
+#pragma unroll
+          for (int i = 0; i < EPC; ++i) buf[c * EPC + i] = acc[k][i];
+      }
+      if (lane == 0) {
+        A ws = 0, ls = 0;
+        for (int q = 0; q < WPB; ++q) { ws += lw[q * 2]; ls += lw[q * 2 + 1]; }
+        buf[d] = ws;
+        buf[d + 1] = ls;
+      }
+    }
+    __syncthreads();
+    glm_round_tail_atomic<A>(tl, d, coef, state, e, buf, sflag);
+    return;
+  }
   if (wave == 0) {
     A* out = partials + (long)blockIdx.x * (d + 2);
+    // sc1 (write-through) stores when the fused tail consumes the row inside this launch
+    const bool wt1 = tl.mode != TAIL_PARTIALS;
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
       const int c = lane + 64 * k;
       if (c < nch)
 #pragma unroll
-        for (int i = 0; i < EPC; ++i) out[c * EPC + i] = acc[k][i];
+        for (int i = 0; i < EPC; ++i) {
+          if (wt1) st_agent(out + c * EPC + i, acc[k][i]);
+          else out[c * EPC + i] = acc[k][i];
+        }
     }
     if (lane == 0) {
       A ws = 0, ls = 0;
       for (int q = 0; q < WPB; ++q) { ws += lw[q * 2]; ls += lw[q * 2 + 1]; }
-      out[d] = ws;
-      out[d + 1] = ls;
+      if (wt1) {
+        st_agent(out + d, ws);
+        st_agent(out + d + 1, ls);
+      } else {
+        out[d] = ws;
+        out[d + 1] = ls;
+      }
     }
   }
   if (tl.mode == TAIL_PARTIALS) return;
-  glm_round_tail<A>(tl, partials, d, coef, state, e, buf, reinterpret_cast<int*>(lw + WPB * 2));
+  glm_round_tail_det<A>(tl, partials, d, coef, state, e, buf, sflag);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -547,7 +749,7 @@ __global__ __launch_bounds__(256) void glm_grad_csr_kernel(const long* __restric
     const A yy = y[r];
     const A ww = wt ? wt[r] : (A)1;
     A l, m;
-    loss_and_mult<A>(loss, s, yy, ww, l, m);
+    loss_and_mult(loss, s, yy, ww, l, m);
     wsum += ww;
     lsum += l;
     if (m != (A)0)
@@ -577,57 +779,84 @@ __global__ void glm_csr_predict_kernel(const long* __restrict__ indptr, const in
 // ---------------------------- host-side dispatch ------------------------------------------
 constexpr int WPB = 8;
 
+// Grid spreading: the dispatcher may stack up to 32 waves of this kernel on one CU while others
+// idle; requesting enough LDS per block that at most ceil(nblocks / 256) blocks fit a CU makes
+// every CU take its equal share (measured −11 % round time at 512 blocks). g_lds_pad < 0 = auto.
+// Non-temporal row loads (`flags & 1`) for batches streamed once per pass (−12 %, measured).
+static long g_lds_pad = -1;
+static int g_nt = -1;
+constexpr long LDS_PER_CU = 160 * 1024;
+constexpr int NUM_CU = 256;
+
 template <typename T, int EPC, int CPL, int U>
 int launch_grad_u(const void* X, long ld, const void* y, const void* wt, void* coef, long n, int d, long B, int loss,
-                  int* state, void* partials, int nblocks, const GlmTail& tl, hipStream_t s) {
+                  int* state, void* partials, int nblocks, const GlmTail& tl, int flags, hipStream_t s) {
   typedef typename AccOf<T>::type A;
   // [WPB/2][d] tree buffer (reused as the final block's feedback row) | [WPB][2] | ticket flag
   size_t shmem = (size_t)(WPB / 2) * d * sizeof(A) + WPB * 2 * sizeof(A) + 16;
-  hipLaunchKernelGGL((glm_round_kernel<T, EPC, CPL, U, WPB>), dim3(nblocks), dim3(WPB * 64), shmem, s, (const T*)X,
-                     ld, (const A*)y, (const A*)wt, (A*)coef, n, d, B, loss, state, (A*)partials, tl);
+  if (g_lds_pad >= 0) {
+    shmem += (size_t)g_lds_pad;
+  } else {
+    const long per_cu = (nblocks + NUM_CU - 1) / NUM_CU;
+    if (per_cu <= 3) {
+      const size_t want = (size_t)(LDS_PER_CU / (per_cu + 1) + 1024);
+      if (shmem < want) shmem = want;
+    }
+  }
+  const bool nt = g_nt >= 0 ? g_nt != 0 : (flags & 1) != 0;
+  if constexpr (EPC * sizeof(T) == 16 && sizeof(T) == 2) {
+    if (nt) {
+      hipLaunchKernelGGL((glm_round_kernel<T, EPC, CPL, U, WPB, true>), dim3(nblocks), dim3(WPB * 64), shmem, s,
+                         (const T*)X, ld, (const A*)y, (const A*)wt, (A*)coef, n, d, B, loss, state, (A*)partials, tl);
+      return (int)hipGetLastError();
+    }
+  }
+  hipLaunchKernelGGL((glm_round_kernel<T, EPC, CPL, U, WPB, false>), dim3(nblocks), dim3(WPB * 64), shmem, s,
+                     (const T*)X, ld, (const A*)y, (const A*)wt, (A*)coef, n, d, B, loss, state, (A*)partials, tl);
   return (int)hipGetLastError();
 }
 
 // rows in flight per wave = 2·U (software pipeline); u == 0 picks the default for the shape
 template <typename T, int EPC, int CPL>
 int launch_grad(int u, const void* X, long ld, const void* y, const void* wt, void* coef, long n, int d, long B,
-                int loss, int* state, void* partials, int nblocks, const GlmTail& tl, hipStream_t s) {
+                int loss, int* state, void* partials, int nblocks, const GlmTail& tl, int flags, hipStream_t s) {
   constexpr int BYTES = CPL * EPC * (int)sizeof(T);
   if (u == 0) u = BYTES <= 64 ? 2 : 1;
   if (u >= 4 && BYTES <= 32)
-    return launch_grad_u<T, EPC, CPL, 4>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
+    return launch_grad_u<T, EPC, CPL, 4>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
   if (u >= 2 && BYTES <= 64)
-    return launch_grad_u<T, EPC, CPL, 2>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
-  return launch_grad_u<T, EPC, CPL, 1>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
+    return launch_grad_u<T, EPC, CPL, 2>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
+  return launch_grad_u<T, EPC, CPL, 1>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
 }
 
 template <typename T, int EPC>
 int launch_grad_cpl(int cpl, int u, const void* X, long ld, const void* y, const void* wt, void* coef, long n, int d,
-                    long B, int loss, int* state, void* partials, int nblocks, const GlmTail& tl, hipStream_t s) {
+                    long B, int loss, int* state, void* partials, int nblocks, const GlmTail& tl, int flags,
+                    hipStream_t s) {
   switch (cpl) {
-    case 1: return launch_grad<T, EPC, 1>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
-    case 2: return launch_grad<T, EPC, 2>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
-    case 4: return launch_grad<T, EPC, 4>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
-    case 8: return launch_grad<T, EPC, 8>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
+    case 1: return launch_grad<T, EPC, 1>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
+    case 2: return launch_grad<T, EPC, 2>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
+    case 4: return launch_grad<T, EPC, 4>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
+    case 8: return launch_grad<T, EPC, 8>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
   }
   return -1;
 }
 
 int launch_round(int dtype, int epc, int cpl, int u, const void* X, long ld, const void* y, const void* wt, void* coef,
-                 long n, int d, long B, int loss, int* state, void* partials, int nblocks, const GlmTail& tl,
+                 long n, int d, long B, int loss, int* state, void* partials, int nblocks, const GlmTail& tl, int flags,
                  hipStream_t s) {
   if (dtype == DT_BF16) {
-    if (epc == 8) return launch_grad_cpl<bf16_t, 8>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
-    if (epc == 4) return launch_grad_cpl<bf16_t, 4>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
-    if (epc == 2) return launch_grad_cpl<bf16_t, 2>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
-    if (epc == 1) return launch_grad_cpl<bf16_t, 1>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
+    if (epc == 8) return launch_grad_cpl<bf16_t, 8>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
+    if (epc == 4) return launch_grad_cpl<bf16_t, 4>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
+    if (epc == 2) return launch_grad_cpl<bf16_t, 2>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
+    if (epc == 1) return launch_grad_cpl<bf16_t, 1>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
   } else if (dtype == DT_F32) {
-    if (epc == 4) return launch_grad_cpl<float, 4>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
-    if (epc == 2) return launch_grad_cpl<float, 2>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
-    if (epc == 1) return launch_grad_cpl<float, 1>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
+    if (epc == 4) return launch_grad_cpl<float, 4>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
+    if (epc == 2) return launch_grad_cpl<float, 2>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
+    if (epc == 1) return launch_grad_cpl<float, 1>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
   } else if (dtype == DT_F64) {
-    if (epc == 2) return launch_grad_cpl<double, 2>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
-    if (epc == 1) return launch_grad_cpl<double, 1>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, s);
+    if (epc == 2) return launch_grad_cpl<double, 2>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
+    if (epc == 1) return launch_grad_cpl<double, 1>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
   }
   return -1;
 }
@@ -660,13 +889,19 @@ int launch_pred_cpl(int cpl, const void* X, long ld, long n, int d, const void* 
 
 // epc = elements per 16/8/4/2-byte chunk chosen by the host so that d % epc == 0 and rows are
 // aligned; cpl = chunks per lane (power of two, 64*cpl*epc >= d).
+FMLX_API int fmlx_glm_set_tuning(long lds_pad, int nt) {
+  g_lds_pad = lds_pad;
+  g_nt = nt;
+  return 0;
+}
+
 FMLX_API int fmlx_glm_grad_partials(int dtype, int epc, int cpl, int u, const void* X, long ld, const void* y,
                                     const void* wt, const void* coef, long n, int d, long B, int loss, const int* state,
                                     void* partials, int nblocks, void* stream) {
   GlmTail tl{};
   tl.mode = TAIL_PARTIALS;
   return launch_round(dtype, epc, cpl, u, X, ld, y, wt, const_cast<void*>(coef), n, d, B, loss,
-                      const_cast<int*>(state), partials, nblocks, tl, (hipStream_t)stream);
+                      const_cast<int*>(state), partials, nblocks, tl, 0, (hipStream_t)stream);
 }
 
 // One whole SGD round in one launch (see the header comment). cnt: int32[17] zero-initialised;
@@ -674,16 +909,21 @@ FMLX_API int fmlx_glm_grad_partials(int dtype, int epc, int cpl, int u, const vo
 // peers/gen/err/spin_limit: the xGMI exchange (TAIL_XGMI only, see parallel/xgmi.py).
 FMLX_API int fmlx_glm_round(int dtype, int epc, int cpl, int u, const void* X, long ld, const void* y, const void* wt,
                             void* coef, long n, int d, long B, int loss, int* state, void* partials, int nblocks,
-                            int mode, int* cnt, void* stage1, void* feedback, int max_iter, double tol, double lr,
+                            int mode, int det, int* cnt, void* acc, void* stage1, void* feedback, int max_iter,
+                            double tol, double lr,
                             double reg, double en, void* const* peers, int world, int rank, int* gen, int* err,
-                            long spin_limit, void* stream) {
-  if (mode != TAIL_PARTIALS && (nblocks > TAIL_GROUP * TAIL_MAXG || cnt == nullptr || stage1 == nullptr)) return -4;
+                            long spin_limit, int flags, void* stream) {
+  if (mode != TAIL_PARTIALS && cnt == nullptr) return -4;
+  if (mode != TAIL_PARTIALS && det && (nblocks > TAIL_GROUP * TAIL_MAXG || stage1 == nullptr)) return -4;
+  if (mode != TAIL_PARTIALS && !det && (nblocks > TAIL_GROUP * TAIL_TOP || acc == nullptr)) return -4;
   if (mode == TAIL_FEEDBACK && feedback == nullptr) return -5;
   if (mode == TAIL_XGMI && (d + 2 > xgmi::GLM_MAX || peers == nullptr || world > xgmi::MAX_RANKS)) return -6;
   GlmTail tl{};
   tl.mode = mode;
   tl.max_iter = max_iter;
+  tl.det = det;
   tl.cnt = cnt;
+  tl.acc = acc;
   tl.stage1 = stage1;
   tl.feedback = feedback;
   tl.tol = tol;
@@ -691,7 +931,7 @@ FMLX_API int fmlx_glm_round(int dtype, int epc, int cpl, int u, const void* X, l
   tl.reg = reg;
   tl.en = en;
   tl.x = xgmi::Ctx{peers, world, rank, gen, err, spin_limit};
-  return launch_round(dtype, epc, cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl,
+  return launch_round(dtype, epc, cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags,
                       (hipStream_t)stream);
 }
 

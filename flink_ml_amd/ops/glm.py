@@ -18,7 +18,18 @@ MAX_CPL = 8
 WPB = 8
 # rows in flight per wave = 2*GRAD_UNROLL (0 = kernel default for the shape); tunable for A/B runs
 GRAD_UNROLL = int(os.environ.get("FMLX_GLM_UNROLL", "0"))
-GRAD_BLOCKS = int(os.environ.get("FMLX_GLM_BLOCKS", "512"))
+GRAD_BLOCKS = int(os.environ.get("FMLX_GLM_BLOCKS", "256"))
+
+
+# rows streamed once per pass use non-temporal loads when the data set exceeds the 256 MiB
+# Infinity Cache (otherwise rounds re-read it from there)
+NT_MIN_BYTES = 256 << 20
+
+
+def set_tuning(lds_pad: int = -1, nt: int = -1) -> None:
+    """A/B knobs of the round kernel (-1 = automatic): extra LDS per block (caps blocks per CU)
+    and non-temporal row loads."""
+    native.call("fmlx_glm_set_tuning", int(lds_pad), int(nt))
 
 
 def pick_layout(X: torch.Tensor) -> Optional[Tuple[int, int]]:
@@ -61,17 +72,32 @@ def stage1_rows(nparts: int) -> int:
 
 # fused-round tails (csrc/glm.hip): what the last block of the round does after the reduction
 TAIL_PARTIALS, TAIL_FEEDBACK, TAIL_UPDATE, TAIL_XGMI = 0, 1, 2, 3
-TAIL_MAX_BLOCKS = 512
+TAIL_MAX_BLOCKS = 512         # deterministic (fixed-order) tail
+TAIL_MAX_BLOCKS_ATOMIC = 2048  # float-atomic tail
+# FMLX_DETERMINISTIC=1: fixed-order in-kernel reduction (bit-reproducible run to run); default:
+# float atomics into one accumulator (shorter round tail; last bits vary with arrival order)
+DETERMINISTIC = os.environ.get("FMLX_DETERMINISTIC", "0") == "1"
+
+
+def max_round_blocks() -> int:
+    return TAIL_MAX_BLOCKS if DETERMINISTIC else TAIL_MAX_BLOCKS_ATOMIC
 
 
 class RoundScratch:
-    """Device scratch of one fused round: block partials, group rows, arrival tickets."""
+    """Device scratch of one fused round: block partials / group rows (deterministic tail), the
+    atomic accumulator, arrival tickets (all zero-initialised; the kernel re-arms them)."""
 
-    def __init__(self, nparts: int, d: int, acc: torch.dtype, device):
+    def __init__(self, nparts: int, d: int, acc: torch.dtype, device, det: bool = None):
         self.nparts = nparts
-        self.partials = torch.zeros((nparts, d + 2), dtype=acc, device=device)
-        self.stage1 = torch.zeros((stage1_rows(nparts), d + 2), dtype=acc, device=device)
-        self.cnt = torch.zeros(32, dtype=torch.int32, device=device)  # >= 17 tickets, zero-initialised
+        self.det = DETERMINISTIC if det is None else bool(det)
+        if self.det:
+            self.partials = torch.zeros((nparts, d + 2), dtype=acc, device=device)
+            self.stage1 = torch.zeros((stage1_rows(nparts), d + 2), dtype=acc, device=device)
+        else:
+            self.partials = torch.zeros((1, d + 2), dtype=acc, device=device)
+            self.stage1 = None
+        self.acc = torch.zeros(d + 2, dtype=acc, device=device)
+        self.cnt = torch.zeros(80, dtype=torch.int32, device=device)  # 64 group + 1 top tickets
 
 
 def glm_round(X, y, wt, coef, B: int, loss: int, state, scratch: RoundScratch, mode: int, feedback=None,
@@ -80,15 +106,16 @@ def glm_round(X, y, wt, coef, B: int, loss: int, state, scratch: RoundScratch, m
     """One SGD round (loss+gradient over the round's batch, fixed-order reduction and — by mode —
     feedback output, update, or xGMI exchange + update) as ONE kernel launch."""
     epc, cpl = pick_layout(X)
+    flags = 1 if X.shape[0] * X.stride(0) * X.element_size() > NT_MIN_BYTES else 0
     if xg is not None:
         peers, world, rank, gen, err, spin = xg.kernel_args()
     else:
         peers, world, rank, gen, err, spin = None, 1, 0, None, None, 0
     native.call("fmlx_glm_round", native.dtype_code(X.dtype), epc, cpl, GRAD_UNROLL, native.ptr(X), X.stride(0),
                 native.ptr(y), native.ptr(wt), native.ptr(coef), X.shape[0], X.shape[1], B, loss, native.ptr(state),
-                native.ptr(scratch.partials), scratch.nparts, mode, native.ptr(scratch.cnt),
-                native.ptr(scratch.stage1), native.ptr(feedback), int(max_iter), float(tol), float(lr), float(reg),
-                float(en), peers, world, rank, gen, err, int(spin), native.stream_ptr(X.device))
+                native.ptr(scratch.partials), scratch.nparts, mode, int(scratch.det), native.ptr(scratch.cnt),
+                native.ptr(scratch.acc), native.ptr(scratch.stage1), native.ptr(feedback), int(max_iter), float(tol), float(lr), float(reg),
+                float(en), peers, world, rank, gen, err, int(spin), flags, native.stream_ptr(X.device))
 
 
 def reduce_update(partials, nparts: int, d: int, stage1, coef, feedback, state, max_iter, tol, lr, reg, en) -> None:

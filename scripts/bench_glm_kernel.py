@@ -37,6 +37,8 @@ class SplitTrainer(DeviceGlmTrainer):
         s = self.sgd
         sc = self.scratch
         gk.grad_partials(self.X, self.y, self.w, self.coef, self.B, self.loss, self.state, sc.partials, sc.nparts)
+        if self.mode0_only:
+            return
         gk.reduce_update(sc.partials, sc.nparts, self.d, sc.stage1, self.coef, self.feedback, self.state, s.max_iter,
                          s.tol, s.learning_rate, s.reg, s.elastic_net)
 
@@ -63,9 +65,14 @@ def main():
         for c in cfgs:
             gk.GRAD_UNROLL = c.get("u", 0)
             gk.GRAD_BLOCKS = c.get("b", 512)
+            gk.set_tuning(c.get("pad", -1), c.get("nt", -1))
+            gk.DETERMINISTIC = bool(c.get("det", 0))
             sgd = SGD(max_iter=10 ** 8, learning_rate=0.1, global_batch_size=a.batch, tol=0.0)
-            cls = SplitTrainer if c.get("split") else DeviceGlmTrainer
+            cls = SplitTrainer if (c.get("split") or c.get("m0")) else DeviceGlmTrainer
             tr = cls(sgd, np.zeros(a.dim), X, y, None, "logistic", use_graph=True)
+            tr.mode0_only = bool(c.get("m0"))
+            if cls is SplitTrainer:  # the split round needs the block-partials scratch
+                tr.scratch = gk.RoundScratch(tr.nparts, a.dim, torch.float32, dev, det=True)
             tr.rounds_per_graph = 10
             tr.run_rounds(20)
             torch.cuda.synchronize()
@@ -73,7 +80,7 @@ def main():
             tr.run_rounds(a.rounds)
             torch.cuda.synchronize()
             us = (time.perf_counter() - t0) / a.rounds * 1e6
-            assert tr.rounds_executed() == 20 + a.rounds
+            assert c.get("m0") or tr.rounds_executed() == 20 + a.rounds
             res[json.dumps(c)].append(us)
     gb = a.batch * a.dim * 2 / 1e9
     for k, v in res.items():

@@ -91,10 +91,15 @@ def test_fused_sgd_round_two_ranks_matches_host(xgmi_mode):
         assert b0 == r1[loss][2], loss  # replicas identical
 
 
-def test_fused_round_flagship_shape_matches_torch():
-    """One fused round (TAIL_UPDATE) at the bench shape: 512 blocks → 16 groups, bf16 rows."""
+@pytest.mark.parametrize("det", [False, True])
+def test_fused_round_flagship_shape_matches_torch(det, monkeypatch):
+    """Fused rounds (TAIL_UPDATE) at the bench shape, bf16 rows: 512 blocks with the atomic tail
+    and with the deterministic 16-group fixed-order tail."""
     _need_gpu()
     from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
+    from flink_ml_amd.ops import glm as gk
+
+    monkeypatch.setattr(gk, "DETERMINISTIC", det)
 
     g = torch.Generator(device="cpu").manual_seed(7)
     n, d, B = 200_000, 1000, 100_000
@@ -103,7 +108,7 @@ def test_fused_round_flagship_shape_matches_torch():
     sgd = SGD(max_iter=3, learning_rate=0.1, global_batch_size=B, tol=1e-9)
     ref = TorchGlmTrainer(sgd, np.zeros(d), Xb.to(torch.float64), y, None, "logistic").fit()
     tr = DeviceGlmTrainer(sgd, np.zeros(d), Xb.cuda(), y.cuda(), None, "logistic", use_graph=False)
-    assert tr.nparts == 512
+    assert tr.nparts == 512 and tr.scratch.det == det
     got = tr.fit()
     assert tr.rounds_executed() == 3
     assert np.allclose(got, ref, rtol=2e-4, atol=2e-6), np.abs(got - ref).max()
