@@ -79,7 +79,8 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> SPM
             import datetime
 
             if backend is None:
-                backend = "nccl" if device.type == "cuda" else "gloo"
+                # FMLX_BACKEND=gloo: several ranks sharing one GPU (rehearsals of multi-GPU paths)
+                backend = os.environ.get("FMLX_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             kwargs = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
             if backend == "nccl":

@@ -100,6 +100,7 @@ def test_fused_round_flagship_shape_matches_torch(det, monkeypatch):
     from flink_ml_amd.ops import glm as gk
 
     monkeypatch.setattr(gk, "DETERMINISTIC", det)
+    monkeypatch.setattr(gk, "GRAD_BLOCKS", 512)
 
     g = torch.Generator(device="cpu").manual_seed(7)
     n, d, B = 200_000, 1000, 100_000
