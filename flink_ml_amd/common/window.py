@@ -118,3 +118,18 @@ def _count_to_json(self):
 
 
 CountTumblingWindows.to_json = _count_to_json
+
+
+class EndOfStreamWindows(Windows):
+    """A single window covering the whole bounded input, fired at end of input
+    (``CORE/common/datastream/EndOfStreamWindows.java:36-74``). For the bounded partitions
+    processed here it cuts the same single chunk as ``GlobalWindows``."""
+
+    _INSTANCE = None
+
+    @classmethod
+    def get(cls):
+        if cls._INSTANCE is None:
+            cls._INSTANCE = EndOfStreamWindows()
+        return cls._INSTANCE
+

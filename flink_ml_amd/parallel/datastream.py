@@ -9,7 +9,8 @@ reference                   here
 ==========================  ============================================================
 ``allReduceSum`` (:102)     ``all_reduce_sum`` — RCCL all-reduce of a device tensor
 ``mapPartition`` (:115)     ``map_partition`` — apply fn to the whole local partition
-``reduce`` (:132-155)       ``reduce`` — local fold, all-gather, fold in rank order
+``reduce`` (:132-143)       ``reduce`` — local fold, all-gather, fold in rank order
+keyed ``reduce`` (:155)     ``reduce_by_key`` — per-key local folds, all-gather, merge
 ``aggregate`` (:182-199)    ``aggregate`` — local accumulator, all-gather, merge in rank order
 ``sample`` (:212-227)       ``sample`` — reservoir per rank (java.util.Random), gather, again
 ``generateBatchData``       ``generate_batch_data`` — deterministic per-rank split of a global
@@ -25,7 +26,7 @@ from typing import Any, Callable, Iterable, Iterator, List, Optional, Sequence
 import numpy as np
 import torch
 
-from ..common.window import CountTumblingWindows, GlobalWindows, Windows
+from ..common.window import CountTumblingWindows, EndOfStreamWindows, GlobalWindows, Windows
 from ..table import Table
 from . import comm
 from .context import get_context
@@ -51,6 +52,31 @@ def reduce(value: Any, fn: Callable[[Any, Any], Any]):
     for v in vals[1:]:
         acc = fn(acc, v)
     return acc
+
+
+def reduce_by_key(pairs: Sequence, fn: Callable[[Any, Any], Any]) -> dict:
+    """Keyed ``DataStreamUtils.reduce`` (``DataStreamUtils.java:155``): folds the values of every
+    key with ``fn``. Each rank folds its own (key, value) pairs, the partial maps are exchanged
+    and merged in rank order; every rank gets the full result (the keyed shuffle of the
+    reference becomes one all-gather of per-key partials)."""
+    local: dict = {}
+    for k, v in pairs:
+        local[k] = fn(local[k], v) if k in local else v
+    out: dict = {}
+    for part in comm.all_gather_object(local):
+        for k, v in part.items():
+            out[k] = fn(out[k], v) if k in out else v
+    return out
+
+
+def set_managed_memory_weight(stream, weight: int):
+    """``DataStreamUtils.setManagedMemoryWeight`` (``:237-249``): in the reference it sizes the
+    managed memory of the operator caching the stream. Partitions here are HBM-resident tensors
+    (spilling, if any, is the data cache's job: ``parallel/datacache.py``), so it is a no-op that
+    returns the stream."""
+    if weight < 0:
+        raise ValueError("managed memory weight must be non-negative")
+    return stream
 
 
 class AggregateFunction:
@@ -125,7 +151,7 @@ def window_all_and_process(table: Table, windows: Windows, fn: Callable[[Table],
     if ctx.rank != 0:
         return None
     outs = []
-    if isinstance(windows, GlobalWindows) or windows is None:
+    if isinstance(windows, (GlobalWindows, EndOfStreamWindows)) or windows is None:
         outs.append(fn(full))
     elif isinstance(windows, CountTumblingWindows):
         n = windows.size
