@@ -93,7 +93,21 @@ def run_benchmark(name: str, spec: Dict) -> Dict:
             "stageTimeMs": stage_ms, "stageInputThroughput": n_in * 1000.0 / stage_ms if stage_ms > 0 else None}
 
 
-def run_config(conf: Dict, pattern: Optional[str] = None, verbose: bool = True, warmup: int = 0) -> Dict:
+def _cap_values(spec: Dict, max_values: Optional[int]) -> Dict:
+    """A copy of ``spec`` whose inputData.numValues is at most ``max_values`` (reduced runs of
+    the host-bound string stages; the result records the configured size it stands for)."""
+    if not max_values:
+        return spec
+    spec = json.loads(json.dumps(spec))
+    pm = spec.get("inputData", {}).setdefault("paramMap", {})
+    if int(pm.get("numValues", 0)) > max_values:
+        spec["configuredNumValues"] = int(pm["numValues"])
+        pm["numValues"] = int(max_values)
+    return spec
+
+
+def run_config(conf: Dict, pattern: Optional[str] = None, verbose: bool = True, warmup: int = 0,
+               max_values: Optional[int] = None) -> Dict:
     import re
 
     out = {}
@@ -101,6 +115,7 @@ def run_config(conf: Dict, pattern: Optional[str] = None, verbose: bool = True, 
     for name, spec in conf.items():
         if name == "version" or (rx and not rx.match(name)):
             continue
+        spec = _cap_values(spec, max_values)
         entry = dict(spec)
         if verbose and get_context().rank == 0:
             print("running %s ..." % name, flush=True)
@@ -124,10 +139,12 @@ def main(argv=None):
     ap.add_argument("--output-file", help="Where to write the results JSON")
     ap.add_argument("--pattern", help="Regex of benchmark names to run", default=None)
     ap.add_argument("--warmup", type=int, default=0, help="untimed runs of each benchmark before the timed one")
+    ap.add_argument("--max-values", type=int, default=None,
+                    help="cap inputData.numValues (reduced run; results keep configuredNumValues)")
     args = ap.parse_args(argv)
     if "RANK" in os.environ and "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) > 1:
         init_distributed()
-    res = run_config(load_config(args.config), args.pattern, warmup=args.warmup)
+    res = run_config(load_config(args.config), args.pattern, warmup=args.warmup, max_values=args.max_values)
     if get_context().rank == 0 and args.output_file:
         with open(args.output_file, "w", encoding="utf-8") as f:
             json.dump(res, f, indent=2)

@@ -77,7 +77,7 @@ __device__ __forceinline__ float wsum_dpp(float v) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
-template <int U, int LEVEL, int WPB>
+template <int U, int LEVEL, int WPB, int DACC = 1>
 __global__ __launch_bounds__(WPB * 64) void row_math(const u32x4* x, long rows, const float* coef, float* out) {
   const int lane = threadIdx.x & 63;
   const long W = (long)gridDim.x * WPB;
@@ -116,10 +116,14 @@ __global__ __launch_bounds__(WPB * 64) void row_math(const u32x4* x, long rows, 
     float dot[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      float s = 0.f;
+      float s[DACC];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) s += f[u][i] * w[i];
-      dot[u] = s;
+      for (int q = 0; q < DACC; ++q) s[q] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i % DACC] += f[u][i] * w[i];
+#pragma unroll
+      for (int q = 1; q < DACC; ++q) s[0] += s[q];
+      dot[u] = s[0];
     }
     if constexpr (LEVEL >= 2) {
 #pragma unroll
@@ -201,8 +205,14 @@ int main() {
     run("math L4 +axpy", [&](const u32x4* p) { row_math<2, 4, 8><<<512, 512>>>(p, batch, coef, out); });
     run("math L4 U4", [&](const u32x4* p) { row_math<4, 4, 8><<<512, 512>>>(p, batch, coef, out); });
     run("math L4 1024 blocks", [&](const u32x4* p) { row_math<2, 4, 8><<<1024, 512>>>(p, batch, coef, out); });
+    run("math L4 256 blocks", [&](const u32x4* p) { row_math<2, 4, 8><<<256, 512>>>(p, batch, coef, out); });
+    run("math L4 256x1024", [&](const u32x4* p) { row_math<2, 4, 16><<<256, 1024>>>(p, batch, coef, out); });
+    run("math L4 dacc4 512", [&](const u32x4* p) { row_math<2, 4, 8, 4><<<512, 512>>>(p, batch, coef, out); });
+    run("math L4 dacc4 256", [&](const u32x4* p) { row_math<2, 4, 8, 4><<<256, 512>>>(p, batch, coef, out); });
+    run("math L4 U1 512", [&](const u32x4* p) { row_math<1, 4, 8><<<512, 512>>>(p, batch, coef, out); });
+    run("math L4 U1 1024", [&](const u32x4* p) { row_math<1, 4, 8><<<1024, 512>>>(p, batch, coef, out); });
   }
-  for (int rep = 0; rep < 1; ++rep) {
+  for (int rep = 0; rep < 0; ++rep) {
     run("flat 2048x256", [&](const u32x4* p) { flat_stream<false><<<2048, 256>>>(p, batch * 125, out); });
     run("flat 2048x256 nt", [&](const u32x4* p) { flat_stream<true><<<2048, 256>>>(p, batch * 125, out); });
     run("flat 4096x256 nt", [&](const u32x4* p) { flat_stream<true><<<4096, 256>>>(p, batch * 125, out); });
