@@ -340,6 +340,69 @@ __global__ __launch_bounds__(256) void kmeans_chunk_sum_kernel(const T* __restri
   for (int c = threadIdx.x; c < D; c += 256) partial[b * D + c] = ((sm[0][c] + sm[1][c]) + sm[2][c]) + sm[3][c];
 }
 
+// bf16 rows, D = 8·LPR with LPR | 64: one 16-byte load per lane per row (LPR lanes cover a row,
+// 64/LPR rows per wave-step). The chunk's row indices are staged in LDS first so the gathers are
+// independent loads (4 in flight per lane), not an index→row dependent pair per row. Fixed
+// summation order (lane stripe, xor tree, wave order): deterministic.
+template <int LPR>
+__global__ __launch_bounds__(256) void kmeans_chunk_sum_bf16v_kernel(const bf16_t* __restrict__ X, long ld, int D,
+                                                                     const int* __restrict__ order,
+                                                                     const long* __restrict__ offsets,
+                                                                     const long* __restrict__ chunk_off, int k,
+                                                                     float* __restrict__ partial) {
+  constexpr int RPW = 64 / LPR;  // rows per wave-step
+  const long b = blockIdx.x;
+  if (b >= chunk_off[k]) return;
+  int lo = 0, hi = k;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (chunk_off[mid] <= b) lo = mid; else hi = mid;
+  }
+  const int j = lo;
+  const long p0 = offsets[j] + (b - chunk_off[j]) * KM_CH;
+  long p1 = p0 + KM_CH;
+  if (p1 > offsets[j + 1]) p1 = offsets[j + 1];
+  const int nrow = (int)(p1 - p0);
+  __shared__ int rows_s[KM_CH];
+  __shared__ float sm[4][512];
+  if ((int)threadIdx.x < nrow) rows_s[threadIdx.x] = order[p0 + threadIdx.x];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sub = lane / LPR, cl = lane % LPR;
+  float acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  constexpr int STEP = 4 * RPW;  // rows per block-step
+  for (int q0 = 0; q0 < nrow; q0 += 4 * STEP) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = q0 + u * STEP + wave * RPW + sub;
+      const int qc = q < nrow ? q : 0;  // unconditional load (row 0 of the chunk), masked below
+      v[u] = *reinterpret_cast<const uint4*>(X + (long)rows_s[qc] * ld + cl * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = q0 + u * STEP + wave * RPW + sub < nrow;
+      const unsigned int w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        acc[2 * h] += ok ? __uint_as_float(w4[h] << 16) : 0.f;
+        acc[2 * h + 1] += ok ? __uint_as_float(w4[h] & 0xffff0000u) : 0.f;
+      }
+    }
+  }
+#pragma unroll
+  for (int off = LPR; off < 64; off <<= 1)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] += __shfl_xor(acc[i], off, 64);
+  if (sub == 0)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sm[wave][cl * 8 + i] = acc[i];
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256) partial[b * D + c] = ((sm[0][c] + sm[1][c]) + sm[2][c]) + sm[3][c];
+}
+
 template <typename A>
 __global__ __launch_bounds__(256) void kmeans_cluster_sum_kernel(const A* __restrict__ partial, int D,
                                                                  const long* __restrict__ offsets,
@@ -514,6 +577,29 @@ FMLX_API int fmlx_kmeans_chunk_sum(int dtype, const void* X, long ld, int D, con
   if (dtype == DT_F32) return chunk_sum_vpl<float>(X, ld, D, order, offsets, chunk_off, k, max_chunks, partial, s);
   if (dtype == DT_F64) return chunk_sum_vpl<double>(X, ld, D, order, offsets, chunk_off, k, max_chunks, partial, s);
   return -1;
+}
+
+// bf16 fast path of the centroid accumulation: int32 row order (from the radix sort),
+// D in {8, 16, 32, 64, 128, 256, 512}, rows 16-byte aligned. Returns -2 for other shapes.
+FMLX_API int fmlx_kmeans_chunk_sum_bf16v(const void* X, long ld, int D, const int* order, const long* offsets,
+                                         const long* chunk_off, int k, long max_chunks, float* partial,
+                                         void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (max_chunks <= 0) return 0;
+  if ((ld % 8) != 0 || ((uintptr_t)X % 16) != 0) return -2;
+  dim3 g((unsigned)max_chunks);
+  const bf16_t* x = (const bf16_t*)X;
+  switch (D) {
+    case 8: hipLaunchKernelGGL(kmeans_chunk_sum_bf16v_kernel<1>, g, dim3(256), 0, s, x, ld, D, order, offsets, chunk_off, k, partial); break;
+    case 16: hipLaunchKernelGGL(kmeans_chunk_sum_bf16v_kernel<2>, g, dim3(256), 0, s, x, ld, D, order, offsets, chunk_off, k, partial); break;
+    case 32: hipLaunchKernelGGL(kmeans_chunk_sum_bf16v_kernel<4>, g, dim3(256), 0, s, x, ld, D, order, offsets, chunk_off, k, partial); break;
+    case 64: hipLaunchKernelGGL(kmeans_chunk_sum_bf16v_kernel<8>, g, dim3(256), 0, s, x, ld, D, order, offsets, chunk_off, k, partial); break;
+    case 128: hipLaunchKernelGGL(kmeans_chunk_sum_bf16v_kernel<16>, g, dim3(256), 0, s, x, ld, D, order, offsets, chunk_off, k, partial); break;
+    case 256: hipLaunchKernelGGL(kmeans_chunk_sum_bf16v_kernel<32>, g, dim3(256), 0, s, x, ld, D, order, offsets, chunk_off, k, partial); break;
+    case 512: hipLaunchKernelGGL(kmeans_chunk_sum_bf16v_kernel<64>, g, dim3(256), 0, s, x, ld, D, order, offsets, chunk_off, k, partial); break;
+    default: return -2;
+  }
+  return (int)hipGetLastError();
 }
 
 FMLX_API int fmlx_kmeans_cluster_sum(int acc_f64, const void* partial, int D, const long* offsets,

@@ -21,6 +21,10 @@ native.register_kernel_sigs({
     "fmlx_kmeans_chunk_sum": [c_int, c_void_p, c_long, c_int, c_void_p, c_void_p, c_void_p, c_int, c_long, c_void_p,
                               c_void_p],
     "fmlx_kmeans_cluster_sum": [c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
+    "fmlx_kmeans_chunk_sum_bf16v": [c_void_p, c_long, c_int, c_void_p, c_void_p, c_void_p, c_int, c_long, c_void_p,
+                                    c_void_p],
+    "fmlx_sort_pairs_temp_bytes": ([c_long, c_int], c_long),
+    "fmlx_sort_pairs": [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_long, c_void_p],
     "fmlx_kmeans_finalize": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                              c_void_p],
 })
@@ -127,6 +131,18 @@ class KMeansRound:
         self.partial = torch.zeros((self.max_chunks, self.D), dtype=self.acc, device=dev)
         self.payload = torch.zeros(k * self.D + k, dtype=self.acc, device=dev)
         self.zero_i64 = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.fast = (dev.type == "cuda" and X.dtype == torch.bfloat16 and self.D in (8, 16, 32, 64, 128, 256, 512)
+                     and X.stride(1) == 1 and X.stride(0) % 8 == 0 and X.data_ptr() % 16 == 0)
+        if dev.type == "cuda":
+            # stable radix sort of the labels over ceil(log2 k) bits (not a 64-bit argsort)
+            self.bits = max(1, int(k - 1).bit_length())
+            self.iota = torch.arange(self.n, dtype=torch.int32, device=dev)
+            self.keys_sorted = torch.empty(self.n, dtype=torch.int32, device=dev)
+            self.order32 = torch.empty(self.n, dtype=torch.int32, device=dev)
+            tb = native.kernels().fmlx_sort_pairs_temp_bytes(self.n, self.bits)
+            if tb < 0:
+                raise RuntimeError("radix sort temp-size query failed")
+            self.sort_temp = torch.empty(max(int(tb), 1), dtype=torch.uint8, device=dev)
 
     def run(self, cb: CentroidBuffers) -> torch.Tensor:
         X = self.X
@@ -134,15 +150,23 @@ class KMeansRound:
             self.payload.zero_()
             return self.payload
         assign(X, cb, self.metric, self.labels)
-        lab = self.labels.to(torch.int64)
-        order = torch.argsort(lab, stable=True)
-        counts = torch.bincount(lab, minlength=self.k)
+        stream = native.stream_ptr(X.device)
+        native.call("fmlx_sort_pairs", native.ptr(self.labels), native.ptr(self.keys_sorted), native.ptr(self.iota),
+                    native.ptr(self.order32), self.n, self.bits, native.ptr(self.sort_temp), self.sort_temp.numel(),
+                    stream)
+        counts = torch.bincount(self.labels, minlength=self.k)
         offsets = torch.cat([self.zero_i64, torch.cumsum(counts, 0)])
         chunk_off = torch.cat([self.zero_i64, torch.cumsum((counts + CHUNK - 1) // CHUNK, 0)])
-        Xs = X if X.dtype in (torch.bfloat16, torch.float32, torch.float64) else X.to(torch.float32)
-        native.call("fmlx_kmeans_chunk_sum", native.dtype_code(Xs.dtype), native.ptr(Xs), Xs.stride(0), self.D,
-                    native.ptr(order), native.ptr(offsets), native.ptr(chunk_off), self.k, self.max_chunks,
-                    native.ptr(self.partial), native.stream_ptr(X.device))
+        if self.fast:
+            native.call("fmlx_kmeans_chunk_sum_bf16v", native.ptr(X), X.stride(0), self.D, native.ptr(self.order32),
+                        native.ptr(offsets), native.ptr(chunk_off), self.k, self.max_chunks, native.ptr(self.partial),
+                        stream)
+        else:
+            order = self.order32.to(torch.int64)
+            Xs = X if X.dtype in (torch.bfloat16, torch.float32, torch.float64) else X.to(torch.float32)
+            native.call("fmlx_kmeans_chunk_sum", native.dtype_code(Xs.dtype), native.ptr(Xs), Xs.stride(0), self.D,
+                        native.ptr(order), native.ptr(offsets), native.ptr(chunk_off), self.k, self.max_chunks,
+                        native.ptr(self.partial), stream)
         native.call("fmlx_kmeans_cluster_sum", int(self.acc == torch.float64), native.ptr(self.partial), self.D,
                     native.ptr(offsets), native.ptr(chunk_off), self.k, native.ptr(self.payload),
                     native.stream_ptr(X.device))
