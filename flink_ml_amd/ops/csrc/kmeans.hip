@@ -34,11 +34,12 @@ constexpr int KM_CH = 256;  // rows per gather chunk
 // ------------------------------------------------------------------------------------------
 // MFMA assign (euclidean, bf16)
 // ------------------------------------------------------------------------------------------
-template <int KS>
-__global__ __launch_bounds__(256) void kmeans_assign_bf16_kernel(const bf16_t* __restrict__ X, long ld, long n,
-                                                                 int D, const bf16_t* __restrict__ Cb,
-                                                                 const float* __restrict__ cnorm, int kpad,
-                                                                 int* __restrict__ labels) {
+template <int KS, bool FULL>
+// Cb / cnorm are not __restrict__ so the compiler fence after each tile prefetch keeps the
+// loads where they are issued (with restrict they get sunk next to their use, after the MFMAs).
+__global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t* __restrict__ X, long ld, long n,
+                                                                 int D, const bf16_t* Cb, const float* cnorm,
+                                                                 int kpad, int* __restrict__ labels) {
   constexpr int MT = KS <= 8 ? 2 : 1;     // 32-row m-tiles per wave
   constexpr int DP = KS * 16;             // padded feature dim
   constexpr int ROWB = DP * 2 + 16;       // padded LDS row stride (bytes): conflict-free b128 reads
@@ -52,33 +53,56 @@ __global__ __launch_bounds__(256) void kmeans_assign_bf16_kernel(const bf16_t* _
   const int h = lane >> 5;
   const long rowbase = (long)blockIdx.x * (4 * 32 * MT) + (long)wave * 32 * MT;
 
-  // ---- A fragments: this wave's MT x 32 rows, whole padded K, in registers
+  // ---- A fragments: this wave's MT x 32 rows, whole padded K, in registers. FULL (D == 16·KS,
+  // 16-B aligned rows): unconditional 16-B loads of clamped rows, all in flight together — a
+  // per-fragment branch would make every load wait for the previous one (16 round trips).
   bf16x8_t a[MT][KS];
-  const bool aligned16 = (ld & 7) == 0;
+  if constexpr (FULL) {
 #pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    const long row = rowbase + m * 32 + r32;
-    const bf16_t* xr = X + (row < n ? row : 0) * ld;
+    for (int m = 0; m < MT; ++m) {
+      const long row = rowbase + m * 32 + r32;
+      const bf16_t* xr = X + (row < n ? row : n - 1) * ld;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int k0 = 16 * s + 8 * h;
-      union { uint4 u; bf16x8_t v; uint16_t e[8]; } t;
-      t.u = make_uint4(0, 0, 0, 0);
-      if (row < n) {
-        if (k0 + 8 <= D) {
-          if (aligned16) {
-            t.u = *reinterpret_cast<const uint4*>(xr + k0);
-          } else {
-            const uint32_t* p = reinterpret_cast<const uint32_t*>(xr + k0);
-            t.u = make_uint4(p[0], p[1], p[2], p[3]);
-          }
-        } else {
-          for (int j = 0; j < 8; ++j) t.e[j] = (k0 + j < D) ? xr[k0 + j] : (uint16_t)0;
-        }
+      for (int s = 0; s < KS; ++s) {
+        union { uint4 u; bf16x8_t v; } t;
+        t.u = *reinterpret_cast<const uint4*>(xr + 16 * s + 8 * h);
+        a[m][s] = t.v;
       }
-      a[m][s] = t.v;
+    }
+  } else {
+    const bool aligned16 = (ld & 7) == 0;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const long row = rowbase + m * 32 + r32;
+      const bf16_t* xr = X + (row < n ? row : 0) * ld;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int k0 = 16 * s + 8 * h;
+        union { uint4 u; bf16x8_t v; uint16_t e[8]; } t;
+        t.u = make_uint4(0, 0, 0, 0);
+        if (row < n) {
+          if (k0 + 8 <= D) {
+            if (aligned16) {
+              t.u = *reinterpret_cast<const uint4*>(xr + k0);
+            } else {
+              const uint32_t* p = reinterpret_cast<const uint32_t*>(xr + k0);
+              t.u = make_uint4(p[0], p[1], p[2], p[3]);
+            }
+          } else {
+            for (int j = 0; j < 8; ++j) t.e[j] = (k0 + j < D) ? xr[k0 + j] : (uint16_t)0;
+          }
+        }
+        a[m][s] = t.v;
+      }
     }
   }
+
+  // Consume the fragments once here: the waits for their loads then sit before the tile loop
+  // instead of inside it, where the (static) counts would also drain the next tile's prefetch.
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) asm volatile("" ::"v"(a[m][s]));
 
   float best[MT][16];
   int bidx[MT][16];
@@ -88,32 +112,40 @@ __global__ __launch_bounds__(256) void kmeans_assign_bf16_kernel(const bf16_t* _
     for (int r = 0; r < 16; ++r) { best[m][r] = __builtin_huge_valf(); bidx[m][r] = 0; }
 
   const int ntiles = kpad / 32;
-  // register-staged tile loader: chunk q of the tile = (row q / (DP/8), 16B piece q % (DP/8))
-  uint4 stage[CPT];
-  auto gload = [&](int t) {
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int q = threadIdx.x + 256 * i;
-      if (q < CHUNKS) stage[i] = reinterpret_cast<const uint4*>(Cb + (long)t * 32 * DP)[q];
-    }
-  };
-  auto swrite = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int q = threadIdx.x + 256 * i;
-      if (q < CHUNKS) {
-        const int rr = q / (DP / 8), cc = q % (DP / 8);
-        *reinterpret_cast<uint4*>(lds + buf * 32 * ROWB + rr * ROWB + cc * 16) = stage[i];
-      }
-    }
-  };
-
-  gload(0);
-  swrite(0);
+  // register-staged tile loader: chunk q of the tile = (row q / (DP/8), 16B piece q % (DP/8)).
+  // Loads are unconditional (clamped to the last chunk) so the next tile stays in flight under
+  // this tile's MFMAs; the LDS write is the masked part. (Plain code, no lambdas: a captured
+  // staging array was demoted to scratch, and its spill store waited for the prefetch.)
+#define KM_LD1(I_, T_)                                                                 \
+  if constexpr (CPT > (I_)) {                                                          \
+    int q = threadIdx.x + 256 * (I_);                                                  \
+    if (CHUNKS % 256 != 0) q = q < CHUNKS ? q : CHUNKS - 1;                            \
+    st##I_ = reinterpret_cast<const uint4*>(Cb + (long)(T_) * 32 * DP)[q];             \
+  }
+#define KM_ST1(I_, BUF_)                                                               \
+  if constexpr (CPT > (I_)) {                                                          \
+    const int q = threadIdx.x + 256 * (I_);                                            \
+    if (CHUNKS % 256 == 0 || q < CHUNKS) {                                             \
+      const int rr = q / (DP / 8), cc = q % (DP / 8);                                  \
+      *reinterpret_cast<uint4*>(lds + (BUF_) * 32 * ROWB + rr * ROWB + cc * 16) = st##I_; \
+    }                                                                                  \
+  }
+#define KM_GLOAD(T_) \
+  KM_LD1(0, T_) KM_LD1(1, T_) KM_LD1(2, T_) KM_LD1(3, T_) cn_next = cnorm[(T_) * 32 + r32];
+#define KM_SWRITE(BUF_) KM_ST1(0, BUF_) KM_ST1(1, BUF_) KM_ST1(2, BUF_) KM_ST1(3, BUF_)
+  static_assert(CPT <= 4, "tile staging supports up to 4 chunks per thread");
+  uint4 st0, st1, st2, st3;  // named registers (an indexed array was demoted to scratch)
+  float cn_next;
+  KM_GLOAD(0)
+  KM_SWRITE(0)
+  float cn = cn_next;
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
     const int cur = t & 1;
-    if (t + 1 < ntiles) gload(t + 1);  // in flight during the MFMAs
+    const bool more = t + 1 < ntiles;
+    const int tn = more ? t + 1 : t;  // the last tile re-fetches itself (unconditional loads)
+    KM_GLOAD(tn)
+    asm volatile("" ::: "memory");
     f32x16_t acc[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
@@ -127,7 +159,6 @@ __global__ __launch_bounds__(256) void kmeans_assign_bf16_kernel(const bf16_t* _
       for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m][s], b, acc[m], 0, 0, 0);
     }
     const int col = t * 32 + r32;
-    const float cn = cnorm[col];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -135,9 +166,16 @@ __global__ __launch_bounds__(256) void kmeans_assign_bf16_kernel(const bf16_t* _
         const float v = cn - 2.f * acc[m][r];
         if (v < best[m][r]) { best[m][r] = v; bidx[m][r] = col; }
       }
-    if (t + 1 < ntiles) swrite(cur ^ 1);
+    if (more) {
+      KM_SWRITE(cur ^ 1)
+    }
+    cn = cn_next;
     __syncthreads();
   }
+#undef KM_GLOAD
+#undef KM_SWRITE
+#undef KM_LD1
+#undef KM_ST1
 
   // ---- row argmin across the 32 lanes of each half (ties → lower index)
 #pragma unroll
@@ -473,8 +511,13 @@ int launch_assign_bf16(const void* X, long ld, long n, int D, const void* Cb, co
   const long rows_per_block = 4 * 32 * MT;
   const int blocks = (int)((n + rows_per_block - 1) / rows_per_block);
   if (blocks == 0) return 0;
-  hipLaunchKernelGGL(kmeans_assign_bf16_kernel<KS>, dim3(blocks), dim3(256), 0, s, (const bf16_t*)X, ld, n, D,
-                     (const bf16_t*)Cb, cnorm, kpad, labels);
+  const bool full = D == 16 * KS && (ld % 8) == 0 && ((uintptr_t)X % 16) == 0;
+  if (full)
+    hipLaunchKernelGGL((kmeans_assign_bf16_kernel<KS, true>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)X, ld, n,
+                       D, (const bf16_t*)Cb, cnorm, kpad, labels);
+  else
+    hipLaunchKernelGGL((kmeans_assign_bf16_kernel<KS, false>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)X, ld, n,
+                       D, (const bf16_t*)Cb, cnorm, kpad, labels);
   return (int)hipGetLastError();
 }
 
