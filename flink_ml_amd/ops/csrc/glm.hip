@@ -123,6 +123,8 @@ struct GlmTail {
   int mode;        // TAIL_*
   int max_iter;
   int det;         // 1: deterministic fixed-order group tree; 0: float atomics into `acc`
+  int flat_lds;    // atomic tail with the one-barrier [WPB][d] LDS image (set by the launcher)
+  int nbatch;      // ceil(n / B) (set by the launcher)
   int* cnt;        // int32[TAIL_TOP + 1] arrival tickets: zero-initialised once, re-armed by the
                    // last arrivers, so every launch (and hipGraph replay) starts from zero
   void* acc;       // [d+2] zero-initialised accumulator of the atomic tail (re-zeroed by it)
@@ -281,18 +283,14 @@ __device__ void glm_round_tail_det(const GlmTail& tl, const A* partials, int d, 
 // order).
 template <typename A>
 __device__ void glm_round_tail_atomic(const GlmTail& tl, int d, A* coef, int* state, int e, A* sbuf, int* sflag) {
+  // (the caller has added this block's row into tl.acc with no-return atomics)
   const long stride = d + 2;
-  const int nb = gridDim.x;
   const int nt = blockDim.x;
   A* acc = (A*)tl.acc;
-  for (long c = threadIdx.x; c < stride; c += nt) atomicAdd(acc + c, sbuf[c]);
-  const int ngroups = (nb + TAIL_GROUP - 1) / TAIL_GROUP;
-  const int g = blockIdx.x / TAIL_GROUP;
-  const int gs = nb - g * TAIL_GROUP < TAIL_GROUP ? nb - g * TAIL_GROUP : TAIL_GROUP;
-  if (!arrive_last(&tl.cnt[g], gs, sflag)) return;
-  if (threadIdx.x == 0) tl.cnt[g] = 0;
-  if (!arrive_last(&tl.cnt[TAIL_TOP], ngroups, sflag)) return;
-  if (threadIdx.x == 0) tl.cnt[TAIL_TOP] = 0;
+  // one ticket over all blocks: arrivals are spread over the blocks' finishing times, so a single
+  // counter costs the last block one atomic round trip instead of two
+  if (!arrive_last(&tl.cnt[0], gridDim.x, sflag)) return;
+  if (threadIdx.x == 0) tl.cnt[0] = 0;
   const bool one_pass = stride <= 2L * nt && tl.mode != TAIL_FEEDBACK;
   A wa = (A)0, wb = (A)0;
   if (one_pass) {
@@ -334,8 +332,9 @@ __global__ __launch_bounds__(WPB * 64, (glm_min_waves<T, EPC, CPL, U>())) void g
   if (!round_running(state, e)) return;
   long start = 0, end = 0;  // a rank with no rows (or a zero local batch) still joins the tail
   if (n > 0 && B > 0) {
-    const long P = (n + B - 1) / B;
-    start = (long)(e % P) * B;
+    // batches per pass: precomputed by the launcher (a 64-bit division per wave otherwise)
+    const unsigned P = tl.nbatch > 0 ? (unsigned)tl.nbatch : (unsigned)((n + B - 1) / B);
+    start = (long)((unsigned)e % P) * B;
     end = start + B < n ? start + B : n;
   }
 
@@ -349,14 +348,18 @@ __global__ __launch_bounds__(WPB * 64, (glm_min_waves<T, EPC, CPL, U>())) void g
   A w[CPL][EPC];
   A acc[CPL][EPC];
 #pragma unroll
-  for (int k = 0; k < CPL; ++k) {
-    const int c = lane + 64 * k;
+  for (int k = 0; k < CPL; ++k)
 #pragma unroll
-    for (int i = 0; i < EPC; ++i) {
-      w[k][i] = c < nch ? coef[c * EPC + i] : (A)0;
-      acc[k][i] = (A)0;
+    for (int i = 0; i < EPC; ++i) acc[k][i] = (A)0;
+  // coefficient slices (L2-hot), fetched after the first row loads are on their way
+  auto load_w = [&]() {
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      const int c = lane + 64 * k;
+#pragma unroll
+      for (int i = 0; i < EPC; ++i) w[k][i] = c < nch ? coef[c * EPC + i] : (A)0;
     }
-  }
+  };
   A wsum = 0, lsum = 0;
 
   // Software pipeline, manually unrolled by two so the compiler keeps the next batch's loads in
@@ -448,8 +451,9 @@ __global__ __launch_bounds__(WPB * 64, (glm_min_waves<T, EPC, CPL, U>())) void g
   long r = start + gw;
   long j = 0;
   if (r < end) {
-    load_labels(0);
+    load_labels(0);  // first: load_rows reads the labels right after issuing its row loads
     load_rows(r, 0, r, xa, ya, wa, va);
+    load_w();
     while (true) {
       load_rows(r + step, j + U, r, xb, yb, wb, vb);
       // pin the next batch's loads ahead of this batch's math: without the fences the compiler
@@ -472,11 +476,42 @@ __global__ __launch_bounds__(WPB * 64, (glm_min_waves<T, EPC, CPL, U>())) void g
     }
   }
 
-  // fixed-order tree across the block's waves through LDS
   extern __shared__ __align__(16) unsigned char smem_raw[];
-  A* buf = reinterpret_cast<A*>(smem_raw);         // [WPB/2][d]
-  A* lw = buf + (WPB / 2) * (long)d;                // [WPB][2]
+  A* buf = reinterpret_cast<A*>(smem_raw);          // [WPB][d] (flat) or [WPB/2][d] (tree)
+  const bool flat = tl.mode != TAIL_PARTIALS && !tl.det && tl.flat_lds;
+  A* lw = buf + (flat ? WPB : WPB / 2) * (long)d;   // [WPB][2]
+  int* sflag = reinterpret_cast<int*>(lw + WPB * 2);
   if (lane == 0) { lw[wave * 2] = wsum; lw[wave * 2 + 1] = lsum; }
+  if (flat) {
+    // atomic tail, one barrier: every wave parks its row in LDS, then each thread sums its
+    // columns over the waves (fixed order) and adds them to tl.acc (256 contiguous bytes per
+    // wave-instruction)
+    A* mine = buf + (long)wave * d;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      const int c = lane + 64 * k;
+      if (c < nch)
+#pragma unroll
+        for (int i = 0; i < EPC; ++i) mine[c * EPC + i] = acc[k][i];
+    }
+    __syncthreads();
+    A* gacc = (A*)tl.acc;
+    const long stride = d + 2;
+    for (long c = threadIdx.x; c < stride; c += blockDim.x) {
+      A v = (A)0;
+      if (c < d) {
+#pragma unroll
+        for (int q = 0; q < WPB; ++q) v += buf[(long)q * d + c];
+      } else {
+#pragma unroll
+        for (int q = 0; q < WPB; ++q) v += lw[q * 2 + (int)(c - d)];
+      }
+      atomicAdd(gacc + c, v);
+    }
+    glm_round_tail_atomic<A>(tl, d, coef, state, e, buf, sflag);
+    return;
+  }
+  // fixed-order tree across the block's waves through LDS
 #pragma unroll
   for (int half = WPB / 2; half >= 1; half >>= 1) {
     if (wave >= half && wave < 2 * half) {
@@ -502,9 +537,9 @@ __global__ __launch_bounds__(WPB * 64, (glm_min_waves<T, EPC, CPL, U>())) void g
     }
     __syncthreads();
   }
-  int* sflag = reinterpret_cast<int*>(lw + WPB * 2);
   if (tl.mode != TAIL_PARTIALS && !tl.det) {
-    // atomic tail: the block's row goes to LDS (row 0 of the tree buffer), then to `acc`
+    // atomic tail (rows too wide for the flat LDS image): the tree's result goes to LDS row 0,
+    // then to `acc`
     if (wave == 0) {
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
@@ -521,6 +556,8 @@ __global__ __launch_bounds__(WPB * 64, (glm_min_waves<T, EPC, CPL, U>())) void g
       }
     }
     __syncthreads();
+    A* gacc = (A*)tl.acc;
+    for (long c = threadIdx.x; c < d + 2; c += blockDim.x) atomicAdd(gacc + c, buf[c]);
     glm_round_tail_atomic<A>(tl, d, coef, state, e, buf, sflag);
     return;
   }
@@ -793,7 +830,10 @@ int launch_grad_u(const void* X, long ld, const void* y, const void* wt, void* c
                   int* state, void* partials, int nblocks, const GlmTail& tl, int flags, hipStream_t s) {
   typedef typename AccOf<T>::type A;
   // [WPB/2][d] tree buffer (reused as the final block's feedback row) | [WPB][2] | ticket flag
-  size_t shmem = (size_t)(WPB / 2) * d * sizeof(A) + WPB * 2 * sizeof(A) + 16;
+  GlmTail t2 = tl;
+  t2.nbatch = (n > 0 && B > 0) ? (int)((n + B - 1) / B) : 0;
+  t2.flat_lds = tl.mode != TAIL_PARTIALS && !tl.det && (size_t)WPB * d * sizeof(A) <= 64 * 1024;
+  size_t shmem = (size_t)(t2.flat_lds ? WPB : WPB / 2) * d * sizeof(A) + WPB * 2 * sizeof(A) + 16;
   if (g_lds_pad >= 0) {
     shmem += (size_t)g_lds_pad;
   } else {
@@ -807,12 +847,12 @@ int launch_grad_u(const void* X, long ld, const void* y, const void* wt, void* c
   if constexpr (EPC * sizeof(T) == 16 && sizeof(T) == 2) {
     if (nt) {
       hipLaunchKernelGGL((glm_round_kernel<T, EPC, CPL, U, WPB, true>), dim3(nblocks), dim3(WPB * 64), shmem, s,
-                         (const T*)X, ld, (const A*)y, (const A*)wt, (A*)coef, n, d, B, loss, state, (A*)partials, tl);
+                         (const T*)X, ld, (const A*)y, (const A*)wt, (A*)coef, n, d, B, loss, state, (A*)partials, t2);
       return (int)hipGetLastError();
     }
   }
   hipLaunchKernelGGL((glm_round_kernel<T, EPC, CPL, U, WPB, false>), dim3(nblocks), dim3(WPB * 64), shmem, s,
-                     (const T*)X, ld, (const A*)y, (const A*)wt, (A*)coef, n, d, B, loss, state, (A*)partials, tl);
+                     (const T*)X, ld, (const A*)y, (const A*)wt, (A*)coef, n, d, B, loss, state, (A*)partials, t2);
   return (int)hipGetLastError();
 }
 
