@@ -159,6 +159,26 @@ class OnlineLogisticRegressionParams(HasLabelCol, HasWeightCol, HasBatchStrategy
     BETA = FloatParam("beta", "The beta parameter of ftrl.", 0.1, ParamValidators.gt(0.0))
 
 
+class DeviceDenseVector(DenseVector):
+    """A model version that stays on the device: ``values`` materialises (once) the host copy.
+    Training appends one per mini-batch without a device→host synchronisation."""
+
+    __slots__ = ("_dev", "_host")
+
+    def __init__(self, t: torch.Tensor):
+        self._dev = t
+        self._host = None
+
+    @property
+    def values(self):
+        if self._host is None:
+            self._host = self._dev.to(torch.float64).cpu().numpy()
+        return self._host
+
+    def device_values(self) -> torch.Tensor:
+        return self._dev
+
+
 class FtrlTrainer:
     """Replicated FTRL state on the device + one round per mini-batch."""
 
@@ -173,6 +193,7 @@ class FtrlTrainer:
         self.alpha, self.beta, self.l1, self.l2 = alpha, beta, l1, l2
         self.fcol, self.lcol, self.wcol = features_col, label_col, weight_col
         self.version = 0
+        self._scratch = {}  # (nparts, dtype) -> (RoundScratch, feedback, state): no per-batch allocation
 
     def local_gradient(self, batch: Table):
         X = config.features_for_compute(batch, self.fcol)
@@ -196,11 +217,15 @@ class FtrlTrainer:
         if self.dev.type == "cuda" and gk.pick_layout(X) is not None:
             Xk = X if X.dtype in (torch.float32, torch.float64, torch.bfloat16) else X.to(self.acc)
             kacc = torch.float64 if Xk.dtype == torch.float64 else torch.float32
-            nparts = max(1, min(gk.max_round_blocks(), math.ceil(n / (gk.WPB * 16))))
-            scratch = gk.RoundScratch(nparts, self.d, kacc, self.dev)
-            fb = torch.zeros(self.d + 2, dtype=kacc, device=self.dev)
-            state = torch.tensor([0, 1, 1, 0, 0, 0, 0, 0], dtype=torch.int32, device=self.dev)
-            coef = self.coef.to(kacc).contiguous()
+            nparts = max(1, min(gk.GRAD_BLOCKS, gk.max_round_blocks(), math.ceil(n / (gk.WPB * 16))))
+            key = (nparts, kacc)
+            if key not in self._scratch:
+                state = torch.zeros(8, dtype=torch.int32, device=self.dev)
+                state[1:3] = 1  # running; the feedback-only tail never advances it
+                self._scratch[key] = (gk.RoundScratch(nparts, self.d, kacc, self.dev),
+                                      torch.zeros(self.d + 2, dtype=kacc, device=self.dev), state)
+            scratch, fb, state = self._scratch[key]
+            coef = self.coef if self.coef.dtype == kacc else self.coef.to(kacc)
             # one launch: local gradient + fixed-order reduction → [Σ mult·x | rows | 0]
             gk.glm_round(Xk, y.to(kacc).contiguous(), None, coef, n, gk.LOSS_CODES["ftrl"], state, scratch,
                          gk.TAIL_FEEDBACK, fb)
@@ -223,6 +248,8 @@ class FtrlTrainer:
         else:
             ftrl_update_torch(grad, wsum, self.coef, self.z, self.n, self.alpha, self.beta, self.l1, self.l2)
         self.version += 1
+        if self.dev.type == "cuda":
+            return (DeviceDenseVector(self.coef.clone()), self.version)
         return (DenseVector(self.coef.to(torch.float64).cpu().numpy()), self.version)
 
 
@@ -312,7 +339,8 @@ class OnlineLogisticRegressionModel(_OnlineModelMixin, ModelWithData, OnlineLogi
 
     def _predict_batch(self, t: Table) -> Table:
         ver = self._current(block=True)
-        coef = torch.as_tensor(ver[0].values, dtype=torch.float64)
+        coef = (ver[0].device_values() if isinstance(ver[0], DeviceDenseVector)
+                else torch.as_tensor(ver[0].values, dtype=torch.float64))
         X = config.features_for_compute(t, self.get(self.FEATURES_COL))
         if isinstance(X, SparseColumn):
             pred, raw = gk.predict_csr(X.indptr, X.indices, X.values, coef, len(X), gk.MODE_LR)
