@@ -189,9 +189,15 @@ class DeviceGlmTrainer:
         self.feedback = torch.zeros(self.d + 2, dtype=acc, device=dev)
         self.distributed = ctx.is_distributed
         self.xg = None
+        self.csc = None
         if self.sparse:
             self.scratch = None
             self.nparts = 0
+            if dev.type == "cuda" and self.n > 0:
+                self.csc = gk.BatchCsc.build(self.indptr, self.indices, self.values, self.n, self.d, self.B)
+                if self.csc is not None:
+                    self.mult = torch.zeros(max(1, min(self.B, self.n)), dtype=acc, device=dev)
+                    self.wl = torch.zeros(gk.wl_elems(), dtype=acc, device=dev)  # Σw/Σloss slots per parity
         else:
             self.nparts = max(1, min(gk.GRAD_BLOCKS, gk.max_round_blocks(), math.ceil(max(self.B, 1) / (gk.WPB * 16))))
             self.scratch = gk.RoundScratch(self.nparts, self.d, acc, dev)
@@ -207,6 +213,8 @@ class DeviceGlmTrainer:
             self.mode = gk.TAIL_XGMI if self.distributed else gk.TAIL_UPDATE
         if use_graph is None:
             use_graph = os.environ.get("FMLX_HIPGRAPH", "1") == "1"
+        if self.distributed and self.mode == gk.TAIL_FEEDBACK and ctx.backend != "nccl":
+            use_graph = False  # a gloo all-reduce of device tensors cannot be captured
         self.use_graph = use_graph
         self.graphs = {}
         self.check_every = max(1, int(check_every))
@@ -215,6 +223,17 @@ class DeviceGlmTrainer:
     # -- one round as a fixed launch sequence (capturable) -------------------------------------
     def _launch_round(self) -> None:
         s = self.sgd
+        if self.csc is not None:
+            # forward (per-row multipliers) + atomic-free column-major backward; on 1 GPU the
+            # backward applies the update and the termination check itself
+            gk.csc_round(self.csc, self.indptr, self.indices, self.values, self.y, self.w, self.coef, self.n, self.d,
+                         self.B, self.loss, self.state, self.mult, self.wl, self.feedback, not self.distributed,
+                         s.max_iter, s.tol, s.learning_rate, s.reg, s.elastic_net)
+            if self.distributed:
+                comm.all_reduce_sum(self.feedback)
+                gk.update(self.feedback, self.d, self.coef, self.state, s.max_iter, s.tol, s.learning_rate, s.reg,
+                          s.elastic_net)
+            return
         if self.sparse:
             self.feedback.zero_()
             if self.n > 0:
@@ -238,12 +257,15 @@ class DeviceGlmTrainer:
         the same launch sequence repeats); replaying it costs one host submission per ``rounds``."""
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
-        snapshot = (self.state.clone(), self.coef.clone())
+        # everything a round mutates that the next round reads (the sparse path's Σw/Σloss
+        # parity slots included) is rewound after the warm-up
+        live = [self.state, self.coef] + ([self.wl] if self.csc is not None else [])
+        snapshot = [t.clone() for t in live]
         with torch.cuda.stream(side):
             self._launch_round()  # warm-up outside capture (allocator / RCCL lazy init)
         torch.cuda.current_stream(self.device).wait_stream(side)
-        self.state.copy_(snapshot[0])
-        self.coef.copy_(snapshot[1])
+        for t, v in zip(live, snapshot):
+            t.copy_(v)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             for _ in range(rounds):

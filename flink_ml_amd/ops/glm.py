@@ -140,6 +140,80 @@ def grad_csr(indptr, idx, val, y, wt, coef, n, d, B, loss, state, grad) -> None:
                 native.ptr(state), native.ptr(grad), native.stream_ptr(val.device))
 
 
+# sparse rounds through per-batch transposes (csrc/glm.hip glm_csc_bwd_kernel)
+CSC_MAX_BYTES = int(os.environ.get("FMLX_CSC_MAX_BYTES", str(8 << 30)))
+
+
+class BatchCsc:
+    """Per-batch column-major copy of a CSR partition for atomic-free sparse SGD gradients.
+
+    Batch b is the row range [b·B, min((b+1)·B, n)) (the trainer's slicing); its non-zeros keep
+    their CSR positions [indptr[bB], indptr[bB+B]) but are re-ordered by column (stable, so rows
+    stay ascending within a column) and carry the batch-relative row id. ``colptr[b]`` is the
+    dense int32 column pointer of batch b. Costs one extra copy of the partition plus P·(d+1)·4
+    bytes; ``build`` returns None when that exceeds ``CSC_MAX_BYTES`` or a batch has ≥ 2^31
+    non-zeros (the trainer then keeps the atomic scatter kernel).
+    """
+
+    def __init__(self, colptr, erow, evals, G: int):
+        self.colptr, self.erow, self.evals, self.G = colptr, erow, evals, G
+
+    @staticmethod
+    def pick_group(avg_nnz: float) -> int:
+        g = 4
+        while g < 64 and g < avg_nnz / 2:
+            g *= 2
+        return g
+
+    @staticmethod
+    def build(indptr, indices, values, n: int, d: int, B: int):
+        if os.environ.get("FMLX_CSR_TRANSPOSE", "1") == "0" or n <= 0 or B <= 0:
+            return None
+        P = (n + B - 1) // B
+        nnz = int(indptr[-1].item())
+        extra = P * (d + 1) * 4 + nnz * (4 + values.element_size())
+        if extra > CSC_MAX_BYTES:
+            return None
+        dev = values.device
+        bounds = indptr[torch.arange(0, P + 1, device=indptr.device).mul_(B).clamp_(max=n)].tolist()
+        if max(bounds[i + 1] - bounds[i] for i in range(P)) >= 2 ** 31:
+            return None
+        colptr = torch.zeros((P, d + 1), dtype=torch.int32, device=dev)
+        erow = torch.empty(nnz, dtype=torch.int32, device=dev)
+        evals = torch.empty_like(values)
+        for b in range(P):
+            j0, j1 = bounds[b], bounds[b + 1]
+            if j1 == j0:
+                continue
+            r0, r1 = b * B, min((b + 1) * B, n)
+            cols = indices[j0:j1].to(torch.int64)
+            rows = torch.repeat_interleave(torch.arange(r1 - r0, device=dev, dtype=torch.int32),
+                                           (indptr[r0 + 1:r1 + 1] - indptr[r0:r1]).to(torch.int64))
+            order = torch.sort(cols, stable=True).indices
+            erow[j0:j1] = rows[order]
+            evals[j0:j1] = values[j0:j1][order]
+            colptr[b, 1:] = torch.cumsum(torch.bincount(cols, minlength=d), 0).to(torch.int32)
+            del cols, rows, order
+        return BatchCsc(colptr, erow, evals, BatchCsc.pick_group(nnz / max(n, 1)))
+
+
+def wl_elems() -> int:
+    return int(native.kernels().fmlx_glm_wl_elems())
+
+
+def set_csc_tuning(fwd_cap: int = 0, bwd_cap: int = 0) -> None:
+    """Grid caps of the sparse forward / backward kernels (0 = default; A/B knob)."""
+    native.kernels().fmlx_glm_set_csc_tuning(int(fwd_cap), int(bwd_cap))
+
+
+def csc_round(csc: BatchCsc, indptr, idx, val, y, wt, coef, n, d, B, loss, state, mult, wl, fb, fuse: bool,
+              max_iter, tol, lr, reg, en) -> None:
+    native.call("fmlx_glm_csc_round", int(val.dtype == torch.float64), csc.G, native.ptr(indptr), native.ptr(idx),
+                native.ptr(val), native.ptr(y), native.ptr(wt), native.ptr(coef), n, d, B, loss, native.ptr(state),
+                native.ptr(mult), native.ptr(wl), native.ptr(csc.colptr), native.ptr(csc.erow), native.ptr(csc.evals),
+                native.ptr(fb), int(fuse), max_iter, tol, lr, reg, en, native.stream_ptr(val.device))
+
+
 # ---------------------------------------------------------------------------------------------
 # prediction
 # ---------------------------------------------------------------------------------------------

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--batch", type=int, default=100_000, help="per-GPU batch")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--sweep", default="", help="A/B grid caps, e.g. '65535:1024,4096:1024' (fwd:bwd)")
     a = ap.parse_args()
     ctx = init_distributed()
     dev = ctx.device
@@ -44,9 +45,25 @@ def main():
     X = SparseColumn(indptr, idx.reshape(-1), vals, a.dim)
     y = torch.randint(0, 2, (n,), generator=g, device=dev).to(torch.float32)
     world = ctx.world_size
-    sgd = SGD(max_iter=a.steps + a.warmup + 1, learning_rate=0.1, global_batch_size=a.batch * world, tol=0.0)
+    sgd = SGD(max_iter=10 ** 9, learning_rate=0.1, global_batch_size=a.batch * world, tol=0.0)
     tr = DeviceGlmTrainer(sgd, np.zeros(a.dim), X, y, None, "hinge", use_graph=True)
     tr.rounds_per_graph = 5
+    if a.sweep:
+        from flink_ml_amd.ops import glm as gk
+
+        for cfg in a.sweep.split(","):
+            f, b = (int(v) for v in cfg.split(":"))
+            gk.set_csc_tuning(f, b)
+            tr.graphs.clear()
+            tr.run_rounds(a.warmup)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            tr.run_rounds(a.steps)
+            torch.cuda.synchronize()
+            print(json.dumps({"fwd_cap": f, "bwd_cap": b, "us_per_round": round((time.perf_counter() - t0) / a.steps * 1e6, 2)}),
+                  flush=True)
+        gk.set_csc_tuning(0, 0)
+        tr.graphs.clear()
     tr.run_rounds(a.warmup)
     torch.cuda.synchronize()
     comm.barrier()
@@ -55,7 +72,7 @@ def main():
     torch.cuda.synchronize()
     comm.barrier()
     el = comm.all_reduce_scalar(time.perf_counter() - t0, "max")
-    assert tr.rounds_executed() >= a.warmup + a.steps
+    assert tr.running() and tr.rounds_executed() >= a.warmup + a.steps
     if ctx.rank == 0:
         print(json.dumps({"bench": "LinearSVC sparse CSR", "n_gpus": world, "rows_per_gpu": n, "dim": a.dim,
                           "nnz_per_row": k, "per_gpu_batch": a.batch, "us_per_round": round(el / a.steps * 1e6, 2),
