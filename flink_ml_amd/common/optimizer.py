@@ -172,10 +172,6 @@ class DeviceGlmTrainer:
                 X = X.to(torch.float32)
             X = X.contiguous() if X.stride(-1) != 1 else X
             self.layout = gk.pick_layout(X)
-            if self.layout is None:
-                # too wide for the register-resident path: keep the data, densify rows per round in torch
-                raise NotImplementedError("dense d=%d exceeds the register-resident GLM kernel; use a sparse column"
-                                          % X.shape[1])
             self.X = X
             self.n, self.d = int(X.shape[0]), int(X.shape[1])
             acc = torch.float64 if X.dtype == torch.float64 else torch.float32
@@ -190,6 +186,10 @@ class DeviceGlmTrainer:
         self.distributed = ctx.is_distributed
         self.xg = None
         self.csc = None
+        # dense rows the register-resident round kernel cannot hold (wide or misaligned d): two
+        # bandwidth-bound GEMVs per round (X_b·w, then X_bᵀ·m, rocBLAS) + the device update kernel
+        self.wide = not self.sparse and self.layout is None
+        self._host_round = 0
         if self.sparse:
             self.scratch = None
             self.nparts = 0
@@ -198,6 +198,11 @@ class DeviceGlmTrainer:
                 if self.csc is not None:
                     self.mult = torch.zeros(max(1, min(self.B, self.n)), dtype=acc, device=dev)
                     self.wl = torch.zeros(gk.wl_elems(), dtype=acc, device=dev)  # Σw/Σloss slots per parity
+        elif self.wide:
+            self.scratch = None
+            self.nparts = 0
+            if self.w is None:
+                self.w = torch.ones(self.n, dtype=acc, device=dev)
         else:
             self.nparts = max(1, min(gk.GRAD_BLOCKS, gk.max_round_blocks(), math.ceil(max(self.B, 1) / (gk.WPB * 16))))
             self.scratch = gk.RoundScratch(self.nparts, self.d, acc, dev)
@@ -207,12 +212,14 @@ class DeviceGlmTrainer:
                 self.xg = xgmi.get()
                 if self.xg is not None and self.d + 2 > self.xg.glm_max:
                     self.xg = None
-        if self.sparse or self.distributed and self.xg is None:
+        if self.sparse or self.wide or self.distributed and self.xg is None:
             self.mode = gk.TAIL_FEEDBACK  # feedback → RCCL all-reduce → update kernel
         else:
             self.mode = gk.TAIL_XGMI if self.distributed else gk.TAIL_UPDATE
         if use_graph is None:
             use_graph = os.environ.get("FMLX_HIPGRAPH", "1") == "1"
+        if self.wide:
+            use_graph = False  # the batch slice is chosen on the host each round
         if self.distributed and self.mode == gk.TAIL_FEEDBACK and ctx.backend != "nccl":
             use_graph = False  # a gloo all-reduce of device tensors cannot be captured
         self.use_graph = use_graph
@@ -233,6 +240,30 @@ class DeviceGlmTrainer:
                 comm.all_reduce_sum(self.feedback)
                 gk.update(self.feedback, self.d, self.coef, self.state, s.max_iter, s.tol, s.learning_rate, s.reg,
                           s.elastic_net)
+            return
+        if self.wide:
+            # the device state advances once per launch whether or not the round runs, so the
+            # host round counter selects the same batch as the device epoch
+            e = self._host_round
+            self._host_round += 1
+            if self.n > 0:
+                P = -(-self.n // self.B)
+                b0 = (e % P) * self.B
+                b1 = min(b0 + self.B, self.n)
+                xb = self.X[b0:b1]
+                if xb.dtype != self.acc:
+                    xb = xb.to(self.acc)
+                dot = torch.mv(xb, self.coef)
+                l, m = gk.torch_loss_and_mult(self.loss, dot, self.y[b0:b1], self.w[b0:b1])
+                torch.mv(xb.t(), m, out=self.feedback[: self.d])
+                self.feedback[self.d] = self.w[b0:b1].sum()
+                self.feedback[self.d + 1] = l.sum()
+            else:
+                self.feedback.zero_()
+            if self.distributed:
+                comm.all_reduce_sum(self.feedback)
+            gk.update(self.feedback, self.d, self.coef, self.state, s.max_iter, s.tol, s.learning_rate, s.reg,
+                      s.elastic_net)
             return
         if self.sparse:
             self.feedback.zero_()
@@ -316,6 +347,7 @@ class DeviceGlmTrainer:
             done, st = restored
             self.coef.copy_(st["coef"].to(self.coef.dtype))
             self.state.copy_(st["state"])
+            self._host_round = int(self.state[0].item())
             if st["done"]:
                 return self.coef.to(torch.float64).cpu().numpy()
         step = ck.interval if ck.interval else self.check_every

@@ -124,3 +124,26 @@ def test_lr_estimator_on_gpu_goldens():
         m = LogisticRegression().set_weight_col("weight").fit(t)
     coef = m.get_model_data()[0].rows()[0][0].values
     assert np.allclose(coef, [0.525, -0.283, -0.425, -0.567], atol=0.01)
+
+
+@pytest.mark.parametrize("dtype,d", [(torch.float32, 1001), (torch.float32, 3000), (torch.float64, 3000),
+                                     (torch.bfloat16, 5000)])
+def test_device_sgd_wide_dense_gemv_path(dtype, d):
+    """Rows the register-resident round kernel cannot hold run as two GEMVs + the device update."""
+    _need_gpu()
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
+
+    g = torch.Generator(device="cpu").manual_seed(d)
+    n = 1500
+    X = torch.rand((n, d), generator=g, dtype=torch.float64).to(dtype)
+    y = (X.to(torch.float64) @ torch.linspace(-1, 1, d, dtype=torch.float64) > 0).double()
+    w = torch.rand(n, generator=g, dtype=torch.float64) + 0.5
+    for loss in ("logistic", "hinge", "leastsquare"):
+        sgd = SGD(max_iter=7, learning_rate=0.05, global_batch_size=400, tol=1e-9, reg=0.1, elastic_net=0.5)
+        ref = TorchGlmTrainer(sgd, np.zeros(d), X.to(torch.float64), y, w, loss).fit()
+        tr = DeviceGlmTrainer(sgd, np.zeros(d), X.cuda(), y.cuda(), w.cuda(), loss)
+        assert tr.wide
+        got = tr.fit()
+        assert tr.rounds_executed() == 7
+        tol = (1e-10 if dtype == torch.float64 else 1e-4) * max(1.0, np.abs(ref).max())
+        assert np.abs(got - ref).max() < tol, (loss, np.abs(got - ref).max())
