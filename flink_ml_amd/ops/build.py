@@ -47,6 +47,11 @@ def _run(cmd):
     return p.stdout
 
 
+# per-source compiler options. kmeans.hip: MFMA accumulators in arch VGPRs — its epilogue reads
+# every accumulator with VALU ops each tile, and the AGPR form adds a v_accvgpr_read per value.
+FILE_FLAGS = {"kmeans.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
     os.makedirs(LIBDIR, exist_ok=True)
     os.makedirs(OBJDIR, exist_ok=True)
@@ -60,14 +65,14 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
     for s in srcs:
         o = os.path.join(OBJDIR, os.path.basename(s)[:-4] + ".o")
         objs.append(o)
-        if force or not _newer(o, [s] + headers):
+        if force or not _newer(o, [s] + headers + [__file__]):
             todo.append((s, o))
 
     def comp(so):
         s, o = so
         if verbose:
             print("[hipcc] %s" % os.path.basename(s), flush=True)
-        _run([hipcc] + flags + ["-c", s, "-o", o])
+        _run([hipcc] + flags + FILE_FLAGS.get(os.path.basename(s), []) + ["-c", s, "-o", o])
         return o
 
     if todo:

@@ -12,8 +12,11 @@
 //    centroid tiles of 32 are register-staged into a double-buffered, padded (bank-conflict-free)
 //    LDS image shared by the block's 4 waves, so every centroid byte is read once per block
 //    (from L2: C is tiny) while the block streams its 128–256 rows from HBM exactly once.
-//    Epilogue: v = ‖c‖² − 2·x·c (‖x‖² is row-constant), running (v, idx) per accumulator
-//    register, then a 32-lane butterfly (ties → lower index) per row.
+//    The tile is stored pre-scaled by −2 (exact in bf16) and the accumulators start at a
+//    (slightly biased) ‖x‖², so the MFMA yields ‖x‖² − 2·x·c; the epilogue adds ‖c‖² (packed),
+//    inserts the tile number into the low mantissa bits of the now strictly positive distance
+//    and keeps an unsigned min per accumulator register (3 VALU ops per row×centroid pair, was
+//    AGPR read + compare + 2 selects), then a 32-lane butterfly (ties → lower index) per row.
 //  * kmeans_assign_generic<T>: fp32/fp64 (parity) path, one thread per row, centroids in LDS,
 //    exact reference semantics for euclidean (incl. pruning), manhattan and cosine.
 //  * Centroid update without atomics, deterministic: rows are ordered by label (stable sort),
@@ -104,14 +107,46 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t
 #pragma unroll
     for (int s = 0; s < KS; ++s) asm volatile("" ::"v"(a[m][s]));
 
-  float best[MT][16];
-  int bidx[MT][16];
+  // Row norms ‖x‖² (of the bf16 values), biased by 2^-10·‖x‖² so every computed distance is
+  // strictly positive (the fp32 rounding of ‖x‖² + ‖c‖² − 2x·c is ~2^-15·(‖x‖²+‖c‖²) and cancels
+  // only when x ≈ c, i.e. ‖c‖² ≈ ‖x‖²); a per-row constant does not move the argmin. They seed
+  // the MFMA accumulators, so with the tile pre-scaled by −2 the MFMA yields ‖x‖²' − 2x·c.
+  f32x16_t xnb[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    float p = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float f = (float)a[m][s][j];
+        p = __builtin_fmaf(f, f, p);
+      }
+    p += __shfl_xor(p, 32, 64);  // both K-halves of row r32
+    p *= 1.0f + 0x1p-10f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) xnb[m][r] = __shfl(p, (r & 3) + 8 * (r >> 2) + 4 * h, 64);
+  }
+
+  // Running argmin as one u32 key per accumulator register: the positive distance's bits with the
+  // tile number in the low TB mantissa bits (relative quantisation 2^(TB-24)). Unsigned order =
+  // float order for positive values, and on equal distances the lower tile — the lower centroid
+  // index, since the lane is the column — wins: per (row, centroid) the epilogue is one packed add
+  // (+‖c‖²), one bit-insert and one unsigned min (was compare + two selects + AGPR reads).
+  const int ntiles = kpad / 32;
+  int TB = 0;
+  while ((1 << TB) < ntiles) ++TB;
+  const unsigned tmask = (1u << TB) - 1u;
+  // the keep-mask lives in a VGPR: with it in an SGPR next to the SGPR tile number, gfx9's
+  // one-scalar-operand limit splits the v_and_or_b32 into two instructions
+  unsigned vkeep;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(vkeep) : "s"(~tmask));
+  unsigned best[MT][16];
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) { best[m][r] = __builtin_huge_valf(); bidx[m][r] = 0; }
+    for (int r = 0; r < 16; ++r) best[m][r] = 0xFFFFFFFFu;
 
-  const int ntiles = kpad / 32;
   // register-staged tile loader: chunk q of the tile = (row q / (DP/8), 16B piece q % (DP/8)).
   // Loads are unconditional (clamped to the last chunk) so the next tile stays in flight under
   // this tile's MFMAs; the LDS write is the masked part. (Plain code, no lambdas: a captured
@@ -147,24 +182,31 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t
     KM_GLOAD(tn)
     asm volatile("" ::: "memory");
     f32x16_t acc[MT];
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
     const unsigned char* tb = lds + cur * 32 * ROWB + r32 * ROWB + h * 16;
+    bf16x8_t bfr[KS];  // all B fragments in flight before the first MFMA needs one
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(tb + s * 32);
+    for (int s = 0; s < KS; ++s) bfr[s] = *reinterpret_cast<const bf16x8_t*>(tb + s * 32);
 #pragma unroll
-      for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m][s], b, acc[m], 0, 0, 0);
-    }
-    const int col = t * 32 + r32;
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m][s], bfr[s], s == 0 ? xnb[m] : acc[m], 0, 0, 0);
+    // (a software-pipelined variant — tile t's MFMAs interleaved with tile t-1's epilogue on a
+    // second accumulator set — measured slower: 4.46 ms at 256 VGPRs vs 4.02 ms for this loop at
+    // 190 VGPRs; two resident waves per SIMD already overlap one's MFMAs with the other's VALU)
+    const unsigned tt = (unsigned)t;
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float v = cn - 2.f * acc[m][r];
-        if (v < best[m][r]) { best[m][r] = v; bidx[m][r] = col; }
+      for (int r = 0; r < 16; r += 2) {
+        typedef float f32x2_t __attribute__((ext_vector_type(2)));
+        f32x2_t v = {acc[m][r], acc[m][r + 1]};
+        const f32x2_t c2 = {cn, cn};
+        v = v + c2;
+        const unsigned k0 = (__float_as_uint(v[0]) & vkeep) | tt;
+        const unsigned k1 = (__float_as_uint(v[1]) & vkeep) | tt;
+        best[m][r] = k0 < best[m][r] ? k0 : best[m][r];
+        best[m][r + 1] = k1 < best[m][r + 1] ? k1 : best[m][r + 1];
       }
     if (more) {
       KM_SWRITE(cur ^ 1)
@@ -177,19 +219,21 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t
 #undef KM_LD1
 #undef KM_ST1
 
-  // ---- row argmin across the 32 lanes of each half (ties → lower index)
+  // ---- row argmin across the 32 lanes of each half (equal keys → lower column)
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
     int mine = 0;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      float v = best[m][r];
-      int id = bidx[m][r];
+      unsigned v = best[m][r];
+      int id = (int)(v & tmask) * 32 + r32;
 #pragma unroll
       for (int off = 1; off < 32; off <<= 1) {
-        const float ov = __shfl_xor(v, off, 64);
+        const unsigned ov = (unsigned)__shfl_xor((int)v, off, 64);
         const int oi = __shfl_xor(id, off, 64);
-        if (ov < v || (ov == v && oi < id)) { v = ov; id = oi; }
+        const bool take = ov < v || (ov == v && oi < id);
+        v = take ? ov : v;
+        id = take ? oi : id;
       }
       if (r32 == r) mine = id;
     }
@@ -483,8 +527,8 @@ __global__ __launch_bounds__(256) void kmeans_finalize_kernel(const A* __restric
     if (c < D) cent[(long)j * D + c] = v;
     if (Cb) {
       const bf16_t bv = f32_to_bf16((float)v);
-      Cb[(long)j * DP + c] = bv;
       const float fb = bf16_to_f32(bv);
+      Cb[(long)j * DP + c] = f32_to_bf16(-2.f * fb);  // the assign kernel's −2-scaled tile (exact)
       nb += fb * fb;
     }
     na += v * v;

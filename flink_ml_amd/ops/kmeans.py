@@ -68,7 +68,7 @@ class CentroidBuffers:
         self.cnorm.copy_(torch.linalg.vector_norm(c.to(torch.float64), dim=1).to(self.cent.dtype))
         cb = c.to(torch.bfloat16)
         self.Cb.zero_()
-        self.Cb[: self.k, : self.D] = cb
+        self.Cb[: self.k, : self.D] = -2 * cb  # the MFMA assign consumes −2·c (exact in bf16)
         self.cnorm_b.fill_(float("inf"))
         self.cnorm_b[: self.k] = (cb.float() ** 2).sum(1)
 
