@@ -7,6 +7,8 @@ predict is the K3/K13 hot path: for a block of queries, one GEMM gives Q·Tᵀ (
 fp32 by default / fp64 on CPU), ``dist = sqrt(|‖q‖² + ‖t‖² − 2 q·t|)`` exactly as
 ``KnnModel.predictLabel``, then the k nearest (stable: among equal distances the earlier training
 point wins, like the reference's strict-``>`` priority-queue replacement) and a majority vote.
+On the GPU (fp32, k ≤ 16) the distance and the top-k are one HIP kernel (``ops/csrc/knn.hip``)
+that reads the GEMM block once.
 Vote ties go to the tied label that occurs nearest to the query (resolved on the device, only
 for the rows that tie).
 """
@@ -76,6 +78,18 @@ def knn_predict(Q: torch.Tensor, T: torch.Tensor, tnorm: torch.Tensor, labels: t
     classes = torch.unique(labels)
     kk = min(k, T.shape[0])
     out = []
+    if compute == torch.float32:
+        from ..ops import knn as knn_ops
+
+        if kk <= knn_ops.ROUTE_MAX_K and knn_ops.supported(kk, T.shape[0], dev):
+            tn32 = tn.contiguous()
+            qb = knn_ops.query_block(T.shape[0])
+            for s in range(0, Q.shape[0], qb):
+                q = Q[s:s + qb].to(compute)
+                G = torch.mm(q, Tc.t())
+                idx = knn_ops.topk_from_products(G, (q * q).sum(1), tn32, kk)
+                out.append(knn_vote(labels[idx.long()], classes))
+            return torch.cat(out) if out else torch.zeros(0, dtype=torch.float64, device=dev)
     for s in range(0, Q.shape[0], block):
         q = Q[s:s + block].to(compute)
         qn = (q * q).sum(1)

@@ -1,0 +1,107 @@
+"""KNN predict on the GPU: the fused distance + top-k kernel (``ops/csrc/knn.hip``) against a
+plain PyTorch fp64 reference of the same op, and KnnModel end to end against the CPU path."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+
+
+def _ref_topk(G, qn, tn, k):
+    # same fp32 distance expression, ranked in fp64 with a stable sort (ties → lower index)
+    d = torch.sqrt(torch.abs((qn[:, None] + tn[None, :]) - 2.0 * G)).double().cpu()
+    return torch.sort(d, dim=1, stable=True).indices[:, :k], torch.sort(d, dim=1, stable=True).values[:, :k]
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 5, 8, 13, 16, 32])
+@pytest.mark.parametrize("n", [37, 1000, 4099, 20000])
+def test_topk_kernel_matches_torch(k, n):
+    from flink_ml_amd.ops import knn as ko
+
+    if k > n:
+        pytest.skip("k > n")
+    g = torch.Generator(device="cpu").manual_seed(k * 7919 + n)
+    d = 24
+    Q = torch.randn((301, d), generator=g).cuda()
+    T = torch.randn((n, d), generator=g).cuda()
+    G = Q @ T.t()
+    qn, tn = (Q * Q).sum(1), (T * T).sum(1)
+    idx, dist = ko.topk_from_products(G, qn, tn, k, with_dist=True)
+    ridx, rdist = _ref_topk(G, qn, tn, k)
+    torch.testing.assert_close(dist.double().cpu(), rdist, rtol=2e-7, atol=0)
+    # same distances; indices equal wherever the distance is not tied with a neighbour
+    assert (idx.long().cpu() == ridx).float().mean() > 0.999
+
+
+def test_topk_ties_go_to_lower_index():
+    from flink_ml_amd.ops import knn as ko
+
+    g = torch.Generator(device="cpu").manual_seed(3)
+    base = torch.randn((50, 8), generator=g)
+    T = torch.cat([base, base, base]).cuda()          # every point three times: exact ties
+    Q = torch.randn((64, 8), generator=g).cuda()
+    G = Q @ T.t()
+    idx = ko.topk_from_products(G, (Q * Q).sum(1), (T * T).sum(1), 6).long().cpu()
+    ridx, _ = _ref_topk(G, (Q * Q).sum(1), (T * T).sum(1), 6)
+    assert torch.equal(idx, ridx)
+    # each duplicated pair appears in index order
+    assert torch.all(idx[:, 0] < idx[:, 1]) and torch.all(idx[:, 0] % 50 == idx[:, 1] % 50)
+
+
+def test_topk_misaligned_rows_and_nan():
+    from flink_ml_amd.ops import knn as ko
+
+    g = torch.Generator(device="cpu").manual_seed(5)
+    n = 1001                                            # odd n → scalar path
+    Q = torch.randn((40, 5), generator=g).cuda()
+    T = torch.randn((n, 5), generator=g).cuda()
+    G = Q @ T.t()
+    tn = (T * T).sum(1)
+    tn[7] = float("nan")                                # a NaN distance ranks last
+    idx, dist = ko.topk_from_products(G, (Q * Q).sum(1), tn, 4, with_dist=True)
+    assert not torch.any(idx == 7)
+    ridx, rdist = _ref_topk(G, (Q * Q).sum(1), tn.nan_to_num(float("inf")), 4)
+    torch.testing.assert_close(dist.double().cpu(), rdist, rtol=2e-7, atol=0)
+
+
+def test_knn_model_gpu_matches_cpu():
+    from flink_ml_amd import Table
+    from flink_ml_amd.models import Knn
+
+    rng = np.random.default_rng(0)
+    centers = rng.normal(size=(4, 16)) * 4
+    lab = rng.integers(0, 4, 3000)
+    X = centers[lab] + rng.normal(size=(3000, 16))
+    Xq = centers[lab[:500]] + rng.normal(size=(500, 16))
+    train = Table({"features": torch.tensor(X, dtype=torch.float32).cuda(),
+                   "label": torch.tensor(lab, dtype=torch.float64).cuda()})
+    model = Knn().set_k(7).fit(train)
+    pred = model.transform(Table({"features": torch.tensor(Xq, dtype=torch.float32).cuda()}))[0]
+    p_gpu = pred.column("prediction").cpu().numpy()
+    # fp64 host reference of the same predictor
+    d = np.sqrt(np.abs((Xq ** 2).sum(1)[:, None] + (X ** 2).sum(1)[None, :] - 2 * Xq @ X.T))
+    nn = np.argsort(d, axis=1, kind="stable")[:, :7]
+    votes = np.array([np.bincount(lab[r], minlength=4).argmax() for r in nn])
+    assert (p_gpu == votes).mean() > 0.99
+
+
+@pytest.mark.parametrize("nq,n,k", [(3, 50000, 5), (700, 9000, 32), (64, 200003, 7)])
+def test_topk_segmented_merge(nq, n, k):
+    from flink_ml_amd.ops import knn as ko
+
+    assert ko.segments(nq, n) > 1 or n < 2 * ko.MIN_SEGMENT
+    g = torch.Generator(device="cpu").manual_seed(nq + n)
+    Q = torch.randn((nq, 6), generator=g).cuda()
+    T = torch.randn((n, 6), generator=g).cuda()
+    G = Q @ T.t()
+    qn, tn = (Q * Q).sum(1), (T * T).sum(1)
+    idx, dist = ko.topk_from_products(G, qn, tn, k, with_dist=True)
+    ridx, rdist = _ref_topk(G, qn, tn, k)
+    torch.testing.assert_close(dist.double().cpu(), rdist, rtol=2e-7, atol=0)
+    assert (idx.long().cpu() == ridx).float().mean() > 0.999
