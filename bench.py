@@ -108,7 +108,7 @@ def main():
     value = samples / elapsed
     if rank == 0:
         rec = {
-            "metric": "samples/sec (whole node), LogisticRegression 10M×1K dense",
+            "metric": "samples/sec (whole node), LogisticRegression 10M\u00d71K dense at 1/2/4/8 MI355X",
             "value": round(value, 1),
             "unit": "samples/s",
             "n_gpus": world,
