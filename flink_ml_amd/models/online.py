@@ -198,8 +198,8 @@ class FtrlTrainer:
     def local_gradient(self, batch: Table):
         X = config.features_for_compute(batch, self.fcol)
         y = batch.scalars(self.lcol, dtype=self.acc, device=self.dev)
-        payload = torch.zeros(2 * self.d, dtype=self.acc, device=self.dev)
         if isinstance(X, SparseColumn):
+            payload = torch.zeros(2 * self.d, dtype=self.acc, device=self.dev)
             w = batch.scalars(self.wcol, dtype=self.acc, device=self.dev) if self.wcol and batch.has_column(
                 self.wcol) else torch.ones(len(X), dtype=self.acc, device=self.dev)
             counts = X.indptr[1:] - X.indptr[:-1]
@@ -213,7 +213,7 @@ class FtrlTrainer:
             return payload
         n = X.shape[0]
         if n == 0:
-            return payload
+            return torch.zeros(2 * self.d, dtype=self.acc, device=self.dev)
         if self.dev.type == "cuda" and gk.pick_layout(X) is not None:
             Xk = X if X.dtype in (torch.float32, torch.float64, torch.bfloat16) else X.to(self.acc)
             kacc = torch.float64 if Xk.dtype == torch.float64 else torch.float32
@@ -229,11 +229,15 @@ class FtrlTrainer:
             # one launch: local gradient + fixed-order reduction → [Σ mult·x | rows | 0]
             gk.glm_round(Xk, y.to(kacc).contiguous(), None, coef, n, gk.LOSS_CODES["ftrl"], state, scratch,
                          gk.TAIL_FEEDBACK, fb)
-            payload[: self.d] = fb[: self.d].to(self.acc)
-            payload[self.d:] = fb[self.d].to(self.acc)
-            return payload
+            pay = self._scratch.get("payload")
+            if pay is None:
+                pay = self._scratch["payload"] = torch.empty(2 * self.d, dtype=self.acc, device=self.dev)
+            pay[: self.d].copy_(fb[: self.d])
+            pay[self.d:].copy_(fb[self.d].expand(self.d))
+            return pay
         Xf = X.to(self.acc)
         mult = torch.sigmoid(Xf @ self.coef) - y
+        payload = torch.empty(2 * self.d, dtype=self.acc, device=self.dev)
         payload[: self.d] = mult @ Xf
         payload[self.d:] = float(n)
         return payload

@@ -104,6 +104,15 @@ class SparseColumn:
         return SparseColumn(torch.cat(ptrs), torch.cat([p.indices.to(dev) for p in parts]),
                             torch.cat([p.values.to(dev) for p in parts]), max(p.size for p in parts))
 
+    def slice(self, start: int, end: int) -> "SparseColumn":
+        """Rows [start, end) without copying: views of indices/values and a rebased indptr."""
+        n = len(self)
+        start, end = max(0, min(start, n)), max(0, min(end, n))
+        end = max(end, start)
+        bounds = self.indptr[[start, end]].cpu()
+        s, e = int(bounds[0]), int(bounds[1])
+        return SparseColumn(self.indptr[start:end + 1] - s, self.indices[s:e], self.values[s:e], self.size)
+
     def take(self, idx: torch.Tensor) -> "SparseColumn":
         idx = idx.cpu().long()
         vecs = [self.row(int(i)) for i in idx]
@@ -342,7 +351,17 @@ class Table:
         return Table(cols, num_rows=int(idx_t.shape[0]), time_col=self.time_col)
 
     def slice(self, start: int, end: int) -> "Table":
-        return self.take(torch.arange(start, min(end, self._n)))
+        """Rows [start, end): tensor columns are views (no gather, no HBM traffic), so streaming a
+        device-resident table in mini-batches costs nothing per batch."""
+        start = max(0, min(start, self._n))
+        end = max(start, min(end, self._n))
+        cols = {}
+        for k, c in self._cols.items():
+            if isinstance(c, (torch.Tensor, SparseColumn)):
+                cols[k] = c[start:end] if isinstance(c, torch.Tensor) else c.slice(start, end)
+            else:
+                cols[k] = c[start:end]
+        return Table(cols, num_rows=end - start, time_col=self.time_col)
 
     def filter(self, mask) -> "Table":
         return self.take(torch.as_tensor(mask, dtype=torch.bool))
