@@ -21,7 +21,7 @@ from ..linalg.vectors import DenseVector
 from ..ops.datagen import java_rows
 from ..param.param import IntParam, LongParam, ParamValidators, StringArrayArrayParam, WithParams
 from ..parallel.context import get_context
-from ..table import Table
+from ..table import StringArrayColumn, Table
 from ..utils.java import _i32, java_long_hash
 
 _PKG = "org.apache.flink.ml.benchmark.datagenerator."
@@ -163,10 +163,11 @@ class RandomStringArrayGenerator(InputDataGenerator, HasNumDistinctValues, HasAr
         names = self.get(self.COL_NAMES)
         k, a = len(names[0]), self.get(self.ARRAY_SIZE)
         _, sc = self._rows([self.get(self.NUM_DISTINCT_VALUES)] * (k * a), 0)
-        codes = sc.cpu().numpy().astype(np.int64).reshape(-1, k, a)
+        codes = sc.reshape(sc.shape[0], k, a)
         vocab = [str(i) for i in range(self.get(self.NUM_DISTINCT_VALUES))]
-        return [Table({c: [[vocab[x] for x in row] for row in codes[:, i, :]] for i, c in enumerate(names[0])},
-                      num_rows=codes.shape[0])]
+        # dictionary-encoded, device-resident string arrays (rows materialise as lists on demand)
+        return [Table({c: StringArrayColumn.from_dense_codes(codes[:, i, :].contiguous(), vocab)
+                       for i, c in enumerate(names[0])}, num_rows=codes.shape[0])]
 
 
 @rw.register_stage

@@ -28,7 +28,7 @@ from ...linalg.vectors import DenseVector, SparseVector, Vector
 from ...ops import hashing
 from ...param.param import (BooleanParam, FloatParam, IntParam, ParamValidators, StringArrayParam, StringParam)
 from ...parallel import comm
-from ...table import SparseColumn, Table
+from ...table import SparseColumn, StringArrayColumn, Table
 from ...utils.java import java_hashmap_order as _java_hashmap_order
 from ...utils.java import java_number_to_string, java_string_hash
 from ..base import ModelWithData
@@ -75,6 +75,24 @@ def java_hashmap_order(keys: Sequence[str]) -> List[str]:
 
 def _strings_col(t: Table, col: str) -> list:
     return t.get_list(col)
+
+
+def _dict_col(t: Table, col: str):
+    """The column as a dictionary-encoded ``StringArrayColumn`` on the compute device (codes stay
+    in HBM), or None when it is a plain list column (the per-row host path then applies)."""
+    c = t.column(col)
+    if isinstance(c, StringArrayColumn) and len(c) > 0:
+        return c.to(config.compute_device()).rebased()
+    return None
+
+
+def _count_csr(rows: torch.Tensor, idx: torch.Tensor, n: int, width: int):
+    """Per-row term counts of (row, index) pairs as one sort-unique → (indptr, indices, counts)."""
+    keys, cnt = torch.unique(rows * width + idx, return_counts=True)
+    r = torch.div(keys, width, rounding_mode="floor")
+    indptr = torch.zeros(n + 1, dtype=torch.int64, device=rows.device)
+    indptr[1:] = torch.cumsum(torch.bincount(r, minlength=n), 0)
+    return indptr, (keys - r * width), cnt, r
 
 
 # ------------------------------------------------------------------------------------ Tokenizer
@@ -184,6 +202,17 @@ class StopWordsRemover(Transformer, HasInputCols, HasOutputCols):
         sw = set(self.get(self.STOP_WORDS)) if cs else {w.lower() for w in self.get(self.STOP_WORDS)}
         res = {}
         for c, o in zip(ins, outs):
+            dc = _dict_col(t, c)
+            if dc is not None:
+                # filter the codes on the device: one vocabulary-sized keep mask, a gather and a
+                # prefix sum for the new row offsets
+                keep = torch.tensor([(w if cs else (w.lower() if w is not None else w)) not in sw for w in dc.vocab],
+                                    dtype=torch.bool, device=dc.device)
+                m = keep[dc.codes.long()]
+                csum = torch.zeros(m.shape[0] + 1, dtype=torch.int64, device=dc.device)
+                csum[1:] = torch.cumsum(m, 0)
+                res[o] = StringArrayColumn(csum[dc.offsets], dc.codes[m], dc.vocab)
+                continue
             res[o] = [[w for w in toks if (w if cs else (w.lower() if w is not None else w)) not in sw]
                       for toks in _strings_col(t, c)]
         return [t.with_columns(res)]
@@ -198,6 +227,14 @@ class HashingTF(Transformer, HasInputCol, HasOutputCol, HasNumFeatures):
     def transform(self, *inputs):
         t = inputs[0]
         nf, binary = self.get(self.NUM_FEATURES), self.get(self.BINARY)
+        dc = _dict_col(t, self.get(self.INPUT_COL))
+        if dc is not None and all(isinstance(w, str) for w in dc.vocab):
+            # hash each distinct string once, then gather the buckets by code on the device
+            vb = hashing.non_negative_mod(hashing.hash_strings(dc.vocab), nf).astype(np.int64)
+            idx = torch.from_numpy(vb).to(dc.device)[dc.codes.long()]
+            indptr, ind, cnt, _ = _count_csr(dc.row_ids(), idx, len(dc), nf)
+            vals = torch.ones_like(cnt, dtype=torch.float64) if binary else cnt.to(torch.float64)
+            return [t.with_column(self.get(self.OUTPUT_COL), SparseColumn(indptr, ind.to(torch.int32), vals, nf))]
         docs = _strings_col(t, self.get(self.INPUT_COL))
         flat, lens = [], []
         for d in docs:
@@ -347,6 +384,23 @@ class CountVectorizerModel(ModelWithData, CountVectorizerModelParams):
         vocab = self.model_data_rows()[0][0]
         index = {w: i for i, w in enumerate(vocab)}
         min_tf, binary = self.get(self.MIN_TF), self.get(self.BINARY)
+        dc = _dict_col(t, self.get(self.INPUT_COL))
+        if dc is not None:
+            vmap = torch.tensor([index.get(w, -1) for w in dc.vocab], dtype=torch.int64, device=dc.device)
+            mi = vmap[dc.codes.long()]
+            ok = mi >= 0
+            n = len(dc)
+            indptr, ind, cnt, r = _count_csr(dc.row_ids()[ok], mi[ok], n, max(1, len(vocab)))
+            thr = (torch.full_like(cnt, 0, dtype=torch.float64) + min_tf if min_tf >= 1.0
+                   else dc.row_lengths().to(torch.float64)[r] * min_tf)
+            keep = cnt.to(torch.float64) >= thr
+            if not bool(keep.all()):
+                r, ind, cnt = r[keep], ind[keep], cnt[keep]
+                indptr = torch.zeros(n + 1, dtype=torch.int64, device=dc.device)
+                indptr[1:] = torch.cumsum(torch.bincount(r, minlength=n), 0)
+            vals = torch.ones_like(cnt, dtype=torch.float64) if binary else cnt.to(torch.float64)
+            col = SparseColumn(indptr, ind.to(torch.int32), vals, len(vocab))
+            return [t.with_column(self.get(self.OUTPUT_COL), col)]
         out = []
         for doc in _strings_col(t, self.get(self.INPUT_COL)):
             cnt = Counter(index[w] for w in doc if w in index)
@@ -361,16 +415,36 @@ class CountVectorizer(Estimator, CountVectorizerParams):
     JAVA_CLASS_NAME = "org.apache.flink.ml.feature.countvectorizer.CountVectorizer"
 
     def fit(self, *inputs):
-        docs = _strings_col(inputs[0], self.get(self.INPUT_COL))
-        order, tf, df = [], {}, {}
-        for doc in docs:
-            for w, c in Counter(doc).items():
-                if w not in tf:
-                    order.append(w)
-                    tf[w], df[w] = 0, 0
-                tf[w] += c
-                df[w] += 1
-        parts = comm.all_gather_object((len(docs), order, tf, df))
+        dc = _dict_col(inputs[0], self.get(self.INPUT_COL))
+        if dc is not None and len(set(dc.vocab)) == len(dc.vocab):
+            # term and document frequencies per distinct string from the codes on the device; the
+            # first-occurrence order (it decides HashMap bucket-collision order) via a scatter-min
+            V = len(dc.vocab)
+            codes = dc.codes.long()
+            tf_t = torch.bincount(codes, minlength=V)
+            pairs = torch.unique(dc.row_ids() * V + codes)
+            df_t = torch.bincount(pairs % V, minlength=V)
+            first = torch.full((V,), codes.shape[0], dtype=torch.int64, device=codes.device)
+            first.scatter_reduce_(0, codes, torch.arange(codes.shape[0], device=codes.device), reduce="amin")
+            present = torch.nonzero(tf_t > 0).reshape(-1)
+            present = present[torch.argsort(first[present], stable=True)].cpu().tolist()
+            tf_h, df_h = tf_t.cpu().tolist(), df_t.cpu().tolist()
+            order = [dc.vocab[c] for c in present]
+            tf = {dc.vocab[c]: tf_h[c] for c in present}
+            df = {dc.vocab[c]: df_h[c] for c in present}
+            ndocs = len(dc)
+        else:
+            docs = _strings_col(inputs[0], self.get(self.INPUT_COL))
+            order, tf, df = [], {}, {}
+            for doc in docs:
+                for w, c in Counter(doc).items():
+                    if w not in tf:
+                        order.append(w)
+                        tf[w], df[w] = 0, 0
+                    tf[w] += c
+                    df[w] += 1
+            ndocs = len(docs)
+        parts = comm.all_gather_object((ndocs, order, tf, df))
         rows = sum(p[0] for p in parts)
         if rows == 0:
             raise RuntimeError("The training set is empty.")

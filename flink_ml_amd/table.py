@@ -119,7 +119,95 @@ class SparseColumn:
         return SparseColumn.from_vectors(vecs, self.size)
 
 
-Column = Any  # torch.Tensor | SparseColumn | list
+class StringArrayColumn:
+    """Ragged arrays of dictionary-encoded strings: row i is
+    ``[vocab[c] for c in codes[offsets[i]:offsets[i + 1]]]``.
+
+    ``offsets``/``codes`` are tensors (HBM-resident on the GPU), ``vocab`` a host list of the
+    distinct strings. String-array stages (StopWordsRemover, CountVectorizer, HashingTF) work on
+    the codes with device kernels; everything else sees a sequence of Python lists (rows are
+    materialised on demand), so the column is a drop-in for a list-of-lists column.
+    """
+
+    __slots__ = ("offsets", "codes", "vocab")
+
+    def __init__(self, offsets: torch.Tensor, codes: torch.Tensor, vocab: Sequence[Optional[str]]):
+        self.offsets = offsets
+        self.codes = codes
+        self.vocab = list(vocab)
+
+    @staticmethod
+    def from_dense_codes(codes: torch.Tensor, vocab) -> "StringArrayColumn":
+        """[n, a] code matrix (every row holds a strings)."""
+        n, a = codes.shape
+        off = torch.arange(0, (n + 1) * a, a, dtype=torch.int64, device=codes.device)[: n + 1]
+        return StringArrayColumn(off, codes.reshape(-1).to(torch.int32), vocab)
+
+    @staticmethod
+    def from_lists(rows: Sequence[Sequence[Optional[str]]]) -> "StringArrayColumn":
+        index, vocab, codes, off = {}, [], [], [0]
+        for r in rows:
+            for w in r:
+                c = index.get(w)
+                if c is None:
+                    c = index[w] = len(vocab)
+                    vocab.append(w)
+                codes.append(c)
+            off.append(len(codes))
+        return StringArrayColumn(torch.tensor(off, dtype=torch.int64), torch.tensor(codes, dtype=torch.int32), vocab)
+
+    def __len__(self):
+        return int(self.offsets.shape[0]) - 1
+
+    @property
+    def device(self):
+        return self.codes.device
+
+    def row_lengths(self) -> torch.Tensor:
+        return self.offsets[1:] - self.offsets[:-1]
+
+    def row_ids(self) -> torch.Tensor:
+        """Row index of every code (int64, on the codes' device)."""
+        n = len(self)
+        return torch.repeat_interleave(torch.arange(n, device=self.codes.device), self.row_lengths().to(self.codes.device),
+                                       output_size=int(self.codes.shape[0]))
+
+    def to(self, device=None) -> "StringArrayColumn":
+        if device is None:
+            return self
+        return StringArrayColumn(self.offsets.to(device), self.codes.to(device), self.vocab)
+
+    def to_lists(self) -> List[List[Optional[str]]]:
+        off = self.offsets.cpu().numpy()
+        words = np.empty(len(self.vocab), dtype=object)
+        words[:] = self.vocab
+        flat = words[self.codes.cpu().numpy().astype(np.int64)].tolist()
+        return [flat[off[i] - off[0]:off[i + 1] - off[0]] for i in range(len(self))]
+
+    def __iter__(self):
+        return iter(self.to_lists())
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            start, stop, step = i.indices(len(self))
+            if step != 1:
+                return self.to_lists()[i]
+            stop = max(stop, start)
+            b = self.offsets[[start, stop]].cpu()
+            return StringArrayColumn(self.offsets[start:stop + 1], self.codes[int(b[0]):int(b[1])], self.vocab)
+        i = int(i)
+        if i < 0:
+            i += len(self)
+        b = self.offsets[[i, i + 1]].cpu()
+        return [self.vocab[c] for c in self.codes[int(b[0]):int(b[1])].cpu().tolist()]
+
+    def rebased(self) -> "StringArrayColumn":
+        """The same rows with offsets starting at 0 (slices keep the parent's offsets)."""
+        o0 = self.offsets[:1]
+        return StringArrayColumn(self.offsets - o0, self.codes, self.vocab)
+
+
+Column = Any  # torch.Tensor | SparseColumn | StringArrayColumn | list
 
 
 def _col_len(col) -> int:
@@ -249,6 +337,8 @@ class Table:
         col = self.column(name)
         if isinstance(col, list):
             return col
+        if isinstance(col, StringArrayColumn):
+            return col.to_lists()
         return [_row_value(col, i) for i in range(self._n)]
 
     def rows(self) -> List[tuple]:
@@ -346,6 +436,9 @@ class Table:
                 cols[k] = c[idx_t.to(c.device)]
             elif isinstance(c, SparseColumn):
                 cols[k] = c.take(idx_t)
+            elif isinstance(c, StringArrayColumn):
+                lists = c.to_lists()
+                cols[k] = [lists[int(i)] for i in idx_t]
             else:
                 cols[k] = [c[int(i)] for i in idx_t]
         return Table(cols, num_rows=int(idx_t.shape[0]), time_col=self.time_col)
@@ -369,7 +462,7 @@ class Table:
     def to(self, device) -> "Table":
         cols = {}
         for k, c in self._cols.items():
-            if isinstance(c, (torch.Tensor, SparseColumn)):
+            if isinstance(c, (torch.Tensor, SparseColumn, StringArrayColumn)):
                 cols[k] = c.to(device)
             else:
                 cols[k] = c

@@ -1,0 +1,81 @@
+"""Dictionary-encoded string-array columns (``StringArrayColumn``): the device fast paths of the
+string-array stages must give exactly what the per-row host path gives on the same rows as plain
+lists (StopWordsRemover.java, HashingTF.java, CountVectorizer(Model).java semantics)."""
+import numpy as np
+import torch
+
+from flink_ml_amd import Table
+from flink_ml_amd.lib.feature.countvectorizer import CountVectorizer
+from flink_ml_amd.lib.feature.hashingtf import HashingTF
+from flink_ml_amd.lib.feature.stopwordsremover import StopWordsRemover
+from flink_ml_amd.table import StringArrayColumn
+
+ROWS = [["The", "a", "quick", "fox"], [], ["fox", "fox", "The", "zebra", "a"], ["b", "quick"],
+        ["a", "a", "a"], ["x", "y", "b", "fox", "quick", "quick"]]
+
+
+def _both():
+    return Table({"input": [list(r) for r in ROWS]}), Table({"input": StringArrayColumn.from_lists(ROWS)})
+
+
+def _dense(col, n):
+    return [v.to_array().tolist() for v in Table({"c": col}, num_rows=n).get_list("c")]
+
+
+def test_column_behaves_like_list_of_lists():
+    c = StringArrayColumn.from_lists(ROWS)
+    assert len(c) == len(ROWS)
+    assert c.to_lists() == ROWS
+    assert c[2] == ROWS[2] and c[-1] == ROWS[-1]
+    assert c[1:4].to_lists() == ROWS[1:4]
+    t = Table({"input": c, "id": torch.arange(len(ROWS))})
+    assert t.slice(2, 5).get_list("input") == ROWS[2:5]
+    assert t.take(torch.tensor([5, 0])).get_list("input") == [ROWS[5], ROWS[0]]
+    assert Table.concat([t.slice(0, 2), t.slice(2, 6)]).get_list("input") == ROWS
+    dense = StringArrayColumn.from_dense_codes(torch.tensor([[0, 1], [1, 1]]), ["u", "v"])
+    assert dense.to_lists() == [["u", "v"], ["v", "v"]]
+
+
+def test_stopwords_remover_matches_host_path():
+    tl, tc = _both()
+    for cs in (False, True):
+        st = StopWordsRemover().set_input_cols("input").set_output_cols("output").set_case_sensitive(cs)
+        assert st.transform(tc)[0].get_list("output") == st.transform(tl)[0].get_list("output")
+    # a slice (offsets not starting at 0) goes through the same path
+    st = StopWordsRemover().set_input_cols("input").set_output_cols("output")
+    assert st.transform(tc.slice(2, 6))[0].get_list("output") == st.transform(tl.slice(2, 6))[0].get_list("output")
+
+
+def test_hashingtf_matches_host_path():
+    tl, tc = _both()
+    for binary in (False, True):
+        h = HashingTF().set_num_features(64).set_binary(binary)
+        a = h.transform(tl)[0].get_list("output")
+        b = h.transform(tc)[0].get_list("output")
+        assert [(v.indices.tolist(), v.values.tolist()) for v in a] == [(v.indices.tolist(), v.values.tolist()) for v in b]
+
+
+def test_countvectorizer_fit_and_transform_match_host_path():
+    tl, tc = _both()
+    for min_tf, binary in ((1.0, False), (2.0, False), (0.3, True)):
+        cv = CountVectorizer().set_min_tf(min_tf).set_binary(binary)
+        ml, mc = cv.fit(tl), cv.fit(tc)
+        vl = ml.get_model_data()[0].get_list("vocabulary")
+        assert vl == mc.get_model_data()[0].get_list("vocabulary")
+        a = ml.transform(tl)[0].get_list("output")
+        b = mc.transform(tc)[0].get_list("output")
+        assert [(v.size(), v.indices.tolist(), v.values.tolist()) for v in a] == \
+               [(v.size(), v.indices.tolist(), v.values.tolist()) for v in b]
+
+
+def test_generator_emits_dictionary_encoded_arrays():
+    from flink_ml_amd.bench.generators import RandomStringArrayGenerator
+
+    g = RandomStringArrayGenerator().set_col_names([["input"]]).set_num_values(50).set_array_size(7) \
+        .set_num_distinct_values(10).set_seed(2)
+    t = g.get_data()[0]
+    col = t.column("input")
+    assert isinstance(col, StringArrayColumn)
+    rows = t.get_list("input")
+    assert len(rows) == 50 and all(len(r) == 7 for r in rows)
+    assert set(np.concatenate(rows)) <= {str(i) for i in range(10)}
