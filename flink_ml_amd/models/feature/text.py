@@ -135,6 +135,32 @@ class NGram(Transformer, HasInputCol, HasOutputCol):
     def transform(self, *inputs):
         t = inputs[0]
         n = self.get(self.N)
+        dc = _dict_col(t, self.get(self.INPUT_COL))
+        V = len(dc.vocab) if dc is not None else 0
+        if dc is not None and all(isinstance(w, str) for w in dc.vocab) and V > 0 and (V + 1) ** n < (1 << 62):
+            # grams as base-V integers over consecutive codes of a row, dictionary-encoded again;
+            # only the distinct grams are joined into strings on the host
+            codes = dc.codes.long()
+            N = codes.shape[0]
+            pos = torch.arange(N, device=codes.device)
+            rid = dc.row_ids()
+            valid = (pos - dc.offsets[rid] + n) <= dc.offsets[rid + 1] - dc.offsets[rid]
+            gram = torch.zeros(N, dtype=torch.int64, device=codes.device)
+            for j in range(n):
+                shifted = torch.zeros_like(codes)
+                shifted[: N - j] = codes[j:]
+                gram = gram * V + shifted
+            uniq, inv = torch.unique(gram[valid], return_inverse=True)
+            digits, u = [], uniq.cpu().numpy()
+            for _ in range(n):
+                digits.append(u % V)
+                u = u // V
+            words = dc.vocab
+            vocab = [" ".join(words[digits[n - 1 - j][i]] for j in range(n)) for i in range(len(uniq))]
+            csum = torch.zeros(N + 1, dtype=torch.int64, device=codes.device)
+            csum[1:] = torch.cumsum(valid, 0)
+            out = StringArrayColumn(csum[dc.offsets], inv.to(torch.int32), vocab)
+            return [t.with_column(self.get(self.OUTPUT_COL), out)]
         out = [[" ".join(toks[i:i + n]) for i in range(len(toks) - n + 1)]
                for toks in _strings_col(t, self.get(self.INPUT_COL))]
         return [t.with_column(self.get(self.OUTPUT_COL), out)]
@@ -421,12 +447,26 @@ class CountVectorizer(Estimator, CountVectorizerParams):
             # first-occurrence order (it decides HashMap bucket-collision order) via a scatter-min
             V = len(dc.vocab)
             codes = dc.codes.long()
+            N, nd = codes.shape[0], len(dc)
             tf_t = torch.bincount(codes, minlength=V)
-            pairs = torch.unique(dc.row_ids() * V + codes)
-            df_t = torch.bincount(pairs % V, minlength=V)
-            first = torch.full((V,), codes.shape[0], dtype=torch.int64, device=codes.device)
-            first.scatter_reduce_(0, codes, torch.arange(codes.shape[0], device=codes.device), reduce="amin")
+            if nd * V <= (1 << 32):  # (doc, term) presence bitmap: a scatter instead of a sort
+                pres = torch.zeros(nd * V, dtype=torch.bool, device=codes.device)
+                pres[dc.row_ids() * V + codes] = True
+                df_t = pres.view(nd, V).sum(0)
+                del pres
+            else:
+                df_t = torch.bincount(torch.unique(dc.row_ids() * V + codes) % V, minlength=V)
             present = torch.nonzero(tf_t > 0).reshape(-1)
+            # first occurrences over a geometrically growing prefix: every term usually shows up
+            # early, so the scatter-min does not run over (and contend on) all N codes
+            first = torch.full((V,), N, dtype=torch.int64, device=codes.device)
+            s0, step = 0, 1 << 20
+            while s0 < N:
+                e0 = min(N, s0 + step)
+                first.scatter_reduce_(0, codes[s0:e0], torch.arange(s0, e0, device=codes.device), reduce="amin")
+                if not bool((first[present] == N).any()):
+                    break
+                s0, step = e0, step * 4
             present = present[torch.argsort(first[present], stable=True)].cpu().tolist()
             tf_h, df_h = tf_t.cpu().tolist(), df_t.cpu().tolist()
             order = [dc.vocab[c] for c in present]

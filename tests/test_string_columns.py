@@ -79,3 +79,16 @@ def test_generator_emits_dictionary_encoded_arrays():
     rows = t.get_list("input")
     assert len(rows) == 50 and all(len(r) == 7 for r in rows)
     assert set(np.concatenate(rows)) <= {str(i) for i in range(10)}
+
+
+def test_ngram_matches_host_path():
+    from flink_ml_amd.lib.feature.ngram import NGram
+
+    tl, tc = _both()
+    for n in (1, 2, 3, 5):
+        ng = NGram().set_n(n)
+        got = ng.transform(tc)[0]
+        assert isinstance(got.column("output"), StringArrayColumn)
+        assert got.get_list("output") == ng.transform(tl)[0].get_list("output")
+    ng = NGram().set_n(2)
+    assert ng.transform(tc.slice(1, 5))[0].get_list("output") == ng.transform(tl.slice(1, 5))[0].get_list("output")
