@@ -21,7 +21,7 @@ from ..linalg.vectors import DenseVector
 from ..ops.datagen import java_rows
 from ..param.param import IntParam, LongParam, ParamValidators, StringArrayArrayParam, WithParams
 from ..parallel.context import get_context
-from ..table import StringArrayColumn, Table
+from ..table import StringArrayColumn, StringColumn, Table
 from ..utils.java import _i32, java_long_hash
 
 _PKG = "org.apache.flink.ml.benchmark.datagenerator."
@@ -150,9 +150,10 @@ class RandomStringGenerator(InputDataGenerator, HasNumDistinctValues):
         names = self.get(self.COL_NAMES)
         k = len(names[0])
         _, sc = self._rows([self.get(self.NUM_DISTINCT_VALUES)] * k, 0)
-        codes = sc.cpu().numpy().astype(np.int64)
         vocab = [str(i) for i in range(self.get(self.NUM_DISTINCT_VALUES))]
-        return [Table({c: [vocab[x] for x in codes[:, i]] for i, c in enumerate(names[0])}, num_rows=codes.shape[0])]
+        # dictionary-encoded, device-resident strings (rows materialise as str on demand)
+        return [Table({c: StringColumn(sc[:, i].contiguous().to(torch.int32), vocab) for i, c in enumerate(names[0])},
+                      num_rows=sc.shape[0])]
 
 
 @rw.register_stage

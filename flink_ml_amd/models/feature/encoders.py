@@ -34,7 +34,7 @@ from ...linalg.vectors import DenseVector, SparseVector, Vector
 from ...ops import features as fo
 from ...param.param import BooleanParam, FloatParam, IntParam, ParamValidators, StringParam
 from ...parallel import comm
-from ...table import SparseColumn, Table
+from ...table import SparseColumn, StringColumn, Table, first_occurrence
 from ...utils.java import (java_double_hash, java_hashmap_order, java_int_hash, java_number_to_string,
                            java_string_hash)
 from ..base import ModelWithData
@@ -49,6 +49,21 @@ def _dev():
 
 def _numeric_col(t: Table, col: str) -> torch.Tensor:
     c = t.column(col)
+    if isinstance(c, StringColumn) and len(c) > 0:
+        if any(not isinstance(w, str) for w in c.vocab):
+            raise RuntimeError("The input column only supports string and numeric type.")
+        # counts per distinct string by code on the device, in first-seen order
+        codes = c.codes.to(config.compute_device()).long()
+        V = len(c.vocab)
+        cnt = torch.bincount(codes, minlength=V)
+        first = first_occurrence(codes, V)
+        present = torch.nonzero(cnt > 0).reshape(-1)
+        order = present[torch.argsort(first[present], stable=True)].cpu().tolist()
+        cnt_h = cnt.cpu().tolist()
+        out: Dict[str, int] = {}
+        for i in order:
+            out[c.vocab[i]] = out.get(c.vocab[i], 0) + int(cnt_h[i])
+        return out
     if isinstance(c, torch.Tensor):
         if c.dim() != 1:
             raise ValueError("Column %s is not a scalar column" % col)
@@ -177,6 +192,21 @@ def _java_str_key(s: str) -> bytes:
 def _string_counts(t: Table, col: str) -> Dict[str, int]:
     """Per-rank ``Map<String, Long>`` of a column in first-seen order (numbers via String.valueOf)."""
     c = t.column(col)
+    if isinstance(c, StringColumn) and len(c) > 0:
+        if any(not isinstance(w, str) for w in c.vocab):
+            raise RuntimeError("The input column only supports string and numeric type.")
+        # counts per distinct string by code on the device, in first-seen order
+        codes = c.codes.to(config.compute_device()).long()
+        V = len(c.vocab)
+        cnt = torch.bincount(codes, minlength=V)
+        first = first_occurrence(codes, V)
+        present = torch.nonzero(cnt > 0).reshape(-1)
+        order = present[torch.argsort(first[present], stable=True)].cpu().tolist()
+        cnt_h = cnt.cpu().tolist()
+        out: Dict[str, int] = {}
+        for i in order:
+            out[c.vocab[i]] = out.get(c.vocab[i], 0) + int(cnt_h[i])
+        return out
     if isinstance(c, torch.Tensor):
         if c.dim() != 1:
             raise RuntimeError("The input column only supports string and numeric type.")
@@ -257,7 +287,26 @@ class StringIndexerModel(_StringArraysModel, StringIndexerModelParams):
         for i, (c, o) in enumerate(zip(ins, outs)):
             m = maps[i]
             col = t.column(c)
-            if isinstance(col, torch.Tensor) and col.dim() == 1:
+            if isinstance(col, StringColumn):
+                # look up each distinct string once, gather by code
+                codes = col.codes.to(config.compute_device()).long()
+                keys = col.vocab
+                for w in keys:
+                    if not isinstance(w, str):
+                        raise RuntimeError("The input column only supports string and numeric type.")
+                lut = torch.tensor([m.get(k, -1.0) for k in keys], dtype=torch.float64, device=codes.device)
+                idx = lut[codes]
+                bad = idx < 0
+                if bool(bad.any()):
+                    if hi == self.ERROR_INVALID:
+                        k = keys[int(codes[bad][0])]
+                        raise RuntimeError("The input contains unseen string: %s. See handleInvalid parameter for "
+                                           "more options." % k)
+                    if hi == self.SKIP_INVALID:
+                        keep_rows &= ~bad.cpu()
+                    idx = torch.where(bad, torch.full_like(idx, float(len(m))), idx)
+                res[o] = idx
+            elif isinstance(col, torch.Tensor) and col.dim() == 1:
                 u, inv = torch.unique(col, return_inverse=True)
                 is_int = not col.dtype.is_floating_point
                 keys = [str(int(v)) if is_int else java_number_to_string(v) for v in u.tolist()]

@@ -28,7 +28,7 @@ from ...linalg.vectors import DenseVector, SparseVector, Vector
 from ...ops import hashing
 from ...param.param import (BooleanParam, FloatParam, IntParam, ParamValidators, StringArrayParam, StringParam)
 from ...parallel import comm
-from ...table import SparseColumn, StringArrayColumn, Table
+from ...table import SparseColumn, StringArrayColumn, StringColumn, Table
 from ...utils.java import java_hashmap_order as _java_hashmap_order
 from ...utils.java import java_number_to_string, java_string_hash
 from ..base import ModelWithData
@@ -86,6 +86,38 @@ def _dict_col(t: Table, col: str):
     return None
 
 
+def _per_string_arrays(t: Table, col: str, fn):
+    """``fn`` (str -> list of str) applied once per distinct string of a dictionary-encoded
+    ``StringColumn``, expanded to every row by code on the device → ``StringArrayColumn``; None for
+    a plain list column."""
+    c = t.column(col)
+    if not isinstance(c, StringColumn) or len(c) == 0 or any(not isinstance(w, str) for w in c.vocab):
+        return None
+    dev = config.compute_device()
+    codes = c.codes.to(dev).long()
+    index, vocab, flat, vlen = {}, [], [], []
+    for w in c.vocab:
+        toks = fn(w)
+        vlen.append(len(toks))
+        for x in toks:
+            k = index.get(x)
+            if k is None:
+                k = index[x] = len(vocab)
+                vocab.append(x)
+            flat.append(k)
+    vlen_t = torch.tensor(vlen, dtype=torch.int64, device=dev)
+    voff = torch.zeros(len(vlen) + 1, dtype=torch.int64, device=dev)
+    voff[1:] = torch.cumsum(vlen_t, 0)
+    vflat = torch.tensor(flat, dtype=torch.int32, device=dev)
+    lens = vlen_t[codes]
+    off = torch.zeros(codes.shape[0] + 1, dtype=torch.int64, device=dev)
+    off[1:] = torch.cumsum(lens, 0)
+    total = int(off[-1])
+    rid = torch.repeat_interleave(torch.arange(codes.shape[0], device=dev), lens, output_size=total)
+    local = torch.arange(total, device=dev) - off[rid]
+    return StringArrayColumn(off, vflat[voff[codes[rid]] + local] if total else vflat[:0], vocab)
+
+
 def _count_csr(rows: torch.Tensor, idx: torch.Tensor, n: int, width: int):
     """Per-row term counts of (row, index) pairs as one sort-unique → (indptr, indices, counts)."""
     keys, cnt = torch.unique(rows * width + idx, return_counts=True)
@@ -102,7 +134,9 @@ class Tokenizer(Transformer, HasInputCol, HasOutputCol):
 
     def transform(self, *inputs):
         t = inputs[0]
-        out = [java_split(r"\s", s.lower()) for s in _strings_col(t, self.get(self.INPUT_COL))]
+        out = _per_string_arrays(t, self.get(self.INPUT_COL), lambda s: java_split(r"\s", s.lower()))
+        if out is None:
+            out = [java_split(r"\s", s.lower()) for s in _strings_col(t, self.get(self.INPUT_COL))]
         return [t.with_column(self.get(self.OUTPUT_COL), out)]
 
 
@@ -119,11 +153,14 @@ class RegexTokenizer(Transformer, HasInputCol, HasOutputCol):
         t = inputs[0]
         pat = re.compile(self.get(self.PATTERN))
         gaps, low, mn = self.get(self.GAPS), self.get(self.TO_LOWERCASE), self.get(self.MIN_TOKEN_LENGTH)
-        out = []
-        for s in _strings_col(t, self.get(self.INPUT_COL)):
+        def tokenize(s):
             s = s.lower() if low else s
             toks = java_split(pat.pattern, s) if gaps else [m.group(0) for m in pat.finditer(s)]
-            out.append([x for x in toks if len(x) >= mn])
+            return [x for x in toks if len(x) >= mn]
+
+        out = _per_string_arrays(t, self.get(self.INPUT_COL), tokenize)
+        if out is None:
+            out = [tokenize(s) for s in _strings_col(t, self.get(self.INPUT_COL))]
         return [t.with_column(self.get(self.OUTPUT_COL), out)]
 
 

@@ -207,7 +207,75 @@ class StringArrayColumn:
         return StringArrayColumn(self.offsets - o0, self.codes, self.vocab)
 
 
-Column = Any  # torch.Tensor | SparseColumn | StringArrayColumn | list
+def first_occurrence(codes: torch.Tensor, V: int) -> torch.Tensor:
+    """Position of the first occurrence of every code in ``codes`` (``len(codes)`` if absent).
+    A scatter-min over a geometrically growing prefix: codes usually all appear early, so the
+    min does not run over (and contend on) the whole column."""
+    codes = codes.long()
+    N = int(codes.shape[0])
+    present = torch.nonzero(torch.bincount(codes, minlength=V) > 0).reshape(-1)
+    first = torch.full((V,), N, dtype=torch.int64, device=codes.device)
+    s0, step = 0, 1 << 20
+    while s0 < N:
+        e0 = min(N, s0 + step)
+        first.scatter_reduce_(0, codes[s0:e0], torch.arange(s0, e0, device=codes.device), reduce="amin")
+        if not bool((first[present] == N).any()):
+            break
+        s0, step = e0, step * 4
+    return first
+
+
+class StringColumn:
+    """Dictionary-encoded strings: row i is ``vocab[codes[i]]`` (int32 codes on the device, the
+    distinct strings on the host). Stages that act per string (Tokenizer, RegexTokenizer,
+    StringIndexer) do their work once per distinct string and gather by code; everything else sees
+    a sequence of Python strings."""
+
+    __slots__ = ("codes", "vocab")
+
+    def __init__(self, codes: torch.Tensor, vocab: Sequence[Optional[str]]):
+        self.codes = codes
+        self.vocab = list(vocab)
+
+    @staticmethod
+    def from_list(values: Sequence[Optional[str]]) -> "StringColumn":
+        index, vocab, codes = {}, [], []
+        for w in values:
+            c = index.get(w)
+            if c is None:
+                c = index[w] = len(vocab)
+                vocab.append(w)
+            codes.append(c)
+        return StringColumn(torch.tensor(codes, dtype=torch.int32), vocab)
+
+    def __len__(self):
+        return int(self.codes.shape[0])
+
+    @property
+    def device(self):
+        return self.codes.device
+
+    def to(self, device=None) -> "StringColumn":
+        return self if device is None else StringColumn(self.codes.to(device), self.vocab)
+
+    def to_list(self) -> List[Optional[str]]:
+        words = np.empty(len(self.vocab), dtype=object)
+        words[:] = self.vocab
+        return words[self.codes.cpu().numpy().astype(np.int64)].tolist()
+
+    def __iter__(self):
+        return iter(self.to_list())
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return StringColumn(self.codes[i], self.vocab)
+        return self.vocab[int(self.codes[int(i)])]
+
+    def take(self, idx: torch.Tensor) -> "StringColumn":
+        return StringColumn(self.codes[idx.to(self.codes.device)], self.vocab)
+
+
+Column = Any  # torch.Tensor | SparseColumn | StringArrayColumn | StringColumn | list
 
 
 def _col_len(col) -> int:
@@ -339,6 +407,8 @@ class Table:
             return col
         if isinstance(col, StringArrayColumn):
             return col.to_lists()
+        if isinstance(col, StringColumn):
+            return col.to_list()
         return [_row_value(col, i) for i in range(self._n)]
 
     def rows(self) -> List[tuple]:
@@ -436,6 +506,8 @@ class Table:
                 cols[k] = c[idx_t.to(c.device)]
             elif isinstance(c, SparseColumn):
                 cols[k] = c.take(idx_t)
+            elif isinstance(c, StringColumn):
+                cols[k] = c.take(idx_t)
             elif isinstance(c, StringArrayColumn):
                 lists = c.to_lists()
                 cols[k] = [lists[int(i)] for i in idx_t]
@@ -462,7 +534,7 @@ class Table:
     def to(self, device) -> "Table":
         cols = {}
         for k, c in self._cols.items():
-            if isinstance(c, (torch.Tensor, SparseColumn, StringArrayColumn)):
+            if isinstance(c, (torch.Tensor, SparseColumn, StringArrayColumn, StringColumn)):
                 cols[k] = c.to(device)
             else:
                 cols[k] = c
