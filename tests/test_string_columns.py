@@ -2,6 +2,7 @@
 string-array stages must give exactly what the per-row host path gives on the same rows as plain
 lists (StopWordsRemover.java, HashingTF.java, CountVectorizer(Model).java semantics)."""
 import numpy as np
+import pytest
 import torch
 
 from flink_ml_amd import Table
@@ -140,3 +141,22 @@ def test_stringindexer_matches_host_path():
     assert m.transform(test)[0].get_list("o") == ref
     m.set_handle_invalid("skip")
     assert m.transform(test)[0].num_rows == 2
+
+
+@pytest.mark.gpu
+def test_string_stages_run_on_device():
+    """The same equivalences with the codes in HBM (the device gathers/scans/sorts are what run)."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from flink_ml_amd import config
+
+    assert config.compute_device().type == "cuda"
+    test_stopwords_remover_matches_host_path()
+    test_hashingtf_matches_host_path()
+    test_countvectorizer_fit_and_transform_match_host_path()
+    test_ngram_matches_host_path()
+    test_tokenizers_match_host_path()
+    test_stringindexer_matches_host_path()
+    _, tc = _both()
+    out = StopWordsRemover().set_input_cols("input").set_output_cols("output").transform(tc)[0].column("output")
+    assert out.codes.device.type == "cuda"
