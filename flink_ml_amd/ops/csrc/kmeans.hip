@@ -313,22 +313,33 @@ __global__ __launch_bounds__(256) void kmeans_assign_wave_kernel(const T* __rest
   constexpr int KG = 8;
   extern __shared__ __align__(16) unsigned char smem_raw[];
   T* Cs = reinterpret_cast<T*>(smem_raw);
+  // centroid norms next to the centroids in LDS: as per-centroid scalar loads they would share
+  // lgkmcnt with the LDS reads, so every LDS wait would also wait for an SMEM round trip
+  T* Ns = Cs + (use_lds ? (long)k * D : 0);
   if (use_lds) {
     for (int i = threadIdx.x; i < k * D; i += blockDim.x) Cs[i] = C[i];
+    for (int i = threadIdx.x; i < k; i += blockDim.x) Ns[i] = cnrm[i];
     __syncthreads();
   }
   const T* Cp = use_lds ? Cs : C;
+  const T* Np = use_lds ? Ns : cnrm;
   const int lane = threadIdx.x & 63;
   const long wave = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const long nwaves = (long)gridDim.x * (blockDim.x >> 6);
-  for (long row = wave; row < n; row += nwaves) {
-    const T* x = X + row * ld;
-    T xv[VPL];
+  // the next row's elements are loaded before this row's reductions start (one row of load
+  // latency hidden behind the DPP chains; a wave otherwise waits a full HBM trip per row)
+  T xv[VPL], xn[VPL];
+  auto load_row = [&](long r, T (&dst)[VPL]) {
+    const T* x = X + (r < n ? r : n - 1) * ld;
 #pragma unroll
     for (int v = 0; v < VPL; ++v) {
       const int c = lane + 64 * v;
-      xv[v] = c < D ? x[c] : (T)0;
+      dst[v] = c < D ? x[c] : (T)0;
     }
+  };
+  if (wave < n) load_row(wave, xv);
+  for (long row = wave; row < n; row += nwaves) {
+    load_row(row + nwaves, xn);
     T pn2 = 0;
 #pragma unroll
     for (int v = 0; v < VPL; ++v) pn2 += xv[v] * xv[v];
@@ -354,20 +365,21 @@ __global__ __launch_bounds__(256) void kmeans_assign_wave_kernel(const T* __rest
         }
       }
 #pragma unroll
-      for (int g = 0; g < KG; ++g) acc[g] = wave_allsum(acc[g]);
+      for (int g = 0; g < KG; ++g)
+        if (i0 + g < k) acc[g] = wave_allsum(acc[g]);  // (k is uniform: no reductions of padding)
 #pragma unroll
       for (int g = 0; g < KG; ++g) {
         const int i = i0 + g;
         if (i >= k) break;
         T dist;
         if (metric == 0) {
-          const T cn = cnrm[i];
+          const T cn = Np[i];
           dist = pn * pn + cn * cn - (T)2 * acc[g];
           dist = dist > (T)0 ? dist : (T)0;
         } else if (metric == 1) {
           dist = acc[g];
         } else {
-          dist = (T)1 - acc[g] / pn / cnrm[i];
+          dist = (T)1 - acc[g] / pn / Np[i];
         }
         if (dist < best) {
           best = dist;
@@ -376,6 +388,8 @@ __global__ __launch_bounds__(256) void kmeans_assign_wave_kernel(const T* __rest
       }
     }
     if (lane == 0) labels[row] = bi;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) xv[v] = xn[v];
   }
 }
 
@@ -611,7 +625,7 @@ FMLX_API int fmlx_kmeans_assign_bf16(const void* X, long ld, long n, int D, int 
 template <typename T, int VPL>
 int launch_assign_wave(const void* X, long ld, long n, int D, const void* C, const void* cnrm, int k, int metric,
                        int* labels, hipStream_t s) {
-  const size_t need = (size_t)k * D * sizeof(T);
+  const size_t need = ((size_t)k * D + k) * sizeof(T);
   const int use_lds = need <= 64 * 1024;
   const size_t sh = use_lds ? need : 0;
   long waves = n;

@@ -73,6 +73,11 @@ class CentroidBuffers:
         self.cnorm_b[: self.k] = (cb.float() ** 2).sum(1)
 
 
+GEMM_ASSIGN_MAX_K = 64       # fp32 euclidean assign through a library GEMM up to this many centroids
+GEMM_ASSIGN_ROWS = 1 << 22   # rows per GEMM chunk (bounds the n×k distance block)
+GEMM_ASSIGN_MIN_ROWS = 1 << 18  # below this the one-launch wave kernel wins (the GEMM path is ~6 launches)
+
+
 def assign(X: torch.Tensor, cb: CentroidBuffers, metric: str, out: torch.Tensor = None) -> torch.Tensor:
     """Index of the closest centroid for every row (reference ``DistanceMeasure.findClosest``)."""
     n, D = X.shape
@@ -89,6 +94,17 @@ def assign(X: torch.Tensor, cb: CentroidBuffers, metric: str, out: torch.Tensor 
     if X.dtype not in (torch.float32, torch.float64):
         X = X.to(torch.float32)
     X = X if X.stride(1) == 1 else X.contiguous()
+    if X.dtype == torch.float32 and metric == "euclidean" and cb.k <= GEMM_ASSIGN_MAX_K and n >= GEMM_ASSIGN_MIN_ROWS:
+        # few centroids: the distance "GEMM" X·Cᵀ is one bandwidth-bound library GEMM (fp32
+        # accumulate) plus an n×k argmin; the wave-per-row kernel is latency-bound at this shape
+        C = cb.cent.to(torch.float32)
+        cn2 = (C * C).sum(1)
+        for r0 in range(0, n, GEMM_ASSIGN_ROWS):
+            Xc = X[r0:r0 + GEMM_ASSIGN_ROWS]
+            d = torch.addmm(cn2.unsqueeze(0), Xc, C.t(), alpha=-2.0)
+            d.add_((Xc * Xc).sum(1, keepdim=True)).clamp_(min=0.0)
+            out[r0:r0 + Xc.shape[0]] = torch.argmin(d, dim=1).to(torch.int32)  # first (lowest) index on ties
+        return out
     C = cb.cent.to(X.dtype).contiguous()
     cn = cb.cnorm.to(X.dtype).contiguous()
     native.call("fmlx_kmeans_assign_generic", native.dtype_code(X.dtype), native.ptr(X), X.stride(0), n, D,
