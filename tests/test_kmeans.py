@@ -202,3 +202,25 @@ def test_gpu_kmeans_fit_golden():
             model = KMeans().set_max_iter(2).fit(_table())
             out = model.transform(_table())[0]
         assert _groups(out) == sorted(GROUPS, key=lambda s: min(s)), dt
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1000, 300_000])
+def test_gpu_assign_fp32_euclidean_both_paths(n):
+    """fp32 euclidean assign: the wave kernel (small n) and the GEMM + argmin path (large n, few
+    centroids) against the fp64 torch reference; near-ties may differ only by rounding."""
+    from flink_ml_amd.ops import kmeans as kk
+
+    g = torch.Generator(device="cpu").manual_seed(n)
+    X = torch.rand((n, 100), generator=g)
+    C = torch.rand((10, 100), generator=g)
+    cb = kk.CentroidBuffers(10, 100, torch.device("cuda"), torch.float32)
+    cb.set(C)
+    got = kk.assign(X.cuda(), cb, "euclidean").cpu().long()
+    d = torch.cdist(X.double(), C.double())
+    ref = d.argmin(1)
+    diff = got != ref
+    if bool(diff.any()):
+        gap = (d[diff, got[diff]] - d[diff, ref[diff]]).abs()
+        assert float(gap.max()) < 1e-4, float(gap.max())
+    assert float(diff.double().mean()) < 1e-3
