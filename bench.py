@@ -30,6 +30,35 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
+def timed_region(tr, ctx, warmup: int, steps: int):
+    """Warm-up, then EXACTLY ``steps`` SGD rounds between barrier + synchronize brackets.
+
+    Every hipGraph the timed ``run_rounds(steps)`` replays is captured, instantiated and
+    replayed once BEFORE the clock starts (``precapture`` + one priming replay each), so the
+    timed region only replays graphs, whatever ``--steps``/``--warmup`` the driver passes.
+    Returns (host wall seconds, device seconds measured by events around the same region).
+    """
+    tr.precapture(steps)
+    for r in tr.graph_sizes(steps):
+        tr.graphs[r].replay()
+    tr.run_rounds(warmup)
+    torch.cuda.synchronize()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    tr.timing = True
+    t0 = time.perf_counter()
+    ev0.record()
+    tr.run_rounds(steps)
+    ev1.record()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    tr.timing = False
+    return elapsed, ev0.elapsed_time(ev1) * 1e-3
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -53,6 +82,7 @@ def main():
     dev = ctx.device
 
     from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer
+    from flink_ml_amd.ops import glm as gk
 
     dt = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp64": torch.float64}[args.dtype]
     n_local = args.rows // world + (1 if args.rows % world > rank else 0)
@@ -67,38 +97,38 @@ def main():
     y = torch.randint(0, 2, (n_local,), generator=gen, device=dev).to(torch.float32)
     torch.cuda.synchronize()
 
-    total_rounds = args.warmup + args.steps + 1
-    sgd = SGD(max_iter=total_rounds, learning_rate=0.1, global_batch_size=args.batch * world, tol=1e-6)
     import numpy as np
 
-    trainer = DeviceGlmTrainer(sgd, np.zeros(args.dim), X, y, None, "logistic", use_graph=not args.no_graph)
+    # rounds the run executes: warm-up, one priming replay of every graph the timed region
+    # replays (hipGraph upload / first-launch costs), the timed steps, plus one
+    def make_trainer():
+        sgd = SGD(max_iter=1, learning_rate=0.1, global_batch_size=args.batch * world, tol=1e-6)
+        tr = DeviceGlmTrainer(sgd, np.zeros(args.dim), X, y, None, "logistic", use_graph=not args.no_graph)
+        tr.rounds_per_graph = args.graph_rounds
+        sgd.max_iter = args.warmup + sum(tr.graph_sizes(args.steps)) + args.steps + 1  # read at capture
+        return tr
 
-    trainer.rounds_per_graph = args.graph_rounds
-
-    def timed(tr):
-        tr.run_rounds(args.warmup)
-        torch.cuda.synchronize()
-        ctx.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        tr.run_rounds(args.steps)
-        torch.cuda.synchronize()
-        ctx.barrier()
-        torch.cuda.synchronize()
-        return time.perf_counter() - t0
-
-    elapsed = timed(trainer)
+    if world > 1 and not ctx.is_distributed:
+        raise SystemExit("WORLD_SIZE=%d but the process group did not come up" % world)
+    trainer = make_trainer()
+    if world > 1 and ctx.backend == "nccl" and trainer.xg is None and os.environ.get("FMLX_XGMI", "1") != "0":
+        msg = "xGMI one-shot exchange did not come up (allocation, IPC mapping or self-test); rounds use RCCL"
+        if os.environ.get("FMLX_REQUIRE_XGMI", "0") == "1":
+            raise SystemExit(msg)
+        if rank == 0:
+            print("WARNING: " + msg, file=sys.stderr, flush=True)
+    elapsed, kernel_s = timed_region(trainer, ctx, args.warmup, args.steps)
     # a bounded xGMI wait that gave up (a peer never arrived) means partial feedback: never
     # report it — re-time the same rounds on the RCCL path instead (decided on every rank)
     ok = trainer.xg is None or trainer.xg.healthy()
     if comm.all_reduce_scalar(1.0 if ok else 0.0, "min") < 1.0:
-        from flink_ml_amd.ops import glm as gk
-
-        trainer = DeviceGlmTrainer(sgd, np.zeros(args.dim), X, y, None, "logistic", use_graph=not args.no_graph)
+        if rank == 0:
+            print("xGMI exchange timed out; re-timing on the RCCL path", file=sys.stderr)
+        trainer = make_trainer()
         trainer.xg, trainer.mode = None, gk.TAIL_FEEDBACK
-        trainer.rounds_per_graph = args.graph_rounds
-        elapsed = timed(trainer)
+        elapsed, kernel_s = timed_region(trainer, ctx, args.warmup, args.steps)
     elapsed = comm.all_reduce_scalar(elapsed, "max")
+    kernel_s = comm.all_reduce_scalar(kernel_s, "max")
     executed = trainer.rounds_executed()
     if executed < args.warmup + args.steps:
         raise SystemExit("SGD terminated early (%d rounds): timing would skip work" % executed)
@@ -115,6 +145,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 4),
+            "kernel_us_per_step": round(kernel_s / args.steps * 1e6, 2),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -128,7 +159,8 @@ def main():
                 "rows": args.rows,
                 "dim": args.dim,
                 "per_gpu_batch": args.batch,
-                "hipgraph": not args.no_graph,
+                "hipgraph": trainer.use_graph,
+                "collective": "none" if world == 1 else ("xgmi" if trainer.xg is not None else ctx.backend),
                 "round": {1: "fused kernel + rccl all-reduce + update", 2: "one fused kernel",
                           3: "one fused kernel with in-kernel xgmi exchange"}[trainer.mode],
                 "hbm_gb_per_s": round(args.batch * args.dim * X.element_size() / (ms * 1e-3) / 1e9, 1),

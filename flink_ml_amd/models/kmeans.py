@@ -163,7 +163,9 @@ def kmeans_lloyd(X: torch.Tensor, init: np.ndarray, max_iter: int, metric: str):
                 comm.all_reduce_sum(payload)
                 rnd.finalize(cb, payload)
                 ck.maybe_save(e + 1, lambda: {"centroids": cb.cent.to(torch.float64), "weights": cb.weights})
-        return cb.cent.to(torch.float64).cpu().numpy(), cb.weights.cpu().numpy()
+        out = cb.cent.to(torch.float64).cpu().numpy(), cb.weights.cpu().numpy()
+        comm.check_collectives()  # after the host sync: no round used a partial xGMI exchange
+        return out
     C = torch.as_tensor(init, dtype=torch.float64)
     counts = counts0.to(torch.float64) if restored is not None else torch.zeros(kc, dtype=torch.float64)
     for e in range(start, max_iter):

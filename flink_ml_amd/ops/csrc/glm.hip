@@ -171,8 +171,11 @@ __device__ void glm_xgmi_exchange(const xgmi::Ctx& x, A* fb, long stride) {
   const long rec = GLM_DATA + (long)slot * GLM_MAX * (long)sizeof(A);
   A* mine = at<A>(x.peers[x.rank], rec);
   for (long c = threadIdx.x; c < stride; c += blockDim.x) st_sys(mine + c, fb[c]);
-  signal_and_wait(x, GLM_FLAGS, slot, g + 1);
-  for (long c = threadIdx.x; c < stride; c += blockDim.x) fb[c] = sum_ranks<A>(x, rec, c);
+  const bool ok = signal_and_wait(x, GLM_FLAGS, slot, g + 1);
+  // a timed-out exchange poisons the feedback: with a NaN Σw the update is skipped and the
+  // termination test (L/W > tol) fails, so the iteration stops on the last good coefficients;
+  // the host raises on the error word (parallel/xgmi.py)
+  for (long c = threadIdx.x; c < stride; c += blockDim.x) fb[c] = ok ? sum_ranks<A>(x, rec, c) : poison<A>();
   __syncthreads();
   if (threadIdx.x == 0) x.gen[GEN_GLM] = g + 1;
 }

@@ -41,7 +41,8 @@ struct Ctx {
   void* const* peers;
   int world, rank;
   int* gen;         // int32[GEN_SIZE], local memory
-  int* err;         // int32[1], local: set to 1 when a peer never arrived
+  int* err;         // int32[1] in host-mapped coherent memory: set to 1 when a peer never
+                    // arrived (the host reads it without a device sync, parallel/xgmi.py)
   long spin_limit;  // polls before giving up
 };
 
@@ -67,8 +68,13 @@ __device__ __forceinline__ T* at(void* buf, long byte_off) {
 
 // Called by EVERY thread of the block after it stored its share of this rank's record with
 // st_sys: drain every wave's stores, raise my tag, then wait until every peer raised the same
-// tag (one polling lane per peer, bounded). On return the peers' records are readable.
-__device__ __forceinline__ void signal_and_wait(const Ctx& x, long flag_off, int idx, int tag) {
+// tag (one polling lane per peer, bounded). Returns true (block-uniform) when every peer
+// arrived: the peers' records are then readable. On a timeout the error word is raised and the
+// caller must NOT sum (it poisons its output with NaN instead), so a partial exchange can never
+// pass for a result.
+__device__ __forceinline__ bool signal_and_wait(const Ctx& x, long flag_off, int idx, int tag) {
+  __shared__ int s_timeout;
+  if (threadIdx.x == 0) s_timeout = 0;
   __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0) st_sys(at<int>(x.peers[x.rank], flag_off) + idx, tag);
@@ -77,7 +83,8 @@ __device__ __forceinline__ void signal_and_wait(const Ctx& x, long flag_off, int
     long it = 0;
     while (ld_sys(f) != tag) {
       if (++it > x.spin_limit) {
-        atomicOr(x.err, 1);
+        st_sys(x.err, 1);  // plain system-scope store (host memory: no PCIe atomics needed)
+        s_timeout = 1;     // any writer, same value
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -85,6 +92,12 @@ __device__ __forceinline__ void signal_and_wait(const Ctx& x, long flag_off, int
   }
   __syncthreads();
   __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  return s_timeout == 0;
+}
+
+template <typename A>
+__device__ __forceinline__ A poison() {
+  return (A)__builtin_nan("");
 }
 
 // Σ over ranks 0..world-1, in rank order, of element `i` of the records at byte offset `off`

@@ -14,7 +14,7 @@
 // P−1 different xGMI links at once. Block b only depends on block b of the peers, never on
 // another block of its own grid, so nothing assumes co-residency. Every spin is bounded; a
 // timeout sets the error word that the host checks (parallel/xgmi.py), so a lost peer cannot
-// hang the GPU.
+// hang the GPU; a block whose wait gave up writes NaN instead of a partial sum.
 #include "xgmi.h"
 
 namespace {
@@ -38,10 +38,10 @@ __global__ __launch_bounds__(xgmi::THREADS) void xar_oneshot_kernel(xgmi::Ctx x,
     const long j = (long)i * THREADS + threadIdx.x;
     if (base + j < n) st_sys(mine + j, src[base + j]);
   }
-  signal_and_wait(x, FLAGS, slot * MAX_BLOCKS + b, g + 1);
+  const bool ok = signal_and_wait(x, FLAGS, slot * MAX_BLOCKS + b, g + 1);
   A out[VEC];
 #pragma unroll
-  for (int i = 0; i < VEC; ++i) out[i] = sum_ranks<A>(x, rec, (long)i * THREADS + threadIdx.x);
+  for (int i = 0; i < VEC; ++i) out[i] = ok ? sum_ranks<A>(x, rec, (long)i * THREADS + threadIdx.x) : poison<A>();
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
     const long j = (long)i * THREADS + threadIdx.x;
@@ -91,6 +91,25 @@ FMLX_API int fmlx_xar_open(const void* handle, void** out_ptr) {
 }
 
 FMLX_API int fmlx_xar_close(void* p) { return (int)hipIpcCloseMemHandle(p); }
+
+// Host-mapped, coherent (fine-grained) int32 words for device→host status flags: the device
+// writes them with system-scope stores and the host reads them without synchronising.
+FMLX_API int fmlx_host_flags_alloc(int n, void** host_ptr, void** dev_ptr) {
+  void* h = nullptr;
+  hipError_t e = hipHostMalloc(&h, (size_t)n * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) return (int)e;
+  __builtin_memset(h, 0, (size_t)n * sizeof(int));
+  void* d = nullptr;
+  e = hipHostGetDevicePointer(&d, h, 0);
+  if (e != hipSuccess) {
+    (void)hipHostFree(h);
+    return (int)e;
+  }
+  *host_ptr = h;
+  *dev_ptr = d;
+  return 0;
+}
+FMLX_API int fmlx_host_flags_free(void* h) { return (int)hipHostFree(h); }
 FMLX_API int fmlx_xar_free(void* p) { return (int)hipFree(p); }
 
 // In-place allowed (dst == src). dtype: 0 = f32, 1 = f64. state: optional SGD round state that

@@ -70,13 +70,24 @@ def all_reduce_sum(t: torch.Tensor) -> torch.Tensor:
     return all_reduce(t, "sum")
 
 
+def check_collectives() -> None:
+    """Raises if an earlier one-shot xGMI collective of this process gave up waiting for a peer
+    (its output was poisoned with NaN). No device sync: call it after a host sync point so the
+    kernels in question have finished."""
+    from . import xgmi
+
+    xgmi.check()
+
+
 def all_reduce_scalar(x: float, op: str = "sum", dtype=torch.float64) -> float:
     ctx = get_context()
     if not ctx.is_distributed:
         return x
     t = torch.tensor([x], dtype=dtype, device=_backend_device(ctx))
     all_reduce(t, op)
-    return t.item()
+    v = t.item()  # host sync: every earlier collective on this stream has finished
+    check_collectives()
+    return v
 
 
 def broadcast_tensor(t: torch.Tensor, src: int = 0) -> torch.Tensor:

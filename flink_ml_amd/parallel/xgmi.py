@@ -17,8 +17,11 @@ Enablement is collective, so ranks never disagree on the path: world sizes 2..8 
 (RCCL) group, every rank allocates and maps every peer, and a self-test against exact expected
 sums passes on ALL ranks; otherwise collectives stay on RCCL. ``FMLX_XGMI=0`` disables the path;
 ``FMLX_XGMI=force`` also enables it on a gloo group (several ranks sharing one GPU: how the GPU
-test rehearses it on a one-GPU box). Every device-side wait is bounded; ``healthy()`` reports a
-timed-out wait and callers raise instead of returning numbers computed from a partial exchange.
+test rehearses it on a one-GPU box). Every device-side wait is bounded. A wait that gives up
+writes NaN instead of a partial sum and raises an error word that lives in host-mapped coherent
+memory, so the host reads it with no device sync: ``comm.all_reduce`` checks it before every
+xGMI launch and algorithms check it at their host sync points (``check()``); either raises
+``XgmiTimeout`` instead of returning numbers computed from a partial exchange.
 """
 from __future__ import annotations
 
@@ -47,6 +50,8 @@ native.register_kernel_sigs({
     "fmlx_xar_open": [c_void_p, c_void_p],
     "fmlx_xar_close": [c_void_p],
     "fmlx_xar_free": [c_void_p],
+    "fmlx_host_flags_alloc": [c_int, c_void_p, c_void_p],
+    "fmlx_host_flags_free": [c_void_p],
     "fmlx_xar_allreduce": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p,
                            c_long, c_void_p],
 })
@@ -54,6 +59,36 @@ native.register_kernel_sigs({
 # polls (each ≈ one xGMI round trip + s_sleep) before a wait gives up: several seconds, far
 # beyond any lockstep drift between ranks, far below a hang
 DEFAULT_SPIN = int(os.environ.get("FMLX_XGMI_SPIN", str(1 << 22)))
+
+
+class XgmiTimeout(RuntimeError):
+    """A bounded xGMI wait gave up: some peer never arrived (its outputs were poisoned)."""
+
+
+class HostFlags:
+    """int32 words in host-mapped coherent memory, written by kernels, read by the host with no
+    device synchronisation (a plain load of pinned host memory)."""
+
+    def __init__(self, n: int = 1):
+        lib = native.kernels()
+        h, d = c_void_p(), c_void_p()
+        rc = lib.fmlx_host_flags_alloc(int(n), ctypes.byref(h), ctypes.byref(d))
+        if rc != 0:
+            raise RuntimeError("hipHostMalloc of the status words failed (%d)" % rc)
+        self.lib, self.n = lib, n
+        self.host, self.dev = h.value, d.value
+        self._view = (ctypes.c_int32 * n).from_address(self.host)
+
+    def get(self, i: int = 0) -> int:
+        return int(self._view[i])
+
+    def clear(self, i: int = 0) -> None:
+        self._view[i] = 0
+
+    def close(self) -> None:
+        if self.host:
+            self.lib.fmlx_host_flags_free(c_void_p(self.host))
+            self.host = None
 
 
 class XgmiComm:
@@ -106,12 +141,12 @@ class XgmiComm:
         self.map_ok = ok
         self.peers = torch.tensor(ptrs, dtype=torch.int64, device=self.device)  # device pointer table
         self.gen = torch.zeros(lib.fmlx_xar_gen_size(), dtype=torch.int32, device=self.device)
-        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.err = HostFlags(1)
 
     # -- kernel plumbing --------------------------------------------------------------------------
     def kernel_args(self):
         """(peers, world, rank, gen, err, spin_limit) as passed to the HIP launchers."""
-        return (self.peers.data_ptr(), self.world, self.rank, self.gen.data_ptr(), self.err.data_ptr(),
+        return (self.peers.data_ptr(), self.world, self.rank, self.gen.data_ptr(), self.err.dev,
                 self.spin_limit)
 
     def accepts(self, t: torch.Tensor) -> bool:
@@ -121,14 +156,22 @@ class XgmiComm:
     def all_reduce_(self, t: torch.Tensor, state: Optional[torch.Tensor] = None) -> torch.Tensor:
         """In-place sum over the group (same shape on every rank), stream-ordered on the current
         stream and capturable in a hipGraph. ``state``: optional SGD round state predicating the call."""
+        self.check()  # an earlier exchange of this group gave up: its peers' tags no longer line up
         dt = 0 if t.dtype == torch.float32 else 1
         native.call("fmlx_xar_allreduce", dt, self.peers.data_ptr(), self.world, self.rank, t.data_ptr(),
-                    t.data_ptr(), t.numel(), self.gen.data_ptr(), self.err.data_ptr(), native.ptr(state),
+                    t.data_ptr(), t.numel(), self.gen.data_ptr(), self.err.dev, native.ptr(state),
                     self.spin_limit, native.stream_ptr(t.device))
         return t
 
     def healthy(self) -> bool:
-        return int(self.err.item()) == 0
+        """False once any exchange of this group gave up (no device sync: host-mapped word;
+        kernels still in flight are seen once they finish)."""
+        return self.err.get() == 0
+
+    def check(self) -> None:
+        if self.err.get() != 0:
+            raise XgmiTimeout("xGMI exchange timed out on rank %d: a peer never arrived; results of the "
+                              "affected collectives were poisoned (NaN)" % self.rank)
 
     def self_test(self) -> bool:
         """Exact-integer sums through both slots, partial and multi-block chunks, f32 and f64."""
@@ -146,6 +189,8 @@ class XgmiComm:
         return ok and self.healthy()
 
     def close(self) -> None:
+        if getattr(self, "err", None) is not None:
+            self.err.close()
         for p in self._opened:
             self.lib.fmlx_xar_close(c_void_p(p))
         self._opened = []
@@ -201,6 +246,13 @@ def get() -> Optional[XgmiComm]:
             return None
         _COMM = comm
         return _COMM
+
+
+def check() -> None:
+    """Raises ``XgmiTimeout`` if any xGMI exchange of this process gave up. Cheap (no device sync);
+    algorithms call it at their host sync points, after the device work they waited for."""
+    if _COMM is not None:
+        _COMM.check()
 
 
 def reset() -> None:

@@ -134,3 +134,55 @@ def test_java_rows_gpu_matches_cpu(ops, nvec, n):
     assert torch.equal(gv.cpu(), cv) and torch.equal(gs.cpu(), cs)
     g32, _ = java_rows(77, n, ops, nvec, device="cuda", vec_dtype=torch.float32)
     assert torch.equal(g32.cpu(), cv.float())
+
+
+class _FakeGraph:
+    def __init__(self, log, r):
+        self.log, self.r = log, r
+
+    def replay(self):
+        self.log.append(("replay", self.r))
+
+
+class _FakeEvent:
+    def __init__(self, **kw):
+        pass
+
+    def record(self):
+        pass
+
+    def elapsed_time(self, other):
+        return 1.0
+
+
+@pytest.mark.parametrize("steps,warmup,R", [(20, 5, 10), (7, 0, 10), (200, 20, 10), (3, 1, 1), (25, 5, 10)])
+def test_bench_timed_region_only_replays(monkeypatch, steps, warmup, R):
+    """bench.py: no hipGraph capture may happen between the timing barriers (round-1 driver run
+    captured the 10-round graph inside the timed region)."""
+    import bench
+    from flink_ml_amd.common.optimizer import DeviceGlmTrainer
+
+    tr = object.__new__(DeviceGlmTrainer)
+    tr.use_graph, tr.rounds_per_graph, tr.graphs, tr.timing = True, R, {}, False
+    log = []
+
+    def capture(r):
+        assert not tr.timing, "hipGraph captured inside the timed region"
+        log.append(("capture", r))
+        tr.graphs[r] = _FakeGraph(log, r)
+        return tr.graphs[r]
+
+    tr._capture = capture
+    monkeypatch.setattr(bench.torch.cuda, "synchronize", lambda *a: None)
+    monkeypatch.setattr(bench.torch.cuda, "Event", _FakeEvent)
+
+    class Ctx:
+        def barrier(self):
+            log.append(("barrier",))
+
+    elapsed, dev_s = bench.timed_region(tr, Ctx(), warmup, steps)
+    assert dev_s == 1e-3 and elapsed >= 0
+    first_timed = max(i for i, e in enumerate(log) if e == ("barrier",) and i < len(log) - 1) + 1
+    timed = [e for e in log[first_timed:] if e != ("barrier",)]
+    assert all(e[0] == "replay" for e in timed)
+    assert sum(e[1] for e in timed) == steps  # exactly `steps` rounds timed

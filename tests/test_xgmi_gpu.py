@@ -113,3 +113,35 @@ def test_fused_round_flagship_shape_matches_torch(det, monkeypatch):
     got = tr.fit()
     assert tr.rounds_executed() == 3
     assert np.allclose(got, ref, rtol=2e-4, atol=2e-6), np.abs(got - ref).max()
+
+
+def _timeout_worker(rank, world):
+    import time
+
+    import torch
+
+    from flink_ml_amd.parallel import comm, xgmi
+
+    x = xgmi.get()
+    assert x is not None, "xGMI exchange did not come up"
+    x.spin_limit = 2000  # a few ms of polling
+    if rank == 1:
+        time.sleep(3.0)  # rank 0's wait gives up long before this rank publishes
+    t = torch.full((2000,), float(rank + 1), device="cuda:0")
+    x.all_reduce_(t)
+    torch.cuda.synchronize()
+    out = {"nan": bool(torch.isnan(t).all().item()), "healthy": x.healthy()}
+    try:
+        comm.all_reduce_sum(torch.ones(8, device="cuda:0"))  # refuses once the error word is set
+        out["raised"] = False
+    except xgmi.XgmiTimeout:
+        out["raised"] = True
+    return out
+
+
+def test_xgmi_timeout_poisons_and_raises():
+    """a peer later than the spin limit must never yield a silent partial sum."""
+    _need_gpu()
+    res = run_spmd(_timeout_worker, 2, env=ENV, timeout=300)
+    r0 = res[0]
+    assert r0["nan"] and not r0["healthy"] and r0["raised"], r0
