@@ -228,7 +228,13 @@ class DeviceGlmTrainer:
         self.rounds_per_graph = self.check_every
 
     # -- one round as a fixed launch sequence (capturable) -------------------------------------
-    def _launch_round(self) -> None:
+    def _launch_round(self, rounds: int = 1) -> None:
+        """Launches ``rounds`` consecutive rounds (one host call on the fused dense path,
+        else ``rounds`` launch sequences)."""
+        if rounds > 1 and not (self.csc is None and not self.wide and not self.sparse and self.mode != gk.TAIL_FEEDBACK):
+            for _ in range(rounds):
+                self._launch_round(1)
+            return
         s = self.sgd
         if self.csc is not None:
             # forward (per-row multipliers) + atomic-free column-major backward; on 1 GPU the
@@ -277,7 +283,7 @@ class DeviceGlmTrainer:
             return
         # every rank launches the round, also one without rows: it still joins the reduction tail
         gk.glm_round(self.X, self.y, self.w, self.coef, self.B, self.loss, self.state, self.scratch, self.mode,
-                     self.feedback, s.max_iter, s.tol, s.learning_rate, s.reg, s.elastic_net, xg=self.xg)
+                     self.feedback, s.max_iter, s.tol, s.learning_rate, s.reg, s.elastic_net, xg=self.xg, rounds=rounds)
         if self.mode == gk.TAIL_FEEDBACK:
             comm.all_reduce_sum(self.feedback)
             gk.update(self.feedback, self.d, self.coef, self.state, s.max_iter, s.tol, s.learning_rate, s.reg,
@@ -299,8 +305,7 @@ class DeviceGlmTrainer:
             t.copy_(v)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            for _ in range(rounds):
-                self._launch_round()
+            self._launch_round(rounds)
         self.graphs[rounds] = g
         return g
 
@@ -322,8 +327,9 @@ class DeviceGlmTrainer:
     def run_rounds(self, k: int) -> None:
         """Runs ``k`` SGD rounds (each predicated on the device running flag), no host sync."""
         if not self.use_graph:
-            for _ in range(k):
-                self._launch_round()
+            R = self.rounds_per_graph
+            for i in range(0, k, R):
+                self._launch_round(min(R, k - i))
             return
         R = self.rounds_per_graph
         full, rem = divmod(k, R)

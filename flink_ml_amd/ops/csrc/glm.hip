@@ -52,9 +52,11 @@ __device__ __forceinline__ void loss_and_mult(int loss, float dot, float y, floa
   if (loss == LOSS_LOGISTIC) {
     const float ys = 2.f * y - 1.f;
     const float z = -dot * ys;
-    const float t = __expf(-fabsf(z));
-    const float r = __frcp_rn(1.f + t);
-    l = wt * (fmaxf(z, 0.f) + __logf(1.f + t));
+    // raw v_exp_f32 / v_log_f32 (base 2): t ∈ (0, 1] and 1 + t ∈ (1, 2] need none of the
+    // denormal range fix-ups of expf/logf; v_rcp_f32 (1 ulp), not the IEEE division sequence
+    const float t = __builtin_amdgcn_exp2f(-fabsf(z) * 1.4426950408889634f);
+    const float r = __builtin_amdgcn_rcpf(1.f + t);
+    l = wt * (fmaxf(z, 0.f) + __builtin_amdgcn_logf(1.f + t) * 0.6931471805599453f);
     m = wt * (-ys) * (z > 0.f ? r : t * r);
   } else if (loss == LOSS_HINGE) {
     const float ys = 2.f * y - 1.f;
@@ -63,7 +65,7 @@ __device__ __forceinline__ void loss_and_mult(int loss, float dot, float y, floa
     l = pos ? wt * h : 0.f;
     m = pos ? -ys * wt : 0.f;
   } else if (loss == LOSS_FTRL) {
-    m = __frcp_rn(1.f + __expf(-dot)) - y;
+    m = __builtin_amdgcn_rcpf(1.f + __expf(-dot)) - y;
     l = 0.f;
   } else {
     const float r = dot - y;
@@ -132,6 +134,7 @@ struct GlmTail {
   void* feedback;  // [d+2]: output of TAIL_FEEDBACK, a copy of the global feedback otherwise
   double tol, lr, reg, en;
   xgmi::Ctx x;     // TAIL_XGMI only
+  int red_off;     // byte offset of the grouped row path's per-wave reduction scratch in LDS
 };
 
 // Write-through (sc1) hand-off of the partial rows (cdna_hip_programming.md Guideline 16, the
@@ -316,6 +319,17 @@ __device__ void glm_round_tail_atomic(const GlmTail& tl, int d, A* coef, int* st
 // ------------------------------------------------------------------------------------------
 // K4/K5/K6 — fused minibatch loss + gradient partials
 // ------------------------------------------------------------------------------------------
+// Sum over aligned segments of L lanes (L = 8 or 16) with DPP; every lane of a segment gets the
+// segment's total. Quad xor1 / xor2 → row_half_mirror (8) → row_mirror (16).
+template <int L>
+__device__ __forceinline__ float seg_sum_dpp(float v) {
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror: quads of an 8-lane half swap
+  if constexpr (L == 16) v += dpp_mov<0x140>(v);  // row_mirror: 8-lane halves of a row swap
+  return v;
+}
+
 // register-light shapes are capped at 128 VGPRs (4 waves per SIMD) so that two 8-wave blocks
 // share a CU; heavier ones (which would spill under the cap) keep the compiler's choice
 template <typename T, int EPC, int CPL, int U>
@@ -325,8 +339,8 @@ constexpr int glm_min_waves() {
 
 // X / y / wt are deliberately NOT __restrict__: with restrict the compiler may move the row
 // prefetch loads below the compiler fence that pins them ahead of the math (see the row loop).
-template <typename T, int EPC, int CPL, int U, int WPB, bool NT>
-__global__ __launch_bounds__(WPB * 64, (glm_min_waves<T, EPC, CPL, U>())) void glm_round_kernel(
+template <typename T, int EPC, int CPL, int U, int WPB, bool NT, int G = 0>
+__global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U>())) void glm_round_kernel(
     const T* X, long ld, const typename AccOf<T>::type* y,
     const typename AccOf<T>::type* wt, typename AccOf<T>::type* coef,
     long n, int d, long B, int loss, int* state, typename AccOf<T>::type* partials, GlmTail tl) {
@@ -348,19 +362,34 @@ __global__ __launch_bounds__(WPB * 64, (glm_min_waves<T, EPC, CPL, U>())) void g
   const long W = (long)gridDim.x * WPB;
   const long gw = (long)blockIdx.x * WPB + wave;
 
+  // bf16 rows: packed fp32 math on {lo, hi} pairs (one dword = two bf16, widened exactly by a
+  // shift / a mask): the dot and the gradient axpy are one v_pk_fma_f32 per pair each
+  constexpr bool kPacked = sizeof(T) == 2 && EPC % 2 == 0;
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  constexpr int EP = kPacked ? EPC / 2 : 1;
   A w[CPL][EPC];
   A acc[CPL][EPC];
+  f2_t w2[CPL][EP], acc2[CPL][EP];  // packed-pair views used by the bf16 path
 #pragma unroll
-  for (int k = 0; k < CPL; ++k)
+  for (int k = 0; k < CPL; ++k) {
 #pragma unroll
     for (int i = 0; i < EPC; ++i) acc[k][i] = (A)0;
+#pragma unroll
+    for (int i = 0; i < EP; ++i) acc2[k][i] = f2_t{0.f, 0.f};
+  }
   // coefficient slices (L2-hot), fetched after the first row loads are on their way
   auto load_w = [&]() {
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
       const int c = lane + 64 * k;
+      if constexpr (kPacked) {
 #pragma unroll
-      for (int i = 0; i < EPC; ++i) w[k][i] = c < nch ? coef[c * EPC + i] : (A)0;
+        for (int i = 0; i < EP; ++i)
+          w2[k][i] = c < nch ? f2_t{(float)coef[c * EPC + 2 * i], (float)coef[c * EPC + 2 * i + 1]} : f2_t{0.f, 0.f};
+      } else {
+#pragma unroll
+        for (int i = 0; i < EPC; ++i) w[k][i] = c < nch ? coef[c * EPC + i] : (A)0;
+      }
     }
   };
   A wsum = 0, lsum = 0;
@@ -424,32 +453,186 @@ __global__ __launch_bounds__(WPB * 64, (glm_min_waves<T, EPC, CPL, U>())) void g
     }
   };
   auto process = [&](Chunk<T, EPC> (&x)[U][CPL], A (&yy)[U], A (&ww)[U], bool (&vv)[U]) {
-    A dot[U];
+    if constexpr (kPacked) {
+      f2_t xf[U][CPL][EP];
+      A dot[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      A s = 0;
+      for (int u = 0; u < U; ++u) {
+        f2_t s2[2] = {{0.f, 0.f}, {0.f, 0.f}};  // two chains: half the dependent-FMA latency
 #pragma unroll
-      for (int k = 0; k < CPL; ++k)
+        for (int k = 0; k < CPL; ++k) {
+          const uint32_t* q = reinterpret_cast<const uint32_t*>(x[u][k].v);
 #pragma unroll
-        for (int i = 0; i < EPC; ++i) s += (A)Ld<T>::f(x[u][k].v[i]) * w[k][i];
-      dot[u] = s;
-    }
+          for (int i = 0; i < EP; ++i) {
+            xf[u][k][i] = f2_t{__uint_as_float(q[i] << 16), __uint_as_float(q[i] & 0xffff0000u)};
+            s2[i & 1] = __builtin_elementwise_fma(xf[u][k][i], w2[k][i], s2[i & 1]);
+          }
+        }
+        const f2_t st = s2[0] + s2[1];
+        dot[u] = st.x + st.y;
+      }
 #pragma unroll
-    for (int u = 0; u < U; ++u) dot[u] = wave_sum_dpp(dot[u]);
+      for (int u = 0; u < U; ++u) dot[u] = wave_sum_dpp(dot[u]);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      A l, m;
-      const A wu = has_wt ? ww[u] : (A)1;
-      loss_and_mult(loss, dot[u], yy[u], wu, l, m);
-      if (!vv[u]) { l = (A)0; m = (A)0; }
-      wsum += vv[u] ? wu : (A)0;
-      lsum += l;
+      for (int u = 0; u < U; ++u) {
+        A l, m;
+        const A wu = has_wt ? ww[u] : (A)1;
+        loss_and_mult(loss, dot[u], yy[u], wu, l, m);
+        if (!vv[u]) { l = (A)0; m = (A)0; }
+        wsum += vv[u] ? wu : (A)0;
+        lsum += l;
+        const f2_t m2 = {m, m};
 #pragma unroll
-      for (int k = 0; k < CPL; ++k)
+        for (int k = 0; k < CPL; ++k)
 #pragma unroll
-        for (int i = 0; i < EPC; ++i) acc[k][i] += m * (A)Ld<T>::f(x[u][k].v[i]);
+          for (int i = 0; i < EP; ++i) acc2[k][i] = __builtin_elementwise_fma(m2, xf[u][k][i], acc2[k][i]);
+      }
+    } else {
+      A dot[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        A s = 0;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+#pragma unroll
+          for (int i = 0; i < EPC; ++i) s += (A)Ld<T>::f(x[u][k].v[i]) * w[k][i];
+        dot[u] = s;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) dot[u] = wave_sum_dpp(dot[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        A l, m;
+        const A wu = has_wt ? ww[u] : (A)1;
+        loss_and_mult(loss, dot[u], yy[u], wu, l, m);
+        if (!vv[u]) { l = (A)0; m = (A)0; }
+        wsum += vv[u] ? wu : (A)0;
+        lsum += l;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+#pragma unroll
+          for (int i = 0; i < EPC; ++i) acc[k][i] += m * (A)Ld<T>::f(x[u][k].v[i]);
+      }
     }
   };
+  if constexpr (G > 0) {
+    // ---- grouped row path (bf16, EPC 8): G rows per step. The per-row chain dot → wave sum →
+    // loss → multiplier is the latency that bounds the row-at-a-time loop (measured: the loss
+    // step alone +6 µs on the 200 MB flagship batch); here the G dots of a step are reduced
+    // together (one LDS transpose + a 3–4 step DPP segment sum instead of G full wave sums), the
+    // loss runs once for all G rows (one row per segment of L = 64/G lanes) and the G
+    // multipliers come back with readlane for the packed axpy.
+    static_assert(kPacked && EPC == 8 && (G == 4 || G == 8), "grouped path: bf16 rows, 16-byte chunks");
+    constexpr int L = 64 / G;  // lanes per row in the loss step
+    extern __shared__ __align__(16) unsigned char smem_g[];
+    float* red = reinterpret_cast<float*>(smem_g + tl.red_off) + wave * (G * 64);  // wave-private [G][64]
+    const int gi = lane / L, seg = lane % L;
+    const long r0w = start + gw;      // this wave's first row
+    const long stepg = (long)G * W;   // rows between consecutive groups of the wave
+    Chunk<T, EPC> xa[G][CPL], xb[G][CPL];
+    A yla = (A)0, wla = (A)1, ylb = (A)0, wlb = (A)1;
+    auto load_group = [&](long g0, Chunk<T, EPC> (&dst)[G][CPL], A& yl, A& wl) {
+      // labels of the group's rows, one row per L-lane segment (clamped: masked in the loss)
+      long rl = g0 + gi * W;
+      rl = rl < end ? rl : (end > 0 ? end - 1 : 0);
+      yl = y[rl];
+      wl = wsrc[rl];
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        const long ri0 = g0 + i * W;
+        const long ri = ri0 < end ? ri0 : r0w;  // r0w < end whenever a group is loaded
+        const T* row = X + ri * ld;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+          const int c = lane + 64 * k;
+          if constexpr (NT) load_chunk_nt<T, EPC>(row + (c < nch ? c : nch - 1) * EPC, dst[i][k]);
+          else load_chunk<T, EPC>(row + (c < nch ? c : nch - 1) * EPC, dst[i][k]);
+        }
+      }
+    };
+    auto unpack = [&](const Chunk<T, EPC>& ch, int q) -> f2_t {
+      const uint32_t v = reinterpret_cast<const uint32_t*>(ch.v)[q];
+      return f2_t{__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u)};
+    };
+    auto process_group = [&](long g0, Chunk<T, EPC> (&x)[G][CPL], A yl, A wl) {
+      // 1. per-lane dot partials of the G rows (packed fp32, two chains per row)
+      float pd[G];
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        f2_t s2[2] = {{0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+#pragma unroll
+          for (int q = 0; q < EPC / 2; ++q) s2[q & 1] = __builtin_elementwise_fma(unpack(x[i][k], q), w2[k][q], s2[q & 1]);
+        const f2_t st = s2[0] + s2[1];
+        pd[i] = st.x + st.y;
+      }
+      // 2. transposed reduction: [G][64] through the wave's LDS slot (one wave: LDS in order),
+      // lane (gi, seg) sums row gi's partials of lanes seg·G .. seg·G + G − 1, then the segment
+#pragma unroll
+      for (int i = 0; i < G; ++i) red[i * 64 + lane] = pd[i];
+      float s = 0.f;
+      const float4* src = reinterpret_cast<const float4*>(red + gi * 64 + seg * G);
+#pragma unroll
+      for (int q = 0; q < G / 4; ++q) {
+        const float4 v = src[q];
+        s += (v.x + v.y) + (v.z + v.w);
+      }
+      const float dot = seg_sum_dpp<L>(s);
+      // 3. loss + multiplier, one row per segment
+      const bool valid = g0 + gi * W < end;
+      A l, m;
+      const A wu = has_wt ? wl : (A)1;
+      loss_and_mult(loss, dot, yl, wu, l, m);
+      if (!valid) { l = (A)0; m = (A)0; }
+      if (seg == 0) {
+        wsum += valid ? wu : (A)0;
+        lsum += l;
+      }
+      // 4. gradient axpy with the G multipliers (wave-uniform scalars). The rows are widened
+      // again from the raw dwords (2 VALU per pair) instead of keeping G·16 widened floats live
+      // across the reduction: the empty asm hides the raw registers' identity from CSE.
+#pragma unroll
+      for (int i = 0; i < G; ++i)
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+          uint32_t* q = reinterpret_cast<uint32_t*>(x[i][k].v);
+#pragma unroll
+          for (int j = 0; j < EPC / 2; ++j) asm volatile("" : "+v"(q[j]));
+        }
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        const float mi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m), i * L));
+        const f2_t m2 = {mi, mi};
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+#pragma unroll
+          for (int q = 0; q < EPC / 2; ++q) acc2[k][q] = __builtin_elementwise_fma(m2, unpack(x[i][k], q), acc2[k][q]);
+      }
+    };
+    long g0 = r0w;
+    if (g0 < end) {
+      load_group(g0, xa, yla, wla);
+      load_w();
+      while (true) {
+        load_group(g0 + stepg, xb, ylb, wlb);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        process_group(g0, xa, yla, wla);
+        g0 += stepg;
+        if (g0 >= end) break;
+        load_group(g0 + stepg, xa, yla, wla);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        process_group(g0, xb, ylb, wlb);
+        g0 += stepg;
+        if (g0 >= end) break;
+      }
+    }
+    // Σweight / Σloss were accumulated by the segment-leader lanes: lane 0 reports the wave's
+    wsum = wave_sum_dpp(wsum);
+    lsum = wave_sum_dpp(lsum);
+  } else {
   const long step = (long)U * W;
   long r = start + gw;
   long j = 0;
@@ -477,6 +660,17 @@ __global__ __launch_bounds__(WPB * 64, (glm_min_waves<T, EPC, CPL, U>())) void g
       j += U;
       if (r >= end) break;
     }
+  }
+  }  // classic row-at-a-time path
+
+  if constexpr (kPacked) {
+#pragma unroll
+    for (int k = 0; k < CPL; ++k)
+#pragma unroll
+      for (int i = 0; i < EP; ++i) {
+        acc[k][2 * i] = acc2[k][i].x;
+        acc[k][2 * i + 1] = acc2[k][i].y;
+      }
   }
 
   extern __shared__ __align__(16) unsigned char smem_raw[];
@@ -1007,7 +1201,7 @@ static int g_nt = -1;
 constexpr long LDS_PER_CU = 160 * 1024;
 constexpr int NUM_CU = 256;
 
-template <typename T, int EPC, int CPL, int U>
+template <typename T, int EPC, int CPL, int U, int G = 0>
 int launch_grad_u(const void* X, long ld, const void* y, const void* wt, void* coef, long n, int d, long B, int loss,
                   int* state, void* partials, int nblocks, const GlmTail& tl, int flags, hipStream_t s) {
   typedef typename AccOf<T>::type A;
@@ -1025,15 +1219,20 @@ int launch_grad_u(const void* X, long ld, const void* y, const void* wt, void* c
       if (shmem < want) shmem = want;
     }
   }
+  if constexpr (G > 0) {
+    // grouped path: per-wave [G][64] fp32 transpose scratch after the epilogue's buffers
+    t2.red_off = (int)((shmem + 15) & ~(size_t)15);
+    shmem = (size_t)t2.red_off + (size_t)WPB * G * 64 * sizeof(float);
+  }
   const bool nt = g_nt >= 0 ? g_nt != 0 : (flags & 1) != 0;
   if constexpr (EPC * sizeof(T) == 16 && sizeof(T) == 2) {
     if (nt) {
-      hipLaunchKernelGGL((glm_round_kernel<T, EPC, CPL, U, WPB, true>), dim3(nblocks), dim3(WPB * 64), shmem, s,
+      hipLaunchKernelGGL((glm_round_kernel<T, EPC, CPL, U, WPB, true, G>), dim3(nblocks), dim3(WPB * 64), shmem, s,
                          (const T*)X, ld, (const A*)y, (const A*)wt, (A*)coef, n, d, B, loss, state, (A*)partials, t2);
       return (int)hipGetLastError();
     }
   }
-  hipLaunchKernelGGL((glm_round_kernel<T, EPC, CPL, U, WPB, false>), dim3(nblocks), dim3(WPB * 64), shmem, s,
+  hipLaunchKernelGGL((glm_round_kernel<T, EPC, CPL, U, WPB, false, G>), dim3(nblocks), dim3(WPB * 64), shmem, s,
                      (const T*)X, ld, (const A*)y, (const A*)wt, (A*)coef, n, d, B, loss, state, (A*)partials, t2);
   return (int)hipGetLastError();
 }
@@ -1043,7 +1242,17 @@ template <typename T, int EPC, int CPL>
 int launch_grad(int u, const void* X, long ld, const void* y, const void* wt, void* coef, long n, int d, long B,
                 int loss, int* state, void* partials, int nblocks, const GlmTail& tl, int flags, hipStream_t s) {
   constexpr int BYTES = CPL * EPC * (int)sizeof(T);
-  if (u == 0) u = BYTES <= 64 ? 2 : 1;
+  // grouped path (bf16, 16-byte chunks, d ≤ 2048): default; u = -4 / -8 forces G, u > 0 the
+  // row-at-a-time loop with U rows per step
+  if constexpr (sizeof(T) == 2 && EPC == 8 && CPL <= 4) {
+    if (u <= 0) {
+      const int g = u < 0 ? -u : (CPL <= 2 ? 8 : 4);
+      if (g == 8 && CPL <= 2)
+        return launch_grad_u<T, EPC, CPL, 1, 8>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
+      return launch_grad_u<T, EPC, CPL, 1, 4>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
+    }
+  }
+  if (u <= 0) u = BYTES <= 64 ? 2 : 1;
   if (u >= 4 && BYTES <= 32)
     return launch_grad_u<T, EPC, CPL, 4>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
   if (u >= 2 && BYTES <= 64)
@@ -1134,7 +1343,7 @@ FMLX_API int fmlx_glm_round(int dtype, int epc, int cpl, int u, const void* X, l
                             int mode, int det, int* cnt, void* acc, void* stage1, void* feedback, int max_iter,
                             double tol, double lr,
                             double reg, double en, void* const* peers, int world, int rank, int* gen, int* err,
-                            long spin_limit, int flags, void* stream) {
+                            long spin_limit, int flags, int rounds, void* stream) {
   if (mode != TAIL_PARTIALS && cnt == nullptr) return -4;
   if (mode != TAIL_PARTIALS && det && (nblocks > TAIL_GROUP * TAIL_MAXG || stage1 == nullptr)) return -4;
   if (mode != TAIL_PARTIALS && !det && (nblocks > TAIL_GROUP * TAIL_TOP || acc == nullptr)) return -4;
@@ -1153,8 +1362,14 @@ FMLX_API int fmlx_glm_round(int dtype, int epc, int cpl, int u, const void* X, l
   tl.reg = reg;
   tl.en = en;
   tl.x = xgmi::Ctx{peers, world, rank, gen, err, spin_limit};
-  return launch_round(dtype, epc, cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags,
-                      (hipStream_t)stream);
+  // `rounds` consecutive rounds, one launch each (a kernel boundary, ~1.5 µs, is cheaper than an
+  // in-kernel grid-wide round barrier: measured, scripts/stream_probe2.hip)
+  for (int i = 0; i < (rounds > 0 ? rounds : 1); ++i) {
+    const int rc = launch_round(dtype, epc, cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl,
+                                flags, (hipStream_t)stream);
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 // stage1 scratch: [ceil(nparts/16)][d+2] of the accumulator type (nparts <= 512)

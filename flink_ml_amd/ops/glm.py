@@ -16,7 +16,9 @@ from . import native
 LOSS_CODES = {"logistic": 0, "hinge": 1, "leastsquare": 2, "ftrl": 3}
 MAX_CPL = 8
 WPB = 8
-# rows in flight per wave = 2*GRAD_UNROLL (0 = kernel default for the shape); tunable for A/B runs
+# row loop of the round kernel (A/B knob): 0 = default for the shape (bf16 rows of 16-byte chunks:
+# the grouped path, 8 rows per step), -4 / -8 = grouped with 4 / 8 rows, U > 0 = row-at-a-time
+# with 2·U rows in flight per wave
 GRAD_UNROLL = int(os.environ.get("FMLX_GLM_UNROLL", "0"))
 GRAD_BLOCKS = int(os.environ.get("FMLX_GLM_BLOCKS", "256"))
 
@@ -102,9 +104,10 @@ class RoundScratch:
 
 def glm_round(X, y, wt, coef, B: int, loss: int, state, scratch: RoundScratch, mode: int, feedback=None,
               max_iter: int = 1, tol: float = 0.0, lr: float = 0.0, reg: float = 0.0, en: float = 0.0,
-              xg=None) -> None:
-    """One SGD round (loss+gradient over the round's batch, fixed-order reduction and — by mode —
-    feedback output, update, or xGMI exchange + update) as ONE kernel launch."""
+              xg=None, rounds: int = 1) -> None:
+    """``rounds`` SGD rounds (loss+gradient over the round's batch, fixed-order reduction and — by
+    mode — feedback output, update, or xGMI exchange + update), each ONE kernel launch predicated
+    on the device running flag (one host call issues all ``rounds`` launches)."""
     epc, cpl = pick_layout(X)
     flags = 1 if X.shape[0] * X.stride(0) * X.element_size() > NT_MIN_BYTES else 0
     if xg is not None:
@@ -115,7 +118,7 @@ def glm_round(X, y, wt, coef, B: int, loss: int, state, scratch: RoundScratch, m
                 native.ptr(y), native.ptr(wt), native.ptr(coef), X.shape[0], X.shape[1], B, loss, native.ptr(state),
                 native.ptr(scratch.partials), scratch.nparts, mode, int(scratch.det), native.ptr(scratch.cnt),
                 native.ptr(scratch.acc), native.ptr(scratch.stage1), native.ptr(feedback), int(max_iter), float(tol), float(lr), float(reg),
-                float(en), peers, world, rank, gen, err, int(spin), flags, native.stream_ptr(X.device))
+                float(en), peers, world, rank, gen, err, int(spin), flags, int(rounds), native.stream_ptr(X.device))
 
 
 def reduce_update(partials, nparts: int, d: int, stage1, coef, feedback, state, max_iter, tol, lr, reg, en) -> None:

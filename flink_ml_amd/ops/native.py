@@ -49,7 +49,8 @@ _KERNEL_SIGS = {
     "fmlx_glm_round": [c_int, c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_long, c_int,
                        c_long, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                        c_int, c_double,
-                       c_double, c_double, c_double, c_void_p, c_int, c_int, c_void_p, c_void_p, c_long, c_int, c_void_p],
+                       c_double, c_double, c_double, c_void_p, c_int, c_int, c_void_p, c_void_p, c_long, c_int, c_int,
+                       c_void_p],
     "fmlx_glm_set_tuning": [c_long, c_int],
     "fmlx_glm_reduce_update": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                c_double, c_double, c_double, c_double, c_void_p],

@@ -156,10 +156,8 @@ def all_to_all_v(chunks: Sequence[torch.Tensor]) -> List[torch.Tensor]:
     tail = tuple(ref.shape[1:])
     inp = torch.cat(send, dim=0) if send else torch.zeros((0,) + tail, dtype=ref.dtype, device=dev)
     out = torch.empty((int(recv_sizes.sum().item()),) + tail, dtype=ref.dtype, device=dev)
-    if ctx.backend == "gloo":
-        # gloo has no all_to_all_single; emulate with all_gather of padded buffers
-        gathered = all_gather_object([c.cpu() for c in send])
-        return [g[ctx.rank].to(ref.device) for g in gathered]
+    # one exchange of the payload on both backends (gloo implements all_to_all_single with
+    # uneven splits for CPU tensors; RCCL for device tensors)
     dist.all_to_all_single(out, inp, output_split_sizes=recv_sizes.tolist(), input_split_sizes=sizes.tolist())
     return [p.to(ref.device) for p in torch.split(out, recv_sizes.tolist(), dim=0)]
 

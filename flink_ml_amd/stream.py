@@ -105,36 +105,46 @@ class StreamTable:
 
 
 def _prefetch(it: Iterator[Table], dev) -> Iterator[Table]:
+    """Copies batch k+1 host→device on a side stream while batch k is consumed. The device
+    copies are allocated on the side stream, so each is marked used by the consumer stream
+    (``record_stream``) before it is handed out: the caching allocator then cannot give its
+    blocks to a later side-stream copy while consumer kernels still read them."""
     side = torch.cuda.Stream(dev)
     nxt = None
 
     def issue(t):
         if t is None:
             return None
+        fresh = []
         with torch.cuda.stream(side):
             cols = {}
             for k, c in t._cols.items():
                 if isinstance(c, torch.Tensor) and c.device.type == "cpu":
                     cols[k] = c.pin_memory().to(dev, non_blocking=True)
+                    fresh.append(cols[k])
                 elif isinstance(c, SparseColumn) and c.values.device.type == "cpu":
                     cols[k] = c.to(dev)
+                    fresh.extend([cols[k].indptr, cols[k].indices, cols[k].values])
                 else:
                     cols[k] = c
             ev = torch.cuda.Event()
             ev.record(side)
-        return Table(cols, num_rows=t.num_rows), ev
+        return Table(cols, num_rows=t.num_rows), ev, fresh
 
     try:
         nxt = issue(next(it))
     except StopIteration:
         return
     while nxt is not None:
-        cur, ev = nxt
+        cur, ev, fresh = nxt
+        consumer = torch.cuda.current_stream(dev)
+        consumer.wait_event(ev)
+        for t in fresh:
+            t.record_stream(consumer)
         try:
             nxt = issue(next(it))
         except StopIteration:
             nxt = None
-        torch.cuda.current_stream(dev).wait_event(ev)
         yield cur
 
 

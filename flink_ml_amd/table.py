@@ -194,7 +194,10 @@ class StringArrayColumn:
                 return self.to_lists()[i]
             stop = max(stop, start)
             b = self.offsets[[start, stop]].cpu()
-            return StringArrayColumn(self.offsets[start:stop + 1], self.codes[int(b[0]):int(b[1])], self.vocab)
+            # self-consistent slice: offsets rebased onto the cut codes (offsets[0] == 0), so a
+            # slice of a slice and row indexing of a slice read the right codes
+            off = self.offsets[start:stop + 1]
+            return StringArrayColumn(off - off[:1], self.codes[int(b[0]):int(b[1])], self.vocab)
         i = int(i)
         if i < 0:
             i += len(self)
@@ -202,7 +205,8 @@ class StringArrayColumn:
         return [self.vocab[c] for c in self.codes[int(b[0]):int(b[1])].cpu().tolist()]
 
     def rebased(self) -> "StringArrayColumn":
-        """The same rows with offsets starting at 0 (slices keep the parent's offsets)."""
+        """The same rows with offsets starting at 0 (a no-op for slices, which are rebased; kept for
+        columns built with an offset base)."""
         o0 = self.offsets[:1]
         return StringArrayColumn(self.offsets - o0, self.codes, self.vocab)
 

@@ -33,7 +33,11 @@ def parse(cfgs):
 class SplitTrainer(DeviceGlmTrainer):
     """The pre-fusion round: 3 launches (kept for the A/B)."""
 
-    def _launch_round(self):
+    def _launch_round(self, rounds=1):
+        for _ in range(rounds):
+            self._split_round()
+
+    def _split_round(self):
         s = self.sgd
         sc = self.scratch
         gk.grad_partials(self.X, self.y, self.w, self.coef, self.B, self.loss, self.state, sc.partials, sc.nparts)
@@ -73,7 +77,7 @@ def main():
             tr.mode0_only = bool(c.get("m0"))
             if cls is SplitTrainer:  # the split round needs the block-partials scratch
                 tr.scratch = gk.RoundScratch(tr.nparts, a.dim, torch.float32, dev, det=True)
-            tr.rounds_per_graph = 10
+            tr.rounds_per_graph = c.get("R", 10)
             tr.run_rounds(20)
             torch.cuda.synchronize()
             t0 = time.perf_counter()

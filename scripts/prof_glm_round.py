@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""Runs fused SGD rounds of the flagship shape (100k × 1000 bf16 batch, 10M rows) for a profiler:
+``--unroll`` picks the row loop (see ops/glm.py GRAD_UNROLL), ``--blocks`` the grid."""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer  # noqa: E402
+from flink_ml_amd.ops import glm as gk  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=10_000_000)
+    ap.add_argument("--dim", type=int, default=1000)
+    ap.add_argument("--batch", type=int, default=100_000)
+    ap.add_argument("--rounds", type=int, default=30)
+    ap.add_argument("--unroll", type=int, default=0)
+    ap.add_argument("--blocks", type=int, default=256)
+    a = ap.parse_args()
+    gk.GRAD_UNROLL, gk.GRAD_BLOCKS = a.unroll, a.blocks
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(1)
+    X = torch.empty((a.rows, a.dim), dtype=torch.bfloat16, device=dev)
+    for s in range(0, a.rows, 1 << 20):
+        e = min(s + (1 << 20), a.rows)
+        X[s:e] = torch.rand((e - s, a.dim), generator=g, device=dev).to(torch.bfloat16)
+    y = torch.randint(0, 2, (a.rows,), generator=g, device=dev).float()
+    tr = DeviceGlmTrainer(SGD(max_iter=10 ** 6, global_batch_size=a.batch, tol=0.0), np.zeros(a.dim), X, y, None,
+                          "logistic", use_graph=False)
+    tr.run_rounds(a.rounds)
+    torch.cuda.synchronize()
+    print("rounds", tr.rounds_executed())
+
+
+if __name__ == "__main__":
+    main()

@@ -74,3 +74,20 @@ def test_labeled_point_with_weight_table_roundtrip():
     back = LabeledPointWithWeight.from_table(t, weight_col="weight")
     assert [(p.get_label(), p.get_weight()) for p in back] == [(1.0, 0.5), (0.0, 1.0)]
     assert back[1].get_features() == Vectors.dense(3.0, 4.0)
+
+
+def _a2a_worker(rank, world):
+    import torch
+
+    from flink_ml_amd.parallel import comm
+
+    # rank r sends (r + 1) * (dst + 1) rows of width 3 to every dst, filled with 100 r + dst
+    chunks = [torch.full(((rank + 1) * (dst + 1), 3), float(100 * rank + dst)) for dst in range(world)]
+    got = comm.all_to_all_v(chunks)
+    return [(tuple(g.shape), float(g[0, 0]) if g.numel() else None) for g in got]
+
+
+def test_all_to_all_v_uneven_splits():
+    res = run_spmd(_a2a_worker, 3)
+    for dst, recv in enumerate(res):
+        assert recv == [(((src + 1) * (dst + 1), 3), float(100 * src + dst)) for src in range(3)]

@@ -160,3 +160,18 @@ def test_string_stages_run_on_device():
     _, tc = _both()
     out = StopWordsRemover().set_input_cols("input").set_output_cols("output").transform(tc)[0].column("output")
     assert out.codes.device.type == "cuda"
+
+
+def test_string_array_slice_of_slice_and_indexing():
+    """slicing a sliced StringArrayColumn and indexing rows of a slice read the right codes."""
+    from flink_ml_amd.table import StringArrayColumn
+
+    rows = [["a", "b"], [], ["c"], ["d", "e", "f"], ["g"], ["h", "i"], []]
+    col = StringArrayColumn.from_lists(rows)
+    s1 = col[2:7]
+    assert s1.to_lists() == rows[2:7]
+    s2 = s1[1:4]
+    assert s2.to_lists() == rows[3:6]
+    assert [s2[i] for i in range(len(s2))] == rows[3:6]
+    assert s1[3] == rows[5] and s1[-1] == rows[6]
+    assert s2[1:2].to_lists() == [rows[4]]

@@ -91,16 +91,19 @@ def test_fused_sgd_round_two_ranks_matches_host(xgmi_mode):
         assert b0 == r1[loss][2], loss  # replicas identical
 
 
-@pytest.mark.parametrize("det", [False, True])
-def test_fused_round_flagship_shape_matches_torch(det, monkeypatch):
-    """Fused rounds (TAIL_UPDATE) at the bench shape, bf16 rows: 512 blocks with the atomic tail
-    and with the deterministic 16-group fixed-order tail."""
+@pytest.mark.parametrize("det,blocks,unroll", [(False, 256, 0), (False, 256, -4), (False, 256, 2), (False, 512, 0),
+                                               (True, 512, 0), (True, 256, 1)])
+def test_fused_round_flagship_shape_matches_torch(det, blocks, unroll, monkeypatch):
+    """Fused rounds (TAIL_UPDATE) at the bench shape, bf16 rows: the bench's 256-block grid and
+    512 blocks, the grouped row loop (8 / 4 rows per step) and the row-at-a-time loop, atomic
+    tail and the deterministic 16-group fixed-order tail."""
     _need_gpu()
     from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
     from flink_ml_amd.ops import glm as gk
 
     monkeypatch.setattr(gk, "DETERMINISTIC", det)
-    monkeypatch.setattr(gk, "GRAD_BLOCKS", 512)
+    monkeypatch.setattr(gk, "GRAD_BLOCKS", blocks)
+    monkeypatch.setattr(gk, "GRAD_UNROLL", unroll)
 
     g = torch.Generator(device="cpu").manual_seed(7)
     n, d, B = 200_000, 1000, 100_000
@@ -109,10 +112,34 @@ def test_fused_round_flagship_shape_matches_torch(det, monkeypatch):
     sgd = SGD(max_iter=3, learning_rate=0.1, global_batch_size=B, tol=1e-9)
     ref = TorchGlmTrainer(sgd, np.zeros(d), Xb.to(torch.float64), y, None, "logistic").fit()
     tr = DeviceGlmTrainer(sgd, np.zeros(d), Xb.cuda(), y.cuda(), None, "logistic", use_graph=False)
-    assert tr.nparts == 512 and tr.scratch.det == det
+    assert tr.nparts == blocks and tr.scratch.det == det
     got = tr.fit()
     assert tr.rounds_executed() == 3
     assert np.allclose(got, ref, rtol=2e-4, atol=2e-6), np.abs(got - ref).max()
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_multi_round_launch_terminates_mid_way(graph):
+    """One host call issuing many rounds (and a replayed 16-round hipGraph) stops exactly where
+    TerminateOnMaxIterOrTol says, even in the middle of the call."""
+    _need_gpu()
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
+
+    g = torch.Generator(device="cpu").manual_seed(3)
+    n, d, B = 60_000, 64, 20_000
+    X = torch.rand((n, d), generator=g) - 0.5
+    y = (X @ torch.linspace(-1, 1, d) > 0).to(torch.float64)
+    ref_tr = TorchGlmTrainer(SGD(max_iter=40, learning_rate=2.0, global_batch_size=B, tol=0.4), np.zeros(d),
+                             X.to(torch.float64), y, None, "logistic")
+    ref = ref_tr.fit()
+    assert 16 < ref_tr.rounds < 32, ref_tr.rounds  # stops inside the second 16-round call / graph
+    sgd = SGD(max_iter=40, learning_rate=2.0, global_batch_size=B, tol=0.4)
+    tr = DeviceGlmTrainer(sgd, np.zeros(d), X.cuda(), y.cuda(), None, "logistic", use_graph=graph)
+    tr.rounds_per_graph = 16
+    tr.run_rounds(40)
+    torch.cuda.synchronize()
+    assert tr.rounds_executed() == ref_tr.rounds
+    assert np.allclose(tr.coef.double().cpu().numpy(), ref, rtol=1e-4, atol=1e-6)
 
 
 def _timeout_worker(rank, world):
