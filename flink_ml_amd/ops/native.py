@@ -119,6 +119,7 @@ def kernels():
                     _build.build_kernels()
                 else:
                     raise RuntimeError("native kernel library missing: %s (run python -m flink_ml_amd.ops.build)" % path)
+            _build.check_fresh("kernels")  # never load a binary built from other sources
             lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
             _apply_sigs(lib, _KERNEL_SIGS)
             _KLIB = lib
@@ -132,9 +133,12 @@ def host():
         return _HLIB
     with _LOCK:
         if _HLIB is None:
-            path = _build.HOST_LIB
+            # FMLX_HOST_LIB: an alternative build of the host runtime (the ASan/UBSan one in tests)
+            path = os.environ.get("FMLX_HOST_LIB") or _build.HOST_LIB
             if not os.path.exists(path):
                 _build.build_host()
+            if path == _build.HOST_LIB:
+                _build.check_fresh("host")
             lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
             _apply_sigs(lib, _HOST_SIGS, restype=None)
             _HLIB = lib
