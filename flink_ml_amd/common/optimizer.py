@@ -141,6 +141,8 @@ class TorchGlmTrainer:
             self._apply(fb)
             W, L = float(fb[self.d]), float(fb[self.d + 1])
             crit = L / W if W != 0 else float("nan")
+            tracing.log_round(kind="sgd", path="host", rank=get_context().rank, epoch=e, loss=L, weight=W,
+                              bytes=int(fb.numel() * fb.element_size()))
             cont = e + 1 < self.sgd.max_iter and crit > self.sgd.tol
             ck.maybe_save(e + 1, lambda: {"coef": self.coef, "offset": self.offset, "rounds": self.rounds,
                                           "done": not cont})
@@ -371,12 +373,26 @@ class DeviceGlmTrainer:
             if st["done"]:
                 return self.coef.to(torch.float64).cpu().numpy()
         step = ck.interval if ck.interval else self.check_every
+        log = tracing.rounds_enabled()
         with tracing.range("sgd.fit"):
             while done < self.sgd.max_iter:
                 fault_point(done)
                 k = min(step, self.sgd.max_iter - done)
-                self.run_rounds(k)
+                if log:
+                    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    ev0.record()
+                with tracing.range("sgd.rounds[%d]" % k):
+                    self.run_rounds(k)
                 done += k
+                if log:
+                    # the device keeps the last round's global feedback [Σg | Σw | Σloss]
+                    ev1.record()
+                    fb = self.feedback[self.d:self.d + 2].double().cpu()
+                    tracing.log_round(kind="sgd", path="device", rank=self.ctx.rank, epoch=self.rounds_executed() - 1,
+                                      rounds=k, loss=float(fb[1]), weight=float(fb[0]),
+                                      kernel_ms=round(ev0.elapsed_time(ev1), 4),
+                                      bytes_per_round=int(self.B * (self.d * self.X.element_size() if not self.sparse
+                                                                    and not self.wide else 0)))
                 stop = done < self.sgd.max_iter and not self.running()
                 ck.maybe_save(done, lambda: {"coef": self.coef, "state": self.state,
                                              "done": stop or done >= self.sgd.max_iter})

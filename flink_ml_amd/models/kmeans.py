@@ -156,12 +156,27 @@ def kmeans_lloyd(X: torch.Tensor, init: np.ndarray, max_iter: int, metric: str):
         if restored is not None:
             cb.weights.copy_(counts0.to(cb.weights.dtype))
         rnd = kk.KMeansRound(X, kc, metric)
+        log = tracing.rounds_enabled()
         with tracing.range("kmeans.fit"):
             for e in range(start, max_iter):
                 fault_point(e)
-                payload = rnd.run(cb)
-                comm.all_reduce_sum(payload)
-                rnd.finalize(cb, payload)
+                with tracing.range("kmeans.round"):
+                    if log:
+                        evs = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                        evs[0].record()
+                    payload = rnd.run(cb)
+                    if log:
+                        evs[1].record()
+                    comm.all_reduce_sum(payload)
+                    if log:
+                        evs[2].record()
+                    rnd.finalize(cb, payload)
+                if log:
+                    evs[2].synchronize()
+                    tracing.log_round(kind="kmeans", rank=get_context().rank, epoch=e,
+                                      kernel_ms=round(evs[0].elapsed_time(evs[1]), 4),
+                                      collective_ms=round(evs[1].elapsed_time(evs[2]), 4),
+                                      bytes=int(payload.numel() * payload.element_size()))
                 ck.maybe_save(e + 1, lambda: {"centroids": cb.cent.to(torch.float64), "weights": cb.weights})
         out = cb.cent.to(torch.float64).cpu().numpy(), cb.weights.cpu().numpy()
         comm.check_collectives()  # after the host sync: no round used a partial xGMI exchange

@@ -135,7 +135,11 @@ struct GlmTail {
   double tol, lr, reg, en;
   xgmi::Ctx x;     // TAIL_XGMI only
   int red_off;     // byte offset of the grouped row path's per-wave reduction scratch in LDS
+  int acc_reps;    // atomic tail: replicas of `acc` (block b adds into replica b mod acc_reps)
+  long acc_ld;     // elements between replicas (d + 2 rounded up to whole 256-B lines)
+  int ticket2;     // atomic tail: two-level arrival tickets (per-residue groups, then a top one)
 };
+constexpr int ACC_MAX_REPS = 8;
 
 // Write-through (sc1) hand-off of the partial rows (cdna_hip_programming.md Guideline 16, the
 // sc1 form of the split-K combine): every handed-off value is stored with an agent-scope store
@@ -293,25 +297,48 @@ __device__ void glm_round_tail_atomic(const GlmTail& tl, int d, A* coef, int* st
   const long stride = d + 2;
   const int nt = blockDim.x;
   A* acc = (A*)tl.acc;
-  // one ticket over all blocks: arrivals are spread over the blocks' finishing times, so a single
-  // counter costs the last block one atomic round trip instead of two
-  if (!arrive_last(&tl.cnt[0], gridDim.x, sflag)) return;
-  if (threadIdx.x == 0) tl.cnt[0] = 0;
+  const int R = tl.acc_reps > 1 ? tl.acc_reps : 1;
+  const long ald = tl.acc_ld > 0 ? tl.acc_ld : stride;
+  if (tl.ticket2) {
+    // two levels: the blocks of one residue class b mod R (one XCD under round-robin dispatch)
+    // share a counter, the last of each class draws the top ticket — no counter takes more than
+    // ceil(nb / R) arrivals at once
+    const int nb = gridDim.x;
+    const int g = blockIdx.x % R;
+    const int gs = nb / R + (g < nb % R ? 1 : 0);
+    if (!arrive_last(&tl.cnt[g], gs, sflag)) return;
+    if (threadIdx.x == 0) st_agent(&tl.cnt[g], 0);
+    if (!arrive_last(&tl.cnt[TAIL_TOP], nb < R ? nb : R, sflag)) return;
+    if (threadIdx.x == 0) st_agent(&tl.cnt[TAIL_TOP], 0);
+  } else {
+    // one ticket over all blocks: arrivals are spread over the blocks' finishing times, so a
+    // single counter costs the last block one atomic round trip instead of two
+    if (!arrive_last(&tl.cnt[0], gridDim.x, sflag)) return;
+    if (threadIdx.x == 0) tl.cnt[0] = 0;
+  }
   const bool one_pass = stride <= 2L * nt && tl.mode != TAIL_FEEDBACK;
   A wa = (A)0, wb = (A)0;
+  // Σ of the replicas in a fixed order (all R loads of a column in flight together), then re-zero
+  auto take = [&](long c) -> A {
+    A v[ACC_MAX_REPS];
+#pragma unroll
+    for (int q = 0; q < ACC_MAX_REPS; ++q) v[q] = q < R ? ld_agent(acc + q * ald + c) : (A)0;
+    A t = (A)0;
+#pragma unroll
+    for (int q = 0; q < ACC_MAX_REPS; ++q) t += v[q];
+#pragma unroll
+    for (int q = 0; q < ACC_MAX_REPS; ++q)
+      if (q < R) st_agent(acc + q * ald + c, (A)0);
+    return t;
+  };
   if (one_pass) {
     const long ca = threadIdx.x, cb = threadIdx.x + nt;
-    const A a0 = ld_agent(acc + ca);
-    const A a1 = ld_agent(acc + (cb < stride ? cb : ca));
     wa = coef[ca < d ? ca : 0];
     wb = coef[cb < d ? cb : 0];
-    if (ca < stride) { sbuf[ca] = a0; st_agent(acc + ca, (A)0); }
-    if (cb < stride) { sbuf[cb] = a1; st_agent(acc + cb, (A)0); }
+    if (ca < stride) sbuf[ca] = take(ca);
+    if (cb < stride) sbuf[cb] = take(cb);
   } else {
-    for (long c = threadIdx.x; c < stride; c += nt) {
-      sbuf[c] = ld_agent(acc + c);
-      st_agent(acc + c, (A)0);
-    }
+    for (long c = threadIdx.x; c < stride; c += nt) sbuf[c] = take(c);
   }
   glm_round_finish<A>(tl, sbuf, d, coef, state, e, one_pass, wa, wb);
 }
@@ -692,7 +719,9 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
         for (int i = 0; i < EPC; ++i) mine[c * EPC + i] = acc[k][i];
     }
     __syncthreads();
-    A* gacc = (A*)tl.acc;
+    // replica b mod acc_reps: at most ceil(nb / reps) adders per address (float atomics keep
+    // their full rate up to ~32 adders per address; 256 on one 4 KB row serialise)
+    A* gacc = (A*)tl.acc + (long)(blockIdx.x % (tl.acc_reps > 1 ? tl.acc_reps : 1)) * tl.acc_ld;
     const long stride = d + 2;
     for (long c = threadIdx.x; c < stride; c += blockDim.x) {
       A v = (A)0;
@@ -753,7 +782,7 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
       }
     }
     __syncthreads();
-    A* gacc = (A*)tl.acc;
+    A* gacc = (A*)tl.acc + (long)(blockIdx.x % (tl.acc_reps > 1 ? tl.acc_reps : 1)) * tl.acc_ld;
     for (long c = threadIdx.x; c < d + 2; c += blockDim.x) atomicAdd(gacc + c, buf[c]);
     glm_round_tail_atomic<A>(tl, d, coef, state, e, buf, sflag);
     return;
@@ -1198,6 +1227,8 @@ constexpr int WPB = 8;
 // Non-temporal row loads (`flags & 1`) for batches streamed once per pass (−12 %, measured).
 static long g_lds_pad = -1;
 static int g_nt = -1;
+static int g_acc_reps = 8;  // atomic-tail accumulator replicas (A/B knob, <= ACC_MAX_REPS)
+static int g_ticket2 = 0;   // two-level tickets (A/B knob)
 constexpr long LDS_PER_CU = 160 * 1024;
 constexpr int NUM_CU = 256;
 
@@ -1326,6 +1357,16 @@ FMLX_API int fmlx_glm_set_tuning(long lds_pad, int nt) {
   return 0;
 }
 
+FMLX_API int fmlx_glm_set_tail_tuning(int acc_reps, int ticket2) {
+  if (acc_reps < 1 || acc_reps > ACC_MAX_REPS) return -1;
+  g_acc_reps = acc_reps;
+  g_ticket2 = ticket2;
+  return 0;
+}
+
+// elements of the atomic-tail accumulator for row width d + 2 (all replicas)
+FMLX_API long fmlx_glm_acc_elems(int d) { return (long)ACC_MAX_REPS * (((long)d + 2 + 63) / 64 * 64); }
+
 FMLX_API int fmlx_glm_grad_partials(int dtype, int epc, int cpl, int u, const void* X, long ld, const void* y,
                                     const void* wt, const void* coef, long n, int d, long B, int loss, const int* state,
                                     void* partials, int nblocks, void* stream) {
@@ -1355,6 +1396,9 @@ FMLX_API int fmlx_glm_round(int dtype, int epc, int cpl, int u, const void* X, l
   tl.det = det;
   tl.cnt = cnt;
   tl.acc = acc;
+  tl.acc_reps = g_acc_reps;
+  tl.acc_ld = ((long)d + 2 + 63) / 64 * 64;
+  tl.ticket2 = g_ticket2;
   tl.stage1 = stage1;
   tl.feedback = feedback;
   tl.tol = tol;

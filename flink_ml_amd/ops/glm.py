@@ -34,6 +34,12 @@ def set_tuning(lds_pad: int = -1, nt: int = -1) -> None:
     native.call("fmlx_glm_set_tuning", int(lds_pad), int(nt))
 
 
+def set_tail_tuning(acc_reps: int = 8, ticket2: bool = False) -> None:
+    """A/B knobs of the atomic round tail: accumulator replicas (block b adds into replica
+    b mod reps) and two-level arrival tickets."""
+    native.call("fmlx_glm_set_tail_tuning", int(acc_reps), int(bool(ticket2)))
+
+
 def pick_layout(X: torch.Tensor) -> Optional[Tuple[int, int]]:
     """(epc, cpl) for the register-resident path, or None if d is too wide / misaligned."""
     if X.dim() != 2:
@@ -98,7 +104,8 @@ class RoundScratch:
         else:
             self.partials = torch.zeros((1, d + 2), dtype=acc, device=device)
             self.stage1 = None
-        self.acc = torch.zeros(d + 2, dtype=acc, device=device)
+        # atomic tail: ACC_MAX_REPS replicas of the [d+2] accumulator on whole 256-B lines
+        self.acc = torch.zeros(int(native.kernels().fmlx_glm_acc_elems(d)), dtype=acc, device=device)
         self.cnt = torch.zeros(80, dtype=torch.int32, device=device)  # 64 group + 1 top tickets
 
 

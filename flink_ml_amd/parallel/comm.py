@@ -29,6 +29,7 @@ from typing import Any, List, Optional, Sequence
 import torch
 import torch.distributed as dist
 
+from ..utils import tracing
 from .context import get_context
 
 
@@ -48,6 +49,13 @@ def all_reduce(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
     ctx = get_context()
     if not ctx.is_distributed:
         return t
+    if tracing.enabled():  # roctx range per collective (name carries op and bytes)
+        with tracing.range("allreduce.%s[%dB]" % (op, t.numel() * t.element_size())):
+            return _all_reduce(t, op, ctx)
+    return _all_reduce(t, op, ctx)
+
+
+def _all_reduce(t: torch.Tensor, op: str, ctx) -> torch.Tensor:
     if op == "sum" and t.is_cuda:
         from . import xgmi
 

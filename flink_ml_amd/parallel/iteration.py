@@ -24,8 +24,15 @@ and the termination decision is one all-reduce of two record counts. Semantics k
 * ``OperatorLifeCycle.ALL_ROUND`` keeps one body instance for all rounds; ``PER_ROUND`` builds
   a fresh body (operator state reset) every round from a factory.
 * Unbounded iterations consume an input stream of mini-batches and run until it ends.
-* Round-level checkpoints: ``checkpoint_fn`` / ``restore`` hooks let ``parallel.checkpoint``
-  persist (variables, epoch, body state) every N rounds and resume after a failure.
+* side outputs: ``context.output(tag, record)`` — from the body or from a listener callback
+  (``IterationListener.Context.output``, ``IterationListener.java:66-73``) — is delivered as a
+  named stream of the returned ``IterationResult`` (``get_side_output(tag)``), in emission order.
+* Round-level checkpoints (bounded AND unbounded): a ``RoundCheckpointer`` persists (variables,
+  epoch, outputs, side outputs) every N rounds; an unbounded run also records how many input
+  batches it consumed and skips them on resume (the source replays from the start, like a
+  checkpointed Flink source rewinding to its offset).
+* Observability: each round is a roctx range (``FMLX_TRACE=1``) and, with
+  ``FMLX_LOG_ROUNDS=1``, one structured JSON log line (rank, epoch, fed-back records, ms).
 """
 from __future__ import annotations
 
@@ -33,7 +40,10 @@ import enum
 from dataclasses import dataclass, field
 from typing import Any, Callable, Iterable, Iterator, List, Optional, Sequence
 
+import time
+
 from . import comm
+from ..utils import tracing
 
 
 class OperatorLifeCycle(enum.Enum):
@@ -71,6 +81,19 @@ class DataStreamList(list):
 
     def get(self, i: int):
         return self[i]
+
+
+class IterationResult(DataStreamList):
+    """The output streams of an iteration plus its side outputs by tag."""
+
+    def __init__(self, outputs, side_outputs=None):
+        super().__init__(outputs)
+        self.side_outputs = dict(side_outputs or {})
+
+    def get_side_output(self, tag: str) -> list:
+        return list(self.side_outputs.get(tag, []))
+
+    getSideOutput = get_side_output
 
 
 class ReplayableDataStreamList:
@@ -163,9 +186,10 @@ class Iterations:
 
     @staticmethod
     def iterate_unbounded_streams(init_variables: Sequence, data_batches: Iterable, body,
-                                  config: IterationConfig = None) -> DataStreamList:
+                                  config: IterationConfig = None,
+                                  checkpoint: Optional["RoundCheckpointer"] = None) -> DataStreamList:
         """One round per arriving mini-batch; terminates when the stream ends on any rank."""
-        return _run_unbounded(init_variables, data_batches, config or IterationConfig(), body)
+        return _run_unbounded(init_variables, data_batches, config or IterationConfig(), body, checkpoint)
 
     iterateBoundedStreamsUntilTermination = iterate_bounded_streams_until_termination
     iterateUnboundedStreams = iterate_unbounded_streams
@@ -182,9 +206,15 @@ def _make_body(body, config, epoch):
     return body()
 
 
+def _merge_side(side: dict, ctx: IterationContext) -> None:
+    for tag, recs in ctx.side_outputs.items():
+        side.setdefault(tag, []).extend(recs)
+    ctx.side_outputs = {}
+
+
 def _emit_listener_records(result: IterationBodyResult, outputs: List[list], epoch: int, terminated: bool,
                            ctx: IterationContext):
-    for item in result.listeners or ():
+    for item in (result.listeners or ()) if result is not None else ():
         listener, out_idx = item if isinstance(item, tuple) else (item, None)
         coll = Collector()
         if terminated:
@@ -198,11 +228,13 @@ def _emit_listener_records(result: IterationBodyResult, outputs: List[list], epo
 def _run_bounded(init_variables, data, config, body_or_factory, max_rounds, checkpoint):
     variables = DataStreamList(init_variables)
     outputs: List[list] = []
+    side: dict = {}
     epoch = 0
     if checkpoint is not None:
         restored = checkpoint.restore()
         if restored is not None:
             epoch, variables, outputs = restored["epoch"], DataStreamList(restored["variables"]), restored["outputs"]
+            side = restored.get("side", {})
     body = _make_body(body_or_factory, config, epoch)
     last_result = None
     while True:
@@ -214,38 +246,67 @@ def _run_bounded(init_variables, data, config, body_or_factory, max_rounds, chec
         ctx = IterationContext(epoch)
         streams = DataStreamList(list(data.replayed) + (list(data.non_replayed) if epoch == 0 else
                                                         [None] * len(data.non_replayed)))
-        result = body.process(variables, streams, ctx)
-        if not outputs:
-            outputs = [[] for _ in result.output_streams]
-        for i, o in enumerate(result.output_streams):
-            if o is not None:
-                outputs[i].extend(o if isinstance(o, list) else [o])
-        _emit_listener_records(result, outputs, epoch, False, ctx)
-        for tag, recs in ctx.side_outputs.items():
-            pass
-        n_feedback = sum(_count(s) for s in result.feedback_variable_streams)
-        n_crit = _count(result.termination_criteria) if result.termination_criteria is not None else -1
-        tot = comm.all_reduce_scalar(float(n_feedback), "sum")
-        crit_tot = comm.all_reduce_scalar(float(max(n_crit, 0)), "sum") if n_crit >= 0 else 1.0
+        t0 = time.perf_counter()
+        with tracing.range("iteration.round"):
+            result = body.process(variables, streams, ctx)
+            if not outputs:
+                outputs = [[] for _ in result.output_streams]
+            for i, o in enumerate(result.output_streams):
+                if o is not None:
+                    outputs[i].extend(o if isinstance(o, list) else [o])
+            _emit_listener_records(result, outputs, epoch, False, ctx)
+            _merge_side(side, ctx)
+            n_feedback = sum(_count(s) for s in result.feedback_variable_streams)
+            n_crit = _count(result.termination_criteria) if result.termination_criteria is not None else -1
+            # the coordinator's alignment (SharedProgressAligner): global record counts decide
+            tot, crit_tot = _global_counts(float(n_feedback), float(max(n_crit, 0)) if n_crit >= 0 else None)
+        tracing.log_round(kind="bounded", rank=ctx.rank, epoch=epoch, feedback_records=int(tot),
+                          criteria_records=None if crit_tot is None else int(crit_tot),
+                          ms=round((time.perf_counter() - t0) * 1e3, 3))
         last_result = result
         epoch += 1
         if tot == 0 or crit_tot == 0 or (max_rounds is not None and epoch >= max_rounds):
             break
         variables = DataStreamList(result.feedback_variable_streams)
         if checkpoint is not None:
-            checkpoint.maybe_save(epoch, variables, outputs)
+            checkpoint.maybe_save(epoch, variables, outputs, side=side)
     ctx = IterationContext(epoch)
     _emit_listener_records(last_result, outputs, epoch, True, ctx)
-    return DataStreamList(outputs)
+    _merge_side(side, ctx)
+    return IterationResult(outputs, side)
 
 
-def _run_unbounded(init_variables, data_batches, config, body_or_factory):
+def _global_counts(n_feedback: float, n_crit):
+    """ONE all-reduce of [feedback records, criteria records] (instead of one per count)."""
+    import torch
+
+    from .context import get_context
+
+    if not get_context().is_distributed:
+        return n_feedback, n_crit
+    t = torch.tensor([n_feedback, -1.0 if n_crit is None else n_crit], dtype=torch.float64)
+    comm.all_reduce_sum(t)
+    crit = None if n_crit is None else float(t[1])
+    return float(t[0]), crit
+
+
+def _run_unbounded(init_variables, data_batches, config, body_or_factory, checkpoint=None):
     variables = DataStreamList(init_variables)
     outputs: List[list] = []
+    side: dict = {}
     epoch = 0
     it: Iterator = iter(data_batches)
+    if checkpoint is not None:
+        restored = checkpoint.restore()
+        if restored is not None:
+            epoch, variables, outputs = restored["epoch"], DataStreamList(restored["variables"]), restored["outputs"]
+            side = restored.get("side", {})
+            for _ in range(epoch):  # the batches those rounds consumed (the source rewinds)
+                next(it, None)
     body = _make_body(body_or_factory, config, epoch)
     last_result = None
+    from .checkpoint import fault_point
+
     while True:
         try:
             batch = next(it)
@@ -254,22 +315,31 @@ def _run_unbounded(init_variables, data_batches, config, body_or_factory):
             batch, has = None, 0.0
         if comm.all_reduce_scalar(has, "min") == 0.0:
             break
+        fault_point(epoch)
         if config.operator_life_cycle == OperatorLifeCycle.PER_ROUND:
             body = _make_body(body_or_factory, config, epoch)
         ctx = IterationContext(epoch)
-        result = body.process(variables, DataStreamList([batch]), ctx)
-        if not outputs:
-            outputs = [[] for _ in result.output_streams]
-        for i, o in enumerate(result.output_streams):
-            if o is not None:
-                outputs[i].extend(o if isinstance(o, list) else [o])
-        _emit_listener_records(result, outputs, epoch, False, ctx)
+        t0 = time.perf_counter()
+        with tracing.range("iteration.round"):
+            result = body.process(variables, DataStreamList([batch]), ctx)
+            if not outputs:
+                outputs = [[] for _ in result.output_streams]
+            for i, o in enumerate(result.output_streams):
+                if o is not None:
+                    outputs[i].extend(o if isinstance(o, list) else [o])
+            _emit_listener_records(result, outputs, epoch, False, ctx)
+            _merge_side(side, ctx)
+        tracing.log_round(kind="unbounded", rank=ctx.rank, epoch=epoch, ms=round((time.perf_counter() - t0) * 1e3, 3))
         variables = DataStreamList(result.feedback_variable_streams)
         last_result = result
         epoch += 1
+        if checkpoint is not None:
+            checkpoint.maybe_save(epoch, variables, outputs, side=side)
     if last_result is not None:
-        _emit_listener_records(last_result, outputs, epoch, True, IterationContext(epoch))
-    return DataStreamList(outputs)
+        ctx = IterationContext(epoch)
+        _emit_listener_records(last_result, outputs, epoch, True, ctx)
+        _merge_side(side, ctx)
+    return IterationResult(outputs, side)
 
 
 class TerminateOnMaxIter(IterationListener):
@@ -327,7 +397,8 @@ class RoundCheckpointer:
         if r is None:
             return None
         epoch, st = r
-        return {"epoch": epoch, "variables": st["variables"], "outputs": st["outputs"]}
+        return {"epoch": epoch, "variables": st["variables"], "outputs": st["outputs"], "side": st.get("side", {})}
 
-    def maybe_save(self, epoch: int, variables, outputs) -> None:
-        self._ck.maybe_save(epoch, lambda: {"variables": list(variables), "outputs": [list(o) for o in outputs]})
+    def maybe_save(self, epoch: int, variables, outputs, side=None) -> None:
+        self._ck.maybe_save(epoch, lambda: {"variables": list(variables), "outputs": [list(o) for o in outputs],
+                                            "side": {k: list(v) for k, v in (side or {}).items()}})

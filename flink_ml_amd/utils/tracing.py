@@ -68,9 +68,29 @@ def records():
     return list(_RECORDS)
 
 
+_LOG_ROUNDS = os.environ.get("FMLX_LOG_ROUNDS", "0") == "1"
+_LOG_SINK = None  # file-like; default stderr
+
+
+def rounds_enabled() -> bool:
+    """Per-round structured logging is on (``FMLX_LOG_ROUNDS=1`` or ``log_rounds(True)``); callers
+    only then pay the device syncs / event timings a round record needs."""
+    return _LOG_ROUNDS
+
+
+def log_rounds(on: bool = True, sink=None) -> None:
+    global _LOG_ROUNDS, _LOG_SINK
+    _LOG_ROUNDS, _LOG_SINK = on, sink
+
+
 def log_round(**fields) -> None:
-    if os.environ.get("FMLX_LOG_ROUNDS", "0") == "1":
-        sys.stderr.write(json.dumps(fields) + "\n")
+    """One JSON line per round: rank, epoch, loss, Σweight, kernel / collective ms, bytes, ..."""
+    if _LOG_ROUNDS:
+        (_LOG_SINK or sys.stderr).write(json.dumps(fields) + "\n")
+
+
+def enabled() -> bool:
+    return _ENABLED
 
 
 class MetricGroup:

@@ -71,6 +71,7 @@ def main():
             gk.GRAD_BLOCKS = c.get("b", 512)
             gk.set_tuning(c.get("pad", -1), c.get("nt", -1))
             gk.DETERMINISTIC = bool(c.get("det", 0))
+            gk.set_tail_tuning(c.get("reps", 8), bool(c.get("t2", 0)))
             sgd = SGD(max_iter=10 ** 8, learning_rate=0.1, global_batch_size=a.batch, tol=0.0)
             cls = SplitTrainer if (c.get("split") or c.get("m0")) else DeviceGlmTrainer
             tr = cls(sgd, np.zeros(a.dim), X, y, None, "logistic", use_graph=True)

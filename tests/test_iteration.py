@@ -172,3 +172,102 @@ def test_window_all_and_process():
     assert out.column("s").tolist() == [6.0, 22.0]
     out = ds.window_all_and_process(t, GlobalWindows.get_instance(), lambda w: Table({"s": w.column("x").sum()[None]}))
     assert out.column("s").tolist() == [45.0]
+
+
+def test_side_outputs_from_body_and_listeners():
+    """``Context.output(tag, record)`` (IterationListener.java:66-73) from the body and from the
+    listener callbacks arrives as a named side-output stream, in emission order."""
+
+    class L(IterationListener):
+        def on_epoch_watermark_incremented(self, epoch, context, collector):
+            context.output("wm", ("wm", epoch))
+
+        def on_iteration_terminated(self, context, collector):
+            context.output("wm", ("done", context.epoch))
+            collector.collect("final")
+
+    class B(IterationBody):
+        def __init__(self):
+            self.listener = L()
+
+        def process(self, variables, data, ctx):
+            ctx.output("body", ctx.epoch * 10)
+            fb = [variables[0][0] + 1] if ctx.epoch < 2 else []
+            return IterationBodyResult([fb], [[ctx.epoch]], listeners=[(self.listener, 0)])
+
+    out = Iterations.iterate_bounded_streams_until_termination([[0]], ReplayableDataStreamList.replay([1]),
+                                                               IterationConfig(), B())
+    assert out[0] == [0, 1, 2, "final"]
+    assert out.get_side_output("body") == [0, 10, 20]
+    assert out.get_side_output("wm") == [("wm", 0), ("wm", 1), ("wm", 2), ("done", 3)]
+    assert out.getSideOutput("missing") == []
+
+    class U(IterationBody):
+        def process(self, variables, data, ctx):
+            ctx.output("seen", sum(data[0]))
+            return IterationBodyResult([variables[0]], [[]])
+
+    res = Iterations.iterate_unbounded_streams([[0]], iter([[1, 2], [3]]), U())
+    assert res.get_side_output("seen") == [3, 3]
+
+
+def _unbounded_ck(rank, world, ck_dir, attempt, fail_round):
+    import os
+
+    os.environ["FMLX_ATTEMPT"] = str(attempt)
+    from flink_ml_amd.parallel import checkpoint as ckpt
+    from flink_ml_amd.parallel.comm import all_reduce_scalar
+    from flink_ml_amd.parallel.iteration import RoundCheckpointer
+
+    ckpt.clear_faults()
+    ckpt.enable(ck_dir, interval=2)
+    if fail_round is not None:
+        ckpt.inject(ckpt.FailAfter(fail_round, rank=0, on_attempt=0))
+
+    class Acc(IterationBody):
+        def process(self, variables, data, ctx):
+            model = variables[0][0] + all_reduce_scalar(float(sum(data[0])), "sum")
+            ctx.output("versions", ctx.epoch)
+            return IterationBodyResult([[model]], [[model]])
+
+    batches = [[rank * 100 + i, i] for i in range(9)]  # a replayable source: the same batches again
+    out = Iterations.iterate_unbounded_streams([[0.0]], iter(batches), Acc(), checkpoint=RoundCheckpointer("online"))
+    return out[0], out.get_side_output("versions")
+
+
+def test_unbounded_iteration_failover_resumes_exactly(tmp_path):
+    """An unbounded (online) iteration checkpoints every 2 batches; after an injected failure at
+    batch 5 the restarted job skips the consumed batches and ends with the uninterrupted result."""
+    clean = run_spmd(_unbounded_ck, 2, str(tmp_path / "clean"), 0, None)
+    ck = str(tmp_path / "ck")
+    with pytest.raises(RuntimeError, match="injected failure"):
+        run_spmd(_unbounded_ck, 2, ck, 0, 5)
+    resumed = run_spmd(_unbounded_ck, 2, ck, 1, 5)
+    for (m0, v0), (m1, v1) in zip(clean, resumed):
+        assert m0 == m1 and v0 == v1 == list(range(9))
+
+
+def test_round_logs_are_structured_json(capsys):
+    """FMLX_LOG_ROUNDS: one JSON record per round from the iteration runtime and the SGD trainer."""
+    import io
+    import json
+
+    from flink_ml_amd import Table
+    from flink_ml_amd.models import LogisticRegression
+    from flink_ml_amd.utils import tracing
+
+    sink = io.StringIO()
+    tracing.log_rounds(True, sink)
+    try:
+        Iterations.iterate_bounded_streams_until_termination([[0]], ReplayableDataStreamList.replay(list(range(10))),
+                                                             IterationConfig(), SumBody(3))
+        X = torch.rand(200, 4, dtype=torch.float64)
+        LogisticRegression().set_max_iter(4).set_global_batch_size(50).set_tol(0.0).fit(
+            Table({"features": X, "label": (X[:, 0] > 0.5).double()}, num_rows=200))
+    finally:
+        tracing.log_rounds(False)
+    recs = [json.loads(l) for l in sink.getvalue().splitlines()]
+    it = [r for r in recs if r["kind"] == "bounded"]
+    sgd = [r for r in recs if r["kind"] == "sgd"]
+    assert [r["epoch"] for r in it] == [0, 1, 2] and all("ms" in r and r["rank"] == 0 for r in it)
+    assert [r["epoch"] for r in sgd] == [0, 1, 2, 3] and all(r["weight"] == 50.0 and r["loss"] > 0 for r in sgd)
