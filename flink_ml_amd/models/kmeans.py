@@ -139,6 +139,16 @@ class KMeans(Estimator, KMeansParams):
         return model
 
 
+def _graph_ok(ck, log: bool) -> bool:
+    """A KMeans round can be replayed from a hipGraph: no per-round host work (checkpoints,
+    round logs) and a capturable collective (single rank, or RCCL / the xGMI kernel)."""
+    import os
+
+    ctx = get_context()
+    return (os.environ.get("FMLX_HIPGRAPH", "1") == "1" and not ck.interval and not log
+            and (not ctx.is_distributed or ctx.backend == "nccl"))
+
+
 def kmeans_lloyd(X: torch.Tensor, init: np.ndarray, max_iter: int, metric: str):
     """``maxIter`` Lloyd rounds; returns (centroids [k,D] f64, weights [k] f64)."""
     from ..parallel.checkpoint import AlgorithmCheckpoint, fault_point
@@ -157,6 +167,26 @@ def kmeans_lloyd(X: torch.Tensor, init: np.ndarray, max_iter: int, metric: str):
             cb.weights.copy_(counts0.to(cb.weights.dtype))
         rnd = kk.KMeansRound(X, kc, metric)
         log = tracing.rounds_enabled()
+        if _graph_ok(ck, log) and max_iter - start >= 3:
+            # the round is host-sync free: run it once eagerly (warm-up), capture ONE round into a
+            # hipGraph and replay it for the remaining rounds (one submission per round)
+            with tracing.range("kmeans.fit"):
+                fault_point(start)
+                payload = rnd.run(cb)
+                comm.all_reduce_sum(payload)
+                rnd.finalize(cb, payload)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    payload = rnd.run(cb)
+                    comm.all_reduce_sum(payload)
+                    rnd.finalize(cb, payload)
+                # the capture did not execute the round: replay max_iter - start - 1 times
+                for e in range(start + 1, max_iter):
+                    fault_point(e)
+                    g.replay()
+            out = cb.cent.to(torch.float64).cpu().numpy(), cb.weights.cpu().numpy()
+            comm.check_collectives()
+            return out
         with tracing.range("kmeans.fit"):
             for e in range(start, max_iter):
                 fault_point(e)

@@ -1273,17 +1273,19 @@ template <typename T, int EPC, int CPL>
 int launch_grad(int u, const void* X, long ld, const void* y, const void* wt, void* coef, long n, int d, long B,
                 int loss, int* state, void* partials, int nblocks, const GlmTail& tl, int flags, hipStream_t s) {
   constexpr int BYTES = CPL * EPC * (int)sizeof(T);
-  // grouped path (bf16, 16-byte chunks, d ≤ 2048): default; u = -4 / -8 forces G, u > 0 the
-  // row-at-a-time loop with U rows per step
+  // grouped path (bf16, 16-byte chunks, d ≤ 2048): u = -4 / -8 (A/B knob; measured slower
+  // than the row-at-a-time loop on the flagship shape: 40.6 / 42.2 vs 37.9 µs per round)
   if constexpr (sizeof(T) == 2 && EPC == 8 && CPL <= 4) {
-    if (u <= 0) {
-      const int g = u < 0 ? -u : (CPL <= 2 ? 8 : 4);
+    if (u < 0) {
+      const int g = -u;
       if (g == 8 && CPL <= 2)
         return launch_grad_u<T, EPC, CPL, 1, 8>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
       return launch_grad_u<T, EPC, CPL, 1, 4>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
     }
   }
-  if (u <= 0) u = BYTES <= 64 ? 2 : 1;
+  // default: 2 rows in flight per wave for narrow rows, 1 from 32 bytes per lane (flagship
+  // 1000 × bf16: U=1 37.9 µs vs U=2 39.1 µs per round, 256 blocks, measured)
+  if (u <= 0) u = BYTES <= 16 ? 2 : 1;
   if (u >= 4 && BYTES <= 32)
     return launch_grad_u<T, EPC, CPL, 4>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
   if (u >= 2 && BYTES <= 64)

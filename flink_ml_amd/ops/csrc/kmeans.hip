@@ -499,6 +499,56 @@ __global__ __launch_bounds__(256) void kmeans_chunk_sum_bf16v_kernel(const bf16_
   for (int c = threadIdx.x; c < D; c += 256) partial[b * D + c] = ((sm[0][c] + sm[1][c]) + sm[2][c]) + sm[3][c];
 }
 
+// Cluster boundaries from the sorted labels, no host sync: offsets[c] = first position of a
+// label ≥ c (binary search, one thread per cluster), chunk_off = exclusive scan of
+// ceil(count / KM_CH) (one block, fixed order). Replaces bincount + cumsum (bincount's min/max
+// range check synchronised the host every round).
+__global__ __launch_bounds__(1024) void kmeans_offsets_kernel(const int* __restrict__ keys_sorted, long n, int k,
+                                                              long* __restrict__ offsets, long* __restrict__ chunk_off) {
+  __shared__ long warp_tot[16];
+  __shared__ long carry;
+  if (threadIdx.x == 0) carry = 0;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int base = 0; base <= k; base += 1024) {
+    const int c = base + threadIdx.x;
+    long lo = 0, hi = n;  // lower_bound(keys_sorted, c)
+    if (c <= k) {
+      while (lo < hi) {
+        const long mid = (lo + hi) >> 1;
+        if (keys_sorted[mid] < c) lo = mid + 1; else hi = mid;
+      }
+      offsets[c] = lo;
+    }
+    __syncthreads();
+    // chunks of cluster c need offsets[c + 1]: recompute it the same way (cheap, log2 n loads)
+    long chunks = 0;
+    if (c < k) {
+      long lo2 = lo, hi2 = n;
+      while (lo2 < hi2) {
+        const long mid = (lo2 + hi2) >> 1;
+        if (keys_sorted[mid] < c + 1) lo2 = mid + 1; else hi2 = mid;
+      }
+      chunks = (lo2 - lo + KM_CH - 1) / KM_CH;
+    }
+    // block-wide exclusive scan of `chunks` (fixed order: wave prefix, then wave totals)
+    long incl = chunks;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const long o = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += o;
+    }
+    if (lane == 63) warp_tot[wv] = incl;
+    __syncthreads();
+    long wpre = 0;
+    for (int i = 0; i < wv; ++i) wpre += warp_tot[i];
+    const long excl = carry + wpre + incl - chunks;
+    if (c <= k) chunk_off[c] = excl;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = excl + chunks;
+    __syncthreads();
+  }
+}
+
 template <typename A>
 __global__ __launch_bounds__(256) void kmeans_cluster_sum_kernel(const A* __restrict__ partial, int D,
                                                                  const long* __restrict__ offsets,
@@ -700,6 +750,12 @@ FMLX_API int fmlx_kmeans_chunk_sum_bf16v(const void* X, long ld, int D, const in
     case 512: hipLaunchKernelGGL(kmeans_chunk_sum_bf16v_kernel<64>, g, dim3(256), 0, s, x, ld, D, order, offsets, chunk_off, k, partial); break;
     default: return -2;
   }
+  return (int)hipGetLastError();
+}
+
+FMLX_API int fmlx_kmeans_offsets(const int* keys_sorted, long n, int k, long* offsets, long* chunk_off, void* stream) {
+  hipLaunchKernelGGL(kmeans_offsets_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, keys_sorted, n, k, offsets,
+                     chunk_off);
   return (int)hipGetLastError();
 }
 

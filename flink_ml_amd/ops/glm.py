@@ -16,9 +16,9 @@ from . import native
 LOSS_CODES = {"logistic": 0, "hinge": 1, "leastsquare": 2, "ftrl": 3}
 MAX_CPL = 8
 WPB = 8
-# row loop of the round kernel (A/B knob): 0 = default for the shape (bf16 rows of 16-byte chunks:
-# the grouped path, 8 rows per step), -4 / -8 = grouped with 4 / 8 rows, U > 0 = row-at-a-time
-# with 2·U rows in flight per wave
+# row loop of the round kernel (A/B knob): 0 = default for the shape (row-at-a-time, U = 1 from
+# 32 bytes per lane, else 2), U > 0 = row-at-a-time with 2·U rows in flight per wave, -4 / -8 =
+# the grouped loop (bf16: 4 / 8 rows per step share one transposed reduction and loss pass)
 GRAD_UNROLL = int(os.environ.get("FMLX_GLM_UNROLL", "0"))
 GRAD_BLOCKS = int(os.environ.get("FMLX_GLM_BLOCKS", "256"))
 

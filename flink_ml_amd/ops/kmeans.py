@@ -23,6 +23,7 @@ native.register_kernel_sigs({
     "fmlx_kmeans_cluster_sum": [c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
     "fmlx_kmeans_chunk_sum_bf16v": [c_void_p, c_long, c_int, c_void_p, c_void_p, c_void_p, c_int, c_long, c_void_p,
                                     c_void_p],
+    "fmlx_kmeans_offsets": [c_void_p, c_long, c_int, c_void_p, c_void_p, c_void_p],
     "fmlx_sort_pairs_temp_bytes": ([c_long, c_int], c_long),
     "fmlx_sort_pairs": [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_long, c_void_p],
     "fmlx_kmeans_finalize": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
@@ -101,8 +102,9 @@ def assign(X: torch.Tensor, cb: CentroidBuffers, metric: str, out: torch.Tensor 
         cn2 = (C * C).sum(1)
         for r0 in range(0, n, GEMM_ASSIGN_ROWS):
             Xc = X[r0:r0 + GEMM_ASSIGN_ROWS]
+            # ‖c‖² − 2x·c: the per-row ‖x‖² does not move the argmin (no n×D temporary for it)
             d = torch.addmm(cn2.unsqueeze(0), Xc, C.t(), alpha=-2.0)
-            d.add_((Xc * Xc).sum(1, keepdim=True)).clamp_(min=0.0)
+            d.nan_to_num_(nan=float("inf"))  # NaN distances never win, like torch_assign / the kernels
             out[r0:r0 + Xc.shape[0]] = torch.argmin(d, dim=1).to(torch.int32)  # first (lowest) index on ties
         return out
     C = cb.cent.to(X.dtype).contiguous()
@@ -159,6 +161,8 @@ class KMeansRound:
             if tb < 0:
                 raise RuntimeError("radix sort temp-size query failed")
             self.sort_temp = torch.empty(max(int(tb), 1), dtype=torch.uint8, device=dev)
+            self.offsets = torch.zeros(k + 1, dtype=torch.int64, device=dev)
+            self.chunk_off = torch.zeros(k + 1, dtype=torch.int64, device=dev)
 
     def run(self, cb: CentroidBuffers) -> torch.Tensor:
         X = self.X
@@ -170,9 +174,10 @@ class KMeansRound:
         native.call("fmlx_sort_pairs", native.ptr(self.labels), native.ptr(self.keys_sorted), native.ptr(self.iota),
                     native.ptr(self.order32), self.n, self.bits, native.ptr(self.sort_temp), self.sort_temp.numel(),
                     stream)
-        counts = torch.bincount(self.labels, minlength=self.k)
-        offsets = torch.cat([self.zero_i64, torch.cumsum(counts, 0)])
-        chunk_off = torch.cat([self.zero_i64, torch.cumsum((counts + CHUNK - 1) // CHUNK, 0)])
+        # cluster boundaries on the device (no host sync: the round is hipGraph-capturable)
+        native.call("fmlx_kmeans_offsets", native.ptr(self.keys_sorted), self.n, self.k, native.ptr(self.offsets),
+                    native.ptr(self.chunk_off), stream)
+        offsets, chunk_off = self.offsets, self.chunk_off
         if self.fast:
             native.call("fmlx_kmeans_chunk_sum_bf16v", native.ptr(X), X.stride(0), self.D, native.ptr(self.order32),
                         native.ptr(offsets), native.ptr(chunk_off), self.k, self.max_chunks, native.ptr(self.partial),

@@ -209,6 +209,8 @@ def test_gpu_kmeans_fit_golden():
 def test_gpu_assign_fp32_euclidean_both_paths(n):
     """fp32 euclidean assign: the wave kernel (small n) and the GEMM + argmin path (large n, few
     centroids) against the fp64 torch reference; near-ties may differ only by rounding."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
     from flink_ml_amd.ops import kmeans as kk
 
     g = torch.Generator(device="cpu").manual_seed(n)
@@ -224,3 +226,65 @@ def test_gpu_assign_fp32_euclidean_both_paths(n):
         gap = (d[diff, got[diff]] - d[diff, ref[diff]]).abs()
         assert float(gap.max()) < 1e-4, float(gap.max())
     assert float(diff.double().mean()) < 1e-3
+
+
+@pytest.mark.gpu
+def test_gpu_assign_bf16_north_star_shape():
+    """The MFMA assign instance the north-star shard runs (kmeans_assign_bf16_kernel<8, true>:
+    D=128, k=1024) on 1.2M rows against fp32 torch distances of the same bf16 operands."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from flink_ml_amd.ops import kmeans as kk
+
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(11)
+    n, D, k = 1_200_000, 128, 1024
+    X = torch.rand((n, D), generator=g, device=dev).to(torch.bfloat16)
+    C = torch.rand((k, D), generator=g, device=dev, dtype=torch.float64)
+    cb = kk.CentroidBuffers(k, D, dev, torch.float32)
+    cb.set(C)
+    assert kk.mfma_ok(X, "euclidean") and cb.KS == 8
+    lab = kk.assign(X, cb, "euclidean").long()
+    Cf = C.to(torch.bfloat16).float()
+    cn = (Cf ** 2).sum(1)
+    bad = 0
+    for r0 in range(0, n, 200_000):
+        Xf = X[r0:r0 + 200_000].float()
+        d = cn[None, :] - 2.0 * (Xf @ Cf.T)
+        ref = d.argmin(1)
+        got = lab[r0:r0 + 200_000]
+        diff = got != ref
+        if bool(diff.any()):
+            dsel = d.gather(1, got[:, None]).squeeze(1)[diff]
+            dref = d.gather(1, ref[:, None]).squeeze(1)[diff]
+            xn = (Xf[diff] ** 2).sum(1)
+            # near-ties only: within fp32 accumulation noise of the full distance ‖x‖² + d
+            assert bool(((dsel - dref).abs() <= 2e-3 * (xn + dref).abs()).all())
+            bad += int(diff.sum())
+    assert bad / n < 2e-3
+
+
+@pytest.mark.gpu
+def test_gpu_round_offsets_with_empty_clusters():
+    """Device cluster boundaries (sorted labels → offsets / chunk offsets, no host sync) with
+    empty clusters and clusters larger than one gather chunk."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from flink_ml_amd.ops import kmeans as kk
+
+    g = torch.Generator().manual_seed(4)
+    n, D, k = 50_000, 16, 300
+    X = torch.rand((n, D), generator=g).to(torch.bfloat16)
+    C = torch.cat([X[:200].double(), torch.full((100, D), 50.0, dtype=torch.float64)])  # 100 far-away centroids
+    cb = kk.CentroidBuffers(k, D, torch.device("cuda"), torch.float32)
+    cb.set(C)
+    rnd = kk.KMeansRound(X.cuda(), k, "euclidean")
+    p = rnd.run(cb).cpu().double()
+    lab = rnd.labels.cpu().long()
+    cnt = torch.bincount(lab, minlength=k)
+    assert torch.equal(p[k * D:], cnt.double()) and int((cnt == 0).sum()) >= 100
+    assert torch.equal(rnd.offsets.cpu(), torch.cat([torch.zeros(1, dtype=torch.int64), cnt.cumsum(0)]))
+    ch = (cnt + kk.CHUNK - 1) // kk.CHUNK
+    assert torch.equal(rnd.chunk_off.cpu(), torch.cat([torch.zeros(1, dtype=torch.int64), ch.cumsum(0)]))
+    sums = torch.zeros((k, D), dtype=torch.float64).index_add_(0, lab, X.double())
+    assert torch.allclose(p[: k * D].reshape(k, D), sums, rtol=1e-5, atol=1e-3)

@@ -91,7 +91,7 @@ def test_fused_sgd_round_two_ranks_matches_host(xgmi_mode):
         assert b0 == r1[loss][2], loss  # replicas identical
 
 
-@pytest.mark.parametrize("det,blocks,unroll", [(False, 256, 0), (False, 256, -4), (False, 256, 2), (False, 512, 0),
+@pytest.mark.parametrize("det,blocks,unroll", [(False, 256, 0), (False, 256, -4), (False, 256, -8), (False, 256, 2), (False, 512, 0),
                                                (True, 512, 0), (True, 256, 1)])
 def test_fused_round_flagship_shape_matches_torch(det, blocks, unroll, monkeypatch):
     """Fused rounds (TAIL_UPDATE) at the bench shape, bf16 rows: the bench's 256-block grid and
