@@ -5,9 +5,13 @@ Reference: ``LIB/classification/logisticregression/OnlineLogisticRegression{,Mod
 
 Execution model (SURVEY §7.1 "unbounded streams"): each rank ingests its own stream shard,
 re-batched to ``globalBatchSize / P`` rows (remainder to low ranks) with async H2D prefetch;
-one training round per global mini-batch = fused local-gradient kernel (``glm.hip`` loss code 3)
-→ ONE RCCL all-reduce of ``[grad | weightSum]`` → fused FTRL kernel (``ftrl.hip``). Every rank
-holds the FTRL state (z, n) replicated, so no model broadcast is needed (C1/C3 disappear).
+one training round per global mini-batch = fused local-gradient kernel (``glm.hip`` loss code 3,
+or ``online.hip`` for CSR rows) → ONE all-reduce of ``[grad | weightSum | batch flag]`` (one-shot
+xGMI kernel or RCCL) → predicated FTRL kernel (``online.hip``). OnlineKMeans: MFMA assign + ordered
+cluster sums → decayed local update kernel → ONE all-reduce of ``[c·w | w | flag]`` → predicated
+merge kernel. Every rank holds the model state replicated, so no model broadcast is needed
+(C1/C3 disappear); nothing is copied to the host per batch, and the end of the stream rides in
+the payload (``VersionedModelStream``: pipelined rounds, no extra collective).
 Models produced by training form a *versioned model-data stream*; a ``transform`` predicts each
 input batch with the latest version available at that moment (pulling training batches that are
 already queued, blocking only until the first version exists — the reference buffers points
@@ -45,6 +49,13 @@ from .linear import LogisticRegressionModel, rw_update
 native.register_kernel_sigs({
     "fmlx_ftrl_update": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_double, c_double,
                          c_double, c_double, c_void_p],
+    "fmlx_ftrl_update2": [c_int, c_void_p, c_void_p, c_long, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                          c_long, c_double, c_double, c_double, c_double, c_void_p],
+    "fmlx_ftrl_grad_csr": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_long,
+                           c_void_p, c_void_p],
+    "fmlx_okm_local_update": [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double, c_void_p, c_void_p],
+    "fmlx_okm_merge": [c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                       c_void_p, c_void_p],
 })
 
 
@@ -58,26 +69,99 @@ def _as_stream(inp, batch_rows: Optional[int] = None) -> Iterable[Table]:
     return StreamTable(inp)
 
 
+class VersionLog:
+    """Append-only log of model versions that keeps only the newest ``keep`` entries (device
+    snapshots are not free: an unbounded stream must not hold every version). ``len`` counts
+    every version ever appended; indexing an evicted version raises ``IndexError``."""
+
+    def __init__(self, initial=(), keep: Optional[int] = None):
+        import os
+        from collections import deque
+
+        self.keep = int(keep or os.environ.get("FMLX_MODEL_VERSIONS_KEEP", "64"))
+        self._items = deque(initial, maxlen=self.keep)
+        self._total = len(self._items)
+
+    def append(self, v) -> None:
+        self._items.append(v)
+        self._total += 1
+
+    def advance(self, n: int) -> None:
+        """Counts ``n`` versions that are not retained (a restored stream's earlier versions)."""
+        self._total += int(n)
+
+    def __len__(self) -> int:
+        return self._total
+
+    def __bool__(self) -> bool:
+        return self._total > 0
+
+    def __getitem__(self, i: int):
+        if i < 0:
+            i += self._total
+        first = self._total - len(self._items)
+        if i < first or i >= self._total:
+            raise IndexError("model version %d is not retained (keep=%d)" % (i, self.keep))
+        return self._items[i - first]
+
+
+class _Round:
+    """One launched training round: the version snapshot, and (world > 1) the pinned host copy of
+    the all-reduced batch-present flag with the event that completes it."""
+
+    __slots__ = ("version", "flag", "event", "state", "index")
+
+    def __init__(self, version, flag=None, event=None, state=None, index=0):
+        self.version, self.flag, self.event, self.state, self.index = version, flag, event, state, index
+
+
 class VersionedModelStream:
     """Lazily-trained sequence of model versions shared by the estimator's output model.
 
-    ``pull(block)`` trains on the next mini-batch (collectively across ranks) and appends the
-    resulting version. With an ``InMemorySource`` the non-blocking pull only consumes batches
-    that every rank has already received.
+    ``pull(block)`` trains on the next global mini-batch (collectively across ranks) and appends
+    the resulting version. Blocking pulls are pipelined: the end of the stream travels as a flag
+    INSIDE the round's gradient all-reduce (the update kernels are predicated on every rank having
+    contributed a batch), round r+1 is queued before the host reads round r's flag, and a pull
+    returns once round r is confirmed — no separate end-of-stream collective and no host stall
+    between rounds. With an ``InMemorySource`` the non-blocking pull only consumes batches that
+    every rank has already received (one agreement collective, as before).
+
+    Round checkpoints: every confirmed version v with ``AlgorithmCheckpoint.due(v)`` saves the
+    trainer state snapshotted (on the device, in stream order) right after that round; a restart
+    restores it and skips the v local batches the source had delivered.
     """
 
-    def __init__(self, source, rebatch: int, step_fn, initial_versions: List = ()):
-        self.versions: List = list(initial_versions)
+    def __init__(self, source, rebatch: int, trainer, initial_versions: List = (), name: str = "online"):
+        from ..parallel.checkpoint import AlgorithmCheckpoint
+        from ..parallel.context import get_context
+
+        self.versions = VersionLog(initial_versions)
         self._source = source
-        self._step = step_fn
+        self._trainer = trainer
         self._iter = None
         self._pending = None
         self._done = False
+        self._ended = False  # this rank's source is exhausted
         self._rebatch = rebatch
+        self._inflight: Optional[_Round] = None
+        self._world = get_context().world_size
+        self._ck = AlgorithmCheckpoint(name)
+        self._launched = 0  # rounds launched (confirmed or in flight)
+        self._skip = 0
+        restored = self._ck.restore()
+        if restored is not None:
+            v, st = restored
+            trainer.load_state(st)
+            self._launched = self._skip = int(v)
+            self.versions.advance(int(v) - 1)
+            self.versions.append(trainer.version_from_state())
 
+    # -- local batches ------------------------------------------------------------------------
     def _next_local(self, block: bool):
         if self._pending is not None:
             return self._pending
+        if self._ended:
+            return None
         if isinstance(self._source, InMemorySource) and not block:
             item = self._source.poll(timeout=0)
             if item is None:
@@ -85,7 +169,7 @@ class VersionedModelStream:
             from ..stream import END
 
             if item is END:
-                self._done = True
+                self._ended = True
                 return None
             self._pending = _BatchBuf.feed(self, item)
             return self._pending
@@ -94,22 +178,84 @@ class VersionedModelStream:
             stream = _as_stream(src)
             self._iter = iter(stream.rebatch(self._rebatch).to_device() if isinstance(stream, StreamTable)
                               else stream)
+            for _ in range(self._skip):  # batches consumed before the restored checkpoint
+                next(self._iter, None)
         try:
             self._pending = next(self._iter)
         except StopIteration:
-            self._done = True
+            self._pending = None
+            self._ended = True  # multi-rank: the flag in the round's payload / the agreement decides
             return None
         return self._pending
 
-    def pull(self, block: bool = True) -> bool:
-        if self._done and self._pending is None:
-            return False
-        got = self._next_local(block) is not None
-        if comm.all_reduce_scalar(1.0 if got else 0.0, "min") == 0.0:
-            return False
-        batch = self._pending
+    def _take_local(self, block: bool):
+        b = self._next_local(block)
         self._pending = None
-        self.versions.append(self._step(batch))
+        return b
+
+    # -- rounds -------------------------------------------------------------------------------
+    def _launch(self, batch) -> _Round:
+        from ..parallel.checkpoint import fault_point
+
+        v = self._launched + 1
+        fault_point(v - 1)
+        rnd = self._trainer.launch(batch, self._world, snapshot_state=self._ck.mgr is not None and self._ck.mgr.due(v))
+        rnd.index = v
+        self._launched += 1
+        return rnd
+
+    def _commit(self, rnd: _Round) -> None:
+        self.versions.append(rnd.version)
+        if rnd.state is not None:
+            self._ck.maybe_save(rnd.index, lambda: rnd.state)
+
+    def _confirmed(self, rnd: _Round) -> bool:
+        if rnd.flag is None:
+            return True
+        if rnd.event is not None:
+            rnd.event.synchronize()
+            comm.check_collectives()
+        return float(rnd.flag[0]) > self._world - 0.5
+
+    def flush(self) -> None:
+        """Confirms the round in flight (blocking pulls leave one queued)."""
+        if self._inflight is not None:
+            rnd, self._inflight = self._inflight, None
+            if self._confirmed(rnd):
+                self._commit(rnd)
+            else:
+                self._done = True
+
+    def pull(self, block: bool = True) -> bool:
+        if self._done:
+            self.flush()
+            return False
+        if not block or self._world == 1:
+            # synchronous protocol: agree on batch availability first (world > 1 only)
+            self.flush()
+            if self._done:
+                return False
+            got = self._next_local(block) is not None
+            # agreement: 2 = a batch is ready, 1 = nothing yet, 0 = this rank's stream ended
+            st = 2.0 if got else (0.0 if self._ended else 1.0)
+            if self._world > 1:
+                st = comm.all_reduce_scalar(st, "min")
+            if st == 0.0:
+                self._done = True  # every rank learns it in the same agreement
+            if st < 2.0:
+                return False
+            self._commit(self._launch(self._take_local(block)))
+            return True
+        # pipelined protocol (world > 1): every rank launches the same rounds in the same order
+        if self._inflight is None:
+            self._inflight = self._launch(self._take_local(True))
+        nxt = self._launch(self._take_local(True))  # queued behind the round being confirmed
+        rnd, self._inflight = self._inflight, nxt
+        if not self._confirmed(rnd):
+            self._done = True  # every later round is a device no-op (a rank's stream has ended)
+            self._inflight = None
+            return False
+        self._commit(rnd)
         return True
 
     def drain_available(self) -> None:
@@ -119,10 +265,12 @@ class VersionedModelStream:
         else:
             while self.pull(block=True):
                 pass
+            self.flush()
 
     def latest(self, block_until_first: bool = True):
         if not self.versions and block_until_first:
             self.pull(block=True)
+            self.flush()
         return self.versions[-1] if self.versions else None
 
 
@@ -180,9 +328,12 @@ class DeviceDenseVector(DenseVector):
 
 
 class FtrlTrainer:
-    """Replicated FTRL state on the device + one round per mini-batch."""
+    """Replicated FTRL state (z, n, coef) on the device; one round per global mini-batch:
+    local gradient kernel → ONE all-reduce of ``[grad | weightSum | batch flag]`` → predicated
+    FTRL update kernel → device snapshot of the new coefficients (the model version)."""
 
-    def __init__(self, coef0: np.ndarray, alpha, beta, l1, l2, features_col, label_col, weight_col):
+    def __init__(self, coef0: np.ndarray, alpha, beta, l1, l2, features_col, label_col, weight_col,
+                 version0: int = 0):
         self.dev = config.compute_device()
         self.acc = config.acc_dtype() if self.dev.type == "cuda" else torch.float64
         d = coef0.shape[0]
@@ -192,69 +343,152 @@ class FtrlTrainer:
         self.n = torch.zeros(d, dtype=self.acc, device=self.dev)
         self.alpha, self.beta, self.l1, self.l2 = alpha, beta, l1, l2
         self.fcol, self.lcol, self.wcol = features_col, label_col, weight_col
-        self.version = 0
-        self._scratch = {}  # (nparts, dtype) -> (RoundScratch, feedback, state): no per-batch allocation
+        self.version = int(version0)  # host count of launched updates (confirmed ones are kept)
+        self.dev_version = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        # fixed-size payload [grad d | wsum d | flag]: every rank (even one whose stream has
+        # ended) all-reduces the same shape; the dense path uses wsum slot 0 (stride 0)
+        self.payload = torch.zeros(2 * d + 1, dtype=self.acc, device=self.dev)
+        self._dense_layout = True
+        self._scratch = {}  # (nparts, dtype) -> (RoundScratch, state): no per-batch allocation
+        self._flags = _FlagRing(self.dev)
 
-    def local_gradient(self, batch: Table):
+    # -- state (checkpoints) ------------------------------------------------------------------
+    def snapshot(self):
+        return {"coef": self.coef.clone(), "z": self.z.clone(), "n": self.n.clone(), "version": self.version}
+
+    def load_state(self, st) -> None:
+        self.coef.copy_(st["coef"].to(self.coef))
+        self.z.copy_(st["z"].to(self.z))
+        self.n.copy_(st["n"].to(self.n))
+        self.version = int(st["version"])
+
+    def version_from_state(self):
+        return self._version_obj(self.coef.clone())
+
+    def _version_obj(self, coef):
+        if self.dev.type == "cuda":
+            return (DeviceDenseVector(coef), self.version)
+        return (DenseVector(coef.to(torch.float64).numpy()), self.version)
+
+    # -- local gradient -----------------------------------------------------------------------
+    def _local_payload(self, batch: Optional[Table]):
+        """Fills ``self.payload`` with this rank's [grad | wsum | 1] (zeros if no batch); returns
+        the weight-sum stride (0 = one weight sum for every coordinate)."""
+        P, d = self.payload, self.d
+        if batch is None or batch.num_rows == 0:
+            P.zero_()
+            return 0
         X = config.features_for_compute(batch, self.fcol)
         y = batch.scalars(self.lcol, dtype=self.acc, device=self.dev)
         if isinstance(X, SparseColumn):
-            payload = torch.zeros(2 * self.d, dtype=self.acc, device=self.dev)
             w = batch.scalars(self.wcol, dtype=self.acc, device=self.dev) if self.wcol and batch.has_column(
-                self.wcol) else torch.ones(len(X), dtype=self.acc, device=self.dev)
+                self.wcol) else None
+            self._dense_layout = False
+            if self.dev.type == "cuda":
+                vals = X.values.to(self.dev, self.acc).contiguous()
+                native.call("fmlx_ftrl_grad_csr", int(self.acc == torch.float64),
+                            native.ptr(X.indptr.to(self.dev, torch.int64).contiguous()),
+                            native.ptr(X.indices.to(self.dev, torch.int32).contiguous()), native.ptr(vals),
+                            native.ptr(y.contiguous()), native.ptr(w), native.ptr(self.coef), len(X), d,
+                            native.ptr(P), native.stream_ptr(self.dev))
+                return 1
+            P.zero_()
             counts = X.indptr[1:] - X.indptr[:-1]
-            rows = torch.repeat_interleave(torch.arange(len(X), device=self.dev), counts.to(self.dev))
-            idx = X.indices.to(self.dev).long()
-            vals = X.values.to(self.dev, self.acc)
-            dot = torch.zeros(len(X), dtype=self.acc, device=self.dev).index_add_(0, rows, vals * self.coef[idx])
+            rows = torch.repeat_interleave(torch.arange(len(X)), counts)
+            idx = X.indices.long()
+            vals = X.values.to(self.acc)
+            dot = torch.zeros(len(X), dtype=self.acc).index_add_(0, rows, vals * self.coef[idx])
             mult = torch.sigmoid(dot) - y
-            payload[: self.d].index_add_(0, idx, mult[rows] * vals)
-            payload[self.d:].index_add_(0, idx, w[rows])
-            return payload
+            P[:d].index_add_(0, idx, mult[rows] * vals)
+            P[d:2 * d].index_add_(0, idx, (w if w is not None else torch.ones(len(X), dtype=self.acc))[rows])
+            P[2 * d] = 1
+            return 1
+        if not self._dense_layout:
+            P.zero_()  # the sparse layout filled the per-coordinate weight sums
+            self._dense_layout = True
         n = X.shape[0]
-        if n == 0:
-            return torch.zeros(2 * self.d, dtype=self.acc, device=self.dev)
         if self.dev.type == "cuda" and gk.pick_layout(X) is not None:
             Xk = X if X.dtype in (torch.float32, torch.float64, torch.bfloat16) else X.to(self.acc)
             kacc = torch.float64 if Xk.dtype == torch.float64 else torch.float32
+            if kacc != self.acc:
+                Xk, kacc = Xk.to(self.acc), self.acc
             nparts = max(1, min(gk.GRAD_BLOCKS, gk.max_round_blocks(), math.ceil(n / (gk.WPB * 16))))
             key = (nparts, kacc)
             if key not in self._scratch:
                 state = torch.zeros(8, dtype=torch.int32, device=self.dev)
                 state[1:3] = 1  # running; the feedback-only tail never advances it
-                self._scratch[key] = (gk.RoundScratch(nparts, self.d, kacc, self.dev),
-                                      torch.zeros(self.d + 2, dtype=kacc, device=self.dev), state)
-            scratch, fb, state = self._scratch[key]
-            coef = self.coef if self.coef.dtype == kacc else self.coef.to(kacc)
-            # one launch: local gradient + fixed-order reduction → [Σ mult·x | rows | 0]
-            gk.glm_round(Xk, y.to(kacc).contiguous(), None, coef, n, gk.LOSS_CODES["ftrl"], state, scratch,
-                         gk.TAIL_FEEDBACK, fb)
-            pay = self._scratch.get("payload")
-            if pay is None:
-                pay = self._scratch["payload"] = torch.empty(2 * self.d, dtype=self.acc, device=self.dev)
-            pay[: self.d].copy_(fb[: self.d])
-            pay[self.d:].copy_(fb[self.d].expand(self.d))
-            return pay
+                self._scratch[key] = (gk.RoundScratch(nparts, d, kacc, self.dev), state)
+            scratch, state = self._scratch[key]
+            # one launch: local gradient + reduction → P[0:d+2] = [Σ mult·x | rows | 0]
+            gk.glm_round(Xk, y.to(kacc).contiguous(), None, self.coef, n, gk.LOSS_CODES["ftrl"], state, scratch,
+                         gk.TAIL_FEEDBACK, P)
+            P[2 * d:].fill_(1.0)
+            return 0
         Xf = X.to(self.acc)
         mult = torch.sigmoid(Xf @ self.coef) - y
-        payload = torch.empty(2 * self.d, dtype=self.acc, device=self.dev)
-        payload[: self.d] = mult @ Xf
-        payload[self.d:] = float(n)
-        return payload
+        P[:d] = mult @ Xf
+        P[d] = float(n)
+        P[2 * d] = 1
+        return 0
+
+    def local_gradient(self, batch: Table) -> torch.Tensor:
+        """This rank's payload for ``batch`` (a view of the persistent buffer: valid until the next
+        call)."""
+        self._local_payload(batch)
+        return self.payload
+
+    # -- one round ----------------------------------------------------------------------------
+    def launch(self, batch: Optional[Table], world: int, snapshot_state: bool = False) -> "_Round":
+        d = self.d
+        stride = self._local_payload(batch)
+        P = comm.all_reduce_sum(self.payload)
+        flag = P[2 * d:] if world > 1 else None  # 1 GPU: the host knows a batch was there
+        if self.dev.type == "cuda":
+            native.call("fmlx_ftrl_update2", int(self.acc == torch.float64), native.ptr(P), native.ptr(P[d:]), stride,
+                        native.ptr(flag), world, native.ptr(self.coef), native.ptr(self.z), native.ptr(self.n),
+                        native.ptr(self.dev_version), d, self.alpha, self.beta, self.l1, self.l2,
+                        native.stream_ptr(self.dev))
+        else:
+            if flag is None or float(flag[0]) > world - 0.5:
+                wsum = P[d:2 * d] if stride else P[d].expand(d)
+                ftrl_update_torch(P[:d], wsum, self.coef, self.z, self.n, self.alpha, self.beta, self.l1, self.l2)
+        self.version += 1
+        rnd = _Round(self._version_obj(self.coef.clone()),
+                     state=self.snapshot() if snapshot_state else None)
+        if flag is not None:
+            rnd.flag, rnd.event = self._flags.copy(flag)
+        if world > 1 and flag is not None:
+            pass
+        return rnd
 
     def step(self, batch: Table):
-        payload = comm.all_reduce_sum(self.local_gradient(batch))
-        grad, wsum = payload[: self.d], payload[self.d:]
-        if self.dev.type == "cuda":
-            native.call("fmlx_ftrl_update", int(self.acc == torch.float64), native.ptr(grad), native.ptr(wsum),
-                        native.ptr(self.coef), native.ptr(self.z), native.ptr(self.n), self.d, self.alpha,
-                        self.beta, self.l1, self.l2, native.stream_ptr(self.dev))
+        """Synchronous single round (1 GPU / tests): returns the new version."""
+        from ..parallel.context import get_context
+
+        return self.launch(batch, get_context().world_size).version
+
+
+class _FlagRing:
+    """Pinned host slots receiving the all-reduced batch flag of each round (async D2H copy)."""
+
+    def __init__(self, dev, n: int = 4):
+        self.dev = dev
+        self.i = 0
+        if dev.type == "cuda":
+            self.slots = [torch.zeros(1, dtype=torch.float64).pin_memory() for _ in range(n)]
         else:
-            ftrl_update_torch(grad, wsum, self.coef, self.z, self.n, self.alpha, self.beta, self.l1, self.l2)
-        self.version += 1
-        if self.dev.type == "cuda":
-            return (DeviceDenseVector(self.coef.clone()), self.version)
-        return (DenseVector(self.coef.to(torch.float64).cpu().numpy()), self.version)
+            self.slots = [torch.zeros(1, dtype=torch.float64) for _ in range(n)]
+
+    def copy(self, flag: torch.Tensor):
+        slot = self.slots[self.i]
+        self.i = (self.i + 1) % len(self.slots)
+        if self.dev.type != "cuda":
+            slot.copy_(flag.to(torch.float64))
+            return slot, None
+        slot.copy_(flag.to(torch.float64), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return slot, ev
 
 
 def ftrl_update_torch(grad, wsum, coef, z, n, alpha, beta, l1, l2):
@@ -329,7 +563,9 @@ class OnlineLogisticRegressionModel(_OnlineModelMixin, ModelWithData, OnlineLogi
                 while True:
                     while i >= len(s.versions):
                         if not s.pull(block=True):
-                            return
+                            s.flush()
+                            if i >= len(s.versions):
+                                return
                     yield Table.from_rows([s.versions[i]], list(self.MODEL_DATA_COLUMNS))
                     i += 1
             return [StreamTable(gen())]
@@ -383,7 +619,7 @@ class OnlineLogisticRegression(Estimator, OnlineLogisticRegressionParams):
                               self.get(self.FEATURES_COL), self.get(self.LABEL_COL), self.get(self.WEIGHT_COL))
         src = inputs[0]
         stream = VersionedModelStream(src if not isinstance(src, Table) else StreamTable.from_table(src, 1 << 30),
-                                      self.get(self.GLOBAL_BATCH_SIZE), trainer.step)
+                                      self.get(self.GLOBAL_BATCH_SIZE), trainer, name="online-lr")
         model = OnlineLogisticRegressionModel().set_model_data(stream)
         rw_update(model, self)
         return model
@@ -422,42 +658,130 @@ def generate_random_kmeans_model_data(k: int, dim: int, weight: float, seed: int
     return KMeansModel.make_model_data_table([(cents, DenseVector(np.full(k, weight)))])
 
 
+class DeviceCentroids:
+    """A model version's centroids kept on the device (``device_values()``), read as a list of
+    ``DenseVector`` on demand (materialised once)."""
+
+    __slots__ = ("_dev", "_host")
+
+    def __init__(self, t: torch.Tensor):
+        self._dev = t
+        self._host = None
+
+    def _h(self):
+        if self._host is None:
+            self._host = [DenseVector(r) for r in self._dev.to(torch.float64).cpu().numpy()]
+        return self._host
+
+    def __len__(self):
+        return int(self._dev.shape[0])
+
+    def __getitem__(self, i):
+        return self._h()[i]
+
+    def __iter__(self):
+        return iter(self._h())
+
+    def device_values(self) -> torch.Tensor:
+        return self._dev
+
+
 class OnlineKMeansTrainer:
+    """Replicated centroids / weights on the device; one round per global mini-batch: MFMA assign
+    + ordered cluster sums (``KMeansRound``, kept across batches) → decayed local update kernel →
+    ONE all-reduce of ``[c·w | w | batch flag]`` → predicated merge kernel (also refreshes the
+    bf16 centroid image of the next assign). No host copy per batch."""
+
     def __init__(self, cents: np.ndarray, weights: np.ndarray, k: int, metric: str, decay: float, fcol: str):
         self.k, self.metric, self.decay, self.fcol = k, metric, decay, fcol
-        self.C = torch.as_tensor(cents, dtype=torch.float64)
-        self.W = torch.as_tensor(weights, dtype=torch.float64)
-
-    def step(self, batch: Table):
-        """Local decayed update (OnlineKMeans.java:292-321) then weight-averaged global merge (:188-211)
-        as one all-reduce of [Σ c·w | Σ w]."""
-        from ..parallel.context import get_context
-
-        P = get_context().world_size
-        X = config.features_for_compute(batch, self.fcol, allow_sparse=False)
-        kc, D = self.C.shape
-        if X.device.type == "cuda" and X.shape[0] > 0:
-            acc = torch.float64 if X.dtype == torch.float64 else torch.float32
-            cb = kk.CentroidBuffers(kc, D, X.device, acc)
-            cb.set(self.C)
-            rnd = kk.KMeansRound(X, kc, self.metric)
-            payload = rnd.run(cb).to(torch.float64).cpu()
+        self.dev = config.compute_device()
+        self.acc = config.acc_dtype() if self.dev.type == "cuda" else torch.float64
+        kc, D = cents.shape
+        self.D = D
+        if self.dev.type == "cuda":
+            self.cb = kk.CentroidBuffers(kc, D, self.dev, self.acc)
+            self.cb.set(torch.as_tensor(cents, dtype=torch.float64))
+            self.C = self.cb.cent
         else:
-            payload = kk.torch_round_payload(X.cpu() if X.shape[0] else X.cpu(), self.C, self.metric)
+            self.cb = None
+            self.C = torch.as_tensor(cents, dtype=torch.float64).clone()
+        self.W = torch.as_tensor(weights, dtype=self.acc, device=self.dev).clone()
+        self.merge = torch.zeros(kc * D + kc + 1, dtype=self.acc, device=self.dev)
+        self.dev_version = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self._rounds = {}  # (n, dtype) -> KMeansRound over batches of that shape
+        self._flags = _FlagRing(self.dev)
+
+    def snapshot(self):
+        return {"C": self.C.clone(), "W": self.W.clone()}
+
+    def load_state(self, st) -> None:
+        if self.cb is not None:
+            self.cb.set(st["C"].to(torch.float64))
+        else:
+            self.C.copy_(st["C"].to(self.C))
+        self.W.copy_(st["W"].to(self.W))
+
+    def version_from_state(self):
+        return self._version_obj()
+
+    def _version_obj(self):
+        if self.dev.type == "cuda":
+            return (DeviceCentroids(self.C.clone()), DeviceDenseVector(self.W.clone()))
+        return ([DenseVector(c) for c in self.C.numpy()], DenseVector(self.W.to(torch.float64).numpy()))
+
+    def _local_merge_payload(self, batch: Optional[Table], P: int) -> None:
+        kc, D = self.C.shape
+        M = self.merge
+        X = None if batch is None else config.features_for_compute(batch, self.fcol, allow_sparse=False)
+        if X is None or X.shape[0] == 0:
+            M.zero_()
+            return
+        if self.dev.type == "cuda":
+            key = (int(X.shape[0]), X.dtype, X.stride(0), X.data_ptr() % 16)
+            rnd = self._rounds.get(key)
+            if rnd is None:
+                rnd = self._rounds[key] = kk.KMeansRound(X, kc, self.metric)
+            rnd.X = X  # same shape and alignment: the round's buffers are reused
+            red = rnd.run(self.cb)
+            native.call("fmlx_okm_local_update", int(self.acc == torch.float64), native.ptr(red), native.ptr(self.C),
+                        native.ptr(self.W), kc, D, self.decay / P, native.ptr(M), native.stream_ptr(self.dev))
+            return
+        payload = kk.torch_round_payload(X.cpu(), self.C, self.metric)
         sums = payload[: kc * D].reshape(kc, D)
         counts = payload[kc * D:]
-        C = self.C.clone()
         W = self.W * (self.decay / P)
         nz = counts > 0
         W = torch.where(nz, W + counts, W)
         lam = torch.where(nz, counts / torch.where(nz, W, torch.ones_like(W)), torch.zeros_like(W))
-        C = torch.where(nz[:, None], C * (1.0 - lam)[:, None] + sums * (lam / torch.where(nz, counts, torch.ones_like(
-            counts)))[:, None], C)
-        merged = comm.all_reduce_sum(torch.cat([(C * W[:, None]).reshape(-1), W]))
-        Wt = merged[kc * D:]
-        self.C = merged[: kc * D].reshape(kc, D) / torch.clamp(Wt, min=1e-16)[:, None]
-        self.W = Wt
-        return ([DenseVector(c) for c in self.C.numpy()], DenseVector(self.W.numpy()))
+        C = torch.where(nz[:, None], self.C * (1.0 - lam)[:, None] + sums * (lam / torch.where(
+            nz, counts, torch.ones_like(counts)))[:, None], self.C)
+        M[: kc * D] = (C * W[:, None]).reshape(-1)
+        M[kc * D: kc * D + kc] = W
+        M[-1] = 1
+
+    def launch(self, batch: Optional[Table], world: int, snapshot_state: bool = False) -> "_Round":
+        kc, D = self.C.shape
+        self._local_merge_payload(batch, world)
+        M = comm.all_reduce_sum(self.merge)
+        flag = M[kc * D + kc:]
+        if self.dev.type == "cuda":
+            cb = self.cb
+            native.call("fmlx_okm_merge", int(self.acc == torch.float64), native.ptr(M), kc, D, world if world > 1 else 1,
+                        native.ptr(self.C), native.ptr(self.W), native.ptr(cb.Cb), cb.DP, native.ptr(cb.cnorm_b),
+                        native.ptr(cb.cnorm), native.ptr(self.dev_version), native.stream_ptr(self.dev))
+        elif float(flag[0]) > world - 0.5:
+            Wt = M[kc * D: kc * D + kc]
+            self.C = M[: kc * D].reshape(kc, D) / torch.clamp(Wt, min=1e-16)[:, None]
+            self.W = Wt.clone()
+        rnd = _Round(self._version_obj(), state=self.snapshot() if snapshot_state else None)
+        if world > 1:
+            rnd.flag, rnd.event = self._flags.copy(flag)
+        return rnd
+
+    def step(self, batch: Table):
+        from ..parallel.context import get_context
+
+        return self.launch(batch, get_context().world_size).version
 
 
 @rw.register_stage
@@ -495,7 +819,8 @@ class OnlineKMeansModel(_OnlineModelMixin, ModelWithData, OnlineKMeansModelParam
 
     def _predict_batch(self, t: Table) -> Table:
         ver = self._current(block=True)
-        C = torch.as_tensor(np.stack([c.to_array() for c in ver[0]]), dtype=torch.float64)
+        C = (ver[0].device_values().to(torch.float64) if isinstance(ver[0], DeviceCentroids)
+             else torch.as_tensor(np.stack([c.to_array() for c in ver[0]]), dtype=torch.float64))
         X = config.features_for_compute(t, self.get(self.FEATURES_COL), allow_sparse=False)
         metric = self.get(self.DISTANCE_MEASURE)
         if X.device.type == "cuda":
@@ -533,8 +858,8 @@ class OnlineKMeans(Estimator, OnlineKMeansParams):
                                  self.get(self.DECAY_FACTOR), self.get(self.FEATURES_COL))
         src = inputs[0]
         stream = VersionedModelStream(src if not isinstance(src, Table) else StreamTable.from_table(src, 1 << 30),
-                                      self.get(self.GLOBAL_BATCH_SIZE), tr.step,
-                                      initial_versions=[(list(cents), weights)])
+                                      self.get(self.GLOBAL_BATCH_SIZE), tr, initial_versions=[(list(cents), weights)],
+                                      name="online-kmeans")
         model = OnlineKMeansModel().set_model_data(stream)
         rw_update(model, self)
         return model

@@ -188,3 +188,207 @@ def test_gpu_online_kmeans():
         pytest.skip("no GPU")
     test_online_kmeans_decay()
     test_online_kmeans_streaming()
+
+
+def _spmd_olr_uneven(rank, world):
+    """Rank 0's shard holds one more global batch than the others: every rank must stop after
+    the batches ALL ranks have (the end of a stream travels in the round's payload flag)."""
+    init = Table.from_rows([(Vectors.dense(0.41233679404769874, -0.18088118293232122), 0)],
+                           ["coefficient", "modelVersion"])
+    train = Table.from_rows(TRAIN1 + TRAIN2 + TRAIN1, ["features", "label"])
+    b = 10 // world + (1 if 10 % world > rank else 0)
+    off = sum(10 // world + (1 if 10 % world > r else 0) for r in range(rank))
+    nb = 3 if rank == 0 else 2
+    local = Table.concat([train.slice(10 * i + off, 10 * i + off + b) for i in range(nb)])
+    model = (OnlineLogisticRegression().set_reg(0.2).set_elastic_net(0.5).set_global_batch_size(10)
+             .set_initial_model_data(init).fit(local))
+    versions = [t.rows()[0][1] for t in model.get_model_data()[0]]
+    out = model.transform(Table.from_rows(PREDICT, ["features", "label"]))[0]
+    return versions, _raw(out)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_online_lr_uneven_streams_stop_together(world):
+    for versions, raw in run_spmd(_spmd_olr_uneven, world):
+        assert versions == [1, 2]
+        assert np.allclose(raw, EXP2, atol=1e-7)
+
+
+def _okm_stream(rank, world, nbatches=4, seed=0):
+    g = np.random.default_rng(seed)
+    pts = np.concatenate([g.normal(c, 0.3, size=(60, 2)) for c in ((0, 0), (5, 5), (0, 5))])
+    g.shuffle(pts)
+    rows = [(Vectors.dense(*p),) for p in pts[: 12 * nbatches]]
+    glob = Table.from_rows(rows, ["features"])
+    b = 12 // world + (1 if 12 % world > rank else 0)
+    off = sum(12 // world + (1 if 12 % world > r else 0) for r in range(rank))
+    return Table.concat([glob.slice(12 * i + off, 12 * i + off + b) for i in range(nbatches)])
+
+
+def _spmd_okm(rank, world):
+    init = generate_random_kmeans_model_data(3, 2, 0.0, 7)
+    model = (OnlineKMeans().set_k(3).set_global_batch_size(12).set_decay_factor(0.5).set_initial_model_data(init)
+             .fit(_okm_stream(rank, world)))
+    model._stream.drain_available()
+    cents, w = model._stream.latest()
+    return np.stack([c.values for c in cents]).tolist(), w.values.tolist(), model.model_data_version()
+
+
+def test_online_kmeans_ranks_agree_with_one_rank():
+    ref = _spmd_okm(0, 1)
+    for got in run_spmd(_spmd_okm, 3):
+        assert got[2] == ref[2] == 5  # initial model + 4 updates
+        assert np.allclose(got[0], ref[0], atol=1e-9) and np.allclose(got[1], ref[1], atol=1e-9)
+
+
+def _online_ck(rank, world, ck_dir, attempt, fail_round, which):
+    import os
+
+    os.environ["FMLX_ATTEMPT"] = str(attempt)
+    from flink_ml_amd.parallel import checkpoint as ckpt
+
+    ckpt.clear_faults()
+    ckpt.enable(ck_dir, interval=2)
+    if fail_round is not None:
+        ckpt.inject(ckpt.FailAfter(fail_round, rank=0, on_attempt=0))
+    if which == "lr":
+        init = Table.from_rows([(Vectors.dense(0.41233679404769874, -0.18088118293232122), 0)],
+                               ["coefficient", "modelVersion"])
+        train = Table.from_rows((TRAIN1 + TRAIN2) * 3, ["features", "label"])
+        b = 10 // world + (1 if 10 % world > rank else 0)
+        off = sum(10 // world + (1 if 10 % world > r else 0) for r in range(rank))
+        local = Table.concat([train.slice(10 * i + off, 10 * i + off + b) for i in range(6)])
+        model = (OnlineLogisticRegression().set_reg(0.2).set_elastic_net(0.5).set_global_batch_size(10)
+                 .set_initial_model_data(init).fit(local))
+        model._stream.drain_available()
+        coef, ver = model._stream.latest()
+        return coef.values.tolist(), int(ver)
+    init = generate_random_kmeans_model_data(3, 2, 0.0, 7)
+    model = (OnlineKMeans().set_k(3).set_global_batch_size(12).set_decay_factor(0.5).set_initial_model_data(init)
+             .fit(_okm_stream(rank, world, nbatches=7)))
+    model._stream.drain_available()
+    cents, w = model._stream.latest()
+    return np.stack([c.values for c in cents]).tolist(), model.model_data_version()
+
+
+@pytest.mark.parametrize("which", ["lr", "kmeans"])
+def test_online_failover_resumes_exactly(which, tmp_path):
+    """Online (unbounded) training checkpoints the FTRL state (z, n, coef, version) / the
+    centroids and weights every 2 model versions; after an injected failure at version 5 the
+    restarted job resumes from version 4, skips the consumed batches and ends identical."""
+    clean = run_spmd(_online_ck, 2, str(tmp_path / "clean"), 0, None, which)
+    ck = str(tmp_path / "ck")
+    with pytest.raises(RuntimeError, match="injected failure"):
+        run_spmd(_online_ck, 2, ck, 0, 5, which)
+    resumed = run_spmd(_online_ck, 2, ck, 1, 5, which)
+    for a, b in zip(clean, resumed):
+        assert a[1] == b[1] and np.allclose(a[0], b[0], atol=0, rtol=0)
+
+
+def _rand_sparse_rows(n, d, nnz, seed):
+    g = np.random.default_rng(seed)
+    rows = []
+    for i in range(n):
+        idx = np.sort(g.choice(d, size=nnz, replace=False))
+        lab = float(idx.sum() % 2)
+        rows.append((Vectors.sparse(d, idx.tolist(), g.random(nnz).tolist()), lab, 0.5 + g.random()))
+    return rows
+
+
+def _train_olr(policy, rows, d, gb, weighted):
+    from flink_ml_amd.config import dtype_policy
+
+    with dtype_policy(policy):
+        init = Table.from_rows([(Vectors.dense(*([0.01] * d)), 0)], ["coefficient", "modelVersion"])
+        est = (OnlineLogisticRegression().set_reg(0.1).set_elastic_net(0.3).set_global_batch_size(gb)
+               .set_initial_model_data(init))
+        if weighted:
+            est.set_weight_col("w")
+        model = est.fit(Table.from_rows(rows, ["features", "label", "w"]))
+        model._stream.drain_available()
+        coef, ver = model._stream.latest()
+        return np.asarray(coef.values), int(ver)
+
+
+@pytest.mark.gpu
+def test_gpu_online_lr_sparse_kernel_matches_host():
+    """online.hip ftrl_grad_csr (wave per CSR row, scatter-add) + the predicated FTRL update vs
+    the host implementation of the reference's sparse branch (weighted weight sums)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rows = _rand_sparse_rows(3000, 500, 17, 3)
+    ref, rv = _train_olr_on("cpu", rows)
+    got, gv = _train_olr("fp64", rows, 500, 600, True)
+    assert gv == rv == 5
+    assert np.allclose(got, ref, rtol=1e-9, atol=1e-12)
+
+
+def _train_olr_on(device, rows):
+    import os
+
+    old = os.environ.get("FMLX_DEVICE")
+    os.environ["FMLX_DEVICE"] = device
+    from flink_ml_amd.parallel import context
+
+    context.reset_context()
+    try:
+        return _train_olr("fp64", rows, 500, 600, True)
+    finally:
+        if old is None:
+            os.environ.pop("FMLX_DEVICE", None)
+        else:
+            os.environ["FMLX_DEVICE"] = old
+        context.reset_context()
+
+
+@pytest.mark.gpu
+def test_gpu_online_kmeans_device_update_matches_host():
+    """Device OnlineKMeans round (assign + ordered sums, okm_local_update, okm_merge) in fp64 vs
+    the host reference implementation, over several batches."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import os
+
+    from flink_ml_amd.config import dtype_policy
+    from flink_ml_amd.parallel import context
+
+    g = np.random.default_rng(5)
+    pts = np.concatenate([g.normal(c, 0.5, size=(1000, 16)) for c in range(8)])
+    g.shuffle(pts)
+    init = Table({"centroids": [[Vectors.dense(*p) for p in pts[:8]]], "weights": [Vectors.dense(*([1.0] * 8))]},
+                 num_rows=1)
+    data = Table({"features": torch.as_tensor(pts)}, num_rows=len(pts))
+
+    def run():
+        with dtype_policy("fp64"):
+            m = OnlineKMeans().set_k(8).set_global_batch_size(1600).set_decay_factor(0.7).set_initial_model_data(
+                init).fit(data)
+            m._stream.drain_available()
+            c, w = m._stream.latest()
+            return np.stack([v.values for v in c]), np.asarray(w.values), m.model_data_version()
+
+    got = run()
+    os.environ["FMLX_DEVICE"] = "cpu"
+    context.reset_context()
+    try:
+        ref = run()
+    finally:
+        os.environ.pop("FMLX_DEVICE", None)
+        context.reset_context()
+    assert got[2] == ref[2] == 6
+    assert np.allclose(got[0], ref[0], rtol=1e-9, atol=1e-9) and np.allclose(got[1], ref[1], rtol=1e-12)
+
+
+@pytest.mark.gpu
+def test_gpu_stream_prefetch_to_device():
+    """StreamTable.to_device: batches copied host→device on a side stream, handed to the consumer
+    stream (record_stream) — identical values, device-resident."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    X = torch.rand(10_000, 33, dtype=torch.float64)
+    t = Table({"features": X, "label": torch.arange(10_000, dtype=torch.float64)}, num_rows=10_000)
+    got = list(StreamTable.from_table(t, 1000).to_device(torch.device("cuda")))
+    assert len(got) == 10
+    for i, b in enumerate(got):
+        f = b.column("features")
+        assert f.is_cuda and torch.equal(f.cpu(), X[1000 * i:1000 * (i + 1)])
