@@ -737,12 +737,16 @@ class OnlineKMeansTrainer:
             M.zero_()
             return
         if self.dev.type == "cuda":
+            if X.dtype not in (torch.bfloat16, self.acc):
+                X = X.to(self.acc)  # the round's [sums | counts] must come in the trainer's dtype
             key = (int(X.shape[0]), X.dtype, X.stride(0), X.data_ptr() % 16)
             rnd = self._rounds.get(key)
             if rnd is None:
                 rnd = self._rounds[key] = kk.KMeansRound(X, kc, self.metric)
             rnd.X = X  # same shape and alignment: the round's buffers are reused
             red = rnd.run(self.cb)
+            if red.dtype != self.acc:
+                red = red.to(self.acc)
             native.call("fmlx_okm_local_update", int(self.acc == torch.float64), native.ptr(red), native.ptr(self.C),
                         native.ptr(self.W), kc, D, self.decay / P, native.ptr(M), native.stream_ptr(self.dev))
             return
