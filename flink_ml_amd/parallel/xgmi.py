@@ -59,6 +59,7 @@ native.register_kernel_sigs({
 # polls (each ≈ one xGMI round trip + s_sleep) before a wait gives up: several seconds, far
 # beyond any lockstep drift between ranks, far below a hang
 DEFAULT_SPIN = int(os.environ.get("FMLX_XGMI_SPIN", str(1 << 22)))
+MAX_ONESHOT_ELEMS = int(os.environ.get("FMLX_XGMI_MAX_ELEMS", str(1 << 18)))
 
 
 class XgmiTimeout(RuntimeError):
@@ -150,8 +151,12 @@ class XgmiComm:
                 self.spin_limit)
 
     def accepts(self, t: torch.Tensor) -> bool:
+        """Small payloads only (≤ ``FMLX_XGMI_MAX_ELEMS``, default 256K elements = 1 MB fp32): the
+        one-shot exchange is latency-optimal there; above it RCCL's ring/tree pipelines win on
+        bandwidth, and a one-shot grid of ~1000 spinning blocks per rank must not have to share
+        CUs with its peers' grids (ranks rehearsed on one GPU)."""
         return (t.is_cuda and t.device == self.device and t.dtype in (torch.float32, torch.float64)
-                and t.is_contiguous() and t.numel() <= self.max_elems)
+                and t.is_contiguous() and t.numel() <= min(self.max_elems, MAX_ONESHOT_ELEMS))
 
     def all_reduce_(self, t: torch.Tensor, state: Optional[torch.Tensor] = None) -> torch.Tensor:
         """In-place sum over the group (same shape on every rank), stream-ordered on the current

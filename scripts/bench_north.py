@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""North-star configs 3–5 of BASELINE.json as one launchable script (one rank per GPU):
+
+  --config kmeans      KMeans k=1024 on 100M × 128 dense (bf16), the 100M rows sharded over N ranks
+  --config svc_sparse  LinearSVC on 50M × 1M sparse CSR features (hinge SGD), sharded over N ranks
+  --config online_lr   OnlineLogisticRegression on an unbounded stream, global batch 100k
+
+Every rank generates its own shard on its device (synthetic data of the configured shape), the
+timed region is the whole fit including collectives (bracketed by barrier + synchronize, max over
+ranks), and rank 0 prints ONE JSON line shaped like bench.py's, plus the collective path actually
+taken (``xgmi`` one-shot kernel / ``nccl`` = RCCL / ``gloo``) and the world size the process group
+reports. Launch:
+
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
+      --master-port 29500 scripts/bench_north.py --config kmeans
+
+Rehearsal of N ranks on ONE GPU (what this repo's 1-GPU box can run): FMLX_DEVICE=cuda:0
+FMLX_BACKEND=gloo FMLX_XGMI=force and ``--scale`` < 1 to shrink the shards.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from flink_ml_amd.parallel import comm  # noqa: E402
+from flink_ml_amd.parallel.context import init_distributed  # noqa: E402
+
+
+def _path(ctx) -> str:
+    if ctx.world_size == 1:
+        return "none"
+    from flink_ml_amd.parallel import xgmi
+
+    return "xgmi" if xgmi.get() is not None else ctx.backend
+
+
+def _timed(ctx, fn):
+    torch.cuda.synchronize()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = fn()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    return comm.all_reduce_scalar(time.perf_counter() - t0, "max"), out
+
+
+def _shard_rows(total: int, world: int, rank: int) -> int:
+    return total // world + (1 if total % world > rank else 0)
+
+
+def run_kmeans(a, ctx):
+    from flink_ml_amd import Table
+    from flink_ml_amd.config import dtype_policy
+    from flink_ml_amd.models import KMeans
+    from flink_ml_amd.models.kmeans import kmeans_lloyd, sample_rows
+
+    total = int(100_000_000 * a.scale)
+    n = _shard_rows(total, ctx.world_size, ctx.rank)
+    g = torch.Generator(device=ctx.device).manual_seed(17 + ctx.rank)
+    X = torch.empty((n, 128), dtype=torch.bfloat16, device=ctx.device)
+    for s in range(0, n, 1 << 22):
+        e = min(s + (1 << 22), n)
+        X[s:e] = torch.rand((e - s, 128), generator=g, device=ctx.device).to(torch.bfloat16)
+    t = Table({"features": X})
+    k, iters = 1024, a.iters
+    with dtype_policy("bf16"):
+        KMeans().set_k(k).set_max_iter(1).fit(t)  # untimed warm-up: library load, allocator, graphs
+        fit_s, _ = _timed(ctx, lambda: KMeans().set_k(k).set_max_iter(iters).set_seed(1).fit(t))
+        init = sample_rows(X, k, 1)
+        lloyd_s, _ = _timed(ctx, lambda: kmeans_lloyd(X, init, iters, "euclidean"))
+    flops = 2.0 * total * k * 128 * iters
+    return {"metric": "KMeans fit inputThroughput (whole job), k=1024 on 100M x 128 dense",
+            "value": round(total / fit_s, 1), "unit": "records/s", "higher_is_better": True,
+            "totalTimeMs": round(fit_s * 1e3, 2), "ms_per_iter": round(lloyd_s * 1e3 / iters, 3),
+            "train_samples_per_s": round(total * iters / lloyd_s, 1),
+            "distance_tflops_per_s": round(flops / lloyd_s / 1e12, 1),
+            "config": {"model": "KMeans", "k": k, "rows": total, "dim": 128, "maxIter": iters, "rows_per_gpu": n,
+                       "dtype": "bf16"}}
+
+
+def run_svc_sparse(a, ctx):
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer
+    from flink_ml_amd.table import SparseColumn
+
+    total = int(50_000_000 * a.scale)
+    n = _shard_rows(total, ctx.world_size, ctx.rank)
+    dim, nnz = 1_000_000, a.nnz
+    g = torch.Generator(device=ctx.device).manual_seed(7 + ctx.rank)
+    idx = torch.empty((n, nnz), dtype=torch.int32, device=ctx.device)
+    for s in range(0, n, 1 << 20):
+        e = min(s + (1 << 20), n)
+        blk = torch.randint(0, dim, (e - s, nnz), generator=g, device=ctx.device, dtype=torch.int32)
+        idx[s:e] = torch.sort(blk, dim=1).values
+    indptr = torch.arange(0, (n + 1) * nnz, nnz, dtype=torch.int64, device=ctx.device)
+    vals = torch.rand((n * nnz,), generator=g, device=ctx.device, dtype=torch.float32)
+    X = SparseColumn(indptr, idx.reshape(-1), vals, dim)
+    y = torch.randint(0, 2, (n,), generator=g, device=ctx.device).to(torch.float32)
+    gb = a.batch * ctx.world_size
+    iters = a.iters
+    sgd = SGD(max_iter=iters, learning_rate=0.1, global_batch_size=gb, tol=0.0)
+    tr = DeviceGlmTrainer(sgd, np.zeros(dim), X, y, None, "hinge")
+    tr.run_rounds(1)  # untimed warm-up (CSC build happened in the constructor)
+    tr2 = DeviceGlmTrainer(SGD(max_iter=iters, learning_rate=0.1, global_batch_size=gb, tol=0.0), np.zeros(dim), X, y,
+                           None, "hinge")
+    fit_s, _ = _timed(ctx, tr2.fit)
+    return {"metric": "LinearSVC training samples/s (whole job), 50M x 1M sparse CSR",
+            "value": round(gb * iters / fit_s, 1), "unit": "samples/s", "higher_is_better": True,
+            "ms_per_round": round(fit_s * 1e3 / iters, 4),
+            "config": {"model": "LinearSVC (hinge SGD)", "rows": total, "dim": dim, "nnz_per_row": nnz,
+                       "global_batch": gb, "maxIter": iters, "rows_per_gpu": n, "dtype": "fp32",
+                       "csr_transpose": tr2.csc is not None}}
+
+
+def run_online_lr(a, ctx):
+    from flink_ml_amd import Table
+    from flink_ml_amd.lib.classification.logisticregression import OnlineLogisticRegression
+    from flink_ml_amd.linalg import Vectors
+    from flink_ml_amd.stream import StreamTable
+
+    world, rank = ctx.world_size, ctx.rank
+    gb, dim = a.batch, 1000
+    local = _shard_rows(gb, world, rank)
+    nb = a.iters + 3
+    g = torch.Generator(device=ctx.device).manual_seed(100 + rank)
+    X = torch.rand((local * nb, dim), generator=g, device=ctx.device).to(torch.bfloat16)
+    y = (X[:, :8].float().sum(1) > 4).double()
+    if a.host_stream:
+        X, y = X.cpu().pin_memory(), y.cpu().pin_memory()  # the stream arrives from host memory
+    t = Table({"features": X, "label": y})
+    init = Table.from_rows([(Vectors.dense(np.zeros(dim)), 0)], ["coefficient", "modelVersion"])
+    model = OnlineLogisticRegression().set_global_batch_size(gb).set_initial_model_data(init).fit(
+        StreamTable.from_table(t, local))
+    stream = model._stream
+    for _ in range(2):  # warm-up batches (first version, kernel / graph set-up)
+        assert stream.pull(block=True)
+    done = [0]
+
+    def body():
+        while done[0] < a.iters and stream.pull(block=True):
+            done[0] += 1
+        stream.flush()
+
+    el, _ = _timed(ctx, body)
+    return {"metric": "OnlineLogisticRegression stream samples/s (whole job), global batch 100k, dim 1000",
+            "value": round(done[0] * gb / el, 1), "unit": "samples/s", "higher_is_better": True,
+            "ms_per_batch": round(el * 1e3 / max(done[0], 1), 4),
+            "config": {"model": "OnlineLogisticRegression (FTRL)", "global_batch": gb, "dim": dim,
+                       "batches": done[0], "dtype": "bf16",
+                       "ingest": "host (pinned) -> H2D copy stream" if a.host_stream else "device-resident shard"}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", required=True, choices=["kmeans", "svc_sparse", "online_lr"])
+    ap.add_argument("--scale", type=float, default=1.0, help="fraction of the configured rows (rehearsals)")
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=100_000, help="svc: per-GPU batch; online_lr: global batch")
+    ap.add_argument("--nnz", type=int, default=64, help="svc: non-zeros per row")
+    ap.add_argument("--host-stream", action="store_true", help="online_lr: stream the batches from host memory")
+    a = ap.parse_args()
+    ctx = init_distributed()
+    if ctx.device.type != "cuda":
+        raise SystemExit("bench_north.py needs a GPU")
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not ctx.is_distributed:
+        raise SystemExit("WORLD_SIZE > 1 but the process group did not come up")
+    rec = {"run_kmeans": run_kmeans, "run_svc_sparse": run_svc_sparse, "run_online_lr": run_online_lr}[
+        "run_" + a.config](a, ctx)
+    if ctx.rank == 0:
+        rec.update({"n_gpus": ctx.world_size, "world_size_reported": ctx.world_size, "backend": ctx.backend,
+                    "collective_path": _path(ctx), "scale": a.scale,
+                    "data": "synthetic, generated on each rank's device", "scaling": "weak" if a.config ==
+                    "svc_sparse" else "strong"})
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
