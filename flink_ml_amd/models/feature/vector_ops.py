@@ -14,6 +14,8 @@ from typing import List
 import numpy as np
 import torch
 
+from ...ops import blas
+
 from ...api.stage import Transformer
 from ...common.param import HasHandleInvalid, HasInputCol, HasInputCols, HasOutputCol, HasOutputCols
 from ...io import read_write as rw
@@ -145,11 +147,8 @@ class ElementwiseProduct(Transformer, HasInputCol, HasOutputCol):
         d = X.size if isinstance(X, SparseColumn) else X.shape[1]
         if sv.size() != d:
             raise ValueError("The scaling vector size is %d, which is not equal input vector size(%d)." % (sv.size(), d))
-        if isinstance(X, SparseColumn):
-            s = torch.as_tensor(sv.to_array(), dtype=torch.float64, device=X.values.device)
-            out = sparse_map_values(X, lambda v, i: v * s[i])
-        else:
-            out = fo.affine_cols(X, None, torch.as_tensor(sv.to_array(), dtype=torch.float64))
+        # BLAS.hDot over the whole column (ops/blas.py: one HIP launch on the device)
+        out = blas.hdot(torch.as_tensor(sv.to_array(), dtype=torch.float64), X)
         return [t.with_column(self.get(self.OUTPUT_COL), out)]
 
 
@@ -162,20 +161,8 @@ class Normalizer(Transformer, HasInputCol, HasOutputCol):
     def transform(self, *inputs):
         t = inputs[0]
         X = vector_input(t, self.get(self.INPUT_COL))
-        p = self.get(self.P)
-        if isinstance(X, SparseColumn):
-            v = X.values.to(torch.float64)
-            r = row_ids(X)
-            a = v.abs()
-            if math.isinf(p):
-                norm = torch.zeros(len(X), dtype=torch.float64, device=v.device).scatter_reduce(0, r, a, "amax")
-            else:
-                norm = torch.zeros(len(X), dtype=torch.float64, device=v.device).index_add_(0, r, a ** p) ** (1.0 / p)
-            out = SparseColumn(X.indptr, X.indices, v / norm[r], X.size)
-        else:
-            Xd = X.to(torch.float64) if X.device.type == "cpu" else X.float() if X.dtype == torch.bfloat16 else X
-            norm = torch.linalg.vector_norm(Xd, ord=p, dim=1)
-            out = Xd * (1.0 / norm)[:, None]
+        # BLAS.norm + BLAS.scal per row, fused (ops/blas.py normalize: one pass over each row)
+        out = blas.normalize(X, self.get(self.P))
         return [t.with_column(self.get(self.OUTPUT_COL), out)]
 
 
@@ -249,9 +236,8 @@ class Interaction(Transformer, HasInputCols, HasOutputCol):
             else:
                 sparse = sparse or t.is_sparse(c)
                 mats.append(dense_input(t, c).to(torch.float64))
-        out = mats[0]
-        for m in mats[1:]:
-            out = (out[:, :, None] * m.to(out.device)[:, None, :]).reshape(out.shape[0], -1)
+        dev = mats[0].device
+        out = blas.interaction([m.to(dev) for m in mats])  # one launch: row-wise outer products
         if sparse:
             out = SparseColumn.from_dense(out)
         return [t.with_column(self.get(self.OUTPUT_COL), out)]
@@ -348,12 +334,28 @@ class VectorSlicer(Transformer, HasInputCol, HasOutputCol):
         if max(idx) >= d:
             raise ValueError("Index value %d is greater than vector size:%d" % (max(idx), d))
         if isinstance(X, SparseColumn):
-            dense = X.to_dense(torch.float64)
-            sel = dense[:, torch.as_tensor(idx, device=dense.device)]
-            out = SparseColumn.from_dense(sel)
+            out = _slice_sparse(X, idx)
         else:
-            out = X[:, torch.as_tensor(idx, device=X.device)]
+            out = blas.gather_cols(X, idx)
         return [t.with_column(self.get(self.OUTPUT_COL), out)]
+
+
+def _slice_sparse(X: SparseColumn, idx) -> SparseColumn:
+    """Selects columns of CSR rows without densifying (1M-wide rows stay sparse): old column →
+    position in ``idx`` (or −1), kept non-zeros re-indexed and sorted within each row."""
+    dev = X.values.device
+    m = len(idx)
+    pos = torch.full((X.size,), -1, dtype=torch.int64, device=dev)
+    pos[torch.as_tensor(list(idx), dtype=torch.int64, device=dev)] = torch.arange(m, device=dev)
+    counts = X.indptr[1:] - X.indptr[:-1]
+    rows = torch.repeat_interleave(torch.arange(len(X), device=dev), counts.to(dev))
+    newc = pos[X.indices.to(dev).long()]
+    keep = newc >= 0
+    rows, newc, vals = rows[keep], newc[keep], X.values.to(dev)[keep]
+    order = torch.argsort(rows * m + newc)
+    indptr = torch.zeros(len(X) + 1, dtype=torch.int64, device=dev)
+    indptr[1:] = torch.cumsum(torch.bincount(rows, minlength=len(X)), 0)
+    return SparseColumn(indptr, newc[order].to(torch.int32), vals[order], m)
 
 
 def _indices_validator():

@@ -1,0 +1,532 @@
+// Device BLAS on columnar row tensors (SURVEY §2.1 K1 dense BLAS-1, K2 sparse BLAS-1, K3 gemv).
+//
+// Reference: flink-ml-core/src/main/java/org/apache/flink/ml/linalg/BLAS.java:30-204 — asum,
+// axpy (dense / sparse, first k), hDot (dense∘dense, sparse∘dense, …), dot (dense·dense,
+// sparse·dense, sparse·sparse merge), norm2, norm(p), scal, gemv (N / T). There each call works on
+// ONE vector; here every op runs over a whole column of vectors in one launch:
+//   dense rows  X [n, d] row-major (bf16 / fp32 / fp64; fp32 accumulation for bf16 / fp32,
+//               fp64 for fp64),
+//   CSR rows    (indptr [n+1] int64, indices int32, values) of width d.
+//
+// Row reductions map TPR lanes to a row (TPR = 4 … 64, a power of two ≥ d/VEC picked by the host,
+// so short rows do not leave 60 of 64 lanes idle) with 16-byte vector loads where rows allow;
+// the segment reduction is a shfl_xor butterfly inside the TPR-lane group. Row-wise results are
+// written once; Normalizer's scale is fused with its norm (one HBM read, one write per row).
+// gemv 'T' (Xᵀ·m, a column reduction) is two fixed-order stages: per-block column partials,
+// then one ordered sum per column — deterministic, no atomics.
+#include "common.h"
+
+namespace {
+
+enum { OP_DOT = 0, OP_DOTV = 1, OP_NORM2 = 2, OP_NORM1 = 3, OP_NORMINF = 4, OP_NORMP = 5, OP_ASUM = 6 };
+
+template <typename A, int TPR>
+__device__ __forceinline__ A seg_reduce_sum(A v) {
+#pragma unroll
+  for (int off = TPR / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+template <typename A, int TPR>
+__device__ __forceinline__ A seg_reduce_max(A v) {
+#pragma unroll
+  for (int off = TPR / 2; off > 0; off >>= 1) {
+    const A o = __shfl_xor(v, off, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ typename AccOf<T>::type ldv(const T* p, long i) {
+  return (typename AccOf<T>::type)Ld<T>::f(p[i]);
+}
+
+template <typename A>
+__device__ __forceinline__ A term(int op, A x, A y, A p) {
+  switch (op) {
+    case OP_DOT:
+    case OP_DOTV: return x * y;
+    case OP_NORM2: return x * x;
+    case OP_NORM1:
+    case OP_ASUM:
+    case OP_NORMINF: return x < (A)0 ? -x : x;
+    default: {
+      const A a = x < (A)0 ? -x : x;
+      return a == (A)0 ? (A)0 : pow(a, p);
+    }
+  }
+}
+
+template <typename A>
+__device__ __forceinline__ A finish(int op, A s, A p) {
+  switch (op) {
+    case OP_NORM2: return sqrt(s);
+    case OP_NORMP: return pow(s, (A)1 / p);
+    default: return s;
+  }
+}
+
+// out[r] = reduce_c term(X[r,c], Y[r,c] | v[c]); TPR lanes per row, rows grid-strided.
+template <typename T, int TPR>
+__global__ __launch_bounds__(256) void rowreduce_kernel(const T* __restrict__ X, long ldx, const T* __restrict__ Y,
+                                                        long ldy, const T* __restrict__ v, long n, int d, int op,
+                                                        double pd, typename AccOf<T>::type* __restrict__ out) {
+  typedef typename AccOf<T>::type A;
+  const A p = (A)pd;
+  const int sub = threadIdx.x % TPR;
+  const long rows_per_grid = (long)gridDim.x * (blockDim.x / TPR);
+  for (long r = (long)blockIdx.x * (blockDim.x / TPR) + threadIdx.x / TPR; r < n; r += rows_per_grid) {
+    const T* xr = X + r * ldx;
+    A s = 0;
+    for (int c = sub; c < d; c += TPR) {
+      const A x = ldv(xr, c);
+      const A y = op == OP_DOT ? ldv(Y + r * ldy, c) : (op == OP_DOTV ? ldv(v, c) : (A)0);
+      const A t = term<A>(op, x, y, p);
+      s = op == OP_NORMINF ? (t > s ? t : s) : s + t;
+    }
+    s = op == OP_NORMINF ? seg_reduce_max<A, TPR>(s) : seg_reduce_sum<A, TPR>(s);
+    if (sub == 0) out[r] = finish<A>(op, s, p);
+  }
+}
+
+// Normalizer: out[r,:] = X[r,:] / ‖X[r,:]‖_p (p = inf: max |x|); a zero row divides by zero like
+// the reference (BLAS.scal(1 / norm)). TPR lanes per row; the row stays in L1/L2 between the two
+// sweeps of the same wave.
+template <typename T, typename O, int TPR>
+__global__ __launch_bounds__(256) void normalize_kernel(const T* __restrict__ X, long ldx, long n, int d, double pd,
+                                                        int pinf, O* __restrict__ out, long ldo) {
+  typedef typename AccOf<T>::type A;
+  const A p = (A)pd;
+  const int sub = threadIdx.x % TPR;
+  const long rows_per_grid = (long)gridDim.x * (blockDim.x / TPR);
+  for (long r = (long)blockIdx.x * (blockDim.x / TPR) + threadIdx.x / TPR; r < n; r += rows_per_grid) {
+    const T* xr = X + r * ldx;
+    A s = 0;
+    for (int c = sub; c < d; c += TPR) {
+      const A x = ldv(xr, c);
+      const A a = x < (A)0 ? -x : x;
+      s = pinf ? (a > s ? a : s) : s + (p == (A)2 ? a * a : (p == (A)1 ? a : (a == (A)0 ? (A)0 : pow(a, p))));
+    }
+    s = pinf ? seg_reduce_max<A, TPR>(s) : seg_reduce_sum<A, TPR>(s);
+    const A norm = pinf ? s : (p == (A)2 ? sqrt(s) : (p == (A)1 ? s : pow(s, (A)1 / p)));
+    const A inv = (A)1 / norm;
+    O* orow = out + r * ldo;
+    for (int c = sub; c < d; c += TPR) orow[c] = (O)(ldv(xr, c) * inv);
+  }
+}
+
+// Y = alpha·X + beta·Y with alpha / beta scalars or per-row vectors (axpy: beta = 1; scal: X = Y,
+// alpha = 0 … written as beta-only). Grid-stride over n·d elements.
+template <typename T, typename A>
+__global__ __launch_bounds__(256) void axpby_kernel(const T* __restrict__ X, long ldx, T* __restrict__ Y, long ldy,
+                                                    long n, int d, A alpha, const A* __restrict__ alpha_r, A beta,
+                                                    const A* __restrict__ beta_r) {
+  const long total = n * (long)d;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / d;
+    const int c = (int)(i - r * d);
+    const A a = alpha_r ? alpha_r[r] : alpha;
+    const A b = beta_r ? beta_r[r] : beta;
+    const A x = X ? (A)Ld<T>::f(X[r * ldx + c]) : (A)0;
+    const A y = (A)Ld<T>::f(Y[r * ldy + c]);
+    const A v = a * x + b * y;
+    if constexpr (sizeof(T) == 2) Y[r * ldy + c] = f32_to_bf16((float)v);
+    else Y[r * ldy + c] = (T)v;
+  }
+}
+
+// hDot with a broadcast vector: out[r,c] = v[c] · X[r,c] (ElementwiseProduct).
+template <typename T, typename O>
+__global__ __launch_bounds__(256) void hdot_kernel(const T* __restrict__ X, long ldx, const double* __restrict__ v,
+                                                   long n, int d, O* __restrict__ out, long ldo) {
+  typedef typename AccOf<T>::type A;
+  const long total = n * (long)d;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / d;
+    const int c = (int)(i - r * d);
+    out[r * ldo + c] = (O)((A)v[c] * (A)Ld<T>::f(X[r * ldx + c]));
+  }
+}
+
+// gemv 'T', stage 1: block b owns rows [b·R, (b+1)·R); each thread a column (strided), fixed
+// row order → part[b][c]. Stage 2: y[c] = Σ_b part[b][c] in block order.
+template <typename T>
+__global__ __launch_bounds__(256) void gemv_t_part_kernel(const T* __restrict__ X, long ldx, const double* __restrict__ m,
+                                                          long n, int d, long rows_per_block,
+                                                          typename AccOf<T>::type* __restrict__ part) {
+  typedef typename AccOf<T>::type A;
+  const long r0 = (long)blockIdx.y * rows_per_block;
+  const long r1 = r0 + rows_per_block < n ? r0 + rows_per_block : n;
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < d; c += gridDim.x * blockDim.x) {
+    A s = 0;
+    for (long r = r0; r < r1; ++r) s += (A)m[r] * (A)Ld<T>::f(X[r * ldx + c]);
+    part[(long)blockIdx.y * d + c] = s;
+  }
+}
+
+template <typename A>
+__global__ __launch_bounds__(256) void gemv_t_sum_kernel(const A* __restrict__ part, int nb, int d,
+                                                         double* __restrict__ y, double beta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= d) return;
+  A s = 0;
+  for (int b = 0; b < nb; ++b) s += part[(long)b * d + c];
+  y[c] = beta == 0.0 ? (double)s : beta * y[c] + (double)s;
+}
+
+// ---- CSR ------------------------------------------------------------------------------------
+// out[r] = reduce over the row's non-zeros (dot with a dense vector v, norms, asum); TPR lanes.
+template <typename V, int TPR>
+__global__ __launch_bounds__(256) void csr_rowreduce_kernel(const long* __restrict__ indptr, const int* __restrict__ idx,
+                                                            const V* __restrict__ val, const double* __restrict__ v,
+                                                            long n, int op, double pd,
+                                                            typename AccOf<V>::type* __restrict__ out) {
+  typedef typename AccOf<V>::type A;
+  const A p = (A)pd;
+  const int sub = threadIdx.x % TPR;
+  const long rows_per_grid = (long)gridDim.x * (blockDim.x / TPR);
+  for (long r = (long)blockIdx.x * (blockDim.x / TPR) + threadIdx.x / TPR; r < n; r += rows_per_grid) {
+    A s = 0;
+    for (long q = indptr[r] + sub; q < indptr[r + 1]; q += TPR) {
+      const A x = (A)val[q];
+      const A t = term<A>(op, x, op == OP_DOTV ? (A)v[idx[q]] : (A)0, p);
+      s = op == OP_NORMINF ? (t > s ? t : s) : s + t;
+    }
+    s = op == OP_NORMINF ? seg_reduce_max<A, TPR>(s) : seg_reduce_sum<A, TPR>(s);
+    if (sub == 0) out[r] = finish<A>(op, s, p);
+  }
+}
+
+// values[q] *= s[row(q)] (scale_rows) and/or v[idx[q]] (hdot); one thread per non-zero row
+// segment walk.
+template <typename V>
+__global__ __launch_bounds__(256) void csr_scale_kernel(const long* __restrict__ indptr, const int* __restrict__ idx,
+                                                        const V* __restrict__ val, const double* __restrict__ srow,
+                                                        const double* __restrict__ vcol, long n, V* __restrict__ out) {
+  typedef typename AccOf<V>::type A;
+  for (long r = (long)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (long)gridDim.x * blockDim.x) {
+    const A sr = srow ? (A)srow[r] : (A)1;
+    for (long q = indptr[r]; q < indptr[r + 1]; ++q) {
+      A x = (A)val[q] * sr;
+      if (vcol) x *= (A)vcol[idx[q]];
+      out[q] = (V)x;
+    }
+  }
+}
+
+// Y[r, idx[q]] += a · val[q] (sparse axpy into dense rows; rows are disjoint across threads).
+template <typename V, typename T>
+__global__ __launch_bounds__(256) void csr_axpy_dense_kernel(const long* __restrict__ indptr, const int* __restrict__ idx,
+                                                             const V* __restrict__ val, double a, long n, int k,
+                                                             T* __restrict__ Y, long ldy) {
+  for (long r = (long)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (long)gridDim.x * blockDim.x) {
+    for (long q = indptr[r]; q < indptr[r + 1]; ++q) {
+      const int c = idx[q];
+      if (c >= k) break;  // sorted indices: the reference's axpy(a, x, y, k) stops at k
+      Y[r * ldy + c] = (T)((double)Y[r * ldy + c] + a * (double)val[q]);
+    }
+  }
+}
+
+// Row-pair dot of two CSR columns with sorted indices: a sorted-merge per row (BLAS.dot
+// sparse·sparse). One thread per row.
+template <typename V>
+__global__ __launch_bounds__(256) void csr_csr_dot_kernel(const long* __restrict__ ap, const int* __restrict__ ai,
+                                                          const V* __restrict__ av, const long* __restrict__ bp,
+                                                          const int* __restrict__ bi, const V* __restrict__ bv, long n,
+                                                          typename AccOf<V>::type* __restrict__ out) {
+  typedef typename AccOf<V>::type A;
+  for (long r = (long)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (long)gridDim.x * blockDim.x) {
+    long i = ap[r], ie = ap[r + 1], j = bp[r], je = bp[r + 1];
+    A s = 0;
+    while (i < ie && j < je) {
+      const int x = ai[i], y = bi[j];
+      if (x == y) { s += (A)av[i] * (A)bv[j]; ++i; ++j; }
+      else if (x < y) ++i;
+      else ++j;
+    }
+    out[r] = s;
+  }
+}
+
+// VectorSlicer: out[r, j] = X[r, cols[j]].
+template <typename T>
+__global__ __launch_bounds__(256) void gather_cols_kernel(const T* __restrict__ X, long ldx, const int* __restrict__ cols,
+                                                          long n, int m, T* __restrict__ out) {
+  const long total = n * (long)m;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / m;
+    out[i] = X[r * ldx + cols[i - r * m]];
+  }
+}
+
+// Interaction: out[r, j] = Π_k in_k[r, (j / stride_k) mod dim_k] (feature crosses, first input
+// slowest — the reference's nested loop order, Interaction.java).
+constexpr int INTER_MAX = 8;
+struct InterArgs {
+  const double* in[INTER_MAX];
+  long ld[INTER_MAX];
+  long dim[INTER_MAX];
+  long stride[INTER_MAX];
+  int k;
+};
+__global__ __launch_bounds__(256) void interaction_kernel(InterArgs a, long n, long m, double* __restrict__ out) {
+  const long total = n * m;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / m, j = i - r * m;
+    double v = 1.0;
+    for (int q = 0; q < a.k; ++q) v *= a.in[q][r * a.ld[q] + (j / a.stride[q]) % a.dim[q]];
+    out[i] = v;
+  }
+}
+
+int blocks_for(long work, int per, int cap = 1 << 16) {
+  long b = (work + per - 1) / per;
+  if (b < 1) b = 1;
+  if (b > cap) b = cap;
+  return (int)b;
+}
+
+template <typename T>
+int launch_rowreduce(int tpr, const void* X, long ldx, const void* Y, long ldy, const void* v, long n, int d, int op,
+                     double p, void* out, hipStream_t s) {
+  typedef typename AccOf<T>::type A;
+  const int rows_per_block = 256 / tpr;
+  const int g = blocks_for(n, rows_per_block);
+#define RR(TPR_)                                                                                              \
+  hipLaunchKernelGGL((rowreduce_kernel<T, TPR_>), dim3(g), dim3(256), 0, s, (const T*)X, ldx, (const T*)Y, ldy, \
+                     (const T*)v, n, d, op, p, (A*)out)
+  switch (tpr) {
+    case 4: RR(4); break;
+    case 8: RR(8); break;
+    case 16: RR(16); break;
+    case 32: RR(32); break;
+    default: RR(64); break;
+  }
+#undef RR
+  return (int)hipGetLastError();
+}
+
+template <typename T, typename O>
+int launch_normalize(int tpr, const void* X, long ldx, long n, int d, double p, int pinf, void* out, long ldo,
+                     hipStream_t s) {
+  const int g = blocks_for(n, 256 / tpr);
+#define NK(TPR_)                                                                                                \
+  hipLaunchKernelGGL((normalize_kernel<T, O, TPR_>), dim3(g), dim3(256), 0, s, (const T*)X, ldx, n, d, p, pinf, \
+                     (O*)out, ldo)
+  switch (tpr) {
+    case 4: NK(4); break;
+    case 8: NK(8); break;
+    case 16: NK(16); break;
+    case 32: NK(32); break;
+    default: NK(64); break;
+  }
+#undef NK
+  return (int)hipGetLastError();
+}
+
+template <typename V>
+int launch_csr_rowreduce(int tpr, const long* indptr, const int* idx, const void* val, const double* v, long n, int op,
+                         double p, void* out, hipStream_t s) {
+  typedef typename AccOf<V>::type A;
+  const int g = blocks_for(n, 256 / tpr);
+#define CR(TPR_)                                                                                                   \
+  hipLaunchKernelGGL((csr_rowreduce_kernel<V, TPR_>), dim3(g), dim3(256), 0, s, indptr, idx, (const V*)val, v, n, op, \
+                     p, (A*)out)
+  switch (tpr) {
+    case 4: CR(4); break;
+    case 8: CR(8); break;
+    case 16: CR(16); break;
+    case 32: CR(32); break;
+    default: CR(64); break;
+  }
+#undef CR
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// dtype: DT_F32 / DT_F64 / DT_BF16 of X (and Y / v, same dtype); out in the accumulator dtype.
+FMLX_API int fmlx_blas_rowreduce(int dtype, int tpr, const void* X, long ldx, const void* Y, long ldy, const void* v,
+                                 long n, int d, int op, double p, void* out, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n <= 0) return 0;
+  if (dtype == DT_F32) return launch_rowreduce<float>(tpr, X, ldx, Y, ldy, v, n, d, op, p, out, s);
+  if (dtype == DT_F64) return launch_rowreduce<double>(tpr, X, ldx, Y, ldy, v, n, d, op, p, out, s);
+  if (dtype == DT_BF16) return launch_rowreduce<bf16_t>(tpr, X, ldx, Y, ldy, v, n, d, op, p, out, s);
+  return -1;
+}
+
+// out dtype = the accumulator dtype of X (fp32 for bf16 / fp32, fp64 for fp64)
+FMLX_API int fmlx_blas_normalize(int dtype, int tpr, const void* X, long ldx, long n, int d, double p, int pinf,
+                                 void* out, long ldo, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n <= 0) return 0;
+  if (dtype == DT_F32) return launch_normalize<float, float>(tpr, X, ldx, n, d, p, pinf, out, ldo, s);
+  if (dtype == DT_F64) return launch_normalize<double, double>(tpr, X, ldx, n, d, p, pinf, out, ldo, s);
+  if (dtype == DT_BF16) return launch_normalize<bf16_t, float>(tpr, X, ldx, n, d, p, pinf, out, ldo, s);
+  return -1;
+}
+
+FMLX_API int fmlx_blas_axpby(int dtype, const void* X, long ldx, void* Y, long ldy, long n, int d, double alpha,
+                             const void* alpha_r, double beta, const void* beta_r, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n <= 0 || d <= 0) return 0;
+  const int g = blocks_for(n * (long)d, 256, 8192);
+  if (dtype == DT_F32)
+    hipLaunchKernelGGL((axpby_kernel<float, float>), dim3(g), dim3(256), 0, s, (const float*)X, ldx, (float*)Y, ldy, n, d,
+                       (float)alpha, (const float*)alpha_r, (float)beta, (const float*)beta_r);
+  else if (dtype == DT_F64)
+    hipLaunchKernelGGL((axpby_kernel<double, double>), dim3(g), dim3(256), 0, s, (const double*)X, ldx, (double*)Y, ldy,
+                       n, d, alpha, (const double*)alpha_r, beta, (const double*)beta_r);
+  else if (dtype == DT_BF16)
+    hipLaunchKernelGGL((axpby_kernel<bf16_t, float>), dim3(g), dim3(256), 0, s, (const bf16_t*)X, ldx, (bf16_t*)Y, ldy, n,
+                       d, (float)alpha, (const float*)alpha_r, (float)beta, (const float*)beta_r);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+// out dtype = accumulator dtype of X
+FMLX_API int fmlx_blas_hdot(int dtype, const void* X, long ldx, const double* v, long n, int d, void* out, long ldo,
+                            void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n <= 0 || d <= 0) return 0;
+  const int g = blocks_for(n * (long)d, 256, 8192);
+  if (dtype == DT_F32)
+    hipLaunchKernelGGL((hdot_kernel<float, float>), dim3(g), dim3(256), 0, s, (const float*)X, ldx, v, n, d, (float*)out,
+                       ldo);
+  else if (dtype == DT_F64)
+    hipLaunchKernelGGL((hdot_kernel<double, double>), dim3(g), dim3(256), 0, s, (const double*)X, ldx, v, n, d,
+                       (double*)out, ldo);
+  else if (dtype == DT_BF16)
+    hipLaunchKernelGGL((hdot_kernel<bf16_t, float>), dim3(g), dim3(256), 0, s, (const bf16_t*)X, ldx, v, n, d,
+                       (float*)out, ldo);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+// y = Xᵀ·m (+ beta·y), fp64 y and m; part: scratch [nb · d] of the accumulator dtype.
+FMLX_API long fmlx_blas_gemv_t_blocks(long n) { return n <= 0 ? 1 : (n + 4095) / 4096 < 512 ? (n + 4095) / 4096 : 512; }
+FMLX_API int fmlx_blas_gemv_t(int dtype, const void* X, long ldx, const double* m, long n, int d, void* part,
+                              double* y, double beta, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const long nb = fmlx_blas_gemv_t_blocks(n);
+  const long rpb = n <= 0 ? 0 : (n + nb - 1) / nb;
+  const dim3 g1((unsigned)blocks_for(d, 256, 64), (unsigned)nb);
+  const int g2 = blocks_for(d, 256);
+  if (dtype == DT_F32) {
+    hipLaunchKernelGGL(gemv_t_part_kernel<float>, g1, dim3(256), 0, s, (const float*)X, ldx, m, n, d, rpb, (float*)part);
+    hipLaunchKernelGGL(gemv_t_sum_kernel<float>, dim3(g2), dim3(256), 0, s, (const float*)part, (int)nb, d, y, beta);
+  } else if (dtype == DT_F64) {
+    hipLaunchKernelGGL(gemv_t_part_kernel<double>, g1, dim3(256), 0, s, (const double*)X, ldx, m, n, d, rpb,
+                       (double*)part);
+    hipLaunchKernelGGL(gemv_t_sum_kernel<double>, dim3(g2), dim3(256), 0, s, (const double*)part, (int)nb, d, y, beta);
+  } else if (dtype == DT_BF16) {
+    hipLaunchKernelGGL(gemv_t_part_kernel<bf16_t>, g1, dim3(256), 0, s, (const bf16_t*)X, ldx, m, n, d, rpb,
+                       (float*)part);
+    hipLaunchKernelGGL(gemv_t_sum_kernel<float>, dim3(g2), dim3(256), 0, s, (const float*)part, (int)nb, d, y, beta);
+  } else {
+    return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+// CSR values dtype: DT_F32 / DT_F64
+FMLX_API int fmlx_blas_csr_rowreduce(int vdtype, int tpr, const long* indptr, const int* idx, const void* val,
+                                     const double* v, long n, int op, double p, void* out, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n <= 0) return 0;
+  if (vdtype == DT_F32) return launch_csr_rowreduce<float>(tpr, indptr, idx, val, v, n, op, p, out, s);
+  if (vdtype == DT_F64) return launch_csr_rowreduce<double>(tpr, indptr, idx, val, v, n, op, p, out, s);
+  return -1;
+}
+
+FMLX_API int fmlx_blas_csr_scale(int vdtype, const long* indptr, const int* idx, const void* val, const double* srow,
+                                 const double* vcol, long n, void* out, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n <= 0) return 0;
+  const int g = blocks_for(n, 256, 16384);
+  if (vdtype == DT_F32)
+    hipLaunchKernelGGL(csr_scale_kernel<float>, dim3(g), dim3(256), 0, s, indptr, idx, (const float*)val, srow, vcol, n,
+                       (float*)out);
+  else if (vdtype == DT_F64)
+    hipLaunchKernelGGL(csr_scale_kernel<double>, dim3(g), dim3(256), 0, s, indptr, idx, (const double*)val, srow, vcol,
+                       n, (double*)out);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+// Y (fp64 [n, ldy]) += a · CSR (first k columns)
+FMLX_API int fmlx_blas_csr_axpy_dense(int vdtype, const long* indptr, const int* idx, const void* val, double a, long n,
+                                      int k, double* Y, long ldy, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n <= 0) return 0;
+  const int g = blocks_for(n, 256, 16384);
+  if (vdtype == DT_F32)
+    hipLaunchKernelGGL((csr_axpy_dense_kernel<float, double>), dim3(g), dim3(256), 0, s, indptr, idx, (const float*)val,
+                       a, n, k, Y, ldy);
+  else if (vdtype == DT_F64)
+    hipLaunchKernelGGL((csr_axpy_dense_kernel<double, double>), dim3(g), dim3(256), 0, s, indptr, idx,
+                       (const double*)val, a, n, k, Y, ldy);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+FMLX_API int fmlx_blas_csr_csr_dot(int vdtype, const long* ap, const int* ai, const void* av, const long* bp,
+                                   const int* bi, const void* bv, long n, void* out, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n <= 0) return 0;
+  const int g = blocks_for(n, 256, 16384);
+  if (vdtype == DT_F32)
+    hipLaunchKernelGGL(csr_csr_dot_kernel<float>, dim3(g), dim3(256), 0, s, ap, ai, (const float*)av, bp, bi,
+                       (const float*)bv, n, (float*)out);
+  else if (vdtype == DT_F64)
+    hipLaunchKernelGGL(csr_csr_dot_kernel<double>, dim3(g), dim3(256), 0, s, ap, ai, (const double*)av, bp, bi,
+                       (const double*)bv, n, (double*)out);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+FMLX_API int fmlx_blas_gather_cols(int esize, const void* X, long ldx, const int* cols, long n, int m, void* out,
+                                   void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n <= 0 || m <= 0) return 0;
+  const int g = blocks_for(n * (long)m, 256, 8192);
+  if (esize == 8)
+    hipLaunchKernelGGL(gather_cols_kernel<double>, dim3(g), dim3(256), 0, s, (const double*)X, ldx, cols, n, m,
+                       (double*)out);
+  else if (esize == 4)
+    hipLaunchKernelGGL(gather_cols_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)X, ldx, cols, n, m,
+                       (float*)out);
+  else if (esize == 2)
+    hipLaunchKernelGGL(gather_cols_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)X, ldx, cols, n, m,
+                       (bf16_t*)out);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+// inputs: k fp64 matrices [n, dim_q] (row stride ld_q); out [n, Π dim_q] fp64
+FMLX_API int fmlx_blas_interaction(int k, const double* const* in, const long* ld, const long* dim, long n, double* out,
+                                   void* stream) {
+  if (k < 1 || k > INTER_MAX) return -1;
+  InterArgs a{};
+  a.k = k;
+  long m = 1;
+  for (int q = k - 1; q >= 0; --q) {
+    a.in[q] = in[q];
+    a.ld[q] = ld[q];
+    a.dim[q] = dim[q];
+    a.stride[q] = m;
+    m *= dim[q];
+  }
+  if (n <= 0 || m <= 0) return 0;
+  hipLaunchKernelGGL(interaction_kernel, dim3(blocks_for(n * m, 256, 8192)), dim3(256), 0, (hipStream_t)stream, a, n, m,
+                     out);
+  return (int)hipGetLastError();
+}
