@@ -28,7 +28,7 @@ def _csr(n, d, nnz, seed):
         idx.extend(cols.tolist())
         val.extend(g.normal(size=k).tolist())
         indptr.append(len(idx))
-    return SparseColumn(torch.tensor(indptr), torch.tensor(idx, dtype=torch.int32), torch.tensor(val), d)
+    return SparseColumn(torch.tensor(indptr), torch.tensor(idx, dtype=torch.int32), torch.tensor(val, dtype=torch.float64), d)
 
 
 def _tol(dtype):
