@@ -7,8 +7,9 @@ predict is the K3/K13 hot path: for a block of queries, one GEMM gives Q·Tᵀ (
 fp32 by default / fp64 on CPU), ``dist = sqrt(|‖q‖² + ‖t‖² − 2 q·t|)`` exactly as
 ``KnnModel.predictLabel``, then the k nearest (stable: among equal distances the earlier training
 point wins, like the reference's strict-``>`` priority-queue replacement) and a majority vote.
-On the GPU (fp32, k ≤ 16) the distance and the top-k are one HIP kernel (``ops/csrc/knn.hip``)
-that reads the GEMM block once.
+On the GPU (fp32, D ≤ 128, k ≤ 64) distances and top-k are ONE fused HIP kernel (fp32 matrix-core
+products, top-k in registers: the nq×n distance block never reaches HBM, ``ops/csrc/knn.hip``);
+wider features take the split path (library GEMM block + one top-k scan of it, k ≤ 16).
 Vote ties go to the tied label that occurs nearest to the query (resolved on the device, only
 for the rows that tie).
 """
@@ -68,16 +69,31 @@ def knn_vote(top_labels: torch.Tensor, classes: torch.Tensor) -> torch.Tensor:
     return pred
 
 
+# queries per fused launch: bounds the segment workspace (nq·S·k) and the vote temporaries
+FUSED_QUERY_BLOCK = 1 << 18
+
+
 def knn_predict(Q: torch.Tensor, T: torch.Tensor, tnorm: torch.Tensor, labels: torch.Tensor, k: int,
-                block: int = 4096) -> torch.Tensor:
-    """Predicted labels of queries Q [nq, d] against training points T [n, d]."""
+                block: int = 4096, pack=None) -> torch.Tensor:
+    """Predicted labels of queries Q [nq, d] against training points T [n, d]. ``pack``: a cached
+    ``ops.knn.TrainPack`` of T for the fused GPU path (built here when not given)."""
     dev = Q.device
     compute = torch.float64 if dev.type == "cpu" else config.acc_dtype()
-    Tc = T.to(compute)
-    tn = tnorm.to(compute)
     classes = torch.unique(labels)
     kk = min(k, T.shape[0])
     out = []
+    if compute == torch.float32:
+        from ..ops import knn as knn_ops
+
+        if knn_ops.fused_supported(kk, T.shape[0], T.shape[1], dev):
+            if pack is None:
+                pack = knn_ops.TrainPack(T, tnorm)
+            for s in range(0, Q.shape[0], FUSED_QUERY_BLOCK):
+                idx = knn_ops.fused_topk(Q[s:s + FUSED_QUERY_BLOCK].to(torch.float32), pack, kk)
+                out.append(knn_vote(labels[idx.long()], classes))
+            return torch.cat(out) if out else torch.zeros(0, dtype=torch.float64, device=dev)
+    Tc = T.to(compute)
+    tn = tnorm.to(compute)
     if compute == torch.float32:
         from ..ops import knn as knn_ops
 
@@ -131,11 +147,23 @@ class KnnModel(ModelWithData, KnnModelParams):
         return (T, torch.as_tensor(np.asarray(norms.values), device=dev),
                 torch.as_tensor(np.asarray(labels.values), device=dev))
 
+    def _train_pack(self, T, tnorm):
+        """The fused kernel's tile-ordered copy of the training points, built once per model data."""
+        from ..ops import knn as knn_ops
+
+        if not knn_ops.fused_supported(1, T.shape[0], T.shape[1], T.device) or config.acc_dtype() != torch.float32:
+            return None
+        cached = getattr(self, "_pack_cache", None)
+        if cached is None or cached[0] is not T:
+            cached = (T, knn_ops.TrainPack(T, tnorm))
+            self._pack_cache = cached
+        return cached[1]
+
     def transform(self, *inputs):
         t = inputs[0]
         T, tnorm, labels = self._model_state()
         Q = _query_matrix(t, self.get(self.FEATURES_COL), T.device)
-        pred = knn_predict(Q, T, tnorm, labels, self.get(self.K))
+        pred = knn_predict(Q, T, tnorm, labels, self.get(self.K), pack=self._train_pack(T, tnorm))
         return [t.with_column(self.get(self.PREDICTION_COL), pred.to(torch.float64))]
 
 

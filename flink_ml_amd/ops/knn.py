@@ -1,8 +1,13 @@
-"""Bindings for ``csrc/knn.hip``: KNN predict's distance epilogue + per-query top-k (K13).
+"""Bindings for ``csrc/knn.hip``: KNN predict's distances + per-query top-k (K13).
 
-``topk_from_products(G, qn, tn, k)`` takes the fp32 product block ``G = Q·Tᵀ`` (one hipBLASLt GEMM)
-and returns the indices of the k nearest training points per query, nearest first, ties to the
-lower index — ``KnnModel.predictLabel`` (reference ``KnnModel.java:154-194``) semantics.
+Two device paths, both with ``KnnModel.predictLabel`` (reference ``KnnModel.java:154-194``)
+semantics — the k nearest training points per query, nearest first, ties to the lower index:
+
+* ``fused_topk(Q, pack, k)`` (D ≤ 128, k ≤ 64): ONE kernel computes the distances on the fp32
+  matrix cores and keeps the top-k in registers; the nq×n distance block never reaches HBM.
+  ``TrainPack`` is the training matrix pre-arranged once per model for the kernel's tile copy.
+* ``topk_from_products(G, qn, tn, k)`` (any D, k ≤ 32): takes an fp32 product block
+  ``G = Q·Tᵀ`` from a library GEMM and scans it once (the fallback for D > 128).
 """
 from __future__ import annotations
 
@@ -16,7 +21,91 @@ from .native import c_int, c_long, c_void_p
 native.register_kernel_sigs({
     "fmlx_knn_topk": [c_void_p, c_long, c_long, c_long, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                       c_void_p, c_void_p, c_void_p],
+    "fmlx_knn_fused": [c_void_p, c_long, c_long, c_int, c_void_p, c_long, c_int, c_int, c_int, c_void_p, c_void_p,
+                       c_void_p, c_void_p, c_void_p],
+    "fmlx_knn_fused_blocks_per_cu": [c_int, c_int],
 })
+
+FUSED_MAX_K = 64
+FUSED_MAX_D = 128
+# the shortest training segment worth a block (in 64-row tiles) and the most segments tried
+FUSED_MIN_TILES = 16
+FUSED_MAX_SEGMENTS = 64
+_SLOTS = {}
+
+
+def _slots(k: int, dp: int, device) -> int:
+    """Fused-kernel blocks resident at once on the device (occupancy × CUs)."""
+    key = (k, dp, str(device))
+    if key not in _SLOTS:
+        per_cu = native.kernels().fmlx_knn_fused_blocks_per_cu(k, dp)
+        _SLOTS[key] = max(1, per_cu) * torch.cuda.get_device_properties(device).multi_processor_count
+    return _SLOTS[key]
+
+
+def fused_supported(k: int, n: int, d: int, device) -> bool:
+    return (torch.device(device).type == "cuda" and 1 <= k <= FUSED_MAX_K and k <= n < 2 ** 31 - 128
+            and 1 <= d <= FUSED_MAX_D)
+
+
+class TrainPack:
+    """Training points as the fused kernel's LDS image, one block of floats per 64-row tile
+    (built once per model, on the device): ``[sub 2][h 2][r 32][dp + 4]`` with
+    ``T[64·t + 32·sub + r][2·s + h]`` at ``s`` (zero padded: D to 2·dp, dp = ceil(D/2) rounded up
+    to 4, and 4 pad columns that keep the kernel's LDS reads conflict-free), then the tile's 64
+    squared norms in a 256-float block, so the kernel stages a tile with plain 1-KiB LDS-DMA copies."""
+
+    def __init__(self, T: torch.Tensor, tnorm: torch.Tensor):
+        n, d = T.shape
+        self.n, self.d = int(n), int(d)
+        self.dp = -(-(-(-d // 2)) // 4) * 4
+        nt = -(-n // 64)
+        dp = self.dp
+        Tp = torch.zeros((nt * 64, 2 * dp), dtype=torch.float32, device=T.device)
+        Tp[:n, :d] = T.to(torch.float32)
+        rows = torch.zeros((nt, 2, 2, 32, dp + 4), dtype=torch.float32, device=T.device)
+        rows[..., :dp] = Tp.view(nt, 2, 32, dp, 2).permute(0, 1, 4, 2, 3)
+        norms = torch.zeros((nt, 256), dtype=torch.float32, device=T.device)
+        tn = torch.zeros(nt * 64, dtype=torch.float32, device=T.device)
+        tn[:n] = tnorm.to(torch.float32)
+        norms[:, :64] = tn.view(nt, 64)
+        self.Tt = torch.cat([rows.reshape(nt, -1), norms], dim=1).contiguous()
+        assert self.Tt.shape[1] == 128 * (dp + 4) + 256
+
+
+def fused_segments(nq: int, n: int, k: int, slots: int) -> int:
+    """Training segments per query block. Cost model in tile units: the blocks run in
+    ceil(blocks / slots) rounds of (tiles per segment + a list fill of ~1 + k/16 tiles); a bad
+    split strands a mostly empty last round (782 query blocks × 2 segments on 512 slots ran 4
+    rounds for 3.05 rounds of work), so every S up to the cap is scored and the cheapest wins."""
+    bq = -(-nq // 128)
+    nt = -(-n // 64)
+    smax = int(max(1, min(FUSED_MAX_SEGMENTS, nt // FUSED_MIN_TILES, 256)))
+    fill = 1.0 + k / 16.0
+    best, best_cost = 1, None
+    for S in range(1, smax + 1):
+        cost = -(-(bq * S) // slots) * (-(-nt // S) + fill)
+        if best_cost is None or cost < best_cost * 0.995:
+            best, best_cost = S, cost
+    return best
+
+
+def fused_topk(Q: torch.Tensor, pack: "TrainPack", k: int, with_dist: bool = False, segments: int = 0):
+    """k nearest training points of every row of ``Q`` [nq, D] (fp32) in one fused kernel."""
+    nq, d = Q.shape
+    if Q.dtype != torch.float32 or d != pack.d or not fused_supported(k, pack.n, d, Q.device):
+        raise ValueError("knn fused: bad inputs Q=%s %s, D=%d, n=%d, k=%d" % (tuple(Q.shape), Q.dtype, pack.d,
+                                                                              pack.n, k))
+    if Q.stride(1) != 1:
+        Q = Q.contiguous()
+    S = int(segments) or fused_segments(nq, pack.n, k, _slots(k, pack.dp, Q.device))
+    idx = torch.empty((nq, k), dtype=torch.int32, device=Q.device)
+    dist = torch.empty((nq, k), dtype=torch.float32, device=Q.device) if with_dist else None
+    ws_d = torch.empty(nq * S * k, dtype=torch.float32, device=Q.device) if S > 1 else None
+    ws_i = torch.empty(nq * S * k, dtype=torch.int32, device=Q.device) if S > 1 else None
+    native.call("fmlx_knn_fused", native.ptr(Q), Q.stride(0), nq, d, native.ptr(pack.Tt), pack.n, pack.dp, k, S,
+                native.ptr(idx), native.ptr(dist), native.ptr(ws_d), native.ptr(ws_i), native.stream_ptr(Q.device))
+    return (idx, dist) if with_dist else idx
 
 MAX_K = 32
 # KnnModel routes k above this to the sort path: the per-lane insertion lists get long enough that

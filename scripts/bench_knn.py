@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """KnnModel.transform throughput on one MI355X (K3/K13; reference ``KnnModel.java:154-194``).
 
-Compares, on the same device-resident data, the fused path (hipBLASLt fp32 GEMM per MALL-sized
-query block + ``knn.hip`` distance/top-k kernel) with the unfused PyTorch chain
-(addmm with the norm broadcast → abs → sqrt → topk), and times the whole ``KnnModel.transform``.
+Compares, on the same device-resident data: the production predict (ONE fused kernel: fp32
+matrix-core distances + top-k in registers, training pack cached as the model caches it), the
+split path (hipBLASLt fp32 GEMM block + one ``knn.hip`` top-k scan of it) and the unfused PyTorch
+chain (addmm with the norm broadcast → abs → sqrt → topk).
 Prints one JSON line per config. Synthetic Gaussian data; no reference number is published.
 """
 import argparse
@@ -33,9 +34,14 @@ def timeit(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
-    args = ap.parse_args()
     dev = torch.device("cuda")
-    for nq, n, d, k in [(100_000, 100_000, 100, 5), (100_000, 1_000_000, 64, 10), (10_000, 100_000, 100, 32)]:
+    ap.add_argument("--configs", default="all")
+    args = ap.parse_args()
+    configs = [(100_000, 100_000, 100, 5), (100_000, 1_000_000, 64, 10), (10_000, 100_000, 100, 32),
+               (10_000, 100_000, 100, 64)]
+    if args.configs != "all":
+        configs = [configs[int(i)] for i in args.configs.split(",")]
+    for nq, n, d, k in configs:
         g = torch.Generator(device=dev).manual_seed(0)
         Q = torch.randn((nq, d), device=dev, generator=g)
         T = torch.randn((n, d), device=dev, generator=g)
@@ -43,8 +49,17 @@ def main():
         classes = torch.unique(labels)
         tn = (T * T).sum(1)
 
-        def fused():  # the production KnnModel path (routes k > ROUTE_MAX_K to the sort chain)
-            knn_predict(Q, T, tn, labels, k)
+        pack = ko.TrainPack(T, tn)
+
+        def fused():  # the production KnnModel path (pack cached per model)
+            knn_predict(Q, T, tn, labels, k, pack=pack)
+
+        def split():  # library GEMM block + top-k scan (the D > 128 path)
+            qb = ko.query_block(n)
+            for s in range(0, nq, qb):
+                q = Q[s:s + qb]
+                idx = ko.topk_from_products(torch.mm(q, T.t()), (q * q).sum(1), tn, k)
+                knn_vote(labels[idx.long()], classes)
 
         def unfused():
             for s in range(0, nq, 4096):
@@ -54,13 +69,15 @@ def main():
                 knn_vote(labels[idx], classes)
 
         tf = timeit(fused, args.reps)
+        ts = timeit(split, args.reps) if k <= ko.MAX_K else None
         tu = timeit(unfused, args.reps)
         gemm_tflops = 2.0 * nq * n * d / tf / 1e12
         print(json.dumps({"bench": "KnnModel predict", "queries": nq, "train": n, "dim": d, "k": k,
-                          "fused_ms": round(tf * 1e3, 2), "torch_chain_ms": round(tu * 1e3, 2),
-                          "speedup": round(tu / tf, 2), "fused_kernel": k <= ko.ROUTE_MAX_K, "queries_per_s": round(nq / tf, 1),
-                          "effective_gemm_tflops": round(gemm_tflops, 1)}), flush=True)
-        del Q, T, labels, tn
+                          "fused_ms": round(tf * 1e3, 2), "split_ms": None if ts is None else round(ts * 1e3, 2),
+                          "torch_chain_ms": round(tu * 1e3, 2), "speedup_vs_torch": round(tu / tf, 2),
+                          "fused_kernel": ko.fused_supported(k, n, d, dev), "queries_per_s": round(nq / tf, 1),
+                          "effective_fp32_tflops": round(gemm_tflops, 1)}), flush=True)
+        del Q, T, labels, tn, pack
         torch.cuda.empty_cache()
 
 

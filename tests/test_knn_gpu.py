@@ -105,3 +105,81 @@ def test_topk_segmented_merge(nq, n, k):
     ridx, rdist = _ref_topk(G, qn, tn, k)
     torch.testing.assert_close(dist.double().cpu(), rdist, rtol=2e-7, atol=0)
     assert (idx.long().cpu() == ridx).float().mean() > 0.999
+
+
+# ---- fused distance + top-k kernel (one kernel, fp32 matrix cores, no nq×n block in HBM)
+
+def _int_data(nq, n, d, seed, lo=-3, hi=4):
+    # small integers: every product, norm and distance is exact in fp32, so the fused kernel's
+    # ranking must equal the fp64 ranking exactly, ties (there are many) going to the lower index
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    Q = torch.randint(lo, hi, (nq, d), generator=g).double()
+    T = torch.randint(lo, hi, (n, d), generator=g).double()
+    return Q, T
+
+
+def _ref_fp64(Q, T, k):
+    d2 = ((Q * Q).sum(1)[:, None] + (T * T).sum(1)[None, :] - 2.0 * Q @ T.t()).abs().sqrt()
+    s = torch.sort(d2, dim=1, stable=True)
+    return s.indices[:, :k], s.values[:, :k]
+
+
+@pytest.mark.parametrize("d", [1, 3, 8, 24, 100, 128])
+@pytest.mark.parametrize("k", [1, 3, 5, 16, 33, 64])
+def test_fused_topk_exact_vs_fp64(d, k):
+    from flink_ml_amd.ops import knn as ko
+
+    n = 4099
+    Q, T = _int_data(301, n, d, seed=d * 101 + k)
+    pack = ko.TrainPack(T.float().cuda(), (T * T).sum(1).cuda())
+    idx, dist = ko.fused_topk(Q.float().cuda(), pack, k, with_dist=True)
+    ridx, rdist = _ref_fp64(Q, T, k)
+    assert torch.equal(idx.long().cpu(), ridx)
+    torch.testing.assert_close(dist.double().cpu(), rdist, rtol=1e-6, atol=0)
+
+
+@pytest.mark.parametrize("segments", [1, 2, 5, 64])
+@pytest.mark.parametrize("n", [37, 64, 1000, 20011])
+def test_fused_topk_segments_and_tails(segments, n):
+    from flink_ml_amd.ops import knn as ko
+
+    k = min(9, n)
+    Q, T = _int_data(130, n, 17, seed=n + segments)
+    pack = ko.TrainPack(T.float().cuda(), (T * T).sum(1).cuda())
+    idx = ko.fused_topk(Q.float().cuda(), pack, k, segments=segments)
+    ridx, _ = _ref_fp64(Q, T, k)
+    assert torch.equal(idx.long().cpu(), ridx)
+
+
+def test_fused_topk_random_floats_and_nan():
+    from flink_ml_amd.ops import knn as ko
+
+    g = torch.Generator(device="cpu").manual_seed(11)
+    Q = torch.randn((1000, 64), generator=g)
+    T = torch.randn((30000, 64), generator=g)
+    tn = (T * T).sum(1)
+    tn[5] = float("nan")                                 # a NaN distance ranks last: never chosen
+    pack = ko.TrainPack(T.cuda(), tn.cuda())
+    idx, dist = ko.fused_topk(Q.cuda(), pack, 20, with_dist=True)
+    assert not torch.any(idx == 5)
+    tn_ref = tn.double().clone()
+    tn_ref[5] = float("inf")
+    d2 = ((Q.double() ** 2).sum(1)[:, None] + tn_ref[None, :] - 2.0 * Q.double() @ T.double().t()).abs().sqrt()
+    rd, ri = torch.sort(d2, dim=1, stable=True)
+    torch.testing.assert_close(dist.double().cpu(), rd[:, :20], rtol=1e-5, atol=1e-5)
+    assert (idx.long().cpu() == ri[:, :20]).float().mean() > 0.999
+
+
+def test_knn_model_routes_fused_for_k64():
+    from flink_ml_amd import Table
+    from flink_ml_amd.models import Knn
+
+    Q, T = _int_data(257, 5000, 12, seed=2)
+    lab = (T[:, 0] > 0).double() + (T[:, 1] > 0).double()
+    model = Knn().set_k(64).fit(Table({"features": T.float().cuda(), "label": lab.cuda()}))
+    pred = model.transform(Table({"features": Q.float().cuda()}))[0].column("prediction").cpu()
+    ridx, _ = _ref_fp64(Q, T, 64)
+    from flink_ml_amd.models.knn import knn_vote
+
+    ref = knn_vote(lab[ridx], torch.unique(lab))
+    assert torch.equal(pred.double(), ref.double())
