@@ -74,12 +74,14 @@ FUSED_QUERY_BLOCK = 1 << 18
 
 
 def knn_predict(Q: torch.Tensor, T: torch.Tensor, tnorm: torch.Tensor, labels: torch.Tensor, k: int,
-                block: int = 4096, pack=None) -> torch.Tensor:
+                block: int = 4096, pack=None, classes=None) -> torch.Tensor:
     """Predicted labels of queries Q [nq, d] against training points T [n, d]. ``pack``: a cached
-    ``ops.knn.TrainPack`` of T for the fused GPU path (built here when not given)."""
+    ``ops.knn.TrainPack`` of T for the fused GPU path (built here when not given); ``classes``:
+    the cached sorted distinct labels (a sort of all n labels otherwise)."""
     dev = Q.device
     compute = torch.float64 if dev.type == "cpu" else config.acc_dtype()
-    classes = torch.unique(labels)
+    if classes is None:
+        classes = torch.unique(labels)
     kk = min(k, T.shape[0])
     out = []
     if compute == torch.float32:
@@ -147,23 +149,26 @@ class KnnModel(ModelWithData, KnnModelParams):
         return (T, torch.as_tensor(np.asarray(norms.values), device=dev),
                 torch.as_tensor(np.asarray(labels.values), device=dev))
 
-    def _train_pack(self, T, tnorm):
-        """The fused kernel's tile-ordered copy of the training points, built once per model data."""
+    def _predict_cache(self, T, tnorm, labels):
+        """Per model data, built once: the fused kernel's tile-ordered copy of the training points
+        (GPU fp32 only) and the sorted distinct labels."""
         from ..ops import knn as knn_ops
 
-        if not knn_ops.fused_supported(1, T.shape[0], T.shape[1], T.device) or config.acc_dtype() != torch.float32:
-            return None
         cached = getattr(self, "_pack_cache", None)
         if cached is None or cached[0] is not T:
-            cached = (T, knn_ops.TrainPack(T, tnorm))
+            pack = None
+            if knn_ops.fused_supported(1, T.shape[0], T.shape[1], T.device) and config.acc_dtype() == torch.float32:
+                pack = knn_ops.TrainPack(T, tnorm)
+            cached = (T, pack, torch.unique(labels))
             self._pack_cache = cached
-        return cached[1]
+        return cached[1], cached[2]
 
     def transform(self, *inputs):
         t = inputs[0]
         T, tnorm, labels = self._model_state()
         Q = _query_matrix(t, self.get(self.FEATURES_COL), T.device)
-        pred = knn_predict(Q, T, tnorm, labels, self.get(self.K), pack=self._train_pack(T, tnorm))
+        pack, classes = self._predict_cache(T, tnorm, labels)
+        pred = knn_predict(Q, T, tnorm, labels, self.get(self.K), pack=pack, classes=classes)
         return [t.with_column(self.get(self.PREDICTION_COL), pred.to(torch.float64))]
 
 

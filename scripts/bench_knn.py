@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     dev = torch.device("cuda")
     ap.add_argument("--configs", default="all")
+    ap.add_argument("--only-fused", action="store_true", help="time only the production path (for kernel traces)")
     args = ap.parse_args()
     configs = [(100_000, 100_000, 100, 5), (100_000, 1_000_000, 64, 10), (10_000, 100_000, 100, 32),
                (10_000, 100_000, 100, 64)]
@@ -52,7 +53,7 @@ def main():
         pack = ko.TrainPack(T, tn)
 
         def fused():  # the production KnnModel path (pack cached per model)
-            knn_predict(Q, T, tn, labels, k, pack=pack)
+            knn_predict(Q, T, tn, labels, k, pack=pack, classes=classes)
 
         def split():  # library GEMM block + top-k scan (the D > 128 path)
             qb = ko.query_block(n)
@@ -69,12 +70,13 @@ def main():
                 knn_vote(labels[idx], classes)
 
         tf = timeit(fused, args.reps)
-        ts = timeit(split, args.reps) if k <= ko.MAX_K else None
-        tu = timeit(unfused, args.reps)
+        ts = timeit(split, args.reps) if k <= ko.MAX_K and not args.only_fused else None
+        tu = None if args.only_fused else timeit(unfused, args.reps)
         gemm_tflops = 2.0 * nq * n * d / tf / 1e12
         print(json.dumps({"bench": "KnnModel predict", "queries": nq, "train": n, "dim": d, "k": k,
                           "fused_ms": round(tf * 1e3, 2), "split_ms": None if ts is None else round(ts * 1e3, 2),
-                          "torch_chain_ms": round(tu * 1e3, 2), "speedup_vs_torch": round(tu / tf, 2),
+                          "torch_chain_ms": None if tu is None else round(tu * 1e3, 2),
+                          "speedup_vs_torch": None if tu is None else round(tu / tf, 2),
                           "fused_kernel": ko.fused_supported(k, n, d, dev), "queries_per_s": round(nq / tf, 1),
                           "effective_fp32_tflops": round(gemm_tflops, 1)}), flush=True)
         del Q, T, labels, tn, pack
