@@ -3,10 +3,12 @@
 * RandomSplitter: each rank draws ``java.util.Random(Tuple2.of(seed, rank).hashCode())``
   doubles (native host loop, bit-identical to ``SplitterOperator``) and routes row i to split
   ``#{cumulative fractions < r_i}`` — one searchsorted and one gather per output.
-* SQLTransformer: the statement (``__THIS__`` = the input) runs on SQLite (stdlib) with the
-  input's scalar columns; vector/object columns pass through as opaque references. Row-wise
-  statements run per rank; statements that aggregate, sort, join or de-duplicate are evaluated
-  over the gathered table and the result is re-partitioned round-robin.
+* SQLTransformer: statements in the device subset (projections, arithmetic, built-in math
+  functions, WHERE, GROUP BY with SUM/COUNT/AVG/MIN/MAX — ``sql_device.py``) are evaluated
+  column-at-a-time on the input's device. Anything else runs on SQLite (stdlib) with the input's
+  scalar columns; vector/object columns pass through as opaque references. Row-wise statements
+  run per rank; statements that aggregate, sort, join or de-duplicate are evaluated over the
+  gathered table and the result is re-partitioned round-robin.
 """
 from __future__ import annotations
 
@@ -140,8 +142,20 @@ class SQLTransformer(AlgoOperator):
     STATEMENT = StringParam("statement", "SQL statement.", None, ParamValidator(_statement_ok, "statement"))
 
     def transform(self, *inputs) -> List[Table]:
+        from . import sql_device
+
         t = inputs[0]
         stmt = self.get(self.STATEMENT)
+        world, rank = 1, 0
+        if get_world_distributed():
+            from ...parallel.context import get_context
+
+            world, rank = get_context().world_size, get_context().rank
+        # the statement subset a feature pipeline uses runs column-at-a-time on the device
+        # (sql_device.py); the rest falls back to SQLite over host rows
+        out = sql_device.try_evaluate(stmt, t, world, rank)
+        if out is not None:
+            return [out]
         if get_world_distributed() and _GLOBAL_SQL.search(stmt):
             from ...parallel.context import get_context
 

@@ -372,11 +372,17 @@ class FeatureHasher(Transformer, HasInputCols, HasOutputCol, HasCategoricalCols,
         for c in [c for c in ins if is_cat(c)]:
             col = t.column(c)
             if isinstance(col, torch.Tensor) and col.dtype.is_floating_point:
-                # Double.toString + murmur3 of every value in native multi-threaded host code
-                h = hashing.hash_prefixed_doubles(c + "=", col.detach().to("cpu", torch.float64).numpy())
-                h = np.where(h == -(1 << 31), h.astype(np.int64), np.abs(h.astype(np.int64)))
+                if col.device.type == "cuda":
+                    # Double.toString + murmur3 of every value on the device (csrc/javastr.hip)
+                    h = hashing.hash_prefixed_doubles_device(c + "=", col.detach()).to(torch.int64)
+                    h = torch.where(h == -(1 << 31), h, h.abs())  # Math.abs(Integer.MIN_VALUE) stays negative
+                    idx_l.append(torch.remainder(h, nf).to(dev))
+                else:
+                    # the same in native multi-threaded host code
+                    h = hashing.hash_prefixed_doubles(c + "=", col.detach().to("cpu", torch.float64).numpy())
+                    h = np.where(h == -(1 << 31), h.astype(np.int64), np.abs(h.astype(np.int64)))
+                    idx_l.append(torch.from_numpy(np.mod(h, nf)).to(dev))
                 rows_l.append(ar)
-                idx_l.append(torch.from_numpy(np.mod(h, nf)).to(dev))
                 val_l.append(torch.ones(n, dtype=torch.float64, device=dev))
             elif isinstance(col, torch.Tensor):
                 u, inv = torch.unique(col, return_inverse=True)

@@ -112,6 +112,53 @@ def hash_prefixed_doubles(prefix: str, vals: np.ndarray, nthreads: int = 0) -> n
     return out
 
 
+native.register_kernel_sigs({
+    "fmlx_hash_prefixed_doubles_dev": [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
+})
+_RYU_TABLES = {}
+
+
+def ryu_tables(device):
+    """The shortest-digits kernel's 128-bit multipliers, computed exactly with Python integers:
+    ``inv[q] = ⌊2^(bitlen(5^q) − 1 + 125) / 5^q⌋ + 1`` (q < 342) and ``pow[i] = 5^i`` scaled to 125
+    significant bits (i < 326), each as (low, high) 64-bit words."""
+    key = str(device)
+    if key not in _RYU_TABLES:
+        mask = (1 << 64) - 1
+        inv, pw = [], []
+        for q in range(342):
+            p = 5 ** q
+            v = (1 << (p.bit_length() - 1 + 125)) // p + 1
+            inv += [v & mask, v >> 64]
+        for i in range(326):
+            p = 5 ** i
+            sh = p.bit_length() - 125
+            v = p >> sh if sh >= 0 else p << -sh
+            pw += [v & mask, v >> 64]
+
+        def dev(words):
+            return torch.from_numpy(np.array(words, dtype=np.uint64).view(np.int64)).to(device)
+
+        _RYU_TABLES[key] = (dev(inv), dev(pw))
+    return _RYU_TABLES[key]
+
+
+def hash_prefixed_doubles_device(prefix: str, vals: torch.Tensor) -> torch.Tensor:
+    """murmur3_32(prefix + Double.toString(v)) for every value of a device tensor, computed on the
+    device (``csrc/javastr.hip``) — the same bits as ``hash_prefixed_doubles``."""
+    vals = vals.to(torch.float64).contiguous()
+    dev = vals.device
+    units = torch.from_numpy(np.frombuffer(prefix.encode("utf-16-le"), dtype=np.uint16).astype(np.int16)).to(dev)
+    out = torch.empty(vals.shape[0], dtype=torch.int32, device=dev)
+    inv, pw = ryu_tables(dev)
+    if vals.shape[0]:
+        native.call("fmlx_hash_prefixed_doubles_dev", native.ptr(units) if units.numel() else None, int(units.numel()),
+                    native.ptr(vals), int(vals.shape[0]), native.ptr(inv), native.ptr(pw), native.ptr(out),
+                    native.stream_ptr(dev))
+    return out
+
+
 def java_double_strings(vals) -> list:
     """``Double.toString`` of every value (native)."""
     vals = np.ascontiguousarray(vals, dtype=np.float64)
