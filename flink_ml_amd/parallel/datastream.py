@@ -10,7 +10,9 @@ reference                   here
 ``allReduceSum`` (:102)     ``all_reduce_sum`` — RCCL all-reduce of a device tensor
 ``mapPartition`` (:115)     ``map_partition`` — apply fn to the whole local partition
 ``reduce`` (:132-143)       ``reduce`` — local fold, all-gather, fold in rank order
-keyed ``reduce`` (:155)     ``reduce_by_key`` — per-key local folds, all-gather, merge
+keyed ``reduce`` (:155)     ``reduce_by_key`` — per-key local folds, all-gather, merge (host
+                              objects); ``reduce_by_key_tensor`` — device keys/values: local
+                              segment reduce, hash-partitioned all-to-all, owner-side merge
 ``aggregate`` (:182-199)    ``aggregate`` — local accumulator, all-gather, merge in rank order
 ``sample`` (:212-227)       ``sample`` — reservoir per rank (java.util.Random), gather, again
 ``generateBatchData``       ``generate_batch_data`` — deterministic per-rank split of a global
@@ -67,6 +69,52 @@ def reduce_by_key(pairs: Sequence, fn: Callable[[Any, Any], Any]) -> dict:
         for k, v in part.items():
             out[k] = fn(out[k], v) if k in out else v
     return out
+
+
+def _segment_reduce(keys: torch.Tensor, values: torch.Tensor, op: str):
+    uk, inv = torch.unique(keys, return_inverse=True)
+    shape = (uk.shape[0],) + tuple(values.shape[1:])
+    if op == "sum":
+        out = torch.zeros(shape, dtype=values.dtype, device=values.device).index_add_(0, inv, values)
+    elif op in ("min", "max"):
+        idx = inv.view(-1, *([1] * (values.dim() - 1))).expand_as(values)
+        out = torch.empty(shape, dtype=values.dtype, device=values.device).scatter_reduce_(
+            0, idx, values, "amin" if op == "min" else "amax", include_self=False)
+    else:
+        raise ValueError("op must be sum, min or max")
+    return uk, out
+
+
+def reduce_by_key_tensor(keys: torch.Tensor, values: torch.Tensor, op: str = "sum", gather: bool = False):
+    """Keyed ``DataStreamUtils.reduce`` (``DataStreamUtils.java:155``) for device data: integer
+    ``keys`` [n] and ``values`` [n, ...] stay on the device. Each rank folds its own rows per key
+    (sort-unique + index_add / scatter_reduce), sends every partial to the key's owner rank
+    (``key mod P`` — the keyBy shuffle) in ONE all-to-all, and the owner folds what it receives.
+    Returns this rank's (sorted keys, reduced values) — every key lives on exactly one rank, like
+    the reference's keyed reduce output; ``gather=True`` all-gathers the full result instead.
+    ``op`` is an associative, commutative reduction: sum, min or max."""
+    if keys.dim() != 1 or values.shape[0] != keys.shape[0]:
+        raise ValueError("keys [n] and values [n, ...] expected")
+    keys = keys.to(torch.int64)
+    uk, part = _segment_reduce(keys, values, op)
+    ctx = get_context()
+    if not ctx.is_distributed:
+        return uk, part
+    P = ctx.world_size
+    owner = torch.remainder(uk, P)
+    order = torch.argsort(owner, stable=True)
+    uk, part, owner = uk[order], part[order], owner[order]
+    counts = torch.bincount(owner, minlength=P).tolist()
+    k_in = comm.all_to_all_v(list(torch.split(uk, counts)))
+    v_in = comm.all_to_all_v(list(torch.split(part, counts)))
+    mk, mv = _segment_reduce(torch.cat(k_in), torch.cat(v_in), op)
+    if gather:
+        ks = comm.all_gather_tensor(mk)
+        vs = comm.all_gather_tensor(mv)
+        ak, av = torch.cat(ks), torch.cat(vs)
+        o = torch.argsort(ak)
+        return ak[o], av[o]
+    return mk, mv
 
 
 def set_managed_memory_weight(stream, weight: int):

@@ -91,3 +91,35 @@ def test_all_to_all_v_uneven_splits():
     res = run_spmd(_a2a_worker, 3)
     for dst, recv in enumerate(res):
         assert recv == [(((src + 1) * (dst + 1), 3), float(100 * src + dst)) for src in range(3)]
+
+
+def _keyed_tensor_worker(rank, world):
+    from flink_ml_amd.parallel.datastream import reduce_by_key_tensor
+
+    g = torch.Generator().manual_seed(rank)
+    keys = torch.randint(-20, 50, (500,), generator=g)
+    vals = torch.randn((500, 3), generator=g, dtype=torch.float64)
+    own = {op: reduce_by_key_tensor(keys, vals, op) for op in ("sum", "min", "max")}
+    full = reduce_by_key_tensor(keys, vals, "sum", gather=True)
+    return keys, vals, own, full
+
+
+def test_reduce_by_key_tensor_across_ranks():
+    world = 3
+    res = run_spmd(_keyed_tensor_worker, world)
+    K = torch.cat([r[0] for r in res])
+    V = torch.cat([r[1] for r in res])
+    uk = torch.unique(K)
+    for op, red in (("sum", lambda x: x.sum(0)), ("min", lambda x: x.min(0).values),
+                    ("max", lambda x: x.max(0).values)):
+        seen = []
+        for rank, (_, _, own, _) in enumerate(res):
+            k, v = own[op]
+            assert torch.all(torch.remainder(k, world) == rank)  # each key reduced on its owner only
+            for kk, vv in zip(k.tolist(), v):
+                torch.testing.assert_close(vv, red(V[K == kk]))
+            seen += k.tolist()
+        assert sorted(seen) == uk.tolist()
+    for _, _, _, (k, v) in res:  # gather=True: everyone has every key
+        assert k.tolist() == uk.tolist()
+        torch.testing.assert_close(v[3], V[K == uk[3]].sum(0))
