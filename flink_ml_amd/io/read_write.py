@@ -9,11 +9,17 @@ Layout on disk (identical to the reference):
 ``className`` is the *Java* class name of the equivalent reference stage, so metadata files
 are interchangeable; ``load_stage`` dispatches on it through the stage registry.
 Only rank 0 writes (model data is replicated across ranks in this engine).
+
+Paths: plain paths use the local filesystem; a URL (``scheme://...``: ``file://``,
+``memory://``, and any remote filesystem fsspec has a driver for — the reference round-trips
+through any Flink FileSystem, ``ReadWriteUtilsTest.java:48-83``) goes through fsspec.
 """
 from __future__ import annotations
 
 import json
 import os
+import posixpath
+import re
 import time
 from typing import Any, Callable, Dict, Iterable, List, Optional
 
@@ -50,6 +56,60 @@ def all_registered_stages() -> Dict[str, type]:
     return {k: v for k, v in _REGISTRY.items() if k.startswith("org.apache.flink")}
 
 
+_URL = re.compile(r"^[A-Za-z][A-Za-z0-9+.-]*://")
+
+
+class _LocalFS:
+    join = staticmethod(os.path.join)
+    exists = staticmethod(os.path.exists)
+    open = staticmethod(open)
+
+    @staticmethod
+    def makedirs(p):
+        os.makedirs(p, exist_ok=True)
+
+    @staticmethod
+    def walk(p):
+        return os.walk(p)
+
+
+class _FsspecFS:
+    def __init__(self, path):
+        import fsspec
+
+        self.fs, _ = fsspec.core.url_to_fs(path)
+        self.proto = path.split("://", 1)[0]
+
+    def _p(self, p):
+        return self.fs._strip_protocol(p)
+
+    @staticmethod
+    def join(*parts):
+        return posixpath.join(*parts)
+
+    def exists(self, p):
+        return self.fs.exists(self._p(p))
+
+    def open(self, p, mode="r"):
+        return self.fs.open(self._p(p), mode)
+
+    def makedirs(self, p):
+        self.fs.makedirs(self._p(p), exist_ok=True)
+
+    def walk(self, p):
+        for root, dirs, names in self.fs.walk(self._p(p)):
+            yield root, dirs, names
+
+
+def fs_for(path: str):
+    """The filesystem behind ``path``: local for plain paths, fsspec for URLs."""
+    return _FsspecFS(path) if _URL.match(str(path)) else _LocalFS
+
+
+def path_join(path: str, *parts: str) -> str:
+    return fs_for(path).join(path, *parts)
+
+
 def _is_writer() -> bool:
     from ..parallel.context import get_context
 
@@ -63,10 +123,12 @@ def _barrier():
 
 
 def save_to_file(path: str, content: str, overwrite: bool = False) -> None:
-    if not overwrite and os.path.exists(path):
+    fs = fs_for(path)
+    if not overwrite and fs.exists(path):
         raise IOError("File %s already exists." % path)
-    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
-    with open(path, "w") as f:
+    parent = (posixpath.dirname(path) if fs is not _LocalFS else os.path.dirname(path)) or "."
+    fs.makedirs(parent)
+    with fs.open(path, "w") as f:
         f.write(content)
 
 
@@ -81,7 +143,7 @@ def save_metadata(stage, path: str, extra: Optional[Dict[str, Any]] = None) -> N
     meta["timestamp"] = int(time.time() * 1000)
     meta["paramMap"] = param_map_to_json(stage)
     if _is_writer():
-        save_to_file(os.path.join(path, "metadata"), json.dumps(meta), overwrite=False)
+        save_to_file(path_join(path, "metadata"), json.dumps(meta), overwrite=False)
     _barrier()
 
 
@@ -122,7 +184,7 @@ def loads_json_with_comments(text: str):
 
 
 def load_metadata(path: str, expected_class_name: str = "") -> Dict[str, Any]:
-    with open(os.path.join(path, "metadata")) as f:
+    with fs_for(path).open(path_join(path, "metadata"), "r") as f:
         lines = [l for l in f.read().splitlines() if not l.startswith("#")]
     meta = loads_json_with_comments("".join(lines))
     cls = meta.get("className")
@@ -158,7 +220,7 @@ def load_stage(path: str):
 
 
 def stage_path(parent: str, idx: int, num: int) -> str:
-    return os.path.join(parent, "stages", str(idx).zfill(len(str(num))))
+    return path_join(parent, "stages", str(idx).zfill(len(str(num))))
 
 
 def save_pipeline(pipeline, stages: List, path: str) -> None:
@@ -174,37 +236,44 @@ def load_pipeline(path: str, expected_class_name: str) -> List:
 
 
 def data_path(path: str) -> str:
-    return os.path.join(path, "data")
+    return path_join(path, "data")
 
 
 def save_model_data(path: str, records: Iterable[Any], encode: Callable[[DataOutput, Any], None]) -> None:
     """Writes model-data records (one FileSink part file, rank 0 only)."""
     if _is_writer():
+        fs = fs_for(path)
         d = data_path(path)
-        os.makedirs(d, exist_ok=True)
+        fs.makedirs(d)
         out = DataOutput()
         for r in records:
             encode(out, r)
-        with open(os.path.join(d, "part-0-0"), "wb") as f:
+        with fs.open(path_join(d, "part-0-0"), "wb") as f:
             f.write(out.getvalue())
     _barrier()
 
 
 def _data_files(path: str) -> List[str]:
+    fs = fs_for(path)
     files = []
-    for root, dirs, names in os.walk(data_path(path)):
-        dirs[:] = sorted(d for d in dirs if not d.startswith((".", "_")))
+    d = data_path(path)
+    if fs is not _LocalFS and not fs.exists(d):
+        return files
+    for root, dirs, names in fs.walk(d):
+        if isinstance(dirs, list):
+            dirs[:] = sorted(x for x in dirs if not x.startswith((".", "_")))
         for n in sorted(names):
             if not n.startswith((".", "_")):
-                files.append(os.path.join(root, n))
-    return files
+                files.append(fs.join(root, n) if fs is _LocalFS else "%s://%s" % (fs.proto, posixpath.join(root, n)))
+    return sorted(files)
 
 
 def load_model_data(path: str, decode: Callable[[DataInput], Any]) -> List[Any]:
     """Reads every record of every part file under ``<path>/data`` (FileSource semantics)."""
     out = []
+    fs = fs_for(path)
     for fn in _data_files(path):
-        with open(fn, "rb") as f:
+        with fs.open(fn, "rb") as f:
             inp = DataInput(f.read())
         while not inp.eof():
             out.append(decode(inp))

@@ -59,18 +59,23 @@ class TrainPack:
         n, d = T.shape
         self.n, self.d = int(n), int(d)
         self.dp = -(-(-(-d // 2)) // 4) * 4
-        nt = -(-n // 64)
-        dp = self.dp
-        Tp = torch.zeros((nt * 64, 2 * dp), dtype=torch.float32, device=T.device)
-        Tp[:n, :d] = T.to(torch.float32)
-        rows = torch.zeros((nt, 2, 2, 32, dp + 4), dtype=torch.float32, device=T.device)
-        rows[..., :dp] = Tp.view(nt, 2, 32, dp, 2).permute(0, 1, 4, 2, 3)
-        norms = torch.zeros((nt, 256), dtype=torch.float32, device=T.device)
-        tn = torch.zeros(nt * 64, dtype=torch.float32, device=T.device)
-        tn[:n] = tnorm.to(torch.float32)
-        norms[:, :64] = tn.view(nt, 64)
-        self.Tt = torch.cat([rows.reshape(nt, -1), norms], dim=1).contiguous()
-        assert self.Tt.shape[1] == 128 * (dp + 4) + 256
+        self.nt = -(-n // 64)
+        dev = T.device
+        self.Tt = torch.zeros((self.nt, 128 * (self.dp + 4) + 256), dtype=torch.float32, device=dev)
+        self._Tp = torch.zeros((self.nt * 64, 2 * self.dp), dtype=torch.float32, device=dev)
+        self._tn = torch.zeros(self.nt * 64, dtype=torch.float32, device=dev)
+        self.refresh(T, tnorm)
+
+    def refresh(self, T: torch.Tensor, tnorm: torch.Tensor) -> "TrainPack":
+        """Re-fills the pack in place from new values of the same shape (device copies only, so
+        it can run inside a captured graph — KMeans re-packs its centroids every round)."""
+        nt, dp, n, d = self.nt, self.dp, self.n, self.d
+        self._Tp[:n, :d].copy_(T)
+        rows = self.Tt[:, :128 * (dp + 4)].view(nt, 2, 2, 32, dp + 4)
+        rows[..., :dp].copy_(self._Tp.view(nt, 2, 32, dp, 2).permute(0, 1, 4, 2, 3))
+        self._tn[:n].copy_(tnorm)
+        self.Tt[:, 128 * (dp + 4):128 * (dp + 4) + 64].copy_(self._tn.view(nt, 64))
+        return self
 
 
 def fused_segments(nq: int, n: int, k: int, slots: int) -> int:

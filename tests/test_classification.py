@@ -148,3 +148,30 @@ def test_naive_bayes_integer_and_general_paths_agree():
         for ma, mb in zip(ra, rb):
             assert [k + 0.5 for k in ma] == list(mb) and list(ma.values()) == list(mb.values())
     assert np.array_equal(a[1].values, b[1].values)
+
+
+@pytest.mark.parametrize("n,d", [(130, 37), (64, 1), (1, 128)])
+def test_knn_train_pack_layout(n, d):
+    """The fused KNN kernel's tile image (CPU-built, device-consumed): element T[64t+32sub+r][2s+h]
+    at row (sub, h, r), column s of tile t, zero padding, norms after the rows; refresh in place."""
+    import torch
+
+    from flink_ml_amd.ops import knn as ko
+
+    g = torch.Generator().manual_seed(n + d)
+    T = torch.randn((n, d), generator=g)
+    p = ko.TrainPack(T, (T * T).sum(1))
+    T2 = torch.randn((n, d), generator=g)
+    p.refresh(T2, (T2 * T2).sum(1))
+    dp, nt = p.dp, p.nt
+    Tpad = torch.zeros((nt * 64, 2 * dp))
+    Tpad[:n, :d] = T2
+    rows = p.Tt[:, :128 * (dp + 4)].view(nt, 2, 2, 32, dp + 4)
+    for h in range(2):
+        want = Tpad[:, h::2].reshape(nt, 2, 32, dp)
+        assert torch.equal(rows[:, :, h, :, :dp], want)
+    assert torch.count_nonzero(rows[..., dp:]) == 0
+    tn = torch.zeros(nt * 64)
+    tn[:n] = (T2 * T2).sum(1)
+    assert torch.equal(p.Tt[:, 128 * (dp + 4):128 * (dp + 4) + 64].reshape(-1), tn)
+    assert torch.count_nonzero(p.Tt[:, 128 * (dp + 4) + 64:]) == 0

@@ -183,3 +183,4 @@ def test_knn_model_routes_fused_for_k64():
 
     ref = knn_vote(lab[ridx], torch.unique(lab))
     assert torch.equal(pred.double(), ref.double())
+
