@@ -1,3 +1,110 @@
 """Algorithm modules laid out like the reference Python API (``pyflink.ml.lib.<group>.<algo>``),
 so ``from flink_ml_amd.lib.classification.logisticregression import LogisticRegression`` mirrors
-``from pyflink.ml.lib.classification.logisticregression import LogisticRegression``."""
+``from pyflink.ml.lib.classification.logisticregression import LogisticRegression``.
+
+The layout is a table, not a tree of files: a meta-path finder materialises
+``flink_ml_amd.lib.<group>`` and ``flink_ml_amd.lib.<group>.<algo>`` on import, each exposing the
+stage classes (from ``flink_ml_amd.models``) that the reference module of the same path defines.
+"""
+from __future__ import annotations
+
+import importlib
+import importlib.abc
+import importlib.machinery
+import sys
+import types
+
+# group -> module -> stage classes (reference pyflink/ml/lib/<group>/<module>.py)
+LAYOUT = {
+    "classification": {
+        "knn": ("KNN", "KNNModel"),
+        "linearsvc": ("LinearSVC", "LinearSVCModel"),
+        "logisticregression": ("LogisticRegression", "LogisticRegressionModel", "OnlineLogisticRegression", "OnlineLogisticRegressionModel"),
+        "naivebayes": ("NaiveBayes", "NaiveBayesModel"),
+    },
+    "clustering": {
+        "agglomerativeclustering": ("AgglomerativeClustering",),
+        "kmeans": ("KMeans", "KMeansModel", "OnlineKMeans", "OnlineKMeansModel"),
+    },
+    "evaluation": {
+        "binaryclassificationevaluator": ("BinaryClassificationEvaluator",),
+    },
+    "feature": {
+        "binarizer": ("Binarizer",),
+        "bucketizer": ("Bucketizer",),
+        "countvectorizer": ("CountVectorizer", "CountVectorizerModel"),
+        "dct": ("DCT",),
+        "elementwiseproduct": ("ElementwiseProduct",),
+        "featurehasher": ("FeatureHasher",),
+        "hashingtf": ("HashingTF",),
+        "idf": ("IDF", "IDFModel"),
+        "imputer": ("Imputer", "ImputerModel"),
+        "interaction": ("Interaction",),
+        "kbinsdiscretizer": ("KBinsDiscretizer", "KBinsDiscretizerModel"),
+        "lsh": ("MinHashLSH", "MinHashLSHModel"),
+        "maxabsscaler": ("MaxAbsScaler", "MaxAbsScalerModel"),
+        "minmaxscaler": ("MinMaxScaler", "MinMaxScalerModel"),
+        "ngram": ("NGram",),
+        "normalizer": ("Normalizer",),
+        "onehotencoder": ("OneHotEncoder", "OneHotEncoderModel"),
+        "polynomialexpansion": ("PolynomialExpansion",),
+        "randomsplitter": ("RandomSplitter",),
+        "regextokenizer": ("RegexTokenizer",),
+        "robustscaler": ("RobustScaler", "RobustScalerModel"),
+        "sqltransformer": ("SQLTransformer",),
+        "standardscaler": ("StandardScaler", "StandardScalerModel"),
+        "stopwordsremover": ("StopWordsRemover",),
+        "stringindexer": ("StringIndexer", "StringIndexerModel", "IndexToStringModel"),
+        "tokenizer": ("Tokenizer",),
+        "univariatefeatureselector": ("UnivariateFeatureSelector", "UnivariateFeatureSelectorModel"),
+        "variancethresholdselector": ("VarianceThresholdSelector", "VarianceThresholdSelectorModel"),
+        "vectorassembler": ("VectorAssembler",),
+        "vectorindexer": ("VectorIndexer", "VectorIndexerModel"),
+        "vectorslicer": ("VectorSlicer",),
+    },
+    "regression": {
+        "linearregression": ("LinearRegression", "LinearRegressionModel"),
+    },
+    "stats": {
+        "anovatest": ("ANOVATest",),
+        "chisqtest": ("ChiSqTest",),
+        "fvaluetest": ("FValueTest",),
+    },
+}
+
+
+class _Loader(importlib.abc.Loader):
+    def create_module(self, spec):
+        return types.ModuleType(spec.name)
+
+    def exec_module(self, module):
+        parts = module.__name__.split(".")[2:]  # flink_ml_amd.lib.<group>[.<algo>]
+        if len(parts) == 1:
+            module.__path__ = []  # a package: its algorithm modules resolve through the finder
+            module.__all__ = sorted(LAYOUT[parts[0]])
+            module.__doc__ = "``%s`` algorithm modules." % parts[0]
+            return
+        names = LAYOUT[parts[0]][parts[1]]
+        models = importlib.import_module("flink_ml_amd.models")
+        for n in names:
+            setattr(module, n, getattr(models, n))
+        module.__all__ = list(names)
+        module.__doc__ = "``%s.%s`` stages." % (parts[0], parts[1])
+
+
+class _Finder(importlib.abc.MetaPathFinder):
+    _loader = _Loader()
+
+    def find_spec(self, fullname, path=None, target=None):
+        parts = fullname.split(".")
+        if parts[:2] != ["flink_ml_amd", "lib"] or len(parts) not in (3, 4):
+            return None
+        if parts[2] not in LAYOUT or (len(parts) == 4 and parts[3] not in LAYOUT[parts[2]]):
+            return None
+        return importlib.machinery.ModuleSpec(fullname, self._loader, is_package=len(parts) == 3)
+
+
+if not any(isinstance(f, _Finder) for f in sys.meta_path):
+    sys.meta_path.insert(0, _Finder())
+
+__all__ = sorted(LAYOUT)

@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""Runs only the MFMA KMeans assign (north-star shard shape by default) for rocprofv3 passes:
+``--n --d --k --reps``; prints ms and TFLOP/s per call."""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from flink_ml_amd.ops import kmeans as kk  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=12_500_000)
+    ap.add_argument("--d", type=int, default=128)
+    ap.add_argument("--k", type=int, default=1024)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    X = torch.rand((a.n, a.d), device="cuda", generator=g).to(torch.bfloat16)
+    C = torch.rand((a.k, a.d), device="cuda", generator=g)
+    cb = kk.CentroidBuffers(a.k, a.d, X.device, torch.float32)
+    cb.set(C)
+    out = torch.empty(a.n, dtype=torch.int32, device="cuda")
+    kk.assign(X, cb, "euclidean", out)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.reps):
+        kk.assign(X, cb, "euclidean", out)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / a.reps
+    print("n=%d d=%d k=%d ms=%.3f tflops=%.1f" % (a.n, a.d, a.k, ms, 2.0 * a.n * a.k * a.d / ms / 1e9), flush=True)
+
+
+if __name__ == "__main__":
+    main()

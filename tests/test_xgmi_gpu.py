@@ -118,6 +118,32 @@ def test_fused_round_flagship_shape_matches_torch(det, blocks, unroll, monkeypat
     assert np.allclose(got, ref, rtol=2e-4, atol=2e-6), np.abs(got - ref).max()
 
 
+@pytest.mark.parametrize("blocks", [256, 512])
+def test_deterministic_tail_is_bitwise_reproducible(blocks, monkeypatch):
+    """FMLX_DETERMINISTIC=1: two fits from the same data give bit-identical coefficients (the
+    fixed-order group tree); a regression to an order-dependent reduction fails here. The default
+    atomic tail is only checked to agree to rounding."""
+    _need_gpu()
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer
+    from flink_ml_amd.ops import glm as gk
+
+    monkeypatch.setattr(gk, "GRAD_BLOCKS", blocks)
+    g = torch.Generator(device="cpu").manual_seed(11)
+    n, d, B = 120_000, 1000, 60_000
+    Xb = torch.rand((n, d), generator=g).to(torch.bfloat16).cuda()
+    y = torch.randint(0, 2, (n,), generator=g).to(torch.float64).cuda()
+
+    def fit(det):
+        monkeypatch.setattr(gk, "DETERMINISTIC", det)
+        sgd = SGD(max_iter=6, learning_rate=0.1, global_batch_size=B, tol=0.0)
+        return DeviceGlmTrainer(sgd, np.zeros(d), Xb, y, None, "logistic", use_graph=False).fit()
+
+    a, b = fit(True), fit(True)
+    assert np.array_equal(a, b)
+    c = fit(False)
+    assert np.allclose(a, c, rtol=1e-5, atol=1e-7)
+
+
 @pytest.mark.parametrize("graph", [False, True])
 def test_multi_round_launch_terminates_mid_way(graph):
     """One host call issuing many rounds (and a replayed 16-round hipGraph) stops exactly where
