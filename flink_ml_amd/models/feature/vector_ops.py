@@ -213,8 +213,7 @@ class PolynomialExpansion(Transformer, HasInputCol, HasOutputCol):
         Xd = X.to(torch.float64) if X.device.type == "cpu" else (X.float() if X.dtype == torch.bfloat16 else X)
         d = Xd.shape[1]
         terms = torch.as_tensor(_poly_terms(d, self.get(self.DEGREE)), device=Xd.device)
-        Xp = torch.cat([Xd, torch.ones((Xd.shape[0], 1), dtype=Xd.dtype, device=Xd.device)], dim=1)
-        out = Xp[:, terms].prod(dim=2)
+        out = blas.gather_prod(Xd, terms)  # one launch on the device (column index d = the constant 1)
         if sparse_in:
             out = SparseColumn.from_dense(out)
         return [t.with_column(self.get(self.OUTPUT_COL), out)]

@@ -49,6 +49,7 @@ native.register_kernel_sigs({
     "fmlx_blas_csr_csr_dot": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p,
                               c_void_p],
     "fmlx_blas_gather_cols": [c_int, c_void_p, c_long, c_void_p, c_long, c_int, c_void_p, c_void_p],
+    "fmlx_blas_gather_prod": [c_int, c_void_p, c_long, c_int, c_void_p, c_int, c_long, c_int, c_void_p, c_void_p],
     "fmlx_blas_interaction": [c_int, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p],
 })
 
@@ -324,6 +325,22 @@ def gather_cols(X: torch.Tensor, cols: Sequence[int]) -> torch.Tensor:
                     native.ptr(out), native.stream_ptr(X.device))
         return out
     return X[:, idx.long()]
+
+
+def gather_prod(X: torch.Tensor, terms: torch.Tensor) -> torch.Tensor:
+    """out[:, j] = Π_q X[:, terms[j, q]] with a term index ≥ D meaning the constant 1
+    (PolynomialExpansion's monomials) — one launch, no [n, T, degree] gather temporary."""
+    n, d = X.shape
+    T, deg = terms.shape
+    if X.is_cuda and X.dtype in (torch.float32, torch.float64) and n and T:
+        X = _rowmajor(X)
+        tt = terms.to(device=X.device, dtype=torch.int32).contiguous()
+        out = torch.empty((n, T), dtype=X.dtype, device=X.device)
+        native.call("fmlx_blas_gather_prod", native.dtype_code(X.dtype), native.ptr(X), X.stride(0), d, native.ptr(tt),
+                    deg, n, T, native.ptr(out), native.stream_ptr(X.device))
+        return out
+    Xp = torch.cat([X, torch.ones((n, 1), dtype=X.dtype, device=X.device)], dim=1)
+    return Xp[:, terms.to(X.device).long().clamp(max=d)].prod(dim=2)
 
 
 def interaction(mats: Sequence[torch.Tensor]) -> torch.Tensor:

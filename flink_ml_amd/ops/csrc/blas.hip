@@ -260,6 +260,26 @@ __global__ __launch_bounds__(256) void gather_cols_kernel(const T* __restrict__ 
   }
 }
 
+// PolynomialExpansion: out[r, j] = Π_q X[r, terms[j·deg + q]], a term index >= d standing for the
+// constant 1 (monomials of degree < deg). Thread per output element, terms from L1/L2 (small).
+template <typename T>
+__global__ __launch_bounds__(256) void gather_prod_kernel(const T* __restrict__ X, long ldx, int d,
+                                                          const int* __restrict__ terms, int deg, long n, int m,
+                                                          T* __restrict__ out) {
+  const long total = n * (long)m;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / m;
+    const int* tj = terms + (i - r * m) * deg;
+    const T* x = X + r * ldx;
+    T v = (T)1;
+    for (int q = 0; q < deg; ++q) {
+      const int c = tj[q];
+      if (c < d) v *= x[c];
+    }
+    out[i] = v;
+  }
+}
+
 // Interaction: out[r, j] = Π_k in_k[r, (j / stride_k) mod dim_k] (feature crosses, first input
 // slowest — the reference's nested loop order, Interaction.java).
 constexpr int INTER_MAX = 8;
@@ -506,6 +526,24 @@ FMLX_API int fmlx_blas_gather_cols(int esize, const void* X, long ldx, const int
   else if (esize == 2)
     hipLaunchKernelGGL(gather_cols_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)X, ldx, cols, n, m,
                        (bf16_t*)out);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+// out [n, m] = products of the columns listed per output term (see gather_prod_kernel); fp32/fp64
+FMLX_API int fmlx_blas_gather_prod(int dtype, const void* X, long ldx, int d, const int* terms, int deg, long n, int m,
+                                   void* out, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n <= 0 || m <= 0) return 0;
+  if (deg < 1 || d < 1) return -1;
+  const int g = blocks_for(n * (long)m, 256, 8192);
+  if (dtype == DT_F64)
+    hipLaunchKernelGGL(gather_prod_kernel<double>, dim3(g), dim3(256), 0, s, (const double*)X, ldx, d, terms, deg, n,
+                       m, (double*)out);
+  else if (dtype == DT_F32)
+    hipLaunchKernelGGL(gather_prod_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)X, ldx, d, terms, deg, n,
+                       m, (float*)out);
   else
     return -1;
   return (int)hipGetLastError();

@@ -5,6 +5,10 @@ The HIP kernels are plain ``extern "C"`` launchers that take device pointers and
 with torch ops and RCCL collectives and can be captured into a hipGraph
 (``torch.cuda.CUDAGraph``) together with them.
 
+Debugging: ``FMLX_SYNC_CHECK=1`` synchronises the device after every native launch and reports an
+asynchronous fault under the name of the kernel that caused it (the HIP analogue of a blocking
+launch mode; slow, off by default).
+
 Policy: on a GPU host the native library is REQUIRED — ``kernels()`` raises if it is
 missing (no silent eager fallback). On CPU-only hosts the ops layer runs its torch reference
 implementation (same semantics, fp64), which is what the CPU test-suite exercises.
@@ -166,6 +170,14 @@ def check(rc: int, what: str) -> None:
         raise RuntimeError("HIP launch %s failed with error %d" % (what, rc))
 
 
+SYNC_CHECK = os.environ.get("FMLX_SYNC_CHECK", "0") == "1"
+
+
 def call(name: str, *args) -> None:
     rc = getattr(kernels(), name)(*args)
     check(rc, name)
+    if SYNC_CHECK and torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
+        try:
+            torch.cuda.synchronize()
+        except RuntimeError as e:
+            raise RuntimeError("native kernel %s failed asynchronously: %s" % (name, e)) from e

@@ -136,3 +136,30 @@ def test_interaction(dev):
 def test_invalid_p_rejected():
     with pytest.raises(ValueError):
         blas.row_norm(torch.ones(2, 2), 0.5)
+
+
+@pytest.mark.parametrize("dev", [pytest.param(d, marks=_mark(d)) for d in ["cpu", "cuda"]])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_gather_prod_polynomial_terms(dev, dtype):
+    _need(dev)
+    from flink_ml_amd.models.feature.vector_ops import _poly_terms
+
+    X = _dense(300, 5, 4).to(dtype)
+    terms = torch.as_tensor(_poly_terms(5, 3))
+    got = blas.gather_prod(_to(X, dev), terms).cpu()
+    Xp = torch.cat([X.double(), torch.ones(300, 1, dtype=torch.float64)], 1)
+    ref = Xp[:, terms.long()].prod(2)
+    assert got.dtype == dtype and got.shape == ref.shape
+    assert torch.allclose(got.double(), ref, rtol=_tol(dtype), atol=_tol(dtype))
+
+
+@pytest.mark.gpu
+def test_sync_check_mode_runs_kernels(monkeypatch):
+    """FMLX_SYNC_CHECK: every native launch is followed by a device sync (faults are attributed to
+    the launching kernel); results are unchanged."""
+    _need("cuda")
+    from flink_ml_amd.ops import native
+
+    monkeypatch.setattr(native, "SYNC_CHECK", True)
+    X = _dense(64, 7, 9).cuda()
+    assert torch.allclose(blas.row_norm(X, 2.0).cpu(), torch.linalg.vector_norm(X.cpu(), dim=1), rtol=1e-12)
