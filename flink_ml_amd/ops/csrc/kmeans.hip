@@ -37,7 +37,7 @@ constexpr int KM_CH = 256;  // rows per gather chunk
 // ------------------------------------------------------------------------------------------
 // MFMA assign (euclidean, bf16)
 // ------------------------------------------------------------------------------------------
-template <int KS, bool FULL>
+template <int KS, bool FULL, bool SCHED>
 // Cb / cnorm are not __restrict__ so the compiler fence after each tile prefetch keeps the
 // loads where they are issued (with restrict they get sunk next to their use, after the MFMAs).
 __global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t* __restrict__ X, long ld, long n,
@@ -186,31 +186,57 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t
     bf16x8_t bfr[KS];  // all B fragments in flight before the first MFMA needs one
 #pragma unroll
     for (int s = 0; s < KS; ++s) bfr[s] = *reinterpret_cast<const bf16x8_t*>(tb + s * 32);
+    const unsigned tt = (unsigned)t;
+    typedef float f32x2_t __attribute__((ext_vector_type(2)));
+    const f32x2_t c2 = {cn, cn};
+    // epilogue of accumulator registers r, r+1 of m-tile m: + ‖c‖² (packed), tile id into the low
+    // mantissa bits, unsigned running min — 5 VALU instructions
+#define KM_EPI2(M_, R_)                                                        \
+    {                                                                          \
+      f32x2_t v = {acc[M_][R_], acc[M_][(R_) + 1]};                            \
+      v = v + c2;                                                              \
+      const unsigned k0 = (__float_as_uint(v[0]) & vkeep) | tt;                \
+      const unsigned k1 = (__float_as_uint(v[1]) & vkeep) | tt;                \
+      best[M_][R_] = k0 < best[M_][R_] ? k0 : best[M_][R_];                    \
+      best[M_][(R_) + 1] = k1 < best[M_][(R_) + 1] ? k1 : best[M_][(R_) + 1]; \
+    }
+    if constexpr (SCHED && MT == 2) {
+      // every B read issued up front (one LDS wait per tile, not one per k-step), the m-tile 0
+      // chain, then the m-tile 1 chain with m-tile 0's epilogue in its MFMA gaps (one register
+      // pair = 5 VALU per 32-cycle MFMA), so half the epilogue runs under the matrix core
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int s = 0; s < KS; ++s)
+      for (int s = 0; s < KS; ++s)
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][s], bfr[s], s == 0 ? xnb[0] : acc[0], 0, 0, 0);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][s], bfr[s], s == 0 ? xnb[1] : acc[1], 0, 0, 0);
+        if (2 * s < 16) KM_EPI2(0, 2 * s)
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // then 5 VALU
+      }
+#pragma unroll
+      for (int r = 2 * KS; r < 16; r += 2) KM_EPI2(0, r)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) KM_EPI2(1, r)
+    } else {
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m][s], bfr[s], s == 0 ? xnb[m] : acc[m], 0, 0, 0);
+      // (a software-pipelined variant — tile t's MFMAs interleaved with tile t-1's epilogue on a
+      // second accumulator set — measured slower: 4.46 ms at 256 VGPRs vs 4.02 ms for this loop at
+      // 190 VGPRs; two resident waves per SIMD already overlap one's MFMAs with the other's VALU)
 #pragma unroll
       for (int m = 0; m < MT; ++m)
-        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m][s], bfr[s], s == 0 ? xnb[m] : acc[m], 0, 0, 0);
-    // (a software-pipelined variant — tile t's MFMAs interleaved with tile t-1's epilogue on a
-    // second accumulator set — measured slower: 4.46 ms at 256 VGPRs vs 4.02 ms for this loop at
-    // 190 VGPRs; two resident waves per SIMD already overlap one's MFMAs with the other's VALU)
-    const unsigned tt = (unsigned)t;
 #pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        typedef float f32x2_t __attribute__((ext_vector_type(2)));
-        f32x2_t v = {acc[m][r], acc[m][r + 1]};
-        const f32x2_t c2 = {cn, cn};
-        v = v + c2;
-        const unsigned k0 = (__float_as_uint(v[0]) & vkeep) | tt;
-        const unsigned k1 = (__float_as_uint(v[1]) & vkeep) | tt;
-        best[m][r] = k0 < best[m][r] ? k0 : best[m][r];
-        best[m][r + 1] = k1 < best[m][r + 1] ? k1 : best[m][r + 1];
-      }
-    if (more) {
-      KM_SWRITE(cur ^ 1)
+        for (int r = 0; r < 16; r += 2) KM_EPI2(m, r)
     }
+#undef KM_EPI2
+    // unconditional (after the last tile it rewrites the idle buffer with the re-fetched last
+    // tile, which nobody reads): a branch here split the tile body into two scheduling regions
+    KM_SWRITE(cur ^ 1)
     cn = cn_next;
     __syncthreads();
   }
@@ -612,6 +638,8 @@ __global__ __launch_bounds__(256) void kmeans_finalize_kernel(const A* __restric
   }
 }
 
+int g_km_sched = 0;  // interleaved MFMA/epilogue schedule of the MFMA assign (fmlx_kmeans_set_sched)
+
 template <int KS>
 int launch_assign_bf16(const void* X, long ld, long n, int D, const void* Cb, const float* cnorm, int kpad, int* labels,
                        hipStream_t s) {
@@ -620,11 +648,14 @@ int launch_assign_bf16(const void* X, long ld, long n, int D, const void* Cb, co
   const int blocks = (int)((n + rows_per_block - 1) / rows_per_block);
   if (blocks == 0) return 0;
   const bool full = D == 16 * KS && (ld % 8) == 0 && ((uintptr_t)X % 16) == 0;
-  if (full)
-    hipLaunchKernelGGL((kmeans_assign_bf16_kernel<KS, true>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)X, ld, n,
+  if (full && g_km_sched)
+    hipLaunchKernelGGL((kmeans_assign_bf16_kernel<KS, true, true>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)X, ld,
+                       n, D, (const bf16_t*)Cb, cnorm, kpad, labels);
+  else if (full)
+    hipLaunchKernelGGL((kmeans_assign_bf16_kernel<KS, true, false>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)X, ld, n,
                        D, (const bf16_t*)Cb, cnorm, kpad, labels);
   else
-    hipLaunchKernelGGL((kmeans_assign_bf16_kernel<KS, false>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)X, ld, n,
+    hipLaunchKernelGGL((kmeans_assign_bf16_kernel<KS, false, false>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)X, ld, n,
                        D, (const bf16_t*)Cb, cnorm, kpad, labels);
   return (int)hipGetLastError();
 }
@@ -652,6 +683,11 @@ int chunk_sum_vpl(const void* X, long ld, int D, const long* order, const long* 
 }  // namespace
 
 // KS = padded K-steps of 16 (one of 1..8,10,12,16; >= ceil(D/16)); Cb is [kpad][16*KS] zero-padded
+FMLX_API int fmlx_kmeans_set_sched(int on) {
+  g_km_sched = on;
+  return 0;
+}
+
 FMLX_API int fmlx_kmeans_assign_bf16(const void* X, long ld, long n, int D, int KS, const void* Cb, const float* cnorm,
                                      int kpad, int* labels, void* stream) {
   hipStream_t s = (hipStream_t)stream;

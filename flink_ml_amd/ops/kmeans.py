@@ -16,6 +16,7 @@ from . import native
 from .native import c_int, c_long, c_void_p
 
 native.register_kernel_sigs({
+    "fmlx_kmeans_set_sched": [c_int],
     "fmlx_kmeans_assign_bf16": [c_void_p, c_long, c_long, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
                                 c_void_p],
     "fmlx_kmeans_assign_generic": [c_int, c_void_p, c_long, c_long, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p,

@@ -18,7 +18,11 @@ def main():
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--k", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--sched", type=int, default=1, help="interleaved MFMA/epilogue schedule (1) or not (0)")
     a = ap.parse_args()
+    from flink_ml_amd.ops import native
+
+    native.call("fmlx_kmeans_set_sched", a.sched)
     g = torch.Generator(device="cuda").manual_seed(0)
     X = torch.rand((a.n, a.d), device="cuda", generator=g).to(torch.bfloat16)
     C = torch.rand((a.k, a.d), device="cuda", generator=g)
@@ -34,7 +38,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.reps
-    print("n=%d d=%d k=%d ms=%.3f tflops=%.1f" % (a.n, a.d, a.k, ms, 2.0 * a.n * a.k * a.d / ms / 1e9), flush=True)
+    print("sched=%d n=%d d=%d k=%d ms=%.3f tflops=%.1f" % (a.sched, a.n, a.d, a.k, ms, 2.0 * a.n * a.k * a.d / ms / 1e9), flush=True)
 
 
 if __name__ == "__main__":
