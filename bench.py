@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp64"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--graph-rounds", type=int, default=10, help="SGD rounds captured per hipGraph replay")
+    ap.add_argument("--torch-profile", default="", help="after the timed region, record a torch.profiler trace of "
+                                                        "extra rounds into this directory (not timed)")
     args = ap.parse_args()
 
     from flink_ml_amd.parallel.context import init_distributed
@@ -106,6 +108,8 @@ def main():
         tr = DeviceGlmTrainer(sgd, np.zeros(args.dim), X, y, None, "logistic", use_graph=not args.no_graph)
         tr.rounds_per_graph = args.graph_rounds
         sgd.max_iter = args.warmup + sum(tr.graph_sizes(args.steps)) + args.steps + 1  # read at capture
+        if args.torch_profile:
+            sgd.max_iter += PROFILE_ROUNDS
         return tr
 
     if world > 1 and not ctx.is_distributed:
@@ -167,7 +171,15 @@ def main():
             },
         }
         print(json.dumps(rec), flush=True)
+    if args.torch_profile:
+        from flink_ml_amd.utils import tracing
 
+        with tracing.torch_profile(args.torch_profile):
+            trainer.run_rounds(PROFILE_ROUNDS)
+            torch.cuda.synchronize()
+
+
+PROFILE_ROUNDS = 20
 
 if __name__ == "__main__":
     main()

@@ -6,6 +6,8 @@
   the online models (``OnlineKMeansModel.java:58,163-166``, ``OnlineLogisticRegressionModel.java:59,129-133``)
   that the streaming tests synchronise on.
 * ``log_round`` — structured JSON per-round log lines (rank, epoch, loss, weight, ms).
+* ``torch_profile(path)`` — a ``torch.profiler`` session (host ops + HIP kernels) exported as a
+  Chrome trace per rank (``FMLX_TORCH_PROFILE=<dir>`` or ``bench.py --torch-profile <dir>``).
 """
 from __future__ import annotations
 
@@ -91,6 +93,26 @@ def log_round(**fields) -> None:
 
 def enabled() -> bool:
     return _ENABLED
+
+
+@contextlib.contextmanager
+def torch_profile(path: Optional[str]):
+    """Records a torch.profiler trace of the enclosed work into ``<path>/trace_rank<r>.json``
+    (no-op when ``path`` is falsy)."""
+    if not path:
+        yield None
+        return
+    import torch
+    from torch.profiler import ProfilerActivity, profile
+
+    acts = [ProfilerActivity.CPU]
+    if torch.cuda.is_available():
+        acts.append(ProfilerActivity.CUDA)
+    rank = int(os.environ.get("RANK", "0"))
+    os.makedirs(path, exist_ok=True)
+    with profile(activities=acts, record_shapes=False) as prof:
+        yield prof
+    prof.export_chrome_trace(os.path.join(path, "trace_rank%d.json" % rank))
 
 
 class MetricGroup:
