@@ -86,29 +86,77 @@ def _dict_col(t: Table, col: str):
     return None
 
 
-def _per_string_arrays(t: Table, col: str, fn):
+def _register_textops():
+    import ctypes
+
+    from ...ops import native
+
+    vp, i64 = ctypes.c_void_p, ctypes.c_int64
+    native.register_host_sigs({"fmlx_tokenize_ws_lower": ([vp, vp, i64, vp, vp, i64, vp, vp, vp], i64)})
+
+
+_register_textops()
+
+
+def _native_ws_lower_tokens(strings: List[str]):
+    """Tokenizer's lowercase + ``split("\\s")`` over distinct strings in native code
+    (``csrc/host/textops.cpp``): (tokens per string, flat token ids, token vocabulary), or None
+    when a string is not ASCII (the Unicode-aware Python path then applies)."""
+    from ...ops import native
+
+    try:
+        raw = "".join(strings).encode("ascii")
+    except UnicodeEncodeError:
+        return None
+    n = len(strings)
+    offs = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.fromiter(map(len, strings), dtype=np.int64, count=n), out=offs[1:])
+    cap = int(offs[-1]) + n + 1
+    ntok = np.zeros(n, dtype=np.int32)
+    ids = np.zeros(cap, dtype=np.int32)
+    vbytes = np.zeros(int(offs[-1]) + cap, dtype=np.uint8)
+    voffs = np.zeros(cap + 1, dtype=np.int64)
+    nv = np.zeros(1, dtype=np.int64)
+    buf = np.frombuffer(raw, dtype=np.uint8) if raw else np.zeros(1, dtype=np.uint8)
+    nt = native.host().fmlx_tokenize_ws_lower(buf.ctypes.data, offs.ctypes.data, n, ntok.ctypes.data, ids.ctypes.data,
+                                              cap, vbytes.ctypes.data, voffs.ctypes.data, nv.ctypes.data)
+    if nt < 0:
+        return None
+    nvoc = int(nv[0])
+    vocab = vbytes[: int(voffs[nvoc])].tobytes().decode("ascii").split("\n")[:nvoc] if nvoc else []
+    return ntok.astype(np.int64), ids[:nt], vocab
+
+
+def _per_string_arrays(t: Table, col: str, fn, native_kind: str = ""):
     """``fn`` (str -> list of str) applied once per distinct string of a dictionary-encoded
     ``StringColumn``, expanded to every row by code on the device → ``StringArrayColumn``; None for
-    a plain list column."""
+    a plain list column. ``native_kind="ws_lower"``: ``fn`` is Tokenizer's lowercase + ``\\s``
+    split, done for all distinct strings at once in native code when they are ASCII."""
     c = t.column(col)
     if not isinstance(c, StringColumn) or len(c) == 0 or any(not isinstance(w, str) for w in c.vocab):
         return None
     dev = config.compute_device()
     codes = c.codes.to(dev).long()
-    index, vocab, flat, vlen = {}, [], [], []
-    for w in c.vocab:
-        toks = fn(w)
-        vlen.append(len(toks))
-        for x in toks:
-            k = index.get(x)
-            if k is None:
-                k = index[x] = len(vocab)
-                vocab.append(x)
-            flat.append(k)
-    vlen_t = torch.tensor(vlen, dtype=torch.int64, device=dev)
-    voff = torch.zeros(len(vlen) + 1, dtype=torch.int64, device=dev)
+    nat = _native_ws_lower_tokens(c.vocab) if native_kind == "ws_lower" else None
+    if nat is not None:
+        vlen_np, flat_np, vocab = nat
+        vlen_t = torch.from_numpy(vlen_np).to(dev)
+        vflat = torch.from_numpy(flat_np).to(dev)
+    else:
+        index, vocab, flat, vlen = {}, [], [], []
+        for w in c.vocab:
+            toks = fn(w)
+            vlen.append(len(toks))
+            for x in toks:
+                k = index.get(x)
+                if k is None:
+                    k = index[x] = len(vocab)
+                    vocab.append(x)
+                flat.append(k)
+        vlen_t = torch.tensor(vlen, dtype=torch.int64, device=dev)
+        vflat = torch.tensor(flat, dtype=torch.int32, device=dev)
+    voff = torch.zeros(vlen_t.shape[0] + 1, dtype=torch.int64, device=dev)
     voff[1:] = torch.cumsum(vlen_t, 0)
-    vflat = torch.tensor(flat, dtype=torch.int32, device=dev)
     lens = vlen_t[codes]
     off = torch.zeros(codes.shape[0] + 1, dtype=torch.int64, device=dev)
     off[1:] = torch.cumsum(lens, 0)
@@ -134,7 +182,7 @@ class Tokenizer(Transformer, HasInputCol, HasOutputCol):
 
     def transform(self, *inputs):
         t = inputs[0]
-        out = _per_string_arrays(t, self.get(self.INPUT_COL), lambda s: java_split(r"\s", s.lower()))
+        out = _per_string_arrays(t, self.get(self.INPUT_COL), lambda s: java_split(r"\s", s.lower()), "ws_lower")
         if out is None:
             out = [java_split(r"\s", s.lower()) for s in _strings_col(t, self.get(self.INPUT_COL))]
         return [t.with_column(self.get(self.OUTPUT_COL), out)]

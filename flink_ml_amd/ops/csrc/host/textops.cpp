@@ -1,0 +1,96 @@
+// Text-stage helpers over the DISTINCT strings of a dictionary-encoded column (the rows
+// themselves stay device codes): Tokenizer's `toLowerCase()` + `String.split("\\s")` for a batch
+// of strings with the produced tokens deduplicated into a vocabulary — the per-distinct-string
+// host work that dominates high-cardinality columns (reference Tokenizer.java:55-66).
+//
+// ASCII only: a string with a byte >= 0x80 makes the call return -1 so the caller takes the
+// general (Unicode-aware) path. Java semantics kept: `\s` = [ \t\n\x0B\f\r]; "" splits to [""];
+// a leading delimiter yields a leading empty token; trailing empty tokens are removed.
+#include <cstdint>
+#include <cstring>
+#include <string_view>
+#include <unordered_map>
+
+namespace {
+inline bool java_ws(unsigned char c) { return c == ' ' || c == '\t' || c == '\n' || c == 0x0B || c == '\f' || c == '\r'; }
+inline char lower_ascii(char c) { return (c >= 'A' && c <= 'Z') ? (char)(c + 32) : c; }
+}  // namespace
+
+extern "C" {
+
+// bytes/offs: n strings (offs[n+1]). Outputs: ntok[n] tokens per string, tok_ids[] (capacity
+// tok_cap) the vocabulary id of every token in order, vocab_bytes (capacity = total bytes +
+// tok_cap) the distinct tokens in first-seen order, each followed by '\n' (a token never contains
+// one), with vocab_offs[] (capacity tok_cap + 1) their start offsets and *nvocab their count.
+// Returns the total number of tokens, -1 for non-ASCII input, -2 when a capacity is too small.
+int64_t fmlx_tokenize_ws_lower(const char* bytes, const int64_t* offs, int64_t n, int32_t* ntok, int32_t* tok_ids,
+                               int64_t tok_cap, char* vocab_bytes, int64_t* vocab_offs, int64_t* nvocab) {
+  const int64_t total_bytes = offs[n];
+  for (int64_t i = 0; i < total_bytes; ++i)
+    if ((unsigned char)bytes[i] >= 0x80) return -1;
+  // lowercased copy lives in vocab_bytes' scratch? no: tokens are views into a lowered buffer
+  char* low = new char[total_bytes > 0 ? total_bytes : 1];
+  for (int64_t i = 0; i < total_bytes; ++i) low[i] = lower_ascii(bytes[i]);
+  std::unordered_map<std::string_view, int32_t> index;
+  index.reserve((size_t)(n * 2 + 16));
+  int64_t nt = 0, vb = 0, nv = 0;
+  vocab_offs[0] = 0;
+  auto emit = [&](const char* p, int64_t len) -> bool {
+    if (nt >= tok_cap) return false;
+    std::string_view key(p, (size_t)len);
+    auto it = index.find(key);
+    int32_t id;
+    if (it == index.end()) {
+      std::memcpy(vocab_bytes + vb, p, (size_t)len);
+      id = (int32_t)nv;
+      index.emplace(std::string_view(vocab_bytes + vb, (size_t)len), id);
+      vb += len;
+      vocab_bytes[vb++] = '\n';
+      vocab_offs[++nv] = vb;
+    } else {
+      id = it->second;
+    }
+    tok_ids[nt++] = id;
+    return true;
+  };
+  for (int64_t s = 0; s < n; ++s) {
+    const char* p = low + offs[s];
+    const int64_t len = offs[s + 1] - offs[s];
+    const int64_t before = nt;
+    if (len == 0) {
+      if (!emit(p, 0)) { delete[] low; return -2; }
+      ntok[s] = 1;
+      continue;
+    }
+    // trailing empty tokens are dropped: the last token ends at the last non-delimiter
+    int64_t end = len;
+    while (end > 0 && java_ws((unsigned char)p[end - 1])) --end;
+    if (end == 0) {  // only delimiters: Java yields an empty array
+      ntok[s] = 0;
+      continue;
+    }
+    int64_t start = 0;
+    for (int64_t i = 0; i <= end; ++i) {
+      if (i == end || java_ws((unsigned char)p[i])) {
+        if (!emit(p + start, i - start)) { delete[] low; return -2; }
+        start = i + 1;
+      }
+    }
+    ntok[s] = (int32_t)(nt - before);
+  }
+  delete[] low;
+  *nvocab = nv;
+  return nt;
+}
+}
+
+extern "C" {
+// String.hashCode() of n strings given as UTF-16 code units (offs in units): s[0]·31^(n-1) + ...
+void fmlx_java_string_hashes(const uint16_t* units, const int64_t* offs, int64_t n, int32_t* out) {
+  for (int64_t s = 0; s < n; ++s) {
+    uint32_t h = 0;
+    for (int64_t i = offs[s]; i < offs[s + 1]; ++i) h = 31u * h + units[i];
+    out[s] = (int32_t)h;
+  }
+}
+}

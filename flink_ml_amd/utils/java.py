@@ -32,6 +32,39 @@ def java_string_hash(s: str) -> int:
     return _i32(h)
 
 
+_HASH_SIG = False
+
+
+def java_string_hashes(strings) -> "np.ndarray":
+    """``String.hashCode()`` of many strings at once (native loop over their UTF-16 units)."""
+    import ctypes
+
+    import numpy as np
+
+    from ..ops import native
+
+    global _HASH_SIG
+    if not _HASH_SIG:
+        native.register_host_sigs({"fmlx_java_string_hashes": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                                               ctypes.c_void_p]})
+        _HASH_SIG = True
+    strings = list(strings)
+    n = len(strings)
+    out = np.zeros(n, dtype=np.int32)
+    if n == 0:
+        return out
+    raw = "".join(strings).encode("utf-16-le", "surrogatepass")
+    units = np.frombuffer(raw, dtype=np.uint16) if raw else np.zeros(1, dtype=np.uint16)
+    lens = np.fromiter(map(len, strings), dtype=np.int64, count=n)
+    if int(lens.sum()) != len(raw) // 2:  # astral characters take two UTF-16 units
+        lens = np.fromiter((len(w.encode("utf-16-le", "surrogatepass")) // 2 for w in strings), dtype=np.int64,
+                           count=n)
+    offs = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(lens, out=offs[1:])
+    native.host().fmlx_java_string_hashes(units.ctypes.data, offs.ctypes.data, n, out.ctypes.data)
+    return out
+
+
 def java_long_hash(v: int) -> int:
     v &= 0xFFFFFFFFFFFFFFFF
     return _i32(v ^ (v >> 32))
@@ -83,6 +116,14 @@ def java_hashmap_order(keys, hash_fn=java_hash, initial_capacity: int = 16):
         size += 1
         if size > cap * 0.75:
             cap *= 2
+
+    if hash_fn is java_string_hash and len(keys) > 256 and all(isinstance(k, str) for k in keys):
+        # many string keys: hashes in one native pass, buckets and the stable order in numpy
+        import numpy as np
+
+        h = java_string_hashes(keys).view(np.uint32).astype(np.uint64)
+        b = (h ^ (h >> np.uint64(16))) & np.uint64(cap - 1)
+        return [keys[i] for i in np.argsort(b, kind="stable").tolist()]
 
     def bucket(k):
         h = hash_fn(k) & 0xFFFFFFFF
