@@ -131,6 +131,38 @@ int launch(unsigned long long seed, unsigned long long start_draw, long row0, lo
 // seed: the already scrambled LCG state ((seed ^ 0x5DEECE66D) & mask); start_draw: draws consumed
 // before row0. first_reject must be preset to ULLONG_MAX; it receives the smallest local row index
 // (relative to row0) whose nextInt would have rejected.
+namespace {
+// Raw nextInt(bound) draws at consecutive sequence positions [start, start + count): r = u % bound
+// and whether Java's rejection loop accepts u (u − r + bound − 1 < 2^31). 16 positions per thread
+// after one jump-ahead. The host compacts the accepted draws with a prefix sum, which reproduces
+// Random.nextInt's sequential rejection loop for rows whose draws all use the same bound.
+__global__ __launch_bounds__(256) void java_int_draws_kernel(unsigned long long x0, unsigned long long start,
+                                                             long count, int bound, int* __restrict__ r_out,
+                                                             unsigned char* __restrict__ ok_out) {
+  const long base = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (base >= count) return;
+  unsigned long long s = jump(x0, start + (unsigned long long)base);
+  const long end = base + 16 < count ? base + 16 : count;
+  for (long p = base; p < end; ++p) {
+    const int u = next_bits(s, 31);
+    const int r = u % bound;
+    r_out[p] = r;
+    ok_out[p] = ((long long)u - r + bound - 1) < (1LL << 31) ? 1 : 0;
+  }
+}
+}  // namespace
+
+// seed: the scrambled Random state; see java_int_draws_kernel.
+FMLX_API int fmlx_java_int_draws(unsigned long long seed, unsigned long long start, long count, int bound, int* r_out,
+                                 unsigned char* ok_out, void* stream) {
+  if (count <= 0) return 0;
+  if (bound <= 0) return -1;
+  const long threads = (count + 15) / 16;
+  hipLaunchKernelGGL(java_int_draws_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, seed, start, count, bound, r_out, ok_out);
+  return (int)hipGetLastError();
+}
+
 FMLX_API int fmlx_java_rows(int vec_dtype, unsigned long long seed, unsigned long long start_draw, long row0,
                             long nrows, const int* ops, const int* slot_off, int nslots, int nvec, int draws_per_row,
                             void* vec, double* scal, unsigned long long* first_reject, void* stream) {

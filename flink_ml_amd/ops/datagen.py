@@ -23,6 +23,7 @@ _ADD = 0xB
 _MASK = (1 << 48) - 1
 
 native.register_kernel_sigs({
+    "fmlx_java_int_draws": [native.c_ulonglong, native.c_ulonglong, c_long, c_int, c_void_p, c_void_p, c_void_p],
     "fmlx_java_rows": [c_int, native.c_ulonglong, native.c_ulonglong, c_long, c_long, c_void_p, c_void_p, c_int, c_int,
                        c_int, c_void_p, c_void_p, c_void_p, c_void_p],
 })
@@ -117,10 +118,42 @@ def _cpu_rows(x0: int, start: int, n: int, ops, nvec, vec: np.ndarray, scal: np.
     return int(bad[0]) if bad.size else -1
 
 
+def java_uniform_int_rows(seed: int, n: int, k: int, bound: int, device) -> torch.Tensor:
+    """[n, k] int32 of ``k`` successive ``Random.nextInt(bound)`` per row (rows back to back in one
+    ``java.util.Random(seed)`` stream), on the device for any bound: raw draws and their rejection
+    test in parallel (``fmlx_java_int_draws``), then the accepted ones compacted by a prefix sum —
+    the same values as the sequential rejection loop, without a host round trip per rejection
+    (bounds like 1,000,000 reject ~1 draw in 4,400)."""
+    need = n * k
+    x0 = scramble(seed)
+    p_rej = ((1 << 31) % bound) / float(1 << 31)
+    out = torch.empty(need, dtype=torch.int32, device=device)
+    got, pos = 0, 0
+    while got < need:
+        rem = need - got
+        count = int(rem / max(1e-9, 1.0 - p_rej)) + 64 + int(4 * (rem * p_rej) ** 0.5)
+        r = torch.empty(count, dtype=torch.int32, device=device)
+        ok = torch.empty(count, dtype=torch.uint8, device=device)
+        native.call("fmlx_java_int_draws", x0, pos, count, bound, native.ptr(r), native.ptr(ok), native.stream_ptr(device))
+        acc = r[ok.bool()]
+        take = min(rem, acc.numel())
+        out[got:got + take] = acc[:take]
+        if take == rem:
+            break
+        got += take
+        pos += count
+    return out.view(n, k)
+
+
 def java_rows(seed: int, n: int, ops: Sequence[int], nvec: int, device=None, vec_dtype=torch.float64):
     """Rows of one generator task: (vec [n, nvec] in ``vec_dtype``, scalars [n, len(ops)-nvec] fp64)."""
     device = torch.device(device) if device is not None else torch.device("cpu")
     ops = [int(o) for o in ops]
+    if (device.type == "cuda" and nvec == 0 and ops and len(set(ops)) == 1 and ops[0] > 0
+            and ops[0] & (ops[0] - 1) != 0 and n > 0):
+        # every draw is nextInt(b) with the same non-power-of-two b: compact accepted draws
+        codes = java_uniform_int_rows(seed, n, len(ops), ops[0], device)
+        return torch.empty((n, 0), dtype=vec_dtype, device=device), codes.to(torch.float64)
     ns = len(ops) - nvec
     dpr = _draws_per_row(ops)
     x0 = scramble(seed)

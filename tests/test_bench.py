@@ -186,3 +186,20 @@ def test_bench_timed_region_only_replays(monkeypatch, steps, warmup, R):
     timed = [e for e in log[first_timed:] if e != ("barrier",)]
     assert all(e[0] == "replay" for e in timed)
     assert sum(e[1] for e in timed) == steps  # exactly `steps` rounds timed
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bound,k,n", [(1_000_000, 100, 3000), ((1 << 30) + 3, 3, 5000), (100, 10, 20000), (7, 1, 999)])
+def test_java_uniform_int_rows_gpu_matches_sequential(bound, k, n):
+    """Every draw nextInt(b) with one non-power-of-two b: the compacted parallel draws equal the
+    sequential java.util.Random rejection loop (bound 2^30+3 rejects ~half of all draws)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from flink_ml_amd.ops.datagen import java_uniform_int_rows
+
+    got = java_uniform_int_rows(77, n, k, bound, torch.device("cuda")).cpu().numpy()
+    r = JavaRandom(77)
+    ref = np.array([[r.next_int(bound) for _ in range(k)] for _ in range(n)], dtype=np.int64)
+    np.testing.assert_array_equal(got.astype(np.int64), ref)
+    _, cs = java_rows(77, n, [bound] * k, 0, device="cuda")
+    np.testing.assert_array_equal(cs.cpu().numpy(), ref.astype(np.float64))
