@@ -34,7 +34,7 @@ def test_task_seed_and_split():
 def test_dense_vector_generator_exact():
     g = DenseVectorGenerator().set_seed(2).set_col_names([["features"]]).set_num_values(50).set_vector_dim(7)
     t = g.get_data()[0]
-    np.testing.assert_array_equal(t.column("features").numpy(), _java_rows(task_seed(2, 0), 50, [0] * 7))
+    np.testing.assert_array_equal(t.column("features").cpu().numpy(), _java_rows(task_seed(2, 0), 50, [0] * 7))
     assert DenseVectorGenerator().get_seed() == java_string_hash(
         "org.apache.flink.ml.benchmark.datagenerator.common.DenseVectorGenerator")
 
@@ -44,12 +44,12 @@ def test_labeled_point_and_double_generators_exact():
         .set_vector_dim(4).set_feature_arity(20).set_label_arity(10)
     t = g.get_data()[0]
     ref = _java_rows(task_seed(5, 0), 40, [20] * 4 + [10, 0])
-    np.testing.assert_array_equal(t.column("f").numpy(), ref[:, :4])
-    np.testing.assert_array_equal(t.column("l").numpy(), ref[:, 4])
-    np.testing.assert_array_equal(t.column("w").numpy(), ref[:, 5])
+    np.testing.assert_array_equal(t.column("f").cpu().numpy(), ref[:, :4])
+    np.testing.assert_array_equal(t.column("l").cpu().numpy(), ref[:, 4])
+    np.testing.assert_array_equal(t.column("w").cpu().numpy(), ref[:, 5])
     d = DoubleGenerator().set_seed(1).set_col_names([["a", "b"]]).set_num_values(30).set_arity(3).get_data()[0]
     ref = _java_rows(task_seed(1, 0), 30, [3, 3])
-    np.testing.assert_array_equal(np.stack([d.column("a").numpy(), d.column("b").numpy()], 1), ref)
+    np.testing.assert_array_equal(np.stack([d.column("a").cpu().numpy(), d.column("b").cpu().numpy()], 1), ref)
     s = RandomStringGenerator().set_seed(9).set_col_names([["s"]]).set_num_values(20).set_num_distinct_values(7)
     ref = _java_rows(task_seed(9, 0), 20, [7])
     assert s.get_data()[0].get_list("s") == [str(int(x)) for x in ref[:, 0]]
@@ -113,7 +113,7 @@ def _spmd_bench(rank, world):
                      verbose=False)
     g = DenseVectorGenerator().set_seed(2).set_col_names([["f"]]).set_num_values(11).set_vector_dim(3)
     return res["KMeans-1"]["results"]["outputRecordNum"], res["KMeansModel-2"]["results"]["outputRecordNum"], \
-        g.get_data()[0].column("f").numpy().tolist()
+        g.get_data()[0].column("f").cpu().numpy().tolist()
 
 
 def test_runner_distributed():
