@@ -19,7 +19,9 @@ struct JRandom {
     int32_t r = next(31);
     int32_t m = bound - 1;
     if ((bound & m) == 0) return (int32_t)(((int64_t)bound * (int64_t)r) >> 31);
-    for (int32_t u = r; u - (r = u % bound) + m < 0; u = next(31)) {
+    // Java's rejection test relies on int overflow (u - r + m < 0): wrap explicitly (signed
+    // overflow is undefined in C++ and an optimiser may drop the test)
+    for (int32_t u = r; (int32_t)((uint32_t)u - (uint32_t)(r = u % bound) + (uint32_t)m) < 0; u = next(31)) {
     }
     return r;
   }

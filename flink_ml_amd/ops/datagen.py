@@ -149,11 +149,20 @@ def java_rows(seed: int, n: int, ops: Sequence[int], nvec: int, device=None, vec
     """Rows of one generator task: (vec [n, nvec] in ``vec_dtype``, scalars [n, len(ops)-nvec] fp64)."""
     device = torch.device(device) if device is not None else torch.device("cpu")
     ops = [int(o) for o in ops]
-    if (device.type == "cuda" and nvec == 0 and ops and len(set(ops)) == 1 and ops[0] > 0
-            and ops[0] & (ops[0] - 1) != 0 and n > 0):
-        # every draw is nextInt(b) with the same non-power-of-two b: compact accepted draws
-        codes = java_uniform_int_rows(seed, n, len(ops), ops[0], device)
-        return torch.empty((n, 0), dtype=vec_dtype, device=device), codes.to(torch.float64)
+    if nvec == 0 and ops and len(set(ops)) == 1 and ops[0] > 0 and ops[0] & (ops[0] - 1) != 0 and n > 0:
+        # every draw is nextInt(b) with the same non-power-of-two b: compact accepted draws on the
+        # device, or run the sequential Random on the host (native) — no per-rejection restarts
+        if device.type == "cuda":
+            codes = java_uniform_int_rows(seed, n, len(ops), ops[0], device)
+            return torch.empty((n, 0), dtype=vec_dtype, device=device), codes.to(torch.float64)
+        import ctypes
+
+        native.register_host_sigs({"fmlx_java_next_ints": [ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
+                                                           ctypes.c_void_p]})
+        out = np.empty(n * len(ops), dtype=np.int32)
+        native.host().fmlx_java_next_ints(int(seed), out.size, int(ops[0]), out.ctypes.data)
+        return (torch.empty((n, 0), dtype=vec_dtype),
+                torch.from_numpy(out.reshape(n, len(ops)).astype(np.float64)))
     ns = len(ops) - nvec
     dpr = _draws_per_row(ops)
     x0 = scramble(seed)
