@@ -11,3 +11,4 @@ __version__ = "0.1.0"
 
 from .table import SparseColumn, Table  # noqa: F401,E402
 from .linalg import DenseMatrix, DenseVector, SparseVector, Vectors  # noqa: F401,E402
+from . import lib as _lib  # noqa: F401,E402  (registers the reference module-path layout)

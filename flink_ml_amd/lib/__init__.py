@@ -5,6 +5,9 @@ so ``from flink_ml_amd.lib.classification.logisticregression import LogisticRegr
 The layout is a table, not a tree of files: a meta-path finder materialises
 ``flink_ml_amd.lib.<group>`` and ``flink_ml_amd.lib.<group>.<algo>`` on import, each exposing the
 stage classes (from ``flink_ml_amd.models``) that the reference module of the same path defines.
+The reference's other Python module paths are aliases of the modules that implement them here
+(``ALIASES``: ``core.api`` → ``api.stage``, ``core.builder`` → ``api.pipeline``, ``core.linalg``,
+``core.param``, ``core.windows``, ``lib.functions``, ``lib.param``, ``util.read_write_utils``).
 """
 from __future__ import annotations
 
@@ -73,6 +76,39 @@ LAYOUT = {
 }
 
 
+# reference module path (pyflink.ml.<path>) -> implementing module here
+ALIASES = {
+    "flink_ml_amd.core.api": "flink_ml_amd.api.stage",
+    "flink_ml_amd.core.builder": "flink_ml_amd.api.pipeline",
+    "flink_ml_amd.core.linalg": "flink_ml_amd.linalg.vectors",
+    "flink_ml_amd.core.param": "flink_ml_amd.param.param",
+    "flink_ml_amd.core.windows": "flink_ml_amd.common.window",
+    "flink_ml_amd.lib.functions": "flink_ml_amd.functions",
+    "flink_ml_amd.lib.param": "flink_ml_amd.common.param",
+    "flink_ml_amd.util.read_write_utils": "flink_ml_amd.io.read_write",
+}
+_ALIAS_PACKAGES = {"flink_ml_amd.core", "flink_ml_amd.util"}
+
+
+class _AliasLoader(importlib.abc.Loader):
+    _specs = {}
+
+    def create_module(self, spec):
+        if spec.name in ALIASES:
+            mod = importlib.import_module(ALIASES[spec.name])
+            self._specs[id(mod)] = mod.__spec__  # the import machinery overwrites __spec__
+            return mod
+        return types.ModuleType(spec.name)
+
+    def exec_module(self, module):
+        if id(module) in self._specs:
+            module.__spec__ = self._specs.pop(id(module))
+            return
+        if module.__name__ in _ALIAS_PACKAGES:
+            module.__path__ = []
+            module.__all__ = sorted(k.rsplit(".", 1)[1] for k in ALIASES if k.startswith(module.__name__ + "."))
+
+
 class _Loader(importlib.abc.Loader):
     def create_module(self, spec):
         return types.ModuleType(spec.name)
@@ -94,8 +130,12 @@ class _Loader(importlib.abc.Loader):
 
 class _Finder(importlib.abc.MetaPathFinder):
     _loader = _Loader()
+    _alias_loader = _AliasLoader()
 
     def find_spec(self, fullname, path=None, target=None):
+        if fullname in ALIASES or fullname in _ALIAS_PACKAGES:
+            return importlib.machinery.ModuleSpec(fullname, self._alias_loader,
+                                                  is_package=fullname in _ALIAS_PACKAGES)
         parts = fullname.split(".")
         if parts[:2] != ["flink_ml_amd", "lib"] or len(parts) not in (3, 4):
             return None

@@ -86,3 +86,20 @@ def test_functions():
     assert torch.equal(back, torch.tensor([[1.0, 2.0], [3.0, 4.0]], dtype=torch.float64))
     ragged = array_to_vector([[1.0], [2.0, 3.0]])
     assert ragged[1] == Vectors.dense(2.0, 3.0)
+
+
+@pytest.mark.parametrize("path,names", [
+    ("flink_ml_amd.core.api", ["Stage", "AlgoOperator", "Transformer", "Model", "Estimator"]),
+    ("flink_ml_amd.core.builder", ["Pipeline", "PipelineModel"]),
+    ("flink_ml_amd.core.linalg", ["Vectors", "DenseVector", "SparseVector", "DenseMatrix"]),
+    ("flink_ml_amd.core.windows", ["GlobalWindows", "CountTumblingWindows", "EventTimeTumblingWindows",
+                                   "ProcessingTimeTumblingWindows", "EventTimeSessionWindows",
+                                   "ProcessingTimeSessionWindows"]),
+    ("flink_ml_amd.lib.functions", ["vector_to_array", "array_to_vector"]),
+    ("flink_ml_amd.util.read_write_utils", ["save_metadata", "load_stage"]),
+])
+def test_reference_core_module_paths(path, names):
+    """pyflink.ml.core.* / lib.functions / util.read_write_utils resolve to the implementing modules."""
+    m = importlib.import_module(path)
+    for n in names:
+        assert hasattr(m, n), (path, n)
