@@ -115,13 +115,18 @@ class _Loader(importlib.abc.Loader):
 
     def exec_module(self, module):
         parts = module.__name__.split(".")[2:]  # flink_ml_amd.lib.<group>[.<algo>]
+        models = importlib.import_module("flink_ml_amd.models")
         if len(parts) == 1:
-            module.__path__ = []  # a package: its algorithm modules resolve through the finder
-            module.__all__ = sorted(LAYOUT[parts[0]])
-            module.__doc__ = "``%s`` algorithm modules." % parts[0]
+            # a package: its algorithm modules resolve through the finder, and every stage class
+            # of the group is also importable from it (``from ...lib.feature import Binarizer``)
+            module.__path__ = []
+            names = [n for m in sorted(LAYOUT[parts[0]]) for n in LAYOUT[parts[0]][m]]
+            for n in names:
+                setattr(module, n, getattr(models, n))
+            module.__all__ = sorted(LAYOUT[parts[0]]) + names
+            module.__doc__ = "``%s`` stages (reference ``pyflink.ml.lib.%s``)." % (parts[0], parts[0])
             return
         names = LAYOUT[parts[0]][parts[1]]
-        models = importlib.import_module("flink_ml_amd.models")
         for n in names:
             setattr(module, n, getattr(models, n))
         module.__all__ = list(names)
