@@ -37,7 +37,11 @@ constexpr int KM_CH = 256;  // rows per gather chunk
 // ------------------------------------------------------------------------------------------
 // MFMA assign (euclidean, bf16)
 // ------------------------------------------------------------------------------------------
-template <int KS, bool FULL, bool SCHED>
+// per-CU arrival parity of the persistent assign (see PERSIST below); grows forever, only its
+// low bit is used, so it needs no reset between launches or graph replays
+__device__ int g_km_cu_arrivals[1024];
+
+template <int KS, bool FULL, bool SCHED, bool PERSIST = false>
 // Cb / cnorm are not __restrict__ so the compiler fence after each tile prefetch keeps the
 // loads where they are issued (with restrict they get sunk next to their use, after the MFMAs).
 __global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t* __restrict__ X, long ld, long n,
@@ -54,7 +58,23 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t
   const int wave = threadIdx.x >> 6;
   const int r32 = lane & 31;
   const int h = lane >> 5;
-  const long rowbase = (long)blockIdx.x * (4 * 32 * MT) + (long)wave * 32 * MT;
+  // PERSIST: a grid of 2 blocks per CU walks the 256-row groups. Launched blocks finish together
+  // and their successors start together, so the two blocks of a CU load their X rows (the
+  // ~1 ms of a 12.5M-row pass that no MFMA hides) at the same moments; here the second block to
+  // arrive on a CU first sleeps half a group, which keeps one block computing while the other
+  // loads. Non-persistent: one group per block.
+  const long ngroups = (n + 4 * 32 * MT - 1) / (4 * 32 * MT);
+  if constexpr (PERSIST) {
+    __shared__ int s_stagger;
+    if (threadIdx.x == 0) s_stagger = atomicAdd(&g_km_cu_arrivals[__smid() & 1023], 1) & 1;
+    __syncthreads();
+    if (s_stagger) {
+      const int naps = (kpad / 32) * KS * MT * 32 / 8128 + 1;  // s_sleep 127 = 8128 cycles
+      for (int i = 0; i < naps; ++i) __builtin_amdgcn_s_sleep(127);
+    }
+  }
+  for (long grp = blockIdx.x; grp < (PERSIST ? ngroups : (long)blockIdx.x + 1); grp += gridDim.x) {
+  const long rowbase = grp * (4 * 32 * MT) + (long)wave * 32 * MT;
 
   // ---- A fragments: this wave's MT x 32 rows, whole padded K, in registers. FULL (D == 16·KS,
   // 16-B aligned rows): unconditional 16-B loads of clamped rows, all in flight together — a
@@ -245,22 +265,27 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t
 #undef KM_LD1
 #undef KM_ST1
 
-  // ---- row argmin across the 32 lanes of each half (equal keys → lower column)
+  // ---- row argmin across the 32 lanes of each half (equal keys → lower column). Per row: the
+  // minimum key of each 32-lane half by 4 DPP steps within 16-lane rows plus one swap of the
+  // 16-lane halves, then the lowest lane holding it from a ballot (the key carries the tile, the
+  // lane is the column) — ~10 instructions and one LDS-permute per row, where a butterfly of
+  // (key, index) pairs took 10 dependent ds_bpermutes
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
     int mine = 0;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      unsigned v = best[m][r];
-      int id = (int)(v & tmask) * 32 + r32;
-#pragma unroll
-      for (int off = 1; off < 32; off <<= 1) {
-        const unsigned ov = (unsigned)__shfl_xor((int)v, off, 64);
-        const int oi = __shfl_xor(id, off, 64);
-        const bool take = ov < v || (ov == v && oi < id);
-        v = take ? ov : v;
-        id = take ? oi : id;
-      }
+      const unsigned v0 = best[m][r];
+      unsigned v = v0;
+      v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));   // quad xor 1
+      v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));   // quad xor 2
+      v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+      v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));  // row_mirror
+      v = min(v, (unsigned)__shfl_xor((int)v, 16, 64));                                      // 16-lane halves
+      const unsigned long long hit = __ballot(v0 == v);
+      const unsigned lo = (unsigned)hit, hi = (unsigned)(hit >> 32);
+      const int l0 = __builtin_ctz(lo | 0x80000000u), l1 = __builtin_ctz(hi | 0x80000000u);
+      const int id = (int)(v & tmask) * 32 + (h ? l1 : l0);
       if (r32 == r) mine = id;
     }
     if (r32 < 16) {
@@ -268,6 +293,7 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t
       if (row < n) labels[row] = mine;
     }
   }
+  }  // row groups
 }
 
 // ------------------------------------------------------------------------------------------
@@ -642,6 +668,7 @@ __global__ __launch_bounds__(256) void kmeans_finalize_kernel(const A* __restric
 // 4.07 ms vs 3.95-4.00 ms for the plain loop at 12.5M x 128, k=1024 (and within 3 % either way
 // at D=64, k=64/256) — the second resident wave per SIMD already fills the epilogue gaps.
 int g_km_sched = 0;
+int g_km_persist = 0;  // persistent, CU-staggered assign (fmlx_kmeans_set_sched(2))
 
 template <int KS>
 int launch_assign_bf16(const void* X, long ld, long n, int D, const void* Cb, const float* cnorm, int kpad, int* labels,
@@ -651,7 +678,18 @@ int launch_assign_bf16(const void* X, long ld, long n, int D, const void* Cb, co
   const int blocks = (int)((n + rows_per_block - 1) / rows_per_block);
   if (blocks == 0) return 0;
   const bool full = D == 16 * KS && (ld % 8) == 0 && ((uintptr_t)X % 16) == 0;
-  if (full && g_km_sched)
+  if (full && g_km_persist) {
+    static int cus = 0;
+    if (cus == 0) {
+      int dev = 0;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (cus <= 0) cus = 256;
+    }
+    const int grid = blocks < 2 * cus ? blocks : 2 * cus;
+    hipLaunchKernelGGL((kmeans_assign_bf16_kernel<KS, true, false, true>), dim3(grid), dim3(256), 0, s,
+                       (const bf16_t*)X, ld, n, D, (const bf16_t*)Cb, cnorm, kpad, labels);
+  } else if (full && g_km_sched)
     hipLaunchKernelGGL((kmeans_assign_bf16_kernel<KS, true, true>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)X, ld,
                        n, D, (const bf16_t*)Cb, cnorm, kpad, labels);
   else if (full)
@@ -686,8 +724,10 @@ int chunk_sum_vpl(const void* X, long ld, int D, const long* order, const long* 
 }  // namespace
 
 // KS = padded K-steps of 16 (one of 1..8,10,12,16; >= ceil(D/16)); Cb is [kpad][16*KS] zero-padded
-FMLX_API int fmlx_kmeans_set_sched(int on) {
-  g_km_sched = on;
+// 0: plain loop, 1: interleaved MFMA/epilogue schedule, 2: persistent CU-staggered grid
+FMLX_API int fmlx_kmeans_set_sched(int mode) {
+  g_km_sched = mode == 1;
+  g_km_persist = mode == 2;
   return 0;
 }
 

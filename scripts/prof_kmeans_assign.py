@@ -29,7 +29,11 @@ def main():
     cb = kk.CentroidBuffers(a.k, a.d, X.device, torch.float32)
     cb.set(C)
     out = torch.empty(a.n, dtype=torch.int32, device="cuda")
+    native.call("fmlx_kmeans_set_sched", 0)
+    ref = kk.assign(X, cb, "euclidean").clone()
+    native.call("fmlx_kmeans_set_sched", a.sched)
     kk.assign(X, cb, "euclidean", out)
+    same = bool(torch.equal(out, ref))
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -38,7 +42,8 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.reps
-    print("sched=%d n=%d d=%d k=%d ms=%.3f tflops=%.1f" % (a.sched, a.n, a.d, a.k, ms, 2.0 * a.n * a.k * a.d / ms / 1e9), flush=True)
+    print("sched=%d n=%d d=%d k=%d ms=%.3f tflops=%.1f labels_match_plain=%s"
+          % (a.sched, a.n, a.d, a.k, ms, 2.0 * a.n * a.k * a.d / ms / 1e9, same), flush=True)
 
 
 if __name__ == "__main__":
