@@ -144,8 +144,15 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t
       }
     p += __shfl_xor(p, 32, 64);  // both K-halves of row r32
     p *= 1.0f + 0x1p-10f;
+    // register r of half h holds row (r&3) + 8(r>>2) + 4h: two wave-uniform readlanes + a select
+    // per register (was one ds_bpermute each)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) xnb[m][r] = __shfl(p, (r & 3) + 8 * (r >> 2) + 4 * h, 64);
+    for (int r = 0; r < 16; ++r) {
+      const int src = (r & 3) + 8 * (r >> 2);
+      const float a0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), src));
+      const float a1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), src + 4));
+      xnb[m][r] = h ? a1 : a0;
+    }
   }
 
   // Running argmin as one u32 key per accumulator register: the positive distance's bits with the
