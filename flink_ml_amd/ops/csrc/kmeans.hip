@@ -37,11 +37,7 @@ constexpr int KM_CH = 256;  // rows per gather chunk
 // ------------------------------------------------------------------------------------------
 // MFMA assign (euclidean, bf16)
 // ------------------------------------------------------------------------------------------
-// per-CU arrival parity of the persistent assign (see PERSIST below); grows forever, only its
-// low bit is used, so it needs no reset between launches or graph replays
-__device__ int g_km_cu_arrivals[1024];
-
-template <int KS, bool FULL, bool SCHED, bool PERSIST = false>
+template <int KS, bool FULL, bool SCHED, bool XLDS = false>
 // Cb / cnorm are not __restrict__ so the compiler fence after each tile prefetch keeps the
 // loads where they are issued (with restrict they get sunk next to their use, after the MFMAs).
 __global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t* __restrict__ X, long ld, long n,
@@ -52,35 +48,52 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t
   constexpr int ROWB = DP * 2 + 16;       // padded LDS row stride (bytes): conflict-free b128 reads
   constexpr int CHUNKS = 32 * DP / 8;     // 16-byte chunks per 32-centroid tile
   constexpr int CPT = (CHUNKS + 255) / 256;
-  __shared__ __align__(16) unsigned char lds[2 * 32 * ROWB];
+  // XLDS: the block's rows are first copied into LDS by LDS-DMA (1 KiB contiguous per
+  // wave-instruction; the register path reads 32 rows x 32 B per instruction) and the A
+  // fragments are read from there; the same LDS then holds the centroid tiles
+  constexpr int XBYTES = 4 * 32 * MT * DP * 2;
+  constexpr int LDSB = XLDS && XBYTES > 2 * 32 * ROWB ? XBYTES : 2 * 32 * ROWB;
+  __shared__ __align__(16) unsigned char lds[LDSB];
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int r32 = lane & 31;
   const int h = lane >> 5;
-  // PERSIST: a grid of 2 blocks per CU walks the 256-row groups. Launched blocks finish together
-  // and their successors start together, so the two blocks of a CU load their X rows (the
-  // ~1 ms of a 12.5M-row pass that no MFMA hides) at the same moments; here the second block to
-  // arrive on a CU first sleeps half a group, which keeps one block computing while the other
-  // loads. Non-persistent: one group per block.
   const long ngroups = (n + 4 * 32 * MT - 1) / (4 * 32 * MT);
-  if constexpr (PERSIST) {
-    __shared__ int s_stagger;
-    if (threadIdx.x == 0) s_stagger = atomicAdd(&g_km_cu_arrivals[__smid() & 1023], 1) & 1;
-    __syncthreads();
-    if (s_stagger) {
-      const int naps = (kpad / 32) * KS * MT * 32 / 8128 + 1;  // s_sleep 127 = 8128 cycles
-      for (int i = 0; i < naps; ++i) __builtin_amdgcn_s_sleep(127);
-    }
-  }
-  for (long grp = blockIdx.x; grp < (PERSIST ? ngroups : (long)blockIdx.x + 1); grp += gridDim.x) {
+  for (long grp = blockIdx.x; grp < (long)blockIdx.x + 1 && grp < ngroups; grp += gridDim.x) {
   const long rowbase = grp * (4 * 32 * MT) + (long)wave * 32 * MT;
 
   // ---- A fragments: this wave's MT x 32 rows, whole padded K, in registers. FULL (D == 16·KS,
   // 16-B aligned rows): unconditional 16-B loads of clamped rows, all in flight together — a
   // per-fragment branch would make every load wait for the previous one (16 round trips).
   bf16x8_t a[MT][KS];
-  if constexpr (FULL) {
+  if constexpr (XLDS) {
+    static_assert(FULL && (KS & (KS - 1)) == 0, "LDS-staged rows need whole power-of-two rows");
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    typedef __attribute__((address_space(1))) void* glb_ptr_t;
+    constexpr int XROWB = DP * 2;   // bytes per row in LDS
+    constexpr int NS = 2 * KS;      // 16-B slots per row; slot s' of row r holds chunk s' ^ (r mod NS)
+    constexpr int PIECES = XBYTES / 1024;
+    const long grow0 = grp * (4 * 32 * MT);
+    for (int p = wave; p < PIECES; p += 4) {
+      const int off = p * 1024 + lane * 16;
+      const int lrow = off / XROWB, slot = (off % XROWB) / 16;
+      long grow = grow0 + lrow;
+      grow = grow < n ? grow : n - 1;
+      __builtin_amdgcn_global_load_lds((glb_ptr_t)(X + grow * ld + (slot ^ (lrow & (NS - 1))) * 8),
+                                       (lds_ptr_t)(lds + p * 1024), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int lrow = wave * 32 * MT + m * 32 + r32;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        a[m][s] = *reinterpret_cast<const bf16x8_t*>(lds + lrow * XROWB + (((2 * s + h) ^ (lrow & (NS - 1))) * 16));
+    }
+    __syncthreads();  // every wave has its fragments before the centroid tiles reuse the LDS
+  } else if constexpr (FULL) {
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       const long row = rowbase + m * 32 + r32;
@@ -675,7 +688,9 @@ __global__ __launch_bounds__(256) void kmeans_finalize_kernel(const A* __restric
 // 4.07 ms vs 3.95-4.00 ms for the plain loop at 12.5M x 128, k=1024 (and within 3 % either way
 // at D=64, k=64/256) — the second resident wave per SIMD already fills the epilogue gaps.
 int g_km_sched = 0;
-int g_km_persist = 0;  // persistent, CU-staggered assign (fmlx_kmeans_set_sched(2))
+// rows staged through LDS by LDS-DMA (fmlx_kmeans_set_sched(2)): within noise of the register
+// path (3.71-3.74 vs 3.74-3.75 ms at 12.5M x 128, k=1024; 0.87 vs 0.91 ms at k=32), kept off
+int g_km_xlds = 0;
 
 template <int KS>
 int launch_assign_bf16(const void* X, long ld, long n, int D, const void* Cb, const float* cnorm, int kpad, int* labels,
@@ -685,18 +700,14 @@ int launch_assign_bf16(const void* X, long ld, long n, int D, const void* Cb, co
   const int blocks = (int)((n + rows_per_block - 1) / rows_per_block);
   if (blocks == 0) return 0;
   const bool full = D == 16 * KS && (ld % 8) == 0 && ((uintptr_t)X % 16) == 0;
-  if (full && g_km_persist) {
-    static int cus = 0;
-    if (cus == 0) {
-      int dev = 0;
-      hipGetDevice(&dev);
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      if (cus <= 0) cus = 256;
+  if constexpr ((KS & (KS - 1)) == 0 && KS <= 8) {
+    if (full && g_km_xlds) {
+      hipLaunchKernelGGL((kmeans_assign_bf16_kernel<KS, true, false, true>), dim3(blocks), dim3(256), 0, s,
+                         (const bf16_t*)X, ld, n, D, (const bf16_t*)Cb, cnorm, kpad, labels);
+      return (int)hipGetLastError();
     }
-    const int grid = blocks < 2 * cus ? blocks : 2 * cus;
-    hipLaunchKernelGGL((kmeans_assign_bf16_kernel<KS, true, false, true>), dim3(grid), dim3(256), 0, s,
-                       (const bf16_t*)X, ld, n, D, (const bf16_t*)Cb, cnorm, kpad, labels);
-  } else if (full && g_km_sched)
+  }
+  if (full && g_km_sched)
     hipLaunchKernelGGL((kmeans_assign_bf16_kernel<KS, true, true>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)X, ld,
                        n, D, (const bf16_t*)Cb, cnorm, kpad, labels);
   else if (full)
@@ -731,10 +742,10 @@ int chunk_sum_vpl(const void* X, long ld, int D, const long* order, const long* 
 }  // namespace
 
 // KS = padded K-steps of 16 (one of 1..8,10,12,16; >= ceil(D/16)); Cb is [kpad][16*KS] zero-padded
-// 0: plain loop, 1: interleaved MFMA/epilogue schedule, 2: persistent CU-staggered grid
+// 0: plain loop, 1: interleaved MFMA/epilogue schedule, 2: rows staged through LDS (LDS-DMA)
 FMLX_API int fmlx_kmeans_set_sched(int mode) {
   g_km_sched = mode == 1;
-  g_km_persist = mode == 2;
+  g_km_xlds = mode == 2;
   return 0;
 }
 
