@@ -39,8 +39,7 @@ def timed_region(tr, ctx, warmup: int, steps: int):
     Returns (host wall seconds, device seconds measured by events around the same region).
     """
     tr.precapture(steps)
-    for r in tr.graph_sizes(steps):
-        tr.graphs[r].replay()
+    tr.prime(steps)
     tr.run_rounds(warmup)
     torch.cuda.synchronize()
     ctx.barrier()
@@ -107,7 +106,7 @@ def main():
         sgd = SGD(max_iter=1, learning_rate=0.1, global_batch_size=args.batch * world, tol=1e-6)
         tr = DeviceGlmTrainer(sgd, np.zeros(args.dim), X, y, None, "logistic", use_graph=not args.no_graph)
         tr.rounds_per_graph = args.graph_rounds
-        sgd.max_iter = args.warmup + sum(tr.graph_sizes(args.steps)) + args.steps + 1  # read at capture
+        sgd.max_iter = args.warmup + tr.priming_rounds(args.steps) + args.steps + 1  # read at capture
         if args.torch_profile:
             sgd.max_iter += PROFILE_ROUNDS
         return tr

@@ -225,7 +225,16 @@ class DeviceGlmTrainer:
         if self.distributed and self.mode == gk.TAIL_FEEDBACK and ctx.backend != "nccl":
             use_graph = False  # a gloo all-reduce of device tensors cannot be captured
         self.use_graph = use_graph
+        # 1 GPU, fused dense round with the atomic tail: launch e completes round e − 1 in its
+        # prologue (no ticket / serial tail); launches alternate between two round-number words
+        # (``parity``), so hipGraphs are keyed by (rounds, starting parity)
+        self.defer = (self.mode == gk.TAIL_UPDATE and self.scratch is not None and not self.scratch.det
+                      and gk.defer_supported(self.d, acc))
+        self.parity = 0
+        self.cw = torch.zeros((2, self.d), dtype=acc, device=dev) if self.defer else None
+        self._flushed = False
         self.graphs = {}
+        self.timing = False
         self.check_every = max(1, int(check_every))
         self.rounds_per_graph = self.check_every
 
@@ -285,31 +294,55 @@ class DeviceGlmTrainer:
             return
         # every rank launches the round, also one without rows: it still joins the reduction tail
         gk.glm_round(self.X, self.y, self.w, self.coef, self.B, self.loss, self.state, self.scratch, self.mode,
-                     self.feedback, s.max_iter, s.tol, s.learning_rate, s.reg, s.elastic_net, xg=self.xg, rounds=rounds)
+                     self.feedback, s.max_iter, s.tol, s.learning_rate, s.reg, s.elastic_net, xg=self.xg, rounds=rounds,
+                     defer=self.defer, parity=self.parity, cw=self.cw)
+        if self.defer:
+            self.parity = (self.parity + rounds) & 1
         if self.mode == gk.TAIL_FEEDBACK:
             comm.all_reduce_sum(self.feedback)
             gk.update(self.feedback, self.d, self.coef, self.state, s.max_iter, s.tol, s.learning_rate, s.reg,
                       s.elastic_net)
 
-    def _capture(self, rounds: int):
+    def _graph_key(self, rounds: int, parity=None):
+        if not self.defer:
+            return rounds
+        return (rounds, self.parity if parity is None else parity)
+
+    def _capture(self, key):
         """Captures ``rounds`` consecutive SGD rounds into one hipGraph (state lives on device, so
-        the same launch sequence repeats); replaying it costs one host submission per ``rounds``."""
+        the same launch sequence repeats); replaying it costs one host submission per ``rounds``.
+        Deferred mode: ``key`` = (rounds, starting parity)."""
+        rounds, parity = key if self.defer else (key, None)
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         # everything a round mutates that the next round reads (the sparse path's Σw/Σloss
-        # parity slots included) is rewound after the warm-up
+        # parity slots, the deferred mode's accumulator ring and coefficient ring included) is
+        # rewound after the warm-up
         live = [self.state, self.coef] + ([self.wl] if self.csc is not None else [])
+        if self.defer:
+            live += [self.scratch.acc, self.cw]
         snapshot = [t.clone() for t in live]
+        saved_parity = self.parity
         with torch.cuda.stream(side):
             self._launch_round()  # warm-up outside capture (allocator / RCCL lazy init)
         torch.cuda.current_stream(self.device).wait_stream(side)
         for t, v in zip(live, snapshot):
             t.copy_(v)
         g = torch.cuda.CUDAGraph()
+        if self.defer:
+            self.parity = parity
         with torch.cuda.graph(g):
             self._launch_round(rounds)
-        self.graphs[rounds] = g
+        self.parity = saved_parity
+        self.graphs[key] = g
         return g
+
+    def _replay(self, rounds: int) -> None:
+        key = self._graph_key(rounds)
+        g = self.graphs.get(key) or self._capture(key)
+        g.replay()
+        if self.defer:
+            self.parity = (self.parity + rounds) & 1
 
     def graph_sizes(self, k: int):
         """Round counts of the hipGraphs ``run_rounds(k)`` replays (R-round graphs, then the
@@ -319,12 +352,38 @@ class DeviceGlmTrainer:
         full, rem = divmod(k, self.rounds_per_graph)
         return ([self.rounds_per_graph] if full else []) + ([1] if rem else [])
 
+    def graph_keys(self, k: int):
+        """Keys of every hipGraph ``run_rounds(k)`` may replay, whatever the starting parity."""
+        sizes = self.graph_sizes(k)
+        return [(r, p) for r in sizes for p in (0, 1)] if self.defer else sizes
+
+    def priming_rounds(self, k: int) -> int:
+        """Upper bound of the rounds ``prime(k)`` runs."""
+        keys = self.graph_keys(k)
+        return sum(kk[0] + 1 for kk in keys) if self.defer else sum(keys)
+
     def precapture(self, k: int) -> None:
         """Captures (and instantiates) every hipGraph that ``run_rounds(k)`` will replay, so a
         timed ``run_rounds(k)`` afterwards only replays (capture costs ~1 ms per graph)."""
-        for r in self.graph_sizes(k):
-            if r not in self.graphs:
-                self._capture(r)
+        for key in self.graph_keys(k):
+            if key not in self.graphs:
+                self._capture(key)
+
+    def prime(self, k: int) -> int:
+        """Replays every graph of ``graph_keys(k)`` once (first-replay upload costs), each at its
+        own starting parity (a direct 1-round launch switches parity). Returns rounds run."""
+        done = 0
+        for key in self.graph_keys(k):
+            if self.defer and key[1] != self.parity:
+                self._launch_round(1)
+                done += 1
+            g = self.graphs.get(key) or self._capture(key)
+            g.replay()
+            r = key[0] if self.defer else key
+            if self.defer:
+                self.parity = (self.parity + r) & 1
+            done += r
+        return done
 
     def run_rounds(self, k: int) -> None:
         """Runs ``k`` SGD rounds (each predicated on the device running flag), no host sync."""
@@ -335,14 +394,17 @@ class DeviceGlmTrainer:
             return
         R = self.rounds_per_graph
         full, rem = divmod(k, R)
-        if full:
-            g = self.graphs.get(R) or self._capture(R)
-            for _ in range(full):
-                g.replay()
-        if rem:
-            g1 = self.graphs.get(1) or self._capture(1)
-            for _ in range(rem):
-                g1.replay()
+        for _ in range(full):
+            self._replay(R)
+        for _ in range(rem):
+            self._replay(1)
+
+    def flush(self) -> None:
+        """Deferred mode: the last round's update is applied by the NEXT launch; one more launch
+        (a no-op round once the iteration stopped) completes it."""
+        if self.defer and not self._flushed:
+            self._launch_round(1)
+            self._flushed = True
 
     def step(self) -> None:
         """Runs one SGD round (predicated on the device running flag)."""
@@ -350,6 +412,8 @@ class DeviceGlmTrainer:
 
     def running(self) -> bool:
         st = self.state.cpu()
+        if self.defer:
+            return not bool(st[6])
         e = int(st[0])
         return bool(st[1 + (e & 1)])
 
@@ -365,6 +429,10 @@ class DeviceGlmTrainer:
         ck = AlgorithmCheckpoint("sgd")
         done = 0
         restored = ck.restore()
+        if self.defer and (ck.mgr is not None or tracing.rounds_enabled()):
+            # checkpoints and per-round logs read the round's own coefficients / feedback
+            self.defer, self.cw = False, None
+            self.graphs.clear()
         if restored is not None:
             done, st = restored
             self.coef.copy_(st["coef"].to(self.coef.dtype))
@@ -398,5 +466,6 @@ class DeviceGlmTrainer:
                                              "done": stop or done >= self.sgd.max_iter})
                 if stop:
                     break
+            self.flush()
         self.check_exchange()
         return self.coef.to(torch.float64).cpu().numpy()

@@ -37,7 +37,7 @@
 namespace {
 
 enum { LOSS_LOGISTIC = 0, LOSS_HINGE = 1, LOSS_LSQ = 2, LOSS_FTRL = 3 };
-enum { ST_ROUND = 0, ST_RUN0 = 1, ST_ARRIVE = 3, ST_EXECUTED = 4 };
+enum { ST_ROUND = 0, ST_RUN0 = 1, ST_ARRIVE = 3, ST_EXECUTED = 4, ST_ROUND_ALT = 5, ST_DONE = 6 };
 enum { TAIL_PARTIALS = 0, TAIL_FEEDBACK = 1, TAIL_UPDATE = 2, TAIL_XGMI = 3 };
 constexpr int TAIL_GROUP = 32;  // block partials summed per group finisher
 constexpr int TAIL_MAXG = 16;   // groups of the deterministic tail (=> at most 512 blocks)
@@ -138,6 +138,12 @@ struct GlmTail {
   int acc_reps;    // atomic tail: replicas of `acc` (block b adds into replica b mod acc_reps)
   long acc_ld;     // elements between replicas (d + 2 rounded up to whole 256-B lines)
   int ticket2;     // atomic tail: two-level arrival tickets (per-residue groups, then a top one)
+  int defer;       // deferred completion (TAIL_UPDATE, atomic flat tail): see defer_prologue
+  int parity;      // deferred: this launch reads its round number from state[parity ? ALT : ROUND]
+  void* cw;        // deferred: [2][d] coefficients of the last two rounds
+  int wl_off;      // deferred: byte offset of the block's [d] coefficient image in LDS
+  long long* trace;  // diagnostics (null = off): per block {start, rows done, end, hw id} in
+                     // 100 MHz s_memrealtime ticks (scripts/trace_glm_blocks.py)
 };
 constexpr int ACC_MAX_REPS = 8;
 
@@ -343,6 +349,80 @@ __device__ void glm_round_tail_atomic(const GlmTail& tl, int d, A* coef, int* st
   glm_round_finish<A>(tl, sbuf, d, coef, state, e, one_pass, wa, wb);
 }
 
+// Deferred round completion (1 GPU, TAIL_UPDATE with the atomic tail). Launch e first completes
+// round e − 1: every block sums the replicas of that round's accumulator slot (fixed order, as
+// the ticketed tail does), evaluates TerminateOnMaxIterOrTol and applies the SGD update into an
+// LDS image of w_e; then it computes round e's gradient with w_e and adds it into slot e % 3 with
+// no-return atomics — no arrival ticket and no serial last-block tail remain on the critical
+// path. Ring of 3 slots: launch e reads slot (e − 1) % 3, adds into e % 3, zeroes (e + 1) % 3
+// (read by launch e − 1, added into by launch e + 1; kernel boundaries order all three). Block 0
+// publishes w_e (cw[e & 1] for launch e + 1, coef for the host) and the round counter into the
+// state word the NEXT launch reads (launches alternate between two words, so no block of this
+// launch can observe the update). Returns true (for every thread) when the iteration ended.
+template <typename A>
+__device__ bool defer_prologue(const GlmTail& tl, A* coef, int* state, int e, int d, A* wl) {
+  const int nt = blockDim.x, tid = threadIdx.x;
+  const int R = tl.acc_reps > 1 ? tl.acc_reps : 1;
+  const long ald = tl.acc_ld;
+  const long slot = (long)ACC_MAX_REPS * ald;
+  A* ring = (A*)tl.acc;
+  A* cw = (A*)tl.cw;
+  A* fb = (A*)tl.feedback;
+  const bool lead = blockIdx.x == 0;
+  bool stop = false;
+  if (e == 0) {
+    for (long c = tid; c < d; c += nt) wl[c] = coef[c];
+  } else {
+    const A* prev = ring + (long)((e + 2) % 3) * slot;
+    A vw[ACC_MAX_REPS], vl[ACC_MAX_REPS];
+#pragma unroll
+    for (int q = 0; q < ACC_MAX_REPS; ++q) {
+      vw[q] = q < R ? ld_agent(prev + q * ald + d) : (A)0;
+      vl[q] = q < R ? ld_agent(prev + q * ald + d + 1) : (A)0;
+    }
+    A W = (A)0, L = (A)0;
+#pragma unroll
+    for (int q = 0; q < ACC_MAX_REPS; ++q) {
+      W += vw[q];
+      L += vl[q];
+    }
+    stop = !(e < tl.max_iter && L / W > (A)tl.tol);
+    const A lr = (A)tl.lr, reg = (A)tl.reg, en = (A)tl.en;
+    const A* wp = cw + (long)((e - 1) & 1) * d;
+    for (long c = tid; c < d; c += nt) {
+      A v[ACC_MAX_REPS];
+#pragma unroll
+      for (int q = 0; q < ACC_MAX_REPS; ++q) v[q] = q < R ? ld_agent(prev + q * ald + c) : (A)0;
+      const A w0 = wp[c];
+      A g = (A)0;
+#pragma unroll
+      for (int q = 0; q < ACC_MAX_REPS; ++q) g += v[q];
+      wl[c] = sgd_apply<A>(w0, g, W, lr, reg, en);
+      if (lead && fb) fb[c] = g;
+    }
+    if (lead && fb && tid == 0) {
+      fb[d] = W;
+      fb[d + 1] = L;
+    }
+  }
+  A* nxt = ring + (long)((e + 1) % 3) * slot;
+  for (long i = (long)blockIdx.x * nt + tid; i < slot; i += (long)gridDim.x * nt) nxt[i] = (A)0;
+  __syncthreads();
+  if (lead) {
+    A* wc = cw + (long)(e & 1) * d;
+    for (long c = tid; c < d; c += nt) {
+      wc[c] = wl[c];
+      coef[c] = wl[c];  // launch 0: the value every block just read
+    }
+    if (tid == 0) {
+      state[tl.parity ? ST_ROUND : ST_ROUND_ALT] = e + 1;
+      if (e > 0) state[ST_EXECUTED] += 1;
+      if (stop) state[ST_DONE] = 1;
+    }
+  }
+  return stop;
+}
+
 // ------------------------------------------------------------------------------------------
 // K4/K5/K6 — fused minibatch loss + gradient partials
 // ------------------------------------------------------------------------------------------
@@ -372,8 +452,12 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
     const typename AccOf<T>::type* wt, typename AccOf<T>::type* coef,
     long n, int d, long B, int loss, int* state, typename AccOf<T>::type* partials, GlmTail tl) {
   typedef typename AccOf<T>::type A;
+  const long long t_start = tl.trace ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
   int e;
-  if (!round_running(state, e)) return;
+  if (tl.defer) {
+    if (state[ST_DONE]) return;
+    e = state[tl.parity ? ST_ROUND_ALT : ST_ROUND];
+  } else if (!round_running(state, e)) return;
   long start = 0, end = 0;  // a rank with no rows (or a zero local batch) still joins the tail
   if (n > 0 && B > 0) {
     // batches per pass: precomputed by the launcher (a 64-bit division per wave otherwise)
@@ -405,7 +489,24 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
     for (int i = 0; i < EP; ++i) acc2[k][i] = f2_t{0.f, 0.f};
   }
   // coefficient slices (L2-hot), fetched after the first row loads are on their way
+  extern __shared__ __align__(16) unsigned char smem_w[];
+  A* wdef = reinterpret_cast<A*>(smem_w + tl.wl_off);  // deferred mode: w_e, built by the prologue
   auto load_w = [&]() {
+    if (tl.defer) {
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const int c = lane + 64 * k;
+        if constexpr (kPacked) {
+#pragma unroll
+          for (int i = 0; i < EP; ++i)
+            w2[k][i] = c < nch ? f2_t{(float)wdef[c * EPC + 2 * i], (float)wdef[c * EPC + 2 * i + 1]} : f2_t{0.f, 0.f};
+        } else {
+#pragma unroll
+          for (int i = 0; i < EPC; ++i) w[k][i] = c < nch ? wdef[c * EPC + i] : (A)0;
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
       const int c = lane + 64 * k;
@@ -666,6 +767,10 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
   if (r < end) {
     load_labels(0);  // first: load_rows reads the labels right after issuing its row loads
     load_rows(r, 0, r, xa, ya, wa, va);
+  }
+  // deferred mode: complete the previous round while the first rows are in flight
+  if (tl.defer && defer_prologue<A>(tl, coef, state, e, d, wdef)) return;
+  if (r < end) {
     load_w();
     while (true) {
       load_rows(r + step, j + U, r, xb, yb, wb, vb);
@@ -690,6 +795,21 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
   }
   }  // classic row-at-a-time path
 
+  if (tl.trace) {
+    // every wave's rows are in: stamp once the whole block got here (the LDS reduction below
+    // has its own barrier)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      long long* tr = tl.trace + (long)blockIdx.x * 4;
+      tr[0] = t_start;
+      tr[1] = (long long)__builtin_amdgcn_s_memrealtime();
+      unsigned hw;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      unsigned xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      tr[3] = ((long long)xcc << 32) | hw;
+    }
+  }
   if constexpr (kPacked) {
 #pragma unroll
     for (int k = 0; k < CPL; ++k)
@@ -721,7 +841,8 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
     __syncthreads();
     // replica b mod acc_reps: at most ceil(nb / reps) adders per address (float atomics keep
     // their full rate up to ~32 adders per address; 256 on one 4 KB row serialise)
-    A* gacc = (A*)tl.acc + (long)(blockIdx.x % (tl.acc_reps > 1 ? tl.acc_reps : 1)) * tl.acc_ld;
+    A* gacc = (A*)tl.acc + (long)(blockIdx.x % (tl.acc_reps > 1 ? tl.acc_reps : 1)) * tl.acc_ld +
+              (tl.defer ? (long)(e % 3) * ACC_MAX_REPS * tl.acc_ld : 0L);
     const long stride = d + 2;
     for (long c = threadIdx.x; c < stride; c += blockDim.x) {
       A v = (A)0;
@@ -734,6 +855,12 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
       }
       atomicAdd(gacc + c, v);
     }
+    if (tl.trace) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) tl.trace[(long)blockIdx.x * 4 + 2] = (long long)__builtin_amdgcn_s_memrealtime();
+    }
+    if (tl.defer) return;  // launch e + 1 completes this round
     glm_round_tail_atomic<A>(tl, d, coef, state, e, buf, sflag);
     return;
   }
@@ -1227,8 +1354,9 @@ constexpr int WPB = 8;
 // Non-temporal row loads (`flags & 1`) for batches streamed once per pass (−12 %, measured).
 static long g_lds_pad = -1;
 static int g_nt = -1;
-static int g_acc_reps = 8;  // atomic-tail accumulator replicas (A/B knob, <= ACC_MAX_REPS)
+static int g_acc_reps = 4;  // atomic-tail accumulator replicas (A/B knob, <= ACC_MAX_REPS)
 static int g_ticket2 = 0;   // two-level tickets (A/B knob)
+static long long* g_trace = nullptr;  // per-block timestamps of the next launches (diagnostics)
 constexpr long LDS_PER_CU = 160 * 1024;
 constexpr int NUM_CU = 256;
 
@@ -1241,6 +1369,12 @@ int launch_grad_u(const void* X, long ld, const void* y, const void* wt, void* c
   t2.nbatch = (n > 0 && B > 0) ? (int)((n + B - 1) / B) : 0;
   t2.flat_lds = tl.mode != TAIL_PARTIALS && !tl.det && (size_t)WPB * d * sizeof(A) <= 64 * 1024;
   size_t shmem = (size_t)(t2.flat_lds ? WPB : WPB / 2) * d * sizeof(A) + WPB * 2 * sizeof(A) + 16;
+  if (t2.defer) {
+    // the deferred prologue needs the flat atomic tail and the row-at-a-time loop
+    if (!t2.flat_lds || G > 0 || tl.mode != TAIL_UPDATE || tl.det || tl.cw == nullptr) return -7;
+    t2.wl_off = (int)((shmem + 15) & ~(size_t)15);
+    shmem = (size_t)t2.wl_off + (size_t)d * sizeof(A);
+  }
   if (g_lds_pad >= 0) {
     shmem += (size_t)g_lds_pad;
   } else {
@@ -1359,6 +1493,9 @@ FMLX_API int fmlx_glm_set_tuning(long lds_pad, int nt) {
   return 0;
 }
 
+// diagnostics: launches record per-block timestamps into trace[nblocks][4] (null: off)
+FMLX_API void fmlx_glm_set_trace(void* trace) { g_trace = (long long*)trace; }
+
 FMLX_API int fmlx_glm_set_tail_tuning(int acc_reps, int ticket2) {
   if (acc_reps < 1 || acc_reps > ACC_MAX_REPS) return -1;
   g_acc_reps = acc_reps;
@@ -1366,8 +1503,9 @@ FMLX_API int fmlx_glm_set_tail_tuning(int acc_reps, int ticket2) {
   return 0;
 }
 
-// elements of the atomic-tail accumulator for row width d + 2 (all replicas)
-FMLX_API long fmlx_glm_acc_elems(int d) { return (long)ACC_MAX_REPS * (((long)d + 2 + 63) / 64 * 64); }
+// elements of the atomic-tail accumulator for row width d + 2: the deferred mode's ring of 3
+// slots of ACC_MAX_REPS replicas (the ticketed tail uses slot 0)
+FMLX_API long fmlx_glm_acc_elems(int d) { return 3L * ACC_MAX_REPS * (((long)d + 2 + 63) / 64 * 64); }
 
 FMLX_API int fmlx_glm_grad_partials(int dtype, int epc, int cpl, int u, const void* X, long ld, const void* y,
                                     const void* wt, const void* coef, long n, int d, long B, int loss, const int* state,
@@ -1386,7 +1524,8 @@ FMLX_API int fmlx_glm_round(int dtype, int epc, int cpl, int u, const void* X, l
                             int mode, int det, int* cnt, void* acc, void* stage1, void* feedback, int max_iter,
                             double tol, double lr,
                             double reg, double en, void* const* peers, int world, int rank, int* gen, int* err,
-                            long spin_limit, int flags, int rounds, void* stream) {
+                            long spin_limit, int flags, int rounds, int defer, int parity, void* cw,
+                            void* stream) {
   if (mode != TAIL_PARTIALS && cnt == nullptr) return -4;
   if (mode != TAIL_PARTIALS && det && (nblocks > TAIL_GROUP * TAIL_MAXG || stage1 == nullptr)) return -4;
   if (mode != TAIL_PARTIALS && !det && (nblocks > TAIL_GROUP * TAIL_TOP || acc == nullptr)) return -4;
@@ -1408,9 +1547,13 @@ FMLX_API int fmlx_glm_round(int dtype, int epc, int cpl, int u, const void* X, l
   tl.reg = reg;
   tl.en = en;
   tl.x = xgmi::Ctx{peers, world, rank, gen, err, spin_limit};
+  tl.defer = defer;
+  tl.cw = cw;
+  tl.trace = g_trace;
   // `rounds` consecutive rounds, one launch each (a kernel boundary, ~1.5 µs, is cheaper than an
   // in-kernel grid-wide round barrier: measured, scripts/stream_probe2.hip)
   for (int i = 0; i < (rounds > 0 ? rounds : 1); ++i) {
+    tl.parity = (parity + i) & 1;  // deferred mode: launches alternate their round-number word
     const int rc = launch_round(dtype, epc, cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl,
                                 flags, (hipStream_t)stream);
     if (rc) return rc;

@@ -34,10 +34,16 @@ def set_tuning(lds_pad: int = -1, nt: int = -1) -> None:
     native.call("fmlx_glm_set_tuning", int(lds_pad), int(nt))
 
 
-def set_tail_tuning(acc_reps: int = 8, ticket2: bool = False) -> None:
+def set_tail_tuning(acc_reps: int = 4, ticket2: bool = False) -> None:
     """A/B knobs of the atomic round tail: accumulator replicas (block b adds into replica
     b mod reps) and two-level arrival tickets."""
     native.call("fmlx_glm_set_tail_tuning", int(acc_reps), int(bool(ticket2)))
+
+
+def set_trace(buf: Optional[torch.Tensor]) -> None:
+    """Diagnostics: fused-round launches write per-block {start, rows done, atomics drained, hw
+    id} s_memrealtime stamps (100 MHz) into ``buf`` (int64 [blocks, 4]); None switches off."""
+    native.call("fmlx_glm_set_trace", native.ptr(buf))
 
 
 def pick_layout(X: torch.Tensor) -> Optional[Tuple[int, int]]:
@@ -85,6 +91,16 @@ TAIL_MAX_BLOCKS_ATOMIC = 2048  # float-atomic tail
 # FMLX_DETERMINISTIC=1: fixed-order in-kernel reduction (bit-reproducible run to run); default:
 # float atomics into one accumulator (shorter round tail; last bits vary with arrival order)
 DETERMINISTIC = os.environ.get("FMLX_DETERMINISTIC", "0") == "1"
+# 1-GPU fused rounds complete round e − 1 in the prologue of launch e (no arrival ticket / serial
+# last-block tail; csrc/glm.hip defer_prologue)
+DEFER = os.environ.get("FMLX_GLM_DEFER", "1") == "1"
+
+
+def defer_supported(d: int, acc: torch.dtype) -> bool:
+    """Deferred completion needs the flat atomic tail ([WPB][d] LDS image ≤ 64 KiB) and the
+    row-at-a-time loop."""
+    es = 8 if acc == torch.float64 else 4
+    return DEFER and not DETERMINISTIC and GRAD_UNROLL >= 0 and WPB * d * es <= 64 * 1024
 
 
 def max_round_blocks() -> int:
@@ -111,10 +127,14 @@ class RoundScratch:
 
 def glm_round(X, y, wt, coef, B: int, loss: int, state, scratch: RoundScratch, mode: int, feedback=None,
               max_iter: int = 1, tol: float = 0.0, lr: float = 0.0, reg: float = 0.0, en: float = 0.0,
-              xg=None, rounds: int = 1) -> None:
+              xg=None, rounds: int = 1, defer: bool = False, parity: int = 0, cw=None) -> None:
     """``rounds`` SGD rounds (loss+gradient over the round's batch, fixed-order reduction and — by
     mode — feedback output, update, or xGMI exchange + update), each ONE kernel launch predicated
-    on the device running flag (one host call issues all ``rounds`` launches)."""
+    on the device running flag (one host call issues all ``rounds`` launches).
+
+    ``defer``: 1-GPU TAIL_UPDATE with the atomic tail only — launch e completes round e − 1 in its
+    prologue; launch i of the call reads its round number from state word ``(parity + i) & 1``
+    and ``cw`` is the [2, d] coefficient ring."""
     epc, cpl = pick_layout(X)
     flags = 1 if X.shape[0] * X.stride(0) * X.element_size() > NT_MIN_BYTES else 0
     if xg is not None:
@@ -125,7 +145,8 @@ def glm_round(X, y, wt, coef, B: int, loss: int, state, scratch: RoundScratch, m
                 native.ptr(y), native.ptr(wt), native.ptr(coef), X.shape[0], X.shape[1], B, loss, native.ptr(state),
                 native.ptr(scratch.partials), scratch.nparts, mode, int(scratch.det), native.ptr(scratch.cnt),
                 native.ptr(scratch.acc), native.ptr(scratch.stage1), native.ptr(feedback), int(max_iter), float(tol), float(lr), float(reg),
-                float(en), peers, world, rank, gen, err, int(spin), flags, int(rounds), native.stream_ptr(X.device))
+                float(en), peers, world, rank, gen, err, int(spin), flags, int(rounds), int(bool(defer)), int(parity),
+                native.ptr(cw), native.stream_ptr(X.device))
 
 
 def reduce_update(partials, nparts: int, d: int, stage1, coef, feedback, state, max_iter, tol, lr, reg, en) -> None:

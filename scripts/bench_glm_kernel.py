@@ -3,7 +3,8 @@
 (cdna_hip_programming.md §5.4 rule 24): µs per round of the flagship shape for each variant.
 
 Variants: ``u`` (rows in flight per wave = 2u), ``b`` (blocks = partial rows), ``split``
-(legacy 3-launch round: grad partials → stage-1 → reduce+update) vs the fused one-launch round.
+(legacy 3-launch round: grad partials → stage-1 → reduce+update) vs the fused one-launch round,
+``defer`` (0: ticketed atomic tail; 1: round e − 1 completed in launch e's prologue).
 Usage: python scripts/bench_glm_kernel.py --configs "u=2,b=512;u=4,b=256;split=1"
 """
 import argparse
@@ -71,13 +72,15 @@ def main():
             gk.GRAD_BLOCKS = c.get("b", 512)
             gk.set_tuning(c.get("pad", -1), c.get("nt", -1))
             gk.DETERMINISTIC = bool(c.get("det", 0))
-            gk.set_tail_tuning(c.get("reps", 8), bool(c.get("t2", 0)))
+            gk.DEFER = bool(c.get("defer", 1))
+            gk.set_tail_tuning(c.get("reps", 4), bool(c.get("t2", 0)))
             sgd = SGD(max_iter=10 ** 8, learning_rate=0.1, global_batch_size=a.batch, tol=0.0)
             cls = SplitTrainer if (c.get("split") or c.get("m0")) else DeviceGlmTrainer
             tr = cls(sgd, np.zeros(a.dim), X, y, None, "logistic", use_graph=True)
             tr.mode0_only = bool(c.get("m0"))
             if cls is SplitTrainer:  # the split round needs the block-partials scratch
                 tr.scratch = gk.RoundScratch(tr.nparts, a.dim, torch.float32, dev, det=True)
+                tr.defer, tr.cw = False, None
             tr.rounds_per_graph = c.get("R", 10)
             tr.run_rounds(20)
             torch.cuda.synchronize()
@@ -85,7 +88,8 @@ def main():
             tr.run_rounds(a.rounds)
             torch.cuda.synchronize()
             us = (time.perf_counter() - t0) / a.rounds * 1e6
-            assert c.get("m0") or tr.rounds_executed() == 20 + a.rounds
+            # deferred rounds: the last launch's round completes in the next launch
+            assert c.get("m0") or tr.rounds_executed() == 20 + a.rounds - int(tr.defer)
             res[json.dumps(c)].append(us)
     gb = a.batch * a.dim * 2 / 1e9
     for k, v in res.items():

@@ -155,24 +155,43 @@ class _FakeEvent:
         return 1.0
 
 
-@pytest.mark.parametrize("steps,warmup,R", [(20, 5, 10), (7, 0, 10), (200, 20, 10), (3, 1, 1), (25, 5, 10)])
-def test_bench_timed_region_only_replays(monkeypatch, steps, warmup, R):
+@pytest.mark.parametrize("defer", [False, True])
+@pytest.mark.parametrize("steps,warmup,R", [(20, 5, 10), (7, 0, 10), (200, 20, 10), (3, 1, 1), (25, 5, 10), (13, 3, 4)])
+def test_bench_timed_region_only_replays(monkeypatch, steps, warmup, R, defer):
     """bench.py: no hipGraph capture may happen between the timing barriers (round-1 driver run
-    captured the 10-round graph inside the timed region)."""
+    captured the 10-round graph inside the timed region). Deferred mode: every replay starts at
+    the parity its graph was captured for."""
     import bench
     from flink_ml_amd.common.optimizer import DeviceGlmTrainer
 
     tr = object.__new__(DeviceGlmTrainer)
     tr.use_graph, tr.rounds_per_graph, tr.graphs, tr.timing = True, R, {}, False
+    tr.defer, tr.parity = defer, 0
     log = []
 
-    def capture(r):
+    class Graph(_FakeGraph):
+        def __init__(self, log, key):
+            super().__init__(log, key[0] if defer else key)
+            self.key = key
+
+        def replay(self):
+            if defer:
+                assert tr.parity == self.key[1], "graph replayed at the wrong round-number parity"
+            super().replay()
+
+    def capture(key):
         assert not tr.timing, "hipGraph captured inside the timed region"
-        log.append(("capture", r))
-        tr.graphs[r] = _FakeGraph(log, r)
-        return tr.graphs[r]
+        log.append(("capture", key))
+        tr.graphs[key] = Graph(log, key)
+        return tr.graphs[key]
+
+    def launch(rounds=1):
+        assert not tr.timing, "direct launch inside the timed region"
+        log.append(("launch", rounds))
+        tr.parity = (tr.parity + rounds) & 1
 
     tr._capture = capture
+    tr._launch_round = launch
     monkeypatch.setattr(bench.torch.cuda, "synchronize", lambda *a: None)
     monkeypatch.setattr(bench.torch.cuda, "Event", _FakeEvent)
 

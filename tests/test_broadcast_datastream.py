@@ -101,12 +101,16 @@ def _keyed_tensor_worker(rank, world):
     vals = torch.randn((500, 3), generator=g, dtype=torch.float64)
     own = {op: reduce_by_key_tensor(keys, vals, op) for op in ("sum", "min", "max")}
     full = reduce_by_key_tensor(keys, vals, "sum", gather=True)
-    return keys, vals, own, full
+    # numpy across the result queue: torch tensors travel as shared-memory fds that vanish
+    # once the worker exits
+    npy = lambda kv: (kv[0].numpy(), kv[1].numpy())  # noqa: E731
+    return keys.numpy(), vals.numpy(), {op: npy(kv) for op, kv in own.items()}, npy(full)
 
 
 def test_reduce_by_key_tensor_across_ranks():
     world = 3
-    res = run_spmd(_keyed_tensor_worker, world)
+    res = [(torch.from_numpy(k), torch.from_numpy(v), {op: tuple(map(torch.from_numpy, kv)) for op, kv in own.items()},
+            tuple(map(torch.from_numpy, full))) for k, v, own, full in run_spmd(_keyed_tensor_worker, world)]
     K = torch.cat([r[0] for r in res])
     V = torch.cat([r[1] for r in res])
     uk = torch.unique(K)

@@ -91,9 +91,10 @@ def test_fused_sgd_round_two_ranks_matches_host(xgmi_mode):
         assert b0 == r1[loss][2], loss  # replicas identical
 
 
-@pytest.mark.parametrize("det,blocks,unroll", [(False, 256, 0), (False, 256, -4), (False, 256, -8), (False, 256, 2), (False, 512, 0),
-                                               (True, 512, 0), (True, 256, 1)])
-def test_fused_round_flagship_shape_matches_torch(det, blocks, unroll, monkeypatch):
+@pytest.mark.parametrize("det,blocks,unroll,defer", [(False, 256, 0, True), (False, 256, 0, False), (False, 256, -4, True),
+                                                     (False, 256, -8, True), (False, 256, 2, True), (False, 512, 0, True),
+                                                     (True, 512, 0, True), (True, 256, 1, True)])
+def test_fused_round_flagship_shape_matches_torch(det, blocks, unroll, defer, monkeypatch):
     """Fused rounds (TAIL_UPDATE) at the bench shape, bf16 rows: the bench's 256-block grid and
     512 blocks, the grouped row loop (8 / 4 rows per step) and the row-at-a-time loop, atomic
     tail and the deterministic 16-group fixed-order tail."""
@@ -104,6 +105,7 @@ def test_fused_round_flagship_shape_matches_torch(det, blocks, unroll, monkeypat
     monkeypatch.setattr(gk, "DETERMINISTIC", det)
     monkeypatch.setattr(gk, "GRAD_BLOCKS", blocks)
     monkeypatch.setattr(gk, "GRAD_UNROLL", unroll)
+    monkeypatch.setattr(gk, "DEFER", defer)
 
     g = torch.Generator(device="cpu").manual_seed(7)
     n, d, B = 200_000, 1000, 100_000
@@ -113,6 +115,7 @@ def test_fused_round_flagship_shape_matches_torch(det, blocks, unroll, monkeypat
     ref = TorchGlmTrainer(sgd, np.zeros(d), Xb.to(torch.float64), y, None, "logistic").fit()
     tr = DeviceGlmTrainer(sgd, np.zeros(d), Xb.cuda(), y.cuda(), None, "logistic", use_graph=False)
     assert tr.nparts == blocks and tr.scratch.det == det
+    assert tr.defer == (defer and not det and unroll >= 0)
     got = tr.fit()
     assert tr.rounds_executed() == 3
     assert np.allclose(got, ref, rtol=2e-4, atol=2e-6), np.abs(got - ref).max()
@@ -144,12 +147,16 @@ def test_deterministic_tail_is_bitwise_reproducible(blocks, monkeypatch):
     assert np.allclose(a, c, rtol=1e-5, atol=1e-7)
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_multi_round_launch_terminates_mid_way(graph):
+@pytest.mark.parametrize("graph,defer", [(False, True), (True, True), (False, False), (True, False)])
+def test_multi_round_launch_terminates_mid_way(graph, defer, monkeypatch):
     """One host call issuing many rounds (and a replayed 16-round hipGraph) stops exactly where
-    TerminateOnMaxIterOrTol says, even in the middle of the call."""
+    TerminateOnMaxIterOrTol says, even in the middle of the call (deferred completion: the
+    launch after the last round applies its update and stops)."""
     _need_gpu()
     from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
+    from flink_ml_amd.ops import glm as gk
+
+    monkeypatch.setattr(gk, "DEFER", defer)
 
     g = torch.Generator(device="cpu").manual_seed(3)
     n, d, B = 60_000, 64, 20_000
@@ -162,6 +169,7 @@ def test_multi_round_launch_terminates_mid_way(graph):
     sgd = SGD(max_iter=40, learning_rate=2.0, global_batch_size=B, tol=0.4)
     tr = DeviceGlmTrainer(sgd, np.zeros(d), X.cuda(), y.cuda(), None, "logistic", use_graph=graph)
     tr.rounds_per_graph = 16
+    assert tr.defer == defer
     tr.run_rounds(40)
     torch.cuda.synchronize()
     assert tr.rounds_executed() == ref_tr.rounds
@@ -198,3 +206,31 @@ def test_xgmi_timeout_poisons_and_raises():
     res = run_spmd(_timeout_worker, 2, env=ENV, timeout=300)
     r0 = res[0]
     assert r0["nan"] and not r0["healthy"] and r0["raised"], r0
+
+
+@pytest.mark.parametrize("rem", [0, 3])
+def test_deferred_rounds_match_ticketed_tail(rem, monkeypatch):
+    """Deferred completion vs the ticketed atomic tail over many graph replays with odd remainders
+    (both round-number parities), stopping at max_iter: same rounds, coefficients to rounding."""
+    _need_gpu()
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer
+    from flink_ml_amd.ops import glm as gk
+
+    g = torch.Generator(device="cpu").manual_seed(5)
+    n, d, B = 90_000, 1000, 30_000
+    Xb = torch.rand((n, d), generator=g).to(torch.bfloat16).cuda()
+    y = torch.randint(0, 2, (n,), generator=g).to(torch.float32).cuda()
+    out = {}
+    for defer in (True, False):
+        monkeypatch.setattr(gk, "DEFER", defer)
+        sgd = SGD(max_iter=40 + rem, learning_rate=0.1, global_batch_size=B, tol=0.0)
+        tr = DeviceGlmTrainer(sgd, np.zeros(d), Xb, y, None, "logistic", use_graph=True)
+        assert tr.defer == defer
+        tr.rounds_per_graph = 8
+        for k in (5, 8, 1, 16, 3, 7 + rem):  # mixes graph replays and parities
+            tr.run_rounds(k)
+        tr.run_rounds(4)  # past max_iter: no-ops (deferred: the first one completes the last round)
+        torch.cuda.synchronize()
+        assert tr.rounds_executed() == 40 + rem and not tr.running()
+        out[defer] = tr.coef.double().cpu().numpy()
+    assert np.allclose(out[True], out[False], rtol=1e-5, atol=1e-7), np.abs(out[True] - out[False]).max()
