@@ -317,6 +317,310 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t
 }
 
 // ------------------------------------------------------------------------------------------
+// MFMA assign, pipelined (euclidean, bf16, whole 16-B aligned rows, D = 64 or 128)
+// ------------------------------------------------------------------------------------------
+// Counters of the kernel above at 12.5M x 128, k = 1024 (profiles/r2/kmeans_assign_plain_pmc.json; the variant: kmeans_assign_pipe_pmc.json):
+// MFMA busy 44 % of SIMD cycles; per wave and 32-centroid tile 16 MFMAs (512 cycles) but ≈110
+// VALU (≈570 cycles of vector issue, the MFMAs' own 8 issue cycles included) that run AFTER the
+// MFMAs; a register-staged centroid load waited on right before every barrier; and a label
+// stage of 32 dependent ds_bpermute round trips plus exec-masked selects per wave. This variant:
+//  * folds BOTH norms into the matrix core: one extra k-step of 16 per m-tile multiplies
+//    A_aug = [1, 1, 1, x_h, x_m, x_l, 0…] (the biased ‖x‖² split into three truncated bf16s,
+//    exact to fp32) by B_aug = [c_h, c_m, c_l, 1, 1, 1, 0…] (‖c‖², same split), so with the
+//    tile pre-scaled by −2 the MFMA chain alone yields ‖x‖²' + ‖c‖² − 2x·c, strictly positive,
+//    from a zero seed: the epilogue is one bit-insert (tile id into the low mantissa bits) and
+//    one unsigned min per (row, centroid) — 2 VALU instead of 3, and no ‖x‖² seed registers
+//    (+12.5 % MFMA work, −40 % epilogue VALU: the tile becomes MFMA-bound);
+//  * centroid tiles (and their ‖c‖²) land in LDS by LDS-DMA TWO tiles ahead into a 3-slot
+//    ring — no staging registers, no ds_write; the per-tile wait only covers a load issued a
+//    tile earlier. Unpadded XOR-swizzled image (16-B slot s of row r holds chunk s ^ (r mod
+//    2·KS)): the B-fragment ds_read_b128s are bank-conflict free;
+//  * each m-tile's epilogue runs in the MFMA gaps of the OTHER m-tile's chain (tile t's
+//    m-tile-0 MFMAs carry tile t−1's m-tile-1 epilogue, its m-tile-1 MFMAs carry tile t's
+//    m-tile-0 epilogue), so the VALU hides under the matrix core instead of following it;
+//  * labels: every wave transposes its 64×32 final keys through LDS so that each lane owns one
+//    row and scans its 32 column keys (min3 tree, then the lowest column holding the minimum):
+//    ≈100 VALU and 40 LDS ops per wave, no cross-lane round trips.
+// Same keys and tie rule as kmeans_assign_bf16_kernel (lower tile, then lower column = lower
+// centroid index); the distances differ from it only by fp32 summation order.
+template <int KS, bool PF>
+__global__ __launch_bounds__(256, 2) void kmeans_assign_bf16_pipe_kernel(const bf16_t* __restrict__ X, long ld,
+                                                                         long n, const bf16_t* Cb,
+                                                                         const float* cnorm, int kpad,
+                                                                         int* __restrict__ labels) {
+  static_assert(KS == 4 || KS == 8, "pipelined assign: D = 64 or 128");
+  constexpr int MT = 2;
+  constexpr int DP = KS * 16;
+  constexpr int ROWB = DP * 2;            // bytes per centroid row in LDS (unpadded, swizzled)
+  constexpr int NS = 2 * KS;              // 16-B slots per row
+  constexpr int TILEB = 32 * ROWB;        // bytes per 32-centroid tile
+  constexpr int PW = TILEB / 1024 / 4;    // 1-KiB LDS-DMA pieces per wave per tile (1 or 2)
+  constexpr int SLOTB = TILEB + 4 * 256;  // + the tile's 32 centroid norms, one 256-B copy per wave
+  constexpr int LSTR = 40;                // label transpose: words per row (4·LSTR ≡ 32 mod 64 banks)
+  constexpr int LDSB = 3 * SLOTB > 4 * 64 * LSTR * 4 ? 3 * SLOTB : 4 * 64 * LSTR * 4;
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  typedef short s16x8_t __attribute__((ext_vector_type(8)));
+  __shared__ __align__(16) unsigned char lds[LDSB];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+  const long rowbase = (long)blockIdx.x * (4 * 32 * MT) + (long)wave * 32 * MT;
+  const int ntiles = kpad / 32;
+
+  // tile T → ring slot B: piece p = wave + 4i covers tile rows [p·1024/ROWB, …); lane l of the
+  // piece lands at LDS byte p·1024 + 16·l = (row, slot) and fetches chunk slot ^ (row mod NS);
+  // then the tile's 32 norms (one copy per wave). Issued by inline asm, not
+  // __builtin_amdgcn_global_load_lds: with the builtin the compiler cannot tell the ring slots
+  // apart and puts a vmcnt(0) in front of every ds_read of the current slot, draining the tile
+  // in flight; here the ordering is explicit (vmcnt + barrier at the end of every tile). The
+  // compiler's own vmcnt waits stay correct: VMEM ops it does not know of can only make them
+  // over-wait.
+  const unsigned lds_base = (unsigned)(uintptr_t)(lds_ptr_t)lds;
+#define KP_DMA(T_, B_)                                                                                  \
+  {                                                                                                     \
+    _Pragma("unroll") for (int i_ = 0; i_ < PW; ++i_) {                                                 \
+      const int p_ = wave + 4 * i_;                                                                     \
+      const int off_ = p_ * 1024 + lane * 16;                                                           \
+      const int row_ = off_ / ROWB, slot_ = (off_ % ROWB) / 16;                                         \
+      const bf16_t* src_ = Cb + ((long)(T_) * 32 + row_) * DP + (slot_ ^ (row_ & (NS - 1))) * 8;        \
+      const unsigned dst_ = __builtin_amdgcn_readfirstlane(lds_base + (B_) * SLOTB + p_ * 1024);        \
+      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src_), "s"(dst_)         \
+                   : "memory", "m0");                                                                   \
+    }                                                                                                   \
+    const float* csrc_ = cnorm + (long)(T_) * 32 + r32;                                                 \
+    const unsigned cdst_ = __builtin_amdgcn_readfirstlane(lds_base + (B_) * SLOTB + TILEB + wave * 256); \
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(csrc_), "s"(cdst_)          \
+                 : "memory", "m0");                                                                     \
+  }
+
+  // the first two tiles go out before the row loads, so their L2 latency overlaps the rows' HBM one
+  const int t1 = ntiles > 1 ? 1 : 0;
+  KP_DMA(0, 0)
+  KP_DMA(t1, 1)
+
+  // A fragments: this wave's 2 x 32 rows, whole K, in registers (clamped rows, unconditional)
+  bf16x8_t a[MT][KS];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const long row = rowbase + m * 32 + r32;
+    const bf16_t* xr = X + (row < n ? row : n - 1) * ld;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      union { uint4 u; bf16x8_t v; } t;
+      t.u = *reinterpret_cast<const uint4*>(xr + 16 * s + 8 * h);
+      a[m][s] = t.v;
+    }
+  }
+
+  // A_aug: lanes of half 0 hold [1, 1, 1, x_h, x_m, x_l, 0, 0] for their row (‖x‖² of the bf16
+  // values, biased by 2^-10·‖x‖² so every distance is strictly positive — the fp32 rounding of
+  // ‖x‖² + ‖c‖² − 2x·c is ~2^-15·(‖x‖²+‖c‖²) and cancels only when x ≈ c; a per-row constant
+  // does not move the argmin); half 1 holds zeros, so B_aug's half 1 never contributes.
+  bf16x8_t aaug[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    float p = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      union { bf16x8_t v; uint32_t u[4]; } t;
+      t.v = a[m][s];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+        union { uint32_t u; bf16x2_t v; } q;
+        q.u = t.u[j];
+        p = __builtin_amdgcn_fdot2_f32_bf16(q.v, q.v, p, false);
+      }
+    }
+    p += __shfl_xor(p, 32, 64);  // both K-halves of row r32
+    p *= 1.0f + 0x1p-10f;
+    const uint32_t pb = __float_as_uint(p);
+    const float r1 = p - __uint_as_float(pb & 0xffff0000u);
+    const uint32_t r1b = __float_as_uint(r1);
+    const float r2 = r1 - __uint_as_float(r1b & 0xffff0000u);
+    union { uint32_t u[4]; bf16x8_t v; } q;
+    q.u[0] = 0x3F803F80u;                                    // 1, 1
+    q.u[1] = 0x3F80u | (pb & 0xffff0000u);                   // 1, x_h
+    q.u[2] = (r1b >> 16) | (__float_as_uint(r2) & 0xffff0000u);  // x_m, x_l
+    q.u[3] = 0u;
+    if (h) q.u[0] = q.u[1] = q.u[2] = 0u;
+    aaug[m] = q.v;
+  }
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) asm volatile("" ::"v"(a[m][s]));
+    asm volatile("" ::"v"(aaug[m]));
+  }
+
+  int TB = 0;
+  while ((1 << TB) < ntiles) ++TB;
+  const unsigned tmask = (1u << TB) - 1u;
+  unsigned vkeep;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(vkeep) : "s"(~tmask));
+  unsigned best[MT][16];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) best[m][r] = 0xFFFFFFFFu;
+
+  // one accumulator register: tile id into the low mantissa bits, unsigned running min (2 VALU)
+#define KP_EPI(ACC_, M_, R_, TT_)                                         \
+  {                                                                       \
+    const unsigned k_ = (__float_as_uint(ACC_[R_]) & vkeep) | (TT_);      \
+    best[M_][R_] = k_ < best[M_][R_] ? k_ : best[M_][R_];                 \
+  }
+  constexpr int EPG = 16 / (KS + 1) + 1;  // epilogue registers per MFMA gap (KS + 1 gaps)
+
+  // m-tile-1 accumulator of the "previous tile" before tile 0: FLT_MAX keys lose to every
+  // finite distance (NaN rows resolve to label 0 as in the plain kernel)
+  f32x16_t acc0, acc1;
+  const f32x16_t zero16 = {};
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc1[r] = 3.4028235e38f;
+  unsigned tprev = 0;
+  int s_cur = 0, s_n1 = 1, s_n2 = 2;  // ring slots of tiles t, t+1, t+2
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // rows, tiles 0 and 1
+  __syncthreads();
+
+  // B fragments of a ring slot, and B_aug = [c_h, c_m, c_l, 1, 1, 1, 0, 0] from the slot's
+  // norms (half 1 multiplies A_aug's zeros)
+#define KP_LDB(SLOT_, BF_, CB_)                                                                   \
+  {                                                                                               \
+    const unsigned char* tb_ = lds + (SLOT_) * SLOTB + r32 * ROWB;                                \
+    CB_ = *reinterpret_cast<const uint32_t*>(lds + (SLOT_) * SLOTB + TILEB + wave * 256 + r32 * 4); \
+    _Pragma("unroll") for (int s_ = 0; s_ < KS; ++s_)                                             \
+        BF_[s_] = *reinterpret_cast<const bf16x8_t*>(tb_ + (((2 * s_ + h) ^ (r32 & (NS - 1))) * 16)); \
+  }
+#define KP_AUG(CB_, BA_)                                                   \
+  {                                                                        \
+    const float c_ = __uint_as_float(CB_);                                 \
+    const float c1_ = c_ - __uint_as_float((CB_) & 0xffff0000u);           \
+    const uint32_t c1b_ = __float_as_uint(c1_);                            \
+    const float c2_ = c1_ - __uint_as_float(c1b_ & 0xffff0000u);           \
+    union { uint32_t u[4]; bf16x8_t v; } q_;                               \
+    q_.u[0] = ((CB_) >> 16) | (c1b_ & 0xffff0000u);                        \
+    q_.u[1] = (__float_as_uint(c2_) >> 16) | 0x3F800000u;                  \
+    q_.u[2] = 0x3F803F80u;                                                 \
+    q_.u[3] = 0u;                                                          \
+    BA_ = q_.v;                                                            \
+  }
+  // one m-tile chain: KS MFMAs + the norm step, carrying the OTHER accumulator's epilogue
+#define KP_CHAIN(ACC_, M_, BF_, BA_, EACC_, EM_, ETT_)                                               \
+  _Pragma("unroll") for (int s_ = 0; s_ <= KS; ++s_) {                                               \
+    if (s_ < KS)                                                                                     \
+      ACC_ = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[M_][s_], BF_[s_], s_ == 0 ? zero16 : ACC_, 0, 0, 0); \
+    else                                                                                             \
+      ACC_ = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aaug[M_], BA_, ACC_, 0, 0, 0);                  \
+    _Pragma("unroll") for (int e_ = 0; e_ < EPG; ++e_) if (s_ * EPG + e_ < 16)                      \
+        KP_EPI(EACC_, EM_, s_ * EPG + e_, ETT_)                                                      \
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                               \
+    __builtin_amdgcn_sched_group_barrier(0x002, 2 * EPG, 0);                                         \
+  }
+
+  if constexpr (!PF) {
+    for (int t = 0; t < ntiles; ++t) {
+      const int t2 = t + 2 < ntiles ? t + 2 : ntiles - 1;  // the tail re-fetches the last tile
+      KP_DMA(t2, s_n2)
+      bf16x8_t bfr[KS], baug;
+      uint32_t cb;
+      KP_LDB(s_cur, bfr, cb)
+      KP_AUG(cb, baug)
+      const unsigned tt = (unsigned)t;
+      __builtin_amdgcn_sched_barrier(0);
+      KP_CHAIN(acc0, 0, bfr, baug, acc1, 1, tprev)  // m-tile 0 of tile t | m-tile 1 of tile t − 1
+      KP_CHAIN(acc1, 1, bfr, baug, acc0, 0, tt)     // m-tile 1 of tile t | m-tile 0 of tile t
+      __builtin_amdgcn_sched_barrier(0);
+      // tile t + 1 (issued a tile ago) complete for this wave, then for every wave
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW + 1) : "memory");
+      __syncthreads();
+      tprev = tt;
+      const int s_old = s_cur;
+      s_cur = s_n1;
+      s_n1 = s_n2;
+      s_n2 = s_old;
+    }
+  } else {
+    // B fragments one tile ahead in registers: the ring wait + barrier sit between the two
+    // chains of a tile, and the next tile's ds_reads are issued under the second chain, so no
+    // chain ever starts on an LDS round trip. Two named register sets, loop unrolled by two.
+    bf16x8_t bA[KS], bB[KS], gA, gB;
+    uint32_t cA, cB;
+    KP_LDB(0, bA, cA)
+    KP_AUG(cA, gA)
+#define KP_TILE(BF_, BA_, NBF_, NBA_, NCB_)                                                     \
+    {                                                                                           \
+      const int t2_ = t + 2 < ntiles ? t + 2 : ntiles - 1; /* the tail re-fetches the last tile */ \
+      KP_DMA(t2_, s_n2)                                                                         \
+      const unsigned tt_ = (unsigned)t;                                                         \
+      __builtin_amdgcn_sched_barrier(0);                                                        \
+      KP_CHAIN(acc0, 0, BF_, BA_, acc1, 1, tprev)                                               \
+      __builtin_amdgcn_sched_barrier(0);                                                        \
+      /* tile t + 1 (issued a tile ago) complete for this wave, then for every wave */          \
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW + 1) : "memory");                             \
+      __syncthreads();                                                                          \
+      KP_LDB(s_n1, NBF_, NCB_)                                                                  \
+      KP_CHAIN(acc1, 1, BF_, BA_, acc0, 0, tt_)                                                 \
+      KP_AUG(NCB_, NBA_)                                                                        \
+      __builtin_amdgcn_sched_barrier(0);                                                        \
+      tprev = tt_;                                                                              \
+      const int s_old_ = s_cur;                                                                 \
+      s_cur = s_n1;                                                                             \
+      s_n1 = s_n2;                                                                              \
+      s_n2 = s_old_;                                                                            \
+    }
+    int t = 0;
+    while (true) {
+      KP_TILE(bA, gA, bB, gB, cB)
+      if (++t == ntiles) break;
+      KP_TILE(bB, gB, bA, gA, cA)
+      if (++t == ntiles) break;
+    }
+#undef KP_TILE
+  }
+#undef KP_CHAIN
+#undef KP_AUG
+#undef KP_LDB
+#pragma unroll
+  for (int r = 0; r < 16; ++r) KP_EPI(acc1, 1, r, tprev)
+#undef KP_EPI
+#undef KP_DMA
+  // every wave's tail re-fetches landed before the ring is reused for the label transpose
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // labels: key of (row ρ, column c) → word (m·32 + ρ)·LSTR + c of this wave's region; register
+  // r of half h holds row ρ = (r&3) + 8(r>>2) + 4h. Then lane L owns row L (m = L / 32).
+  uint32_t* reg = reinterpret_cast<uint32_t*>(lds) + wave * 64 * LSTR;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      reg[(m * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * LSTR + r32] = best[m][r];
+  // (no barrier: the region is this wave's own, and a wave's LDS accesses complete in order)
+  unsigned key[32];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint4 v = *reinterpret_cast<const uint4*>(reg + lane * LSTR + 4 * j);
+    key[4 * j] = v.x;
+    key[4 * j + 1] = v.y;
+    key[4 * j + 2] = v.z;
+    key[4 * j + 3] = v.w;
+  }
+  unsigned mn = key[0];
+#pragma unroll
+  for (int c = 1; c < 31; c += 2) mn = min(min(mn, key[c]), key[c + 1]);
+  mn = min(mn, key[31]);
+  int col = 0;
+#pragma unroll
+  for (int c = 31; c >= 0; --c) col = key[c] == mn ? c : col;
+  const long row = rowbase + lane;
+  if (row < n) labels[row] = (int)(mn & tmask) * 32 + col;
+}
+
+// ------------------------------------------------------------------------------------------
 // generic assign (fp32 / fp64): exact reference semantics
 // ------------------------------------------------------------------------------------------
 template <typename T>
@@ -691,6 +995,8 @@ int g_km_sched = 0;
 // rows staged through LDS by LDS-DMA (fmlx_kmeans_set_sched(2)): within noise of the register
 // path (3.71-3.74 vs 3.74-3.75 ms at 12.5M x 128, k=1024; 0.87 vs 0.91 ms at k=32), kept off
 int g_km_xlds = 0;
+// LDS-DMA centroid ring + cross-m-tile epilogue interleave (kmeans_assign_bf16_pipe_kernel)
+int g_km_pipe = 0;
 
 template <int KS>
 int launch_assign_bf16(const void* X, long ld, long n, int D, const void* Cb, const float* cnorm, int kpad, int* labels,
@@ -704,6 +1010,17 @@ int launch_assign_bf16(const void* X, long ld, long n, int D, const void* Cb, co
     if (full && g_km_xlds) {
       hipLaunchKernelGGL((kmeans_assign_bf16_kernel<KS, true, false, true>), dim3(blocks), dim3(256), 0, s,
                          (const bf16_t*)X, ld, n, D, (const bf16_t*)Cb, cnorm, kpad, labels);
+      return (int)hipGetLastError();
+    }
+  }
+  if constexpr (KS == 4 || KS == 8) {
+    if (full && g_km_pipe) {
+      if (g_km_pipe == 2)
+        hipLaunchKernelGGL((kmeans_assign_bf16_pipe_kernel<KS, true>), dim3(blocks), dim3(256), 0, s,
+                           (const bf16_t*)X, ld, n, (const bf16_t*)Cb, cnorm, kpad, labels);
+      else
+        hipLaunchKernelGGL((kmeans_assign_bf16_pipe_kernel<KS, false>), dim3(blocks), dim3(256), 0, s,
+                           (const bf16_t*)X, ld, n, (const bf16_t*)Cb, cnorm, kpad, labels);
       return (int)hipGetLastError();
     }
   }
@@ -742,10 +1059,13 @@ int chunk_sum_vpl(const void* X, long ld, int D, const long* order, const long* 
 }  // namespace
 
 // KS = padded K-steps of 16 (one of 1..8,10,12,16; >= ceil(D/16)); Cb is [kpad][16*KS] zero-padded
-// 0: plain loop, 1: interleaved MFMA/epilogue schedule, 2: rows staged through LDS (LDS-DMA)
+// 0: plain loop, 1: interleaved MFMA/epilogue schedule, 2: rows staged through LDS (LDS-DMA),
+// 3: pipelined (LDS-DMA centroid ring, norms in the MFMA, epilogues in the other m-tile's MFMA
+// gaps; D = 64/128), 4: the same with the B fragments prefetched one tile ahead
 FMLX_API int fmlx_kmeans_set_sched(int mode) {
   g_km_sched = mode == 1;
   g_km_xlds = mode == 2;
+  g_km_pipe = mode == 3 ? 1 : mode == 4 ? 2 : 0;
   return 0;
 }
 

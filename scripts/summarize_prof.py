@@ -43,18 +43,25 @@ def stats(src, dst):
 
 
 def pmc(src, dst, match, note=""):
-    per = defaultdict(lambda: defaultdict(float))
+    med = {}
     meta = {}
-    for r in csv.DictReader(open(src)):
-        if match not in r["Kernel_Name"]:
-            continue
-        per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
+    ndisp = 0
+    for one in src.split(","):  # several counter passes of the same program: medians merged
+        per = defaultdict(lambda: defaultdict(float))
+        for r in csv.DictReader(open(one)):
+            if match not in r["Kernel_Name"]:
+                continue
+            per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
         meta = {"kernel": short(r["Kernel_Name"]), "vgpr": r.get("VGPR_Count") or r.get("Arch_VGPR_Count"),
                 "agpr": r.get("Accum_VGPR_Count"), "sgpr": r.get("SGPR_Count"), "lds_bytes": r.get("LDS_Block_Size"),
                 "grid": r.get("Grid_Size"), "workgroup": r.get("Workgroup_Size")}
-    names = sorted({c for d in per.values() for c in d})
-    med = {c: statistics.median(d[c] for d in per.values() if c in d) for c in names}
+        names = sorted({c for d in per.values() for c in d})
+        med.update({c: statistics.median(d[c] for d in per.values() if c in d) for c in names})
+        ndisp = max(ndisp, len(per))
     der = {}
+    if med.get("GRBM_GUI_ACTIVE") and "SQ_VALU_MFMA_BUSY_CYCLES" in med:
+        # GRBM_GUI_ACTIVE sums the 8 XCDs; 1024 SIMDs
+        der["mfma_busy_share_of_simd_cycles"] = med["SQ_VALU_MFMA_BUSY_CYCLES"] / (med["GRBM_GUI_ACTIVE"] / 8 * 1024)
     if med.get("SQ_WAVES"):
         for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_MFMA"):
             if c in med:
@@ -63,7 +70,7 @@ def pmc(src, dst, match, note=""):
         for c in ("SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY"):
             if c in med:
                 der[c.lower() + "_share_of_wave_cycles"] = med[c] / med["SQ_WAVE_CYCLES"]
-    out = {"kernel": meta, "dispatches": len(per), "pmc_median_per_dispatch": med, "derived": der, "notes": note}
+    out = {"kernel": meta, "dispatches": ndisp, "pmc_median_per_dispatch": med, "derived": der, "notes": note}
     json.dump(out, open(dst, "w"), indent=1)
 
 
