@@ -343,8 +343,8 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t
 //    ≈100 VALU and 40 LDS ops per wave, no cross-lane round trips.
 // Same keys and tie rule as kmeans_assign_bf16_kernel (lower tile, then lower column = lower
 // centroid index); the distances differ from it only by fp32 summation order.
-template <int KS, bool PF>
-__global__ __launch_bounds__(256, 2) void kmeans_assign_bf16_pipe_kernel(const bf16_t* __restrict__ X, long ld,
+template <int KS, bool PF, int NW = 4>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kernel(const bf16_t* __restrict__ X, long ld,
                                                                          long n, const bf16_t* Cb,
                                                                          const float* cnorm, int kpad,
                                                                          int* __restrict__ labels) {
@@ -354,10 +354,11 @@ __global__ __launch_bounds__(256, 2) void kmeans_assign_bf16_pipe_kernel(const b
   constexpr int ROWB = DP * 2;            // bytes per centroid row in LDS (unpadded, swizzled)
   constexpr int NS = 2 * KS;              // 16-B slots per row
   constexpr int TILEB = 32 * ROWB;        // bytes per 32-centroid tile
-  constexpr int PW = TILEB / 1024 / 4;    // 1-KiB LDS-DMA pieces per wave per tile (1 or 2)
-  constexpr int SLOTB = TILEB + 4 * 256;  // + the tile's 32 centroid norms, one 256-B copy per wave
+  constexpr int PW = TILEB / 1024 / NW;   // 1-KiB LDS-DMA pieces per wave per tile (1 or 2)
+  static_assert(PW >= 1 && PW * NW * 1024 == TILEB, "tile pieces must split evenly over the waves");
+  constexpr int SLOTB = TILEB + NW * 256; // + the tile's 32 centroid norms, one 256-B copy per wave
   constexpr int LSTR = 40;                // label transpose: words per row (4·LSTR ≡ 32 mod 64 banks)
-  constexpr int LDSB = 3 * SLOTB > 4 * 64 * LSTR * 4 ? 3 * SLOTB : 4 * 64 * LSTR * 4;
+  constexpr int LDSB = 3 * SLOTB > NW * 64 * LSTR * 4 ? 3 * SLOTB : NW * 64 * LSTR * 4;
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   typedef short s16x8_t __attribute__((ext_vector_type(8)));
   __shared__ __align__(16) unsigned char lds[LDSB];
@@ -366,7 +367,7 @@ __global__ __launch_bounds__(256, 2) void kmeans_assign_bf16_pipe_kernel(const b
   const int wave = threadIdx.x >> 6;
   const int r32 = lane & 31;
   const int h = lane >> 5;
-  const long rowbase = (long)blockIdx.x * (4 * 32 * MT) + (long)wave * 32 * MT;
+  const long rowbase = (long)blockIdx.x * (NW * 32 * MT) + (long)wave * 32 * MT;
   const int ntiles = kpad / 32;
 
   // tile T → ring slot B: piece p = wave + 4i covers tile rows [p·1024/ROWB, …); lane l of the
@@ -381,7 +382,7 @@ __global__ __launch_bounds__(256, 2) void kmeans_assign_bf16_pipe_kernel(const b
 #define KP_DMA(T_, B_)                                                                                  \
   {                                                                                                     \
     _Pragma("unroll") for (int i_ = 0; i_ < PW; ++i_) {                                                 \
-      const int p_ = wave + 4 * i_;                                                                     \
+      const int p_ = wave + NW * i_;                                                                    \
       const int off_ = p_ * 1024 + lane * 16;                                                           \
       const int row_ = off_ / ROWB, slot_ = (off_ % ROWB) / 16;                                         \
       const bf16_t* src_ = Cb + ((long)(T_) * 32 + row_) * DP + (slot_ ^ (row_ & (NS - 1))) * 8;        \
@@ -1061,7 +1062,9 @@ int chunk_sum_vpl(const void* X, long ld, int D, const long* order, const long* 
 // KS = padded K-steps of 16 (one of 1..8,10,12,16; >= ceil(D/16)); Cb is [kpad][16*KS] zero-padded
 // 0: plain loop, 1: interleaved MFMA/epilogue schedule, 2: rows staged through LDS (LDS-DMA),
 // 3: pipelined (LDS-DMA centroid ring, norms in the MFMA, epilogues in the other m-tile's MFMA
-// gaps; D = 64/128), 4: the same with the B fragments prefetched one tile ahead
+// gaps; D = 64/128), 4: the same with the B fragments prefetched one tile ahead. (8-wave,
+// 512-row blocks — half the centroid bytes and DMA issues per row — measured within noise:
+// 3.17 vs 3.19 ms at 12.5M x 128, k = 1024, and slower at k = 32; NW stays a template knob.)
 FMLX_API int fmlx_kmeans_set_sched(int mode) {
   g_km_sched = mode == 1;
   g_km_xlds = mode == 2;
