@@ -20,7 +20,10 @@ WPB = 8
 # 32 bytes per lane, else 2), U > 0 = row-at-a-time with 2·U rows in flight per wave, -4 / -8 =
 # the grouped loop (bf16: 4 / 8 rows per step share one transposed reduction and loss pass)
 GRAD_UNROLL = int(os.environ.get("FMLX_GLM_UNROLL", "0"))
-GRAD_BLOCKS = int(os.environ.get("FMLX_GLM_BLOCKS", "256"))
+# 512 blocks x 8 waves = 4 waves per SIMD (the 128-VGPR cap of the flagship layout): interleaved
+# A/B at 10M x 1000 bf16 on one MI355X, 3 repeats (profiles/r2/lr_grid_ab_1gpu.log): 41.0 µs per
+# round vs 43.4 (256), 43.5 (384), 48.4 (768), 48.2 (1024)
+GRAD_BLOCKS = int(os.environ.get("FMLX_GLM_BLOCKS", "512"))
 
 
 # rows streamed once per pass use non-temporal loads when the data set exceeds the 256 MiB

@@ -93,10 +93,10 @@ def test_fused_sgd_round_two_ranks_matches_host(xgmi_mode):
 
 @pytest.mark.parametrize("det,blocks,unroll,defer", [(False, 256, 0, True), (False, 256, 0, False), (False, 256, -4, True),
                                                      (False, 256, -8, True), (False, 256, 2, True), (False, 512, 0, True),
-                                                     (True, 512, 0, True), (True, 256, 1, True)])
+                                                     (False, 512, 0, False), (True, 512, 0, True), (True, 256, 1, True)])
 def test_fused_round_flagship_shape_matches_torch(det, blocks, unroll, defer, monkeypatch):
-    """Fused rounds (TAIL_UPDATE) at the bench shape, bf16 rows: the bench's 256-block grid and
-    512 blocks, the grouped row loop (8 / 4 rows per step) and the row-at-a-time loop, atomic
+    """Fused rounds (TAIL_UPDATE) at the bench shape, bf16 rows: the bench's 512-block grid
+    (deferred and ticketed tails) and 256 blocks, the grouped row loop (8 / 4 rows per step) and the row-at-a-time loop, atomic
     tail and the deterministic 16-group fixed-order tail."""
     _need_gpu()
     from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
