@@ -44,9 +44,20 @@ def _timed(ctx, fn):
     torch.cuda.synchronize()
     ctx.barrier()
     torch.cuda.synchronize()
+    prof = None
+    if os.environ.get("BENCH_PYPROFILE"):  # host-side profile of the timed body only (diagnostics)
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     out = fn()
     torch.cuda.synchronize()
+    if prof is not None:
+        import pstats
+
+        prof.disable()
+        pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(30)
     ctx.barrier()
     torch.cuda.synchronize()
     return comm.all_reduce_scalar(time.perf_counter() - t0, "max"), out
