@@ -109,34 +109,43 @@ def _prefetch(it: Iterator[Table], dev) -> Iterator[Table]:
     copies are allocated on the side stream, so each is marked used by the consumer stream
     (``record_stream``) before it is handed out: the caching allocator then cannot give its
     blocks to a later side-stream copy while consumer kernels still read them."""
+    from .utils import streamcheck
+
     side = torch.cuda.Stream(dev)
     nxt = None
+    check = streamcheck.enabled()  # FMLX_STREAM_CHECK=1: verify every hand-off (slow)
+    count = [0]
 
     def issue(t):
         if t is None:
             return None
-        fresh = []
+        fresh, pairs = [], []
         with torch.cuda.stream(side):
             cols = {}
             for k, c in t._cols.items():
                 if isinstance(c, torch.Tensor) and c.device.type == "cpu":
                     cols[k] = c.pin_memory().to(dev, non_blocking=True)
                     fresh.append(cols[k])
+                    pairs.append((k, c, cols[k]))
                 elif isinstance(c, SparseColumn) and c.values.device.type == "cpu":
                     cols[k] = c.to(dev)
                     fresh.extend([cols[k].indptr, cols[k].indices, cols[k].values])
+                    pairs.extend([(k + ".indptr", c.indptr, cols[k].indptr), (k + ".indices", c.indices, cols[k].indices),
+                                  (k + ".values", c.values, cols[k].values)])
                 else:
                     cols[k] = c
             ev = torch.cuda.Event()
             ev.record(side)
-        return Table(cols, num_rows=t.num_rows), ev, fresh
+        hand = streamcheck.HandOff(count[0], ev, pairs) if check else None
+        count[0] += 1
+        return Table(cols, num_rows=t.num_rows), ev, fresh, hand
 
     try:
         nxt = issue(next(it))
     except StopIteration:
         return
     while nxt is not None:
-        cur, ev, fresh = nxt
+        cur, ev, fresh, hand = nxt
         consumer = torch.cuda.current_stream(dev)
         consumer.wait_event(ev)
         for t in fresh:
@@ -146,6 +155,8 @@ def _prefetch(it: Iterator[Table], dev) -> Iterator[Table]:
         except StopIteration:
             nxt = None
         yield cur
+        if hand is not None:  # the consumer queued its work on `cur` and asks for the next batch
+            hand.verify(consumer)
 
 
 def _rebatch(it: Iterator[Table], global_batch: int) -> Iterator[Table]:
