@@ -998,6 +998,11 @@ int g_km_sched = 0;
 int g_km_xlds = 0;
 // LDS-DMA centroid ring + cross-m-tile epilogue interleave (kmeans_assign_bf16_pipe_kernel)
 int g_km_pipe = 0;
+// A/B knob: extra dynamic LDS per pipelined block (caps the blocks, i.e. waves per SIMD, per CU).
+// One wave per SIMD (90 KB): 3.68 vs 3.22 ms at 12.5M x 128, k = 1024 — the second wave covers
+// part of the first's issue stalls. (Issuing the tile's LDS-DMA pieces inside the MFMA chain
+// instead of ahead of it: 3.15 vs 3.15 ms, not kept.)
+int g_km_ldspad = 0;
 
 template <int KS>
 int launch_assign_bf16(const void* X, long ld, long n, int D, const void* Cb, const float* cnorm, int kpad, int* labels,
@@ -1017,10 +1022,10 @@ int launch_assign_bf16(const void* X, long ld, long n, int D, const void* Cb, co
   if constexpr (KS == 4 || KS == 8) {
     if (full && g_km_pipe) {
       if (g_km_pipe == 2)
-        hipLaunchKernelGGL((kmeans_assign_bf16_pipe_kernel<KS, true>), dim3(blocks), dim3(256), 0, s,
+        hipLaunchKernelGGL((kmeans_assign_bf16_pipe_kernel<KS, true>), dim3(blocks), dim3(256), g_km_ldspad, s,
                            (const bf16_t*)X, ld, n, (const bf16_t*)Cb, cnorm, kpad, labels);
       else
-        hipLaunchKernelGGL((kmeans_assign_bf16_pipe_kernel<KS, false>), dim3(blocks), dim3(256), 0, s,
+        hipLaunchKernelGGL((kmeans_assign_bf16_pipe_kernel<KS, false>), dim3(blocks), dim3(256), g_km_ldspad, s,
                            (const bf16_t*)X, ld, n, (const bf16_t*)Cb, cnorm, kpad, labels);
       return (int)hipGetLastError();
     }
@@ -1065,6 +1070,11 @@ int chunk_sum_vpl(const void* X, long ld, int D, const long* order, const long* 
 // gaps; D = 64/128), 4: the same with the B fragments prefetched one tile ahead. (8-wave,
 // 512-row blocks — half the centroid bytes and DMA issues per row — measured within noise:
 // 3.17 vs 3.19 ms at 12.5M x 128, k = 1024, and slower at k = 32; NW stays a template knob.)
+FMLX_API int fmlx_kmeans_set_ldspad(int bytes) {
+  g_km_ldspad = bytes > 0 ? bytes : 0;
+  return 0;
+}
+
 FMLX_API int fmlx_kmeans_set_sched(int mode) {
   g_km_sched = mode == 1;
   g_km_xlds = mode == 2;

@@ -17,6 +17,7 @@ from .native import c_int, c_long, c_void_p
 
 native.register_kernel_sigs({
     "fmlx_kmeans_set_sched": [c_int],
+    "fmlx_kmeans_set_ldspad": [c_int],
     "fmlx_kmeans_assign_bf16": [c_void_p, c_long, c_long, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
                                 c_void_p],
     "fmlx_kmeans_assign_generic": [c_int, c_void_p, c_long, c_long, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p,
@@ -59,6 +60,7 @@ _sched_applied = None
 def set_assign_sched(mode: int) -> None:
     global _sched_applied
     native.call("fmlx_kmeans_set_sched", int(mode))
+    native.call("fmlx_kmeans_set_ldspad", int(os.environ.get("FMLX_KMEANS_LDSPAD", "0")))
     _sched_applied = int(mode)
 
 
