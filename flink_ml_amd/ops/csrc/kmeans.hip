@@ -1001,7 +1001,9 @@ int g_km_pipe = 0;
 // A/B knob: extra dynamic LDS per pipelined block (caps the blocks, i.e. waves per SIMD, per CU).
 // One wave per SIMD (90 KB): 3.68 vs 3.22 ms at 12.5M x 128, k = 1024 — the second wave covers
 // part of the first's issue stalls. (Issuing the tile's LDS-DMA pieces inside the MFMA chain
-// instead of ahead of it: 3.15 vs 3.15 ms, not kept.)
+// instead of ahead of it: 3.15 vs 3.15 ms, not kept. Dropping the per-tile barrier altogether —
+// wrong labels, a diagnostic — ran 3.13-3.16 vs 3.17-3.19 ms: the barrier costs ~1 %; what is
+// left is the per-wave issue budget, ≈100 VALU + 18 MFMA per 32-centroid tile.)
 int g_km_ldspad = 0;
 
 template <int KS>
