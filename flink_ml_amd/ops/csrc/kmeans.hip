@@ -377,7 +377,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
   // apart and puts a vmcnt(0) in front of every ds_read of the current slot, draining the tile
   // in flight; here the ordering is explicit (vmcnt + barrier at the end of every tile). The
   // compiler's own vmcnt waits stay correct: VMEM ops it does not know of can only make them
-  // over-wait.
+  // over-wait. M0 is reserved for the compiler, which warns that a clobber of it is not
+  // guaranteed to be honoured: nothing else in this kernel reads or writes M0 (checked in the
+  // ISA: the only M0 writes are these blocks'), so no compiler-held M0 value can be disturbed.
   const unsigned lds_base = (unsigned)(uintptr_t)(lds_ptr_t)lds;
 #define KP_DMA(T_, B_)                                                                                  \
   {                                                                                                     \
