@@ -351,6 +351,7 @@ class FtrlTrainer:
         self._dense_layout = True
         self._scratch = {}  # (nparts, dtype) -> (RoundScratch, state): no per-batch allocation
         self._flags = _FlagRing(self.dev)
+        self._label_cache = {}
 
     # -- state (checkpoints) ------------------------------------------------------------------
     def snapshot(self):
@@ -371,15 +372,34 @@ class FtrlTrainer:
         return (DenseVector(coef.to(torch.float64).numpy()), self.version)
 
     # -- local gradient -----------------------------------------------------------------------
-    def _local_payload(self, batch: Optional[Table]):
+    def _labels(self, batch: Table) -> torch.Tensor:
+        """The batch's labels in the accumulator dtype on the device. A streamed batch is usually a
+        zero-copy slice of one resident label column: that column is converted once (cached while
+        its storage is unchanged, torch's version counter) and the batch takes a view, instead of
+        one conversion kernel + allocation per batch on the host's critical path."""
+        col = batch.column(self.lcol)
+        if (isinstance(col, torch.Tensor) and col.dim() == 1 and col.device == self.dev and col.dtype != self.acc
+                and col._base is not None and col._base.dim() == 1 and col.stride(0) == 1):
+            base = col._base
+            key = (base.data_ptr(), base.numel(), base._version, base.dtype)
+            conv = self._label_cache.get("base")
+            if conv is None or conv[0] != key:
+                conv = (key, base.to(self.acc))
+                self._label_cache["base"] = conv
+            off = (col.data_ptr() - base.data_ptr()) // col.element_size()
+            return conv[1][off:off + col.numel()]
+        return batch.scalars(self.lcol, dtype=self.acc, device=self.dev)
+
+    def _local_payload(self, batch: Optional[Table], need_flag: bool = True):
         """Fills ``self.payload`` with this rank's [grad | wsum | 1] (zeros if no batch); returns
-        the weight-sum stride (0 = one weight sum for every coordinate)."""
+        the weight-sum stride (0 = one weight sum for every coordinate). ``need_flag=False`` (one
+        rank: nothing reads the batch flag) may leave the flag slot stale on the dense GPU path."""
         P, d = self.payload, self.d
         if batch is None or batch.num_rows == 0:
             P.zero_()
             return 0
         X = config.features_for_compute(batch, self.fcol)
-        y = batch.scalars(self.lcol, dtype=self.acc, device=self.dev)
+        y = self._labels(batch)
         if isinstance(X, SparseColumn):
             w = batch.scalars(self.wcol, dtype=self.acc, device=self.dev) if self.wcol and batch.has_column(
                 self.wcol) else None
@@ -422,7 +442,8 @@ class FtrlTrainer:
             # one launch: local gradient + reduction → P[0:d+2] = [Σ mult·x | rows | 0]
             gk.glm_round(Xk, y.to(kacc).contiguous(), None, self.coef, n, gk.LOSS_CODES["ftrl"], state, scratch,
                          gk.TAIL_FEEDBACK, P)
-            P[2 * d:].fill_(1.0)
+            if need_flag:
+                P[2 * d:].fill_(1.0)
             return 0
         Xf = X.to(self.acc)
         mult = torch.sigmoid(Xf @ self.coef) - y
@@ -440,7 +461,7 @@ class FtrlTrainer:
     # -- one round ----------------------------------------------------------------------------
     def launch(self, batch: Optional[Table], world: int, snapshot_state: bool = False) -> "_Round":
         d = self.d
-        stride = self._local_payload(batch)
+        stride = self._local_payload(batch, need_flag=world > 1)
         P = comm.all_reduce_sum(self.payload)
         flag = P[2 * d:] if world > 1 else None  # 1 GPU: the host knows a batch was there
         if self.dev.type == "cuda":
