@@ -20,6 +20,7 @@ until the first model arrives) and reports the ``modelDataVersion`` gauge.
 from __future__ import annotations
 
 import math
+import os
 from typing import Iterable, List, Optional
 
 import numpy as np
@@ -105,6 +106,13 @@ class VersionLog:
         return self._items[i - first]
 
 
+# rounds queued on the device behind the one a blocking multi-rank pull confirms. 1 measured
+# best in the only multi-rank setting available (2 / 4 ranks sharing one MI355X, gloo + forced
+# xGMI, 200 batches): 95 / 157 µs per batch vs 106 / 200 at depth 2 — queued exchange kernels
+# spin on the shared device; a deeper queue is an FMLX_ONLINE_DEPTH knob for one GPU per rank
+PIPELINE_DEPTH = max(1, int(os.environ.get("FMLX_ONLINE_DEPTH", "1")))
+
+
 class _Round:
     """One launched training round: the version snapshot, and (world > 1) the pinned host copy of
     the all-reduced batch-present flag with the event that completes it."""
@@ -143,7 +151,9 @@ class VersionedModelStream:
         self._done = False
         self._ended = False  # this rank's source is exhausted
         self._rebatch = rebatch
-        self._inflight: Optional[_Round] = None
+        # rounds launched but not yet confirmed (world > 1, blocking pulls), oldest first: up to
+        # DEPTH queued on the device while the host confirms the oldest one's batch flag
+        self._inflight: List[_Round] = []
         self._world = get_context().world_size
         self._ck = AlgorithmCheckpoint(name)
         self._launched = 0  # rounds launched (confirmed or in flight)
@@ -218,9 +228,12 @@ class VersionedModelStream:
         return float(rnd.flag[0]) > self._world - 0.5
 
     def flush(self) -> None:
-        """Confirms the round in flight (blocking pulls leave one queued)."""
-        if self._inflight is not None:
-            rnd, self._inflight = self._inflight, None
+        """Confirms the rounds in flight (blocking pulls leave up to ``PIPELINE_DEPTH`` queued), in
+        order; rounds after an unconfirmed one were device no-ops and are dropped."""
+        while self._inflight:
+            rnd = self._inflight.pop(0)
+            if self._done:
+                continue
             if self._confirmed(rnd):
                 self._commit(rnd)
             else:
@@ -246,14 +259,15 @@ class VersionedModelStream:
                 return False
             self._commit(self._launch(self._take_local(block)))
             return True
-        # pipelined protocol (world > 1): every rank launches the same rounds in the same order
-        if self._inflight is None:
-            self._inflight = self._launch(self._take_local(True))
-        nxt = self._launch(self._take_local(True))  # queued behind the round being confirmed
-        rnd, self._inflight = self._inflight, nxt
+        # pipelined protocol (world > 1): every rank launches the same rounds in the same order;
+        # PIPELINE_DEPTH rounds stay queued behind the one being confirmed, so the device never
+        # waits for the host's confirmation and the next launches
+        while len(self._inflight) <= PIPELINE_DEPTH:
+            self._inflight.append(self._launch(self._take_local(True)))
+        rnd = self._inflight.pop(0)
         if not self._confirmed(rnd):
             self._done = True  # every later round is a device no-op (a rank's stream has ended)
-            self._inflight = None
+            self._inflight = []
             return False
         self._commit(rnd)
         return True
@@ -350,7 +364,7 @@ class FtrlTrainer:
         self.payload = torch.zeros(2 * d + 1, dtype=self.acc, device=self.dev)
         self._dense_layout = True
         self._scratch = {}  # (nparts, dtype) -> (RoundScratch, state): no per-batch allocation
-        self._flags = _FlagRing(self.dev)
+        self._flags = _FlagRing(self.dev, PIPELINE_DEPTH + 3)
         self._label_cache = {}
 
     # -- state (checkpoints) ------------------------------------------------------------------
@@ -730,7 +744,7 @@ class OnlineKMeansTrainer:
         self.merge = torch.zeros(kc * D + kc + 1, dtype=self.acc, device=self.dev)
         self.dev_version = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self._rounds = {}  # (n, dtype) -> KMeansRound over batches of that shape
-        self._flags = _FlagRing(self.dev)
+        self._flags = _FlagRing(self.dev, PIPELINE_DEPTH + 3)
 
     def snapshot(self):
         return {"C": self.C.clone(), "W": self.W.clone()}
