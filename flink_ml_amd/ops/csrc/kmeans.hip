@@ -1005,7 +1005,9 @@ int g_km_pipe = 0;
 // part of the first's issue stalls. (Issuing the tile's LDS-DMA pieces inside the MFMA chain
 // instead of ahead of it: 3.15 vs 3.15 ms, not kept. Dropping the per-tile barrier altogether —
 // wrong labels, a diagnostic — ran 3.13-3.16 vs 3.17-3.19 ms: the barrier costs ~1 %; what is
-// left is the per-wave issue budget, ≈100 VALU + 18 MFMA per 32-centroid tile.)
+// left is the per-wave issue budget, ≈86 VALU + 18 MFMA per 32-centroid tile. An epilogue over
+// tile PAIRS — two bit-inserts + one v_min3_u32 per register, 75 VALU per tile at 244 VGPRs —
+// ran 3.11-3.14 vs 3.17 ms there but 0.126 vs 0.105 ms at 2M x 64, k = 256: not kept.)
 int g_km_ldspad = 0;
 
 template <int KS>

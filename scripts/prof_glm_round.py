@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--batch", type=int, default=100_000)
     ap.add_argument("--rounds", type=int, default=30)
     ap.add_argument("--unroll", type=int, default=0)
-    ap.add_argument("--blocks", type=int, default=256)
+    ap.add_argument("--blocks", type=int, default=gk.GRAD_BLOCKS)
     a = ap.parse_args()
     gk.GRAD_UNROLL, gk.GRAD_BLOCKS = a.unroll, a.blocks
     dev = torch.device("cuda")
