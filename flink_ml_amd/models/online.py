@@ -395,13 +395,14 @@ class FtrlTrainer:
         if (isinstance(col, torch.Tensor) and col.dim() == 1 and col.device == self.dev and col.dtype != self.acc
                 and col._base is not None and col._base.dim() == 1 and col.stride(0) == 1):
             base = col._base
-            key = (base.data_ptr(), base.numel(), base._version, base.dtype)
             conv = self._label_cache.get("base")
-            if conv is None or conv[0] != key:
-                conv = (key, base.to(self.acc))
+            # the entry holds the base tensor itself: identity (not its address, which the
+            # allocator could hand to a later tensor) plus torch's in-place version counter
+            if conv is None or conv[0] is not base or conv[1] != base._version:
+                conv = (base, base._version, base.to(self.acc))
                 self._label_cache["base"] = conv
             off = (col.data_ptr() - base.data_ptr()) // col.element_size()
-            return conv[1][off:off + col.numel()]
+            return conv[2][off:off + col.numel()]
         return batch.scalars(self.lcol, dtype=self.acc, device=self.dev)
 
     def _local_payload(self, batch: Optional[Table], need_flag: bool = True):

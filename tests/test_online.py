@@ -392,3 +392,26 @@ def test_gpu_stream_prefetch_to_device():
     for i, b in enumerate(got):
         f = b.column("features")
         assert f.is_cuda and torch.equal(f.cpu(), X[1000 * i:1000 * (i + 1)])
+
+
+def test_label_cache_tracks_base_identity_and_version():
+    """FtrlTrainer._labels: slices of one resident label column share one conversion; an
+    in-place change of the column, or a different column, is never served from the cache."""
+    from flink_ml_amd.models.online import FtrlTrainer
+
+    tr = FtrlTrainer(np.zeros(3), 0.1, 0.1, 0.0, 0.0, "features", "label", None)
+    tr.dev = torch.device("cpu")
+    tr.acc = torch.float32
+    y = torch.arange(10, dtype=torch.float64)
+    X = torch.zeros((10, 3))
+    t = Table({"features": X, "label": y})
+    a = tr._labels(t.slice(2, 5))
+    assert a.dtype == torch.float32 and a.tolist() == [2.0, 3.0, 4.0]
+    cached = tr._label_cache["base"][2]
+    b = tr._labels(t.slice(5, 9))
+    assert b.tolist() == [5.0, 6.0, 7.0, 8.0] and tr._label_cache["base"][2] is cached
+    y[6] = 100.0  # in place: version bump
+    assert tr._labels(t.slice(5, 9)).tolist() == [5.0, 100.0, 7.0, 8.0]
+    y2 = torch.arange(10, 20, dtype=torch.float64)
+    t2 = Table({"features": X, "label": y2})
+    assert tr._labels(t2.slice(0, 2)).tolist() == [10.0, 11.0]
