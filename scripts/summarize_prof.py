@@ -52,9 +52,10 @@ def pmc(src, dst, match, note=""):
             if match not in r["Kernel_Name"]:
                 continue
             per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
-        meta = {"kernel": short(r["Kernel_Name"]), "vgpr": r.get("VGPR_Count") or r.get("Arch_VGPR_Count"),
-                "agpr": r.get("Accum_VGPR_Count"), "sgpr": r.get("SGPR_Count"), "lds_bytes": r.get("LDS_Block_Size"),
-                "grid": r.get("Grid_Size"), "workgroup": r.get("Workgroup_Size")}
+            meta = {"kernel": short(r["Kernel_Name"]), "vgpr": r.get("VGPR_Count") or r.get("Arch_VGPR_Count"),
+                    "agpr": r.get("Accum_VGPR_Count"), "sgpr": r.get("SGPR_Count"),
+                    "lds_bytes": r.get("LDS_Block_Size"), "grid": r.get("Grid_Size"),
+                    "workgroup": r.get("Workgroup_Size")}
         names = sorted({c for d in per.values() for c in d})
         med.update({c: statistics.median(d[c] for d in per.values() if c in d) for c in names})
         ndisp = max(ndisp, len(per))
