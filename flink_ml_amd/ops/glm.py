@@ -22,7 +22,9 @@ WPB = 8
 GRAD_UNROLL = int(os.environ.get("FMLX_GLM_UNROLL", "0"))
 # 512 blocks x 8 waves = 4 waves per SIMD (the 128-VGPR cap of the flagship layout): interleaved
 # A/B at 10M x 1000 bf16 on one MI355X, 3 repeats (profiles/r2/lr_grid_ab_1gpu.log): 41.0 µs per
-# round vs 43.4 (256), 43.5 (384), 48.4 (768), 48.2 (1024)
+# round vs 43.4 (256), 43.5 (384), 48.4 (768), 48.2 (1024). Accumulator replicas 2/4/8 and one
+# contiguous run of rows per wave instead of the interleaved rows measured within 1-2 % (the
+# latter slower): scripts/bench_glm_kernel.py, round-2 log in profiles/r2/INDEX.md
 GRAD_BLOCKS = int(os.environ.get("FMLX_GLM_BLOCKS", "512"))
 
 
