@@ -121,7 +121,7 @@ def test_config1_plumbing_100_points_4_ranks():
 
 # ------------------------------------------------------------------------------------ GPU
 @pytest.mark.gpu
-@pytest.mark.parametrize("D", [2, 10, 100, 128, 200])
+@pytest.mark.parametrize("D", [2, 10, 64, 100, 128, 200])
 @pytest.mark.parametrize("k", [2, 10, 33, 257])
 def test_gpu_assign_bf16_matches_torch(D, k):
     if not torch.cuda.is_available():
@@ -226,6 +226,41 @@ def test_gpu_assign_fp32_euclidean_both_paths(n):
         gap = (d[diff, got[diff]] - d[diff, ref[diff]]).abs()
         assert float(gap.max()) < 1e-4, float(gap.max())
     assert float(diff.double().mean()) < 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sched", [0, 3, 4])
+def test_gpu_assign_bf16_variants_agree(sched):
+    """Every MFMA assign variant (plain loop, pipelined, pipelined + B prefetch) on D = 64 / 128
+    with a centroid count that is not a multiple of the 32-wide tile: labels equal the plain
+    kernel's except at fp32 near-ties."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from flink_ml_amd.ops import kmeans as kk
+
+    dev = torch.device("cuda")
+    try:
+        for D, k in ((64, 250), (128, 97)):
+            g = torch.Generator(device=dev).manual_seed(D + k)
+            X = torch.rand((200_003, D), generator=g, device=dev).to(torch.bfloat16)
+            C = torch.rand((k, D), generator=g, device=dev, dtype=torch.float64)
+            cb = kk.CentroidBuffers(k, D, dev, torch.float32)
+            cb.set(C)
+            kk.set_assign_sched(0)
+            ref = kk.assign(X, cb, "euclidean").long()
+            kk.set_assign_sched(sched)
+            lab = kk.assign(X, cb, "euclidean").long()
+            assert int(lab.max()) < k and int(lab.min()) >= 0
+            diff = lab != ref
+            if bool(diff.any()):
+                Xf, Cf = X[diff].float(), C.to(torch.bfloat16).float()
+                d = (Xf ** 2).sum(1, keepdim=True) + (Cf ** 2).sum(1)[None, :] - 2.0 * Xf @ Cf.T
+                g1 = d.gather(1, lab[diff][:, None]).squeeze(1)
+                g0 = d.gather(1, ref[diff][:, None]).squeeze(1)
+                assert bool(((g1 - g0).abs() <= 1e-4 * d.min(1).values.abs().clamp_min(1e-6)).all())
+            assert float(diff.double().mean()) < 1e-3
+    finally:
+        kk.set_assign_sched(kk.ASSIGN_SCHED)
 
 
 @pytest.mark.gpu
