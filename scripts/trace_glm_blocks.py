@@ -74,6 +74,16 @@ def main():
         })
     for s in summary:
         print(json.dumps(s))
+    # is the imbalance systematic? correlation of each block's rows-done time between rounds,
+    # and how often the same XCD is the slowest
+    done = np.stack([(t[:, 1] - t[:, 0].min()).astype(np.float64) for t in rows])
+    cc = [float(np.corrcoef(done[i], done[i + 1])[0, 1]) for i in range(len(done) - 1)]
+    xcc = (rows[0][:, 3] >> 32) & 0xF
+    slow = [int(max(set(xcc.tolist()), key=lambda x: done[i][xcc == x].mean())) for i in range(len(done))]
+    print(json.dumps({"block_done_corr_between_rounds_median": round(statistics.median(cc), 3),
+                      "slowest_xcd_per_round": slow,
+                      "block_done_spread_us_if_per_block_mean_removed": round(float(
+                          np.median(np.ptp(done - done.mean(0, keepdims=True), axis=1)) * TICK_US), 2)}))
     keys = ["start_max_us", "rows_done_min_us", "rows_done_med_us", "rows_done_max_us", "block_rows_us_med"]
     print(json.dumps({"median_over_rounds": {k: round(statistics.median(s[k] for s in summary), 2) for k in keys},
                       "blocks": nb}))
