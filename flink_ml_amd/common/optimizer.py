@@ -440,8 +440,10 @@ class DeviceGlmTrainer:
             self._host_round = int(self.state[0].item())
             if st["done"]:
                 return self.coef.to(torch.float64).cpu().numpy()
-        step = ck.interval if ck.interval else self.check_every
         log = tracing.rounds_enabled()
+        # per-round logs (a diagnostic mode) read every round's own feedback: one round per host
+        # step; otherwise check-interval (or checkpoint-interval) rounds per host step
+        step = 1 if log else (ck.interval if ck.interval else self.check_every)
         with tracing.range("sgd.fit"):
             while done < self.sgd.max_iter:
                 fault_point(done)

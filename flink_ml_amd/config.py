@@ -54,22 +54,24 @@ def dtype_policy(name: str):
         _OVERRIDE = old
 
 
-def features_for_compute(table: Table, col: str, allow_sparse: bool = True):
-    """The feature column as a device-resident dense tensor [n, d] or a ``SparseColumn``."""
+def features_for_compute(table: Table, col: str, allow_sparse: bool = True, exact: bool = False):
+    """The feature column as a device-resident dense tensor [n, d] or a ``SparseColumn``.
+    ``exact``: for stages that only move values (slicing, assembling), float64 inputs keep float64
+    on the device instead of taking the compute dtype, so no value changes."""
     dev = compute_device()
     c = table.column(col)
     if isinstance(c, torch.Tensor) and c.dim() == 2:
         if c.device == dev and c.dtype in (torch.float32, torch.float64, torch.bfloat16) and (
                 dev.type == "cuda" or c.dtype == torch.float64):
             return c
+        if exact and c.dtype in (torch.float32, torch.float64, torch.bfloat16):
+            return c.to(device=dev)
         return c.to(device=dev, dtype=compute_dtype() if dev.type == "cuda" else torch.float64)
+    wide = torch.float64 if exact or dev.type != "cuda" else None
     if allow_sparse and isinstance(c, SparseColumn):
-        acc = acc_dtype() if dev.type == "cuda" else torch.float64
-        return c.to(device=dev, dtype=acc)
+        return c.to(device=dev, dtype=wide or acc_dtype())
     if allow_sparse and table.is_sparse(col):
         vecs = table.get_list(col)
         sc = SparseColumn.from_vectors([v.to_sparse() for v in vecs], table.vector_size(col))
-        acc = acc_dtype() if dev.type == "cuda" else torch.float64
-        return sc.to(device=dev, dtype=acc)
-    dt = compute_dtype() if dev.type == "cuda" else torch.float64
-    return table.vectors_as_matrix(col, dtype=dt, device=dev)
+        return sc.to(device=dev, dtype=wide or acc_dtype())
+    return table.vectors_as_matrix(col, dtype=wide or compute_dtype(), device=dev)

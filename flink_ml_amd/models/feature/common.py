@@ -20,9 +20,10 @@ def dense_input(table: Table, col: str) -> torch.Tensor:
     return config.features_for_compute(table, col, allow_sparse=False)
 
 
-def vector_input(table: Table, col: str):
-    """Dense tensor or SparseColumn (kept sparse) on the compute device."""
-    return config.features_for_compute(table, col, allow_sparse=True)
+def vector_input(table: Table, col: str, exact: bool = False):
+    """Dense tensor or SparseColumn (kept sparse) on the compute device; ``exact`` keeps float64
+    values unrounded (stages that only move values)."""
+    return config.features_for_compute(table, col, allow_sparse=True, exact=exact)
 
 
 def sparse_map_values(sc: SparseColumn, fn: Callable[[torch.Tensor, torch.Tensor], torch.Tensor]) -> SparseColumn:

@@ -328,7 +328,7 @@ class VectorSlicer(Transformer, HasInputCol, HasOutputCol):
         idx = self.get(self.INDICES)
         if idx is None or len(idx) == 0:
             raise ValueError("Parameter indices's value should not be null")
-        X = vector_input(t, self.get(self.INPUT_COL))
+        X = vector_input(t, self.get(self.INPUT_COL), exact=True)  # slicing moves values only
         d = X.size if isinstance(X, SparseColumn) else X.shape[1]
         if max(idx) >= d:
             raise ValueError("Index value %d is greater than vector size:%d" % (max(idx), d))
