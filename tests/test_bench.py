@@ -34,7 +34,10 @@ def test_task_seed_and_split():
 def test_dense_vector_generator_exact():
     g = DenseVectorGenerator().set_seed(2).set_col_names([["features"]]).set_num_values(50).set_vector_dim(7)
     t = g.get_data()[0]
-    np.testing.assert_array_equal(t.column("features").cpu().numpy(), _java_rows(task_seed(2, 0), 50, [0] * 7))
+    got = t.column("features").cpu()
+    # exact java.util.Random doubles, stored in the column's dtype (the compute dtype on a GPU host)
+    ref = torch.from_numpy(_java_rows(task_seed(2, 0), 50, [0] * 7)).to(got.dtype)
+    np.testing.assert_array_equal(got.numpy(), ref.numpy())
     assert DenseVectorGenerator().get_seed() == java_string_hash(
         "org.apache.flink.ml.benchmark.datagenerator.common.DenseVectorGenerator")
 
