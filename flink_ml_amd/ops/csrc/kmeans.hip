@@ -888,28 +888,22 @@ __global__ __launch_bounds__(1024) void kmeans_offsets_kernel(const int* __restr
   __shared__ long carry;
   if (threadIdx.x == 0) carry = 0;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // 1. offsets[c] = lower_bound(keys_sorted, c) for c = 0..k, every cluster's search in parallel
+  for (int c = threadIdx.x; c <= k; c += 1024) {
+    long lo = 0, hi = n;
+    while (lo < hi) {
+      const long mid = (lo + hi) >> 1;
+      if (keys_sorted[mid] < c) lo = mid + 1; else hi = mid;
+    }
+    offsets[c] = lo;
+  }
+  __syncthreads();  // this block's global writes are visible to the block after the barrier
+  // 2. chunk_off = exclusive scan of ceil(count / KM_CH), fixed order (wave prefix, wave totals,
+  // carry across 1024-cluster passes); counts from neighbouring offsets — one binary search per
+  // cluster instead of two dependent ones
   for (int base = 0; base <= k; base += 1024) {
     const int c = base + threadIdx.x;
-    long lo = 0, hi = n;  // lower_bound(keys_sorted, c)
-    if (c <= k) {
-      while (lo < hi) {
-        const long mid = (lo + hi) >> 1;
-        if (keys_sorted[mid] < c) lo = mid + 1; else hi = mid;
-      }
-      offsets[c] = lo;
-    }
-    __syncthreads();
-    // chunks of cluster c need offsets[c + 1]: recompute it the same way (cheap, log2 n loads)
-    long chunks = 0;
-    if (c < k) {
-      long lo2 = lo, hi2 = n;
-      while (lo2 < hi2) {
-        const long mid = (lo2 + hi2) >> 1;
-        if (keys_sorted[mid] < c + 1) lo2 = mid + 1; else hi2 = mid;
-      }
-      chunks = (lo2 - lo + KM_CH - 1) / KM_CH;
-    }
-    // block-wide exclusive scan of `chunks` (fixed order: wave prefix, then wave totals)
+    const long chunks = c < k ? (offsets[c + 1] - offsets[c] + KM_CH - 1) / KM_CH : 0;
     long incl = chunks;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
