@@ -111,7 +111,7 @@ def main():
             sgd.max_iter += PROFILE_ROUNDS
         return tr
 
-    if world > 1 and not ctx.is_distributed:
+    if (world > 1 or ctx.forced) and not ctx.is_distributed:
         raise SystemExit("WORLD_SIZE=%d but the process group did not come up" % world)
     trainer = make_trainer()
     if world > 1 and ctx.backend == "nccl" and trainer.xg is None and os.environ.get("FMLX_XGMI", "1") != "0":
@@ -163,7 +163,11 @@ def main():
                 "dim": args.dim,
                 "per_gpu_batch": args.batch,
                 "hipgraph": trainer.use_graph,
-                "collective": "none" if world == 1 else ("xgmi" if trainer.xg is not None else ctx.backend),
+                "collective": "none" if not ctx.is_distributed else ("xgmi" if trainer.xg is not None else ctx.backend),
+                "collective_path": {1: "rccl all-reduce of the (d+2) feedback" if ctx.backend == "nccl" else
+                                    "%s all-reduce of the (d+2) feedback" % ctx.backend,
+                                    2: "none (1 GPU: the update is fused into the round kernel)",
+                                    3: "in-kernel xgmi exchange"}[trainer.mode],
                 "round": {1: "fused kernel + rccl all-reduce + update", 2: "one fused kernel",
                           3: "one fused kernel with in-kernel xgmi exchange"}[trainer.mode],
                 "hbm_gb_per_s": round(args.batch * args.dim * X.element_size() / (ms * 1e-3) / 1e9, 1),

@@ -320,7 +320,7 @@ class DeviceGlmTrainer:
         # rewound after the warm-up
         live = [self.state, self.coef] + ([self.wl] if self.csc is not None else [])
         if self.defer:
-            live += [self.scratch.acc, self.cw]
+            live += [self.scratch.acc, self.cw, self.scratch.cnt]  # cnt: the dynamic schedule's counters
         snapshot = [t.clone() for t in live]
         saved_parity = self.parity
         with torch.cuda.stream(side):

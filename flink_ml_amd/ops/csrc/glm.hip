@@ -144,8 +144,63 @@ struct GlmTail {
   int wl_off;      // deferred: byte offset of the block's [d] coefficient image in LDS
   long long* trace;  // diagnostics (null = off): per block {start, rows done, end, hw id} in
                      // 100 MHz s_memrealtime ticks (scripts/trace_glm_blocks.py)
+  int* heads;      // dynamic schedule: [2 parities][DYN_HEADS][DYN_HSTRIDE] chunk counters
+  int dyn;         // 1: dynamic row schedule (deferred mode, row-at-a-time loop, U = 1)
+  int dyn_off;     // byte offset of the block's DynLds in LDS
+  int dyn_lg;      // log2(rows per chunk)
+  int dyn_sync;    // diagnostics: vmcnt(0) before a claim's result is read
+  int* dyn_dbg;    // diagnostics (null = off): per batch-row visit counters of the dynamic schedule
 };
 constexpr int ACC_MAX_REPS = 8;
+
+// ------------------------------------------------------------------------------------------
+// Dynamic row schedule (work distribution of the fused round, deferred mode)
+// ------------------------------------------------------------------------------------------
+// A static row stride leaves the round waiting for its slowest XCD: per-block timelines
+// (profiles/r2/lr_round_block_timeline_512_corr.jsonl) show per-XCD mean finish times 31–35 µs and a
+// 4 µs random spread between blocks. Here the batch is cut into chunks of CH = WPB·DYN_K rows
+// (wave w of a block takes rows w, w + WPB, … of each chunk the block gets):
+//  * block b owns chunks b, b + NB, …, b + (DYN_L−1)·NB outright (its first rows are in flight
+//    before any atomic); the remaining chunks are split into DYN_HEADS equal ranges, one per XCD,
+//    each served by a device-scope counter on its own 128-B line (≈25 claims/µs per word at the
+//    flagship shape; one word saturates near 88/µs, MI355X_MICROARCH.md 'dequeue'). A block claims
+//    from its own XCD's counter and, once that range is drained, steals from the counter with the
+//    most chunks left;
+//  * every wave walks the block-local chunk sequence q = 0, 1, 2, … (an LDS ring of {q, chunk}
+//    words). Wave q mod WPB claims chunk q + DYN_L at the start of its iteration over chunk q and
+//    publishes it at the end of that iteration: the claim is issued before the iteration's row
+//    loads and consumed after them, so its wait is a counted vmcnt inside one iteration (no
+//    loop-carried atomic result, whose copy at a join would force vmcnt(0)), and the readers of
+//    chunk q + DYN_L reach it ≈DYN_L·DYN_K rows later. A wave never waits on a ring slot while
+//    holding an unpublished claim, so there is no wait cycle.
+// Termination: claims of one block complete out of order (the claim for q + 1 may succeed on a
+// counter switched to by a concurrent steal while the claim for q fails), so an empty chunk (−1)
+// is skipped, not taken as the end. A wave stops at chunk q only once no claim can succeed (exh),
+// none is in flight, and no later chunk was published (q > lastv) — conditions that, once true,
+// stay true, so every wave of the block stops at the same point; a wave waiting on a ring slot
+// re-checks them (the slot's claimer may have stopped). Every claimer raises `inflight` before it
+// reads `exh`, so a claim that sees exh = 0 is always waited for.
+// Steal probes read the counters with atomic adds of an opaque 0: an sc1 load is served by the
+// XCD's L2, which keeps a stale line of a counter that other XCDs advance at the memory side.
+// The claim atomics must not go through the AMDGPU atomic optimizer (its lane-0 result fix-up
+// forces vmcnt(0) at the issue point): glm.hip is built with
+// -amdgpu-atomic-optimizer-strategy=None (ops/build.py FILE_FLAGS).
+// The counters of launch parity p are used by that launch and zeroed for the next one by block 0 of
+// the launch with parity 1 − p (the host snapshots them around hipGraph warm-ups).
+// Reference: the work is the SGD minibatch loop of SGD.java:246-285 (the rows a batch covers are
+// unchanged — only which wave reads which row varies).
+constexpr int DYN_HEADS = 8;
+constexpr int DYN_HSTRIDE = 32;  // ints between counters (128 B)
+constexpr int DYN_L = 4;         // chunks of lookahead (and statically owned chunks per block)
+constexpr int DYN_R = 32;        // LDS ring slots (> DYN_L + the chunks any wave can lag behind)
+constexpr int DYN_K = 2;         // rows per wave per chunk (the software pipeline's two buffers)
+struct DynLds {
+  int head;      // counter the block claims from
+  int exh;       // no claim can succeed any more (every counter drained, or none exists)
+  int inflight;  // claims issued and not yet published
+  int lastv;     // highest block-local chunk number published with a real chunk
+  long long ring[DYN_R];  // (q << 32) | (unsigned)chunk, chunk −1 = empty
+};
 
 // Write-through (sc1) hand-off of the partial rows (cdna_hip_programming.md Guideline 16, the
 // sc1 form of the split-K combine): every handed-off value is stored with an agent-scope store
@@ -491,18 +546,22 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
   // coefficient slices (L2-hot), fetched after the first row loads are on their way
   extern __shared__ __align__(16) unsigned char smem_w[];
   A* wdef = reinterpret_cast<A*>(smem_w + tl.wl_off);  // deferred mode: w_e, built by the prologue
-  auto load_w = [&]() {
-    if (tl.defer) {
+  // the same image through an LDS-typed pointer: generic (flat) loads would count in vmcnt AND
+  // lgkmcnt, and one still pending at the row loop's header turns its counted waits into vmcnt(0)
+  typedef __attribute__((address_space(3))) A lds_acc_t;
+  const lds_acc_t* wlds = (const lds_acc_t*)(smem_w + tl.wl_off);
+  auto load_w = [&](bool lds_only = false) {
+    if (lds_only || tl.defer) {
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
         const int c = lane + 64 * k;
         if constexpr (kPacked) {
 #pragma unroll
           for (int i = 0; i < EP; ++i)
-            w2[k][i] = c < nch ? f2_t{(float)wdef[c * EPC + 2 * i], (float)wdef[c * EPC + 2 * i + 1]} : f2_t{0.f, 0.f};
+            w2[k][i] = c < nch ? f2_t{(float)wlds[c * EPC + 2 * i], (float)wlds[c * EPC + 2 * i + 1]} : f2_t{0.f, 0.f};
         } else {
 #pragma unroll
-          for (int i = 0; i < EPC; ++i) w[k][i] = c < nch ? wdef[c * EPC + i] : (A)0;
+          for (int i = 0; i < EPC; ++i) w[k][i] = c < nch ? wlds[c * EPC + i] : (A)0;
         }
       }
       return;
@@ -761,6 +820,190 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
     wsum = wave_sum_dpp(wsum);
     lsum = wave_sum_dpp(lsum);
   } else {
+  bool dyn_done = false;
+  if constexpr (U == 1) if (tl.dyn) {
+    // ---- dynamic row schedule (see DynLds): DYN_K = 2 rows per wave per chunk, one in each
+    // pipeline buffer, so an iteration of the loop below is one chunk
+    dyn_done = true;
+    extern __shared__ __align__(16) unsigned char smem_d[];
+    DynLds* D = reinterpret_cast<DynLds*>(smem_d + tl.dyn_off);
+    constexpr int CH = WPB * DYN_K;
+    const long nrows = end - start;
+    const long C = (nrows + CH - 1) / CH;                // chunks of this round
+    const long NB = gridDim.x;
+    const long S0 = (long)DYN_L * NB;                    // statically owned chunks
+    const long Dn = C > S0 ? C - S0 : 0;                 // chunks served by the counters
+    int* heads = tl.heads + tl.parity * (DYN_HEADS * DYN_HSTRIDE);
+    auto lo_of = [&](int h) -> long { return S0 + (Dn * h) / DYN_HEADS; };
+    auto hi_of = [&](int h) -> long { return S0 + (Dn * (h + 1)) / DYN_HEADS; };
+    if (blockIdx.x == 0 && threadIdx.x < DYN_HEADS)  // the next launch's counters
+      st_agent(&tl.heads[(tl.parity ^ 1) * (DYN_HEADS * DYN_HSTRIDE) + threadIdx.x * DYN_HSTRIDE], 0);
+    if (wave == 0) {  // wave 0's own first access to D follows in program order; the rest of
+                      // the block reads D only after the prologue's barrier
+      unsigned xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      if (lane == 0) {
+        D->head = (int)(xcc & (DYN_HEADS - 1));
+        D->exh = Dn == 0;
+        D->inflight = 0;
+        const long b = blockIdx.x;  // last statically owned chunk number that exists
+        D->lastv = b < C ? (int)((C - 1 - b) / NB < DYN_L - 1 ? (C - 1 - b) / NB : DYN_L - 1) : -1;
+      }
+      if (lane < DYN_R) D->ring[lane] = -1LL;  // tag −1: nothing published
+    }
+    auto put = [&](int q, long c) {
+      if (lane == 0)
+        __hip_atomic_store(&D->ring[q & (DYN_R - 1)], ((long long)q << 32) | (unsigned int)(int)c, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto lds_ld = [&](int* p) -> int {
+      return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    };
+    auto lds_add = [&](int* p, int v) {
+      if (lane == 0) __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto done_at = [&](int q) -> bool {  // no real chunk can appear at q or later
+      return lds_ld(&D->exh) && lds_ld(&D->inflight) == 0 && q > lds_ld(&D->lastv);
+    };
+    auto steal = [&]() -> long {
+      // every counter's fill level (lanes 0..7, coherent atomic reads), then a claim on the
+      // fullest; a failed claim means that counter is drained, so it is not probed again
+      unsigned tried = 0;
+      int zero;  // opaque 0: an add of a literal 0 is folded into a plain (L2-served) atomic load
+      asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
+      for (int it = 0; it < DYN_HEADS; ++it) {
+        const int hv = lane < DYN_HEADS ? __hip_atomic_fetch_add(&heads[lane * DYN_HSTRIDE], zero, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT) : 0;
+        long best = 0;
+        int bh = -1;
+#pragma unroll
+        for (int h = 0; h < DYN_HEADS; ++h) {
+          const long rem = (hi_of(h) - lo_of(h)) - (long)__builtin_amdgcn_readlane(hv, h);
+          if (!((tried >> h) & 1) && rem > best) { best = rem; bh = h; }
+        }
+        if (bh < 0) break;
+        int t = 0;
+        if (lane == 0) t = __hip_atomic_fetch_add(&heads[bh * DYN_HSTRIDE], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = __builtin_amdgcn_readfirstlane(t);
+        if (lo_of(bh) + t < hi_of(bh)) {
+          if (lane == 0) __hip_atomic_store(&D->head, bh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          return lo_of(bh) + t;
+        }
+        tried |= 1u << bh;
+      }
+      if (lane == 0) __hip_atomic_store(&D->exh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return -1;
+    };
+    // chunk of block-local number q: −1 empty, −2 the block is done
+    auto chunk_of = [&](int q) -> long {
+      if (q < DYN_L) {
+        const long c = blockIdx.x + (long)q * NB;
+        return c < C ? c : -1;
+      }
+      long long v;
+      for (int spin = 0;; ++spin) {
+        v = __hip_atomic_load(&D->ring[q & (DYN_R - 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const int vh = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+        if (vh == q) break;
+        if ((spin & 63) == 63 && done_at(q)) return -2;  // the slot's claimer may have stopped
+        // never reached by the protocol (every slot is published once, before the ring wraps):
+        // a bounded wait keeps a broken invariant a wrong result, not a GPU hang
+        if (vh > q || spin > (1 << 22)) return -2;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      return (long)__builtin_amdgcn_readfirstlane((int)(v & 0xffffffffLL));
+    };
+    // the next chunk with rows at or after q (q advanced past empty ones; −1: the block is done).
+    // Wave q mod WPB publishes q + DYN_L for every q it passes (−1 once nothing can be claimed).
+    int claim_q = -1, claim_h = 0;
+    auto walk = [&](int& q) -> long {
+      for (int spin = 0;; ++spin) {
+        const long c = chunk_of(q);
+        if (c >= 0) return c;
+        if (c == -2 || done_at(q) || spin > (1 << 20)) return -1;
+        if ((q & (WPB - 1)) == wave) put(q + DYN_L, -1);  // exh is set: every −1 follows it
+        ++q;
+      }
+    };
+    // claim for chunk q + DYN_L if this wave owns q (issued before the iteration's row loads)
+    auto claim_issue = [&](int q, int& t) {
+      claim_q = -1;
+      if ((q & (WPB - 1)) != wave) return;
+      lds_add(&D->inflight, 1);  // before reading exh (see the termination note)
+      if (lds_ld(&D->exh)) {
+        put(q + DYN_L, -1);
+        lds_add(&D->inflight, -1);
+        return;
+      }
+      claim_q = q + DYN_L;
+      claim_h = lds_ld(&D->head);
+      if (lane == 0) t = __hip_atomic_fetch_add(&heads[claim_h * DYN_HSTRIDE], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    auto claim_publish = [&](int t) {
+      if (claim_q < 0) return;
+      if (tl.dyn_sync) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      long cn = lo_of(claim_h) + __builtin_amdgcn_readfirstlane(t);
+      if (cn >= hi_of(claim_h)) cn = steal();
+      put(claim_q, cn);
+      if (cn >= 0 && lane == 0)
+        __hip_atomic_fetch_max(&D->lastv, claim_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      lds_add(&D->inflight, -1);  // after the publication and lastv
+    };
+    // row j of chunk c for this wave (c < 0 or past `end`: `rsafe` again, masked)
+    auto load_j = [&](long c, int j, long rsafe, Chunk<T, EPC> (&dst)[1][CPL], A (&yy)[1], A (&ww)[1],
+                      bool (&vv)[1]) {
+      const long r = start + c * CH + j * WPB + wave;
+      const bool ok = c >= 0 && r < end;
+      long rr = ok ? r : rsafe;
+      vv[0] = ok;
+      const T* row = X + rr * ld;
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const int cc = lane + 64 * k;
+        if constexpr (NT) load_chunk_nt<T, EPC>(row + (cc < nch ? cc : nch - 1) * EPC, dst[0][k]);
+        else load_chunk<T, EPC>(row + (cc < nch ? cc : nch - 1) * EPC, dst[0][k]);
+      }
+      // label / weight as vector loads: ordered with the row loads under vmcnt (a scalar load
+      // would share lgkmcnt with the LDS ring)
+      asm volatile("" : "+v"(rr));
+      yy[0] = y[rr];
+      ww[0] = wsrc[rr];
+      if (tl.dyn_dbg && ok && lane == 0) atomicAdd(&tl.dyn_dbg[r - start], 1);
+    };
+    int q = 0;
+    long c = nrows > 0 ? walk(q) : -1;
+    if (c >= 0) load_j(c, 0, start, xa, ya, wa, va);
+    if (tl.defer && defer_prologue<A>(tl, coef, state, e, d, wdef)) return;
+    // nothing in flight at the loop header but the back edge's own loads (otherwise the header
+    // merges the pre-loop loads' registers into every iteration's waits); the prologue's own
+    // loads came after the first row's, so this wait is already satisfied in deferred mode
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    if (c >= 0) {
+      load_w(true);  // dynamic schedule ⇒ deferred mode: w_e is in LDS (no global-load branch)
+      while (true) {
+        // xa: row 0 of chunk c (in flight). The claim is issued and consumed inside this
+        // iteration: before row 1's loads, after row 0 of the next chunk went out
+        int t = 0;
+        claim_issue(q, t);
+        const long rs = start + c * CH + wave < end ? start + c * CH + wave : start;
+        load_j(c, 1, rs, xb, yb, wb, vb);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        process(xa, ya, wa, va);
+        int qn = q + 1;
+        const long cn = walk(qn);
+        load_j(cn, 0, rs, xa, ya, wa, va);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        process(xb, yb, wb, vb);
+        claim_publish(t);
+        if (cn < 0) break;
+        q = qn;
+        c = cn;
+      }
+    }
+  }
+  if (!dyn_done) {
   const long step = (long)U * W;
   long r = start + gw;
   long j = 0;
@@ -794,6 +1037,7 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
     }
   }
   }  // classic row-at-a-time path
+  }
 
   if (tl.trace) {
     // every wave's rows are in: stamp once the whole block got here (the LDS reduction below
@@ -1357,6 +1601,10 @@ static int g_nt = -1;
 static int g_acc_reps = 4;  // atomic-tail accumulator replicas (A/B knob, <= ACC_MAX_REPS)
 static int g_ticket2 = 0;   // two-level tickets (A/B knob)
 static long long* g_trace = nullptr;  // per-block timestamps of the next launches (diagnostics)
+static int g_dyn = 1;       // dynamic row schedule (A/B knob)
+static int g_dyn_lg = 3;    // log2(rows per claimed chunk), >= log2(WPB)
+static int g_dyn_sync = 0;
+static int* g_dyn_dbg = nullptr;
 constexpr long LDS_PER_CU = 160 * 1024;
 constexpr int NUM_CU = 256;
 
@@ -1383,6 +1631,13 @@ int launch_grad_u(const void* X, long ld, const void* y, const void* wt, void* c
       const size_t want = (size_t)(LDS_PER_CU / (per_cu + 1) + 1024);
       if (shmem < want) shmem = want;
     }
+  }
+  // dynamic row schedule: deferred mode, row-at-a-time loop with one row per draw
+  t2.dyn = g_dyn && U == 1 && G == 0 && t2.defer && !tl.det && tl.heads != nullptr;
+  if (t2.dyn) {
+    t2.dyn_lg = g_dyn_lg;
+    t2.dyn_off = (int)((shmem + 15) & ~(size_t)15);
+    shmem = (size_t)t2.dyn_off + sizeof(DynLds);
   }
   if constexpr (G > 0) {
     // grouped path: per-wave [G][64] fp32 transpose scratch after the epilogue's buffers
@@ -1443,6 +1698,9 @@ int launch_grad_cpl(int cpl, int u, const void* X, long ld, const void* y, const
 int launch_round(int dtype, int epc, int cpl, int u, const void* X, long ld, const void* y, const void* wt, void* coef,
                  long n, int d, long B, int loss, int* state, void* partials, int nblocks, const GlmTail& tl, int flags,
                  hipStream_t s) {
+#ifdef FMLX_ISA_PROBE  // ISA inspection builds: the flagship instantiation only
+  return launch_grad<bf16_t, 8, 2>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
+#endif
   if (dtype == DT_BF16) {
     if (epc == 8) return launch_grad_cpl<bf16_t, 8>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
     if (epc == 4) return launch_grad_cpl<bf16_t, 4>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
@@ -1495,6 +1753,25 @@ FMLX_API int fmlx_glm_set_tuning(long lds_pad, int nt) {
 
 // diagnostics: launches record per-block timestamps into trace[nblocks][4] (null: off)
 FMLX_API void fmlx_glm_set_trace(void* trace) { g_trace = (long long*)trace; }
+
+// dynamic row schedule of the deferred fused round: on/off and log2(rows per chunk)
+FMLX_API int fmlx_glm_set_dyn(int on, int lg) {
+  if (lg < 3 || lg > 10) return -1;
+  g_dyn = on;
+  g_dyn_lg = lg;
+  return 0;
+}
+
+// diagnostics of the dynamic schedule: vmcnt(0) before claim results are read; per-row visit
+// counters (int32[batch rows], null = off)
+FMLX_API void fmlx_glm_set_dyn_debug(int sync, void* dbg) {
+  g_dyn_sync = sync;
+  g_dyn_dbg = (int*)dbg;
+}
+
+// ints of the fused round's counter block: tickets (TAIL_TOP + 1, padded to 128) + the dynamic
+// schedule's [2][DYN_HEADS][DYN_HSTRIDE] chunk counters
+FMLX_API int fmlx_glm_cnt_elems() { return 128 + 2 * DYN_HEADS * DYN_HSTRIDE; }
 
 FMLX_API int fmlx_glm_set_tail_tuning(int acc_reps, int ticket2) {
   if (acc_reps < 1 || acc_reps > ACC_MAX_REPS) return -1;
@@ -1550,6 +1827,9 @@ FMLX_API int fmlx_glm_round(int dtype, int epc, int cpl, int u, const void* X, l
   tl.defer = defer;
   tl.cw = cw;
   tl.trace = g_trace;
+  tl.dyn_sync = g_dyn_sync;
+  tl.dyn_dbg = g_dyn_dbg;
+  tl.heads = (flags & 2) && cnt ? cnt + 128 : nullptr;  // flags bit 1: cnt has fmlx_glm_cnt_elems ints
   // `rounds` consecutive rounds, one launch each (a kernel boundary, ~1.5 µs, is cheaper than an
   // in-kernel grid-wide round barrier: measured, scripts/stream_probe2.hip)
   for (int i = 0; i < (rounds > 0 ? rounds : 1); ++i) {

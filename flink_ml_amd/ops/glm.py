@@ -45,6 +45,22 @@ def set_tail_tuning(acc_reps: int = 4, ticket2: bool = False) -> None:
     native.call("fmlx_glm_set_tail_tuning", int(acc_reps), int(bool(ticket2)))
 
 
+# deferred fused rounds: dynamic row schedule (csrc/glm.hip DynLds) instead of the static row
+# stride; FMLX_GLM_DYN=1/0 (the process-wide default, applied when the first round scratch is made)
+DYN_DEFAULT = os.environ.get("FMLX_GLM_DYN", "1") == "1"
+_dyn_set = False
+
+
+def set_dyn(on: bool = True, chunk_rows: int = 8) -> None:
+    """A/B knob of the deferred fused round's dynamic row schedule (csrc/glm.hip DynLds): on/off
+    (``chunk_rows`` is kept for the A/B scripts; the kernel's chunk is WPB·DYN_K rows)."""
+    global _dyn_set
+    lg = int(chunk_rows).bit_length() - 1
+    if chunk_rows != 1 << lg or native.kernels().fmlx_glm_set_dyn(int(bool(on)), lg) != 0:
+        raise ValueError("chunk_rows must be a power of two in [8, 1024]")
+    _dyn_set = True
+
+
 def set_trace(buf: Optional[torch.Tensor]) -> None:
     """Diagnostics: fused-round launches write per-block {start, rows done, atomics drained, hw
     id} s_memrealtime stamps (100 MHz) into ``buf`` (int64 [blocks, 4]); None switches off."""
@@ -117,6 +133,8 @@ class RoundScratch:
     atomic accumulator, arrival tickets (all zero-initialised; the kernel re-arms them)."""
 
     def __init__(self, nparts: int, d: int, acc: torch.dtype, device, det: bool = None):
+        if not _dyn_set:
+            set_dyn(DYN_DEFAULT)
         self.nparts = nparts
         self.det = DETERMINISTIC if det is None else bool(det)
         if self.det:
@@ -127,7 +145,8 @@ class RoundScratch:
             self.stage1 = None
         # atomic tail: ACC_MAX_REPS replicas of the [d+2] accumulator on whole 256-B lines
         self.acc = torch.zeros(int(native.kernels().fmlx_glm_acc_elems(d)), dtype=acc, device=device)
-        self.cnt = torch.zeros(80, dtype=torch.int32, device=device)  # 64 group + 1 top tickets
+        # 64 group + 1 top tickets, then the dynamic row schedule's chunk counters (2 parities × 8)
+        self.cnt = torch.zeros(int(native.kernels().fmlx_glm_cnt_elems()), dtype=torch.int32, device=device)
 
 
 def glm_round(X, y, wt, coef, B: int, loss: int, state, scratch: RoundScratch, mode: int, feedback=None,
@@ -142,6 +161,7 @@ def glm_round(X, y, wt, coef, B: int, loss: int, state, scratch: RoundScratch, m
     and ``cw`` is the [2, d] coefficient ring."""
     epc, cpl = pick_layout(X)
     flags = 1 if X.shape[0] * X.stride(0) * X.element_size() > NT_MIN_BYTES else 0
+    flags |= 2  # scratch.cnt carries the dynamic schedule's counters
     if xg is not None:
         peers, world, rank, gen, err, spin = xg.kernel_args()
     else:

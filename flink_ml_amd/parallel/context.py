@@ -25,10 +25,11 @@ class SPMDContext:
     local_rank: int = 0
     device: torch.device = torch.device("cpu")
     backend: Optional[str] = None
+    forced: bool = False  # FMLX_FORCE_PG=1: a process group (and its collectives) even at world 1
 
     @property
     def is_distributed(self) -> bool:
-        return self.world_size > 1 and dist.is_available() and dist.is_initialized()
+        return (self.world_size > 1 or self.forced) and dist.is_available() and dist.is_initialized()
 
     @property
     def is_gpu(self) -> bool:
@@ -65,6 +66,23 @@ def default_device(local_rank: int = 0) -> torch.device:
     return torch.device("cpu")
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def force_pg() -> bool:
+    """FMLX_FORCE_PG=1: create the process group even at WORLD_SIZE=1, so every collective of the
+    distributed code path (RCCL all-reduces, hipGraph-captured ones included; the xGMI set-up and
+    its fallback) runs on a one-GPU host exactly as it would on eight."""
+    return os.environ.get("FMLX_FORCE_PG", "0") == "1"
+
+
 def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> SPMDContext:
     """Initialises the process group from the environment (idempotent)."""
     global _CTX
@@ -75,13 +93,18 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> SPM
         device = default_device(local_rank)
         if device.type == "cuda":
             torch.cuda.set_device(device)
-        if world > 1 and not dist.is_initialized():
+        forced = world == 1 and force_pg()
+        if (world > 1 or forced) and not dist.is_initialized():
             import datetime
 
             if backend is None:
                 # FMLX_BACKEND=gloo: several ranks sharing one GPU (rehearsals of multi-GPU paths)
                 backend = os.environ.get("FMLX_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if forced:
+                os.environ.setdefault("RANK", "0")
+                os.environ.setdefault("WORLD_SIZE", "1")
+                os.environ.setdefault("MASTER_PORT", str(_free_port()))
             kwargs = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
             if backend == "nccl":
                 kwargs["device_id"] = device
@@ -90,7 +113,9 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> SPM
             backend = dist.get_backend()
             world = dist.get_world_size()
             rank = dist.get_rank()
-        _CTX = SPMDContext(rank=rank, world_size=world, local_rank=local_rank, device=device, backend=backend)
+            forced = world == 1
+        _CTX = SPMDContext(rank=rank, world_size=world, local_rank=local_rank, device=device, backend=backend,
+                           forced=forced)
     if _CTX.is_distributed and _CTX.is_gpu and backend == "nccl":
         from . import xgmi
 

@@ -244,13 +244,22 @@ def get() -> Optional[XgmiComm]:
         if not _all_ok(ok, ctx):
             comm.close()
             return None
-        ok = comm.self_test()
+        ok = comm.self_test() and os.environ.get("FMLX_XGMI_INJECT_FAIL", "0") != "1"  # test hook
         if not _all_ok(ok, ctx):
             warnings.warn("xGMI all-reduce self-test failed; collectives stay on RCCL")
             comm.close()
             return None
         _COMM = comm
         return _COMM
+
+
+def collective_path() -> str:
+    """What a device all-reduce of this process runs on: 'none' (no process group), 'xgmi' (the
+    one-shot exchange is up), or the process group's backend ('nccl' = RCCL, 'gloo')."""
+    ctx = get_context()
+    if not ctx.is_distributed:
+        return "none"
+    return "xgmi" if get() is not None else str(ctx.backend)
 
 
 def check() -> None:

@@ -16,7 +16,7 @@ def _free_port() -> int:
     return port
 
 
-def _worker(rank, world, port, fn, args, q, env=None):
+def _worker(rank, world, port, fn, args, q, env=None, backend="gloo"):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "FMLX_DEVICE": "cpu"})
     os.environ.update(env or {})
@@ -26,7 +26,7 @@ def _worker(rank, world, port, fn, args, q, env=None):
         torch.set_num_threads(1)
         from flink_ml_amd.parallel.context import init_distributed, shutdown
 
-        init_distributed(backend="gloo", timeout_s=120)
+        init_distributed(backend=backend, timeout_s=120)
         res = fn(rank, world, *args)
         q.put((rank, "ok", res))
         shutdown()
@@ -34,13 +34,14 @@ def _worker(rank, world, port, fn, args, q, env=None):
         q.put((rank, "err", traceback.format_exc()))
 
 
-def run_spmd(fn, world: int, *args, timeout: float = 180, env=None):
+def run_spmd(fn, world: int, *args, timeout: float = 180, env=None, backend="gloo"):
     """``env``: extra environment for every rank (e.g. ``{"FMLX_DEVICE": "cuda:0"}`` to put all
-    ranks on one GPU with a gloo group)."""
+    ranks on one GPU with a gloo group). ``backend=None``: the context's choice (``nccl`` = RCCL
+    on a GPU)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, q, env)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, q, env, backend)) for r in range(world)]
     for p in procs:
         p.start()
     results = {}
