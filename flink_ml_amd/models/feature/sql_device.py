@@ -531,13 +531,21 @@ def evaluate(statement: str, t: Table, world: int = 1, rank: int = 0) -> Table:
     subset. ``world > 1``: aggregates are merged across ranks and dealt round-robin."""
     items, where, group = parse(statement)
     dev = _device_of(t)
-    if where is not None:
-        ev = _Eval(t, t.num_rows, dev)
-        mask = ev.boolean(ev(where))
-        if _has_agg(where):
-            raise Unsupported("aggregate in WHERE")
-        t = t.take(torch.nonzero(mask, as_tuple=True)[0])
     aggregate = group is not None or any(_has_agg(e) for e, _ in items)
+    werr = None
+    if where is not None:
+        try:
+            ev = _Eval(t, t.num_rows, dev)
+            mask = ev.boolean(ev(where))
+            if _has_agg(where):
+                raise Unsupported("aggregate in WHERE")
+            t = t.take(torch.nonzero(mask, as_tuple=True)[0])
+        except Unsupported as e:
+            # a data-dependent failure (integer division by zero) may hit one rank only: an
+            # aggregate's ranks must still agree on the path (ADVICE r2), so it joins the agreement
+            if not (aggregate and world > 1):
+                raise
+            werr = e
     if not aggregate:
         ev = _Eval(t, t.num_rows, dev)
         out, used = {}, set()
@@ -552,7 +560,7 @@ def evaluate(statement: str, t: Table, world: int = 1, rank: int = 0) -> Table:
             name = _out_name(e, alias, i, used)
             out[name] = ev.full(ev(e))
         return Table(out, num_rows=t.num_rows)
-    return _aggregate(items, group or [], t, dev, world, rank)
+    return _aggregate(items, group or [], t, dev, world, rank, werr)
 
 
 # ---- aggregation: per-group partial states (sum, count, min, max) so ranks can merge them
@@ -627,12 +635,13 @@ def _local_states(items, group, t: Table, dev, world):
     return aggs, states, outs, keys, uk, ng
 
 
-def _aggregate(items, group, t: Table, dev, world, rank) -> Table:
-    err = None
-    try:
-        local = _local_states(items, group, t, dev, world)
-    except Unsupported as e:
-        err, local = e, None
+def _aggregate(items, group, t: Table, dev, world, rank, werr=None) -> Table:
+    err, local = werr, None
+    if err is None:
+        try:
+            local = _local_states(items, group, t, dev, world)
+        except Unsupported as e:
+            err = e
     if world > 1:
         # every rank must take the same path: the merge below and the host fallback are collective
         from ...parallel import comm
@@ -645,6 +654,11 @@ def _aggregate(items, group, t: Table, dev, world, rank) -> Table:
     if world > 1:
         uk, states, _ = _merge_ranks(uk, states, dev, bool(keys))
         ng = uk.shape[0]
+        if not keys and states and int(states[0]["count"].sum().item()) == 0:
+            # no rows on any rank (e.g. WHERE filtered everything): Flink returns NULLs, which
+            # only the host fallback produces; the merged count is the same on every rank, so
+            # every rank takes the fallback together
+            raise Unsupported("aggregate over an empty input (NULL result)")
     res = {}
     used = set()
     key_cols = [uk[:, i].to(keys[i].dtype) for i in range(len(keys))]

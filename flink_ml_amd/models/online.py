@@ -94,6 +94,10 @@ class VersionLog:
     def __len__(self) -> int:
         return self._total
 
+    def first(self) -> int:
+        """Index of the oldest retained version."""
+        return self._total - len(self._items)
+
     def __bool__(self) -> bool:
         return self._total > 0
 
@@ -181,7 +185,13 @@ class VersionedModelStream:
             if item is END:
                 self._ended = True
                 return None
-            self._pending = _BatchBuf.feed(self, item)
+            b = _BatchBuf.feed(self, item)
+            if b is not None and self._skip > 0:
+                # a restored checkpoint already includes this local batch (the iterator path
+                # skips the same count below): the source is replayed, not rewound
+                self._skip -= 1
+                return None
+            self._pending = b
             return self._pending
         if self._iter is None:
             src = self._source
@@ -190,6 +200,7 @@ class VersionedModelStream:
                               else stream)
             for _ in range(self._skip):  # batches consumed before the restored checkpoint
                 next(self._iter, None)
+            self._skip = 0
         try:
             self._pending = next(self._iter)
         except StopIteration:
@@ -493,8 +504,6 @@ class FtrlTrainer:
                      state=self.snapshot() if snapshot_state else None)
         if flag is not None:
             rnd.flag, rnd.event = self._flags.copy(flag)
-        if world > 1 and flag is not None:
-            pass
         return rnd
 
     def step(self, batch: Table):
@@ -595,13 +604,17 @@ class OnlineLogisticRegressionModel(_OnlineModelMixin, ModelWithData, OnlineLogi
             s = self._stream
 
             def gen():
-                i = 0
+                # the reference's model-data stream emits every version; versions older than the
+                # log's retention window (evicted while this reader was behind, or before a
+                # checkpoint restore) are skipped instead of raising
+                i = s.versions.first()
                 while True:
                     while i >= len(s.versions):
                         if not s.pull(block=True):
                             s.flush()
                             if i >= len(s.versions):
                                 return
+                    i = max(i, s.versions.first())
                     yield Table.from_rows([s.versions[i]], list(self.MODEL_DATA_COLUMNS))
                     i += 1
             return [StreamTable(gen())]

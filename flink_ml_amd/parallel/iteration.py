@@ -54,6 +54,12 @@ class OperatorLifeCycle(enum.Enum):
 @dataclass
 class IterationConfig:
     operator_life_cycle: OperatorLifeCycle = OperatorLifeCycle.ALL_ROUND
+    # unbounded iterations: rounds per end-of-stream agreement. The ranks agree on how many
+    # batches every rank has (one scalar all-reduce per ``agree_interval`` rounds, on up to that
+    # many prefetched local batches) instead of once per batch; 0 = no agreement at all (the
+    # caller guarantees equally long streams; the round counts are checked once at the end).
+    # Semantics are unchanged: the iteration ends when the stream ends on any rank.
+    agree_interval: int = 1
 
     @staticmethod
     def new_builder():
@@ -63,13 +69,18 @@ class IterationConfig:
 class _ConfigBuilder:
     def __init__(self):
         self._lc = OperatorLifeCycle.ALL_ROUND
+        self._agree = 1
 
     def set_operator_life_cycle(self, lc: OperatorLifeCycle):
         self._lc = lc
         return self
 
+    def set_agree_interval(self, k: int):
+        self._agree = int(k)
+        return self
+
     def build(self) -> IterationConfig:
-        return IterationConfig(self._lc)
+        return IterationConfig(self._lc, self._agree)
 
 
 class DataStreamList(list):
@@ -305,15 +316,42 @@ def _run_unbounded(init_variables, data_batches, config, body_or_factory, checkp
                 next(it, None)
     body = _make_body(body_or_factory, config, epoch)
     last_result = None
+    from collections import deque
+
     from .checkpoint import fault_point
 
+    K = max(0, int(getattr(config, "agree_interval", 1)))
+    ready: deque = deque()  # prefetched local batches every rank is known to have
+    agreed = 0              # rounds still covered by the last agreement
+    ended = False
+    last = False            # the last agreement covered fewer than K rounds: some stream ended
+
+    def next_batch():
+        nonlocal agreed, ended, last
+        if K == 0:  # aligned streams: no per-round collective
+            try:
+                return next(it), True
+            except StopIteration:
+                return None, False
+        if agreed == 0:
+            if last:
+                return None, False
+            # prefetch up to K local batches, then one agreement on the common count
+            while len(ready) < K and not ended:
+                try:
+                    ready.append(next(it))
+                except StopIteration:
+                    ended = True
+            agreed = int(comm.all_reduce_scalar(float(len(ready)), "min"))
+            last = agreed < K  # a rank came up short only because its stream ended
+            if agreed == 0:
+                return None, False
+        agreed -= 1
+        return ready.popleft(), True
+
     while True:
-        try:
-            batch = next(it)
-            has = 1.0
-        except StopIteration:
-            batch, has = None, 0.0
-        if comm.all_reduce_scalar(has, "min") == 0.0:
+        batch, ok = next_batch()
+        if not ok:
             break
         fault_point(epoch)
         if config.operator_life_cycle == OperatorLifeCycle.PER_ROUND:
@@ -335,6 +373,10 @@ def _run_unbounded(init_variables, data_batches, config, body_or_factory, checkp
         epoch += 1
         if checkpoint is not None:
             checkpoint.maybe_save(epoch, variables, outputs, side=side)
+    if K == 0:
+        lo, hi = comm.all_reduce_scalar(float(epoch), "min"), comm.all_reduce_scalar(float(epoch), "max")
+        if lo != hi:
+            raise RuntimeError("agree_interval=0 needs equally long streams: ranks ran %d..%d rounds" % (lo, hi))
     if last_result is not None:
         ctx = IterationContext(epoch)
         _emit_listener_records(last_result, outputs, epoch, True, ctx)

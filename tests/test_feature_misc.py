@@ -158,3 +158,25 @@ def test_sql_device_distributed_agreement():
     res = run_spmd(_spmd_sql_fallback, 2)
     assert sum(n for n, _ in res) == 2
     assert set(x for _, a in res for x in a) == {(3.0, 2, 2.0), (2.0, 2, 4.0)}
+
+
+def _spmd_sql_where_edge(rank, world):
+    t = _t().partition(rank, world)
+    # WHERE division by zero on one rank only: the aggregate's ranks still take one path together
+    a = SQLTransformer().set_statement(
+        "SELECT v2, COUNT(*) AS c FROM __THIS__ WHERE id / (id - 1) >= 0 GROUP BY v2").transform(t)[0].rows()
+    # WHERE filters every row on every rank, no GROUP BY: Flink returns one row of NULLs
+    e = SQLTransformer().set_statement("SELECT SUM(v1) AS s, MAX(id) AS m FROM __THIS__ WHERE id < 0") \
+        .transform(t)[0].rows()
+    return a, e
+
+
+def test_sql_distributed_where_agreement_and_empty_input():
+    """WHERE errors join the aggregate's rank agreement; an input every rank
+    filters to nothing gives NULLs (host fallback), not sentinel values."""
+    res = run_spmd(_spmd_sql_where_edge, 2)
+    for _, e in res:
+        for row in e:
+            assert all(v is None or (isinstance(v, float) and math.isnan(v)) for v in row), e
+    assert sum(len(e) for _, e in res) == 1
+    assert sum(c for a, _ in res for (_, c) in a) >= 1

@@ -271,3 +271,47 @@ def test_round_logs_are_structured_json(capsys):
     sgd = [r for r in recs if r["kind"] == "sgd"]
     assert [r["epoch"] for r in it] == [0, 1, 2] and all("ms" in r and r["rank"] == 0 for r in it)
     assert [r["epoch"] for r in sgd] == [0, 1, 2, 3] and all(r["weight"] == 50.0 and r["loss"] > 0 for r in sgd)
+
+
+def _spmd_unbounded_agree(rank, world, k, counts):
+    from flink_ml_amd.parallel import comm
+
+    calls = {"n": 0}
+    orig = comm.all_reduce_scalar
+
+    def counting(x, op="sum", **kw):
+        calls["n"] += 1
+        return orig(x, op, **kw)
+
+    comm.all_reduce_scalar = counting
+
+    class B(IterationBody):
+        def process(self, variables, data, ctx):
+            model = variables[0][0] + sum(data[0])
+            return IterationBodyResult([[model]], [[model]])
+
+    batches = [[rank * 100 + i] for i in range(counts[rank])]
+    cfg = IterationConfig.new_builder().set_agree_interval(k).build()
+    try:
+        out = Iterations.iterate_unbounded_streams([[0]], iter(batches), B(), config=cfg)
+    finally:
+        comm.all_reduce_scalar = orig
+    return out[0], calls["n"]
+
+
+@pytest.mark.parametrize("k", [1, 4, 0])
+def test_unbounded_agreement_interval(k):
+    """the end-of-stream agreement runs once per ``agree_interval`` rounds (0 =
+    never during the run) and the iteration still stops when the shortest stream ends."""
+    counts = [10, 10] if k == 0 else [10, 7]
+    res = run_spmd(_spmd_unbounded_agree, 2, k, counts)
+    n = min(counts)
+    for rank, (out, calls) in enumerate(res):
+        assert len(out) == n
+        assert out[-1] == sum(rank * 100 + i for i in range(n))
+        if k == 1:
+            assert calls == n + 1
+        elif k == 4:
+            assert calls == -(-n // 4) + (1 if n % 4 == 0 else 0)
+        else:
+            assert calls == 2  # the final min/max check of the round counts

@@ -415,3 +415,18 @@ def test_label_cache_tracks_base_identity_and_version():
     y2 = torch.arange(10, 20, dtype=torch.float64)
     t2 = Table({"features": X, "label": y2})
     assert tr._labels(t2.slice(0, 2)).tolist() == [10.0, 11.0]
+
+
+def test_model_data_stream_after_version_eviction(monkeypatch):
+    """once more versions exist than the log retains, get_model_data must
+    start at the oldest retained version instead of raising IndexError."""
+    monkeypatch.setenv("FMLX_MODEL_VERSIONS_KEEP", "2")
+    init = Table.from_rows([(Vectors.dense(0.0, 0.0), 0)], ["coefficient", "modelVersion"])
+    rows = (TRAIN1 + TRAIN2) * 4  # 8 batches of 10
+    model = (OnlineLogisticRegression().set_global_batch_size(10).set_initial_model_data(init)
+             .fit(Table.from_rows(rows, ["features", "label"])))
+    pred = Table.from_rows(PREDICT, ["features", "label"])
+    model.transform(pred)  # drains the stream: versions 1..8 (only the last 2 retained)
+    out = list(model.get_model_data()[0])
+    versions = [int(t.rows()[0][1]) for t in out]
+    assert versions == sorted(versions) and versions[-1] == 8 and len(versions) == 2
