@@ -48,9 +48,15 @@ def reservoir_sample_indices(n: int, k: int, seed: int) -> np.ndarray:
 def sample_rows(X: torch.Tensor, k: int, seed: int) -> np.ndarray:
     """``DataStreamUtils.sample``: reservoir per rank (only the k chosen rows leave the device),
     gather in rank order, reservoir again over the union."""
-    idx = reservoir_sample_indices(int(X.shape[0]), k, seed)
-    local = X[torch.as_tensor(idx, device=X.device)].to(torch.float64).cpu().numpy() if len(idx) else np.zeros(
-        (0, X.shape[1]))
+    if X.device.type == "cuda":
+        # the n-long draw stream in parallel on the device (bit-exact; ops/datagen.py); only the
+        # k chosen rows leave HBM
+        from ..ops.datagen import reservoir_sample_device
+
+        idx = reservoir_sample_device(int(X.shape[0]), k, seed, X.device)
+    else:
+        idx = torch.as_tensor(reservoir_sample_indices(int(X.shape[0]), k, seed))
+    local = X[idx.to(X.device)].to(torch.float64).cpu().numpy() if len(idx) else np.zeros((0, X.shape[1]))
     gathered = comm.all_gather_object(local)
     allrows = np.concatenate([g for g in gathered if g.shape[0] > 0], axis=0) if any(
         g.shape[0] for g in gathered) else np.zeros((0, X.shape[1]))

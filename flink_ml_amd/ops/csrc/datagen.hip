@@ -152,6 +152,28 @@ __global__ __launch_bounds__(256) void java_int_draws_kernel(unsigned long long 
 }
 }  // namespace
 
+namespace {
+// Raw next(31) values at consecutive sequence positions [start, start + count), 16 per thread
+// after one jump-ahead (the device reservoir sampler's draw stream, ops/datagen.py).
+__global__ __launch_bounds__(256) void java_next31_kernel(unsigned long long x0, unsigned long long start, long count,
+                                                          int* __restrict__ u_out) {
+  const long base = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (base >= count) return;
+  unsigned long long s = jump(x0, start + (unsigned long long)base);
+  const long end = base + 16 < count ? base + 16 : count;
+  for (long p = base; p < end; ++p) u_out[p] = next_bits(s, 31);
+}
+}  // namespace
+
+FMLX_API int fmlx_java_next31(unsigned long long seed, unsigned long long start, long count, int* u_out,
+                              void* stream) {
+  if (count <= 0) return 0;
+  const long threads = (count + 15) / 16;
+  hipLaunchKernelGGL(java_next31_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     seed, start, count, u_out);
+  return (int)hipGetLastError();
+}
+
 // seed: the scrambled Random state; see java_int_draws_kernel.
 FMLX_API int fmlx_java_int_draws(unsigned long long seed, unsigned long long start, long count, int bound, int* r_out,
                                  unsigned char* ok_out, void* stream) {

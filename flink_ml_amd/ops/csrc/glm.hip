@@ -150,6 +150,7 @@ struct GlmTail {
   int dyn_lg;      // log2(rows per chunk)
   int dyn_sync;    // diagnostics: vmcnt(0) before a claim's result is read
   int* dyn_dbg;    // diagnostics (null = off): per batch-row visit counters of the dynamic schedule
+  int* dyn_dbg2;   // diagnostics (null = off): per (block, wave) {exit q, walk steps, caps, exh, inflight, lastv, 0, 0}
 };
 constexpr int ACC_MAX_REPS = 8;
 
@@ -913,21 +914,12 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
       }
       return (long)__builtin_amdgcn_readfirstlane((int)(v & 0xffffffffLL));
     };
-    // the next chunk with rows at or after q (q advanced past empty ones; −1: the block is done).
-    // Wave q mod WPB publishes q + DYN_L for every q it passes (−1 once nothing can be claimed).
-    int claim_q = -1, claim_h = 0;
-    auto walk = [&](int& q) -> long {
-      for (int spin = 0;; ++spin) {
-        const long c = chunk_of(q);
-        if (c >= 0) return c;
-        if (c == -2 || done_at(q) || spin > (1 << 20)) return -1;
-        if ((q & (WPB - 1)) == wave) put(q + DYN_L, -1);  // exh is set: every −1 follows it
-        ++q;
-      }
-    };
+    int claim_q = -1, claim_h = 0, claim_t = 0;
+    int dbg_steps = 0, dbg_caps = 0;
     // claim for chunk q + DYN_L if this wave owns q (issued before the iteration's row loads)
-    auto claim_issue = [&](int q, int& t) {
+    auto claim_issue = [&](int q) {
       claim_q = -1;
+      claim_t = 0;
       if ((q & (WPB - 1)) != wave) return;
       lds_add(&D->inflight, 1);  // before reading exh (see the termination note)
       if (lds_ld(&D->exh)) {
@@ -937,17 +929,35 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
       }
       claim_q = q + DYN_L;
       claim_h = lds_ld(&D->head);
-      if (lane == 0) t = __hip_atomic_fetch_add(&heads[claim_h * DYN_HSTRIDE], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0)
+        claim_t = __hip_atomic_fetch_add(&heads[claim_h * DYN_HSTRIDE], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
-    auto claim_publish = [&](int t) {
+    auto claim_publish = [&]() {
       if (claim_q < 0) return;
       if (tl.dyn_sync) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-      long cn = lo_of(claim_h) + __builtin_amdgcn_readfirstlane(t);
+      long cn = lo_of(claim_h) + __builtin_amdgcn_readfirstlane(claim_t);
       if (cn >= hi_of(claim_h)) cn = steal();
       put(claim_q, cn);
       if (cn >= 0 && lane == 0)
         __hip_atomic_fetch_max(&D->lastv, claim_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       lds_add(&D->inflight, -1);  // after the publication and lastv
+      claim_q = -1;
+    };
+    // the next chunk with rows at or after q (q advanced past empty ones; −1: the block is done).
+    // Wave q mod WPB publishes q + DYN_L for every q it passes (−1 once nothing can be claimed).
+    // A walk past empty chunks can reach the slot of this wave's own unpublished claim: it is
+    // published first (otherwise the wave waits on itself, and done_at counts the claim in flight).
+    auto walk = [&](int& q) -> long {
+      for (int spin = 0;; ++spin) {
+        if (q == claim_q) claim_publish();
+        const long c = chunk_of(q);
+        if (c >= 0) return c;
+        ++dbg_steps;
+        if (c == -2) ++dbg_caps;
+        if (c == -2 || done_at(q) || spin > (1 << 20)) return -1;
+        if ((q & (WPB - 1)) == wave) put(q + DYN_L, -1);  // exh is set: every −1 follows it
+        ++q;
+      }
     };
     // row j of chunk c for this wave (c < 0 or past `end`: `rsafe` again, masked)
     auto load_j = [&](long c, int j, long rsafe, Chunk<T, EPC> (&dst)[1][CPL], A (&yy)[1], A (&ww)[1],
@@ -983,8 +993,7 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
       while (true) {
         // xa: row 0 of chunk c (in flight). The claim is issued and consumed inside this
         // iteration: before row 1's loads, after row 0 of the next chunk went out
-        int t = 0;
-        claim_issue(q, t);
+        claim_issue(q);
         const long rs = start + c * CH + wave < end ? start + c * CH + wave : start;
         load_j(c, 1, rs, xb, yb, wb, vb);
         asm volatile("" ::: "memory");
@@ -996,11 +1005,23 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         process(xb, yb, wb, vb);
-        claim_publish(t);
-        if (cn < 0) break;
+        claim_publish();
+        if (cn < 0) {
+          q = qn;
+          break;
+        }
         q = qn;
         c = cn;
       }
+    }
+    if (tl.dyn_dbg2 && lane == 0) {
+      int* o = tl.dyn_dbg2 + ((long)blockIdx.x * WPB + wave) * 8;
+      o[0] = q;
+      o[1] = dbg_steps;
+      o[2] = dbg_caps;
+      o[3] = __hip_atomic_load(&D->exh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      o[4] = __hip_atomic_load(&D->inflight, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      o[5] = __hip_atomic_load(&D->lastv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
   if (!dyn_done) {
@@ -1605,6 +1626,7 @@ static int g_dyn = 1;       // dynamic row schedule (A/B knob)
 static int g_dyn_lg = 3;    // log2(rows per claimed chunk), >= log2(WPB)
 static int g_dyn_sync = 0;
 static int* g_dyn_dbg = nullptr;
+static int* g_dyn_dbg2 = nullptr;
 constexpr long LDS_PER_CU = 160 * 1024;
 constexpr int NUM_CU = 256;
 
@@ -1768,6 +1790,7 @@ FMLX_API void fmlx_glm_set_dyn_debug(int sync, void* dbg) {
   g_dyn_sync = sync;
   g_dyn_dbg = (int*)dbg;
 }
+FMLX_API void fmlx_glm_set_dyn_debug2(void* dbg2) { g_dyn_dbg2 = (int*)dbg2; }
 
 // ints of the fused round's counter block: tickets (TAIL_TOP + 1, padded to 128) + the dynamic
 // schedule's [2][DYN_HEADS][DYN_HSTRIDE] chunk counters
@@ -1829,6 +1852,7 @@ FMLX_API int fmlx_glm_round(int dtype, int epc, int cpl, int u, const void* X, l
   tl.trace = g_trace;
   tl.dyn_sync = g_dyn_sync;
   tl.dyn_dbg = g_dyn_dbg;
+  tl.dyn_dbg2 = g_dyn_dbg2;
   tl.heads = (flags & 2) && cnt ? cnt + 128 : nullptr;  // flags bit 1: cnt has fmlx_glm_cnt_elems ints
   // `rounds` consecutive rounds, one launch each (a kernel boundary, ~1.5 µs, is cheaper than an
   // in-kernel grid-wide round barrier: measured, scripts/stream_probe2.hip)

@@ -61,6 +61,37 @@ int fmlx_reservoir_sample(int64_t n, int32_t k, int64_t seed, int64_t* out) {
   return (int)filled;
 }
 
+// The sequential part of the device reservoir sampler (ops/datagen.py reservoir_sample_device):
+// draw i (i = k .. n-1) is Random.nextInt(i + 1) on the stream after the draws before it. A
+// position p of the raw next(31) stream can only be a rejected draw if u_p ≥ 2^31 − n (for
+// every bound b ≤ n, u < 2^31 − b + 1 is accepted), so only those "candidates" are scanned here,
+// in order: the draw at p is i = p + k − R with R the rejections before p; it is rejected iff b is
+// not a power of two and u − u % b + b − 1 ≥ 2^31. Writes the rejected positions (ascending) to
+// rej and returns their count; *done receives 1 if the scan proved that draw n − 1 happens before
+// position `npos` (the generated stream was long enough), else 0.
+int64_t fmlx_reservoir_rejections(int64_t n, int32_t k, int64_t npos, const int64_t* cand_p, const int32_t* cand_u,
+                                  int64_t ncand, int64_t* rej, int32_t* done) {
+  int64_t R = 0;
+  for (int64_t c = 0; c < ncand; ++c) {
+    const int64_t p = cand_p[c];
+    const int64_t i = p + k - R;
+    if (i >= n) break;
+    const int64_t b = i + 1;
+    if ((b & (b - 1)) == 0) continue;
+    const int64_t u = cand_u[c];
+    if (u - u % b + b - 1 >= (1LL << 31)) rej[R++] = p;
+  }
+  // the last draw (i = n − 1) sits at position n − 1 − k + R; it must be inside the stream
+  *done = (n - 1 - k + R) < npos ? 1 : 0;
+  return R;
+}
+
+void fmlx_java_next31(int64_t seed, int64_t start, int64_t n, int32_t* out) {
+  JRandom rnd(seed);
+  for (int64_t i = 0; i < start; ++i) rnd.next(31);
+  for (int64_t i = 0; i < n; ++i) out[i] = rnd.next(31);
+}
+
 void fmlx_java_next_doubles(int64_t seed, int64_t n, double* out) {
   JRandom rnd(seed);
   for (int64_t i = 0; i < n; ++i) out[i] = rnd.next_double();

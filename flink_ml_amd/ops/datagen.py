@@ -204,3 +204,93 @@ def java_rows(seed: int, n: int, ops: Sequence[int], nvec: int, device=None, vec
         start += bad * dpr + used
         row0 = r + 1
     return torch.from_numpy(vec_np).to(vec_dtype), torch.from_numpy(scal_np)
+
+
+# ---------------------------------------------------------------------------------------------
+# reservoir sampling (DataStreamUtils.SamplingOperator, DataStreamUtils.java:633-704) on device
+# ---------------------------------------------------------------------------------------------
+native.register_kernel_sigs({
+    "fmlx_java_next31": [native.c_ulonglong, native.c_ulonglong, c_long, c_void_p, c_void_p],
+})
+_host_sigs_done = False
+
+
+def _host_sigs():
+    global _host_sigs_done
+    if not _host_sigs_done:
+        import ctypes
+
+        native.register_host_sigs({
+            "fmlx_reservoir_rejections": ([ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p],
+                                          ctypes.c_int64),
+            "fmlx_java_next31": [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p],
+        })
+        _host_sigs_done = True
+
+
+def next31_stream(seed: int, start: int, count: int, device) -> torch.Tensor:
+    """Raw ``next(31)`` values of ``new Random(seed)`` at positions [start, start + count) (int32)."""
+    out = torch.empty(max(int(count), 0), dtype=torch.int32, device=device)
+    if count <= 0:
+        return out
+    if out.device.type == "cuda":
+        native.call("fmlx_java_next31", scramble(seed), int(start), int(count), native.ptr(out),
+                    native.stream_ptr(out.device))
+    else:
+        _host_sigs()
+        native.host().fmlx_java_next31(int(seed), int(start), int(count), out.data_ptr())
+    return out
+
+
+def reservoir_sample_device(n: int, k: int, seed: int, device) -> torch.Tensor:
+    """Positions ``SamplingOperator`` keeps (a java.util.Random(seed) reservoir of size k over n
+    elements), in reservoir-slot order — bit-exact with the sequential sampler
+    (``javarand.cpp fmlx_reservoir_sample``), but with the n-long draw stream on the device:
+
+      1. draw i (i = k .. n−1) is ``nextInt(i + 1)``; without rejections it reads stream position
+         p = i − k. The raw next(31) stream is generated in parallel (jump-ahead, datagen.hip);
+      2. only positions with u ≥ 2^31 − n can be rejected draws (≈ n / 2^31 of them); those
+         candidates are scanned in order on the host (``fmlx_reservoir_rejections``) — the only
+         sequential step, over a few percent of the stream;
+      3. every position p then knows its draw i = p + k − R(p) (R = rejections before p), and the
+         slot it writes; the last writer of every slot wins (a max-reduction by i).
+    Returns int64 [min(n, k)] on ``device``."""
+    n, k = int(n), int(k)
+    dev = torch.device(device)
+    if n <= 0 or k <= 0:
+        return torch.zeros(0, dtype=torch.int64, device=dev)
+    if n <= k:
+        return torch.arange(n, dtype=torch.int64, device=dev)
+    _host_sigs()
+    m = n - k
+    npos = m + m * n // (1 << 31) + 65536
+    while True:
+        u = next31_stream(seed, 0, npos, dev)
+        thr = (1 << 31) - n
+        cand = torch.nonzero(u >= thr).view(-1)
+        cand_p = cand.to(torch.int64).cpu().numpy()
+        cand_u = u[cand].cpu().numpy().astype(np.int32)
+        rej = np.zeros(max(len(cand_p), 1), dtype=np.int64)
+        done = np.zeros(1, dtype=np.int32)
+        nrej = int(native.host().fmlx_reservoir_rejections(n, k, npos, cand_p.ctypes.data, cand_u.ctypes.data,
+                                                           len(cand_p), rej.ctypes.data, done.ctypes.data))
+        if done[0]:
+            break
+        npos = npos * 3 // 2  # the stream ran out before the last draw: regenerate longer
+    end = m + nrej  # positions consumed by draws k .. n−1
+    u = u[:end].to(torch.int64)
+    p = torch.arange(end, dtype=torch.int64, device=dev)
+    rejt = torch.as_tensor(rej[:nrej], dtype=torch.int64, device=dev)
+    R = torch.searchsorted(rejt, p) if nrej else torch.zeros_like(p)
+    ok = torch.ones(end, dtype=torch.bool, device=dev)
+    if nrej:
+        ok[rejt] = False
+    i = p + k - R
+    b = i + 1
+    pow2 = (b & (b - 1)) == 0
+    slot = torch.where(pow2, (b * u) >> 31, u % b)
+    sel = ok & (slot < k)
+    out = torch.arange(k, dtype=torch.int64, device=dev)
+    out.scatter_reduce_(0, slot[sel], i[sel], "amax")
+    return out

@@ -46,8 +46,13 @@ def set_tail_tuning(acc_reps: int = 4, ticket2: bool = False) -> None:
 
 
 # deferred fused rounds: dynamic row schedule (csrc/glm.hip DynLds) instead of the static row
-# stride; FMLX_GLM_DYN=1/0 (the process-wide default, applied when the first round scratch is made)
-DYN_DEFAULT = os.environ.get("FMLX_GLM_DYN", "1") == "1"
+# stride; FMLX_GLM_DYN=1/0 (the process-wide default, applied when the first round scratch is made).
+# Off by default: exact (every row once, profiles/r3/lr_dyn_schedule_row_census.jsonl) but slower at
+# the flagship shape — 56.2 vs 39.6 µs per round (profiles/r3/lr_dyn_schedule_ab_1gpu.jsonl): the
+# chunk claims' device-scope atomics return in microseconds under full HBM streaming, and the
+# claiming wave waits for them once per chunk it owns, which costs more than the XCD imbalance
+# (≈4 µs) the schedule removes.
+DYN_DEFAULT = os.environ.get("FMLX_GLM_DYN", "0") == "1"
 _dyn_set = False
 
 
