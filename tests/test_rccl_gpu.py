@@ -131,8 +131,8 @@ def _online_fit():
     while n < 6 and stream.pull(block=True):
         n += 1
     stream.flush()
-    rows = model.get_model_data()[0].rows()
-    return np.asarray(rows[-1][0].values), n
+    ver = model.model_data_rows()[0]  # (coefficient, modelVersion) of the newest version
+    return np.asarray(ver[0].values, dtype=np.float64), n
 
 
 def test_kmeans_and_online_lr_on_rccl():
