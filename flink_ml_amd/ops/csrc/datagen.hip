@@ -165,6 +165,48 @@ __global__ __launch_bounds__(256) void java_next31_kernel(unsigned long long x0,
 }
 }  // namespace
 
+namespace {
+// Final pass of the device reservoir sampler: position p of the draw stream (not rejected) is the
+// accepted draw of element i = p + k − R(p), R(p) = rejected positions before p (rej: ascending);
+// it writes slot nextInt-result if that is < k. The last writer of a slot wins: atomicMax over i.
+// The stream is regenerated by jump-ahead (16 positions per thread), not read back.
+__global__ __launch_bounds__(256) void reservoir_final_kernel(unsigned long long x0, long end, int k,
+                                                              const long* __restrict__ rej, long nrej,
+                                                              int* __restrict__ out) {
+  const long base = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (base >= end) return;
+  long lo = 0, hi = nrej;  // R(base) = lower_bound(rej, base)
+  while (lo < hi) {
+    const long mid = (lo + hi) >> 1;
+    if (rej[mid] < base) lo = mid + 1; else hi = mid;
+  }
+  long R = lo;
+  unsigned long long s = jump(x0, (unsigned long long)base);
+  const long stop = base + 16 < end ? base + 16 : end;
+  for (long p = base; p < stop; ++p) {
+    const long long u = next_bits(s, 31);
+    if (R < nrej && rej[R] == p) {  // a rejected draw: the same element draws again at p + 1
+      ++R;
+      continue;
+    }
+    const long i = p + k - R;
+    const long b = i + 1;
+    const long slot = (b & (b - 1)) == 0 ? (long)((b * u) >> 31) : (long)(u % b);
+    if (slot < k) atomicMax(&out[slot], (int)i);
+  }
+}
+}  // namespace
+
+// out: int32[k], preset to 0 .. k − 1 (the reservoir's initial fill)
+FMLX_API int fmlx_reservoir_final(unsigned long long seed, long end, int k, const long* rej, long nrej, int* out,
+                                  void* stream) {
+  if (end <= 0) return 0;
+  const long threads = (end + 15) / 16;
+  hipLaunchKernelGGL(reservoir_final_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     seed, end, k, rej, nrej, out);
+  return (int)hipGetLastError();
+}
+
 FMLX_API int fmlx_java_next31(unsigned long long seed, unsigned long long start, long count, int* u_out,
                               void* stream) {
   if (count <= 0) return 0;

@@ -69,17 +69,30 @@ int fmlx_reservoir_sample(int64_t n, int32_t k, int64_t seed, int64_t* out) {
 // not a power of two and u − u % b + b − 1 ≥ 2^31. Writes the rejected positions (ascending) to
 // rej and returns their count; *done receives 1 if the scan proved that draw n − 1 happens before
 // position `npos` (the generated stream was long enough), else 0.
-int64_t fmlx_reservoir_rejections(int64_t n, int32_t k, int64_t npos, const int64_t* cand_p, const int32_t* cand_u,
+int64_t fmlx_reservoir_rejections(int64_t n, int32_t k, int64_t npos, const int32_t* cand_p, const int32_t* cand_u,
                                   int64_t ncand, int64_t* rej, int32_t* done) {
+  // The decision for a candidate depends on R through its bound; the dependency chain through
+  // R would put a division on every step's critical path. Instead the next candidate's decision is
+  // computed for both values R can take there (R, R + 1) while this one's is resolved — two
+  // independent 32-bit divisions per step off the chain, one select on it (u < 2^31 and
+  // b ≤ n < 2^31 keep everything in 32 bits).
+  auto dec = [&](int64_t c, int64_t R) -> int {
+    const uint32_t b = (uint32_t)((int64_t)cand_p[c] + k - R + 1);
+    const uint32_t u = (uint32_t)cand_u[c];
+    return ((b & (b - 1)) != 0) & ((uint64_t)(u - u % b) + b - 1 >= (1ULL << 31));
+  };
   int64_t R = 0;
+  int d = ncand > 0 ? dec(0, 0) : 0;
   for (int64_t c = 0; c < ncand; ++c) {
-    const int64_t p = cand_p[c];
-    const int64_t i = p + k - R;
-    if (i >= n) break;
-    const int64_t b = i + 1;
-    if ((b & (b - 1)) == 0) continue;
-    const int64_t u = cand_u[c];
-    if (u - u % b + b - 1 >= (1LL << 31)) rej[R++] = p;
+    if ((int64_t)cand_p[c] + k - R >= n) break;
+    int n0 = 0, n1 = 0;
+    if (c + 1 < ncand) {
+      n0 = dec(c + 1, R);
+      n1 = dec(c + 1, R + 1);
+    }
+    rej[R] = cand_p[c];  // kept only if d (R advances)
+    R += d;
+    d = d ? n1 : n0;
   }
   // the last draw (i = n − 1) sits at position n − 1 − k + R; it must be inside the stream
   *done = (n - 1 - k + R) < npos ? 1 : 0;

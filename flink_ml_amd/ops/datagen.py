@@ -211,6 +211,7 @@ def java_rows(seed: int, n: int, ops: Sequence[int], nvec: int, device=None, vec
 # ---------------------------------------------------------------------------------------------
 native.register_kernel_sigs({
     "fmlx_java_next31": [native.c_ulonglong, native.c_ulonglong, c_long, c_void_p, c_void_p],
+    "fmlx_reservoir_final": [native.c_ulonglong, c_long, c_int, c_void_p, c_long, c_void_p, c_void_p],
 })
 _host_sigs_done = False
 
@@ -267,10 +268,14 @@ def reservoir_sample_device(n: int, k: int, seed: int, device) -> torch.Tensor:
     npos = m + m * n // (1 << 31) + 65536
     while True:
         u = next31_stream(seed, 0, npos, dev)
-        thr = (1 << 31) - n
-        cand = torch.nonzero(u >= thr).view(-1)
-        cand_p = cand.to(torch.int64).cpu().numpy()
-        cand_u = u[cand].cpu().numpy().astype(np.int32)
+        # position p can only hold a rejected draw if u_p ≥ 2^31 − b for its bound b ≤ p + k + 1
+        # (b shrinks with the rejections before p): ≈ half as many candidates as u ≥ 2^31 − n
+        pos = torch.arange(npos, dtype=torch.int64, device=dev)
+        cand = torch.nonzero(u.to(torch.int64) + pos >= (1 << 31) - k - 1).view(-1)
+        del pos
+        both = torch.stack([cand.to(torch.int32), u[cand]])  # one D2H copy of [positions | values]
+        both = both.cpu().numpy()
+        cand_p, cand_u = np.ascontiguousarray(both[0]), np.ascontiguousarray(both[1])
         rej = np.zeros(max(len(cand_p), 1), dtype=np.int64)
         done = np.zeros(1, dtype=np.int32)
         nrej = int(native.host().fmlx_reservoir_rejections(n, k, npos, cand_p.ctypes.data, cand_u.ctypes.data,
@@ -279,6 +284,16 @@ def reservoir_sample_device(n: int, k: int, seed: int, device) -> torch.Tensor:
             break
         npos = npos * 3 // 2  # the stream ran out before the last draw: regenerate longer
     end = m + nrej  # positions consumed by draws k .. n−1
+    if dev.type == "cuda":
+        # one fused pass: the stream regenerated by jump-ahead, R(p) by binary search, atomicMax
+        # per slot (no n-long int64 temporaries)
+        del u
+        rejt = torch.as_tensor(rej[:nrej], dtype=torch.int64).to(dev) if nrej else torch.zeros(1, dtype=torch.int64,
+                                                                                               device=dev)
+        out32 = torch.arange(k, dtype=torch.int32, device=dev)
+        native.call("fmlx_reservoir_final", scramble(seed), end, k, native.ptr(rejt), nrej, native.ptr(out32),
+                    native.stream_ptr(dev))
+        return out32.to(torch.int64)
     u = u[:end].to(torch.int64)
     p = torch.arange(end, dtype=torch.int64, device=dev)
     rejt = torch.as_tensor(rej[:nrej], dtype=torch.int64, device=dev)

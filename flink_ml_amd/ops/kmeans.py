@@ -32,7 +32,14 @@ native.register_kernel_sigs({
     "fmlx_sort_pairs": [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_long, c_void_p],
     "fmlx_kmeans_finalize": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                              c_void_p],
+    "fmlx_group_max_keys": [],
+    "fmlx_group_by_key": [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
 })
+
+# rows grouped by cluster with the hand-written counting sort (csrc/groupsort.hip: three launches,
+# order inside a cluster from atomic arrival) unless FMLX_DETERMINISTIC=1 asks for bit-reproducible
+# centroids (the stable radix sort of sort.hip)
+GROUP_SORT = os.environ.get("FMLX_DETERMINISTIC", "0") != "1"
 
 METRICS = {"euclidean": 0, "manhattan": 1, "cosine": 2}
 CHUNK = 256
@@ -202,18 +209,23 @@ class KMeansRound:
         self.zero_i64 = torch.zeros(1, dtype=torch.int64, device=dev)
         self.fast = (dev.type == "cuda" and X.dtype == torch.bfloat16 and self.D in (8, 16, 32, 64, 128, 256, 512)
                      and X.stride(1) == 1 and X.stride(0) % 8 == 0 and X.data_ptr() % 16 == 0)
+        self.group = dev.type == "cuda" and GROUP_SORT and k <= native.kernels().fmlx_group_max_keys()
         if dev.type == "cuda":
+            self.offsets = torch.zeros(k + 1, dtype=torch.int64, device=dev)
+            self.chunk_off = torch.zeros(k + 1, dtype=torch.int64, device=dev)
+            self.order32 = torch.empty(self.n, dtype=torch.int32, device=dev)
+        if self.group:
+            self.gcounts = torch.zeros(k, dtype=torch.int32, device=dev)  # re-zeroed by the scan kernel
+            self.gcursor = torch.zeros(k, dtype=torch.int32, device=dev)
+        elif dev.type == "cuda":
             # stable radix sort of the labels over ceil(log2 k) bits (not a 64-bit argsort)
             self.bits = max(1, int(k - 1).bit_length())
             self.iota = torch.arange(self.n, dtype=torch.int32, device=dev)
             self.keys_sorted = torch.empty(self.n, dtype=torch.int32, device=dev)
-            self.order32 = torch.empty(self.n, dtype=torch.int32, device=dev)
             tb = native.kernels().fmlx_sort_pairs_temp_bytes(self.n, self.bits)
             if tb < 0:
                 raise RuntimeError("radix sort temp-size query failed")
             self.sort_temp = torch.empty(max(int(tb), 1), dtype=torch.uint8, device=dev)
-            self.offsets = torch.zeros(k + 1, dtype=torch.int64, device=dev)
-            self.chunk_off = torch.zeros(k + 1, dtype=torch.int64, device=dev)
 
     def run(self, cb: CentroidBuffers) -> torch.Tensor:
         X = self.X
@@ -222,12 +234,18 @@ class KMeansRound:
             return self.payload
         assign(X, cb, self.metric, self.labels)
         stream = native.stream_ptr(X.device)
-        native.call("fmlx_sort_pairs", native.ptr(self.labels), native.ptr(self.keys_sorted), native.ptr(self.iota),
-                    native.ptr(self.order32), self.n, self.bits, native.ptr(self.sort_temp), self.sort_temp.numel(),
-                    stream)
-        # cluster boundaries on the device (no host sync: the round is hipGraph-capturable)
-        native.call("fmlx_kmeans_offsets", native.ptr(self.keys_sorted), self.n, self.k, native.ptr(self.offsets),
-                    native.ptr(self.chunk_off), stream)
+        if self.group:
+            # counting sort by cluster + cluster / chunk offsets, no library sort (groupsort.hip)
+            native.call("fmlx_group_by_key", native.ptr(self.labels), self.n, self.k, CHUNK, native.ptr(self.gcounts),
+                        native.ptr(self.gcursor), native.ptr(self.offsets), native.ptr(self.chunk_off),
+                        native.ptr(self.order32), stream)
+        else:
+            native.call("fmlx_sort_pairs", native.ptr(self.labels), native.ptr(self.keys_sorted), native.ptr(self.iota),
+                        native.ptr(self.order32), self.n, self.bits, native.ptr(self.sort_temp),
+                        self.sort_temp.numel(), stream)
+            # cluster boundaries on the device (no host sync: the round is hipGraph-capturable)
+            native.call("fmlx_kmeans_offsets", native.ptr(self.keys_sorted), self.n, self.k, native.ptr(self.offsets),
+                        native.ptr(self.chunk_off), stream)
         offsets, chunk_off = self.offsets, self.chunk_off
         if self.fast:
             native.call("fmlx_kmeans_chunk_sum_bf16v", native.ptr(X), X.stride(0), self.D, native.ptr(self.order32),
@@ -269,3 +287,22 @@ def torch_finalize(payload: torch.Tensor, k: int, D: int):
     counts = payload[k * D:]
     cent = sums * (1.0 / counts)[:, None]  # scal(1/count): 0 rows → NaN like the reference
     return cent, counts
+
+
+def group_by_key(keys: torch.Tensor, k: int, chunk: int = 0):
+    """Rows grouped by an int32 key in [0, k) on the device (csrc/groupsort.hip counting sort):
+    returns (order int32 [m], offsets int64 [k + 1], chunk_off int64 [k + 1] or None), where
+    ``order[offsets[c]:offsets[c+1]]`` are the rows with key c (order inside a key unspecified) and
+    m = offsets[k] (keys outside [0, k) are dropped). k ≤ ``fmlx_group_max_keys()``."""
+    dev = keys.device
+    n = keys.numel()
+    keys = keys.to(torch.int32).contiguous()
+    counts = torch.zeros(k, dtype=torch.int32, device=dev)
+    cursor = torch.empty(k, dtype=torch.int32, device=dev)
+    offsets = torch.empty(k + 1, dtype=torch.int64, device=dev)
+    chunk_off = torch.empty(k + 1, dtype=torch.int64, device=dev) if chunk > 0 else None
+    order = torch.empty(n, dtype=torch.int32, device=dev)
+    native.call("fmlx_group_by_key", native.ptr(keys), n, int(k), int(chunk), native.ptr(counts), native.ptr(cursor),
+                native.ptr(offsets), native.ptr(chunk_off), native.ptr(order), native.stream_ptr(dev))
+    m = int(offsets[k].item())
+    return order[:m], offsets, chunk_off

@@ -164,12 +164,16 @@ def test_gpu_assign_generic(dtype, metric):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("det", [False, True])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32, torch.float64])
-def test_gpu_round_payload_matches_torch(dtype):
+def test_gpu_round_payload_matches_torch(dtype, det, monkeypatch):
+    """One round's [sums | counts] against torch; FMLX_DETERMINISTIC's stable radix grouping is
+    bit-reproducible, the default counting sort reproducible to rounding (exact counts)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from flink_ml_amd.ops import kmeans as kk
 
+    monkeypatch.setattr(kk, "GROUP_SORT", not det)
     g = torch.Generator().manual_seed(2)
     n, D, k = 20000, 100, 10
     X = torch.rand((n, D), generator=g, dtype=torch.float64).to(dtype)
@@ -178,9 +182,13 @@ def test_gpu_round_payload_matches_torch(dtype):
     cb = kk.CentroidBuffers(k, D, torch.device("cuda"), acc)
     cb.set(C)
     rnd = kk.KMeansRound(X.cuda(), k, "euclidean")
+    assert rnd.group == (not det)
     p1 = rnd.run(cb).clone()
     p2 = rnd.run(cb).clone()
-    assert torch.equal(p1, p2)  # deterministic
+    if det:
+        assert torch.equal(p1, p2)  # bit-reproducible
+    else:
+        assert torch.equal(p1[k * D:], p2[k * D:]) and torch.allclose(p1, p2, rtol=1e-6, atol=1e-4)
     lab = rnd.labels.cpu().long()
     ref_sums = torch.zeros((k, D), dtype=torch.float64).index_add_(0, lab, X.to(torch.float64))
     ref_cnt = torch.bincount(lab, minlength=k).double()
@@ -323,3 +331,36 @@ def test_gpu_round_offsets_with_empty_clusters():
     assert torch.equal(rnd.chunk_off.cpu(), torch.cat([torch.zeros(1, dtype=torch.int64), ch.cumsum(0)]))
     sums = torch.zeros((k, D), dtype=torch.float64).index_add_(0, lab, X.double())
     assert torch.allclose(p[: k * D].reshape(k, D), sums, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k", [(1, 1), (1000, 7), (3_000_001, 1024), (200_000, 16384)])
+def test_group_by_key_counting_sort(n, k):
+    """The KMeans grouping kernel (csrc/groupsort.hip) against torch: every row once, grouped by
+    key, offsets = cumulative counts, chunk offsets = cumulative ceil(count / 256); empty keys,
+    one huge key (half the rows) and keys outside [0, k) (dropped)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from flink_ml_amd.ops import kmeans as kk
+
+    g = torch.Generator(device="cpu").manual_seed(n + k)
+    keys = torch.randint(0, max(k // 2, 1), (n,), generator=g, dtype=torch.int32) * 2  # odd keys empty
+    keys[: n // 2] = k - 1 if k > 1 else 0  # one huge cluster
+    if n > 10:
+        keys[3] = -1
+        keys[5] = k  # out of range: dropped
+    order, offsets, chunk_off = kk.group_by_key(keys.cuda(), k, 256)
+    valid = (keys >= 0) & (keys < k)
+    counts = torch.bincount(keys[valid].long(), minlength=k)
+    exp_off = torch.zeros(k + 1, dtype=torch.int64)
+    exp_off[1:] = torch.cumsum(counts, 0)
+    assert torch.equal(offsets.cpu(), exp_off)
+    exp_chk = torch.zeros(k + 1, dtype=torch.int64)
+    exp_chk[1:] = torch.cumsum((counts + 255) // 256, 0)
+    assert torch.equal(chunk_off.cpu(), exp_chk)
+    o = order.cpu().long()
+    assert torch.equal(torch.sort(o).values, torch.nonzero(valid).view(-1))  # a permutation of the valid rows
+    assert torch.all(keys[o][1:] >= keys[o][:-1])  # grouped by key
+    # second call reuses the re-zeroed counts (the hipGraph replay contract)
+    order2, offsets2, _ = kk.group_by_key(keys.cuda(), k, 256)
+    assert torch.equal(offsets2.cpu(), exp_off)
