@@ -151,7 +151,15 @@ struct GlmTail {
   int dyn_sync;    // diagnostics: vmcnt(0) before a claim's result is read
   int* dyn_dbg;    // diagnostics (null = off): per batch-row visit counters of the dynamic schedule
   int* dyn_dbg2;   // diagnostics (null = off): per (block, wave) {exit q, walk steps, caps, exh, inflight, lastv, 0, 0}
+  int rowmap;      // static schedule: block → row-stripe mapping (ROWMAP_*)
 };
+// Static row schedule: wave slot gw of the W = NB·WPB slots reads rows start + gw + j·W.
+//  ROWMAP_BLOCK: gw = b·WPB + wave — the blocks of one XCD (b mod 8 under round-robin dispatch)
+//                read 16-KB pieces 128 KB apart of every 8-MB stripe;
+//  ROWMAP_XCD:   gw = (b mod 8 · NB/8 + b / 8)·WPB + wave — each XCD reads one contiguous
+//                1/8 of every stripe (its 64 blocks side by side);
+//  ROWMAP_WAVE:  gw = wave·NB + b — a block's waves read rows NB apart.
+enum { ROWMAP_BLOCK = 0, ROWMAP_XCD = 1, ROWMAP_WAVE = 2 };
 constexpr int ACC_MAX_REPS = 8;
 
 // ------------------------------------------------------------------------------------------
@@ -527,7 +535,13 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nch = d / EPC;
   const long W = (long)gridDim.x * WPB;
-  const long gw = (long)blockIdx.x * WPB + wave;
+  long gw;
+  if (tl.rowmap == ROWMAP_XCD && (gridDim.x & 7) == 0)
+    gw = ((long)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3)) * WPB + wave;
+  else if (tl.rowmap == ROWMAP_WAVE)
+    gw = (long)wave * gridDim.x + blockIdx.x;
+  else
+    gw = (long)blockIdx.x * WPB + wave;
 
   // bf16 rows: packed fp32 math on {lo, hi} pairs (one dword = two bf16, widened exactly by a
   // shift / a mask): the dot and the gradient axpy are one v_pk_fma_f32 per pair each
@@ -1627,6 +1641,7 @@ static int g_dyn_lg = 3;    // log2(rows per claimed chunk), >= log2(WPB)
 static int g_dyn_sync = 0;
 static int* g_dyn_dbg = nullptr;
 static int* g_dyn_dbg2 = nullptr;
+static int g_rowmap = ROWMAP_BLOCK;
 constexpr long LDS_PER_CU = 160 * 1024;
 constexpr int NUM_CU = 256;
 
@@ -1636,6 +1651,7 @@ int launch_grad_u(const void* X, long ld, const void* y, const void* wt, void* c
   typedef typename AccOf<T>::type A;
   // [WPB/2][d] tree buffer (reused as the final block's feedback row) | [WPB][2] | ticket flag
   GlmTail t2 = tl;
+  t2.rowmap = g_rowmap;
   t2.nbatch = (n > 0 && B > 0) ? (int)((n + B - 1) / B) : 0;
   t2.flat_lds = tl.mode != TAIL_PARTIALS && !tl.det && (size_t)WPB * d * sizeof(A) <= 64 * 1024;
   size_t shmem = (size_t)(t2.flat_lds ? WPB : WPB / 2) * d * sizeof(A) + WPB * 2 * sizeof(A) + 16;
@@ -1777,6 +1793,13 @@ FMLX_API int fmlx_glm_set_tuning(long lds_pad, int nt) {
 FMLX_API void fmlx_glm_set_trace(void* trace) { g_trace = (long long*)trace; }
 
 // dynamic row schedule of the deferred fused round: on/off and log2(rows per chunk)
+// static row schedule's block → row-stripe mapping (ROWMAP_*; A/B knob)
+FMLX_API int fmlx_glm_set_rowmap(int m) {
+  if (m < ROWMAP_BLOCK || m > ROWMAP_WAVE) return -1;
+  g_rowmap = m;
+  return 0;
+}
+
 FMLX_API int fmlx_glm_set_dyn(int on, int lg) {
   if (lg < 3 || lg > 10) return -1;
   g_dyn = on;

@@ -66,6 +66,17 @@ def set_dyn(on: bool = True, chunk_rows: int = 8) -> None:
     _dyn_set = True
 
 
+ROWMAP_BLOCK, ROWMAP_XCD, ROWMAP_WAVE = 0, 1, 2
+
+
+def set_rowmap(m: int) -> None:
+    """A/B knob of the static row schedule's block → row-stripe mapping (csrc/glm.hip ROWMAP_*):
+    0 = consecutive wave slots per block, 1 = one contiguous 1/8 of every stripe per XCD,
+    2 = a block's waves NB rows apart."""
+    if native.kernels().fmlx_glm_set_rowmap(int(m)) != 0:
+        raise ValueError("rowmap must be 0, 1 or 2")
+
+
 def set_trace(buf: Optional[torch.Tensor]) -> None:
     """Diagnostics: fused-round launches write per-block {start, rows done, atomics drained, hw
     id} s_memrealtime stamps (100 MHz) into ``buf`` (int64 [blocks, 4]); None switches off."""

@@ -30,7 +30,9 @@ def main():
     ap.add_argument("--batch", type=int, default=100_000)
     ap.add_argument("--rounds", type=int, default=20)
     ap.add_argument("--defer", type=int, default=1)
+    ap.add_argument("--rowmap", type=int, default=0, help="static schedule mapping (glm.ROWMAP_*)")
     a = ap.parse_args()
+    gk.set_rowmap(a.rowmap)
     dev = torch.device("cuda")
     gk.DEFER = bool(a.defer)
     g = torch.Generator(device=dev).manual_seed(1)
@@ -85,8 +87,10 @@ def main():
                       "block_done_spread_us_if_per_block_mean_removed": round(float(
                           np.median(np.ptp(done - done.mean(0, keepdims=True), axis=1)) * TICK_US), 2)}))
     keys = ["start_max_us", "rows_done_min_us", "rows_done_med_us", "rows_done_max_us", "block_rows_us_med"]
+    xm = {x: round(statistics.median(s["rows_done_mean_by_xcd"][x] for s in summary), 2)
+          for x in summary[0]["rows_done_mean_by_xcd"]}
     print(json.dumps({"median_over_rounds": {k: round(statistics.median(s[k] for s in summary), 2) for k in keys},
-                      "blocks": nb}))
+                      "rows_done_mean_by_xcd_median": xm, "blocks": nb, "rowmap": a.rowmap}))
 
 
 if __name__ == "__main__":
