@@ -152,6 +152,9 @@ struct GlmTail {
   int* dyn_dbg;    // diagnostics (null = off): per batch-row visit counters of the dynamic schedule
   int* dyn_dbg2;   // diagnostics (null = off): per (block, wave) {exit q, walk steps, caps, exh, inflight, lastv, 0, 0}
   int rowmap;      // static schedule: block → row-stripe mapping (ROWMAP_*)
+  int pairs;       // pair schedule (deferred mode, U = 1): static prefix + claimed row pairs
+  int pair_q;      // static fraction of the batch in 1/256
+  int pair_nh;     // pair heads (counters) in use, <= PAIR_NH_MAX
 };
 // Static row schedule: wave slot gw of the W = NB·WPB slots reads rows start + gw + j·W.
 //  ROWMAP_BLOCK: gw = b·WPB + wave — the blocks of one XCD (b mod 8 under round-robin dispatch)
@@ -160,6 +163,23 @@ struct GlmTail {
 //                1/8 of every stripe (its 64 blocks side by side);
 //  ROWMAP_WAVE:  gw = wave·NB + b — a block's waves read rows NB apart.
 enum { ROWMAP_BLOCK = 0, ROWMAP_XCD = 1, ROWMAP_WAVE = 2 };
+
+// Pair schedule (deferred 1-GPU rounds, row-at-a-time loop). Per-block timelines show a ≈4 µs
+// spread of the blocks' finishing times that is random round to round (per-block mean removed:
+// profiles/r3/lr_rowmap_ab_1gpu.jsonl) on top of a ≈2 µs per-XCD offset, so no static split can
+// remove it. Here each wave slot first takes J = ⌊q·B / W⌋ static rows (the stride above), then
+// claims PAIRS of adjacent rows of the remaining pool with one returning device-scope atomic per
+// pair on one of PAIR_NH counters (the pool split into equal ranges; counter h serves the 64
+// waves of blocks 8h … 8h + 7 — one block of every XCD under round-robin dispatch — so every
+// counter drains at the chip's mean rate and no stealing is needed). A wave stops at its first
+// failed claim. Latency: the claim for pair m + 1 is issued at the top of the iteration over pair
+// m (before the second row's loads) and read after the first row's math (≈1 row time later), so
+// a claim's result never crosses the loop back edge; the first pair is claimed at kernel entry and
+// its first row is the static loop's last prefetch. Counters of launch parity p are zeroed by
+// block 0 of every launch with parity 1 − p (launches alternate, kernel boundaries order them).
+constexpr int PAIR_NH_MAX = 64;
+constexpr int PAIR_STRIDE = 32;  // ints between counters (128 B)
+constexpr int PAIR_OFF = 2 * 8 * 32;  // after the DynLds schedule's counters in tl.heads
 constexpr int ACC_MAX_REPS = 8;
 
 // ------------------------------------------------------------------------------------------
@@ -203,6 +223,7 @@ constexpr int DYN_HSTRIDE = 32;  // ints between counters (128 B)
 constexpr int DYN_L = 4;         // chunks of lookahead (and statically owned chunks per block)
 constexpr int DYN_R = 32;        // LDS ring slots (> DYN_L + the chunks any wave can lag behind)
 constexpr int DYN_K = 2;         // rows per wave per chunk (the software pipeline's two buffers)
+static_assert(PAIR_OFF == 2 * DYN_HEADS * DYN_HSTRIDE, "pair counters follow the DynLds schedule's");
 struct DynLds {
   int head;      // counter the block claims from
   int exh;       // no claim can succeed any more (every counter drained, or none exists)
@@ -519,6 +540,8 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
   const long long t_start = tl.trace ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
   int e;
   if (tl.defer) {
+    if (tl.pairs && blockIdx.x == 0 && threadIdx.x < tl.pair_nh)  // the next launch's counters
+      st_agent(&tl.heads[PAIR_OFF + (tl.parity ^ 1) * (PAIR_NH_MAX * PAIR_STRIDE) + threadIdx.x * PAIR_STRIDE], 0);
     if (state[ST_DONE]) return;
     e = state[tl.parity ? ST_ROUND_ALT : ST_ROUND];
   } else if (!round_running(state, e)) return;
@@ -612,6 +635,35 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
   // a full memory latency per row pair; the vector loads are ordered with the row loads.
   const long r_first = start + gw;
   A ylab = (A)0, wlab = (A)1;
+  // pair schedule (see PAIR_NH_MAX): static rows end at `lim`; the pool [lim, end) is served by
+  // pair counter `pctr` (pairs [plo, phi) of the pool); pair `pm0`, claimed at entry, is the
+  // static loop's last prefetch (row `pra0`, label / weight `pyl0` / `pwl0`) when `pok0`
+  long lim = end;
+  bool pairs = false, pok0 = false;
+  long plo = 0, phi = 0, pm0 = 0, pra0 = 0;
+  A pyl0 = (A)0, pwl0 = (A)1;
+  int* pctr = nullptr;
+  auto claim = [&]() -> int {
+    int t = 0;
+    if (lane == 0) t = __hip_atomic_fetch_add(pctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return t;
+  };
+  int pclaim0 = 0;
+  if constexpr (U == 1) {
+    if (tl.pairs && tl.defer && tl.heads && end > start) {
+      pairs = true;
+      const long J = ((end - start) * (long)tl.pair_q) / (256L * W);  // static rows per wave slot
+      lim = start + J * W;
+      const long npairs = (end - lim + 1) >> 1;
+      const int nh = tl.pair_nh;
+      const int h = (int)((blockIdx.x >> 3) % (unsigned)nh);
+      const long per = (npairs + nh - 1) / nh;
+      plo = (long)h * per;
+      phi = plo + per < npairs ? plo + per : npairs;
+      pctr = tl.heads + PAIR_OFF + tl.parity * (PAIR_NH_MAX * PAIR_STRIDE) + h * PAIR_STRIDE;
+      pclaim0 = claim();  // the oldest load of the wave: read after the first rows are issued
+    }
+  }
   auto load_labels = [&](long j0) {
     long rr = r_first + (j0 + lane) * W;
     rr = rr < end ? rr : (end > 0 ? end - 1 : 0);
@@ -633,12 +685,15 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
   auto load_rows = [&](long r0, long j0, long rsafe, Chunk<T, EPC> (&dst)[U][CPL], A (&yy)[U], A (&ww)[U],
                        bool (&vv)[U]) {
     if ((j0 & 63) == 0 && j0 > 0) load_labels(j0);
+    bool okr[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long ru0 = r0 + u * W;
-      const bool ok = ru0 < end;
-      const long ru = ok ? ru0 : rsafe;
-      vv[u] = ok;
+      const bool ok = ru0 < lim;
+      okr[u] = ok;
+      // pair schedule (U = 1): past the static rows the prefetch is the first claimed pair's row
+      const long ru = ok ? ru0 : (pok0 ? pra0 : rsafe);
+      vv[u] = ok || pok0;
       const T* row = X + ru * ld;
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
@@ -652,7 +707,26 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
     for (int u = 0; u < U; ++u) {
       yy[u] = lane_val(ylab, (int)((j0 + u) & 63));
       ww[u] = lane_val(wlab, (int)((j0 + u) & 63));
+      if (!okr[u]) {
+        yy[u] = pyl0;
+        ww[u] = pwl0;
+      }
     }
+  };
+  // one row of a claimed pair: row data plus its label / weight as vector loads (ordered with the
+  // row loads under vmcnt; a scalar load would share lgkmcnt with the LDS traffic)
+  auto load_pair_row = [&](long rr, bool ok, Chunk<T, EPC> (&dst)[U][CPL], A (&yy)[U], A (&ww)[U], bool (&vv)[U]) {
+    vv[0] = ok;
+    const T* row = X + rr * ld;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      const int c = lane + 64 * k;
+      if constexpr (NT) load_chunk_nt<T, EPC>(row + (c < nch ? c : nch - 1) * EPC, dst[0][k]);
+      else load_chunk<T, EPC>(row + (c < nch ? c : nch - 1) * EPC, dst[0][k]);
+    }
+    asm volatile("" : "+v"(rr));
+    yy[0] = y[rr];
+    ww[0] = wsrc[rr];
   };
   auto process = [&](Chunk<T, EPC> (&x)[U][CPL], A (&yy)[U], A (&ww)[U], bool (&vv)[U]) {
     if constexpr (kPacked) {
@@ -1042,13 +1116,52 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
   const long step = (long)U * W;
   long r = start + gw;
   long j = 0;
-  if (r < end) {
+  if (r < lim) {
     load_labels(0);  // first: load_rows reads the labels right after issuing its row loads
     load_rows(r, 0, r, xa, ya, wa, va);
   }
   // deferred mode: complete the previous round while the first rows are in flight
   if (tl.defer && defer_prologue<A>(tl, coef, state, e, d, wdef)) return;
-  if (r < end) {
+  // pair schedule: the first claim (issued at entry) and its row's label / weight
+  if (pairs) {
+    pm0 = plo + __builtin_amdgcn_readfirstlane(pclaim0);
+    pok0 = pm0 < phi;
+    pra0 = lim + 2 * pm0;
+    long rl = pok0 ? pra0 : start;
+    asm volatile("" : "+v"(rl));
+    pyl0 = y[rl];
+    pwl0 = wsrc[rl];
+  }
+  // iterations over claimed pairs; xp holds the (in-flight) first row `ra` of the current pair
+  auto pair_loop = [&](Chunk<T, EPC> (&xp)[U][CPL], A (&yp)[U], A (&wp)[U], bool (&vp)[U],
+                       Chunk<T, EPC> (&xq)[U][CPL], A (&yq)[U], A (&wq)[U], bool (&vq)[U], long ra) {
+    if constexpr (U == 1) {
+      while (true) {
+        const int tn = claim();  // pair m + 1, read after this iteration's first row
+        const long rb = ra + 1;
+        const bool okb = rb < end;
+        load_pair_row(okb ? rb : ra, okb, xq, yq, wq, vq);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        process(xp, yp, wp, vp);
+        const long mn = plo + __builtin_amdgcn_readfirstlane(tn);
+        const bool okn = mn < phi;
+        const long rn = okn ? lim + 2 * mn : ra;
+        load_pair_row(rn, okn, xp, yp, wp, vp);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        process(xq, yq, wq, vq);
+        if (!okn) break;
+        ra = rn;
+      }
+    }
+  };
+  if (r >= lim && pok0) {  // no static rows for this wave slot: start with the claimed pair
+    load_w();
+    load_pair_row(pra0, true, xa, ya, wa, va);
+    pair_loop(xa, ya, wa, va, xb, yb, wb, vb, pra0);
+  }
+  if (r < lim) {
     load_w();
     while (true) {
       load_rows(r + step, j + U, r, xb, yb, wb, vb);
@@ -1061,14 +1174,20 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
       process(xa, ya, wa, va);
       r += step;
       j += U;
-      if (r >= end) break;
+      if (r >= lim) {
+        if (pok0) pair_loop(xb, yb, wb, vb, xa, ya, wa, va, pra0);
+        break;
+      }
       load_rows(r + step, j + U, r, xa, ya, wa, va);
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       process(xb, yb, wb, vb);
       r += step;
       j += U;
-      if (r >= end) break;
+      if (r >= lim) {
+        if (pok0) pair_loop(xa, ya, wa, va, xb, yb, wb, vb, pra0);
+        break;
+      }
     }
   }
   }  // classic row-at-a-time path
@@ -1642,6 +1761,8 @@ static int g_dyn_sync = 0;
 static int* g_dyn_dbg = nullptr;
 static int* g_dyn_dbg2 = nullptr;
 static int g_rowmap = ROWMAP_BLOCK;
+static int g_pairs = 0;      // pair schedule (A/B knob)
+static int g_pair_q = 205;   // static fraction of the batch, 1/256 units
 constexpr long LDS_PER_CU = 160 * 1024;
 constexpr int NUM_CU = 256;
 
@@ -1652,6 +1773,10 @@ int launch_grad_u(const void* X, long ld, const void* y, const void* wt, void* c
   // [WPB/2][d] tree buffer (reused as the final block's feedback row) | [WPB][2] | ticket flag
   GlmTail t2 = tl;
   t2.rowmap = g_rowmap;
+  // pair schedule: deferred mode, row-at-a-time loop, counters present
+  t2.pairs = g_pairs && U == 1 && G == 0 && tl.defer && !tl.det && tl.heads != nullptr && !(g_dyn && tl.heads);
+  t2.pair_q = g_pair_q;
+  t2.pair_nh = nblocks / 8 < 1 ? 1 : (nblocks / 8 > PAIR_NH_MAX ? PAIR_NH_MAX : nblocks / 8);
   t2.nbatch = (n > 0 && B > 0) ? (int)((n + B - 1) / B) : 0;
   t2.flat_lds = tl.mode != TAIL_PARTIALS && !tl.det && (size_t)WPB * d * sizeof(A) <= 64 * 1024;
   size_t shmem = (size_t)(t2.flat_lds ? WPB : WPB / 2) * d * sizeof(A) + WPB * 2 * sizeof(A) + 16;
@@ -1817,7 +1942,15 @@ FMLX_API void fmlx_glm_set_dyn_debug2(void* dbg2) { g_dyn_dbg2 = (int*)dbg2; }
 
 // ints of the fused round's counter block: tickets (TAIL_TOP + 1, padded to 128) + the dynamic
 // schedule's [2][DYN_HEADS][DYN_HSTRIDE] chunk counters
-FMLX_API int fmlx_glm_cnt_elems() { return 128 + 2 * DYN_HEADS * DYN_HSTRIDE; }
+FMLX_API int fmlx_glm_cnt_elems() { return 128 + PAIR_OFF + 2 * PAIR_NH_MAX * PAIR_STRIDE; }
+
+// pair schedule of the deferred fused round: on/off and the static fraction (1/256 units)
+FMLX_API int fmlx_glm_set_pairs(int on, int q) {
+  if (q < 0 || q > 256) return -1;
+  g_pairs = on;
+  g_pair_q = q;
+  return 0;
+}
 
 FMLX_API int fmlx_glm_set_tail_tuning(int acc_reps, int ticket2) {
   if (acc_reps < 1 || acc_reps > ACC_MAX_REPS) return -1;

@@ -69,6 +69,30 @@ def set_dyn(on: bool = True, chunk_rows: int = 8) -> None:
 ROWMAP_BLOCK, ROWMAP_XCD, ROWMAP_WAVE = 0, 1, 2
 
 
+# deferred fused rounds: pair schedule (csrc/glm.hip PAIR_NH_MAX) — static rows for the first
+# PAIR_STATIC of the batch, then adjacent row pairs claimed from 64 XCD-mixed counters.
+# FMLX_GLM_PAIRS=1/0 and FMLX_GLM_PAIR_STATIC (fraction) set the process-wide default. Off by
+# default: exact (tests/test_xgmi_gpu.py::test_pair_schedule_*) and it evens out the per-XCD
+# means (34.7-35.6 us vs 31.7-34.0), but the claimed rows cost more than they save: 39.2-39.8 vs
+# 38.95 us per round at the flagship shape (profiles/r3/lr_pair_schedule_ab_1gpu.jsonl; block
+# timeline lr_pair_schedule_block_timeline.jsonl: median block done 35.4 vs 33.3 us).
+PAIRS_DEFAULT = os.environ.get("FMLX_GLM_PAIRS", "0") == "1"
+PAIR_STATIC = float(os.environ.get("FMLX_GLM_PAIR_STATIC", "0.8"))
+
+
+def set_pairs(on: bool = True, static_frac: float = PAIR_STATIC) -> None:
+    """A/B knob of the deferred fused round's pair schedule: on/off and the static fraction of
+    the batch (the rest is claimed in row pairs)."""
+    global _pairs_set
+    q = int(round(float(static_frac) * 256))
+    if native.kernels().fmlx_glm_set_pairs(int(bool(on)), q) != 0:
+        raise ValueError("static_frac must be in [0, 1]")
+    _pairs_set = True
+
+
+_pairs_set = False
+
+
 def set_rowmap(m: int) -> None:
     """A/B knob of the static row schedule's block → row-stripe mapping (csrc/glm.hip ROWMAP_*):
     0 = consecutive wave slots per block, 1 = one contiguous 1/8 of every stripe per XCD,
@@ -151,6 +175,8 @@ class RoundScratch:
     def __init__(self, nparts: int, d: int, acc: torch.dtype, device, det: bool = None):
         if not _dyn_set:
             set_dyn(DYN_DEFAULT)
+        if not _pairs_set:
+            set_pairs(PAIRS_DEFAULT, PAIR_STATIC)
         self.nparts = nparts
         self.det = DETERMINISTIC if det is None else bool(det)
         if self.det:

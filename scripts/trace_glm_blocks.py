@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--rowmap", type=int, default=0, help="static schedule mapping (glm.ROWMAP_*)")
     a = ap.parse_args()
     gk.set_rowmap(a.rowmap)
+    ap2 = os.environ.get("TRACE_PAIRS", "")
+    if ap2:
+        gk.set_pairs(True, float(ap2))
     dev = torch.device("cuda")
     gk.DEFER = bool(a.defer)
     g = torch.Generator(device=dev).manual_seed(1)

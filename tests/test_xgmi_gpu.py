@@ -271,7 +271,7 @@ def test_dynamic_schedule_covers_every_row_once(chunk, dtype, d, monkeypatch):
                 got = float(tr.feedback[d].item())
                 assert got == want, (B, e, got, want)
     finally:
-        gk.set_dyn(True, 8)
+        gk.set_dyn(gk.DYN_DEFAULT, 8)
 
 
 @pytest.mark.parametrize("dyn", [True, False])
@@ -295,4 +295,69 @@ def test_dynamic_schedule_matches_static(dyn, monkeypatch):
         assert tr.rounds_executed() == 5
         assert np.allclose(got, ref, rtol=2e-4, atol=2e-6), np.abs(got - ref).max()
     finally:
-        gk.set_dyn(True, 8)
+        gk.set_dyn(gk.DYN_DEFAULT, 8)
+
+
+@pytest.mark.parametrize("frac", [0.0, 0.5, 0.8, 1.0])
+@pytest.mark.parametrize("dtype,d", [("bf16", 1000), ("bf16", 520), ("fp32", 300)])
+def test_pair_schedule_covers_every_row_once(frac, dtype, d, monkeypatch):
+    """The deferred round's pair schedule (static prefix + claimed row pairs, csrc/glm.hip
+    PAIR_NH_MAX) processes every row of the batch exactly once for any batch size and static
+    fraction (all claimed, all static, odd pools, fewer pairs than waves). Integer row weights
+    make Σweight (feedback[d]) an exact, order-independent row census."""
+    _need_gpu()
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer
+    from flink_ml_amd.ops import glm as gk
+
+    monkeypatch.setattr(gk, "DEFER", True)
+    monkeypatch.setattr(gk, "DETERMINISTIC", False)
+    gk.set_dyn(False, 8)
+    gk.set_pairs(True, frac)
+    try:
+        g = torch.Generator(device="cpu").manual_seed(9)
+        n = 157_003
+        X = torch.rand((n, d), generator=g)
+        X = X.to(torch.bfloat16) if dtype == "bf16" else X
+        y = torch.randint(0, 2, (n,), generator=g).to(torch.float32)
+        wt = (torch.arange(n) % 7 + 1).to(torch.float32)
+        for B in (1_000, 31_337, 157_003, 100_000):
+            tr = DeviceGlmTrainer(SGD(max_iter=6, learning_rate=0.1, global_batch_size=B, tol=0.0), np.zeros(d),
+                                  X.cuda(), y.cuda(), wt.cuda(), "logistic", use_graph=False)
+            assert tr.defer
+            P = -(-n // B)
+            tr._launch_round(1)  # round 0
+            for e in range(5):  # both launch parities twice: the counters are re-armed
+                tr._launch_round(1)  # launch e + 1 completes round e and publishes its feedback
+                torch.cuda.synchronize()
+                b0 = (e % P) * B
+                want = float(wt[b0:min(b0 + B, n)].sum())
+                got = float(tr.feedback[d].item())
+                assert got == want, (B, e, got, want)
+    finally:
+        gk.set_pairs(gk.PAIRS_DEFAULT, gk.PAIR_STATIC)
+        gk.set_dyn(gk.DYN_DEFAULT, 8)
+
+
+@pytest.mark.parametrize("pairs", [True, False])
+def test_pair_schedule_matches_torch(pairs, monkeypatch):
+    """Flagship-shape fit (graph-captured deferred rounds) with the pair schedule on and off
+    against the fp64 torch reference."""
+    _need_gpu()
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
+    from flink_ml_amd.ops import glm as gk
+
+    monkeypatch.setattr(gk, "DEFER", True)
+    gk.set_pairs(pairs, 0.8)
+    try:
+        g = torch.Generator(device="cpu").manual_seed(13)
+        n, d, B = 300_000, 1000, 100_000
+        Xb = torch.rand((n, d), generator=g).to(torch.bfloat16)
+        y = torch.randint(0, 2, (n,), generator=g).to(torch.float64)
+        sgd = SGD(max_iter=7, learning_rate=0.1, global_batch_size=B, tol=0.0)
+        ref = TorchGlmTrainer(sgd, np.zeros(d), Xb.to(torch.float64), y, None, "logistic").fit()
+        tr = DeviceGlmTrainer(sgd, np.zeros(d), Xb.cuda(), y.cuda(), None, "logistic", use_graph=True)
+        got = tr.fit()
+        assert tr.rounds_executed() == 7
+        assert np.allclose(got, ref, rtol=2e-4, atol=2e-6), np.abs(got - ref).max()
+    finally:
+        gk.set_pairs(gk.PAIRS_DEFAULT, gk.PAIR_STATIC)
