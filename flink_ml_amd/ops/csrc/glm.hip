@@ -155,6 +155,7 @@ struct GlmTail {
   int pairs;       // pair schedule (deferred mode, U = 1): static prefix + claimed row pairs
   int pair_q;      // static fraction of the batch in 1/256
   int pair_nh;     // pair heads (counters) in use, <= PAIR_NH_MAX
+  int l2acc;       // deferred flat tail: per-XCD replicas accumulated in the XCD's L2
 };
 // Static row schedule: wave slot gw of the W = NB·WPB slots reads rows start + gw + j·W.
 //  ROWMAP_BLOCK: gw = b·WPB + wave — the blocks of one XCD (b mod 8 under round-robin dispatch)
@@ -1239,8 +1240,16 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
     __syncthreads();
     // replica b mod acc_reps: at most ceil(nb / reps) adders per address (float atomics keep
     // their full rate up to ~32 adders per address; 256 on one 4 KB row serialise)
-    A* gacc = (A*)tl.acc + (long)(blockIdx.x % (tl.acc_reps > 1 ? tl.acc_reps : 1)) * tl.acc_ld +
-              (tl.defer ? (long)(e % 3) * ACC_MAX_REPS * tl.acc_ld : 0L);
+    // l2acc (deferred mode): replica = this block's XCD, added with workgroup-scope atomics that
+    // the XCD's own L2 performs (only blocks of that XCD touch the replica; the kernel boundary
+    // writes the L2 back before the next launch's prologue reads it)
+    int rep = (int)(blockIdx.x % (tl.acc_reps > 1 ? tl.acc_reps : 1));
+    if (tl.l2acc) {
+      unsigned xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      rep = (int)(xcc & (ACC_MAX_REPS - 1));
+    }
+    A* gacc = (A*)tl.acc + (long)rep * tl.acc_ld + (tl.defer ? (long)(e % 3) * ACC_MAX_REPS * tl.acc_ld : 0L);
     const long stride = d + 2;
     for (long c = threadIdx.x; c < stride; c += blockDim.x) {
       A v = (A)0;
@@ -1251,7 +1260,8 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
 #pragma unroll
         for (int q = 0; q < WPB; ++q) v += lw[q * 2 + (int)(c - d)];
       }
-      atomicAdd(gacc + c, v);
+      if (tl.l2acc) __hip_atomic_fetch_add(gacc + c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      else atomicAdd(gacc + c, v);
     }
     if (tl.trace) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1763,6 +1773,7 @@ static int* g_dyn_dbg2 = nullptr;
 static int g_rowmap = ROWMAP_BLOCK;
 static int g_pairs = 0;      // pair schedule (A/B knob)
 static int g_pair_q = 205;   // static fraction of the batch, 1/256 units
+static int g_l2acc = 0;      // deferred flat tail: per-XCD L2 replicas (A/B knob)
 constexpr long LDS_PER_CU = 160 * 1024;
 constexpr int NUM_CU = 256;
 
@@ -1776,6 +1787,8 @@ int launch_grad_u(const void* X, long ld, const void* y, const void* wt, void* c
   // pair schedule: deferred mode, row-at-a-time loop, counters present
   t2.pairs = g_pairs && U == 1 && G == 0 && tl.defer && !tl.det && tl.heads != nullptr && !(g_dyn && tl.heads);
   t2.pair_q = g_pair_q;
+  t2.l2acc = g_l2acc && tl.defer && !tl.det && tl.mode == TAIL_UPDATE;
+  if (t2.l2acc) t2.acc_reps = ACC_MAX_REPS;  // the prologue sums every XCD's replica
   t2.pair_nh = nblocks / 8 < 1 ? 1 : (nblocks / 8 > PAIR_NH_MAX ? PAIR_NH_MAX : nblocks / 8);
   t2.nbatch = (n > 0 && B > 0) ? (int)((n + B - 1) / B) : 0;
   t2.flat_lds = tl.mode != TAIL_PARTIALS && !tl.det && (size_t)WPB * d * sizeof(A) <= 64 * 1024;
@@ -1943,6 +1956,12 @@ FMLX_API void fmlx_glm_set_dyn_debug2(void* dbg2) { g_dyn_dbg2 = (int*)dbg2; }
 // ints of the fused round's counter block: tickets (TAIL_TOP + 1, padded to 128) + the dynamic
 // schedule's [2][DYN_HEADS][DYN_HSTRIDE] chunk counters
 FMLX_API int fmlx_glm_cnt_elems() { return 128 + PAIR_OFF + 2 * PAIR_NH_MAX * PAIR_STRIDE; }
+
+// deferred flat tail: per-XCD replicas with L2-performed (workgroup-scope) atomics
+FMLX_API int fmlx_glm_set_l2acc(int on) {
+  g_l2acc = on;
+  return 0;
+}
 
 // pair schedule of the deferred fused round: on/off and the static fraction (1/256 units)
 FMLX_API int fmlx_glm_set_pairs(int on, int q) {

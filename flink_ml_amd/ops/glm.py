@@ -93,6 +93,12 @@ def set_pairs(on: bool = True, static_frac: float = PAIR_STATIC) -> None:
 _pairs_set = False
 
 
+def set_l2acc(on: bool) -> None:
+    """A/B knob of the deferred flat tail: accumulate into one replica per XCD with atomics
+    performed in that XCD's L2 (workgroup scope) instead of device-scope atomics."""
+    native.call("fmlx_glm_set_l2acc", int(bool(on)))
+
+
 def set_rowmap(m: int) -> None:
     """A/B knob of the static row schedule's block → row-stripe mapping (csrc/glm.hip ROWMAP_*):
     0 = consecutive wave slots per block, 1 = one contiguous 1/8 of every stripe per XCD,

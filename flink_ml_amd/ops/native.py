@@ -61,6 +61,7 @@ _KERNEL_SIGS = {
     "fmlx_glm_set_dyn": [c_int, c_int],
     "fmlx_glm_set_rowmap": [c_int],
     "fmlx_glm_set_pairs": [c_int, c_int],
+    "fmlx_glm_set_l2acc": [c_int],
     "fmlx_glm_cnt_elems": [],
     "fmlx_glm_set_dyn_debug": ([c_int, c_void_p], None),
     "fmlx_glm_set_dyn_debug2": ([c_void_p], None),

@@ -78,6 +78,7 @@ def main():
             gk.set_tail_tuning(c.get("reps", 4), bool(c.get("t2", 0)))
             gk.set_dyn(bool(c.get("dyn", 0)), c.get("ch", 8))
             gk.set_rowmap(c.get("rm", 0))
+            gk.set_l2acc(bool(c.get("l2", 0)))
             gk.set_pairs(bool(c.get("pairs", 0)), c.get("q", 205) / 256.0)
             sgd = SGD(max_iter=10 ** 8, learning_rate=0.1, global_batch_size=a.batch, tol=0.0)
             cls = SplitTrainer if (c.get("split") or c.get("m0")) else DeviceGlmTrainer

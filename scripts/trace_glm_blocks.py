@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--rowmap", type=int, default=0, help="static schedule mapping (glm.ROWMAP_*)")
     a = ap.parse_args()
     gk.set_rowmap(a.rowmap)
+    gk.set_l2acc(os.environ.get("TRACE_L2ACC", "0") == "1")
     ap2 = os.environ.get("TRACE_PAIRS", "")
     if ap2:
         gk.set_pairs(True, float(ap2))
