@@ -151,6 +151,12 @@ class TorchGlmTrainer:
         return self.coef.numpy().copy()
 
 
+# sparse trainer: a batch's column-major copy is built when the fit visits each batch at least
+# CSC_BUILD_ROUNDS times or runs at least CSC_MIN_ITERS rounds
+CSC_BUILD_ROUNDS = float(os.environ.get("FMLX_CSC_BUILD_ROUNDS", "3"))
+CSC_MIN_ITERS = int(os.environ.get("FMLX_CSC_MIN_ITERS", "64"))
+
+
 class DeviceGlmTrainer:
     """HBM-resident SGD on MI355X via the fused HIP kernels (one process per GPU)."""
 
@@ -195,8 +201,9 @@ class DeviceGlmTrainer:
         if self.sparse:
             self.scratch = None
             self.nparts = 0
-            if dev.type == "cuda" and self.n > 0:
-                self.csc = gk.BatchCsc.build(self.indptr, self.indices, self.values, self.n, self.d, self.B)
+            if dev.type == "cuda" and self.n > 0 and self._csc_pays(sgd):
+                # allocated here, batches transposed lazily before the rounds that visit them
+                self.csc = gk.BatchCsc.alloc(self.indptr, self.indices, self.values, self.n, self.d, self.B)
                 if self.csc is not None:
                     self.mult = torch.zeros(max(1, min(self.B, self.n)), dtype=acc, device=dev)
                     self.wl = torch.zeros(gk.wl_elems(), dtype=acc, device=dev)  # Σw/Σloss slots per parity
@@ -233,11 +240,21 @@ class DeviceGlmTrainer:
         self.parity = 0
         self.cw = torch.zeros((2, self.d), dtype=acc, device=dev) if self.defer else None
         self._flushed = False
+        self._short = False  # fit(): too few rounds for hipGraph capture to pay (direct launches)
         self.graphs = {}
         self.timing = False
         self.check_every = max(1, int(check_every))
         self.rounds_per_graph = self.check_every
+        self._launched = 0  # rounds launched so far (round e visits batch e mod P)
 
+    def _csc_pays(self, sgd: SGD) -> bool:
+        """Whether the per-batch column-major copy pays for itself in this fit: transposing a
+        batch costs about CSC_BUILD_ROUNDS rounds of the atomic-scatter gradient it replaces
+        (measured at the north-star shape: ≈1.1 ms per 100k × 64-nnz batch vs 0.49 → 0.09 ms per
+        round), so a fit that visits each batch fewer times than that keeps the scatter kernel."""
+        P = -(-self.n // max(self.B, 1))
+        visits = sgd.max_iter / max(P, 1) if P else 0
+        return visits >= CSC_BUILD_ROUNDS or sgd.max_iter >= CSC_MIN_ITERS
     # -- one round as a fixed launch sequence (capturable) -------------------------------------
     def _launch_round(self, rounds: int = 1) -> None:
         """Launches ``rounds`` consecutive rounds (one host call on the fused dense path,
@@ -248,6 +265,8 @@ class DeviceGlmTrainer:
             return
         s = self.sgd
         if self.csc is not None:
+            if not torch.cuda.is_current_stream_capturing():
+                self.csc.ensure_rounds(self._launched, 1)
             # forward (per-row multipliers) + atomic-free column-major backward; on 1 GPU the
             # backward applies the update and the termination check itself
             gk.csc_round(self.csc, self.indptr, self.indices, self.values, self.y, self.w, self.coef, self.n, self.d,
@@ -376,10 +395,14 @@ class DeviceGlmTrainer:
         for key in self.graph_keys(k):
             if self.defer and key[1] != self.parity:
                 self._launch_round(1)
+                self._launched += 1
                 done += 1
+            r = key[0] if self.defer else key
+            if self.csc is not None:
+                self.csc.ensure_rounds(self._launched, r)
             g = self.graphs.get(key) or self._capture(key)
             g.replay()
-            r = key[0] if self.defer else key
+            self._launched += r
             if self.defer:
                 self.parity = (self.parity + r) & 1
             done += r
@@ -387,10 +410,16 @@ class DeviceGlmTrainer:
 
     def run_rounds(self, k: int) -> None:
         """Runs ``k`` SGD rounds (each predicated on the device running flag), no host sync."""
-        if not self.use_graph:
+        if self.csc is not None:
+            self.csc.ensure_rounds(self._launched, k)  # the batches these rounds visit
+        first = self._launched
+        self._launched += k
+        if not self.use_graph or self._short:
             R = self.rounds_per_graph
             for i in range(0, k, R):
+                self._launched = first + i
                 self._launch_round(min(R, k - i))
+            self._launched = first + k
             return
         R = self.rounds_per_graph
         full, rem = divmod(k, R)
@@ -438,8 +467,13 @@ class DeviceGlmTrainer:
             self.coef.copy_(st["coef"].to(self.coef.dtype))
             self.state.copy_(st["state"])
             self._host_round = int(self.state[0].item())
+            self._launched = self._host_round
             if st["done"]:
                 return self.coef.to(torch.float64).cpu().numpy()
+        # a fit shorter than two graphs' worth of rounds launches directly: capture + first replay
+        # (~1 ms per graph) would cost more than the launches it saves
+        if not self.graphs and self.sgd.max_iter < 2 * self.rounds_per_graph:
+            self._short = True
         log = tracing.rounds_enabled()
         # per-round logs (a diagnostic mode) read every round's own feedback: one round per host
         # step; otherwise check-interval (or checkpoint-interval) rounds per host step

@@ -255,12 +255,20 @@ class BatchCsc:
     their CSR positions [indptr[bB], indptr[bB+B]) but are re-ordered by column (stable, so rows
     stay ascending within a column) and carry the batch-relative row id. ``colptr[b]`` is the
     dense int32 column pointer of batch b. Costs one extra copy of the partition plus P·(d+1)·4
-    bytes; ``build`` returns None when that exceeds ``CSC_MAX_BYTES`` or a batch has ≥ 2^31
+    bytes; ``alloc`` returns None when that exceeds ``CSC_MAX_BYTES`` or a batch has ≥ 2^31
     non-zeros (the trainer then keeps the atomic scatter kernel).
+
+    Batches are transposed lazily (``ensure``): a fit transposes only the batches its rounds
+    visit, before the rounds are launched (SGD.java:263-268 visits batch e mod P in round e), so
+    a short fit over a large partition does not pay for the whole partition.
     """
 
-    def __init__(self, colptr, erow, evals, G: int):
+    def __init__(self, colptr, erow, evals, G: int, bounds, indptr, indices, values, n: int, d: int, B: int):
         self.colptr, self.erow, self.evals, self.G = colptr, erow, evals, G
+        self.bounds, self.P = bounds, len(bounds) - 1
+        self._src = (indptr, indices, values)
+        self.n, self.d, self.B = n, d, B
+        self.built = [False] * self.P
 
     @staticmethod
     def pick_group(avg_nnz: float) -> int:
@@ -270,7 +278,7 @@ class BatchCsc:
         return g
 
     @staticmethod
-    def build(indptr, indices, values, n: int, d: int, B: int):
+    def alloc(indptr, indices, values, n: int, d: int, B: int):
         if os.environ.get("FMLX_CSR_TRANSPOSE", "1") == "0" or n <= 0 or B <= 0:
             return None
         P = (n + B - 1) // B
@@ -285,8 +293,27 @@ class BatchCsc:
         colptr = torch.zeros((P, d + 1), dtype=torch.int32, device=dev)
         erow = torch.empty(nnz, dtype=torch.int32, device=dev)
         evals = torch.empty_like(values)
-        for b in range(P):
-            j0, j1 = bounds[b], bounds[b + 1]
+        return BatchCsc(colptr, erow, evals, BatchCsc.pick_group(nnz / max(n, 1)), bounds, indptr, indices, values,
+                        n, d, B)
+
+    @staticmethod
+    def build(indptr, indices, values, n: int, d: int, B: int):
+        """Allocates and transposes every batch up front."""
+        csc = BatchCsc.alloc(indptr, indices, values, n, d, B)
+        if csc is not None:
+            csc.ensure(range(csc.P))
+        return csc
+
+    def ensure(self, batches) -> None:
+        """Transposes the listed batches that are not yet (idempotent; never inside a capture)."""
+        indptr, indices, values = self._src
+        dev = values.device
+        n, d, B = self.n, self.d, self.B
+        for b in sorted(set(int(x) % self.P for x in batches)):
+            if self.built[b]:
+                continue
+            self.built[b] = True
+            j0, j1 = self.bounds[b], self.bounds[b + 1]
             if j1 == j0:
                 continue
             r0, r1 = b * B, min((b + 1) * B, n)
@@ -294,11 +321,16 @@ class BatchCsc:
             rows = torch.repeat_interleave(torch.arange(r1 - r0, device=dev, dtype=torch.int32),
                                            (indptr[r0 + 1:r1 + 1] - indptr[r0:r1]).to(torch.int64))
             order = torch.sort(cols, stable=True).indices
-            erow[j0:j1] = rows[order]
-            evals[j0:j1] = values[j0:j1][order]
-            colptr[b, 1:] = torch.cumsum(torch.bincount(cols, minlength=d), 0).to(torch.int32)
+            self.erow[j0:j1] = rows[order]
+            self.evals[j0:j1] = values[j0:j1][order]
+            self.colptr[b, 1:] = torch.cumsum(torch.bincount(cols, minlength=d), 0).to(torch.int32)
             del cols, rows, order
-        return BatchCsc(colptr, erow, evals, BatchCsc.pick_group(nnz / max(n, 1)))
+
+    def ensure_rounds(self, first_epoch: int, k: int) -> None:
+        """Transposes the batches of rounds first_epoch … first_epoch + k − 1."""
+        if all(self.built):
+            return
+        self.ensure(range(first_epoch, first_epoch + min(k, self.P)))
 
 
 def wl_elems() -> int:

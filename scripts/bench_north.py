@@ -116,14 +116,23 @@ def run_svc_sparse(a, ctx):
     y = torch.randint(0, 2, (n,), generator=g, device=ctx.device).to(torch.float32)
     gb = a.batch * ctx.world_size
     iters = a.iters
-    sgd = SGD(max_iter=iters, learning_rate=0.1, global_batch_size=gb, tol=0.0)
-    tr = DeviceGlmTrainer(sgd, np.zeros(dim), X, y, None, "hinge")
-    tr.run_rounds(1)  # untimed warm-up (CSC build happened in the constructor)
-    tr2 = DeviceGlmTrainer(SGD(max_iter=iters, learning_rate=0.1, global_batch_size=gb, tol=0.0), np.zeros(dim), X, y,
-                           None, "hinge")
-    fit_s, _ = _timed(ctx, tr2.fit)
-    # steady state: rounds of an already warmed trainer (graphs captured and primed), as
-    # bench.py times the dense flagship — the fit above also pays the per-fit set-up
+    warm = DeviceGlmTrainer(SGD(max_iter=2, learning_rate=0.1, global_batch_size=gb, tol=0.0), np.zeros(dim), X, y,
+                            None, "hinge")
+    warm.fit()  # untimed warm-up: library load, allocator (a 2-round fit, no transpose)
+    del warm
+
+    def whole_fit():
+        # the whole fit as the reference's netRuntime counts it: trainer set-up (device copies of
+        # the shard's CSR views, the lazy per-batch column-major copies of the visited batches,
+        # graph capture when it pays) + maxIter rounds + the coefficient read-back
+        tr = DeviceGlmTrainer(SGD(max_iter=iters, learning_rate=0.1, global_batch_size=gb, tol=0.0), np.zeros(dim),
+                              X, y, None, "hinge")
+        tr.fit()
+        return tr
+
+    fit_s, tr2 = _timed(ctx, whole_fit)
+    # steady state: rounds of an already warmed trainer (graphs captured and primed, every batch
+    # transposed), as bench.py times the dense flagship
     steady = a.steady_rounds
     tr3 = DeviceGlmTrainer(SGD(max_iter=10 ** 8, learning_rate=0.1, global_batch_size=gb, tol=0.0), np.zeros(dim), X,
                            y, None, "hinge")
@@ -136,14 +145,16 @@ def run_svc_sparse(a, ctx):
 
     steady_s, _ = _timed(ctx, body)
     return {"metric": "LinearSVC training samples/s (whole job), 50M x 1M sparse CSR",
-            "value": round(gb * steady / steady_s, 1), "unit": "samples/s", "higher_is_better": True,
-            "ms_per_round": round(steady_s * 1e3 / steady, 4),
-            "fit_ms_per_round": round(fit_s * 1e3 / iters, 4), "fit_samples_per_s": round(gb * iters / fit_s, 1),
-            "note": "value / ms_per_round: steady-state rounds of a warmed trainer (like bench.py); fit_*: one "
-                    "maxIter-round fit() including its graph capture and coefficient read-back",
+            "value": round(gb * iters / fit_s, 1), "unit": "samples/s", "higher_is_better": True,
+            "totalTimeMs": round(fit_s * 1e3, 3), "fit_ms_per_round": round(fit_s * 1e3 / iters, 4),
+            "steady_ms_per_round": round(steady_s * 1e3 / steady, 4),
+            "steady_samples_per_s": round(gb * steady / steady_s, 1),
+            "note": "value / totalTimeMs: one whole maxIter-round fit (trainer set-up incl. the column-major "
+                    "copies it builds, rounds, coefficient read-back); steady_*: rounds of a warmed trainer",
             "config": {"model": "LinearSVC (hinge SGD)", "rows": total, "dim": dim, "nnz_per_row": nnz,
                        "global_batch": gb, "maxIter": iters, "rows_per_gpu": n, "dtype": "fp32",
-                       "csr_transpose": tr2.csc is not None}}
+                       "fit_csr_transpose": tr2.csc is not None, "fit_hipgraph": bool(tr2.graphs),
+                       "steady_csr_transpose": tr3.csc is not None}}
 
 
 def run_online_lr(a, ctx):
