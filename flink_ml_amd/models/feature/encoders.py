@@ -34,7 +34,9 @@ from ...linalg.vectors import DenseVector, SparseVector, Vector
 from ...ops import features as fo
 from ...param.param import BooleanParam, FloatParam, IntParam, ParamValidators, StringParam
 from ...parallel import comm
+from ...parallel import datastream as ds
 from ...table import SparseColumn, StringColumn, Table, first_occurrence
+from ...utils.strtable import StrTable, hashmap_order_from_hashes
 from ...utils.java import (java_double_hash, java_hashmap_order, java_int_hash, java_number_to_string,
                            java_string_hash)
 from ..base import ModelWithData
@@ -50,20 +52,12 @@ def _dev():
 def _numeric_col(t: Table, col: str) -> torch.Tensor:
     c = t.column(col)
     if isinstance(c, StringColumn) and len(c) > 0:
-        if any(not isinstance(w, str) for w in c.vocab):
-            raise RuntimeError("The input column only supports string and numeric type.")
-        # counts per distinct string by code on the device, in first-seen order
-        codes = c.codes.to(config.compute_device()).long()
-        V = len(c.vocab)
-        cnt = torch.bincount(codes, minlength=V)
-        first = first_occurrence(codes, V)
-        present = torch.nonzero(cnt > 0).reshape(-1)
-        order = present[torch.argsort(first[present], stable=True)].cpu().tolist()
-        cnt_h = cnt.cpu().tolist()
-        out: Dict[str, int] = {}
-        for i in order:
-            out[c.vocab[i]] = out.get(c.vocab[i], 0) + int(cnt_h[i])
-        return out
+        # numeric strings: parse each distinct value once, gather by code
+        try:
+            lut = torch.tensor([float(w) for w in c.vocab], dtype=torch.float64)
+        except (TypeError, ValueError):
+            raise RuntimeError("Column %s is not numeric." % col) from None
+        return lut.to(c.codes.device)[c.codes.long()]
     if isinstance(c, torch.Tensor):
         if c.dim() != 1:
             raise ValueError("Column %s is not a scalar column" % col)
@@ -189,60 +183,120 @@ def _java_str_key(s: str) -> bytes:
     return s.encode("utf-16-be")
 
 
-def _string_counts(t: Table, col: str) -> Dict[str, int]:
-    """Per-rank ``Map<String, Long>`` of a column in first-seen order (numbers via String.valueOf)."""
+def _string_counts_table(t: Table, col: str):
+    """This rank's distinct strings of a column (numbers via String.valueOf) as a StrTable, their
+    counts and first-seen row positions (the insertion order of the reference's per-partition
+    ``Map<String, Long>``)."""
     c = t.column(col)
     if isinstance(c, StringColumn) and len(c) > 0:
-        if any(not isinstance(w, str) for w in c.vocab):
-            raise RuntimeError("The input column only supports string and numeric type.")
-        # counts per distinct string by code on the device, in first-seen order
+        try:
+            tab = StrTable.from_strings(c.vocab)
+        except TypeError:
+            raise RuntimeError("The input column only supports string and numeric type.") from None
+        # counts and first occurrences per vocabulary entry by code on the device
         codes = c.codes.to(config.compute_device()).long()
         V = len(c.vocab)
         cnt = torch.bincount(codes, minlength=V)
         first = first_occurrence(codes, V)
         present = torch.nonzero(cnt > 0).reshape(-1)
-        order = present[torch.argsort(first[present], stable=True)].cpu().tolist()
-        cnt_h = cnt.cpu().tolist()
-        out: Dict[str, int] = {}
-        for i in order:
-            out[c.vocab[i]] = out.get(c.vocab[i], 0) + int(cnt_h[i])
-        return out
+        pres = present.cpu().numpy()
+        return tab.take(pres), cnt[present].cpu().numpy(), first[present].cpu().numpy()
     if isinstance(c, torch.Tensor):
         if c.dim() != 1:
             raise RuntimeError("The input column only supports string and numeric type.")
-        # device: unique + counts; first-seen order is recovered from the first occurrence index
         u, inv, cnt = torch.unique(c, return_inverse=True, return_counts=True)
         first = torch.full((u.numel(),), c.numel(), dtype=torch.int64, device=c.device)
         first.scatter_reduce_(0, inv, torch.arange(c.numel(), device=c.device), "amin")
-        order = torch.argsort(first).tolist()
-        uvals, ucnt = u.tolist(), cnt.tolist()
         is_int = not c.dtype.is_floating_point
-        return {(str(int(uvals[i])) if is_int else java_number_to_string(uvals[i])): int(ucnt[i]) for i in order}
-    out: Dict[str, int] = {}
-    for v in c:
+        strs = [str(int(v)) if is_int else java_number_to_string(v) for v in u.tolist()]
+        return StrTable.from_strings(strs), cnt.cpu().numpy(), first.cpu().numpy()
+    counts: Dict[str, int] = {}
+    firsts: Dict[str, int] = {}
+    for r, v in enumerate(c):
         if isinstance(v, str):
-            s = v
+            w = v
         elif isinstance(v, (int, float, np.integer, np.floating)) and not isinstance(v, bool):
-            s = java_number_to_string(v.item() if hasattr(v, "item") else v)
+            w = java_number_to_string(v.item() if hasattr(v, "item") else v)
         else:
             raise RuntimeError("The input column only supports string and numeric type.")
-        out[s] = out.get(s, 0) + 1
-    return out
+        if w not in counts:
+            counts[w] = 0
+            firsts[w] = r
+        counts[w] += 1
+    keys = list(counts)
+    return (StrTable.from_strings(keys), np.array([counts[k] for k in keys], dtype=np.int64),
+            np.array([firsts[k] for k in keys], dtype=np.int64))
+
+
+def _string_counts(t: Table, col: str) -> Dict[str, int]:
+    """Per-rank ``Map<String, Long>`` of a column in first-seen order (numbers via String.valueOf)."""
+    tab, cnt, first = _string_counts_table(t, col)
+    tab, sums, _ = _local_merge(tab, cnt, first)
+    return dict(zip(tab.strings(), sums[:, 0].astype(np.int64).tolist()))
+
+
+def _local_merge(tab: StrTable, cnt: np.ndarray, first: np.ndarray):
+    order = np.argsort(first, kind="stable")
+    tab, cnt, first = tab.take(order), cnt[order], first[order]
+    rep = tab.first_of_equal()
+    if len(tab) and not np.array_equal(rep, np.arange(len(tab))):
+        uniq, inv = np.unique(rep, return_inverse=True)
+        s2 = np.zeros((uniq.shape[0], 1), dtype=np.float64)
+        np.add.at(s2[:, 0], inv, cnt)
+        return tab.take(uniq), s2, first[uniq]
+    return tab, cnt.astype(np.float64)[:, None], first
+
+
+def order_string_table(tab: StrTable, counts: np.ndarray, order: str) -> np.ndarray:
+    """Positions of ``tab``'s strings (inserted in table order into a Java HashMap) in the
+    requested StringIndexer order (``StringIndexer.java:160-178``): HashMap iteration order,
+    then a stable sort by frequency, or ``String.compareTo`` order."""
+    if order == ALPHABET_ASC_ORDER:
+        return tab.argsort(False)
+    if order == ALPHABET_DESC_ORDER:
+        return tab.argsort(True)
+    hm = hashmap_order_from_hashes(tab.java_hashes())
+    if order == FREQUENCY_ASC_ORDER:
+        return hm[np.argsort(counts[hm], kind="stable")]
+    if order == FREQUENCY_DESC_ORDER:
+        return hm[np.argsort(-counts[hm], kind="stable")]
+    if order != ARBITRARY_ORDER:
+        raise ValueError("Unsupported stringOrderType type: %s." % order)
+    return hm
 
 
 def _order_strings(counts: Dict[str, int], order: str) -> List[str]:
-    items = [(k, counts[k]) for k in java_hashmap_order(list(counts.keys()), java_string_hash)]
-    if order == ALPHABET_ASC_ORDER:
-        items.sort(key=lambda kv: _java_str_key(kv[0]))
-    elif order == ALPHABET_DESC_ORDER:
-        items.sort(key=lambda kv: _java_str_key(kv[0]), reverse=True)
-    elif order == FREQUENCY_ASC_ORDER:
-        items.sort(key=lambda kv: kv[1])
-    elif order == FREQUENCY_DESC_ORDER:
-        items.sort(key=lambda kv: -kv[1])
-    elif order != ARBITRARY_ORDER:
-        raise ValueError("Unsupported stringOrderType type: %s." % order)
-    return [k for k, _ in items]
+    keys = list(counts)
+    tab = StrTable.from_strings(keys)
+    perm = order_string_table(tab, np.array([counts[k] for k in keys], dtype=np.int64), order)
+    return [keys[i] for i in perm.tolist()]
+
+
+class _LookupTable:
+    """string → index of one model array, as the reference's ``HashMap`` built by putting the
+    array's strings in order (a later duplicate overwrites an earlier one): a native hash join for
+    batches of distinct strings, a dict only for the per-row list path."""
+
+    def __init__(self, arr: Sequence[str]):
+        self.arr = list(arr)
+        self._rev = None
+        self._dict = None
+
+    def __len__(self) -> int:
+        return len(self.arr)
+
+    def lookup(self, queries: StrTable) -> np.ndarray:
+        """Index of every query string (−1 if absent)."""
+        if self._rev is None:
+            self._rev = StrTable.from_strings(self.arr[::-1])
+        r = self._rev.lookup(queries)
+        return np.where(r >= 0, len(self.arr) - 1 - r, -1)
+
+    @property
+    def dict(self) -> Dict[str, float]:
+        if self._dict is None:
+            self._dict = {w: float(i) for i, w in enumerate(self.arr)}
+        return self._dict
 
 
 class _StringArraysModel(ModelWithData):
@@ -260,10 +314,13 @@ class _StringArraysModel(ModelWithData):
         return ([ser.read_string_array(inp) for _ in range(inp.read_int())],)
 
     @classmethod
-    def make_model_data_table(cls, rows):
+    def make_model_data_table(cls, rows, strings_only: bool = False):
+        """``strings_only``: the arrays already hold str objects only (no String.valueOf pass)."""
         def as_str(v):
             return v if isinstance(v, str) else java_number_to_string(v)
 
+        if strings_only:
+            return Table({"stringArrays": [[list(a) for a in r[0]] for r in rows]}, num_rows=len(rows))
         return Table({"stringArrays": [[[as_str(v) for v in a] for a in r[0]] for r in rows]}, num_rows=len(rows))
 
 
@@ -275,7 +332,9 @@ class StringIndexerModel(_StringArraysModel, StringIndexerModelParams):
     JAVA_CLASS_NAME = "org.apache.flink.ml.feature.stringindexer.StringIndexerModel"
 
     def _build_state(self, rows):
-        return [{s: float(i) for i, s in enumerate(arr)} for arr in rows[0][0]]
+        # one native string table per input column (first index of equal strings wins, like the
+        # reference's HashMap built in array order); the per-row dict is made only if needed
+        return [_LookupTable(arr) for arr in rows[0][0]]
 
     def transform(self, *inputs):
         t = inputs[0]
@@ -288,13 +347,14 @@ class StringIndexerModel(_StringArraysModel, StringIndexerModelParams):
             m = maps[i]
             col = t.column(c)
             if isinstance(col, StringColumn):
-                # look up each distinct string once, gather by code
+                # look up each distinct string once (native hash join), gather by code
                 codes = col.codes.to(config.compute_device()).long()
                 keys = col.vocab
-                for w in keys:
-                    if not isinstance(w, str):
-                        raise RuntimeError("The input column only supports string and numeric type.")
-                lut = torch.tensor([m.get(k, -1.0) for k in keys], dtype=torch.float64, device=codes.device)
+                try:
+                    qtab = StrTable.from_strings(keys)
+                except TypeError:
+                    raise RuntimeError("The input column only supports string and numeric type.") from None
+                lut = torch.from_numpy(m.lookup(qtab).astype(np.float64)).to(codes.device)
                 idx = lut[codes]
                 bad = idx < 0
                 if bool(bad.any()):
@@ -310,7 +370,7 @@ class StringIndexerModel(_StringArraysModel, StringIndexerModelParams):
                 u, inv = torch.unique(col, return_inverse=True)
                 is_int = not col.dtype.is_floating_point
                 keys = [str(int(v)) if is_int else java_number_to_string(v) for v in u.tolist()]
-                lut = torch.tensor([m.get(k, -1.0) for k in keys], dtype=torch.float64, device=col.device)
+                lut = torch.from_numpy(m.lookup(StrTable.from_strings(keys)).astype(np.float64)).to(col.device)
                 idx = lut[inv]
                 bad = idx < 0
                 if bool(bad.any()):
@@ -331,8 +391,8 @@ class StringIndexerModel(_StringArraysModel, StringIndexerModelParams):
                         s = java_number_to_string(v.item() if hasattr(v, "item") else v)
                     else:
                         raise RuntimeError("The input column only supports string and numeric type.")
-                    if s in m:
-                        vals.append(m[s])
+                    if s in m.dict:
+                        vals.append(m.dict[s])
                     elif hi == self.ERROR_INVALID:
                         raise RuntimeError("The input contains unseen string: %s. See handleInvalid parameter for "
                                            "more options." % s)
@@ -357,16 +417,17 @@ class StringIndexer(Estimator, StringIndexerParams):
         cols = self.get(self.INPUT_COLS)
         if len(cols) != len(self.get(self.OUTPUT_COLS)):
             raise ValueError("The number of input columns and output columns must be equal.")
-        local = [_string_counts(t, c) for c in cols]
-        parts = comm.all_gather_object(local) if get_world_distributed() else [local]
         arrays = []
-        for ci in range(len(cols)):
-            merged: Dict[str, int] = {}
-            for p in parts:
-                for k, v in p[ci].items():
-                    merged[k] = merged.get(k, 0) + v
-            arrays.append(_order_strings(merged, self.get(self.STRING_ORDER_TYPE)))
-        m = StringIndexerModel().set_model_data(StringIndexerModel.make_model_data_table([(arrays,)]))
+        for c in cols:
+            # per-rank (string, count, first position) tables merged by a keyed shuffle of the
+            # strings (all-to-all to the owner of each string's hash, owners' maps all-gathered)
+            tab, cnt, first = _string_counts_table(t, c)
+            tab, sums, _ = ds.reduce_strings_by_key(tab, cnt[:, None], first)
+            perm = order_string_table(tab, sums[:, 0], self.get(self.STRING_ORDER_TYPE))
+            strs = tab.strings()
+            arrays.append([strs[i] for i in perm.tolist()])
+        m = StringIndexerModel().set_model_data(StringIndexerModel.make_model_data_table([(arrays,)],
+                                                                                         strings_only=True))
         rw_update(m, self)
         return m
 
@@ -382,15 +443,14 @@ class IndexToStringModel(_StringArraysModel, HasInputCols, HasOutputCols):
         arrays = self.model_data_rows()[0][0]
         res = {}
         for i, (c, o) in enumerate(zip(self.get(self.INPUT_COLS), self.get(self.OUTPUT_COLS))):
-            ids = _numeric_col(t, c).to(torch.int64).tolist()
+            # the output is dictionary-encoded: codes = the indices (validated on the device),
+            # dictionary = the model array — no per-row strings are built
+            ids = _numeric_col(t, c).to(torch.int64)
             arr = arrays[i]
-            out = []
-            for sid in ids:
-                if 0 <= sid < len(arr):
-                    out.append(arr[sid])
-                else:
-                    raise RuntimeError("The input contains unseen index: %d." % sid)
-            res[o] = out
+            bad = (ids < 0) | (ids >= len(arr))
+            if bool(bad.any()):
+                raise RuntimeError("The input contains unseen index: %d." % int(ids[bad][0]))
+            res[o] = StringColumn(ids.to(torch.int32), arr)
         return [t.with_columns(res)]
 
 
@@ -493,28 +553,47 @@ class VectorIndexer(Estimator, VectorIndexerParams):
         t = inputs[0]
         max_cat = self.get(self.MAX_CATEGORIES)
         X = _dense_matrix(t, self.get(self.INPUT_COL)).to(torch.float64)
-        local: List[Optional[List[float]]] = []
-        if X.shape[0]:
+        n, d = X.shape
+        dist = get_world_distributed()
+        # a column is categorical when its GLOBAL distinct count is <= maxCategories; a rank with
+        # more local distinct values already rules it out (agreed by one all-reduce)
+        stats = torch.zeros(d + 2, dtype=torch.float64)
+        stats[d], stats[d + 1] = float(n), float(d)
+        if n:
             S, _ = torch.sort(X, dim=0)
-            distinct = 1 + (S[1:] != S[:-1]).sum(0)
-            ok = (distinct <= max_cat).tolist()
-            for c in range(X.shape[1]):
-                local.append(torch.unique(S[:, c]).tolist() if ok[c] else None)
-        parts = comm.all_gather_object(local) if get_world_distributed() else [local]
-        parts = [p for p in parts if p]
-        if not parts:
+            stats[:d] = (1 + (S[1:] != S[:-1]).sum(0)).to(torch.float64).cpu()
+        if dist:
+            dmax = comm.all_reduce(stats[d + 1:].clone(), "max")
+            if n and float(dmax[0]) != d:
+                raise ValueError("Feature vectors should be of equal length.")
+            d = int(dmax[0])
+            loc = torch.zeros(d + 1, dtype=torch.float64)
+            loc[:stats.shape[0] - 2] = stats[:-2] if n else 0.0
+            loc[d] = float(n)
+            red_max = comm.all_reduce(loc[:d].clone(), "max")
+            total = comm.all_reduce_scalar(float(n), "sum")
+        else:
+            red_max, total = stats[:d], float(n)
+        if total == 0:
             raise RuntimeError("The training set is empty.")
-        d = len(parts[0])
+        cand = [c for c in range(d) if red_max[c] <= max_cat]
         maps = {}
-        for c in range(d):
-            vals = set()
-            for p in parts:
-                if p[c] is None:
-                    vals = None
-                    break
-                vals.update(p[c])
-            if vals is not None and len(vals) <= max_cat:
-                maps[c] = _category_map(vals)
+        if cand:
+            # distinct (column, value) keys over all ranks: one keyed shuffle (VectorIndexer.java's
+            # per-column distinct-value aggregation)
+            if n:
+                Xc = X[:, cand]
+                keys = torch.stack([torch.arange(len(cand), device=X.device)[None, :].expand(n, len(cand)),
+                                    ds.float_keys(Xc).reshape(n, len(cand))], -1).reshape(-1, 2)
+            else:
+                keys = torch.zeros((0, 2), dtype=torch.int64, device=X.device)
+            uk, _ = ds.global_distinct(keys)
+            uk = uk.cpu()
+            col, vals = uk[:, 0].numpy(), ds.keys_to_float(uk[:, 1]).numpy()
+            for i, c in enumerate(cand):
+                v = vals[col == i]
+                if v.shape[0] <= max_cat:
+                    maps[c] = _category_map(v.tolist())
         m = VectorIndexerModel().set_model_data(VectorIndexerModel.make_model_data_table([(maps,)]))
         rw_update(m, self)
         return m
@@ -756,18 +835,14 @@ class Imputer(Estimator, ImputerParams):
                 sur[c] = float(exact_quantiles(x[:, None], [0.5], self.get(self.RELATIVE_ERROR))[0, 0])
         else:
             for c, x in zip(cols, xs):
-                u, cnt = torch.unique(x, return_counts=True)
-                local = list(zip(u.tolist(), cnt.tolist()))
-                parts = comm.all_gather_object(local) if dist else [local]
-                counts: Counter = Counter()
-                for p in parts:
-                    for v, n in p:
-                        counts[v] += n
-                if not counts:
+                # value counts over all ranks by a keyed shuffle of the values' bit patterns
+                k, cnt = ds.global_distinct(ds.float_keys(x.reshape(-1)))
+                if k.numel() == 0:
                     sur[c] = float("nan")
                     continue
-                best = max(counts.values())
-                sur[c] = min(v for v, n in counts.items() if n == best)
+                v = ds.keys_to_float(k)
+                best = cnt.max()
+                sur[c] = float(v[cnt == best].min())
             if all(math.isnan(v) for v in sur.values()):
                 raise RuntimeError("The training set is empty or does not contains valid data.")
         m = ImputerModel().set_model_data(ImputerModel.make_model_data_table([(sur,)]))

@@ -28,12 +28,14 @@ from ...linalg.vectors import DenseVector, SparseVector, Vector
 from ...ops import hashing
 from ...param.param import (BooleanParam, FloatParam, IntParam, ParamValidators, StringArrayParam, StringParam)
 from ...parallel import comm
+from ...parallel import datastream as ds
 from ...table import SparseColumn, StringArrayColumn, StringColumn, Table
 from ...utils.java import java_hashmap_order as _java_hashmap_order
 from ...utils.java import java_number_to_string, java_string_hash
+from ...utils.strtable import StrTable, hashmap_order_from_hashes
 from ..base import ModelWithData
 from ..linear import rw_update
-from .common import dec_dense, enc_dense, vector_input
+from .common import dec_dense, enc_dense, get_world_distributed, vector_input
 
 ENGLISH_STOP_WORDS = (
     'a', 'about', 'above', 'after', 'again', 'against', 'all', 'am', 'an', 'and', 'any', 'are', "aren't",
@@ -533,7 +535,15 @@ class CountVectorizer(Estimator, CountVectorizerParams):
 
     def fit(self, *inputs):
         dc = _dict_col(inputs[0], self.get(self.INPUT_COL))
-        if dc is not None and len(set(dc.vocab)) == len(dc.vocab):
+        tab = None
+        if dc is not None:
+            try:
+                tab = StrTable.from_strings(dc.vocab)
+            except TypeError:
+                tab = None
+            if tab is not None and not np.array_equal(tab.first_of_equal(), np.arange(len(tab))):
+                tab = None  # repeated dictionary entries: per-document counting on the host path
+        if tab is not None:
             # term and document frequencies per distinct string from the codes on the device; the
             # first-occurrence order (it decides HashMap bucket-collision order) via a scatter-min
             V = len(dc.vocab)
@@ -558,11 +568,10 @@ class CountVectorizer(Estimator, CountVectorizerParams):
                 if not bool((first[present] == N).any()):
                     break
                 s0, step = e0, step * 4
-            present = present[torch.argsort(first[present], stable=True)].cpu().tolist()
-            tf_h, df_h = tf_t.cpu().tolist(), df_t.cpu().tolist()
-            order = [dc.vocab[c] for c in present]
-            tf = {dc.vocab[c]: tf_h[c] for c in present}
-            df = {dc.vocab[c]: df_h[c] for c in present}
+            pres_h = present.cpu().numpy()
+            tab = tab.take(pres_h)
+            sums = torch.stack([tf_t[present], df_t[present]], 1).cpu().numpy().astype(np.float64)
+            firsts = first[present].cpu().numpy()
             ndocs = len(dc)
         else:
             docs = _strings_col(inputs[0], self.get(self.INPUT_COL))
@@ -575,27 +584,28 @@ class CountVectorizer(Estimator, CountVectorizerParams):
                     tf[w] += c
                     df[w] += 1
             ndocs = len(docs)
-        parts = comm.all_gather_object((ndocs, order, tf, df))
-        rows = sum(p[0] for p in parts)
+            tab = StrTable.from_strings(order)
+            sums = np.array([[tf[w], df[w]] for w in order], dtype=np.float64).reshape(-1, 2)
+            firsts = np.arange(len(order), dtype=np.int64)
+        # the per-rank vocabularies merged by a keyed shuffle of the strings (first-seen order:
+        # rank, then position), document counts summed
+        tab, sums, _ = ds.reduce_strings_by_key(tab, sums, firsts)
+        rows = int(comm.all_reduce_scalar(float(ndocs), "sum")) if get_world_distributed() else ndocs
         if rows == 0:
             raise RuntimeError("The training set is empty.")
-        g_order, g_df = [], {}
-        for _, o, _tf, d in parts:
-            for w in o:
-                if w not in g_df:
-                    g_order.append(w)
-                    g_df[w] = 0
-                g_df[w] += d[w]
+        g_df = sums[:, 1]
         min_df, max_df = self.get(self.MIN_DF), self.get(self.MAX_DF)
-        keys = java_hashmap_order(g_order)
+        keys = hashmap_order_from_hashes(tab.java_hashes())
         if min_df != self.MIN_DF.default_value or max_df != self.MAX_DF.default_value:
             amin = min_df if min_df >= 1.0 else min_df * rows
             amax = max_df if max_df >= 1.0 else max_df * rows
             if amax < amin:
                 raise RuntimeError("maxDF must be >= minDF.")
-            keys = java_hashmap_order([k for k in keys if amin <= g_df[k] <= amax])
-        keys = sorted(keys, key=lambda k: -g_df[k])  # stable, like List.sort
-        vocab = keys[: self.get(self.VOCABULARY_SIZE)]
+            kept = keys[(g_df[keys] >= amin) & (g_df[keys] <= amax)]
+            keys = kept[hashmap_order_from_hashes(tab.java_hashes()[kept])]
+        keys = keys[np.argsort(-g_df[keys], kind="stable")]  # stable, like List.sort
+        strs = tab.strings()
+        vocab = [strs[i] for i in keys[: self.get(self.VOCABULARY_SIZE)].tolist()]
         m = CountVectorizerModel().set_model_data(CountVectorizerModel.make_model_data_table([(vocab,)]))
         rw_update(m, self)
         return m

@@ -32,7 +32,7 @@ from ..utils.java import java_double_hash, java_hashmap_order
 from .base import ModelWithData
 from .feature.common import get_world_distributed
 from .linear import rw_update
-from .stats import features_and_labels, global_sorted_unique
+from .stats import features_and_labels, global_sorted_unique, value_label_counts
 
 
 class NaiveBayesModelParams(HasFeaturesCol, HasPredictionCol):
@@ -118,8 +118,10 @@ def _label_value_counts(X: torch.Tensor, li: torch.Tensor, L: int, dist: bool):
     aggregations) as one device histogram. Returns counts [d, L, Vmax] (numpy), per-feature sorted
     distinct values and their slots in the last axis, and per-label row counts.
 
-    Small non-negative integer features (the categorical case) index the histogram directly;
-    anything else goes through one column-wise sort + batched searchsorted."""
+    Small non-negative integer features (the categorical case) index the histogram directly
+    (one all-reduce of the dense histogram across ranks); anything else goes through one
+    column-wise sort + batched searchsorted on one rank, and through the keyed (feature, value,
+    label) shuffle of ``stats.value_label_counts`` across ranks."""
     n, d = X.shape
     dev = X.device
     n_lab = torch.bincount(li, minlength=L).to(torch.float64)
@@ -142,36 +144,34 @@ def _label_value_counts(X: torch.Tensor, li: torch.Tensor, L: int, dist: bool):
         present = counts.sum(1) > 0
         slots = [np.nonzero(present[j])[0] for j in range(d)]
         return counts, [sl.astype(np.float64) for sl in slots], slots, n_lab.cpu().numpy()
+    if dist:
+        # (feature, value, label) counts and the distinct values in one keyed shuffle
+        vals_t, flat, Vn = value_label_counts(X, li, L)
+        Vmax = max(1, int(Vn.max()) if d else 1)
+        counts = np.zeros((d, L, Vmax), dtype=np.float64)
+        off = 0
+        for j in range(d):
+            V = int(Vn[j])
+            counts[j, :, :V] = flat[off:off + V * L].reshape(V, L).T
+            off += V * L
+        n_lab = comm.all_reduce_sum(n_lab)
+        return (counts, [v.cpu().numpy() for v in vals_t], [np.arange(int(Vn[j])) for j in range(d)],
+                n_lab.cpu().numpy())
     Xt = X.t().contiguous()
     S = torch.sort(Xt, dim=1).values if n else Xt
-    if dist:
-        local = [S[j][torch.cat([S.new_ones(1, dtype=torch.bool), S[j, 1:] != S[j, :-1]])].cpu().tolist()
-                 if n else [] for j in range(d)]
-        parts = comm.all_gather_object(local)
-        vals_list = [sorted(set(x for p in parts for x in p[j])) for j in range(d)]
-        Vn = np.array([len(v) for v in vals_list], dtype=np.int64)
-        Vmax = max(1, int(Vn.max()) if d else 1)
-        table = torch.full((d, Vmax), float("inf"), dtype=torch.float64)
-        for j, v in enumerate(vals_list):
-            table[j, :len(v)] = torch.tensor(v, dtype=torch.float64)
-        table = table.to(dev)
-    else:
-        start = torch.ones_like(S, dtype=torch.bool)
-        if n > 1:
-            start[:, 1:] = S[:, 1:] != S[:, :-1]
-        pos = torch.cumsum(start.to(torch.int64), dim=1) - 1
-        Vn = (pos[:, -1] + 1).cpu().numpy() if n else np.zeros(d, dtype=np.int64)
-        Vmax = max(1, int(Vn.max()) if d else 1)
-        table = torch.full((d, Vmax), float("inf"), dtype=torch.float64, device=dev)
-        # every element of a run writes the same value to its slot; padding stays +inf
-        table.scatter_(1, pos, S.to(torch.float64))
+    start = torch.ones_like(S, dtype=torch.bool)
+    if n > 1:
+        start[:, 1:] = S[:, 1:] != S[:, :-1]
+    pos = torch.cumsum(start.to(torch.int64), dim=1) - 1
+    Vn = (pos[:, -1] + 1).cpu().numpy() if n else np.zeros(d, dtype=np.int64)
+    Vmax = max(1, int(Vn.max()) if d else 1)
+    table = torch.full((d, Vmax), float("inf"), dtype=torch.float64, device=dev)
+    # every element of a run writes the same value to its slot; padding stays +inf
+    table.scatter_(1, pos, S.to(torch.float64))
     codes = torch.searchsorted(table, Xt.to(torch.float64))
     jj = torch.arange(d, device=dev, dtype=torch.int64)[:, None]
     key = (jj * L + li[None, :]) * Vmax + codes
     cnt = torch.bincount(key.reshape(-1), minlength=d * L * Vmax).to(torch.float64)
-    if dist:
-        both = comm.all_reduce_sum(torch.cat([cnt, n_lab]))
-        cnt, n_lab = both[:-L], both[-L:]
     table_np = table.cpu().numpy()
     slots = [np.arange(int(Vn[j])) for j in range(d)]
     return (cnt.reshape(d, L, Vmax).cpu().numpy(), [table_np[j, :int(Vn[j])] for j in range(d)], slots,
@@ -195,9 +195,11 @@ class NaiveBayes(Estimator, NaiveBayesParams):
             raise ValueError("Label value should be indexed number.")
         s = self.get(self.SMOOTHING)
         dist = get_world_distributed()
-        dims = comm.all_gather_object(int(X.shape[1])) if dist else [int(X.shape[1])]
-        if len(set(d for d, r in zip(dims, range(len(dims))))) > 1:
-            raise ValueError("Feature vectors should be of equal length.")
+        if dist:
+            try:
+                comm.check_equal_across_ranks(int(X.shape[1]), "feature vector length")
+            except ValueError:
+                raise ValueError("Feature vectors should be of equal length.") from None
         labels = global_sorted_unique(y)
         L, d = labels.numel(), X.shape[1]
         li = torch.searchsorted(labels, y)

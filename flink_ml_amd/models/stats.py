@@ -29,6 +29,7 @@ from ..io import read_write as rw
 from ..linalg.vectors import DenseVector
 from ..ops import features as fo
 from ..parallel import comm
+from ..parallel import datastream as ds
 from ..table import SparseColumn, Table
 from .feature.common import get_world_distributed
 
@@ -52,12 +53,43 @@ def features_and_labels(t: Table, features_col: str, label_col: str,
 
 
 def global_sorted_unique(v: torch.Tensor) -> torch.Tensor:
-    """Sorted union of the ranks' distinct values (small: labels / categories)."""
+    """Sorted union of the ranks' distinct values (labels / categories): a keyed distinct over
+    the values' bit patterns (all-to-all to the key owners, all-gather of their results)."""
     u = torch.unique(v)
     if get_world_distributed():
-        parts = comm.all_gather_object(u.cpu().tolist())
-        u = torch.tensor(sorted(set(x for p in parts for x in p)), dtype=v.dtype, device=v.device)
+        k, _ = ds.global_distinct(ds.float_keys(u))
+        u = torch.sort(ds.keys_to_float(k)).values.to(device=v.device, dtype=v.dtype)
     return u
+
+
+def value_label_counts(X: torch.Tensor, li: torch.Tensor, L: int):
+    """(feature, value, label) counts over all ranks as ONE keyed reduce — the keyed
+    aggregations of ``ChiSqTest.java:127-130`` and ``NaiveBayes.java:95-103``: keys
+    (j, value bits, label) are summed rank-locally, shuffled to their owner rank
+    (``datastream.reduce_by_key_tensor``) and the owners' results gathered.
+
+    Returns (vals, flat, Vn): per feature the sorted distinct values (float64 tensors), the
+    counts as one flat float64 array with feature j's [V_j, L] block (value-major) at offset
+    Σ_{i<j} V_i·L, and V_j per feature."""
+    n, d = X.shape
+    dev = X.device
+    jj = torch.arange(d, device=dev, dtype=torch.int64)[None, :].expand(n, d)
+    keys = torch.stack([jj, ds.float_keys(X).reshape(n, d), li.to(torch.int64)[:, None].expand(n, d)], -1)
+    uk, cnt = ds.global_distinct(keys.reshape(-1, 3))
+    jb, inv = torch.unique(uk[:, :2], dim=0, return_inverse=True)
+    fl = ds.keys_to_float(jb[:, 1])
+    o1 = torch.argsort(fl, stable=True)
+    o2 = o1[torch.argsort(jb[o1, 0], stable=True)]  # (feature, value) order
+    U = jb.shape[0]
+    rank = torch.empty(U, dtype=torch.int64, device=uk.device)
+    rank[o2] = torch.arange(U, device=uk.device)
+    Vn = torch.bincount(jb[:, 0], minlength=d)
+    start = torch.cumsum(Vn, 0) - Vn
+    vidx = rank[inv] - start[uk[:, 0]]
+    flat = torch.zeros(U * L, dtype=torch.float64, device=uk.device)
+    flat[(start[uk[:, 0]] + vidx) * L + uk[:, 2]] = cnt.to(torch.float64)
+    vals = list(torch.split(fl[o2], Vn.tolist())) if d else []
+    return [v.to(dev) for v in vals], flat.cpu().numpy(), Vn.cpu().numpy()
 
 
 def class_sums(X: torch.Tensor, ci: torch.Tensor, C: int, chunk: int = 1 << 20) -> torch.Tensor:
@@ -176,18 +208,16 @@ class ChiSqTest(AlgoOperator, _TestParams):
         labels = global_sorted_unique(y)
         L, d = labels.numel(), X.shape[1]
         li = torch.searchsorted(labels, y)
-        local_vals = [torch.unique(X[:, j]) for j in range(d)]
         if get_world_distributed():
-            parts = comm.all_gather_object([v.cpu().tolist() for v in local_vals])
-            vals = [torch.tensor(sorted(set(x for p in parts for x in p[j])), dtype=torch.float64, device=X.device)
-                    for j in range(d)]
+            # distinct values and contingency counts in one keyed shuffle (no value lists pickled)
+            vals, flat, _ = value_label_counts(X, li, L)
         else:
-            vals = local_vals
-        tables = []
-        for j in range(d):
-            vi = torch.searchsorted(vals[j], X[:, j].contiguous())
-            tables.append(torch.bincount(vi * L + li, minlength=vals[j].numel() * L).to(torch.float64))
-        flat = _reduce(torch.cat(tables)).cpu().numpy() if tables else np.zeros(0)
+            vals = [torch.unique(X[:, j]) for j in range(d)]
+            tables = []
+            for j in range(d):
+                vi = torch.searchsorted(vals[j], X[:, j].contiguous())
+                tables.append(torch.bincount(vi * L + li, minlength=vals[j].numel() * L).to(torch.float64))
+            flat = torch.cat(tables).cpu().numpy() if tables else np.zeros(0)
         p_out, dof_out, stat_out, off = [], [], [], 0
         for j in range(d):
             V = vals[j].numel()

@@ -12,7 +12,8 @@ reference                   here
 ``reduce`` (:132-143)       ``reduce`` — local fold, all-gather, fold in rank order
 keyed ``reduce`` (:155)     ``reduce_by_key`` — per-key local folds, all-gather, merge (host
                               objects); ``reduce_by_key_tensor`` — device keys/values: local
-                              segment reduce, hash-partitioned all-to-all, owner-side merge
+                              segment reduce, hash-partitioned all-to-all, owner-side merge;
+                              ``reduce_strings_by_key`` — string keys (code-unit tensors)
 ``aggregate`` (:182-199)    ``aggregate`` — local accumulator, all-gather, merge in rank order
 ``sample`` (:212-227)       ``sample`` — reservoir per rank (java.util.Random), gather, again
 ``generateBatchData``       ``generate_batch_data`` — deterministic per-rank split of a global
@@ -71,8 +72,15 @@ def reduce_by_key(pairs: Sequence, fn: Callable[[Any, Any], Any]) -> dict:
     return out
 
 
+def _unique_rows(keys: torch.Tensor):
+    """Sorted unique keys (rows, lexicographic, for [n, m] keys) and the inverse map."""
+    if keys.dim() == 1:
+        return torch.unique(keys, return_inverse=True)
+    return torch.unique(keys, dim=0, return_inverse=True)
+
+
 def _segment_reduce(keys: torch.Tensor, values: torch.Tensor, op: str):
-    uk, inv = torch.unique(keys, return_inverse=True)
+    uk, inv = _unique_rows(keys)
     shape = (uk.shape[0],) + tuple(values.shape[1:])
     if op == "sum":
         out = torch.zeros(shape, dtype=values.dtype, device=values.device).index_add_(0, inv, values)
@@ -85,23 +93,38 @@ def _segment_reduce(keys: torch.Tensor, values: torch.Tensor, op: str):
     return uk, out
 
 
+def key_owner(keys: torch.Tensor, world: int) -> torch.Tensor:
+    """Owner rank of every key (``keyBy`` partitioning): a 64-bit mix of the key's columns mod
+    ``world`` — the same on every rank and for every world size's own partitioning."""
+    h = keys if keys.dim() == 1 else keys[:, 0]
+    h = h.to(torch.int64)
+    if keys.dim() == 2:
+        for c in range(1, keys.shape[1]):
+            h = h * 0x100000001B3 + keys[:, c].to(torch.int64)  # wraps in two's complement
+    h = h ^ (h >> 29)
+    h = h * 0x2545F4914F6CDD1D
+    h = h ^ (h >> 32)
+    return torch.remainder(h, world)
+
+
 def reduce_by_key_tensor(keys: torch.Tensor, values: torch.Tensor, op: str = "sum", gather: bool = False):
     """Keyed ``DataStreamUtils.reduce`` (``DataStreamUtils.java:155``) for device data: integer
-    ``keys`` [n] and ``values`` [n, ...] stay on the device. Each rank folds its own rows per key
-    (sort-unique + index_add / scatter_reduce), sends every partial to the key's owner rank
-    (``key mod P`` — the keyBy shuffle) in ONE all-to-all, and the owner folds what it receives.
-    Returns this rank's (sorted keys, reduced values) — every key lives on exactly one rank, like
-    the reference's keyed reduce output; ``gather=True`` all-gathers the full result instead.
+    ``keys`` ([n], or [n, m] multi-column keys compared as rows) and ``values`` [n, ...] stay on
+    the device. Each rank folds its own rows per key (sort-unique + index_add / scatter_reduce),
+    sends every partial to the key's owner rank (``key_owner`` — the keyBy shuffle) in ONE
+    all-to-all, and the owner folds what it receives. Returns this rank's (sorted keys, reduced
+    values) — every key lives on exactly one rank, like the reference's keyed reduce output;
+    ``gather=True`` all-gathers the full result (sorted keys) instead.
     ``op`` is an associative, commutative reduction: sum, min or max."""
-    if keys.dim() != 1 or values.shape[0] != keys.shape[0]:
-        raise ValueError("keys [n] and values [n, ...] expected")
+    if keys.dim() not in (1, 2) or values.shape[0] != keys.shape[0]:
+        raise ValueError("keys [n] or [n, m] and values [n, ...] expected")
     keys = keys.to(torch.int64)
     uk, part = _segment_reduce(keys, values, op)
     ctx = get_context()
     if not ctx.is_distributed:
         return uk, part
     P = ctx.world_size
-    owner = torch.remainder(uk, P)
+    owner = key_owner(uk, P)
     order = torch.argsort(owner, stable=True)
     uk, part, owner = uk[order], part[order], owner[order]
     counts = torch.bincount(owner, minlength=P).tolist()
@@ -109,12 +132,103 @@ def reduce_by_key_tensor(keys: torch.Tensor, values: torch.Tensor, op: str = "su
     v_in = comm.all_to_all_v(list(torch.split(part, counts)))
     mk, mv = _segment_reduce(torch.cat(k_in), torch.cat(v_in), op)
     if gather:
-        ks = comm.all_gather_tensor(mk)
-        vs = comm.all_gather_tensor(mv)
-        ak, av = torch.cat(ks), torch.cat(vs)
-        o = torch.argsort(ak)
-        return ak[o], av[o]
+        ak = torch.cat(comm.all_gather_tensor(mk))
+        av = torch.cat(comm.all_gather_tensor(mv))
+        sk, inv = _unique_rows(ak)  # keys are unique across owners: a permutation
+        out = torch.empty_like(av)
+        out[inv] = av
+        return sk, out
     return mk, mv
+
+
+def float_keys(x: torch.Tensor) -> torch.Tensor:
+    """int64 keys of float64 values that compare equal exactly when the values are equal
+    (−0.0 folded into +0.0)."""
+    return (x.to(torch.float64) + 0.0).contiguous().view(torch.int64)
+
+
+def keys_to_float(k: torch.Tensor) -> torch.Tensor:
+    return k.to(torch.int64).contiguous().view(torch.float64)
+
+
+def global_distinct(keys: torch.Tensor):
+    """Distinct keys over all ranks (sorted; rows for [n, m] keys) with their global counts, on
+    every rank: one keyed reduce (all-to-all to the owners) + an all-gather of the owners'
+    results."""
+    ones = torch.ones(keys.shape[0], dtype=torch.float64, device=keys.device)
+    return reduce_by_key_tensor(keys, ones, "sum", gather=True)
+
+
+def _np_to_tensor(a: np.ndarray) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def reduce_strings_by_key(table, sums: np.ndarray, firsts: np.ndarray):
+    """Keyed merge of per-rank string maps (StringIndexer / CountVectorizer vocabularies,
+    ``StringIndexer.java:110-114`` keyBy + reduce): ``table`` (utils.strtable.StrTable) holds this
+    rank's strings, ``sums`` [n, k] their counters (summed per string), ``firsts`` [n] their
+    first-seen positions in the rank's data. Rows of one string are routed to the owner of its
+    64-bit content hash in one all-to-all of the tables (code units as tensors), the owner
+    merges equal strings (exact comparison: hash collisions stay apart), and the owners' results
+    are all-gathered. Returns (StrTable, sums, order key) on every rank, ordered by the global
+    first-seen key (rank, local first position) — the insertion order of the reference's merged
+    map when partitions are merged in rank order."""
+    from ..utils.strtable import StrTable
+
+    sums = np.asarray(sums, dtype=np.float64).reshape(len(table), -1)
+    firsts = np.asarray(firsts, dtype=np.int64)
+    ctx = get_context()
+    key = firsts + (np.int64(ctx.rank) << np.int64(40))
+
+    def merge_local(tab, sm, ky):
+        rep = tab.first_of_equal()
+        if len(tab) and not np.array_equal(rep, np.arange(len(tab))):
+            uniq, inv = np.unique(rep, return_inverse=True)
+            s2 = np.zeros((uniq.shape[0], sm.shape[1]), dtype=np.float64)
+            np.add.at(s2, inv, sm)
+            k2 = np.full(uniq.shape[0], np.iinfo(np.int64).max, dtype=np.int64)
+            np.minimum.at(k2, inv, ky)
+            return tab.take(uniq), s2, k2
+        return tab, sm, ky
+
+    table, sums, key = merge_local(table, sums, key)
+    if ctx.is_distributed:
+        P = ctx.world_size
+        owner = (table.hash64().view(np.uint64) % np.uint64(P)).astype(np.int64)
+        order = np.argsort(owner, kind="stable")
+        tab = table.take(order)
+        sm, ky, ow = sums[order], key[order], owner[order]
+        cnt = np.bincount(ow, minlength=P)
+        bounds = np.concatenate([[0], np.cumsum(cnt)])
+        ubounds = tab.offs[bounds]
+        lens = np.diff(tab.offs)
+        units = tab.units.astype(np.int32)
+        u_in = comm.all_to_all_v([_np_to_tensor(units[ubounds[r]:ubounds[r + 1]]) for r in range(P)])
+        l_in = comm.all_to_all_v([_np_to_tensor(lens[bounds[r]:bounds[r + 1]]) for r in range(P)])
+        s_in = comm.all_to_all_v([_np_to_tensor(sm[bounds[r]:bounds[r + 1]]) for r in range(P)])
+        k_in = comm.all_to_all_v([_np_to_tensor(ky[bounds[r]:bounds[r + 1]]) for r in range(P)])
+
+        def table_of(u_parts, l_parts):
+            u = np.concatenate([p.numpy() for p in u_parts]).astype(np.uint16) if u_parts else np.zeros(0, np.uint16)
+            ln = np.concatenate([p.numpy() for p in l_parts]) if l_parts else np.zeros(0, np.int64)
+            offs = np.zeros(ln.shape[0] + 1, dtype=np.int64)
+            np.cumsum(ln, out=offs[1:])
+            return StrTable(u, offs)
+
+        mine = table_of(u_in, l_in)
+        msum = np.concatenate([p.numpy().reshape(-1, sums.shape[1]) for p in s_in])
+        mkey = np.concatenate([p.numpy() for p in k_in])
+        mine, msum, mkey = merge_local(mine, msum, mkey)
+        # every rank gets the whole merged map
+        g_units = comm.all_gather_tensor(_np_to_tensor(mine.units.astype(np.int32)))
+        g_lens = comm.all_gather_tensor(_np_to_tensor(np.diff(mine.offs)))
+        g_sums = comm.all_gather_tensor(_np_to_tensor(msum))
+        g_keys = comm.all_gather_tensor(_np_to_tensor(mkey))
+        table = table_of(g_units, g_lens)
+        sums = np.concatenate([p.numpy().reshape(-1, msum.shape[1]) for p in g_sums])
+        key = np.concatenate([p.numpy() for p in g_keys])
+    order = np.argsort(key, kind="stable")
+    return table.take(order), sums[order], key[order]
 
 
 def set_managed_memory_weight(stream, weight: int):

@@ -108,6 +108,8 @@ def _keyed_tensor_worker(rank, world):
 
 
 def test_reduce_by_key_tensor_across_ranks():
+    from flink_ml_amd.parallel.datastream import key_owner
+
     world = 3
     res = [(torch.from_numpy(k), torch.from_numpy(v), {op: tuple(map(torch.from_numpy, kv)) for op, kv in own.items()},
             tuple(map(torch.from_numpy, full))) for k, v, own, full in run_spmd(_keyed_tensor_worker, world)]
@@ -119,7 +121,7 @@ def test_reduce_by_key_tensor_across_ranks():
         seen = []
         for rank, (_, _, own, _) in enumerate(res):
             k, v = own[op]
-            assert torch.all(torch.remainder(k, world) == rank)  # each key reduced on its owner only
+            assert torch.all(key_owner(k, world) == rank)  # each key reduced on its owner only
             for kk, vv in zip(k.tolist(), v):
                 torch.testing.assert_close(vv, red(V[K == kk]))
             seen += k.tolist()

@@ -1,0 +1,105 @@
+"""Keyed (hash) shuffles in the algorithms: NaiveBayes, ChiSqTest,
+StringIndexer, CountVectorizer, VectorIndexer and Imputer merge their per-rank maps through
+``datastream.reduce_by_key_tensor`` / ``reduce_strings_by_key`` (an all-to-all to the key owners,
+then an all-gather of the owners' results) instead of pickled host lists. A 4-rank gloo run over
+≥ 100k distinct keys must equal the 1-rank fit of the concatenated data exactly (reference:
+``NaiveBayes.java:95-103``, ``ChiSqTest.java:127-130``, ``StringIndexer.java:110-114``; the
+reference tests run the same jobs on a parallelism-4 MiniCluster)."""
+import numpy as np
+import torch
+
+from tests.spmd import run_spmd
+
+WORLD = 4
+N = 160_000
+
+
+def _data():
+    g = torch.Generator().manual_seed(21)
+    X = torch.floor(torch.rand((N, 3), generator=g, dtype=torch.float64) * 60_000) / 7.0  # non-integer values
+    y = (torch.rand(N, generator=g) < 0.4).to(torch.float64)
+    words = ["w%d" % v for v in torch.randint(0, 250_000, (N,), generator=g).tolist()]
+    doc_lens = torch.randint(1, 6, (N // 8,), generator=g).tolist()
+    toks = torch.randint(0, 150_000, (sum(doc_lens),), generator=g).tolist()
+    docs, k = [], 0
+    for ln in doc_lens:
+        docs.append(["t%d" % v for v in toks[k:k + ln]])
+        k += ln
+    C = torch.randint(0, 12, (N, 4), generator=g).to(torch.float64) * 0.5
+    C[:, 3] = torch.floor(torch.rand(N, generator=g, dtype=torch.float64) * 1000)  # not categorical
+    imp = torch.randint(0, 40_000, (N,), generator=g).to(torch.float64)
+    return X, y, words, docs, C, imp
+
+
+def _fit_all(X, y, words, docs, C, imp):
+    from flink_ml_amd import Table
+    from flink_ml_amd.models import NaiveBayes
+    from flink_ml_amd.models.feature.encoders import Imputer, StringIndexer, VectorIndexer
+    from flink_ml_amd.models.feature.text import CountVectorizer
+    from flink_ml_amd.models.stats import ChiSqTest
+    from flink_ml_amd.table import StringArrayColumn, StringColumn
+
+    out = {}
+    t = Table({"features": X, "label": y})
+    nb = NaiveBayes().fit(t).get_model_data()[0].rows()[0]
+    theta, pi, labels = nb
+    out["nb"] = ([[sorted(m.items()) for m in row] for row in theta], list(pi.values), list(labels.values))
+    chi = ChiSqTest().set_flatten(True).transform(t)[0]
+    out["chi"] = [chi.column(c).cpu().numpy().tolist() if hasattr(chi.column(c), "cpu") else list(chi.column(c))
+                  for c in chi.column_names]
+    ts = Table({"col0": StringColumn.from_list(words)})
+    for order in ("alphabetAsc", "frequencyDesc", "arbitrary"):
+        m = StringIndexer().set_input_cols("col0").set_output_cols("o").set_string_order_type(order).fit(ts)
+        out["si_" + order] = m.get_model_data()[0].rows()[0][0][0]
+    td = Table({"input": StringArrayColumn.from_lists(docs)})
+    out["cv"] = CountVectorizer().fit(td).get_model_data()[0].rows()[0][0]
+    vi = VectorIndexer().set_max_categories(30).fit(Table({"input": C})).get_model_data()[0].rows()[0][0]
+    out["vi"] = {k: sorted(v.items()) for k, v in vi.items()}
+    im = Imputer().set_input_cols("a").set_output_cols("b").set_strategy("most_frequent")
+    out["imp"] = im.fit(Table({"a": imp})).get_model_data()[0].rows()[0][0]
+    return out
+
+
+def _worker(rank, world):
+    X, y, words, docs, C, imp = _data()
+    lo, hi = N * rank // world, N * (rank + 1) // world
+    dlo, dhi = len(docs) * rank // world, len(docs) * (rank + 1) // world
+    return _fit_all(X[lo:hi], y[lo:hi], words[lo:hi], docs[dlo:dhi], C[lo:hi], imp[lo:hi])
+
+
+def test_keyed_shuffles_match_one_rank():
+    X, y, words, docs, C, imp = _data()
+    assert len(set(words)) > 100_000 and len(set(X[:, 0].tolist())) * 3 > 100_000  # distinct keys
+    ref = _fit_all(X, y, words, docs, C, imp)
+    res = run_spmd(_worker, WORLD, timeout=600)
+    for r in res:
+        for k in ref:
+            assert r[k] == ref[k], k
+    assert len(ref["si_alphabetAsc"]) > 100_000 and len(ref["vi"]) == 3
+
+
+def _no_pickle_worker(rank, world):
+    """The keyed merges never go through ``all_gather_object``."""
+    from flink_ml_amd.parallel import comm
+
+    calls = []
+    orig = comm.all_gather_object
+
+    def spy(obj):
+        calls.append(type(obj).__name__)
+        return orig(obj)
+
+    comm.all_gather_object = spy
+    try:
+        X, y, words, docs, C, imp = _data()
+        n = 4000
+        lo = n * rank
+        _fit_all(X[lo:lo + n], y[lo:lo + n], words[lo:lo + n], docs[:200], C[lo:lo + n], imp[lo:lo + n])
+    finally:
+        comm.all_gather_object = orig
+    return calls
+
+
+def test_keyed_merges_do_not_pickle():
+    for calls in run_spmd(_no_pickle_worker, 2, timeout=300):
+        assert calls == [], calls
