@@ -200,7 +200,9 @@ def _string_counts_table(t: Table, col: str):
         first = first_occurrence(codes, V)
         present = torch.nonzero(cnt > 0).reshape(-1)
         pres = present.cpu().numpy()
-        return tab.take(pres), cnt[present].cpu().numpy(), first[present].cpu().numpy()
+        if pres.shape[0] != V:  # vocabulary entries with no rows left (a filtered column)
+            tab = tab.take(pres)
+        return tab, cnt[present].cpu().numpy(), first[present].cpu().numpy()
     if isinstance(c, torch.Tensor):
         if c.dim() != 1:
             raise RuntimeError("The input column only supports string and numeric type.")
@@ -424,8 +426,7 @@ class StringIndexer(Estimator, StringIndexerParams):
             tab, cnt, first = _string_counts_table(t, c)
             tab, sums, _ = ds.reduce_strings_by_key(tab, cnt[:, None], first)
             perm = order_string_table(tab, sums[:, 0], self.get(self.STRING_ORDER_TYPE))
-            strs = tab.strings()
-            arrays.append([strs[i] for i in perm.tolist()])
+            arrays.append(tab.take_strings(perm))
         m = StringIndexerModel().set_model_data(StringIndexerModel.make_model_data_table([(arrays,)],
                                                                                          strings_only=True))
         rw_update(m, self)

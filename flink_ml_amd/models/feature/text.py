@@ -70,6 +70,48 @@ def java_split(pattern: str, s: str) -> List[str]:
     return parts
 
 
+_ZERO_WIDTH = ("^", "$", "\\b", "\\B", "\\A", "\\Z", "\\G", "(?=", "(?!", "(?<")
+
+
+def batched_java_split(strings: List[str], pat: "re.Pattern", lower: bool):
+    """``java_split`` of many strings with ONE regex pass over their concatenation: the strings
+    are joined by a separator the pattern cannot match, the pattern splits the whole text, and
+    the pieces are cut back per string with C-level splits and numpy (no Python call per string).
+    Returns (tokens per string [n] int64, flat token object array) or None when the pattern is not
+    safe to run across string boundaries (groups, anchors, lookarounds, empty matches) or the
+    data holds the separator characters — the per-string path applies then."""
+    if pat.groups or any(z in pat.pattern for z in _ZERO_WIDTH) or pat.search("") is not None:
+        return None
+    seps = [c for c in ("\x00", "\x01", "\x02", "\ue000", "\ue001", "\ue002") if pat.search(c) is None]
+    if len(seps) < 3:
+        return None
+    text = seps[0].join(strings)
+    if lower:
+        text = text.lower()
+    sep, mark, end = seps[0], seps[1], seps[2]
+    if text.count(sep) != max(len(strings) - 1, 0) or mark in text or end in text:
+        return None
+    pieces = pat.split(text)
+    # every string ends with the `end` token; pieces of one string are joined by `mark`
+    flat = np.array(mark.join(pieces).replace(sep, mark + end + mark).split(mark) + [end], dtype=object)
+    is_end = flat == end
+    if int(is_end.sum()) != len(strings):
+        return None
+    sid = np.cumsum(is_end) - is_end  # string id of every token (the end token: its own string)
+    ntok_raw = np.bincount(sid[~is_end], minlength=len(strings))
+    tok = flat[~is_end]
+    tsid = sid[~is_end]
+    # Java removes trailing empty strings when the string had a match (> 1 piece); a string
+    # without a match is returned whole (also "")
+    nonempty = np.fromiter(map(len, tok), dtype=np.int64, count=tok.shape[0]) > 0
+    pos = np.arange(tok.shape[0])
+    last = np.full(len(strings), -1, dtype=np.int64)
+    np.maximum.at(last, tsid[nonempty], pos[nonempty])
+    keep = (pos <= last[tsid]) | (ntok_raw[tsid] == 1)
+    tok, tsid = tok[keep], tsid[keep]
+    return np.bincount(tsid, minlength=len(strings)).astype(np.int64), tok
+
+
 def java_hashmap_order(keys: Sequence[str]) -> List[str]:
     """Iteration order of a ``java.util.HashMap<String, _>`` filled in ``keys`` order."""
     return _java_hashmap_order(keys, java_string_hash)
@@ -129,17 +171,36 @@ def _native_ws_lower_tokens(strings: List[str]):
     return ntok.astype(np.int64), ids[:nt], vocab
 
 
-def _per_string_arrays(t: Table, col: str, fn, native_kind: str = ""):
+def _all_str(values) -> bool:
+    """Whether every element is a str (one C-level join instead of a Python loop)."""
+    try:
+        "".join(values)
+        return True
+    except TypeError:
+        return False
+
+
+def _per_string_arrays(t: Table, col: str, fn, native_kind: str = "", batched=None):
     """``fn`` (str -> list of str) applied once per distinct string of a dictionary-encoded
     ``StringColumn``, expanded to every row by code on the device → ``StringArrayColumn``; None for
     a plain list column. ``native_kind="ws_lower"``: ``fn`` is Tokenizer's lowercase + ``\\s``
-    split, done for all distinct strings at once in native code when they are ASCII."""
+    split, done for all distinct strings at once in native code when they are ASCII. ``batched``
+    (list of str -> (tokens per string, flat tokens) or None): a whole-batch version of ``fn``."""
     c = t.column(col)
-    if not isinstance(c, StringColumn) or len(c) == 0 or any(not isinstance(w, str) for w in c.vocab):
+    if not isinstance(c, StringColumn) or len(c) == 0 or not _all_str(c.vocab):
         return None
     dev = config.compute_device()
     codes = c.codes.to(dev).long()
     nat = _native_ws_lower_tokens(c.vocab) if native_kind == "ws_lower" else None
+    if nat is None and batched is not None:
+        # one regex pass over all distinct strings, the token dictionary by a native hash join
+        res = batched(c.vocab)
+        if res is not None:
+            ntok, tok = res
+            tab = StrTable.from_strings(tok.tolist())
+            rep = tab.first_of_equal()
+            uniq, inv = np.unique(rep, return_inverse=True)
+            nat = ntok, inv.astype(np.int32), tab.take_strings(uniq)
     if nat is not None:
         vlen_np, flat_np, vocab = nat
         vlen_t = torch.from_numpy(vlen_np).to(dev)
@@ -208,7 +269,16 @@ class RegexTokenizer(Transformer, HasInputCol, HasOutputCol):
             toks = java_split(pat.pattern, s) if gaps else [m.group(0) for m in pat.finditer(s)]
             return [x for x in toks if len(x) >= mn]
 
-        out = _per_string_arrays(t, self.get(self.INPUT_COL), tokenize)
+        def batched(strings):
+            res = batched_java_split(strings, pat, low) if gaps else None
+            if res is None or mn <= 0:
+                return res
+            ntok, tok = res
+            ok = np.fromiter(map(len, tok), dtype=np.int64, count=tok.shape[0]) >= mn
+            sid = np.repeat(np.arange(ntok.shape[0]), ntok)
+            return np.bincount(sid[ok], minlength=ntok.shape[0]).astype(np.int64), tok[ok]
+
+        out = _per_string_arrays(t, self.get(self.INPUT_COL), tokenize, batched=batched)
         if out is None:
             out = [tokenize(s) for s in _strings_col(t, self.get(self.INPUT_COL))]
         return [t.with_column(self.get(self.OUTPUT_COL), out)]
@@ -604,8 +674,7 @@ class CountVectorizer(Estimator, CountVectorizerParams):
             kept = keys[(g_df[keys] >= amin) & (g_df[keys] <= amax)]
             keys = kept[hashmap_order_from_hashes(tab.java_hashes()[kept])]
         keys = keys[np.argsort(-g_df[keys], kind="stable")]  # stable, like List.sort
-        strs = tab.strings()
-        vocab = [strs[i] for i in keys[: self.get(self.VOCABULARY_SIZE)].tolist()]
+        vocab = tab.take_strings(keys[: self.get(self.VOCABULARY_SIZE)])
         m = CountVectorizerModel().set_model_data(CountVectorizerModel.make_model_data_table([(vocab,)]))
         rw_update(m, self)
         return m

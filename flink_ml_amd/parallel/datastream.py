@@ -227,8 +227,10 @@ def reduce_strings_by_key(table, sums: np.ndarray, firsts: np.ndarray):
         table = table_of(g_units, g_lens)
         sums = np.concatenate([p.numpy().reshape(-1, msum.shape[1]) for p in g_sums])
         key = np.concatenate([p.numpy() for p in g_keys])
-    order = np.argsort(key, kind="stable")
-    return table.take(order), sums[order], key[order]
+    if key.shape[0] > 1 and not bool(np.all(key[1:] >= key[:-1])):
+        order = np.argsort(key, kind="stable")
+        table, sums, key = table.take(order), sums[order], key[order]
+    return table, sums, key
 
 
 def set_managed_memory_weight(stream, weight: int):

@@ -42,7 +42,8 @@ class StrTable:
 
     __slots__ = ("units", "offs", "_strs")
 
-    def __init__(self, units: np.ndarray, offs: np.ndarray, strs: Optional[List[str]] = None):
+    # _strs: the Python strings when known (a list, or an object array after a gather)
+    def __init__(self, units: np.ndarray, offs: np.ndarray, strs=None):
         self.units = np.ascontiguousarray(units, dtype=np.uint16)
         self.offs = np.ascontiguousarray(offs, dtype=np.int64)
         self._strs = strs
@@ -70,6 +71,8 @@ class StrTable:
         return u.ctypes.data, self.offs.ctypes.data, u
 
     def strings(self) -> List[str]:
+        if isinstance(self._strs, np.ndarray):
+            self._strs = self._strs.tolist()
         if self._strs is None:
             s = self.units.tobytes().decode("utf-16-le", "surrogatepass")
             if len(s) == self.units.shape[0]:  # BMP only: code units = characters
@@ -96,9 +99,13 @@ class StrTable:
             units = np.zeros(0, dtype=np.uint16)
         strs = None
         if self._strs is not None:
-            src = self._strs
-            strs = [src[i] for i in idx.tolist()]
+            strs = _obj_array(self._strs)[idx]
         return StrTable(units, offs, strs)
+
+    def take_strings(self, idx: np.ndarray) -> List[str]:
+        """The strings at ``idx`` as a list (one object-array gather)."""
+        src = self._strs if self._strs is not None else self.strings()
+        return _obj_array(src)[np.asarray(idx, dtype=np.int64)].tolist()
 
     @staticmethod
     def concat(tables: Sequence["StrTable"]) -> "StrTable":
@@ -110,7 +117,7 @@ class StrTable:
             base += int(t.offs[-1])
         strs = None
         if tables and all(t._strs is not None for t in tables):
-            strs = [s for t in tables for s in t._strs]
+            strs = [s for t in tables for s in t.strings()]
         return StrTable(units, np.concatenate(offs), strs)
 
     # ---- native batch operations ---------------------------------------------------------
@@ -154,6 +161,14 @@ class StrTable:
     def first_of_equal(self) -> np.ndarray:
         """For every string, the index of its first occurrence in this table."""
         return self.lookup(self)
+
+
+def _obj_array(strs) -> np.ndarray:
+    if isinstance(strs, np.ndarray):
+        return strs
+    a = np.empty(len(strs), dtype=object)
+    a[:] = strs
+    return a
 
 
 def hashmap_order_from_hashes(h: np.ndarray, initial_capacity: int = 16) -> np.ndarray:
