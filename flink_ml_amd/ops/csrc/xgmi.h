@@ -11,6 +11,7 @@
 //   GLM_FLAGS  int32 [2] (256-B block)           fused GLM round feedback exchange
 //   DATA       [2][MAX_BLOCKS][CHUNK] x 8 B      generic records (f32 or f64 elements)
 //   GLM_DATA   [2][GLM_MAX] x 8 B                fused GLM feedback record [grad | Σw | Σloss]
+//   TS_*                                         two-shot all-reduce regions (below)
 // Slot = tag parity; tags are per-channel counters kept in LOCAL memory (gen[]), advanced by the
 // consuming block itself, so every rank — issuing the same call sequence — uses the same tags and
 // hipGraph replays keep advancing them (they are read from memory, never frozen arguments).
@@ -32,9 +33,22 @@ constexpr long FLAGS = 0;
 constexpr long GLM_FLAGS = FLAGS + 2L * MAX_BLOCKS * 4;
 constexpr long DATA = GLM_FLAGS + 256;
 constexpr long GLM_DATA = DATA + 2L * MAX_BLOCKS * CHUNK * 8;
-constexpr long TOTAL = GLM_DATA + 2L * GLM_MAX * 8;
+// Two-shot all-reduce (xgmi_allreduce.hip, 1-8 MB payloads): block b of every rank handles the
+// chunk group {b·P … b·P + P − 1}; chunk c is reduced by rank c mod P.
+//   TS_PFLAGS  int32 [2][TS_MAX_BLOCKS]          "my copy of group b is published"
+//   TS_RFLAGS  int32 [2][TS_MAX_BLOCKS]          "my reduced chunk of group b is published"
+//   TS_DATA    [2][TS_MAX_ELEMS] x 8 B           every rank's full input (published copies)
+//   TS_RED     [2][TS_MAX_ELEMS] x 8 B           reduced chunks, at their own positions
+constexpr long TS_MAX_ELEMS = 2L << 20;  // 2M elements: 8 MB f32 / 16 MB f64
+constexpr int TS_MAX_BLOCKS = (int)(TS_MAX_ELEMS / CHUNK);
+constexpr long TS_PFLAGS = GLM_DATA + 2L * GLM_MAX * 8;
+constexpr long TS_RFLAGS = TS_PFLAGS + 2L * TS_MAX_BLOCKS * 4;
+constexpr long TS_DATA = TS_RFLAGS + 2L * TS_MAX_BLOCKS * 4;
+constexpr long TS_RED = TS_DATA + 2L * TS_MAX_ELEMS * 8;
+constexpr long TOTAL = TS_RED + 2L * TS_MAX_ELEMS * 8;
 constexpr int GEN_GLM = MAX_BLOCKS;   // index of the fused-GLM counter in gen[]
-constexpr int GEN_SIZE = MAX_BLOCKS + 1;
+constexpr int GEN_TS = MAX_BLOCKS + 1;  // first two-shot block counter in gen[]
+constexpr int GEN_SIZE = GEN_TS + TS_MAX_BLOCKS;
 
 // Kernel-argument bundle. `peers` is a DEVICE array of `world` buffer pointers (mine at `rank`).
 struct Ctx {

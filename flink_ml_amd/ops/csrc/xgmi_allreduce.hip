@@ -50,6 +50,83 @@ __global__ __launch_bounds__(xgmi::THREADS) void xar_oneshot_kernel(xgmi::Ctx x,
   if (threadIdx.x == 0) x.gen[b] = g + 1;  // every thread read gen[b] before the first barrier
 }
 
+// Two-shot all-reduce for 1-8 MB payloads (the reference's chunked reduce-scatter + all-gather,
+// AllReduceImpl.java:108-199, here over peer-mapped xGMI memory in ONE kernel per rank). Block b
+// owns the chunk group {b·P … b·P + P − 1} on every rank:
+//   1. publish my P chunks of the group, raise publish tag (slot, b), wait for every peer's;
+//   2. reduce chunk b·P + rank: pull it from every peer (all P − 1 links at once), sum in rank
+//      order, publish the reduced chunk, raise reduced tag (slot, b), wait for every peer's;
+//   3. gather: pull every other rank's reduced chunk of the group.
+// Per rank 2·(P − 1)/P·n elements cross xGMI instead of (P − 1)·n for the one-shot pull, spread
+// over all P − 1 links. Block b of one rank only waits on block b of its peers, so nothing
+// assumes co-residency of a grid; both waits are bounded (NaN + error word on a timeout). The
+// sums are in rank order, so every rank gets identical bits.
+template <typename A>
+__global__ __launch_bounds__(xgmi::THREADS) void xar_twoshot_kernel(xgmi::Ctx x, const A* src, A* dst, long n,
+                                                                   const int* __restrict__ state) {
+  using namespace xgmi;
+  if (state) {
+    const int e = state[0];
+    if (state[1 + (e & 1)] == 0) return;
+  }
+  const int b = blockIdx.x;
+  const int P = x.world;
+  const int g = x.gen[GEN_TS + b];
+  const int slot = g & 1;
+  const long pub = TS_DATA + (long)slot * TS_MAX_ELEMS * (long)sizeof(A);
+  const long red = TS_RED + (long)slot * TS_MAX_ELEMS * (long)sizeof(A);
+  const long c0 = (long)b * P;
+  A* mine = at<A>(x.peers[x.rank], pub);
+  for (int q = 0; q < P; ++q) {
+    const long base = (c0 + q) * CHUNK;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      const long j = base + (long)i * THREADS + threadIdx.x;
+      if (j < n) st_sys(mine + j, src[j]);
+    }
+  }
+  bool ok = signal_and_wait(x, TS_PFLAGS, slot * TS_MAX_BLOCKS + b, g + 1);
+  // 2. my chunk of the group, summed over ranks in rank order
+  const long mbase = (c0 + x.rank) * CHUNK;
+  A r[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) r[i] = ok ? sum_ranks<A>(x, pub, mbase + (long)i * THREADS + threadIdx.x) : poison<A>();
+  A* rmine = at<A>(x.peers[x.rank], red);
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    const long j = mbase + (long)i * THREADS + threadIdx.x;
+    if (j < n) {
+      st_sys(rmine + j, r[i]);
+      dst[j] = r[i];
+    }
+  }
+  ok = signal_and_wait(x, TS_RFLAGS, slot * TS_MAX_BLOCKS + b, g + 1) && ok;
+  // 3. every other rank's reduced chunk (all loads in flight together)
+  A v[MAX_RANKS][VEC];
+#pragma unroll
+  for (int q = 0; q < MAX_RANKS; ++q) {
+    const int qq = q < P ? q : x.rank;
+    const long base = (c0 + qq) * CHUNK;
+    const A* rp = at<A>(x.peers[qq], red);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      const long j = base + (long)i * THREADS + threadIdx.x;
+      v[q][i] = ld_sys(rp + (j < n ? j : 0));  // past the end: an in-buffer word, masked below
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < MAX_RANKS; ++q) {
+    if (q >= P || q == x.rank) continue;
+    const long base = (c0 + q) * CHUNK;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      const long j = base + (long)i * THREADS + threadIdx.x;
+      if (j < n) dst[j] = ok ? v[q][i] : poison<A>();
+    }
+  }
+  if (threadIdx.x == 0) x.gen[GEN_TS + b] = g + 1;  // every thread read it before the first barrier
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
@@ -62,6 +139,7 @@ FMLX_API int fmlx_xar_max_ranks() { return xgmi::MAX_RANKS; }
 FMLX_API int fmlx_xar_gen_size() { return xgmi::GEN_SIZE; }
 FMLX_API int fmlx_xar_glm_max() { return xgmi::GLM_MAX; }
 FMLX_API int fmlx_xar_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+FMLX_API long fmlx_xar_twoshot_max() { return xgmi::TS_MAX_ELEMS; }
 
 // Allocates `bytes` of uncached device memory on the current device, zeroes it and exports its
 // IPC handle (64 bytes) into out_handle.
@@ -127,6 +205,25 @@ FMLX_API int fmlx_xar_allreduce(int dtype, void* const* peers_dev, int world, in
                        (const float*)src, (float*)dst, n, state);
   else
     hipLaunchKernelGGL(xar_oneshot_kernel<double>, dim3((unsigned)nb), dim3(xgmi::THREADS), 0, s, x,
+                       (const double*)src, (double*)dst, n, state);
+  return (int)hipGetLastError();
+}
+
+// Two-shot all-reduce (1-8 MB payloads); same contract as fmlx_xar_allreduce (in-place allowed).
+FMLX_API int fmlx_xar_allreduce2(int dtype, void* const* peers_dev, int world, int rank, const void* src, void* dst,
+                                 long n, int* gen, int* err, const int* state, long spin_limit, void* stream) {
+  if (world < 1 || world > xgmi::MAX_RANKS || rank < 0 || rank >= world) return -1;
+  if (n > xgmi::TS_MAX_ELEMS) return -3;
+  const long group = (long)world * xgmi::CHUNK;
+  const long nb = (n + group - 1) / group;
+  if (nb == 0) return 0;
+  xgmi::Ctx x{peers_dev, world, rank, gen, err, spin_limit};
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == 0)
+    hipLaunchKernelGGL(xar_twoshot_kernel<float>, dim3((unsigned)nb), dim3(xgmi::THREADS), 0, s, x,
+                       (const float*)src, (float*)dst, n, state);
+  else
+    hipLaunchKernelGGL(xar_twoshot_kernel<double>, dim3((unsigned)nb), dim3(xgmi::THREADS), 0, s, x,
                        (const double*)src, (double*)dst, n, state);
   return (int)hipGetLastError();
 }

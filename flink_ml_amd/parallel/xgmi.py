@@ -54,12 +54,20 @@ native.register_kernel_sigs({
     "fmlx_host_flags_free": [c_void_p],
     "fmlx_xar_allreduce": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p,
                            c_long, c_void_p],
+    "fmlx_xar_allreduce2": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p,
+                            c_long, c_void_p],
+    "fmlx_xar_twoshot_max": ([], c_long),
 })
 
 # polls (each ≈ one xGMI round trip + s_sleep) before a wait gives up: several seconds, far
 # beyond any lockstep drift between ranks, far below a hang
 DEFAULT_SPIN = int(os.environ.get("FMLX_XGMI_SPIN", str(1 << 22)))
-MAX_ONESHOT_ELEMS = int(os.environ.get("FMLX_XGMI_MAX_ELEMS", str(1 << 18)))
+# payload routing: one-shot pull up to MAX_ONESHOT_ELEMS (latency-bound: one cross-rank wait),
+# two-shot (reduce-scatter + all-gather over the peer buffers, 2·(P−1)/P·n per rank on xGMI
+# instead of (P−1)·n) up to MAX_TWOSHOT_ELEMS, RCCL above. A 512 KB KMeans payload (k = 1024,
+# D = 128) and the 4 MB sparse-SVC feedback (dim 1M) take the two-shot.
+MAX_ONESHOT_ELEMS = int(os.environ.get("FMLX_XGMI_MAX_ELEMS", str(1 << 17)))
+MAX_TWOSHOT_ELEMS = int(os.environ.get("FMLX_XGMI_TWOSHOT_MAX", str(2 << 20)))
 
 
 class XgmiTimeout(RuntimeError):
@@ -105,6 +113,7 @@ class XgmiComm:
         self.device = ctx.device
         self.chunk = lib.fmlx_xar_chunk()
         self.max_elems = self.chunk * lib.fmlx_xar_max_blocks()
+        self.twoshot_max = int(lib.fmlx_xar_twoshot_max())
         self.glm_max = lib.fmlx_xar_glm_max()
         self.spin_limit = int(spin_limit)
         self._base = None
@@ -150,20 +159,30 @@ class XgmiComm:
         return (self.peers.data_ptr(), self.world, self.rank, self.gen.data_ptr(), self.err.dev,
                 self.spin_limit)
 
-    def accepts(self, t: torch.Tensor) -> bool:
-        """Small payloads only (≤ ``FMLX_XGMI_MAX_ELEMS``, default 256K elements = 1 MB fp32): the
-        one-shot exchange is latency-optimal there; above it RCCL's ring/tree pipelines win on
-        bandwidth, and a one-shot grid of ~1000 spinning blocks per rank must not have to share
-        CUs with its peers' grids (ranks rehearsed on one GPU)."""
-        return (t.is_cuda and t.device == self.device and t.dtype in (torch.float32, torch.float64)
-                and t.is_contiguous() and t.numel() <= min(self.max_elems, MAX_ONESHOT_ELEMS))
+    def path(self, n: int) -> str:
+        """'oneshot', 'twoshot' or 'rccl' for an n-element payload."""
+        if n <= min(self.max_elems, MAX_ONESHOT_ELEMS):
+            return "oneshot"
+        if n <= min(self.twoshot_max, MAX_TWOSHOT_ELEMS):
+            return "twoshot"
+        return "rccl"
 
-    def all_reduce_(self, t: torch.Tensor, state: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def accepts(self, t: torch.Tensor) -> bool:
+        """Payloads up to ``FMLX_XGMI_TWOSHOT_MAX`` (default 2M elements = 8 MB fp32): one-shot
+        pull up to ``FMLX_XGMI_MAX_ELEMS`` (128K), two-shot above; beyond that RCCL's pipelined
+        ring/tree wins on bandwidth."""
+        return (t.is_cuda and t.device == self.device and t.dtype in (torch.float32, torch.float64)
+                and t.is_contiguous() and self.path(t.numel()) != "rccl")
+
+    def all_reduce_(self, t: torch.Tensor, state: Optional[torch.Tensor] = None, path: Optional[str] = None) -> torch.Tensor:
         """In-place sum over the group (same shape on every rank), stream-ordered on the current
-        stream and capturable in a hipGraph. ``state``: optional SGD round state predicating the call."""
+        stream and capturable in a hipGraph. ``state``: optional SGD round state predicating the call.
+        ``path``: force 'oneshot' / 'twoshot' (tests); default by size."""
         self.check()  # an earlier exchange of this group gave up: its peers' tags no longer line up
         dt = 0 if t.dtype == torch.float32 else 1
-        native.call("fmlx_xar_allreduce", dt, self.peers.data_ptr(), self.world, self.rank, t.data_ptr(),
+        kind = path or self.path(t.numel())
+        fn = "fmlx_xar_allreduce2" if kind == "twoshot" else "fmlx_xar_allreduce"
+        native.call(fn, dt, self.peers.data_ptr(), self.world, self.rank, t.data_ptr(),
                     t.data_ptr(), t.numel(), self.gen.data_ptr(), self.err.dev, native.ptr(state),
                     self.spin_limit, native.stream_ptr(t.device))
         return t
@@ -183,10 +202,11 @@ class XgmiComm:
         W = self.world
         ok = True
         for dt in (torch.float32, torch.float64):
-            for n in (1, 1000, 3 * self.chunk + 5):
+            for n, kind in ((1, "oneshot"), (1000, "oneshot"), (3 * self.chunk + 5, "oneshot"),
+                            (1, "twoshot"), ((2 * W + 1) * self.chunk + 7, "twoshot")):
                 for rep in range(2):
                     t = torch.arange(n, device=self.device, dtype=dt) * (self.rank + 1) + (self.rank + rep)
-                    self.all_reduce_(t)
+                    self.all_reduce_(t, path=kind)
                     exp = (torch.arange(n, dtype=torch.float64) * (W * (W + 1) // 2)
                            + (W * (W - 1) // 2 + rep * W))
                     ok = ok and bool(torch.equal(t.to(torch.float64).cpu(), exp))

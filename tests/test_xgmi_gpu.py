@@ -50,6 +50,48 @@ def test_xgmi_allreduce_two_ranks_one_gpu():
     assert run_spmd(_allreduce_worker, 2, env=ENV, timeout=300) == [True, True]
 
 
+def _twoshot_worker(rank, world, sizes):
+    import torch
+
+    from flink_ml_amd.parallel import comm, xgmi
+
+    x = xgmi.get()
+    assert x is not None, "xGMI exchange did not come up"
+    S = world * (world + 1) // 2
+    for dt in (torch.float32, torch.float64):
+        for n in sizes:
+            for rep in range(3):  # both slots, then slot 0 again
+                t = torch.arange(n, device="cuda:0", dtype=dt) * (rank + 1) + rep
+                x.all_reduce_(t, path="twoshot")
+                exp = torch.arange(n, dtype=torch.float64) * S + rep * world
+                assert torch.equal(t.to(torch.float64).cpu(), exp), (dt, n, rep)
+    # size routing: a 4 MB feedback (dim 1M + 2) goes through the two-shot, a small one one-shot
+    assert x.path(1_000_002) == "twoshot" and x.path(1000) == "oneshot" and x.path(3 << 20) == "rccl"
+    v = torch.full((1_000_002,), float(rank + 1), device="cuda:0", dtype=torch.float32)
+    comm.all_reduce_sum(v)
+    assert torch.all(v.cpu() == S)
+    # interleaved one-shot / two-shot calls keep their own tags
+    for i in range(4):
+        a = torch.full((5000,), float(rank + i), device="cuda:0")
+        b = torch.full((200_000,), float(rank * 2 + i), device="cuda:0")
+        x.all_reduce_(a, path="oneshot")
+        x.all_reduce_(b, path="twoshot")
+        assert torch.all(a.cpu() == sum(r + i for r in range(world)))
+        assert torch.all(b.cpu() == sum(2 * r + i for r in range(world)))
+    torch.cuda.synchronize()
+    assert x.healthy()
+    return True
+
+
+@pytest.mark.parametrize("world,sizes", [(2, (1, 1023, 1025, 2 * 1024 * 2 + 5, 300_000, 1_100_007)),
+                                         (4, (1, 4097, 4 * 1024 * 3 + 1, 600_001))])
+def test_xgmi_twoshot_allreduce_ranks_on_one_gpu(world, sizes):
+    """Two-shot (reduce-scatter + all-gather over the peer-mapped buffers): exact integer sums
+    for partial chunk groups, both slots, f32/f64; routing of a 4 MB payload through it."""
+    _need_gpu()
+    assert run_spmd(_twoshot_worker, world, sizes, env=ENV, timeout=300) == [True] * world
+
+
 def _sgd_worker(rank, world, xgmi_mode, dtype_name):
     import os
 
