@@ -68,7 +68,9 @@ def main():
     ap.add_argument("--batch", type=int, default=100_000, help="per-GPU minibatch rows")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp64"])
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--graph-rounds", type=int, default=10, help="SGD rounds captured per hipGraph replay")
+    ap.add_argument("--graph-rounds", type=int, default=0,
+                    help="SGD rounds captured per hipGraph replay (0: the timed steps, at most 200, in one replay "
+                         "— every graph is captured and primed before the clock starts)")
     ap.add_argument("--torch-profile", default="", help="after the timed region, record a torch.profiler trace of "
                                                         "extra rounds into this directory (not timed)")
     args = ap.parse_args()
@@ -105,7 +107,7 @@ def main():
     def make_trainer():
         sgd = SGD(max_iter=1, learning_rate=0.1, global_batch_size=args.batch * world, tol=1e-6)
         tr = DeviceGlmTrainer(sgd, np.zeros(args.dim), X, y, None, "logistic", use_graph=not args.no_graph)
-        tr.rounds_per_graph = args.graph_rounds
+        tr.rounds_per_graph = args.graph_rounds if args.graph_rounds > 0 else max(1, min(args.steps, 200))
         sgd.max_iter = args.warmup + tr.priming_rounds(args.steps) + args.steps + 1  # read at capture
         if args.torch_profile:
             sgd.max_iter += PROFILE_ROUNDS
