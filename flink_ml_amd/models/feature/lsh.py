@@ -8,9 +8,10 @@ MinHashLSHModel,MinHashLSHModelData}.java``).
 * approx_nearest_neighbors: bucket filter (any table whose signature equals the key's), device
   Jaccard distances from sorted-key membership, per-rank top-k then a global top-k; each rank
   returns its own rows of the global answer.
-* approx_similarity_join: broadcast join — dataset B's signatures and sets are all-gathered, each
-  rank joins its partition of A on (table, signature) via ``unique(dim=0)`` group ids, dedupes the
-  candidate pairs and keeps those with Jaccard distance <= threshold.
+* approx_similarity_join: on one rank, a join on (table, signature) via ``unique(dim=0)`` group ids,
+  deduplicated candidate pairs, Jaccard distance <= threshold; across ranks the reference's keyed
+  join (``_keyed_similarity_join``: signature entries all-to-all'ed to their key owners, pairs to
+  their A row's rank, B sets fetched on demand) — a broadcast of B only for non-numeric ids.
 """
 from __future__ import annotations
 
@@ -177,7 +178,10 @@ class MinHashLSHModel(ModelWithData, LSHModelParams):
         sb = _sets(vector_input(dataset_b, self.get(self.INPUT_COL))).to(dev)
         ids_b = dataset_b.get_list(id_col)
         if get_world_distributed():
-            # broadcast join: every rank sees all of B
+            ids_a = dataset_a.get_list(id_col)
+            if _numeric_ids(ids_a) and _numeric_ids(ids_b):
+                return _keyed_similarity_join(ha, hb, sa, sb, ids_a, ids_b, threshold, dist_col)
+            # non-numeric ids: broadcast join (every rank sees all of B)
             parts = comm.all_gather_object((hb.cpu(), sb.to("cpu"), ids_b))
             hb = torch.cat([p[0] for p in parts]).to(dev)
             sb = SparseColumn.concat([p[1] for p in parts]).to(dev)
@@ -207,6 +211,111 @@ class MinHashLSHModel(ModelWithData, LSHModelParams):
                      num_rows=len(ia))
 
     approxSimilarityJoin = approx_similarity_join
+
+
+def _numeric_ids(ids) -> bool:
+    return all(isinstance(v, (int, float, np.integer, np.floating)) and not isinstance(v, bool) for v in ids)
+
+
+def _gather_rows(sets: SparseColumn, rows: torch.Tensor):
+    """Row lengths and concatenated column indices of ``sets[rows]``."""
+    ptr = sets.indptr.to(rows.device)
+    ln = ptr[rows + 1] - ptr[rows]
+    pid = torch.repeat_interleave(torch.arange(rows.numel(), device=rows.device), ln)
+    off = torch.arange(pid.numel(), device=rows.device) - torch.repeat_interleave(torch.cumsum(ln, 0) - ln, ln)
+    return ln, sets.indices.to(rows.device).long()[ptr[rows][pid] + off]
+
+
+def _keyed_similarity_join(ha, hb, sa: SparseColumn, sb: SparseColumn, ids_a, ids_b, threshold: float,
+                           dist_col: str) -> Table:
+    """``approxSimilarityJoin`` across ranks as the reference's keyed join (LSHModel.java:201-258:
+    both sides keyed by (table, signature), co-grouped, candidate pairs deduplicated, distances):
+
+    1. every (table, signature) entry of A and B goes to the owner of its key (one all-to-all);
+       each owner pairs the A and B entries of every key it owns;
+    2. candidate pairs go to the rank holding their A row (all-to-all) and are deduplicated there;
+    3. the B sets (and ids) those pairs need are fetched from B's ranks (request / response
+       all-to-alls) and the Jaccard distances computed next to the A rows.
+    Each rank returns the pairs of its own A rows."""
+    from ...parallel import datastream as ds
+    from ...parallel.context import get_context
+
+    ctx = get_context()
+    P, me = ctx.world_size, ctx.rank
+    dev = ha.device
+
+    def entries(h, side):
+        n, T, F = h.shape
+        hk = ds.float_keys(h).reshape(n, T, F)
+        tb = torch.arange(T, device=dev, dtype=torch.int64)[None, :, None].expand(n, T, 1)
+        keys = torch.cat([tb, hk], 2).reshape(n * T, F + 1)
+        row = torch.arange(n, device=dev, dtype=torch.int64)[:, None].expand(n, T).reshape(-1)
+        meta = torch.stack([torch.full_like(row, side), torch.full_like(row, me), row], 1)
+        return keys, meta
+
+    ka, ma = entries(ha, 0)
+    kb, mb = entries(hb, 1)
+    keys, meta = torch.cat([ka, kb]), torch.cat([ma, mb])
+    own = ds.key_owner(keys, P)
+    o = torch.argsort(own, stable=True)
+    cnt = torch.bincount(own, minlength=P).tolist()
+    keys = torch.cat(comm.all_to_all_v(list(torch.split(keys[o], cnt))))
+    meta = torch.cat(comm.all_to_all_v(list(torch.split(meta[o], cnt))))
+    # 1. co-group the owned keys: A entries × B entries of every group
+    if keys.shape[0]:
+        _, g = torch.unique(keys, dim=0, return_inverse=True)
+    else:
+        g = torch.zeros(0, dtype=torch.int64, device=dev)
+    isa = meta[:, 0] == 0
+    ga, gb = g[isa], g[~isa]
+    ea, eb = meta[isa], meta[~isa]
+    ob = torch.argsort(gb, stable=True)
+    gbs = gb[ob]
+    lo = torch.searchsorted(gbs, ga)
+    hi = torch.searchsorted(gbs, ga, right=True)
+    c = hi - lo
+    ia = torch.repeat_interleave(torch.arange(ga.numel(), device=dev), c)
+    off = torch.arange(ia.numel(), device=dev) - torch.repeat_interleave(torch.cumsum(c, 0) - c, c)
+    jb = ob[lo[ia] + off]
+    pairs = torch.stack([ea[ia, 1], ea[ia, 2], eb[jb, 1], eb[jb, 2]], 1)  # a_rank, a_row, b_rank, b_row
+    # 2. to the A row's rank, deduplicated (a pair can share several tables)
+    own = pairs[:, 0]
+    o = torch.argsort(own, stable=True)
+    cnt = torch.bincount(own, minlength=P).tolist()
+    pairs = torch.cat(comm.all_to_all_v(list(torch.split(pairs[o], cnt))))
+    pairs = torch.unique(pairs[:, 1:], dim=0) if pairs.shape[0] else pairs[:, 1:]
+    arow, brank, brow = pairs[:, 0], pairs[:, 1], pairs[:, 2]
+    # 3. the B rows these pairs need: request from their ranks, answer with sets and ids
+    need = torch.unique(torch.stack([brank, brow], 1), dim=0) if brow.numel() else torch.zeros(
+        (0, 2), dtype=torch.int64, device=dev)
+    cnt = torch.bincount(need[:, 0], minlength=P).tolist()
+    req = comm.all_to_all_v(list(torch.split(need[:, 1].contiguous(), cnt)))  # rows others need from me
+    idb = torch.tensor([float(v) for v in ids_b], dtype=torch.float64, device=dev)
+    sb_d = sb.to(dev)
+    lens, cols, idv = [], [], []
+    for r in range(P):
+        ln, cl = _gather_rows(sb_d, req[r].to(dev))
+        lens.append(ln)
+        cols.append(cl)
+        idv.append(idb[req[r].to(dev)])
+    got_len = torch.cat(comm.all_to_all_v(lens))
+    got_cols = torch.cat(comm.all_to_all_v(cols))
+    got_ids = torch.cat(comm.all_to_all_v(idv))
+    ptr = torch.zeros(got_len.numel() + 1, dtype=torch.int64, device=dev)
+    ptr[1:] = torch.cumsum(got_len.to(dev), 0)
+    fetched = SparseColumn(ptr, got_cols.to(dev).to(torch.int32), torch.ones(got_cols.numel(), dtype=torch.float64,
+                                                                            device=dev), sb.size)
+    # fetched row i = need[i] (need is sorted by (rank, row), the answers arrive in the same order)
+    nkey = need[:, 0] * (1 << 40) + need[:, 1]
+    fi = torch.searchsorted(nkey, brank * (1 << 40) + brow)
+    dist = _pair_jaccard(sa.to(dev), fetched, arow, fi)
+    keep = dist <= threshold
+    arow, fi, dist = arow[keep].cpu().tolist(), fi[keep], dist[keep].cpu()
+    bid = got_ids.to(dev)[fi].cpu().tolist()
+    ida = [ids_a[i] for i in arow]
+    ints = comm.all_reduce_scalar(1.0 if all(isinstance(v, (int, np.integer)) for v in ids_b) else 0.0, "min")
+    idb_out = [int(v) for v in bid] if ints > 0.5 else bid
+    return Table({"datasetA.id": ida, "datasetB.id": idb_out, dist_col: dist}, num_rows=len(ida))
 
 
 @rw.register_stage

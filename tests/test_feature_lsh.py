@@ -120,3 +120,30 @@ def test_minhash_kernel_matches_exact():
     gpu = lsh_ops.minhash(sc.to("cuda"), a, b)
     assert gpu.is_cuda
     assert torch.equal(gpu.cpu(), cpu)
+
+
+def _rand_sets(seed, n, d=60):
+    rng = np.random.default_rng(seed)
+    rows = []
+    for i in range(n):
+        k = int(rng.integers(1, 8))
+        cols = np.sort(rng.choice(d, size=k, replace=False)).tolist()
+        rows.append((i + 1000 * seed, Vectors.sparse(d, cols, [1.0] * k)))
+    return Table.from_rows(rows, ["id", "vec"])
+
+
+def _spmd_keyed_join(rank, world):
+    a, b = _rand_sets(1, 900), _rand_sets(2, 700)
+    model = _lsh(4, 2).fit(a)
+    join = model.approx_similarity_join(a.partition(rank, world), b.partition(rank, world), 0.7, "id")
+    return join.rows()
+
+
+def test_lsh_keyed_similarity_join_matches_one_rank():
+    """Distributed approxSimilarityJoin (keyed join: signatures to key owners, pairs to A's rank,
+    B sets fetched on demand) equals the single-rank join on random sets."""
+    a, b = _rand_sets(1, 900), _rand_sets(2, 700)
+    ref = sorted(_lsh(4, 2).fit(a).approx_similarity_join(a, b, 0.7, "id").rows())
+    assert len(ref) > 50
+    got = sorted(r for part in run_spmd(_spmd_keyed_join, 3) for r in part)
+    assert got == ref
