@@ -152,17 +152,22 @@ class MinHashLSHModel(ModelWithData, LSHModelParams):
         idx = torch.nonzero(cand, as_tuple=True)[0]
         dist = _pair_jaccard(kset, sets, torch.zeros_like(idx), idx)
         order = torch.argsort(dist, stable=True)[:k]
-        loc_idx, loc_dist = idx[order].cpu().tolist(), dist[order].cpu().tolist()
+        loc_idx, loc_dist = idx[order], dist[order]
         if get_world_distributed():
             from ...parallel.context import get_context
 
             me = get_context().rank
-            allc = [(d, r, i) for r, part in enumerate(comm.all_gather_object(list(zip(loc_dist, loc_idx))))
-                    for d, i in part]
-            allc.sort(key=lambda x: (x[0], x[1], x[2]))
-            chosen = [(i, d) for d, r, i in allc[:k] if r == me]
+            # global top-k over the ranks' local top-k: (distance, rank, row) tensors gathered,
+            # ordered by distance then rank then row
+            mine = torch.stack([loc_dist.to(torch.float64), torch.full_like(loc_dist, float(me), dtype=torch.float64),
+                                loc_idx.to(torch.float64)], 1)
+            allc = torch.cat(comm.all_gather_tensor(mine)).cpu()
+            o = np.lexsort((allc[:, 2].numpy(), allc[:, 1].numpy(), allc[:, 0].numpy()))[:k]
+            top = allc[torch.as_tensor(o, dtype=torch.int64)]
+            sel = top[top[:, 1] == me]
+            chosen = list(zip(sel[:, 2].to(torch.int64).tolist(), sel[:, 0].tolist()))
         else:
-            chosen = list(zip(loc_idx, loc_dist))
+            chosen = list(zip(loc_idx.cpu().tolist(), loc_dist.cpu().tolist()))
         rows = [i for i, _ in chosen]
         out = dataset.with_column(self.get(self.OUTPUT_COL), H).take(rows)
         return out.with_column(dist_col, torch.tensor([d for _, d in chosen], dtype=torch.float64))
@@ -332,7 +337,10 @@ class MinHashLSH(Estimator, LSHParams, HasSeed):
         else:
             sizes = {v.size() for v in col}
         if get_world_distributed():
-            sizes = set(x for p in comm.all_gather_object(sorted(sizes)) for x in p)
+            # (min, max) vector size over the ranks; −1 / large sentinels for an empty partition
+            lo = comm.all_reduce_scalar(float(min(sizes)) if sizes else float(1 << 40), "min")
+            hi = comm.all_reduce_scalar(float(max(sizes)) if sizes else -1.0, "max")
+            sizes = set() if hi < 0 else {int(lo), int(hi)}
         if len(sizes) > 1:
             s = sorted(sizes)
             raise RuntimeError("Vector sizes are not the same: %d %d." % (s[0], s[1]))
