@@ -34,12 +34,18 @@ native.register_kernel_sigs({
                              c_void_p],
     "fmlx_group_max_keys": [],
     "fmlx_group_by_key": [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "fmlx_group_stable_max_keys": [],
+    "fmlx_group_stable_scratch": ([c_long, c_int], c_long),
+    "fmlx_group_by_key_stable": [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
 })
 
-# rows grouped by cluster with the hand-written counting sort (csrc/groupsort.hip: three launches,
-# order inside a cluster from atomic arrival) unless FMLX_DETERMINISTIC=1 asks for bit-reproducible
-# centroids (the stable radix sort of sort.hip)
-GROUP_SORT = os.environ.get("FMLX_DETERMINISTIC", "0") != "1"
+# rows grouped by cluster with the hand-written STABLE counting sort (csrc/groupsort.hip
+# st_*: per-tile histograms, column scan, ordered scatter — rows of a cluster stay in row order,
+# so the centroid sums are bit-reproducible) for k <= 2048; larger k takes the arrival-order
+# counting sort (sums reproducible to rounding), or the stable radix sort of sort.hip when
+# FMLX_DETERMINISTIC=1. GROUP_SORT=False forces the radix sort (A/B and tests).
+GROUP_SORT = True
+DETERMINISTIC = os.environ.get("FMLX_DETERMINISTIC", "0") == "1"
 
 METRICS = {"euclidean": 0, "manhattan": 1, "cosine": 2}
 CHUNK = 256
@@ -209,12 +215,18 @@ class KMeansRound:
         self.zero_i64 = torch.zeros(1, dtype=torch.int64, device=dev)
         self.fast = (dev.type == "cuda" and X.dtype == torch.bfloat16 and self.D in (8, 16, 32, 64, 128, 256, 512)
                      and X.stride(1) == 1 and X.stride(0) % 8 == 0 and X.data_ptr() % 16 == 0)
-        self.group = dev.type == "cuda" and GROUP_SORT and k <= native.kernels().fmlx_group_max_keys()
+        lib = native.kernels() if dev.type == "cuda" else None
+        self.stable = dev.type == "cuda" and GROUP_SORT and k <= lib.fmlx_group_stable_max_keys()
+        self.group = (dev.type == "cuda" and GROUP_SORT and not self.stable and not DETERMINISTIC
+                      and k <= lib.fmlx_group_max_keys())
         if dev.type == "cuda":
             self.offsets = torch.zeros(k + 1, dtype=torch.int64, device=dev)
             self.chunk_off = torch.zeros(k + 1, dtype=torch.int64, device=dev)
             self.order32 = torch.empty(self.n, dtype=torch.int32, device=dev)
-        if self.group:
+        if self.stable:
+            self.gscratch = torch.empty(max(1, int(lib.fmlx_group_stable_scratch(self.n, k))), dtype=torch.int32,
+                                        device=dev)
+        elif self.group:
             self.gcounts = torch.zeros(k, dtype=torch.int32, device=dev)  # re-zeroed by the scan kernel
             self.gcursor = torch.zeros(k, dtype=torch.int32, device=dev)
         elif dev.type == "cuda":
@@ -234,7 +246,12 @@ class KMeansRound:
             return self.payload
         assign(X, cb, self.metric, self.labels)
         stream = native.stream_ptr(X.device)
-        if self.group:
+        if self.stable:
+            # stable counting sort by cluster + cluster / chunk offsets (groupsort.hip st_*)
+            native.call("fmlx_group_by_key_stable", native.ptr(self.labels), self.n, self.k, CHUNK,
+                        native.ptr(self.gscratch), native.ptr(self.offsets), native.ptr(self.chunk_off),
+                        native.ptr(self.order32), stream)
+        elif self.group:
             # counting sort by cluster + cluster / chunk offsets, no library sort (groupsort.hip)
             native.call("fmlx_group_by_key", native.ptr(self.labels), self.n, self.k, CHUNK, native.ptr(self.gcounts),
                         native.ptr(self.gcursor), native.ptr(self.offsets), native.ptr(self.chunk_off),
@@ -289,14 +306,25 @@ def torch_finalize(payload: torch.Tensor, k: int, D: int):
     return cent, counts
 
 
-def group_by_key(keys: torch.Tensor, k: int, chunk: int = 0):
+def group_by_key(keys: torch.Tensor, k: int, chunk: int = 0, stable: bool = False):
     """Rows grouped by an int32 key in [0, k) on the device (csrc/groupsort.hip counting sort):
     returns (order int32 [m], offsets int64 [k + 1], chunk_off int64 [k + 1] or None), where
-    ``order[offsets[c]:offsets[c+1]]`` are the rows with key c (order inside a key unspecified) and
-    m = offsets[k] (keys outside [0, k) are dropped). k ≤ ``fmlx_group_max_keys()``."""
+    ``order[offsets[c]:offsets[c+1]]`` are the rows with key c (in row order with ``stable``,
+    k ≤ ``fmlx_group_stable_max_keys()``; otherwise in arrival order, k ≤ ``fmlx_group_max_keys()``)
+    and m = offsets[k] (keys outside [0, k) are dropped)."""
     dev = keys.device
     n = keys.numel()
     keys = keys.to(torch.int32).contiguous()
+    if stable:
+        lib = native.kernels()
+        scratch = torch.empty(max(1, int(lib.fmlx_group_stable_scratch(n, int(k)))), dtype=torch.int32, device=dev)
+        offsets = torch.empty(k + 1, dtype=torch.int64, device=dev)
+        chunk_off = torch.empty(k + 1, dtype=torch.int64, device=dev) if chunk > 0 else None
+        order = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        native.call("fmlx_group_by_key_stable", native.ptr(keys), n, int(k), int(chunk), native.ptr(scratch),
+                    native.ptr(offsets), native.ptr(chunk_off), native.ptr(order), native.stream_ptr(dev))
+        m = int(offsets[k].item())
+        return order[:m], offsets, chunk_off
     counts = torch.zeros(k, dtype=torch.int32, device=dev)
     cursor = torch.empty(k, dtype=torch.int32, device=dev)
     offsets = torch.empty(k + 1, dtype=torch.int64, device=dev)

@@ -10,6 +10,10 @@ step xgmi
 timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_xgmi_gpu.py \
   -k "allreduce" > $O/xgmi_pytest.log 2>&1 || { echo "xgmi pytest failed"; tail -40 $O/xgmi_pytest.log; exit 1; }
 tail -3 $O/xgmi_pytest.log
+step groupsort
+timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_kmeans.py \
+  -k "group_by_key or round_payload" > $O/kmeans_pytest.log 2>&1 || { echo "kmeans pytest failed"; tail -40 $O/kmeans_pytest.log; exit 1; }
+tail -3 $O/kmeans_pytest.log
 step svc
 timeout -k 10 300 python -u scripts/bench_north.py --config svc_sparse --scale 0.125 > $O/svc_shard.jsonl 2>&1 || { echo svc failed; tail -20 $O/svc_shard.jsonl; exit 1; }
 tail -1 $O/svc_shard.jsonl

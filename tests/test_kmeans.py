@@ -164,16 +164,21 @@ def test_gpu_assign_generic(dtype, metric):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("det", [False, True])
+@pytest.mark.parametrize("mode", ["stable", "radix", "arrival"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32, torch.float64])
-def test_gpu_round_payload_matches_torch(dtype, det, monkeypatch):
-    """One round's [sums | counts] against torch; FMLX_DETERMINISTIC's stable radix grouping is
-    bit-reproducible, the default counting sort reproducible to rounding (exact counts)."""
+def test_gpu_round_payload_matches_torch(dtype, mode, monkeypatch):
+    """One round's [sums | counts] against torch: the default stable counting sort and the radix
+    sort are bit-reproducible, the arrival-order counting sort (k > 2048 without
+    FMLX_DETERMINISTIC) reproducible to rounding (exact counts)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from flink_ml_amd.ops import kmeans as kk
+    from flink_ml_amd.ops import native
 
-    monkeypatch.setattr(kk, "GROUP_SORT", not det)
+    monkeypatch.setattr(kk, "GROUP_SORT", mode != "radix")
+    if mode == "arrival":  # what k > fmlx_group_stable_max_keys() takes
+        monkeypatch.setattr(native.kernels(), "fmlx_group_stable_max_keys", lambda: 0)
+    det = mode != "arrival"
     g = torch.Generator().manual_seed(2)
     n, D, k = 20000, 100, 10
     X = torch.rand((n, D), generator=g, dtype=torch.float64).to(dtype)
@@ -182,7 +187,7 @@ def test_gpu_round_payload_matches_torch(dtype, det, monkeypatch):
     cb = kk.CentroidBuffers(k, D, torch.device("cuda"), acc)
     cb.set(C)
     rnd = kk.KMeansRound(X.cuda(), k, "euclidean")
-    assert rnd.group == (not det)
+    assert rnd.stable == (mode == "stable") and rnd.group == (mode == "arrival")
     p1 = rnd.run(cb).clone()
     p2 = rnd.run(cb).clone()
     if det:
@@ -364,3 +369,30 @@ def test_group_by_key_counting_sort(n, k):
     # second call reuses the re-zeroed counts (the hipGraph replay contract)
     order2, offsets2, _ = kk.group_by_key(keys.cuda(), k, 256)
     assert torch.equal(offsets2.cpu(), exp_off)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k", [(1, 1), (1000, 7), (8192, 3), (8193, 2048), (3_000_001, 1024), (700_001, 2048)])
+def test_group_by_key_stable_equals_torch_stable_sort(n, k):
+    """The stable counting sort (groupsort.hip st_*) equals torch's stable sort by key exactly:
+    rows of a key in row order; empty keys, a huge key, keys outside [0, k) dropped, partial tiles
+    and tile groups; a second call (scratch reuse) gives the same."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from flink_ml_amd.ops import kmeans as kk
+
+    g = torch.Generator(device="cpu").manual_seed(n * 7 + k)
+    keys = torch.randint(0, max(k // 2, 1), (n,), generator=g, dtype=torch.int32) * 2
+    keys[: n // 3] = k - 1 if k > 1 else 0
+    if n > 10:
+        keys[3] = -1
+        keys[5] = k
+    valid = (keys >= 0) & (keys < k)
+    idx = torch.nonzero(valid).view(-1)
+    ref = idx[torch.sort(keys[idx].long(), stable=True).indices]
+    for _ in range(2):
+        order, offsets, chunk_off = kk.group_by_key(keys.cuda(), k, 256, stable=True)
+        assert torch.equal(order.cpu().long(), ref)
+        counts = torch.bincount(keys[valid].long(), minlength=k)
+        assert torch.equal(offsets.cpu()[1:], torch.cumsum(counts, 0)) and int(offsets[0]) == 0
+        assert torch.equal(chunk_off.cpu()[1:], torch.cumsum((counts + 255) // 256, 0))

@@ -101,9 +101,7 @@ def _kmeans_online_worker(rank, world):
     from flink_ml_amd.parallel import xgmi
 
     assert xgmi.collective_path() == "nccl"
-    # the default counting sort orders rows inside a cluster by atomic arrival (sums reproducible
-    # only to rounding); the comparison with the no-group fit needs the stable grouping
-    kk.GROUP_SORT = False
+    assert kk.GROUP_SORT  # the default stable counting sort: bit-reproducible sums
     return {"kmeans": _kmeans_fit(), "online": _online_fit()}
 
 
@@ -143,9 +141,6 @@ def test_kmeans_and_online_lr_on_rccl(monkeypatch):
     """KMeans (centroid all-reduce) and OnlineLogisticRegression (FTRL payload all-reduce) with the
     xGMI exchange off: every collective is an RCCL all-reduce; same results as without a group."""
     _need_gpu()
-    from flink_ml_amd.ops import kmeans as kk
-
-    monkeypatch.setattr(kk, "GROUP_SORT", False)
     (res,) = run_spmd(_kmeans_online_worker, 1, env=RCCL, backend=None, timeout=300)
     ref_k = _kmeans_fit()
     assert np.allclose(res["kmeans"], ref_k, rtol=1e-5, atol=1e-6)
