@@ -152,8 +152,11 @@ class TorchGlmTrainer:
 
 
 # sparse trainer: a batch's column-major copy is built when the fit visits each batch at least
-# CSC_BUILD_ROUNDS times or runs at least CSC_MIN_ITERS rounds
-CSC_BUILD_ROUNDS = float(os.environ.get("FMLX_CSC_BUILD_ROUNDS", "3"))
+# CSC_BUILD_ROUNDS times or runs at least CSC_MIN_ITERS rounds. Default 0 (always): at the
+# north-star shape (100k × 64-nnz batches, dim 1M) one atomic-scatter round took 3.3 ms against a
+# 0.09 ms column-major round, so transposing a batch pays off even for a single visit
+# (profiles/r3/svc_sparse_shard_fit_atomic.jsonl)
+CSC_BUILD_ROUNDS = float(os.environ.get("FMLX_CSC_BUILD_ROUNDS", "0"))
 CSC_MIN_ITERS = int(os.environ.get("FMLX_CSC_MIN_ITERS", "64"))
 
 
@@ -248,10 +251,8 @@ class DeviceGlmTrainer:
         self._launched = 0  # rounds launched so far (round e visits batch e mod P)
 
     def _csc_pays(self, sgd: SGD) -> bool:
-        """Whether the per-batch column-major copy pays for itself in this fit: transposing a
-        batch costs about CSC_BUILD_ROUNDS rounds of the atomic-scatter gradient it replaces
-        (measured at the north-star shape: ≈1.1 ms per 100k × 64-nnz batch vs 0.49 → 0.09 ms per
-        round), so a fit that visits each batch fewer times than that keeps the scatter kernel."""
+        """Whether the per-batch column-major copy pays for itself in this fit (a fit that visits
+        each batch fewer than CSC_BUILD_ROUNDS times keeps the atomic-scatter gradient)."""
         P = -(-self.n // max(self.B, 1))
         visits = sgd.max_iter / max(P, 1) if P else 0
         return visits >= CSC_BUILD_ROUNDS or sgd.max_iter >= CSC_MIN_ITERS

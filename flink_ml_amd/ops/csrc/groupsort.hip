@@ -122,9 +122,10 @@ __global__ __launch_bounds__(GS_THREADS) void group_scatter_kernel(const int* __
 //  3. st_base      one block: per key the exclusive prefix over groups (+ the key offset), the key
 //                  offsets / chunk offsets (same outputs as group_scan);
 //  4. st_scatter   per tile: per-wave histograms again, cursors = group base + in-group prefix +
-//                  earlier waves; each wave walks its segment 64 rows at a time in row order, a
-//                  lane's rank among equal keys of the 64 from ballots (one round per distinct key),
-//                  and the last lane of each key advances the cursor.
+//                  earlier waves; each wave walks its segment 64 rows at a time in row order:
+//                  a 21-step bitonic sort of the packed (key, lane) values across the wave gives
+//                  every row its rank among equal keys of the 64 (lane order = row order), and
+//                  the last lane of each key's run advances the cursor.
 // Every step is order-deterministic; no global atomics.
 constexpr int ST_WAVES = 8;
 constexpr int ST_THREADS = ST_WAVES * 64;
@@ -260,7 +261,6 @@ __global__ __launch_bounds__(ST_THREADS) void st_scatter_kernel(const int* __res
   }
   __syncthreads();
   int* cur = sh + (long)w * k;
-  const unsigned long long below = lane ? (~0ULL >> (64 - lane)) : 0ULL;  // lanes < lane
   for (int i0 = 0; i0 < ST_SEG; i0 += 64) {
     const long r = seg0 + i0 + lane;
     int key = -1;
@@ -268,23 +268,37 @@ __global__ __launch_bounds__(ST_THREADS) void st_scatter_kernel(const int* __res
       key = keys[r];
       if ((unsigned)key >= (unsigned)k) key = -1;
     }
-    unsigned long long todo = __ballot(key >= 0);
-    int rank = 0, cnt = 0;
-    while (todo) {  // one round per distinct key among the 64 rows
-      const int leader = __builtin_ctzll(todo);
-      const int kl = __shfl(key, leader, 64);
-      const unsigned long long m = __ballot(key == kl);
-      if (key == kl) {
-        rank = __popcll(m & below);
-        cnt = __popcll(m);
+    // stable in-wave order of the 64 rows: a bitonic sort of (key, lane) packed into one int
+    // (invalid rows last), then each element's rank inside its key's run
+    int v = key >= 0 ? (key << 6) | lane : 0x7fffffff;
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        const int other = __shfl_xor(v, stride, 64);
+        const bool asc = (lane & size) == 0 || size == 64;
+        const bool low = (lane & stride) == 0;
+        const int mn = v < other ? v : other, mx = v < other ? other : v;
+        v = (low == asc) ? mn : mx;
       }
-      todo &= ~m;
     }
-    if (key >= 0) order[cur[key] + rank] = (int)r;
-    // every lane read its cursor above before the last lane of its key advances it (one wave:
-    // the LDS read and write of a key are ordered by the wave's program order)
+    const bool valid = v != 0x7fffffff;
+    const int ks = v >> 6;
+    const int prev = __shfl_up(v, 1, 64);
+    const int next = __shfl_down(v, 1, 64);
+    int start = (lane == 0 || (prev >> 6) != ks) ? lane : 0;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {  // run start = inclusive prefix max of the starts
+      const int o = __shfl_up(start, off, 64);
+      if (lane >= off && o > start) start = o;
+    }
+    const int rank = lane - start;
+    const bool last = lane == 63 || (next >> 6) != ks;
+    if (valid) order[cur[ks] + rank] = (int)(seg0 + i0 + (v & 63));
+    // every lane of a run read its cursor above before the run's last lane advances it (one
+    // wave: the LDS read and the later write are ordered by the wave's program order)
     __builtin_amdgcn_wave_barrier();
-    if (key >= 0 && rank == cnt - 1) cur[key] += cnt;
+    if (valid && last) cur[ks] += rank + 1;
     __builtin_amdgcn_wave_barrier();
   }
 }

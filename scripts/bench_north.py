@@ -136,6 +136,8 @@ def run_svc_sparse(a, ctx):
     steady = a.steady_rounds
     tr3 = DeviceGlmTrainer(SGD(max_iter=10 ** 8, learning_rate=0.1, global_batch_size=gb, tol=0.0), np.zeros(dim), X,
                            y, None, "hinge")
+    if tr3.csc is not None:
+        tr3.csc.ensure(range(tr3.csc.P))  # steady state: every batch's column-major copy exists
     tr3.run_rounds(2 * tr3.rounds_per_graph)
     torch.cuda.synchronize()
 
