@@ -599,6 +599,12 @@ class CountVectorizerModel(ModelWithData, CountVectorizerModelParams):
         return [t.with_column(self.get(self.OUTPUT_COL), SparseColumn.from_vectors(out, len(vocab)) if out else out)]
 
 
+# document frequencies: a (doc, term) presence bitmap up to this many bits, else a per-document
+# segmented sort (equal-length documents), else one global unique of (doc, term) keys
+DF_BITMAP_MAX = 1 << 32
+DF_SEGMENTED_SORT = True
+
+
 @rw.register_stage
 class CountVectorizer(Estimator, CountVectorizerParams):
     JAVA_CLASS_NAME = "org.apache.flink.ml.feature.countvectorizer.CountVectorizer"
@@ -620,11 +626,21 @@ class CountVectorizer(Estimator, CountVectorizerParams):
             codes = dc.codes.long()
             N, nd = codes.shape[0], len(dc)
             tf_t = torch.bincount(codes, minlength=V)
-            if nd * V <= (1 << 32):  # (doc, term) presence bitmap: a scatter instead of a sort
+            lens = dc.offsets[1:] - dc.offsets[:-1]
+            L = int(lens[0]) if nd else 0
+            if nd * V <= DF_BITMAP_MAX:  # (doc, term) presence bitmap: a scatter instead of a sort
                 pres = torch.zeros(nd * V, dtype=torch.bool, device=codes.device)
                 pres[dc.row_ids() * V + codes] = True
                 df_t = pres.view(nd, V).sum(0)
                 del pres
+            elif 0 < L <= 4096 and DF_SEGMENTED_SORT and bool((lens == L).all()):
+                # equal-length documents: sort each document's codes (a segmented sort along
+                # dim 1), count every term once per document
+                S = torch.sort(dc.codes.view(nd, L), dim=1).values
+                first_in_doc = torch.ones_like(S, dtype=torch.bool)
+                first_in_doc[:, 1:] = S[:, 1:] != S[:, :-1]
+                df_t = torch.bincount(S[first_in_doc].long(), minlength=V)
+                del S, first_in_doc
             else:
                 df_t = torch.bincount(torch.unique(dc.row_ids() * V + codes) % V, minlength=V)
             present = torch.nonzero(tf_t > 0).reshape(-1)

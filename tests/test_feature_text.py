@@ -171,3 +171,24 @@ def test_text_distributed():
     for vocab, df, nd in run_spmd(_spmd_text, 2):
         assert vocab == ["c", "a", "b", "e", "d", "f"]
         assert df == [0, 3, 1, 2] and nd == 3
+
+
+def test_count_vectorizer_document_frequency_paths_agree(monkeypatch):
+    """The three document-frequency paths (presence bitmap, per-document segmented sort, global
+    unique of (doc, term) keys) give the same vocabulary (ordered by document frequency)."""
+    import random
+
+    from flink_ml_amd.models.feature import text as tx
+    from flink_ml_amd.models.feature.text import CountVectorizer
+    from flink_ml_amd.table import StringArrayColumn
+
+    rnd = random.Random(4)
+    docs = [["t%d" % rnd.randrange(300) for _ in range(12)] for _ in range(400)]
+    t = Table({"input": StringArrayColumn.from_lists(docs)})
+    out = []
+    for bitmap_max, seg in ((1 << 32, True), (0, True), (0, False)):
+        monkeypatch.setattr(tx, "DF_BITMAP_MAX", bitmap_max)
+        monkeypatch.setattr(tx, "DF_SEGMENTED_SORT", seg)
+        m = CountVectorizer().set_min_df(3.0).set_max_df(200.0).fit(t)
+        out.append(m.get_model_data()[0].rows()[0][0])
+    assert out[0] == out[1] == out[2] and len(out[0]) > 100
