@@ -199,10 +199,9 @@ def _string_counts_table(t: Table, col: str):
         cnt = torch.bincount(codes, minlength=V)
         first = first_occurrence(codes, V)
         present = torch.nonzero(cnt > 0).reshape(-1)
-        pres = present.cpu().numpy()
-        if pres.shape[0] != V:  # vocabulary entries with no rows left (a filtered column)
-            tab = tab.take(pres)
-        return tab, cnt[present].cpu().numpy(), first[present].cpu().numpy()
+        # present entries in first-seen order (the device sorts; first positions are distinct)
+        present = present[torch.argsort(first[present])]
+        return tab.take(present.cpu().numpy()), cnt[present].cpu().numpy(), first[present].cpu().numpy()
     if isinstance(c, torch.Tensor):
         if c.dim() != 1:
             raise RuntimeError("The input column only supports string and numeric type.")

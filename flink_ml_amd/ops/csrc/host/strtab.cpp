@@ -152,6 +152,19 @@ void fmlx_str_lookup(const uint16_t* du, const int64_t* doffs, int64_t nd, const
   });
 }
 
+// Gather strings idx[0..m) of a table into (out_units, out_offs); out_offs[m] = total units.
+void fmlx_str_gather(const uint16_t* units, const int64_t* offs, const int64_t* idx, int64_t m, uint16_t* out_units,
+                     int64_t* out_offs) {
+  out_offs[0] = 0;
+  for (int64_t i = 0; i < m; ++i) out_offs[i + 1] = out_offs[i] + (offs[idx[i] + 1] - offs[idx[i]]);
+  parallel_for(m, 1 << 16, [&](int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i) {
+      const int64_t len = out_offs[i + 1] - out_offs[i];
+      if (len) std::memcpy(out_units + out_offs[i], units + offs[idx[i]], (size_t)len * 2);
+    }
+  });
+}
+
 // Iteration order of a java.util.HashMap (table capacity `cap`, a power of two) filled with keys
 // of Java hashes h[0..n) in index order, no treeified bins: by bucket (h ^ h >>> 16) & (cap − 1),
 // insertion order inside a bucket (HashMap.java putVal / resize keep it) — a counting sort.

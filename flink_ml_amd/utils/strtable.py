@@ -31,6 +31,7 @@ def _lib():
             "fmlx_str_lookup": [vp, vp, i64, vp, vp, i64, vp],
             "fmlx_java_string_hashes": [vp, vp, i64, vp],
             "fmlx_hashmap_order": [vp, i64, i64, vp],
+            "fmlx_str_gather": [vp, vp, vp, i64, vp, vp],
         })
         _SIGS = True
     return native.host()
@@ -85,16 +86,15 @@ class StrTable:
         return self._strs
 
     def take(self, idx: np.ndarray) -> "StrTable":
-        idx = np.asarray(idx, dtype=np.int64)
-        lens = self.offs[idx + 1] - self.offs[idx]
-        offs = np.zeros(idx.shape[0] + 1, dtype=np.int64)
-        np.cumsum(lens, out=offs[1:])
-        total = int(offs[-1])
-        if total:
-            # gather the code units of every selected string: position p of output string i is
-            # unit offs_src[idx[i]] + (p − offs[i])
-            rep = np.repeat(self.offs[idx] - offs[:-1], lens)
-            units = self.units[np.arange(total, dtype=np.int64) + rep]
+        idx = np.ascontiguousarray(idx, dtype=np.int64)
+        m = idx.shape[0]
+        offs = np.zeros(m + 1, dtype=np.int64)
+        if m:
+            total = int((self.offs[idx + 1] - self.offs[idx]).sum())
+            units = np.empty(max(total, 1), dtype=np.uint16)
+            u, o, _keep = self._ptrs()
+            _lib().fmlx_str_gather(u, o, idx.ctypes.data, m, units.ctypes.data, offs.ctypes.data)
+            units = units[:total]
         else:
             units = np.zeros(0, dtype=np.uint16)
         strs = None
