@@ -654,6 +654,7 @@ class CountVectorizer(Estimator, CountVectorizerParams):
                 if not bool((first[present] == N).any()):
                     break
                 s0, step = e0, step * 4
+            present = present[torch.argsort(first[present])]  # first-seen order, sorted on the device
             pres_h = present.cpu().numpy()
             tab = tab.take(pres_h)
             sums = torch.stack([tf_t[present], df_t[present]], 1).cpu().numpy().astype(np.float64)
