@@ -33,7 +33,7 @@ from ..parallel import comm
 from ..parallel.checkpoint import AlgorithmCheckpoint, fault_point
 from ..parallel.context import get_context
 from ..table import SparseColumn
-from ..utils import tracing
+from ..utils import graphs, tracing
 
 
 def local_batch_size(global_batch: int, rank: int, world: int) -> int:
@@ -348,11 +348,9 @@ class DeviceGlmTrainer:
         torch.cuda.current_stream(self.device).wait_stream(side)
         for t, v in zip(live, snapshot):
             t.copy_(v)
-        g = torch.cuda.CUDAGraph()
         if self.defer:
             self.parity = parity
-        with torch.cuda.graph(g):
-            self._launch_round(rounds)
+        g = graphs.capture(lambda: self._launch_round(rounds), self.device)
         self.parity = saved_parity
         self.graphs[key] = g
         return g

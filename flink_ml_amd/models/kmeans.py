@@ -28,7 +28,7 @@ from ..param.param import IntParam, ParamValidators, StringParam
 from ..parallel import comm
 from ..parallel.context import get_context
 from ..table import SparseColumn, Table
-from ..utils import tracing
+from ..utils import graphs, tracing
 from .base import ModelWithData
 from .linear import rw_update
 
@@ -181,11 +181,13 @@ def kmeans_lloyd(X: torch.Tensor, init: np.ndarray, max_iter: int, metric: str):
                 payload = rnd.run(cb)
                 comm.all_reduce_sum(payload)
                 rnd.finalize(cb, payload)
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    payload = rnd.run(cb)
-                    comm.all_reduce_sum(payload)
-                    rnd.finalize(cb, payload)
+
+                def one_round():
+                    p = rnd.run(cb)
+                    comm.all_reduce_sum(p)
+                    rnd.finalize(cb, p)
+
+                g = graphs.capture(one_round, X.device)
                 # the capture did not execute the round: replay max_iter - start - 1 times
                 for e in range(start + 1, max_iter):
                     fault_point(e)

@@ -246,6 +246,7 @@ def grad_csr(indptr, idx, val, y, wt, coef, n, d, B, loss, state, grad) -> None:
 
 # sparse rounds through per-batch transposes (csrc/glm.hip glm_csc_bwd_kernel)
 CSC_MAX_BYTES = int(os.environ.get("FMLX_CSC_MAX_BYTES", str(8 << 30)))
+CSC_RUN_MAX = int(os.environ.get("FMLX_CSC_RUN_MAX", "16"))  # consecutive batches transposed per sort
 
 
 class BatchCsc:
@@ -305,26 +306,46 @@ class BatchCsc:
         return csc
 
     def ensure(self, batches) -> None:
-        """Transposes the listed batches that are not yet (idempotent; never inside a capture)."""
+        """Transposes the listed batches that are not yet (idempotent; never inside a capture).
+        Runs of consecutive batches are transposed together: ONE stable sort of int32 keys
+        (batch slot · d + column) over the run's non-zeros — entries of a batch stay in its own
+        CSR range, columns ascend inside it and rows ascend inside a column — one gather of the
+        row ids and values, one bincount for the column pointers."""
         indptr, indices, values = self._src
         dev = values.device
         n, d, B = self.n, self.d, self.B
-        for b in sorted(set(int(x) % self.P for x in batches)):
-            if self.built[b]:
-                continue
-            self.built[b] = True
-            j0, j1 = self.bounds[b], self.bounds[b + 1]
+        todo = [b for b in sorted(set(int(x) % self.P for x in batches)) if not self.built[b]]
+        if not todo:
+            return
+        max_slots = max(1, min(CSC_RUN_MAX, (2 ** 31 - 1) // max(d, 1)))
+        runs, cur = [], [todo[0]]
+        for b in todo[1:]:
+            if b == cur[-1] + 1 and len(cur) < max_slots:
+                cur.append(b)
+            else:
+                runs.append(cur)
+                cur = [b]
+        runs.append(cur)
+        for run in runs:
+            for b in run:
+                self.built[b] = True
+            b0, b1 = run[0], run[-1] + 1
+            j0, j1 = self.bounds[b0], self.bounds[b1]
             if j1 == j0:
                 continue
-            r0, r1 = b * B, min((b + 1) * B, n)
-            cols = indices[j0:j1].to(torch.int64)
-            rows = torch.repeat_interleave(torch.arange(r1 - r0, device=dev, dtype=torch.int32),
-                                           (indptr[r0 + 1:r1 + 1] - indptr[r0:r1]).to(torch.int64))
-            order = torch.sort(cols, stable=True).indices
-            self.erow[j0:j1] = rows[order]
+            r0, r1 = b0 * B, min(b1 * B, n)
+            lens = indptr[r0 + 1:r1 + 1] - indptr[r0:r1]
+            rows = torch.arange(r0, r1, device=dev, dtype=torch.int64)
+            slot = torch.div(rows - r0, B, rounding_mode="floor")
+            rel = (rows - (b0 * B) - slot * B).to(torch.int32)  # batch-relative row id
+            ent_slot = torch.repeat_interleave(slot.to(torch.int32), lens, output_size=j1 - j0)
+            key = ent_slot * d + indices[j0:j1]
+            order = torch.sort(key, stable=True).indices
+            self.erow[j0:j1] = torch.repeat_interleave(rel, lens, output_size=j1 - j0)[order]
             self.evals[j0:j1] = values[j0:j1][order]
-            self.colptr[b, 1:] = torch.cumsum(torch.bincount(cols, minlength=d), 0).to(torch.int32)
-            del cols, rows, order
+            cnt = torch.bincount(key, minlength=len(run) * d).view(len(run), d)
+            self.colptr[b0:b1, 1:] = torch.cumsum(cnt, 1).to(torch.int32)
+            del key, order, ent_slot, cnt
 
     def ensure_rounds(self, first_epoch: int, k: int) -> None:
         """Transposes the batches of rounds first_epoch … first_epoch + k − 1."""
