@@ -189,7 +189,12 @@ class DeviceGlmTrainer:
         self.acc = acc
         self.y = y.to(device=dev, dtype=acc).reshape(-1).contiguous()
         self.w = weight.to(device=dev, dtype=acc).reshape(-1).contiguous() if weight is not None else None
-        self.coef = torch.as_tensor(np.asarray(init_coef, dtype=np.float64)).to(device=dev, dtype=acc).contiguous()
+        c0 = np.asarray(init_coef, dtype=np.float64)
+        if not c0.any():  # the usual zero init (1M-wide sparse models): no pageable H2D copy
+            self.coef = torch.zeros(c0.shape, dtype=acc, device=dev)
+        else:
+            c0 = torch.from_numpy(np.ascontiguousarray(c0)).to(acc)
+            self.coef = (c0.pin_memory() if dev.type == "cuda" else c0).to(dev, non_blocking=True).contiguous()
         self.B = local_batch_size(sgd.global_batch_size, ctx.rank, ctx.world_size)
         self.state = torch.zeros(8, dtype=torch.int32, device=dev)
         self.state[1] = 1  # running[0]

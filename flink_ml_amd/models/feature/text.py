@@ -136,10 +136,78 @@ def _register_textops():
     from ...ops import native
 
     vp, i64 = ctypes.c_void_p, ctypes.c_int64
-    native.register_host_sigs({"fmlx_tokenize_ws_lower": ([vp, vp, i64, vp, vp, i64, vp, vp, vp], i64)})
+    native.register_host_sigs({"fmlx_tokenize_ws_lower": ([vp, vp, i64, vp, vp, i64, vp, vp, vp], i64),
+                               "fmlx_tokenize_class": ([vp, vp, i64, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                        vp, vp, i64, vp, vp, vp], i64)})
 
 
 _register_textops()
+
+
+def simple_class_pattern(pattern: str):
+    """(delimiter table over ASCII [128] uint8, plus) when ``pattern`` is ONE character atom (a
+    literal, an escape, ``.``, a ``[...]`` class, ``\\s``/``\\d``/``\\w``) optionally followed by
+    ``+`` — the split the native class tokenizer does; None otherwise."""
+    try:
+        import re._parser as sre_parse  # Python >= 3.11
+    except ImportError:  # pragma: no cover - Python 3.10
+        import sre_parse
+    try:
+        parsed = list(sre_parse.parse(pattern))
+    except Exception:
+        return None
+    if len(parsed) != 1:
+        return None
+    op, av = parsed[0]
+    plus = False
+    atom = pattern
+    if op is sre_parse.MAX_REPEAT or op is sre_parse.MIN_REPEAT:
+        lo, hi, sub = av
+        if op is not sre_parse.MAX_REPEAT or lo != 1 or hi != sre_parse.MAXREPEAT or len(sub) != 1:
+            return None
+        op = list(sub)[0][0]
+        plus = True
+        atom = pattern[:-1]
+        if not pattern.endswith("+"):
+            return None
+    if op not in (sre_parse.LITERAL, sre_parse.IN, sre_parse.ANY, sre_parse.NOT_LITERAL):
+        return None
+    try:
+        rx = re.compile(atom)
+    except re.error:
+        return None
+    table = np.array([1 if rx.fullmatch(chr(c)) else 0 for c in range(128)], dtype=np.uint8)
+    return table, plus
+
+
+def native_class_tokens(strings: List[str], table: np.ndarray, plus: bool, lower: bool, min_len: int):
+    """RegexTokenizer's split (gaps) on a one-character pattern in native code for ASCII strings:
+    (tokens per string, flat token ids, token vocabulary), or None for non-ASCII input."""
+    from ...ops import native
+
+    try:
+        raw = "".join(strings).encode("ascii")
+    except UnicodeEncodeError:
+        return None
+    n = len(strings)
+    offs = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.fromiter(map(len, strings), dtype=np.int64, count=n), out=offs[1:])
+    cap = int(offs[-1]) + n + 1
+    ntok = np.zeros(n, dtype=np.int32)
+    ids = np.zeros(cap, dtype=np.int32)
+    vbytes = np.zeros(int(offs[-1]) + cap, dtype=np.uint8)
+    voffs = np.zeros(cap + 1, dtype=np.int64)
+    nv = np.zeros(1, dtype=np.int64)
+    buf = np.frombuffer(raw, dtype=np.uint8) if raw else np.zeros(1, dtype=np.uint8)
+    tab = np.ascontiguousarray(table, dtype=np.uint8)
+    nt = native.host().fmlx_tokenize_class(buf.ctypes.data, offs.ctypes.data, n, tab.ctypes.data, int(plus),
+                                           int(lower), int(min_len), ntok.ctypes.data, ids.ctypes.data, cap,
+                                           vbytes.ctypes.data, voffs.ctypes.data, nv.ctypes.data)
+    if nt < 0:
+        return None
+    nvoc = int(nv[0])
+    vocab = vbytes[: int(voffs[nvoc])].tobytes().decode("ascii").split("\n")[:nvoc] if nvoc else []
+    return ntok.astype(np.int64), ids[:nt], vocab
 
 
 def _native_ws_lower_tokens(strings: List[str]):
@@ -192,6 +260,8 @@ def _per_string_arrays(t: Table, col: str, fn, native_kind: str = "", batched=No
     dev = config.compute_device()
     codes = c.codes.to(dev).long()
     nat = _native_ws_lower_tokens(c.vocab) if native_kind == "ws_lower" else None
+    if nat is None and callable(native_kind):
+        nat = native_kind(c.vocab)
     if nat is None and batched is not None:
         # one regex pass over all distinct strings, the token dictionary by a native hash join
         res = batched(c.vocab)
@@ -278,7 +348,9 @@ class RegexTokenizer(Transformer, HasInputCol, HasOutputCol):
             sid = np.repeat(np.arange(ntok.shape[0]), ntok)
             return np.bincount(sid[ok], minlength=ntok.shape[0]).astype(np.int64), tok[ok]
 
-        out = _per_string_arrays(t, self.get(self.INPUT_COL), tokenize, batched=batched)
+        simple = simple_class_pattern(pat.pattern) if gaps else None
+        nat = (lambda strings: native_class_tokens(strings, simple[0], simple[1], low, mn)) if simple else ""
+        out = _per_string_arrays(t, self.get(self.INPUT_COL), tokenize, native_kind=nat, batched=batched)
         if out is None:
             out = [tokenize(s) for s in _strings_col(t, self.get(self.INPUT_COL))]
         return [t.with_column(self.get(self.OUTPUT_COL), out)]

@@ -38,14 +38,19 @@ extern "C" {
 // tok_cap) the distinct tokens in first-seen order, each followed by '\n' (a token never contains
 // one), with vocab_offs[] (capacity tok_cap + 1) their start offsets and *nvocab their count.
 // Returns the total number of tokens, -1 for non-ASCII input, -2 when a capacity is too small.
-int64_t fmlx_tokenize_ws_lower(const char* bytes, const int64_t* offs, int64_t n, int32_t* ntok, int32_t* tok_ids,
-                               int64_t tok_cap, char* vocab_bytes, int64_t* vocab_offs, int64_t* nvocab) {
+// General form: split on a single-character class (`delim`, a 128-entry table over ASCII), `plus`
+// = runs of delimiters are ONE delimiter (pattern `X+`), optional lowercasing, tokens shorter than
+// `min_len` dropped (RegexTokenizer.java:74-90 with gaps = true on a one-character pattern).
+int64_t fmlx_tokenize_class(const char* bytes, const int64_t* offs, int64_t n, const uint8_t* delim, int plus,
+                            int lower, int min_len, int32_t* ntok, int32_t* tok_ids, int64_t tok_cap,
+                            char* vocab_bytes, int64_t* vocab_offs, int64_t* nvocab) {
+  auto isd = [&](unsigned char c) -> bool { return delim[c & 0x7f] != 0; };
   const int64_t total_bytes = offs[n];
   for (int64_t i = 0; i < total_bytes; ++i)
     if ((unsigned char)bytes[i] >= 0x80) return -1;
   // lowercased copy lives in vocab_bytes' scratch? no: tokens are views into a lowered buffer
   char* low = new char[total_bytes > 0 ? total_bytes : 1];
-  for (int64_t i = 0; i < total_bytes; ++i) low[i] = lower_ascii(bytes[i]);
+  for (int64_t i = 0; i < total_bytes; ++i) low[i] = lower ? lower_ascii(bytes[i]) : bytes[i];
   // token → id: open addressing over token hashes (ids index vocab_offs; a flat table is several
   // times faster than std::unordered_map at a million distinct tokens)
   int64_t cap = 16;
@@ -98,22 +103,24 @@ int64_t fmlx_tokenize_ws_lower(const char* bytes, const int64_t* offs, int64_t n
     const char* p = low + offs[s];
     const int64_t len = offs[s + 1] - offs[s];
     const int64_t before = nt;
-    if (len == 0) {
-      if (!emit(p, 0)) { delete[] low; return -2; }
-      ntok[s] = 1;
+    if (len == 0) {  // no match: the (empty) string itself
+      if (min_len <= 0 && !emit(p, 0)) { delete[] low; return -2; }
+      ntok[s] = (int32_t)(nt - before);
       continue;
     }
     // trailing empty tokens are dropped: the last token ends at the last non-delimiter
     int64_t end = len;
-    while (end > 0 && java_ws((unsigned char)p[end - 1])) --end;
+    while (end > 0 && isd((unsigned char)p[end - 1])) --end;
     if (end == 0) {  // only delimiters: Java yields an empty array
       ntok[s] = 0;
       continue;
     }
     int64_t start = 0;
     for (int64_t i = 0; i <= end; ++i) {
-      if (i == end || java_ws((unsigned char)p[i])) {
-        if (!emit(p + start, i - start)) { delete[] low; return -2; }
+      if (i == end || isd((unsigned char)p[i])) {
+        if (i - start >= min_len && !emit(p + start, i - start)) { delete[] low; return -2; }
+        if (plus)
+          while (i + 1 < end && isd((unsigned char)p[i + 1])) ++i;  // a run is ONE delimiter
         start = i + 1;
       }
     }
@@ -122,6 +129,13 @@ int64_t fmlx_tokenize_ws_lower(const char* bytes, const int64_t* offs, int64_t n
   delete[] low;
   *nvocab = nv;
   return nt;
+}
+
+int64_t fmlx_tokenize_ws_lower(const char* bytes, const int64_t* offs, int64_t n, int32_t* ntok, int32_t* tok_ids,
+                               int64_t tok_cap, char* vocab_bytes, int64_t* vocab_offs, int64_t* nvocab) {
+  uint8_t ws[128] = {0};
+  for (int c = 0; c < 128; ++c) ws[c] = java_ws((unsigned char)c) ? 1 : 0;
+  return fmlx_tokenize_class(bytes, offs, n, ws, 0, 1, 0, ntok, tok_ids, tok_cap, vocab_bytes, vocab_offs, nvocab);
 }
 }
 

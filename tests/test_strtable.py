@@ -85,3 +85,25 @@ def test_string_indexer_high_cardinality_orders_and_index_to_string():
     out = dup.transform(Table({"c": StringColumn.from_list(["x", "y"])}))[0].column("i")
     assert out.tolist() == [2.0, 1.0]
     assert md is not None and torch.is_tensor(out)
+
+
+def test_native_class_tokenizer_matches_java_split():
+    """RegexTokenizer's native path for one-character patterns (optionally `X+`) equals
+    String.split + minTokenLength on every string; other patterns are not taken."""
+    from flink_ml_amd.models.feature.text import native_class_tokens, simple_class_pattern
+
+    rnd = random.Random(3)
+    strs = ["".join(rnd.choice("ab1 1\tB.,") for _ in range(rnd.randrange(0, 10))) for _ in range(3000)]
+    strs += ["", "1", "11", "1a", "a1", "A11B", " x ", "  "]
+    for p in ("1+", "1", "\\s+", "\\s", "[ab]+", "[^a-z]", ".", "\\.", "a|b"):
+        table, plus = simple_class_pattern(p)
+        for low in (True, False):
+            for mn in (0, 1, 2):
+                ntok, ids, vocab = native_class_tokens(strs, table, plus, low, mn)
+                offs = np.concatenate([[0], np.cumsum(ntok)])
+                for i, s in enumerate(strs):
+                    ref = [x for x in java_split(p, s.lower() if low else s) if len(x) >= mn]
+                    assert [vocab[j] for j in ids[offs[i]:offs[i + 1]]] == ref, (p, low, mn, s)
+    for p in ("x*", "ab", "1{2}", "^a", "(1)+"):
+        assert simple_class_pattern(p) is None
+    assert native_class_tokens(["é1"], *simple_class_pattern("1"), True, 1) is None  # non-ASCII: Python path
