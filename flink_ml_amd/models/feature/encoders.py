@@ -563,14 +563,14 @@ class VectorIndexer(Estimator, VectorIndexerParams):
             S, _ = torch.sort(X, dim=0)
             stats[:d] = (1 + (S[1:] != S[:-1]).sum(0)).to(torch.float64).cpu()
         if dist:
-            dmax = comm.all_reduce(stats[d + 1:].clone(), "max")
-            if n and float(dmax[0]) != d:
+            # vector length agreement over the ranks that hold rows (every rank raises together)
+            dd = torch.tensor([float(d) if n else -1.0, -float(d) if n else -float(1 << 40)], dtype=torch.float64)
+            dd = comm.all_reduce(dd, "max")
+            if dd[0] >= 0 and float(dd[0]) != -float(dd[1]):
                 raise ValueError("Feature vectors should be of equal length.")
-            d = int(dmax[0])
-            loc = torch.zeros(d + 1, dtype=torch.float64)
-            loc[:stats.shape[0] - 2] = stats[:-2] if n else 0.0
-            loc[d] = float(n)
-            red_max = comm.all_reduce(loc[:d].clone(), "max")
+            d = max(int(dd[0]), 0)
+            loc = stats[:d].clone() if n else torch.zeros(d, dtype=torch.float64)
+            red_max = comm.all_reduce(loc, "max") if d else loc
             total = comm.all_reduce_scalar(float(n), "sum")
         else:
             red_max, total = stats[:d], float(n)
