@@ -419,10 +419,19 @@ class StringIndexer(Estimator, StringIndexerParams):
         if len(cols) != len(self.get(self.OUTPUT_COLS)):
             raise ValueError("The number of input columns and output columns must be equal.")
         arrays = []
+        dist = get_world_distributed()
         for c in cols:
             # per-rank (string, count, first position) tables merged by a keyed shuffle of the
             # strings (all-to-all to the owner of each string's hash, owners' maps all-gathered)
-            tab, cnt, first = _string_counts_table(t, c)
+            err = None
+            try:
+                tab, cnt, first = _string_counts_table(t, c)
+            except RuntimeError as e:  # a bad column on one rank: every rank raises, none blocks
+                err = e
+            if dist and comm.all_reduce_scalar(0.0 if err else 1.0, "min") < 1.0:
+                raise err or RuntimeError("The input column only supports string and numeric type.")
+            if err is not None:
+                raise err
             tab, sums, _ = ds.reduce_strings_by_key(tab, cnt[:, None], first)
             perm = order_string_table(tab, sums[:, 0], self.get(self.STRING_ORDER_TYPE))
             arrays.append(tab.take_strings(perm))
