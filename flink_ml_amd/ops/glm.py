@@ -340,7 +340,7 @@ class BatchCsc:
             rel = (rows - (b0 * B) - slot * B).to(torch.int32)  # batch-relative row id
             ent_slot = torch.repeat_interleave(slot.to(torch.int32), lens, output_size=j1 - j0)
             key = ent_slot * d + indices[j0:j1]
-            order = torch.sort(key, stable=True).indices
+            order = _stable_order(key, len(run) * d)
             self.erow[j0:j1] = torch.repeat_interleave(rel, lens, output_size=j1 - j0)[order]
             self.evals[j0:j1] = values[j0:j1][order]
             cnt = torch.bincount(key, minlength=len(run) * d).view(len(run), d)
@@ -352,6 +352,30 @@ class BatchCsc:
         if all(self.built):
             return
         self.ensure(range(first_epoch, first_epoch + min(k, self.P)))
+
+
+def _stable_order(key: torch.Tensor, bound: int) -> torch.Tensor:
+    """Stable argsort of int32 keys in [0, bound): on the GPU an LSD radix sort over only the
+    ceil(log2 bound) key bits with int32 payloads (sort.hip, e.g. 3 digit passes instead of
+    torch.sort's 4 plus int64 indices for 16 batches × 1M columns); torch.sort elsewhere."""
+    m = key.numel()
+    if key.device.type != "cuda" or m == 0:
+        return torch.sort(key, stable=True).indices
+    from . import kmeans as _kk  # registers the sort signatures
+
+    lib = native.kernels()
+    bits = max(1, int(bound - 1).bit_length())
+    tb = int(lib.fmlx_sort_pairs_temp_bytes(m, bits))
+    if tb < 0:
+        return torch.sort(key, stable=True).indices
+    temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=key.device)
+    iota = torch.arange(m, dtype=torch.int32, device=key.device)
+    keys_out = torch.empty_like(key)
+    order = torch.empty(m, dtype=torch.int32, device=key.device)
+    native.call("fmlx_sort_pairs", native.ptr(key.contiguous()), native.ptr(keys_out), native.ptr(iota),
+                native.ptr(order), m, bits, native.ptr(temp), tb, native.stream_ptr(key.device))
+    del _kk
+    return order.long()
 
 
 def wl_elems() -> int:
