@@ -340,12 +340,14 @@ class BatchCsc:
             rel = (rows - (b0 * B) - slot * B).to(torch.int32)  # batch-relative row id
             ent_slot = torch.repeat_interleave(slot.to(torch.int32), lens, output_size=j1 - j0)
             key = ent_slot * d + indices[j0:j1]
-            order = _stable_order(key, len(run) * d)
+            order, starts = _stable_order(key, len(run) * d)
             self.erow[j0:j1] = torch.repeat_interleave(rel, lens, output_size=j1 - j0)[order]
             self.evals[j0:j1] = values[j0:j1][order]
-            cnt = torch.bincount(key, minlength=len(run) * d).view(len(run), d)
-            self.colptr[b0:b1, 1:] = torch.cumsum(cnt, 1).to(torch.int32)
-            del key, order, ent_slot, cnt
+            # batch s of the run starts at starts[s·d]; its column c at starts[s·d + c]
+            S = starts[:-1].view(len(run), d)
+            self.colptr[b0:b1, :d] = S - S[:, :1]
+            self.colptr[b0:b1, d] = starts[d::d] - S[:, 0]
+            del key, order, ent_slot, starts, S
 
     def ensure_rounds(self, first_epoch: int, k: int) -> None:
         """Transposes the batches of rounds first_epoch … first_epoch + k − 1."""
@@ -354,28 +356,36 @@ class BatchCsc:
         self.ensure(range(first_epoch, first_epoch + min(k, self.P)))
 
 
-def _stable_order(key: torch.Tensor, bound: int) -> torch.Tensor:
-    """Stable argsort of int32 keys in [0, bound): on the GPU an LSD radix sort over only the
+def _stable_order(key: torch.Tensor, bound: int):
+    """Stable argsort of int32 keys in [0, bound) and the bucket starts of the sorted keys
+    (int32 [bound + 1]: first position of a key >= c). On the GPU an LSD radix sort over only the
     ceil(log2 bound) key bits with int32 payloads (sort.hip, e.g. 3 digit passes instead of
-    torch.sort's 4 plus int64 indices for 16 batches × 1M columns); torch.sort elsewhere."""
+    torch.sort's 4 plus int64 indices for 16 batches × 1M columns) and one boundary kernel;
+    torch elsewhere."""
     m = key.numel()
     if key.device.type != "cuda" or m == 0:
-        return torch.sort(key, stable=True).indices
+        order = torch.sort(key, stable=True).indices
+        starts = torch.zeros(bound + 1, dtype=torch.int32, device=key.device)
+        starts[1:] = torch.cumsum(torch.bincount(key.long(), minlength=bound), 0).to(torch.int32)
+        return order, starts
     from . import kmeans as _kk  # registers the sort signatures
 
     lib = native.kernels()
     bits = max(1, int(bound - 1).bit_length())
     tb = int(lib.fmlx_sort_pairs_temp_bytes(m, bits))
     if tb < 0:
-        return torch.sort(key, stable=True).indices
+        raise RuntimeError("radix sort temp-size query failed")
     temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=key.device)
     iota = torch.arange(m, dtype=torch.int32, device=key.device)
     keys_out = torch.empty_like(key)
     order = torch.empty(m, dtype=torch.int32, device=key.device)
     native.call("fmlx_sort_pairs", native.ptr(key.contiguous()), native.ptr(keys_out), native.ptr(iota),
                 native.ptr(order), m, bits, native.ptr(temp), tb, native.stream_ptr(key.device))
+    starts = torch.empty(bound + 1, dtype=torch.int32, device=key.device)
+    native.call("fmlx_sorted_bounds", native.ptr(keys_out), m, int(bound), native.ptr(starts),
+                native.stream_ptr(key.device))
     del _kk
-    return order.long()
+    return order.long(), starts
 
 
 def wl_elems() -> int:

@@ -30,6 +30,7 @@ native.register_kernel_sigs({
     "fmlx_kmeans_offsets": [c_void_p, c_long, c_int, c_void_p, c_void_p, c_void_p],
     "fmlx_sort_pairs_temp_bytes": ([c_long, c_int], c_long),
     "fmlx_sort_pairs": [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_long, c_void_p],
+    "fmlx_sorted_bounds": [c_void_p, c_long, c_int, c_void_p, c_void_p],
     "fmlx_kmeans_finalize": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                              c_void_p],
     "fmlx_group_max_keys": [],

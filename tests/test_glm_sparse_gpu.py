@@ -112,3 +112,28 @@ def test_sparse_sgd_two_ranks_one_gpu():
     res = run_spmd(_sparse_worker, 2, env={"FMLX_DEVICE": "cuda:0", "FMLX_XGMI": "0"}, timeout=300)
     assert res[0][0] < 1e-10 and res[1][0] < 1e-10
     assert res[0][1] == res[1][1]  # replicas identical
+
+
+@pytest.mark.parametrize("run_max", [1, 3, 16])
+def test_batch_csc_device_transpose_matches_host(run_max, monkeypatch):
+    """Per-batch column-major copies built on the device (bit-limited radix sort + bucket-start
+    kernel, runs of consecutive batches in one sort) equal the host construction exactly."""
+    _need_gpu()
+    from flink_ml_amd.ops import glm as gk
+
+    monkeypatch.setattr(gk, "CSC_RUN_MAX", run_max)
+    g = torch.Generator().manual_seed(0)
+    n, d, B = 20_037, 3_001, 1_000
+    lens = torch.randint(0, 12, (n,), generator=g)
+    indptr = torch.zeros(n + 1, dtype=torch.int64)
+    indptr[1:] = torch.cumsum(lens, 0)
+    idx = torch.cat([torch.sort(torch.randperm(d, generator=g)[:int(k)]).values for k in lens]).to(torch.int32)
+    vals = torch.rand(int(indptr[-1]), generator=g, dtype=torch.float32)
+    dev = gk.BatchCsc.alloc(indptr.cuda(), idx.cuda(), vals.cuda(), n, d, B)
+    dev.ensure([0, 1, 2, 7, 8, 12, 19, 20])
+    dev.ensure(range(dev.P))
+    host = gk.BatchCsc.alloc(indptr, idx, vals, n, d, B)
+    host.ensure(range(host.P))
+    assert torch.equal(dev.colptr.cpu(), host.colptr)
+    assert torch.equal(dev.erow.cpu(), host.erow)
+    assert torch.equal(dev.evals.cpu(), host.evals)
