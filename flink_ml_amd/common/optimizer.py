@@ -211,7 +211,8 @@ class DeviceGlmTrainer:
             self.nparts = 0
             if dev.type == "cuda" and self.n > 0 and self._csc_pays(sgd):
                 # allocated here, batches transposed lazily before the rounds that visit them
-                self.csc = gk.BatchCsc.alloc(self.indptr, self.indices, self.values, self.n, self.d, self.B)
+                self.csc = gk.BatchCsc.alloc(self.indptr, self.indices, self.values, self.n, self.d, self.B,
+                                             max_rounds=sgd.max_iter)
                 if self.csc is not None:
                     self.mult = torch.zeros(max(1, min(self.B, self.n)), dtype=acc, device=dev)
                     self.wl = torch.zeros(gk.wl_elems(), dtype=acc, device=dev)  # Σw/Σloss slots per parity
@@ -272,7 +273,7 @@ class DeviceGlmTrainer:
         s = self.sgd
         if self.csc is not None:
             if not torch.cuda.is_current_stream_capturing():
-                self.csc.ensure_rounds(self._launched, 1)
+                self._ensure_csc(self._launched, 1)
             # forward (per-row multipliers) + atomic-free column-major backward; on 1 GPU the
             # backward applies the update and the termination check itself
             gk.csc_round(self.csc, self.indptr, self.indices, self.values, self.y, self.w, self.coef, self.n, self.d,
@@ -327,6 +328,18 @@ class DeviceGlmTrainer:
             comm.all_reduce_sum(self.feedback)
             gk.update(self.feedback, self.d, self.coef, self.state, s.max_iter, s.tol, s.learning_rate, s.reg,
                       s.elastic_net)
+
+    def _ensure_csc(self, first: int, k: int) -> None:
+        """Column-major copies of the batches rounds first … first + k − 1 visit; rounds at or
+        past max_iter never run (the device running flag predicates them off before any load).
+        A storage re-allocation moves the device pointers the captured hipGraphs hold."""
+        k = min(k, self.sgd.max_iter - first)
+        if k <= 0:
+            return
+        v = self.csc.version
+        self.csc.ensure_rounds(first, k)
+        if self.csc.version != v:
+            self.graphs.clear()
 
     def _graph_key(self, rounds: int, parity=None):
         if not self.defer:
@@ -403,7 +416,7 @@ class DeviceGlmTrainer:
                 done += 1
             r = key[0] if self.defer else key
             if self.csc is not None:
-                self.csc.ensure_rounds(self._launched, r)
+                self._ensure_csc(self._launched, r)
             g = self.graphs.get(key) or self._capture(key)
             g.replay()
             self._launched += r
@@ -415,7 +428,7 @@ class DeviceGlmTrainer:
     def run_rounds(self, k: int) -> None:
         """Runs ``k`` SGD rounds (each predicated on the device running flag), no host sync."""
         if self.csc is not None:
-            self.csc.ensure_rounds(self._launched, k)  # the batches these rounds visit
+            self._ensure_csc(self._launched, k)  # the batches these rounds visit
         first = self._launched
         self._launched += k
         if not self.use_graph or self._short:

@@ -261,15 +261,24 @@ class BatchCsc:
 
     Batches are transposed lazily (``ensure``): a fit transposes only the batches its rounds
     visit, before the rounds are launched (SGD.java:263-268 visits batch e mod P in round e), so
-    a short fit over a large partition does not pay for the whole partition.
+    a short fit over a large partition does not pay for the whole partition. The storage is
+    allocated at the first ``ensure`` for the leading ``cap`` batches only (a fit of
+    ``max_rounds`` < P rounds from round 0 visits batches 0 … max_rounds − 1, whose entries are the
+    CSR prefix [0, indptr[max_rounds·B])); a batch beyond it re-allocates the whole partition,
+    copies what was built and bumps ``version`` (device pointers changed: captured hipGraphs
+    must be re-captured).
     """
 
-    def __init__(self, colptr, erow, evals, G: int, bounds, indptr, indices, values, n: int, d: int, B: int):
-        self.colptr, self.erow, self.evals, self.G = colptr, erow, evals, G
+    def __init__(self, G: int, bounds, indptr, indices, values, n: int, d: int, B: int, cap: int):
+        self.G = G
         self.bounds, self.P = bounds, len(bounds) - 1
         self._src = (indptr, indices, values)
         self.n, self.d, self.B = n, d, B
         self.built = [False] * self.P
+        self.cap = 0  # leading batches the storage covers (0: not allocated yet)
+        self._want = max(1, min(cap, self.P))
+        self.colptr = self.erow = self.evals = None
+        self.version = 0
 
     @staticmethod
     def pick_group(avg_nnz: float) -> int:
@@ -279,7 +288,9 @@ class BatchCsc:
         return g
 
     @staticmethod
-    def alloc(indptr, indices, values, n: int, d: int, B: int):
+    def alloc(indptr, indices, values, n: int, d: int, B: int, max_rounds: Optional[int] = None):
+        """Checks the size limits and returns an (empty) BatchCsc, or None. ``max_rounds``: the
+        rounds the fit can run from round 0 (sizes the first allocation)."""
         if os.environ.get("FMLX_CSR_TRANSPOSE", "1") == "0" or n <= 0 or B <= 0:
             return None
         P = (n + B - 1) // B
@@ -287,15 +298,11 @@ class BatchCsc:
         extra = P * (d + 1) * 4 + nnz * (4 + values.element_size())
         if extra > CSC_MAX_BYTES:
             return None
-        dev = values.device
         bounds = indptr[torch.arange(0, P + 1, device=indptr.device).mul_(B).clamp_(max=n)].tolist()
         if max(bounds[i + 1] - bounds[i] for i in range(P)) >= 2 ** 31:
             return None
-        colptr = torch.zeros((P, d + 1), dtype=torch.int32, device=dev)
-        erow = torch.empty(nnz, dtype=torch.int32, device=dev)
-        evals = torch.empty_like(values)
-        return BatchCsc(colptr, erow, evals, BatchCsc.pick_group(nnz / max(n, 1)), bounds, indptr, indices, values,
-                        n, d, B)
+        return BatchCsc(BatchCsc.pick_group(nnz / max(n, 1)), bounds, indptr, indices, values, n, d, B,
+                        P if max_rounds is None else int(max_rounds))
 
     @staticmethod
     def build(indptr, indices, values, n: int, d: int, B: int):
@@ -305,18 +312,37 @@ class BatchCsc:
             csc.ensure(range(csc.P))
         return csc
 
+    def _storage(self, need: int) -> None:
+        """Storage for at least the leading ``need`` batches (grows to the whole partition)."""
+        if need <= self.cap:
+            return
+        cap = self._want if self.cap == 0 and need <= self._want else self.P
+        values = self._src[2]
+        dev = values.device
+        ne = self.bounds[cap]
+        colptr = torch.empty((cap, self.d + 1), dtype=torch.int32, device=dev)
+        erow = torch.empty(max(ne, 1), dtype=torch.int32, device=dev)
+        evals = torch.empty(max(ne, 1), dtype=values.dtype, device=dev)
+        if self.cap:
+            old = self.bounds[self.cap]
+            colptr[:self.cap] = self.colptr
+            erow[:old] = self.erow[:old]
+            evals[:old] = self.evals[:old]
+            self.version += 1
+        self.colptr, self.erow, self.evals, self.cap = colptr, erow, evals, cap
+
     def ensure(self, batches) -> None:
         """Transposes the listed batches that are not yet (idempotent; never inside a capture).
         Runs of consecutive batches are transposed together: ONE stable sort of int32 keys
         (batch slot · d + column) over the run's non-zeros — entries of a batch stay in its own
-        CSR range, columns ascend inside it and rows ascend inside a column — one gather of the
-        row ids and values, one bincount for the column pointers."""
+        CSR range, columns ascend inside it and rows ascend inside a column — then the row ids,
+        values and column pointers straight from the sorted order (csrc/csc_build.hip)."""
         indptr, indices, values = self._src
-        dev = values.device
         n, d, B = self.n, self.d, self.B
         todo = [b for b in sorted(set(int(x) % self.P for x in batches)) if not self.built[b]]
         if not todo:
             return
+        self._storage(todo[-1] + 1)
         max_slots = max(1, min(CSC_RUN_MAX, (2 ** 31 - 1) // max(d, 1)))
         runs, cur = [], [todo[0]]
         for b in todo[1:]:
@@ -332,22 +358,56 @@ class BatchCsc:
             b0, b1 = run[0], run[-1] + 1
             j0, j1 = self.bounds[b0], self.bounds[b1]
             if j1 == j0:
+                self.colptr[b0:b1].zero_()
                 continue
             r0, r1 = b0 * B, min(b1 * B, n)
-            lens = indptr[r0 + 1:r1 + 1] - indptr[r0:r1]
-            rows = torch.arange(r0, r1, device=dev, dtype=torch.int64)
-            slot = torch.div(rows - r0, B, rounding_mode="floor")
-            rel = (rows - (b0 * B) - slot * B).to(torch.int32)  # batch-relative row id
-            ent_slot = torch.repeat_interleave(slot.to(torch.int32), lens, output_size=j1 - j0)
-            key = ent_slot * d + indices[j0:j1]
-            order, starts = _stable_order(key, len(run) * d)
-            self.erow[j0:j1] = torch.repeat_interleave(rel, lens, output_size=j1 - j0)[order]
-            self.evals[j0:j1] = values[j0:j1][order]
-            # batch s of the run starts at starts[s·d]; its column c at starts[s·d + c]
-            S = starts[:-1].view(len(run), d)
-            self.colptr[b0:b1, :d] = S - S[:, :1]
-            self.colptr[b0:b1, d] = starts[d::d] - S[:, 0]
-            del key, order, ent_slot, starts, S
+            if values.device.type == "cuda":
+                self._transpose_native(b0, len(run), r0, r1, j0, j1)
+            else:
+                self._transpose_torch(b0, len(run), r0, r1, j0, j1)
+
+    def _transpose_native(self, b0, slots, r0, r1, j0, j1) -> None:
+        indptr, indices, values = self._src
+        dev = values.device
+        m, d = j1 - j0, self.d
+        stream = native.stream_ptr(dev)
+        key = torch.empty(m, dtype=torch.int32, device=dev)
+        rel = torch.empty(m, dtype=torch.int32, device=dev)
+        iota = torch.empty(m, dtype=torch.int32, device=dev)
+        native.call("fmlx_csc_keys", native.ptr(indptr), native.ptr(indices), r0, r1, self.B, d, j0, native.ptr(key),
+                    native.ptr(rel), native.ptr(iota), stream)
+        bits = max(1, int(slots * d - 1).bit_length())
+        tb = int(native.kernels().fmlx_sort_pairs_temp_bytes(m, bits))
+        if tb < 0:
+            raise RuntimeError("radix sort temp-size query failed")
+        temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)
+        keys_out = torch.empty_like(key)
+        order = torch.empty_like(key)
+        native.call("fmlx_sort_pairs", native.ptr(key), native.ptr(keys_out), native.ptr(iota), native.ptr(order), m,
+                    bits, native.ptr(temp), tb, stream)
+        del key, iota, temp
+        native.call("fmlx_csc_fill", int(values.dtype == torch.float64), native.ptr(order), m, j0, native.ptr(rel),
+                    native.ptr(values), native.ptr(self.erow), native.ptr(self.evals), stream)
+        native.call("fmlx_csc_colptr", native.ptr(keys_out), m, slots, d, native.ptr(indptr), b0, self.B, self.n, j0,
+                    native.ptr(self.colptr), stream)
+
+    def _transpose_torch(self, b0, slots, r0, r1, j0, j1) -> None:
+        indptr, indices, values = self._src
+        dev = values.device
+        d, B = self.d, self.B
+        lens = indptr[r0 + 1:r1 + 1] - indptr[r0:r1]
+        rows = torch.arange(r0, r1, device=dev, dtype=torch.int64)
+        slot = torch.div(rows - r0, B, rounding_mode="floor")
+        rel = (rows - r0 - slot * B).to(torch.int32)  # batch-relative row id
+        ent_slot = torch.repeat_interleave(slot.to(torch.int32), lens, output_size=j1 - j0)
+        key = ent_slot * d + indices[j0:j1]
+        order, starts = _stable_order(key, slots * d)
+        self.erow[j0:j1] = torch.repeat_interleave(rel, lens, output_size=j1 - j0)[order]
+        self.evals[j0:j1] = values[j0:j1][order]
+        # batch s of the run starts at starts[s·d]; its column c at starts[s·d + c]
+        S = starts[:-1].view(slots, d)
+        self.colptr[b0:b0 + slots, :d] = S - S[:, :1]
+        self.colptr[b0:b0 + slots, d] = starts[d::d] - S[:, 0]
 
     def ensure_rounds(self, first_epoch: int, k: int) -> None:
         """Transposes the batches of rounds first_epoch … first_epoch + k − 1."""
@@ -368,8 +428,6 @@ def _stable_order(key: torch.Tensor, bound: int):
         starts = torch.zeros(bound + 1, dtype=torch.int32, device=key.device)
         starts[1:] = torch.cumsum(torch.bincount(key.long(), minlength=bound), 0).to(torch.int32)
         return order, starts
-    from . import kmeans as _kk  # registers the sort signatures
-
     lib = native.kernels()
     bits = max(1, int(bound - 1).bit_length())
     tb = int(lib.fmlx_sort_pairs_temp_bytes(m, bits))
@@ -384,7 +442,6 @@ def _stable_order(key: torch.Tensor, bound: int):
     starts = torch.empty(bound + 1, dtype=torch.int32, device=key.device)
     native.call("fmlx_sorted_bounds", native.ptr(keys_out), m, int(bound), native.ptr(starts),
                 native.stream_ptr(key.device))
-    del _kk
     return order.long(), starts
 
 
@@ -399,6 +456,8 @@ def set_csc_tuning(fwd_cap: int = 0, bwd_cap: int = 0) -> None:
 
 def csc_round(csc: BatchCsc, indptr, idx, val, y, wt, coef, n, d, B, loss, state, mult, wl, fb, fuse: bool,
               max_iter, tol, lr, reg, en) -> None:
+    if csc.cap == 0:
+        raise RuntimeError("BatchCsc.ensure must run before the first round")
     native.call("fmlx_glm_csc_round", int(val.dtype == torch.float64), csc.G, native.ptr(indptr), native.ptr(idx),
                 native.ptr(val), native.ptr(y), native.ptr(wt), native.ptr(coef), n, d, B, loss, native.ptr(state),
                 native.ptr(mult), native.ptr(wl), native.ptr(csc.colptr), native.ptr(csc.erow), native.ptr(csc.evals),

@@ -81,6 +81,15 @@ _KERNEL_SIGS = {
     "fmlx_glm_csc_round": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int,
                            c_long, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                            c_int, c_double, c_double, c_double, c_double, c_void_p],
+    # sort.hip
+    "fmlx_sort_pairs_temp_bytes": ([c_long, c_int], c_long),
+    "fmlx_sort_pairs": [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_long, c_void_p],
+    "fmlx_sorted_bounds": [c_void_p, c_long, c_int, c_void_p, c_void_p],
+    # csc_build.hip
+    "fmlx_csc_keys": [c_void_p, c_void_p, c_long, c_long, c_long, c_int, c_long, c_void_p, c_void_p, c_void_p,
+                      c_void_p],
+    "fmlx_csc_fill": [c_int, c_void_p, c_long, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "fmlx_csc_colptr": [c_void_p, c_long, c_int, c_int, c_void_p, c_long, c_long, c_long, c_long, c_void_p, c_void_p],
 }
 
 _HOST_SIGS = {}

@@ -45,9 +45,18 @@ def _timed(ctx, fn):
     ctx.barrier()
     torch.cuda.synchronize()
     prof = None
+    gc_log = []
     if os.environ.get("BENCH_PYPROFILE"):  # host-side profile of the timed body only (diagnostics)
         import cProfile
+        import gc
 
+        def on_gc(phase, info, _t=[0.0]):
+            if phase == "start":
+                _t[0] = time.perf_counter()
+            else:
+                gc_log.append((info["generation"], time.perf_counter() - _t[0]))
+
+        gc.callbacks.append(on_gc)
         prof = cProfile.Profile()
         prof.enable()
     t0 = time.perf_counter()
@@ -57,6 +66,10 @@ def _timed(ctx, fn):
         import pstats
 
         prof.disable()
+        import gc
+
+        gc.callbacks.pop()
+        print("gc collections in the timed body: %s" % [(g, round(t * 1e3, 3)) for g, t in gc_log], file=sys.stderr)
         pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(30)
     ctx.barrier()
     torch.cuda.synchronize()

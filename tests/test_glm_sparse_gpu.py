@@ -114,10 +114,12 @@ def test_sparse_sgd_two_ranks_one_gpu():
     assert res[0][1] == res[1][1]  # replicas identical
 
 
-@pytest.mark.parametrize("run_max", [1, 3, 16])
-def test_batch_csc_device_transpose_matches_host(run_max, monkeypatch):
-    """Per-batch column-major copies built on the device (bit-limited radix sort + bucket-start
-    kernel, runs of consecutive batches in one sort) equal the host construction exactly."""
+@pytest.mark.parametrize("run_max,vdtype", [(1, torch.float32), (3, torch.float64), (16, torch.float32)])
+def test_batch_csc_device_transpose_matches_host(run_max, vdtype, monkeypatch):
+    """Per-batch column-major copies built on the device (csc_build.hip keys → bit-limited radix
+    sort → fill + column pointers straight from the sorted keys, runs of consecutive batches in
+    one sort) equal the host construction exactly — also after the storage, first sized for the
+    leading batches of a short fit, grows to the whole partition (pointers move: ``version``)."""
     _need_gpu()
     from flink_ml_amd.ops import glm as gk
 
@@ -125,12 +127,16 @@ def test_batch_csc_device_transpose_matches_host(run_max, monkeypatch):
     g = torch.Generator().manual_seed(0)
     n, d, B = 20_037, 3_001, 1_000
     lens = torch.randint(0, 12, (n,), generator=g)
+    lens[3 * B:4 * B] = 0  # an empty batch
     indptr = torch.zeros(n + 1, dtype=torch.int64)
     indptr[1:] = torch.cumsum(lens, 0)
     idx = torch.cat([torch.sort(torch.randperm(d, generator=g)[:int(k)]).values for k in lens]).to(torch.int32)
-    vals = torch.rand(int(indptr[-1]), generator=g, dtype=torch.float32)
-    dev = gk.BatchCsc.alloc(indptr.cuda(), idx.cuda(), vals.cuda(), n, d, B)
+    vals = torch.rand(int(indptr[-1]), generator=g, dtype=torch.float64).to(vdtype)
+    dev = gk.BatchCsc.alloc(indptr.cuda(), idx.cuda(), vals.cuda(), n, d, B, max_rounds=5)
+    dev.ensure([0, 1, 2, 3, 4])
+    assert dev.cap == 5 and dev.version == 0 and dev.erow.numel() == int(indptr[5 * B])
     dev.ensure([0, 1, 2, 7, 8, 12, 19, 20])
+    assert dev.cap == dev.P and dev.version == 1
     dev.ensure(range(dev.P))
     host = gk.BatchCsc.alloc(indptr, idx, vals, n, d, B)
     host.ensure(range(host.P))
