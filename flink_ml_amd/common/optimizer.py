@@ -197,7 +197,7 @@ class DeviceGlmTrainer:
             self.coef = (c0.pin_memory() if dev.type == "cuda" else c0).to(dev, non_blocking=True).contiguous()
         self.B = local_batch_size(sgd.global_batch_size, ctx.rank, ctx.world_size)
         self.state = torch.zeros(8, dtype=torch.int32, device=dev)
-        self.state[1] = 1  # running[0]
+        self.state[1:2].fill_(1)  # running[0] (a fill kernel: `t[i] = scalar` is a blocking pageable copy)
         self.feedback = torch.zeros(self.d + 2, dtype=acc, device=dev)
         self.distributed = ctx.is_distributed
         self.xg = None

@@ -462,7 +462,7 @@ class FtrlTrainer:
             key = (nparts, kacc)
             if key not in self._scratch:
                 state = torch.zeros(8, dtype=torch.int32, device=self.dev)
-                state[1:3] = 1  # running; the feedback-only tail never advances it
+                state[1:3].fill_(1)  # running; the feedback-only tail never advances it
                 self._scratch[key] = (gk.RoundScratch(nparts, d, kacc, self.dev), state)
             scratch, state = self._scratch[key]
             # one launch: local gradient + reduction → P[0:d+2] = [Σ mult·x | rows | 0]
@@ -474,8 +474,8 @@ class FtrlTrainer:
         Xf = X.to(self.acc)
         mult = torch.sigmoid(Xf @ self.coef) - y
         P[:d] = mult @ Xf
-        P[d] = float(n)
-        P[2 * d] = 1
+        P[d:d + 1].fill_(float(n))
+        P[2 * d:2 * d + 1].fill_(1)
         return 0
 
     def local_gradient(self, batch: Table) -> torch.Tensor:
@@ -810,7 +810,7 @@ class OnlineKMeansTrainer:
             nz, counts, torch.ones_like(counts)))[:, None], self.C)
         M[: kc * D] = (C * W[:, None]).reshape(-1)
         M[kc * D: kc * D + kc] = W
-        M[-1] = 1
+        M[-1:].fill_(1)  # a fill kernel: a scalar setitem would wait for the queued rounds
 
     def launch(self, batch: Optional[Table], world: int, snapshot_state: bool = False) -> "_Round":
         kc, D = self.C.shape

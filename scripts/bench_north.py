@@ -59,9 +59,38 @@ def _timed(ctx, fn):
         gc.callbacks.append(on_gc)
         prof = cProfile.Profile()
         prof.enable()
+    lines = {}
+    if os.environ.get("BENCH_LINETRACE"):  # per-line host time of the trainer constructor (diagnostics)
+        from flink_ml_amd.common.optimizer import DeviceGlmTrainer
+
+        code = DeviceGlmTrainer.__init__.__code__
+        last = [None, 0.0]
+
+        def tracer(frame, event, arg):
+            if frame.f_code is not code:
+                return None
+
+            sync = os.environ.get("BENCH_LINETRACE") == "sync"  # charge each line its GPU work too
+
+            def local(frame, event, arg):
+                if sync:
+                    torch.cuda.synchronize()
+                now = time.perf_counter()
+                if last[0] is not None:
+                    lines[last[0]] = lines.get(last[0], 0.0) + now - last[1]
+                last[0] = frame.f_lineno if event == "line" else None
+                last[1] = time.perf_counter()
+                return local
+            return local
+
+        sys.settrace(tracer)
     t0 = time.perf_counter()
     out = fn()
     torch.cuda.synchronize()
+    if lines or os.environ.get("BENCH_LINETRACE"):
+        sys.settrace(None)
+        print("constructor lines (ms): %s" % [(ln, round(t * 1e3, 3)) for ln, t in
+                                             sorted(lines.items(), key=lambda kv: -kv[1])[:8]], file=sys.stderr)
     if prof is not None:
         import pstats
 
