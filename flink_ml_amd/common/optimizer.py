@@ -491,6 +491,10 @@ class DeviceGlmTrainer:
         # (~1 ms per graph) would cost more than the launches it saves
         if not self.graphs and self.sgd.max_iter < 2 * self.rounds_per_graph:
             self._short = True
+        if self.csc is not None:
+            # every batch this fit visits in one go: one sort per run of up to CSC_RUN_MAX batches
+            # instead of one per check interval
+            self._ensure_csc(self._launched, self.sgd.max_iter - done)
         log = tracing.rounds_enabled()
         # per-round logs (a diagnostic mode) read every round's own feedback: one round per host
         # step; otherwise check-interval (or checkpoint-interval) rounds per host step

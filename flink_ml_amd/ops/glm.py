@@ -371,23 +371,40 @@ class BatchCsc:
         dev = values.device
         m, d = j1 - j0, self.d
         stream = native.stream_ptr(dev)
-        key = torch.empty(m, dtype=torch.int32, device=dev)
-        rel = torch.empty(m, dtype=torch.int32, device=dev)
-        iota = torch.empty(m, dtype=torch.int32, device=dev)
-        native.call("fmlx_csc_keys", native.ptr(indptr), native.ptr(indices), r0, r1, self.B, d, j0, native.ptr(key),
-                    native.ptr(rel), native.ptr(iota), stream)
+        lib = native.kernels()
         bits = max(1, int(slots * d - 1).bit_length())
-        tb = int(native.kernels().fmlx_sort_pairs_temp_bytes(m, bits))
-        if tb < 0:
-            raise RuntimeError("radix sort temp-size query failed")
-        temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)
+        key = torch.empty(m, dtype=torch.int32, device=dev)
         keys_out = torch.empty_like(key)
-        order = torch.empty_like(key)
-        native.call("fmlx_sort_pairs", native.ptr(key), native.ptr(keys_out), native.ptr(iota), native.ptr(order), m,
-                    bits, native.ptr(temp), tb, stream)
-        del key, iota, temp
-        native.call("fmlx_csc_fill", int(values.dtype == torch.float64), native.ptr(order), m, j0, native.ptr(rel),
-                    native.ptr(values), native.ptr(self.erow), native.ptr(self.evals), stream)
+        if values.dtype == torch.float32:
+            # (value bits, row) as one 64-bit payload through the sort, then a sequential split
+            pay = torch.empty(m, dtype=torch.int64, device=dev)
+            native.call("fmlx_csc_keys64", native.ptr(indptr), native.ptr(indices), native.ptr(values), r0, r1, self.B,
+                        d, j0, native.ptr(key), native.ptr(pay), stream)
+            tb = int(lib.fmlx_sort_pairs64_temp_bytes(m, bits))
+            if tb < 0:
+                raise RuntimeError("radix sort temp-size query failed")
+            temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)
+            pay_out = torch.empty_like(pay)
+            native.call("fmlx_sort_pairs64", native.ptr(key), native.ptr(keys_out), native.ptr(pay), native.ptr(pay_out),
+                        m, bits, native.ptr(temp), tb, stream)
+            del key, pay, temp
+            native.call("fmlx_csc_unpack", native.ptr(pay_out), m, j0, native.ptr(self.erow), native.ptr(self.evals),
+                        stream)
+        else:
+            rel = torch.empty(m, dtype=torch.int32, device=dev)
+            iota = torch.empty(m, dtype=torch.int32, device=dev)
+            native.call("fmlx_csc_keys", native.ptr(indptr), native.ptr(indices), r0, r1, self.B, d, j0,
+                        native.ptr(key), native.ptr(rel), native.ptr(iota), stream)
+            tb = int(lib.fmlx_sort_pairs_temp_bytes(m, bits))
+            if tb < 0:
+                raise RuntimeError("radix sort temp-size query failed")
+            temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)
+            order = torch.empty_like(key)
+            native.call("fmlx_sort_pairs", native.ptr(key), native.ptr(keys_out), native.ptr(iota), native.ptr(order),
+                        m, bits, native.ptr(temp), tb, stream)
+            del key, iota, temp
+            native.call("fmlx_csc_fill", 1, native.ptr(order), m, j0, native.ptr(rel), native.ptr(values),
+                        native.ptr(self.erow), native.ptr(self.evals), stream)
         native.call("fmlx_csc_colptr", native.ptr(keys_out), m, slots, d, native.ptr(indptr), b0, self.B, self.n, j0,
                     native.ptr(self.colptr), stream)
 

@@ -85,7 +85,12 @@ _KERNEL_SIGS = {
     "fmlx_sort_pairs_temp_bytes": ([c_long, c_int], c_long),
     "fmlx_sort_pairs": [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_long, c_void_p],
     "fmlx_sorted_bounds": [c_void_p, c_long, c_int, c_void_p, c_void_p],
+    "fmlx_sort_pairs64_temp_bytes": ([c_long, c_int], c_long),
+    "fmlx_sort_pairs64": [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_long, c_void_p],
     # csc_build.hip
+    "fmlx_csc_keys64": [c_void_p, c_void_p, c_void_p, c_long, c_long, c_long, c_int, c_long, c_void_p, c_void_p,
+                        c_void_p],
+    "fmlx_csc_unpack": [c_void_p, c_long, c_long, c_void_p, c_void_p, c_void_p],
     "fmlx_csc_keys": [c_void_p, c_void_p, c_long, c_long, c_long, c_int, c_long, c_void_p, c_void_p, c_void_p,
                       c_void_p],
     "fmlx_csc_fill": [c_int, c_void_p, c_long, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
