@@ -99,6 +99,24 @@ def set_l2acc(on: bool) -> None:
     native.call("fmlx_glm_set_l2acc", int(bool(on)))
 
 
+# deferred fused rounds: tail prefetch of the next round's rows (FMLX_GLM_PF = rows per wave,
+# FMLX_GLM_PF_STOP = fraction of finished waves after which prefetching stops)
+PF_ROWS = int(os.environ.get("FMLX_GLM_PF", "0"))
+PF_STOP = float(os.environ.get("FMLX_GLM_PF_STOP", "0.9"))
+_pf_set = False
+
+
+def set_prefetch(rows: int, stop_frac: float = PF_STOP) -> None:
+    """A/B knob of the deferred fused round: after its gradient is issued, a wave among the first
+    ``stop_frac`` of the launch's waves to finish reads up to ``rows`` of the rows it will own in the
+    next round (cache warm-up of the XCD's L2 / Infinity Cache while the stragglers finish)."""
+    q = max(1, min(256, int(round(float(stop_frac) * 256))))
+    global _pf_set
+    if native.kernels().fmlx_glm_set_prefetch(int(rows), q) != 0:
+        raise ValueError("rows must be in [0, 64]")
+    _pf_set = True
+
+
 def set_rowmap(m: int) -> None:
     """A/B knob of the static row schedule's block → row-stripe mapping (csrc/glm.hip ROWMAP_*):
     0 = consecutive wave slots per block, 1 = one contiguous 1/8 of every stripe per XCD,
@@ -183,6 +201,8 @@ class RoundScratch:
             set_dyn(DYN_DEFAULT)
         if not _pairs_set:
             set_pairs(PAIRS_DEFAULT, PAIR_STATIC)
+        if not _pf_set:
+            set_prefetch(PF_ROWS, PF_STOP)
         self.nparts = nparts
         self.det = DETERMINISTIC if det is None else bool(det)
         if self.det:

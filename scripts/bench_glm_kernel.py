@@ -80,6 +80,7 @@ def main():
             gk.set_rowmap(c.get("rm", 0))
             gk.set_l2acc(bool(c.get("l2", 0)))
             gk.set_pairs(bool(c.get("pairs", 0)), c.get("q", 205) / 256.0)
+            gk.set_prefetch(c.get("pf", 0), c.get("ps", 230) / 256.0)
             sgd = SGD(max_iter=10 ** 8, learning_rate=0.1, global_batch_size=a.batch, tol=0.0)
             cls = SplitTrainer if (c.get("split") or c.get("m0")) else DeviceGlmTrainer
             tr = cls(sgd, np.zeros(a.dim), X, y, None, "logistic", use_graph=True)

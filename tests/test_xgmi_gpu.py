@@ -438,3 +438,39 @@ def test_l2_replica_tail_matches_torch(l2acc, monkeypatch):
             assert float(tr.feedback[d].item()) == float(wt[b0:b0 + B].sum())
     finally:
         gk.set_l2acc(False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pf", [0, 8])
+def test_tail_prefetch_matches_torch(pf, monkeypatch):
+    """Deferred rounds with the next-round tail prefetch (a cache hint only) against the fp64
+    torch reference, plus the exact per-round weight census through integer weights."""
+    _need_gpu()
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
+    from flink_ml_amd.ops import glm as gk
+
+    monkeypatch.setattr(gk, "DEFER", True)
+    monkeypatch.setattr(gk, "DETERMINISTIC", False)
+    gk.set_prefetch(pf, 0.9)
+    try:
+        g = torch.Generator(device="cpu").manual_seed(17)
+        n, d, B = 300_000, 1000, 100_000
+        Xb = torch.rand((n, d), generator=g).to(torch.bfloat16)
+        y = torch.randint(0, 2, (n,), generator=g).to(torch.float64)
+        sgd = SGD(max_iter=7, learning_rate=0.1, global_batch_size=B, tol=0.0)
+        ref = TorchGlmTrainer(sgd, np.zeros(d), Xb.to(torch.float64), y, None, "logistic").fit()
+        tr = DeviceGlmTrainer(sgd, np.zeros(d), Xb.cuda(), y.cuda(), None, "logistic", use_graph=True)
+        got = tr.fit()
+        assert tr.rounds_executed() == 7
+        assert np.allclose(got, ref, rtol=2e-4, atol=2e-6), np.abs(got - ref).max()
+        wt = (torch.arange(n) % 7 + 1).to(torch.float32)
+        tr = DeviceGlmTrainer(SGD(max_iter=6, learning_rate=0.1, global_batch_size=B, tol=0.0), np.zeros(d),
+                              Xb.cuda(), y.float().cuda(), wt.cuda(), "logistic", use_graph=False)
+        tr._launch_round(1)
+        for e in range(4):
+            tr._launch_round(1)
+            torch.cuda.synchronize()
+            b0 = (e % 3) * B
+            assert float(tr.feedback[d].item()) == float(wt[b0:b0 + B].sum())
+    finally:
+        gk.set_prefetch(0)
