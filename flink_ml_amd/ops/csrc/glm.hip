@@ -157,7 +157,7 @@ struct GlmTail {
   int pair_nh;     // pair heads (counters) in use, <= PAIR_NH_MAX
   int l2acc;       // deferred flat tail: per-XCD replicas accumulated in the XCD's L2
   int pf;          // deferred static schedule: next-round rows each wave prefetches in the tail
-  int pf_stop;     // ... while fewer than pf_stop/256 of the launch's waves are done
+  int pf_stop;     // ... if the wave is done within pf_stop s_memrealtime ticks of its block's start
   int* pf_sink;    // always null: keeps the prefetch loads alive (never written)
 };
 // Static row schedule: wave slot gw of the W = NB·WPB slots reads rows start + gw + j·W.
@@ -185,16 +185,14 @@ constexpr int PAIR_NH_MAX = 64;
 constexpr int PAIR_STRIDE = 32;  // ints between counters (128 B)
 constexpr int PAIR_OFF = 2 * 8 * 32;  // after the DynLds schedule's counters in tl.heads
 constexpr int ACC_MAX_REPS = 8;
-// Tail prefetch (deferred 1-GPU rounds, static schedule). A round's blocks finish their rows over
-// a ≈4–6 µs window (median 33.5, slowest 37.7 µs) during which HBM runs below its streaming rate
-// while the stragglers finish. A wave that is done counts itself on its launch's counter, then —
-// until every wave of the launch is counted, at most tl.pf rows — reads the first rows it will own
-// in the NEXT round (one dword per 64 B, two rows per wave-instruction), so that round finds them
-// in its XCD's L2 (kernel boundaries do not evict L2) or in the Infinity Cache. Pure cache hint:
-// no result depends on it. Counters of parity p are zeroed by block 0 of the launches of parity
-// 1 − p, as the pair counters are; a stale counter only switches the prefetch off.
-constexpr int PF_OFF = PAIR_OFF + 2 * PAIR_NH_MAX * PAIR_STRIDE;
-constexpr int PF_STRIDE = 32;
+// Tail prefetch (deferred 1-GPU rounds, static schedule; A/B knob). A round's blocks finish their
+// rows over a ≈4–6 µs window (median 33.5, slowest 37.7 µs) during which HBM runs below its
+// streaming rate while the stragglers finish. A wave done before tl.pf_stop ticks (100 MHz) of its
+// block's start reads the first tl.pf (≤ PF_MAX) rows it will own in the NEXT round (one dword
+// per 64 B, two rows per wave-instruction), so that round finds them in its XCD's L2 or in the
+// Infinity Cache. Pure cache hint: no result depends on it. (A first version stopped on a shared
+// count of finished waves: 4096 returning atomics on one address serialise, 109–128 µs rounds.)
+constexpr int PF_MAX = 8;
 
 // ------------------------------------------------------------------------------------------
 // Dynamic row schedule (work distribution of the fused round, deferred mode)
@@ -551,13 +549,11 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
     const typename AccOf<T>::type* wt, typename AccOf<T>::type* coef,
     long n, int d, long B, int loss, int* state, typename AccOf<T>::type* partials, GlmTail tl) {
   typedef typename AccOf<T>::type A;
-  const long long t_start = tl.trace ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
+  const long long t_start = (tl.trace || tl.pf) ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
   int e;
   if (tl.defer) {
     if (tl.pairs && blockIdx.x == 0 && threadIdx.x < tl.pair_nh)  // the next launch's counters
       st_agent(&tl.heads[PAIR_OFF + (tl.parity ^ 1) * (PAIR_NH_MAX * PAIR_STRIDE) + threadIdx.x * PAIR_STRIDE], 0);
-    if (tl.pf > 0 && blockIdx.x == 0 && threadIdx.x == 0)  // the next launch's prefetch counter
-      st_agent(&tl.heads[PF_OFF + (tl.parity ^ 1) * PF_STRIDE], 0);
     if (state[ST_DONE]) return;
     e = state[tl.parity ? ST_ROUND_ALT : ST_ROUND];
   } else if (!round_running(state, e)) return;
@@ -1280,31 +1276,28 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
     }
     if constexpr (G == 0) {
       if (tl.pf > 0) {
-        // tail prefetch (see PF_OFF): this block's gradient is on its way; a wave among the first
-        // `pf_stop` of the launch to get here reads its next-round rows until that many waves have
-        int* pc = tl.heads + PF_OFF + tl.parity * PF_STRIDE;
-        const int total = (int)W;
-        const int stop_at = (int)(((long)total * tl.pf_stop) >> 8);
-        int tk = 0;
-        if (lane == 0) tk = __hip_atomic_fetch_add(pc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        tk = __builtin_amdgcn_readfirstlane(tk);
-        if (tk + 1 < stop_at && e + 1 < tl.max_iter && n > 0 && B > 0) {
+        // tail prefetch (see PF_MAX): this block's gradient is on its way; a wave done before
+        // pf_stop ticks of its block's start reads its first pf rows of the next round (one
+        // decision per wave, loads issued back to back, one wait)
+        const long long now = (long long)__builtin_amdgcn_s_memrealtime();
+        if (now - t_start < (long long)tl.pf_stop && e + 1 < tl.max_iter && n > 0 && B > 0) {
           const unsigned P1 = tl.nbatch > 0 ? (unsigned)tl.nbatch : (unsigned)((n + B - 1) / B);
           const long s1 = (long)((unsigned)(e + 1) % P1) * B;
           const long e1 = s1 + B < n ? s1 + B : n;
           const int rowb = d * (int)sizeof(T);
-          uint32_t sink = 0;
-          int seen = tk + 1;
-          for (int j = 0; j < tl.pf && seen < stop_at; j += 2) {
-            const long rr = s1 + gw + (long)(j + (lane >> 5)) * W;
-            uint32_t v = 0;
-            if (rr < e1) {
+          uint32_t v[PF_MAX / 2];
+#pragma unroll
+          for (int q = 0; q < PF_MAX / 2; ++q) {
+            v[q] = 0;
+            const long rr = s1 + gw + (long)(2 * q + (lane >> 5)) * W;
+            if (2 * q < tl.pf && rr < e1) {
               const char* rp = reinterpret_cast<const char*>(X + rr * ld);
-              for (int off = (lane & 31) * 64; off < rowb; off += 32 * 64) v ^= *reinterpret_cast<const uint32_t*>(rp + off);
+              for (int off = (lane & 31) * 64; off < rowb; off += 32 * 64) v[q] ^= *reinterpret_cast<const uint32_t*>(rp + off);
             }
-            seen = __builtin_amdgcn_readfirstlane(__hip_atomic_load(pc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            sink ^= v;
           }
+          uint32_t sink = 0;
+#pragma unroll
+          for (int q = 0; q < PF_MAX / 2; ++q) sink ^= v[q];
           if (tl.pf_sink) tl.pf_sink[threadIdx.x] = (int)sink;  // never taken: pf_sink is null
         }
       }
@@ -1821,7 +1814,7 @@ static int g_pairs = 0;      // pair schedule (A/B knob)
 static int g_pair_q = 205;   // static fraction of the batch, 1/256 units
 static int g_l2acc = 0;      // deferred flat tail: per-XCD L2 replicas (A/B knob)
 static int g_pf = 0;         // deferred static schedule: tail prefetch rows per wave (A/B knob)
-static int g_pf_stop = 230;  // ... until this many /256 of the launch's waves are done
+static int g_pf_stop = 3400; // ... by waves done within this many 10-ns ticks of their block's start
 constexpr long LDS_PER_CU = 160 * 1024;
 constexpr int NUM_CU = 256;
 
@@ -1863,7 +1856,7 @@ int launch_grad_u(const void* X, long ld, const void* y, const void* wt, void* c
     t2.dyn_off = (int)((shmem + 15) & ~(size_t)15);
     shmem = (size_t)t2.dyn_off + sizeof(DynLds);
   }
-  t2.pf = (g_pf > 0 && G == 0 && t2.defer && !tl.det && tl.heads != nullptr && !t2.pairs && !t2.dyn) ? g_pf : 0;
+  t2.pf = (g_pf > 0 && G == 0 && t2.defer && !tl.det && !t2.pairs && !t2.dyn) ? g_pf : 0;
   t2.pf_stop = g_pf_stop;
   t2.pf_sink = nullptr;
   if constexpr (G > 0) {
@@ -2006,12 +1999,12 @@ FMLX_API void fmlx_glm_set_dyn_debug2(void* dbg2) { g_dyn_dbg2 = (int*)dbg2; }
 
 // ints of the fused round's counter block: tickets (TAIL_TOP + 1, padded to 128) + the dynamic
 // schedule's [2][DYN_HEADS][DYN_HSTRIDE] chunk counters
-FMLX_API int fmlx_glm_cnt_elems() { return 128 + PF_OFF + 2 * PF_STRIDE; }
+FMLX_API int fmlx_glm_cnt_elems() { return 128 + PAIR_OFF + 2 * PAIR_NH_MAX * PAIR_STRIDE; }
 
-// tail prefetch of the deferred fused round (see PF_OFF): rows per wave (0 = off) and the
-// fraction (1/256 units) of the launch's waves after which no wave starts or continues one
+// tail prefetch of the deferred fused round (see PF_MAX): rows per wave (0 = off) and the
+// s_memrealtime ticks (10 ns) after a block's start past which its waves skip it
 FMLX_API int fmlx_glm_set_prefetch(int rows, int stop_q) {
-  if (rows < 0 || rows > 64 || stop_q < 1 || stop_q > 256) return -1;
+  if (rows < 0 || rows > PF_MAX || stop_q < 1) return -1;
   g_pf = rows;
   g_pf_stop = stop_q;
   return 0;

@@ -99,21 +99,21 @@ def set_l2acc(on: bool) -> None:
     native.call("fmlx_glm_set_l2acc", int(bool(on)))
 
 
-# deferred fused rounds: tail prefetch of the next round's rows (FMLX_GLM_PF = rows per wave,
-# FMLX_GLM_PF_STOP = fraction of finished waves after which prefetching stops)
+# deferred fused rounds: tail prefetch of the next round's rows (csrc/glm.hip PF_MAX).
+# FMLX_GLM_PF = rows per wave (0 = off), FMLX_GLM_PF_STOP_US = only waves done within this many
+# microseconds of their block's start prefetch.
 PF_ROWS = int(os.environ.get("FMLX_GLM_PF", "0"))
-PF_STOP = float(os.environ.get("FMLX_GLM_PF_STOP", "0.9"))
+PF_STOP_US = float(os.environ.get("FMLX_GLM_PF_STOP_US", "34"))
 _pf_set = False
 
 
-def set_prefetch(rows: int, stop_frac: float = PF_STOP) -> None:
-    """A/B knob of the deferred fused round: after its gradient is issued, a wave among the first
-    ``stop_frac`` of the launch's waves to finish reads up to ``rows`` of the rows it will own in the
-    next round (cache warm-up of the XCD's L2 / Infinity Cache while the stragglers finish)."""
-    q = max(1, min(256, int(round(float(stop_frac) * 256))))
+def set_prefetch(rows: int, stop_us: float = PF_STOP_US) -> None:
+    """A/B knob of the deferred fused round: after its gradient is issued, a wave done within
+    ``stop_us`` of its block's start reads the first ``rows`` (<= 8) rows it will own in the next
+    round (cache warm-up of the XCD's L2 / Infinity Cache while the stragglers finish)."""
     global _pf_set
-    if native.kernels().fmlx_glm_set_prefetch(int(rows), q) != 0:
-        raise ValueError("rows must be in [0, 64]")
+    if native.kernels().fmlx_glm_set_prefetch(int(rows), max(1, int(round(float(stop_us) * 100)))) != 0:
+        raise ValueError("rows must be in [0, 8]")
     _pf_set = True
 
 
@@ -202,7 +202,7 @@ class RoundScratch:
         if not _pairs_set:
             set_pairs(PAIRS_DEFAULT, PAIR_STATIC)
         if not _pf_set:
-            set_prefetch(PF_ROWS, PF_STOP)
+            set_prefetch(PF_ROWS, PF_STOP_US)
         self.nparts = nparts
         self.det = DETERMINISTIC if det is None else bool(det)
         if self.det:

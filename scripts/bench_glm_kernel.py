@@ -57,11 +57,13 @@ def main():
     ap.add_argument("--batch", type=int, default=100_000)
     ap.add_argument("--rounds", type=int, default=200)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--ld", type=int, default=0, help="row pitch in elements (0: dense rows)")
     ap.add_argument("--configs", default="u=2,b=512;u=1,b=512;u=4,b=512;u=2,b=256;u=4,b=256;split=1")
     a = ap.parse_args()
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(1)
-    X = torch.empty((a.rows, a.dim), dtype=torch.bfloat16, device=dev)
+    ld = a.ld if a.ld > 0 else a.dim
+    X = torch.empty((a.rows, ld), dtype=torch.bfloat16, device=dev)[:, :a.dim]
     for s in range(0, a.rows, 1 << 20):
         e = min(s + (1 << 20), a.rows)
         X[s:e] = torch.rand((e - s, a.dim), generator=g, device=dev).to(torch.bfloat16)
@@ -80,7 +82,7 @@ def main():
             gk.set_rowmap(c.get("rm", 0))
             gk.set_l2acc(bool(c.get("l2", 0)))
             gk.set_pairs(bool(c.get("pairs", 0)), c.get("q", 205) / 256.0)
-            gk.set_prefetch(c.get("pf", 0), c.get("ps", 230) / 256.0)
+            gk.set_prefetch(c.get("pf", 0), c.get("ps", 34))
             sgd = SGD(max_iter=10 ** 8, learning_rate=0.1, global_batch_size=a.batch, tol=0.0)
             cls = SplitTrainer if (c.get("split") or c.get("m0")) else DeviceGlmTrainer
             tr = cls(sgd, np.zeros(a.dim), X, y, None, "logistic", use_graph=True)
@@ -101,7 +103,7 @@ def main():
     gb = a.batch * a.dim * 2 / 1e9
     for k, v in res.items():
         med = statistics.median(v)
-        print(json.dumps({"config": json.loads(k), "us_per_round_median": round(med, 2),
+        print(json.dumps({"config": json.loads(k), "ld": ld, "us_per_round_median": round(med, 2),
                           "us_min": round(min(v), 2), "samples_per_s": round(a.batch / med * 1e6),
                           "batch_TB_per_s": round(gb / med * 1e6 / 1e3, 3)}), flush=True)
 

@@ -451,7 +451,7 @@ def test_tail_prefetch_matches_torch(pf, monkeypatch):
 
     monkeypatch.setattr(gk, "DEFER", True)
     monkeypatch.setattr(gk, "DETERMINISTIC", False)
-    gk.set_prefetch(pf, 0.9)
+    gk.set_prefetch(pf, 1e6)  # every wave prefetches
     try:
         g = torch.Generator(device="cpu").manual_seed(17)
         n, d, B = 300_000, 1000, 100_000
