@@ -1019,6 +1019,19 @@ int launch_assign_bf16(const void* X, long ld, long n, int D, const void* Cb, co
       return (int)hipGetLastError();
     }
   }
+  if constexpr (KS == 8) {
+    if (full && g_km_pipe >= 3) {
+      // A/B: 8 waves per block (one block per CU) share each centroid tile's LDS-DMA
+      const int blocks8 = (int)((n + 8 * 32 * MT - 1) / (8 * 32 * MT));
+      if (g_km_pipe == 4)
+        hipLaunchKernelGGL((kmeans_assign_bf16_pipe_kernel<KS, true, 8>), dim3(blocks8), dim3(512), g_km_ldspad, s,
+                           (const bf16_t*)X, ld, n, (const bf16_t*)Cb, cnorm, kpad, labels);
+      else
+        hipLaunchKernelGGL((kmeans_assign_bf16_pipe_kernel<KS, false, 8>), dim3(blocks8), dim3(512), g_km_ldspad, s,
+                           (const bf16_t*)X, ld, n, (const bf16_t*)Cb, cnorm, kpad, labels);
+      return (int)hipGetLastError();
+    }
+  }
   if constexpr (KS == 4 || KS == 8) {
     if (full && g_km_pipe) {
       if (g_km_pipe == 2)
@@ -1078,7 +1091,7 @@ FMLX_API int fmlx_kmeans_set_ldspad(int bytes) {
 FMLX_API int fmlx_kmeans_set_sched(int mode) {
   g_km_sched = mode == 1;
   g_km_xlds = mode == 2;
-  g_km_pipe = mode == 3 ? 1 : mode == 4 ? 2 : 0;
+  g_km_pipe = mode == 3 ? 1 : mode == 4 ? 2 : mode == 5 ? 3 : mode == 6 ? 4 : 0;  // 5/6: 8-wave blocks
   return 0;
 }
 
