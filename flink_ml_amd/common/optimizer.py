@@ -222,7 +222,7 @@ class DeviceGlmTrainer:
             if self.w is None:
                 self.w = torch.ones(self.n, dtype=acc, device=dev)
         else:
-            self.nparts = max(1, min(gk.GRAD_BLOCKS, gk.max_round_blocks(), math.ceil(max(self.B, 1) / (gk.WPB * 16))))
+            self.nparts = max(1, min(gk.round_blocks(self.X), gk.max_round_blocks(), math.ceil(max(self.B, 1) / (gk.WPB * 16))))
             self.scratch = gk.RoundScratch(self.nparts, self.d, acc, dev)
             if self.distributed:
                 from ..parallel import xgmi

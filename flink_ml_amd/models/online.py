@@ -458,7 +458,7 @@ class FtrlTrainer:
             kacc = torch.float64 if Xk.dtype == torch.float64 else torch.float32
             if kacc != self.acc:
                 Xk, kacc = Xk.to(self.acc), self.acc
-            nparts = max(1, min(gk.GRAD_BLOCKS, gk.max_round_blocks(), math.ceil(n / (gk.WPB * 16))))
+            nparts = max(1, min(gk.round_blocks(Xk), gk.max_round_blocks(), math.ceil(n / (gk.WPB * 16))))
             key = (nparts, kacc)
             if key not in self._scratch:
                 state = torch.zeros(8, dtype=torch.int32, device=self.dev)

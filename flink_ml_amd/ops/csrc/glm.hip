@@ -1892,9 +1892,11 @@ int launch_grad(int u, const void* X, long ld, const void* y, const void* wt, vo
       return launch_grad_u<T, EPC, CPL, 1, 4>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
     }
   }
-  // default: 2 rows in flight per wave for narrow rows, 1 from 32 bytes per lane (flagship
-  // 1000 × bf16: U=1 37.9 µs vs U=2 39.1 µs per round, 256 blocks, measured)
-  if (u <= 0) u = BYTES <= 16 ? 2 : 1;
+  // default: 4 rows in flight per wave (U = 2) up to 32 bytes per lane, 2 above. Flagship
+  // 1000 × bf16 (32 bytes per lane) with the deferred tail, round 3: U=2 on 256 blocks 38.97 µs
+  // vs U=1 on 512 blocks 40.09 µs (ops/glm.py round_blocks picks the grid; round 1, before the
+  // deferred tail, had measured U=1 faster: 37.9 vs 39.1 µs)
+  if (u <= 0) u = BYTES <= 32 ? 2 : 1;
   if (u >= 4 && BYTES <= 32)
     return launch_grad_u<T, EPC, CPL, 4>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
   if (u >= 2 && BYTES <= 64)

@@ -25,7 +25,20 @@ GRAD_UNROLL = int(os.environ.get("FMLX_GLM_UNROLL", "0"))
 # round vs 43.4 (256), 43.5 (384), 48.4 (768), 48.2 (1024). Accumulator replicas 2/4/8 and one
 # contiguous run of rows per wave instead of the interleaved rows measured within 1-2 % (the
 # latter slower): scripts/bench_glm_kernel.py, round-2 log in profiles/r2/INDEX.md
-GRAD_BLOCKS = int(os.environ.get("FMLX_GLM_BLOCKS", "512"))
+# round 3: 0 = by shape (round_blocks). Rows of 32 bytes per lane (bf16 d 513-1024, the flagship
+# 1000) take 4 rows in flight per wave on 256 blocks: 38.97 vs 40.09 us per round for U=1 on 512
+# blocks, interleaved on one MI355X (profiles/r3/lr_unroll_grid_ab_1gpu_run*.jsonl)
+GRAD_BLOCKS = int(os.environ.get("FMLX_GLM_BLOCKS", "0"))
+
+
+def round_blocks(X) -> int:
+    """Grid of the fused round for rows ``X`` (FMLX_GLM_BLOCKS / GRAD_BLOCKS > 0 overrides)."""
+    if GRAD_BLOCKS > 0:
+        return GRAD_BLOCKS
+    lay = pick_layout(X) if X is not None else None
+    if lay is not None and GRAD_UNROLL == 0 and lay[0] * lay[1] * X.element_size() == 32:
+        return 256
+    return 512
 
 
 # rows streamed once per pass use non-temporal loads when the data set exceeds the 256 MiB

@@ -11,3 +11,11 @@ for cfg in "1 512" "2 256" "1 512" "2 256"; do
   FMLX_GLM_UNROLL=$1 FMLX_GLM_BLOCKS=$2 timeout -k 10 120 python -u bench.py --steps 20 --warmup 5 > $O/bench_u$1_b$2.log 2>&1 || { echo "bench failed"; tail -20 $O/bench_u$1_b$2.log; exit 1; }
   echo "u=$1 b=$2 $(tail -1 $O/bench_u$1_b$2.log | python -c 'import json,sys; r=json.loads(sys.stdin.read()); print(r["ms_per_step"], r["kernel_us_per_step"])')"
 done
+timeout -k 10 150 python -u __graft_entry__.py smoke > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 120 python -u bench.py --steps 20 --warmup 5 > $O/bench_default.log 2>&1 || { echo "bench failed"; tail -20 $O/bench_default.log; exit 1; }
+tail -1 $O/bench_default.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gputest.log 2>&1
+rc=$?
+tail -5 $O/gputest.log
+exit $rc
