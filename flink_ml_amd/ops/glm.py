@@ -26,8 +26,9 @@ GRAD_UNROLL = int(os.environ.get("FMLX_GLM_UNROLL", "0"))
 # contiguous run of rows per wave instead of the interleaved rows measured within 1-2 % (the
 # latter slower): scripts/bench_glm_kernel.py, round-2 log in profiles/r2/INDEX.md
 # round 3: 0 = by shape (round_blocks). Rows of 32 bytes per lane (bf16 d 513-1024, the flagship
-# 1000) take 4 rows in flight per wave on 256 blocks: 38.97 vs 40.09 us per round for U=1 on 512
-# blocks, interleaved on one MI355X (profiles/r3/lr_unroll_grid_ab_1gpu_run*.jsonl)
+# 1000) take 4 rows in flight per wave on 224 blocks (28 per XCD): 37.31 us per round vs 38.56 on
+# 256 blocks and 39.75 for U=1 on 512, interleaved on one MI355X (profiles/r3/lr_unroll_grid_*,
+# lr_unroll2_grid_*; bench.py 39.5 vs 40.8 us per step)
 GRAD_BLOCKS = int(os.environ.get("FMLX_GLM_BLOCKS", "0"))
 
 
@@ -37,7 +38,7 @@ def round_blocks(X) -> int:
         return GRAD_BLOCKS
     lay = pick_layout(X) if X is not None else None
     if lay is not None and GRAD_UNROLL == 0 and lay[0] * lay[1] * X.element_size() == 32:
-        return 256
+        return 224
     return 512
 
 
