@@ -66,14 +66,24 @@ def default_device(local_rank: int = 0) -> torch.device:
     return torch.device("cpu")
 
 
-def _free_port() -> int:
-    import socket
+def _rendezvous_store(world: int, forced: bool, timeout_s: int):
+    """The store the process group rendezvous on, or None for torch's env:// default.
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+    - FMLX_FORCE_PG at world 1: an in-process ``HashStore``; no socket is bound at all.
+    - ``FMLX_STORE=host:port``: a TCPStore some parent already hosts (``tests/spmd.py`` binds it
+      with port 0 and hands out the port it got); every rank connects as a client. This never
+      binds-then-closes a port, so two concurrent groups cannot race for the same number.
+    """
+    import datetime
+
+    if forced:
+        return dist.HashStore()
+    spec = os.environ.get("FMLX_STORE")
+    if spec:
+        host, port = spec.rsplit(":", 1)
+        return dist.TCPStore(host, int(port), world, is_master=False,
+                             timeout=datetime.timedelta(seconds=timeout_s))
+    return None
 
 
 def force_pg() -> bool:
@@ -101,11 +111,10 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> SPM
                 # FMLX_BACKEND=gloo: several ranks sharing one GPU (rehearsals of multi-GPU paths)
                 backend = os.environ.get("FMLX_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            if forced:
-                os.environ.setdefault("RANK", "0")
-                os.environ.setdefault("WORLD_SIZE", "1")
-                os.environ.setdefault("MASTER_PORT", str(_free_port()))
             kwargs = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+            store = _rendezvous_store(world, forced, timeout_s)
+            if store is not None:
+                kwargs.update(store=store, rank=rank, world_size=world)
             if backend == "nccl":
                 kwargs["device_id"] = device
             dist.init_process_group(**kwargs)

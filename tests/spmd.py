@@ -1,24 +1,18 @@
 """Multi-process SPMD test harness (the analogue of the reference's local MiniCluster with
 parallelism 4): spawns ``world`` CPU ranks over the gloo backend on 127.0.0.1 and returns
 each rank's result."""
+import datetime
 import os
-import socket
 import traceback
 
+import torch.distributed as dist
 import torch.multiprocessing as mp
-
-
-def _free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
 
 
 def _worker(rank, world, port, fn, args, q, env=None, backend="gloo"):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
-                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "FMLX_DEVICE": "cpu"})
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "FMLX_DEVICE": "cpu",
+                       "FMLX_STORE": "127.0.0.1:%d" % port})
     os.environ.update(env or {})
     try:
         import torch
@@ -40,7 +34,12 @@ def run_spmd(fn, world: int, *args, timeout: float = 180, env=None, backend="glo
     on a GPU)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    # The parent hosts the rendezvous store on a port the kernel assigns at bind time and keeps it
+    # bound until every rank is done; the ranks connect as clients (FMLX_STORE). Handing out a
+    # bind-then-closed "free" port instead races other groups for the number (GPUTEST_r03).
+    store = dist.TCPStore("127.0.0.1", 0, world, is_master=True, wait_for_workers=False,
+                          timeout=datetime.timedelta(seconds=timeout))
+    port = store.port
     procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, q, env, backend)) for r in range(world)]
     for p in procs:
         p.start()
@@ -56,4 +55,5 @@ def run_spmd(fn, world: int, *args, timeout: float = 180, env=None, backend="glo
             p.join(timeout=10)
             if p.is_alive():
                 p.kill()
+        del store
     return [results[r] for r in range(world)]
