@@ -263,16 +263,18 @@ class DeviceGlmTrainer:
         visits = sgd.max_iter / max(P, 1) if P else 0
         return visits >= CSC_BUILD_ROUNDS or sgd.max_iter >= CSC_MIN_ITERS
     # -- one round as a fixed launch sequence (capturable) -------------------------------------
-    def _launch_round(self, rounds: int = 1) -> None:
+    def _launch_round(self, rounds: int = 1, ensure: bool = True) -> None:
         """Launches ``rounds`` consecutive rounds (one host call on the fused dense path,
-        else ``rounds`` launch sequences)."""
+        else ``rounds`` launch sequences). ``ensure=False``: the caller already ensured the
+        column-major batches (the capture warm-up, whose ``_launched`` is already advanced past
+        the rounds it replays — ensuring there could regrow the storage mid-replay)."""
         if rounds > 1 and not (self.csc is None and not self.wide and not self.sparse and self.mode != gk.TAIL_FEEDBACK):
             for _ in range(rounds):
-                self._launch_round(1)
+                self._launch_round(1, ensure)
             return
         s = self.sgd
         if self.csc is not None:
-            if not torch.cuda.is_current_stream_capturing():
+            if ensure and not torch.cuda.is_current_stream_capturing():
                 self._ensure_csc(self._launched, 1)
             # forward (per-row multipliers) + atomic-free column-major backward; on 1 GPU the
             # backward applies the update and the termination check itself
@@ -362,7 +364,7 @@ class DeviceGlmTrainer:
         snapshot = [t.clone() for t in live]
         saved_parity = self.parity
         with torch.cuda.stream(side):
-            self._launch_round()  # warm-up outside capture (allocator / RCCL lazy init)
+            self._launch_round(ensure=False)  # warm-up outside capture (allocator / RCCL lazy init)
         torch.cuda.current_stream(self.device).wait_stream(side)
         for t, v in zip(live, snapshot):
             t.copy_(v)

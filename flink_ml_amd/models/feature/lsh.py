@@ -184,7 +184,10 @@ class MinHashLSHModel(ModelWithData, LSHModelParams):
         ids_b = dataset_b.get_list(id_col)
         if get_world_distributed():
             ids_a = dataset_a.get_list(id_col)
-            if _numeric_ids(ids_a) and _numeric_ids(ids_b):
+            # every rank must take the same branch (they issue different collectives): agree on
+            # it; an empty partition votes "numeric" 
+            mine = 1.0 if _numeric_ids(ids_a) and _numeric_ids(ids_b) else 0.0
+            if comm.all_reduce_scalar(mine, "min") > 0.5:
                 return _keyed_similarity_join(ha, hb, sa, sb, ids_a, ids_b, threshold, dist_col)
             # non-numeric ids: broadcast join (every rank sees all of B)
             parts = comm.all_gather_object((hb.cpu(), sb.to("cpu"), ids_b))
@@ -295,7 +298,10 @@ def _keyed_similarity_join(ha, hb, sa: SparseColumn, sb: SparseColumn, ids_a, id
         (0, 2), dtype=torch.int64, device=dev)
     cnt = torch.bincount(need[:, 0], minlength=P).tolist()
     req = comm.all_to_all_v(list(torch.split(need[:, 1].contiguous(), cnt)))  # rows others need from me
-    idb = torch.tensor([float(v) for v in ids_b], dtype=torch.float64, device=dev)
+    # integer ids (Java longs, possibly above 2^53) travel as int64 when every rank's are integers
+    ints = comm.all_reduce_scalar(1.0 if all(isinstance(v, (int, np.integer)) for v in ids_b) else 0.0, "min") > 0.5
+    idb = torch.tensor([int(v) for v in ids_b] if ints else [float(v) for v in ids_b],
+                       dtype=torch.int64 if ints else torch.float64, device=dev)
     sb_d = sb.to(dev)
     lens, cols, idv = [], [], []
     for r in range(P):
@@ -318,9 +324,7 @@ def _keyed_similarity_join(ha, hb, sa: SparseColumn, sb: SparseColumn, ids_a, id
     arow, fi, dist = arow[keep].cpu().tolist(), fi[keep], dist[keep].cpu()
     bid = got_ids.to(dev)[fi].cpu().tolist()
     ida = [ids_a[i] for i in arow]
-    ints = comm.all_reduce_scalar(1.0 if all(isinstance(v, (int, np.integer)) for v in ids_b) else 0.0, "min")
-    idb_out = [int(v) for v in bid] if ints > 0.5 else bid
-    return Table({"datasetA.id": ida, "datasetB.id": idb_out, dist_col: dist}, num_rows=len(ida))
+    return Table({"datasetA.id": ida, "datasetB.id": bid, dist_col: dist}, num_rows=len(ida))
 
 
 @rw.register_stage

@@ -142,9 +142,18 @@ def reduce_by_key_tensor(keys: torch.Tensor, values: torch.Tensor, op: str = "su
 
 
 def float_keys(x: torch.Tensor) -> torch.Tensor:
-    """int64 keys of float64 values that compare equal exactly when the values are equal
-    (−0.0 folded into +0.0)."""
-    return (x.to(torch.float64) + 0.0).contiguous().view(torch.int64)
+    """int64 keys of float64 values: one key per distinct value.
+
+    - every NaN maps to the one canonical pattern 0x7ff8000000000000, as ``Double.equals`` /
+      ``doubleToLongBits`` treat all NaNs as one value (VectorIndexer.java:96-106's HashSet);
+    - −0.0 is folded into +0.0. This deliberately differs from ``Double.equals``: the models
+      that consume these keys look values up by float comparison (VectorIndexerModel's sorted
+      category search, ChiSqTest's value order), where −0.0 == +0.0, so keeping two keys would
+      give a category no input can ever hit. Parity with the reference on −0.0 is unpinned (no
+      reference fixture holds −0.0)."""
+    x = x.to(torch.float64).contiguous() + 0.0
+    k = x.view(torch.int64)
+    return torch.where(torch.isnan(x), torch.full_like(k, 0x7FF8000000000000), k)
 
 
 def keys_to_float(k: torch.Tensor) -> torch.Tensor:

@@ -147,3 +147,47 @@ def test_lsh_keyed_similarity_join_matches_one_rank():
     assert len(ref) > 50
     got = sorted(r for part in run_spmd(_spmd_keyed_join, 3) for r in part)
     assert got == ref
+
+
+def _str_sets(seed, n):
+    t = _rand_sets(seed, n)
+    return Table.from_rows([("s%d" % i, v) for i, v in t.rows()], ["id", "vec"])
+
+
+def _spmd_mixed_join(rank, world):
+    """Rank 0 holds empty partitions (whose ids vote "numeric"), rank 1 all rows with string ids:
+    the ranks must agree on the broadcast join, not split between two collective sequences."""
+    a, b = _str_sets(1, 300), _str_sets(2, 200)
+    model = _lsh(4, 2).fit(a)
+    if rank == 0:
+        a, b = a.take([]), b.take([])
+    return model.approx_similarity_join(a, b, 0.7, "id").rows()
+
+
+def test_lsh_join_agrees_on_branch_with_empty_partition():
+    a, b = _str_sets(1, 300), _str_sets(2, 200)
+    ref = sorted(_lsh(4, 2).fit(a).approx_similarity_join(a, b, 0.7, "id").rows())
+    assert len(ref) > 10
+    part = run_spmd(_spmd_mixed_join, 2)
+    assert part[0] == []
+    assert sorted(part[1]) == ref
+
+
+def _big_ids(seed, n):
+    t = _rand_sets(seed, n)
+    return Table.from_rows([((1 << 60) + 2 * i + 1, v) for i, v in t.rows()], ["id", "vec"])
+
+
+def _spmd_big_id_join(rank, world):
+    a, b = _big_ids(1, 400), _big_ids(2, 300)
+    model = _lsh(4, 2).fit(a)
+    return model.approx_similarity_join(a.partition(rank, world), b.partition(rank, world), 0.7, "id").rows()
+
+
+def test_lsh_keyed_join_keeps_int64_ids_above_2p53():
+    a, b = _big_ids(1, 400), _big_ids(2, 300)
+    ref = sorted(_lsh(4, 2).fit(a).approx_similarity_join(a, b, 0.7, "id").rows())
+    assert len(ref) > 10
+    got = sorted(r for part in run_spmd(_spmd_big_id_join, 2) for r in part)
+    assert got == ref
+    assert all(isinstance(r[1], int) and r[1] > (1 << 53) for r in got)

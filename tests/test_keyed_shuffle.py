@@ -103,3 +103,17 @@ def _no_pickle_worker(rank, world):
 def test_keyed_merges_do_not_pickle():
     for calls in run_spmd(_no_pickle_worker, 2, timeout=300):
         assert calls == [], calls
+
+
+def test_float_keys_one_key_per_value():
+    """All NaN bit patterns are one key (Double.equals); -0.0 folds into +0.0 (documented)."""
+    from flink_ml_amd.parallel import datastream as ds
+
+    nan2 = torch.tensor([0x7FF0000000000001], dtype=torch.int64).view(torch.float64)
+    x = torch.cat([torch.tensor([float("nan"), -0.0, 0.0, 1.5, -float("nan")], dtype=torch.float64), nan2])
+    k = ds.float_keys(x)
+    assert k[0] == k[4] == k[5] == 0x7FF8000000000000
+    assert k[1] == k[2]
+    assert torch.unique(k).numel() == 3
+    back = ds.keys_to_float(torch.unique(k))
+    assert torch.isnan(back).sum() == 1
