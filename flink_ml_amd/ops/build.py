@@ -119,7 +119,7 @@ def _run(cmd):
 # per-source compiler options. kmeans.hip: MFMA accumulators in arch VGPRs — its epilogue reads
 # every accumulator with VALU ops each tile, and the AGPR form adds a v_accvgpr_read per value.
 FILE_FLAGS = {"kmeans.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-Wno-inline-asm"],
-              # the fused round's chunk claims (csrc/glm.hip DynLds) must keep counted vmcnt waits
+              # the fused round's ticket atomics: no lane-0 result fix-up (keeps counted vmcnt waits)
               "glm.hip": ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]}
 
 

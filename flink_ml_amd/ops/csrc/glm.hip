@@ -144,105 +144,8 @@ struct GlmTail {
   int wl_off;      // deferred: byte offset of the block's [d] coefficient image in LDS
   long long* trace;  // diagnostics (null = off): per block {start, rows done, end, hw id} in
                      // 100 MHz s_memrealtime ticks (scripts/trace_glm_blocks.py)
-  int* heads;      // dynamic schedule: [2 parities][DYN_HEADS][DYN_HSTRIDE] chunk counters
-  int dyn;         // 1: dynamic row schedule (deferred mode, row-at-a-time loop, U = 1)
-  int dyn_off;     // byte offset of the block's DynLds in LDS
-  int dyn_lg;      // log2(rows per chunk)
-  int dyn_sync;    // diagnostics: vmcnt(0) before a claim's result is read
-  int* dyn_dbg;    // diagnostics (null = off): per batch-row visit counters of the dynamic schedule
-  int* dyn_dbg2;   // diagnostics (null = off): per (block, wave) {exit q, walk steps, caps, exh, inflight, lastv, 0, 0}
-  int rowmap;      // static schedule: block → row-stripe mapping (ROWMAP_*)
-  int pairs;       // pair schedule (deferred mode, U = 1): static prefix + claimed row pairs
-  int pair_q;      // static fraction of the batch in 1/256
-  int pair_nh;     // pair heads (counters) in use, <= PAIR_NH_MAX
-  int l2acc;       // deferred flat tail: per-XCD replicas accumulated in the XCD's L2
-  int pf;          // deferred static schedule: next-round rows each wave prefetches in the tail
-  int pf_stop;     // ... if the wave is done within pf_stop s_memrealtime ticks of its block's start
-  int* pf_sink;    // always null: keeps the prefetch loads alive (never written)
 };
-// Static row schedule: wave slot gw of the W = NB·WPB slots reads rows start + gw + j·W.
-//  ROWMAP_BLOCK: gw = b·WPB + wave — the blocks of one XCD (b mod 8 under round-robin dispatch)
-//                read 16-KB pieces 128 KB apart of every 8-MB stripe;
-//  ROWMAP_XCD:   gw = (b mod 8 · NB/8 + b / 8)·WPB + wave — each XCD reads one contiguous
-//                1/8 of every stripe (its 64 blocks side by side);
-//  ROWMAP_WAVE:  gw = wave·NB + b — a block's waves read rows NB apart.
-enum { ROWMAP_BLOCK = 0, ROWMAP_XCD = 1, ROWMAP_WAVE = 2 };
-
-// Pair schedule (deferred 1-GPU rounds, row-at-a-time loop). Per-block timelines show a ≈4 µs
-// spread of the blocks' finishing times that is random round to round (per-block mean removed:
-// profiles/r3/lr_rowmap_ab_1gpu.jsonl) on top of a ≈2 µs per-XCD offset, so no static split can
-// remove it. Here each wave slot first takes J = ⌊q·B / W⌋ static rows (the stride above), then
-// claims PAIRS of adjacent rows of the remaining pool with one returning device-scope atomic per
-// pair on one of PAIR_NH counters (the pool split into equal ranges; counter h serves the 64
-// waves of blocks 8h … 8h + 7 — one block of every XCD under round-robin dispatch — so every
-// counter drains at the chip's mean rate and no stealing is needed). A wave stops at its first
-// failed claim. Latency: the claim for pair m + 1 is issued at the top of the iteration over pair
-// m (before the second row's loads) and read after the first row's math (≈1 row time later), so
-// a claim's result never crosses the loop back edge; the first pair is claimed at kernel entry and
-// its first row is the static loop's last prefetch. Counters of launch parity p are zeroed by
-// block 0 of every launch with parity 1 − p (launches alternate, kernel boundaries order them).
-constexpr int PAIR_NH_MAX = 64;
-constexpr int PAIR_STRIDE = 32;  // ints between counters (128 B)
-constexpr int PAIR_OFF = 2 * 8 * 32;  // after the DynLds schedule's counters in tl.heads
 constexpr int ACC_MAX_REPS = 8;
-// Tail prefetch (deferred 1-GPU rounds, static schedule; A/B knob). A round's blocks finish their
-// rows over a ≈4–6 µs window (median 33.5, slowest 37.7 µs) during which HBM runs below its
-// streaming rate while the stragglers finish. A wave done before tl.pf_stop ticks (100 MHz) of its
-// block's start reads the first tl.pf (≤ PF_MAX) rows it will own in the NEXT round (one dword
-// per 64 B, two rows per wave-instruction), so that round finds them in its XCD's L2 or in the
-// Infinity Cache. Pure cache hint: no result depends on it. (A first version stopped on a shared
-// count of finished waves: 4096 returning atomics on one address serialise, 109–128 µs rounds.)
-constexpr int PF_MAX = 8;
-
-// ------------------------------------------------------------------------------------------
-// Dynamic row schedule (work distribution of the fused round, deferred mode)
-// ------------------------------------------------------------------------------------------
-// A static row stride leaves the round waiting for its slowest XCD: per-block timelines
-// (profiles/r2/lr_round_block_timeline_512_corr.jsonl) show per-XCD mean finish times 31–35 µs and a
-// 4 µs random spread between blocks. Here the batch is cut into chunks of CH = WPB·DYN_K rows
-// (wave w of a block takes rows w, w + WPB, … of each chunk the block gets):
-//  * block b owns chunks b, b + NB, …, b + (DYN_L−1)·NB outright (its first rows are in flight
-//    before any atomic); the remaining chunks are split into DYN_HEADS equal ranges, one per XCD,
-//    each served by a device-scope counter on its own 128-B line (≈25 claims/µs per word at the
-//    flagship shape; one word saturates near 88/µs, MI355X_MICROARCH.md 'dequeue'). A block claims
-//    from its own XCD's counter and, once that range is drained, steals from the counter with the
-//    most chunks left;
-//  * every wave walks the block-local chunk sequence q = 0, 1, 2, … (an LDS ring of {q, chunk}
-//    words). Wave q mod WPB claims chunk q + DYN_L at the start of its iteration over chunk q and
-//    publishes it at the end of that iteration: the claim is issued before the iteration's row
-//    loads and consumed after them, so its wait is a counted vmcnt inside one iteration (no
-//    loop-carried atomic result, whose copy at a join would force vmcnt(0)), and the readers of
-//    chunk q + DYN_L reach it ≈DYN_L·DYN_K rows later. A wave never waits on a ring slot while
-//    holding an unpublished claim, so there is no wait cycle.
-// Termination: claims of one block complete out of order (the claim for q + 1 may succeed on a
-// counter switched to by a concurrent steal while the claim for q fails), so an empty chunk (−1)
-// is skipped, not taken as the end. A wave stops at chunk q only once no claim can succeed (exh),
-// none is in flight, and no later chunk was published (q > lastv) — conditions that, once true,
-// stay true, so every wave of the block stops at the same point; a wave waiting on a ring slot
-// re-checks them (the slot's claimer may have stopped). Every claimer raises `inflight` before it
-// reads `exh`, so a claim that sees exh = 0 is always waited for.
-// Steal probes read the counters with atomic adds of an opaque 0: an sc1 load is served by the
-// XCD's L2, which keeps a stale line of a counter that other XCDs advance at the memory side.
-// The claim atomics must not go through the AMDGPU atomic optimizer (its lane-0 result fix-up
-// forces vmcnt(0) at the issue point): glm.hip is built with
-// -amdgpu-atomic-optimizer-strategy=None (ops/build.py FILE_FLAGS).
-// The counters of launch parity p are used by that launch and zeroed for the next one by block 0 of
-// the launch with parity 1 − p (the host snapshots them around hipGraph warm-ups).
-// Reference: the work is the SGD minibatch loop of SGD.java:246-285 (the rows a batch covers are
-// unchanged — only which wave reads which row varies).
-constexpr int DYN_HEADS = 8;
-constexpr int DYN_HSTRIDE = 32;  // ints between counters (128 B)
-constexpr int DYN_L = 4;         // chunks of lookahead (and statically owned chunks per block)
-constexpr int DYN_R = 32;        // LDS ring slots (> DYN_L + the chunks any wave can lag behind)
-constexpr int DYN_K = 2;         // rows per wave per chunk (the software pipeline's two buffers)
-static_assert(PAIR_OFF == 2 * DYN_HEADS * DYN_HSTRIDE, "pair counters follow the DynLds schedule's");
-struct DynLds {
-  int head;      // counter the block claims from
-  int exh;       // no claim can succeed any more (every counter drained, or none exists)
-  int inflight;  // claims issued and not yet published
-  int lastv;     // highest block-local chunk number published with a real chunk
-  long long ring[DYN_R];  // (q << 32) | (unsigned)chunk, chunk −1 = empty
-};
 
 // Write-through (sc1) hand-off of the partial rows (cdna_hip_programming.md Guideline 16, the
 // sc1 form of the split-K combine): every handed-off value is stored with an agent-scope store
@@ -543,17 +446,21 @@ constexpr int glm_min_waves() {
 
 // X / y / wt are deliberately NOT __restrict__: with restrict the compiler may move the row
 // prefetch loads below the compiler fence that pins them ahead of the math (see the row loop).
-template <typename T, int EPC, int CPL, int U, int WPB, bool NT, int G = 0>
-__global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U>())) void glm_round_kernel(
+//
+// Row schedule: wave slot gw = b·WPB + wave of the W = NB·WPB slots reads rows start + gw + j·W,
+// U rows per step, two steps in flight. (Round 3 measured, and removed again, four alternatives
+// on the flagship shape — a dynamic chunk-claim schedule, claimed row pairs after a static prefix,
+// per-XCD L2 accumulator replicas, and a tail prefetch of the next round's rows; all exact, all
+// slower: profiles/r3/lr_{dyn_schedule,pair_schedule,l2acc,tail_prefetch_timegated}_ab_1gpu.jsonl.)
+template <typename T, int EPC, int CPL, int U, int WPB, bool NT>
+__global__ __launch_bounds__(WPB * 64, (glm_min_waves<T, EPC, CPL, U>())) void glm_round_kernel(
     const T* X, long ld, const typename AccOf<T>::type* y,
     const typename AccOf<T>::type* wt, typename AccOf<T>::type* coef,
     long n, int d, long B, int loss, int* state, typename AccOf<T>::type* partials, GlmTail tl) {
   typedef typename AccOf<T>::type A;
-  const long long t_start = (tl.trace || tl.pf) ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
+  const long long t_start = tl.trace ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
   int e;
   if (tl.defer) {
-    if (tl.pairs && blockIdx.x == 0 && threadIdx.x < tl.pair_nh)  // the next launch's counters
-      st_agent(&tl.heads[PAIR_OFF + (tl.parity ^ 1) * (PAIR_NH_MAX * PAIR_STRIDE) + threadIdx.x * PAIR_STRIDE], 0);
     if (state[ST_DONE]) return;
     e = state[tl.parity ? ST_ROUND_ALT : ST_ROUND];
   } else if (!round_running(state, e)) return;
@@ -570,13 +477,7 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nch = d / EPC;
   const long W = (long)gridDim.x * WPB;
-  long gw;
-  if (tl.rowmap == ROWMAP_XCD && (gridDim.x & 7) == 0)
-    gw = ((long)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3)) * WPB + wave;
-  else if (tl.rowmap == ROWMAP_WAVE)
-    gw = (long)wave * gridDim.x + blockIdx.x;
-  else
-    gw = (long)blockIdx.x * WPB + wave;
+  const long gw = (long)blockIdx.x * WPB + wave;
 
   // bf16 rows: packed fp32 math on {lo, hi} pairs (one dword = two bf16, widened exactly by a
   // shift / a mask): the dot and the gradient axpy are one v_pk_fma_f32 per pair each
@@ -600,8 +501,8 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
   // lgkmcnt, and one still pending at the row loop's header turns its counted waits into vmcnt(0)
   typedef __attribute__((address_space(3))) A lds_acc_t;
   const lds_acc_t* wlds = (const lds_acc_t*)(smem_w + tl.wl_off);
-  auto load_w = [&](bool lds_only = false) {
-    if (lds_only || tl.defer) {
+  auto load_w = [&]() {
+    if (tl.defer) {
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
         const int c = lane + 64 * k;
@@ -647,35 +548,6 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
   // a full memory latency per row pair; the vector loads are ordered with the row loads.
   const long r_first = start + gw;
   A ylab = (A)0, wlab = (A)1;
-  // pair schedule (see PAIR_NH_MAX): static rows end at `lim`; the pool [lim, end) is served by
-  // pair counter `pctr` (pairs [plo, phi) of the pool); pair `pm0`, claimed at entry, is the
-  // static loop's last prefetch (row `pra0`, label / weight `pyl0` / `pwl0`) when `pok0`
-  long lim = end;
-  bool pairs = false, pok0 = false;
-  long plo = 0, phi = 0, pm0 = 0, pra0 = 0;
-  A pyl0 = (A)0, pwl0 = (A)1;
-  int* pctr = nullptr;
-  auto claim = [&]() -> int {
-    int t = 0;
-    if (lane == 0) t = __hip_atomic_fetch_add(pctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return t;
-  };
-  int pclaim0 = 0;
-  if constexpr (U == 1) {
-    if (tl.pairs && tl.defer && tl.heads && end > start) {
-      pairs = true;
-      const long J = ((end - start) * (long)tl.pair_q) / (256L * W);  // static rows per wave slot
-      lim = start + J * W;
-      const long npairs = (end - lim + 1) >> 1;
-      const int nh = tl.pair_nh;
-      const int h = (int)((blockIdx.x >> 3) % (unsigned)nh);
-      const long per = (npairs + nh - 1) / nh;
-      plo = (long)h * per;
-      phi = plo + per < npairs ? plo + per : npairs;
-      pctr = tl.heads + PAIR_OFF + tl.parity * (PAIR_NH_MAX * PAIR_STRIDE) + h * PAIR_STRIDE;
-      pclaim0 = claim();  // the oldest load of the wave: read after the first rows are issued
-    }
-  }
   auto load_labels = [&](long j0) {
     long rr = r_first + (j0 + lane) * W;
     rr = rr < end ? rr : (end > 0 ? end - 1 : 0);
@@ -697,15 +569,12 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
   auto load_rows = [&](long r0, long j0, long rsafe, Chunk<T, EPC> (&dst)[U][CPL], A (&yy)[U], A (&ww)[U],
                        bool (&vv)[U]) {
     if ((j0 & 63) == 0 && j0 > 0) load_labels(j0);
-    bool okr[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long ru0 = r0 + u * W;
-      const bool ok = ru0 < lim;
-      okr[u] = ok;
-      // pair schedule (U = 1): past the static rows the prefetch is the first claimed pair's row
-      const long ru = ok ? ru0 : (pok0 ? pra0 : rsafe);
-      vv[u] = ok || pok0;
+      const bool ok = ru0 < end;
+      const long ru = ok ? ru0 : rsafe;
+      vv[u] = ok;
       const T* row = X + ru * ld;
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
@@ -719,26 +588,7 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
     for (int u = 0; u < U; ++u) {
       yy[u] = lane_val(ylab, (int)((j0 + u) & 63));
       ww[u] = lane_val(wlab, (int)((j0 + u) & 63));
-      if (!okr[u]) {
-        yy[u] = pyl0;
-        ww[u] = pwl0;
-      }
     }
-  };
-  // one row of a claimed pair: row data plus its label / weight as vector loads (ordered with the
-  // row loads under vmcnt; a scalar load would share lgkmcnt with the LDS traffic)
-  auto load_pair_row = [&](long rr, bool ok, Chunk<T, EPC> (&dst)[U][CPL], A (&yy)[U], A (&ww)[U], bool (&vv)[U]) {
-    vv[0] = ok;
-    const T* row = X + rr * ld;
-#pragma unroll
-    for (int k = 0; k < CPL; ++k) {
-      const int c = lane + 64 * k;
-      if constexpr (NT) load_chunk_nt<T, EPC>(row + (c < nch ? c : nch - 1) * EPC, dst[0][k]);
-      else load_chunk<T, EPC>(row + (c < nch ? c : nch - 1) * EPC, dst[0][k]);
-    }
-    asm volatile("" : "+v"(rr));
-    yy[0] = y[rr];
-    ww[0] = wsrc[rr];
   };
   auto process = [&](Chunk<T, EPC> (&x)[U][CPL], A (&yy)[U], A (&ww)[U], bool (&vv)[U]) {
     if constexpr (kPacked) {
@@ -803,377 +653,16 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
       }
     }
   };
-  if constexpr (G > 0) {
-    // ---- grouped row path (bf16, EPC 8): G rows per step. The per-row chain dot → wave sum →
-    // loss → multiplier is the latency that bounds the row-at-a-time loop (measured: the loss
-    // step alone +6 µs on the 200 MB flagship batch); here the G dots of a step are reduced
-    // together (one LDS transpose + a 3–4 step DPP segment sum instead of G full wave sums), the
-    // loss runs once for all G rows (one row per segment of L = 64/G lanes) and the G
-    // multipliers come back with readlane for the packed axpy.
-    static_assert(kPacked && EPC == 8 && (G == 4 || G == 8), "grouped path: bf16 rows, 16-byte chunks");
-    constexpr int L = 64 / G;  // lanes per row in the loss step
-    extern __shared__ __align__(16) unsigned char smem_g[];
-    float* red = reinterpret_cast<float*>(smem_g + tl.red_off) + wave * (G * 64);  // wave-private [G][64]
-    const int gi = lane / L, seg = lane % L;
-    const long r0w = start + gw;      // this wave's first row
-    const long stepg = (long)G * W;   // rows between consecutive groups of the wave
-    Chunk<T, EPC> xa[G][CPL], xb[G][CPL];
-    A yla = (A)0, wla = (A)1, ylb = (A)0, wlb = (A)1;
-    auto load_group = [&](long g0, Chunk<T, EPC> (&dst)[G][CPL], A& yl, A& wl) {
-      // labels of the group's rows, one row per L-lane segment (clamped: masked in the loss)
-      long rl = g0 + gi * W;
-      rl = rl < end ? rl : (end > 0 ? end - 1 : 0);
-      yl = y[rl];
-      wl = wsrc[rl];
-#pragma unroll
-      for (int i = 0; i < G; ++i) {
-        const long ri0 = g0 + i * W;
-        const long ri = ri0 < end ? ri0 : r0w;  // r0w < end whenever a group is loaded
-        const T* row = X + ri * ld;
-#pragma unroll
-        for (int k = 0; k < CPL; ++k) {
-          const int c = lane + 64 * k;
-          if constexpr (NT) load_chunk_nt<T, EPC>(row + (c < nch ? c : nch - 1) * EPC, dst[i][k]);
-          else load_chunk<T, EPC>(row + (c < nch ? c : nch - 1) * EPC, dst[i][k]);
-        }
-      }
-    };
-    auto unpack = [&](const Chunk<T, EPC>& ch, int q) -> f2_t {
-      const uint32_t v = reinterpret_cast<const uint32_t*>(ch.v)[q];
-      return f2_t{__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u)};
-    };
-    auto process_group = [&](long g0, Chunk<T, EPC> (&x)[G][CPL], A yl, A wl) {
-      // 1. per-lane dot partials of the G rows (packed fp32, two chains per row)
-      float pd[G];
-#pragma unroll
-      for (int i = 0; i < G; ++i) {
-        f2_t s2[2] = {{0.f, 0.f}, {0.f, 0.f}};
-#pragma unroll
-        for (int k = 0; k < CPL; ++k)
-#pragma unroll
-          for (int q = 0; q < EPC / 2; ++q) s2[q & 1] = __builtin_elementwise_fma(unpack(x[i][k], q), w2[k][q], s2[q & 1]);
-        const f2_t st = s2[0] + s2[1];
-        pd[i] = st.x + st.y;
-      }
-      // 2. transposed reduction: [G][64] through the wave's LDS slot (one wave: LDS in order),
-      // lane (gi, seg) sums row gi's partials of lanes seg·G .. seg·G + G − 1, then the segment
-#pragma unroll
-      for (int i = 0; i < G; ++i) red[i * 64 + lane] = pd[i];
-      float s = 0.f;
-      const float4* src = reinterpret_cast<const float4*>(red + gi * 64 + seg * G);
-#pragma unroll
-      for (int q = 0; q < G / 4; ++q) {
-        const float4 v = src[q];
-        s += (v.x + v.y) + (v.z + v.w);
-      }
-      const float dot = seg_sum_dpp<L>(s);
-      // 3. loss + multiplier, one row per segment
-      const bool valid = g0 + gi * W < end;
-      A l, m;
-      const A wu = has_wt ? wl : (A)1;
-      loss_and_mult(loss, dot, yl, wu, l, m);
-      if (!valid) { l = (A)0; m = (A)0; }
-      if (seg == 0) {
-        wsum += valid ? wu : (A)0;
-        lsum += l;
-      }
-      // 4. gradient axpy with the G multipliers (wave-uniform scalars). The rows are widened
-      // again from the raw dwords (2 VALU per pair) instead of keeping G·16 widened floats live
-      // across the reduction: the empty asm hides the raw registers' identity from CSE.
-#pragma unroll
-      for (int i = 0; i < G; ++i)
-#pragma unroll
-        for (int k = 0; k < CPL; ++k) {
-          uint32_t* q = reinterpret_cast<uint32_t*>(x[i][k].v);
-#pragma unroll
-          for (int j = 0; j < EPC / 2; ++j) asm volatile("" : "+v"(q[j]));
-        }
-#pragma unroll
-      for (int i = 0; i < G; ++i) {
-        const float mi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m), i * L));
-        const f2_t m2 = {mi, mi};
-#pragma unroll
-        for (int k = 0; k < CPL; ++k)
-#pragma unroll
-          for (int q = 0; q < EPC / 2; ++q) acc2[k][q] = __builtin_elementwise_fma(m2, unpack(x[i][k], q), acc2[k][q]);
-      }
-    };
-    long g0 = r0w;
-    if (g0 < end) {
-      load_group(g0, xa, yla, wla);
-      load_w();
-      while (true) {
-        load_group(g0 + stepg, xb, ylb, wlb);
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        process_group(g0, xa, yla, wla);
-        g0 += stepg;
-        if (g0 >= end) break;
-        load_group(g0 + stepg, xa, yla, wla);
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        process_group(g0, xb, ylb, wlb);
-        g0 += stepg;
-        if (g0 >= end) break;
-      }
-    }
-    // Σweight / Σloss were accumulated by the segment-leader lanes: lane 0 reports the wave's
-    wsum = wave_sum_dpp(wsum);
-    lsum = wave_sum_dpp(lsum);
-  } else {
-  bool dyn_done = false;
-  if constexpr (U == 1) if (tl.dyn) {
-    // ---- dynamic row schedule (see DynLds): DYN_K = 2 rows per wave per chunk, one in each
-    // pipeline buffer, so an iteration of the loop below is one chunk
-    dyn_done = true;
-    extern __shared__ __align__(16) unsigned char smem_d[];
-    DynLds* D = reinterpret_cast<DynLds*>(smem_d + tl.dyn_off);
-    constexpr int CH = WPB * DYN_K;
-    const long nrows = end - start;
-    const long C = (nrows + CH - 1) / CH;                // chunks of this round
-    const long NB = gridDim.x;
-    const long S0 = (long)DYN_L * NB;                    // statically owned chunks
-    const long Dn = C > S0 ? C - S0 : 0;                 // chunks served by the counters
-    int* heads = tl.heads + tl.parity * (DYN_HEADS * DYN_HSTRIDE);
-    auto lo_of = [&](int h) -> long { return S0 + (Dn * h) / DYN_HEADS; };
-    auto hi_of = [&](int h) -> long { return S0 + (Dn * (h + 1)) / DYN_HEADS; };
-    if (blockIdx.x == 0 && threadIdx.x < DYN_HEADS)  // the next launch's counters
-      st_agent(&tl.heads[(tl.parity ^ 1) * (DYN_HEADS * DYN_HSTRIDE) + threadIdx.x * DYN_HSTRIDE], 0);
-    if (wave == 0) {  // wave 0's own first access to D follows in program order; the rest of
-                      // the block reads D only after the prologue's barrier
-      unsigned xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      if (lane == 0) {
-        D->head = (int)(xcc & (DYN_HEADS - 1));
-        D->exh = Dn == 0;
-        D->inflight = 0;
-        const long b = blockIdx.x;  // last statically owned chunk number that exists
-        D->lastv = b < C ? (int)((C - 1 - b) / NB < DYN_L - 1 ? (C - 1 - b) / NB : DYN_L - 1) : -1;
-      }
-      if (lane < DYN_R) D->ring[lane] = -1LL;  // tag −1: nothing published
-    }
-    auto put = [&](int q, long c) {
-      if (lane == 0)
-        __hip_atomic_store(&D->ring[q & (DYN_R - 1)], ((long long)q << 32) | (unsigned int)(int)c, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    auto lds_ld = [&](int* p) -> int {
-      return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-    };
-    auto lds_add = [&](int* p, int v) {
-      if (lane == 0) __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    auto done_at = [&](int q) -> bool {  // no real chunk can appear at q or later
-      return lds_ld(&D->exh) && lds_ld(&D->inflight) == 0 && q > lds_ld(&D->lastv);
-    };
-    auto steal = [&]() -> long {
-      // every counter's fill level (lanes 0..7, coherent atomic reads), then a claim on the
-      // fullest; a failed claim means that counter is drained, so it is not probed again
-      unsigned tried = 0;
-      int zero;  // opaque 0: an add of a literal 0 is folded into a plain (L2-served) atomic load
-      asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
-      for (int it = 0; it < DYN_HEADS; ++it) {
-        const int hv = lane < DYN_HEADS ? __hip_atomic_fetch_add(&heads[lane * DYN_HSTRIDE], zero, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_AGENT) : 0;
-        long best = 0;
-        int bh = -1;
-#pragma unroll
-        for (int h = 0; h < DYN_HEADS; ++h) {
-          const long rem = (hi_of(h) - lo_of(h)) - (long)__builtin_amdgcn_readlane(hv, h);
-          if (!((tried >> h) & 1) && rem > best) { best = rem; bh = h; }
-        }
-        if (bh < 0) break;
-        int t = 0;
-        if (lane == 0) t = __hip_atomic_fetch_add(&heads[bh * DYN_HSTRIDE], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        t = __builtin_amdgcn_readfirstlane(t);
-        if (lo_of(bh) + t < hi_of(bh)) {
-          if (lane == 0) __hip_atomic_store(&D->head, bh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          return lo_of(bh) + t;
-        }
-        tried |= 1u << bh;
-      }
-      if (lane == 0) __hip_atomic_store(&D->exh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      return -1;
-    };
-    // chunk of block-local number q: −1 empty, −2 the block is done
-    auto chunk_of = [&](int q) -> long {
-      if (q < DYN_L) {
-        const long c = blockIdx.x + (long)q * NB;
-        return c < C ? c : -1;
-      }
-      long long v;
-      for (int spin = 0;; ++spin) {
-        v = __hip_atomic_load(&D->ring[q & (DYN_R - 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const int vh = __builtin_amdgcn_readfirstlane((int)(v >> 32));
-        if (vh == q) break;
-        if ((spin & 63) == 63 && done_at(q)) return -2;  // the slot's claimer may have stopped
-        // never reached by the protocol (every slot is published once, before the ring wraps):
-        // a bounded wait keeps a broken invariant a wrong result, not a GPU hang
-        if (vh > q || spin > (1 << 22)) return -2;
-        __builtin_amdgcn_s_sleep(1);
-      }
-      return (long)__builtin_amdgcn_readfirstlane((int)(v & 0xffffffffLL));
-    };
-    int claim_q = -1, claim_h = 0, claim_t = 0;
-    int dbg_steps = 0, dbg_caps = 0;
-    // claim for chunk q + DYN_L if this wave owns q (issued before the iteration's row loads)
-    auto claim_issue = [&](int q) {
-      claim_q = -1;
-      claim_t = 0;
-      if ((q & (WPB - 1)) != wave) return;
-      lds_add(&D->inflight, 1);  // before reading exh (see the termination note)
-      if (lds_ld(&D->exh)) {
-        put(q + DYN_L, -1);
-        lds_add(&D->inflight, -1);
-        return;
-      }
-      claim_q = q + DYN_L;
-      claim_h = lds_ld(&D->head);
-      if (lane == 0)
-        claim_t = __hip_atomic_fetch_add(&heads[claim_h * DYN_HSTRIDE], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
-    auto claim_publish = [&]() {
-      if (claim_q < 0) return;
-      if (tl.dyn_sync) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-      long cn = lo_of(claim_h) + __builtin_amdgcn_readfirstlane(claim_t);
-      if (cn >= hi_of(claim_h)) cn = steal();
-      put(claim_q, cn);
-      if (cn >= 0 && lane == 0)
-        __hip_atomic_fetch_max(&D->lastv, claim_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      lds_add(&D->inflight, -1);  // after the publication and lastv
-      claim_q = -1;
-    };
-    // the next chunk with rows at or after q (q advanced past empty ones; −1: the block is done).
-    // Wave q mod WPB publishes q + DYN_L for every q it passes (−1 once nothing can be claimed).
-    // A walk past empty chunks can reach the slot of this wave's own unpublished claim: it is
-    // published first (otherwise the wave waits on itself, and done_at counts the claim in flight).
-    auto walk = [&](int& q) -> long {
-      for (int spin = 0;; ++spin) {
-        if (q == claim_q) claim_publish();
-        const long c = chunk_of(q);
-        if (c >= 0) return c;
-        ++dbg_steps;
-        if (c == -2) ++dbg_caps;
-        if (c == -2 || done_at(q) || spin > (1 << 20)) return -1;
-        if ((q & (WPB - 1)) == wave) put(q + DYN_L, -1);  // exh is set: every −1 follows it
-        ++q;
-      }
-    };
-    // row j of chunk c for this wave (c < 0 or past `end`: `rsafe` again, masked)
-    auto load_j = [&](long c, int j, long rsafe, Chunk<T, EPC> (&dst)[1][CPL], A (&yy)[1], A (&ww)[1],
-                      bool (&vv)[1]) {
-      const long r = start + c * CH + j * WPB + wave;
-      const bool ok = c >= 0 && r < end;
-      long rr = ok ? r : rsafe;
-      vv[0] = ok;
-      const T* row = X + rr * ld;
-#pragma unroll
-      for (int k = 0; k < CPL; ++k) {
-        const int cc = lane + 64 * k;
-        if constexpr (NT) load_chunk_nt<T, EPC>(row + (cc < nch ? cc : nch - 1) * EPC, dst[0][k]);
-        else load_chunk<T, EPC>(row + (cc < nch ? cc : nch - 1) * EPC, dst[0][k]);
-      }
-      // label / weight as vector loads: ordered with the row loads under vmcnt (a scalar load
-      // would share lgkmcnt with the LDS ring)
-      asm volatile("" : "+v"(rr));
-      yy[0] = y[rr];
-      ww[0] = wsrc[rr];
-      if (tl.dyn_dbg && ok && lane == 0) atomicAdd(&tl.dyn_dbg[r - start], 1);
-    };
-    int q = 0;
-    long c = nrows > 0 ? walk(q) : -1;
-    if (c >= 0) load_j(c, 0, start, xa, ya, wa, va);
-    if (tl.defer && defer_prologue<A>(tl, coef, state, e, d, wdef)) return;
-    // nothing in flight at the loop header but the back edge's own loads (otherwise the header
-    // merges the pre-loop loads' registers into every iteration's waits); the prologue's own
-    // loads came after the first row's, so this wait is already satisfied in deferred mode
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    if (c >= 0) {
-      load_w(true);  // dynamic schedule ⇒ deferred mode: w_e is in LDS (no global-load branch)
-      while (true) {
-        // xa: row 0 of chunk c (in flight). The claim is issued and consumed inside this
-        // iteration: before row 1's loads, after row 0 of the next chunk went out
-        claim_issue(q);
-        const long rs = start + c * CH + wave < end ? start + c * CH + wave : start;
-        load_j(c, 1, rs, xb, yb, wb, vb);
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        process(xa, ya, wa, va);
-        int qn = q + 1;
-        const long cn = walk(qn);
-        load_j(cn, 0, rs, xa, ya, wa, va);
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        process(xb, yb, wb, vb);
-        claim_publish();
-        if (cn < 0) {
-          q = qn;
-          break;
-        }
-        q = qn;
-        c = cn;
-      }
-    }
-    if (tl.dyn_dbg2 && lane == 0) {
-      int* o = tl.dyn_dbg2 + ((long)blockIdx.x * WPB + wave) * 8;
-      o[0] = q;
-      o[1] = dbg_steps;
-      o[2] = dbg_caps;
-      o[3] = __hip_atomic_load(&D->exh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      o[4] = __hip_atomic_load(&D->inflight, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      o[5] = __hip_atomic_load(&D->lastv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-  }
-  if (!dyn_done) {
   const long step = (long)U * W;
   long r = start + gw;
   long j = 0;
-  if (r < lim) {
+  if (r < end) {
     load_labels(0);  // first: load_rows reads the labels right after issuing its row loads
     load_rows(r, 0, r, xa, ya, wa, va);
   }
   // deferred mode: complete the previous round while the first rows are in flight
   if (tl.defer && defer_prologue<A>(tl, coef, state, e, d, wdef)) return;
-  // pair schedule: the first claim (issued at entry) and its row's label / weight
-  if (pairs) {
-    pm0 = plo + __builtin_amdgcn_readfirstlane(pclaim0);
-    pok0 = pm0 < phi;
-    pra0 = lim + 2 * pm0;
-    long rl = pok0 ? pra0 : start;
-    asm volatile("" : "+v"(rl));
-    pyl0 = y[rl];
-    pwl0 = wsrc[rl];
-  }
-  // iterations over claimed pairs; xp holds the (in-flight) first row `ra` of the current pair
-  auto pair_loop = [&](Chunk<T, EPC> (&xp)[U][CPL], A (&yp)[U], A (&wp)[U], bool (&vp)[U],
-                       Chunk<T, EPC> (&xq)[U][CPL], A (&yq)[U], A (&wq)[U], bool (&vq)[U], long ra) {
-    if constexpr (U == 1) {
-      while (true) {
-        const int tn = claim();  // pair m + 1, read after this iteration's first row
-        const long rb = ra + 1;
-        const bool okb = rb < end;
-        load_pair_row(okb ? rb : ra, okb, xq, yq, wq, vq);
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        process(xp, yp, wp, vp);
-        const long mn = plo + __builtin_amdgcn_readfirstlane(tn);
-        const bool okn = mn < phi;
-        const long rn = okn ? lim + 2 * mn : ra;
-        load_pair_row(rn, okn, xp, yp, wp, vp);
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        process(xq, yq, wq, vq);
-        if (!okn) break;
-        ra = rn;
-      }
-    }
-  };
-  if (r >= lim && pok0) {  // no static rows for this wave slot: start with the claimed pair
-    load_w();
-    load_pair_row(pra0, true, xa, ya, wa, va);
-    pair_loop(xa, ya, wa, va, xb, yb, wb, vb, pra0);
-  }
-  if (r < lim) {
+  if (r < end) {
     load_w();
     while (true) {
       load_rows(r + step, j + U, r, xb, yb, wb, vb);
@@ -1186,23 +675,15 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
       process(xa, ya, wa, va);
       r += step;
       j += U;
-      if (r >= lim) {
-        if (pok0) pair_loop(xb, yb, wb, vb, xa, ya, wa, va, pra0);
-        break;
-      }
+      if (r >= end) break;
       load_rows(r + step, j + U, r, xa, ya, wa, va);
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       process(xb, yb, wb, vb);
       r += step;
       j += U;
-      if (r >= lim) {
-        if (pok0) pair_loop(xa, ya, wa, va, xb, yb, wb, vb, pra0);
-        break;
-      }
+      if (r >= end) break;
     }
-  }
-  }  // classic row-at-a-time path
   }
 
   if (tl.trace) {
@@ -1251,15 +732,7 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
     __syncthreads();
     // replica b mod acc_reps: at most ceil(nb / reps) adders per address (float atomics keep
     // their full rate up to ~32 adders per address; 256 on one 4 KB row serialise)
-    // l2acc (deferred mode): replica = this block's XCD, added with workgroup-scope atomics that
-    // the XCD's own L2 performs (only blocks of that XCD touch the replica; the kernel boundary
-    // writes the L2 back before the next launch's prologue reads it)
-    int rep = (int)(blockIdx.x % (tl.acc_reps > 1 ? tl.acc_reps : 1));
-    if (tl.l2acc) {
-      unsigned xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      rep = (int)(xcc & (ACC_MAX_REPS - 1));
-    }
+    const int rep = (int)(blockIdx.x % (tl.acc_reps > 1 ? tl.acc_reps : 1));
     A* gacc = (A*)tl.acc + (long)rep * tl.acc_ld + (tl.defer ? (long)(e % 3) * ACC_MAX_REPS * tl.acc_ld : 0L);
     const long stride = d + 2;
     for (long c = threadIdx.x; c < stride; c += blockDim.x) {
@@ -1271,36 +744,7 @@ __global__ __launch_bounds__(WPB * 64, (G > 0 ? 2 : glm_min_waves<T, EPC, CPL, U
 #pragma unroll
         for (int q = 0; q < WPB; ++q) v += lw[q * 2 + (int)(c - d)];
       }
-      if (tl.l2acc) __hip_atomic_fetch_add(gacc + c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      else atomicAdd(gacc + c, v);
-    }
-    if constexpr (G == 0) {
-      if (tl.pf > 0) {
-        // tail prefetch (see PF_MAX): this block's gradient is on its way; a wave done before
-        // pf_stop ticks of its block's start reads its first pf rows of the next round (one
-        // decision per wave, loads issued back to back, one wait)
-        const long long now = (long long)__builtin_amdgcn_s_memrealtime();
-        if (now - t_start < (long long)tl.pf_stop && e + 1 < tl.max_iter && n > 0 && B > 0) {
-          const unsigned P1 = tl.nbatch > 0 ? (unsigned)tl.nbatch : (unsigned)((n + B - 1) / B);
-          const long s1 = (long)((unsigned)(e + 1) % P1) * B;
-          const long e1 = s1 + B < n ? s1 + B : n;
-          const int rowb = d * (int)sizeof(T);
-          uint32_t v[PF_MAX / 2];
-#pragma unroll
-          for (int q = 0; q < PF_MAX / 2; ++q) {
-            v[q] = 0;
-            const long rr = s1 + gw + (long)(2 * q + (lane >> 5)) * W;
-            if (2 * q < tl.pf && rr < e1) {
-              const char* rp = reinterpret_cast<const char*>(X + rr * ld);
-              for (int off = (lane & 31) * 64; off < rowb; off += 32 * 64) v[q] ^= *reinterpret_cast<const uint32_t*>(rp + off);
-            }
-          }
-          uint32_t sink = 0;
-#pragma unroll
-          for (int q = 0; q < PF_MAX / 2; ++q) sink ^= v[q];
-          if (tl.pf_sink) tl.pf_sink[threadIdx.x] = (int)sink;  // never taken: pf_sink is null
-        }
-      }
+      atomicAdd(gacc + c, v);
     }
     if (tl.trace) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1804,39 +1248,21 @@ static int g_nt = -1;
 static int g_acc_reps = 4;  // atomic-tail accumulator replicas (A/B knob, <= ACC_MAX_REPS)
 static int g_ticket2 = 0;   // two-level tickets (A/B knob)
 static long long* g_trace = nullptr;  // per-block timestamps of the next launches (diagnostics)
-static int g_dyn = 1;       // dynamic row schedule (A/B knob)
-static int g_dyn_lg = 3;    // log2(rows per claimed chunk), >= log2(WPB)
-static int g_dyn_sync = 0;
-static int* g_dyn_dbg = nullptr;
-static int* g_dyn_dbg2 = nullptr;
-static int g_rowmap = ROWMAP_BLOCK;
-static int g_pairs = 0;      // pair schedule (A/B knob)
-static int g_pair_q = 205;   // static fraction of the batch, 1/256 units
-static int g_l2acc = 0;      // deferred flat tail: per-XCD L2 replicas (A/B knob)
-static int g_pf = 0;         // deferred static schedule: tail prefetch rows per wave (A/B knob)
-static int g_pf_stop = 3400; // ... by waves done within this many 10-ns ticks of their block's start
 constexpr long LDS_PER_CU = 160 * 1024;
 constexpr int NUM_CU = 256;
 
-template <typename T, int EPC, int CPL, int U, int G = 0>
+template <typename T, int EPC, int CPL, int U>
 int launch_grad_u(const void* X, long ld, const void* y, const void* wt, void* coef, long n, int d, long B, int loss,
                   int* state, void* partials, int nblocks, const GlmTail& tl, int flags, hipStream_t s) {
   typedef typename AccOf<T>::type A;
   // [WPB/2][d] tree buffer (reused as the final block's feedback row) | [WPB][2] | ticket flag
   GlmTail t2 = tl;
-  t2.rowmap = g_rowmap;
-  // pair schedule: deferred mode, row-at-a-time loop, counters present
-  t2.pairs = g_pairs && U == 1 && G == 0 && tl.defer && !tl.det && tl.heads != nullptr && !(g_dyn && tl.heads);
-  t2.pair_q = g_pair_q;
-  t2.l2acc = g_l2acc && tl.defer && !tl.det && tl.mode == TAIL_UPDATE;
-  if (t2.l2acc) t2.acc_reps = ACC_MAX_REPS;  // the prologue sums every XCD's replica
-  t2.pair_nh = nblocks / 8 < 1 ? 1 : (nblocks / 8 > PAIR_NH_MAX ? PAIR_NH_MAX : nblocks / 8);
   t2.nbatch = (n > 0 && B > 0) ? (int)((n + B - 1) / B) : 0;
   t2.flat_lds = tl.mode != TAIL_PARTIALS && !tl.det && (size_t)WPB * d * sizeof(A) <= 64 * 1024;
   size_t shmem = (size_t)(t2.flat_lds ? WPB : WPB / 2) * d * sizeof(A) + WPB * 2 * sizeof(A) + 16;
   if (t2.defer) {
-    // the deferred prologue needs the flat atomic tail and the row-at-a-time loop
-    if (!t2.flat_lds || G > 0 || tl.mode != TAIL_UPDATE || tl.det || tl.cw == nullptr) return -7;
+    // the deferred prologue needs the flat atomic tail
+    if (!t2.flat_lds || tl.mode != TAIL_UPDATE || tl.det || tl.cw == nullptr) return -7;
     t2.wl_off = (int)((shmem + 15) & ~(size_t)15);
     shmem = (size_t)t2.wl_off + (size_t)d * sizeof(A);
   }
@@ -1849,30 +1275,15 @@ int launch_grad_u(const void* X, long ld, const void* y, const void* wt, void* c
       if (shmem < want) shmem = want;
     }
   }
-  // dynamic row schedule: deferred mode, row-at-a-time loop with one row per draw
-  t2.dyn = g_dyn && U == 1 && G == 0 && t2.defer && !tl.det && tl.heads != nullptr;
-  if (t2.dyn) {
-    t2.dyn_lg = g_dyn_lg;
-    t2.dyn_off = (int)((shmem + 15) & ~(size_t)15);
-    shmem = (size_t)t2.dyn_off + sizeof(DynLds);
-  }
-  t2.pf = (g_pf > 0 && G == 0 && t2.defer && !tl.det && !t2.pairs && !t2.dyn) ? g_pf : 0;
-  t2.pf_stop = g_pf_stop;
-  t2.pf_sink = nullptr;
-  if constexpr (G > 0) {
-    // grouped path: per-wave [G][64] fp32 transpose scratch after the epilogue's buffers
-    t2.red_off = (int)((shmem + 15) & ~(size_t)15);
-    shmem = (size_t)t2.red_off + (size_t)WPB * G * 64 * sizeof(float);
-  }
   const bool nt = g_nt >= 0 ? g_nt != 0 : (flags & 1) != 0;
   if constexpr (EPC * sizeof(T) == 16 && sizeof(T) == 2) {
     if (nt) {
-      hipLaunchKernelGGL((glm_round_kernel<T, EPC, CPL, U, WPB, true, G>), dim3(nblocks), dim3(WPB * 64), shmem, s,
+      hipLaunchKernelGGL((glm_round_kernel<T, EPC, CPL, U, WPB, true>), dim3(nblocks), dim3(WPB * 64), shmem, s,
                          (const T*)X, ld, (const A*)y, (const A*)wt, (A*)coef, n, d, B, loss, state, (A*)partials, t2);
       return (int)hipGetLastError();
     }
   }
-  hipLaunchKernelGGL((glm_round_kernel<T, EPC, CPL, U, WPB, false, G>), dim3(nblocks), dim3(WPB * 64), shmem, s,
+  hipLaunchKernelGGL((glm_round_kernel<T, EPC, CPL, U, WPB, false>), dim3(nblocks), dim3(WPB * 64), shmem, s,
                      (const T*)X, ld, (const A*)y, (const A*)wt, (A*)coef, n, d, B, loss, state, (A*)partials, t2);
   return (int)hipGetLastError();
 }
@@ -1882,16 +1293,6 @@ template <typename T, int EPC, int CPL>
 int launch_grad(int u, const void* X, long ld, const void* y, const void* wt, void* coef, long n, int d, long B,
                 int loss, int* state, void* partials, int nblocks, const GlmTail& tl, int flags, hipStream_t s) {
   constexpr int BYTES = CPL * EPC * (int)sizeof(T);
-  // grouped path (bf16, 16-byte chunks, d ≤ 2048): u = -4 / -8 (A/B knob; measured slower
-  // than the row-at-a-time loop on the flagship shape: 40.6 / 42.2 vs 37.9 µs per round)
-  if constexpr (sizeof(T) == 2 && EPC == 8 && CPL <= 4) {
-    if (u < 0) {
-      const int g = -u;
-      if (g == 8 && CPL <= 2)
-        return launch_grad_u<T, EPC, CPL, 1, 8>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
-      return launch_grad_u<T, EPC, CPL, 1, 4>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
-    }
-  }
   // default: 4 rows in flight per wave (U = 2) up to 32 bytes per lane, 2 above. Flagship
   // 1000 × bf16 (32 bytes per lane) with the deferred tail, round 3: U=2 on 256 blocks 38.97 µs
   // vs U=1 on 512 blocks 40.09 µs (ops/glm.py round_blocks picks the grid; round 1, before the
@@ -1976,55 +1377,8 @@ FMLX_API int fmlx_glm_set_tuning(long lds_pad, int nt) {
 // diagnostics: launches record per-block timestamps into trace[nblocks][4] (null: off)
 FMLX_API void fmlx_glm_set_trace(void* trace) { g_trace = (long long*)trace; }
 
-// dynamic row schedule of the deferred fused round: on/off and log2(rows per chunk)
-// static row schedule's block → row-stripe mapping (ROWMAP_*; A/B knob)
-FMLX_API int fmlx_glm_set_rowmap(int m) {
-  if (m < ROWMAP_BLOCK || m > ROWMAP_WAVE) return -1;
-  g_rowmap = m;
-  return 0;
-}
-
-FMLX_API int fmlx_glm_set_dyn(int on, int lg) {
-  if (lg < 3 || lg > 10) return -1;
-  g_dyn = on;
-  g_dyn_lg = lg;
-  return 0;
-}
-
-// diagnostics of the dynamic schedule: vmcnt(0) before claim results are read; per-row visit
-// counters (int32[batch rows], null = off)
-FMLX_API void fmlx_glm_set_dyn_debug(int sync, void* dbg) {
-  g_dyn_sync = sync;
-  g_dyn_dbg = (int*)dbg;
-}
-FMLX_API void fmlx_glm_set_dyn_debug2(void* dbg2) { g_dyn_dbg2 = (int*)dbg2; }
-
-// ints of the fused round's counter block: tickets (TAIL_TOP + 1, padded to 128) + the dynamic
-// schedule's [2][DYN_HEADS][DYN_HSTRIDE] chunk counters
-FMLX_API int fmlx_glm_cnt_elems() { return 128 + PAIR_OFF + 2 * PAIR_NH_MAX * PAIR_STRIDE; }
-
-// tail prefetch of the deferred fused round (see PF_MAX): rows per wave (0 = off) and the
-// s_memrealtime ticks (10 ns) after a block's start past which its waves skip it
-FMLX_API int fmlx_glm_set_prefetch(int rows, int stop_q) {
-  if (rows < 0 || rows > PF_MAX || stop_q < 1) return -1;
-  g_pf = rows;
-  g_pf_stop = stop_q;
-  return 0;
-}
-
-// deferred flat tail: per-XCD replicas with L2-performed (workgroup-scope) atomics
-FMLX_API int fmlx_glm_set_l2acc(int on) {
-  g_l2acc = on;
-  return 0;
-}
-
-// pair schedule of the deferred fused round: on/off and the static fraction (1/256 units)
-FMLX_API int fmlx_glm_set_pairs(int on, int q) {
-  if (q < 0 || q > 256) return -1;
-  g_pairs = on;
-  g_pair_q = q;
-  return 0;
-}
+// ints of the fused round's counter block: the arrival tickets (TAIL_TOP + 1, padded to 128)
+FMLX_API int fmlx_glm_cnt_elems() { return 128; }
 
 FMLX_API int fmlx_glm_set_tail_tuning(int acc_reps, int ticket2) {
   if (acc_reps < 1 || acc_reps > ACC_MAX_REPS) return -1;
@@ -2080,10 +1434,6 @@ FMLX_API int fmlx_glm_round(int dtype, int epc, int cpl, int u, const void* X, l
   tl.defer = defer;
   tl.cw = cw;
   tl.trace = g_trace;
-  tl.dyn_sync = g_dyn_sync;
-  tl.dyn_dbg = g_dyn_dbg;
-  tl.dyn_dbg2 = g_dyn_dbg2;
-  tl.heads = (flags & 2) && cnt ? cnt + 128 : nullptr;  // flags bit 1: cnt has fmlx_glm_cnt_elems ints
   // `rounds` consecutive rounds, one launch each (a kernel boundary, ~1.5 µs, is cheaper than an
   // in-kernel grid-wide round barrier: measured, scripts/stream_probe2.hip)
   for (int i = 0; i < (rounds > 0 ? rounds : 1); ++i) {

@@ -16,9 +16,9 @@ from . import native
 LOSS_CODES = {"logistic": 0, "hinge": 1, "leastsquare": 2, "ftrl": 3}
 MAX_CPL = 8
 WPB = 8
-# row loop of the round kernel (A/B knob): 0 = default for the shape (row-at-a-time, U = 1 from
-# 32 bytes per lane, else 2), U > 0 = row-at-a-time with 2·U rows in flight per wave, -4 / -8 =
-# the grouped loop (bf16: 4 / 8 rows per step share one transposed reduction and loss pass)
+# row loop of the round kernel (A/B knob): 0 = default for the shape (U = 2 up to 32 bytes per
+# lane, else 1), U > 0 = 2·U rows in flight per wave. (The grouped loop, -4 / -8, measured slower
+# on the flagship shape — 40.6 / 42.2 vs 37.9 µs — and was removed in round 4.)
 GRAD_UNROLL = int(os.environ.get("FMLX_GLM_UNROLL", "0"))
 # 512 blocks x 8 waves = 4 waves per SIMD (the 128-VGPR cap of the flagship layout): interleaved
 # A/B at 10M x 1000 bf16 on one MI355X, 3 repeats (profiles/r2/lr_grid_ab_1gpu.log): 41.0 µs per
@@ -57,87 +57,6 @@ def set_tail_tuning(acc_reps: int = 4, ticket2: bool = False) -> None:
     """A/B knobs of the atomic round tail: accumulator replicas (block b adds into replica
     b mod reps) and two-level arrival tickets."""
     native.call("fmlx_glm_set_tail_tuning", int(acc_reps), int(bool(ticket2)))
-
-
-# deferred fused rounds: dynamic row schedule (csrc/glm.hip DynLds) instead of the static row
-# stride; FMLX_GLM_DYN=1/0 (the process-wide default, applied when the first round scratch is made).
-# Off by default: exact (every row once, profiles/r3/lr_dyn_schedule_row_census.jsonl) but slower at
-# the flagship shape — 56.2 vs 39.6 µs per round (profiles/r3/lr_dyn_schedule_ab_1gpu.jsonl): the
-# chunk claims' device-scope atomics return in microseconds under full HBM streaming, and the
-# claiming wave waits for them once per chunk it owns, which costs more than the XCD imbalance
-# (≈4 µs) the schedule removes.
-DYN_DEFAULT = os.environ.get("FMLX_GLM_DYN", "0") == "1"
-_dyn_set = False
-
-
-def set_dyn(on: bool = True, chunk_rows: int = 8) -> None:
-    """A/B knob of the deferred fused round's dynamic row schedule (csrc/glm.hip DynLds): on/off
-    (``chunk_rows`` is kept for the A/B scripts; the kernel's chunk is WPB·DYN_K rows)."""
-    global _dyn_set
-    lg = int(chunk_rows).bit_length() - 1
-    if chunk_rows != 1 << lg or native.kernels().fmlx_glm_set_dyn(int(bool(on)), lg) != 0:
-        raise ValueError("chunk_rows must be a power of two in [8, 1024]")
-    _dyn_set = True
-
-
-ROWMAP_BLOCK, ROWMAP_XCD, ROWMAP_WAVE = 0, 1, 2
-
-
-# deferred fused rounds: pair schedule (csrc/glm.hip PAIR_NH_MAX) — static rows for the first
-# PAIR_STATIC of the batch, then adjacent row pairs claimed from 64 XCD-mixed counters.
-# FMLX_GLM_PAIRS=1/0 and FMLX_GLM_PAIR_STATIC (fraction) set the process-wide default. Off by
-# default: exact (tests/test_xgmi_gpu.py::test_pair_schedule_*) and it evens out the per-XCD
-# means (34.7-35.6 us vs 31.7-34.0), but the claimed rows cost more than they save: 39.2-39.8 vs
-# 38.95 us per round at the flagship shape (profiles/r3/lr_pair_schedule_ab_1gpu.jsonl; block
-# timeline lr_pair_schedule_block_timeline.jsonl: median block done 35.4 vs 33.3 us).
-PAIRS_DEFAULT = os.environ.get("FMLX_GLM_PAIRS", "0") == "1"
-PAIR_STATIC = float(os.environ.get("FMLX_GLM_PAIR_STATIC", "0.8"))
-
-
-def set_pairs(on: bool = True, static_frac: float = PAIR_STATIC) -> None:
-    """A/B knob of the deferred fused round's pair schedule: on/off and the static fraction of
-    the batch (the rest is claimed in row pairs)."""
-    global _pairs_set
-    q = int(round(float(static_frac) * 256))
-    if native.kernels().fmlx_glm_set_pairs(int(bool(on)), q) != 0:
-        raise ValueError("static_frac must be in [0, 1]")
-    _pairs_set = True
-
-
-_pairs_set = False
-
-
-def set_l2acc(on: bool) -> None:
-    """A/B knob of the deferred flat tail: accumulate into one replica per XCD with atomics
-    performed in that XCD's L2 (workgroup scope) instead of device-scope atomics."""
-    native.call("fmlx_glm_set_l2acc", int(bool(on)))
-
-
-# deferred fused rounds: tail prefetch of the next round's rows (csrc/glm.hip PF_MAX).
-# FMLX_GLM_PF = rows per wave (0 = off), FMLX_GLM_PF_STOP_US = only waves done within this many
-# microseconds of their block's start prefetch. Off by default: exact, but 39.7-41.1 vs 39.5 us per
-# round at the flagship shape (profiles/r3/lr_tail_prefetch_timegated_ab_1gpu.jsonl).
-PF_ROWS = int(os.environ.get("FMLX_GLM_PF", "0"))
-PF_STOP_US = float(os.environ.get("FMLX_GLM_PF_STOP_US", "34"))
-_pf_set = False
-
-
-def set_prefetch(rows: int, stop_us: float = PF_STOP_US) -> None:
-    """A/B knob of the deferred fused round: after its gradient is issued, a wave done within
-    ``stop_us`` of its block's start reads the first ``rows`` (<= 8) rows it will own in the next
-    round (cache warm-up of the XCD's L2 / Infinity Cache while the stragglers finish)."""
-    global _pf_set
-    if native.kernels().fmlx_glm_set_prefetch(int(rows), max(1, int(round(float(stop_us) * 100)))) != 0:
-        raise ValueError("rows must be in [0, 8]")
-    _pf_set = True
-
-
-def set_rowmap(m: int) -> None:
-    """A/B knob of the static row schedule's block → row-stripe mapping (csrc/glm.hip ROWMAP_*):
-    0 = consecutive wave slots per block, 1 = one contiguous 1/8 of every stripe per XCD,
-    2 = a block's waves NB rows apart."""
-    if native.kernels().fmlx_glm_set_rowmap(int(m)) != 0:
-        raise ValueError("rowmap must be 0, 1 or 2")
 
 
 def set_trace(buf: Optional[torch.Tensor]) -> None:
@@ -200,7 +119,7 @@ def defer_supported(d: int, acc: torch.dtype) -> bool:
     """Deferred completion needs the flat atomic tail ([WPB][d] LDS image ≤ 64 KiB) and the
     row-at-a-time loop."""
     es = 8 if acc == torch.float64 else 4
-    return DEFER and not DETERMINISTIC and GRAD_UNROLL >= 0 and WPB * d * es <= 64 * 1024
+    return DEFER and not DETERMINISTIC and WPB * d * es <= 64 * 1024
 
 
 def max_round_blocks() -> int:
@@ -212,12 +131,6 @@ class RoundScratch:
     atomic accumulator, arrival tickets (all zero-initialised; the kernel re-arms them)."""
 
     def __init__(self, nparts: int, d: int, acc: torch.dtype, device, det: bool = None):
-        if not _dyn_set:
-            set_dyn(DYN_DEFAULT)
-        if not _pairs_set:
-            set_pairs(PAIRS_DEFAULT, PAIR_STATIC)
-        if not _pf_set:
-            set_prefetch(PF_ROWS, PF_STOP_US)
         self.nparts = nparts
         self.det = DETERMINISTIC if det is None else bool(det)
         if self.det:
@@ -228,7 +141,7 @@ class RoundScratch:
             self.stage1 = None
         # atomic tail: ACC_MAX_REPS replicas of the [d+2] accumulator on whole 256-B lines
         self.acc = torch.zeros(int(native.kernels().fmlx_glm_acc_elems(d)), dtype=acc, device=device)
-        # 64 group + 1 top tickets, then the dynamic row schedule's chunk counters (2 parities × 8)
+        # 64 group + 1 top tickets
         self.cnt = torch.zeros(int(native.kernels().fmlx_glm_cnt_elems()), dtype=torch.int32, device=device)
 
 
@@ -244,7 +157,6 @@ def glm_round(X, y, wt, coef, B: int, loss: int, state, scratch: RoundScratch, m
     and ``cw`` is the [2, d] coefficient ring."""
     epc, cpl = pick_layout(X)
     flags = 1 if X.shape[0] * X.stride(0) * X.element_size() > NT_MIN_BYTES else 0
-    flags |= 2  # scratch.cnt carries the dynamic schedule's counters
     if xg is not None:
         peers, world, rank, gen, err, spin = xg.kernel_args()
     else:

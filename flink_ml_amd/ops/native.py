@@ -58,13 +58,7 @@ _KERNEL_SIGS = {
     "fmlx_glm_set_tuning": [c_long, c_int],
     "fmlx_glm_set_tail_tuning": [c_int, c_int],
     "fmlx_glm_set_trace": [c_void_p],
-    "fmlx_glm_set_dyn": [c_int, c_int],
-    "fmlx_glm_set_rowmap": [c_int],
-    "fmlx_glm_set_pairs": [c_int, c_int],
-    "fmlx_glm_set_l2acc": [c_int],
     "fmlx_glm_cnt_elems": [],
-    "fmlx_glm_set_dyn_debug": ([c_int, c_void_p], None),
-    "fmlx_glm_set_dyn_debug2": ([c_void_p], None),
     "fmlx_glm_acc_elems": ([c_int], c_long),
     "fmlx_glm_reduce_update": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                c_double, c_double, c_double, c_double, c_void_p],

@@ -4,9 +4,7 @@
 
 Variants: ``u`` (rows in flight per wave = 2u), ``b`` (blocks = partial rows), ``split``
 (legacy 3-launch round: grad partials → stage-1 → reduce+update) vs the fused one-launch round,
-``defer`` (0: ticketed atomic tail; 1: round e − 1 completed in launch e's prologue), ``dyn`` /
-``ch`` (dynamic row schedule on/off, rows per claimed chunk), ``rm`` (static schedule's
-block → row-stripe mapping, glm.ROWMAP_*).
+``defer`` (0: ticketed atomic tail; 1: round e − 1 completed in launch e's prologue).
 Usage: python scripts/bench_glm_kernel.py --configs "u=2,b=512;u=4,b=256;split=1"
 """
 import argparse
@@ -78,11 +76,6 @@ def main():
             gk.DETERMINISTIC = bool(c.get("det", 0))
             gk.DEFER = bool(c.get("defer", 1))
             gk.set_tail_tuning(c.get("reps", 4), bool(c.get("t2", 0)))
-            gk.set_dyn(bool(c.get("dyn", 0)), c.get("ch", 8))
-            gk.set_rowmap(c.get("rm", 0))
-            gk.set_l2acc(bool(c.get("l2", 0)))
-            gk.set_pairs(bool(c.get("pairs", 0)), c.get("q", 205) / 256.0)
-            gk.set_prefetch(c.get("pf", 0), c.get("ps", 34))
             sgd = SGD(max_iter=10 ** 8, learning_rate=0.1, global_batch_size=a.batch, tol=0.0)
             cls = SplitTrainer if (c.get("split") or c.get("m0")) else DeviceGlmTrainer
             tr = cls(sgd, np.zeros(a.dim), X, y, None, "logistic", use_graph=True)

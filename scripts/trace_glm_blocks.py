@@ -30,13 +30,7 @@ def main():
     ap.add_argument("--batch", type=int, default=100_000)
     ap.add_argument("--rounds", type=int, default=20)
     ap.add_argument("--defer", type=int, default=1)
-    ap.add_argument("--rowmap", type=int, default=0, help="static schedule mapping (glm.ROWMAP_*)")
     a = ap.parse_args()
-    gk.set_rowmap(a.rowmap)
-    gk.set_l2acc(os.environ.get("TRACE_L2ACC", "0") == "1")
-    ap2 = os.environ.get("TRACE_PAIRS", "")
-    if ap2:
-        gk.set_pairs(True, float(ap2))
     dev = torch.device("cuda")
     gk.DEFER = bool(a.defer)
     g = torch.Generator(device=dev).manual_seed(1)

@@ -133,13 +133,14 @@ def test_fused_sgd_round_two_ranks_matches_host(xgmi_mode):
         assert b0 == r1[loss][2], loss  # replicas identical
 
 
-@pytest.mark.parametrize("det,blocks,unroll,defer", [(False, 256, 0, True), (False, 256, 0, False), (False, 256, -4, True),
-                                                     (False, 256, -8, True), (False, 256, 2, True), (False, 512, 0, True),
+@pytest.mark.parametrize("det,blocks,unroll,defer", [(False, 0, 0, True), (False, 0, 0, False), (False, 256, 0, True),
+                                                     (False, 256, 2, True), (False, 224, 4, True), (False, 512, 0, True),
                                                      (False, 512, 0, False), (True, 512, 0, True), (True, 256, 1, True)])
 def test_fused_round_flagship_shape_matches_torch(det, blocks, unroll, defer, monkeypatch):
-    """Fused rounds (TAIL_UPDATE) at the bench shape, bf16 rows: the bench's 512-block grid
-    (deferred and ticketed tails) and 256 blocks, the grouped row loop (8 / 4 rows per step) and the row-at-a-time loop, atomic
-    tail and the deterministic 16-group fixed-order tail."""
+    """Fused rounds (TAIL_UPDATE) at the bench shape, bf16 rows: the shipped default (blocks = 0 →
+    round_blocks(), unroll = 0 → the shape's row loop; deferred and ticketed tails), 224 / 256 /
+    512-block grids, 2 / 4 / 8 rows in flight per wave, atomic tail and the deterministic 16-group
+    fixed-order tail."""
     _need_gpu()
     from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
     from flink_ml_amd.ops import glm as gk
@@ -156,8 +157,8 @@ def test_fused_round_flagship_shape_matches_torch(det, blocks, unroll, defer, mo
     sgd = SGD(max_iter=3, learning_rate=0.1, global_batch_size=B, tol=1e-9)
     ref = TorchGlmTrainer(sgd, np.zeros(d), Xb.to(torch.float64), y, None, "logistic").fit()
     tr = DeviceGlmTrainer(sgd, np.zeros(d), Xb.cuda(), y.cuda(), None, "logistic", use_graph=False)
-    assert tr.nparts == blocks and tr.scratch.det == det
-    assert tr.defer == (defer and not det and unroll >= 0)
+    assert tr.nparts == (blocks or gk.round_blocks(tr.X)) and tr.scratch.det == det
+    assert tr.defer == (defer and not det)
     got = tr.fit()
     assert tr.rounds_executed() == 3
     assert np.allclose(got, ref, rtol=2e-4, atol=2e-6), np.abs(got - ref).max()
@@ -278,199 +279,56 @@ def test_deferred_rounds_match_ticketed_tail(rem, monkeypatch):
     assert np.allclose(out[True], out[False], rtol=1e-5, atol=1e-7), np.abs(out[True] - out[False]).max()
 
 
-@pytest.mark.parametrize("chunk", [8, 16, 64])
-@pytest.mark.parametrize("dtype,d", [("bf16", 520), ("fp32", 300)])
-def test_dynamic_schedule_covers_every_row_once(chunk, dtype, d, monkeypatch):
-    """The deferred round's dynamic row schedule (chunk claims + in-block draws, csrc/glm.hip
-    DynLds) must process every row of the round's batch exactly once, whatever the batch size:
-    all-static (fewer chunks than DYN_L·blocks), partial last chunk, drained counters + steals.
-    Integer row weights make Σweight (feedback[d]) an exact, order-independent row census."""
-    _need_gpu()
-    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer
-    from flink_ml_amd.ops import glm as gk
-
-    monkeypatch.setattr(gk, "DEFER", True)
-    monkeypatch.setattr(gk, "DETERMINISTIC", False)
-    gk.set_dyn(True, chunk)
-    try:
-        g = torch.Generator(device="cpu").manual_seed(9)
-        n = 157_003
-        X = torch.rand((n, d), generator=g)
-        X = X.to(torch.bfloat16) if dtype == "bf16" else X
-        y = torch.randint(0, 2, (n,), generator=g).to(torch.float32)
-        wt = (torch.arange(n) % 7 + 1).to(torch.float32)
-        for B in (1_000, 31_337, 157_003, 100_000):
-            tr = DeviceGlmTrainer(SGD(max_iter=4, learning_rate=0.1, global_batch_size=B, tol=0.0), np.zeros(d),
-                                  X.cuda(), y.cuda(), wt.cuda(), "logistic", use_graph=False)
-            assert tr.defer
-            P = -(-n // B)
-            tr._launch_round(1)  # round 0
-            for e in range(3):
-                tr._launch_round(1)  # launch e + 1 completes round e and publishes its feedback
-                torch.cuda.synchronize()
-                b0 = (e % P) * B
-                want = float(wt[b0:min(b0 + B, n)].sum())
-                got = float(tr.feedback[d].item())
-                assert got == want, (B, e, got, want)
-    finally:
-        gk.set_dyn(gk.DYN_DEFAULT, 8)
-
-
-@pytest.mark.parametrize("dyn", [True, False])
-def test_dynamic_schedule_matches_static(dyn, monkeypatch):
-    """Flagship-shape fit with the dynamic schedule on and off: same coefficients to rounding."""
-    _need_gpu()
-    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
-    from flink_ml_amd.ops import glm as gk
-
-    monkeypatch.setattr(gk, "DEFER", True)
-    gk.set_dyn(dyn, 8)
-    try:
-        g = torch.Generator(device="cpu").manual_seed(13)
-        n, d, B = 300_000, 1000, 100_000
-        Xb = torch.rand((n, d), generator=g).to(torch.bfloat16)
-        y = torch.randint(0, 2, (n,), generator=g).to(torch.float64)
-        sgd = SGD(max_iter=5, learning_rate=0.1, global_batch_size=B, tol=0.0)
-        ref = TorchGlmTrainer(sgd, np.zeros(d), Xb.to(torch.float64), y, None, "logistic").fit()
-        tr = DeviceGlmTrainer(sgd, np.zeros(d), Xb.cuda(), y.cuda(), None, "logistic", use_graph=True)
-        got = tr.fit()
-        assert tr.rounds_executed() == 5
-        assert np.allclose(got, ref, rtol=2e-4, atol=2e-6), np.abs(got - ref).max()
-    finally:
-        gk.set_dyn(gk.DYN_DEFAULT, 8)
-
-
-@pytest.mark.parametrize("frac", [0.0, 0.5, 0.8, 1.0])
 @pytest.mark.parametrize("dtype,d", [("bf16", 1000), ("bf16", 520), ("fp32", 300)])
-def test_pair_schedule_covers_every_row_once(frac, dtype, d, monkeypatch):
-    """The deferred round's pair schedule (static prefix + claimed row pairs, csrc/glm.hip
-    PAIR_NH_MAX) processes every row of the batch exactly once for any batch size and static
-    fraction (all claimed, all static, odd pools, fewer pairs than waves). Integer row weights
-    make Σweight (feedback[d]) an exact, order-independent row census."""
+def test_round_covers_every_row_once(dtype, d, monkeypatch):
+    """The deferred round's row schedule at the shipped grid processes every row of the round's
+    batch exactly once for any batch size (fewer rows than wave slots, a partial last step, the
+    whole set). Integer row weights make Σweight (feedback[d]) an exact, order-independent row
+    census of each round."""
     _need_gpu()
     from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer
     from flink_ml_amd.ops import glm as gk
 
     monkeypatch.setattr(gk, "DEFER", True)
     monkeypatch.setattr(gk, "DETERMINISTIC", False)
-    gk.set_dyn(False, 8)
-    gk.set_pairs(True, frac)
-    try:
-        g = torch.Generator(device="cpu").manual_seed(9)
-        n = 157_003
-        X = torch.rand((n, d), generator=g)
-        X = X.to(torch.bfloat16) if dtype == "bf16" else X
-        y = torch.randint(0, 2, (n,), generator=g).to(torch.float32)
-        wt = (torch.arange(n) % 7 + 1).to(torch.float32)
-        for B in (1_000, 31_337, 157_003, 100_000):
-            tr = DeviceGlmTrainer(SGD(max_iter=6, learning_rate=0.1, global_batch_size=B, tol=0.0), np.zeros(d),
-                                  X.cuda(), y.cuda(), wt.cuda(), "logistic", use_graph=False)
-            assert tr.defer
-            P = -(-n // B)
-            tr._launch_round(1)  # round 0
-            for e in range(5):  # both launch parities twice: the counters are re-armed
-                tr._launch_round(1)  # launch e + 1 completes round e and publishes its feedback
-                torch.cuda.synchronize()
-                b0 = (e % P) * B
-                want = float(wt[b0:min(b0 + B, n)].sum())
-                got = float(tr.feedback[d].item())
-                assert got == want, (B, e, got, want)
-    finally:
-        gk.set_pairs(gk.PAIRS_DEFAULT, gk.PAIR_STATIC)
-        gk.set_dyn(gk.DYN_DEFAULT, 8)
-
-
-@pytest.mark.parametrize("pairs", [True, False])
-def test_pair_schedule_matches_torch(pairs, monkeypatch):
-    """Flagship-shape fit (graph-captured deferred rounds) with the pair schedule on and off
-    against the fp64 torch reference."""
-    _need_gpu()
-    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
-    from flink_ml_amd.ops import glm as gk
-
-    monkeypatch.setattr(gk, "DEFER", True)
-    gk.set_pairs(pairs, 0.8)
-    try:
-        g = torch.Generator(device="cpu").manual_seed(13)
-        n, d, B = 300_000, 1000, 100_000
-        Xb = torch.rand((n, d), generator=g).to(torch.bfloat16)
-        y = torch.randint(0, 2, (n,), generator=g).to(torch.float64)
-        sgd = SGD(max_iter=7, learning_rate=0.1, global_batch_size=B, tol=0.0)
-        ref = TorchGlmTrainer(sgd, np.zeros(d), Xb.to(torch.float64), y, None, "logistic").fit()
-        tr = DeviceGlmTrainer(sgd, np.zeros(d), Xb.cuda(), y.cuda(), None, "logistic", use_graph=True)
-        got = tr.fit()
-        assert tr.rounds_executed() == 7
-        assert np.allclose(got, ref, rtol=2e-4, atol=2e-6), np.abs(got - ref).max()
-    finally:
-        gk.set_pairs(gk.PAIRS_DEFAULT, gk.PAIR_STATIC)
-
-
-@pytest.mark.parametrize("l2acc", [True, False])
-def test_l2_replica_tail_matches_torch(l2acc, monkeypatch):
-    """Deferred rounds with the per-XCD L2-performed accumulator replicas (and without) against
-    the fp64 torch reference, plus an exact row census through integer weights."""
-    _need_gpu()
-    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
-    from flink_ml_amd.ops import glm as gk
-
-    monkeypatch.setattr(gk, "DEFER", True)
-    monkeypatch.setattr(gk, "DETERMINISTIC", False)
-    gk.set_l2acc(l2acc)
-    try:
-        g = torch.Generator(device="cpu").manual_seed(13)
-        n, d, B = 300_000, 1000, 100_000
-        Xb = torch.rand((n, d), generator=g).to(torch.bfloat16)
-        y = torch.randint(0, 2, (n,), generator=g).to(torch.float64)
-        sgd = SGD(max_iter=7, learning_rate=0.1, global_batch_size=B, tol=0.0)
-        ref = TorchGlmTrainer(sgd, np.zeros(d), Xb.to(torch.float64), y, None, "logistic").fit()
-        tr = DeviceGlmTrainer(sgd, np.zeros(d), Xb.cuda(), y.cuda(), None, "logistic", use_graph=True)
-        got = tr.fit()
-        assert tr.rounds_executed() == 7
-        assert np.allclose(got, ref, rtol=2e-4, atol=2e-6), np.abs(got - ref).max()
-        wt = (torch.arange(n) % 7 + 1).to(torch.float32)
+    g = torch.Generator(device="cpu").manual_seed(9)
+    n = 157_003
+    X = torch.rand((n, d), generator=g)
+    X = X.to(torch.bfloat16) if dtype == "bf16" else X
+    y = torch.randint(0, 2, (n,), generator=g).to(torch.float32)
+    wt = (torch.arange(n) % 7 + 1).to(torch.float32)
+    for B in (1_000, 31_337, 157_003, 100_000):
         tr = DeviceGlmTrainer(SGD(max_iter=6, learning_rate=0.1, global_batch_size=B, tol=0.0), np.zeros(d),
-                              Xb.cuda(), y.float().cuda(), wt.cuda(), "logistic", use_graph=False)
-        tr._launch_round(1)
-        for e in range(4):
-            tr._launch_round(1)
+                              X.cuda(), y.cuda(), wt.cuda(), "logistic", use_graph=False)
+        assert tr.defer
+        P = -(-n // B)
+        tr._launch_round(1)  # round 0
+        for e in range(5):  # both launch parities twice
+            tr._launch_round(1)  # launch e + 1 completes round e and publishes its feedback
             torch.cuda.synchronize()
-            b0 = (e % 3) * B
-            assert float(tr.feedback[d].item()) == float(wt[b0:b0 + B].sum())
-    finally:
-        gk.set_l2acc(False)
+            b0 = (e % P) * B
+            want = float(wt[b0:min(b0 + B, n)].sum())
+            got = float(tr.feedback[d].item())
+            assert got == want, (B, e, got, want)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("pf", [0, 8])
-def test_tail_prefetch_matches_torch(pf, monkeypatch):
-    """Deferred rounds with the next-round tail prefetch (a cache hint only) against the fp64
-    torch reference, plus the exact per-round weight census through integer weights."""
+def test_shipped_default_graph_fit_matches_torch(monkeypatch):
+    """The shipped configuration exactly as bench.py runs it — default grid (round_blocks), default
+    row loop, deferred completion, hipGraph-captured rounds — against the fp64 torch reference."""
     _need_gpu()
     from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
     from flink_ml_amd.ops import glm as gk
 
-    monkeypatch.setattr(gk, "DEFER", True)
-    monkeypatch.setattr(gk, "DETERMINISTIC", False)
-    gk.set_prefetch(pf, 1e6)  # every wave prefetches
-    try:
-        g = torch.Generator(device="cpu").manual_seed(17)
-        n, d, B = 300_000, 1000, 100_000
-        Xb = torch.rand((n, d), generator=g).to(torch.bfloat16)
-        y = torch.randint(0, 2, (n,), generator=g).to(torch.float64)
-        sgd = SGD(max_iter=7, learning_rate=0.1, global_batch_size=B, tol=0.0)
-        ref = TorchGlmTrainer(sgd, np.zeros(d), Xb.to(torch.float64), y, None, "logistic").fit()
-        tr = DeviceGlmTrainer(sgd, np.zeros(d), Xb.cuda(), y.cuda(), None, "logistic", use_graph=True)
-        got = tr.fit()
-        assert tr.rounds_executed() == 7
-        assert np.allclose(got, ref, rtol=2e-4, atol=2e-6), np.abs(got - ref).max()
-        wt = (torch.arange(n) % 7 + 1).to(torch.float32)
-        tr = DeviceGlmTrainer(SGD(max_iter=6, learning_rate=0.1, global_batch_size=B, tol=0.0), np.zeros(d),
-                              Xb.cuda(), y.float().cuda(), wt.cuda(), "logistic", use_graph=False)
-        tr._launch_round(1)
-        for e in range(4):
-            tr._launch_round(1)
-            torch.cuda.synchronize()
-            b0 = (e % 3) * B
-            assert float(tr.feedback[d].item()) == float(wt[b0:b0 + B].sum())
-    finally:
-        gk.set_prefetch(0)
+    monkeypatch.setattr(gk, "GRAD_BLOCKS", 0)
+    monkeypatch.setattr(gk, "GRAD_UNROLL", 0)
+    g = torch.Generator(device="cpu").manual_seed(13)
+    n, d, B = 300_000, 1000, 100_000
+    Xb = torch.rand((n, d), generator=g).to(torch.bfloat16)
+    y = torch.randint(0, 2, (n,), generator=g).to(torch.float64)
+    sgd = SGD(max_iter=7, learning_rate=0.1, global_batch_size=B, tol=0.0)
+    ref = TorchGlmTrainer(sgd, np.zeros(d), Xb.to(torch.float64), y, None, "logistic").fit()
+    tr = DeviceGlmTrainer(sgd, np.zeros(d), Xb.cuda(), y.cuda(), None, "logistic", use_graph=True)
+    assert tr.defer and tr.nparts == gk.round_blocks(tr.X)
+    got = tr.fit()
+    assert tr.rounds_executed() == 7
+    assert np.allclose(got, ref, rtol=2e-4, atol=2e-6), np.abs(got - ref).max()
