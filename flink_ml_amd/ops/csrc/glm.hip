@@ -142,6 +142,7 @@ struct GlmTail {
   int parity;      // deferred: this launch reads its round number from state[parity ? ALT : ROUND]
   void* cw;        // deferred: [2][d] coefficients of the last two rounds
   int wl_off;      // deferred: byte offset of the block's [d] coefficient image in LDS
+  int ring_off;    // LDS-DMA row path: byte offset of the [WPB][DEPTH][U][2 KiB] row ring
   long long* trace;  // diagnostics (null = off): per block {start, rows done, end, hw id} in
                      // 100 MHz s_memrealtime ticks (scripts/trace_glm_blocks.py)
 };
@@ -437,11 +438,25 @@ __device__ __forceinline__ float seg_sum_dpp(float v) {
   return v;
 }
 
-// register-light shapes are capped at 128 VGPRs (4 waves per SIMD) so that two 8-wave blocks
-// share a CU; heavier ones (which would spill under the cap) keep the compiler's choice
+// register-light shapes with one row per step are capped at 128 VGPRs (4 waves per SIMD) so
+// that two 8-wave blocks share a CU (the 512-block grids); U >= 2 runs one block per CU (the
+// flagship's 224 blocks: 2 waves per SIMD) and keeps the compiler's choice — under the 128 cap
+// the paired row loop spills to scratch, and every spill reload is a vmcnt(0) in the loop
 template <typename T, int EPC, int CPL, int U>
 constexpr int glm_min_waves() {
-  return CPL * EPC * (int)sizeof(T) * U <= 64 ? 4 : 1;
+  return (U == 1 && CPL * EPC * (int)sizeof(T) <= 64) || (U == 2 && CPL * EPC * (int)sizeof(T) <= 16) ? 4 : 1;
+}
+
+// One 16-byte-per-lane LDS-DMA load (global_load_lds_dwordx4 … nt): lane i's 16 bytes land at LDS
+// byte address lds + 16·i; no VGPR is written, the load counts in vmcnt and the caller waits for
+// it itself (hipcc does not count asm loads). M0 (the LDS base) is compiler-reserved: saved and
+// restored inside the same statement (cdna_hip_programming.md §5.7, LDS-DMA recipe).
+__device__ __forceinline__ void dma16_nt(const void* g, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(lds)
+               : "memory");
 }
 
 // X / y / wt are deliberately NOT __restrict__: with restrict the compiler may move the row
@@ -452,7 +467,7 @@ constexpr int glm_min_waves() {
 // on the flagship shape — a dynamic chunk-claim schedule, claimed row pairs after a static prefix,
 // per-XCD L2 accumulator replicas, and a tail prefetch of the next round's rows; all exact, all
 // slower: profiles/r3/lr_{dyn_schedule,pair_schedule,l2acc,tail_prefetch_timegated}_ab_1gpu.jsonl.)
-template <typename T, int EPC, int CPL, int U, int WPB, bool NT>
+template <typename T, int EPC, int CPL, int U, int WPB, bool NT, int DEPTH = 0>
 __global__ __launch_bounds__(WPB * 64, (glm_min_waves<T, EPC, CPL, U>())) void glm_round_kernel(
     const T* X, long ld, const typename AccOf<T>::type* y,
     const typename AccOf<T>::type* wt, typename AccOf<T>::type* coef,
@@ -653,37 +668,121 @@ __global__ __launch_bounds__(WPB * 64, (glm_min_waves<T, EPC, CPL, U>())) void g
       }
     }
   };
+  if constexpr (DEPTH > 0) {
+    // ---- LDS-DMA row path (bf16 rows of 65–128 16-byte chunks). Each wave owns a ring of DEPTH
+    // steps × U rows × 2 KiB in LDS; row loads are global_load_lds_dwordx4 … nt (two per row:
+    // chunks lane and lane + 64), so DEPTH − 1 steps stay in flight through the math whatever
+    // the registers hold, and the loads never write VGPRs (the streaming probe: 31.7 µs per 200 MB
+    // batch vs 33.3 for 16-byte register loads, profiles/r4/lr_probe_lds.log). A step's rows are
+    // read back with ds_read_b128 into the same per-lane chunk layout the register path uses.
+    static_assert(sizeof(T) == 2 && EPC == 8 && CPL == 2, "LDS-DMA ring: bf16 rows of 65-128 chunks");
+    extern __shared__ __align__(16) unsigned char smem_r[];
+    typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) u32x4_t lds_u4_t;
+    unsigned char* ring_w = smem_r + tl.ring_off + (long)wave * (DEPTH * U * 2048);
+    const unsigned ring_a = __builtin_amdgcn_readfirstlane((unsigned)(size_t)ring_w);
+    const long nrw = r_first < end ? (end - r_first + W - 1) / W : 0;  // rows of this wave
+    const long nst = (nrw + U - 1) / U;                                 // steps of this wave
+    const int c1 = lane + 64 < nch ? lane + 64 : nch - 1;
+    auto issue = [&](long t) {
+      const unsigned base = ring_a + (unsigned)((t % DEPTH) * U) * 2048u;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        long ru = r_first + (t * U + u) * W;
+        ru = ru < end ? ru : r_first;  // past the wave's rows: a valid row again, masked below
+        const T* row = X + ru * ld;
+        dma16_nt(row + lane * EPC, base + u * 2048u);
+        dma16_nt(row + c1 * EPC, base + u * 2048u + 1024u);
+      }
+    };
+    auto read = [&](long t, Chunk<T, EPC> (&x)[U][CPL], A (&yy)[U], A (&ww)[U], bool (&vv)[U]) {
+      const long j0 = t * U;
+      if ((j0 & 63) == 0 && j0 > 0) load_labels(j0);
+      const unsigned char* sl = ring_w + (t % DEPTH) * U * 2048;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+          const u32x4_t v = *(const lds_u4_t*)(sl + u * 2048 + k * 1024 + lane * 16);
+          __builtin_memcpy(x[u][k].v, &v, 16);
+        }
+        vv[u] = j0 + u < nrw;
+        yy[u] = lane_val(ylab, (int)((j0 + u) & 63));
+        ww[u] = lane_val(wlab, (int)((j0 + u) & 63));
+      }
+    };
+    if (nst > 0) {
+      load_labels(0);
+#pragma unroll
+      for (int t = 0; t < DEPTH - 1; ++t)
+        if (t < nst) issue(t);
+    }
+    if (tl.defer && defer_prologue<A>(tl, coef, state, e, d, wdef)) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the wave exits
+      return;
+    }
+    if (nst > 0) {
+      load_w();
+      for (long t = 0; t < nst; ++t) {
+        // step t + DEPTH − 1 goes into the slot step t − 1 was read from (its ds_reads are done:
+        // their values fed step t − 1's math)
+        if (t + DEPTH - 1 < nst) {
+          issue(t + DEPTH - 1);
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * U * (DEPTH - 1)) : "memory");  // step t landed
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        read(t, xa, ya, wa, va);
+        process(xa, ya, wa, va);
+      }
+    }
+    // the epilogue's LDS buffers alias the ring: every wave of the block is past its last read
+    __syncthreads();
+  } else {
   const long step = (long)U * W;
   long r = start + gw;
-  long j = 0;
-  if (r < end) {
+  // steps of U rows this wave owns; the loop runs them in pairs (xa, xb) with ONE exit test per
+  // pair at the latch. (A `break` after each half gives the structurizer a flow block whose
+  // conditional back edge carries the first half's pending loads into the header, where the
+  // waitcnt pass then puts a vmcnt(0) at the top of EVERY iteration: round 3's loop had it, so the
+  // next step's loads only went out once the current step had landed.)
+  const long nst = r < end ? ((end - r + W - 1) / W + U - 1) / U : 0;
+  if (nst > 0) {
+    // the first TWO steps go out before the deferred prologue, whose sc1 reads of the previous
+    // round's accumulator and SGD update take a few microseconds: HBM streams meanwhile
     load_labels(0);  // first: load_rows reads the labels right after issuing its row loads
     load_rows(r, 0, r, xa, ya, wa, va);
+    load_rows(r + step, U, r, xb, yb, wb, vb);
   }
   // deferred mode: complete the previous round while the first rows are in flight
   if (tl.defer && defer_prologue<A>(tl, coef, state, e, d, wdef)) return;
-  if (r < end) {
+  if (nst > 0) {
     load_w();
-    while (true) {
-      load_rows(r + step, j + U, r, xb, yb, wb, vb);
-      // pin the next batch's loads ahead of this batch's math: without the fences the compiler
-      // sinks them into the math (IR code motion, then the scheduler) to recycle registers and
-      // only ~1 row stays in flight per wave (measured: 47 µs vs a 33 µs streaming floor for
-      // the 200 MB batch). The asm is a compiler-only memory fence (no instruction, no wait).
+    // nothing in flight at the loop header but the back edge's own loads (the deferred prologue
+    // has already waited for these)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    long t = 0;
+    for (; t + 2 <= nst; t += 2) {
+      // steps t (xa) and t + 1 (xb) are loaded; a buffer's next step (t + 2, t + 3) goes out as
+      // soon as its math is done (rows past the wave's last one are clamped to a valid row and
+      // masked). The empty asm + sched_barrier pin each load batch between the two math blocks:
+      // without them the compiler sinks loads into the math to recycle registers.
+      process(xa, ya, wa, va);
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      process(xa, ya, wa, va);
-      r += step;
-      j += U;
-      if (r >= end) break;
-      load_rows(r + step, j + U, r, xa, ya, wa, va);
+      load_rows(r + 2 * step, (t + 2) * U, r, xa, ya, wa, va);
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       process(xb, yb, wb, vb);
-      r += step;
-      j += U;
-      if (r >= end) break;
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      load_rows(r + 3 * step, (t + 3) * U, r, xb, yb, wb, vb);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      r += 2 * step;
     }
+    if (t < nst) process(xa, ya, wa, va);  // odd step count: the last step is in xa
+  }
   }
 
   if (tl.trace) {
@@ -1251,18 +1350,19 @@ static long long* g_trace = nullptr;  // per-block timestamps of the next launch
 constexpr long LDS_PER_CU = 160 * 1024;
 constexpr int NUM_CU = 256;
 
-template <typename T, int EPC, int CPL, int U>
-int launch_grad_u(const void* X, long ld, const void* y, const void* wt, void* coef, long n, int d, long B, int loss,
-                  int* state, void* partials, int nblocks, const GlmTail& tl, int flags, hipStream_t s) {
+static int g_dma_depth = 0;  // LDS-DMA row ring depth in steps (0 = 16-byte register loads)
+
+template <typename T, int EPC, int CPL, int U, int DEPTH>
+int launch_grad_k(const void* X, long ld, const void* y, const void* wt, void* coef, long n, int d, long B, int loss,
+                  int* state, void* partials, int nblocks, GlmTail t2, bool nt, hipStream_t s) {
   typedef typename AccOf<T>::type A;
-  // [WPB/2][d] tree buffer (reused as the final block's feedback row) | [WPB][2] | ticket flag
-  GlmTail t2 = tl;
-  t2.nbatch = (n > 0 && B > 0) ? (int)((n + B - 1) / B) : 0;
-  t2.flat_lds = tl.mode != TAIL_PARTIALS && !tl.det && (size_t)WPB * d * sizeof(A) <= 64 * 1024;
-  size_t shmem = (size_t)(t2.flat_lds ? WPB : WPB / 2) * d * sizeof(A) + WPB * 2 * sizeof(A) + 16;
+  // epilogue LDS: [WPB or WPB/2][d] wave rows | [WPB][2] | ticket flag; the DMA ring (if any)
+  // starts at 0 and the epilogue buffers alias it; the deferred mode's w image follows both
+  const size_t tail = (size_t)(t2.flat_lds ? WPB : WPB / 2) * d * sizeof(A) + WPB * 2 * sizeof(A) + 16;
+  const size_t ring = (size_t)WPB * DEPTH * U * 2048;
+  size_t shmem = tail > ring ? tail : ring;
+  t2.ring_off = 0;
   if (t2.defer) {
-    // the deferred prologue needs the flat atomic tail
-    if (!t2.flat_lds || tl.mode != TAIL_UPDATE || tl.det || tl.cw == nullptr) return -7;
     t2.wl_off = (int)((shmem + 15) & ~(size_t)15);
     shmem = (size_t)t2.wl_off + (size_t)d * sizeof(A);
   }
@@ -1275,17 +1375,45 @@ int launch_grad_u(const void* X, long ld, const void* y, const void* wt, void* c
       if (shmem < want) shmem = want;
     }
   }
-  const bool nt = g_nt >= 0 ? g_nt != 0 : (flags & 1) != 0;
+  if (shmem > (size_t)LDS_PER_CU) return -8;
   if constexpr (EPC * sizeof(T) == 16 && sizeof(T) == 2) {
     if (nt) {
-      hipLaunchKernelGGL((glm_round_kernel<T, EPC, CPL, U, WPB, true>), dim3(nblocks), dim3(WPB * 64), shmem, s,
+      hipLaunchKernelGGL((glm_round_kernel<T, EPC, CPL, U, WPB, true, DEPTH>), dim3(nblocks), dim3(WPB * 64), shmem, s,
                          (const T*)X, ld, (const A*)y, (const A*)wt, (A*)coef, n, d, B, loss, state, (A*)partials, t2);
       return (int)hipGetLastError();
     }
   }
-  hipLaunchKernelGGL((glm_round_kernel<T, EPC, CPL, U, WPB, false>), dim3(nblocks), dim3(WPB * 64), shmem, s,
-                     (const T*)X, ld, (const A*)y, (const A*)wt, (A*)coef, n, d, B, loss, state, (A*)partials, t2);
-  return (int)hipGetLastError();
+  if constexpr (DEPTH == 0) {
+    hipLaunchKernelGGL((glm_round_kernel<T, EPC, CPL, U, WPB, false>), dim3(nblocks), dim3(WPB * 64), shmem, s,
+                       (const T*)X, ld, (const A*)y, (const A*)wt, (A*)coef, n, d, B, loss, state, (A*)partials, t2);
+    return (int)hipGetLastError();
+  }
+  return -9;
+}
+
+template <typename T, int EPC, int CPL, int U>
+int launch_grad_u(const void* X, long ld, const void* y, const void* wt, void* coef, long n, int d, long B, int loss,
+                  int* state, void* partials, int nblocks, const GlmTail& tl, int flags, hipStream_t s) {
+  typedef typename AccOf<T>::type A;
+  GlmTail t2 = tl;
+  t2.nbatch = (n > 0 && B > 0) ? (int)((n + B - 1) / B) : 0;
+  t2.flat_lds = tl.mode != TAIL_PARTIALS && !tl.det && (size_t)WPB * d * sizeof(A) <= 64 * 1024;
+  // the deferred prologue needs the flat atomic tail
+  if (t2.defer && (!t2.flat_lds || tl.mode != TAIL_UPDATE || tl.det || tl.cw == nullptr)) return -7;
+  const bool nt = g_nt >= 0 ? g_nt != 0 : (flags & 1) != 0;
+  // LDS-DMA ring: bf16 rows of 65–128 16-byte chunks (d 513–1024), 16-byte aligned, non-temporal
+#ifndef FMLX_ISA_PROBE_U
+  if constexpr (sizeof(T) == 2 && EPC == 8 && CPL == 2) {
+    if (g_dma_depth > 0 && nt) {
+      switch (g_dma_depth) {
+        case 2: return launch_grad_k<T, EPC, CPL, U, 2>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, t2, nt, s);
+        case 3: return launch_grad_k<T, EPC, CPL, U, 3>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, t2, nt, s);
+        default: return launch_grad_k<T, EPC, CPL, U, 4>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, t2, nt, s);
+      }
+    }
+  }
+#endif
+  return launch_grad_k<T, EPC, CPL, U, 0>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, t2, nt, s);
 }
 
 // rows in flight per wave = 2·U (software pipeline); u == 0 picks the default for the shape
@@ -1298,6 +1426,9 @@ int launch_grad(int u, const void* X, long ld, const void* y, const void* wt, vo
   // vs U=1 on 512 blocks 40.09 µs (ops/glm.py round_blocks picks the grid; round 1, before the
   // deferred tail, had measured U=1 faster: 37.9 vs 39.1 µs)
   if (u <= 0) u = BYTES <= 32 ? 2 : 1;
+#ifdef FMLX_ISA_PROBE_U  // one row-loop variant only (ISA inspection)
+  return launch_grad_u<T, EPC, CPL, FMLX_ISA_PROBE_U>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
+#endif
   if (u >= 4 && BYTES <= 32)
     return launch_grad_u<T, EPC, CPL, 4>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
   if (u >= 2 && BYTES <= 64)
@@ -1305,6 +1436,7 @@ int launch_grad(int u, const void* X, long ld, const void* y, const void* wt, vo
   return launch_grad_u<T, EPC, CPL, 1>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
 }
 
+#ifndef FMLX_ISA_PROBE
 template <typename T, int EPC>
 int launch_grad_cpl(int cpl, int u, const void* X, long ld, const void* y, const void* wt, void* coef, long n, int d,
                     long B, int loss, int* state, void* partials, int nblocks, const GlmTail& tl, int flags,
@@ -1321,9 +1453,6 @@ int launch_grad_cpl(int cpl, int u, const void* X, long ld, const void* y, const
 int launch_round(int dtype, int epc, int cpl, int u, const void* X, long ld, const void* y, const void* wt, void* coef,
                  long n, int d, long B, int loss, int* state, void* partials, int nblocks, const GlmTail& tl, int flags,
                  hipStream_t s) {
-#ifdef FMLX_ISA_PROBE  // ISA inspection builds: the flagship instantiation only
-  return launch_grad<bf16_t, 8, 2>(u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
-#endif
   if (dtype == DT_BF16) {
     if (epc == 8) return launch_grad_cpl<bf16_t, 8>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
     if (epc == 4) return launch_grad_cpl<bf16_t, 4>(cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
@@ -1364,7 +1493,16 @@ int launch_pred_cpl(int cpl, const void* X, long ld, long n, int d, const void* 
   return -1;
 }
 
+#endif  // FMLX_ISA_PROBE
 }  // namespace
+
+#ifdef FMLX_ISA_PROBE
+// ISA inspection builds (hipcc --offload-device-only -S -DFMLX_ISA_PROBE): only the flagship round
+// kernel's variants are instantiated, so the .s comes out in seconds, not minutes
+FMLX_API int fmlx_glm_isa_probe(int u, const void* X, long ld, const void* y, void* coef, int* state, const GlmTail* tl) {
+  return launch_grad<bf16_t, 8, 2>(u, X, ld, y, nullptr, coef, 1, 1000, 1, 0, state, nullptr, 224, *tl, 1, 0);
+}
+#else
 
 // epc = elements per 16/8/4/2-byte chunk chosen by the host so that d % epc == 0 and rows are
 // aligned; cpl = chunks per lane (power of two, 64*cpl*epc >= d).
@@ -1379,6 +1517,13 @@ FMLX_API void fmlx_glm_set_trace(void* trace) { g_trace = (long long*)trace; }
 
 // ints of the fused round's counter block: the arrival tickets (TAIL_TOP + 1, padded to 128)
 FMLX_API int fmlx_glm_cnt_elems() { return 128; }
+
+// LDS-DMA row ring of the fused round (bf16 rows of d 513–1024): depth in steps, 0 = off
+FMLX_API int fmlx_glm_set_dma(int depth) {
+  if (depth < 0 || depth > 4 || depth == 1) return -1;
+  g_dma_depth = depth;
+  return 0;
+}
 
 FMLX_API int fmlx_glm_set_tail_tuning(int acc_reps, int ticket2) {
   if (acc_reps < 1 || acc_reps > ACC_MAX_REPS) return -1;
@@ -1622,3 +1767,4 @@ FMLX_API int fmlx_glm_csr_predict(int acc_f64, const long* indptr, const int* id
                        (const float*)coef, n, dots);
   return (int)hipGetLastError();
 }
+#endif  // FMLX_ISA_PROBE

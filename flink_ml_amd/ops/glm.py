@@ -59,6 +59,18 @@ def set_tail_tuning(acc_reps: int = 4, ticket2: bool = False) -> None:
     native.call("fmlx_glm_set_tail_tuning", int(acc_reps), int(bool(ticket2)))
 
 
+# LDS-DMA row ring of the fused round (csrc/glm.hip, DEPTH): bf16 rows of d 513–1024 stream into a
+# per-wave LDS ring by global_load_lds (DEPTH − 1 steps of U rows in flight through the math).
+# FMLX_GLM_DMA = ring depth in steps (0 = 16-byte register loads).
+DMA_DEPTH = int(os.environ.get("FMLX_GLM_DMA", "0"))
+
+
+def set_dma(depth: int) -> None:
+    """Ring depth of the fused round's LDS-DMA row path (0 = off; 2–4 steps)."""
+    if native.kernels().fmlx_glm_set_dma(int(depth)) != 0:
+        raise ValueError("depth must be 0, 2, 3 or 4")
+
+
 def set_trace(buf: Optional[torch.Tensor]) -> None:
     """Diagnostics: fused-round launches write per-block {start, rows done, atomics drained, hw
     id} s_memrealtime stamps (100 MHz) into ``buf`` (int64 [blocks, 4]); None switches off."""
@@ -126,11 +138,18 @@ def max_round_blocks() -> int:
     return TAIL_MAX_BLOCKS if DETERMINISTIC else TAIL_MAX_BLOCKS_ATOMIC
 
 
+_dma_applied = False
+
+
 class RoundScratch:
     """Device scratch of one fused round: block partials / group rows (deterministic tail), the
     atomic accumulator, arrival tickets (all zero-initialised; the kernel re-arms them)."""
 
     def __init__(self, nparts: int, d: int, acc: torch.dtype, device, det: bool = None):
+        global _dma_applied
+        if not _dma_applied:
+            set_dma(DMA_DEPTH)
+            _dma_applied = True
         self.nparts = nparts
         self.det = DETERMINISTIC if det is None else bool(det)
         if self.det:
@@ -194,6 +213,48 @@ def grad_csr(indptr, idx, val, y, wt, coef, n, d, B, loss, state, grad) -> None:
 # sparse rounds through per-batch transposes (csrc/glm.hip glm_csc_bwd_kernel)
 CSC_MAX_BYTES = int(os.environ.get("FMLX_CSC_MAX_BYTES", str(8 << 30)))
 CSC_RUN_MAX = int(os.environ.get("FMLX_CSC_RUN_MAX", "16"))  # consecutive batches transposed per sort
+
+
+def seg_sort_passes(key_bits: int) -> int:
+    """Digit passes of ``seg_sort`` (digits of <= 11 bits, balanced)."""
+    return -(-int(key_bits) // 11)
+
+
+def seg_sort_scratch(bounds, key_bits: int) -> int:
+    import numpy as np
+
+    b = np.ascontiguousarray(np.asarray(bounds, dtype=np.int64))
+    need = int(native.kernels().fmlx_seg_sort_scratch(b.ctypes.data, len(bounds) - 1, int(key_bits), 11))
+    if need < 0:
+        raise ValueError("seg_sort: bad segment table (S=%d, key_bits=%d)" % (len(bounds) - 1, key_bits))
+    return max(need, 1)
+
+
+def seg_sort(keys: torch.Tensor, vals: torch.Tensor, bounds, kbase, key_bits: int, keys_alt=None, vals_alt=None,
+             scratch=None):
+    """Stable segmented LSD radix sort (csrc/radix.hip, no library sort) of int32 ``keys`` with
+    int32 / int64 payloads ``vals``: segment s = positions [bounds[s], bounds[s + 1]) is sorted by
+    the low ``key_bits`` bits of (key − kbase[s]); equal keys keep their input order. The passes
+    ping-pong between (keys, vals) and (keys_alt, vals_alt), so the inputs are overwritten; the
+    sorted pair ends in the alt buffers when ``seg_sort_passes(key_bits)`` is odd. Returns the
+    sorted (keys, vals). Pre-allocated ``keys_alt`` / ``vals_alt`` / ``scratch`` (int32,
+    ``seg_sort_scratch``) make the call allocation-free (hipGraph capture)."""
+    import numpy as np
+
+    S = len(bounds) - 1
+    b = np.ascontiguousarray(np.asarray(bounds, dtype=np.int64))
+    kb = np.ascontiguousarray(np.asarray(kbase, dtype=np.int32))
+    lib = native.kernels()
+    if scratch is None:
+        scratch = torch.empty(seg_sort_scratch(bounds, key_bits), dtype=torch.int32, device=keys.device)
+    k2 = torch.empty_like(keys) if keys_alt is None else keys_alt
+    v2 = torch.empty_like(vals) if vals_alt is None else vals_alt
+    fn = lib.fmlx_seg_sort64 if vals.element_size() == 8 else lib.fmlx_seg_sort32
+    rc = fn(native.ptr(keys), native.ptr(vals), native.ptr(k2), native.ptr(v2), b.ctypes.data, kb.ctypes.data, S,
+            int(key_bits), 11, native.ptr(scratch), scratch.numel(), native.stream_ptr(keys.device))
+    if rc < 0:
+        raise RuntimeError("fmlx_seg_sort failed: %d" % rc)
+    return (k2, v2) if rc == 1 else (keys, vals)
 
 
 class BatchCsc:
@@ -318,23 +379,18 @@ class BatchCsc:
         dev = values.device
         m, d = j1 - j0, self.d
         stream = native.stream_ptr(dev)
-        lib = native.kernels()
-        bits = max(1, int(slots * d - 1).bit_length())
+        # one segment per batch of the run, sorted by column (key − slot·d: ceil(log2 d) bits,
+        # two 10-bit passes for 1M columns) — the batches' entries are already contiguous
+        seg = [self.bounds[b0 + s] - j0 for s in range(slots + 1)]
+        kbase = [s * d for s in range(slots)]
+        bits = max(1, int(d - 1).bit_length())
         key = torch.empty(m, dtype=torch.int32, device=dev)
-        keys_out = torch.empty_like(key)
         if values.dtype == torch.float32:
             # (value bits, row) as one 64-bit payload through the sort, then a sequential split
             pay = torch.empty(m, dtype=torch.int64, device=dev)
             native.call("fmlx_csc_keys64", native.ptr(indptr), native.ptr(indices), native.ptr(values), r0, r1, self.B,
                         d, j0, native.ptr(key), native.ptr(pay), stream)
-            tb = int(lib.fmlx_sort_pairs64_temp_bytes(m, bits))
-            if tb < 0:
-                raise RuntimeError("radix sort temp-size query failed")
-            temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)
-            pay_out = torch.empty_like(pay)
-            native.call("fmlx_sort_pairs64", native.ptr(key), native.ptr(keys_out), native.ptr(pay), native.ptr(pay_out),
-                        m, bits, native.ptr(temp), tb, stream)
-            del key, pay, temp
+            keys_out, pay_out = seg_sort(key, pay, seg, kbase, bits)
             native.call("fmlx_csc_unpack", native.ptr(pay_out), m, j0, native.ptr(self.erow), native.ptr(self.evals),
                         stream)
         else:
@@ -342,14 +398,7 @@ class BatchCsc:
             iota = torch.empty(m, dtype=torch.int32, device=dev)
             native.call("fmlx_csc_keys", native.ptr(indptr), native.ptr(indices), r0, r1, self.B, d, j0,
                         native.ptr(key), native.ptr(rel), native.ptr(iota), stream)
-            tb = int(lib.fmlx_sort_pairs_temp_bytes(m, bits))
-            if tb < 0:
-                raise RuntimeError("radix sort temp-size query failed")
-            temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)
-            order = torch.empty_like(key)
-            native.call("fmlx_sort_pairs", native.ptr(key), native.ptr(keys_out), native.ptr(iota), native.ptr(order),
-                        m, bits, native.ptr(temp), tb, stream)
-            del key, iota, temp
+            keys_out, order = seg_sort(key, iota, seg, kbase, bits)
             native.call("fmlx_csc_fill", 1, native.ptr(order), m, j0, native.ptr(rel), native.ptr(values),
                         native.ptr(self.erow), native.ptr(self.evals), stream)
         native.call("fmlx_csc_colptr", native.ptr(keys_out), m, slots, d, native.ptr(indptr), b0, self.B, self.n, j0,
@@ -383,26 +432,17 @@ class BatchCsc:
 def _stable_order(key: torch.Tensor, bound: int):
     """Stable argsort of int32 keys in [0, bound) and the bucket starts of the sorted keys
     (int32 [bound + 1]: first position of a key >= c). On the GPU an LSD radix sort over only the
-    ceil(log2 bound) key bits with int32 payloads (sort.hip, e.g. 3 digit passes instead of
-    torch.sort's 4 plus int64 indices for 16 batches × 1M columns) and one boundary kernel;
-    torch elsewhere."""
+    ceil(log2 bound) key bits with int32 payloads (radix.hip ``seg_sort``) and one boundary
+    kernel; torch elsewhere."""
     m = key.numel()
     if key.device.type != "cuda" or m == 0:
         order = torch.sort(key, stable=True).indices
         starts = torch.zeros(bound + 1, dtype=torch.int32, device=key.device)
         starts[1:] = torch.cumsum(torch.bincount(key.long(), minlength=bound), 0).to(torch.int32)
         return order, starts
-    lib = native.kernels()
     bits = max(1, int(bound - 1).bit_length())
-    tb = int(lib.fmlx_sort_pairs_temp_bytes(m, bits))
-    if tb < 0:
-        raise RuntimeError("radix sort temp-size query failed")
-    temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=key.device)
     iota = torch.arange(m, dtype=torch.int32, device=key.device)
-    keys_out = torch.empty_like(key)
-    order = torch.empty(m, dtype=torch.int32, device=key.device)
-    native.call("fmlx_sort_pairs", native.ptr(key.contiguous()), native.ptr(keys_out), native.ptr(iota),
-                native.ptr(order), m, bits, native.ptr(temp), tb, native.stream_ptr(key.device))
+    keys_out, order = seg_sort(key.clone(), iota, [0, m], [0], bits)
     starts = torch.empty(bound + 1, dtype=torch.int32, device=key.device)
     native.call("fmlx_sorted_bounds", native.ptr(keys_out), m, int(bound), native.ptr(starts),
                 native.stream_ptr(key.device))

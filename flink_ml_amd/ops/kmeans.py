@@ -28,8 +28,6 @@ native.register_kernel_sigs({
     "fmlx_kmeans_chunk_sum_bf16v": [c_void_p, c_long, c_int, c_void_p, c_void_p, c_void_p, c_int, c_long, c_void_p,
                                     c_void_p],
     "fmlx_kmeans_offsets": [c_void_p, c_long, c_int, c_void_p, c_void_p, c_void_p],
-    "fmlx_sort_pairs_temp_bytes": ([c_long, c_int], c_long),
-    "fmlx_sort_pairs": [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_long, c_void_p],
     "fmlx_sorted_bounds": [c_void_p, c_long, c_int, c_void_p, c_void_p],
     "fmlx_kmeans_finalize": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                              c_void_p],
@@ -50,6 +48,13 @@ DETERMINISTIC = os.environ.get("FMLX_DETERMINISTIC", "0") == "1"
 
 METRICS = {"euclidean": 0, "manhattan": 1, "cosine": 2}
 CHUNK = 256
+# Lloyd rounds over large shards (bf16 fast path, stable grouping): the rows are cut into
+# SPLIT_PARTS parts; part p's grouping + gather-sum (memory-bound: it re-reads the part's rows)
+# runs on a side stream while part p + 1's assign (MFMA-bound) runs on the main stream, and the
+# parts' [sums | counts] are added in part order (deterministic). KMeans.java:291-295 sums each
+# point into its cluster in the assignment loop itself; here the sum trails the assign by a part.
+SPLIT_PARTS = int(os.environ.get("FMLX_KMEANS_SPLIT", "4"))
+SPLIT_MIN_ROWS = int(os.environ.get("FMLX_KMEANS_SPLIT_MIN_ROWS", str(1 << 20)))
 MFMA_KS = (1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16)
 
 
@@ -230,21 +235,52 @@ class KMeansRound:
         elif self.group:
             self.gcounts = torch.zeros(k, dtype=torch.int32, device=dev)  # re-zeroed by the scan kernel
             self.gcursor = torch.zeros(k, dtype=torch.int32, device=dev)
-        elif dev.type == "cuda":
-            # stable radix sort of the labels over ceil(log2 k) bits (not a 64-bit argsort)
+        self.parts = []
+        if (self.fast and self.stable and SPLIT_PARTS > 1 and self.n >= max(SPLIT_MIN_ROWS, SPLIT_PARTS)
+                and metric == "euclidean"):
+            lib = native.kernels()
+            per = -(-self.n // SPLIT_PARTS)
+            per = -(-per // 256) * 256  # whole assign blocks per part
+            for r0 in range(0, self.n, per):
+                r1 = min(r0 + per, self.n)
+                m = r1 - r0
+                mc = (m + CHUNK - 1) // CHUNK + k
+                self.parts.append({
+                    "r0": r0, "r1": r1, "max_chunks": mc,
+                    "order32": torch.empty(m, dtype=torch.int32, device=dev),
+                    "offsets": torch.zeros(k + 1, dtype=torch.int64, device=dev),
+                    "chunk_off": torch.zeros(k + 1, dtype=torch.int64, device=dev),
+                    "gscratch": torch.empty(max(1, int(lib.fmlx_group_stable_scratch(m, k))), dtype=torch.int32,
+                                            device=dev),
+                    "partial": torch.zeros((mc, self.D), dtype=self.acc, device=dev),
+                    "payload": torch.zeros(k * self.D + k, dtype=self.acc, device=dev),
+                    "event": torch.cuda.Event(),
+                })
+            self.side = torch.cuda.Stream(dev)
+        if dev.type == "cuda" and not self.stable and not self.group:
+            # more keys than the counting sort's LDS histograms hold: the stable segmented LSD radix
+            # sort (radix.hip, one segment) over ceil(log2 k) bits, buffers allocated once
+            from . import glm as _glm
+
             self.bits = max(1, int(k - 1).bit_length())
             self.iota = torch.arange(self.n, dtype=torch.int32, device=dev)
-            self.keys_sorted = torch.empty(self.n, dtype=torch.int32, device=dev)
-            tb = native.kernels().fmlx_sort_pairs_temp_bytes(self.n, self.bits)
-            if tb < 0:
-                raise RuntimeError("radix sort temp-size query failed")
-            self.sort_temp = torch.empty(max(int(tb), 1), dtype=torch.uint8, device=dev)
+            self.sort_keys = torch.empty(self.n, dtype=torch.int32, device=dev)
+            self.sort_vals = torch.empty(self.n, dtype=torch.int32, device=dev)
+            self.sort_keys_alt = torch.empty(self.n, dtype=torch.int32, device=dev)
+            self.sort_vals_alt = torch.empty(self.n, dtype=torch.int32, device=dev)
+            self.sort_scratch = torch.empty(_glm.seg_sort_scratch([0, self.n], self.bits), dtype=torch.int32,
+                                            device=dev)
+            odd = _glm.seg_sort_passes(self.bits) & 1
+            self.keys_sorted = self.sort_keys_alt if odd else self.sort_keys
+            self.order32 = self.sort_vals_alt if odd else self.sort_vals
 
     def run(self, cb: CentroidBuffers) -> torch.Tensor:
         X = self.X
         if self.n == 0:
             self.payload.zero_()
             return self.payload
+        if self.parts:
+            return self._run_split(cb)
         assign(X, cb, self.metric, self.labels)
         stream = native.stream_ptr(X.device)
         if self.stable:
@@ -258,9 +294,12 @@ class KMeansRound:
                         native.ptr(self.gcursor), native.ptr(self.offsets), native.ptr(self.chunk_off),
                         native.ptr(self.order32), stream)
         else:
-            native.call("fmlx_sort_pairs", native.ptr(self.labels), native.ptr(self.keys_sorted), native.ptr(self.iota),
-                        native.ptr(self.order32), self.n, self.bits, native.ptr(self.sort_temp),
-                        self.sort_temp.numel(), stream)
+            from . import glm as _glm
+
+            self.sort_keys.copy_(self.labels)
+            self.sort_vals.copy_(self.iota)
+            _glm.seg_sort(self.sort_keys, self.sort_vals, [0, self.n], [0], self.bits, self.sort_keys_alt,
+                          self.sort_vals_alt, self.sort_scratch)
             # cluster boundaries on the device (no host sync: the round is hipGraph-capturable)
             native.call("fmlx_kmeans_offsets", native.ptr(self.keys_sorted), self.n, self.k, native.ptr(self.offsets),
                         native.ptr(self.chunk_off), stream)
@@ -278,6 +317,36 @@ class KMeansRound:
         native.call("fmlx_kmeans_cluster_sum", int(self.acc == torch.float64), native.ptr(self.partial), self.D,
                     native.ptr(offsets), native.ptr(chunk_off), self.k, native.ptr(self.payload),
                     native.stream_ptr(X.device))
+        return self.payload
+
+    def _run_split(self, cb: CentroidBuffers) -> torch.Tensor:
+        """The round over SPLIT_PARTS row parts: assign of part p + 1 (main stream) overlaps the
+        stable grouping, gather-sum and cluster sums of part p (side stream); fork / join by
+        events, so the whole round stays one capturable hipGraph."""
+        X, k, D = self.X, self.k, self.D
+        main = torch.cuda.current_stream(X.device)
+        side = self.side
+        side.wait_stream(main)  # centroids of this round, buffers of the last
+        for p in self.parts:
+            r0, r1 = p["r0"], p["r1"]
+            assign(X[r0:r1], cb, self.metric, self.labels[r0:r1])
+            p["event"].record(main)
+            with torch.cuda.stream(side):
+                side.wait_event(p["event"])
+                st = native.stream_ptr(X.device)
+                Xp = X[r0:r1]
+                native.call("fmlx_group_by_key_stable", native.ptr(self.labels[r0:r1]), r1 - r0, k, CHUNK,
+                            native.ptr(p["gscratch"]), native.ptr(p["offsets"]), native.ptr(p["chunk_off"]),
+                            native.ptr(p["order32"]), st)
+                native.call("fmlx_kmeans_chunk_sum_bf16v", native.ptr(Xp), Xp.stride(0), D, native.ptr(p["order32"]),
+                            native.ptr(p["offsets"]), native.ptr(p["chunk_off"]), k, p["max_chunks"],
+                            native.ptr(p["partial"]), st)
+                native.call("fmlx_kmeans_cluster_sum", int(self.acc == torch.float64), native.ptr(p["partial"]), D,
+                            native.ptr(p["offsets"]), native.ptr(p["chunk_off"]), k, native.ptr(p["payload"]), st)
+        main.wait_stream(side)
+        self.payload.copy_(self.parts[0]["payload"])
+        for p in self.parts[1:]:  # fixed part order: bit-reproducible
+            self.payload.add_(p["payload"])
         return self.payload
 
     def finalize(self, cb: CentroidBuffers, payload: torch.Tensor) -> None:

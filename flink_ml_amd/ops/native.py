@@ -59,6 +59,7 @@ _KERNEL_SIGS = {
     "fmlx_glm_set_tail_tuning": [c_int, c_int],
     "fmlx_glm_set_trace": [c_void_p],
     "fmlx_glm_cnt_elems": [],
+    "fmlx_glm_set_dma": [c_int],
     "fmlx_glm_acc_elems": ([c_int], c_long),
     "fmlx_glm_reduce_update": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                c_double, c_double, c_double, c_double, c_void_p],
@@ -76,11 +77,12 @@ _KERNEL_SIGS = {
                            c_long, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                            c_int, c_double, c_double, c_double, c_double, c_void_p],
     # sort.hip
-    "fmlx_sort_pairs_temp_bytes": ([c_long, c_int], c_long),
-    "fmlx_sort_pairs": [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_long, c_void_p],
     "fmlx_sorted_bounds": [c_void_p, c_long, c_int, c_void_p, c_void_p],
-    "fmlx_sort_pairs64_temp_bytes": ([c_long, c_int], c_long),
-    "fmlx_sort_pairs64": [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_long, c_void_p],
+    "fmlx_seg_sort_scratch": ([c_void_p, c_int, c_int, c_int], c_long),
+    "fmlx_seg_sort64": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                        c_long, c_void_p],
+    "fmlx_seg_sort32": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                        c_long, c_void_p],
     # csc_build.hip
     "fmlx_csc_keys64": [c_void_p, c_void_p, c_void_p, c_long, c_long, c_long, c_int, c_long, c_void_p, c_void_p,
                         c_void_p],

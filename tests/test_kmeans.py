@@ -396,3 +396,44 @@ def test_group_by_key_stable_equals_torch_stable_sort(n, k):
         counts = torch.bincount(keys[valid].long(), minlength=k)
         assert torch.equal(offsets.cpu()[1:], torch.cumsum(counts, 0)) and int(offsets[0]) == 0
         assert torch.equal(chunk_off.cpu()[1:], torch.cumsum((counts + 255) // 256, 0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parts", [2, 3, 4])
+def test_gpu_split_round_overlaps_and_matches_torch(parts, monkeypatch):
+    """Lloyd round over row parts (assign of part p + 1 on the main stream, grouping + gather-sum
+    of part p on a side stream, parts' payloads added in order): equals torch to rounding with
+    exact counts, is bit-reproducible run to run, and replays from a captured hipGraph."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from flink_ml_amd.ops import kmeans as kk
+    from flink_ml_amd.utils import graphs
+
+    monkeypatch.setattr(kk, "SPLIT_PARTS", parts)
+    monkeypatch.setattr(kk, "SPLIT_MIN_ROWS", 1000)
+    g = torch.Generator().manual_seed(4)
+    n, D, k = 30_011, 128, 37
+    X = torch.rand((n, D), generator=g, dtype=torch.float64).to(torch.bfloat16)
+    C = X[:k].to(torch.float64)
+    cb = kk.CentroidBuffers(k, D, torch.device("cuda"), torch.float32)
+    cb.set(C)
+    rnd = kk.KMeansRound(X.cuda(), k, "euclidean")
+    assert len(rnd.parts) == parts
+    p1 = rnd.run(cb).clone()
+    p2 = rnd.run(cb).clone()
+    assert torch.equal(p1, p2)
+    lab = rnd.labels.cpu().long()
+    ref_sums = torch.zeros((k, D), dtype=torch.float64).index_add_(0, lab, X.to(torch.float64))
+    ref_cnt = torch.bincount(lab, minlength=k).double()
+    got = p1.cpu().double()
+    assert torch.allclose(got[: k * D].reshape(k, D), ref_sums, rtol=1e-5, atol=1e-3)
+    assert torch.equal(got[k * D:], ref_cnt)
+    out = {}
+
+    def one():
+        out["p"] = rnd.run(cb)
+
+    gr = graphs.capture(one, torch.device("cuda"))
+    gr.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out["p"], p1)

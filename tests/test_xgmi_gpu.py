@@ -3,6 +3,8 @@
 IPC handles and the two processes map each other's uncached exchange buffers on the same device.
 Kernels, tags, slot reuse, bounded waits and the rank-order sum are the code that runs across
 8 GPUs; only the link is local. References: exact integer sums, and the fp64 host SGD trainer."""
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -133,10 +135,12 @@ def test_fused_sgd_round_two_ranks_matches_host(xgmi_mode):
         assert b0 == r1[loss][2], loss  # replicas identical
 
 
-@pytest.mark.parametrize("det,blocks,unroll,defer", [(False, 0, 0, True), (False, 0, 0, False), (False, 256, 0, True),
-                                                     (False, 256, 2, True), (False, 224, 4, True), (False, 512, 0, True),
-                                                     (False, 512, 0, False), (True, 512, 0, True), (True, 256, 1, True)])
-def test_fused_round_flagship_shape_matches_torch(det, blocks, unroll, defer, monkeypatch):
+@pytest.mark.parametrize("det,blocks,unroll,defer,dma", [
+    (False, 0, 0, True, None), (False, 0, 0, False, None), (False, 256, 0, True, 0), (False, 256, 2, True, 0),
+    (False, 224, 4, True, 0), (False, 512, 0, True, 0), (False, 512, 0, False, 0), (True, 512, 0, True, 0),
+    (True, 256, 1, True, 0), (False, 224, 2, True, 3), (False, 512, 1, True, 4), (False, 224, 2, False, 3),
+    (True, 256, 2, True, 3)])
+def test_fused_round_flagship_shape_matches_torch(det, blocks, unroll, defer, dma, monkeypatch):
     """Fused rounds (TAIL_UPDATE) at the bench shape, bf16 rows: the shipped default (blocks = 0 →
     round_blocks(), unroll = 0 → the shape's row loop; deferred and ticketed tails), 224 / 256 /
     512-block grids, 2 / 4 / 8 rows in flight per wave, atomic tail and the deterministic 16-group
@@ -149,6 +153,8 @@ def test_fused_round_flagship_shape_matches_torch(det, blocks, unroll, defer, mo
     monkeypatch.setattr(gk, "GRAD_BLOCKS", blocks)
     monkeypatch.setattr(gk, "GRAD_UNROLL", unroll)
     monkeypatch.setattr(gk, "DEFER", defer)
+    gk.RoundScratch(1, 8, torch.float32, "cuda")  # applies the process default first
+    gk.set_dma(gk.DMA_DEPTH if dma is None else dma)  # None: the shipped default
 
     g = torch.Generator(device="cpu").manual_seed(7)
     n, d, B = 200_000, 1000, 100_000
@@ -159,7 +165,10 @@ def test_fused_round_flagship_shape_matches_torch(det, blocks, unroll, defer, mo
     tr = DeviceGlmTrainer(sgd, np.zeros(d), Xb.cuda(), y.cuda(), None, "logistic", use_graph=False)
     assert tr.nparts == (blocks or gk.round_blocks(tr.X)) and tr.scratch.det == det
     assert tr.defer == (defer and not det)
-    got = tr.fit()
+    try:
+        got = tr.fit()
+    finally:
+        gk.set_dma(gk.DMA_DEPTH)
     assert tr.rounds_executed() == 3
     assert np.allclose(got, ref, rtol=2e-4, atol=2e-6), np.abs(got - ref).max()
 
@@ -279,37 +288,48 @@ def test_deferred_rounds_match_ticketed_tail(rem, monkeypatch):
     assert np.allclose(out[True], out[False], rtol=1e-5, atol=1e-7), np.abs(out[True] - out[False]).max()
 
 
-@pytest.mark.parametrize("dtype,d", [("bf16", 1000), ("bf16", 520), ("fp32", 300)])
-def test_round_covers_every_row_once(dtype, d, monkeypatch):
-    """The deferred round's row schedule at the shipped grid processes every row of the round's
-    batch exactly once for any batch size (fewer rows than wave slots, a partial last step, the
-    whole set). Integer row weights make Σweight (feedback[d]) an exact, order-independent row
-    census of each round."""
+@pytest.mark.parametrize("dtype,d,dma,unroll", [("bf16", 1000, 0, 0), ("bf16", 520, 0, 0), ("fp32", 300, 0, 0),
+                                                ("bf16", 1000, 3, 0), ("bf16", 520, 2, 1), ("bf16", 1000, 4, 2),
+                                                ("bf16", 1000, 2, 4)])
+def test_round_covers_every_row_once(dtype, d, dma, unroll, monkeypatch):
+    """The deferred round's row schedule processes every row of the round's batch exactly once
+    for any batch size (fewer rows than wave slots, a partial last step, the whole set), with
+    16-byte register loads and with the LDS-DMA row ring (``dma`` = ring depth in steps) at 2, 4
+    and 8 rows in flight. Integer row weights make Σweight (feedback[d]) an exact,
+    order-independent row census of each round; Σloss agrees with a torch evaluation."""
     _need_gpu()
     from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer
     from flink_ml_amd.ops import glm as gk
 
     monkeypatch.setattr(gk, "DEFER", True)
     monkeypatch.setattr(gk, "DETERMINISTIC", False)
-    g = torch.Generator(device="cpu").manual_seed(9)
-    n = 157_003
-    X = torch.rand((n, d), generator=g)
-    X = X.to(torch.bfloat16) if dtype == "bf16" else X
-    y = torch.randint(0, 2, (n,), generator=g).to(torch.float32)
-    wt = (torch.arange(n) % 7 + 1).to(torch.float32)
-    for B in (1_000, 31_337, 157_003, 100_000):
-        tr = DeviceGlmTrainer(SGD(max_iter=6, learning_rate=0.1, global_batch_size=B, tol=0.0), np.zeros(d),
-                              X.cuda(), y.cuda(), wt.cuda(), "logistic", use_graph=False)
-        assert tr.defer
-        P = -(-n // B)
-        tr._launch_round(1)  # round 0
-        for e in range(5):  # both launch parities twice
-            tr._launch_round(1)  # launch e + 1 completes round e and publishes its feedback
-            torch.cuda.synchronize()
-            b0 = (e % P) * B
-            want = float(wt[b0:min(b0 + B, n)].sum())
-            got = float(tr.feedback[d].item())
-            assert got == want, (B, e, got, want)
+    monkeypatch.setattr(gk, "GRAD_UNROLL", unroll)
+    gk.RoundScratch(1, 8, torch.float32, "cuda")  # applies the process default first
+    gk.set_dma(dma)
+    try:
+        g = torch.Generator(device="cpu").manual_seed(9)
+        n = 157_003
+        X = torch.rand((n, d), generator=g)
+        X = X.to(torch.bfloat16) if dtype == "bf16" else X
+        y = torch.randint(0, 2, (n,), generator=g).to(torch.float32)
+        wt = (torch.arange(n) % 7 + 1).to(torch.float32)
+        for B in (1_000, 31_337, 157_003, 100_000):
+            tr = DeviceGlmTrainer(SGD(max_iter=6, learning_rate=0.1, global_batch_size=B, tol=0.0), np.zeros(d),
+                                  X.cuda(), y.cuda(), wt.cuda(), "logistic", use_graph=False)
+            assert tr.defer
+            P = -(-n // B)
+            tr._launch_round(1)  # round 0 (w = 0: every row's loss is log 2)
+            for e in range(5):  # both launch parities twice
+                tr._launch_round(1)  # launch e + 1 completes round e and publishes its feedback
+                torch.cuda.synchronize()
+                b0 = (e % P) * B
+                want = float(wt[b0:min(b0 + B, n)].sum())
+                got = float(tr.feedback[d].item())
+                assert got == want, (B, e, got, want)
+                if e == 0:
+                    assert abs(float(tr.feedback[d + 1].item()) - want * math.log(2.0)) <= 1e-5 * want
+    finally:
+        gk.set_dma(gk.DMA_DEPTH)
 
 
 def test_shipped_default_graph_fit_matches_torch(monkeypatch):
