@@ -244,8 +244,10 @@ class DeviceGlmTrainer:
         # 1 GPU, fused dense round with the atomic tail: launch e completes round e − 1 in its
         # prologue (no ticket / serial tail); launches alternate between two round-number words
         # (``parity``), so hipGraphs are keyed by (rounds, starting parity)
-        self.defer = (self.mode == gk.TAIL_UPDATE and self.scratch is not None and not self.scratch.det
-                      and gk.defer_supported(self.d, acc))
+        # N GPUs over the in-kernel xGMI exchange: launch e + 1's lead block exchanges and applies
+        # round e (csrc/glm.hip defer_prologue_xgmi); FMLX_GLM_DEFER_XGMI=0 keeps the ticketed tail
+        self.defer = ((self.mode == gk.TAIL_UPDATE or self.mode == gk.TAIL_XGMI and gk.DEFER_XGMI)
+                      and self.scratch is not None and not self.scratch.det and gk.defer_supported(self.d, acc))
         self.parity = 0
         self.cw = torch.zeros((2, self.d), dtype=acc, device=dev) if self.defer else None
         self._flushed = False

@@ -138,11 +138,12 @@ struct GlmTail {
   int acc_reps;    // atomic tail: replicas of `acc` (block b adds into replica b mod acc_reps)
   long acc_ld;     // elements between replicas (d + 2 rounded up to whole 256-B lines)
   int ticket2;     // atomic tail: two-level arrival tickets (per-residue groups, then a top one)
-  int defer;       // deferred completion (TAIL_UPDATE, atomic flat tail): see defer_prologue
+  int defer;       // deferred completion (TAIL_UPDATE / TAIL_XGMI, atomic flat tail): see defer_prologue
   int parity;      // deferred: this launch reads its round number from state[parity ? ALT : ROUND]
   void* cw;        // deferred: [2][d] coefficients of the last two rounds
   int wl_off;      // deferred: byte offset of the block's [d] coefficient image in LDS
   int ring_off;    // LDS-DMA row path: byte offset of the [WPB][DEPTH][U][2 KiB] row ring
+  int xb_off;      // deferred TAIL_XGMI: byte offset of the lead block's [d+2] exchange row in LDS
   long long* trace;  // diagnostics (null = off): per block {start, rows done, end, hw id} in
                      // 100 MHz s_memrealtime ticks (scripts/trace_glm_blocks.py)
 };
@@ -421,6 +422,108 @@ __device__ bool defer_prologue(const GlmTail& tl, A* coef, int* state, int e, in
       if (stop) state[ST_DONE] = 1;
     }
   }
+  return stop;
+}
+
+// Deferred round completion across ranks (TAIL_XGMI with the atomic flat tail; SGD.java:246-255
+// applies round e's update at the start of round e + 1). Launch e's blocks add round e's gradient
+// into this rank's accumulator slot e % 3 and exit — no ticket, no serial last-block tail. Launch
+// e + 1's LEAD block (block 0) sums that slot's replicas (fixed order), exchanges the row with
+// every peer over xGMI (one record per rank, rank-order sum: bit-identical on every rank),
+// evaluates TerminateOnMaxIterOrTol, applies the update into cw[e' & 1] (write-through) and raises
+// a flag word; every other block keeps its first row steps in flight, waits for the flag (one
+// polling lane, bounded) and reads w_{e'} from cw. So the exchange latency overlaps the next
+// round's first row loads instead of following the last block's arrival. Returns true (for every
+// thread) when the iteration ended.
+constexpr int WFLAG_IDX = 120;  // tl.cnt word: (round << 1) | stop, published by the lead block
+template <typename A>
+__device__ bool defer_prologue_xgmi(const GlmTail& tl, A* coef, int* state, int e, int d, A* wl) {
+  const int nt = blockDim.x, tid = threadIdx.x;
+  const int R = tl.acc_reps > 1 ? tl.acc_reps : 1;
+  const long ald = tl.acc_ld;
+  const long slot = (long)ACC_MAX_REPS * ald;
+  const long stride = d + 2;
+  A* ring = (A*)tl.acc;
+  A* cw = (A*)tl.cw;
+  A* fb = (A*)tl.feedback;
+  int* wflag = tl.cnt + WFLAG_IDX;
+  __shared__ int s_stop;
+  const bool lead = blockIdx.x == 0;
+  if (e == 0) {
+    for (long c = tid; c < d; c += nt) wl[c] = coef[c];
+    if (tid == 0) s_stop = 0;
+  } else if (lead) {
+    extern __shared__ __align__(16) unsigned char smem_x[];
+    A* xr = reinterpret_cast<A*>(smem_x + tl.xb_off);
+    const A* prev = ring + (long)((e + 2) % 3) * slot;
+    for (long c = tid; c < stride; c += nt) {
+      A v[ACC_MAX_REPS];
+#pragma unroll
+      for (int q = 0; q < ACC_MAX_REPS; ++q) v[q] = q < R ? ld_agent(prev + q * ald + c) : (A)0;
+      A g = (A)0;
+#pragma unroll
+      for (int q = 0; q < ACC_MAX_REPS; ++q) g += v[q];
+      xr[c] = g;
+    }
+    __syncthreads();
+    glm_xgmi_exchange<A>(tl.x, xr, stride);  // xr ← Σ over ranks (NaN-poisoned on a timeout)
+    const A W = xr[d], L = xr[d + 1];
+    const bool stop = !(e < tl.max_iter && L / W > (A)tl.tol);
+    const A lr = (A)tl.lr, reg = (A)tl.reg, en = (A)tl.en;
+    const A* wp = cw + (long)((e - 1) & 1) * d;
+    A* wc = cw + (long)(e & 1) * d;
+    for (long c = tid; c < d; c += nt) {
+      const A w = sgd_apply<A>(wp[c], xr[c], W, lr, reg, en);
+      wl[c] = w;
+      st_agent(wc + c, w);
+      coef[c] = w;
+      if (fb) fb[c] = xr[c];
+    }
+    if (tid == 0) {
+      if (fb) {
+        fb[d] = W;
+        fb[d + 1] = L;
+      }
+      s_stop = stop;
+    }
+    // every wave's write-through stores of w drained, then the flag (write-through, agent scope)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) st_agent(wflag, (e << 1) | (stop ? 1 : 0));
+  } else {
+    if (tid == 0) {
+      int v = 0;
+      long it = 0;
+      for (;;) {
+        v = ld_agent(wflag);
+        if ((v >> 1) == e) break;
+        if (++it > 4 * tl.x.spin_limit) {  // the lead never published: stop, and say so
+          xgmi::st_sys(tl.x.err, 1);
+          v = (e << 1) | 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      s_stop = v & 1;
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the wait
+    if (!s_stop) {
+      const A* wc = cw + (long)(e & 1) * d;
+      for (long c = tid; c < d; c += nt) wl[c] = ld_agent(wc + c);
+    }
+  }
+  __syncthreads();
+  const bool stop = s_stop != 0;
+  A* nxt = ring + (long)((e + 1) % 3) * slot;
+  for (long i = (long)blockIdx.x * nt + tid; i < slot; i += (long)gridDim.x * nt) nxt[i] = (A)0;
+  if (lead && tid == 0) {
+    state[tl.parity ? ST_ROUND : ST_ROUND_ALT] = e + 1;
+    if (e > 0) state[ST_EXECUTED] += 1;
+    if (stop) state[ST_DONE] = 1;
+  }
+  if (lead && e == 0)  // launch 0: w_0 (the value every block just read) for launch 1's lead
+    for (long c = tid; c < d; c += nt) cw[c] = wl[c];
   return stop;
 }
 
@@ -717,7 +820,8 @@ __global__ __launch_bounds__(WPB * 64, (glm_min_waves<T, EPC, CPL, U>())) void g
       for (int t = 0; t < DEPTH - 1; ++t)
         if (t < nst) issue(t);
     }
-    if (tl.defer && defer_prologue<A>(tl, coef, state, e, d, wdef)) {
+    if (tl.defer && (tl.mode == TAIL_XGMI ? defer_prologue_xgmi<A>(tl, coef, state, e, d, wdef)
+                                          : defer_prologue<A>(tl, coef, state, e, d, wdef))) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the wave exits
       return;
     }
@@ -755,7 +859,9 @@ __global__ __launch_bounds__(WPB * 64, (glm_min_waves<T, EPC, CPL, U>())) void g
     load_rows(r + step, U, r, xb, yb, wb, vb);
   }
   // deferred mode: complete the previous round while the first rows are in flight
-  if (tl.defer && defer_prologue<A>(tl, coef, state, e, d, wdef)) return;
+  if (tl.defer && (tl.mode == TAIL_XGMI ? defer_prologue_xgmi<A>(tl, coef, state, e, d, wdef)
+                                        : defer_prologue<A>(tl, coef, state, e, d, wdef)))
+    return;
   if (nst > 0) {
     load_w();
     // nothing in flight at the loop header but the back edge's own loads (the deferred prologue
@@ -1365,6 +1471,10 @@ int launch_grad_k(const void* X, long ld, const void* y, const void* wt, void* c
   if (t2.defer) {
     t2.wl_off = (int)((shmem + 15) & ~(size_t)15);
     shmem = (size_t)t2.wl_off + (size_t)d * sizeof(A);
+    if (t2.mode == TAIL_XGMI) {  // the lead block's exchange row (never aliased with the ring)
+      t2.xb_off = (int)((shmem + 15) & ~(size_t)15);
+      shmem = (size_t)t2.xb_off + (size_t)(d + 2) * sizeof(A);
+    }
   }
   if (g_lds_pad >= 0) {
     shmem += (size_t)g_lds_pad;
@@ -1399,7 +1509,8 @@ int launch_grad_u(const void* X, long ld, const void* y, const void* wt, void* c
   t2.nbatch = (n > 0 && B > 0) ? (int)((n + B - 1) / B) : 0;
   t2.flat_lds = tl.mode != TAIL_PARTIALS && !tl.det && (size_t)WPB * d * sizeof(A) <= 64 * 1024;
   // the deferred prologue needs the flat atomic tail
-  if (t2.defer && (!t2.flat_lds || tl.mode != TAIL_UPDATE || tl.det || tl.cw == nullptr)) return -7;
+  if (t2.defer && (!t2.flat_lds || (tl.mode != TAIL_UPDATE && tl.mode != TAIL_XGMI) || tl.det || tl.cw == nullptr))
+    return -7;
   const bool nt = g_nt >= 0 ? g_nt != 0 : (flags & 1) != 0;
   // LDS-DMA ring: bf16 rows of 65–128 16-byte chunks (d 513–1024), 16-byte aligned, non-temporal
 #ifndef FMLX_ISA_PROBE_U

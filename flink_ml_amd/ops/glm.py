@@ -125,6 +125,8 @@ DETERMINISTIC = os.environ.get("FMLX_DETERMINISTIC", "0") == "1"
 # 1-GPU fused rounds complete round e − 1 in the prologue of launch e (no arrival ticket / serial
 # last-block tail; csrc/glm.hip defer_prologue)
 DEFER = os.environ.get("FMLX_GLM_DEFER", "1") == "1"
+# the same across ranks over the in-kernel xGMI exchange (TAIL_XGMI)
+DEFER_XGMI = os.environ.get("FMLX_GLM_DEFER_XGMI", "1") == "1"
 
 
 def defer_supported(d: int, acc: torch.dtype) -> bool:

@@ -94,7 +94,7 @@ def test_xgmi_twoshot_allreduce_ranks_on_one_gpu(world, sizes):
     assert run_spmd(_twoshot_worker, world, sizes, env=ENV, timeout=300) == [True] * world
 
 
-def _sgd_worker(rank, world, xgmi_mode, dtype_name):
+def _sgd_worker(rank, world, xgmi_mode, dtype_name, defer_xgmi="1"):
     import os
 
     import numpy as np
@@ -117,22 +117,27 @@ def _sgd_worker(rank, world, xgmi_mode, dtype_name):
         tr = DeviceGlmTrainer(sgd, np.zeros(d), Xd, y.cuda(), w.cuda(), loss, use_graph=(loss == "hinge" and xgmi_mode == "force"))
         expect = gk.TAIL_XGMI if xgmi_mode == "force" else gk.TAIL_FEEDBACK
         assert tr.mode == expect, (tr.mode, expect)
+        # the in-kernel exchange runs deferred (launch e + 1's lead block completes round e)
+        assert tr.defer == (xgmi_mode == "force" and defer_xgmi == "1"), tr.defer
         got = tr.fit()
         out[loss] = (float(np.abs(got - ref).max()), float(np.abs(ref).max()), got.tobytes())
     return out
 
 
-@pytest.mark.parametrize("xgmi_mode", ["force", "0"])
-def test_fused_sgd_round_two_ranks_matches_host(xgmi_mode):
-    """TAIL_XGMI (in-kernel xGMI exchange) and TAIL_FEEDBACK (+ process-group all-reduce) both
-    reproduce the fp64 host trainer, and both ranks end with bit-identical coefficients."""
+@pytest.mark.parametrize("xgmi_mode,world,defer_xgmi", [("force", 2, "1"), ("force", 2, "0"), ("force", 4, "1"),
+                                                       ("0", 2, "1")])
+def test_fused_sgd_round_two_ranks_matches_host(xgmi_mode, world, defer_xgmi):
+    """TAIL_XGMI (in-kernel xGMI exchange: deferred — launch e + 1's lead block exchanges and
+    applies round e — and ticketed) and TAIL_FEEDBACK (+ process-group all-reduce) reproduce the
+    fp64 host trainer at 2 and 4 ranks, and every rank ends with bit-identical coefficients."""
     _need_gpu()
-    env = dict(ENV, FMLX_XGMI=xgmi_mode)
-    r0, r1 = run_spmd(_sgd_worker, 2, xgmi_mode, "float64", env=env, timeout=300)
-    for loss in r0:
-        err, scale, b0 = r0[loss]
+    env = dict(ENV, FMLX_XGMI=xgmi_mode, FMLX_GLM_DEFER_XGMI=defer_xgmi)
+    res = run_spmd(_sgd_worker, world, xgmi_mode, "float64", defer_xgmi, env=env, timeout=300)
+    for loss in res[0]:
+        err, scale, b0 = res[0][loss]
         assert err <= 1e-9 * max(1.0, scale), (loss, err)
-        assert b0 == r1[loss][2], loss  # replicas identical
+        for r in res[1:]:
+            assert b0 == r[loss][2], loss  # replicas identical
 
 
 @pytest.mark.parametrize("det,blocks,unroll,defer,dma", [
