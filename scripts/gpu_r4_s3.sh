@@ -19,4 +19,6 @@ for sp in 4 1; do
   FMLX_KMEANS_SPLIT=$sp timeout -k 10 300 python scripts/bench_north.py --config kmeans --scale 0.125 >> gpurun_out/r4_kmeans_split_shard.jsonl 2>&1 || exit $?
 done
 tail -2 gpurun_out/r4_kmeans_split_shard.jsonl | cut -c1-400
+timeout -k 10 400 python scripts/bench_north.py --config svc_sparse --scale 0.125 > gpurun_out/r4_svc_shard.jsonl 2>&1 || exit $?
+tail -1 gpurun_out/r4_svc_shard.jsonl | cut -c1-700
 AB_TAG=r4_ahead2_ab AB_CONFIGS="u=2,b=224;u=2,b=256;u=2,b=240;u=1,b=512;u=4,b=224" bash scripts/gpu_r4_dma.sh

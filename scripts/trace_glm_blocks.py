@@ -88,7 +88,7 @@ def main():
     xm = {x: round(statistics.median(s["rows_done_mean_by_xcd"][x] for s in summary), 2)
           for x in summary[0]["rows_done_mean_by_xcd"]}
     print(json.dumps({"median_over_rounds": {k: round(statistics.median(s[k] for s in summary), 2) for k in keys},
-                      "rows_done_mean_by_xcd_median": xm, "blocks": nb, "rowmap": a.rowmap}))
+                      "rows_done_mean_by_xcd_median": xm, "blocks": nb}))
 
 
 if __name__ == "__main__":
