@@ -355,7 +355,7 @@ class DeviceGlmTrainer:
         the same launch sequence repeats); replaying it costs one host submission per ``rounds``.
         Deferred mode: ``key`` = (rounds, starting parity)."""
         rounds, parity = key if self.defer else (key, None)
-        side = torch.cuda.Stream(self.device)
+        side = graphs.aux_stream(self.device, "sgd-warmup")
         side.wait_stream(torch.cuda.current_stream(self.device))
         # everything a round mutates that the next round reads (the sparse path's Σw/Σloss
         # parity slots, the deferred mode's accumulator ring and coefficient ring included) is

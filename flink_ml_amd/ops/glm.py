@@ -217,16 +217,20 @@ CSC_MAX_BYTES = int(os.environ.get("FMLX_CSC_MAX_BYTES", str(8 << 30)))
 CSC_RUN_MAX = int(os.environ.get("FMLX_CSC_RUN_MAX", "16"))  # consecutive batches transposed per sort
 
 
+SEG_SORT_DIGIT_BITS = 10  # radix.hip RS_MAX_DIGIT_BITS
+
+
 def seg_sort_passes(key_bits: int) -> int:
-    """Digit passes of ``seg_sort`` (digits of <= 11 bits, balanced)."""
-    return -(-int(key_bits) // 11)
+    """Digit passes of ``seg_sort`` (digits of <= 10 bits, balanced)."""
+    return -(-int(key_bits) // SEG_SORT_DIGIT_BITS)
 
 
 def seg_sort_scratch(bounds, key_bits: int) -> int:
     import numpy as np
 
     b = np.ascontiguousarray(np.asarray(bounds, dtype=np.int64))
-    need = int(native.kernels().fmlx_seg_sort_scratch(b.ctypes.data, len(bounds) - 1, int(key_bits), 11))
+    need = int(native.kernels().fmlx_seg_sort_scratch(b.ctypes.data, len(bounds) - 1, int(key_bits),
+                                                             SEG_SORT_DIGIT_BITS))
     if need < 0:
         raise ValueError("seg_sort: bad segment table (S=%d, key_bits=%d)" % (len(bounds) - 1, key_bits))
     return max(need, 1)
@@ -253,7 +257,7 @@ def seg_sort(keys: torch.Tensor, vals: torch.Tensor, bounds, kbase, key_bits: in
     v2 = torch.empty_like(vals) if vals_alt is None else vals_alt
     fn = lib.fmlx_seg_sort64 if vals.element_size() == 8 else lib.fmlx_seg_sort32
     rc = fn(native.ptr(keys), native.ptr(vals), native.ptr(k2), native.ptr(v2), b.ctypes.data, kb.ctypes.data, S,
-            int(key_bits), 11, native.ptr(scratch), scratch.numel(), native.stream_ptr(keys.device))
+            int(key_bits), SEG_SORT_DIGIT_BITS, native.ptr(scratch), scratch.numel(), native.stream_ptr(keys.device))
     if rc < 0:
         raise RuntimeError("fmlx_seg_sort failed: %d" % rc)
     return (k2, v2) if rc == 1 else (keys, vals)

@@ -258,8 +258,10 @@ class KMeansRound:
                 })
             # FMLX_KMEANS_SIDE_PRIO=1: the side stream at high priority, so its blocks are dispatched
             # as soon as assign blocks retire instead of after the assign grid drains (A/B knob)
-            self.side = torch.cuda.Stream(dev, priority=-1 if os.environ.get("FMLX_KMEANS_SIDE_PRIO", "0") == "1"
-                                          else 0)
+            from ..utils import graphs as _graphs
+
+            self.side = _graphs.aux_stream(dev, "kmeans-split",
+                                           -1 if os.environ.get("FMLX_KMEANS_SIDE_PRIO", "0") == "1" else 0)
         if dev.type == "cuda" and not self.stable and not self.group:
             # more keys than the counting sort's LDS histograms hold: the stable segmented LSD radix
             # sort (radix.hip, one segment) over ceil(log2 k) bits, buffers allocated once

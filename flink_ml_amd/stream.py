@@ -111,7 +111,9 @@ def _prefetch(it: Iterator[Table], dev) -> Iterator[Table]:
     blocks to a later side-stream copy while consumer kernels still read them."""
     from .utils import streamcheck
 
-    side = torch.cuda.Stream(dev)
+    from .utils import graphs
+
+    side = graphs.aux_stream(dev, "h2d-prefetch")
     nxt = None
     check = streamcheck.enabled()  # FMLX_STREAM_CHECK=1: verify every hand-off (slow)
     count = [0]
