@@ -4,11 +4,11 @@
 //
 //   csc_keys    one wave per row: key = slot·d + column (slot = batch within the run), the
 //               entry's batch-relative row, and the identity payload for the sort
-//   (radix sort of the keys over ceil(log2(slots·d)) bits, sort.hip — stable)
+//   (stable segmented radix sort of the keys by column, one segment per batch: radix.hip)
 //   csc_fill    erow / evals of the run in sorted order, written straight into the partition-wide
 //               arrays (one gather of the row id and of the value per entry; fp64 values)
-//   csc_keys64 / csc_unpack  fp32 values: (value bits, row) ride through the sort as one 64-bit
-//               payload and are split into erow / evals by a sequential pass
+//   csc_keys64  fp32 values: (value bits, row) ride through the sort as one 64-bit payload that
+//               the sort's last pass splits straight into erow / evals (radix.hip split output)
 //   csc_colptr  every batch's dense column pointer straight from the sorted keys: thread i writes
 //               the bins (key[i−1], key[i]] (each bin exactly once), relative to its batch's first
 //               entry, which is indptr[batch·B] − j0 (a batch's entries are its own CSR range)
@@ -60,16 +60,6 @@ __global__ __launch_bounds__(256) void csc_keys64_kernel(const long* __restrict_
       key[o] = kb + idx[j];
       payload[o] = ((uint64_t)__float_as_uint(values[j]) << 32) | rr;
     }
-  }
-}
-
-__global__ __launch_bounds__(256) void csc_unpack_kernel(const uint64_t* __restrict__ payload, long m, long j0,
-                                                         int* __restrict__ erow, float* __restrict__ evals) {
-  const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
-    const uint64_t p = payload[i];
-    erow[j0 + i] = (int)(uint32_t)p;
-    evals[j0 + i] = __uint_as_float((uint32_t)(p >> 32));
   }
 }
 
@@ -134,12 +124,6 @@ FMLX_API int fmlx_csc_keys64(const long* indptr, const int* idx, const float* va
   return (int)hipGetLastError();
 }
 
-FMLX_API int fmlx_csc_unpack(const uint64_t* payload, long m, long j0, int* erow, float* evals, void* stream) {
-  if (m <= 0) return 0;
-  hipLaunchKernelGGL(csc_unpack_kernel, dim3(grid_for(m, 256, 1u << 16)), dim3(256), 0, (hipStream_t)stream, payload,
-                     m, j0, erow, evals);
-  return (int)hipGetLastError();
-}
 
 FMLX_API int fmlx_csc_fill(int f64, const int* order, long m, long j0, const int* rel, const void* values, int* erow,
                            void* evals, void* stream) {

@@ -123,9 +123,9 @@ __global__ __launch_bounds__(GS_THREADS) void group_scatter_kernel(const int* __
 //                  offsets / chunk offsets (same outputs as group_scan);
 //  4. st_scatter   per tile: per-wave histograms again, cursors = group base + in-group prefix +
 //                  earlier waves; each wave walks its segment 64 rows at a time in row order:
-//                  a 21-step bitonic sort of the packed (key, lane) values across the wave gives
-//                  every row its rank among equal keys of the 64 (lane order = row order), and
-//                  the last lane of each key's run advances the cursor.
+//                  one ballot per key bit gives every row the set of lanes holding its key and
+//                  its rank among them (lane order = row order); the highest lane of each key's
+//                  run advances the cursor (was a 21-step bitonic sort of packed (key, lane)).
 // Every step is order-deterministic; no global atomics.
 constexpr int ST_WAVES = 8;
 constexpr int ST_THREADS = ST_WAVES * 64;
@@ -261,6 +261,9 @@ __global__ __launch_bounds__(ST_THREADS) void st_scatter_kernel(const int* __res
   }
   __syncthreads();
   int* cur = sh + (long)w * k;
+  int kb = 0;  // key bits
+  while ((1 << kb) < k) ++kb;
+  const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;  // lanes below this one
   for (int i0 = 0; i0 < ST_SEG; i0 += 64) {
     const long r = seg0 + i0 + lane;
     int key = -1;
@@ -268,37 +271,24 @@ __global__ __launch_bounds__(ST_THREADS) void st_scatter_kernel(const int* __res
       key = keys[r];
       if ((unsigned)key >= (unsigned)k) key = -1;
     }
-    // stable in-wave order of the 64 rows: a bitonic sort of (key, lane) packed into one int
-    // (invalid rows last), then each element's rank inside its key's run
-    int v = key >= 0 ? (key << 6) | lane : 0x7fffffff;
-#pragma unroll
-    for (int size = 2; size <= 64; size <<= 1) {
-#pragma unroll
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
-        const int other = __shfl_xor(v, stride, 64);
-        const bool asc = (lane & size) == 0 || size == 64;
-        const bool low = (lane & stride) == 0;
-        const int mn = v < other ? v : other, mx = v < other ? other : v;
-        v = (low == asc) ? mn : mx;
-      }
+    const bool valid = key >= 0;
+    // stable rank among equal keys of the 64 rows (lane order = row order): the lanes holding
+    // my key (one ballot per key bit, no cross-lane data movement), then those below me
+    unsigned long long peers = __ballot(valid);
+    for (int bit = 0; bit < kb; ++bit) {
+      const bool mine = (key >> bit) & 1;
+      const unsigned long long bb = __ballot(mine);
+      peers &= mine ? bb : ~bb;
     }
-    const bool valid = v != 0x7fffffff;
-    const int ks = v >> 6;
-    const int prev = __shfl_up(v, 1, 64);
-    const int next = __shfl_down(v, 1, 64);
-    int start = (lane == 0 || (prev >> 6) != ks) ? lane : 0;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {  // run start = inclusive prefix max of the starts
-      const int o = __shfl_up(start, off, 64);
-      if (lane >= off && o > start) start = o;
-    }
-    const int rank = lane - start;
-    const bool last = lane == 63 || (next >> 6) != ks;
-    if (valid) order[cur[ks] + rank] = (int)(seg0 + i0 + (v & 63));
-    // every lane of a run read its cursor above before the run's last lane advances it (one
-    // wave: the LDS read and the later write are ordered by the wave's program order)
+    const int rank = __popcll(peers & lt);
+    const bool leader = valid && (peers >> lane) == 1ull;  // the highest lane of my key's run
+    int pos = 0;
+    if (valid) pos = cur[key] + rank;
+    // every lane read its cursor above before a leader advances it (one wave: its LDS accesses
+    // complete in program order)
     __builtin_amdgcn_wave_barrier();
-    if (valid && last) cur[ks] += rank + 1;
+    if (leader) cur[key] = pos + 1;
+    if (valid) order[pos] = (int)r;
     __builtin_amdgcn_wave_barrier();
   }
 }

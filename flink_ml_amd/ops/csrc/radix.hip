@@ -19,8 +19,10 @@
 //               then over the digits (+ the segment's first position) → G[group][digit] = where
 //               the group's pairs of that digit start;
 //   rs_scatter  per tile: per-wave histograms again → cursors; each wave walks its 1024-pair
-//               segment 64 pairs at a time in input order, a bitonic sort of the packed
-//               (digit, lane) values across the wave gives every pair its rank among equal digits.
+//               segment 64 pairs at a time in input order; one ballot per digit bit gives every
+//               pair the set of lanes holding its digit, and its rank among them (lanes below);
+//               the pairs are placed in LDS in tile-local sorted order, then written out digit
+//               run by digit run.
 // Every step is order-deterministic; no global atomics.
 #include "common.h"
 
@@ -146,11 +148,15 @@ __global__ __launch_bounds__(1024) void rs_base_kernel(int* __restrict__ G, SegT
 // The tile is ranked into LDS first and written out in digit order: consecutive threads store
 // consecutive positions of one digit's run, instead of 64 lanes each storing 12 bytes into 64
 // different buckets (the direct form measured 1.95 ms per pass over 64M pairs: 0.8 TB/s).
-template <typename V>
+// SPLIT (64-bit payloads, last pass): the payload's low / high words go straight to two arrays
+// (the column-major copy's row ids and values) at split_off + position, so no separate unpack pass.
+template <typename V, bool SPLIT>
 __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const int* __restrict__ kin, const V* __restrict__ vin,
                                                                 int* __restrict__ kout, V* __restrict__ vout,
                                                                 const int* __restrict__ T, const int* __restrict__ G,
-                                                                SegTable tb, int shift, int mask) {
+                                                                SegTable tb, int shift, int mask,
+                                                                int* __restrict__ split_lo,
+                                                                unsigned* __restrict__ split_hi, long split_off) {
   extern __shared__ __align__(16) int shs[];
   const int nd = mask + 1;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -217,61 +223,38 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const int* __res
   }
   __syncthreads();
   int* cur = hw + (long)w * nd;
+  const int db = 31 - __builtin_clz(nd);  // digit bits
+  const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;  // lanes below this one
   for (long i0 = wa; i0 < wb; i0 += 64) {
     const long i = i0 + lane;
-    int key = 0, dg = -1;
+    const bool valid = i < wb;
+    int key = 0, dg = 0;
     V val = 0;
-    if (i < wb) {
+    if (valid) {
       key = kin[i];
       val = vin[i];
       dg = ((key - kb) >> shift) & mask;
     }
-    // stable in-wave order of the 64 pairs: bitonic sort of (digit, lane) packed into one int
-    // (lanes past the end last), then each element's rank inside its digit's run
-    int v = dg >= 0 ? (dg << 6) | lane : 0x7fffffff;
-#pragma unroll
-    for (int size = 2; size <= 64; size <<= 1) {
-#pragma unroll
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
-        const int other = __shfl_xor(v, stride, 64);
-        const bool asc = (lane & size) == 0 || size == 64;
-        const bool low = (lane & stride) == 0;
-        const int mn = v < other ? v : other, mx = v < other ? other : v;
-        v = (low == asc) ? mn : mx;
-      }
+    // stable rank among equal digits of the 64: the lanes holding my digit (one ballot per digit
+    // bit, no cross-lane data movement), then the count of those below me
+    unsigned long long peers = __ballot(valid);
+    for (int bit = 0; bit < db; ++bit) {
+      const bool mine = (dg >> bit) & 1;
+      const unsigned long long bb = __ballot(mine);
+      peers &= mine ? bb : ~bb;
     }
-    const bool valid = v != 0x7fffffff;
-    const int ds = v >> 6;
-    const int src = v & 63;
-    const int prev = __shfl_up(v, 1, 64);
-    const int next = __shfl_down(v, 1, 64);
-    int start = (lane == 0 || (prev >> 6) != ds) ? lane : 0;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {  // run start = inclusive prefix max of the starts
-      const int o = __shfl_up(start, off, 64);
-      if (lane >= off && o > start) start = o;
-    }
-    const int rank = lane - start;
-    const bool last = lane == 63 || (next >> 6) != ds;
-    // the pair this lane places is the one lane `src` read
-    const int k2 = __shfl(key, src, 64);
-    V v2;
-    if constexpr (sizeof(V) == 8) {
-      const uint64_t u = (uint64_t)val;
-      const unsigned lo = __shfl((unsigned)u, src, 64), hi = __shfl((unsigned)(u >> 32), src, 64);
-      v2 = (V)(((uint64_t)hi << 32) | lo);
-    } else {
-      v2 = (V)__shfl((unsigned)val, src, 64);
-    }
-    if (valid) {
-      const int pos = cur[ds] + rank;  // tile-local
-      lk[pos] = k2;
-      lv[pos] = v2;
-    }
-    // every lane of a run read its cursor above before the run's last lane advances it (one
-    // wave: the LDS read and the later write are ordered by the wave's program order)
+    const int rank = __popcll(peers & lt);
+    const bool leader = valid && (peers >> lane) == 1ull;  // the highest lane of my digit's run
+    int pos = 0;
+    if (valid) pos = cur[dg] + rank;  // tile-local
+    // every lane read its cursor above before a leader advances it (one wave: its LDS accesses
+    // complete in program order)
     __builtin_amdgcn_wave_barrier();
-    if (valid && last) cur[ds] += rank + 1;
+    if (leader) cur[dg] = pos + 1;
+    if (valid) {
+      lk[pos] = key;
+      lv[pos] = val;
+    }
     __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
@@ -282,7 +265,13 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const int* __res
     const int dg = ((key - kb) >> shift) & mask;
     const int gp = gbase[dg] + (i - loc[dg]);
     kout[gp] = key;
-    vout[gp] = lv[i];
+    if constexpr (SPLIT) {
+      const uint64_t u = (uint64_t)lv[i];
+      split_lo[split_off + gp] = (int)(unsigned)u;
+      split_hi[split_off + gp] = (unsigned)(u >> 32);
+    } else {
+      vout[gp] = lv[i];
+    }
   }
 }
 
@@ -313,7 +302,8 @@ static int make_table(const long* bound, const int* kbase, int S, SegTable& tb) 
 
 template <typename V>
 int seg_sort(int* keys, V* vals, int* keys_alt, V* vals_alt, const long* bound, const int* kbase, int S, int key_bits,
-             int digit_bits, int* scratch, long scratch_ints, hipStream_t st) {
+             int digit_bits, int* scratch, long scratch_ints, hipStream_t st, int* split_lo = nullptr,
+             unsigned* split_hi = nullptr, long split_off = 0) {
   SegTable tb{};
   int rc = make_table(bound, kbase, S, tb);
   if (rc) return rc;
@@ -339,8 +329,12 @@ int seg_sort(int* keys, V* vals, int* keys_alt, V* vals_alt, const long* bound, 
     hipLaunchKernelGGL(rs_hist_kernel, dim3(tb.ntile), dim3(RS_THREADS), lds, st, kin, tb, shift, mask, T);
     hipLaunchKernelGGL(rs_colscan_kernel, dim3((nd + 255) / 256, tb.ngrp), dim3(256), 0, st, T, tb, nd, G);
     hipLaunchKernelGGL(rs_base_kernel, dim3(tb.S), dim3(1024), 0, st, G, tb, nd);
-    hipLaunchKernelGGL((rs_scatter_kernel<V>), dim3(tb.ntile), dim3(RS_THREADS), lds_sc, st, kin, vin, kout, vout, T,
-                       G, tb, shift, mask);
+    if (sizeof(V) == 8 && split_lo != nullptr && p == passes - 1)
+      hipLaunchKernelGGL((rs_scatter_kernel<V, true>), dim3(tb.ntile), dim3(RS_THREADS), lds_sc, st, kin, vin, kout,
+                         vout, T, G, tb, shift, mask, split_lo, split_hi, split_off);
+    else
+      hipLaunchKernelGGL((rs_scatter_kernel<V, false>), dim3(tb.ntile), dim3(RS_THREADS), lds_sc, st, kin, vin, kout,
+                         vout, T, G, tb, shift, mask, (int*)nullptr, (unsigned*)nullptr, 0L);
     int* tk = kin;
     kin = kout;
     kout = tk;
@@ -373,11 +367,14 @@ FMLX_API long fmlx_seg_sort_scratch(const long* bound, int S, int key_bits, int 
 // Sorts pairs [bound[0], bound[S]) (positions relative to the arrays' starts) segment by segment
 // by the low key_bits bits of (key − kbase[s]); `bound` / `kbase` are HOST arrays. Returns 0 when
 // the result is in keys / vals, 1 when it is in keys_alt / vals_alt, < 0 on a bad argument.
+// split_lo / split_hi (may be null): the last pass writes the payloads' low / high 32-bit words to
+// split_lo[split_off + i] / split_hi[split_off + i] instead of vals (the keys still go to the
+// returned key buffer).
 FMLX_API int fmlx_seg_sort64(int* keys, uint64_t* vals, int* keys_alt, uint64_t* vals_alt, const long* bound,
                              const int* kbase, int S, int key_bits, int digit_bits, int* scratch, long scratch_ints,
-                             void* stream) {
+                             int* split_lo, unsigned* split_hi, long split_off, void* stream) {
   return seg_sort<uint64_t>(keys, vals, keys_alt, vals_alt, bound, kbase, S, key_bits, digit_bits, scratch,
-                            scratch_ints, (hipStream_t)stream);
+                            scratch_ints, (hipStream_t)stream, split_lo, split_hi, split_off);
 }
 
 FMLX_API int fmlx_seg_sort32(int* keys, uint32_t* vals, int* keys_alt, uint32_t* vals_alt, const long* bound,

@@ -237,14 +237,16 @@ def seg_sort_scratch(bounds, key_bits: int) -> int:
 
 
 def seg_sort(keys: torch.Tensor, vals: torch.Tensor, bounds, kbase, key_bits: int, keys_alt=None, vals_alt=None,
-             scratch=None):
+             scratch=None, split=None):
     """Stable segmented LSD radix sort (csrc/radix.hip, no library sort) of int32 ``keys`` with
     int32 / int64 payloads ``vals``: segment s = positions [bounds[s], bounds[s + 1]) is sorted by
     the low ``key_bits`` bits of (key − kbase[s]); equal keys keep their input order. The passes
     ping-pong between (keys, vals) and (keys_alt, vals_alt), so the inputs are overwritten; the
     sorted pair ends in the alt buffers when ``seg_sort_passes(key_bits)`` is odd. Returns the
     sorted (keys, vals). Pre-allocated ``keys_alt`` / ``vals_alt`` / ``scratch`` (int32,
-    ``seg_sort_scratch``) make the call allocation-free (hipGraph capture)."""
+    ``seg_sort_scratch``) make the call allocation-free (hipGraph capture). ``split`` = (lo, hi,
+    offset), int64 payloads only: the last pass writes the payloads' low / high 32-bit words to
+    lo[offset + i] / hi[offset + i] (int32 / 32-bit tensors) instead of the payload buffers."""
     import numpy as np
 
     S = len(bounds) - 1
@@ -255,9 +257,15 @@ def seg_sort(keys: torch.Tensor, vals: torch.Tensor, bounds, kbase, key_bits: in
         scratch = torch.empty(seg_sort_scratch(bounds, key_bits), dtype=torch.int32, device=keys.device)
     k2 = torch.empty_like(keys) if keys_alt is None else keys_alt
     v2 = torch.empty_like(vals) if vals_alt is None else vals_alt
-    fn = lib.fmlx_seg_sort64 if vals.element_size() == 8 else lib.fmlx_seg_sort32
-    rc = fn(native.ptr(keys), native.ptr(vals), native.ptr(k2), native.ptr(v2), b.ctypes.data, kb.ctypes.data, S,
-            int(key_bits), SEG_SORT_DIGIT_BITS, native.ptr(scratch), scratch.numel(), native.stream_ptr(keys.device))
+    args = (native.ptr(keys), native.ptr(vals), native.ptr(k2), native.ptr(v2), b.ctypes.data, kb.ctypes.data, S,
+            int(key_bits), SEG_SORT_DIGIT_BITS, native.ptr(scratch), scratch.numel())
+    if vals.element_size() == 8:
+        lo, hi, off = split if split is not None else (None, None, 0)
+        rc = lib.fmlx_seg_sort64(*args, native.ptr(lo), native.ptr(hi), int(off), native.stream_ptr(keys.device))
+    else:
+        if split is not None:
+            raise ValueError("seg_sort: split output needs int64 payloads")
+        rc = lib.fmlx_seg_sort32(*args, native.stream_ptr(keys.device))
     if rc < 0:
         raise RuntimeError("fmlx_seg_sort failed: %d" % rc)
     return (k2, v2) if rc == 1 else (keys, vals)
@@ -396,9 +404,8 @@ class BatchCsc:
             pay = torch.empty(m, dtype=torch.int64, device=dev)
             native.call("fmlx_csc_keys64", native.ptr(indptr), native.ptr(indices), native.ptr(values), r0, r1, self.B,
                         d, j0, native.ptr(key), native.ptr(pay), stream)
-            keys_out, pay_out = seg_sort(key, pay, seg, kbase, bits)
-            native.call("fmlx_csc_unpack", native.ptr(pay_out), m, j0, native.ptr(self.erow), native.ptr(self.evals),
-                        stream)
+            # the last pass writes (row, value bits) straight into erow / evals (no unpack pass)
+            keys_out, _ = seg_sort(key, pay, seg, kbase, bits, split=(self.erow, self.evals, j0))
         else:
             rel = torch.empty(m, dtype=torch.int32, device=dev)
             iota = torch.empty(m, dtype=torch.int32, device=dev)

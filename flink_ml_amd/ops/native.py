@@ -80,13 +80,12 @@ _KERNEL_SIGS = {
     "fmlx_sorted_bounds": [c_void_p, c_long, c_int, c_void_p, c_void_p],
     "fmlx_seg_sort_scratch": ([c_void_p, c_int, c_int, c_int], c_long),
     "fmlx_seg_sort64": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
-                        c_long, c_void_p],
+                        c_long, c_void_p, c_void_p, c_long, c_void_p],
     "fmlx_seg_sort32": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
                         c_long, c_void_p],
     # csc_build.hip
     "fmlx_csc_keys64": [c_void_p, c_void_p, c_void_p, c_long, c_long, c_long, c_int, c_long, c_void_p, c_void_p,
                         c_void_p],
-    "fmlx_csc_unpack": [c_void_p, c_long, c_long, c_void_p, c_void_p, c_void_p],
     "fmlx_csc_keys": [c_void_p, c_void_p, c_long, c_long, c_long, c_int, c_long, c_void_p, c_void_p, c_void_p,
                       c_void_p],
     "fmlx_csc_fill": [c_int, c_void_p, c_long, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],

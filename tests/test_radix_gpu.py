@@ -76,3 +76,30 @@ def test_segments_with_key_offsets_match_per_segment_sort(vdtype):
     got_k2, got_v2 = gk.seg_sort(keys.clone(), vals.clone(), bounds, kbase, bits, k2, v2, sc)
     assert torch.equal(got_k2, ref_k) and torch.equal(got_v2, ref_v)
     assert (got_k2.data_ptr() == k2.data_ptr()) == bool(gk.seg_sort_passes(bits) & 1)
+
+
+def test_split_output_writes_payload_halves():
+    """Last pass with split output: keys sorted, payload low words → lo[off + i], high words →
+    hi[off + i] (the column-major copy's rows / value bits), bit-exact against the unsplit sort."""
+    _need_gpu()
+    g = torch.Generator(device="cuda").manual_seed(9)
+    bounds = [0, 70_000, 70_001, 200_000]
+    d = 50_000
+    n = bounds[-1]
+    keys = torch.empty(n, dtype=torch.int32, device="cuda")
+    for s in range(3):
+        a, b = bounds[s], bounds[s + 1]
+        keys[a:b] = s * d + torch.randint(0, d, (b - a,), generator=g, device="cuda", dtype=torch.int32)
+    rows = torch.randint(0, 1 << 20, (n,), generator=g, device="cuda", dtype=torch.int64)
+    vals = torch.rand(n, generator=g, device="cuda", dtype=torch.float32)
+    pay = (vals.view(torch.int32).to(torch.int64) << 32) | rows
+    kbase = [s * d for s in range(3)]
+    bits = (d - 1).bit_length()
+    ref_k, ref_p = _reference(keys, pay, bounds, kbase, bits)
+    off = 123
+    lo = torch.zeros(n + off, dtype=torch.int32, device="cuda")
+    hi = torch.zeros(n + off, dtype=torch.float32, device="cuda")
+    got_k, _ = gk.seg_sort(keys.clone(), pay.clone(), bounds, kbase, bits, split=(lo, hi, off))
+    assert torch.equal(got_k, ref_k)
+    assert torch.equal(lo[off:], (ref_p & 0xFFFFFFFF).to(torch.int32))
+    assert torch.equal(hi[off:].view(torch.int32), (ref_p >> 32).to(torch.int32))
