@@ -58,10 +58,29 @@ __device__ __forceinline__ void tile_range(const SegTable& tb, int t, long& a, l
   kb = tb.kbase[s];
 }
 
-__device__ __forceinline__ void rs_wave_hist(const int* __restrict__ keys, long a, long b, int kb, int shift, int mask,
-                                             int* h) {
+constexpr int RS_PER_LANE = RS_SEG / 64;  // pairs per lane of a wave segment
+
+// the wave's segment [wa, wb) into registers, all loads in flight at once (one memory latency
+// per segment, not one per 64 pairs: at one 136 KiB-LDS block per CU the scatter has 2 waves per
+// SIMD and a load-then-use loop waited out each load)
+template <typename V>
+__device__ __forceinline__ void rs_load_seg(const int* __restrict__ kin, const V* __restrict__ vin, long wa, long wb,
+                                            int (&k)[RS_PER_LANE], V (&v)[RS_PER_LANE]) {
   const int lane = threadIdx.x & 63;
-  for (long i = a + lane; i < b; i += 64) atomicAdd(&h[((keys[i] - kb) >> shift) & mask], 1);  // LDS
+#pragma unroll
+  for (int j = 0; j < RS_PER_LANE; ++j) {
+    const long i = wa + j * 64 + lane;
+    k[j] = i < wb ? kin[i] : 0;
+    if (vin != nullptr) v[j] = i < wb ? vin[i] : V(0);
+  }
+}
+
+__device__ __forceinline__ void rs_wave_hist(const int (&k)[RS_PER_LANE], long wa, long wb, int kb, int shift,
+                                             int mask, int* h) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < RS_PER_LANE; ++j)
+    if (wa + j * 64 + lane < wb) atomicAdd(&h[((k[j] - kb) >> shift) & mask], 1);  // LDS
 }
 
 __global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const int* __restrict__ keys, SegTable tb, int shift,
@@ -74,7 +93,11 @@ __global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const int* __restri
   int kb;
   tile_range(tb, blockIdx.x, a, b, kb);
   const long wa = a + (long)w * RS_SEG;
-  rs_wave_hist(keys, wa, wa + RS_SEG < b ? wa + RS_SEG : b, kb, shift, mask, sh + (long)w * nd);
+  const long wb = wa + RS_SEG < b ? wa + RS_SEG : b;
+  int k[RS_PER_LANE];
+  int dummy[RS_PER_LANE];
+  rs_load_seg<int>(keys, nullptr, wa, wb, k, dummy);
+  rs_wave_hist(k, wa, wb, kb, shift, mask, sh + (long)w * nd);
   __syncthreads();
   int* out = T + (long)blockIdx.x * nd;
   for (int c = threadIdx.x; c < nd; c += RS_THREADS) {
@@ -145,43 +168,11 @@ __global__ __launch_bounds__(1024) void rs_base_kernel(int* __restrict__ G, SegT
   }
 }
 
-// The tile is ranked into LDS first and written out in digit order: consecutive threads store
-// consecutive positions of one digit's run, instead of 64 lanes each storing 12 bytes into 64
-// different buckets (the direct form measured 1.95 ms per pass over 64M pairs: 0.8 TB/s).
-// SPLIT (64-bit payloads, last pass): the payload's low / high words go straight to two arrays
-// (the column-major copy's row ids and values) at split_off + position, so no separate unpack pass.
-template <typename V, bool SPLIT>
-__global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const int* __restrict__ kin, const V* __restrict__ vin,
-                                                                int* __restrict__ kout, V* __restrict__ vout,
-                                                                const int* __restrict__ T, const int* __restrict__ G,
-                                                                SegTable tb, int shift, int mask,
-                                                                int* __restrict__ split_lo,
-                                                                unsigned* __restrict__ split_hi, long split_off) {
-  extern __shared__ __align__(16) int shs[];
-  const int nd = mask + 1;
+// Per-wave digit counts hw[q][c] of one tile → loc[c] = the tile-local start of digit c (an
+// exclusive scan over the digits, block-wide) and hw[q][c] = wave q's cursor for digit c (loc[c]
+// plus the counts of the waves before q). Block-wide; ends with a barrier.
+__device__ __forceinline__ void rs_tile_cursors(int* hw, int nd, int* loc, int* wsum) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int t = blockIdx.x;
-  int* hw = shs;                                 // [RS_WAVES][nd] per-wave counts → wave cursors
-  int* loc = hw + RS_WAVES * nd;                 // [nd] tile-local start of each digit
-  int* gbase = loc + nd;                         // [nd] global start of the tile's digit run
-  int* lk = gbase + nd;                          // [RS_TILE] keys in tile-local sorted order
-  V* lv = reinterpret_cast<V*>(lk + RS_TILE);    // [RS_TILE] payloads (8-B aligned: nd even)
-  int* wsum = reinterpret_cast<int*>(lv + RS_TILE);  // [RS_WAVES] wave totals of the digit scan
-  for (int i = threadIdx.x; i < RS_WAVES * nd; i += RS_THREADS) hw[i] = 0;
-  __syncthreads();
-  long a, b;
-  int kb;
-  tile_range(tb, t, a, b, kb);
-  const long wa = a + (long)w * RS_SEG;
-  const long wb = wa + RS_SEG < b ? wa + RS_SEG : b;
-  rs_wave_hist(kin, wa, wb, kb, shift, mask, hw + (long)w * nd);
-  __syncthreads();
-  // tile totals per digit → exclusive scan over the digits (block-wide) → loc; wave cursors;
-  // global bases (group base + in-group prefix of this tile)
-  const int s = seg_of(tb.tile0, tb.S, t);
-  const int g = tb.grp0[s] + (t - tb.tile0[s]) / RS_TG;
-  const int* Tt = T + (long)t * nd;
-  const int* Gg = G + (long)g * nd;
   constexpr int DPT = 4;  // digits per thread (nd <= RS_THREADS·DPT = 2048)
   int tot[DPT];
   int run = 0;
@@ -210,7 +201,6 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const int* __res
     const int c = threadIdx.x * DPT + j;
     if (c < nd) {
       loc[c] = base;
-      gbase[c] = Gg[c] + Tt[c];
       int r = base;
 #pragma unroll
       for (int q = 0; q < RS_WAVES; ++q) {
@@ -222,21 +212,23 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const int* __res
     base += tot[j];
   }
   __syncthreads();
-  int* cur = hw + (long)w * nd;
-  const int db = 31 - __builtin_clz(nd);  // digit bits
+}
+
+// The wave's segment (registers kr / vr, positions wa … wb) placed in tile-local stable digit order:
+// place(pos, key, val, digit) for every valid pair, pos = the wave's cursor for the digit + the
+// pair's rank among the equal digits of its 64. The rank: the lanes holding my digit (one ballot
+// per digit bit, no cross-lane data movement), then the count of those below me.
+template <typename V, typename Place>
+__device__ __forceinline__ void rs_rank_place(const int (&kr)[RS_PER_LANE], const V (&vr)[RS_PER_LANE], long wa,
+                                              long wb, int kb, int shift, int mask, int* cur, Place place) {
+  const int lane = threadIdx.x & 63;
+  const int db = 31 - __builtin_clz(mask + 1);  // digit bits
   const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;  // lanes below this one
-  for (long i0 = wa; i0 < wb; i0 += 64) {
-    const long i = i0 + lane;
-    const bool valid = i < wb;
-    int key = 0, dg = 0;
-    V val = 0;
-    if (valid) {
-      key = kin[i];
-      val = vin[i];
-      dg = ((key - kb) >> shift) & mask;
-    }
-    // stable rank among equal digits of the 64: the lanes holding my digit (one ballot per digit
-    // bit, no cross-lane data movement), then the count of those below me
+#pragma unroll
+  for (int j = 0; j < RS_PER_LANE; ++j) {
+    const bool valid = wa + j * 64 + lane < wb;
+    const int key = kr[j];
+    const int dg = valid ? ((key - kb) >> shift) & mask : 0;
     unsigned long long peers = __ballot(valid);
     for (int bit = 0; bit < db; ++bit) {
       const bool mine = (dg >> bit) & 1;
@@ -251,12 +243,56 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const int* __res
     // complete in program order)
     __builtin_amdgcn_wave_barrier();
     if (leader) cur[dg] = pos + 1;
-    if (valid) {
-      lk[pos] = key;
-      lv[pos] = val;
-    }
+    if (valid) place(pos, key, vr[j], dg);
     __builtin_amdgcn_wave_barrier();
   }
+}
+
+// The tile is ranked into LDS first and written out in digit order: consecutive threads store
+// consecutive positions of one digit's run, instead of 64 lanes each storing 12 bytes into 64
+// different buckets (the direct form measured 1.95 ms per pass over 64M pairs: 0.8 TB/s).
+// SPLIT (64-bit payloads, last pass): the payload's low / high words go straight to two arrays
+// (the column-major copy's row ids and values) at split_off + position, so no separate unpack pass.
+template <typename V, bool SPLIT>
+__global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const int* __restrict__ kin, const V* __restrict__ vin,
+                                                                int* __restrict__ kout, V* __restrict__ vout,
+                                                                const int* __restrict__ T, const int* __restrict__ G,
+                                                                SegTable tb, int shift, int mask,
+                                                                int* __restrict__ split_lo,
+                                                                unsigned* __restrict__ split_hi, long split_off) {
+  extern __shared__ __align__(16) int shs[];
+  const int nd = mask + 1;
+  const int w = threadIdx.x >> 6;
+  const int t = blockIdx.x;
+  int* hw = shs;                                 // [RS_WAVES][nd] per-wave counts → wave cursors
+  int* loc = hw + RS_WAVES * nd;                 // [nd] tile-local start of each digit
+  int* gbase = loc + nd;                         // [nd] global start of the tile's digit run
+  int* lk = gbase + nd;                          // [RS_TILE] keys in tile-local sorted order
+  V* lv = reinterpret_cast<V*>(lk + RS_TILE);    // [RS_TILE] payloads (8-B aligned: nd even)
+  int* wsum = reinterpret_cast<int*>(lv + RS_TILE);  // [RS_WAVES] wave totals of the digit scan
+  for (int i = threadIdx.x; i < RS_WAVES * nd; i += RS_THREADS) hw[i] = 0;
+  __syncthreads();
+  long a, b;
+  int kb;
+  tile_range(tb, t, a, b, kb);
+  const long wa = a + (long)w * RS_SEG;
+  const long wb = wa + RS_SEG < b ? wa + RS_SEG : b;
+  int kr[RS_PER_LANE];
+  V vr[RS_PER_LANE];
+  rs_load_seg<V>(kin, vin, wa, wb, kr, vr);
+  rs_wave_hist(kr, wa, wb, kb, shift, mask, hw + (long)w * nd);
+  __syncthreads();
+  rs_tile_cursors(hw, nd, loc, wsum);
+  // global bases: group base + in-group prefix of this tile
+  const int s = seg_of(tb.tile0, tb.S, t);
+  const int g = tb.grp0[s] + (t - tb.tile0[s]) / RS_TG;
+  const int* Tt = T + (long)t * nd;
+  const int* Gg = G + (long)g * nd;
+  for (int c = threadIdx.x; c < nd; c += RS_THREADS) gbase[c] = Gg[c] + Tt[c];
+  rs_rank_place(kr, vr, wa, wb, kb, shift, mask, hw + (long)w * nd, [&](int pos, int key, V val, int) {
+    lk[pos] = key;
+    lv[pos] = val;
+  });
   __syncthreads();
   // out in tile-local sorted order: a digit's run of the tile is one contiguous global range
   const int len = (int)(b - a);
@@ -272,6 +308,83 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const int* __res
     } else {
       vout[gp] = lv[i];
     }
+  }
+}
+
+// The column-major copy's second (last) pass, bucket-local: after a stable pass on the HIGH
+// column digit (key bits 10 …), segment s's pairs of high digit h — the columns h·1024 … h·1024 +
+// 1023 of batch s — are one contiguous run ("bucket") of the array. One block per bucket sorts it
+// by the low 10 bits, stably, in chunks of RS_TILE pairs (one chunk for a bucket of ≤ 8192 pairs:
+// the 64M-pair, 1M-column SVC run averages 6,250), and writes
+//   * the payload halves (row id, value bits) to erow / evals, each pair straight from registers
+//     to its final position: the stores of a block stay inside its bucket's ~25 KB of each array,
+//     so L2 assembles whole lines (no LDS staging: 40 KB of LDS, 3 blocks per CU);
+//   * the bucket's columns' entries of the column pointer, from its column histogram — no sorted
+//     keys are written and no separate column-pointer pass reads them back.
+// Replaces an LSD second pass (global digit scatter + its histogram / scans) plus the column-
+// pointer kernel (155–241 µs over the 256 MB of sorted keys).
+constexpr int CB_ND = 1024;  // columns per bucket (low digit)
+
+__global__ __launch_bounds__(RS_THREADS) void rs_csc_bucket_kernel(const int* __restrict__ kin,
+                                                                   const uint64_t* __restrict__ vin,
+                                                                   const int* __restrict__ G, SegTable tb, int ndA,
+                                                                   int d, long b0, int* __restrict__ colptr,
+                                                                   int* __restrict__ erow,
+                                                                   unsigned* __restrict__ evals, long split_off) {
+  extern __shared__ __align__(16) int shs[];
+  int* hw = shs;                     // [RS_WAVES][CB_ND] per-wave counts → wave cursors
+  int* loc = hw + RS_WAVES * CB_ND;  // [CB_ND] chunk-local start of each column
+  int* cb = loc + CB_ND;             // [CB_ND] bucket-local start of each column's next entries
+  int* wsum = cb + CB_ND;            // [RS_WAVES]
+  const int w = threadIdx.x >> 6;
+  const int s = blockIdx.x / ndA, h = blockIdx.x - s * ndA;
+  const long seg0 = tb.bound[s], seg1 = tb.bound[s + 1];
+  long start = seg0, end = seg0;
+  if (seg1 > seg0) {  // an empty segment has no group rows in G
+    const int* Gs = G + (long)tb.grp0[s] * ndA;
+    start = Gs[h];
+    end = h + 1 < ndA ? Gs[h + 1] : seg1;
+  }
+  const int kb = tb.kbase[s];
+  const int c0 = h * CB_ND;
+  const int ncol = d - c0 < CB_ND ? d - c0 : CB_ND;
+  int* cp = colptr + (b0 + s) * (long)(d + 1);
+  const int rel = (int)(start - seg0);
+  if (h == 0 && threadIdx.x == 0) cp[d] = (int)(seg1 - seg0);
+  const bool one = end - start <= RS_TILE;
+  if (!one) {  // the whole bucket's column histogram first → bucket-local column starts
+    for (int i = threadIdx.x; i < RS_WAVES * CB_ND; i += RS_THREADS) hw[i] = 0;
+    __syncthreads();
+    for (long i = start + threadIdx.x; i < end; i += RS_THREADS) atomicAdd(&hw[(kin[i] - kb) & (CB_ND - 1)], 1);
+    __syncthreads();
+    rs_tile_cursors(hw, CB_ND, cb, wsum);  // (one row of counts: the others are zero)
+    for (int c = threadIdx.x; c < ncol; c += RS_THREADS) cp[c0 + c] = rel + cb[c];
+  }
+  const int* base = one ? loc : cb;  // a one-chunk bucket: the chunk's column starts are the bucket's
+  for (long a = start; a < end || (one && a == start); a += RS_TILE) {
+    const long b = a + RS_TILE < end ? a + RS_TILE : end;
+    for (int i = threadIdx.x; i < RS_WAVES * CB_ND; i += RS_THREADS) hw[i] = 0;
+    __syncthreads();
+    const long wa = a + (long)w * RS_SEG;
+    const long wb = wa + RS_SEG < b ? wa + RS_SEG : b;
+    int kr[RS_PER_LANE];
+    uint64_t vr[RS_PER_LANE];
+    rs_load_seg<uint64_t>(kin, vin, wa, wb, kr, vr);
+    rs_wave_hist(kr, wa, wb, kb, 0, CB_ND - 1, hw + (long)w * CB_ND);
+    __syncthreads();
+    rs_tile_cursors(hw, CB_ND, loc, wsum);
+    if (one)
+      for (int c = threadIdx.x; c < ncol; c += RS_THREADS) cp[c0 + c] = rel + loc[c];
+    rs_rank_place(kr, vr, wa, wb, kb, 0, CB_ND - 1, hw + (long)w * CB_ND, [&](int pos, int, uint64_t val, int dg) {
+      const long gp = split_off + start + base[dg] + (pos - loc[dg]);  // = start + pos for one chunk
+      erow[gp] = (int)(unsigned)val;
+      evals[gp] = (unsigned)(val >> 32);
+    });
+    if (one) break;
+    __syncthreads();
+    const int len = (int)(b - a);
+    for (int c = threadIdx.x; c < CB_ND; c += RS_THREADS) cb[c] += (c + 1 < CB_ND ? loc[c + 1] : len) - loc[c];
+    __syncthreads();
   }
 }
 
@@ -382,4 +495,38 @@ FMLX_API int fmlx_seg_sort32(int* keys, uint32_t* vals, int* keys_alt, uint32_t*
                              void* stream) {
   return seg_sort<uint32_t>(keys, vals, keys_alt, vals_alt, bound, kbase, S, key_bits, digit_bits, scratch,
                             scratch_ints, (hipStream_t)stream);
+}
+
+// The fp32 column-major copy of a run of batches in two passes (see rs_csc_bucket_kernel):
+// keys = slot·d + column over 11 … 20 key bits, 64-bit (value bits << 32 | row) payloads. Pass 1
+// sorts every segment stably by the key's high bits (keys / vals → keys_alt / vals_alt), pass 2
+// writes erow / evals at split_off + position and the column pointer rows b0 … b0 + S − 1
+// (int32 [*, d + 1]). `bound` / `kbase` are HOST arrays; scratch as fmlx_seg_sort_scratch.
+FMLX_API int fmlx_csc_sort_split(int* keys, uint64_t* vals, int* keys_alt, uint64_t* vals_alt, const long* bound,
+                                 const int* kbase, int S, int key_bits, int d, int* scratch, long scratch_ints,
+                                 int* erow, unsigned* evals, long split_off, int* colptr, long b0, void* stream) {
+  SegTable tb{};
+  int rc = make_table(bound, kbase, S, tb);
+  if (rc) return rc;
+  if (key_bits < 11 || key_bits > 20 || d < 1 || d > (1 << key_bits)) return -5;
+  const int dbA = key_bits - 10;
+  const int ndA = 1 << dbA;
+  if (scratch_ints < (long)(tb.ntile + tb.ngrp) * ndA) return -6;
+  hipStream_t st = (hipStream_t)stream;
+  int* T = scratch;
+  int* G = scratch + (long)tb.ntile * ndA;
+  if (tb.ntile > 0) {
+    const size_t lds = (size_t)RS_WAVES * ndA * sizeof(int);
+    const size_t lds_sc = (size_t)(RS_WAVES + 2) * ndA * sizeof(int) + (size_t)RS_TILE * (sizeof(int) + 8) +
+                          RS_WAVES * sizeof(int);
+    hipLaunchKernelGGL(rs_hist_kernel, dim3(tb.ntile), dim3(RS_THREADS), lds, st, keys, tb, 10, ndA - 1, T);
+    hipLaunchKernelGGL(rs_colscan_kernel, dim3((ndA + 255) / 256, tb.ngrp), dim3(256), 0, st, T, tb, ndA, G);
+    hipLaunchKernelGGL(rs_base_kernel, dim3(tb.S), dim3(1024), 0, st, G, tb, ndA);
+    hipLaunchKernelGGL((rs_scatter_kernel<uint64_t, false>), dim3(tb.ntile), dim3(RS_THREADS), lds_sc, st, keys, vals,
+                       keys_alt, vals_alt, T, G, tb, 10, ndA - 1, (int*)nullptr, (unsigned*)nullptr, 0L);
+  }
+  const size_t lds_b = (size_t)(RS_WAVES + 2) * CB_ND * sizeof(int) + RS_WAVES * sizeof(int);
+  hipLaunchKernelGGL(rs_csc_bucket_kernel, dim3((unsigned)(S * ndA)), dim3(RS_THREADS), lds_b, st, keys_alt, vals_alt,
+                     G, tb, ndA, d, b0, colptr, erow, evals, split_off);
+  return (int)hipGetLastError();
 }

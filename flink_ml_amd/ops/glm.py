@@ -215,6 +215,8 @@ def grad_csr(indptr, idx, val, y, wt, coef, n, d, B, loss, state, grad) -> None:
 # sparse rounds through per-batch transposes (csrc/glm.hip glm_csc_bwd_kernel)
 CSC_MAX_BYTES = int(os.environ.get("FMLX_CSC_MAX_BYTES", str(8 << 30)))
 CSC_RUN_MAX = int(os.environ.get("FMLX_CSC_RUN_MAX", "16"))  # consecutive batches transposed per sort
+# fp32 copies over 11–20 column bits: high-bits pass + bucket-local pass (0: two LSD passes + colptr)
+CSC_BUCKET = os.environ.get("FMLX_CSC_BUCKET", "1") != "0"
 
 
 SEG_SORT_DIGIT_BITS = 10  # radix.hip RS_MAX_DIGIT_BITS
@@ -389,6 +391,8 @@ class BatchCsc:
                 self._transpose_torch(b0, len(run), r0, r1, j0, j1)
 
     def _transpose_native(self, b0, slots, r0, r1, j0, j1) -> None:
+        import numpy as np
+
         indptr, indices, values = self._src
         dev = values.device
         m, d = j1 - j0, self.d
@@ -398,6 +402,26 @@ class BatchCsc:
         seg = [self.bounds[b0 + s] - j0 for s in range(slots + 1)]
         kbase = [s * d for s in range(slots)]
         bits = max(1, int(d - 1).bit_length())
+        starts = np.ascontiguousarray(np.asarray(seg, dtype=np.int64))  # batch starts, run-relative
+        if values.dtype == torch.float32 and CSC_BUCKET and 11 <= bits <= 20:
+            # (value bits, row) as one 64-bit payload; the sort's keys are the CSR columns
+            # themselves (segment = batch, so no slot offset): a stable pass on the high column
+            # bits, then one block per (batch, 1024-column) bucket writes rows / values in column
+            # order and the column pointers — no key array, no sorted keys
+            pay = torch.empty(m, dtype=torch.int64, device=dev)
+            native.call("fmlx_csc_keys64", native.ptr(indptr), native.ptr(indices), native.ptr(values), r0, r1, self.B,
+                        d, j0, None, native.ptr(pay), stream)
+            cols = indices[j0:j1]
+            key_alt, pay_alt = torch.empty_like(cols), torch.empty_like(pay)  # held: no aliasing
+            sc = torch.empty(seg_sort_scratch(seg, bits), dtype=torch.int32, device=dev)
+            kb = np.zeros(slots, dtype=np.int32)
+            rc = native.kernels().fmlx_csc_sort_split(
+                native.ptr(cols), native.ptr(pay), native.ptr(key_alt), native.ptr(pay_alt), starts.ctypes.data,
+                kb.ctypes.data, slots, bits, d, native.ptr(sc), sc.numel(), native.ptr(self.erow),
+                native.ptr(self.evals), j0, native.ptr(self.colptr), b0, stream)
+            if rc != 0:
+                raise RuntimeError("fmlx_csc_sort_split failed: %d" % rc)
+            return
         key = torch.empty(m, dtype=torch.int32, device=dev)
         if values.dtype == torch.float32:
             # (value bits, row) as one 64-bit payload through the sort, then a sequential split
@@ -414,7 +438,7 @@ class BatchCsc:
             keys_out, order = seg_sort(key, iota, seg, kbase, bits)
             native.call("fmlx_csc_fill", 1, native.ptr(order), m, j0, native.ptr(rel), native.ptr(values),
                         native.ptr(self.erow), native.ptr(self.evals), stream)
-        native.call("fmlx_csc_colptr", native.ptr(keys_out), m, slots, d, native.ptr(indptr), b0, self.B, self.n, j0,
+        native.call("fmlx_csc_colptr", native.ptr(keys_out), m, slots, d, starts.ctypes.data, b0,
                     native.ptr(self.colptr), stream)
 
     def _transpose_torch(self, b0, slots, r0, r1, j0, j1) -> None:

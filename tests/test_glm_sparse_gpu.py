@@ -114,28 +114,45 @@ def test_sparse_sgd_two_ranks_one_gpu():
     assert res[0][1] == res[1][1]  # replicas identical
 
 
-@pytest.mark.parametrize("run_max,vdtype", [(1, torch.float32), (3, torch.float64), (16, torch.float32)])
-def test_batch_csc_device_transpose_matches_host(run_max, vdtype, monkeypatch):
-    """Per-batch column-major copies built on the device (csc_build.hip keys → bit-limited radix
-    sort → fill + column pointers straight from the sorted keys, runs of consecutive batches in
+@pytest.mark.parametrize("run_max,vdtype,d,B,skew,bucket", [
+    (1, torch.float32, 3_001, 1_000, False, True), (3, torch.float64, 3_001, 1_000, False, True),
+    (16, torch.float32, 3_001, 1_000, False, True),
+    (16, torch.float32, 3_001, 1_000, False, False),      # two LSD passes + the column-pointer kernel
+    (4, torch.float32, 700, 1_000, False, True),          # 10 column bits: one LSD pass
+    (6, torch.float32, 1_000_000, 1_000, False, True),    # 20 column bits (the SVC shape's width)
+    (5, torch.float32, 3_001, 4_000, True, True),         # buckets of > 8192 entries: chunked
+])
+def test_batch_csc_device_transpose_matches_host(run_max, vdtype, d, B, skew, bucket, monkeypatch):
+    """Per-batch column-major copies built on the device (csc_build.hip keys → radix.hip: a stable
+    pass on the high column bits + one block per (batch, 1024-column) bucket writing rows, values
+    and column pointers; or LSD passes + the column-pointer kernel; runs of consecutive batches in
     one sort) equal the host construction exactly — also after the storage, first sized for the
     leading batches of a short fit, grows to the whole partition (pointers move: ``version``)."""
     _need_gpu()
     from flink_ml_amd.ops import glm as gk
 
     monkeypatch.setattr(gk, "CSC_RUN_MAX", run_max)
+    monkeypatch.setattr(gk, "CSC_BUCKET", bucket)
     g = torch.Generator().manual_seed(0)
-    n, d, B = 20_037, 3_001, 1_000
+    n = 20_037
     lens = torch.randint(0, 12, (n,), generator=g)
     lens[3 * B:4 * B] = 0  # an empty batch
     indptr = torch.zeros(n + 1, dtype=torch.int64)
     indptr[1:] = torch.cumsum(lens, 0)
-    idx = torch.cat([torch.sort(torch.randperm(d, generator=g)[:int(k)]).values for k in lens]).to(torch.int32)
+    rows = []
+    for k in lens.tolist():
+        if skew and torch.rand(1, generator=g).item() < 0.8:  # most rows inside the first 1024 columns
+            rows.append(torch.sort(torch.randperm(1024, generator=g)[:k]).values)
+        else:
+            rows.append(torch.sort(torch.randint(0, d, (4 * k + 4,), generator=g).unique()[:k]).values)
+    idx = torch.cat(rows).to(torch.int32)
+    lens = torch.tensor([len(r) for r in rows])
+    indptr[1:] = torch.cumsum(lens, 0)
     vals = torch.rand(int(indptr[-1]), generator=g, dtype=torch.float64).to(vdtype)
     dev = gk.BatchCsc.alloc(indptr.cuda(), idx.cuda(), vals.cuda(), n, d, B, max_rounds=5)
     dev.ensure([0, 1, 2, 3, 4])
     assert dev.cap == 5 and dev.version == 0 and dev.erow.numel() == int(indptr[5 * B])
-    dev.ensure([0, 1, 2, 7, 8, 12, 19, 20])
+    dev.ensure([0, 1, 2, 7, 8, 12, 19, 20, dev.P - 1])
     assert dev.cap == dev.P and dev.version == 1
     dev.ensure(range(dev.P))
     host = gk.BatchCsc.alloc(indptr, idx, vals, n, d, B)
