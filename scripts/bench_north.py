@@ -196,10 +196,14 @@ def run_svc_sparse(a, ctx):
     # five independent whole fits (a new trainer each: its own lazy transposes); every sample and
     # their max are reported, the value is the max (round 3 saw single launches wait 20–35 ms)
     samples = []
+    mem_deltas = []  # device allocations / frees the caching allocator made inside each fit
     tr2 = None
     for _ in range(int(os.environ.get("BENCH_FIT_SAMPLES", "5"))):
         tr2 = None
+        m0 = torch.cuda.memory_stats(ctx.device)
         fit_i, tr2 = _timed(ctx, whole_fit)
+        m1 = torch.cuda.memory_stats(ctx.device)
+        mem_deltas.append([m1.get(k, 0) - m0.get(k, 0) for k in ("num_device_alloc", "num_device_free")])
         samples.append(fit_i)
     fit_s = max(samples)
     # steady state: rounds of an already warmed trainer (graphs captured and primed, every batch
@@ -221,7 +225,7 @@ def run_svc_sparse(a, ctx):
             "value": round(gb * iters / fit_s, 1), "unit": "samples/s", "higher_is_better": True,
             "totalTimeMs": round(fit_s * 1e3, 3), "fit_ms_per_round": round(fit_s * 1e3 / iters, 4),
             "whole_fit_samples_ms": [round(x * 1e3, 3) for x in samples],
-            "whole_fit_max_ms": round(max(samples) * 1e3, 3), "whole_fit_median_ms": round(sorted(samples)[len(samples) // 2] * 1e3, 3),
+            "whole_fit_max_ms": round(max(samples) * 1e3, 3), "whole_fit_device_alloc_free": mem_deltas, "whole_fit_median_ms": round(sorted(samples)[len(samples) // 2] * 1e3, 3),
             "steady_ms_per_round": round(steady_s * 1e3 / steady, 4),
             "steady_samples_per_s": round(gb * steady / steady_s, 1),
             "note": "value / totalTimeMs: the MAX of 5 whole maxIter-round fits (trainer set-up incl. the "
