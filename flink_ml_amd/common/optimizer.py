@@ -248,11 +248,6 @@ class DeviceGlmTrainer:
         # round e (csrc/glm.hip defer_prologue_xgmi); FMLX_GLM_DEFER_XGMI=0 keeps the ticketed tail
         self.defer = ((self.mode == gk.TAIL_UPDATE or self.mode == gk.TAIL_XGMI and gk.DEFER_XGMI)
                       and self.scratch is not None and not self.scratch.det and gk.defer_supported(self.d, acc))
-        # 1 GPU: consecutive deferred launches overlap on two streams (csrc/glm.hip overlap_wait);
-        # its round-number protocol needs the odd launches' word pre-set to 1
-        self.overlap = self.defer and self.mode == gk.TAIL_UPDATE and gk.OVERLAP
-        if self.overlap:
-            self.state[gk.ST_ROUND_ALT:gk.ST_ROUND_ALT + 1].fill_(1)
         self.parity = 0
         self.cw = torch.zeros((2, self.d), dtype=acc, device=dev) if self.defer else None
         self._flushed = False
@@ -330,7 +325,7 @@ class DeviceGlmTrainer:
         # every rank launches the round, also one without rows: it still joins the reduction tail
         gk.glm_round(self.X, self.y, self.w, self.coef, self.B, self.loss, self.state, self.scratch, self.mode,
                      self.feedback, s.max_iter, s.tol, s.learning_rate, s.reg, s.elastic_net, xg=self.xg, rounds=rounds,
-                     defer=self.defer, parity=self.parity, cw=self.cw, overlap=self.overlap)
+                     defer=self.defer, parity=self.parity, cw=self.cw)
         if self.defer:
             self.parity = (self.parity + rounds) & 1
         if self.mode == gk.TAIL_FEEDBACK:
@@ -476,11 +471,9 @@ class DeviceGlmTrainer:
         return int(self.state[4].item())
 
     def check_exchange(self) -> None:
-        """Raises if a bounded xGMI wait gave up (a peer never arrived), or an overlapped launch
-        stopped waiting for the previous one: the rounds since then must not be reported."""
+        """Raises if a bounded xGMI wait gave up (a peer never arrived): the rounds since then
+        used a partial feedback and must not be reported."""
         comm.check_collectives()
-        if self.overlap and int(self.scratch.cnt[gk.ARR_ERR].item()) != 0:
-            raise RuntimeError("SGD round: an overlapped launch timed out waiting for the previous round")
 
     def fit(self) -> np.ndarray:
         ck = AlgorithmCheckpoint("sgd")
@@ -488,7 +481,7 @@ class DeviceGlmTrainer:
         restored = ck.restore()
         if self.defer and (ck.mgr is not None or tracing.rounds_enabled()):
             # checkpoints and per-round logs read the round's own coefficients / feedback
-            self.defer, self.cw, self.overlap = False, None, False
+            self.defer, self.cw = False, None
             self.graphs.clear()
         if restored is not None:
             done, st = restored

@@ -32,8 +32,6 @@
 //    The batch of round e is rows [(e mod P)·B, min(+B, n)), P = ceil(n/B): exactly the
 //    reference's sequential slicing with reset-to-0 (SGD.java:263-268).
 #include "common.h"
-
-#include <mutex>
 #include "xgmi.h"
 
 namespace {
@@ -146,8 +144,6 @@ struct GlmTail {
   int wl_off;      // deferred: byte offset of the block's [d] coefficient image in LDS
   int ring_off;    // LDS-DMA row path: byte offset of the [WPB][DEPTH][U][2 KiB] row ring
   int xb_off;      // deferred TAIL_XGMI: byte offset of the lead block's [d+2] exchange row in LDS
-  int overlap;     // deferred TAIL_UPDATE: consecutive launches may overlap (two streams) — see
-                   // overlap_wait
   long long* trace;  // diagnostics (null = off): per block {start, rows done, end, hw id} in
                      // 100 MHz s_memrealtime ticks (scripts/trace_glm_blocks.py)
 };
@@ -355,43 +351,6 @@ __device__ void glm_round_tail_atomic(const GlmTail& tl, int d, A* coef, int* st
   glm_round_finish<A>(tl, sbuf, d, coef, state, e, one_pass, wa, wb);
 }
 
-// Overlapped deferred launches (tl.overlap; the launcher alternates launches between two streams,
-// so launch e + 1's blocks start while launch e's last blocks still run: no kernel boundary —
-// drain, end-of-kernel release, next dispatch — between two rounds). The hand-off the boundary
-// gave becomes an arrival count: every block of launch e adds 1 to cnt[ARR_IDX + e % 3] once all
-// its writes of the round (gradient atomics, the zeroed slot, the lead's coefficients / state
-// words, all agent-scope) are performed; launch e + 1 waits for gridDim.x arrivals of launch e
-// right after issuing its first row loads, before it reads anything launch e wrote. The lead
-// block of launch e re-arms the counter launch e + 1 is not using (cnt[ARR_IDX + (e + 1) % 3]:
-// launch e − 1 waited on it, launch e + 1 adds into it only after its own wait). At most two
-// launches are in flight (a stream orders e and e + 2) and two blocks of the kernel fit on a CU,
-// so a waiting block never keeps a block it waits for from being dispatched. The wait is
-// bounded: a timeout raises cnt[ARR_ERR] (the host checks it) instead of hanging the GPU.
-constexpr int ARR_IDX = 124;  // tl.cnt words 124..126: arrival counters; 127: wait timed out
-constexpr int ARR_ERR = 127;
-constexpr long OVERLAP_SPIN_LIMIT = 1L << 22;  // polls of ~0.1 µs: ~0.5 s
-
-__device__ __forceinline__ void overlap_wait(const GlmTail& tl, int e) {
-  if (e > 0 && threadIdx.x == 0) {
-    const int* c = tl.cnt + ARR_IDX + (e + 2) % 3;
-    long spins = 0;
-    while (ld_agent(c) < (int)gridDim.x) {
-      if (++spins > OVERLAP_SPIN_LIMIT) {
-        st_agent(tl.cnt + ARR_ERR, 1);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __syncthreads();
-}
-
-__device__ __forceinline__ void overlap_arrive(const GlmTail& tl, int e) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's writes of the round performed
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(tl.cnt + ARR_IDX + e % 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // Deferred round completion (1 GPU, TAIL_UPDATE with the atomic tail). Launch e first completes
 // round e − 1: every block sums the replicas of that round's accumulator slot (fixed order, as
 // the ticketed tail does), evaluates TerminateOnMaxIterOrTol and applies the SGD update into an
@@ -412,16 +371,7 @@ __device__ bool defer_prologue(const GlmTail& tl, A* coef, int* state, int e, in
   A* cw = (A*)tl.cw;
   A* fb = (A*)tl.feedback;
   const bool lead = blockIdx.x == 0;
-  const bool ov = tl.overlap != 0;
   bool stop = false;
-  if (ov) {
-    overlap_wait(tl, e);
-    if (lead && tid == 0) st_agent(tl.cnt + ARR_IDX + (e + 1) % 3, 0);
-    if (ld_agent(&state[ST_DONE])) {  // an earlier launch ended the iteration: a no-op round
-      overlap_arrive(tl, e);
-      return true;
-    }
-  }
   if (e == 0) {
     for (long c = tid; c < d; c += nt) wl[c] = coef[c];
   } else {
@@ -445,7 +395,7 @@ __device__ bool defer_prologue(const GlmTail& tl, A* coef, int* state, int e, in
       A v[ACC_MAX_REPS];
 #pragma unroll
       for (int q = 0; q < ACC_MAX_REPS; ++q) v[q] = q < R ? ld_agent(prev + q * ald + c) : (A)0;
-      const A w0 = ov ? ld_agent(wp + c) : wp[c];
+      const A w0 = wp[c];
       A g = (A)0;
 #pragma unroll
       for (int q = 0; q < ACC_MAX_REPS; ++q) g += v[q];
@@ -458,33 +408,20 @@ __device__ bool defer_prologue(const GlmTail& tl, A* coef, int* state, int e, in
     }
   }
   A* nxt = ring + (long)((e + 1) % 3) * slot;
-  for (long i = (long)blockIdx.x * nt + tid; i < slot; i += (long)gridDim.x * nt) {
-    if (ov) st_agent(nxt + i, (A)0);
-    else nxt[i] = (A)0;
-  }
+  for (long i = (long)blockIdx.x * nt + tid; i < slot; i += (long)gridDim.x * nt) nxt[i] = (A)0;
   __syncthreads();
   if (lead) {
     A* wc = cw + (long)(e & 1) * d;
     for (long c = tid; c < d; c += nt) {
-      if (ov) st_agent(wc + c, wl[c]);
-      else wc[c] = wl[c];
+      wc[c] = wl[c];
       coef[c] = wl[c];  // launch 0: the value every block just read
     }
     if (tid == 0) {
-      if (ov) {
-        // the round word of the launch two later (same stream: a kernel boundary orders it);
-        // executed / done are read by the overlapping next launch
-        state[tl.parity ? ST_ROUND_ALT : ST_ROUND] = e + 2;
-        if (e > 0) st_agent(&state[ST_EXECUTED], ld_agent(&state[ST_EXECUTED]) + 1);
-        if (stop) st_agent(&state[ST_DONE], 1);
-      } else {
-        state[tl.parity ? ST_ROUND : ST_ROUND_ALT] = e + 1;
-        if (e > 0) state[ST_EXECUTED] += 1;
-        if (stop) state[ST_DONE] = 1;
-      }
+      state[tl.parity ? ST_ROUND : ST_ROUND_ALT] = e + 1;
+      if (e > 0) state[ST_EXECUTED] += 1;
+      if (stop) state[ST_DONE] = 1;
     }
   }
-  if (ov && stop) overlap_arrive(tl, e);
   return stop;
 }
 
@@ -642,9 +579,7 @@ __global__ __launch_bounds__(WPB * 64, (glm_min_waves<T, EPC, CPL, U>())) void g
   const long long t_start = tl.trace ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
   int e;
   if (tl.defer) {
-    // (overlapped launches read the done word after waiting for the previous launch: it may be
-    // the one that sets it)
-    if (!tl.overlap && state[ST_DONE]) return;
+    if (state[ST_DONE]) return;
     e = state[tl.parity ? ST_ROUND_ALT : ST_ROUND];
   } else if (!round_running(state, e)) return;
   long start = 0, end = 0;  // a rank with no rows (or a zero local batch) still joins the tail
@@ -1021,10 +956,7 @@ __global__ __launch_bounds__(WPB * 64, (glm_min_waves<T, EPC, CPL, U>())) void g
       __syncthreads();
       if (threadIdx.x == 0) tl.trace[(long)blockIdx.x * 4 + 2] = (long long)__builtin_amdgcn_s_memrealtime();
     }
-    if (tl.defer) {  // launch e + 1 completes this round
-      if (tl.overlap) overlap_arrive(tl, e);
-      return;
-    }
+    if (tl.defer) return;  // launch e + 1 completes this round
     glm_round_tail_atomic<A>(tl, d, coef, state, e, buf, sflag);
     return;
   }
@@ -1724,29 +1656,6 @@ FMLX_API int fmlx_glm_grad_partials(int dtype, int epc, int cpl, int u, const vo
                       const_cast<int*>(state), partials, nblocks, tl, 0, (hipStream_t)stream);
 }
 
-// The second stream (+ fork / join events) of the overlapped deferred launches, one per device,
-// created on first use and kept (a stream costs ~7 ms to create).
-struct OverlapStreams {
-  hipStream_t s;
-  hipEvent_t fork, join;
-};
-static OverlapStreams* overlap_streams() {
-  static OverlapStreams tab[64];
-  static bool made[64];
-  static std::mutex mu;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  std::lock_guard<std::mutex> lock(mu);
-  if (!made[dev]) {
-    OverlapStreams& o = tab[dev];
-    if (hipStreamCreateWithFlags(&o.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&o.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&o.join, hipEventDisableTiming) != hipSuccess) return nullptr;
-    made[dev] = true;
-  }
-  return &tab[dev];
-}
-
 // One whole SGD round in one launch (see the header comment). cnt: int32[17] zero-initialised;
 // stage1: [ceil(nblocks/32)][d+2]; feedback: [d+2] (may be null for TAIL_UPDATE / TAIL_XGMI).
 // peers/gen/err/spin_limit: the xGMI exchange (TAIL_XGMI only, see parallel/xgmi.py).
@@ -1756,7 +1665,7 @@ FMLX_API int fmlx_glm_round(int dtype, int epc, int cpl, int u, const void* X, l
                             double tol, double lr,
                             double reg, double en, void* const* peers, int world, int rank, int* gen, int* err,
                             long spin_limit, int flags, int rounds, int defer, int parity, void* cw,
-                            int overlap, void* stream) {
+                            void* stream) {
   if (mode != TAIL_PARTIALS && cnt == nullptr) return -4;
   if (mode != TAIL_PARTIALS && det && (nblocks > TAIL_GROUP * TAIL_MAXG || stage1 == nullptr)) return -4;
   if (mode != TAIL_PARTIALS && !det && (nblocks > TAIL_GROUP * TAIL_TOP || acc == nullptr)) return -4;
@@ -1781,32 +1690,13 @@ FMLX_API int fmlx_glm_round(int dtype, int epc, int cpl, int u, const void* X, l
   tl.defer = defer;
   tl.cw = cw;
   tl.trace = g_trace;
-  tl.overlap = overlap && defer && mode == TAIL_UPDATE && !det;
-  const int nr = rounds > 0 ? rounds : 1;
-  hipStream_t s0 = (hipStream_t)stream, s1 = s0;
-  OverlapStreams* os = nullptr;
-  if (tl.overlap && nr > 1) {
-    // odd launches on a second stream forked from (and joined back into) the caller's: launch
-    // i + 1 may start while launch i drains (hipGraph capture records the fork / join)
-    os = overlap_streams();
-    if (os == nullptr) return -9;
-    s1 = os->s;
-    hipError_t er = hipEventRecord(os->fork, s0);
-    if (er == hipSuccess) er = hipStreamWaitEvent(s1, os->fork, 0);
-    if (er != hipSuccess) return (int)er;
-  }
   // `rounds` consecutive rounds, one launch each (a kernel boundary, ~1.5 µs, is cheaper than an
   // in-kernel grid-wide round barrier: measured, scripts/stream_probe2.hip)
-  for (int i = 0; i < nr; ++i) {
+  for (int i = 0; i < (rounds > 0 ? rounds : 1); ++i) {
     tl.parity = (parity + i) & 1;  // deferred mode: launches alternate their round-number word
     const int rc = launch_round(dtype, epc, cpl, u, X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl,
-                                flags, (i & 1) ? s1 : s0);
+                                flags, (hipStream_t)stream);
     if (rc) return rc;
-  }
-  if (os != nullptr) {
-    hipError_t er = hipEventRecord(os->join, s1);
-    if (er == hipSuccess) er = hipStreamWaitEvent(s0, os->join, 0);
-    if (er != hipSuccess) return (int)er;
   }
   return 0;
 }

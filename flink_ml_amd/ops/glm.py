@@ -168,18 +168,14 @@ class RoundScratch:
 
 def glm_round(X, y, wt, coef, B: int, loss: int, state, scratch: RoundScratch, mode: int, feedback=None,
               max_iter: int = 1, tol: float = 0.0, lr: float = 0.0, reg: float = 0.0, en: float = 0.0,
-              xg=None, rounds: int = 1, defer: bool = False, parity: int = 0, cw=None, overlap: bool = False) -> None:
+              xg=None, rounds: int = 1, defer: bool = False, parity: int = 0, cw=None) -> None:
     """``rounds`` SGD rounds (loss+gradient over the round's batch, fixed-order reduction and — by
     mode — feedback output, update, or xGMI exchange + update), each ONE kernel launch predicated
     on the device running flag (one host call issues all ``rounds`` launches).
 
     ``defer``: 1-GPU TAIL_UPDATE with the atomic tail only — launch e completes round e − 1 in its
     prologue; launch i of the call reads its round number from state word ``(parity + i) & 1``
-    and ``cw`` is the [2, d] coefficient ring. ``overlap`` (deferred TAIL_UPDATE): the call's odd
-    launches go to a second stream and every launch waits in-kernel for the previous one's
-    arrivals, so consecutive rounds overlap instead of meeting at a kernel boundary; the trainer
-    must use it for ALL its launches (the round-number words follow a different protocol) and
-    start with state[ST_ROUND_ALT] = 1."""
+    and ``cw`` is the [2, d] coefficient ring."""
     epc, cpl = pick_layout(X)
     flags = 1 if X.shape[0] * X.stride(0) * X.element_size() > NT_MIN_BYTES else 0
     if xg is not None:
@@ -191,7 +187,7 @@ def glm_round(X, y, wt, coef, B: int, loss: int, state, scratch: RoundScratch, m
                 native.ptr(scratch.partials), scratch.nparts, mode, int(scratch.det), native.ptr(scratch.cnt),
                 native.ptr(scratch.acc), native.ptr(scratch.stage1), native.ptr(feedback), int(max_iter), float(tol), float(lr), float(reg),
                 float(en), peers, world, rank, gen, err, int(spin), flags, int(rounds), int(bool(defer)), int(parity),
-                native.ptr(cw), int(bool(overlap)), native.stream_ptr(X.device))
+                native.ptr(cw), native.stream_ptr(X.device))
 
 
 def reduce_update(partials, nparts: int, d: int, stage1, coef, feedback, state, max_iter, tol, lr, reg, en) -> None:
@@ -217,11 +213,6 @@ def grad_csr(indptr, idx, val, y, wt, coef, n, d, B, loss, state, grad) -> None:
 
 
 # sparse rounds through per-batch transposes (csrc/glm.hip glm_csc_bwd_kernel)
-# deferred 1-GPU rounds: consecutive launches overlap on two streams (arrival-count hand-off)
-OVERLAP = os.environ.get("FMLX_GLM_OVERLAP", "0") == "1"
-ST_ROUND_ALT = 5  # csrc/glm.hip state word of the odd launches' round number
-ARR_IDX, ARR_ERR = 124, 127  # csrc/glm.hip arrival counters / wait-timeout word in RoundScratch.cnt
-
 CSC_MAX_BYTES = int(os.environ.get("FMLX_CSC_MAX_BYTES", str(8 << 30)))
 CSC_RUN_MAX = int(os.environ.get("FMLX_CSC_RUN_MAX", "16"))  # consecutive batches transposed per sort
 # fp32 copies over 11–20 column bits: high-bits pass + bucket-local pass (0: two LSD passes + colptr)

@@ -5,8 +5,7 @@
 Variants: ``u`` (rows in flight per wave = 2u), ``b`` (blocks = partial rows), ``split``
 (legacy 3-launch round: grad partials → stage-1 → reduce+update) vs the fused one-launch round,
 ``defer`` (0: ticketed atomic tail; 1: round e − 1 completed in launch e's prologue), ``dma``
-(LDS-DMA row ring depth in steps, 0 = register loads), ``ov`` (1: consecutive deferred launches
-overlap on two streams, arrival-count hand-off).
+(LDS-DMA row ring depth in steps, 0 = register loads).
 Usage: python scripts/bench_glm_kernel.py --configs "u=2,b=512;u=4,b=256;split=1"
 """
 import argparse
@@ -79,7 +78,6 @@ def main():
             gk.DEFER = bool(c.get("defer", 1))
             gk.set_tail_tuning(c.get("reps", 4), bool(c.get("t2", 0)))
             gk.set_dma(c.get("dma", 0))
-            gk.OVERLAP = bool(c.get("ov", 0))
             sgd = SGD(max_iter=10 ** 8, learning_rate=0.1, global_batch_size=a.batch, tol=0.0)
             cls = SplitTrainer if (c.get("split") or c.get("m0")) else DeviceGlmTrainer
             tr = cls(sgd, np.zeros(a.dim), X, y, None, "logistic", use_graph=True)
