@@ -86,10 +86,14 @@ __device__ __forceinline__ T* at(void* buf, long byte_off) {
 // arrived: the peers' records are then readable. On a timeout the error word is raised and the
 // caller must NOT sum (it poisons its output with NaN instead), so a partial exchange can never
 // pass for a result.
+// Every record word crosses with system-scope stores / loads on the uncached buffers, so the
+// hand-off needs the stores DONE, not a cache write-back: a vmcnt(0) drain before the tag (a
+// system-scope release fence here wrote back the whole L2 once per block — twice per block per
+// two-shot call, ~1,000 write-backs for a 4 MB payload) and a workgroup-scope acquire after it.
 __device__ __forceinline__ bool signal_and_wait(const Ctx& x, long flag_off, int idx, int tag) {
   __shared__ int s_timeout;
   if (threadIdx.x == 0) s_timeout = 0;
-  __threadfence_system();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) st_sys(at<int>(x.peers[x.rank], flag_off) + idx, tag);
   if ((int)threadIdx.x < x.world && (int)threadIdx.x != x.rank) {
@@ -105,7 +109,7 @@ __device__ __forceinline__ bool signal_and_wait(const Ctx& x, long flag_off, int
     }
   }
   __syncthreads();
-  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the record loads below stay below the wait
   return s_timeout == 0;
 }
 
