@@ -31,7 +31,7 @@ import torch
 from ..ops import glm as gk
 from ..parallel import comm
 from ..parallel.checkpoint import AlgorithmCheckpoint, fault_point
-from ..parallel.context import get_context
+from ..parallel.context import device_sharers, get_context
 from ..table import SparseColumn
 from ..utils import graphs, tracing
 
@@ -223,13 +223,21 @@ class DeviceGlmTrainer:
                 self.w = torch.ones(self.n, dtype=acc, device=dev)
         else:
             self.nparts = max(1, min(gk.round_blocks(self.X), gk.max_round_blocks(), math.ceil(max(self.B, 1) / (gk.WPB * 16))))
-            self.scratch = gk.RoundScratch(self.nparts, self.d, acc, dev)
             if self.distributed:
                 from ..parallel import xgmi
 
                 self.xg = xgmi.get()
                 if self.xg is not None and self.d + 2 > self.xg.glm_max:
                     self.xg = None
+                share = device_sharers(ctx)
+                if self.xg is not None and share > 2:
+                    # ranks rehearsing on ONE GPU: the in-kernel exchange waits for the peers'
+                    # kernels, so every rank's grid must be resident at once — measured: 4 ranks
+                    # of 85 blocks time out, 4 × 64 run (2 ranks of 224 run: the second rank's lead
+                    # block always finds a free CU). A GPU per rank never hits this cap.
+                    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+                    self.nparts = max(1, min(self.nparts, cus // share))
+            self.scratch = gk.RoundScratch(self.nparts, self.d, acc, dev)
         if self.sparse or self.wide or self.distributed and self.xg is None:
             self.mode = gk.TAIL_FEEDBACK  # feedback → RCCL all-reduce → update kernel
         else:

@@ -132,6 +132,18 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> SPM
     return _CTX
 
 
+def device_sharers(ctx: SPMDContext) -> int:
+    """Ranks of this node running on this rank's GPU: 1 with a GPU per rank; every local rank in
+    the one-GPU multi-rank rehearsals (``FMLX_DEVICE=cuda:0`` for all ranks)."""
+    if not ctx.is_gpu or ctx.world_size <= 1:
+        return 1
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", ctx.world_size))
+    if os.environ.get("FMLX_DEVICE", "").lower().startswith("cuda:"):
+        return local
+    n = max(1, torch.cuda.device_count())
+    return max(1, -(-local // n))
+
+
 def get_context() -> SPMDContext:
     global _CTX
     if _CTX is None:
