@@ -67,18 +67,63 @@ def _statement_ok(s) -> bool:
     return s is not None and "__THIS__" in s
 
 
+class _FlinkAvg:
+    """AVG with Flink's result type: over integral values the average of an INT / BIGINT column is
+    integral (Flink's IntegralAvgAggFunction: BIGINT sum / BIGINT count, Java division — truncated
+    toward zero); over anything floating it is the floating mean. NULLs are skipped; no rows → NULL."""
+
+    def __init__(self):
+        self.s, self.n, self.ints = 0, 0, True
+
+    def step(self, v):
+        if v is None:
+            return
+        if not isinstance(v, int):
+            self.ints = False
+        self.s += v
+        self.n += 1
+
+    def finalize(self):
+        if self.n == 0:
+            return None
+        if self.ints:
+            q = abs(self.s) // self.n
+            return q if self.s >= 0 else -q
+        return self.s / self.n
+
+
+def _keep_type(fn):
+    """CEIL / FLOOR / SIGN of a DOUBLE stay DOUBLE (Python's return ints); of an integer, integer."""
+    return lambda x: None if x is None else (float(fn(x)) if isinstance(x, float) else int(fn(x)))
+
+
+def _java_mod(a, b):
+    """MOD / % with Java semantics: the dividend's sign; integral for integers (Flink's MOD(INT, INT)
+    is INT)."""
+    if a is None or b is None:
+        return None
+    if isinstance(a, int) and isinstance(b, int):
+        if b == 0:
+            return None
+        r = abs(a) % abs(b)
+        return r if a >= 0 else -r
+    return math.fmod(a, b)
+
+
 def _register_functions(con: sqlite3.Connection) -> None:
     def f1(fn):
         return lambda x: None if x is None else fn(x)
 
     for name, fn in (("SQRT", math.sqrt), ("LN", math.log), ("LOG10", math.log10), ("EXP", math.exp),
-                     ("ABS", abs), ("CEIL", math.ceil), ("FLOOR", math.floor), ("SIN", math.sin), ("COS", math.cos),
-                     ("TAN", math.tan), ("SIGN", lambda x: (x > 0) - (x < 0))):
+                     ("ABS", abs), ("SIN", math.sin), ("COS", math.cos), ("TAN", math.tan)):
         con.create_function(name, 1, f1(fn), deterministic=True)
+    for name, fn in (("CEIL", math.ceil), ("CEILING", math.ceil), ("FLOOR", math.floor),
+                     ("SIGN", lambda x: (x > 0) - (x < 0))):
+        con.create_function(name, 1, _keep_type(fn), deterministic=True)
     con.create_function("POWER", 2, lambda a, b: None if a is None or b is None else math.pow(a, b),
                         deterministic=True)
-    con.create_function("MOD", 2, lambda a, b: None if a is None or b is None else math.fmod(a, b),
-                        deterministic=True)
+    con.create_function("MOD", 2, _java_mod, deterministic=True)
+    con.create_aggregate("AVG", 1, _FlinkAvg)
 
 
 def _sql_value(v):

@@ -17,7 +17,9 @@ reference, and a ``WHERE`` is one mask + one gather per column:
 
 Types follow Flink: integer op integer stays integer ('/' truncates toward zero, '%' keeps the
 dividend's sign), anything with a floating operand is floating, comparisons are BOOLEAN, unnamed
-expressions are called ``EXPR$<i>``. GROUP BY output is ordered by key (ascending). Distributed:
+expressions are called ``EXPR$<i>``, SUM keeps its argument's type and AVG of an integer column is
+an integer (sum / count truncated toward zero, Flink's IntegralAvgAggFunction), CAST to INT /
+BIGINT truncates toward zero, ROUND is half away from zero. GROUP BY output is ordered by key (ascending). Distributed:
 row-wise statements run per rank; aggregates are computed per rank, the small partial tables are
 all-gathered and merged on every rank, and the result is dealt round-robin.
 
@@ -467,10 +469,14 @@ class _Eval:
         if name == "ROUND" and len(args) in (1, 2):
             a = _num(args[0])
             d = int(args[1]) if len(args) == 2 else 0
-            if not isinstance(a, torch.Tensor) or not a.dtype.is_floating_point:
-                raise Unsupported("ROUND of a non-floating value")
+            if _is_int(a) and d >= 0:
+                return a  # ROUND(INT) is the INT itself
+            if not _is_float(a):
+                raise Unsupported("ROUND of a non-numeric value")
             # SQL ROUND is half away from zero (torch.round is half to even)
             s = 10.0 ** d
+            if not isinstance(a, torch.Tensor):
+                return math.copysign(math.floor(abs(a) * s + 0.5) / s, a) if a == a else a
             return torch.sign(a) * torch.floor(torch.abs(a) * s + 0.5) / s
         if name in ("LEAST", "GREATEST") and len(args) >= 2:
             out = self.full(_num(args[0]))
@@ -581,8 +587,8 @@ def _local_states(items, group, t: Table, dev, world):
                 return ("keyref", gi)
         if e[0] == "agg":
             arg = None if e[2] is None else ev.full(ev(e[2]))
-            if e[1] == "AVG" and arg is not None and not arg.dtype.is_floating_point:
-                raise Unsupported("AVG over an integer column")
+            if e[1] in ("SUM", "AVG", "MIN", "MAX") and arg is not None and arg.dtype == torch.bool:
+                raise Unsupported("%s over BOOLEAN" % e[1])
             aggs.append((e[1], arg))
             return ("aggref", len(aggs) - 1)
         if e[0] in ("bin",):
@@ -670,8 +676,14 @@ def _aggregate(items, group, t: Table, dev, world, rank, werr=None) -> Table:
             if name == "COUNT":
                 return st["count"]
             if name == "SUM":
-                return st["sum"].to(st["dtype"]) if st["dtype"] in (torch.float32,) else st["sum"]
+                # Flink: SUM keeps its argument's type (an INT sum wraps like Java's int)
+                return st["sum"].to(st["dtype"]) if st["dtype"] in (torch.float32, torch.int32, torch.int16,
+                                                                      torch.int8) else st["sum"]
             if name == "AVG":
+                if not st["dtype"].is_floating_point:
+                    # Flink's IntegralAvgAggFunction: BIGINT sum / BIGINT count truncated toward
+                    # zero, in the argument's type
+                    return torch.div(st["sum"], st["count"], rounding_mode="trunc").to(st["dtype"])
                 return st["sum"] / st["count"].to(torch.float64)
             if name == "MIN":
                 return st["min"].to(st["dtype"])
