@@ -357,11 +357,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
   constexpr int PW = TILEB / 1024 / NW;   // 1-KiB LDS-DMA pieces per wave per tile (1 or 2)
   static_assert(PW >= 1 && PW * NW * 1024 == TILEB, "tile pieces must split evenly over the waves");
   constexpr int SLOTB = TILEB + NW * 256; // + the tile's 32 centroid norms, one 256-B copy per wave
-  // label transpose: words per row. 36 (not the conflict-free 40: a 2-way conflict on half the
-  // banks of a once-per-wave stage) keeps the block at 36 KB, so four blocks leave 16 KB of a
-  // CU's LDS for a centroid gather-sum block of the previous row part (kmeans.py split round) to
-  // run beside them; with 40 KB blocks it could only start where assign blocks had drained.
-  constexpr int LSTR = 36;
+  // label transpose: words per row (4·LSTR ≡ 32 mod 64 banks). (A 36-word stride — 36 KB blocks,
+  // so a gather-sum block of the previous row part fits beside four assign blocks — measured the
+  // same round time as this 40 KB layout, split or not: profiles/r4/kmeans_assign_lds_split_ab.jsonl.)
+  constexpr int LSTR = 40;
   constexpr int LDSB = 3 * SLOTB > NW * 64 * LSTR * 4 ? 3 * SLOTB : NW * 64 * LSTR * 4;
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   typedef short s16x8_t __attribute__((ext_vector_type(8)));

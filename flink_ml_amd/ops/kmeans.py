@@ -53,7 +53,10 @@ CHUNK = 256
 # runs on a side stream while part p + 1's assign (MFMA-bound) runs on the main stream, and the
 # parts' [sums | counts] are added in part order (deterministic). KMeans.java:291-295 sums each
 # point into its cluster in the assignment loop itself; here the sum trails the assign by a part.
-SPLIT_PARTS = int(os.environ.get("FMLX_KMEANS_SPLIT", "4"))
+# Off by default: interleaved same-box A/Bs at the 12.5M x 128, k = 1024 shard measured the split
+# round 3.98-4.06 vs 3.77-3.86 ms/iter unsplit (the assign fills every CU; the gather-sum beside
+# it slows it more than it hides) — profiles/r4/kmeans_assign_lds_split_ab.jsonl. FMLX_KMEANS_SPLIT=4.
+SPLIT_PARTS = int(os.environ.get("FMLX_KMEANS_SPLIT", "1"))
 SPLIT_MIN_ROWS = int(os.environ.get("FMLX_KMEANS_SPLIT_MIN_ROWS", str(1 << 20)))
 MFMA_KS = (1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16)
 
