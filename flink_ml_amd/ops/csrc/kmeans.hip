@@ -1004,7 +1004,10 @@ int g_km_pipe = 0;
 // wrong labels, a diagnostic — ran 3.13-3.16 vs 3.17-3.19 ms: the barrier costs ~1 %; what is
 // left is the per-wave issue budget, ≈86 VALU + 18 MFMA per 32-centroid tile. An epilogue over
 // tile PAIRS — two bit-inserts + one v_min3_u32 per register, 75 VALU per tile at 244 VGPRs —
-// ran 3.11-3.14 vs 3.17 ms there but 0.126 vs 0.105 ms at 2M x 64, k = 256: not kept.)
+// ran 3.11-3.14 vs 3.17 ms there but 0.126 vs 0.105 ms at 2M x 64, k = 256: not kept. Round 4: a
+// 4-slot ring, DMA three tiles ahead, 3.417-3.427 vs 3.407-3.430 ms — the DMA wait is not what
+// the waves wait on (profiles/r4/kmeans_assign_ring4_ab.log); three blocks per CU (≤ 168 of the
+// D = 128 kernel's ~207 VGPRs) spill 420-444 bytes per lane: neither kept.)
 int g_km_ldspad = 0;
 
 template <int KS>
