@@ -845,6 +845,9 @@ __global__ __launch_bounds__(WPB * 64, (glm_min_waves<T, EPC, CPL, U>())) void g
   } else {
   const long step = (long)U * W;
   long r = start + gw;
+  // (Round 4 also measured issuing a buffer's next loads right after widening its bf16 step to
+  // fp32 pairs, before the step's math: 38.35 vs 38.33 µs — the loop is not limited by where the
+  // loads go out, profiles/r4/lr_early_issue_ab_1gpu.jsonl.)
   // steps of U rows this wave owns; the loop runs them in pairs (xa, xb) with ONE exit test per
   // pair at the latch. (A `break` after each half gives the structurizer a flow block whose
   // conditional back edge carries the first half's pending loads into the header, where the
