@@ -42,7 +42,15 @@ __global__ __launch_bounds__(256) void csc_keys_kernel(const long* __restrict__ 
 }
 
 // fp32 values: the payload is (value bits << 32) | batch-relative row, so the sort moves both and
-// the copy out is sequential (no random gathers; csc_fill's two gathers per entry cost ~4× more)
+// the copy out is sequential (no random gathers; csc_fill's two gathers per entry cost ~4× more).
+// A wave takes KR_ROWS consecutive rows per step: one load brings their KR_ROWS + 1 row starts (a
+// lane each), their entries are one contiguous range whose loads all go out together (a lane finds
+// its entry's row among the KR_ROWS starts), and the slot division is done once per row. (A wave
+// per row — indptr, then entries, then the next row — measured 233 µs over 64M entries: 89 % of
+// wave cycles waiting on memory.)
+constexpr int KR_ROWS = 8;
+constexpr int KR_K = 4;  // 64-entry chunks per lane in flight
+
 __global__ __launch_bounds__(256) void csc_keys64_kernel(const long* __restrict__ indptr, const int* __restrict__ idx,
                                                          const float* __restrict__ values, long r0, long r1, long B,
                                                          int d, long j0, int* __restrict__ key,
@@ -50,15 +58,46 @@ __global__ __launch_bounds__(256) void csc_keys64_kernel(const long* __restrict_
   const int lane = threadIdx.x & 63;
   const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const long nw = ((long)gridDim.x * blockDim.x) >> 6;
-  for (long r = r0 + wave; r < r1; r += nw) {
-    const long s0 = indptr[r], s1 = indptr[r + 1];
-    const long slot = (r - r0) / B;
-    const int kb = (int)(slot * d);
-    const uint32_t rr = (uint32_t)(r - r0 - slot * B);
-    for (long j = s0 + lane; j < s1; j += 64) {
-      const long o = j - j0;
-      if (key != nullptr) key[o] = kb + idx[j];  // (the bucket path sorts the CSR columns in place of keys)
-      payload[o] = ((uint64_t)__float_as_uint(values[j]) << 32) | rr;
+  for (long rg = r0 + wave * KR_ROWS; rg < r1; rg += nw * KR_ROWS) {
+    const int nr = r1 - rg < KR_ROWS ? (int)(r1 - rg) : KR_ROWS;
+    // lane q <= nr: start of row rg + q; lane q < nr: that row's slot key base and batch row
+    const long ip = lane <= nr ? indptr[rg + lane] : 0;
+    int kbl = 0;
+    uint32_t rrl = 0;
+    if (lane < nr) {
+      const long rel = rg + lane - r0;
+      const long slot = rel / B;
+      kbl = (int)(slot * d);
+      rrl = (uint32_t)(rel - slot * B);
+    }
+    long st[KR_ROWS + 1];
+#pragma unroll
+    for (int q = 0; q <= KR_ROWS; ++q) st[q] = __shfl(ip, q < nr ? q : nr, 64);  // uniform
+    const long e0 = st[0], e1 = st[KR_ROWS];
+    for (long jb = e0; jb < e1; jb += 64 * KR_K) {
+      int iv[KR_K];
+      float vv[KR_K];
+#pragma unroll
+      for (int k = 0; k < KR_K; ++k) {
+        const long j = jb + k * 64 + lane;
+        const long jj = j < e1 ? j : e0;
+        iv[k] = __builtin_nontemporal_load(idx + jj);
+        vv[k] = __builtin_nontemporal_load(values + jj);
+      }
+#pragma unroll
+      for (int k = 0; k < KR_K; ++k) {
+        const long j = jb + k * 64 + lane;
+        int q = 0;
+#pragma unroll
+        for (int t = 1; t < KR_ROWS; ++t) q += j >= st[t] ? 1 : 0;  // row of entry j (st ascends)
+        const int kb = __shfl(kbl, q, 64);
+        const uint32_t rr = (uint32_t)__shfl((int)rrl, q, 64);
+        if (j < e1) {
+          const long o = j - j0;
+          if (key != nullptr) key[o] = kb + iv[k];  // (the bucket path sorts the CSR columns instead)
+          payload[o] = ((uint64_t)__float_as_uint(vv[k]) << 32) | rr;
+        }
+      }
     }
   }
 }
@@ -144,7 +183,7 @@ FMLX_API int fmlx_csc_keys64(const long* indptr, const int* idx, const float* va
                              long j0, int* key, uint64_t* payload, void* stream) {
   if (r1 <= r0) return 0;
   if (B <= 0 || d <= 0) return -1;
-  hipLaunchKernelGGL(csc_keys64_kernel, dim3(grid_for(r1 - r0, 4, 1u << 16)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(csc_keys64_kernel, dim3(grid_for(r1 - r0, 4 * KR_ROWS, 1u << 16)), dim3(256), 0, (hipStream_t)stream,
                      indptr, idx, values, r0, r1, B, d, j0, key, payload);
   return (int)hipGetLastError();
 }

@@ -231,9 +231,12 @@ __device__ __forceinline__ void rs_rank_place(const int (&kr)[RS_PER_LANE], cons
     const int dg = valid ? ((key - kb) >> shift) & mask : 0;
     unsigned long long peers = __ballot(valid);
     for (int bit = 0; bit < db; ++bit) {
-      const bool mine = (dg >> bit) & 1;
-      const unsigned long long bb = __ballot(mine);
-      peers &= mine ? bb : ~bb;
+      // M = all ones where my digit has this bit, else 0; the lanes agreeing with me on it are
+      // ballot XNOR M (one bfe, one compare, two xnor, two and per bit)
+      const int M = (int)((unsigned)dg << (31 - bit)) >> 31;
+      const unsigned long long bb = __ballot(M != 0);
+      const unsigned lo = ~((unsigned)bb ^ (unsigned)M), hi = ~((unsigned)(bb >> 32) ^ (unsigned)M);
+      peers &= ((unsigned long long)hi << 32) | lo;
     }
     const int rank = __popcll(peers & lt);
     const bool leader = valid && (peers >> lane) == 1ull;  // the highest lane of my digit's run
