@@ -276,9 +276,11 @@ __global__ __launch_bounds__(ST_THREADS) void st_scatter_kernel(const int* __res
     // my key (one ballot per key bit, no cross-lane data movement), then those below me
     unsigned long long peers = __ballot(valid);
     for (int bit = 0; bit < kb; ++bit) {
-      const bool mine = (key >> bit) & 1;
-      const unsigned long long bb = __ballot(mine);
-      peers &= mine ? bb : ~bb;
+      // M = all ones where my key has this bit: the lanes agreeing with me are ballot XNOR M
+      const int M = (int)((unsigned)key << (31 - bit)) >> 31;
+      const unsigned long long bb = __ballot(M != 0);
+      const unsigned lo = ~((unsigned)bb ^ (unsigned)M), hi = ~((unsigned)(bb >> 32) ^ (unsigned)M);
+      peers &= ((unsigned long long)hi << 32) | lo;
     }
     const int rank = __popcll(peers & lt);
     const bool leader = valid && (peers >> lane) == 1ull;  // the highest lane of my key's run
