@@ -54,7 +54,7 @@ constexpr int KR_K = 4;  // 64-entry chunks per lane in flight
 __global__ __launch_bounds__(256) void csc_keys64_kernel(const long* __restrict__ indptr, const int* __restrict__ idx,
                                                          const float* __restrict__ values, long r0, long r1, long B,
                                                          int d, long j0, int* __restrict__ key,
-                                                         uint64_t* __restrict__ payload) {
+                                                         uint64_t* __restrict__ payload, int pack) {
   const int lane = threadIdx.x & 63;
   const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const long nw = ((long)gridDim.x * blockDim.x) >> 6;
@@ -95,7 +95,9 @@ __global__ __launch_bounds__(256) void csc_keys64_kernel(const long* __restrict_
         if (j < e1) {
           const long o = j - j0;
           if (key != nullptr) key[o] = kb + iv[k];  // (the bucket path sorts the CSR columns instead)
-          payload[o] = ((uint64_t)__float_as_uint(vv[k]) << 32) | rr;
+          // pack: the column's low 10 bits ride at bits 22..31 above the 22-bit batch row
+          const uint32_t lo = pack ? (rr | ((uint32_t)iv[k] & 1023u) << 22) : rr;
+          payload[o] = ((uint64_t)__float_as_uint(vv[k]) << 32) | lo;
         }
       }
     }
@@ -180,11 +182,11 @@ FMLX_API int fmlx_csc_keys(const long* indptr, const int* idx, long r0, long r1,
 }
 
 FMLX_API int fmlx_csc_keys64(const long* indptr, const int* idx, const float* values, long r0, long r1, long B, int d,
-                             long j0, int* key, uint64_t* payload, void* stream) {
+                             long j0, int* key, uint64_t* payload, int pack, void* stream) {
   if (r1 <= r0) return 0;
-  if (B <= 0 || d <= 0) return -1;
+  if (B <= 0 || d <= 0 || (pack && B > (1L << 22))) return -1;
   hipLaunchKernelGGL(csc_keys64_kernel, dim3(grid_for(r1 - r0, 4 * KR_ROWS, 1u << 16)), dim3(256), 0, (hipStream_t)stream,
-                     indptr, idx, values, r0, r1, B, d, j0, key, payload);
+                     indptr, idx, values, r0, r1, B, d, j0, key, payload, pack);
   return (int)hipGetLastError();
 }
 

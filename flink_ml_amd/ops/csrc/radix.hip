@@ -70,7 +70,7 @@ __device__ __forceinline__ void rs_load_seg(const int* __restrict__ kin, const V
 #pragma unroll
   for (int j = 0; j < RS_PER_LANE; ++j) {
     const long i = wa + j * 64 + lane;
-    k[j] = i < wb ? kin[i] : 0;
+    if (kin != nullptr) k[j] = i < wb ? kin[i] : 0;
     if (vin != nullptr) v[j] = i < wb ? vin[i] : V(0);
   }
 }
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const int* __res
     const int key = lk[i];
     const int dg = ((key - kb) >> shift) & mask;
     const int gp = gbase[dg] + (i - loc[dg]);
-    kout[gp] = key;
+    if (kout != nullptr) kout[gp] = key;  // (the packed column-major copy carries no keys out)
     if constexpr (SPLIT) {
       const uint64_t u = (uint64_t)lv[i];
       split_lo[split_off + gp] = (int)(unsigned)u;
@@ -328,6 +328,9 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const int* __res
 // pointer kernel (155–241 µs over the 256 MB of sorted keys).
 constexpr int CB_ND = 1024;  // columns per bucket (low digit)
 
+// PACKED: the payload carries the column's low 10 bits at bits 22..31 above a 22-bit batch row
+// (fmlx_csc_keys64 packing), so this pass reads no keys at all.
+template <bool PACKED>
 __global__ __launch_bounds__(RS_THREADS) void rs_csc_bucket_kernel(const int* __restrict__ kin,
                                                                    const uint64_t* __restrict__ vin,
                                                                    const int* __restrict__ G, SegTable tb, int ndA,
@@ -358,7 +361,10 @@ __global__ __launch_bounds__(RS_THREADS) void rs_csc_bucket_kernel(const int* __
   if (!one) {  // the whole bucket's column histogram first → bucket-local column starts
     for (int i = threadIdx.x; i < RS_WAVES * CB_ND; i += RS_THREADS) hw[i] = 0;
     __syncthreads();
-    for (long i = start + threadIdx.x; i < end; i += RS_THREADS) atomicAdd(&hw[(kin[i] - kb) & (CB_ND - 1)], 1);
+    for (long i = start + threadIdx.x; i < end; i += RS_THREADS) {
+      const int c = PACKED ? (int)(vin[i] >> 22) : kin[i] - kb;
+      atomicAdd(&hw[c & (CB_ND - 1)], 1);
+    }
     __syncthreads();
     rs_tile_cursors(hw, CB_ND, cb, wsum);  // (one row of counts: the others are zero)
     for (int c = threadIdx.x; c < ncol; c += RS_THREADS) cp[c0 + c] = rel + cb[c];
@@ -372,15 +378,20 @@ __global__ __launch_bounds__(RS_THREADS) void rs_csc_bucket_kernel(const int* __
     const long wb = wa + RS_SEG < b ? wa + RS_SEG : b;
     int kr[RS_PER_LANE];
     uint64_t vr[RS_PER_LANE];
-    rs_load_seg<uint64_t>(kin, vin, wa, wb, kr, vr);
-    rs_wave_hist(kr, wa, wb, kb, 0, CB_ND - 1, hw + (long)w * CB_ND);
+    rs_load_seg<uint64_t>(PACKED ? nullptr : kin, vin, wa, wb, kr, vr);
+    if constexpr (PACKED) {
+#pragma unroll
+      for (int j = 0; j < RS_PER_LANE; ++j) kr[j] = (int)(vr[j] >> 22) & (CB_ND - 1);  // (kb = 0 below)
+    }
+    const int kbk = PACKED ? 0 : kb;
+    rs_wave_hist(kr, wa, wb, kbk, 0, CB_ND - 1, hw + (long)w * CB_ND);
     __syncthreads();
     rs_tile_cursors(hw, CB_ND, loc, wsum);
     if (one)
       for (int c = threadIdx.x; c < ncol; c += RS_THREADS) cp[c0 + c] = rel + loc[c];
-    rs_rank_place(kr, vr, wa, wb, kb, 0, CB_ND - 1, hw + (long)w * CB_ND, [&](int pos, int, uint64_t val, int dg) {
+    rs_rank_place(kr, vr, wa, wb, kbk, 0, CB_ND - 1, hw + (long)w * CB_ND, [&](int pos, int, uint64_t val, int dg) {
       const long gp = split_off + start + base[dg] + (pos - loc[dg]);  // = start + pos for one chunk
-      erow[gp] = (int)(unsigned)val;
+      erow[gp] = PACKED ? (int)((unsigned)val & 0x3FFFFFu) : (int)(unsigned)val;
       evals[gp] = (unsigned)(val >> 32);
     });
     if (one) break;
@@ -507,7 +518,8 @@ FMLX_API int fmlx_seg_sort32(int* keys, uint32_t* vals, int* keys_alt, uint32_t*
 // (int32 [*, d + 1]). `bound` / `kbase` are HOST arrays; scratch as fmlx_seg_sort_scratch.
 FMLX_API int fmlx_csc_sort_split(int* keys, uint64_t* vals, int* keys_alt, uint64_t* vals_alt, const long* bound,
                                  const int* kbase, int S, int key_bits, int d, int* scratch, long scratch_ints,
-                                 int* erow, unsigned* evals, long split_off, int* colptr, long b0, void* stream) {
+                                 int* erow, unsigned* evals, long split_off, int* colptr, long b0, int packed,
+                                 void* stream) {
   SegTable tb{};
   int rc = make_table(bound, kbase, S, tb);
   if (rc) return rc;
@@ -526,10 +538,15 @@ FMLX_API int fmlx_csc_sort_split(int* keys, uint64_t* vals, int* keys_alt, uint6
     hipLaunchKernelGGL(rs_colscan_kernel, dim3((ndA + 255) / 256, tb.ngrp), dim3(256), 0, st, T, tb, ndA, G);
     hipLaunchKernelGGL(rs_base_kernel, dim3(tb.S), dim3(1024), 0, st, G, tb, ndA);
     hipLaunchKernelGGL((rs_scatter_kernel<uint64_t, false>), dim3(tb.ntile), dim3(RS_THREADS), lds_sc, st, keys, vals,
-                       keys_alt, vals_alt, T, G, tb, 10, ndA - 1, (int*)nullptr, (unsigned*)nullptr, 0L);
+                       packed ? nullptr : keys_alt, vals_alt, T, G, tb, 10, ndA - 1, (int*)nullptr,
+                       (unsigned*)nullptr, 0L);
   }
   const size_t lds_b = (size_t)(RS_WAVES + 2) * CB_ND * sizeof(int) + RS_WAVES * sizeof(int);
-  hipLaunchKernelGGL(rs_csc_bucket_kernel, dim3((unsigned)(S * ndA)), dim3(RS_THREADS), lds_b, st, keys_alt, vals_alt,
-                     G, tb, ndA, d, b0, colptr, erow, evals, split_off);
+  if (packed)
+    hipLaunchKernelGGL(rs_csc_bucket_kernel<true>, dim3((unsigned)(S * ndA)), dim3(RS_THREADS), lds_b, st, keys_alt,
+                       vals_alt, G, tb, ndA, d, b0, colptr, erow, evals, split_off);
+  else
+    hipLaunchKernelGGL(rs_csc_bucket_kernel<false>, dim3((unsigned)(S * ndA)), dim3(RS_THREADS), lds_b, st, keys_alt,
+                       vals_alt, G, tb, ndA, d, b0, colptr, erow, evals, split_off);
   return (int)hipGetLastError();
 }

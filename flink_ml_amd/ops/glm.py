@@ -431,17 +431,21 @@ class BatchCsc:
             # themselves (segment = batch, so no slot offset): a stable pass on the high column
             # bits, then one block per (batch, 1024-column) bucket writes rows / values in column
             # order and the column pointers — no key array, no sorted keys
+            # a batch of ≤ 2^22 rows: the column's low 10 bits ride in the payload (bits 22..31 above
+            # the row), so the high-bits pass writes no keys and the bucket pass reads none
+            pack = int(self.B <= (1 << 22))
             pay = torch.empty(m, dtype=torch.int64, device=dev)
             native.call("fmlx_csc_keys64", native.ptr(indptr), native.ptr(indices), native.ptr(values), r0, r1, self.B,
-                        d, j0, None, native.ptr(pay), stream)
+                        d, j0, None, native.ptr(pay), pack, stream)
             cols = indices[j0:j1]
-            key_alt, pay_alt = torch.empty_like(cols), torch.empty_like(pay)  # held: no aliasing
+            # held (no aliasing); packed: no key leaves the high-bits pass, so no key buffer
+            key_alt, pay_alt = (cols if pack else torch.empty_like(cols)), torch.empty_like(pay)
             sc = torch.empty(seg_sort_scratch(seg, bits), dtype=torch.int32, device=dev)
             kb = np.zeros(slots, dtype=np.int32)
             rc = native.kernels().fmlx_csc_sort_split(
                 native.ptr(cols), native.ptr(pay), native.ptr(key_alt), native.ptr(pay_alt), starts.ctypes.data,
                 kb.ctypes.data, slots, bits, d, native.ptr(sc), sc.numel(), native.ptr(self.erow),
-                native.ptr(self.evals), j0, native.ptr(self.colptr), b0, stream)
+                native.ptr(self.evals), j0, native.ptr(self.colptr), b0, pack, stream)
             if rc != 0:
                 raise RuntimeError("fmlx_csc_sort_split failed: %d" % rc)
             return
@@ -450,7 +454,7 @@ class BatchCsc:
             # (value bits, row) as one 64-bit payload through the sort, then a sequential split
             pay = torch.empty(m, dtype=torch.int64, device=dev)
             native.call("fmlx_csc_keys64", native.ptr(indptr), native.ptr(indices), native.ptr(values), r0, r1, self.B,
-                        d, j0, native.ptr(key), native.ptr(pay), stream)
+                        d, j0, native.ptr(key), native.ptr(pay), 0, stream)
             # the last pass writes (row, value bits) straight into erow / evals (no unpack pass)
             keys_out, _ = seg_sort(key, pay, seg, kbase, bits, split=(self.erow, self.evals, j0))
         else:

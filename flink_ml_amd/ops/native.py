@@ -85,12 +85,12 @@ _KERNEL_SIGS = {
                         c_long, c_void_p],
     # csc_build.hip
     "fmlx_csc_keys64": [c_void_p, c_void_p, c_void_p, c_long, c_long, c_long, c_int, c_long, c_void_p, c_void_p,
-                        c_void_p],
+                        c_int, c_void_p],
     "fmlx_csc_keys": [c_void_p, c_void_p, c_long, c_long, c_long, c_int, c_long, c_void_p, c_void_p, c_void_p,
                       c_void_p],
     "fmlx_csc_fill": [c_int, c_void_p, c_long, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "fmlx_csc_sort_split": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
-                            c_long, c_void_p, c_void_p, c_long, c_void_p, c_long, c_void_p],
+                            c_long, c_void_p, c_void_p, c_long, c_void_p, c_long, c_int, c_void_p],
     "fmlx_csc_colptr": [c_void_p, c_long, c_int, c_int, c_void_p, c_long, c_void_p, c_void_p],
 }
 

@@ -40,7 +40,7 @@ def main(d=3000, lens=(20_000, 0, 7_001, 30_000), seed=0):
     rc = native.kernels().fmlx_csc_sort_split(native.ptr(k), native.ptr(p), native.ptr(k2), native.ptr(p2),
                                               bound.ctypes.data, kb.ctypes.data, S, bits, d, native.ptr(sc),
                                               sc.numel(), native.ptr(erow), native.ptr(evals), off,
-                                              native.ptr(colptr), b0, native.stream_ptr(dev))
+                                              native.ptr(colptr), b0, 0, native.stream_ptr(dev))
     torch.cuda.synchronize()
     print("rc", rc, "bits", bits)
     # pass 1 reference: per segment stable by high bits (key - kbase) >> 10
