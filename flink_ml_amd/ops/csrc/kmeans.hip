@@ -34,6 +34,12 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 
 constexpr int KM_CH = 256;  // rows per gather chunk
 
+// in-kernel phase stamps of the pipelined assign, for scripts/kmeans_stamp_probe.hip only (the
+// library build defines nothing here: no stamp executes in the shipped kernel)
+#ifndef KM_STAMP
+#define KM_STAMP(i_)
+#endif
+
 // ------------------------------------------------------------------------------------------
 // MFMA assign (euclidean, bf16)
 // ------------------------------------------------------------------------------------------
@@ -372,6 +378,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
   const int h = lane >> 5;
   const long rowbase = (long)blockIdx.x * (NW * 32 * MT) + (long)wave * 32 * MT;
   const int ntiles = kpad / 32;
+  KM_STAMP(4)
 
   // tile T → ring slot B: piece p = wave + 4i covers tile rows [p·1024/ROWB, …); lane l of the
   // piece lands at LDS byte p·1024 + 16·l = (row, slot) and fetches chunk slot ^ (row mod NS);
@@ -488,8 +495,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
   for (int r = 0; r < 16; ++r) acc1[r] = 3.4028235e38f;
   unsigned tprev = 0;
   int s_cur = 0, s_n1 = 1, s_n2 = 2;  // ring slots of tiles t, t+1, t+2
+  KM_STAMP(0)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // rows, tiles 0 and 1
   __syncthreads();
+  KM_STAMP(1)
 
   // B fragments of a ring slot, and B_aug = [c_h, c_m, c_l, 1, 1, 1, 0, 0] from the slot's
   // norms (half 1 multiplies A_aug's zeros)
@@ -591,6 +600,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
 #undef KP_LDB
 #pragma unroll
   for (int r = 0; r < 16; ++r) KP_EPI(acc1, 1, r, tprev)
+  KM_STAMP(2)
 #undef KP_EPI
 #undef KP_DMA
   // every wave's tail re-fetches landed before the ring is reused for the label transpose
@@ -624,6 +634,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
   for (int c = 31; c >= 0; --c) col = key[c] == mn ? c : col;
   const long row = rowbase + lane;
   if (row < n) labels[row] = (int)(mn & tmask) * 32 + col;
+  KM_STAMP(3)
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1007,7 +1018,14 @@ int g_km_pipe = 0;
 // ran 3.11-3.14 vs 3.17 ms there but 0.126 vs 0.105 ms at 2M x 64, k = 256: not kept. Round 4: a
 // 4-slot ring, DMA three tiles ahead, 3.417-3.427 vs 3.407-3.430 ms — the DMA wait is not what
 // the waves wait on (profiles/r4/kmeans_assign_ring4_ab.log); three blocks per CU (≤ 168 of the
-// D = 128 kernel's ~207 VGPRs) spill 420-444 bytes per lane: neither kept.)
+// D = 128 kernel's ~207 VGPRs) spill 420-444 bytes per lane: neither kept. Phase stamps
+// (scripts/kmeans_stamp_probe.hip): a wave spends 14 % of its life waiting for its rows and first
+// tiles, 82 % in the tile loop at ~1,430 cycles per tile (2 waves per SIMD: ~80 % MFMA in the
+// loop), 4 % on labels, at a 1.69-1.75 GHz in-kernel clock. A persistent grid (2 blocks per CU
+// walking the row groups, the next group's rows loaded under the label transpose and its first
+// tiles riding the ring's tail fetches; 256 VGPRs, identical labels) ran 3.12-3.22 vs 3.09-3.10 ms
+// interleaved: the entry wait is already covered by the CU's other wave — not kept;
+// profiles/r4/kmeans_assign_phase_stamps.log, kmeans_assign_persistent_ab.log.)
 int g_km_ldspad = 0;
 
 template <int KS>
