@@ -1025,7 +1025,10 @@ int g_km_pipe = 0;
 // walking the row groups, the next group's rows loaded under the label transpose and its first
 // tiles riding the ring's tail fetches; 256 VGPRs, identical labels) ran 3.12-3.22 vs 3.09-3.10 ms
 // interleaved: the entry wait is already covered by the CU's other wave — not kept;
-// profiles/r4/kmeans_assign_phase_stamps.log, kmeans_assign_persistent_ab.log.)
+// profiles/r4/kmeans_assign_phase_stamps.log, kmeans_assign_persistent_ab.log. The tile norms
+// fetched once per block by wave 0 instead of once per wave (3 of 12 LDS-DMA issues per tile
+// saved): 1,566 vs 1,430 cycles per tile, 3.24-3.26 vs 3.17-3.18 ms — not kept;
+// kmeans_assign_norm_once_ab.log.)
 int g_km_ldspad = 0;
 
 template <int KS>

@@ -80,6 +80,13 @@ int main() {
     CK(hipEventElapsedTime(&ms, a, b));
     std::printf("launch %d: %.3f ms\n", it, ms);
   }
+  {
+    std::vector<int> h(n);
+    CK(hipMemcpy(h.data(), labels, n * 4, hipMemcpyDeviceToHost));
+    unsigned long long cs = 1469598103934665603ull;
+    for (long i = 0; i < n; ++i) cs = (cs ^ (unsigned)h[i]) * 1099511628211ull;
+    std::printf("labels checksum %016llx\n", cs);
+  }
   std::vector<unsigned long long> st(waves * 16);
   CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_km_st), waves * 16 * 8));
   std::vector<double> life, start, loop, tail, clk;
