@@ -349,10 +349,31 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t
 //    ≈100 VALU and 40 LDS ops per wave, no cross-lane round trips.
 // Same keys and tie rule as kmeans_assign_bf16_kernel (lower tile, then lower column = lower
 // centroid index); the distances differ from it only by fp32 summation order.
+// B_aug row of a centroid from its ‖c‖² (fp32 bits): [c_h, c_m, c_l, 1, 1, 1, 0, 0], ‖c‖² split
+// into three truncated bf16s (exact to fp32; +inf padding rows give inf/NaN words, whose keys lose
+// to every finite distance). Built once per assign by kmeans_baug_kernel, not per tile per lane;
+// only the first two words vary, so a centroid's row is 8 bytes (the rest is constant).
+__device__ __forceinline__ uint2 km_baug_words(uint32_t cb) {
+  const float c = __uint_as_float(cb);
+  const float c1 = c - __uint_as_float(cb & 0xffff0000u);
+  const uint32_t c1b = __float_as_uint(c1);
+  const float c2 = c1 - __uint_as_float(c1b & 0xffff0000u);
+  uint2 q;
+  q.x = (cb >> 16) | (c1b & 0xffff0000u);
+  q.y = (__float_as_uint(c2) >> 16) | 0x3F800000u;
+  return q;
+}
+
+__global__ __launch_bounds__(256) void kmeans_baug_kernel(const float* __restrict__ cnorm, int kpad,
+                                                          uint2* __restrict__ baug) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j < kpad) baug[j] = km_baug_words(__float_as_uint(cnorm[j]));
+}
+
 template <int KS, bool PF, int NW = 4>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kernel(const bf16_t* __restrict__ X, long ld,
                                                                          long n, const bf16_t* Cb,
-                                                                         const float* cnorm, int kpad,
+                                                                         const uint2* baug, int kpad,
                                                                          int* __restrict__ labels) {
   static_assert(KS == 4 || KS == 8, "pipelined assign: D = 64 or 128");
   constexpr int MT = 2;
@@ -362,7 +383,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
   constexpr int TILEB = 32 * ROWB;        // bytes per 32-centroid tile
   constexpr int PW = TILEB / 1024 / NW;   // 1-KiB LDS-DMA pieces per wave per tile (1 or 2)
   static_assert(PW >= 1 && PW * NW * 1024 == TILEB, "tile pieces must split evenly over the waves");
-  constexpr int SLOTB = TILEB + NW * 256; // + the tile's 32 centroid norms, one 256-B copy per wave
+  constexpr int SLOTB = TILEB + NW * 256; // + the tile's 32 B_aug rows (8 B each), one copy per wave
   // label transpose: words per row (4·LSTR ≡ 32 mod 64 banks). (A 36-word stride — 36 KB blocks,
   // so a gather-sum block of the previous row part fits beside four assign blocks — measured the
   // same round time as this 40 KB layout, split or not: profiles/r4/kmeans_assign_lds_split_ab.jsonl.)
@@ -393,20 +414,28 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
   const unsigned lds_base = (unsigned)(uintptr_t)(lds_ptr_t)lds;
 #define KP_DMA(T_, B_)                                                                                  \
   {                                                                                                     \
+    const char* tsrc_ = reinterpret_cast<const char*>(Cb) + (long)(T_) * TILEB; /* uniform */          \
     _Pragma("unroll") for (int i_ = 0; i_ < PW; ++i_) {                                                 \
-      const int p_ = wave + NW * i_;                                                                    \
-      const int off_ = p_ * 1024 + lane * 16;                                                           \
-      const int row_ = off_ / ROWB, slot_ = (off_ % ROWB) / 16;                                         \
-      const bf16_t* src_ = Cb + ((long)(T_) * 32 + row_) * DP + (slot_ ^ (row_ & (NS - 1))) * 8;        \
-      const unsigned dst_ = __builtin_amdgcn_readfirstlane(lds_base + (B_) * SLOTB + p_ * 1024);        \
-      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src_), "s"(dst_)         \
+      const unsigned dst_ = __builtin_amdgcn_readfirstlane(lds_base + (B_) * SLOTB + (wave + NW * i_) * 1024); \
+      asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(dma_off[i_]), "s"(tsrc_), "s"(dst_) \
                    : "memory", "m0");                                                                   \
     }                                                                                                   \
-    const float* csrc_ = cnorm + (long)(T_) * 32 + r32;                                                 \
+    const uint2* csrc_ = baug + (long)(T_) * 32; /* uniform */                                           \
     const unsigned cdst_ = __builtin_amdgcn_readfirstlane(lds_base + (B_) * SLOTB + TILEB + wave * 256); \
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(csrc_), "s"(cdst_)          \
+    asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dword %0, %1" ::"v"(dma_noff), "s"(csrc_), "s"(cdst_) \
                  : "memory", "m0");                                                                     \
   }
+
+  // per-lane byte offsets of the pieces inside a tile (and of the norms): the loads take the
+  // tile's address as a scalar base (saddr form), so no per-tile 64-bit address math in VALU
+  unsigned dma_off[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int off = (wave + NW * i) * 1024 + lane * 16;
+    const int row = off / ROWB, slot = (off % ROWB) / 16;
+    dma_off[i] = (unsigned)((row * DP + (slot ^ (row & (NS - 1))) * 8) * 2);
+  }
+  const unsigned dma_noff = (unsigned)lane * 4u;  // the tile's 32 x 8-byte B_aug rows
 
   // the first two tiles go out before the row loads, so their L2 latency overlaps the rows' HBM one
   const int t1 = ntiles > 1 ? 1 : 0;
@@ -500,27 +529,19 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
   __syncthreads();
   KM_STAMP(1)
 
-  // B fragments of a ring slot, and B_aug = [c_h, c_m, c_l, 1, 1, 1, 0, 0] from the slot's
-  // norms (half 1 multiplies A_aug's zeros)
-#define KP_LDB(SLOT_, BF_, CB_)                                                                   \
+  // B fragments of a ring slot, and the tile's B_aug rows (half 1 multiplies A_aug's zeros)
+#define KP_LDB(SLOT_, BF_, BA_)                                                                   \
   {                                                                                               \
     const unsigned char* tb_ = lds + (SLOT_) * SLOTB + r32 * ROWB;                                \
-    CB_ = *reinterpret_cast<const uint32_t*>(lds + (SLOT_) * SLOTB + TILEB + wave * 256 + r32 * 4); \
+    const uint2 w_ = *reinterpret_cast<const uint2*>(lds + (SLOT_) * SLOTB + TILEB + wave * 256 + r32 * 8); \
+    union { uint32_t u[4]; bf16x8_t v; } q_;                                                      \
+    q_.u[0] = w_.x;                                                                               \
+    q_.u[1] = w_.y;                                                                               \
+    q_.u[2] = 0x3F803F80u;                                                                        \
+    q_.u[3] = 0u;                                                                                 \
+    BA_ = q_.v;                                                                                   \
     _Pragma("unroll") for (int s_ = 0; s_ < KS; ++s_)                                             \
         BF_[s_] = *reinterpret_cast<const bf16x8_t*>(tb_ + (((2 * s_ + h) ^ (r32 & (NS - 1))) * 16)); \
-  }
-#define KP_AUG(CB_, BA_)                                                   \
-  {                                                                        \
-    const float c_ = __uint_as_float(CB_);                                 \
-    const float c1_ = c_ - __uint_as_float((CB_) & 0xffff0000u);           \
-    const uint32_t c1b_ = __float_as_uint(c1_);                            \
-    const float c2_ = c1_ - __uint_as_float(c1b_ & 0xffff0000u);           \
-    union { uint32_t u[4]; bf16x8_t v; } q_;                               \
-    q_.u[0] = ((CB_) >> 16) | (c1b_ & 0xffff0000u);                        \
-    q_.u[1] = (__float_as_uint(c2_) >> 16) | 0x3F800000u;                  \
-    q_.u[2] = 0x3F803F80u;                                                 \
-    q_.u[3] = 0u;                                                          \
-    BA_ = q_.v;                                                            \
   }
   // one m-tile chain: KS MFMAs + the norm step, carrying the OTHER accumulator's epilogue
 #define KP_CHAIN(ACC_, M_, BF_, BA_, EACC_, EM_, ETT_)                                               \
@@ -539,14 +560,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
     for (int t = 0; t < ntiles; ++t) {
       const int t2 = t + 2 < ntiles ? t + 2 : ntiles - 1;  // the tail re-fetches the last tile
       KP_DMA(t2, s_n2)
-      bf16x8_t bfr[KS], baug;
-      uint32_t cb;
-      KP_LDB(s_cur, bfr, cb)
-      KP_AUG(cb, baug)
+      bf16x8_t bfr[KS], bag;
+      KP_LDB(s_cur, bfr, bag)
       const unsigned tt = (unsigned)t;
       __builtin_amdgcn_sched_barrier(0);
-      KP_CHAIN(acc0, 0, bfr, baug, acc1, 1, tprev)  // m-tile 0 of tile t | m-tile 1 of tile t − 1
-      KP_CHAIN(acc1, 1, bfr, baug, acc0, 0, tt)     // m-tile 1 of tile t | m-tile 0 of tile t
+      KP_CHAIN(acc0, 0, bfr, bag, acc1, 1, tprev)  // m-tile 0 of tile t | m-tile 1 of tile t − 1
+      KP_CHAIN(acc1, 1, bfr, bag, acc0, 0, tt)     // m-tile 1 of tile t | m-tile 0 of tile t
       __builtin_amdgcn_sched_barrier(0);
       // tile t + 1 (issued a tile ago) complete for this wave, then for every wave
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW + 1) : "memory");
@@ -562,10 +581,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
     // chains of a tile, and the next tile's ds_reads are issued under the second chain, so no
     // chain ever starts on an LDS round trip. Two named register sets, loop unrolled by two.
     bf16x8_t bA[KS], bB[KS], gA, gB;
-    uint32_t cA, cB;
-    KP_LDB(0, bA, cA)
-    KP_AUG(cA, gA)
-#define KP_TILE(BF_, BA_, NBF_, NBA_, NCB_)                                                     \
+    KP_LDB(0, bA, gA)
+#define KP_TILE(BF_, BA_, NBF_, NBA_)                                                     \
     {                                                                                           \
       const int t2_ = t + 2 < ntiles ? t + 2 : ntiles - 1; /* the tail re-fetches the last tile */ \
       KP_DMA(t2_, s_n2)                                                                         \
@@ -576,9 +593,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
       /* tile t + 1 (issued a tile ago) complete for this wave, then for every wave */          \
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW + 1) : "memory");                             \
       __syncthreads();                                                                          \
-      KP_LDB(s_n1, NBF_, NCB_)                                                                  \
+      KP_LDB(s_n1, NBF_, NBA_)                                                                  \
       KP_CHAIN(acc1, 1, BF_, BA_, acc0, 0, tt_)                                                 \
-      KP_AUG(NCB_, NBA_)                                                                        \
       __builtin_amdgcn_sched_barrier(0);                                                        \
       tprev = tt_;                                                                              \
       const int s_old_ = s_cur;                                                                 \
@@ -588,15 +604,14 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
     }
     int t = 0;
     while (true) {
-      KP_TILE(bA, gA, bB, gB, cB)
+      KP_TILE(bA, gA, bB, gB)
       if (++t == ntiles) break;
-      KP_TILE(bB, gB, bA, gA, cA)
+      KP_TILE(bB, gB, bA, gA)
       if (++t == ntiles) break;
     }
 #undef KP_TILE
   }
 #undef KP_CHAIN
-#undef KP_AUG
 #undef KP_LDB
 #pragma unroll
   for (int r = 0; r < 16; ++r) KP_EPI(acc1, 1, r, tprev)
@@ -1028,12 +1043,20 @@ int g_km_pipe = 0;
 // profiles/r4/kmeans_assign_phase_stamps.log, kmeans_assign_persistent_ab.log. The tile norms
 // fetched once per block by wave 0 instead of once per wave (3 of 12 LDS-DMA issues per tile
 // saved): 1,566 vs 1,430 cycles per tile, 3.24-3.26 vs 3.17-3.18 ms — not kept;
-// kmeans_assign_norm_once_ab.log.)
+// kmeans_assign_norm_once_ab.log. The tile loop is ISSUE-bound: per wave and tile ~98 VALU × 4
+// cycles + 18 MFMA issue holds × 8 + 3 LDS-DMA issues, twice per SIMD, ≈ the measured 1,430
+// cycles (the 36 MFMAs alone are 1,152). Kept: the LDS-DMA sources in the saddr form (scalar tile
+// base + loop-invariant lane offsets: no 64-bit address math per tile) and B_aug rows built once
+// per assign (kmeans_baug_kernel) instead of per tile and lane — 78 VALU per tile, 1,316 cycles
+// per tile, 3.08-3.11 vs 3.21 ms at 12.5M x 128 and 23.3-23.4 vs 24.5-24.6 ms at 100M x 128,
+// identical labels (kmeans_assign_saddr_baug_ab.log, kmeans_assign_100M_saddr_baug_ab.log; the
+// saving returns partly as a lower clock, 1.70 vs 1.75 GHz). Unrolling the tile loop by six so the
+// ring slots become immediates spills 150 VGPRs.)
 int g_km_ldspad = 0;
 
 template <int KS>
 int launch_assign_bf16(const void* X, long ld, long n, int D, const void* Cb, const float* cnorm, int kpad, int* labels,
-                       hipStream_t s) {
+                       void* baug, hipStream_t s) {
   constexpr int MT = KS <= 8 ? 2 : 1;
   const long rows_per_block = 4 * 32 * MT;
   const int blocks = (int)((n + rows_per_block - 1) / rows_per_block);
@@ -1046,27 +1069,30 @@ int launch_assign_bf16(const void* X, long ld, long n, int D, const void* Cb, co
       return (int)hipGetLastError();
     }
   }
+  const bool pipe = full && g_km_pipe && baug != nullptr;
+  if constexpr (KS == 4 || KS == 8)
+    if (pipe) hipLaunchKernelGGL(kmeans_baug_kernel, dim3((kpad + 255) / 256), dim3(256), 0, s, cnorm, kpad, (uint2*)baug);
   if constexpr (KS == 8) {
-    if (full && g_km_pipe >= 3) {
+    if (pipe && g_km_pipe >= 3) {
       // A/B: 8 waves per block (one block per CU) share each centroid tile's LDS-DMA
       const int blocks8 = (int)((n + 8 * 32 * MT - 1) / (8 * 32 * MT));
       if (g_km_pipe == 4)
         hipLaunchKernelGGL((kmeans_assign_bf16_pipe_kernel<KS, true, 8>), dim3(blocks8), dim3(512), g_km_ldspad, s,
-                           (const bf16_t*)X, ld, n, (const bf16_t*)Cb, cnorm, kpad, labels);
+                           (const bf16_t*)X, ld, n, (const bf16_t*)Cb, (const uint2*)baug, kpad, labels);
       else
         hipLaunchKernelGGL((kmeans_assign_bf16_pipe_kernel<KS, false, 8>), dim3(blocks8), dim3(512), g_km_ldspad, s,
-                           (const bf16_t*)X, ld, n, (const bf16_t*)Cb, cnorm, kpad, labels);
+                           (const bf16_t*)X, ld, n, (const bf16_t*)Cb, (const uint2*)baug, kpad, labels);
       return (int)hipGetLastError();
     }
   }
   if constexpr (KS == 4 || KS == 8) {
-    if (full && g_km_pipe) {
+    if (pipe) {
       if (g_km_pipe == 2)
         hipLaunchKernelGGL((kmeans_assign_bf16_pipe_kernel<KS, true>), dim3(blocks), dim3(256), g_km_ldspad, s,
-                           (const bf16_t*)X, ld, n, (const bf16_t*)Cb, cnorm, kpad, labels);
+                           (const bf16_t*)X, ld, n, (const bf16_t*)Cb, (const uint2*)baug, kpad, labels);
       else
         hipLaunchKernelGGL((kmeans_assign_bf16_pipe_kernel<KS, false>), dim3(blocks), dim3(256), g_km_ldspad, s,
-                           (const bf16_t*)X, ld, n, (const bf16_t*)Cb, cnorm, kpad, labels);
+                           (const bf16_t*)X, ld, n, (const bf16_t*)Cb, (const uint2*)baug, kpad, labels);
       return (int)hipGetLastError();
     }
   }
@@ -1122,22 +1148,23 @@ FMLX_API int fmlx_kmeans_set_sched(int mode) {
   return 0;
 }
 
+// baug: kpad x 8 bytes of scratch for the pipelined kernel's B_aug rows (nullptr: plain loop)
 FMLX_API int fmlx_kmeans_assign_bf16(const void* X, long ld, long n, int D, int KS, const void* Cb, const float* cnorm,
-                                     int kpad, int* labels, void* stream) {
+                                     int kpad, int* labels, void* baug, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (KS * 16 < D) return -2;
   switch (KS) {
-    case 1: return launch_assign_bf16<1>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
-    case 2: return launch_assign_bf16<2>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
-    case 3: return launch_assign_bf16<3>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
-    case 4: return launch_assign_bf16<4>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
-    case 5: return launch_assign_bf16<5>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
-    case 6: return launch_assign_bf16<6>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
-    case 7: return launch_assign_bf16<7>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
-    case 8: return launch_assign_bf16<8>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
-    case 10: return launch_assign_bf16<10>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
-    case 12: return launch_assign_bf16<12>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
-    case 16: return launch_assign_bf16<16>(X, ld, n, D, Cb, cnorm, kpad, labels, s);
+    case 1: return launch_assign_bf16<1>(X, ld, n, D, Cb, cnorm, kpad, labels, baug, s);
+    case 2: return launch_assign_bf16<2>(X, ld, n, D, Cb, cnorm, kpad, labels, baug, s);
+    case 3: return launch_assign_bf16<3>(X, ld, n, D, Cb, cnorm, kpad, labels, baug, s);
+    case 4: return launch_assign_bf16<4>(X, ld, n, D, Cb, cnorm, kpad, labels, baug, s);
+    case 5: return launch_assign_bf16<5>(X, ld, n, D, Cb, cnorm, kpad, labels, baug, s);
+    case 6: return launch_assign_bf16<6>(X, ld, n, D, Cb, cnorm, kpad, labels, baug, s);
+    case 7: return launch_assign_bf16<7>(X, ld, n, D, Cb, cnorm, kpad, labels, baug, s);
+    case 8: return launch_assign_bf16<8>(X, ld, n, D, Cb, cnorm, kpad, labels, baug, s);
+    case 10: return launch_assign_bf16<10>(X, ld, n, D, Cb, cnorm, kpad, labels, baug, s);
+    case 12: return launch_assign_bf16<12>(X, ld, n, D, Cb, cnorm, kpad, labels, baug, s);
+    case 16: return launch_assign_bf16<16>(X, ld, n, D, Cb, cnorm, kpad, labels, baug, s);
   }
   return -2;  // unsupported D for the MFMA path
 }

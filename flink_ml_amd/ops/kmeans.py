@@ -19,7 +19,7 @@ native.register_kernel_sigs({
     "fmlx_kmeans_set_sched": [c_int],
     "fmlx_kmeans_set_ldspad": [c_int],
     "fmlx_kmeans_assign_bf16": [c_void_p, c_long, c_long, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
-                                c_void_p],
+                                c_void_p, c_void_p],
     "fmlx_kmeans_assign_generic": [c_int, c_void_p, c_long, c_long, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p,
                                    c_void_p],
     "fmlx_kmeans_chunk_sum": [c_int, c_void_p, c_long, c_int, c_void_p, c_void_p, c_void_p, c_int, c_long, c_void_p,
@@ -103,6 +103,9 @@ class CentroidBuffers:
         self.cnorm = torch.zeros(k, dtype=acc_dtype, device=device)          # ‖c‖ (acc dtype)
         self.Cb = torch.zeros((self.kpad, self.DP), dtype=torch.bfloat16, device=device)
         self.cnorm_b = torch.full((self.kpad,), float("inf"), dtype=torch.float32, device=device)  # ‖c_bf16‖²
+        # the pipelined MFMA assign's B_aug rows (‖c‖² split into three bf16s), rebuilt from
+        # cnorm_b by every assign launch
+        self.baug = torch.empty(self.kpad * 2, dtype=torch.int32, device=device)
         self.weights = torch.zeros(k, dtype=torch.float64, device=device)
         self._pack = None
 
@@ -154,7 +157,7 @@ def assign(X: torch.Tensor, cb: CentroidBuffers, metric: str, out: torch.Tensor 
         if _sched_applied is None:
             set_assign_sched(ASSIGN_SCHED)
         native.call("fmlx_kmeans_assign_bf16", native.ptr(X), X.stride(0), n, D, cb.KS, native.ptr(cb.Cb),
-                    native.ptr(cb.cnorm_b), cb.kpad, native.ptr(out), native.stream_ptr(X.device))
+                    native.ptr(cb.cnorm_b), cb.kpad, native.ptr(out), native.ptr(cb.baug), native.stream_ptr(X.device))
         return out
     if X.dtype not in (torch.float32, torch.float64):
         X = X.to(torch.float32)

@@ -9,12 +9,13 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 constexpr long PROBE_MAX_WAVES = 200000;
 __device__ unsigned long long g_km_st[PROBE_MAX_WAVES * 16];
 #define KM_STAMP(i_)                                                                      \
-  if ((threadIdx.x & 63) == 0) {                                                          \
+  if ((threadIdx.x & 63) == 0 && (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6) < PROBE_MAX_WAVES) { \
     const long w_ = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);             \
     g_km_st[w_ * 16 + (i_)] = __builtin_amdgcn_s_memtime();                               \
     g_km_st[w_ * 16 + 8 + (i_)] = __builtin_amdgcn_s_memrealtime();                       \
@@ -50,8 +51,8 @@ static double pct(std::vector<double> v, double q) {
   return v[(size_t)(q * (v.size() - 1))];
 }
 
-int main() {
-  const long n = 12500000, D = 128;
+int main(int argc, char** argv) {
+  const long n = argc > 1 ? atol(argv[1]) : 12500000, D = 128;
   const int k = 1024, kpad = 1024;
   unsigned short *X, *Cb;
   float* cn;
@@ -60,13 +61,16 @@ int main() {
   CK(hipMalloc(&Cb, (long)kpad * D * 2));
   CK(hipMalloc(&cn, kpad * 4));
   CK(hipMalloc(&labels, n * 4));
+  uint2* baug;
+  CK(hipMalloc(&baug, kpad * 8));
   fill_bf16<<<4096, 256>>>(X, n * D, 1234u, 1.0f);
   fill_bf16<<<256, 256>>>(Cb, (long)kpad * D, 99u, -2.0f);  // the tile image is pre-scaled by -2
   fill_f32<<<4, 256>>>(cn, kpad, 40.0f);
+  hipLaunchKernelGGL(kmeans_baug_kernel, dim3((kpad + 255) / 256), dim3(256), 0, 0, cn, kpad, baug);
   CK(hipDeviceSynchronize());
   const int blocks = (int)((n + 255) / 256);
   const long waves = (long)blocks * 4;
-  if (waves > PROBE_MAX_WAVES) return 2;
+  const bool stamps = waves <= PROBE_MAX_WAVES;  // larger runs: timings only
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
@@ -74,7 +78,7 @@ int main() {
   for (int it = 0; it < 6; ++it) {
     CK(hipEventRecord(a));
     hipLaunchKernelGGL((kmeans_assign_bf16_pipe_kernel<8, true>), dim3(blocks), dim3(256), 0, 0,
-                       (const bf16_t*)X, D, n, (const bf16_t*)Cb, cn, kpad, labels);
+                       (const bf16_t*)X, D, n, (const bf16_t*)Cb, baug, kpad, labels);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     CK(hipEventElapsedTime(&ms, a, b));
@@ -87,6 +91,7 @@ int main() {
     for (long i = 0; i < n; ++i) cs = (cs ^ (unsigned)h[i]) * 1099511628211ull;
     std::printf("labels checksum %016llx\n", cs);
   }
+  if (!stamps) return 0;
   std::vector<unsigned long long> st(waves * 16);
   CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_km_st), waves * 16 * 8));
   std::vector<double> life, start, loop, tail, clk;
