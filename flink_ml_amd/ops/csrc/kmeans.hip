@@ -416,12 +416,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
   {                                                                                                     \
     const char* tsrc_ = reinterpret_cast<const char*>(Cb) + (long)(T_) * TILEB; /* uniform */          \
     _Pragma("unroll") for (int i_ = 0; i_ < PW; ++i_) {                                                 \
-      const unsigned dst_ = __builtin_amdgcn_readfirstlane(lds_base + (B_) * SLOTB + (wave + NW * i_) * 1024); \
+      const unsigned dst_ = dma_dst[i_] + (unsigned)((B_) * SLOTB); /* scalar */                        \
       asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(dma_off[i_]), "s"(tsrc_), "s"(dst_) \
                    : "memory", "m0");                                                                   \
     }                                                                                                   \
     const uint2* csrc_ = baug + (long)(T_) * 32; /* uniform */                                           \
-    const unsigned cdst_ = __builtin_amdgcn_readfirstlane(lds_base + (B_) * SLOTB + TILEB + wave * 256); \
+    const unsigned cdst_ = dma_cdst + (unsigned)((B_) * SLOTB); /* scalar */                           \
     asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dword %0, %1" ::"v"(dma_noff), "s"(csrc_), "s"(cdst_) \
                  : "memory", "m0");                                                                     \
   }
@@ -436,6 +436,11 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
     dma_off[i] = (unsigned)((row * DP + (slot ^ (row & (NS - 1))) * 8) * 2);
   }
   const unsigned dma_noff = (unsigned)lane * 4u;  // the tile's 32 x 8-byte B_aug rows
+  // LDS destinations of slot 0 (wave-uniform, made scalar once: per tile only a scalar add)
+  unsigned dma_dst[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) dma_dst[i] = __builtin_amdgcn_readfirstlane(lds_base + (wave + NW * i) * 1024);
+  const unsigned dma_cdst = __builtin_amdgcn_readfirstlane(lds_base + TILEB + wave * 256);
 
   // the first two tiles go out before the row loads, so their L2 latency overlaps the rows' HBM one
   const int t1 = ntiles > 1 ? 1 : 0;
@@ -535,13 +540,20 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
     const unsigned char* tb_ = lds + (SLOT_) * SLOTB + r32 * ROWB;                                \
     const uint2 w_ = *reinterpret_cast<const uint2*>(lds + (SLOT_) * SLOTB + TILEB + wave * 256 + r32 * 8); \
     union { uint32_t u[4]; bf16x8_t v; } q_;                                                      \
+    q_.v = BA_; /* words 2, 3 hold the constant [1, 1, 0, 0] (set once by KP_BA_INIT) */           \
     q_.u[0] = w_.x;                                                                               \
     q_.u[1] = w_.y;                                                                               \
-    q_.u[2] = 0x3F803F80u;                                                                        \
-    q_.u[3] = 0u;                                                                                 \
     BA_ = q_.v;                                                                                   \
     _Pragma("unroll") for (int s_ = 0; s_ < KS; ++s_)                                             \
         BF_[s_] = *reinterpret_cast<const bf16x8_t*>(tb_ + (((2 * s_ + h) ^ (r32 & (NS - 1))) * 16)); \
+  }
+#define KP_BA_INIT(BA_)                             \
+  {                                                 \
+    union { uint32_t u[4]; bf16x8_t v; } q_;        \
+    q_.u[0] = q_.u[1] = 0u;                         \
+    q_.u[2] = 0x3F803F80u;                          \
+    q_.u[3] = 0u;                                   \
+    BA_ = q_.v;                                     \
   }
   // one m-tile chain: KS MFMAs + the norm step, carrying the OTHER accumulator's epilogue
 #define KP_CHAIN(ACC_, M_, BF_, BA_, EACC_, EM_, ETT_)                                               \
@@ -561,6 +573,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
       const int t2 = t + 2 < ntiles ? t + 2 : ntiles - 1;  // the tail re-fetches the last tile
       KP_DMA(t2, s_n2)
       bf16x8_t bfr[KS], bag;
+      KP_BA_INIT(bag)
       KP_LDB(s_cur, bfr, bag)
       const unsigned tt = (unsigned)t;
       __builtin_amdgcn_sched_barrier(0);
@@ -581,6 +594,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
     // chains of a tile, and the next tile's ds_reads are issued under the second chain, so no
     // chain ever starts on an LDS round trip. Two named register sets, loop unrolled by two.
     bf16x8_t bA[KS], bB[KS], gA, gB;
+    KP_BA_INIT(gA)
+    KP_BA_INIT(gB)
     KP_LDB(0, bA, gA)
 #define KP_TILE(BF_, BA_, NBF_, NBA_)                                                     \
     {                                                                                           \
@@ -612,6 +627,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
 #undef KP_TILE
   }
 #undef KP_CHAIN
+#undef KP_BA_INIT
 #undef KP_LDB
 #pragma unroll
   for (int r = 0; r < 16; ++r) KP_EPI(acc1, 1, r, tprev)
@@ -1051,7 +1067,9 @@ int g_km_pipe = 0;
 // per tile, 3.08-3.11 vs 3.21 ms at 12.5M x 128 and 23.3-23.4 vs 24.5-24.6 ms at 100M x 128,
 // identical labels (kmeans_assign_saddr_baug_ab.log, kmeans_assign_100M_saddr_baug_ab.log; the
 // saving returns partly as a lower clock, 1.70 vs 1.75 GHz). Unrolling the tile loop by six so the
-// ring slots become immediates spills 150 VGPRs.)
+// ring slots become immediates spills 150 VGPRs. LDS-DMA destinations made scalar once (no
+// readfirstlane per tile): 1,285 vs 1,314 cycles per tile at the same wall time, 3.02-3.03 ms —
+// the chip is power-bound here, a cycle saving comes back as clock; kmeans_assign_scalar_dst_ab.log.)
 int g_km_ldspad = 0;
 
 template <int KS>
