@@ -383,7 +383,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
   constexpr int TILEB = 32 * ROWB;        // bytes per 32-centroid tile
   constexpr int PW = TILEB / 1024 / NW;   // 1-KiB LDS-DMA pieces per wave per tile (1 or 2)
   static_assert(PW >= 1 && PW * NW * 1024 == TILEB, "tile pieces must split evenly over the waves");
-  constexpr int SLOTB = TILEB + NW * 256; // + the tile's 32 B_aug rows (8 B each), one copy per wave
+  // + the tile's 32 B_aug rows (8 B each), one copy per wave, + the constant B_aug half [1, 1, 0, 0]
+  // that the K-half-1 lanes read (written once at entry; the ring's DMAs never touch it)
+  constexpr int SLOTB = TILEB + NW * 256 + 16;
+  constexpr int BCONST = TILEB + NW * 256;
   // label transpose: words per row (4·LSTR ≡ 32 mod 64 banks). (A 36-word stride — 36 KB blocks,
   // so a gather-sum block of the previous row part fits beside four assign blocks — measured the
   // same round time as this 40 KB layout, split or not: profiles/r4/kmeans_assign_lds_split_ab.jsonl.)
@@ -391,6 +394,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
   constexpr int LDSB = 3 * SLOTB > NW * 64 * LSTR * 4 ? 3 * SLOTB : NW * 64 * LSTR * 4;
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   typedef short s16x8_t __attribute__((ext_vector_type(8)));
+  typedef short s16x4_t __attribute__((ext_vector_type(4)));
   __shared__ __align__(16) unsigned char lds[LDSB];
 
   const int lane = threadIdx.x & 63;
@@ -461,11 +465,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
     }
   }
 
-  // A_aug: lanes of half 0 hold [1, 1, 1, x_h, x_m, x_l, 0, 0] for their row (‖x‖² of the bf16
-  // values, biased by 2^-10·‖x‖² so every distance is strictly positive — the fp32 rounding of
-  // ‖x‖² + ‖c‖² − 2x·c is ~2^-15·(‖x‖²+‖c‖²) and cancels only when x ≈ c; a per-row constant
-  // does not move the argmin); half 1 holds zeros, so B_aug's half 1 never contributes.
-  bf16x8_t aaug[MT];
+  // A_aug, the norm step's A operand (one v_mfma_f32_32x32x8_bf16: K = 8, half the cycles of a
+  // K = 16 step): row [1, 1, 1, x_h, x_m, x_l, 0, 0] — lanes of half 0 hold k 0-3, half 1 k 4-7
+  // (‖x‖² of the bf16 values, biased by 2^-10·‖x‖² so every distance is strictly positive — the
+  // fp32 rounding of ‖x‖² + ‖c‖² − 2x·c is ~2^-15·(‖x‖²+‖c‖²) and cancels only when x ≈ c; a
+  // per-row constant does not move the argmin). B_aug = [c_h, c_m, c_l, 1, 1, 1, 0, 0].
+  s16x4_t aaug[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
     float p = 0.f;
@@ -487,12 +492,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
     const float r1 = p - __uint_as_float(pb & 0xffff0000u);
     const uint32_t r1b = __float_as_uint(r1);
     const float r2 = r1 - __uint_as_float(r1b & 0xffff0000u);
-    union { uint32_t u[4]; bf16x8_t v; } q;
-    q.u[0] = 0x3F803F80u;                                    // 1, 1
-    q.u[1] = 0x3F80u | (pb & 0xffff0000u);                   // 1, x_h
-    q.u[2] = (r1b >> 16) | (__float_as_uint(r2) & 0xffff0000u);  // x_m, x_l
-    q.u[3] = 0u;
-    if (h) q.u[0] = q.u[1] = q.u[2] = 0u;
+    union { uint32_t u[2]; s16x4_t v; } q;
+    q.u[0] = h ? (r1b >> 16) | (__float_as_uint(r2) & 0xffff0000u) : 0x3F803F80u;  // x_m, x_l | 1, 1
+    q.u[1] = h ? 0u : 0x3F80u | (pb & 0xffff0000u);                                 // 0, 0 | 1, x_h
     aaug[m] = q.v;
   }
 #pragma unroll
@@ -529,6 +531,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
   for (int r = 0; r < 16; ++r) acc1[r] = 3.4028235e38f;
   unsigned tprev = 0;
   int s_cur = 0, s_n1 = 1, s_n2 = 2;  // ring slots of tiles t, t+1, t+2
+  if (threadIdx.x < 3) *reinterpret_cast<uint2*>(lds + threadIdx.x * SLOTB + BCONST) = make_uint2(0x3F803F80u, 0u);
+  // B_aug source of this lane in a slot: its centroid's row (half 0) or the constant (half 1)
+  const int ba_off = h ? BCONST : TILEB + wave * 256 + r32 * 8;
   KM_STAMP(0)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // rows, tiles 0 and 1
   __syncthreads();
@@ -538,22 +543,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
 #define KP_LDB(SLOT_, BF_, BA_)                                                                   \
   {                                                                                               \
     const unsigned char* tb_ = lds + (SLOT_) * SLOTB + r32 * ROWB;                                \
-    const uint2 w_ = *reinterpret_cast<const uint2*>(lds + (SLOT_) * SLOTB + TILEB + wave * 256 + r32 * 8); \
-    union { uint32_t u[4]; bf16x8_t v; } q_;                                                      \
-    q_.v = BA_; /* words 2, 3 hold the constant [1, 1, 0, 0] (set once by KP_BA_INIT) */           \
-    q_.u[0] = w_.x;                                                                               \
-    q_.u[1] = w_.y;                                                                               \
-    BA_ = q_.v;                                                                                   \
+    BA_ = *reinterpret_cast<const s16x4_t*>(lds + (SLOT_) * SLOTB + ba_off);                      \
     _Pragma("unroll") for (int s_ = 0; s_ < KS; ++s_)                                             \
         BF_[s_] = *reinterpret_cast<const bf16x8_t*>(tb_ + (((2 * s_ + h) ^ (r32 & (NS - 1))) * 16)); \
-  }
-#define KP_BA_INIT(BA_)                             \
-  {                                                 \
-    union { uint32_t u[4]; bf16x8_t v; } q_;        \
-    q_.u[0] = q_.u[1] = 0u;                         \
-    q_.u[2] = 0x3F803F80u;                          \
-    q_.u[3] = 0u;                                   \
-    BA_ = q_.v;                                     \
   }
   // one m-tile chain: KS MFMAs + the norm step, carrying the OTHER accumulator's epilogue
 #define KP_CHAIN(ACC_, M_, BF_, BA_, EACC_, EM_, ETT_)                                               \
@@ -561,7 +553,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
     if (s_ < KS)                                                                                     \
       ACC_ = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[M_][s_], BF_[s_], s_ == 0 ? zero16 : ACC_, 0, 0, 0); \
     else                                                                                             \
-      ACC_ = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aaug[M_], BA_, ACC_, 0, 0, 0);                  \
+      ACC_ = __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(aaug[M_], BA_, ACC_, 0, 0, 0);                 \
     _Pragma("unroll") for (int e_ = 0; e_ < EPG; ++e_) if (s_ * EPG + e_ < 16)                      \
         KP_EPI(EACC_, EM_, s_ * EPG + e_, ETT_)                                                      \
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                               \
@@ -572,8 +564,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
     for (int t = 0; t < ntiles; ++t) {
       const int t2 = t + 2 < ntiles ? t + 2 : ntiles - 1;  // the tail re-fetches the last tile
       KP_DMA(t2, s_n2)
-      bf16x8_t bfr[KS], bag;
-      KP_BA_INIT(bag)
+      bf16x8_t bfr[KS];
+      s16x4_t bag;
       KP_LDB(s_cur, bfr, bag)
       const unsigned tt = (unsigned)t;
       __builtin_amdgcn_sched_barrier(0);
@@ -593,9 +585,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
     // B fragments one tile ahead in registers: the ring wait + barrier sit between the two
     // chains of a tile, and the next tile's ds_reads are issued under the second chain, so no
     // chain ever starts on an LDS round trip. Two named register sets, loop unrolled by two.
-    bf16x8_t bA[KS], bB[KS], gA, gB;
-    KP_BA_INIT(gA)
-    KP_BA_INIT(gB)
+    bf16x8_t bA[KS], bB[KS];
+    s16x4_t gA, gB;
     KP_LDB(0, bA, gA)
 #define KP_TILE(BF_, BA_, NBF_, NBA_)                                                     \
     {                                                                                           \
@@ -627,7 +618,6 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
 #undef KP_TILE
   }
 #undef KP_CHAIN
-#undef KP_BA_INIT
 #undef KP_LDB
 #pragma unroll
   for (int r = 0; r < 16; ++r) KP_EPI(acc1, 1, r, tprev)
@@ -1069,7 +1059,10 @@ int g_km_pipe = 0;
 // saving returns partly as a lower clock, 1.70 vs 1.75 GHz). Unrolling the tile loop by six so the
 // ring slots become immediates spills 150 VGPRs. LDS-DMA destinations made scalar once (no
 // readfirstlane per tile): 1,285 vs 1,314 cycles per tile at the same wall time, 3.02-3.03 ms —
-// the chip is power-bound here, a cycle saving comes back as clock; kmeans_assign_scalar_dst_ab.log.)
+// the chip is power-bound here, a cycle saving comes back as clock; kmeans_assign_scalar_dst_ab.log.
+// The norm step on v_mfma_f32_32x32x8_bf16 (K = 8: 5.6 % fewer MFMA cycles per tile, 74 VALU,
+// 193 VGPRs): identical labels, 1,285 cycles per tile and the same wall time —
+// kmeans_assign_k8_norm_ab.log; kept for the lighter kernel.)
 int g_km_ldspad = 0;
 
 template <int KS>
