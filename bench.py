@@ -71,6 +71,9 @@ def main():
     ap.add_argument("--graph-rounds", type=int, default=0,
                     help="SGD rounds captured per hipGraph replay (0: the timed steps, at most 200, in one replay "
                          "— every graph is captured and primed before the clock starts)")
+    ap.add_argument("--capture-after-data", action="store_true",
+                    help="A/B: build the trainer and capture its graphs after generating the data (the GPU then "
+                         "idles through the host-side capture right before the timed region)")
     ap.add_argument("--torch-profile", default="", help="after the timed region, record a torch.profiler trace of "
                                                         "extra rounds into this directory (not timed)")
     args = ap.parse_args()
@@ -89,16 +92,20 @@ def main():
 
     dt = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp64": torch.float64}[args.dtype]
     n_local = args.rows // world + (1 if args.rows % world > rank else 0)
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(1234 + rank)
-    # synthetic LabeledPointWithWeight data, generated directly in HBM in the compute dtype
     X = torch.empty((n_local, args.dim), dtype=dt, device=dev)
-    chunk = 1 << 20
-    for s in range(0, n_local, chunk):
-        e = min(s + chunk, n_local)
-        X[s:e] = torch.rand((e - s, args.dim), generator=gen, device=dev, dtype=torch.float32).to(dt)
-    y = torch.randint(0, 2, (n_local,), generator=gen, device=dev).to(torch.float32)
-    torch.cuda.synchronize()
+    # labels in the trainer's accumulation dtype, so the trainer aliases this tensor (no copy)
+    y = torch.empty(n_local, dtype=torch.float64 if dt == torch.float64 else torch.float32, device=dev)
+
+    def generate():
+        # synthetic LabeledPointWithWeight data, generated directly in HBM in the compute dtype
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(1234 + rank)
+        chunk = 1 << 20
+        for s in range(0, n_local, chunk):
+            e = min(s + chunk, n_local)
+            X[s:e] = torch.rand((e - s, args.dim), generator=gen, device=dev, dtype=torch.float32).to(dt)
+        y.copy_(torch.randint(0, 2, (n_local,), generator=gen, device=dev))
+        torch.cuda.synchronize()
 
     import numpy as np
 
@@ -115,7 +122,17 @@ def main():
 
     if (world > 1 or ctx.forced) and not ctx.is_distributed:
         raise SystemExit("WORLD_SIZE=%d but the process group did not come up" % world)
+    if args.capture_after_data:
+        generate()
     trainer = make_trainer()
+    if not args.capture_after_data:
+        # set-up order: the trainer and its hipGraphs (host-side capture, milliseconds with the
+        # GPU idle; kernels hold pointers, nothing reads the data) first, then the data generation,
+        # so the GPU comes to the priming replay, the warm-up and the timed steps from sustained
+        # load at its working clock rather than from the idle gap of the capture. The timed work is
+        # the same either way (profiles/r4/lr_bench_setup_order_ab.log).
+        trainer.precapture(args.steps)
+        generate()
     if world > 1 and ctx.backend == "nccl" and trainer.xg is None and os.environ.get("FMLX_XGMI", "1") != "0":
         msg = "xGMI one-shot exchange did not come up (allocation, IPC mapping or self-test); rounds use RCCL"
         if os.environ.get("FMLX_REQUIRE_XGMI", "0") == "1":
