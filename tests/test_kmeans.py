@@ -242,11 +242,11 @@ def test_gpu_assign_fp32_euclidean_both_paths(n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("sched", [0, 3, 4])
+@pytest.mark.parametrize("sched", [0, 3, 4, 5, 6])
 def test_gpu_assign_bf16_variants_agree(sched):
-    """Every MFMA assign variant (plain loop, pipelined, pipelined + B prefetch) on D = 64 / 128
-    with a centroid count that is not a multiple of the 32-wide tile: labels equal the plain
-    kernel's except at fp32 near-ties."""
+    """Every MFMA assign variant (plain loop, pipelined, pipelined + B prefetch, and both with
+    8-wave blocks at D = 128) on D = 64 / 128 with a centroid count that is not a multiple of the
+    32-wide tile: labels equal the plain kernel's except at fp32 near-ties."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from flink_ml_amd.ops import kmeans as kk
