@@ -11,11 +11,18 @@ over the rank's 100k-row minibatch (HIP kernel), deterministic reduction, RCCL a
 the (d+2) feedback when N > 1, device-side termination check, model update + regularisation.
 Nothing is skipped inside the timed region.
 
-Scaling is *weak*: every GPU keeps a 100k-row local batch (global batch = 100k·N) over its
-1/N shard of the 10M-row dataset. ``value`` = total samples/s over all GPUs.
+Scaling (``--scaling``): *weak* (default, the driver contract) — every GPU keeps a 100k-row local
+batch (global batch = 100k·N) over its 1/N shard of the 10M-row dataset; *strong* — the
+reference's own semantics, a fixed global batch of 100k rows split over the N ranks with the
+remainder to the low ranks (``SGD.java:206-213``, ``logisticregression-benchmark.json``).
+``value`` = total samples/s over all GPUs.
 
-Launch: ``python bench.py`` (1 GPU) or
-``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N``.
+Launch: ``python bench.py --gpus N``. Without a ``WORLD_SIZE`` in the environment and N > 1 this
+process is only a launcher (it never touches the GPU): it hosts the rendezvous TCPStore and
+starts N fresh rank processes of this same script — one per GPU, like the reference's
+``benchmark-run.sh`` → ``flink run`` at the cluster's parallelism — and exits with their status.
+Under ``python -m torch.distributed.run --nproc-per-node N … bench.py --gpus N`` the ranks come
+from the environment, and a ``WORLD_SIZE`` that differs from ``--gpus`` is an error.
 """
 from __future__ import annotations
 
@@ -58,6 +65,73 @@ def timed_region(tr, ctx, warmup: int, steps: int):
     return elapsed, ev0.elapsed_time(ev1) * 1e-3
 
 
+def launch_ranks(n: int, argv, env=None, timeout: float = None) -> int:
+    """Starts ``n`` rank processes of this script (``argv``: its arguments) on this node and
+    returns the first non-zero exit status (0 if every rank succeeded).
+
+    The parent hosts the rendezvous TCPStore on a port the kernel assigns at bind time and keeps
+    it bound until the ranks are done; the ranks connect as clients (``FMLX_STORE``), so no
+    bind-then-close port race. Rank r gets RANK = LOCAL_RANK = r (GPU r), WORLD_SIZE =
+    LOCAL_WORLD_SIZE = n. Nothing here initialises the GPU, and the ranks are children, never an
+    exec of this process. When a rank fails the others are given 30 s, then killed, so a peer
+    stuck in a collective cannot hold the job.
+    """
+    import datetime
+    import subprocess
+
+    import torch.distributed as dist
+
+    store = dist.TCPStore("127.0.0.1", 0, n, is_master=True, wait_for_workers=False,
+                          timeout=datetime.timedelta(seconds=900))
+    base = dict(os.environ if env is None else env)
+    base.pop("FMLX_FORCE_PG", None)
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(store.port),
+                 FMLX_STORE="127.0.0.1:%d" % store.port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=e))
+    rc, t_end = 0, None if timeout is None else time.monotonic() + timeout
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c
+                    grace = time.monotonic() + 30
+                    t_end = grace if t_end is None else min(t_end, grace)
+            if live and t_end is not None and time.monotonic() > t_end:
+                for p in live:
+                    p.kill()
+                rc = rc or 124
+                break
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait()
+        del store
+    return 1 if rc < 0 else rc
+
+
+def check_world(gpus: int, env=None) -> str:
+    """'launch' (spawn ``gpus`` ranks), 'run' (this process is a rank), or raises SystemExit
+    when the environment's WORLD_SIZE contradicts ``--gpus``."""
+    env = os.environ if env is None else env
+    if "WORLD_SIZE" not in env:
+        return "launch" if gpus > 1 else "run"
+    world = int(env["WORLD_SIZE"])
+    if world != gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d (the launcher started a different number of ranks)"
+                         % (gpus, world))
+    return "run"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -65,9 +139,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--rows", type=int, default=10_000_000, help="total dataset rows (sharded over GPUs)")
     ap.add_argument("--dim", type=int, default=1000)
-    ap.add_argument("--batch", type=int, default=100_000, help="per-GPU minibatch rows")
+    ap.add_argument("--batch", type=int, default=100_000,
+                    help="minibatch rows: per GPU (--scaling weak) or global, split over the ranks (strong)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp64"])
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check: every rank joins the process group, prints its rank/world/backend as "
+                         "one JSON line and exits (runs on CPU)")
     ap.add_argument("--graph-rounds", type=int, default=0,
                     help="SGD rounds captured per hipGraph replay (0: the timed steps, at most 200, in one replay "
                          "— every graph is captured and primed before the clock starts)")
@@ -77,12 +156,28 @@ def main():
     ap.add_argument("--torch-profile", default="", help="after the timed region, record a torch.profiler trace of "
                                                         "extra rounds into this directory (not timed)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if check_world(args.gpus) == "launch":
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     from flink_ml_amd.parallel.context import init_distributed
     from flink_ml_amd.parallel import comm
 
     ctx = init_distributed()
     world, rank = ctx.world_size, ctx.rank
+    if ctx.is_distributed:
+        import torch.distributed as dist
+
+        if dist.get_world_size() != args.gpus and not ctx.forced:
+            raise SystemExit("process group has %d ranks, --gpus %d" % (dist.get_world_size(), args.gpus))
+    if args.dry_run:
+        from flink_ml_amd.parallel import comm as _comm
+
+        total = _comm.all_reduce_scalar(float(rank + 1), "sum") if ctx.is_distributed else 1.0
+        print(json.dumps({"rank": rank, "world": world, "backend": ctx.backend if ctx.is_distributed else None,
+                          "device": str(ctx.device), "rank_sum": total}), flush=True)
+        return
     if ctx.device.type != "cuda":
         raise SystemExit("bench.py needs a GPU (torch.cuda.is_available() is False)")
     dev = ctx.device
@@ -109,10 +204,12 @@ def main():
 
     import numpy as np
 
+    global_batch = args.batch * world if args.scaling == "weak" else args.batch
+
     # rounds the run executes: warm-up, one priming replay of every graph the timed region
     # replays (hipGraph upload / first-launch costs), the timed steps, plus one
     def make_trainer():
-        sgd = SGD(max_iter=1, learning_rate=0.1, global_batch_size=args.batch * world, tol=1e-6)
+        sgd = SGD(max_iter=1, learning_rate=0.1, global_batch_size=global_batch, tol=1e-6)
         tr = DeviceGlmTrainer(sgd, np.zeros(args.dim), X, y, None, "logistic", use_graph=not args.no_graph)
         tr.rounds_per_graph = args.graph_rounds if args.graph_rounds > 0 else max(1, min(args.steps, 200))
         sgd.max_iter = args.warmup + tr.priming_rounds(args.steps) + args.steps + 1  # read at capture
@@ -143,11 +240,14 @@ def main():
     # a bounded xGMI wait that gave up (a peer never arrived) means partial feedback: never
     # report it — re-time the same rounds on the RCCL path instead (decided on every rank)
     ok = trainer.xg is None or trainer.xg.healthy()
-    if comm.all_reduce_scalar(1.0 if ok else 0.0, "min") < 1.0:
+    if not comm.all_agree(ok):
         if rank == 0:
             print("xGMI exchange timed out; re-timing on the RCCL path", file=sys.stderr)
+        from flink_ml_amd.parallel import xgmi
+
+        xgmi.disable()  # every later device all-reduce (and check) goes to the process group
         trainer = make_trainer()
-        trainer.xg, trainer.mode = None, gk.TAIL_FEEDBACK
+        trainer.use_rccl()
         elapsed, kernel_s = timed_region(trainer, ctx, args.warmup, args.steps)
     elapsed = comm.all_reduce_scalar(elapsed, "max")
     kernel_s = comm.all_reduce_scalar(kernel_s, "max")
@@ -157,9 +257,13 @@ def main():
         raise SystemExit("SGD terminated early (%d rounds): timing would skip work" % executed)
 
     ms = elapsed / args.steps * 1e3
-    samples = args.batch * world * args.steps
+    samples = global_batch * args.steps
     value = samples / elapsed
+    collective = "none" if not ctx.is_distributed else ("xgmi" if trainer.xg is not None else ctx.backend)
     if rank == 0:
+        print("bench: world_size=%d backend=%s collective=%s gpus_per_device=%d scaling=%s"
+              % (world, ctx.backend if ctx.is_distributed else "none", collective, ctx.sharers, args.scaling),
+              file=sys.stderr, flush=True)
         rec = {
             "metric": "samples/sec (whole node), LogisticRegression 10M\u00d71K dense at 1/2/4/8 MI355X",
             "value": round(value, 1),
@@ -170,27 +274,29 @@ def main():
             "ms_per_step": round(ms, 4),
             "kernel_us_per_step": round(kernel_s / args.steps * 1e6, 2),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic (device-generated U[0,1) features, Bernoulli labels; LabeledPointWithWeightGenerator shape)",
             "config": {
                 "model": "LogisticRegression (SGD, binary logistic loss)",
-                "global_batch": args.batch * world,
+                "global_batch": global_batch,
                 "seq_len": None,
                 "parallelism": "dp%d" % world,
                 "rows": args.rows,
                 "dim": args.dim,
-                "per_gpu_batch": args.batch,
+                "per_gpu_batch": trainer.B if args.scaling == "weak" else global_batch / world,
+                "world_size_observed": world,
+                "backend": ctx.backend if ctx.is_distributed else None,
                 "hipgraph": trainer.use_graph,
-                "collective": "none" if not ctx.is_distributed else ("xgmi" if trainer.xg is not None else ctx.backend),
+                "collective": collective,
                 "collective_path": {1: "rccl all-reduce of the (d+2) feedback" if ctx.backend == "nccl" else
                                     "%s all-reduce of the (d+2) feedback" % ctx.backend,
                                     2: "none (1 GPU: the update is fused into the round kernel)",
                                     3: "in-kernel xgmi exchange"}[trainer.mode],
                 "round": {1: "fused kernel + rccl all-reduce + update", 2: "one fused kernel",
                           3: "one fused kernel with in-kernel xgmi exchange"}[trainer.mode],
-                "hbm_gb_per_s": round(args.batch * args.dim * X.element_size() / (ms * 1e-3) / 1e9, 1),
+                "hbm_gb_per_s": round(trainer.B * args.dim * X.element_size() / (ms * 1e-3) / 1e9, 1),
             },
         }
         print(json.dumps(rec), flush=True)

@@ -230,11 +230,14 @@ class DeviceGlmTrainer:
                 if self.xg is not None and self.d + 2 > self.xg.glm_max:
                     self.xg = None
                 share = device_sharers(ctx)
-                if self.xg is not None and share > 2:
-                    # ranks rehearsing on ONE GPU: the in-kernel exchange waits for the peers'
-                    # kernels, so every rank's grid must be resident at once — measured: 4 ranks
-                    # of 85 blocks time out, 4 × 64 run (2 ranks of 224 run: the second rank's lead
-                    # block always finds a free CU). A GPU per rank never hits this cap.
+                if self.xg is not None and share >= 2:
+                    # ranks rehearsing on ONE GPU: the in-kernel exchange (and, deferred, every
+                    # block spinning on its lead) waits for the peers' kernels, so every rank's
+                    # grid must be resident at once. The round kernel's LDS pad lets at most
+                    # ceil(blocks / CUs) of its blocks share a CU, so `share` grids of at most
+                    # CUs / share blocks always fit (4 ranks of 85 blocks timed out; 2 ranks of
+                    # the 512-block grid fill every slot before the second lead starts — ADVICE
+                    # r4). A GPU per rank (measured by PCI id) never hits this cap.
                     cus = torch.cuda.get_device_properties(dev).multi_processor_count
                     self.nparts = max(1, min(self.nparts, cus // share))
             self.scratch = gk.RoundScratch(self.nparts, self.d, acc, dev)
@@ -265,6 +268,21 @@ class DeviceGlmTrainer:
         self.check_every = max(1, int(check_every))
         self.rounds_per_graph = self.check_every
         self._launched = 0  # rounds launched so far (round e visits batch e mod P)
+
+    def use_rccl(self) -> None:
+        """Switches the dense rounds from the in-kernel xGMI exchange to feedback → RCCL
+        all-reduce → update kernel (e.g. after a bounded xGMI wait gave up). The deferred
+        completion only exists on the fused tails, so it is recomputed with the mode, together
+        with everything captured for the old mode."""
+        if self.defer and self._launched:
+            raise RuntimeError("use_rccl() after deferred rounds ran: their last update is pending")
+        self.xg = None
+        if not self.sparse and not self.wide and self.distributed:
+            self.mode = gk.TAIL_FEEDBACK
+        self.defer, self.cw, self.parity = False, None, 0
+        if self.ctx.backend != "nccl":
+            self.use_graph = False  # a gloo all-reduce of device tensors cannot be captured
+        self.graphs.clear()
 
     def _csc_pays(self, sgd: SGD) -> bool:
         """Whether the per-batch column-major copy pays for itself in this fit (a fit that visits

@@ -18,6 +18,8 @@
 // Two slots make reuse safe: a block that writes slot s in call k+2 has seen every peer publish
 // call k+1, which that peer issued only after its call k (stream order) finished reading slot s.
 #pragma once
+#include <cstdlib>
+
 #include "common.h"
 
 namespace xgmi {
@@ -50,6 +52,19 @@ constexpr int GEN_GLM = MAX_BLOCKS;   // index of the fused-GLM counter in gen[]
 constexpr int GEN_TS = MAX_BLOCKS + 1;  // first two-shot block counter in gen[]
 constexpr int GEN_SIZE = GEN_TS + TS_MAX_BLOCKS;
 
+// FMLX_XGMI_STRICT_FENCE=1 (read once per process, host side): signal_and_wait brackets the tag
+// with system-scope release/acquire fences (an L2 write-back per exchanging block) instead of
+// the vmcnt drain + workgroup acquire that suffice while every record word moves with
+// system-scope stores/loads on the uncached buffers. The switch for a first run on a topology
+// where the relaxed hand-off has not been validated (GPU tests run in both modes).
+inline int strict_fence() {
+  static const int v = [] {
+    const char* e = getenv("FMLX_XGMI_STRICT_FENCE");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  return v;
+}
+
 // Kernel-argument bundle. `peers` is a DEVICE array of `world` buffer pointers (mine at `rank`).
 struct Ctx {
   void* const* peers;
@@ -58,6 +73,7 @@ struct Ctx {
   int* err;         // int32[1] in host-mapped coherent memory: set to 1 when a peer never
                     // arrived (the host reads it without a device sync, parallel/xgmi.py)
   long spin_limit;  // polls before giving up
+  int strict = strict_fence();  // FMLX_XGMI_STRICT_FENCE=1: system-scope release/acquire fences
 };
 
 __device__ __forceinline__ int ld_sys(const int* p) {
@@ -93,7 +109,10 @@ __device__ __forceinline__ T* at(void* buf, long byte_off) {
 __device__ __forceinline__ bool signal_and_wait(const Ctx& x, long flag_off, int idx, int tag) {
   __shared__ int s_timeout;
   if (threadIdx.x == 0) s_timeout = 0;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (x.strict)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: stores done + L2 written back
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) st_sys(at<int>(x.peers[x.rank], flag_off) + idx, tag);
   if ((int)threadIdx.x < x.world && (int)threadIdx.x != x.rank) {
@@ -109,7 +128,10 @@ __device__ __forceinline__ bool signal_and_wait(const Ctx& x, long flag_off, int
     }
   }
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the record loads below stay below the wait
+  if (x.strict)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: stale cached lines invalidated
+  else
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the record loads below stay below the wait
   return s_timeout == 0;
 }
 

@@ -33,6 +33,68 @@ import torch
 
 from .context import get_context
 
+_PKG = __name__.split(".")[0] + "."
+
+
+def _encode(v):
+    """Checkpoint payload → tensors, python scalars/strings and containers only, so restore can
+    use the weights-only unpickler. numpy arrays/scalars become tagged tensors; objects of this
+    package's own classes (DenseVector, …) become tagged attribute dicts."""
+    import numpy as np
+
+    if isinstance(v, torch.Tensor):
+        return v.detach().cpu()
+    if isinstance(v, np.generic):  # before the python types: np.float64 is a float subclass
+        return v.item()
+    if v is None or isinstance(v, (bool, int, float, str, bytes)):
+        return v
+    if isinstance(v, np.ndarray):
+        return {"__np__": torch.from_numpy(np.ascontiguousarray(v)) if v.dtype != object else _encode(v.tolist())}
+    if isinstance(v, dict):
+        return {"__dict__": [[_encode(k), _encode(x)] for k, x in v.items()]}
+    if isinstance(v, tuple):
+        return {"__tuple__": [_encode(x) for x in v]}
+    if isinstance(v, list):
+        return [_encode(x) for x in v]
+    cls = type(v)
+    if cls.__module__.startswith(_PKG):
+        attrs = dict(vars(v)) if hasattr(v, "__dict__") else {}
+        for klass in cls.__mro__:
+            for a in getattr(klass, "__slots__", ()):
+                if a != "__dict__" and hasattr(v, a):
+                    attrs[a] = getattr(v, a)
+        return {"__obj__": "%s:%s" % (cls.__module__, cls.__qualname__), "attrs": _encode(attrs)}
+    raise TypeError("checkpoint state of type %s.%s cannot be saved (tensors, numpy arrays, python scalars, "
+                    "containers and %s* objects only)" % (cls.__module__, cls.__qualname__, _PKG))
+
+
+def _decode(v):
+    import importlib
+
+    if isinstance(v, list):
+        return [_decode(x) for x in v]
+    if not isinstance(v, dict):
+        return v
+    if "__np__" in v:
+        x = v["__np__"]
+        return x.numpy() if isinstance(x, torch.Tensor) else __import__("numpy").array(_decode(x), dtype=object)
+    if "__tuple__" in v:
+        return tuple(_decode(x) for x in v["__tuple__"])
+    if "__dict__" in v:
+        return {_decode(k): _decode(x) for k, x in v["__dict__"]}
+    if "__obj__" in v:
+        mod, name = v["__obj__"].split(":")
+        if not mod.startswith(_PKG):  # only this package's classes are ever rebuilt
+            raise ValueError("checkpoint names a foreign class %s" % v["__obj__"])
+        cls = importlib.import_module(mod)
+        for part in name.split("."):
+            cls = getattr(cls, part)
+        obj = object.__new__(cls)
+        for a, x in _decode(v["attrs"]).items():
+            object.__setattr__(obj, a, x)
+        return obj
+    return {k: _decode(x) for k, x in v.items()}
+
 
 class InjectedFailure(RuntimeError):
     """Raised by ``FailAfter`` (the analogue of the reference's FailingMap exception)."""
@@ -100,7 +162,7 @@ class CheckpointManager:
         d = self._round_dir(name, epoch)
         os.makedirs(d, exist_ok=True)
         payload = {"epoch": epoch, "world_size": ctx.world_size, "rank": ctx.rank,
-                   "state": {k: (v.detach().cpu() if isinstance(v, torch.Tensor) else v) for k, v in state.items()}}
+                   "state": _encode(dict(state))}
         tmp = os.path.join(d, ".rank-%d.tmp" % ctx.rank)
         torch.save(payload, tmp)
         os.replace(tmp, os.path.join(d, "rank-%d.pt" % ctx.rank))
@@ -139,9 +201,10 @@ class CheckpointManager:
         if ws != ctx.world_size:
             raise RuntimeError("Checkpoint %s was written by %d ranks; recovery with %d ranks is not supported "
                                "(no rescaling, like the reference)." % (d, ws, ctx.world_size))
-        # our own files (written by save above); they hold python scalars/lists besides tensors
-        payload = torch.load(os.path.join(d, "rank-%d.pt" % ctx.rank), weights_only=False)
-        return int(payload["epoch"]), payload["state"]
+        # tensors, python scalars, strings, lists and dicts only: the weights-only unpickler
+        # executes nothing from a (possibly shared) checkpoint directory
+        payload = torch.load(os.path.join(d, "rank-%d.pt" % ctx.rank), weights_only=True)
+        return int(payload["epoch"]), _decode(payload["state"])
 
 
 _ACTIVE: Optional[CheckpointManager] = None

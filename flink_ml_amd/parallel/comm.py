@@ -98,6 +98,17 @@ def all_reduce_scalar(x: float, op: str = "sum", dtype=torch.float64) -> float:
     return v
 
 
+def all_agree(flag: bool) -> bool:
+    """True iff ``flag`` holds on every rank: one MIN over the process group itself (never the
+    xGMI exchange, and no check of it), so ranks can agree on leaving a failed exchange."""
+    ctx = get_context()
+    if not ctx.is_distributed:
+        return bool(flag)
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=_backend_device(ctx))
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(int(t.item()))
+
+
 def broadcast_tensor(t: torch.Tensor, src: int = 0) -> torch.Tensor:
     ctx = get_context()
     if not ctx.is_distributed:

@@ -26,6 +26,7 @@ class SPMDContext:
     device: torch.device = torch.device("cpu")
     backend: Optional[str] = None
     forced: bool = False  # FMLX_FORCE_PG=1: a process group (and its collectives) even at world 1
+    sharers: int = 1  # ranks of the group on this rank's physical GPU (measured at init, see below)
 
     @property
     def is_distributed(self) -> bool:
@@ -125,6 +126,8 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> SPM
             forced = world == 1
         _CTX = SPMDContext(rank=rank, world_size=world, local_rank=local_rank, device=device, backend=backend,
                            forced=forced)
+        if _CTX.is_distributed and _CTX.is_gpu and world > 1:
+            _CTX.sharers = _measure_sharers(_CTX)
     if _CTX.is_distributed and _CTX.is_gpu and backend == "nccl":
         from . import xgmi
 
@@ -132,16 +135,35 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> SPM
     return _CTX
 
 
+def device_identity(device: torch.device) -> str:
+    """Host name + PCI domain:bus:device of ``device``: equal strings = the same physical GPU,
+    whatever HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES renumbering each process sees."""
+    import socket
+
+    p = torch.cuda.get_device_properties(device)
+    return "%s/%04x:%02x:%02x" % (socket.gethostname(), p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+
+
+def count_sharers(ids, rank: int) -> int:
+    """Ranks whose device identity equals ``rank``'s (itself included)."""
+    return sum(1 for i in ids if i == ids[rank])
+
+
+def _measure_sharers(ctx: SPMDContext) -> int:
+    """All-gathers every rank's device identity once at init (one tiny collective every rank
+    reaches) and counts the ranks on this rank's GPU: 1 with a GPU per rank; every rank in the
+    one-GPU multi-rank rehearsals (``FMLX_DEVICE=cuda:0`` for all ranks)."""
+    ids = [None] * ctx.world_size
+    dist.all_gather_object(ids, device_identity(ctx.device))
+    return count_sharers(ids, ctx.rank)
+
+
 def device_sharers(ctx: SPMDContext) -> int:
-    """Ranks of this node running on this rank's GPU: 1 with a GPU per rank; every local rank in
-    the one-GPU multi-rank rehearsals (``FMLX_DEVICE=cuda:0`` for all ranks)."""
+    """Ranks of the group running on this rank's physical GPU (measured at ``init_distributed``
+    by comparing PCI ids, so per-process visible-device masks cannot fool it)."""
     if not ctx.is_gpu or ctx.world_size <= 1:
         return 1
-    local = int(os.environ.get("LOCAL_WORLD_SIZE", ctx.world_size))
-    if os.environ.get("FMLX_DEVICE", "").lower().startswith("cuda:"):
-        return local
-    n = max(1, torch.cuda.device_count())
-    return max(1, -(-local // n))
+    return max(1, int(ctx.sharers))
 
 
 def get_context() -> SPMDContext:

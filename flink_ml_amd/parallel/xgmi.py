@@ -57,7 +57,14 @@ native.register_kernel_sigs({
     "fmlx_xar_allreduce2": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p,
                             c_long, c_void_p],
     "fmlx_xar_twoshot_max": ([], c_long),
+    "fmlx_xar_strict_fence": [],
 })
+
+
+def strict_fence() -> bool:
+    """True when the exchange's hand-off uses system-scope release/acquire fences
+    (``FMLX_XGMI_STRICT_FENCE=1``, read once per process by the kernel library)."""
+    return bool(native.kernels().fmlx_xar_strict_fence())
 
 # polls (each ≈ one xGMI round trip + s_sleep) before a wait gives up: several seconds, far
 # beyond any lockstep drift between ranks, far below a hang
@@ -287,6 +294,21 @@ def check() -> None:
     algorithms call it at their host sync points, after the device work they waited for."""
     if _COMM is not None:
         _COMM.check()
+
+
+def disable() -> None:
+    """Retires the exchange for the rest of the process group's life (after a bounded wait gave
+    up, its peers' tags no longer line up): later device all-reduces go to the process group.
+    Collective in effect — every rank must call it at the same point (``comm.all_agree`` first)."""
+    global _COMM, _TRIED
+    with _LOCK:
+        if _COMM is not None:
+            try:
+                torch.cuda.synchronize(_COMM.device)
+            finally:
+                _COMM.close()
+        _COMM = None
+        _TRIED = True
 
 
 def reset() -> None:

@@ -226,3 +226,48 @@ def test_java_uniform_int_rows_gpu_matches_sequential(bound, k, n):
     np.testing.assert_array_equal(got.astype(np.int64), ref)
     _, cs = java_rows(77, n, [bound] * k, 0, device="cuda")
     np.testing.assert_array_equal(cs.cpu().numpy(), ref.astype(np.float64))
+
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench_cmd(*args, env=None, timeout=240):
+    import subprocess
+    import sys
+
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "FMLX_STORE")}
+    e.update({"FMLX_DEVICE": "cpu", "OMP_NUM_THREADS": "1"})
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(_ROOT, "bench.py")] + list(args), env=e, cwd=_ROOT,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_check_world():
+    import bench
+
+    assert bench.check_world(1, {}) == "run"
+    assert bench.check_world(4, {}) == "launch"
+    assert bench.check_world(4, {"WORLD_SIZE": "4"}) == "run"
+    with pytest.raises(SystemExit):
+        bench.check_world(2, {"WORLD_SIZE": "3"})
+    with pytest.raises(SystemExit):
+        bench.check_world(1, {"WORLD_SIZE": "8"})
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """`bench.py --gpus 3` with no WORLD_SIZE: the parent starts 3 rank processes that rendezvous
+    on its store and form one process group (the reference's benchmark-run.sh runs the job at the
+    cluster's parallelism, BenchmarkUtils.java:131-136)."""
+    r = _bench_cmd("--gpus", "3", "--dry-run")
+    assert r.returncode == 0, r.stderr
+    recs = sorted((json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")), key=lambda d: d["rank"])
+    assert [d["rank"] for d in recs] == [0, 1, 2]
+    assert all(d["world"] == 3 and d["backend"] == "gloo" and d["rank_sum"] == 6.0 for d in recs)
+
+
+def test_bench_world_mismatch_and_rank_failure_exit_nonzero():
+    r = _bench_cmd("--gpus", "2", "--dry-run", env={"WORLD_SIZE": "3", "RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr
+    # without --dry-run every CPU rank fails ("needs a GPU"): the launcher reports the failure
+    r = _bench_cmd("--gpus", "2", "--steps", "1", "--warmup", "0")
+    assert r.returncode != 0 and "needs a GPU" in r.stderr

@@ -113,3 +113,34 @@ def test_uncommitted_round_ignored(tmp_path):
     torch.save({"epoch": 2, "state": {}}, os.path.join(str(tmp_path), "job", "round-00000002", "rank-0.pt"))
     e, st = m.restore("job")
     assert e == 1 and st["x"].tolist() == [1.0]
+
+
+def test_checkpoint_restore_is_weights_only(tmp_path):
+    """ADVICE/VERDICT r4: restore never unpickles arbitrary objects. Payloads with numpy arrays,
+    tuples, non-string dict keys and package vectors round-trip through the weights-only loader;
+    a foreign class cannot be saved, and a file naming one is refused."""
+    import numpy as np
+    import torch
+
+    from flink_ml_amd.linalg.vectors import DenseVector
+    from flink_ml_amd.parallel import checkpoint as ck
+
+    mgr = ck.CheckpointManager(str(tmp_path), 1)
+    st = {"coef": torch.arange(4.0), "np": np.arange(6).reshape(2, 3), "t": (1, "a", 2.5), "k": {3: [np.float64(1.5)]},
+          "vec": DenseVector(np.array([1.0, 2.0]))}
+    mgr.save("alg", 3, st)
+    epoch, got = mgr.restore("alg")
+    assert epoch == 3 and torch.equal(got["coef"], st["coef"])
+    np.testing.assert_array_equal(got["np"], st["np"])
+    assert got["t"] == (1, "a", 2.5) and got["k"] == {3: [1.5]}
+    assert isinstance(got["vec"], DenseVector) and list(got["vec"].values) == [1.0, 2.0]
+
+    class Foreign:
+        pass
+
+    import pytest
+
+    with pytest.raises(TypeError):
+        mgr.save("alg", 4, {"x": Foreign()})
+    with pytest.raises(ValueError):
+        ck._decode({"__obj__": "os:system", "attrs": {}})

@@ -7,7 +7,7 @@ import gc
 import torch
 
 from flink_ml_amd.ops import glm as gk
-from flink_ml_amd.parallel.context import SPMDContext, device_sharers
+from flink_ml_amd.parallel.context import SPMDContext, count_sharers, device_sharers
 
 
 def test_batch_bounds_cached_per_tensor_and_version():
@@ -24,16 +24,13 @@ def test_batch_bounds_cached_per_tensor_and_version():
     assert key not in gk._BOUNDS_CACHE  # dropped with the tensor
 
 
-def test_device_sharers(monkeypatch):
+def test_device_sharers():
     cpu = SPMDContext(rank=0, world_size=4, device=torch.device("cpu"))
     assert device_sharers(cpu) == 1
-    gpu = SPMDContext(rank=1, world_size=4, device=torch.device("cuda", 0))
-    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
-    monkeypatch.setenv("FMLX_DEVICE", "cuda:0")  # every rank pinned to one GPU: all four share it
+    gpu = SPMDContext(rank=1, world_size=4, device=torch.device("cuda", 0), sharers=4)
     assert device_sharers(gpu) == 4
-    monkeypatch.delenv("FMLX_DEVICE")
-    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)  # a GPU per rank
-    assert device_sharers(gpu) == 1
-    monkeypatch.setattr(torch.cuda, "device_count", lambda: 2)
-    assert device_sharers(gpu) == 2
-    assert device_sharers(SPMDContext(rank=0, world_size=1, device=torch.device("cuda", 0))) == 1
+    assert device_sharers(SPMDContext(rank=1, world_size=4, device=torch.device("cuda", 0))) == 1
+    assert device_sharers(SPMDContext(rank=0, world_size=1, device=torch.device("cuda", 0), sharers=3)) == 1
+    # sharing is counted from the ranks' PCI identities, not guessed from device_count()
+    ids = ["h/0000:05:00", "h/0000:05:00", "h/0000:15:00", "g/0000:05:00"]
+    assert [count_sharers(ids, r) for r in range(4)] == [2, 2, 1, 1]

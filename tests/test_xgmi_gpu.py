@@ -21,13 +21,14 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-def _allreduce_worker(rank, world):
+def _allreduce_worker(rank, world, strict="0"):
     import torch
 
     from flink_ml_amd.parallel import xgmi
 
     x = xgmi.get()
     assert x is not None, "xGMI exchange did not come up"
+    assert xgmi.strict_fence() == (strict == "1")
     S = world * (world + 1) // 2
     for dt in (torch.float32, torch.float64):
         for n in (1, 7, 1024, 1025, 3 * 4096 + 7, 300_000):
@@ -47,9 +48,12 @@ def _allreduce_worker(rank, world):
     return True
 
 
-def test_xgmi_allreduce_two_ranks_one_gpu():
+@pytest.mark.parametrize("strict", ["0", "1"])
+def test_xgmi_allreduce_two_ranks_one_gpu(strict):
+    """Both fence modes of the hand-off (FMLX_XGMI_STRICT_FENCE)."""
     _need_gpu()
-    assert run_spmd(_allreduce_worker, 2, env=ENV, timeout=300) == [True, True]
+    env = dict(ENV, FMLX_XGMI_STRICT_FENCE=strict)
+    assert run_spmd(_allreduce_worker, 2, strict, env=env, timeout=300) == [True, True]
 
 
 def _twoshot_worker(rank, world, sizes):
@@ -85,16 +89,18 @@ def _twoshot_worker(rank, world, sizes):
     return True
 
 
+@pytest.mark.parametrize("strict", ["0", "1"])
 @pytest.mark.parametrize("world,sizes", [(2, (1, 1023, 1025, 2 * 1024 * 2 + 5, 300_000, 1_100_007)),
                                          (4, (1, 4097, 4 * 1024 * 3 + 1, 600_001))])
-def test_xgmi_twoshot_allreduce_ranks_on_one_gpu(world, sizes):
+def test_xgmi_twoshot_allreduce_ranks_on_one_gpu(world, sizes, strict):
     """Two-shot (reduce-scatter + all-gather over the peer-mapped buffers): exact integer sums
     for partial chunk groups, both slots, f32/f64; routing of a 4 MB payload through it."""
     _need_gpu()
-    assert run_spmd(_twoshot_worker, world, sizes, env=ENV, timeout=300) == [True] * world
+    env = dict(ENV, FMLX_XGMI_STRICT_FENCE=strict)
+    assert run_spmd(_twoshot_worker, world, sizes, env=env, timeout=300) == [True] * world
 
 
-def _sgd_worker(rank, world, xgmi_mode, dtype_name, defer_xgmi="1"):
+def _sgd_worker(rank, world, xgmi_mode, dtype_name, defer_xgmi="1", fallback=False):
     import os
 
     import numpy as np
@@ -119,25 +125,70 @@ def _sgd_worker(rank, world, xgmi_mode, dtype_name, defer_xgmi="1"):
         assert tr.mode == expect, (tr.mode, expect)
         # the in-kernel exchange runs deferred (launch e + 1's lead block completes round e)
         assert tr.defer == (xgmi_mode == "force" and defer_xgmi == "1"), tr.defer
+        if fallback:  # bench.py's re-time after an xGMI timeout: RCCL/gloo feedback path
+            tr.use_rccl()
+            assert tr.mode == gk.TAIL_FEEDBACK and not tr.defer and tr.cw is None and tr.xg is None
         got = tr.fit()
         out[loss] = (float(np.abs(got - ref).max()), float(np.abs(ref).max()), got.tobytes())
     return out
 
 
-@pytest.mark.parametrize("xgmi_mode,world,defer_xgmi", [("force", 2, "1"), ("force", 2, "0"), ("force", 4, "1"),
-                                                       ("0", 2, "1")])
-def test_fused_sgd_round_two_ranks_matches_host(xgmi_mode, world, defer_xgmi):
+@pytest.mark.parametrize("xgmi_mode,world,defer_xgmi,strict", [
+    ("force", 2, "1", "0"), ("force", 2, "0", "0"), ("force", 4, "1", "0"), ("0", 2, "1", "0"),
+    ("force", 2, "1", "1"), ("force", 4, "1", "1")])
+def test_fused_sgd_round_two_ranks_matches_host(xgmi_mode, world, defer_xgmi, strict):
+    _check_sgd_ranks(xgmi_mode, world, defer_xgmi, False, strict)
+
+
+def test_sgd_switch_to_rccl_after_xgmi_matches_host():
+    """DeviceGlmTrainer.use_rccl() (the bench's fallback left defer=1 on the feedback
+    tail and the launcher returned -7) trains through the process-group all-reduce instead."""
+    _check_sgd_ranks("force", 2, "1", True)
+
+
+def _check_sgd_ranks(xgmi_mode, world, defer_xgmi, fallback, strict="0"):
     """TAIL_XGMI (in-kernel xGMI exchange: deferred — launch e + 1's lead block exchanges and
     applies round e — and ticketed) and TAIL_FEEDBACK (+ process-group all-reduce) reproduce the
     fp64 host trainer at 2 and 4 ranks, and every rank ends with bit-identical coefficients."""
     _need_gpu()
-    env = dict(ENV, FMLX_XGMI=xgmi_mode, FMLX_GLM_DEFER_XGMI=defer_xgmi)
-    res = run_spmd(_sgd_worker, world, xgmi_mode, "float64", defer_xgmi, env=env, timeout=300)
+    env = dict(ENV, FMLX_XGMI=xgmi_mode, FMLX_GLM_DEFER_XGMI=defer_xgmi, FMLX_XGMI_STRICT_FENCE=strict)
+    res = run_spmd(_sgd_worker, world, xgmi_mode, "float64", defer_xgmi, fallback, env=env, timeout=300)
     for loss in res[0]:
         err, scale, b0 = res[0][loss]
         assert err <= 1e-9 * max(1.0, scale), (loss, err)
         for r in res[1:]:
             assert b0 == r[loss][2], loss  # replicas identical
+
+
+def _wide_grid_worker(rank, world):
+    import numpy as np
+    import torch
+
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
+    from flink_ml_amd.ops import glm as gk
+    from flink_ml_amd.parallel.context import get_context
+
+    g = torch.Generator(device="cpu").manual_seed(7 + rank)
+    n, d = 140_000, 64
+    X = torch.rand((n, d), generator=g, dtype=torch.float32).to(torch.bfloat16)
+    y = (X.double() @ torch.linspace(-1, 1, d, dtype=torch.float64) > 0).double()
+    sgd = SGD(max_iter=6, learning_rate=0.5, global_batch_size=2 * 70_000, tol=1e-9)
+    tr = DeviceGlmTrainer(sgd, np.zeros(d), X.cuda(), y.cuda(), None, "logistic", use_graph=False)
+    assert gk.round_blocks(tr.X) == 512 and get_context().sharers == world
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    assert tr.mode == gk.TAIL_XGMI and tr.nparts == cus // world, tr.nparts
+    got = tr.fit()
+    ref = TorchGlmTrainer(sgd, np.zeros(d), X.double(), y, None, "logistic").fit()
+    return float(np.abs(got - ref).max()), float(np.abs(ref).max())
+
+
+def test_two_ranks_one_gpu_512_block_shape_runs():
+    """two ranks sharing one GPU at a shape whose 1-rank grid is 512 blocks (two per CU
+    under the LDS pad) — every rank's grid must stay resident for the in-kernel exchange, so the
+    grid is capped to CUs / sharers (measured by PCI id) instead of timing out."""
+    _need_gpu()
+    for err, scale in run_spmd(_wide_grid_worker, 2, env=ENV, timeout=300):
+        assert err <= 1e-4 * max(1.0, scale), err
 
 
 @pytest.mark.parametrize("det,blocks,unroll,defer,dma", [
@@ -254,6 +305,13 @@ def _timeout_worker(rank, world):
         out["raised"] = False
     except xgmi.XgmiTimeout:
         out["raised"] = True
+    # bench.py's recovery: agree over the process group (no exchange check), retire the exchange,
+    # and the next device all-reduce goes to the process group with exact sums
+    out["agree"] = comm.all_agree(x.healthy())
+    xgmi.disable()
+    v = torch.full((8,), float(rank + 1), device="cuda:0")
+    comm.all_reduce_sum(v)
+    out["after"] = v.cpu().tolist()
     return out
 
 
@@ -263,6 +321,8 @@ def test_xgmi_timeout_poisons_and_raises():
     res = run_spmd(_timeout_worker, 2, env=ENV, timeout=300)
     r0 = res[0]
     assert r0["nan"] and not r0["healthy"] and r0["raised"], r0
+    assert not any(r["agree"] for r in res)
+    assert all(r["after"] == [3.0] * 8 for r in res)
 
 
 @pytest.mark.parametrize("rem", [0, 3])
