@@ -6,11 +6,15 @@ AUC by the tie-averaged rank sum and the trapezoid sums for area under PR and Lo
 KS (``BinaryClassificationEvaluator.java:103-460``).
 
 MI355X-native version of the same plan (K21):
-* range partition = sampled boundaries + one ``all_to_all_v`` of (score, label, weight);
-* local descending sort on the device (stable, so ties keep arrival order as in the reference);
+* range partition = sampled boundaries + a stable counting sort of the rows by target rank
+  (``groupsort.hip``) + one ``all_to_all_v`` of (score, label, weight);
+* local descending sort on the device: a stable LSD radix sort of 64-bit score keys over only the
+  bits that differ (``radix.hip``; ties keep arrival order as in the reference);
 * the per-partition summaries are an all-gather of two counts;
-* every metric is a prefix-sum (``cumsum``) expression over the sorted arrays — no per-row loop —
-  and the partial sums / max are all-reduced.
+* every metric comes out of one scan of the sorted rows (``binclass.hip``: cumulative TP/FP,
+  tie-group bounds for the averaged AUC ranks, PR / Lorenz trapezoids, KS max, fixed-order
+  partial sums) and the partial sums / max are all-reduced.
+The torch formulation below (``cumsum`` / ``unique_consecutive``) is the CPU reference.
 """
 from __future__ import annotations
 
@@ -66,9 +70,15 @@ def _range_partition(score, pos, w):
     # part = max i > 0 with score > bounds[i], else 0 (AppendTaskId)
     part = torch.clamp(torch.searchsorted(bounds, score, right=False) - 1, min=0)
     part = torch.where(score > bounds[0], part, torch.zeros_like(part))
-    order = torch.argsort(part, stable=True)
+    if score.is_cuda:
+        from ..ops.kmeans import group_by_key
+
+        order, offsets, _ = group_by_key(part, ctx.world_size, stable=True)  # groupsort.hip counting sort
+        counts = torch.diff(offsets).cpu().tolist()
+    else:
+        order = torch.argsort(part, stable=True)
+        counts = torch.bincount(part, minlength=ctx.world_size).cpu().tolist()
     packed = torch.stack([score, pos.to(torch.float64), w], dim=1)[order]
-    counts = torch.bincount(part, minlength=ctx.world_size).cpu().tolist()
     chunks = list(torch.split(packed, counts))
     recv = comm.all_to_all_v(chunks)
     got = torch.cat([r.to(score.device) for r in recv]) if recv else packed[:0]
@@ -79,6 +89,8 @@ def compute_metrics(score: torch.Tensor, pos: torch.Tensor, w: torch.Tensor) -> 
     dist = get_world_distributed()
     if dist:
         score, pos, w = _range_partition(score, pos, w)
+    if score.is_cuda:
+        return _device_metrics(score.contiguous(), pos, w, dist)
     order = torch.argsort(-score, stable=True)
     s, p, wt = score[order], pos[order], w[order]
     n_pos, n_neg = int(p.sum()), int((~p).sum())
@@ -130,6 +142,39 @@ def compute_metrics(score: torch.Tensor, pos: torch.Tensor, w: torch.Tensor) -> 
     else:
         lorenz = pr = ks = torch.zeros((), dtype=torch.float64, device=dev)
     sums = torch.cat([auc_parts, torch.stack([lorenz, pr])])
+    if dist:
+        sums = comm.all_reduce_sum(sums)
+        ks = comm.all_reduce(ks.reshape(1).clone(), "max")[0]
+    acc, P, N, lorenz, pr = sums.cpu().tolist()
+    auc = (acc - P * (P + 1) / 2) / (P * N) if P > 0 and N > 0 else float("nan")
+    return {AREA_UNDER_ROC: auc, AREA_UNDER_PR: pr, AREA_UNDER_LORENZ: lorenz, KS: float(ks)}
+
+
+def _device_metrics(score: torch.Tensor, pos: torch.Tensor, w: torch.Tensor, dist: bool) -> dict:
+    """The same metrics through the native sort + scan (ops/sorting.py)."""
+    from ..ops import sorting
+
+    n = score.numel()
+    n_pos = int(pos.sum()) if n else 0
+    n_neg = n - n_pos
+    before_t = before_f = 0
+    tot_t, tot_f = n_pos, n_neg
+    if dist:
+        from ..parallel.context import get_context
+
+        ctx = get_context()
+        summ = comm.all_gather_object((n_pos, n_neg))
+        before_t = sum(summ[r][0] for r in range(ctx.rank + 1, ctx.world_size))
+        before_f = sum(summ[r][1] for r in range(ctx.rank + 1, ctx.world_size))
+        tot_t = sum(x[0] for x in summ)
+        tot_f = sum(x[1] for x in summ)
+    total = tot_t + tot_f
+    keys, rows = sorting.sort_scores_desc(score)
+    unit = bool((w == 1).all()) if n else True
+    m = sorting.binary_metrics(keys, rows, pos, None if unit else w, before_t, before_f, tot_t, tot_f)
+    # Σ_g avg_rank_g·PW_g with avg_rank = total − before − (gs + ge)/2 (local positions gs..ge)
+    sums = torch.stack([(total - before_t - before_f) * m[1] - 0.5 * m[0], m[1], m[2], m[3], m[4]])
+    ks = m[5]
     if dist:
         sums = comm.all_reduce_sum(sums)
         ks = comm.all_reduce(ks.reshape(1).clone(), "max")[0]

@@ -104,20 +104,18 @@ class Bucketizer(Transformer, HasInputCols, HasOutputCols, HasHandleInvalid):
 
 
 # ------------------------------------------------------------------------------------ DCT
-@functools.lru_cache(maxsize=32)
 def _dct_matrix(n: int) -> torch.Tensor:
-    k = torch.arange(n, dtype=torch.float64)[:, None]
-    i = torch.arange(n, dtype=torch.float64)[None, :]
-    m = torch.cos(math.pi * (2 * i + 1) * k / (2 * n))
-    m[0] *= math.sqrt(1.0 / n)
-    m[1:] *= math.sqrt(2.0 / n)
-    return m  # orthonormal DCT-II basis (rows)
+    from ...ops.dct import dct_matrix
+
+    return dct_matrix(n)  # orthonormal DCT-II basis (rows)
 
 
 @rw.register_stage
 class DCT(Transformer, HasInputCol, HasOutputCol):
     """Orthonormal DCT-II / DCT-III (JTransforms ``DoubleDCT_1D`` with scaled=true, DCT.java:103-123)
-    as a GEMM against the cached basis (K17: MFMA-friendly, one library GEMM per batch)."""
+    as a product with the basis. K17 on the GPU: f32 rows of n ≤ 128 go through the hand-written
+    f32-MFMA kernel with the basis resident in LDS (``ops/csrc/dct.hip``); fp64 (parity mode),
+    wider rows and the CPU take the same product as a plain GEMM."""
 
     JAVA_CLASS_NAME = "org.apache.flink.ml.feature.dct.DCT"
     INVERSE = BooleanParam("inverse", "Whether to perform the inverse DCT (true) or forward DCT (false).", False)
@@ -126,10 +124,15 @@ class DCT(Transformer, HasInputCol, HasOutputCol):
         t = inputs[0]
         X = dense_input(t, self.get(self.INPUT_COL))
         n = X.shape[1]
+        inv = self.get(self.INVERSE)
         dt = torch.float64 if X.dtype == torch.float64 or X.device.type == "cpu" else torch.float32
-        M = _dct_matrix(n).to(device=X.device, dtype=dt)
         Xd = X.to(dt)
-        out = Xd @ M if self.get(self.INVERSE) else Xd @ M.T
+        if Xd.is_cuda and dt == torch.float32 and 1 <= n <= 128:
+            from ...ops.dct import dct_rows
+
+            return [t.with_column(self.get(self.OUTPUT_COL), dct_rows(Xd, inv))]
+        M = _dct_matrix(n).to(device=X.device, dtype=dt)
+        out = Xd @ M if inv else Xd @ M.T
         return [t.with_column(self.get(self.OUTPUT_COL), out)]
 
 

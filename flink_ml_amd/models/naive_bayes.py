@@ -124,6 +124,8 @@ def _label_value_counts(X: torch.Tensor, li: torch.Tensor, L: int, dist: bool):
     label) shuffle of ``stats.value_label_counts`` across ranks."""
     n, d = X.shape
     dev = X.device
+    if X.is_cuda:
+        return _label_value_counts_device(X, li, L, dist)
     n_lab = torch.bincount(li, minlength=L).to(torch.float64)
     if n:
         flags = torch.stack([-X.min(), X.max(), (X != torch.round(X)).any().to(X.dtype)]).to(torch.float64)
@@ -178,6 +180,47 @@ def _label_value_counts(X: torch.Tensor, li: torch.Tensor, L: int, dist: bool):
             n_lab.cpu().numpy())
 
 
+def _label_value_counts_device(X: torch.Tensor, li: torch.Tensor, L: int, dist: bool):
+    """``_label_value_counts`` through the native contingency kernels (ops/catstats.py): integer
+    features with a table of at most 2^27 cells (the categorical case; value range from the global
+    min / max) are counted by one pass of ``cs_hist`` into [d, L, V] and all-reduced as one dense
+    table; other values take the sorted-column distinct pass on one rank and the keyed shuffle of
+    ``stats.value_label_counts`` across ranks."""
+    from ..ops import catstats
+
+    n, d = X.shape
+    dev = X.device
+    n_lab = catstats.label_counts(li, L).to(torch.float64)
+    mn, mx, non = catstats.flags(X) if n else (float("inf"), float("-inf"), False)
+    if dist:
+        f = comm.all_reduce(torch.tensor([-mn, mx, float(non)], dtype=torch.float64, device=dev), "max").tolist()
+        mn, mx, non = -f[0], f[1], f[2] != 0.0
+    if not non and mx >= mn and (mx - mn + 1) * L * d <= catstats.MAX_TABLE:
+        vmin, V = int(mn), int(mx - mn) + 1
+        cnt = catstats.int_table(X, li, L, vmin, V).to(torch.float64)
+        if dist:
+            both = comm.all_reduce_sum(torch.cat([cnt.reshape(-1), n_lab]))
+            cnt, n_lab = both[:-L].reshape(d, L, V), both[-L:]
+        counts = cnt.cpu().numpy()
+        present = counts.sum(1) > 0
+        slots = [np.nonzero(present[j])[0] for j in range(d)]
+        return counts, [(sl + vmin).astype(np.float64) for sl in slots], slots, n_lab.cpu().numpy()
+    if dist:
+        vals_t, flat, Vn = value_label_counts(X, li, L)
+        Vmax = max(1, int(Vn.max()) if d else 1)
+        counts = np.zeros((d, L, Vmax), dtype=np.float64)
+        off = 0
+        for j in range(d):
+            V = int(Vn[j])
+            counts[j, :, :V] = flat[off:off + V * L].reshape(V, L).T
+            off += V * L
+        n_lab = comm.all_reduce_sum(n_lab)
+        return (counts, [v.cpu().numpy() for v in vals_t], [np.arange(int(Vn[j])) for j in range(d)],
+                n_lab.cpu().numpy())
+    counts, vals, slots = catstats.value_label_counts(X, li, L, int_range=None)
+    return counts.astype(np.float64), vals, slots, n_lab.cpu().numpy()
+
+
 @rw.register_stage
 class NaiveBayes(Estimator, NaiveBayesParams):
     JAVA_CLASS_NAME = "org.apache.flink.ml.classification.naivebayes.NaiveBayes"
@@ -202,7 +245,7 @@ class NaiveBayes(Estimator, NaiveBayesParams):
                 raise ValueError("Feature vectors should be of equal length.") from None
         labels = global_sorted_unique(y)
         L, d = labels.numel(), X.shape[1]
-        li = torch.searchsorted(labels, y)
+        li = torch.searchsorted(labels, y)  # binary search per row
         counts, vals, slots, n_l = _label_value_counts(X, li, L, dist)
         labels_np = labels.cpu().numpy()
         # the reference's model lists labels in HashMap<Double, _> order

@@ -55,7 +55,12 @@ def features_and_labels(t: Table, features_col: str, label_col: str,
 def global_sorted_unique(v: torch.Tensor) -> torch.Tensor:
     """Sorted union of the ranks' distinct values (labels / categories): a keyed distinct over
     the values' bit patterns (all-to-all to the key owners, all-gather of their results)."""
-    u = torch.unique(v)
+    if v.is_cuda:
+        from ..ops import catstats
+
+        u = catstats.sorted_unique(v).to(v.dtype)  # native histogram / sorted distinct (no library sort)
+    else:
+        u = torch.unique(v)
     if get_world_distributed():
         k, _ = ds.global_distinct(ds.float_keys(u))
         u = torch.sort(ds.keys_to_float(k)).values.to(device=v.device, dtype=v.dtype)
@@ -135,7 +140,13 @@ class ANOVATest(AlgoOperator, _TestParams):
         else:
             Xd = X.to(torch.float64)
             S, tot, totsq = class_sums(Xd, ci, C), Xd.sum(0), (Xd * Xd).sum(0)
-        packed = torch.cat([S.reshape(-1), torch.bincount(ci, minlength=C).to(torch.float64), tot, totsq])
+        if ci.is_cuda:
+            from ..ops import catstats
+
+            cls_n = catstats.label_counts(ci, C).to(torch.float64)
+        else:
+            cls_n = torch.bincount(ci, minlength=C).to(torch.float64)
+        packed = torch.cat([S.reshape(-1), cls_n, tot, totsq])
         packed = _reduce(packed).cpu().numpy()
         S = packed[:C * d].reshape(C, d)
         cnt = packed[C * d:C * d + C]
@@ -211,6 +222,14 @@ class ChiSqTest(AlgoOperator, _TestParams):
         if get_world_distributed():
             # distinct values and contingency counts in one keyed shuffle (no value lists pickled)
             vals, flat, _ = value_label_counts(X, li, L)
+        elif X.is_cuda:
+            # native contingency tables (ops/catstats.py: integer table or sorted-column distinct)
+            from ..ops import catstats
+
+            counts, vals_np, slots = catstats.value_label_counts(X, li, L)
+            vals = [torch.as_tensor(v) for v in vals_np]
+            flat = np.concatenate([counts[j][:, slots[j]].T.reshape(-1) for j in range(d)]).astype(np.float64) \
+                if d else np.zeros(0)
         else:
             vals = [torch.unique(X[:, j]) for j in range(d)]
             tables = []

@@ -1,0 +1,179 @@
+"""Device contingency statistics (``csrc/catstats.hip``): sorted distinct values, label indices
+and (feature, value, label) counts for NaiveBayes (K22) and ChiSqTest (K20), with no library
+sort / unique / bincount. Integer-valued columns with a small value range (the categorical
+case) are counted straight into an LDS-privatised table; anything else goes through the stable
+64-bit radix sort of each column (``ops/sorting.py``) and a distinct-id scan.
+
+All functions take CUDA tensors; the CPU reference of every result is the torch code in
+``models/stats.py`` / ``models/naive_bayes.py``.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import native, sorting
+from .native import c_int, c_long, c_void_p
+
+native.register_kernel_sigs({
+    "fmlx_cs_tile": [],
+    "fmlx_cs_lds_ints": [],
+    "fmlx_cs_flags": [c_int, c_void_p, c_long, c_long, c_int, c_void_p, c_void_p, c_void_p],
+    "fmlx_cs_ihist": [c_int, c_void_p, c_long, c_long, c_int, c_long, c_int, c_void_p, c_void_p],
+    "fmlx_cs_hist": [c_int, c_void_p, c_long, c_long, c_int, c_void_p, c_int, c_long, c_int, c_void_p, c_void_p],
+    "fmlx_cs_col_keys": [c_int, c_void_p, c_long, c_long, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "fmlx_cs_distinct": [c_void_p, c_void_p, c_long, c_int, c_int, c_void_p, c_long, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_void_p],
+    "fmlx_cs_chist": [c_void_p, c_long, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
+})
+
+# integer tables up to this many cells are counted directly (value range × labels × features)
+MAX_TABLE = 1 << 27
+# integer labels / values are histogrammed directly up to this range
+MAX_INT_RANGE = 1 << 24
+SORT_SEGMENTS = 32  # columns per segmented sort call (radix.hip RS_MAXS)
+
+
+def _mat(X: torch.Tensor) -> torch.Tensor:
+    if X.dim() == 1:
+        X = X.reshape(-1, 1)
+    if X.dtype not in (torch.float32, torch.float64):
+        X = X.to(torch.float64)
+    if X.stride(1) != 1:
+        X = X.contiguous()
+    return X
+
+
+def flags(X: torch.Tensor) -> Tuple[float, float, bool]:
+    """(min, max, any non-integer or non-finite) of all elements of X (device reduction)."""
+    X = _mat(X)
+    n, d = X.shape
+    if n * d == 0:
+        return float("inf"), float("-inf"), False
+    dev = X.device
+    part = torch.empty(3 * 1024, dtype=torch.float64, device=dev)
+    out = torch.empty(3, dtype=torch.float64, device=dev)
+    native.call("fmlx_cs_flags", native.dtype_code(X.dtype), native.ptr(X), X.stride(0), n, d, native.ptr(part),
+                native.ptr(out), native.stream_ptr(dev))
+    mn, mx, non = out.cpu().tolist()
+    return mn, mx, non != 0.0
+
+
+def int_hist(v: torch.Tensor, lo: int, R: int) -> torch.Tensor:
+    """int32 counts of the integer values lo … lo + R − 1 of the 1-D tensor ``v`` (device)."""
+    dev = v.device
+    if v.dtype not in (torch.float32, torch.float64, torch.int32):
+        v = v.to(torch.float64)
+    v = v.reshape(-1, 1).contiguous()
+    counts = torch.zeros(max(1, R), dtype=torch.int32, device=dev)
+    if v.shape[0]:
+        native.call("fmlx_cs_ihist", native.dtype_code(v.dtype), native.ptr(v), 1, v.shape[0], 0, int(lo), int(R),
+                    native.ptr(counts), native.stream_ptr(dev))
+    return counts[:R]
+
+
+def distinct_codes(X: torch.Tensor) -> Tuple[torch.Tensor, List[torch.Tensor]]:
+    """Per column j of X [n, d]: the sorted distinct values (fp64, device; −0 folded into +0, NaN
+    last) and every row's index into them: codes int32 [d, n]."""
+    X = _mat(X)
+    n, d = X.shape
+    dev = X.device
+    codes = torch.empty((d, n), dtype=torch.int32, device=dev)
+    vals: List[torch.Tensor] = []
+    tile = int(native.kernels().fmlx_cs_tile())
+    for j0 in range(0, d, SORT_SEGMENTS):
+        nc = min(SORT_SEGMENTS, d - j0)
+        m = n * nc
+        keys = torch.empty(m, dtype=torch.int64, device=dev)
+        rows = torch.empty(m, dtype=torch.int32, device=dev)
+        orand = torch.tensor([0, -1], dtype=torch.int64, device=dev)
+        native.call("fmlx_cs_col_keys", native.dtype_code(X.dtype), native.ptr(X), X.stride(0), n, j0, nc,
+                    native.ptr(keys), native.ptr(rows), native.ptr(orand), native.stream_ptr(dev))
+        lo, hi = sorting.bit_range(orand)
+        keys, rows = sorting.sort_u64(keys, rows, [c * n for c in range(nc + 1)], lo, hi)
+        nt = max(1, -(-m // tile))
+        tcnt = torch.empty(nt + 1, dtype=torch.int64, device=dev)
+        uval = torch.empty(max(1, m), dtype=torch.float64, device=dev)
+        ucol = torch.empty(max(1, m), dtype=torch.int32, device=dev)
+        colfirst = torch.zeros(nc, dtype=torch.int64, device=dev)
+        native.call("fmlx_cs_distinct", native.ptr(keys), native.ptr(rows), n, nc, j0, native.ptr(tcnt), 0,
+                    native.ptr(codes[j0:j0 + nc]), native.ptr(uval), native.ptr(ucol), native.ptr(colfirst),
+                    native.stream_ptr(dev))
+        if n == 0:
+            vals += [torch.empty(0, dtype=torch.float64, device=dev) for _ in range(nc)]
+            continue
+        first = colfirst.cpu().tolist() + [int(tcnt[nt].item())]
+        vals += [uval[first[c]:first[c + 1]] for c in range(nc)]
+    return codes, vals
+
+
+def sorted_unique(v: torch.Tensor) -> torch.Tensor:
+    """Sorted distinct values of a 1-D tensor (fp64): a presence histogram for small-range
+    integers, else the sorted-column distinct pass."""
+    v = v.reshape(-1)
+    if v.numel() == 0:
+        return torch.empty(0, dtype=torch.float64, device=v.device)
+    mn, mx, non = flags(v)
+    if not non and mx - mn + 1 <= MAX_INT_RANGE:
+        cnt = int_hist(v, int(mn), int(mx - mn) + 1)
+        present = np.nonzero(cnt.cpu().numpy())[0]
+        return torch.as_tensor(present + int(mn), dtype=torch.float64).to(v.device)
+    return distinct_codes(v)[1][0]
+
+
+def label_index(y: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    """int32 index of every y in the sorted ``labels`` (a binary search per row)."""
+    return torch.searchsorted(labels.to(torch.float64), y.reshape(-1).to(torch.float64)).to(torch.int32)
+
+
+def label_counts(li: torch.Tensor, L: int) -> torch.Tensor:
+    """int64 rows per label index 0 … L − 1."""
+    return int_hist(li.to(torch.int32), 0, L).to(torch.int64)
+
+
+def int_table(X: torch.Tensor, li: torch.Tensor, L: int, vmin: int, V: int) -> torch.Tensor:
+    """int32 [d, L, V] counts of the integer values vmin … vmin + V − 1 per (feature, label
+    index) — one pass over X (LDS-privatised table when d·L·V fits)."""
+    X = _mat(X)
+    n, d = X.shape
+    dev = X.device
+    counts = torch.zeros(max(1, d * L * V), dtype=torch.int32, device=dev)
+    if n and d:
+        native.call("fmlx_cs_hist", native.dtype_code(X.dtype), native.ptr(X), X.stride(0), n, d,
+                    native.ptr(li.to(torch.int32).contiguous()), L, int(vmin), int(V), native.ptr(counts),
+                    native.stream_ptr(dev))
+    return counts[:d * L * V].reshape(d, L, V)
+
+
+def value_label_counts(X: torch.Tensor, li: torch.Tensor, L: int,
+                       int_range: Optional[Tuple[float, float]] = None):
+    """(feature, distinct value, label) counts of one rank's rows.
+
+    Returns (counts int64 [d, L, Vmax] numpy, per-feature sorted distinct values as numpy fp64,
+    per-feature slots of those values in the last axis). ``int_range`` = (min, max) when X is
+    known to hold integers (the caller's flags, possibly all-reduced): the direct table path."""
+    X = _mat(X)
+    n, d = X.shape
+    dev = X.device
+    li = li.to(torch.int32).contiguous()
+    if int_range is None:
+        mn, mx, non = flags(X)
+        int_range = None if non else (mn, mx)
+    if int_range is not None and n and (int_range[1] - int_range[0] + 1) * L * d <= MAX_TABLE:
+        vmin = int(int_range[0])
+        V = int(int_range[1]) - vmin + 1
+        c = int_table(X, li, L, vmin, V).cpu().numpy().astype(np.int64)
+        present = c.sum(1) > 0
+        slots = [np.nonzero(present[j])[0] for j in range(d)]
+        return c, [(sl + vmin).astype(np.float64) for sl in slots], slots
+    codes, vals = distinct_codes(X)
+    Vn = [int(v.numel()) for v in vals]
+    Vmax = max([1] + Vn)
+    coloff = torch.arange(d, dtype=torch.int64, device=dev) * Vmax
+    counts = torch.zeros(max(1, d * Vmax * L), dtype=torch.int32, device=dev)
+    native.call("fmlx_cs_chist", native.ptr(codes), n, d, native.ptr(coloff), native.ptr(li), L, native.ptr(counts),
+                native.stream_ptr(dev))
+    c = counts[:d * Vmax * L].reshape(d, Vmax, L).permute(0, 2, 1).cpu().numpy().astype(np.int64)
+    return c, [v.cpu().numpy() for v in vals], [np.arange(V) for V in Vn]

@@ -568,3 +568,17 @@ FMLX_API int fmlx_blas_interaction(int k, const double* const* in, const long* l
                      out);
   return (int)hipGetLastError();
 }
+
+// Launches every translation unit's anchor kernel once (loads all code objects of the library);
+// returns the number of code objects, or < 0 on a launch error.
+FMLX_API int fmlx_preload_all(void* stream) {
+  int k = 0;
+  for (const void* f : fmlx_preload::registry()) {
+    const hipError_t e = hipLaunchKernel(f, dim3(1), dim3(64), nullptr, 0, (hipStream_t)stream);
+    if (e != hipSuccess) return -(int)e;
+    ++k;
+  }
+  return k;
+}
+
+FMLX_DEFINE_PRELOAD()

@@ -132,3 +132,5 @@ FMLX_API int fmlx_affine_cols(int dtype, int out_dtype, const void* X, long ld, 
     return launch_affine<float, double>(X, ld, n, d, sub, mul, add, out, s);
   return -1;
 }
+
+FMLX_DEFINE_PRELOAD()

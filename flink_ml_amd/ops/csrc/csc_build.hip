@@ -217,3 +217,5 @@ FMLX_API int fmlx_csc_colptr(const int* sorted_keys, long m, int slots, int d, c
                      sorted_keys, (int)m, slots, d, rs, b0, colptr);
   return (int)hipGetLastError();
 }
+
+FMLX_DEFINE_PRELOAD()

@@ -242,3 +242,5 @@ FMLX_API int fmlx_java_rows(int vec_dtype, unsigned long long seed, unsigned lon
                           first_reject, st);
   return -1;
 }
+
+FMLX_DEFINE_PRELOAD()

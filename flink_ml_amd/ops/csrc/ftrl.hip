@@ -39,3 +39,5 @@ FMLX_API int fmlx_ftrl_update(int acc_f64, const void* grad, const void* wsum, v
                        (float)l1, (float)l2);
   return (int)hipGetLastError();
 }
+
+FMLX_DEFINE_PRELOAD()

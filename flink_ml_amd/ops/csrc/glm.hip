@@ -1882,3 +1882,5 @@ FMLX_API int fmlx_glm_csr_predict(int acc_f64, const long* indptr, const int* id
   return (int)hipGetLastError();
 }
 #endif  // FMLX_ISA_PROBE
+
+FMLX_DEFINE_PRELOAD()

@@ -345,3 +345,5 @@ FMLX_API int fmlx_group_by_key(const int* keys, long n, int k, int chunk, int* c
   if (n > 0) hipLaunchKernelGGL(group_scatter_kernel, dim3(tiles), dim3(GS_THREADS), lds, s, keys, n, k, cursor, order);
   return (int)hipGetLastError();
 }
+
+FMLX_DEFINE_PRELOAD()

@@ -101,3 +101,5 @@ FMLX_API int fmlx_group_colstats(int dtype, const void* X, long ld, long n, int 
   if (dtype == DT_BF16) return launch<bf16_t>(X, ld, n, d, gidx, G, w, part, nb, res, s);
   return -1;
 }
+
+FMLX_DEFINE_PRELOAD()

@@ -55,3 +55,5 @@ FMLX_API int fmlx_murmur3_chars_device(const void* units, const long* offsets, l
                      offsets, n, mod, mode, hash_out, index_out);
   return (int)hipGetLastError();
 }
+
+FMLX_DEFINE_PRELOAD()

@@ -306,3 +306,5 @@ FMLX_API int fmlx_hash_prefixed_doubles_dev(const uint16_t* prefix, int plen, co
                      n, inv_tab, pow_tab, out);
   FMLX_CHECK_LAUNCH();
 }
+
+FMLX_DEFINE_PRELOAD()

@@ -1291,3 +1291,5 @@ FMLX_API int fmlx_kmeans_finalize(int acc_f64, const void* red, int D, int k, vo
                        weights, (bf16_t*)Cb, DP, cnorm_bf16, (float*)cnorm_acc);
   return (int)hipGetLastError();
 }
+
+FMLX_DEFINE_PRELOAD()

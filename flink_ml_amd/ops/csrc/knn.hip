@@ -539,3 +539,5 @@ FMLX_API int fmlx_knn_fused(const float* Q, long ldq, long nq, int D, const floa
   if (k <= 32) return launch_fused_k<32>(Q, ldq, nq, D, Tt, n, dp, k, S, idx, dist, ws_d, ws_i, s);
   return launch_fused_k<64>(Q, ldq, nq, D, Tt, n, dp, k, S, idx, dist, ws_d, ws_i, s);
 }
+
+FMLX_DEFINE_PRELOAD()

@@ -65,3 +65,5 @@ FMLX_API int fmlx_minhash_csr(const long* indptr, const int* indices, long n, in
                      n, K, coef_a, coef_b, out);
   return (int)hipGetLastError();
 }
+
+FMLX_DEFINE_PRELOAD()

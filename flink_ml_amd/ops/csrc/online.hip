@@ -208,3 +208,5 @@ FMLX_API int fmlx_okm_merge(int acc_f64, const void* m, int k, int D, int world,
                        (float*)W, (bf16_t*)Cb, DP, cnorm_bf16, (float*)cnorm_acc, version);
   return (int)hipGetLastError();
 }
+
+FMLX_DEFINE_PRELOAD()

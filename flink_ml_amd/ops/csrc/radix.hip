@@ -60,30 +60,39 @@ __device__ __forceinline__ void tile_range(const SegTable& tb, int t, long& a, l
 
 constexpr int RS_PER_LANE = RS_SEG / 64;  // pairs per lane of a wave segment
 
+// digit of a key: int32 keys are offset by the segment's kbase (the column-major copies' slot·d);
+// 64-bit keys (fmlx_sort_u64: ordered fp64 scores / value bits) carry no offset
+__device__ __forceinline__ int rs_digit(int key, int kb, int shift, int mask) { return ((key - kb) >> shift) & mask; }
+__device__ __forceinline__ int rs_digit(uint64_t key, int, int shift, int mask) {
+  return (int)(key >> shift) & mask;
+}
+
 // the wave's segment [wa, wb) into registers, all loads in flight at once (one memory latency
 // per segment, not one per 64 pairs: at one 136 KiB-LDS block per CU the scatter has 2 waves per
 // SIMD and a load-then-use loop waited out each load)
-template <typename V>
-__device__ __forceinline__ void rs_load_seg(const int* __restrict__ kin, const V* __restrict__ vin, long wa, long wb,
-                                            int (&k)[RS_PER_LANE], V (&v)[RS_PER_LANE]) {
+template <typename V, typename K = int>
+__device__ __forceinline__ void rs_load_seg(const K* __restrict__ kin, const V* __restrict__ vin, long wa, long wb,
+                                            K (&k)[RS_PER_LANE], V (&v)[RS_PER_LANE]) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int j = 0; j < RS_PER_LANE; ++j) {
     const long i = wa + j * 64 + lane;
-    if (kin != nullptr) k[j] = i < wb ? kin[i] : 0;
+    if (kin != nullptr) k[j] = i < wb ? kin[i] : K(0);
     if (vin != nullptr) v[j] = i < wb ? vin[i] : V(0);
   }
 }
 
-__device__ __forceinline__ void rs_wave_hist(const int (&k)[RS_PER_LANE], long wa, long wb, int kb, int shift,
+template <typename K>
+__device__ __forceinline__ void rs_wave_hist(const K (&k)[RS_PER_LANE], long wa, long wb, int kb, int shift,
                                              int mask, int* h) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int j = 0; j < RS_PER_LANE; ++j)
-    if (wa + j * 64 + lane < wb) atomicAdd(&h[((k[j] - kb) >> shift) & mask], 1);  // LDS
+    if (wa + j * 64 + lane < wb) atomicAdd(&h[rs_digit(k[j], kb, shift, mask)], 1);  // LDS
 }
 
-__global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const int* __restrict__ keys, SegTable tb, int shift,
+template <typename K>
+__global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const K* __restrict__ keys, SegTable tb, int shift,
                                                              int mask, int* __restrict__ T) {
   extern __shared__ int sh[];
   const int nd = mask + 1, w = threadIdx.x >> 6;
@@ -94,9 +103,9 @@ __global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const int* __restri
   tile_range(tb, blockIdx.x, a, b, kb);
   const long wa = a + (long)w * RS_SEG;
   const long wb = wa + RS_SEG < b ? wa + RS_SEG : b;
-  int k[RS_PER_LANE];
+  K k[RS_PER_LANE];
   int dummy[RS_PER_LANE];
-  rs_load_seg<int>(keys, nullptr, wa, wb, k, dummy);
+  rs_load_seg<int, K>(keys, nullptr, wa, wb, k, dummy);
   rs_wave_hist(k, wa, wb, kb, shift, mask, sh + (long)w * nd);
   __syncthreads();
   int* out = T + (long)blockIdx.x * nd;
@@ -218,8 +227,8 @@ __device__ __forceinline__ void rs_tile_cursors(int* hw, int nd, int* loc, int* 
 // place(pos, key, val, digit) for every valid pair, pos = the wave's cursor for the digit + the
 // pair's rank among the equal digits of its 64. The rank: the lanes holding my digit (one ballot
 // per digit bit, no cross-lane data movement), then the count of those below me.
-template <typename V, typename Place>
-__device__ __forceinline__ void rs_rank_place(const int (&kr)[RS_PER_LANE], const V (&vr)[RS_PER_LANE], long wa,
+template <typename V, typename Place, typename K = int>
+__device__ __forceinline__ void rs_rank_place(const K (&kr)[RS_PER_LANE], const V (&vr)[RS_PER_LANE], long wa,
                                               long wb, int kb, int shift, int mask, int* cur, Place place) {
   const int lane = threadIdx.x & 63;
   const int db = 31 - __builtin_clz(mask + 1);  // digit bits
@@ -227,8 +236,8 @@ __device__ __forceinline__ void rs_rank_place(const int (&kr)[RS_PER_LANE], cons
 #pragma unroll
   for (int j = 0; j < RS_PER_LANE; ++j) {
     const bool valid = wa + j * 64 + lane < wb;
-    const int key = kr[j];
-    const int dg = valid ? ((key - kb) >> shift) & mask : 0;
+    const K key = kr[j];
+    const int dg = valid ? rs_digit(key, kb, shift, mask) : 0;
     unsigned long long peers = __ballot(valid);
     for (int bit = 0; bit < db; ++bit) {
       // M = all ones where my digit has this bit, else 0; the lanes agreeing with me on it are
@@ -256,9 +265,9 @@ __device__ __forceinline__ void rs_rank_place(const int (&kr)[RS_PER_LANE], cons
 // different buckets (the direct form measured 1.95 ms per pass over 64M pairs: 0.8 TB/s).
 // SPLIT (64-bit payloads, last pass): the payload's low / high words go straight to two arrays
 // (the column-major copy's row ids and values) at split_off + position, so no separate unpack pass.
-template <typename V, bool SPLIT>
-__global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const int* __restrict__ kin, const V* __restrict__ vin,
-                                                                int* __restrict__ kout, V* __restrict__ vout,
+template <typename V, bool SPLIT, typename K = int>
+__global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const K* __restrict__ kin, const V* __restrict__ vin,
+                                                                K* __restrict__ kout, V* __restrict__ vout,
                                                                 const int* __restrict__ T, const int* __restrict__ G,
                                                                 SegTable tb, int shift, int mask,
                                                                 int* __restrict__ split_lo,
@@ -270,8 +279,8 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const int* __res
   int* hw = shs;                                 // [RS_WAVES][nd] per-wave counts → wave cursors
   int* loc = hw + RS_WAVES * nd;                 // [nd] tile-local start of each digit
   int* gbase = loc + nd;                         // [nd] global start of the tile's digit run
-  int* lk = gbase + nd;                          // [RS_TILE] keys in tile-local sorted order
-  V* lv = reinterpret_cast<V*>(lk + RS_TILE);    // [RS_TILE] payloads (8-B aligned: nd even)
+  K* lk = reinterpret_cast<K*>(gbase + nd);      // [RS_TILE] keys in tile-local sorted order (8-B aligned: nd even)
+  V* lv = reinterpret_cast<V*>(lk + RS_TILE);    // [RS_TILE] payloads
   int* wsum = reinterpret_cast<int*>(lv + RS_TILE);  // [RS_WAVES] wave totals of the digit scan
   for (int i = threadIdx.x; i < RS_WAVES * nd; i += RS_THREADS) hw[i] = 0;
   __syncthreads();
@@ -280,9 +289,9 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const int* __res
   tile_range(tb, t, a, b, kb);
   const long wa = a + (long)w * RS_SEG;
   const long wb = wa + RS_SEG < b ? wa + RS_SEG : b;
-  int kr[RS_PER_LANE];
+  K kr[RS_PER_LANE];
   V vr[RS_PER_LANE];
-  rs_load_seg<V>(kin, vin, wa, wb, kr, vr);
+  rs_load_seg<V, K>(kin, vin, wa, wb, kr, vr);
   rs_wave_hist(kr, wa, wb, kb, shift, mask, hw + (long)w * nd);
   __syncthreads();
   rs_tile_cursors(hw, nd, loc, wsum);
@@ -292,7 +301,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const int* __res
   const int* Tt = T + (long)t * nd;
   const int* Gg = G + (long)g * nd;
   for (int c = threadIdx.x; c < nd; c += RS_THREADS) gbase[c] = Gg[c] + Tt[c];
-  rs_rank_place(kr, vr, wa, wb, kb, shift, mask, hw + (long)w * nd, [&](int pos, int key, V val, int) {
+  rs_rank_place(kr, vr, wa, wb, kb, shift, mask, hw + (long)w * nd, [&](int pos, K key, V val, int) {
     lk[pos] = key;
     lv[pos] = val;
   });
@@ -300,8 +309,8 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const int* __res
   // out in tile-local sorted order: a digit's run of the tile is one contiguous global range
   const int len = (int)(b - a);
   for (int i = threadIdx.x; i < len; i += RS_THREADS) {
-    const int key = lk[i];
-    const int dg = ((key - kb) >> shift) & mask;
+    const K key = lk[i];
+    const int dg = rs_digit(key, kb, shift, mask);
     const int gp = gbase[dg] + (i - loc[dg]);
     if (kout != nullptr) kout[gp] = key;  // (the packed column-major copy carries no keys out)
     if constexpr (SPLIT) {
@@ -379,7 +388,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_csc_bucket_kernel(const int* __
     const long wb = wa + RS_SEG < b ? wa + RS_SEG : b;
     int kr[RS_PER_LANE];
     uint64_t vr[RS_PER_LANE];
-    rs_load_seg<uint64_t>(PACKED ? nullptr : kin, vin, wa, wb, kr, vr);
+    rs_load_seg<uint64_t, int>(PACKED ? nullptr : kin, vin, wa, wb, kr, vr);
     if constexpr (PACKED) {
 #pragma unroll
       for (int j = 0; j < RS_PER_LANE; ++j) kr[j] = (int)(vr[j] >> 22) & (CB_ND - 1);  // (kb = 0 below)
@@ -420,6 +429,7 @@ static int make_table(const long* bound, const int* kbase, int S, SegTable& tb) 
     nt += (int)tiles;
     ng += (int)((tiles + RS_TG - 1) / RS_TG);
   }
+  if (bound[S] - bound[0] >= (1L << 31) || bound[S] >= (1L << 31)) return -7;  // int32 output positions
   tb.bound[S] = bound[S];
   tb.tile0[S] = nt;
   tb.grp0[S] = ng;
@@ -454,7 +464,7 @@ int seg_sort(int* keys, V* vals, int* keys_alt, V* vals_alt, const long* bound, 
   for (int p = 0; p < passes; ++p) {
     const int shift = p * db;
     const int mask = nd - 1;
-    hipLaunchKernelGGL(rs_hist_kernel, dim3(tb.ntile), dim3(RS_THREADS), lds, st, kin, tb, shift, mask, T);
+    hipLaunchKernelGGL((rs_hist_kernel<int>), dim3(tb.ntile), dim3(RS_THREADS), lds, st, kin, tb, shift, mask, T);
     hipLaunchKernelGGL(rs_colscan_kernel, dim3((nd + 255) / 256, tb.ngrp), dim3(256), 0, st, T, tb, nd, G);
     hipLaunchKernelGGL(rs_base_kernel, dim3(tb.S), dim3(1024), 0, st, G, tb, nd);
     if (sizeof(V) == 8 && split_lo != nullptr && p == passes - 1)
@@ -475,7 +485,77 @@ int seg_sort(int* keys, V* vals, int* keys_alt, V* vals_alt, const long* bound, 
   return (passes & 1) ? 1 : 0;  // 1: the sorted pairs are in the _alt buffers
 }
 
+// Stable LSD sort of every segment by key bits [bit_lo, bit_hi) (kbase 0): balanced digits of at
+// most RS_MAX_DIGIT_BITS bits. 64-bit keys: the ordered bit images of fp64 scores / values, with
+// the constant bits (equal in every key) left out of the range by the caller. Returns 0 / 1 as
+// seg_sort (1: result in the _alt buffers).
+template <typename K, typename V>
+int sort_bits(K* keys, V* vals, K* keys_alt, V* vals_alt, const long* bound, int S, int bit_lo, int bit_hi,
+              int* scratch, long scratch_ints, hipStream_t st) {
+  SegTable tb{};
+  int kb0[RS_MAXS] = {0};
+  int rc = make_table(bound, kb0, S, tb);
+  if (rc) return rc;
+  const int nbits = bit_hi - bit_lo;
+  if (bit_lo < 0 || nbits < 1 || bit_hi > (int)(8 * sizeof(K))) return -5;
+  if (keys == nullptr || vals == nullptr || keys_alt == nullptr || vals_alt == nullptr) return -1;
+  const int passes = (nbits + RS_MAX_DIGIT_BITS - 1) / RS_MAX_DIGIT_BITS;
+  const int db = (nbits + passes - 1) / passes;
+  const int nd = 1 << db;
+  if (scratch_ints < (long)(tb.ntile + tb.ngrp) * nd) return -6;
+  if (tb.ntile == 0) return 0;
+  int* T = scratch;
+  int* G = scratch + (long)tb.ntile * nd;
+  const size_t lds = (size_t)RS_WAVES * nd * sizeof(int);
+  const size_t lds_sc = (size_t)(RS_WAVES + 2) * nd * sizeof(int) + (size_t)RS_TILE * (sizeof(K) + sizeof(V)) +
+                        RS_WAVES * sizeof(int);
+  K* kin = keys;
+  V* vin = vals;
+  K* kout = keys_alt;
+  V* vout = vals_alt;
+  for (int p = 0; p < passes; ++p) {
+    const int shift = bit_lo + p * db;
+    const int mask = nd - 1;
+    hipLaunchKernelGGL((rs_hist_kernel<K>), dim3(tb.ntile), dim3(RS_THREADS), lds, st, kin, tb, shift, mask, T);
+    hipLaunchKernelGGL(rs_colscan_kernel, dim3((nd + 255) / 256, tb.ngrp), dim3(256), 0, st, T, tb, nd, G);
+    hipLaunchKernelGGL(rs_base_kernel, dim3(tb.S), dim3(1024), 0, st, G, tb, nd);
+    hipLaunchKernelGGL((rs_scatter_kernel<V, false, K>), dim3(tb.ntile), dim3(RS_THREADS), lds_sc, st, kin, vin, kout,
+                       vout, T, G, tb, shift, mask, (int*)nullptr, (unsigned*)nullptr, 0L);
+    K* tk = kin;
+    kin = kout;
+    kout = tk;
+    V* tv = vin;
+    vin = vout;
+    vout = tv;
+  }
+  rc = (int)hipGetLastError();
+  if (rc) return rc;
+  return (passes & 1) ? 1 : 0;
+}
+
 }  // namespace
+
+// ints of scratch fmlx_sort_u64 needs for these segments and an nbits-wide key range
+FMLX_API long fmlx_sort_bits_scratch(const long* bound, int S, int nbits) {
+  if (S < 1 || S > RS_MAXS || nbits < 1 || nbits > 64) return -1;
+  long nt = 0, ng = 0;
+  for (int s = 0; s < S; ++s) {
+    const long tiles = (bound[s + 1] - bound[s] + RS_TILE - 1) / RS_TILE;
+    nt += tiles;
+    ng += (tiles + RS_TG - 1) / RS_TG;
+  }
+  const int passes = (nbits + RS_MAX_DIGIT_BITS - 1) / RS_MAX_DIGIT_BITS;
+  const int db = (nbits + passes - 1) / passes;
+  return (nt + ng) * (1L << db);
+}
+
+// Stable sort of (uint64 key, uint32 payload) pairs, segment by segment (`bound`: HOST array of
+// S + 1 positions), by key bits [bit_lo, bit_hi). 0: result in keys / vals; 1: in the _alt buffers.
+FMLX_API int fmlx_sort_u64(uint64_t* keys, uint32_t* vals, uint64_t* keys_alt, uint32_t* vals_alt, const long* bound,
+                           int S, int bit_lo, int bit_hi, int* scratch, long scratch_ints, void* stream) {
+  return sort_bits<uint64_t, uint32_t>(keys, vals, keys_alt, vals_alt, bound, S, bit_lo, bit_hi, scratch, scratch_ints,
+                                       (hipStream_t)stream);
+}
 
 // ints of scratch a sort of S segments with these bounds needs (digits of <= digit_bits bits)
 FMLX_API long fmlx_seg_sort_scratch(const long* bound, int S, int key_bits, int digit_bits) {
@@ -535,7 +615,7 @@ FMLX_API int fmlx_csc_sort_split(int* keys, uint64_t* vals, int* keys_alt, uint6
     const size_t lds = (size_t)RS_WAVES * ndA * sizeof(int);
     const size_t lds_sc = (size_t)(RS_WAVES + 2) * ndA * sizeof(int) + (size_t)RS_TILE * (sizeof(int) + 8) +
                           RS_WAVES * sizeof(int);
-    hipLaunchKernelGGL(rs_hist_kernel, dim3(tb.ntile), dim3(RS_THREADS), lds, st, keys, tb, 10, ndA - 1, T);
+    hipLaunchKernelGGL((rs_hist_kernel<int>), dim3(tb.ntile), dim3(RS_THREADS), lds, st, keys, tb, 10, ndA - 1, T);
     hipLaunchKernelGGL(rs_colscan_kernel, dim3((ndA + 255) / 256, tb.ngrp), dim3(256), 0, st, T, tb, ndA, G);
     hipLaunchKernelGGL(rs_base_kernel, dim3(tb.S), dim3(1024), 0, st, G, tb, ndA);
     hipLaunchKernelGGL((rs_scatter_kernel<uint64_t, false>), dim3(tb.ntile), dim3(RS_THREADS), lds_sc, st, keys, vals,
@@ -551,3 +631,5 @@ FMLX_API int fmlx_csc_sort_split(int* keys, uint64_t* vals, int* keys_alt, uint6
                        vals_alt, G, tb, ndA, d, b0, colptr, erow, evals, split_off);
   return (int)hipGetLastError();
 }
+
+FMLX_DEFINE_PRELOAD()

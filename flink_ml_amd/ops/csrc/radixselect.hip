@@ -122,3 +122,5 @@ FMLX_API int fmlx_radix_hist(int dtype, const void* X, long ld, long n, int d, c
                      out);
   return (int)hipGetLastError();
 }
+
+FMLX_DEFINE_PRELOAD()

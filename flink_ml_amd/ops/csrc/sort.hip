@@ -24,3 +24,5 @@ FMLX_API int fmlx_sorted_bounds(const int* keys, long n, int nbins, int* out, vo
                      (hipStream_t)stream, keys, n, nbins, out);
   return (int)hipGetLastError();
 }
+
+FMLX_DEFINE_PRELOAD()

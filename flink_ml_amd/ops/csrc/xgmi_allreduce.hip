@@ -230,3 +230,5 @@ FMLX_API int fmlx_xar_allreduce2(int dtype, void* const* peers_dev, int world, i
                        (const double*)src, (double*)dst, n, state);
   return (int)hipGetLastError();
 }
+
+FMLX_DEFINE_PRELOAD()

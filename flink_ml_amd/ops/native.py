@@ -26,6 +26,10 @@ from . import build as _build
 _LOCK = threading.Lock()
 _KLIB = None
 _HLIB = None
+# one-time cost of loading every code object of the kernel library at library load (host ms;
+# None: not done — no GPU, or FMLX_PRELOAD=0), and the number of code objects
+PRELOAD_MS = None
+PRELOAD_OBJECTS = 0
 
 DT_F32, DT_F64, DT_BF16, DT_F16, DT_I32, DT_I64 = 0, 1, 2, 3, 4, 5
 
@@ -147,8 +151,30 @@ def kernels():
             _build.check_fresh("kernels")  # never load a binary built from other sources
             lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
             _apply_sigs(lib, _KERNEL_SIGS)
+            _preload(lib)
             _KLIB = lib
     return _KLIB
+
+
+def _preload(lib) -> None:
+    """Loads every code object of the library now (one empty anchor-kernel launch per
+    translation unit, csrc/common.h FMLX_DEFINE_PRELOAD) instead of lazily inside the first fit
+    that launches one of its kernels; the one-time cost goes to PRELOAD_MS."""
+    global PRELOAD_MS, PRELOAD_OBJECTS
+    if os.environ.get("FMLX_PRELOAD", "1") == "0" or not torch.cuda.is_available():
+        return
+    import time
+
+    fn = getattr(lib, "fmlx_preload_all", None)
+    if fn is None:
+        return
+    fn.argtypes, fn.restype = [c_void_p], c_int
+    t0 = time.perf_counter()
+    k = fn(torch.cuda.current_stream().cuda_stream)
+    PRELOAD_MS = (time.perf_counter() - t0) * 1e3
+    if k < 0:
+        raise RuntimeError("preloading the kernel library's code objects failed (%d)" % k)
+    PRELOAD_OBJECTS = k
 
 
 def host():
