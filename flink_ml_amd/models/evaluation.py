@@ -169,9 +169,9 @@ def _device_metrics(score: torch.Tensor, pos: torch.Tensor, w: torch.Tensor, dis
         tot_t = sum(x[0] for x in summ)
         tot_f = sum(x[1] for x in summ)
     total = tot_t + tot_f
-    keys, rows = sorting.sort_scores_desc(score)
+    keys, rows = sorting.sort_scores_desc(score, pos)
     unit = bool((w == 1).all()) if n else True
-    m = sorting.binary_metrics(keys, rows, pos, None if unit else w, before_t, before_f, tot_t, tot_f)
+    m = sorting.binary_metrics(keys, rows, None if unit else w, before_t, before_f, tot_t, tot_f)
     # Σ_g avg_rank_g·PW_g with avg_rank = total − before − (gs + ge)/2 (local positions gs..ge)
     sums = torch.stack([(total - before_t - before_f) * m[1] - 0.5 * m[0], m[1], m[2], m[3], m[4]])
     ks = m[5]

@@ -206,7 +206,7 @@ def _label_value_counts_device(X: torch.Tensor, li: torch.Tensor, L: int, dist: 
         slots = [np.nonzero(present[j])[0] for j in range(d)]
         return counts, [(sl + vmin).astype(np.float64) for sl in slots], slots, n_lab.cpu().numpy()
     if dist:
-        vals_t, flat, Vn = value_label_counts(X, li, L)
+        vals_t, flat, Vn = value_label_counts(X.to(torch.float64), li, L)
         Vmax = max(1, int(Vn.max()) if d else 1)
         counts = np.zeros((d, L, Vmax), dtype=np.float64)
         off = 0
@@ -233,7 +233,8 @@ class NaiveBayes(Estimator, NaiveBayesParams):
         fc = t.column(self.get(self.FEATURES_COL))
         if isinstance(fc, list) and len({v.size() for v in fc}) > 1:
             raise ValueError("Feature vectors should be of equal length.")
-        X, y = features_and_labels(t, self.get(self.FEATURES_COL), self.get(self.LABEL_COL))
+        # on the GPU the stored dtype stays (the contingency kernels read f32 or f64 themselves)
+        X, y = features_and_labels(t, self.get(self.FEATURES_COL), self.get(self.LABEL_COL), keep_dtype=True)
         if bool((y != torch.round(y)).any()):
             raise ValueError("Label value should be indexed number.")
         s = self.get(self.SMOOTHING)

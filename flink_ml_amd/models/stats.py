@@ -215,13 +215,13 @@ class ChiSqTest(AlgoOperator, _TestParams):
     JAVA_CLASS_NAME = "org.apache.flink.ml.stats.chisqtest.ChiSqTest"
 
     def compute(self, t: Table):
-        X, y = features_and_labels(t, self.get(self.FEATURES_COL), self.get(self.LABEL_COL))
+        X, y = features_and_labels(t, self.get(self.FEATURES_COL), self.get(self.LABEL_COL), keep_dtype=True)
         labels = global_sorted_unique(y)
         L, d = labels.numel(), X.shape[1]
         li = torch.searchsorted(labels, y)
         if get_world_distributed():
             # distinct values and contingency counts in one keyed shuffle (no value lists pickled)
-            vals, flat, _ = value_label_counts(X, li, L)
+            vals, flat, _ = value_label_counts(X.to(torch.float64), li, L)
         elif X.is_cuda:
             # native contingency tables (ops/catstats.py: integer table or sorted-column distinct)
             from ..ops import catstats

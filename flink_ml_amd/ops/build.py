@@ -120,7 +120,10 @@ def _run(cmd):
 # every accumulator with VALU ops each tile, and the AGPR form adds a v_accvgpr_read per value.
 FILE_FLAGS = {"kmeans.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-Wno-inline-asm"],
               # the fused round's ticket atomics: no lane-0 result fix-up (keeps counted vmcnt waits)
-              "glm.hip": ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]}
+              "glm.hip": ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"],
+              # MFMA accumulators in arch VGPRs: the AGPR form rotated the DCT's accumulators
+              # through VGPRs every k step
+              "dct.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
 def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:

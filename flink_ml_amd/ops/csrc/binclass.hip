@@ -43,7 +43,12 @@ __device__ __forceinline__ uint64_t desc_key(double s) {
 
 __device__ __forceinline__ bool new_group(uint64_t prev, uint64_t cur) { return cur != prev || cur == NAN_KEY; }
 
-__global__ __launch_bounds__(BC_THREADS) void bc_keys_kernel(const double* __restrict__ score, long n,
+// payload of a row: its id in bits 0..30, its label (1 = positive) in bit 31 — the scans then read
+// the label from the sorted payload instead of gathering it by row id
+constexpr uint32_t POS_BIT = 0x80000000u;
+
+__global__ __launch_bounds__(BC_THREADS) void bc_keys_kernel(const double* __restrict__ score,
+                                                             const uint8_t* __restrict__ pos, long n,
                                                              uint64_t* __restrict__ keys, uint32_t* __restrict__ idx,
                                                              unsigned long long* __restrict__ orand) {
   __shared__ unsigned long long s_or[BC_WAVES], s_and[BC_WAVES];
@@ -51,7 +56,7 @@ __global__ __launch_bounds__(BC_THREADS) void bc_keys_kernel(const double* __res
   for (long i = (long)blockIdx.x * BC_THREADS + threadIdx.x; i < n; i += (long)gridDim.x * BC_THREADS) {
     const uint64_t k = desc_key(score[i]);
     keys[i] = k;
-    idx[i] = (uint32_t)i;
+    idx[i] = (uint32_t)i | (pos[i] ? POS_BIT : 0u);
     o |= k;
     a &= k;
   }
@@ -131,25 +136,68 @@ __device__ __forceinline__ void thread_rows(long n, long& r0, int& cnt) {
   cnt = rem <= 0 ? 0 : (rem < BC_PER ? (int)rem : BC_PER);
 }
 
+// the thread's (up to) BC_PER consecutive sorted keys and payloads: 16-byte loads (the 64 lanes'
+// 128-byte runs are whole lines, reused from L1 by the following loads)
+__device__ __forceinline__ void load_rows(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ idx,
+                                          long r0, int cnt, uint64_t (&k)[BC_PER], uint32_t (&p)[BC_PER]) {
+  if (cnt == BC_PER) {
+#pragma unroll
+    for (int j = 0; j < BC_PER; j += 2) {
+      const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(keys + r0 + j);
+      k[j] = v.x;
+      k[j + 1] = v.y;
+    }
+#pragma unroll
+    for (int j = 0; j < BC_PER; j += 4) {
+      const uint4 v = *reinterpret_cast<const uint4*>(idx + r0 + j);
+      p[j] = v.x;
+      p[j + 1] = v.y;
+      p[j + 2] = v.z;
+      p[j + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < BC_PER; ++j) {
+      k[j] = j < cnt ? keys[r0 + j] : 0;
+      p[j] = j < cnt ? idx[r0 + j] : 0;
+    }
+  }
+}
+
 // agg[t] = {#pos, #neg, last head, first tail} of tile t (head/tail: −1 / n when none)
 __global__ __launch_bounds__(BC_THREADS) void bc_agg_kernel(const uint64_t* __restrict__ keys,
-                                                            const uint32_t* __restrict__ idx,
-                                                            const uint8_t* __restrict__ pos, long n,
+                                                            const uint32_t* __restrict__ idx, long n,
                                                             long* __restrict__ agg) {
   __shared__ long sh[2 * BC_WAVES];
+  __shared__ long sh2[2 * BC_WAVES];
   long r0;
   int cnt;
   thread_rows(n, r0, cnt);
+  uint64_t k[BC_PER];
+  uint32_t pl[BC_PER];
+  load_rows(keys, idx, r0, cnt, k, pl);
+  const uint64_t kprev = (cnt > 0 && r0 > 0) ? keys[r0 - 1] : 0;
+  const uint64_t knext = (cnt > 0 && r0 + cnt < n) ? keys[r0 + cnt] : 0;
   int np = 0, nn = 0;
   long head = -1, tail = n;
-  for (int j = 0; j < cnt; ++j) {
-    const long r = r0 + j;
-    const uint64_t k = keys[r];
-    const bool p = pos[idx[r]] != 0;
-    np += p;
-    nn += !p;
-    if (r == 0 || new_group(keys[r - 1], k)) head = r;
-    if (tail == n && (r == n - 1 || new_group(k, keys[r + 1]))) tail = r;
+#pragma unroll
+  for (int j = 0; j < BC_PER; ++j) {
+    if (j < cnt) {
+      const long r = r0 + j;
+      const bool p = (pl[j] & POS_BIT) != 0;
+      np += p;
+      nn += !p;
+      const uint64_t pk = j == 0 ? kprev : k[j - 1];
+      if (r == 0 || new_group(pk, k[j])) head = r;
+    }
+  }
+#pragma unroll
+  for (int j = BC_PER - 1; j >= 0; --j) {
+    if (j < cnt) {
+      const long r = r0 + j;
+      const uint64_t nk = j + 1 < cnt ? k[j + 1] : knext;
+      if (r == n - 1 || new_group(k[j], nk)) tail = r;
+    }
   }
   // block reductions: sums (ints), max head, min tail
   long a = np, b = nn;
@@ -160,7 +208,6 @@ __global__ __launch_bounds__(BC_THREADS) void bc_agg_kernel(const uint64_t* __re
     head = h > head ? h : head;
     tail = t < tail ? t : tail;
   }
-  __shared__ long sh2[2 * BC_WAVES];
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
     sh[w] = a;
@@ -184,69 +231,83 @@ __global__ __launch_bounds__(BC_THREADS) void bc_agg_kernel(const uint64_t* __re
   }
 }
 
-// one block: carry[t] = {#pos before t, #neg before t, max head before t, min tail after t}
+// one block of 1024: carry[t] = {#pos before t, #neg before t, max head before t, min tail after t},
+// chunks of 1024 tiles with block scans (forward for the first three, backward for the tails)
 __global__ __launch_bounds__(1024) void bc_carry_kernel(const long* __restrict__ agg, long nt,
                                                         long* __restrict__ carry) {
-  // sequential over chunks of 1024 tiles (nt is small: n / 4096), one thread per tile
-  __shared__ long s[4][1024];
+  __shared__ long wsum[3][16];
   __shared__ long run[3];
+  __shared__ long runmin;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (threadIdx.x == 0) {
     run[0] = 0;
     run[1] = 0;
     run[2] = -1;
+    runmin = 0x7fffffffffffffffL;
   }
   __syncthreads();
   for (long base = 0; base < nt; base += 1024) {
     const long t = base + threadIdx.x;
     const bool ok = t < nt;
-    s[0][threadIdx.x] = ok ? agg[t * 4 + 0] : 0;
-    s[1][threadIdx.x] = ok ? agg[t * 4 + 1] : 0;
-    s[2][threadIdx.x] = ok ? agg[t * 4 + 2] : -1;
-    __syncthreads();
-    if (threadIdx.x == 0) {  // 1024 serial steps per chunk: microseconds for any realistic nt
-      long a = run[0], b = run[1], h = run[2];
-      const long m = nt - base < 1024 ? nt - base : 1024;
-      for (long i = 0; i < m; ++i) {
-        const long va = s[0][i], vb = s[1][i], vh = s[2][i];
-        s[0][i] = a;
-        s[1][i] = b;
-        s[2][i] = h;
-        a += va;
-        b += vb;
-        h = vh > h ? vh : h;
+    long a = ok ? agg[t * 4 + 0] : 0, b = ok ? agg[t * 4 + 1] : 0, h = ok ? agg[t * 4 + 2] : -1;
+    long ia = a, ib = b, ih = h;  // inclusive wave scans
+    for (int off = 1; off < 64; off <<= 1) {
+      const long oa = __shfl_up(ia, off, 64), ob = __shfl_up(ib, off, 64), oh = __shfl_up(ih, off, 64);
+      if (lane >= off) {
+        ia += oa;
+        ib += ob;
+        ih = oh > ih ? oh : ih;
       }
-      run[0] = a;
-      run[1] = b;
-      run[2] = h;
+    }
+    if (lane == 63) {
+      wsum[0][w] = ia;
+      wsum[1][w] = ib;
+      wsum[2][w] = ih;
     }
     __syncthreads();
+    long pa = run[0], pb = run[1], ph = run[2];
+    for (int q = 0; q < w; ++q) {
+      pa += wsum[0][q];
+      pb += wsum[1][q];
+      ph = wsum[2][q] > ph ? wsum[2][q] : ph;
+    }
+    const long ea = pa + ia - a, eb = pb + ib - b;  // exclusive
+    long eh = __shfl_up(ih, 1, 64);
+    if (lane == 0) eh = -1;
+    eh = eh > ph ? eh : ph;
     if (ok) {
-      carry[t * 4 + 0] = s[0][threadIdx.x];
-      carry[t * 4 + 1] = s[1][threadIdx.x];
-      carry[t * 4 + 2] = s[2][threadIdx.x];
+      carry[t * 4 + 0] = ea;
+      carry[t * 4 + 1] = eb;
+      carry[t * 4 + 2] = eh;
+    }
+    __syncthreads();
+    if (threadIdx.x == 1023) {
+      run[0] = ea + a;
+      run[1] = eb + b;
+      run[2] = (h > eh ? h : eh);
     }
     __syncthreads();
   }
-  // suffix min of the tails, from the last chunk backwards (none after the last tile)
-  __shared__ long runmin;
-  if (threadIdx.x == 0) runmin = 0x7fffffffffffffffL;
-  __syncthreads();
   for (long top = nt; top > 0; top -= 1024) {
     const long base = top > 1024 ? top - 1024 : 0;
-    const long m = top - base;
-    if ((long)threadIdx.x < m) s[3][threadIdx.x] = agg[(base + threadIdx.x) * 4 + 3];
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      long tmin = runmin;
-      for (long i = m - 1; i >= 0; --i) {
-        const long v = s[3][i];
-        s[3][i] = tmin;
-        tmin = v < tmin ? v : tmin;
-      }
-      runmin = tmin;
+    const long t = base + threadIdx.x;
+    const bool ok = t < top;
+    const long v = ok ? agg[t * 4 + 3] : 0x7fffffffffffffffL;
+    long iv = v;  // inclusive suffix min within the wave
+    for (int off = 1; off < 64; off <<= 1) {
+      const long o = __shfl_down(iv, off, 64);
+      if (lane + off < 64) iv = o < iv ? o : iv;
     }
+    if (lane == 0) wsum[0][w] = iv;
     __syncthreads();
-    if ((long)threadIdx.x < m) carry[(base + threadIdx.x) * 4 + 3] = s[3][threadIdx.x];
+    long sm = runmin;
+    for (int q = 15; q > w; --q) sm = wsum[0][q] < sm ? wsum[0][q] : sm;
+    long ev = __shfl_down(iv, 1, 64);
+    if (lane == 63) ev = 0x7fffffffffffffffL;
+    ev = ev < sm ? ev : sm;
+    if (ok) carry[t * 4 + 3] = ev;
+    __syncthreads();
+    if (threadIdx.x == 0) runmin = v < ev ? v : ev;
     __syncthreads();
   }
 }
@@ -265,7 +326,6 @@ __device__ __forceinline__ void rates(double a, double b, const Totals& T, doubl
 
 __global__ __launch_bounds__(BC_THREADS) void bc_metrics_kernel(const uint64_t* __restrict__ keys,
                                                                 const uint32_t* __restrict__ idx,
-                                                                const uint8_t* __restrict__ pos,
                                                                 const double* __restrict__ wt, long n,
                                                                 const long* __restrict__ carry, Totals T,
                                                                 double* __restrict__ part) {
@@ -280,21 +340,14 @@ __global__ __launch_bounds__(BC_THREADS) void bc_metrics_kernel(const uint64_t* 
   int np = 0, nn = 0;
   long head = -1, tail = 0x7fffffffffffffffL;
   uint64_t k[BC_PER];
+  uint32_t pl[BC_PER];
   bool p[BC_PER];
   double w[BC_PER];
+  load_rows(keys, idx, r0, cnt, k, pl);
 #pragma unroll
   for (int j = 0; j < BC_PER; ++j) {
-    const long r = r0 + j;
-    if (j < cnt) {
-      k[j] = keys[r];
-      const uint32_t id = idx[r];
-      p[j] = pos[id] != 0;
-      w[j] = wt != nullptr ? wt[id] : 1.0;
-    } else {
-      k[j] = 0;
-      p[j] = false;
-      w[j] = 0.0;
-    }
+    p[j] = j < cnt && (pl[j] & POS_BIT) != 0;
+    w[j] = j >= cnt ? 0.0 : (wt != nullptr ? wt[pl[j] & ~POS_BIT] : 1.0);
   }
   const uint64_t kprev = (cnt > 0 && r0 > 0) ? keys[r0 - 1] : 0;
   const uint64_t knext = (cnt > 0 && r0 + cnt < n) ? keys[r0 + cnt] : 0;
@@ -408,22 +461,23 @@ __global__ __launch_bounds__(64) void bc_final_kernel(const double* __restrict__
 
 FMLX_API int fmlx_bc_tile() { return BC_TILE; }
 
-// keys[i] / idx[i] for the sort; orand = {OR, AND} of all keys (device; the caller zero / ~0 fills)
-FMLX_API int fmlx_bc_keys(const double* score, long n, uint64_t* keys, uint32_t* idx, unsigned long long* orand,
-                          void* stream) {
+// keys[i] / payloads (row | label << 31) for the sort; orand = {OR, AND} of all keys (device; the
+// caller fills {0, ~0}); n < 2^31
+FMLX_API int fmlx_bc_keys(const double* score, const uint8_t* pos, long n, uint64_t* keys, uint32_t* idx,
+                          unsigned long long* orand, void* stream) {
   if (n <= 0) return 0;
-  if (n >= (1L << 32)) return -2;
+  if (n >= (1L << 31)) return -2;
   long blocks = (n + BC_THREADS * 8 - 1) / (BC_THREADS * 8);
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(bc_keys_kernel, dim3((unsigned)blocks), dim3(BC_THREADS), 0, (hipStream_t)stream, score, n, keys,
-                     idx, orand);
+  hipLaunchKernelGGL(bc_keys_kernel, dim3((unsigned)blocks), dim3(BC_THREADS), 0, (hipStream_t)stream, score, pos, n,
+                     keys, idx, orand);
   return (int)hipGetLastError();
 }
 
-// Metrics of the sorted rows (keys / idx in sorted order; pos / wt by original row, wt may be
-// null). scratch: int64[8 · tiles], part: double[6 · tiles] with tiles = ceil(n / fmlx_bc_tile()).
+// Metrics of the sorted rows (keys / payloads in sorted order, the payload carrying row id and
+// label; wt by original row, may be null). scratch: int64[8 · tiles], part: double[6 · tiles] with tiles = ceil(n / fmlx_bc_tile()).
 // out[6] = {Σ_pos w·(gs + ge), Σ_pos w, Σ_neg w, lorenz, pr, ks} (gs / ge: local sorted positions).
-FMLX_API int fmlx_bc_metrics(const uint64_t* keys, const uint32_t* idx, const uint8_t* pos, const double* wt, long n,
+FMLX_API int fmlx_bc_metrics(const uint64_t* keys, const uint32_t* idx, const double* wt, long n,
                              double before_t, double before_f, double tot_t, double tot_f, long* scratch,
                              double* part, double* out, void* stream) {
   hipStream_t s = (hipStream_t)stream;
@@ -434,10 +488,10 @@ FMLX_API int fmlx_bc_metrics(const uint64_t* keys, const uint32_t* idx, const ui
   }
   long* agg = scratch;
   long* carry = scratch + nt * 4;
-  hipLaunchKernelGGL(bc_agg_kernel, dim3((unsigned)nt), dim3(BC_THREADS), 0, s, keys, idx, pos, n, agg);
+  hipLaunchKernelGGL(bc_agg_kernel, dim3((unsigned)nt), dim3(BC_THREADS), 0, s, keys, idx, n, agg);
   hipLaunchKernelGGL(bc_carry_kernel, dim3(1), dim3(1024), 0, s, agg, nt, carry);
   Totals T{before_t, before_f, tot_t, tot_f};
-  hipLaunchKernelGGL(bc_metrics_kernel, dim3((unsigned)nt), dim3(BC_THREADS), 0, s, keys, idx, pos, wt, n, carry, T,
+  hipLaunchKernelGGL(bc_metrics_kernel, dim3((unsigned)nt), dim3(BC_THREADS), 0, s, keys, idx, wt, n, carry, T,
                      part);
   hipLaunchKernelGGL(bc_final_kernel, dim3(1), dim3(64), 0, s, part, nt, out);
   return (int)hipGetLastError();

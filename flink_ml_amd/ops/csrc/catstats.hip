@@ -29,26 +29,86 @@ constexpr int CS_LDS_INTS = 32 * 1024;  // privatised table: 128 KiB of LDS (one
 constexpr int CS_PER = 16;
 constexpr int CS_TILE = CS_THREADS * CS_PER;
 
+// Grid-stride walk over the row-major elements of an [n, d] matrix as (row, column) pairs: one
+// 64-bit division at the start, then a constant (row, column) step with a carry — the flat index
+// e / d of every element cost a 64-bit integer division each (~1.6 ms of 2M × 100).
+struct FlatWalk {
+  long i;
+  int j;
+  long di;
+  int dj, d;
+  __device__ FlatWalk(long n, int d_, long start, long stride) : d(d_) {
+    i = start / d_;
+    j = (int)(start - i * d_);
+    di = stride / d_;
+    dj = (int)(stride - di * d_);
+    (void)n;
+  }
+  __device__ __forceinline__ void next() {
+    i += di;
+    j += dj;
+    if (j >= d) {
+      j -= d;
+      ++i;
+    }
+  }
+};
+
 template <typename T>
 __device__ __forceinline__ double ld_val(const T* X, long ld, long i, int j) {
   return (double)X[i * ld + j];
 }
 
-// part[b] = {min, max, nonint} over the block's elements (row-major flat index over n × d)
+// 16 bytes of T: 4 floats or 2 doubles, loaded with one instruction
+template <typename T>
+struct Vec16 {
+  static constexpr int N = 16 / sizeof(T);
+  T v[N];
+};
+template <typename T>
+__device__ __forceinline__ Vec16<T> ld16(const T* p) {
+  Vec16<T> r;
+  *reinterpret_cast<uint4*>(r.v) = *reinterpret_cast<const uint4*>(p);
+  return r;
+}
+
+__device__ __forceinline__ void flag_one(double v, double& mn, double& mx, double& non) {
+  mn = v < mn ? v : mn;
+  mx = v > mx ? v : mx;
+  if (v != rint(v) || v - v != 0.0) non = 1.0;  // fractions, NaN (v != v), ±inf (inf − inf = NaN)
+}
+
+// part[b] = {min, max, nonint} over the block's elements. Contiguous rows (ld == d, 16-byte
+// aligned): one flat stream of 16-byte loads, UNR of them in flight per thread; otherwise a
+// (row, column) walk.
 template <typename T>
 __global__ __launch_bounds__(CS_THREADS) void cs_flags_kernel(const T* __restrict__ X, long ld, long n, int d,
                                                               double* __restrict__ part) {
   __shared__ double smin[CS_WAVES], smax[CS_WAVES], snon[CS_WAVES];
   double mn = __builtin_inf(), mx = -__builtin_inf(), non = 0.0;
-  const long total = n * (long)d;
-  for (long e = (long)blockIdx.x * CS_THREADS + threadIdx.x; e < total; e += (long)gridDim.x * CS_THREADS) {
-    const long i = e / d;
-    const int j = (int)(e - i * d);
-    const double v = ld_val(X, ld, i, j);
-    mn = v < mn ? v : mn;
-    mx = v > mx ? v : mx;
-    if (v != rint(v)) non = 1.0;  // NaN / ±inf (rint(inf) == inf: counted below) / fractions
-    if (v - v != 0.0) non = 1.0;  // inf or NaN
+  const long gt = (long)blockIdx.x * CS_THREADS + threadIdx.x, gs = (long)gridDim.x * CS_THREADS;
+  if (ld == d && (((uintptr_t)X) & 15) == 0) {
+    constexpr int VN = Vec16<T>::N, UNR = 4;
+    const long total = n * (long)d, nv = total / VN;
+    long v = gt;
+    for (; v + (UNR - 1) * gs < nv; v += UNR * gs) {
+      Vec16<T> q[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) q[u] = ld16(X + (v + u * gs) * VN);
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+#pragma unroll
+        for (int c = 0; c < VN; ++c) flag_one((double)q[u].v[c], mn, mx, non);
+    }
+    for (; v < nv; v += gs) {
+      const Vec16<T> q = ld16(X + v * VN);
+#pragma unroll
+      for (int c = 0; c < VN; ++c) flag_one((double)q.v[c], mn, mx, non);
+    }
+    for (long e = nv * VN + gt; e < total; e += gs) flag_one((double)X[e], mn, mx, non);
+  } else {
+    FlatWalk it(n, d, gt, gs);
+    for (; it.i < n; it.next()) flag_one(ld_val(X, ld, it.i, it.j), mn, mx, non);
   }
   for (int off = 32; off > 0; off >>= 1) {
     const double a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64), c = __shfl_xor(non, off, 64);
@@ -120,35 +180,86 @@ __global__ __launch_bounds__(CS_THREADS) void cs_ihist_kernel(const T* __restric
       if (h[i]) atomicAdd(&counts[i], h[i]);
 }
 
-// counts[(j·L + li[i])·V + (x − vmin)] over every element (li outside [0, L): row skipped)
-template <typename T>
+// counts[(j·L + li[i])·V + (x − vmin)] over every element (li outside [0, L): row skipped).
+// Privatised: the block's table lives in LDS with feature j's L·V cells at j·FS, FS = L·V rounded up
+// to an odd count, so the 64 lanes of a wave — 64 consecutive elements, i.e. consecutive features —
+// hit 64 different banks (an even stride put them on stride·j mod 64: 8 banks at L·V = 200).
+// Contiguous rows (ld == d): 16-byte loads of the flat element stream, UNR in flight per thread,
+// row = e / d by a 64-bit multiply-high with the host's magic ceil(2^64 / d) (exact for e < 2^32).
+template <typename T, bool PRIV>
 __global__ __launch_bounds__(CS_THREADS) void cs_hist_kernel(const T* __restrict__ X, long ld, long n, int d,
                                                              const int* __restrict__ li, int L, long vmin, int V,
-                                                             int* __restrict__ counts) {
+                                                             int* __restrict__ counts, uint64_t magic, int FS) {
   extern __shared__ int h[];
-  const long tsize = (long)d * L * V;
-  const bool priv = tsize <= CS_LDS_INTS;
-  if (priv)
+  const long tsize = (long)d * FS;
+  if (PRIV)
     for (long i = threadIdx.x; i < tsize; i += CS_THREADS) h[i] = 0;
   __syncthreads();
-  const long total = n * (long)d;
-  for (long e = (long)blockIdx.x * CS_THREADS + threadIdx.x; e < total; e += (long)gridDim.x * CS_THREADS) {
-    const long i = e / d;
-    const int j = (int)(e - i * d);
+  const long LV = (long)L * V;
+  auto add = [&](long i, int j, double x) {
     const int l = li[i];
-    const long v = (long)ld_val(X, ld, i, j) - vmin;
+    const long v = (long)x - vmin;
     if (l >= 0 && l < L && v >= 0 && v < V) {
-      const long slot = ((long)j * L + l) * V + v;
-      if (priv)
-        atomicAdd(&h[slot], 1);
+      if (PRIV)
+        atomicAdd(&h[(long)j * FS + (long)l * V + v], 1);
       else
-        atomicAdd(&counts[slot], 1);
+        atomicAdd(&counts[(long)j * LV + (long)l * V + v], 1);
     }
+  };
+  const long gt = (long)blockIdx.x * CS_THREADS + threadIdx.x, gs = (long)gridDim.x * CS_THREADS;
+  const long total = n * (long)d;
+  if (ld == d && (((uintptr_t)X) & 15) == 0 && total < (1L << 32) && d >= Vec16<T>::N) {
+    constexpr int VN = Vec16<T>::N, UNR = 4;
+    const long nv = total / VN;
+    auto row_of = [&](long e) -> long { return d == 1 ? e : (long)__umul64hi((uint64_t)e, magic); };
+    long v = gt;
+    for (; v + (UNR - 1) * gs < nv; v += UNR * gs) {
+      Vec16<T> q[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) q[u] = ld16(X + (v + u * gs) * VN);
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const long e = (v + u * gs) * VN;
+        long i = row_of(e);
+        int j = (int)(e - i * d);
+#pragma unroll
+        for (int c = 0; c < VN; ++c) {
+          add(i, j, (double)q[u].v[c]);
+          if (++j == d) {
+            j = 0;
+            ++i;
+          }
+        }
+      }
+    }
+    for (; v < nv; v += gs) {
+      const Vec16<T> q = ld16(X + v * VN);
+      const long e = v * VN;
+      long i = row_of(e);
+      int j = (int)(e - i * d);
+#pragma unroll
+      for (int c = 0; c < VN; ++c) {
+        add(i, j, (double)q.v[c]);
+        if (++j == d) {
+          j = 0;
+          ++i;
+        }
+      }
+    }
+    for (long e = nv * VN + gt; e < total; e += gs) {
+      const long i = row_of(e);
+      add(i, (int)(e - i * d), (double)X[e]);
+    }
+  } else {
+    FlatWalk it(n, d, gt, gs);
+    for (; it.i < n; it.next()) add(it.i, it.j, ld_val(X, ld, it.i, it.j));
   }
   __syncthreads();
-  if (priv)
-    for (long i = threadIdx.x; i < tsize; i += CS_THREADS)
-      if (h[i]) atomicAdd(&counts[i], h[i]);
+  if (PRIV)
+    for (long i = threadIdx.x; i < tsize; i += CS_THREADS) {
+      const int j = (int)(i / FS), r = (int)(i - (long)j * FS);
+      if (r < LV && h[i]) atomicAdd(&counts[(long)j * LV + r], h[i]);
+    }
 }
 
 // ---- general values: ordered keys of columns [j0, j0 + nc), sorted per column ----------------
@@ -381,18 +492,26 @@ FMLX_API int fmlx_cs_hist(int dtype, const void* X, long ld, long n, int d, cons
                           int* counts, void* stream) {
   if (L < 1 || V < 1 || d < 1) return -2;
   hipStream_t s = (hipStream_t)stream;
-  const long tsize = (long)d * L * V;
-  const size_t lds = tsize <= CS_LDS_INTS ? (size_t)tsize * sizeof(int) : 0;
+  const long LV = (long)L * V;
+  const int FS = (int)(LV | 1);  // odd feature stride in LDS
+  const long tsize = (long)d * FS;
+  const bool priv = tsize <= CS_LDS_INTS;
+  const size_t lds = priv ? (size_t)tsize * sizeof(int) : 0;
+  // ceil(2^64 / d): row = umulhi(e, magic) for e < 2^32 (d = 1 handled in the kernel)
+  const uint64_t magic = d > 1 ? (uint64_t)((((unsigned __int128)1) << 64) / (unsigned)d) + 1 : 0;
   // privatised: enough blocks to fill the chip, each amortising its table over many elements
-  const unsigned nb = grid_for(n * (long)d, CS_THREADS * 64L, lds ? 512 : 4096);
-  if (dtype == DT_F64)
-    hipLaunchKernelGGL(cs_hist_kernel<double>, dim3(nb), dim3(CS_THREADS), lds, s, (const double*)X, ld, n, d, li, L,
-                       vmin, V, counts);
-  else if (dtype == DT_F32)
-    hipLaunchKernelGGL(cs_hist_kernel<float>, dim3(nb), dim3(CS_THREADS), lds, s, (const float*)X, ld, n, d, li, L,
-                       vmin, V, counts);
-  else
+  const unsigned nb = grid_for(n * (long)d, CS_THREADS * 64L, priv ? 512 : 4096);
+#define FMLX_CS_HIST(T, P)                                                                                    \
+  hipLaunchKernelGGL((cs_hist_kernel<T, P>), dim3(nb), dim3(CS_THREADS), lds, s, (const T*)X, ld, n, d, li, L, \
+                     vmin, V, counts, magic, FS)
+  if (dtype == DT_F64) {
+    if (priv) FMLX_CS_HIST(double, true); else FMLX_CS_HIST(double, false);
+  } else if (dtype == DT_F32) {
+    if (priv) FMLX_CS_HIST(float, true); else FMLX_CS_HIST(float, false);
+  } else {
     return -1;
+  }
+#undef FMLX_CS_HIST
   return (int)hipGetLastError();
 }
 

@@ -17,8 +17,8 @@ native.register_kernel_sigs({
     "fmlx_sort_u64": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_long,
                       c_void_p],
     "fmlx_bc_tile": [],
-    "fmlx_bc_keys": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_void_p],
-    "fmlx_bc_metrics": [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_double, c_double, c_double, c_double,
+    "fmlx_bc_keys": [c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_void_p],
+    "fmlx_bc_metrics": [c_void_p, c_void_p, c_void_p, c_long, c_double, c_double, c_double, c_double,
                         c_void_p, c_void_p, c_void_p, c_void_p],
 })
 
@@ -58,23 +58,31 @@ def sort_u64(keys: torch.Tensor, vals: torch.Tensor, bounds: Sequence[int], bit_
     return (ka, va) if rc == 1 else (keys, vals)
 
 
-def sort_scores_desc(score: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    """(keys, rows) of fp64 ``score`` in descending order (Double.compare of −score: NaN last, −0
-    tied with +0), stable: equal scores keep their row order."""
+def _u8(pos: torch.Tensor) -> torch.Tensor:
+    return pos.contiguous().view(torch.uint8) if pos.dtype == torch.bool else pos.to(torch.uint8).contiguous()
+
+
+def sort_scores_desc(score: torch.Tensor, pos: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(keys, payloads) of fp64 ``score`` in descending order (Double.compare of −score: NaN last,
+    −0 tied with +0), stable: equal scores keep their row order. Payload = row id | label << 31
+    (``pos``: the rows' labels, bool)."""
     n = score.numel()
     dev = score.device
+    if n >= 1 << 31:
+        raise ValueError("at most 2^31 - 1 rows per rank")
     keys = torch.empty(n, dtype=U64, device=dev)
     rows = torch.empty(n, dtype=torch.int32, device=dev)
     orand = torch.tensor([0, -1], dtype=U64, device=dev)
-    native.call("fmlx_bc_keys", native.ptr(score), n, native.ptr(keys), native.ptr(rows), native.ptr(orand),
-                native.stream_ptr(dev))
+    native.call("fmlx_bc_keys", native.ptr(score), native.ptr(_u8(pos)), n, native.ptr(keys), native.ptr(rows),
+                native.ptr(orand), native.stream_ptr(dev))
     lo, hi = bit_range(orand)
     return sort_u64(keys, rows, [0, n], lo, hi)
 
 
-def binary_metrics(keys: torch.Tensor, rows: torch.Tensor, pos: torch.Tensor, w, before_t: float, before_f: float,
+def binary_metrics(keys: torch.Tensor, rows: torch.Tensor, w, before_t: float, before_f: float,
                    tot_t: float, tot_f: float) -> torch.Tensor:
-    """[Σ_pos w·(gs + ge), Σ_pos w, Σ_neg w, lorenz, pr, ks] over the sorted rows (fp64, device)."""
+    """[Σ_pos w·(gs + ge), Σ_pos w, Σ_neg w, lorenz, pr, ks] over the sorted rows (fp64, device);
+    ``rows``: the payloads of ``sort_scores_desc``; ``w``: weights by original row, or None."""
     n = keys.numel()
     dev = keys.device
     tile = int(native.kernels().fmlx_bc_tile())
@@ -82,9 +90,8 @@ def binary_metrics(keys: torch.Tensor, rows: torch.Tensor, pos: torch.Tensor, w,
     scratch = torch.empty(8 * nt, dtype=torch.int64, device=dev)
     part = torch.empty(6 * nt, dtype=torch.float64, device=dev)
     out = torch.empty(6, dtype=torch.float64, device=dev)
-    pos_u8 = pos.contiguous().view(torch.uint8) if pos.dtype == torch.bool else pos.to(torch.uint8).contiguous()
     w = None if w is None else w.to(torch.float64).contiguous()
-    native.call("fmlx_bc_metrics", native.ptr(keys), native.ptr(rows), native.ptr(pos_u8), native.ptr(w), n,
+    native.call("fmlx_bc_metrics", native.ptr(keys), native.ptr(rows), native.ptr(w), n,
                 float(before_t), float(before_f), float(tot_t), float(tot_f), native.ptr(scratch), native.ptr(part),
                 native.ptr(out), native.stream_ptr(dev))
     return out
