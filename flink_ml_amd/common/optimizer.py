@@ -33,7 +33,17 @@ from ..parallel import comm
 from ..parallel.checkpoint import AlgorithmCheckpoint, fault_point
 from ..parallel.context import device_sharers, get_context
 from ..table import SparseColumn
-from ..utils import graphs, tracing
+from ..utils import graphs, hostsync, tracing
+
+
+def _dzeros(shape, dtype, dev) -> torch.Tensor:
+    """Zero-filled device buffers of the trainers through the library's own fill kernel (torch's
+    fill kernels load lazily: tens of ms inside the first fit of a process)."""
+    if dev.type == "cuda":
+        from ..ops import native
+
+        return native.zeros(shape, dtype, dev)
+    return torch.zeros(shape, dtype=dtype, device=dev)
 
 
 def local_batch_size(global_batch: int, rank: int, world: int) -> int:
@@ -56,13 +66,23 @@ class SGD:
     def optimize(self, init_coef: np.ndarray, X, y: torch.Tensor, weight: Optional[torch.Tensor],
                  loss: str) -> np.ndarray:
         trainer = make_trainer(self, init_coef, X, y, weight, loss)
-        return trainer.fit()
+        try:
+            return trainer.fit()
+        finally:
+            if hasattr(trainer, "close"):
+                trainer.close()
 
 
 def make_trainer(sgd: SGD, init_coef, X, y, weight, loss, use_graph: Optional[bool] = None):
     dev = X.device if isinstance(X, (torch.Tensor, SparseColumn)) else torch.device("cpu")
     if dev.type == "cuda":
         return DeviceGlmTrainer(sgd, init_coef, X, y, weight, loss, use_graph=use_graph)
+    if isinstance(X, torch.Tensor) and isinstance(y, torch.Tensor) and y.device.type == "cuda":
+        # a GPU fit whose dense partition stays in host memory (it exceeds FMLX_HBM_BUDGET): the
+        # out-of-core trainer keeps what fits resident and streams the rest (common/outofcore.py)
+        from .outofcore import StreamedGlmTrainer, hbm_budget
+
+        return StreamedGlmTrainer(sgd, init_coef, X, y, weight, loss, y.device, hbm_budget())
     return TorchGlmTrainer(sgd, init_coef, X, y, weight, loss)
 
 
@@ -191,14 +211,20 @@ class DeviceGlmTrainer:
         self.w = weight.to(device=dev, dtype=acc).reshape(-1).contiguous() if weight is not None else None
         c0 = np.asarray(init_coef, dtype=np.float64)
         if not c0.any():  # the usual zero init (1M-wide sparse models): no pageable H2D copy
-            self.coef = torch.zeros(c0.shape, dtype=acc, device=dev)
+            self.coef = _dzeros(c0.shape, acc, dev)
         else:
             c0 = torch.from_numpy(np.ascontiguousarray(c0)).to(acc)
             self.coef = (c0.pin_memory() if dev.type == "cuda" else c0).to(dev, non_blocking=True).contiguous()
         self.B = local_batch_size(sgd.global_batch_size, ctx.rank, ctx.world_size)
-        self.state = torch.zeros(8, dtype=torch.int32, device=dev)
-        self.state[1:2].fill_(1)  # running[0] (a fill kernel: `t[i] = scalar` is a blocking pageable copy)
-        self.feedback = torch.zeros(self.d + 2, dtype=acc, device=dev)
+        self.state = _dzeros(8, torch.int32, dev)
+        # running[0] (a fill kernel: `t[i] = scalar` is a blocking pageable copy)
+        if dev.type == "cuda":
+            from ..ops import native
+
+            native.fill_i32(self.state[1:2], 1)
+        else:
+            self.state[1:2].fill_(1)
+        self.feedback = _dzeros(self.d + 2, acc, dev)
         self.distributed = ctx.is_distributed
         self.xg = None
         self.csc = None
@@ -214,8 +240,8 @@ class DeviceGlmTrainer:
                 self.csc = gk.BatchCsc.alloc(self.indptr, self.indices, self.values, self.n, self.d, self.B,
                                              max_rounds=sgd.max_iter)
                 if self.csc is not None:
-                    self.mult = torch.zeros(max(1, min(self.B, self.n)), dtype=acc, device=dev)
-                    self.wl = torch.zeros(gk.wl_elems(), dtype=acc, device=dev)  # Σw/Σloss slots per parity
+                    self.mult = _dzeros(max(1, min(self.B, self.n)), acc, dev)
+                    self.wl = _dzeros(gk.wl_elems(), acc, dev)  # Σw/Σloss slots per parity
         elif self.wide:
             self.scratch = None
             self.nparts = 0
@@ -260,7 +286,7 @@ class DeviceGlmTrainer:
         self.defer = ((self.mode == gk.TAIL_UPDATE or self.mode == gk.TAIL_XGMI and gk.DEFER_XGMI)
                       and self.scratch is not None and not self.scratch.det and gk.defer_supported(self.d, acc))
         self.parity = 0
-        self.cw = torch.zeros((2, self.d), dtype=acc, device=dev) if self.defer else None
+        self.cw = _dzeros((2, self.d), acc, dev) if self.defer else None
         self._flushed = False
         self._short = False  # fit(): too few rounds for hipGraph capture to pay (direct launches)
         self.graphs = {}
@@ -487,7 +513,7 @@ class DeviceGlmTrainer:
         self.run_rounds(1)
 
     def running(self) -> bool:
-        st = self.state.cpu()
+        st = hostsync.to_host(self.state)  # polled, no blocking runtime wait
         if self.defer:
             return not bool(st[6])
         e = int(st[0])
@@ -554,5 +580,8 @@ class DeviceGlmTrainer:
                 if stop:
                     break
             self.flush()
+        # the coefficients: one stream-ordered copy into pinned memory, completion polled — a host
+        # sync point, after which the exchange's error word is final
+        coef = hostsync.to_host(self.coef).to(torch.float64).numpy()
         self.check_exchange()
-        return self.coef.to(torch.float64).cpu().numpy()
+        return coef

@@ -48,12 +48,14 @@ def reservoir_sample_indices(n: int, k: int, seed: int) -> np.ndarray:
 def sample_rows(X: torch.Tensor, k: int, seed: int) -> np.ndarray:
     """``DataStreamUtils.sample``: reservoir per rank (only the k chosen rows leave the device),
     gather in rank order, reservoir again over the union."""
-    if X.device.type == "cuda":
+    draw_dev = X.device if X.device.type == "cuda" else config.compute_device()
+    if draw_dev.type == "cuda":
         # the n-long draw stream in parallel on the device (bit-exact; ops/datagen.py); only the
-        # k chosen rows leave HBM
+        # k chosen rows leave HBM (a host-resident out-of-core partition: the draw still runs on
+        # the GPU, the k rows are gathered on the host)
         from ..ops.datagen import reservoir_sample_device
 
-        idx = reservoir_sample_device(int(X.shape[0]), k, seed, X.device)
+        idx = reservoir_sample_device(int(X.shape[0]), k, seed, draw_dev)
     else:
         idx = torch.as_tensor(reservoir_sample_indices(int(X.shape[0]), k, seed))
     local = X[idx.to(X.device)].to(torch.float64).cpu().numpy() if len(idx) else np.zeros((0, X.shape[1]))
@@ -135,11 +137,18 @@ class KMeans(Estimator, KMeansParams):
     def fit(self, *inputs: Table) -> KMeansModel:
         t = inputs[0]
         fcol = self.get(self.FEATURES_COL)
-        X = config.features_for_compute(t, fcol, allow_sparse=False)
+        Xh = config.host_features_if_oversized(t, fcol)  # larger than FMLX_HBM_BUDGET: stays on the host
+        X = Xh if Xh is not None else config.features_for_compute(t, fcol, allow_sparse=False)
         k = self.get(self.K)
         metric = self.get(self.DISTANCE_MEASURE)
         init = sample_rows(X, k, self.get_seed())
-        cents, weights = kmeans_lloyd(X, init, self.get(self.MAX_ITER), metric)
+        if Xh is not None:
+            from ..common.outofcore import hbm_budget, streamed_kmeans
+
+            cents, weights = streamed_kmeans(Xh, init, self.get(self.MAX_ITER), metric, config.compute_device(),
+                                             hbm_budget())
+        else:
+            cents, weights = kmeans_lloyd(X, init, self.get(self.MAX_ITER), metric)
         model = KMeansModel().set_model_data(kmeans_model_data_table(cents, weights))
         rw_update(model, self)
         return model

@@ -34,8 +34,12 @@ from .base import ModelWithData
 
 # ---------------------------------------------------------------------------------------------
 def extract_training_data(est, table: Table, check_labels=None):
-    """(features, labels[n] f64, weights[n] f64 | None) on the compute device."""
-    X = config.features_for_compute(table, est.get(est.FEATURES_COL))
+    """(features, labels[n] f64, weights[n] f64 | None) on the compute device — except a dense
+    host-resident feature column larger than FMLX_HBM_BUDGET on a GPU, which stays in host memory
+    (compute dtype) for the out-of-core trainer (common/outofcore.py)."""
+    X = config.host_features_if_oversized(table, est.get(est.FEATURES_COL))
+    if X is None:
+        X = config.features_for_compute(table, est.get(est.FEATURES_COL))
     dev = config.compute_device()
     y = table.scalars(est.get(est.LABEL_COL), dtype=torch.float64, device=dev)
     wcol = est.get(est.WEIGHT_COL)

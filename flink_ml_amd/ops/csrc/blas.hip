@@ -569,6 +569,53 @@ FMLX_API int fmlx_blas_interaction(int k, const double* const* in, const long* l
   return (int)hipGetLastError();
 }
 
+// ---- set-up helpers of the fit paths (no torch kernels: their code objects load lazily, tens of
+// ms each on first use inside a fit — profiles/r5/svc_cold_first_fit_*) ----------------------
+__global__ __launch_bounds__(256) void fill32_kernel(uint32_t* __restrict__ p, long n, uint32_t v) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) p[i] = v;
+}
+
+// out[0] = indptr[n]; out[1 + b] = indptr[min(b·B, n)] for b = 0 … P
+__global__ __launch_bounds__(256) void batch_bounds_kernel(const long* __restrict__ indptr, long n, long B, long P,
+                                                           long* __restrict__ out) {
+  for (long b = (long)blockIdx.x * 256 + threadIdx.x; b <= P + 1; b += (long)gridDim.x * 256) {
+    if (b == 0)
+      out[0] = indptr[n];
+    else {
+      const long r = (b - 1) * B;
+      out[b] = indptr[r < n ? r : n];
+    }
+  }
+}
+
+// n 32-bit words at p set to v (zeros of any dtype: v = 0, n = bytes / 4)
+FMLX_API int fmlx_fill32(void* p, long n, unsigned v, void* stream) {
+  if (n <= 0) return 0;
+  long b = (n + 1023) / 1024;
+  if (b > 1024) b = 1024;
+  hipLaunchKernelGGL(fill32_kernel, dim3((unsigned)b), dim3(256), 0, (hipStream_t)stream, (uint32_t*)p, n, v);
+  return (int)hipGetLastError();
+}
+
+FMLX_API int fmlx_csr_batch_bounds(const long* indptr, long n, long B, long P, long* out, void* stream) {
+  long b = (P + 2 + 255) / 256;
+  if (b > 1024) b = 1024;
+  hipLaunchKernelGGL(batch_bounds_kernel, dim3((unsigned)b), dim3(256), 0, (hipStream_t)stream, indptr, n, B, P, out);
+  return (int)hipGetLastError();
+}
+
+// ---- host memory for the out-of-core trainers (common/outofcore.py) ---------------------------
+// pin / unpin an existing host range (the data cache's memory segments): the DMA engines then
+// copy batches straight from the cache, no staging copy
+FMLX_API int fmlx_host_register(void* p, long bytes) {
+  return (int)hipHostRegister(p, (size_t)bytes, hipHostRegisterDefault);
+}
+FMLX_API int fmlx_host_unregister(void* p) { return (int)hipHostUnregister(p); }
+// stream-ordered host → device copy from pinned (or registered) memory
+FMLX_API int fmlx_memcpy_h2d(void* dst, const void* src, long bytes, void* stream) {
+  return (int)hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyHostToDevice, (hipStream_t)stream);
+}
+
 // Launches every translation unit's anchor kernel once (loads all code objects of the library);
 // returns the number of code objects, or < 0 on a launch error.
 FMLX_API int fmlx_preload_all(void* stream) {

@@ -96,7 +96,9 @@ int new_segment(Cache* c, int64_t need) {
   Segment s;
   const int64_t cap = need > c->seg_bytes ? need : c->seg_bytes;
   if (c->mem_used + cap <= c->mem_budget) {
-    s.mem = (char*)std::malloc((size_t)cap);
+    // page-aligned: the out-of-core trainers pin memory segments in place (hipHostRegister)
+    void* p = nullptr;
+    s.mem = ::posix_memalign(&p, 4096, (size_t)cap) == 0 ? (char*)p : nullptr;
     if (s.mem) {
       s.cap = cap;
       c->mem_used += cap;
@@ -172,6 +174,24 @@ int fmlx_dc_read(void* h, int64_t i, void* dst) {
 }
 
 // Spills every memory segment to disk (returns 0 or a negative error).
+// address of record i inside a memory segment (nullptr: the record lives in a file segment)
+void* fmlx_dc_record_ptr(void* h, int64_t i) {
+  Cache* c = (Cache*)h;
+  if (i < 0 || i >= (int64_t)c->recs.size()) return nullptr;
+  const Rec r = c->recs[i];
+  const Segment& s = c->segs[r.seg];
+  return s.mem ? (void*)(s.mem + r.off) : nullptr;
+}
+
+// memory segment idx: its base and capacity (0 / nullptr for file segments or a bad index)
+void* fmlx_dc_segment_mem(void* h, int64_t idx, int64_t* cap) {
+  Cache* c = (Cache*)h;
+  *cap = 0;
+  if (idx < 0 || idx >= (int64_t)c->segs.size() || !c->segs[idx].mem) return nullptr;
+  *cap = c->segs[idx].cap;
+  return c->segs[idx].mem;
+}
+
 int fmlx_dc_spill_all(void* h) {
   Cache* c = (Cache*)h;
   std::lock_guard<std::mutex> g(c->mu);

@@ -43,7 +43,7 @@ constexpr int KM_CH = 256;  // rows per gather chunk
 // ------------------------------------------------------------------------------------------
 // MFMA assign (euclidean, bf16)
 // ------------------------------------------------------------------------------------------
-template <int KS, bool FULL, bool SCHED, bool XLDS = false>
+template <int KS, bool FULL>
 // Cb / cnorm are not __restrict__ so the compiler fence after each tile prefetch keeps the
 // loads where they are issued (with restrict they get sunk next to their use, after the MFMAs).
 __global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t* __restrict__ X, long ld, long n,
@@ -54,11 +54,7 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t
   constexpr int ROWB = DP * 2 + 16;       // padded LDS row stride (bytes): conflict-free b128 reads
   constexpr int CHUNKS = 32 * DP / 8;     // 16-byte chunks per 32-centroid tile
   constexpr int CPT = (CHUNKS + 255) / 256;
-  // XLDS: the block's rows are first copied into LDS by LDS-DMA (1 KiB contiguous per
-  // wave-instruction; the register path reads 32 rows x 32 B per instruction) and the A
-  // fragments are read from there; the same LDS then holds the centroid tiles
-  constexpr int XBYTES = 4 * 32 * MT * DP * 2;
-  constexpr int LDSB = XLDS && XBYTES > 2 * 32 * ROWB ? XBYTES : 2 * 32 * ROWB;
+  constexpr int LDSB = 2 * 32 * ROWB;
   __shared__ __align__(16) unsigned char lds[LDSB];
 
   const int lane = threadIdx.x & 63;
@@ -73,33 +69,7 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t
   // 16-B aligned rows): unconditional 16-B loads of clamped rows, all in flight together — a
   // per-fragment branch would make every load wait for the previous one (16 round trips).
   bf16x8_t a[MT][KS];
-  if constexpr (XLDS) {
-    static_assert(FULL && (KS & (KS - 1)) == 0, "LDS-staged rows need whole power-of-two rows");
-    typedef __attribute__((address_space(3))) void* lds_ptr_t;
-    typedef __attribute__((address_space(1))) void* glb_ptr_t;
-    constexpr int XROWB = DP * 2;   // bytes per row in LDS
-    constexpr int NS = 2 * KS;      // 16-B slots per row; slot s' of row r holds chunk s' ^ (r mod NS)
-    constexpr int PIECES = XBYTES / 1024;
-    const long grow0 = grp * (4 * 32 * MT);
-    for (int p = wave; p < PIECES; p += 4) {
-      const int off = p * 1024 + lane * 16;
-      const int lrow = off / XROWB, slot = (off % XROWB) / 16;
-      long grow = grow0 + lrow;
-      grow = grow < n ? grow : n - 1;
-      __builtin_amdgcn_global_load_lds((glb_ptr_t)(X + grow * ld + (slot ^ (lrow & (NS - 1))) * 8),
-                                       (lds_ptr_t)(lds + p * 1024), 16, 0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      const int lrow = wave * 32 * MT + m * 32 + r32;
-#pragma unroll
-      for (int s = 0; s < KS; ++s)
-        a[m][s] = *reinterpret_cast<const bf16x8_t*>(lds + lrow * XROWB + (((2 * s + h) ^ (lrow & (NS - 1))) * 16));
-    }
-    __syncthreads();  // every wave has its fragments before the centroid tiles reuse the LDS
-  } else if constexpr (FULL) {
+  if constexpr (FULL) {
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       const long row = rowbase + m * 32 + r32;
@@ -246,39 +216,20 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_bf16_kernel(const bf16_t
       best[M_][R_] = k0 < best[M_][R_] ? k0 : best[M_][R_];                    \
       best[M_][(R_) + 1] = k1 < best[M_][(R_) + 1] ? k1 : best[M_][(R_) + 1]; \
     }
-    if constexpr (SCHED && MT == 2) {
-      // every B read issued up front (one LDS wait per tile, not one per k-step), the m-tile 0
-      // chain, then the m-tile 1 chain with m-tile 0's epilogue in its MFMA gaps (one register
-      // pair = 5 VALU per 32-cycle MFMA), so half the epilogue runs under the matrix core
-      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
-        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][s], bfr[s], s == 0 ? xnb[0] : acc[0], 0, 0, 0);
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][s], bfr[s], s == 0 ? xnb[1] : acc[1], 0, 0, 0);
-        if (2 * s < 16) KM_EPI2(0, 2 * s)
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // then 5 VALU
-      }
-#pragma unroll
-      for (int r = 2 * KS; r < 16; r += 2) KM_EPI2(0, r)
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) KM_EPI2(1, r)
-    } else {
-#pragma unroll
-      for (int s = 0; s < KS; ++s)
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m][s], bfr[s], s == 0 ? xnb[m] : acc[m], 0, 0, 0);
-      // (a software-pipelined variant — tile t's MFMAs interleaved with tile t-1's epilogue on a
-      // second accumulator set — measured slower: 4.46 ms at 256 VGPRs vs 4.02 ms for this loop at
-      // 190 VGPRs; two resident waves per SIMD already overlap one's MFMAs with the other's VALU)
+    for (int s = 0; s < KS; ++s)
 #pragma unroll
       for (int m = 0; m < MT; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m][s], bfr[s], s == 0 ? xnb[m] : acc[m], 0, 0, 0);
+    // (a software-pipelined variant — tile t's MFMAs interleaved with tile t-1's epilogue on a
+    // second accumulator set — measured slower: 4.46 ms at 256 VGPRs vs 4.02 ms for this loop at
+    // 190 VGPRs; two resident waves per SIMD already overlap one's MFMAs with the other's VALU.
+    // An interleaved MFMA/epilogue schedule and LDS-DMA-staged rows measured 4.07 vs 3.95-4.00 ms
+    // and within noise, and were removed in round 5.)
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) KM_EPI2(m, r)
-    }
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) KM_EPI2(m, r)
 #undef KM_EPI2
     // unconditional (after the last tile it rewrites the idle buffer with the re-fetched last
     // tile, which nobody reads): a branch here split the tile body into two scheduling regions
@@ -370,7 +321,7 @@ __global__ __launch_bounds__(256) void kmeans_baug_kernel(const float* __restric
   if (j < kpad) baug[j] = km_baug_words(__float_as_uint(cnorm[j]));
 }
 
-template <int KS, bool PF, int NW = 4>
+template <int KS, int NW = 4>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kernel(const bf16_t* __restrict__ X, long ld,
                                                                          long n, const bf16_t* Cb,
                                                                          const uint2* baug, int kpad,
@@ -560,28 +511,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void kmeans_assign_bf16_pipe_kerne
     __builtin_amdgcn_sched_group_barrier(0x002, 2 * EPG, 0);                                         \
   }
 
-  if constexpr (!PF) {
-    for (int t = 0; t < ntiles; ++t) {
-      const int t2 = t + 2 < ntiles ? t + 2 : ntiles - 1;  // the tail re-fetches the last tile
-      KP_DMA(t2, s_n2)
-      bf16x8_t bfr[KS];
-      s16x4_t bag;
-      KP_LDB(s_cur, bfr, bag)
-      const unsigned tt = (unsigned)t;
-      __builtin_amdgcn_sched_barrier(0);
-      KP_CHAIN(acc0, 0, bfr, bag, acc1, 1, tprev)  // m-tile 0 of tile t | m-tile 1 of tile t − 1
-      KP_CHAIN(acc1, 1, bfr, bag, acc0, 0, tt)     // m-tile 1 of tile t | m-tile 0 of tile t
-      __builtin_amdgcn_sched_barrier(0);
-      // tile t + 1 (issued a tile ago) complete for this wave, then for every wave
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW + 1) : "memory");
-      __syncthreads();
-      tprev = tt;
-      const int s_old = s_cur;
-      s_cur = s_n1;
-      s_n1 = s_n2;
-      s_n2 = s_old;
-    }
-  } else {
+  {
     // B fragments one tile ahead in registers: the ring wait + barrier sit between the two
     // chains of a tile, and the next tile's ds_reads are issued under the second chain, so no
     // chain ever starts on an LDS round trip. Two named register sets, loop unrolled by two.
@@ -1020,17 +950,10 @@ __global__ __launch_bounds__(256) void kmeans_finalize_kernel(const A* __restric
   }
 }
 
-// interleaved MFMA/epilogue schedule of the MFMA assign (fmlx_kmeans_set_sched). Off: measured
-// 4.07 ms vs 3.95-4.00 ms for the plain loop at 12.5M x 128, k=1024 (and within 3 % either way
-// at D=64, k=64/256) — the second resident wave per SIMD already fills the epilogue gaps.
-int g_km_sched = 0;
-// rows staged through LDS by LDS-DMA (fmlx_kmeans_set_sched(2)): within noise of the register
-// path (3.71-3.74 vs 3.74-3.75 ms at 12.5M x 128, k=1024; 0.87 vs 0.91 ms at k=32), kept off
-int g_km_xlds = 0;
-// LDS-DMA centroid ring + cross-m-tile epilogue interleave (kmeans_assign_bf16_pipe_kernel)
-int g_km_pipe = 0;
-// A/B knob: extra dynamic LDS per pipelined block (caps the blocks, i.e. waves per SIMD, per CU).
-// One wave per SIMD (90 KB): 3.68 vs 3.22 ms at 12.5M x 128, k = 1024 — the second wave covers
+// LDS-DMA centroid ring + cross-m-tile epilogue interleave (kmeans_assign_bf16_pipe_kernel, the
+// B fragments prefetched one tile ahead): the shipped assign for D = 64 / 128; 0 = plain loop.
+// History of the variants measured against it (all removed in round 5): one wave per SIMD via an
+// LDS pad (90 KB): 3.68 vs 3.22 ms at 12.5M x 128, k = 1024 — the second wave covers
 // part of the first's issue stalls. (Issuing the tile's LDS-DMA pieces inside the MFMA chain
 // instead of ahead of it: 3.15 vs 3.15 ms, not kept. Dropping the per-tile barrier altogether —
 // wrong labels, a diagnostic — ran 3.13-3.16 vs 3.17-3.19 ms: the barrier costs ~1 %; what is
@@ -1062,8 +985,10 @@ int g_km_pipe = 0;
 // the chip is power-bound here, a cycle saving comes back as clock; kmeans_assign_scalar_dst_ab.log.
 // The norm step on v_mfma_f32_32x32x8_bf16 (K = 8: 5.6 % fewer MFMA cycles per tile, 74 VALU,
 // 193 VGPRs): identical labels, 1,285 cycles per tile and the same wall time —
-// kmeans_assign_k8_norm_ab.log; kept for the lighter kernel.)
-int g_km_ldspad = 0;
+// kmeans_assign_k8_norm_ab.log; kept for the lighter kernel. 8-wave, 512-row blocks: within
+// noise at k = 1024 and slower at k = 32. The pipelined kernel without the B prefetch: 3.23 vs
+// 3.18 ms.)
+int g_km_pipe = 1;
 
 template <int KS>
 int launch_assign_bf16(const void* X, long ld, long n, int D, const void* Cb, const float* cnorm, int kpad, int* labels,
@@ -1073,48 +998,20 @@ int launch_assign_bf16(const void* X, long ld, long n, int D, const void* Cb, co
   const int blocks = (int)((n + rows_per_block - 1) / rows_per_block);
   if (blocks == 0) return 0;
   const bool full = D == 16 * KS && (ld % 8) == 0 && ((uintptr_t)X % 16) == 0;
-  if constexpr ((KS & (KS - 1)) == 0 && KS <= 8) {
-    if (full && g_km_xlds) {
-      hipLaunchKernelGGL((kmeans_assign_bf16_kernel<KS, true, false, true>), dim3(blocks), dim3(256), 0, s,
-                         (const bf16_t*)X, ld, n, D, (const bf16_t*)Cb, cnorm, kpad, labels);
-      return (int)hipGetLastError();
-    }
-  }
   const bool pipe = full && g_km_pipe && baug != nullptr;
-  if constexpr (KS == 4 || KS == 8)
-    if (pipe) hipLaunchKernelGGL(kmeans_baug_kernel, dim3((kpad + 255) / 256), dim3(256), 0, s, cnorm, kpad, (uint2*)baug);
-  if constexpr (KS == 8) {
-    if (pipe && g_km_pipe >= 3) {
-      // A/B: 8 waves per block (one block per CU) share each centroid tile's LDS-DMA
-      const int blocks8 = (int)((n + 8 * 32 * MT - 1) / (8 * 32 * MT));
-      if (g_km_pipe == 4)
-        hipLaunchKernelGGL((kmeans_assign_bf16_pipe_kernel<KS, true, 8>), dim3(blocks8), dim3(512), g_km_ldspad, s,
-                           (const bf16_t*)X, ld, n, (const bf16_t*)Cb, (const uint2*)baug, kpad, labels);
-      else
-        hipLaunchKernelGGL((kmeans_assign_bf16_pipe_kernel<KS, false, 8>), dim3(blocks8), dim3(512), g_km_ldspad, s,
-                           (const bf16_t*)X, ld, n, (const bf16_t*)Cb, (const uint2*)baug, kpad, labels);
-      return (int)hipGetLastError();
-    }
-  }
   if constexpr (KS == 4 || KS == 8) {
     if (pipe) {
-      if (g_km_pipe == 2)
-        hipLaunchKernelGGL((kmeans_assign_bf16_pipe_kernel<KS, true>), dim3(blocks), dim3(256), g_km_ldspad, s,
-                           (const bf16_t*)X, ld, n, (const bf16_t*)Cb, (const uint2*)baug, kpad, labels);
-      else
-        hipLaunchKernelGGL((kmeans_assign_bf16_pipe_kernel<KS, false>), dim3(blocks), dim3(256), g_km_ldspad, s,
-                           (const bf16_t*)X, ld, n, (const bf16_t*)Cb, (const uint2*)baug, kpad, labels);
+      hipLaunchKernelGGL(kmeans_baug_kernel, dim3((kpad + 255) / 256), dim3(256), 0, s, cnorm, kpad, (uint2*)baug);
+      hipLaunchKernelGGL((kmeans_assign_bf16_pipe_kernel<KS>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)X, ld,
+                         n, (const bf16_t*)Cb, (const uint2*)baug, kpad, labels);
       return (int)hipGetLastError();
     }
   }
-  if (full && g_km_sched)
-    hipLaunchKernelGGL((kmeans_assign_bf16_kernel<KS, true, true>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)X, ld,
-                       n, D, (const bf16_t*)Cb, cnorm, kpad, labels);
-  else if (full)
-    hipLaunchKernelGGL((kmeans_assign_bf16_kernel<KS, true, false>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)X, ld, n,
-                       D, (const bf16_t*)Cb, cnorm, kpad, labels);
+  if (full)
+    hipLaunchKernelGGL((kmeans_assign_bf16_kernel<KS, true>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)X, ld, n, D,
+                       (const bf16_t*)Cb, cnorm, kpad, labels);
   else
-    hipLaunchKernelGGL((kmeans_assign_bf16_kernel<KS, false, false>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)X, ld, n,
+    hipLaunchKernelGGL((kmeans_assign_bf16_kernel<KS, false>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)X, ld, n,
                        D, (const bf16_t*)Cb, cnorm, kpad, labels);
   return (int)hipGetLastError();
 }
@@ -1141,24 +1038,14 @@ int chunk_sum_vpl(const void* X, long ld, int D, const long* order, const long* 
 
 }  // namespace
 
-// KS = padded K-steps of 16 (one of 1..8,10,12,16; >= ceil(D/16)); Cb is [kpad][16*KS] zero-padded
-// 0: plain loop, 1: interleaved MFMA/epilogue schedule, 2: rows staged through LDS (LDS-DMA),
-// 3: pipelined (LDS-DMA centroid ring, norms in the MFMA, epilogues in the other m-tile's MFMA
-// gaps; D = 64/128), 4: the same with the B fragments prefetched one tile ahead. (8-wave,
-// 512-row blocks — half the centroid bytes and DMA issues per row — measured within noise:
-// 3.17 vs 3.19 ms at 12.5M x 128, k = 1024, and slower at k = 32; NW stays a template knob.)
-FMLX_API int fmlx_kmeans_set_ldspad(int bytes) {
-  g_km_ldspad = bytes > 0 ? bytes : 0;
-  return 0;
-}
-
+// Assign schedule: 1 (default) = the pipelined kernel for D = 64 / 128 (other widths: plain loop),
+// 0 = the plain loop everywhere (A/B and tests).
 FMLX_API int fmlx_kmeans_set_sched(int mode) {
-  g_km_sched = mode == 1;
-  g_km_xlds = mode == 2;
-  g_km_pipe = mode == 3 ? 1 : mode == 4 ? 2 : mode == 5 ? 3 : mode == 6 ? 4 : 0;  // 5/6: 8-wave blocks
+  g_km_pipe = mode != 0;
   return 0;
 }
 
+// KS = padded K-steps of 16 (one of 1..8,10,12,16; >= ceil(D/16)); Cb is [kpad][16*KS] zero-padded.
 // baug: kpad x 8 bytes of scratch for the pipelined kernel's B_aug rows (nullptr: plain loop)
 FMLX_API int fmlx_kmeans_assign_bf16(const void* X, long ld, long n, int D, int KS, const void* Cb, const float* cnorm,
                                      int kpad, int* labels, void* baug, void* stream) {

@@ -156,15 +156,15 @@ class RoundScratch:
         self.nparts = nparts
         self.det = DETERMINISTIC if det is None else bool(det)
         if self.det:
-            self.partials = torch.zeros((nparts, d + 2), dtype=acc, device=device)
-            self.stage1 = torch.zeros((stage1_rows(nparts), d + 2), dtype=acc, device=device)
+            self.partials = native.zeros((nparts, d + 2), acc, device)
+            self.stage1 = native.zeros((stage1_rows(nparts), d + 2), acc, device)
         else:
-            self.partials = torch.zeros((1, d + 2), dtype=acc, device=device)
+            self.partials = native.zeros((1, d + 2), acc, device)
             self.stage1 = None
         # atomic tail: ACC_MAX_REPS replicas of the [d+2] accumulator on whole 256-B lines
-        self.acc = torch.zeros(int(native.kernels().fmlx_glm_acc_elems(d)), dtype=acc, device=device)
+        self.acc = native.zeros(int(native.kernels().fmlx_glm_acc_elems(d)), acc, device)
         # 64 group + 1 top tickets
-        self.cnt = torch.zeros(int(native.kernels().fmlx_glm_cnt_elems()), dtype=torch.int32, device=device)
+        self.cnt = native.zeros(int(native.kernels().fmlx_glm_cnt_elems()), torch.int32, device)
 
 
 def glm_round(X, y, wt, coef, B: int, loss: int, state, scratch: RoundScratch, mode: int, feedback=None,
@@ -286,8 +286,18 @@ def _batch_bounds(indptr: torch.Tensor, n: int, B: int):
     if ent is not None and ent[0]() is indptr and key in ent[1]:
         return ent[1][key]
     P = (n + B - 1) // B
-    sel = torch.arange(0, P + 1, device=indptr.device).mul_(B).clamp_(max=n)
-    both = torch.cat([indptr[-1:], indptr[sel]]).tolist()  # one copy for both
+    from ..utils import hostsync
+
+    if indptr.is_cuda:
+        # one library kernel + one polled copy (no torch index / arange / cat kernels: their code
+        # objects load lazily, tens of ms inside the first fit of a process)
+        out = torch.empty(P + 2, dtype=torch.int64, device=indptr.device)
+        native.call("fmlx_csr_batch_bounds", native.ptr(indptr.contiguous()), n, B, P, native.ptr(out),
+                    native.stream_ptr(indptr.device))
+        both = hostsync.to_host(out).tolist()
+    else:
+        sel = torch.arange(0, P + 1).mul_(B).clamp_(max=n)
+        both = torch.cat([indptr[-1:], indptr[sel]]).tolist()
     val = (int(both[0]), both[1:])
     if ent is None or ent[0]() is not indptr:
         ref = weakref.ref(indptr, lambda _r, i=id(indptr): _BOUNDS_CACHE.pop(i, None))

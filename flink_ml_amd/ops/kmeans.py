@@ -17,7 +17,6 @@ from .native import c_int, c_long, c_void_p
 
 native.register_kernel_sigs({
     "fmlx_kmeans_set_sched": [c_int],
-    "fmlx_kmeans_set_ldspad": [c_int],
     "fmlx_kmeans_assign_bf16": [c_void_p, c_long, c_long, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
                                 c_void_p, c_void_p],
     "fmlx_kmeans_assign_generic": [c_int, c_void_p, c_long, c_long, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p,
@@ -48,16 +47,10 @@ DETERMINISTIC = os.environ.get("FMLX_DETERMINISTIC", "0") == "1"
 
 METRICS = {"euclidean": 0, "manhattan": 1, "cosine": 2}
 CHUNK = 256
-# Lloyd rounds over large shards (bf16 fast path, stable grouping): the rows are cut into
-# SPLIT_PARTS parts; part p's grouping + gather-sum (memory-bound: it re-reads the part's rows)
-# runs on a side stream while part p + 1's assign (MFMA-bound) runs on the main stream, and the
-# parts' [sums | counts] are added in part order (deterministic). KMeans.java:291-295 sums each
-# point into its cluster in the assignment loop itself; here the sum trails the assign by a part.
-# Off by default: interleaved same-box A/Bs at the 12.5M x 128, k = 1024 shard measured the split
-# round 3.98-4.06 vs 3.77-3.86 ms/iter unsplit (the assign fills every CU; the gather-sum beside
-# it slows it more than it hides) — profiles/r4/kmeans_assign_lds_split_ab.jsonl. FMLX_KMEANS_SPLIT=4.
-SPLIT_PARTS = int(os.environ.get("FMLX_KMEANS_SPLIT", "1"))
-SPLIT_MIN_ROWS = int(os.environ.get("FMLX_KMEANS_SPLIT_MIN_ROWS", str(1 << 20)))
+# (A split round — part p's grouping + gather-sum on a side stream under part p + 1's assign —
+# measured 3.98-4.06 vs 3.77-3.86 ms/iter unsplit at the 12.5M x 128, k = 1024 shard and was removed
+# in round 5: the assign fills every CU and the gather-sum beside it slows it more than it hides;
+# profiles/r4/kmeans_assign_lds_split_ab.jsonl.)
 MFMA_KS = (1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16)
 
 
@@ -70,19 +63,18 @@ def mfma_ks(D: int) -> int:
     return 0
 
 
-# MFMA assign schedule (fmlx_kmeans_set_sched): 4 = pipelined kernel for D = 64/128 (norms in
-# the matrix core, LDS-DMA centroid ring, B fragments one tile ahead; other widths take the
-# plain loop), 3 = pipelined without the prefetch, 0 = plain loop, 1 = interleaved plain loop,
-# 2 = LDS-DMA-staged rows. FMLX_KMEANS_SCHED overrides. 12.5M x 128, k = 1024 on one MI355X:
-# 3.53 ms (0) → 3.23 ms (3) → 3.18 ms (4).
-ASSIGN_SCHED = int(os.environ.get("FMLX_KMEANS_SCHED", "4"))
+# MFMA assign schedule (fmlx_kmeans_set_sched): 1 = the pipelined kernel for D = 64/128 (norms in
+# the matrix core, LDS-DMA centroid ring, B fragments one tile ahead; other widths take the plain
+# loop), 0 = the plain loop everywhere (A/B and tests). FMLX_KMEANS_SCHED overrides. 12.5M x 128,
+# k = 1024 on one MI355X: 3.53 ms (plain) → 3.18 ms (pipelined); the other variants measured over
+# rounds 2-4 were removed in round 5 (history in csrc/kmeans.hip).
+ASSIGN_SCHED = int(os.environ.get("FMLX_KMEANS_SCHED", "1"))
 _sched_applied = None
 
 
 def set_assign_sched(mode: int) -> None:
     global _sched_applied
     native.call("fmlx_kmeans_set_sched", int(mode))
-    native.call("fmlx_kmeans_set_ldspad", int(os.environ.get("FMLX_KMEANS_LDSPAD", "0")))
     _sched_applied = int(mode)
 
 
@@ -241,33 +233,6 @@ class KMeansRound:
         elif self.group:
             self.gcounts = torch.zeros(k, dtype=torch.int32, device=dev)  # re-zeroed by the scan kernel
             self.gcursor = torch.zeros(k, dtype=torch.int32, device=dev)
-        self.parts = []
-        if (self.fast and self.stable and SPLIT_PARTS > 1 and self.n >= max(SPLIT_MIN_ROWS, SPLIT_PARTS)
-                and metric == "euclidean"):
-            lib = native.kernels()
-            per = -(-self.n // SPLIT_PARTS)
-            per = -(-per // 256) * 256  # whole assign blocks per part
-            for r0 in range(0, self.n, per):
-                r1 = min(r0 + per, self.n)
-                m = r1 - r0
-                mc = (m + CHUNK - 1) // CHUNK + k
-                self.parts.append({
-                    "r0": r0, "r1": r1, "max_chunks": mc,
-                    "order32": torch.empty(m, dtype=torch.int32, device=dev),
-                    "offsets": torch.zeros(k + 1, dtype=torch.int64, device=dev),
-                    "chunk_off": torch.zeros(k + 1, dtype=torch.int64, device=dev),
-                    "gscratch": torch.empty(max(1, int(lib.fmlx_group_stable_scratch(m, k))), dtype=torch.int32,
-                                            device=dev),
-                    "partial": torch.zeros((mc, self.D), dtype=self.acc, device=dev),
-                    "payload": torch.zeros(k * self.D + k, dtype=self.acc, device=dev),
-                    "event": torch.cuda.Event(),
-                })
-            # FMLX_KMEANS_SIDE_PRIO=1: the side stream at high priority, so its blocks are dispatched
-            # as soon as assign blocks retire instead of after the assign grid drains (A/B knob)
-            from ..utils import graphs as _graphs
-
-            self.side = _graphs.aux_stream(dev, "kmeans-split",
-                                           -1 if os.environ.get("FMLX_KMEANS_SIDE_PRIO", "0") == "1" else 0)
         if dev.type == "cuda" and not self.stable and not self.group:
             # more keys than the counting sort's LDS histograms hold: the stable segmented LSD radix
             # sort (radix.hip, one segment) over ceil(log2 k) bits, buffers allocated once
@@ -290,8 +255,6 @@ class KMeansRound:
         if self.n == 0:
             self.payload.zero_()
             return self.payload
-        if self.parts:
-            return self._run_split(cb)
         assign(X, cb, self.metric, self.labels)
         stream = native.stream_ptr(X.device)
         if self.stable:
@@ -328,36 +291,6 @@ class KMeansRound:
         native.call("fmlx_kmeans_cluster_sum", int(self.acc == torch.float64), native.ptr(self.partial), self.D,
                     native.ptr(offsets), native.ptr(chunk_off), self.k, native.ptr(self.payload),
                     native.stream_ptr(X.device))
-        return self.payload
-
-    def _run_split(self, cb: CentroidBuffers) -> torch.Tensor:
-        """The round over SPLIT_PARTS row parts: assign of part p + 1 (main stream) overlaps the
-        stable grouping, gather-sum and cluster sums of part p (side stream); fork / join by
-        events, so the whole round stays one capturable hipGraph."""
-        X, k, D = self.X, self.k, self.D
-        main = torch.cuda.current_stream(X.device)
-        side = self.side
-        side.wait_stream(main)  # centroids of this round, buffers of the last
-        for p in self.parts:
-            r0, r1 = p["r0"], p["r1"]
-            assign(X[r0:r1], cb, self.metric, self.labels[r0:r1])
-            p["event"].record(main)
-            with torch.cuda.stream(side):
-                side.wait_event(p["event"])
-                st = native.stream_ptr(X.device)
-                Xp = X[r0:r1]
-                native.call("fmlx_group_by_key_stable", native.ptr(self.labels[r0:r1]), r1 - r0, k, CHUNK,
-                            native.ptr(p["gscratch"]), native.ptr(p["offsets"]), native.ptr(p["chunk_off"]),
-                            native.ptr(p["order32"]), st)
-                native.call("fmlx_kmeans_chunk_sum_bf16v", native.ptr(Xp), Xp.stride(0), D, native.ptr(p["order32"]),
-                            native.ptr(p["offsets"]), native.ptr(p["chunk_off"]), k, p["max_chunks"],
-                            native.ptr(p["partial"]), st)
-                native.call("fmlx_kmeans_cluster_sum", int(self.acc == torch.float64), native.ptr(p["partial"]), D,
-                            native.ptr(p["offsets"]), native.ptr(p["chunk_off"]), k, native.ptr(p["payload"]), st)
-        main.wait_stream(side)
-        self.payload.copy_(self.parts[0]["payload"])
-        for p in self.parts[1:]:  # fixed part order: bit-reproducible
-            self.payload.add_(p["payload"])
         return self.payload
 
     def finalize(self, cb: CentroidBuffers, payload: torch.Tensor) -> None:

@@ -96,6 +96,12 @@ _KERNEL_SIGS = {
     "fmlx_csc_sort_split": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
                             c_long, c_void_p, c_void_p, c_long, c_void_p, c_long, c_int, c_void_p],
     "fmlx_csc_colptr": [c_void_p, c_long, c_int, c_int, c_void_p, c_long, c_void_p, c_void_p],
+    # blas.hip set-up helpers
+    "fmlx_fill32": [c_void_p, c_long, ctypes.c_uint, c_void_p],
+    "fmlx_csr_batch_bounds": [c_void_p, c_long, c_long, c_long, c_void_p, c_void_p],
+    "fmlx_host_register": [c_void_p, c_long],
+    "fmlx_host_unregister": [c_void_p],
+    "fmlx_memcpy_h2d": [c_void_p, c_void_p, c_long, c_void_p],
 }
 
 _HOST_SIGS = {}
@@ -194,6 +200,25 @@ def host():
             _apply_sigs(lib, _HOST_SIGS, restype=None)
             _HLIB = lib
     return _HLIB
+
+
+def zeros(shape, dtype, device) -> torch.Tensor:
+    """``torch.zeros`` on the GPU through the library's own (preloaded) fill kernel: torch's fill
+    kernels load their code object lazily on first use (tens of ms inside a fit)."""
+    t = torch.empty(shape, dtype=dtype, device=device)
+    nbytes = t.numel() * t.element_size()
+    if t.device.type != "cuda":
+        return t.zero_()
+    if nbytes % 4:
+        return t.zero_()
+    call("fmlx_fill32", t.data_ptr(), nbytes // 4, 0, stream_ptr(t.device))
+    return t
+
+
+def fill_i32(t: torch.Tensor, value: int) -> torch.Tensor:
+    """In-place fill of a contiguous int32 CUDA tensor (library kernel)."""
+    call("fmlx_fill32", t.data_ptr(), t.numel(), int(value) & 0xFFFFFFFF, stream_ptr(t.device))
+    return t
 
 
 def ptr(t) -> int:

@@ -43,6 +43,8 @@ native.register_host_sigs({
     "fmlx_dc_finish": ([_P], ctypes.c_int),
     "fmlx_dc_reopen": ([ctypes.c_char_p], ctypes.c_void_p),
     "fmlx_dc_close": ([_P, ctypes.c_int], None),
+    "fmlx_dc_record_ptr": ([_P, _I], ctypes.c_void_p),
+    "fmlx_dc_segment_mem": ([_P, _I, _P], ctypes.c_void_p),
 })
 
 DEFAULT_SEGMENT_BYTES = 1 << 30          # reference DataCacheWriter: segments up to 1 GB
@@ -100,6 +102,22 @@ class DataCache:
         if out.size:
             self.read_into(i, out)
         return out.tobytes()
+
+    def record_ptr(self, i: int) -> Optional[int]:
+        """Address of record ``i`` in a memory segment (None: it lives in a file segment)."""
+        p = native.host().fmlx_dc_record_ptr(self._h, i)
+        return int(p) if p else None
+
+    def memory_segments(self) -> List[tuple]:
+        """(address, capacity) of every memory-resident segment."""
+        out = []
+        stats = self.stats()
+        cap = ctypes.c_int64()
+        for idx in range(stats["segments"]):
+            p = native.host().fmlx_dc_segment_mem(self._h, idx, ctypes.byref(cap))
+            if p:
+                out.append((int(p), int(cap.value)))
+        return out
 
     def spill(self) -> None:
         rc = native.host().fmlx_dc_spill_all(self._h)

@@ -1,0 +1,43 @@
+"""Device → host reads without a blocking HIP wait.
+
+A blocking copy (``tensor.cpu()``, ``.item()``, ``.tolist()``) waits inside the HIP runtime on
+an HSA completion signal; in the sparse SVC whole-fit traces those waits sat in 4-ms
+``hsa_signal_wait_scacquire`` timeouts with the GPU idle (profiles/r4/svc_stall_systrace_summary.json).
+Here the copy is stream-ordered into pinned host memory (torch's caching host allocator: no
+hipHostMalloc after the first use of a size) and the host polls the completion event
+(``hipEventQuery``: a load of the signal value, no wait), yielding the CPU between polls only
+after a spin budget.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+SPIN_POLLS = 20000  # ≈ tens of µs of busy polling before the poll loop starts yielding
+
+
+def wait_event(ev: "torch.cuda.Event") -> None:
+    """Returns once ``ev`` has completed, by polling (never a blocking runtime wait)."""
+    i = 0
+    while not ev.query():
+        i += 1
+        if i > SPIN_POLLS:
+            time.sleep(0)  # yield; still a poll, not a runtime wait
+
+
+def wait_stream(device=None) -> None:
+    """Completion of everything queued so far on the current stream of ``device``, polled."""
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(device))
+    wait_event(ev)
+
+
+def to_host(t: torch.Tensor) -> torch.Tensor:
+    """A pinned host copy of a device tensor, stream-ordered after the work that produces it."""
+    if t.device.type != "cuda":
+        return t
+    out = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    out.copy_(t, non_blocking=True)
+    wait_stream(t.device)
+    return out

@@ -18,7 +18,7 @@ def main():
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--k", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--sched", type=int, default=3, help="assign schedule (ops/kmeans.py ASSIGN_SCHED)")
+    ap.add_argument("--sched", type=int, default=1, help="assign schedule (ops/kmeans.py ASSIGN_SCHED: 1 pipelined, 0 plain)")
     a = ap.parse_args()
     from flink_ml_amd.ops import native
 
