@@ -110,6 +110,34 @@ def _java_mod(a, b):
     return math.fmod(a, b)
 
 
+def _sign(x):
+    """SIGN with Java's Math.signum / Integer.signum: NaN stays NaN, the input's type is kept."""
+    if x is None:
+        return None
+    if isinstance(x, float):
+        return x if x != x else float((x > 0) - (x < 0))
+    return (x > 0) - (x < 0)
+
+
+def _round(x, d=0):
+    """ROUND(x[, d]) as Flink: HALF_UP (ties away from zero) at d decimals (d < 0: tens, hundreds…),
+    keeping the input's type — ROUND(INT) is an INT (SQLite's built-in returns REAL). Doubles round
+    their shortest decimal representation (BigDecimal.valueOf), so ROUND(2.675, 2) = 2.68."""
+    from decimal import ROUND_HALF_UP, Decimal
+
+    if x is None or d is None:
+        return None
+    d = int(d)
+    if isinstance(x, float):
+        if x != x or x in (float("inf"), float("-inf")):
+            return x
+        return float(Decimal(repr(x)).quantize(Decimal(1).scaleb(-d), rounding=ROUND_HALF_UP)) if d >= 0 else \
+            float(Decimal(repr(x)).scaleb(d).quantize(Decimal(1), rounding=ROUND_HALF_UP).scaleb(-d))
+    if d >= 0:
+        return x
+    return int(Decimal(x).scaleb(d).quantize(Decimal(1), rounding=ROUND_HALF_UP).scaleb(-d))
+
+
 def _register_functions(con: sqlite3.Connection) -> None:
     def f1(fn):
         return lambda x: None if x is None else fn(x)
@@ -117,9 +145,11 @@ def _register_functions(con: sqlite3.Connection) -> None:
     for name, fn in (("SQRT", math.sqrt), ("LN", math.log), ("LOG10", math.log10), ("EXP", math.exp),
                      ("ABS", abs), ("SIN", math.sin), ("COS", math.cos), ("TAN", math.tan)):
         con.create_function(name, 1, f1(fn), deterministic=True)
-    for name, fn in (("CEIL", math.ceil), ("CEILING", math.ceil), ("FLOOR", math.floor),
-                     ("SIGN", lambda x: (x > 0) - (x < 0))):
+    for name, fn in (("CEIL", math.ceil), ("CEILING", math.ceil), ("FLOOR", math.floor)):
         con.create_function(name, 1, _keep_type(fn), deterministic=True)
+    con.create_function("SIGN", 1, _sign, deterministic=True)
+    con.create_function("ROUND", 1, _round, deterministic=True)
+    con.create_function("ROUND", 2, _round, deterministic=True)
     con.create_function("POWER", 2, lambda a, b: None if a is None or b is None else math.pow(a, b),
                         deterministic=True)
     con.create_function("MOD", 2, _java_mod, deterministic=True)

@@ -458,7 +458,9 @@ class _Eval:
             return float((math.ceil if name != "FLOOR" else math.floor)(a)) if isinstance(a, float) else a
         if name == "SIGN" and len(args) == 1:
             a = _num(args[0])
-            return torch.sign(a) if isinstance(a, torch.Tensor) else type(a)((a > 0) - (a < 0))
+            if isinstance(a, torch.Tensor):  # Math.signum: NaN stays NaN (torch.sign gives 0)
+                return torch.where(torch.isnan(a), a, torch.sign(a)) if a.dtype.is_floating_point else torch.sign(a)
+            return a if a != a else type(a)((a > 0) - (a < 0))
         if name == "POWER" and len(args) == 2:
             a, b = _num(args[0]), _num(args[1])
             if not isinstance(a, torch.Tensor):

@@ -307,6 +307,12 @@ def _batch_bounds(indptr: torch.Tensor, n: int, B: int):
     return val
 
 
+# the column-major copy's packed payload (column low bits above a 22-bit batch row: no key array
+# out of the high-bits pass); FMLX_CSC_PACK=0 forces the unpacked bucket pass (batches > 2^22 rows
+# take it anyway) — tests cover both
+CSC_PACK = os.environ.get("FMLX_CSC_PACK", "1") == "1"
+
+
 class BatchCsc:
     """Per-batch column-major copy of a CSR partition for atomic-free sparse SGD gradients.
 
@@ -443,7 +449,7 @@ class BatchCsc:
             # order and the column pointers — no key array, no sorted keys
             # a batch of ≤ 2^22 rows: the column's low 10 bits ride in the payload (bits 22..31 above
             # the row), so the high-bits pass writes no keys and the bucket pass reads none
-            pack = int(self.B <= (1 << 22))
+            pack = int(CSC_PACK and self.B <= (1 << 22))
             pay = torch.empty(m, dtype=torch.int64, device=dev)
             native.call("fmlx_csc_keys64", native.ptr(indptr), native.ptr(indices), native.ptr(values), r0, r1, self.B,
                         d, j0, None, native.ptr(pay), pack, stream)

@@ -116,6 +116,7 @@ def test_sparse_sgd_two_ranks_one_gpu():
 
 @pytest.mark.parametrize("run_max,vdtype,d,B,skew,bucket", [
     (1, torch.float32, 3_001, 1_000, False, True), (3, torch.float64, 3_001, 1_000, False, True),
+    (4, torch.float32, 3_001, 1_000, False, "unpacked"),   # the unpacked bucket pass
     (16, torch.float32, 3_001, 1_000, False, True),
     (16, torch.float32, 3_001, 1_000, False, False),      # two LSD passes + the column-pointer kernel
     (4, torch.float32, 700, 1_000, False, True),          # 10 column bits: one LSD pass
@@ -132,7 +133,8 @@ def test_batch_csc_device_transpose_matches_host(run_max, vdtype, d, B, skew, bu
     from flink_ml_amd.ops import glm as gk
 
     monkeypatch.setattr(gk, "CSC_RUN_MAX", run_max)
-    monkeypatch.setattr(gk, "CSC_BUCKET", bucket)
+    monkeypatch.setattr(gk, "CSC_BUCKET", bool(bucket))
+    monkeypatch.setattr(gk, "CSC_PACK", bucket != "unpacked")
     g = torch.Generator().manual_seed(0)
     n = 20_037
     lens = torch.randint(0, 12, (n,), generator=g)

@@ -82,6 +82,28 @@ def test_column_rules_on_both_engines():
     assert dev == expected and host == expected
 
 
+def test_round_of_int_and_sign_of_nan_on_both_engines():
+    """ROUND(INT) stays an INT on the SQLite engine too (its built-in returns REAL), and
+    SIGN(NaN) is NaN (Math.signum), not 0."""
+    t = _ints()
+    dev, host = _both("SELECT ROUND(i) AS r, SIGN(i) AS s FROM __THIS__", t)
+    expected = [(1, 1), (2, 1), (-1, -1), (-2, -1), (3, 1), (4, 1), (4, 1)]
+    assert host == expected and all(isinstance(r[0], int) for r in host)
+    assert dev == expected
+    tn = Table({"x": torch.tensor([float("nan"), -3.0, 0.0], dtype=torch.float64)}, num_rows=3)
+    from flink_ml_amd.models.feature.misc import _sign, run_sql
+
+    got = sql_device.evaluate("SELECT SIGN(x) AS s FROM __THIS__", tn).get_list("s")
+    assert got[0] != got[0] and got[1:] == [-1.0, 0.0]
+    # SQLite stores a NaN as NULL (it has no NaN), so the host engine sees SIGN(NULL); the function
+    # itself propagates NaN
+    assert _sign(float("nan")) != _sign(float("nan")) and _sign(-2.0) == -1.0 and _sign(3) == 1
+    r2 = run_sql("SELECT ROUND(x, 1) AS r FROM __THIS__", Table({"x": torch.tensor([2.25, -2.25, 1.05],
+                                                                                    dtype=torch.float64)},
+                                                                  num_rows=3)).get_list("r")
+    assert r2 == [2.3, -2.3, 1.1]
+
+
 def _nulls():
     return Table.from_rows([(0, 1.0, 3), (0, None, 4), (1, None, None), (1, None, 5), (2, 4.0, None)],
                            ["k", "x", "j"])
