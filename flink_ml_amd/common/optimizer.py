@@ -519,6 +519,24 @@ class DeviceGlmTrainer:
         e = int(st[0])
         return bool(st[1 + (e & 1)])
 
+    def _poll_stopped(self) -> bool:
+        """Non-blocking termination check: the device state copied to pinned memory at the previous
+        check is read if that copy has landed, and a new copy is queued. A stop is seen one check
+        interval late at worst — the rounds launched meanwhile are predicated off on the device —
+        and the host never waits for the GPU mid-fit (a blocking check drained the launch queue)."""
+        stopped = False
+        ev = getattr(self, "_state_ev", None)
+        if ev is not None and ev.query():
+            st = self._state_host
+            stopped = bool(st[6]) if self.defer else not bool(st[1 + (int(st[0]) & 1)])
+        if ev is None:
+            self._state_host = torch.empty(self.state.shape, dtype=self.state.dtype, pin_memory=True)
+            self._state_ev = ev = torch.cuda.Event()
+        if ev.query():
+            self._state_host.copy_(self.state, non_blocking=True)
+            ev.record()
+        return stopped
+
     def rounds_executed(self) -> int:
         return int(self.state[4].item())
 
@@ -574,7 +592,12 @@ class DeviceGlmTrainer:
                                       kernel_ms=round(ev0.elapsed_time(ev1), 4),
                                       bytes_per_round=int(self.B * (self.d * self.X.element_size() if not self.sparse
                                                                     and not self.wide else 0)))
-                stop = done < self.sgd.max_iter and not self.running()
+                if done >= self.sgd.max_iter:
+                    stop = False
+                elif ck.mgr is not None or log:
+                    stop = not self.running()  # checkpoints / round logs read this round's state
+                else:
+                    stop = self._poll_stopped()  # never drains the queue (see _poll_stopped)
                 ck.maybe_save(done, lambda: {"coef": self.coef, "state": self.state,
                                              "done": stop or done >= self.sgd.max_iter})
                 if stop:
@@ -582,6 +605,8 @@ class DeviceGlmTrainer:
             self.flush()
         # the coefficients: one stream-ordered copy into pinned memory, completion polled — a host
         # sync point, after which the exchange's error word is final
-        coef = hostsync.to_host(self.coef).to(torch.float64).numpy()
+        # (widened on the device: a host-side conversion first-touches a fresh 8 MB array, ~2 ms of
+        # page faults in the first fit of a process; the pinned copy is already faulted in)
+        coef = hostsync.to_host(self.coef.to(torch.float64)).numpy()
         self.check_exchange()
         return coef

@@ -211,8 +211,6 @@ class StreamedGlmTrainer:
         self.inner = DeviceGlmTrainer(sgd, init_coef, first, self.y[:first.shape[0]], w0, loss, use_graph=False,
                                       check_every=check_every)
         self.check_every = max(1, int(check_every))
-        self._state_host = None
-        self._state_ev = None
 
     def _round(self, e: int) -> None:
         st, tr = self.store, self.inner
@@ -236,31 +234,13 @@ class StreamedGlmTrainer:
         if self.ring is not None and st.P and not st.is_resident(b):
             self.ring.release()
 
-    def _stopped(self) -> bool:
-        """Non-blocking termination check: the state copy queued at the previous check, if landed."""
-        stopped = False
-        if self._state_ev is not None and self._state_ev.query():
-            st = self._state_host
-            if self.inner.defer:
-                stopped = bool(st[6])
-            else:
-                e = int(st[0])
-                stopped = not bool(st[1 + (e & 1)])
-        if self._state_host is None:
-            self._state_host = torch.empty(self.inner.state.shape, dtype=self.inner.state.dtype, pin_memory=True)
-            self._state_ev = torch.cuda.Event()
-        if self._state_ev.query():
-            self._state_host.copy_(self.inner.state, non_blocking=True)
-            self._state_ev.record()
-        return stopped
-
     def fit(self) -> np.ndarray:
         from ..utils import hostsync, tracing
 
         with tracing.range("sgd.fit.streamed"):
             for e in range(self.sgd.max_iter):
                 self._round(e)
-                if (e + 1) % self.check_every == 0 and self._stopped():
+                if (e + 1) % self.check_every == 0 and self.inner._poll_stopped():
                     break
             self.inner.flush()
         coef = hostsync.to_host(self.inner.coef).to(torch.float64).numpy()

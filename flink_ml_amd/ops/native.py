@@ -180,6 +180,10 @@ def _preload(lib) -> None:
     PRELOAD_MS = (time.perf_counter() - t0) * 1e3
     if k < 0:
         raise RuntimeError("preloading the kernel library's code objects failed (%d)" % k)
+    from ..utils import hostsync
+
+    hostsync.warm(torch.cuda.current_device())  # pinned read-back block + first-use imports
+    PRELOAD_MS = (time.perf_counter() - t0) * 1e3
     PRELOAD_OBJECTS = k
 
 

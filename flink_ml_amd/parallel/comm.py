@@ -57,9 +57,7 @@ def all_reduce(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
 
 def _all_reduce(t: torch.Tensor, op: str, ctx) -> torch.Tensor:
     if op == "sum" and t.is_cuda:
-        from . import xgmi
-
-        x = xgmi.get()
+        x = _xgmi().get()
         if x is not None and x.accepts(t):
             return x.all_reduce_(t)  # one-shot xGMI kernel (small payloads, bit-identical on all ranks)
     rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN,
@@ -82,9 +80,15 @@ def check_collectives() -> None:
     """Raises if an earlier one-shot xGMI collective of this process gave up waiting for a peer
     (its output was poisoned with NaN). No device sync: call it after a host sync point so the
     kernels in question have finished."""
+    _xgmi().check()
+
+
+def _xgmi():
+    # imported on first use (parallel/xgmi.py imports this package's context); the module import
+    # itself is cheap, but a first import inside a fit was a few ms of its wall time
     from . import xgmi
 
-    xgmi.check()
+    return xgmi
 
 
 def all_reduce_scalar(x: float, op: str = "sum", dtype=torch.float64) -> float:

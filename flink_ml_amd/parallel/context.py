@@ -128,10 +128,11 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> SPM
                            forced=forced)
         if _CTX.is_distributed and _CTX.is_gpu and world > 1:
             _CTX.sharers = _measure_sharers(_CTX)
-    if _CTX.is_distributed and _CTX.is_gpu and backend == "nccl":
-        from . import xgmi
+    if _CTX.is_gpu:
+        from . import xgmi  # noqa: F401  (imported here, at set-up, not inside the first fit)
 
-        xgmi.get()  # collective set-up of the one-shot xGMI exchange, at a point every rank reaches
+        if _CTX.is_distributed and backend == "nccl":
+            xgmi.get()  # collective set-up of the one-shot xGMI exchange, at a point every rank reaches
     return _CTX
 
 

@@ -41,3 +41,23 @@ def to_host(t: torch.Tensor) -> torch.Tensor:
     out.copy_(t, non_blocking=True)
     wait_stream(t.device)
     return out
+
+
+WARM_PINNED_BYTES = 64 << 20
+
+
+def warm(device=None) -> None:
+    """One-time set-up of the read-back path, done at library load instead of inside the first
+    fit: a pinned block in torch's caching host allocator (later read-backs up to its size reuse
+    it instead of a hipHostMalloc each), and one large copy each way (the runtime brings up its
+    copy engine queues on the first large copy: ~2 ms per copy inside the first sparse-SVC fit),
+    plus the event machinery's first-use imports."""
+    dev = torch.device(device if device is not None else "cuda")
+    buf = torch.empty(WARM_PINNED_BYTES, dtype=torch.uint8, pin_memory=True)
+    big = 8 << 20
+    d = torch.empty(big, dtype=torch.uint8, device=dev)
+    d.copy_(buf[:big], non_blocking=True)
+    buf[:big].copy_(d, non_blocking=True)
+    buf[:16].copy_(d[:16], non_blocking=True)
+    wait_stream(dev)
+    del buf, d
