@@ -13,6 +13,17 @@
 //               the bins (key[i−1], key[i]] (each bin exactly once), relative to its batch's first
 //               entry, which is indptr[batch·B] − j0 (a batch's entries are its own CSR range)
 //
+// and, for the tiled backward (glm.hip glm_csc_tile_bwd_kernel), a post-pass over each built batch:
+//
+//   csc_tiles      the batch's columns cut into tiles: runs of consecutive columns holding at most
+//                  ET = EB + EL entries, or one "heavy" column of more than EL entries (start flags
+//                  from the column pointer: per-chunk counts, their scan, the starts written)
+//   csc_tile_keys  per entry: key = tile · 2^(rb+pb) | row · 2^pb | position in the tile's
+//                  column-ordered range (pb bits), payload = the fp32 value bits / the entry index
+//   (stable radix sort of the keys' tile and row bits: entries row-sorted inside their tile)
+//   csc_tile_store erow := row | position << rb (the backward's packed LDS slot), evals in the
+//                  new order
+//
 // replacing ~10 torch ops and their run-sized temporaries (repeat_interleave of the row ids and
 // slots, int64 sort indices, gather copies, the bucket-start array and its two slicing copies):
 // a whole fit that transposes its batches lazily pays for those allocations inside the fit.
@@ -163,6 +174,143 @@ __global__ __launch_bounds__(256) void csc_colptr_kernel(const int* __restrict__
   }
 }
 
+// ---------------------------- row-sorted column tiles ----------------------------------------
+constexpr int TL_THREADS = 1024;
+
+// column c starts a tile: the first column, a heavy column (> EL entries) or the one after it, or
+// the column whose first entry falls in a later EB-entry bucket than its predecessor's. A light
+// tile's columns then start inside one bucket, so it holds < EB + (its last column's ≤ EL)
+// entries; tiles average about EB entries.
+__device__ __forceinline__ bool tile_start(const int* __restrict__ cp, int c, int EB, int EL) {
+  if (c == 0) return true;
+  const int a = cp[c - 1], b = cp[c], z = cp[c + 1];
+  return z - b > EL || b - a > EL || b / EB != a / EB;
+}
+
+// three passes over a batch's columns, TL_CHUNK per block: count the tile starts of every chunk,
+// scan the chunk counts (one block per batch), write the starts at the scanned offsets. (One block
+// walking the 1M column pointers of a batch serially took ~0.4 ms per batch.)
+constexpr int TL_CHUNK = 256;
+
+__device__ __forceinline__ int chunk_rank(bool f, int& total) {  // exclusive rank of f in the block
+  __shared__ int wc[TL_CHUNK / 64];
+  const unsigned long long m = __ballot(f);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) wc[w] = __popcll(m);
+  __syncthreads();
+  int off = 0;
+  total = 0;
+#pragma unroll
+  for (int i = 0; i < TL_CHUNK / 64; ++i) {
+    off += i < w ? wc[i] : 0;
+    total += wc[i];
+  }
+  return off + __popcll(m & ((1ull << lane) - 1));
+}
+
+__global__ __launch_bounds__(TL_CHUNK) void csc_tiles_count_kernel(const int* __restrict__ colptr, long b0, int d,
+                                                                   int EB, int EL, int nchunks, int* __restrict__ cnt) {
+  const long b = b0 + blockIdx.y;
+  const int c = blockIdx.x * TL_CHUNK + threadIdx.x;
+  const bool f = c < d && tile_start(colptr + b * (long)(d + 1), c, EB, EL);
+  int total;
+  chunk_rank(f, total);
+  if (threadIdx.x == 0) cnt[(long)blockIdx.y * nchunks + blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(TL_THREADS) void csc_tiles_scan_kernel(int* __restrict__ cnt, int nchunks, long b0, int d,
+                                                                    int* __restrict__ tiles, int tstride,
+                                                                    int* __restrict__ ntiles) {
+  int* __restrict__ cc = cnt + (long)blockIdx.x * nchunks;
+  const int per = (nchunks + TL_THREADS - 1) / TL_THREADS;
+  const int i0 = (int)threadIdx.x * per;
+  int loc = 0;
+  for (int i = i0; i < i0 + per && i < nchunks; ++i) loc += cc[i];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int inc = loc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
+  }
+  __shared__ int wtot[TL_THREADS / 64];
+  if (lane == 63) wtot[w] = inc;
+  __syncthreads();
+  int off = inc - loc;
+  for (int i = 0; i < w; ++i) off += wtot[i];
+  for (int i = i0; i < i0 + per && i < nchunks; ++i) {  // counts → exclusive offsets, in place
+    const int v = cc[i];
+    cc[i] = off;
+    off += v;
+  }
+  if (threadIdx.x == TL_THREADS - 1) {
+    const long b = b0 + blockIdx.x;
+    const int nt = off < tstride - 1 ? off : tstride - 1;  // (bounded by construction)
+    tiles[b * (long)tstride + nt] = d;
+    ntiles[b] = nt;
+  }
+}
+
+__global__ __launch_bounds__(TL_CHUNK) void csc_tiles_write_kernel(const int* __restrict__ colptr, long b0, int d,
+                                                                   int EB, int EL, int nchunks,
+                                                                   const int* __restrict__ offs,
+                                                                   int* __restrict__ tiles, int tstride) {
+  const long b = b0 + blockIdx.y;
+  const int c = blockIdx.x * TL_CHUNK + threadIdx.x;
+  const bool f = c < d && tile_start(colptr + b * (long)(d + 1), c, EB, EL);
+  int total;
+  const int r = chunk_rank(f, total) + offs[(long)blockIdx.y * nchunks + blockIdx.x];
+  if (f && r < tstride - 1) tiles[b * (long)tstride + r] = c;
+}
+
+// one block per tile (grid-strided over the run's batches' tiles, batch by blockIdx.y)
+template <typename V>
+__global__ __launch_bounds__(256) void csc_tile_keys_kernel(const int* __restrict__ colptr, long b0, int d,
+                                                            const int* __restrict__ tiles, int tstride,
+                                                            const int* __restrict__ ntiles, const long* __restrict__ bstart,
+                                                            const int* __restrict__ erow, const V* __restrict__ evals,
+                                                            long j0, int rb, int pb, int EL, uint64_t* __restrict__ keys,
+                                                            uint32_t* __restrict__ pay) {
+  const long b = b0 + blockIdx.y;
+  const int* __restrict__ cp = colptr + b * (long)(d + 1);
+  const int* __restrict__ tl = tiles + b * (long)tstride;
+  const long base = bstart[blockIdx.y];  // the batch's first entry (absolute)
+  const int nt = ntiles[b];
+  for (int t = blockIdx.x; t < nt; t += gridDim.x) {
+    const int k0 = cp[tl[t]], k1 = cp[tl[t + 1]];
+    const bool heavy = tl[t + 1] - tl[t] == 1 && k1 - k0 > EL;
+    for (int k = k0 + (int)threadIdx.x; k < k1; k += 256) {
+      const long a = base + k;
+      const uint64_t pos = heavy ? 0 : (uint64_t)(k - k0);
+      keys[a - j0] = ((uint64_t)t << (rb + pb)) | ((uint64_t)(uint32_t)erow[a] << pb) | pos;
+      if constexpr (sizeof(V) == 4)
+        pay[a - j0] = __float_as_uint(evals[a]);
+      else
+        pay[a - j0] = (uint32_t)(a - j0);
+    }
+  }
+}
+
+// sorted order → erow (row | pos << rb) and evals (fp32: from the payload; fp64: gathered from a
+// copy of the run's values, `src`)
+template <typename V>
+__global__ __launch_bounds__(256) void csc_tile_store_kernel(const uint64_t* __restrict__ keys,
+                                                             const uint32_t* __restrict__ pay, long m, long j0, int rb,
+                                                             int pb, const V* __restrict__ src, int* __restrict__ erow,
+                                                             V* __restrict__ evals) {
+  const uint64_t rmask = (1ull << rb) - 1, pmask = (1ull << pb) - 1;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+    const uint64_t k = keys[i];
+    const uint32_t row = (uint32_t)((k >> pb) & rmask), pos = (uint32_t)(k & pmask);
+    erow[j0 + i] = (int)(row | (pos << rb));
+    if constexpr (sizeof(V) == 4)
+      evals[j0 + i] = __uint_as_float(pay[i]);
+    else
+      evals[j0 + i] = src[pay[i]];
+  }
+}
+
 inline unsigned grid_for(long work, long per_block, unsigned cap) {
   long g = (work + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -215,6 +363,56 @@ FMLX_API int fmlx_csc_colptr(const int* sorted_keys, long m, int slots, int d, c
   const long threads = m / 4 + 1;  // boundaries 0 … m
   hipLaunchKernelGGL(csc_colptr_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      sorted_keys, (int)m, slots, d, rs, b0, colptr);
+  return (int)hipGetLastError();
+}
+
+// Tiles of batches b0 … b0 + slots − 1 (colptr rows already built): tiles int32 [P][tstride]
+// (tstride ≥ min(d, nnz_b / EB + 2·(nnz_b / EL) + 1) + 1 bounds every batch's tile count: the
+// bucket changes plus two starts per heavy column), ntiles int32 [P].
+FMLX_API int fmlx_csc_tiles(const int* colptr, long b0, int slots, int d, int EB, int EL, int* tiles, int tstride,
+                            int* ntiles, int* scratch, long scratch_ints, void* stream) {
+  if (slots <= 0 || d <= 0 || EB <= 0 || EL <= 0 || tstride < 2) return -1;
+  const int nchunks = (d + TL_CHUNK - 1) / TL_CHUNK;
+  if (scratch_ints < (long)slots * nchunks) return -2;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(csc_tiles_count_kernel, dim3(nchunks, slots), dim3(TL_CHUNK), 0, s, colptr, b0, d, EB, EL, nchunks,
+                     scratch);
+  hipLaunchKernelGGL(csc_tiles_scan_kernel, dim3(slots), dim3(TL_THREADS), 0, s, scratch, nchunks, b0, d, tiles, tstride,
+                     ntiles);
+  hipLaunchKernelGGL(csc_tiles_write_kernel, dim3(nchunks, slots), dim3(TL_CHUNK), 0, s, colptr, b0, d, EB, EL, nchunks,
+                     scratch, tiles, tstride);
+  return (int)hipGetLastError();
+}
+
+FMLX_API long fmlx_csc_tiles_scratch(int slots, int d) { return (long)slots * ((d + TL_CHUNK - 1) / TL_CHUNK); }
+
+// Keys of a run's entries j0 … j0 + m − 1 (batch s starts at bstart[s], DEVICE array, absolute).
+// keys: uint64 [m]; pay: uint32 [m]. rb + pb ≤ 32 (the packed erow), pb ≥ bits(ET − 1).
+FMLX_API int fmlx_csc_tile_keys(int f64, const int* colptr, long b0, int slots, int d, const int* tiles, int tstride,
+                                const int* ntiles, const long* bstart, const int* erow, const void* evals, long j0,
+                                int rb, int pb, int EL, uint64_t* keys, uint32_t* pay, void* stream) {
+  if (slots <= 0 || rb < 1 || pb < 1 || rb + pb > 32) return -1;
+  const dim3 g(tstride < 1024 ? tstride : 1024, slots);
+  if (f64)
+    hipLaunchKernelGGL(csc_tile_keys_kernel<double>, g, dim3(256), 0, (hipStream_t)stream, colptr, b0, d, tiles,
+                       tstride, ntiles, bstart, erow, (const double*)evals, j0, rb, pb, EL, keys, pay);
+  else
+    hipLaunchKernelGGL(csc_tile_keys_kernel<float>, g, dim3(256), 0, (hipStream_t)stream, colptr, b0, d, tiles,
+                       tstride, ntiles, bstart, erow, (const float*)evals, j0, rb, pb, EL, keys, pay);
+  return (int)hipGetLastError();
+}
+
+FMLX_API int fmlx_csc_tile_store(int f64, const uint64_t* keys, const uint32_t* pay, long m, long j0, int rb, int pb,
+                                 const void* src, int* erow, void* evals, void* stream) {
+  if (m <= 0) return 0;
+  if (rb < 1 || pb < 1 || rb + pb > 32 || (f64 && src == nullptr)) return -1;
+  const dim3 g(grid_for(m, 256, 1u << 16));
+  if (f64)
+    hipLaunchKernelGGL(csc_tile_store_kernel<double>, g, dim3(256), 0, (hipStream_t)stream, keys, pay, m, j0, rb, pb,
+                       (const double*)src, erow, (double*)evals);
+  else
+    hipLaunchKernelGGL(csc_tile_store_kernel<float>, g, dim3(256), 0, (hipStream_t)stream, keys, pay, m, j0, rb, pb,
+                       (const float*)nullptr, erow, (float*)evals);
   return (int)hipGetLastError();
 }
 

@@ -1362,13 +1362,26 @@ __global__ __launch_bounds__(256) void glm_csr_fwd_kernel(const long* __restrict
 // products in entry order — deterministic, no atomics, no per-column dependent load chains.
 constexpr int CSC_CAP = 4096;  // entries staged per pass (16 KB fp32 / 32 KB fp64)
 
+// Σweight / Σloss of round e: fixed-order sum of the forward's WL_SLOTS slots (all 256 threads)
+template <typename A>
+__device__ __forceinline__ void slot_sums(const A* __restrict__ wl, int e, A& W, A& L) {
+  __shared__ A red[2][4];
+  const bool own = threadIdx.x < WL_SLOTS;  // (blocks of ≥ 256 threads)
+  const A* sl = wl + ((long)(e & 1) * WL_SLOTS + (own ? threadIdx.x : 0)) * WL_STRIDE;
+  const A w0 = wave_sum(own ? sl[0] : (A)0), l0 = wave_sum(own ? sl[1] : (A)0);
+  if ((threadIdx.x & 63) == 0 && own) { red[0][threadIdx.x >> 6] = w0; red[1][threadIdx.x >> 6] = l0; }
+  __syncthreads();
+  W = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+  L = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+}
+
 template <typename A, bool FUSE>
 __global__ __launch_bounds__(256) void glm_csc_bwd_kernel(const long* __restrict__ indptr,
                                                           const int* __restrict__ colptr, const int* __restrict__ erow,
                                                           const A* __restrict__ eval, const A* __restrict__ mult,
                                                           long n, int d, long B, int* __restrict__ state,
                                                           A* __restrict__ wl, A* __restrict__ fb, A* __restrict__ coef,
-                                                          int max_iter, A tol, A lr, A reg, A en) {
+                                                          int max_iter, A tol, A lr, A reg, A en, int weighted) {
   __shared__ A prod[CSC_CAP];
   int e;
   const bool run = round_running(state, e);
@@ -1388,18 +1401,17 @@ __global__ __launch_bounds__(256) void glm_csc_bwd_kernel(const long* __restrict
   const int* __restrict__ cp = colptr + b * (long)(d + 1);
   const int* __restrict__ er = erow + base;
   const A* __restrict__ ev = eval + base;
-  // Σweight / Σloss of the round: fixed-order sum of the forward's slots (identical in every block)
-  A W, L;
-  {
-    __shared__ A red[2][4];
-    const A* sl = wl + ((long)(e & 1) * WL_SLOTS + threadIdx.x) * WL_STRIDE;
-    A w0 = wave_sum(sl[0]), l0 = wave_sum(sl[1]);
-    if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = w0; red[1][threadIdx.x >> 6] = l0; }
-    __syncthreads();
-    W = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-    L = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  // Σweight of the round: the batch's row count when unweighted, else the fixed-order sum of the
+  // forward's slots (identical in every block). Σloss only feeds the termination test, which the
+  // last arriving block makes (and block 0 of the feedback path, which exports it).
+  A W, L = 0;
+  if (weighted || (!FUSE && blockIdx.x == 0)) {
+    slot_sums(wl, e, W, L);
   }
-  const bool cont = (e + 1 < max_iter) && (L / W > tol);
+  if (!weighted) {
+    const long end = (b + 1) * B < n ? (b + 1) * B : n;
+    W = (A)(end - b * B);
+  }
   for (int cb = blockIdx.x * 256; cb < d; cb += gridDim.x * 256) {
     const int c = cb + (int)threadIdx.x;
     const int ce = cb + 256 < d ? cb + 256 : d;
@@ -1441,7 +1453,199 @@ __global__ __launch_bounds__(256) void glm_csc_bwd_kernel(const long* __restrict
     fb[d] = W;
     fb[d + 1] = L;
   }
-  if (FUSE) arrive_and_advance(state, e, cont, 1);
+  if (FUSE) {
+    __shared__ int last;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      last = __hip_atomic_fetch_add(&state[ST_ARRIVE], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             (int)gridDim.x - 1;
+    __syncthreads();
+    if (last) {  // every other block has finished its reads of the state words (see arrive_and_advance)
+      A w2;
+      slot_sums(wl, e, w2, L);
+      if (threadIdx.x == 0) {
+        const bool cont = (e + 1 < max_iter) && (L / W > tol);
+        state[ST_RUN0 + ((e + 1) & 1)] = cont ? 1 : 0;
+        state[ST_EXECUTED] += 1;
+        state[ST_ROUND] = e + 1;
+        state[ST_ARRIVE] = 0;
+      }
+    }
+  }
+}
+
+// Tiled backward (BatchCsc tiles, csc_build.hip csc_tiles / csc_tile_keys / csc_tile_store): the
+// batch's columns are cut into tiles of ≤ ET entries (or one heavy column of > EL), and inside a light
+// tile the entries are sorted by ROW, each carrying its slot in the tile's column-ordered range
+// (erow = row | slot << rb). A block takes a tile: the multiplier gathers of consecutive lanes
+// then fall on the same or nearby cache lines (the one-column-block form gathers a random row per
+// lane: measured ~40 µs for 6.4M such 4-byte gathers, the cost scaling with distinct lines per
+// wave instruction), each product goes to its column-ordered LDS slot, and a thread per column
+// sums its slots in entry order — the same per-column order as the untiled kernel, so results
+// are deterministic. A heavy column is a block-strided sum with a fixed-order block reduction.
+constexpr int TILE_THREADS = 1024;
+constexpr int TILE_U = 8;     // entries per thread per gather step
+constexpr int TILE_COLS = 8;  // columns per thread whose pointers are prefetched
+
+template <typename A, bool FUSE>
+__global__ __launch_bounds__(TILE_THREADS) void glm_csc_tile_bwd_kernel(
+    const long* __restrict__ indptr, const int* __restrict__ colptr, const int* __restrict__ tiles,
+    const int* __restrict__ ntiles, int tstride, const int* __restrict__ erow, const A* __restrict__ eval,
+    const A* __restrict__ mult, long n, int d, long B, int rb, int EL, int* __restrict__ state, A* __restrict__ wl,
+    A* __restrict__ fb, A* __restrict__ coef, int max_iter, A tol, A lr, A reg, A en, int weighted) {
+  extern __shared__ unsigned char tile_smem[];
+  A* prod = reinterpret_cast<A*>(tile_smem);
+  __shared__ A hred[TILE_THREADS / 64];
+  int e;
+  const bool run = round_running(state, e);
+  if (blockIdx.x == 0 && threadIdx.x < WL_SLOTS) {
+    A* o = wl + ((long)((e + 1) & 1) * WL_SLOTS + threadIdx.x) * WL_STRIDE;
+    o[0] = 0;
+    o[1] = 0;
+  }
+  if (!run) {
+    if (FUSE) arrive_and_advance(state, e, false, 0);
+    return;
+  }
+  const long P = (n + B - 1) / B;
+  const long b = (long)(e % P);
+  const long base = indptr[b * B];
+  const int* __restrict__ cp = colptr + b * (long)(d + 1);
+  const int* __restrict__ tl = tiles + b * (long)tstride;
+  const int nt = ntiles[b];
+  const int* __restrict__ er = erow + base;
+  const A* __restrict__ ev = eval + base;
+  const uint32_t rmask = (1u << rb) - 1;
+  A W, L = 0;
+  if (weighted || (!FUSE && blockIdx.x == 0)) slot_sums(wl, e, W, L);
+  if (!weighted) {
+    const long end = (b + 1) * B < n ? (b + 1) * B : n;
+    W = (A)(end - b * B);
+  }
+  const int tid = threadIdx.x;
+  for (int t = blockIdx.x; t < nt; t += gridDim.x) {
+    const int c0 = tl[t], c1 = tl[t + 1];
+    const int k0 = cp[c0], k1 = cp[c1];
+    if (c1 - c0 == 1 && k1 - k0 > EL) {  // heavy column (block-uniform branch)
+      A g = 0;
+      for (int k = k0 + tid; k < k1; k += TILE_THREADS) {
+        const uint32_t x = (uint32_t)__builtin_nontemporal_load(er + k);
+        g += mult[x & rmask] * __builtin_nontemporal_load(ev + k);
+      }
+      g = wave_sum(g);
+      if ((tid & 63) == 0) hred[tid >> 6] = g;
+      __syncthreads();
+      if (tid == 0) {
+        A s = 0;
+        for (int i = 0; i < TILE_THREADS / 64; ++i) s += hred[i];
+        if (FUSE)
+          coef[c0] = sgd_apply<A>(coef[c0], s, W, lr, reg, en);
+        else
+          fb[c0] = s;
+      }
+      __syncthreads();
+      continue;
+    }
+    // the thread's columns of the tile (c0 + tid + i·TILE_THREADS, i < TILE_COLS): pointers and
+    // coefficients loaded before the gathers, so the column pass after the barrier reads only LDS
+    const bool few = c1 - c0 <= TILE_COLS * TILE_THREADS;  // (block-uniform)
+    int ca[TILE_COLS], cz[TILE_COLS];
+    A cw[TILE_COLS];
+    if (few) {
+#pragma unroll
+      for (int i = 0; i < TILE_COLS; ++i) {
+        const int c = c0 + tid + i * TILE_THREADS;
+        const int cc = c < c1 ? c : c0;
+        ca[i] = cp[cc];
+        cz[i] = c < c1 ? cp[cc + 1] : ca[i];
+        cw[i] = FUSE ? coef[cc] : (A)0;
+      }
+    }
+    // products into their column-ordered slots: TILE_U entries per thread per step, the next
+    // step's entries loaded before this step's multiplier gathers
+    uint32_t xx[TILE_U];
+    A vv[TILE_U];
+#pragma unroll
+    for (int u = 0; u < TILE_U; ++u) {
+      const int k = k0 + tid + u * TILE_THREADS;
+      const int kk = k < k1 ? k : k0;
+      xx[u] = (uint32_t)__builtin_nontemporal_load(er + kk);
+      vv[u] = __builtin_nontemporal_load(ev + kk);
+    }
+    for (int kb = k0 + tid; kb < k1; kb += TILE_U * TILE_THREADS) {
+      uint32_t nx[TILE_U];
+      A nv[TILE_U];
+      const int kn = kb + TILE_U * TILE_THREADS;
+      if (kn < k1) {
+#pragma unroll
+        for (int u = 0; u < TILE_U; ++u) {
+          const int k = kn + u * TILE_THREADS;
+          const int kk = k < k1 ? k : kn;
+          nx[u] = (uint32_t)__builtin_nontemporal_load(er + kk);
+          nv[u] = __builtin_nontemporal_load(ev + kk);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < TILE_U; ++u) {
+        const A p = mult[xx[u] & rmask] * vv[u];
+        if (kb + u * TILE_THREADS < k1) prod[xx[u] >> rb] = p;
+      }
+#pragma unroll
+      for (int u = 0; u < TILE_U; ++u) {
+        xx[u] = nx[u];
+        vv[u] = nv[u];
+      }
+    }
+    __syncthreads();
+    if (few) {
+#pragma unroll
+      for (int i = 0; i < TILE_COLS; ++i) {
+        const int c = c0 + tid + i * TILE_THREADS;
+        A g = 0;
+        for (int j = ca[i] - k0; j < cz[i] - k0; ++j) g += prod[j];
+        if (c < c1) {
+          if (FUSE)
+            coef[c] = sgd_apply<A>(cw[i], g, W, lr, reg, en);
+          else
+            fb[c] = g;
+        }
+      }
+    } else {
+      for (int c = c0 + tid; c < c1; c += TILE_THREADS) {
+        const int a = cp[c] - k0, z = cp[c + 1] - k0;
+        A g = 0;
+        for (int j = a; j < z; ++j) g += prod[j];
+        if (FUSE)
+          coef[c] = sgd_apply<A>(coef[c], g, W, lr, reg, en);
+        else
+          fb[c] = g;
+      }
+    }
+    __syncthreads();
+  }
+  if (!FUSE && blockIdx.x == 0 && tid == 0) {
+    fb[d] = W;
+    fb[d + 1] = L;
+  }
+  if (FUSE) {
+    __shared__ int last;
+    __syncthreads();
+    if (tid == 0)
+      last = __hip_atomic_fetch_add(&state[ST_ARRIVE], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             (int)gridDim.x - 1;
+    __syncthreads();
+    if (last) {
+      A w2;
+      slot_sums(wl, e, w2, L);
+      if (tid == 0) {
+        const bool cont = (e + 1 < max_iter) && (L / W > tol);
+        state[ST_RUN0 + ((e + 1) & 1)] = cont ? 1 : 0;
+        state[ST_EXECUTED] += 1;
+        state[ST_ROUND] = e + 1;
+        state[ST_ARRIVE] = 0;
+      }
+    }
+  }
 }
 
 // ---------------------------- host-side dispatch ------------------------------------------
@@ -1802,43 +2006,69 @@ FMLX_API int fmlx_glm_grad_csr(int acc_f64, const long* indptr, const int* idx, 
   return (int)hipGetLastError();
 }
 
-static int g_csc_fwd_cap = 65535, g_csc_bwd_cap = 1024;
+static int g_csc_fwd_cap = 65535, g_csc_bwd_cap = 1024, g_csc_tile_cap = 0;  // 0: CUs × tile blocks per CU
 FMLX_API void fmlx_glm_set_csc_tuning(int fwd_cap, int bwd_cap) {
   g_csc_fwd_cap = fwd_cap > 0 ? fwd_cap : 65535;
   g_csc_bwd_cap = bwd_cap > 0 ? bwd_cap : 1024;
+  g_csc_tile_cap = bwd_cap > 0 ? bwd_cap : 0;
 }
+
+// tiled backward: the column tiles of the batches (BatchCsc.tiles) and the packing of erow
+struct CscTiles {
+  const int* tiles;   // int32 [P][tstride] tile start columns (nullptr: untiled layout)
+  const int* ntiles;  // int32 [P]
+  int tstride, rb, EL, ET;  // EL: heavy-column threshold (entries)
+};
 FMLX_API int fmlx_glm_wl_elems() { return 2 * WL_SLOTS * WL_STRIDE; }
 
 template <typename A, int G>
 static void launch_csc_round(const long* indptr, const int* idx, const A* val, const A* y, const A* wt, A* coef,
                              long n, int d, long B, int loss, int* state, A* mult, A* wl, const int* colptr,
                              const int* erow, const A* eval, A* fb, int fuse, int max_iter, A tol, A lr, A reg, A en,
-                             hipStream_t s) {
-  long groups = B < n ? B : n;
+                             const CscTiles& ti, hipStream_t s) {
+  const long groups = B < n ? B : n;
   long fb_blocks = (groups * G + 255) / 256;  // one row per lane group: the batch in one pass
   if (fb_blocks > g_csc_fwd_cap) fb_blocks = g_csc_fwd_cap;
   if (fb_blocks < 1) fb_blocks = 1;
   hipLaunchKernelGGL((glm_csr_fwd_kernel<A, G>), dim3((int)fb_blocks), dim3(256), 0, s, indptr, idx, val, y, wt,
                      (const A*)coef, n, B, loss, state, mult, wl);
+  const int weighted = wt != nullptr;
+  if (ti.tiles != nullptr) {
+    const size_t lds = (size_t)ti.ET * sizeof(A);
+    int per_cu = (int)(LDS_PER_CU / (lds + 2048));
+    per_cu = per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu);  // ≤ 32 waves per CU at 1024 threads
+    int tb = g_csc_tile_cap > 0 ? g_csc_tile_cap : NUM_CU * per_cu;
+    if (tb > ti.tstride) tb = ti.tstride;
+    if (fuse)
+      hipLaunchKernelGGL((glm_csc_tile_bwd_kernel<A, true>), dim3(tb), dim3(TILE_THREADS), lds, s, indptr, colptr,
+                         ti.tiles, ti.ntiles, ti.tstride, erow, eval, (const A*)mult, n, d, B, ti.rb, ti.EL, state, wl,
+                         fb, coef, max_iter, tol, lr, reg, en, weighted);
+    else
+      hipLaunchKernelGGL((glm_csc_tile_bwd_kernel<A, false>), dim3(tb), dim3(TILE_THREADS), lds, s, indptr, colptr,
+                         ti.tiles, ti.ntiles, ti.tstride, erow, eval, (const A*)mult, n, d, B, ti.rb, ti.EL, state, wl,
+                         fb, coef, max_iter, tol, lr, reg, en, weighted);
+    return;
+  }
   int bb = (d + 255) / 256;  // grid-strided: each block takes the arrival ticket once
   if (bb > g_csc_bwd_cap) bb = g_csc_bwd_cap;
   if (fuse)
     hipLaunchKernelGGL((glm_csc_bwd_kernel<A, true>), dim3(bb), dim3(256), 0, s, indptr, colptr, erow, eval,
-                       (const A*)mult, n, d, B, state, wl, fb, coef, max_iter, tol, lr, reg, en);
+                       (const A*)mult, n, d, B, state, wl, fb, coef, max_iter, tol, lr, reg, en, weighted);
   else
     hipLaunchKernelGGL((glm_csc_bwd_kernel<A, false>), dim3(bb), dim3(256), 0, s, indptr, colptr, erow, eval,
-                       (const A*)mult, n, d, B, state, wl, fb, coef, max_iter, tol, lr, reg, en);
+                       (const A*)mult, n, d, B, state, wl, fb, coef, max_iter, tol, lr, reg, en, weighted);
 }
 
 template <typename A>
 static int dispatch_csc_round(int G, const long* indptr, const int* idx, const void* val, const void* y,
                               const void* wt, void* coef, long n, int d, long B, int loss, int* state, void* mult,
                               void* wl, const int* colptr, const int* erow, const void* eval, void* fb, int fuse,
-                              int max_iter, double tol, double lr, double reg, double en, hipStream_t s) {
+                              int max_iter, double tol, double lr, double reg, double en, const CscTiles& ti,
+                              hipStream_t s) {
 #define FMLX_CSC(GG)                                                                                                 \
   launch_csc_round<A, GG>(indptr, idx, (const A*)val, (const A*)y, (const A*)wt, (A*)coef, n, d, B, loss, state,     \
                           (A*)mult, (A*)wl, colptr, erow, (const A*)eval, (A*)fb, fuse, max_iter, (A)tol, (A)lr,     \
-                          (A)reg, (A)en, s)
+                          (A)reg, (A)en, ti, s)
   switch (G) {
     case 4: FMLX_CSC(4); break;
     case 8: FMLX_CSC(8); break;
@@ -1857,14 +2087,23 @@ static int dispatch_csc_round(int G, const long* indptr, const int* idx, const v
 FMLX_API int fmlx_glm_csc_round(int acc_f64, int G, const long* indptr, const int* idx, const void* val,
                                 const void* y, const void* wt, void* coef, long n, int d, long B, int loss, int* state,
                                 void* mult, void* wl, const int* colptr, const int* erow, const void* eval, void* fb,
-                                int fuse, int max_iter, double tol, double lr, double reg, double en, void* stream) {
+                                int fuse, int max_iter, double tol, double lr, double reg, double en,
+                                const int* tiles, const int* ntiles, int tstride, int rb, int EL, int ET,
+                                void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (n <= 0 || B <= 0) return -2;
+  const CscTiles ti{tiles, ntiles, tstride, rb, EL, ET};
+  if (tiles != nullptr) {
+    const size_t esz = acc_f64 ? 8 : 4;
+    // the packed erow (row | slot << rb) and the LDS slot array of a light tile (< ET entries)
+    if (rb < 1 || ET < 2 || EL < 1 || EL >= ET || tstride < 2 || (size_t)ET * esz > (size_t)LDS_PER_CU - 1024) return -3;
+    if (((long)ET - 1) >> (32 - rb) != 0 || (B - 1) >> rb != 0) return -4;
+  }
   if (acc_f64)
     return dispatch_csc_round<double>(G, indptr, idx, val, y, wt, coef, n, d, B, loss, state, mult, wl, colptr, erow,
-                                      eval, fb, fuse, max_iter, tol, lr, reg, en, s);
+                                      eval, fb, fuse, max_iter, tol, lr, reg, en, ti, s);
   return dispatch_csc_round<float>(G, indptr, idx, val, y, wt, coef, n, d, B, loss, state, mult, wl, colptr, erow,
-                                   eval, fb, fuse, max_iter, tol, lr, reg, en, s);
+                                   eval, fb, fuse, max_iter, tol, lr, reg, en, ti, s);
 }
 
 FMLX_API int fmlx_glm_csr_predict(int acc_f64, const long* indptr, const int* idx, const void* val, const void* coef,

@@ -313,6 +313,28 @@ def _batch_bounds(indptr: torch.Tensor, n: int, B: int):
 CSC_PACK = os.environ.get("FMLX_CSC_PACK", "1") == "1"
 
 
+TILE_HEAVY_DIV = int(os.environ.get("FMLX_CSC_TILE_HEAVY_DIV", "8"))  # heavy column: > ET / this entries
+# a fit tiles its batches when it visits each at least this often (the tiling costs about as much
+# as TILE_MIN_VISITS rounds save: ~0.15 ms per 6.4M-entry batch vs ~13 µs per round, svc shape)
+TILE_MIN_VISITS = int(os.environ.get("FMLX_CSC_TILE_MIN_VISITS", "16"))
+
+
+def csc_tile_entries(B: int, f64: bool) -> int:
+    """Entry capacity ET of a light column tile of the tiled backward (0 = untiled layout): the
+    LDS slot array of one block (128 KiB: 32768 fp32 / 16384 fp64 slots by default; FMLX_CSC_TILE
+    overrides, 0 disables), bounded so that the packed erow (batch row | slot << row bits) fits
+    32 bits."""
+    want = int(os.environ.get("FMLX_CSC_TILE", "-1"))
+    if want == 0:
+        return 0
+    least = 16 if want > 0 else 1024  # (small explicit tiles: tests)
+    if want < 0:
+        want = 16384 if f64 else 32768
+    rb = max(1, int(B - 1).bit_length())
+    et = min(want, 1 << (32 - rb) if rb < 32 else 1)
+    return et if et >= least else 0
+
+
 class BatchCsc:
     """Per-batch column-major copy of a CSR partition for atomic-free sparse SGD gradients.
 
@@ -343,6 +365,20 @@ class BatchCsc:
         self._want = max(1, min(cap, self.P))
         self.colptr = self.erow = self.evals = None
         self.version = 0
+        # row-sorted column tiles (glm.hip glm_csc_tile_bwd_kernel; CUDA partitions only)
+        self.ET = csc_tile_entries(B, values.dtype == torch.float64) if values.device.type == "cuda" else 0
+        # a column of more than EL entries is a tile of its own (block-strided sum); light tiles
+        # start inside one EB-entry bucket, so they hold ≤ EB + EL = ET entries (≈ EB on average)
+        self.EL = max(1, self.ET // TILE_HEAVY_DIV)
+        self.EB = max(1, self.ET - self.EL)
+        self.rb = max(1, int(B - 1).bit_length())
+        self.pb = max(1, int(self.ET - 1).bit_length())
+        if self.ET:
+            most = max(bounds[i + 1] - bounds[i] for i in range(self.P)) if self.P else 0
+            self.tstride = min(d, most // self.EB + 2 * (most // self.EL) + 1) + 1
+        else:
+            self.tstride = 0
+        self.tiles = self.ntiles = None
 
     @staticmethod
     def pick_group(avg_nnz: float) -> int:
@@ -364,8 +400,16 @@ class BatchCsc:
             return None
         if max(bounds[i + 1] - bounds[i] for i in range(P)) >= 2 ** 31:
             return None
-        return BatchCsc(BatchCsc.pick_group(nnz / max(n, 1)), bounds, indptr, indices, values, n, d, B,
-                        P if max_rounds is None else int(max_rounds))
+        csc = BatchCsc(BatchCsc.pick_group(nnz / max(n, 1)), bounds, indptr, indices, values, n, d, B,
+                       P if max_rounds is None else int(max_rounds))
+        if csc.ET and max_rounds is not None and max_rounds < TILE_MIN_VISITS * P:
+            csc.untiled()  # too few visits per batch to pay back the tiling sort
+        return csc
+
+    def untiled(self) -> None:
+        """Keeps the plain column-major layout (before any batch is built)."""
+        assert self.cap == 0
+        self.ET = self.EL = self.EB = self.tstride = 0
 
     @staticmethod
     def build(indptr, indices, values, n: int, d: int, B: int):
@@ -386,13 +430,21 @@ class BatchCsc:
         colptr = torch.empty((cap, self.d + 1), dtype=torch.int32, device=dev)
         erow = torch.empty(max(ne, 1), dtype=torch.int32, device=dev)
         evals = torch.empty(max(ne, 1), dtype=values.dtype, device=dev)
+        tiles = ntiles = None
+        if self.ET:
+            tiles = torch.empty((cap, self.tstride), dtype=torch.int32, device=dev)
+            ntiles = torch.empty(cap, dtype=torch.int32, device=dev)
         if self.cap:
             old = self.bounds[self.cap]
             colptr[:self.cap] = self.colptr
             erow[:old] = self.erow[:old]
             evals[:old] = self.evals[:old]
+            if tiles is not None:
+                tiles[:self.cap] = self.tiles
+                ntiles[:self.cap] = self.ntiles
             self.version += 1
         self.colptr, self.erow, self.evals, self.cap = colptr, erow, evals, cap
+        self.tiles, self.ntiles = tiles, ntiles
 
     def ensure(self, batches) -> None:
         """Transposes the listed batches that are not yet (idempotent; never inside a capture).
@@ -426,8 +478,39 @@ class BatchCsc:
             r0, r1 = b0 * B, min(b1 * B, n)
             if values.device.type == "cuda":
                 self._transpose_native(b0, len(run), r0, r1, j0, j1)
+                if self.ET:
+                    self._tile(b0, len(run), j0, j1)
             else:
                 self._transpose_torch(b0, len(run), r0, r1, j0, j1)
+
+    def _tile(self, b0, slots, j0, j1) -> None:
+        """Cuts the run's batches into column tiles and re-orders every tile's entries by row
+        (csc_build.hip csc_tiles / csc_tile_keys / radix sort / csc_tile_store)."""
+        import numpy as np
+
+        from . import sorting
+
+        values = self._src[2]
+        dev = values.device
+        m, d = j1 - j0, self.d
+        f64 = int(values.dtype == torch.float64)
+        stream = native.stream_ptr(dev)
+        lib = native.kernels()
+        cnt = torch.empty(max(1, int(lib.fmlx_csc_tiles_scratch(slots, d))), dtype=torch.int32, device=dev)
+        native.call("fmlx_csc_tiles", native.ptr(self.colptr), b0, slots, d, self.EB, self.EL, native.ptr(self.tiles),
+                    self.tstride, native.ptr(self.ntiles), native.ptr(cnt), cnt.numel(), stream)
+        bstart = torch.from_numpy(np.asarray(self.bounds[b0:b0 + slots], dtype=np.int64)).to(dev)
+        keys = torch.empty(m, dtype=sorting.U64, device=dev)
+        pay = torch.empty(m, dtype=torch.int32, device=dev)
+        native.call("fmlx_csc_tile_keys", f64, native.ptr(self.colptr), b0, slots, d, native.ptr(self.tiles),
+                    self.tstride, native.ptr(self.ntiles), native.ptr(bstart), native.ptr(self.erow),
+                    native.ptr(self.evals), j0, self.rb, self.pb, self.EL, native.ptr(keys), native.ptr(pay), stream)
+        tb = max(1, int(self.tstride - 1).bit_length())
+        seg = [self.bounds[b0 + s] - j0 for s in range(slots + 1)]
+        keys, pay = sorting.sort_u64(keys, pay, seg, self.pb, self.pb + self.rb + tb)
+        src = self.evals[j0:j1].clone() if f64 else None
+        native.call("fmlx_csc_tile_store", f64, native.ptr(keys), native.ptr(pay), m, j0, self.rb, self.pb,
+                    native.ptr(src), native.ptr(self.erow), native.ptr(self.evals), stream)
 
     def _transpose_native(self, b0, slots, r0, r1, j0, j1) -> None:
         import numpy as np
@@ -545,7 +628,8 @@ def csc_round(csc: BatchCsc, indptr, idx, val, y, wt, coef, n, d, B, loss, state
     native.call("fmlx_glm_csc_round", int(val.dtype == torch.float64), csc.G, native.ptr(indptr), native.ptr(idx),
                 native.ptr(val), native.ptr(y), native.ptr(wt), native.ptr(coef), n, d, B, loss, native.ptr(state),
                 native.ptr(mult), native.ptr(wl), native.ptr(csc.colptr), native.ptr(csc.erow), native.ptr(csc.evals),
-                native.ptr(fb), int(fuse), max_iter, tol, lr, reg, en, native.stream_ptr(val.device))
+                native.ptr(fb), int(fuse), max_iter, tol, lr, reg, en, native.ptr(csc.tiles), native.ptr(csc.ntiles),
+                csc.tstride, csc.rb, csc.EL, csc.ET, native.stream_ptr(val.device))
 
 
 # ---------------------------------------------------------------------------------------------

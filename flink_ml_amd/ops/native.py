@@ -79,7 +79,8 @@ _KERNEL_SIGS = {
     "fmlx_glm_wl_elems": [],
     "fmlx_glm_csc_round": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int,
                            c_long, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
-                           c_int, c_double, c_double, c_double, c_double, c_void_p],
+                           c_int, c_double, c_double, c_double, c_double, c_void_p, c_void_p, c_int, c_int, c_int,
+                           c_int, c_void_p],
     # sort.hip
     "fmlx_sorted_bounds": [c_void_p, c_long, c_int, c_void_p, c_void_p],
     "fmlx_seg_sort_scratch": ([c_void_p, c_int, c_int, c_int], c_long),
@@ -96,6 +97,13 @@ _KERNEL_SIGS = {
     "fmlx_csc_sort_split": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
                             c_long, c_void_p, c_void_p, c_long, c_void_p, c_long, c_int, c_void_p],
     "fmlx_csc_colptr": [c_void_p, c_long, c_int, c_int, c_void_p, c_long, c_void_p, c_void_p],
+    "fmlx_csc_tiles": [c_void_p, c_long, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_long,
+                       c_void_p],
+    "fmlx_csc_tiles_scratch": ([c_int, c_int], c_long),
+    "fmlx_csc_tile_keys": [c_int, c_void_p, c_long, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                           c_void_p, c_long, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "fmlx_csc_tile_store": [c_int, c_void_p, c_void_p, c_long, c_long, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                            c_void_p],
     # blas.hip set-up helpers
     "fmlx_fill32": [c_void_p, c_long, ctypes.c_uint, c_void_p],
     "fmlx_csr_batch_bounds": [c_void_p, c_long, c_long, c_long, c_void_p, c_void_p],

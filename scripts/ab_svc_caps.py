@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""A/B of the sparse SVC round's backward layout (untiled / row-sorted column tiles of ET entries,
+FMLX_CSC_TILE) and backward grid cap at the svc_sparse
+shard shape (scale 0.125: 6.25M x 1M, 64 nnz/row, batch 100k): steady
+rounds of a warmed trainer, interleaved repeats. One JSON line per (tile, bwd_cap, repeat). (Round 5 also measured a forward taking 2/4/8 rows per
+lane group: 0.0943-0.0977 ms vs 0.0899 for one row; removed.)"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer
+    from flink_ml_amd.ops import native
+    from flink_ml_amd.parallel.context import init_distributed
+    from flink_ml_amd.table import SparseColumn
+
+    ctx = init_distributed()
+    native.kernels()
+    dev = ctx.device
+    n, dim, nnz = 6_250_000, 1_000_000, 64
+    g = torch.Generator(device=dev).manual_seed(7)
+    idx = torch.empty((n, nnz), dtype=torch.int32, device=dev)
+    for s in range(0, n, 1 << 20):
+        e = min(s + (1 << 20), n)
+        idx[s:e] = torch.sort(torch.randint(0, dim, (e - s, nnz), generator=g, device=dev, dtype=torch.int32), 1).values
+    indptr = torch.arange(0, (n + 1) * nnz, nnz, dtype=torch.int64, device=dev)
+    vals = torch.rand((n * nnz,), generator=g, device=dev, dtype=torch.float32)
+    X = SparseColumn(indptr, idx.reshape(-1), vals, dim)
+    y = torch.randint(0, 2, (n,), generator=g, device=dev).to(torch.float32)
+    lib = native.kernels()
+    trainers = {}
+    for tile in (0, 16384, 32768):
+        os.environ["FMLX_CSC_TILE"] = str(tile)
+        tr = DeviceGlmTrainer(SGD(max_iter=10 ** 8, learning_rate=0.1, global_batch_size=100_000, tol=0.0),
+                              np.zeros(dim), X, y, None, "hinge", use_graph=False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tr.csc.ensure(range(tr.csc.P))
+        torch.cuda.synchronize()
+        print(json.dumps({"tile": tile, "build_ms": round((time.perf_counter() - t0) * 1e3, 1),
+                          "batches": tr.csc.P}), flush=True)
+        trainers[tile] = tr
+    cases = [(0, 1024)] + [(t, c) for t in (16384, 32768) for c in (0, 256, 512)]
+    for rep in range(2):
+        for tile, cap in cases:
+            tr = trainers[tile]
+            lib.fmlx_glm_set_csc_tuning(0, cap)
+            tr.run_rounds(20)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            tr.run_rounds(200)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) / 200 * 1e3
+            print(json.dumps({"tile": tile, "bwd_cap": cap, "rep": rep,
+                              "ms_per_round": round(ms, 4)}), flush=True)
+    lib.fmlx_glm_set_csc_tuning(0, 0)
+
+
+if __name__ == "__main__":
+    main()

@@ -61,6 +61,34 @@ def test_sparse_sgd_transpose_path_matches_host(graph):
             assert np.allclose(got, ref, atol=1e-10, rtol=1e-10), (loss, reg, en, np.abs(got - ref).max())
 
 
+@pytest.mark.parametrize("max_nnz", [40, 300])
+def test_sparse_weighted_and_unweighted_rounds_match_host(max_nnz):
+    """Short rows and rows spanning several load steps of a lane group, weighted and unweighted
+    (the backward takes Σweight from the row count when unweighted), with tol termination decided
+    on the device from the loss the last arriving block sums."""
+    _need_gpu()
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
+
+    n, d = 1900, 900
+    indptr, idx, vals, dense, y, w = _csr(n, d, 11 + max_nnz, max_nnz=max_nnz)
+    for wt in (None, w):
+        sgd = SGD(max_iter=8, learning_rate=0.1, global_batch_size=333, tol=1e-9, reg=0.05, elastic_net=0.5)
+        ref = TorchGlmTrainer(sgd, np.zeros(d), dense, y, wt, "logistic").fit()
+        tr = DeviceGlmTrainer(sgd, np.zeros(d), _sparse_col(indptr, idx, vals, d, "cuda"), y.cuda(),
+                              None if wt is None else wt.cuda(), "logistic")
+        assert tr.csc is not None
+        got = tr.fit()
+        assert tr.rounds_executed() == 8
+        assert np.allclose(got, ref, atol=1e-10, rtol=1e-10), np.abs(got - ref).max()
+    sgd2 = SGD(max_iter=200, learning_rate=1.0, global_batch_size=n, tol=0.3)
+    r2 = TorchGlmTrainer(sgd2, np.zeros(d), dense, y, None, "logistic")
+    c2 = r2.fit()
+    t2 = DeviceGlmTrainer(sgd2, np.zeros(d), _sparse_col(indptr, idx, vals, d, "cuda"), y.cuda(), None, "logistic")
+    g2 = t2.fit()
+    assert t2.rounds_executed() == r2.rounds
+    assert np.abs(g2 - c2).max() < 1e-8 * max(1.0, np.abs(c2).max())
+
+
 def test_sparse_sgd_fp32_transpose_vs_atomic_and_termination(monkeypatch):
     _need_gpu()
     from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
@@ -103,13 +131,19 @@ def _sparse_worker(rank, world):
     ref = TorchGlmTrainer(sgd, np.zeros(d), dense, y, w, "hinge").fit()
     tr = DeviceGlmTrainer(sgd, np.zeros(d), _sparse_col(indptr, idx, vals, d, "cuda:0"), y.cuda(), w.cuda(), "hinge")
     assert tr.csc is not None
+    import os
+
+    assert (tr.csc.ET > 0) == (os.environ.get("FMLX_CSC_TILE_MIN_VISITS") == "0")
     got = tr.fit()
     return float(np.abs(got - ref).max()), got.tobytes()
 
 
-def test_sparse_sgd_two_ranks_one_gpu():
+@pytest.mark.parametrize("tiled", [False, True])
+def test_sparse_sgd_two_ranks_one_gpu(tiled):
+    """The feedback path (backward writes the gradient row for the all-reduce), untiled and tiled."""
     _need_gpu()
-    res = run_spmd(_sparse_worker, 2, env={"FMLX_DEVICE": "cuda:0", "FMLX_XGMI": "0"}, timeout=300)
+    env = {"FMLX_DEVICE": "cuda:0", "FMLX_XGMI": "0", "FMLX_CSC_TILE_MIN_VISITS": "0" if tiled else "1000000"}
+    res = run_spmd(_sparse_worker, 2, env=env, timeout=300)
     assert res[0][0] < 1e-10 and res[1][0] < 1e-10
     assert res[0][1] == res[1][1]  # replicas identical
 
@@ -132,6 +166,7 @@ def test_batch_csc_device_transpose_matches_host(run_max, vdtype, d, B, skew, bu
     _need_gpu()
     from flink_ml_amd.ops import glm as gk
 
+    monkeypatch.setenv("FMLX_CSC_TILE", "0")  # the plain column-major layout (tiles: test below)
     monkeypatch.setattr(gk, "CSC_RUN_MAX", run_max)
     monkeypatch.setattr(gk, "CSC_BUCKET", bool(bucket))
     monkeypatch.setattr(gk, "CSC_PACK", bucket != "unpacked")
@@ -162,3 +197,102 @@ def test_batch_csc_device_transpose_matches_host(run_max, vdtype, d, B, skew, bu
     assert torch.equal(dev.colptr.cpu(), host.colptr)
     assert torch.equal(dev.erow.cpu(), host.erow)
     assert torch.equal(dev.evals.cpu(), host.evals)
+
+
+def _untile(csc, b):
+    """The plain column-major (erow, evals) of batch b rebuilt from its tiled layout, checking the
+    tile invariants on the way."""
+    d, rb, EL, ET = csc.d, csc.rb, csc.EL, csc.ET
+    j0, j1 = csc.bounds[b], csc.bounds[b + 1]
+    cp = csc.colptr[b].cpu().numpy()
+    nt = int(csc.ntiles[b])
+    tl = csc.tiles[b, :nt + 1].cpu().numpy()
+    er = csc.erow[j0:j1].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+    ev = csc.evals[j0:j1].cpu().numpy()
+    assert tl[0] == 0 and tl[nt] == d and np.all(np.diff(tl) > 0)
+    rows = np.empty(j1 - j0, dtype=np.int64)
+    vals = np.empty_like(ev)
+    heavy = 0
+    for t in range(nt):
+        k0, k1 = cp[tl[t]], cp[tl[t + 1]]
+        r = er[k0:k1] & ((1 << rb) - 1)
+        assert np.all(np.diff(r) >= 0), "rows sorted inside a tile"
+        if tl[t + 1] - tl[t] == 1 and k1 - k0 > EL:
+            heavy += 1
+            rows[k0:k1], vals[k0:k1] = r, ev[k0:k1]
+            continue
+        assert k1 - k0 <= ET
+        pos = er[k0:k1] >> rb
+        assert sorted(pos.tolist()) == list(range(k1 - k0))
+        rows[k0 + pos], vals[k0 + pos] = r, ev[k0:k1]
+    return rows, vals, heavy
+
+
+@pytest.mark.parametrize("vdtype,tile,d,B", [
+    (torch.float32, 64, 3_001, 1_000), (torch.float64, 64, 3_001, 1_000),
+    (torch.float32, 1024, 1_000_000, 1_000), (torch.float32, -1, 3_001, 4_000),
+])
+def test_batch_csc_row_sorted_tiles(vdtype, tile, d, B, monkeypatch):
+    """The tiled layout of the tiled backward (csc_build.hip csc_tiles / csc_tile_keys / sort /
+    csc_tile_store): tiles cover the columns, light tiles hold ≤ ET entries row-sorted with a
+    permutation of their column-ordered slots, one column of > EL entries is its own (heavy) tile,
+    and undoing the permutation gives the plain layout exactly."""
+    _need_gpu()
+    from flink_ml_amd.ops import glm as gk
+
+    g = torch.Generator().manual_seed(1)
+    n = 9_013
+    lens = torch.randint(0, 12, (n,), generator=g)
+    rows = []
+    for k in lens.tolist():
+        r = torch.randint(1, d, (4 * k + 4,), generator=g).unique()[:k]
+        if torch.rand(1, generator=g).item() < 0.7:
+            r = torch.cat([torch.zeros(1, dtype=r.dtype), r])  # column 0 in most rows: heavy
+        rows.append(torch.sort(r).values)
+    idx = torch.cat(rows).to(torch.int32)
+    indptr = torch.zeros(n + 1, dtype=torch.int64)
+    indptr[1:] = torch.cumsum(torch.tensor([len(r) for r in rows]), 0)
+    vals = torch.rand(int(indptr[-1]), generator=g, dtype=torch.float64).to(vdtype)
+    monkeypatch.setenv("FMLX_CSC_TILE", "0")
+    plain = gk.BatchCsc.build(indptr.cuda(), idx.cuda(), vals.cuda(), n, d, B)
+    monkeypatch.setenv("FMLX_CSC_TILE", str(tile))
+    monkeypatch.setattr(gk, "TILE_MIN_VISITS", 0)
+    csc = gk.BatchCsc.alloc(indptr.cuda(), idx.cuda(), vals.cuda(), n, d, B, max_rounds=3)
+    assert csc.ET == (tile if tile > 0 else (16384 if vdtype == torch.float64 else 32768))
+    csc.ensure([0, 1, 2])
+    csc.ensure(range(csc.P))  # storage growth copies the built tiles
+    heavy = 0
+    for b in range(csc.P):
+        j0, j1 = csc.bounds[b], csc.bounds[b + 1]
+        r, v, h = _untile(csc, b)
+        heavy += h
+        assert np.array_equal(r, plain.erow[j0:j1].cpu().numpy()), b
+        assert np.array_equal(v, plain.evals[j0:j1].cpu().numpy()), b
+    assert torch.equal(csc.colptr.cpu(), plain.colptr.cpu())
+    if tile == 64:
+        assert heavy >= csc.P - 1  # column 0 in every full batch (the last holds 13 rows)
+
+
+@pytest.mark.parametrize("tile", [0, 64, 2048])
+@pytest.mark.parametrize("vdtype", [torch.float32, torch.float64])
+def test_sparse_sgd_tiled_backward_matches_host(tile, vdtype, monkeypatch):
+    """Whole fits through the tiled backward (light and heavy tiles; the feedback path is the
+    two-rank test above) against the fp64 host trainer, weighted and not."""
+    _need_gpu()
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
+
+    n, d = 2100, 800
+    indptr, idx, vals, dense, y, w = _csr(n, d, 21, max_nnz=60, dtype=vdtype)
+    from flink_ml_amd.ops import glm as gk
+
+    monkeypatch.setenv("FMLX_CSC_TILE", str(tile))
+    monkeypatch.setattr(gk, "TILE_MIN_VISITS", 0)
+    for wt in (None, w):
+        sgd = SGD(max_iter=9, learning_rate=0.2, global_batch_size=700, tol=1e-9, reg=0.05, elastic_net=0.4)
+        ref = TorchGlmTrainer(sgd, np.zeros(d), dense, y, wt, "hinge").fit()
+        tr = DeviceGlmTrainer(sgd, np.zeros(d), _sparse_col(indptr, idx, vals, d, "cuda"), y.cuda(),
+                              None if wt is None else wt.cuda(), "hinge")
+        assert tr.csc is not None and tr.csc.ET == tile
+        got = tr.fit()
+        tol = 1e-10 if vdtype == torch.float64 else 1e-5
+        assert np.abs(got - ref).max() <= tol * max(1.0, np.abs(ref).max()), (tile, np.abs(got - ref).max())
