@@ -184,7 +184,7 @@ class DeviceGlmTrainer:
     """HBM-resident SGD on MI355X via the fused HIP kernels (one process per GPU)."""
 
     def __init__(self, sgd: SGD, init_coef, X, y, weight, loss: str, use_graph: Optional[bool] = None,
-                 check_every: int = 8):
+                 check_every: int = 8, pad: bool = True):
         ctx = get_context()
         self.ctx = ctx
         self.sgd = sgd
@@ -203,13 +203,23 @@ class DeviceGlmTrainer:
                 X = X.to(torch.float32)
             X = X.contiguous() if X.stride(-1) != 1 else X
             self.layout = gk.pick_layout(X)
+            d_model = int(X.shape[1])
+            if self.layout is None and pad and dev.type == "cuda":
+                # misaligned width: a zero-padded copy keeps the fused kernel (padding columns'
+                # coefficients stay 0; outputs are cut back to the model's width)
+                Xp = gk.pad_columns(X)
+                if Xp is not None:
+                    X, self.layout = Xp, gk.pick_layout(Xp)
             self.X = X
             self.n, self.d = int(X.shape[0]), int(X.shape[1])
             acc = torch.float64 if X.dtype == torch.float64 else torch.float32
+        self.d_model = d_model if not self.sparse else self.d
         self.acc = acc
         self.y = y.to(device=dev, dtype=acc).reshape(-1).contiguous()
         self.w = weight.to(device=dev, dtype=acc).reshape(-1).contiguous() if weight is not None else None
         c0 = np.asarray(init_coef, dtype=np.float64)
+        if c0.shape[0] < self.d:
+            c0 = np.concatenate([c0, np.zeros(self.d - c0.shape[0])])
         if not c0.any():  # the usual zero init (1M-wide sparse models): no pageable H2D copy
             self.coef = _dzeros(c0.shape, acc, dev)
         else:
@@ -560,7 +570,7 @@ class DeviceGlmTrainer:
             self._host_round = int(self.state[0].item())
             self._launched = self._host_round
             if st["done"]:
-                return self.coef.to(torch.float64).cpu().numpy()
+                return self.coef[:self.d_model].to(torch.float64).cpu().numpy()
         # a fit shorter than two graphs' worth of rounds launches directly: capture + first replay
         # (~1 ms per graph) would cost more than the launches it saves
         if not self.graphs and self.sgd.max_iter < 2 * self.rounds_per_graph:
@@ -607,6 +617,6 @@ class DeviceGlmTrainer:
         # sync point, after which the exchange's error word is final
         # (widened on the device: a host-side conversion first-touches a fresh 8 MB array, ~2 ms of
         # page faults in the first fit of a process; the pinned copy is already faulted in)
-        coef = hostsync.to_host(self.coef.to(torch.float64)).numpy()
+        coef = hostsync.to_host(self.coef[:self.d_model].to(torch.float64)).numpy()
         self.check_exchange()
         return coef

@@ -208,8 +208,9 @@ class StreamedGlmTrainer:
         # pointed at one batch per launch (n = that batch's rows, so the kernel's batch is the view)
         first = self.store.resident_view(0) if self.store.R else self.ring.slots[0]
         w0 = self.w[:first.shape[0]] if self.w is not None else None
+        # (pad=False: the inner trainer is re-pointed at ring slots of the unpadded width)
         self.inner = DeviceGlmTrainer(sgd, init_coef, first, self.y[:first.shape[0]], w0, loss, use_graph=False,
-                                      check_every=check_every)
+                                      check_every=check_every, pad=False)
         self.check_every = max(1, int(check_every))
 
     def _round(self, e: int) -> None:

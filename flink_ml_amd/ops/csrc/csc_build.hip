@@ -218,8 +218,9 @@ __global__ __launch_bounds__(TL_CHUNK) void csc_tiles_count_kernel(const int* __
   if (threadIdx.x == 0) cnt[(long)blockIdx.y * nchunks + blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(TL_THREADS) void csc_tiles_scan_kernel(int* __restrict__ cnt, int nchunks, long b0, int d,
-                                                                    int* __restrict__ tiles, int tstride,
+__global__ __launch_bounds__(TL_THREADS) void csc_tiles_scan_kernel(int* __restrict__ cnt, int nchunks,
+                                                                    const int* __restrict__ colptr, long b0, int d,
+                                                                    int2* __restrict__ tiles, int tstride,
                                                                     int* __restrict__ ntiles) {
   int* __restrict__ cc = cnt + (long)blockIdx.x * nchunks;
   const int per = (nchunks + TL_THREADS - 1) / TL_THREADS;
@@ -246,7 +247,7 @@ __global__ __launch_bounds__(TL_THREADS) void csc_tiles_scan_kernel(int* __restr
   if (threadIdx.x == TL_THREADS - 1) {
     const long b = b0 + blockIdx.x;
     const int nt = off < tstride - 1 ? off : tstride - 1;  // (bounded by construction)
-    tiles[b * (long)tstride + nt] = d;
+    tiles[b * (long)tstride + nt] = make_int2(d, colptr[b * (long)(d + 1) + d]);  // sentinel
     ntiles[b] = nt;
   }
 }
@@ -254,31 +255,33 @@ __global__ __launch_bounds__(TL_THREADS) void csc_tiles_scan_kernel(int* __restr
 __global__ __launch_bounds__(TL_CHUNK) void csc_tiles_write_kernel(const int* __restrict__ colptr, long b0, int d,
                                                                    int EB, int EL, int nchunks,
                                                                    const int* __restrict__ offs,
-                                                                   int* __restrict__ tiles, int tstride) {
+                                                                   int2* __restrict__ tiles, int tstride) {
   const long b = b0 + blockIdx.y;
   const int c = blockIdx.x * TL_CHUNK + threadIdx.x;
-  const bool f = c < d && tile_start(colptr + b * (long)(d + 1), c, EB, EL);
+  const int* __restrict__ cp = colptr + b * (long)(d + 1);
+  const bool f = c < d && tile_start(cp, c, EB, EL);
   int total;
   const int r = chunk_rank(f, total) + offs[(long)blockIdx.y * nchunks + blockIdx.x];
-  if (f && r < tstride - 1) tiles[b * (long)tstride + r] = c;
+  if (f && r < tstride - 1) tiles[b * (long)tstride + r] = make_int2(c, cp[c]);
 }
 
 // one block per tile (grid-strided over the run's batches' tiles, batch by blockIdx.y)
 template <typename V>
 __global__ __launch_bounds__(256) void csc_tile_keys_kernel(const int* __restrict__ colptr, long b0, int d,
-                                                            const int* __restrict__ tiles, int tstride,
+                                                            const int2* __restrict__ tiles, int tstride,
                                                             const int* __restrict__ ntiles, const long* __restrict__ bstart,
                                                             const int* __restrict__ erow, const V* __restrict__ evals,
                                                             long j0, int rb, int pb, int EL, uint64_t* __restrict__ keys,
                                                             uint32_t* __restrict__ pay) {
   const long b = b0 + blockIdx.y;
   const int* __restrict__ cp = colptr + b * (long)(d + 1);
-  const int* __restrict__ tl = tiles + b * (long)tstride;
+  const int2* __restrict__ tl = tiles + b * (long)tstride;
   const long base = bstart[blockIdx.y];  // the batch's first entry (absolute)
   const int nt = ntiles[b];
   for (int t = blockIdx.x; t < nt; t += gridDim.x) {
-    const int k0 = cp[tl[t]], k1 = cp[tl[t + 1]];
-    const bool heavy = tl[t + 1] - tl[t] == 1 && k1 - k0 > EL;
+    const int2 ta = tl[t], tz = tl[t + 1];
+    const int k0 = ta.y, k1 = tz.y;
+    const bool heavy = tz.x - ta.x == 1 && k1 - k0 > EL;
     for (int k = k0 + (int)threadIdx.x; k < k1; k += 256) {
       const long a = base + k;
       const uint64_t pos = heavy ? 0 : (uint64_t)(k - k0);
@@ -366,7 +369,8 @@ FMLX_API int fmlx_csc_colptr(const int* sorted_keys, long m, int slots, int d, c
   return (int)hipGetLastError();
 }
 
-// Tiles of batches b0 … b0 + slots − 1 (colptr rows already built): tiles int32 [P][tstride]
+// Tiles of batches b0 … b0 + slots − 1 (colptr rows already built): tiles int32 [P][tstride][2]
+// = (start column, its batch-relative first entry), the entry after the last tile = (d, nnz_b)
 // (tstride ≥ min(d, nnz_b / EB + 2·(nnz_b / EL) + 1) + 1 bounds every batch's tile count: the
 // bucket changes plus two starts per heavy column), ntiles int32 [P].
 FMLX_API int fmlx_csc_tiles(const int* colptr, long b0, int slots, int d, int EB, int EL, int* tiles, int tstride,
@@ -377,10 +381,10 @@ FMLX_API int fmlx_csc_tiles(const int* colptr, long b0, int slots, int d, int EB
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(csc_tiles_count_kernel, dim3(nchunks, slots), dim3(TL_CHUNK), 0, s, colptr, b0, d, EB, EL, nchunks,
                      scratch);
-  hipLaunchKernelGGL(csc_tiles_scan_kernel, dim3(slots), dim3(TL_THREADS), 0, s, scratch, nchunks, b0, d, tiles, tstride,
-                     ntiles);
+  hipLaunchKernelGGL(csc_tiles_scan_kernel, dim3(slots), dim3(TL_THREADS), 0, s, scratch, nchunks, colptr, b0, d,
+                     (int2*)tiles, tstride, ntiles);
   hipLaunchKernelGGL(csc_tiles_write_kernel, dim3(nchunks, slots), dim3(TL_CHUNK), 0, s, colptr, b0, d, EB, EL, nchunks,
-                     scratch, tiles, tstride);
+                     scratch, (int2*)tiles, tstride);
   return (int)hipGetLastError();
 }
 
@@ -394,10 +398,10 @@ FMLX_API int fmlx_csc_tile_keys(int f64, const int* colptr, long b0, int slots, 
   if (slots <= 0 || rb < 1 || pb < 1 || rb + pb > 32) return -1;
   const dim3 g(tstride < 1024 ? tstride : 1024, slots);
   if (f64)
-    hipLaunchKernelGGL(csc_tile_keys_kernel<double>, g, dim3(256), 0, (hipStream_t)stream, colptr, b0, d, tiles,
+    hipLaunchKernelGGL(csc_tile_keys_kernel<double>, g, dim3(256), 0, (hipStream_t)stream, colptr, b0, d, (const int2*)tiles,
                        tstride, ntiles, bstart, erow, (const double*)evals, j0, rb, pb, EL, keys, pay);
   else
-    hipLaunchKernelGGL(csc_tile_keys_kernel<float>, g, dim3(256), 0, (hipStream_t)stream, colptr, b0, d, tiles,
+    hipLaunchKernelGGL(csc_tile_keys_kernel<float>, g, dim3(256), 0, (hipStream_t)stream, colptr, b0, d, (const int2*)tiles,
                        tstride, ntiles, bstart, erow, (const float*)evals, j0, rb, pb, EL, keys, pay);
   return (int)hipGetLastError();
 }

@@ -1489,11 +1489,13 @@ constexpr int TILE_COLS = 8;  // columns per thread whose pointers are prefetche
 
 template <typename A, bool FUSE>
 __global__ __launch_bounds__(TILE_THREADS) void glm_csc_tile_bwd_kernel(
-    const long* __restrict__ indptr, const int* __restrict__ colptr, const int* __restrict__ tiles,
+    const long* __restrict__ indptr, const int* __restrict__ colptr, const int2* __restrict__ tiles,
     const int* __restrict__ ntiles, int tstride, const int* __restrict__ erow, const A* __restrict__ eval,
     const A* __restrict__ mult, long n, int d, long B, int rb, int EL, int* __restrict__ state, A* __restrict__ wl,
-    A* __restrict__ fb, A* __restrict__ coef, int max_iter, A tol, A lr, A reg, A en, int weighted) {
+    A* __restrict__ fb, A* __restrict__ coef, int max_iter, A tol, A lr, A reg, A en, int weighted,
+    long long* __restrict__ trace) {
   extern __shared__ unsigned char tile_smem[];
+  if (trace && threadIdx.x == 0) trace[(long)blockIdx.x * 4] = (long long)__builtin_amdgcn_s_memrealtime();
   A* prod = reinterpret_cast<A*>(tile_smem);
   __shared__ A hred[TILE_THREADS / 64];
   int e;
@@ -1511,7 +1513,7 @@ __global__ __launch_bounds__(TILE_THREADS) void glm_csc_tile_bwd_kernel(
   const long b = (long)(e % P);
   const long base = indptr[b * B];
   const int* __restrict__ cp = colptr + b * (long)(d + 1);
-  const int* __restrict__ tl = tiles + b * (long)tstride;
+  const int2* __restrict__ tl = tiles + b * (long)tstride;
   const int nt = ntiles[b];
   const int* __restrict__ er = erow + base;
   const A* __restrict__ ev = eval + base;
@@ -1524,8 +1526,8 @@ __global__ __launch_bounds__(TILE_THREADS) void glm_csc_tile_bwd_kernel(
   }
   const int tid = threadIdx.x;
   for (int t = blockIdx.x; t < nt; t += gridDim.x) {
-    const int c0 = tl[t], c1 = tl[t + 1];
-    const int k0 = cp[c0], k1 = cp[c1];
+    const int2 ta = tl[t], tz = tl[t + 1];  // (start column, first entry) of this and the next tile
+    const int c0 = ta.x, c1 = tz.x, k0 = ta.y, k1 = tz.y;
     if (c1 - c0 == 1 && k1 - k0 > EL) {  // heavy column (block-uniform branch)
       A g = 0;
       for (int k = k0 + tid; k < k1; k += TILE_THREADS) {
@@ -1562,7 +1564,8 @@ __global__ __launch_bounds__(TILE_THREADS) void glm_csc_tile_bwd_kernel(
       }
     }
     // products into their column-ordered slots: TILE_U entries per thread per step, the next
-    // step's entries loaded before this step's multiplier gathers
+    // step's entries loaded before this step's multiplier gathers (measured against one step of
+    // 32 per thread: 71.0 vs 72.3 µs per round; 8 without the overlap: 71.8)
     uint32_t xx[TILE_U];
     A vv[TILE_U];
 #pragma unroll
@@ -1596,7 +1599,9 @@ __global__ __launch_bounds__(TILE_THREADS) void glm_csc_tile_bwd_kernel(
         vv[u] = nv[u];
       }
     }
+    if (trace && tid == 0) trace[(long)blockIdx.x * 4 + 1] = (long long)__builtin_amdgcn_s_memrealtime();
     __syncthreads();
+    if (trace && tid == 0) trace[(long)blockIdx.x * 4 + 2] = (long long)__builtin_amdgcn_s_memrealtime();
     if (few) {
 #pragma unroll
       for (int i = 0; i < TILE_COLS; ++i) {
@@ -1627,6 +1632,7 @@ __global__ __launch_bounds__(TILE_THREADS) void glm_csc_tile_bwd_kernel(
     fb[d] = W;
     fb[d + 1] = L;
   }
+  if (trace && tid == 0) trace[(long)blockIdx.x * 4 + 3] = (long long)__builtin_amdgcn_s_memrealtime();
   if (FUSE) {
     __shared__ int last;
     __syncthreads();
@@ -2007,6 +2013,7 @@ FMLX_API int fmlx_glm_grad_csr(int acc_f64, const long* indptr, const int* idx, 
 }
 
 static int g_csc_fwd_cap = 65535, g_csc_bwd_cap = 1024, g_csc_tile_cap = 0;  // 0: CUs × tile blocks per CU
+
 FMLX_API void fmlx_glm_set_csc_tuning(int fwd_cap, int bwd_cap) {
   g_csc_fwd_cap = fwd_cap > 0 ? fwd_cap : 65535;
   g_csc_bwd_cap = bwd_cap > 0 ? bwd_cap : 1024;
@@ -2015,7 +2022,7 @@ FMLX_API void fmlx_glm_set_csc_tuning(int fwd_cap, int bwd_cap) {
 
 // tiled backward: the column tiles of the batches (BatchCsc.tiles) and the packing of erow
 struct CscTiles {
-  const int* tiles;   // int32 [P][tstride] tile start columns (nullptr: untiled layout)
+  const int2* tiles;  // [P][tstride] (start column, first entry) per tile (nullptr: untiled layout)
   const int* ntiles;  // int32 [P]
   int tstride, rb, EL, ET;  // EL: heavy-column threshold (entries)
 };
@@ -2039,14 +2046,15 @@ static void launch_csc_round(const long* indptr, const int* idx, const A* val, c
     per_cu = per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu);  // ≤ 32 waves per CU at 1024 threads
     int tb = g_csc_tile_cap > 0 ? g_csc_tile_cap : NUM_CU * per_cu;
     if (tb > ti.tstride) tb = ti.tstride;
+#define FMLX_TILE_BWD(F)                                                                                             \
+  hipLaunchKernelGGL((glm_csc_tile_bwd_kernel<A, F>), dim3(tb), dim3(TILE_THREADS), lds, s, indptr, colptr, ti.tiles, \
+                     ti.ntiles, ti.tstride, erow, eval, (const A*)mult, n, d, B, ti.rb, ti.EL, state, wl, fb, coef,    \
+                     max_iter, tol, lr, reg, en, weighted, g_trace)
     if (fuse)
-      hipLaunchKernelGGL((glm_csc_tile_bwd_kernel<A, true>), dim3(tb), dim3(TILE_THREADS), lds, s, indptr, colptr,
-                         ti.tiles, ti.ntiles, ti.tstride, erow, eval, (const A*)mult, n, d, B, ti.rb, ti.EL, state, wl,
-                         fb, coef, max_iter, tol, lr, reg, en, weighted);
+      FMLX_TILE_BWD(true);
     else
-      hipLaunchKernelGGL((glm_csc_tile_bwd_kernel<A, false>), dim3(tb), dim3(TILE_THREADS), lds, s, indptr, colptr,
-                         ti.tiles, ti.ntiles, ti.tstride, erow, eval, (const A*)mult, n, d, B, ti.rb, ti.EL, state, wl,
-                         fb, coef, max_iter, tol, lr, reg, en, weighted);
+      FMLX_TILE_BWD(false);
+#undef FMLX_TILE_BWD
     return;
   }
   int bb = (d + 255) / 256;  // grid-strided: each block takes the arrival ticket once
@@ -2092,7 +2100,7 @@ FMLX_API int fmlx_glm_csc_round(int acc_f64, int G, const long* indptr, const in
                                 void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (n <= 0 || B <= 0) return -2;
-  const CscTiles ti{tiles, ntiles, tstride, rb, EL, ET};
+  const CscTiles ti{reinterpret_cast<const int2*>(tiles), ntiles, tstride, rb, EL, ET};
   if (tiles != nullptr) {
     const size_t esz = acc_f64 ? 8 : 4;
     // the packed erow (row | slot << rb) and the LDS slot array of a light tile (< ET entries)

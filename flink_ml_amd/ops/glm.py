@@ -105,6 +105,33 @@ def pick_layout(X: torch.Tensor) -> Optional[Tuple[int, int]]:
     return epc, cpl
 
 
+def pad_columns(X: torch.Tensor) -> Optional[torch.Tensor]:
+    """A copy of X whose rows are zero-padded to a whole number of 16-byte chunks, when that makes
+    it fit the register-resident round kernel (misaligned widths: fp32 d = 1001, bf16 d % 8 ≠ 0,
+    a row stride that breaks 16-byte alignment); None when even the padded row is too wide or the
+    copy does not fit in free device memory. The padding columns are zero, so their gradient is
+    zero and their coefficients stay 0 through every update (SGD step and regularisation)."""
+    if X.dim() != 2 or not X.is_cuda:
+        return None
+    n, d = X.shape
+    epc = 16 // X.element_size()
+    dp = -(-d // epc) * epc
+    nch = dp // epc
+    cpl = 1
+    while cpl * 64 < nch:
+        cpl *= 2
+    if cpl > MAX_CPL:
+        return None
+    need = n * dp * X.element_size()
+    free, _ = torch.cuda.mem_get_info(X.device)
+    if need > 0.8 * free:
+        return None
+    Xp = torch.empty((n, dp), dtype=X.dtype, device=X.device)
+    Xp[:, d:].zero_()
+    Xp[:, :d].copy_(X)
+    return Xp if pick_layout(Xp) is not None else None
+
+
 def grad_partials(X, y, wt, coef, B: int, loss: int, state, partials, nblocks: int) -> None:
     epc, cpl = pick_layout(X)
     native.call("fmlx_glm_grad_partials", native.dtype_code(X.dtype), epc, cpl, GRAD_UNROLL, native.ptr(X), X.stride(0),
@@ -432,7 +459,7 @@ class BatchCsc:
         evals = torch.empty(max(ne, 1), dtype=values.dtype, device=dev)
         tiles = ntiles = None
         if self.ET:
-            tiles = torch.empty((cap, self.tstride), dtype=torch.int32, device=dev)
+            tiles = torch.empty((cap, self.tstride, 2), dtype=torch.int32, device=dev)
             ntiles = torch.empty(cap, dtype=torch.int32, device=dev)
         if self.cap:
             old = self.bounds[self.cap]

@@ -35,22 +35,25 @@ def main():
     X = SparseColumn(indptr, idx.reshape(-1), vals, dim)
     y = torch.randint(0, 2, (n,), generator=g, device=dev).to(torch.float32)
     lib = native.kernels()
+    from flink_ml_amd.ops import glm as gk
+
     trainers = {}
-    for tile in (0, 16384, 32768):
+    for tile, hdiv in ((0, 8), (16384, 8), (32768, 8), (32768, 32), (32768, 128)):
         os.environ["FMLX_CSC_TILE"] = str(tile)
+        gk.TILE_HEAVY_DIV = hdiv
         tr = DeviceGlmTrainer(SGD(max_iter=10 ** 8, learning_rate=0.1, global_batch_size=100_000, tol=0.0),
                               np.zeros(dim), X, y, None, "hinge", use_graph=False)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         tr.csc.ensure(range(tr.csc.P))
         torch.cuda.synchronize()
-        print(json.dumps({"tile": tile, "build_ms": round((time.perf_counter() - t0) * 1e3, 1),
+        print(json.dumps({"tile": tile, "heavy_div": hdiv, "build_ms": round((time.perf_counter() - t0) * 1e3, 1),
                           "batches": tr.csc.P}), flush=True)
-        trainers[tile] = tr
-    cases = [(0, 1024)] + [(t, c) for t in (16384, 32768) for c in (0, 256, 512)]
+        trainers[(tile, hdiv)] = tr
+    cases = [(k, 0) for k in trainers]
     for rep in range(2):
-        for tile, cap in cases:
-            tr = trainers[tile]
+        for key, cap in cases:
+            tr = trainers[key]
             lib.fmlx_glm_set_csc_tuning(0, cap)
             tr.run_rounds(20)
             torch.cuda.synchronize()
@@ -58,9 +61,10 @@ def main():
             tr.run_rounds(200)
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) / 200 * 1e3
-            print(json.dumps({"tile": tile, "bwd_cap": cap, "rep": rep,
+            print(json.dumps({"tile": key[0], "heavy_div": key[1], "bwd_cap": cap, "rep": rep,
                               "ms_per_round": round(ms, 4)}), flush=True)
     lib.fmlx_glm_set_csc_tuning(0, 0)
+
 
 
 if __name__ == "__main__":

@@ -134,8 +134,8 @@ def test_lr_estimator_on_gpu_goldens():
     assert np.allclose(coef, [0.525, -0.283, -0.425, -0.567], atol=0.01)
 
 
-@pytest.mark.parametrize("dtype,d", [(torch.float32, 1001), (torch.float32, 3000), (torch.float64, 3000),
-                                     (torch.bfloat16, 5000)])
+@pytest.mark.parametrize("dtype,d", [(torch.float32, 3000), (torch.float64, 3000), (torch.bfloat16, 5000),
+                                     (torch.bfloat16, 5001)])
 def test_device_sgd_wide_dense_gemv_path(dtype, d):
     """Rows the register-resident round kernel cannot hold run as two GEMVs + the device update."""
     _need_gpu()
@@ -155,3 +155,32 @@ def test_device_sgd_wide_dense_gemv_path(dtype, d):
         assert tr.rounds_executed() == 7
         tol = (1e-10 if dtype == torch.float64 else 1e-4) * max(1.0, np.abs(ref).max())
         assert np.abs(got - ref).max() < tol, (loss, np.abs(got - ref).max())
+
+
+@pytest.mark.parametrize("dtype,d", [(torch.float32, 1001), (torch.float32, 2047), (torch.bfloat16, 1003),
+                                     (torch.bfloat16, 4093), (torch.float64, 1023)])
+def test_device_sgd_misaligned_width_padded_to_fused_kernel(dtype, d):
+    """Widths that break the 16-byte row chunks (fp32 d = 1001, bf16 d % 8 != 0) train on the fused
+    round kernel through a zero-padded copy: the padding coefficients stay 0, the returned model
+    has the input width, and results equal the host trainer (and the GEMV path, pad=False)."""
+    _need_gpu()
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
+
+    g = torch.Generator(device="cpu").manual_seed(d)
+    n = 1300
+    X = torch.rand((n, d), generator=g, dtype=torch.float64).to(dtype)
+    y = (X.to(torch.float64) @ torch.linspace(-1, 1, d, dtype=torch.float64) > 0).double()
+    w = torch.rand(n, generator=g, dtype=torch.float64) + 0.5
+    for loss in ("logistic", "hinge"):
+        sgd = SGD(max_iter=6, learning_rate=0.05, global_batch_size=400, tol=1e-9, reg=0.1, elastic_net=0.5)
+        ref = TorchGlmTrainer(sgd, np.zeros(d), X.to(torch.float64), y, w, loss).fit()
+        tr = DeviceGlmTrainer(sgd, np.zeros(d), X.cuda(), y.cuda(), w.cuda(), loss)
+        assert not tr.wide and tr.layout is not None and tr.X.shape[1] % (16 // X.element_size()) == 0
+        got = tr.fit()
+        assert got.shape == (d,) and tr.rounds_executed() == 6
+        assert float(tr.coef[d:].abs().max() if tr.X.shape[1] > d else 0.0) == 0.0
+        tol = (1e-10 if dtype == torch.float64 else 1e-4) * max(1.0, np.abs(ref).max())
+        assert np.abs(got - ref).max() < tol, (loss, np.abs(got - ref).max())
+        gemv = DeviceGlmTrainer(sgd, np.zeros(d), X.cuda(), y.cuda(), w.cuda(), loss, pad=False)
+        if gemv.wide:
+            assert np.abs(gemv.fit() - got).max() < tol

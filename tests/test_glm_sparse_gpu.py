@@ -206,7 +206,8 @@ def _untile(csc, b):
     j0, j1 = csc.bounds[b], csc.bounds[b + 1]
     cp = csc.colptr[b].cpu().numpy()
     nt = int(csc.ntiles[b])
-    tl = csc.tiles[b, :nt + 1].cpu().numpy()
+    tl = csc.tiles[b, :nt + 1, 0].cpu().numpy()
+    assert np.array_equal(csc.tiles[b, :nt + 1, 1].cpu().numpy(), cp[tl])  # each tile's first entry
     er = csc.erow[j0:j1].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
     ev = csc.evals[j0:j1].cpu().numpy()
     assert tl[0] == 0 and tl[nt] == d and np.all(np.diff(tl) > 0)
