@@ -344,6 +344,7 @@ TILE_HEAVY_DIV = int(os.environ.get("FMLX_CSC_TILE_HEAVY_DIV", "8"))  # heavy co
 # a fit tiles its batches when it visits each at least this often (the tiling costs about as much
 # as TILE_MIN_VISITS rounds save: ~0.15 ms per 6.4M-entry batch vs ~13 µs per round, svc shape)
 TILE_MIN_VISITS = int(os.environ.get("FMLX_CSC_TILE_MIN_VISITS", "16"))
+TILE_SPREAD = os.environ.get("FMLX_CSC_TILE_SPREAD", "1") == "1"  # tile size from the batch and CU count
 
 
 def csc_tile_entries(B: int, f64: bool) -> int:
@@ -402,6 +403,11 @@ class BatchCsc:
         self.pb = max(1, int(self.ET - 1).bit_length())
         if self.ET:
             most = max(bounds[i + 1] - bounds[i] for i in range(self.P)) if self.P else 0
+            if TILE_SPREAD and values.device.type == "cuda":
+                # a block runs one tile, so the round takes one tile's time: cut the largest batch
+                # into about one tile per CU (fewer, fuller tiles leave CUs idle)
+                cus = torch.cuda.get_device_properties(values.device).multi_processor_count
+                self.EB = max(1024, min(self.EB, -(-most // max(1, cus - 2))))
             self.tstride = min(d, most // self.EB + 2 * (most // self.EL) + 1) + 1
         else:
             self.tstride = 0

@@ -38,18 +38,20 @@ def main():
     from flink_ml_amd.ops import glm as gk
 
     trainers = {}
-    for tile, hdiv in ((0, 8), (16384, 8), (32768, 8), (32768, 32), (32768, 128)):
+    for tile, hdiv, spread in ((0, 8, 0), (32768, 8, 0), (32768, 8, 1), (32768, 16, 1)):
         os.environ["FMLX_CSC_TILE"] = str(tile)
         gk.TILE_HEAVY_DIV = hdiv
+        gk.TILE_SPREAD = bool(spread)
         tr = DeviceGlmTrainer(SGD(max_iter=10 ** 8, learning_rate=0.1, global_batch_size=100_000, tol=0.0),
                               np.zeros(dim), X, y, None, "hinge", use_graph=False)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         tr.csc.ensure(range(tr.csc.P))
         torch.cuda.synchronize()
-        print(json.dumps({"tile": tile, "heavy_div": hdiv, "build_ms": round((time.perf_counter() - t0) * 1e3, 1),
-                          "batches": tr.csc.P}), flush=True)
-        trainers[(tile, hdiv)] = tr
+        print(json.dumps({"tile": tile, "heavy_div": hdiv, "spread": spread, "EB": tr.csc.EB,
+                          "tiles_max": int(tr.csc.ntiles.max()) if tr.csc.ET else 0,
+                          "build_ms": round((time.perf_counter() - t0) * 1e3, 1), "batches": tr.csc.P}), flush=True)
+        trainers[(tile, hdiv, spread)] = tr
     cases = [(k, 0) for k in trainers]
     for rep in range(2):
         for key, cap in cases:
@@ -61,7 +63,7 @@ def main():
             tr.run_rounds(200)
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) / 200 * 1e3
-            print(json.dumps({"tile": key[0], "heavy_div": key[1], "bwd_cap": cap, "rep": rep,
+            print(json.dumps({"tile": key[0], "heavy_div": key[1], "spread": key[2], "bwd_cap": cap, "rep": rep,
                               "ms_per_round": round(ms, 4)}), flush=True)
     lib.fmlx_glm_set_csc_tuning(0, 0)
 
