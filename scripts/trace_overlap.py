@@ -3,7 +3,8 @@
 --memory-copy-trace --output-format csv``): how much of the H2D copy time runs while a kernel of
 the same process is executing, and how much of the kernel time runs under a copy.
 
-Usage: python scripts/trace_overlap.py <rocprof output dir> [--kernel-filter SUBSTR]
+Usage: python scripts/trace_overlap.py <rocprof output dir> [--kernel-filter SUBSTR] [--fit-window]
+(--fit-window: only copies that start between the first and last filtered kernel)
 Prints one JSON line.
 """
 import csv
@@ -60,6 +61,10 @@ def main():
     h2d = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in mr
            if "HOST_TO_DEVICE" in r.get("Direction", "").upper() or "H2D" in r.get("Direction", "").upper()]
     big = [c for c in h2d if c[1] - c[0] > 100_000]  # batch-sized copies (> 0.1 ms)
+    if "--fit-window" in sys.argv and kern:
+        # only the copies issued while the filtered kernels run (not the set-up's resident fill)
+        t0, t1 = min(k[0] for k in kern), max(k[1] for k in kern)
+        big = [c for c in big if c[0] >= t0 and c[0] <= t1]
     K, C = _merge(kern), _merge(big)
     ctot = sum(e - s for s, e in C)
     ktot = sum(e - s for s, e in K)
@@ -71,7 +76,6 @@ def main():
         "kernel_time_under_copy_frac": round(ov / ktot, 4) if ktot else None,
         "copy_busy_frac_of_span": round(ctot / span, 4) if span else None,
         "mean_copy_ms": round(ctot / len(big) / 1e6, 4) if big else None,
-        "copy_GB_per_s": None,
     }))
 
 
