@@ -238,9 +238,15 @@ class DeviceGlmTrainer:
         self.distributed = ctx.is_distributed
         self.xg = None
         self.csc = None
-        # dense rows the register-resident round kernel cannot hold (wide or misaligned d): two
-        # bandwidth-bound GEMVs per round (X_b·w, then X_bᵀ·m, rocBLAS) + the device update kernel
-        self.wide = not self.sparse and self.layout is None
+        # dense rows one wave's registers cannot hold: the wide-row kernel (a block's 8 waves split
+        # each row's columns, one read of the batch, fused atomic tail); beyond its width (or in
+        # the deterministic mode) two bandwidth-bound GEMVs per round (X_b·w, then X_bᵀ·m,
+        # rocBLAS) + the device update kernel
+        self.wide_layout = None
+        if not self.sparse and self.layout is None and dev.type == "cuda" and not gk.DETERMINISTIC and gk.WIDE_FUSED:
+            self.wide_layout = gk.pick_wide_layout(self.X)
+        self.wide_fused = self.wide_layout is not None
+        self.wide = not self.sparse and self.layout is None and not self.wide_fused
         self._host_round = 0
         if self.sparse:
             self.scratch = None
@@ -257,6 +263,12 @@ class DeviceGlmTrainer:
             self.nparts = 0
             if self.w is None:
                 self.w = torch.ones(self.n, dtype=acc, device=dev)
+        elif self.wide_fused:
+            # one 8-wave block per CU (~200 VGPRs per lane), each walking its rows two at a time
+            cus = torch.cuda.get_device_properties(dev).multi_processor_count
+            share = device_sharers(ctx) if self.distributed else 1
+            self.nparts = max(1, min(cus // max(1, share), -(-max(self.B, 1) // 2)))
+            self.scratch = gk.RoundScratch(self.nparts, self.d, acc, dev, det=False)
         else:
             self.nparts = max(1, min(gk.round_blocks(self.X), gk.max_round_blocks(), math.ceil(max(self.B, 1) / (gk.WPB * 16))))
             if self.distributed:
@@ -277,7 +289,9 @@ class DeviceGlmTrainer:
                     cus = torch.cuda.get_device_properties(dev).multi_processor_count
                     self.nparts = max(1, min(self.nparts, cus // share))
             self.scratch = gk.RoundScratch(self.nparts, self.d, acc, dev)
-        if self.sparse or self.wide or self.distributed and self.xg is None:
+        if self.wide_fused:
+            self.mode = gk.TAIL_FEEDBACK if self.distributed else gk.TAIL_UPDATE
+        elif self.sparse or self.wide or self.distributed and self.xg is None:
             self.mode = gk.TAIL_FEEDBACK  # feedback → RCCL all-reduce → update kernel
         else:
             self.mode = gk.TAIL_XGMI if self.distributed else gk.TAIL_UPDATE
@@ -294,7 +308,8 @@ class DeviceGlmTrainer:
         # N GPUs over the in-kernel xGMI exchange: launch e + 1's lead block exchanges and applies
         # round e (csrc/glm.hip defer_prologue_xgmi); FMLX_GLM_DEFER_XGMI=0 keeps the ticketed tail
         self.defer = ((self.mode == gk.TAIL_UPDATE or self.mode == gk.TAIL_XGMI and gk.DEFER_XGMI)
-                      and self.scratch is not None and not self.scratch.det and gk.defer_supported(self.d, acc))
+                      and self.scratch is not None and not self.scratch.det and not self.wide_fused
+                      and gk.defer_supported(self.d, acc))
         self.parity = 0
         self.cw = _dzeros((2, self.d), acc, dev) if self.defer else None
         self._flushed = False
@@ -314,7 +329,7 @@ class DeviceGlmTrainer:
             raise RuntimeError("use_rccl() after deferred rounds ran: their last update is pending")
         self.xg = None
         if not self.sparse and not self.wide and self.distributed:
-            self.mode = gk.TAIL_FEEDBACK
+            self.mode = gk.TAIL_FEEDBACK  # (the wide-row kernel already runs its feedback tail)
         self.defer, self.cw, self.parity = False, None, 0
         if self.ctx.backend != "nccl":
             self.use_graph = False  # a gloo all-reduce of device tensors cannot be captured
@@ -332,7 +347,8 @@ class DeviceGlmTrainer:
         else ``rounds`` launch sequences). ``ensure=False``: the caller already ensured the
         column-major batches (the capture warm-up, whose ``_launched`` is already advanced past
         the rounds it replays — ensuring there could regrow the storage mid-replay)."""
-        if rounds > 1 and not (self.csc is None and not self.wide and not self.sparse and self.mode != gk.TAIL_FEEDBACK):
+        if rounds > 1 and not (self.csc is None and not self.wide and not self.wide_fused and not self.sparse
+                               and self.mode != gk.TAIL_FEEDBACK):
             for _ in range(rounds):
                 self._launch_round(1, ensure)
             return
@@ -346,6 +362,14 @@ class DeviceGlmTrainer:
                          self.B, self.loss, self.state, self.mult, self.wl, self.feedback, not self.distributed,
                          s.max_iter, s.tol, s.learning_rate, s.reg, s.elastic_net)
             if self.distributed:
+                comm.all_reduce_sum(self.feedback)
+                gk.update(self.feedback, self.d, self.coef, self.state, s.max_iter, s.tol, s.learning_rate, s.reg,
+                          s.elastic_net)
+            return
+        if self.wide_fused:
+            gk.glm_round_wide(self.X, self.y, self.w, self.coef, self.B, self.loss, self.state, self.scratch, self.mode,
+                              self.feedback, s.max_iter, s.tol, s.learning_rate, s.reg, s.elastic_net)
+            if self.mode == gk.TAIL_FEEDBACK:
                 comm.all_reduce_sum(self.feedback)
                 gk.update(self.feedback, self.d, self.coef, self.state, s.max_iter, s.tol, s.learning_rate, s.reg,
                           s.elastic_net)

@@ -541,13 +541,16 @@ __device__ __forceinline__ float seg_sum_dpp(float v) {
   return v;
 }
 
-// register-light shapes with one row per step are capped at 128 VGPRs (4 waves per SIMD) so
-// that two 8-wave blocks share a CU (the 512-block grids); U >= 2 runs one block per CU (the
-// flagship's 224 blocks: 2 waves per SIMD) and keeps the compiler's choice — under the 128 cap
-// the paired row loop spills to scratch, and every spill reload is a vmcnt(0) in the loop
+// register-light shapes are capped at 128 VGPRs (4 waves per SIMD) so that two 8-wave blocks
+// share a CU (the 512-block grids); everything else keeps the compiler's choice and runs one
+// block per CU — under the 128 cap the row loop spills to scratch, and every spill reload is a
+// vmcnt(0) in the loop. (Round 5's code-object audit found the old 64-byte one-row cap spilling
+// 171–235 VGPRs for bf16 rows of 1025–4096 and fp64 rows; fp64 accumulators never take the cap.)
 template <typename T, int EPC, int CPL, int U>
 constexpr int glm_min_waves() {
-  return (U == 1 && CPL * EPC * (int)sizeof(T) <= 64) || (U == 2 && CPL * EPC * (int)sizeof(T) <= 16) ? 4 : 1;
+  return sizeof(T) <= 4 && ((U == 1 && CPL * EPC * (int)sizeof(T) <= 32) || (U == 2 && CPL * EPC * (int)sizeof(T) <= 16))
+             ? 4
+             : 1;
 }
 
 // One 16-byte-per-lane LDS-DMA load (global_load_lds_dwordx4 … nt): lane i's 16 bytes land at LDS
@@ -1563,25 +1566,27 @@ __global__ __launch_bounds__(TILE_THREADS) void glm_csc_tile_bwd_kernel(
         cw[i] = FUSE ? coef[cc] : (A)0;
       }
     }
-    // products into their column-ordered slots: TILE_U entries per thread per step, the next
+    constexpr int TU = sizeof(A) == 8 ? TILE_U / 2 : TILE_U;
+    // products into their column-ordered slots: TU entries per thread per step (8; 4 for fp64,
+    // which spilled at 8 under the 1024-thread register budget), the next
     // step's entries loaded before this step's multiplier gathers (measured against one step of
     // 32 per thread: 71.0 vs 72.3 µs per round; 8 without the overlap: 71.8)
-    uint32_t xx[TILE_U];
-    A vv[TILE_U];
+    uint32_t xx[TU];
+    A vv[TU];
 #pragma unroll
-    for (int u = 0; u < TILE_U; ++u) {
+    for (int u = 0; u < TU; ++u) {
       const int k = k0 + tid + u * TILE_THREADS;
       const int kk = k < k1 ? k : k0;
       xx[u] = (uint32_t)__builtin_nontemporal_load(er + kk);
       vv[u] = __builtin_nontemporal_load(ev + kk);
     }
-    for (int kb = k0 + tid; kb < k1; kb += TILE_U * TILE_THREADS) {
-      uint32_t nx[TILE_U];
-      A nv[TILE_U];
-      const int kn = kb + TILE_U * TILE_THREADS;
+    for (int kb = k0 + tid; kb < k1; kb += TU * TILE_THREADS) {
+      uint32_t nx[TU];
+      A nv[TU];
+      const int kn = kb + TU * TILE_THREADS;
       if (kn < k1) {
 #pragma unroll
-        for (int u = 0; u < TILE_U; ++u) {
+        for (int u = 0; u < TU; ++u) {
           const int k = kn + u * TILE_THREADS;
           const int kk = k < k1 ? k : kn;
           nx[u] = (uint32_t)__builtin_nontemporal_load(er + kk);
@@ -1589,12 +1594,12 @@ __global__ __launch_bounds__(TILE_THREADS) void glm_csc_tile_bwd_kernel(
         }
       }
 #pragma unroll
-      for (int u = 0; u < TILE_U; ++u) {
+      for (int u = 0; u < TU; ++u) {
         const A p = mult[xx[u] & rmask] * vv[u];
         if (kb + u * TILE_THREADS < k1) prod[xx[u] >> rb] = p;
       }
 #pragma unroll
-      for (int u = 0; u < TILE_U; ++u) {
+      for (int u = 0; u < TU; ++u) {
         xx[u] = nx[u];
         vv[u] = nv[u];
       }
@@ -1652,6 +1657,145 @@ __global__ __launch_bounds__(TILE_THREADS) void glm_csc_tile_bwd_kernel(
       }
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// Wide dense rows: a block's 8 waves split every row's columns
+// ------------------------------------------------------------------------------------------
+// Rows wider than one wave's registers hold (bf16 d > 4096, fp32 > 2048, fp64 > 1024) are cut
+// into 8 column slices, one per wave of the block, each slice up to 64·CPL chunks of EPC: the block
+// walks its rows (block b: rows b, b + G, …) RU at a time (2; 1 for 8 chunks per lane, whose two
+// row buffers would spill), two steps in flight, every wave loads and dots its slice,
+// the 8 partial dots meet in LDS (one barrier per step, double-buffered) and are summed in
+// wave order, so every wave holds the same dot, multiplier and loss; each wave then accumulates
+// its slice of the gradient in registers. At the end the slices (disjoint) form the block's
+// gradient row in LDS and go into the accumulator with coalesced no-return atomics; the atomic
+// tail (ticket, last block) completes the round. One read of the batch per round, against two
+// library GEMVs (X_b·w, then X_bᵀ·m) plus loss and sum kernels on the path this replaces.
+constexpr int WIDE_WAVES = 8;
+
+template <typename T, int EPC, int CPL, int RU>
+__global__ __launch_bounds__(WIDE_WAVES * 64) void glm_round_wide_kernel(
+    const T* __restrict__ X, long ld, const typename AccOf<T>::type* __restrict__ y,
+    const typename AccOf<T>::type* __restrict__ wt, typename AccOf<T>::type* __restrict__ coef, long n, int d, long B,
+    int loss, int* __restrict__ state, GlmTail tl) {
+  typedef typename AccOf<T>::type A;
+  extern __shared__ __align__(16) unsigned char smem_wide[];
+  A* sbuf = reinterpret_cast<A*>(smem_wide);  // [d + 2]: the block's gradient row, then the tail's
+  int* sflag = reinterpret_cast<int*>(sbuf + d + 2);
+  __shared__ A pdot[2][WIDE_WAVES][RU];
+  int e;
+  if (!round_running(state, e)) return;
+  long start = 0, end = 0;
+  if (n > 0 && B > 0) {
+    const unsigned P = tl.nbatch > 0 ? (unsigned)tl.nbatch : (unsigned)((n + B - 1) / B);
+    start = (long)((unsigned)e % P) * B;
+    end = start + B < n ? start + B : n;
+  }
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nch = d / EPC;
+  const int per = (nch + WIDE_WAVES - 1) / WIDE_WAVES;  // chunks per slice (≤ 64·CPL: host-checked)
+  const int c0 = wave * per;
+  const int c1 = c0 + per < nch ? c0 + per : nch;
+  A w[CPL][EPC], acc[CPL][EPC];
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) {
+    const int c = c0 + lane + 64 * k;
+#pragma unroll
+    for (int i = 0; i < EPC; ++i) {
+      w[k][i] = c < c1 ? coef[c * EPC + i] : (A)0;
+      acc[k][i] = (A)0;
+    }
+  }
+  const long G = gridDim.x;
+  const long r0 = start + blockIdx.x;
+  const long nrows = r0 < end ? (end - r0 + G - 1) / G : 0;  // this block's rows
+  const bool has_wt = wt != nullptr;
+  A wsum = 0, lsum = 0;
+  Chunk<T, EPC> xa[RU][CPL], xb[RU][CPL];
+  auto load = [&](long j, Chunk<T, EPC> (&x)[RU][CPL]) {  // rows j … j + RU − 1 of this block
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const long jj = j + u < nrows ? j + u : (nrows > 0 ? nrows - 1 : 0);
+      const T* row = X + (r0 + jj * G) * ld;
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const int c = c0 + lane + 64 * k;
+        load_chunk_nt<T, EPC>(row + (c < c1 ? c : (c0 < c1 ? c0 : 0)) * EPC, x[u][k]);
+      }
+    }
+  };
+  auto process = [&](long j, Chunk<T, EPC> (&x)[RU][CPL], int par) {
+    A part[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      A s = 0;
+#pragma unroll
+      for (int k = 0; k < CPL; ++k)
+#pragma unroll
+        for (int i = 0; i < EPC; ++i) s += (A)Ld<T>::f(x[u][k].v[i]) * w[k][i];
+      part[u] = wave_sum(s);
+    }
+    if (lane == 0)
+#pragma unroll
+      for (int u = 0; u < RU; ++u) pdot[par][wave][u] = part[u];
+    __syncthreads();  // (double-buffered by step parity: one barrier per step)
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      A dot = 0;
+#pragma unroll
+      for (int q = 0; q < WIDE_WAVES; ++q) dot += pdot[par][q][u];
+      const bool ok = j + u < nrows;
+      const long r = r0 + (j + u) * G;
+      A l, m;
+      const A wu = ok ? (has_wt ? wt[r] : (A)1) : (A)0;
+      loss_and_mult(loss, dot, ok ? y[r] : (A)0, wu, l, m);
+      if (!ok) { l = (A)0; m = (A)0; }
+      if (wave == 0) {
+        wsum += wu;
+        lsum += l;
+      }
+#pragma unroll
+      for (int k = 0; k < CPL; ++k)
+#pragma unroll
+        for (int i = 0; i < EPC; ++i) acc[k][i] += m * (A)Ld<T>::f(x[u][k].v[i]);
+    }
+  };
+  if (nrows > 0) {  // (nrows is block-uniform: every wave makes the same barrier calls)
+    load(0, xa);
+    load(RU, xb);
+    int par = 0;
+    for (long j = 0; j < nrows; j += 2 * RU) {
+      process(j, xa, par);
+      par ^= 1;
+      load(j + 2 * RU, xa);  // rows past the block's last are clamped to it and masked
+      if (j + RU < nrows) {
+        process(j + RU, xb, par);
+        par ^= 1;
+        load(j + 3 * RU, xb);
+      }
+    }
+  }
+  // the block's gradient row: the waves' disjoint slices, then Σweight / Σloss
+  for (long c = threadIdx.x; c < d + 2; c += blockDim.x) sbuf[c] = (A)0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) {
+    const int c = c0 + lane + 64 * k;
+    if (c < c1)
+#pragma unroll
+      for (int i = 0; i < EPC; ++i) sbuf[c * EPC + i] = acc[k][i];
+  }
+  if (wave == 0 && lane == 0) {  // (every lane of wave 0 summed the same row values)
+    sbuf[d] = wsum;
+    sbuf[d + 1] = lsum;
+  }
+  __syncthreads();
+  const int rep = (int)(blockIdx.x % (tl.acc_reps > 1 ? tl.acc_reps : 1));
+  A* gacc = (A*)tl.acc + (long)rep * tl.acc_ld;
+  for (long c = threadIdx.x; c < d + 2; c += blockDim.x) atomicAdd(gacc + c, sbuf[c]);
+  glm_round_tail_atomic<A>(tl, d, coef, state, e, sbuf, sflag);
 }
 
 // ---------------------------- host-side dispatch ------------------------------------------
@@ -1753,10 +1897,15 @@ int launch_grad(int u, const void* X, long ld, const void* y, const void* wt, vo
 #ifdef FMLX_ISA_PROBE_U  // one row-loop variant only (ISA inspection)
   return launch_grad_u<T, EPC, CPL, FMLX_ISA_PROBE_U>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
 #endif
-  if (u >= 4 && BYTES <= 32)
-    return launch_grad_u<T, EPC, CPL, 4>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
-  if (u >= 2 && BYTES <= 64)
-    return launch_grad_u<T, EPC, CPL, 2>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
+  // (compile-time guards: the multi-row variants of wide rows would only exist to spill)
+  if constexpr (BYTES <= 32) {
+    if (u >= 4)
+      return launch_grad_u<T, EPC, CPL, 4>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
+  }
+  if constexpr (BYTES <= 32) {
+    if (u >= 2)
+      return launch_grad_u<T, EPC, CPL, 2>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
+  }
   return launch_grad_u<T, EPC, CPL, 1>(X, ld, y, wt, coef, n, d, B, loss, state, partials, nblocks, tl, flags, s);
 }
 
@@ -1912,6 +2061,61 @@ FMLX_API int fmlx_glm_round(int dtype, int epc, int cpl, int u, const void* X, l
     if (rc) return rc;
   }
   return 0;
+}
+
+template <typename T, int EPC, int CPL>
+static int launch_wide(const void* X, long ld, const void* y, const void* wt, void* coef, long n, int d, long B,
+                       int loss, int* state, int nblocks, const GlmTail& tl, hipStream_t s) {
+  typedef typename AccOf<T>::type A;
+  const size_t lds = (size_t)(d + 2) * sizeof(A) + 16;
+  if (lds > (size_t)LDS_PER_CU) return -8;
+  hipLaunchKernelGGL((glm_round_wide_kernel<T, EPC, CPL, CPL >= 8 ? 1 : 2>), dim3(nblocks), dim3(WIDE_WAVES * 64), lds,
+                     s, (const T*)X,
+                     ld, (const A*)y, (const A*)wt, (A*)coef, n, d, B, loss, state, tl);
+  return (int)hipGetLastError();
+}
+
+template <typename T, int EPC>
+static int launch_wide_cpl(int cpl, const void* X, long ld, const void* y, const void* wt, void* coef, long n, int d,
+                           long B, int loss, int* state, int nblocks, const GlmTail& tl, hipStream_t s) {
+  switch (cpl) {
+    case 2: return launch_wide<T, EPC, 2>(X, ld, y, wt, coef, n, d, B, loss, state, nblocks, tl, s);
+    case 4: return launch_wide<T, EPC, 4>(X, ld, y, wt, coef, n, d, B, loss, state, nblocks, tl, s);
+    case 8: return launch_wide<T, EPC, 8>(X, ld, y, wt, coef, n, d, B, loss, state, nblocks, tl, s);
+  }
+  return -1;
+}
+
+// One SGD round on rows too wide for one wave (see glm_round_wide_kernel): 16-byte chunks of EPC
+// elements, the row's chunks split over 8 waves, cpl = chunks per lane of a slice (2, 4 or 8).
+// mode TAIL_UPDATE (1 GPU) or TAIL_FEEDBACK (the caller all-reduces `feedback` and updates).
+FMLX_API int fmlx_glm_round_wide(int dtype, int epc, int cpl, const void* X, long ld, const void* y, const void* wt,
+                                 void* coef, long n, int d, long B, int loss, int* state, int nblocks, int mode,
+                                 int* cnt, void* acc, void* feedback, int max_iter, double tol, double lr, double reg,
+                                 double en, void* stream) {
+  if (mode != TAIL_UPDATE && mode != TAIL_FEEDBACK) return -3;
+  if (cnt == nullptr || acc == nullptr || nblocks < 1 || nblocks > TAIL_GROUP * TAIL_TOP) return -4;
+  if (mode == TAIL_FEEDBACK && feedback == nullptr) return -5;
+  if (d % epc != 0 || (d / epc + WIDE_WAVES - 1) / WIDE_WAVES > 64 * cpl) return -6;
+  GlmTail tl{};
+  tl.mode = mode;
+  tl.max_iter = max_iter;
+  tl.cnt = cnt;
+  tl.acc = acc;
+  tl.acc_reps = g_acc_reps;
+  tl.acc_ld = ((long)d + 2 + 63) / 64 * 64;
+  tl.ticket2 = g_ticket2;
+  tl.feedback = feedback;
+  tl.tol = tol;
+  tl.lr = lr;
+  tl.reg = reg;
+  tl.en = en;
+  tl.nbatch = (n > 0 && B > 0) ? (int)((n + B - 1) / B) : 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == DT_BF16 && epc == 8) return launch_wide_cpl<bf16_t, 8>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, nblocks, tl, s);
+  if (dtype == DT_F32 && epc == 4) return launch_wide_cpl<float, 4>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, nblocks, tl, s);
+  if (dtype == DT_F64 && epc == 2) return launch_wide_cpl<double, 2>(cpl, X, ld, y, wt, coef, n, d, B, loss, state, nblocks, tl, s);
+  return -1;
 }
 
 // stage1 scratch: [ceil(nparts/16)][d+2] of the accumulator type (nparts <= 512)

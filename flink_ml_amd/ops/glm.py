@@ -40,6 +40,8 @@ def round_blocks(X) -> int:
     lay = pick_layout(X) if X is not None else None
     if lay is not None and GRAD_UNROLL == 0 and lay[0] * lay[1] * X.element_size() == 32:
         return 224
+    if lay is not None and (lay[0] * lay[1] * X.element_size() > 32 or X.dtype == torch.float64):
+        return 256  # over 128 VGPRs (csrc/glm.hip glm_min_waves): one block per CU
     return 512
 
 
@@ -100,9 +102,43 @@ def pick_layout(X: torch.Tensor) -> Optional[Tuple[int, int]]:
     cpl = 1
     while cpl * 64 < nch:
         cpl *= 2
-    if cpl > MAX_CPL:
+    if cpl > MAX_CPL or (es == 2 and cpl > 4):
+        # (bf16 rows of 2049–4096: the one-wave kernel needs > 256 VGPRs there and spills — 1.9
+        # TB/s vs 5 TB/s on the wide-row kernel, profiles/r5/glm_widths*.jsonl)
         return None
     return epc, cpl
+
+
+WIDE_WAVES = 8  # csrc/glm.hip glm_round_wide_kernel: waves splitting a row's columns
+WIDE_FUSED = os.environ.get("FMLX_GLM_WIDE_FUSED", "1") == "1"  # 0: wide rows take the GEMV path (A/B)
+
+
+def pick_wide_layout(X: torch.Tensor) -> Optional[Tuple[int, int]]:
+    """(epc, cpl) of the wide-row round kernel (16-byte chunks, a row's chunks split over 8
+    waves, cpl chunks per lane of a slice), or None (misaligned, or wider than 8 × 64 × 8 chunks:
+    bf16 32768, fp32 16384, fp64 8192)."""
+    if X.dim() != 2 or X.stride(1) != 1:
+        return None
+    es = X.element_size()
+    epc = 16 // es
+    d = X.shape[1]
+    if d % epc or (X.stride(0) * es) % 16 or X.data_ptr() % 16:
+        return None
+    per = -(-(d // epc) // WIDE_WAVES)
+    for cpl in (2, 4, 8):
+        if 64 * cpl >= per:
+            return epc, cpl
+    return None
+
+
+def glm_round_wide(X, y, wt, coef, B: int, loss: int, state, scratch: "RoundScratch", mode: int, feedback,
+                   max_iter: int, tol: float, lr: float, reg: float, en: float) -> None:
+    """One round of the wide-row kernel (atomic tail; TAIL_UPDATE or TAIL_FEEDBACK)."""
+    epc, cpl = pick_wide_layout(X)
+    native.call("fmlx_glm_round_wide", native.dtype_code(X.dtype), epc, cpl, native.ptr(X), X.stride(0), native.ptr(y),
+                native.ptr(wt), native.ptr(coef), X.shape[0], X.shape[1], B, loss, native.ptr(state), scratch.nparts,
+                mode, native.ptr(scratch.cnt), native.ptr(scratch.acc), native.ptr(feedback), int(max_iter), float(tol),
+                float(lr), float(reg), float(en), native.stream_ptr(X.device))
 
 
 def pad_columns(X: torch.Tensor) -> Optional[torch.Tensor]:
@@ -120,7 +156,7 @@ def pad_columns(X: torch.Tensor) -> Optional[torch.Tensor]:
     cpl = 1
     while cpl * 64 < nch:
         cpl *= 2
-    if cpl > MAX_CPL:
+    if cpl > MAX_CPL and -(-nch // WIDE_WAVES) > 64 * 8:  # neither the one-wave nor the wide kernel
         return None
     need = n * dp * X.element_size()
     free, _ = torch.cuda.mem_get_info(X.device)
@@ -129,7 +165,7 @@ def pad_columns(X: torch.Tensor) -> Optional[torch.Tensor]:
     Xp = torch.empty((n, dp), dtype=X.dtype, device=X.device)
     Xp[:, d:].zero_()
     Xp[:, :d].copy_(X)
-    return Xp if pick_layout(Xp) is not None else None
+    return Xp if pick_layout(Xp) is not None or pick_wide_layout(Xp) is not None else None
 
 
 def grad_partials(X, y, wt, coef, B: int, loss: int, state, partials, nblocks: int) -> None:
@@ -407,7 +443,7 @@ class BatchCsc:
                 # a block runs one tile, so the round takes one tile's time: cut the largest batch
                 # into about one tile per CU (fewer, fuller tiles leave CUs idle)
                 cus = torch.cuda.get_device_properties(values.device).multi_processor_count
-                self.EB = max(1024, min(self.EB, -(-most // max(1, cus - 2))))
+                self.EB = min(self.EB, max(1024, -(-most // max(1, cus - 2))))  # (EB + EL ≤ ET kept)
             self.tstride = min(d, most // self.EB + 2 * (most // self.EL) + 1) + 1
         else:
             self.tstride = 0

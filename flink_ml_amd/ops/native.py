@@ -59,6 +59,9 @@ _KERNEL_SIGS = {
                        c_int, c_double,
                        c_double, c_double, c_double, c_void_p, c_int, c_int, c_void_p, c_void_p, c_long, c_int, c_int,
                        c_int, c_int, c_void_p, c_void_p],
+    "fmlx_glm_round_wide": [c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_long, c_int, c_long,
+                            c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_double, c_double,
+                            c_double, c_double, c_void_p],
     "fmlx_glm_set_tuning": [c_long, c_int],
     "fmlx_glm_set_tail_tuning": [c_int, c_int],
     "fmlx_glm_set_trace": [c_void_p],

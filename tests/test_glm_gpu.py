@@ -135,9 +135,11 @@ def test_lr_estimator_on_gpu_goldens():
 
 
 @pytest.mark.parametrize("dtype,d", [(torch.float32, 3000), (torch.float64, 3000), (torch.bfloat16, 5000),
-                                     (torch.bfloat16, 5001)])
-def test_device_sgd_wide_dense_gemv_path(dtype, d):
-    """Rows the register-resident round kernel cannot hold run as two GEMVs + the device update."""
+                                     (torch.bfloat16, 5001), (torch.float32, 16384), (torch.float64, 1500)])
+def test_device_sgd_wide_dense_fused_kernel(dtype, d):
+    """Rows one wave cannot hold run on the wide-row kernel (8 waves split each row's columns;
+    d = 5001 through the zero-padded copy), one fused launch per round, weighted and unweighted:
+    results equal the fp64 host trainer, and tol termination is decided on the device."""
     _need_gpu()
     from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
 
@@ -146,11 +148,45 @@ def test_device_sgd_wide_dense_gemv_path(dtype, d):
     X = torch.rand((n, d), generator=g, dtype=torch.float64).to(dtype)
     y = (X.to(torch.float64) @ torch.linspace(-1, 1, d, dtype=torch.float64) > 0).double()
     w = torch.rand(n, generator=g, dtype=torch.float64) + 0.5
+    # (the L1 part of the elastic net flips coefficients near 0 by ±lr·en·reg on a last-bit change of
+    # a 16384-term fp32 dot: L2 only at that width)
+    en = 0.5 if d <= 5001 else 0.0
     for loss in ("logistic", "hinge", "leastsquare"):
-        sgd = SGD(max_iter=7, learning_rate=0.05, global_batch_size=400, tol=1e-9, reg=0.1, elastic_net=0.5)
+        for wt in (w, None):
+            sgd = SGD(max_iter=7, learning_rate=0.05, global_batch_size=400, tol=1e-9, reg=0.1, elastic_net=en)
+            ref = TorchGlmTrainer(sgd, np.zeros(d), X.to(torch.float64), y, wt, loss).fit()
+            tr = DeviceGlmTrainer(sgd, np.zeros(d), X.cuda(), y.cuda(), None if wt is None else wt.cuda(), loss)
+            assert tr.wide_fused and not tr.wide
+            got = tr.fit()
+            assert got.shape == (d,) and tr.rounds_executed() == 7
+            tol = (1e-10 if dtype == torch.float64 else 1e-4) * max(1.0, np.abs(ref).max())
+            assert np.abs(got - ref).max() < tol, (loss, np.abs(got - ref).max())
+    # tol termination decided on the device by the wide kernel's tail
+    sgd2 = SGD(max_iter=100, learning_rate=0.5, global_batch_size=n, tol=0.3)
+    r2 = TorchGlmTrainer(sgd2, np.zeros(d), X.to(torch.float64), y, None, "logistic")
+    c2 = r2.fit()
+    t2 = DeviceGlmTrainer(sgd2, np.zeros(d), X.cuda(), y.cuda(), None, "logistic")
+    g2 = t2.fit()
+    assert t2.rounds_executed() == r2.rounds
+    assert np.abs(g2 - c2).max() < (1e-8 if dtype == torch.float64 else 1e-4) * max(1.0, np.abs(c2).max())
+
+
+@pytest.mark.parametrize("dtype,d", [(torch.float32, 40000), (torch.bfloat16, 40001)])
+def test_device_sgd_wide_dense_gemv_path(dtype, d):
+    """Rows beyond the wide-row kernel (8 × 64 × 8 chunks) run as two GEMVs + the device update."""
+    _need_gpu()
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
+
+    g = torch.Generator(device="cpu").manual_seed(d)
+    n = 300
+    X = torch.rand((n, d), generator=g, dtype=torch.float64).to(dtype)
+    y = (X.to(torch.float64) @ torch.linspace(-1, 1, d, dtype=torch.float64) > 0).double()
+    w = torch.rand(n, generator=g, dtype=torch.float64) + 0.5
+    for loss in ("logistic", "hinge", "leastsquare"):
+        sgd = SGD(max_iter=7, learning_rate=0.05, global_batch_size=100, tol=1e-9, reg=0.1, elastic_net=0.5)
         ref = TorchGlmTrainer(sgd, np.zeros(d), X.to(torch.float64), y, w, loss).fit()
         tr = DeviceGlmTrainer(sgd, np.zeros(d), X.cuda(), y.cuda(), w.cuda(), loss)
-        assert tr.wide
+        assert tr.wide and not tr.wide_fused
         got = tr.fit()
         assert tr.rounds_executed() == 7
         tol = (1e-10 if dtype == torch.float64 else 1e-4) * max(1.0, np.abs(ref).max())
@@ -160,8 +196,9 @@ def test_device_sgd_wide_dense_gemv_path(dtype, d):
 @pytest.mark.parametrize("dtype,d", [(torch.float32, 1001), (torch.float32, 2047), (torch.bfloat16, 1003),
                                      (torch.bfloat16, 4093), (torch.float64, 1023)])
 def test_device_sgd_misaligned_width_padded_to_fused_kernel(dtype, d):
-    """Widths that break the 16-byte row chunks (fp32 d = 1001, bf16 d % 8 != 0) train on the fused
-    round kernel through a zero-padded copy: the padding coefficients stay 0, the returned model
+    """Widths that break the 16-byte row chunks (fp32 d = 1001, bf16 d % 8 != 0) train on a fused
+    round kernel (one-wave, or wide-row for bf16 4093) through a zero-padded copy: the padding
+    coefficients stay 0, the returned model
     has the input width, and results equal the host trainer (and the GEMV path, pad=False)."""
     _need_gpu()
     from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
@@ -175,7 +212,8 @@ def test_device_sgd_misaligned_width_padded_to_fused_kernel(dtype, d):
         sgd = SGD(max_iter=6, learning_rate=0.05, global_batch_size=400, tol=1e-9, reg=0.1, elastic_net=0.5)
         ref = TorchGlmTrainer(sgd, np.zeros(d), X.to(torch.float64), y, w, loss).fit()
         tr = DeviceGlmTrainer(sgd, np.zeros(d), X.cuda(), y.cuda(), w.cuda(), loss)
-        assert not tr.wide and tr.layout is not None and tr.X.shape[1] % (16 // X.element_size()) == 0
+        assert not tr.wide and (tr.layout is not None or tr.wide_fused)
+        assert tr.X.shape[1] % (16 // X.element_size()) == 0
         got = tr.fit()
         assert got.shape == (d,) and tr.rounds_executed() == 6
         assert float(tr.coef[d:].abs().max() if tr.X.shape[1] > d else 0.0) == 0.0
