@@ -264,8 +264,8 @@ class DeviceGlmTrainer:
             if self.w is None:
                 self.w = torch.ones(self.n, dtype=acc, device=dev)
         elif self.wide_fused:
-            # one 8-wave block per CU (~200 VGPRs per lane), each walking its rows two at a time
-            cus = torch.cuda.get_device_properties(dev).multi_processor_count
+            # one or two 8-wave blocks per CU (by the slice's register need), each walking its rows
+            cus = torch.cuda.get_device_properties(dev).multi_processor_count * gk.wide_blocks_per_cu(self.X)
             share = device_sharers(ctx) if self.distributed else 1
             self.nparts = max(1, min(cus // max(1, share), -(-max(self.B, 1) // 2)))
             self.scratch = gk.RoundScratch(self.nparts, self.d, acc, dev, det=False)

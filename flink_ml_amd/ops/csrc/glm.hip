@@ -2079,6 +2079,7 @@ template <typename T, int EPC>
 static int launch_wide_cpl(int cpl, const void* X, long ld, const void* y, const void* wt, void* coef, long n, int d,
                            long B, int loss, int* state, int nblocks, const GlmTail& tl, hipStream_t s) {
   switch (cpl) {
+    case 1: return launch_wide<T, EPC, 1>(X, ld, y, wt, coef, n, d, B, loss, state, nblocks, tl, s);
     case 2: return launch_wide<T, EPC, 2>(X, ld, y, wt, coef, n, d, B, loss, state, nblocks, tl, s);
     case 4: return launch_wide<T, EPC, 4>(X, ld, y, wt, coef, n, d, B, loss, state, nblocks, tl, s);
     case 8: return launch_wide<T, EPC, 8>(X, ld, y, wt, coef, n, d, B, loss, state, nblocks, tl, s);
@@ -2087,7 +2088,7 @@ static int launch_wide_cpl(int cpl, const void* X, long ld, const void* y, const
 }
 
 // One SGD round on rows too wide for one wave (see glm_round_wide_kernel): 16-byte chunks of EPC
-// elements, the row's chunks split over 8 waves, cpl = chunks per lane of a slice (2, 4 or 8).
+// elements, the row's chunks split over 8 waves, cpl = chunks per lane of a slice (1, 2, 4 or 8).
 // mode TAIL_UPDATE (1 GPU) or TAIL_FEEDBACK (the caller all-reduces `feedback` and updates).
 FMLX_API int fmlx_glm_round_wide(int dtype, int epc, int cpl, const void* X, long ld, const void* y, const void* wt,
                                  void* coef, long n, int d, long B, int loss, int* state, int nblocks, int mode,

@@ -125,10 +125,17 @@ def pick_wide_layout(X: torch.Tensor) -> Optional[Tuple[int, int]]:
     if d % epc or (X.stride(0) * es) % 16 or X.data_ptr() % 16:
         return None
     per = -(-(d // epc) // WIDE_WAVES)
-    for cpl in (2, 4, 8):
+    for cpl in (1, 2, 4, 8):
         if 64 * cpl >= per:
             return epc, cpl
     return None
+
+
+def wide_blocks_per_cu(X) -> int:
+    """Blocks of the wide-row kernel per CU: 2 for one chunk per lane (measured: bf16 4096 0.184
+    vs 0.295 ms per round), else 1 (bf16 8192 at two chunks: 0.352 with 2 per CU vs 0.342)."""
+    lay = pick_wide_layout(X)
+    return 2 if lay is not None and lay[1] <= 1 else 1
 
 
 def glm_round_wide(X, y, wt, coef, B: int, loss: int, state, scratch: "RoundScratch", mode: int, feedback,
