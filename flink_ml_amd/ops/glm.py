@@ -80,8 +80,9 @@ def set_trace(buf: Optional[torch.Tensor]) -> None:
     native.call("fmlx_glm_set_trace", native.ptr(buf))
 
 
-def pick_layout(X: torch.Tensor) -> Optional[Tuple[int, int]]:
-    """(epc, cpl) for the register-resident path, or None if d is too wide / misaligned."""
+def pick_layout(X: torch.Tensor, rounds: bool = True) -> Optional[Tuple[int, int]]:
+    """(epc, cpl) for the register-resident path, or None if d is too wide / misaligned.
+    ``rounds=False``: the prediction kernel's limit (no gradient registers: bf16 up to 8 chunks)."""
     if X.dim() != 2:
         return None
     n, d = X.shape
@@ -102,7 +103,7 @@ def pick_layout(X: torch.Tensor) -> Optional[Tuple[int, int]]:
     cpl = 1
     while cpl * 64 < nch:
         cpl *= 2
-    if cpl > MAX_CPL or (es == 2 and cpl > 4):
+    if cpl > MAX_CPL or (rounds and es == 2 and cpl > 4):
         # (bf16 rows of 2049–4096: the one-wave kernel needs > 256 VGPRs there and spills — 1.9
         # TB/s vs 5 TB/s on the wide-row kernel, profiles/r5/glm_widths*.jsonl)
         return None
@@ -718,7 +719,7 @@ def predict_dense(X: torch.Tensor, coef: torch.Tensor, mode: int, threshold: flo
     """Returns (prediction[n] f64, raw[n,2] f64 or None)."""
     n = X.shape[0]
     if X.device.type == "cuda":
-        lay = pick_layout(X)
+        lay = pick_layout(X, rounds=False)
         if lay is not None and X.dtype in (torch.float32, torch.float64, torch.bfloat16):
             acc = torch.float64 if X.dtype == torch.float64 else torch.float32
             c = coef.to(device=X.device, dtype=acc).contiguous()
