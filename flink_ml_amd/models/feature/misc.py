@@ -138,13 +138,50 @@ def _round(x, d=0):
     return int(Decimal(x).scaleb(d).quantize(Decimal(1), rounding=ROUND_HALF_UP).scaleb(-d))
 
 
+def _truncate(x, d=0):
+    """TRUNCATE(x[, d]): toward zero at d decimals, the input's type kept (Flink)."""
+    if x is None or d is None:
+        return None
+    d = int(d)
+    if isinstance(x, int):
+        return x if d >= 0 else int(x / 10 ** -d) * 10 ** -d
+    if x != x or x in (float("inf"), float("-inf")):
+        return x
+    sc = 10.0 ** d
+    return math.trunc(x * sc) / sc
+
+
+def _least(*a):
+    return None if any(v is None for v in a) else min(a)
+
+
+def _greatest(*a):
+    return None if any(v is None for v in a) else max(a)
+
+
 def _register_functions(con: sqlite3.Connection) -> None:
-    def f1(fn):
-        return lambda x: None if x is None else fn(x)
+    from .sql_device import java_math
+
+    def f1(fn):  # NULL in, NULL out; outside the domain NaN like Java's Math (Python raises)
+        return lambda x: None if x is None else java_math(fn, x)
 
     for name, fn in (("SQRT", math.sqrt), ("LN", math.log), ("LOG10", math.log10), ("EXP", math.exp),
-                     ("ABS", abs), ("SIN", math.sin), ("COS", math.cos), ("TAN", math.tan)):
+                     ("ABS", abs), ("SIN", math.sin), ("COS", math.cos), ("TAN", math.tan), ("ASIN", math.asin),
+                     ("ACOS", math.acos), ("ATAN", math.atan), ("DEGREES", math.degrees),
+                     ("RADIANS", math.radians), ("LOG2", math.log2), ("SINH", math.sinh), ("COSH", math.cosh),
+                     ("TANH", math.tanh), ("COT", lambda a: 1.0 / math.tan(a)), ("LOG", math.log)):
         con.create_function(name, 1, f1(fn), deterministic=True)
+    con.create_function("LOG", 2, lambda b, x: None if b is None or x is None else
+                        java_math(lambda u, v: math.log(v) / math.log(u), b, x), deterministic=True)
+    con.create_function("ATAN2", 2, lambda a, b: None if a is None or b is None else math.atan2(a, b),
+                        deterministic=True)
+    con.create_function("TRUNCATE", 1, _truncate, deterministic=True)
+    con.create_function("TRUNCATE", 2, _truncate, deterministic=True)
+    con.create_function("PI", 0, lambda: math.pi, deterministic=True)
+    con.create_function("E", 0, lambda: math.e, deterministic=True)
+    con.create_function("IF", 3, lambda c, a, b: a if c else b, deterministic=True)
+    con.create_function("LEAST", -1, _least, deterministic=True)
+    con.create_function("GREATEST", -1, _greatest, deterministic=True)
     for name, fn in (("CEIL", math.ceil), ("CEILING", math.ceil), ("FLOOR", math.floor)):
         con.create_function(name, 1, _keep_type(fn), deterministic=True)
     con.create_function("SIGN", 1, _sign, deterministic=True)

@@ -6,31 +6,37 @@ The subset a feature pipeline uses is evaluated column-at-a-time on the columns'
 input never leaves HBM, ``SELECT *`` columns (vectors, sparse, strings included) pass through by
 reference, and a ``WHERE`` is one mask + one gather per column:
 
-    SELECT [ALL] item, ... FROM __THIS__ [WHERE cond] [GROUP BY expr, ...]
+    SELECT [ALL | DISTINCT] item, ... FROM __THIS__ [WHERE cond] [GROUP BY expr, ... [HAVING cond]]
+           [ORDER BY expr [ASC | DESC], ...] [LIMIT n [OFFSET m]]
     item  := * | expr [[AS] alias]
     expr  := arithmetic (+ - * / %, unary -), comparisons (= <> != < <= > >=), AND / OR / NOT,
              BETWEEN, IN (...), IS [NOT] NULL, CASE WHEN ... THEN ... [ELSE ...] END,
              CAST(x AS DOUBLE|FLOAT|INT|INTEGER|BIGINT|BOOLEAN), numeric literals, TRUE / FALSE,
-             ABS SQRT LN LOG10 EXP CEIL CEILING FLOOR SIN COS TAN ASIN ACOS ATAN SIGN DEGREES
-             RADIANS POWER MOD ROUND LEAST GREATEST,
+             ABS SQRT LN LOG LOG2 LOG10 EXP CEIL CEILING FLOOR SIN COS TAN COT ASIN ACOS ATAN ATAN2
+             SINH COSH TANH SIGN DEGREES RADIANS POWER MOD ROUND TRUNCATE LEAST GREATEST PI E IF
+             COALESCE,
              aggregates SUM COUNT(*|x) AVG MIN MAX (with or without GROUP BY)
 
 Types follow Flink: integer op integer stays integer ('/' truncates toward zero, '%' keeps the
 dividend's sign), anything with a floating operand is floating, comparisons are BOOLEAN, unnamed
 expressions are called ``EXPR$<i>``, SUM keeps its argument's type and AVG of an integer column is
 an integer (sum / count truncated toward zero, Flink's IntegralAvgAggFunction), CAST to INT /
-BIGINT truncates toward zero, ROUND is half away from zero. GROUP BY output is ordered by key (ascending). Distributed:
-row-wise statements run per rank; aggregates are computed per rank, the small partial tables are
-all-gathered and merged on every rank, and the result is dealt round-robin.
+BIGINT truncates toward zero, ROUND is half away from zero, TRUNCATE toward zero, LOG(x) is the
+natural log and LOG(b, x) = LN(x) / LN(b), math outside a function's domain is NaN (Java's Math).
+GROUP BY and DISTINCT output is ordered by key (ascending). ORDER BY is a stable lexicographic sort
+over output columns (names, 1-based positions or expressions of them) with NaN the largest
+DOUBLE (Double.compare). Distributed: row-wise statements run per rank; aggregates are computed per
+rank, the small partial tables are all-gathered and merged on every rank, and the result is dealt
+round-robin; ORDER BY / LIMIT need the global order and fall back when world > 1.
 
-Anything outside the subset (strings, joins, windows, ORDER BY, integer division by zero, ...)
+Anything outside the subset (strings, joins, windows, NULL results, integer division by zero, ...)
 raises ``Unsupported`` and the caller falls back to the host SQL engine.
 """
 from __future__ import annotations
 
 import math
 import re
-from typing import List, Optional
+from typing import List, NamedTuple, Optional
 
 import numpy as np
 import torch
@@ -86,6 +92,17 @@ def _tokenize(s: str):
 #      ("agg", NAME, arg|None) ("case", [(cond, val)], else) ("cast", a, type) ("isnull", a, negate)
 #      ("in", a, [vals], negate) ("star",)
 
+class Query(NamedTuple):
+    items: list
+    where: object
+    group: Optional[list]
+    having: object
+    order: list  # [(expr, descending)]
+    limit: Optional[int]
+    offset: int
+    distinct: bool
+
+
 class _Parser:
     def __init__(self, toks):
         self.t = toks
@@ -115,8 +132,7 @@ class _Parser:
     def query(self):
         self.expect("kw", "SELECT")
         self.accept("kw", "ALL")
-        if self.peek() == ("kw", "DISTINCT"):
-            raise Unsupported("DISTINCT")
+        distinct = bool(self.accept("kw", "DISTINCT"))
         items = [self.item()]
         while self.accept("op", ","):
             items.append(self.item())
@@ -124,7 +140,8 @@ class _Parser:
         src = self.expect("id")[1]
         if src != "__THIS__":
             raise Unsupported("FROM %s" % src)
-        where = group = None
+        where = group = having = None
+        order, limit, offset = [], None, 0
         if self.accept("kw", "WHERE"):
             where = self.expr()
         if self.accept("kw", "GROUP"):
@@ -132,8 +149,33 @@ class _Parser:
             group = [self.expr()]
             while self.accept("op", ","):
                 group.append(self.expr())
+        if self.accept("kw", "HAVING"):
+            having = self.expr()
+        if self.accept("kw", "ORDER"):
+            self.expect("kw", "BY")
+            while True:
+                e = self.expr()
+                desc = False
+                if self.peek()[0] == "id" and self.peek()[1].upper() in ("ASC", "DESC"):
+                    desc = self.take()[1].upper() == "DESC"
+                if self.peek()[0] == "id" and self.peek()[1].upper() == "NULLS":
+                    raise Unsupported("NULLS FIRST / LAST")
+                order.append((e, desc))
+                if not self.accept("op", ","):
+                    break
+        if self.accept("kw", "LIMIT"):
+            tok = self.expect("num")
+            if not re.fullmatch(r"\d+", tok[1]):
+                raise Unsupported("LIMIT %s" % tok[1])
+            limit = int(tok[1])
+            if self.peek()[0] == "id" and self.peek()[1].upper() == "OFFSET":
+                self.take()
+                tok = self.expect("num")
+                if not re.fullmatch(r"\d+", tok[1]):
+                    raise Unsupported("OFFSET %s" % tok[1])
+                offset = int(tok[1])
         self.expect("eof")
-        return items, where, group
+        return Query(items, where, group, having, order, limit, offset, distinct)
 
     def item(self):
         if self.accept("op", "*"):
@@ -279,6 +321,19 @@ def parse(statement: str):
 
 # ---- evaluation
 
+def java_math(fn, *a):
+    """A scalar math function with Java's Math semantics: outside the domain NaN (Python raises),
+    overflow ±inf."""
+    try:
+        return fn(*a)
+    except ValueError:
+        return math.nan
+    except OverflowError:
+        return math.inf
+    except ZeroDivisionError:
+        return math.inf
+
+
 def _is_int(x) -> bool:
     if isinstance(x, torch.Tensor):
         return not x.dtype.is_floating_point and x.dtype != torch.bool
@@ -302,19 +357,22 @@ def _num(x):
 _FN1 = {
     "ABS": torch.abs, "SQRT": torch.sqrt, "LN": torch.log, "LOG10": torch.log10, "EXP": torch.exp,
     "SIN": torch.sin, "COS": torch.cos, "TAN": torch.tan, "ASIN": torch.asin, "ACOS": torch.acos,
-    "ATAN": torch.atan, "DEGREES": torch.rad2deg, "RADIANS": torch.deg2rad,
+    "ATAN": torch.atan, "DEGREES": torch.rad2deg, "RADIANS": torch.deg2rad, "LOG2": torch.log2,
+    "SINH": torch.sinh, "COSH": torch.cosh, "TANH": torch.tanh, "COT": lambda a: 1.0 / torch.tan(a),
 }
 # host tensors go through numpy: its sqrt is correctly rounded like Java's Math.sqrt (torch's
 # vectorised CPU sqrt is not: sqrt(2.0) comes out one ulp low)
 _FN1_NP = {
     "ABS": np.abs, "SQRT": np.sqrt, "LN": np.log, "LOG10": np.log10, "EXP": np.exp, "SIN": np.sin, "COS": np.cos,
     "TAN": np.tan, "ASIN": np.arcsin, "ACOS": np.arccos, "ATAN": np.arctan, "DEGREES": np.degrees,
-    "RADIANS": np.radians,
+    "RADIANS": np.radians, "LOG2": np.log2, "SINH": np.sinh, "COSH": np.cosh, "TANH": np.tanh,
+    "COT": lambda a: 1.0 / np.tan(a),
 }
 _FN1_PY = {
     "ABS": abs, "SQRT": math.sqrt, "LN": math.log, "LOG10": math.log10, "EXP": math.exp, "SIN": math.sin,
     "COS": math.cos, "TAN": math.tan, "ASIN": math.asin, "ACOS": math.acos, "ATAN": math.atan,
-    "DEGREES": math.degrees, "RADIANS": math.radians,
+    "DEGREES": math.degrees, "RADIANS": math.radians, "LOG2": math.log2, "SINH": math.sinh, "COSH": math.cosh,
+    "TANH": math.tanh, "COT": lambda a: 1.0 / math.tan(a),
 }
 
 
@@ -443,7 +501,7 @@ class _Eval:
         if name in _FN1 and len(args) == 1:
             a = _num(args[0])
             if not isinstance(a, torch.Tensor):
-                return _FN1_PY[name](a)
+                return java_math(_FN1_PY[name], a)
             if name != "ABS" and not a.dtype.is_floating_point:
                 a = a.to(torch.float64)
             if a.device.type == "cpu":
@@ -480,6 +538,42 @@ class _Eval:
             if not isinstance(a, torch.Tensor):
                 return math.copysign(math.floor(abs(a) * s + 0.5) / s, a) if a == a else a
             return torch.sign(a) * torch.floor(torch.abs(a) * s + 0.5) / s
+        if name == "LOG" and len(args) in (1, 2):  # Flink: LOG(x) = LN(x), LOG(b, x) = LN(x) / LN(b)
+            if len(args) == 1:
+                return self.fn("LN", args)
+            return self.binary("/", self.fn("LN", [args[1]]), self.fn("LN", [args[0]]))
+        if name == "ATAN2" and len(args) == 2:
+            a, b = _num(args[0]), _num(args[1])
+            if not isinstance(a, torch.Tensor) and not isinstance(b, torch.Tensor):
+                return math.atan2(a, b)
+            a, b = self.full(a), self.full(b)
+            return torch.atan2(a.to(torch.float64) if not a.dtype.is_floating_point else a,
+                               b.to(torch.float64) if not b.dtype.is_floating_point else b)
+        if name == "TRUNCATE" and len(args) in (1, 2):  # toward zero at d decimals, the type kept
+            a = _num(args[0])
+            d = int(args[1]) if len(args) == 2 else 0
+            if _is_int(a) and d >= 0:
+                return a
+            if not _is_float(a):
+                raise Unsupported("TRUNCATE of a non-numeric value")
+            sc = 10.0 ** d
+            if not isinstance(a, torch.Tensor):
+                return math.trunc(a * sc) / sc if math.isfinite(a) else a
+            return torch.trunc(a * sc) / sc
+        if name in ("PI", "E") and not args:
+            return math.pi if name == "PI" else math.e
+        if name == "IF" and len(args) == 3:
+            c = self.boolean(args[0])
+            a, b = self.promote(self.full(_num(args[1])), self.full(_num(args[2])))
+            return torch.where(self.full(c), a, b)
+        if name == "COALESCE" and args:
+            vals = [v for v in args if v is not None]
+            if not vals:
+                raise Unsupported("COALESCE of NULLs")
+            out = self.full(_num(vals[0]))  # device values are never NULL: the first non-NULL argument
+            for v in vals[1:]:
+                out, _ = self.promote(out, self.full(_num(v)))
+            return out
         if name in ("LEAST", "GREATEST") and len(args) >= 2:
             out = self.full(_num(args[0]))
             for x in args[1:]:
@@ -537,9 +631,19 @@ def _device_of(t: Table):
 def evaluate(statement: str, t: Table, world: int = 1, rank: int = 0) -> Table:
     """Runs ``statement`` against ``t`` on the columns' device; raises ``Unsupported`` outside the
     subset. ``world > 1``: aggregates are merged across ranks and dealt round-robin."""
-    items, where, group = parse(statement)
+    q = parse(statement)
+    items, where, group = q.items, q.where, q.group
+    if (q.order or q.limit is not None) and world > 1:
+        raise Unsupported("ORDER BY / LIMIT over ranks (needs the global order)")
+    if q.distinct:
+        # SELECT DISTINCT e1, e2, ... = GROUP BY e1, e2, ... (ordered by key like every GROUP BY)
+        if group is not None or q.having is not None or any(_has_agg(e) or e[0] == "star" for e, _ in items):
+            raise Unsupported("DISTINCT with aggregates, GROUP BY or *")
+        group = [e for e, _ in items]
     dev = _device_of(t)
     aggregate = group is not None or any(_has_agg(e) for e, _ in items)
+    if q.having is not None and not aggregate:
+        raise Unsupported("HAVING without aggregation")
     werr = None
     if where is not None:
         try:
@@ -567,13 +671,48 @@ def evaluate(statement: str, t: Table, world: int = 1, rank: int = 0) -> Table:
                 continue
             name = _out_name(e, alias, i, used)
             out[name] = ev.full(ev(e))
-        return Table(out, num_rows=t.num_rows)
-    return _aggregate(items, group or [], t, dev, world, rank, werr)
+        res = Table(out, num_rows=t.num_rows)
+        return _order_limit(res, q, t) if q.order or q.limit is not None else res
+    res = _aggregate(items, group or [], t, dev, world, rank, werr, having=q.having)
+    return _order_limit(res, q, None) if q.order or q.limit is not None else res
+
+
+def _order_limit(res: Table, q: "Query", src: Optional[Table]) -> Table:
+    """ORDER BY (stable, lexicographic; NaN the largest DOUBLE as Double.compare) then LIMIT /
+    OFFSET over the result rows. Keys: output columns by name or 1-based position, or expressions
+    of output columns — and, for row-wise statements (``src``: the filtered input, row-aligned with
+    the result), of input columns the output does not shadow."""
+    n = res.num_rows
+    dev = _device_of(res) if res.column_names else torch.device("cpu")
+    perm = torch.arange(n, device=dev)
+    if q.order:
+        names = res.column_names
+        ctx = {c: res.column(c) for c in names}
+        if src is not None:
+            for c in src.column_names:
+                ctx.setdefault(c, src.column(c))
+        ev = _Eval(Table(ctx, num_rows=n), n, dev)
+        keys = []
+        for e, desc in q.order:
+            if e[0] == "lit" and isinstance(e[1], int) and not isinstance(e[1], bool):
+                if not 1 <= e[1] <= len(names):
+                    raise Unsupported("ORDER BY position %d" % e[1])
+                k = res.column(names[e[1] - 1])
+            else:
+                k = ev.full(ev(e))
+            if not isinstance(k, torch.Tensor) or k.dim() != 1:
+                raise Unsupported("ORDER BY a non-scalar column")
+            keys.append((k.to(torch.int8) if k.dtype == torch.bool else k, desc))
+        for k, desc in reversed(keys):
+            perm = perm[torch.sort(k[perm], stable=True, descending=desc).indices]
+    if q.limit is not None or q.offset:
+        perm = perm[q.offset:q.offset + q.limit if q.limit is not None else None]
+    return res.take(perm)
 
 
 # ---- aggregation: per-group partial states (sum, count, min, max) so ranks can merge them
 
-def _local_states(items, group, t: Table, dev, world):
+def _local_states(items, group, t: Table, dev, world, having=None):
     if any(e[0] == "star" for e, _ in items):
         raise Unsupported("SELECT * with aggregates")
     ev = _Eval(t, t.num_rows, dev)
@@ -606,6 +745,7 @@ def _local_states(items, group, t: Table, dev, world):
         raise Unsupported("non-grouped expression in an aggregate query")
 
     outs = [(collect(e), alias) for e, alias in items]
+    having_c = collect(having) if having is not None else None
     n = t.num_rows
     if keys:
         K = torch.stack([k.to(torch.float64) if k.dtype.is_floating_point else k.to(torch.int64) for k in keys], 1) \
@@ -640,14 +780,14 @@ def _local_states(items, group, t: Table, dev, world):
         states.append(st)
     if not keys and world == 1 and n == 0:
         raise Unsupported("aggregate over an empty input (NULL result)")
-    return aggs, states, outs, keys, uk, ng
+    return aggs, states, outs, keys, uk, ng, having_c
 
 
-def _aggregate(items, group, t: Table, dev, world, rank, werr=None) -> Table:
+def _aggregate(items, group, t: Table, dev, world, rank, werr=None, having=None) -> Table:
     err, local = werr, None
     if err is None:
         try:
-            local = _local_states(items, group, t, dev, world)
+            local = _local_states(items, group, t, dev, world, having)
         except Unsupported as e:
             err = e
     if world > 1:
@@ -658,7 +798,7 @@ def _aggregate(items, group, t: Table, dev, world, rank, werr=None) -> Table:
             raise Unsupported("some rank cannot evaluate the statement on the device: %s" % err)
     elif err is not None:
         raise err
-    aggs, states, outs, keys, uk, ng = local
+    aggs, states, outs, keys, uk, ng, having_c = local
     if world > 1:
         uk, states, _ = _merge_ranks(uk, states, dev, bool(keys))
         ng = uk.shape[0]
@@ -714,6 +854,11 @@ def _aggregate(items, group, t: Table, dev, world, rank, werr=None) -> Table:
         v = value(e)
         res[name] = v if isinstance(v, torch.Tensor) else torch.full((ng,), v, device=dev)
     out = Table(res, num_rows=ng)
+    if having_c is not None:  # the groups whose HAVING condition holds (evaluated on the merged states)
+        keep = _Eval(Table({}, num_rows=ng), ng, dev).boolean(value(having_c))
+        out = out.take(torch.nonzero(keep if isinstance(keep, torch.Tensor) else
+                                     torch.full((ng,), bool(keep), device=dev), as_tuple=True)[0])
+        ng = out.num_rows
     if world > 1:
         out = out.take(torch.arange(rank, ng, world, device=dev))
     return out

@@ -132,3 +132,70 @@ def test_null_ordering_lowest():
     desc = SQLTransformer().set_statement("SELECT j FROM __THIS__ ORDER BY j DESC").transform(t)[0].get_list("j")
     assert asc[:2] == [None, None] and asc[2:] == [3, 4, 5]
     assert desc[:3] == [5, 4, 3] and desc[3:] == [None, None]
+
+
+def _mixed():
+    return Table({"k": torch.tensor([2, 0, 1, 0, 2, 1], dtype=torch.int64),
+                  "x": torch.tensor([1.5, 9.0, -2.0, 4.0, 0.5, 3.0], dtype=torch.float64),
+                  "i": torch.tensor([3, 1, 2, 1, 3, 5], dtype=torch.int32)}, num_rows=6)
+
+
+@pytest.mark.parametrize("stmt,expected", [
+    ("SELECT x FROM __THIS__ ORDER BY x", [(-2.0,), (0.5,), (1.5,), (3.0,), (4.0,), (9.0,)]),
+    ("SELECT x FROM __THIS__ ORDER BY x DESC LIMIT 2", [(9.0,), (4.0,)]),
+    ("SELECT k, x FROM __THIS__ ORDER BY k DESC, x", [(2, 0.5), (2, 1.5), (1, -2.0), (1, 3.0), (0, 4.0), (0, 9.0)]),
+    ("SELECT k, x FROM __THIS__ ORDER BY 2 LIMIT 2 OFFSET 1", [(2, 0.5), (2, 1.5)]),
+    ("SELECT x AS v FROM __THIS__ ORDER BY i, v DESC", [(9.0,), (4.0,), (-2.0,), (1.5,), (0.5,), (3.0,)]),
+    ("SELECT k, SUM(i) AS s FROM __THIS__ GROUP BY k HAVING SUM(i) > 4 ORDER BY s DESC", [(1, 7), (2, 6)]),
+    ("SELECT k, COUNT(*) AS c FROM __THIS__ GROUP BY k HAVING k <> 1 ORDER BY k", [(0, 2), (2, 2)]),
+    ("SELECT DISTINCT k FROM __THIS__ ORDER BY k DESC", [(2,), (1,), (0,)]),
+    ("SELECT DISTINCT k, i FROM __THIS__ ORDER BY k, i", [(0, 1), (1, 2), (1, 5), (2, 3)]),
+])
+def test_order_limit_distinct_having_on_both_engines(stmt, expected):
+    """ORDER BY (names, positions, aliases, input columns not in the output; stable, multi-key),
+    LIMIT / OFFSET, DISTINCT and HAVING evaluate on the device (no host fallback) and agree with
+    the SQLite engine and the hand-written Flink results."""
+    t = _mixed()
+    dev, host = _both(stmt, t)
+    assert dev == expected and host == expected
+
+
+def test_order_by_nan_is_the_largest_double_on_the_device():
+    """Double.compare: NaN after +inf ascending, first descending (SQLite has no NaN: NULL)."""
+    t = Table({"x": torch.tensor([1.0, float("nan"), -math.inf, math.inf], dtype=torch.float64)}, num_rows=4)
+    asc = sql_device.evaluate("SELECT x FROM __THIS__ ORDER BY x", t).get_list("x")
+    desc = sql_device.evaluate("SELECT x FROM __THIS__ ORDER BY x DESC", t).get_list("x")
+    assert asc[:3] == [-math.inf, 1.0, math.inf] and asc[3] != asc[3]
+    assert desc[0] != desc[0] and desc[1:] == [math.inf, 1.0, -math.inf]
+
+
+@pytest.mark.parametrize("expr,expected", [
+    ("LOG(8.0)", math.log(8.0)), ("LOG(2, 8)", 3.0), ("LOG2(8.0)", 3.0), ("ATAN2(1.0, 1.0)", math.pi / 4),
+    ("COT(1.0)", 1 / math.tan(1.0)), ("SINH(1.0)", math.sinh(1.0)), ("COSH(1.0)", math.cosh(1.0)),
+    ("TANH(0.5)", math.tanh(0.5)), ("TRUNCATE(-2.77, 1)", -2.7), ("TRUNCATE(2.77)", 2.0), ("TRUNCATE(7)", 7),
+    ("TRUNCATE(123.456, -1)", 120.0), ("PI()", math.pi), ("E()", math.e), ("IF(1 < 2, 2.5, 3.5)", 2.5),
+    ("DEGREES(PI())", 180.0), ("LEAST(3, 1, 2)", 1), ("GREATEST(1.5, 2.5)", 2.5),
+])
+def test_more_scalar_functions_on_both_engines(expr, expected):
+    t = Table({"id": torch.arange(2, dtype=torch.int64)}, num_rows=2)
+    dev, host = _both("SELECT %s AS v FROM __THIS__" % expr, t)
+    for rows in (dev, host):
+        v = rows[0][0]
+        assert type(v) is type(expected) and math.isclose(v, expected, rel_tol=1e-12, abs_tol=1e-15), (expr, v)
+
+
+def test_math_outside_the_domain_is_nan_on_the_device():
+    """Java's Math: SQRT(-1), LN(-1), ASIN(2) are NaN (not an error) — literals and columns."""
+    t = Table({"x": torch.tensor([-1.0, 2.0], dtype=torch.float64)}, num_rows=2)
+    r = sql_device.evaluate("SELECT SQRT(-1.0) AS a, LN(x) AS b, ASIN(x) AS c FROM __THIS__", t).rows()
+    assert all(v != v for v in (r[0][0], r[0][1], r[1][2]))
+    assert math.isclose(r[1][1], math.log(2.0))
+    from flink_ml_amd.models.feature.sql_device import java_math
+
+    assert java_math(math.sqrt, -1.0) != java_math(math.sqrt, -1.0) and java_math(math.exp, 1e6) == math.inf
+
+
+def test_order_by_over_ranks_falls_back():
+    t = _mixed()
+    with pytest.raises(sql_device.Unsupported):
+        sql_device.evaluate("SELECT x FROM __THIS__ ORDER BY x", t, world=2, rank=0)
