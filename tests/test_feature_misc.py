@@ -130,19 +130,23 @@ def test_sql_device_matches_sqlite(stmt):
 
 def test_sql_device_passthrough_and_fallback():
     from flink_ml_amd.models.feature import sql_device
+    from flink_ml_amd.models.feature.misc import run_sql
 
     t = _rand_table(50)
     out = sql_device.evaluate("SELECT *, v1 + v2 AS s FROM __THIS__ WHERE id < 10", t)
     assert out.column_names == ["id", "v1", "v2", "vec", "s"] and out.num_rows == 10
     assert out.column("vec").shape == (10, 3)  # vector column carried by reference (gathered by WHERE)
     assert sql_device.evaluate("SELECT v1 * 2 FROM __THIS__", t).column_names == ["EXPR$0"]
-    for stmt in ("SELECT id FROM __THIS__ ORDER BY v1", "SELECT 'a' AS s FROM __THIS__",
-                 "SELECT id / (id - id) AS z FROM __THIS__", "SELECT DISTINCT v2 FROM __THIS__"):
+    for stmt in ("SELECT id FROM __THIS__ ORDER BY v1 NULLS FIRST", "SELECT 'a' AS s FROM __THIS__",
+                 "SELECT id / (id - id) AS z FROM __THIS__", "SELECT COUNT(DISTINCT v2) FROM __THIS__"):
         with pytest.raises(sql_device.Unsupported):
             sql_device.evaluate(stmt, t)
     # the transformer falls back to the host engine for those
-    got = SQLTransformer().set_statement("SELECT id FROM __THIS__ ORDER BY v1 LIMIT 3").transform(t)[0]
+    got = SQLTransformer().set_statement("SELECT id FROM __THIS__ ORDER BY v1 NULLS FIRST LIMIT 3").transform(t)[0]
     assert got.num_rows == 3
+    # ORDER BY / LIMIT / DISTINCT run on the device (round 5) and match the host engine
+    stmt = "SELECT id FROM __THIS__ ORDER BY v1 LIMIT 3"
+    assert sql_device.evaluate(stmt, t).rows() == run_sql(stmt, t).rows()
 
 
 def _spmd_sql_fallback(rank, world):
