@@ -27,6 +27,8 @@
 // replacing ~10 torch ops and their run-sized temporaries (repeat_interleave of the row ids and
 // slots, int64 sort indices, gather copies, the bucket-start array and its two slicing copies):
 // a whole fit that transposes its batches lazily pays for those allocations inside the fit.
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -314,6 +316,111 @@ __global__ __launch_bounds__(256) void csc_tile_store_kernel(const uint64_t* __r
   }
 }
 
+// ---------------------------- row-block × column-split cells (sparse forward) ----------------
+// glm.hip glm_csr_cell_fwd_kernel reads each batch as cells: rows [rb·RB, (rb+1)·RB) of the batch ×
+// columns [s·CS, (s+1)·CS), cell id rb·S + s. A cell's entries are stored column-sorted (its
+// coefficient gathers walk one column slice in order: lanes of a wave instruction share cache
+// lines), each packed as (column − s·CS) | pos << cb, pos = the entry's rank in the cell's
+// row-major order: the kernel writes each product into LDS slot pos and sums every row's slots
+// from the row offsets of the cell (no float atomics).
+//   cell_keys    wave per row: key = (cell << (RBB + cb)) | row-in-block << cb | (col − s·CS),
+//                payload = fp32 value bits / the entry's run index (fp64)
+//   sort A       stable on the (cell, row) bits: row-major cells (CSR order within a row)
+//   cell_bounds  first entry of every (cell, row) id = cell·RB + row: the row offsets
+//   cell_rekey   key = (cell << cb | col) << 32 | row-major position
+//   sort B       stable on the (cell, column) bits
+//   cell_store   entries (column, pos) and values in column order
+__global__ __launch_bounds__(256) void cell_keys_kernel(const long* __restrict__ indptr, const int* __restrict__ idx,
+                                                        const float* __restrict__ values, long r0, long r1, long B,
+                                                        long j0, int RBB, int S, int CS, int cb,
+                                                        uint64_t* __restrict__ keys, uint32_t* __restrict__ pay,
+                                                        int f64) {
+  const int lane = threadIdx.x & 63;
+  const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long nw = ((long)gridDim.x * blockDim.x) >> 6;
+  for (long r = r0 + wave; r < r1; r += nw) {
+    const long rel = r - r0;
+    const long rl = rel - (rel / B) * B;  // row within its batch
+    const uint64_t rb = (uint64_t)(rl >> RBB), rin = (uint64_t)(rl & ((1L << RBB) - 1));
+    const long s0 = indptr[r], s1 = indptr[r + 1];
+    for (long j = s0 + lane; j < s1; j += 64) {
+      const int c = idx[j];
+      const int sp = c / CS;
+      const uint64_t cell = rb * (uint64_t)S + (uint64_t)sp;
+      keys[j - j0] = (((cell << RBB) | rin) << cb) | (uint64_t)(c - sp * CS);
+      pay[j - j0] = f64 ? (uint32_t)(j - j0) : __float_as_uint(values[j]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void cell_rekey_kernel(const uint64_t* __restrict__ ka, long m, int RBB, int cb,
+                                                         uint64_t* __restrict__ kb) {
+  const uint64_t cm = (1ull << cb) - 1;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+    const uint64_t k = ka[i];
+    const uint64_t cell = k >> (RBB + cb);
+    kb[i] = (((cell << cb) | (k & cm)) << 32) | (uint64_t)i;
+  }
+}
+
+// sorted B keys → ent = column | pos << cb (pos: row-major rank inside the cell, from the row
+// offsets roff of the entry's batch), values from the payload
+template <typename V>
+__global__ __launch_bounds__(256) void cell_store_kernel(const uint64_t* __restrict__ keys,
+                                                         const uint32_t* __restrict__ pay, long m, long j0, RunStarts rs,
+                                                         int slots, long b0, const int* __restrict__ roff, int rstride,
+                                                         int RBB, int cb, const V* __restrict__ src,
+                                                         uint32_t* __restrict__ ent, V* __restrict__ val) {
+  const uint64_t cm = (1ull << cb) - 1;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+    const uint64_t k = keys[i];
+    const long pa = (long)(uint32_t)k;  // run-relative row-major position
+    int s = 0;
+    while (s + 1 < slots && rs.start[s + 1] <= pa) ++s;
+    const long cell = (long)(k >> (32 + cb));
+    const int first = roff[(b0 + s) * (long)rstride + (cell << RBB)];
+    const uint32_t pos = (uint32_t)(pa - rs.start[s] - first);
+    ent[j0 + i] = (uint32_t)((k >> 32) & cm) | (pos << cb);
+    if constexpr (sizeof(V) == 4)
+      val[j0 + i] = __uint_as_float(pay[i]);
+    else
+      val[j0 + i] = src[pay[i]];
+  }
+}
+
+// sorted keys of a run → off[(b0 + s)·cstride + c] = first entry of id c (key >> shift) of batch
+// b0 + s, relative to the batch's first entry; off[..+ ncell] = the batch's entry count. Position i
+// writes the ids (id(key[i−1]), id(key[i])] of the batch holding it; cell_tails_kernel writes the
+// ids after every batch's last key (empty batches: all of them) — each slot exactly once.
+__global__ __launch_bounds__(256) void cell_bounds_kernel(const uint64_t* __restrict__ keys, long m, int shift,
+                                                          RunStarts rs, int slots, long b0, int cstride,
+                                                          int* __restrict__ off) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  int s = 0;
+  while (s < slots && !(rs.start[s] <= i && i < rs.start[s + 1])) ++s;
+  if (s == slots) return;
+  const long bs = rs.start[s];
+  const int lo = i > bs ? (int)(keys[i - 1] >> shift) : -1;
+  const int hi = (int)(keys[i] >> shift);
+  int* o = off + (b0 + s) * (long)cstride;
+  for (int c = lo + 1; c <= hi; ++c) o[c] = (int)(i - bs);
+}
+
+__global__ __launch_bounds__(256) void cell_tails_kernel(const uint64_t* __restrict__ keys, int shift, RunStarts rs,
+                                                         int slots, int ncell, long b0, int cstride,
+                                                         int* __restrict__ off) {
+  const int p = blockIdx.y;
+  if (p >= slots) return;
+  const long bs = rs.start[p], be = rs.start[p + 1];
+  const int last = be > bs ? (int)(keys[be - 1] >> shift) : -1;
+  int* o = off + (b0 + p) * (long)cstride;
+  for (long c = (long)blockIdx.x * blockDim.x + threadIdx.x; c <= ncell; c += (long)gridDim.x * blockDim.x)
+    if (c > last) o[c] = (int)(be - bs);
+}
+
 inline unsigned grid_for(long work, long per_block, unsigned cap) {
   long g = (work + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -417,6 +524,57 @@ FMLX_API int fmlx_csc_tile_store(int f64, const uint64_t* keys, const uint32_t* 
   else
     hipLaunchKernelGGL(csc_tile_store_kernel<float>, g, dim3(256), 0, (hipStream_t)stream, keys, pay, m, j0, rb, pb,
                        (const float*)nullptr, erow, (float*)evals);
+  return (int)hipGetLastError();
+}
+
+// Cells of the run's batches (see cell_keys_kernel): keys uint64 [m], pay uint32 [m] (m = j1 − j0).
+FMLX_API int fmlx_cell_keys(int f64, const long* indptr, const int* idx, const float* values, long r0, long r1, long B,
+                            long j0, int RBB, int S, int CS, int cb, uint64_t* keys, uint32_t* pay, void* stream) {
+  if (r1 <= r0) return 0;
+  if (B <= 0 || RBB < 1 || S < 1 || CS < 1 || cb < 1 || cb + RBB > 32) return -1;
+  hipLaunchKernelGGL(cell_keys_kernel, dim3(grid_for(r1 - r0, 4, 1u << 16)), dim3(256), 0, (hipStream_t)stream,
+                     indptr, idx, values, r0, r1, B, j0, RBB, S, CS, cb, keys, pay, f64);
+  return (int)hipGetLastError();
+}
+
+FMLX_API int fmlx_cell_rekey(const uint64_t* ka, long m, int RBB, int cb, uint64_t* kb, void* stream) {
+  if (m <= 0) return 0;
+  if (m >= (1L << 32) || cb < 1 || cb + RBB > 32) return -1;
+  hipLaunchKernelGGL(cell_rekey_kernel, dim3(grid_for(m, 256, 1u << 16)), dim3(256), 0, (hipStream_t)stream, ka, m,
+                     RBB, cb, kb);
+  return (int)hipGetLastError();
+}
+
+// starts: HOST array of the run's batch starts relative to j0 (slots + 1 values)
+FMLX_API int fmlx_cell_store(int f64, const uint64_t* keys, const uint32_t* pay, long m, long j0, const long* starts,
+                             int slots, long b0, const int* roff, int rstride, int RBB, int cb, const void* src,
+                             uint32_t* ent, void* val, void* stream) {
+  if (m <= 0) return 0;
+  if ((f64 && src == nullptr) || slots <= 0 || slots > CP_MAXS || m >= (1L << 31)) return -1;
+  RunStarts rs{};
+  for (int s = 0; s <= slots; ++s) rs.start[s] = (int)starts[s];
+  const dim3 g(grid_for(m, 256, 1u << 16));
+  if (f64)
+    hipLaunchKernelGGL(cell_store_kernel<double>, g, dim3(256), 0, (hipStream_t)stream, keys, pay, m, j0, rs, slots,
+                       b0, roff, rstride, RBB, cb, (const double*)src, ent, (double*)val);
+  else
+    hipLaunchKernelGGL(cell_store_kernel<float>, g, dim3(256), 0, (hipStream_t)stream, keys, pay, m, j0, rs, slots, b0,
+                       roff, rstride, RBB, cb, (const float*)nullptr, ent, (float*)val);
+  return (int)hipGetLastError();
+}
+
+// starts: HOST array of the run's batch starts relative to j0 (slots + 1 values)
+FMLX_API int fmlx_cell_bounds(const uint64_t* keys, long m, int shift, const long* starts, int slots, int ncell,
+                              long b0, int cstride, int* off, void* stream) {
+  if (slots <= 0 || slots > CP_MAXS || m < 0 || m >= (1L << 31) || ncell + 1 > cstride) return -1;
+  RunStarts rs{};
+  for (int s = 0; s <= slots; ++s) rs.start[s] = (int)starts[s];
+  if (m > 0)
+    hipLaunchKernelGGL(cell_bounds_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, (hipStream_t)stream, keys,
+                       m, shift, rs, slots, b0, cstride, off);
+  const unsigned gx = (unsigned)std::min<long>(((long)ncell + 1 + 255) / 256, 1024);
+  hipLaunchKernelGGL(cell_tails_kernel, dim3(gx, slots), dim3(256), 0, (hipStream_t)stream, keys, shift, rs, slots,
+                     ncell, b0, cstride, off);
   return (int)hipGetLastError();
 }
 

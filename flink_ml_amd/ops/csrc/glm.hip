@@ -1359,6 +1359,140 @@ __global__ __launch_bounds__(256) void glm_csr_fwd_kernel(const long* __restrict
   }
 }
 
+// Forward over row-block × column-split cells (BatchCsc cells, csc_build.hip cell_keys … cell_store):
+// cell (rb, s) holds the batch's entries of rows [rb·2^CELL_RBB, …) with columns in [s·CS, (s+1)·CS),
+// stored column-sorted and packed (column − s·CS) | pos << cb, pos = the entry's rank in the cell's
+// row-major order; roff[cell·2^CELL_RBB + r] = first entry of row r of the cell. A block takes a
+// cell: its lanes gather coefficients in column order from one slice (consecutive lanes share
+// cache lines — the one-row-per-lane-group kernel gathers a random line per lane, ~40 µs per 6.4M,
+// profiles/r5/micro_gather_*), write each product into LDS slot pos (plain stores: LDS float
+// atomics cost ~27 µs more per round, profiles/r5/svc_cell_forward_ab.jsonl), then every row sums
+// its slots in order and the cell stores its row partials. The last of a row block's S cells to
+// arrive sums the S partials of every row in split order (deterministic), evaluates loss and
+// multiplier, and adds Σweight / Σloss into the slots.
+constexpr int CELL_THREADS = 1024;
+constexpr int CELL_RBB_MAX = 11;  // rows per row block: 2^rbb ≤ 2^11 (two rows per thread)
+constexpr int CELL_U = 8;
+
+template <typename A>
+__global__ __launch_bounds__(CELL_THREADS) void glm_csr_cell_fwd_kernel(
+    const long* __restrict__ indptr, const uint32_t* __restrict__ cent, const A* __restrict__ cval,
+    const int* __restrict__ roff, long rstride, int rbb, int S, int CS, int cb, const A* __restrict__ y,
+    const A* __restrict__ wt, const A* __restrict__ coef, long n, long B, int loss, const int* __restrict__ state,
+    A* __restrict__ mult, A* __restrict__ wl, A* __restrict__ partial, int* __restrict__ cnt) {
+  const int RB = 1 << rbb;
+  extern __shared__ __align__(16) unsigned char cell_lds[];
+  A* prod = reinterpret_cast<A*>(cell_lds);  // [the largest cell's entries]
+  __shared__ A red[2][CELL_THREADS / 64];
+  __shared__ int sflag;
+  int e;
+  if (!round_running(state, e)) return;
+  const long P = (n + B - 1) / B;
+  const long b = (long)(e % P);
+  const long start = b * B;
+  const long blen = (start + B < n ? start + B : n) - start;
+  const int nrb = (int)((blen + RB - 1) >> rbb);
+  const int c = blockIdx.x;
+  if (c >= nrb * S) return;  // (the grid covers the largest batch)
+  const int rb = c / S, sp = c - rb * S;
+  const int tid = threadIdx.x;
+  const long base = indptr[start];
+  const int* __restrict__ ro = roff + b * rstride + ((long)c << rbb);
+  const int k0 = ro[0], k1 = ro[RB];
+  const uint32_t* __restrict__ en = cent + base;
+  const A* __restrict__ ev = cval + base;
+  const A* __restrict__ cs = coef + (long)sp * CS;
+  const uint32_t cmask = (1u << cb) - 1;
+  uint32_t xx[CELL_U];
+  A vv[CELL_U];
+  if (k0 < k1) {  // (an empty cell may sit at the end of the array: nothing to load)
+#pragma unroll
+    for (int u = 0; u < CELL_U; ++u) {
+      const int k = k0 + tid + u * CELL_THREADS;
+      const int kk = k < k1 ? k : k0;
+      xx[u] = __builtin_nontemporal_load(en + kk);
+      vv[u] = __builtin_nontemporal_load(ev + kk);
+    }
+  }
+  for (int kb = k0 + tid; kb < k1; kb += CELL_U * CELL_THREADS) {
+    uint32_t nx[CELL_U];
+    A nv[CELL_U];
+    const int kn = kb + CELL_U * CELL_THREADS;
+    if (kn < k1) {
+#pragma unroll
+      for (int u = 0; u < CELL_U; ++u) {
+        const int k = kn + u * CELL_THREADS;
+        const int kk = k < k1 ? k : kn;
+        nx[u] = __builtin_nontemporal_load(en + kk);
+        nv[u] = __builtin_nontemporal_load(ev + kk);
+      }
+    }
+    // every gather first (lanes past the cell hold its first entry: valid addresses), then the
+    // slot stores — a gather per store would serialise CELL_U memory latencies per step
+    A pp[CELL_U];
+#pragma unroll
+    for (int u = 0; u < CELL_U; ++u) pp[u] = vv[u] * cs[xx[u] & cmask];
+#pragma unroll
+    for (int u = 0; u < CELL_U; ++u)
+      if (kb + u * CELL_THREADS < k1) prod[xx[u] >> cb] = pp[u];
+#pragma unroll
+    for (int u = 0; u < CELL_U; ++u) {
+      xx[u] = nx[u];
+      vv[u] = nv[u];
+    }
+  }
+  const long rb0 = (long)rb << rbb;
+  const int nr = blen - rb0 < RB ? (int)(blen - rb0) : RB;
+  constexpr int RQ = (1 << CELL_RBB_MAX) / CELL_THREADS;
+  int r0s[RQ], r1s[RQ];
+#pragma unroll
+  for (int q = 0; q < RQ; ++q) {  // (row offsets loaded before the barrier)
+    const int r = tid + q * CELL_THREADS;
+    r0s[q] = r < nr ? ro[r] - k0 : 0;
+    r1s[q] = r < nr ? ro[r + 1] - k0 : 0;
+  }
+  __syncthreads();
+  A* __restrict__ mine = partial + (long)c * RB;
+#pragma unroll
+  for (int q = 0; q < RQ; ++q) {
+    const int r = tid + q * CELL_THREADS;
+    A t = 0;
+    for (int j = r0s[q]; j < r1s[q]; ++j) t += prod[j];
+    if (r < nr) st_agent(mine + r, t);
+  }
+  if (!arrive_last(&cnt[rb], S, &sflag)) return;
+  if (tid == 0) st_agent(&cnt[rb], 0);  // every arrival of this launch is in: re-arm for the next
+  A ws = 0, ls = 0;
+  for (int r = tid; r < nr; r += CELL_THREADS) {
+    A dot = 0;
+    for (int q = 0; q < S; ++q) dot += ld_agent(partial + ((long)rb * S + q) * RB + r);
+    const long gr = start + rb0 + r;
+    const A ww = wt ? wt[gr] : (A)1;
+    A l, m;
+    loss_and_mult(loss, dot, y[gr], ww, l, m);
+    mult[rb0 + r] = m;
+    ws += ww;
+    ls += l;
+  }
+  ws = wave_sum(ws);
+  ls = wave_sum(ls);
+  if ((tid & 63) == 0) {
+    red[0][tid >> 6] = ws;
+    red[1][tid >> 6] = ls;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    A a0 = 0, a1 = 0;
+    for (int i = 0; i < CELL_THREADS / 64; ++i) {
+      a0 += red[0][i];
+      a1 += red[1][i];
+    }
+    A* slot = wl + ((long)(e & 1) * WL_SLOTS + (rb & (WL_SLOTS - 1))) * WL_STRIDE;
+    if (a0 != (A)0) atomicAdd(&slot[0], a0);
+    if (a1 != (A)0) atomicAdd(&slot[1], a1);
+  }
+}
+
 // Backward: a block owns 256 consecutive columns, whose batch entries are one contiguous CSC
 // range. The block walks that range coalesced (every thread loads independent entries: row id →
 // multiplier gather → product into LDS), then each thread adds its column's slice of the LDS
@@ -1573,12 +1707,14 @@ __global__ __launch_bounds__(TILE_THREADS) void glm_csc_tile_bwd_kernel(
     // 32 per thread: 71.0 vs 72.3 µs per round; 8 without the overlap: 71.8)
     uint32_t xx[TU];
     A vv[TU];
+    if (k0 < k1) {  // (an empty tile may sit at the end of the array: nothing to load)
 #pragma unroll
-    for (int u = 0; u < TU; ++u) {
-      const int k = k0 + tid + u * TILE_THREADS;
-      const int kk = k < k1 ? k : k0;
-      xx[u] = (uint32_t)__builtin_nontemporal_load(er + kk);
-      vv[u] = __builtin_nontemporal_load(ev + kk);
+      for (int u = 0; u < TU; ++u) {
+        const int k = k0 + tid + u * TILE_THREADS;
+        const int kk = k < k1 ? k : k0;
+        xx[u] = (uint32_t)__builtin_nontemporal_load(er + kk);
+        vv[u] = __builtin_nontemporal_load(ev + kk);
+      }
     }
     for (int kb = k0 + tid; kb < k1; kb += TU * TILE_THREADS) {
       uint32_t nx[TU];
@@ -2230,6 +2366,14 @@ struct CscTiles {
   const int2* tiles;  // [P][tstride] (start column, first entry) per tile (nullptr: untiled layout)
   const int* ntiles;  // int32 [P]
   int tstride, rb, EL, ET;  // EL: heavy-column threshold (entries)
+  // row-block × column-split cells of the forward (cent == nullptr: the one-row-per-group forward)
+  const uint32_t* cent;
+  const void* cval;
+  const int* roff;  // [P][rstride] first entry of every (cell, row): cell·2^CELL_RBB + row
+  int rstride, rbb, S, CS, cb, cells;  // cells: grid (cells of the largest batch); rows per block 2^rbb
+  int cmax;         // entries of the largest cell (its LDS slots)
+  void* partial;    // [cells][2^CELL_RBB] row partials
+  int* cnt;         // [row blocks] arrival tickets (zeroed once, re-armed by the finishers)
 };
 FMLX_API int fmlx_glm_wl_elems() { return 2 * WL_SLOTS * WL_STRIDE; }
 
@@ -2238,12 +2382,18 @@ static void launch_csc_round(const long* indptr, const int* idx, const A* val, c
                              long n, int d, long B, int loss, int* state, A* mult, A* wl, const int* colptr,
                              const int* erow, const A* eval, A* fb, int fuse, int max_iter, A tol, A lr, A reg, A en,
                              const CscTiles& ti, hipStream_t s) {
-  const long groups = B < n ? B : n;
-  long fb_blocks = (groups * G + 255) / 256;  // one row per lane group: the batch in one pass
-  if (fb_blocks > g_csc_fwd_cap) fb_blocks = g_csc_fwd_cap;
-  if (fb_blocks < 1) fb_blocks = 1;
-  hipLaunchKernelGGL((glm_csr_fwd_kernel<A, G>), dim3((int)fb_blocks), dim3(256), 0, s, indptr, idx, val, y, wt,
-                     (const A*)coef, n, B, loss, state, mult, wl);
+  if (ti.cent != nullptr) {
+    hipLaunchKernelGGL(glm_csr_cell_fwd_kernel<A>, dim3(ti.cells), dim3(CELL_THREADS), (size_t)ti.cmax * sizeof(A),
+                       s, indptr, ti.cent, (const A*)ti.cval, ti.roff, (long)ti.rstride, ti.rbb, ti.S, ti.CS, ti.cb, y, wt,
+                       (const A*)coef, n, B, loss, state, mult, wl, (A*)ti.partial, ti.cnt);
+  } else {
+    const long groups = B < n ? B : n;
+    long fb_blocks = (groups * G + 255) / 256;  // one row per lane group: the batch in one pass
+    if (fb_blocks > g_csc_fwd_cap) fb_blocks = g_csc_fwd_cap;
+    if (fb_blocks < 1) fb_blocks = 1;
+    hipLaunchKernelGGL((glm_csr_fwd_kernel<A, G>), dim3((int)fb_blocks), dim3(256), 0, s, indptr, idx, val, y, wt,
+                       (const A*)coef, n, B, loss, state, mult, wl);
+  }
   const int weighted = wt != nullptr;
   if (ti.tiles != nullptr) {
     const size_t lds = (size_t)ti.ET * sizeof(A);
@@ -2302,10 +2452,21 @@ FMLX_API int fmlx_glm_csc_round(int acc_f64, int G, const long* indptr, const in
                                 void* mult, void* wl, const int* colptr, const int* erow, const void* eval, void* fb,
                                 int fuse, int max_iter, double tol, double lr, double reg, double en,
                                 const int* tiles, const int* ntiles, int tstride, int rb, int EL, int ET,
-                                void* stream) {
+                                const uint32_t* cent, const void* cval, const int* roff, int rstride, int rbb, int S,
+                                int CS, int cb, int cells, int cmax, void* partial, int* ccnt, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (n <= 0 || B <= 0) return -2;
-  const CscTiles ti{reinterpret_cast<const int2*>(tiles), ntiles, tstride, rb, EL, ET};
+  const CscTiles ti{reinterpret_cast<const int2*>(tiles), ntiles, tstride, rb, EL, ET, cent, cval, roff, rstride,
+                    rbb, S, CS, cb, cells, cmax, partial, ccnt};
+  if (cent != nullptr) {
+    // (cell ids, packed entries and the row blocks of the largest batch: host-checked sizes)
+    const long lds = (long)cmax * (acc_f64 ? 8 : 4);
+    if (cval == nullptr || roff == nullptr || partial == nullptr || ccnt == nullptr || S < 1 || CS < 1 || cb < 1 ||
+        cb >= 32 || rbb < 1 || rbb > CELL_RBB_MAX || cells < 1 || (long)rstride < ((long)cells << rbb) + 1 ||
+        (long)CS * S < d || cmax < 0 ||
+        cmax > (int)(1u << (32 - cb)) || lds > 150 * 1024)
+      return -5;
+  }
   if (tiles != nullptr) {
     const size_t esz = acc_f64 ? 8 : 4;
     // the packed erow (row | slot << rb) and the LDS slot array of a light tile (< ET entries)

@@ -389,6 +389,13 @@ TILE_HEAVY_DIV = int(os.environ.get("FMLX_CSC_TILE_HEAVY_DIV", "8"))  # heavy co
 # as TILE_MIN_VISITS rounds save: ~0.15 ms per 6.4M-entry batch vs ~13 µs per round, svc shape)
 TILE_MIN_VISITS = int(os.environ.get("FMLX_CSC_TILE_MIN_VISITS", "16"))
 TILE_SPREAD = os.environ.get("FMLX_CSC_TILE_SPREAD", "1") == "1"  # tile size from the batch and CU count
+# the forward over row-block × column-split cells (glm.hip glm_csr_cell_fwd_kernel): float atomics
+# in LDS, so off under FMLX_DETERMINISTIC=1 (the one-row-per-lane-group forward is bit-stable)
+CELLS = os.environ.get("FMLX_CSR_CELLS", "1") == "1"
+CELL_RBB_SET = "FMLX_CSR_CELL_RBB" in os.environ  # rows per row block 2^this ≤ 2^11 (unset: 10 or 11)
+CELL_RBB = int(os.environ.get("FMLX_CSR_CELL_RBB", "10"))
+CELL_SPLITS = int(os.environ.get("FMLX_CSR_CELL_SPLITS", "0"))  # column slices per row block (0: auto)
+CELL_LDS_MAX = 128 * 1024  # LDS slots of the largest cell (bytes; larger: the row-group forward)
 
 
 def csc_tile_entries(B: int, f64: bool) -> int:
@@ -456,6 +463,49 @@ class BatchCsc:
         else:
             self.tstride = 0
         self.tiles = self.ntiles = None
+        # forward cells: entries of batch rows [rb·2^CELL_RBB, …) × columns [s·CS, (s+1)·CS),
+        # column-sorted per cell, packed (column − s·CS) | row-major rank << cb; roff: first entry
+        # of every (cell, row); cmax: entries of the largest built cell (the kernel's LDS slots)
+        self.cells = self.cmax = 0
+        self.rbb = max(1, min(11, CELL_RBB))  # (_pick_cells)
+        self.cent = self.cval = self.roff = self.cpart = self.ccnt = None
+        if CELLS and not DETERMINISTIC and values.device.type == "cuda" and self.P and d > 0:
+            self._pick_cells(values, bounds, n, d, B)
+        self.rstride = (self.cells << self.rbb) + 1
+
+    def _pick_cells(self, values, bounds, n: int, d: int, B: int) -> None:
+        """Row-block size 2^rbb and column splits S of the forward cells. About two 1024-thread
+        cells per CU, all in one wave (a third cell on some CUs costs more than it spreads: 686
+        cells 71.8 µs vs 490 cells 62.4 µs per round; 1024-row blocks beat 2048 at the same
+        count, 62.7 vs 64.3 — profiles/r5/svc_cell_forward_ab.jsonl), with the average cell 20 %
+        under its rank bits (2^(32 − column bits)) and the LDS; denser rows take more splits."""
+        cus = torch.cuda.get_device_properties(values.device).multi_processor_count
+        avg_row = bounds[-1] / max(1, n)
+        es = values.element_size()
+        rows = min(B, n)
+        fallback = None
+        for rbb in ((CELL_RBB,) if CELL_RBB_SET else (10, 11)):
+            nrb = -(-rows // (1 << rbb))
+            S = CELL_SPLITS if CELL_SPLITS > 0 else max(1, 2 * cus // nrb)
+            while True:
+                S = max(1, min(S, 64, d))
+                CS = -(-d // S)
+                cb = max(1, int(CS - 1).bit_length())
+                cell = avg_row * min(rows, 1 << rbb) / S
+                fits = cb + rbb <= 32 and cell * 1.2 <= min(1 << (32 - cb), CELL_LDS_MAX // es)
+                if fits or CELL_SPLITS > 0 or S >= min(64, d):
+                    break
+                S += 1
+            cellbits = max(1, int(nrb * S - 1).bit_length())
+            if not (cb + rbb <= 32 and cb + cellbits <= 32 and nrb * S < 2 ** 20):
+                continue
+            cand = (rbb, S, CS, cb, nrb * S)
+            if fits and (CELL_SPLITS > 0 or S == max(1, min(2 * cus // nrb, 64, d))):
+                fallback = cand
+                break
+            fallback = fallback or cand
+        if fallback is not None:
+            self.rbb, self.S, self.CS, self.cb, self.cells = fallback
 
     @staticmethod
     def pick_group(avg_nnz: float) -> int:
@@ -473,20 +523,24 @@ class BatchCsc:
         P = (n + B - 1) // B
         nnz, bounds = _batch_bounds(indptr, n, B)
         extra = P * (d + 1) * 4 + nnz * (4 + values.element_size())
+        if CELLS and values.device.type == "cuda":
+            extra += nnz * (4 + values.element_size())  # (the forward's cell copy)
         if extra > CSC_MAX_BYTES:
             return None
         if max(bounds[i + 1] - bounds[i] for i in range(P)) >= 2 ** 31:
             return None
         csc = BatchCsc(BatchCsc.pick_group(nnz / max(n, 1)), bounds, indptr, indices, values, n, d, B,
                        P if max_rounds is None else int(max_rounds))
-        if csc.ET and max_rounds is not None and max_rounds < TILE_MIN_VISITS * P:
-            csc.untiled()  # too few visits per batch to pay back the tiling sort
+        if (csc.ET or csc.cells) and max_rounds is not None and max_rounds < TILE_MIN_VISITS * P:
+            csc.untiled()  # too few visits per batch to pay back the tiling / cell sorts
         return csc
 
     def untiled(self) -> None:
-        """Keeps the plain column-major layout (before any batch is built)."""
+        """Keeps the plain column-major layout and the row-group forward (before any batch is
+        built)."""
         assert self.cap == 0
         self.ET = self.EL = self.EB = self.tstride = 0
+        self.cells, self.rstride = 0, 1
 
     @staticmethod
     def build(indptr, indices, values, n: int, d: int, B: int):
@@ -511,6 +565,15 @@ class BatchCsc:
         if self.ET:
             tiles = torch.empty((cap, self.tstride, 2), dtype=torch.int32, device=dev)
             ntiles = torch.empty(cap, dtype=torch.int32, device=dev)
+        cent = cval = roff = None
+        if self.cells:
+            cent = torch.empty(max(ne, 1), dtype=torch.int32, device=dev)
+            cval = torch.empty(max(ne, 1), dtype=values.dtype, device=dev)
+            roff = torch.empty((cap, self.rstride), dtype=torch.int32, device=dev)
+            if self.cpart is None:
+                acc = torch.float64 if values.dtype == torch.float64 else torch.float32
+                self.cpart = torch.empty(self.cells << self.rbb, dtype=acc, device=dev)
+                self.ccnt = torch.zeros(self.cells // self.S, dtype=torch.int32, device=dev)
         if self.cap:
             old = self.bounds[self.cap]
             colptr[:self.cap] = self.colptr
@@ -519,9 +582,14 @@ class BatchCsc:
             if tiles is not None:
                 tiles[:self.cap] = self.tiles
                 ntiles[:self.cap] = self.ntiles
+            if cent is not None:
+                cent[:old] = self.cent[:old]
+                cval[:old] = self.cval[:old]
+                roff[:self.cap] = self.roff
             self.version += 1
         self.colptr, self.erow, self.evals, self.cap = colptr, erow, evals, cap
         self.tiles, self.ntiles = tiles, ntiles
+        self.cent, self.cval, self.roff = cent, cval, roff
 
     def ensure(self, batches) -> None:
         """Transposes the listed batches that are not yet (idempotent; never inside a capture).
@@ -557,6 +625,8 @@ class BatchCsc:
                 self._transpose_native(b0, len(run), r0, r1, j0, j1)
                 if self.ET:
                     self._tile(b0, len(run), j0, j1)
+                if self.cells:
+                    self._cells(b0, len(run), r0, r1, j0, j1)
             else:
                 self._transpose_torch(b0, len(run), r0, r1, j0, j1)
 
@@ -588,6 +658,54 @@ class BatchCsc:
         src = self.evals[j0:j1].clone() if f64 else None
         native.call("fmlx_csc_tile_store", f64, native.ptr(keys), native.ptr(pay), m, j0, self.rb, self.pb,
                     native.ptr(src), native.ptr(self.erow), native.ptr(self.evals), stream)
+
+    def _cells(self, b0, slots, r0, r1, j0, j1) -> None:
+        """The run's batches as forward cells (csc_build.hip): keys in row-major cell order, a
+        stable radix sort on the (cell, row) bits, the row offsets, a re-key to (cell, column) with
+        the row-major position riding along, a second stable sort, and the packed entries. Turns
+        the cells off (the row-group forward takes over) when a cell outgrows its rank bits or the
+        LDS."""
+        import numpy as np
+
+        from . import sorting
+
+        indptr, indices, values = self._src
+        dev = values.device
+        m = j1 - j0
+        f64 = int(values.dtype == torch.float64)
+        stream = native.stream_ptr(dev)
+        cellbits = max(1, int(self.cells - 1).bit_length())
+        keys = torch.empty(m, dtype=sorting.U64, device=dev)
+        pay = torch.empty(m, dtype=torch.int32, device=dev)
+        native.call("fmlx_cell_keys", f64, native.ptr(indptr), native.ptr(indices), native.ptr(values), r0, r1, self.B,
+                    j0, self.rbb, self.S, self.CS, self.cb, native.ptr(keys), native.ptr(pay), stream)
+        seg = [self.bounds[b0 + s] - j0 for s in range(slots + 1)]
+        starts = np.ascontiguousarray(np.asarray(seg, dtype=np.int64))
+        keys, pay = sorting.sort_u64(keys, pay, seg, self.cb, self.cb + self.rbb + cellbits)
+        native.call("fmlx_cell_bounds", native.ptr(keys), m, self.cb, starts.ctypes.data, slots,
+                    self.cells << self.rbb, b0, self.rstride, native.ptr(self.roff), stream)
+        kb = torch.empty_like(keys)
+        native.call("fmlx_cell_rekey", native.ptr(keys), m, self.rbb, self.cb, native.ptr(kb), stream)
+        del keys
+        kb, pay = sorting.sort_u64(kb, pay, seg, 32, 32 + self.cb + cellbits)
+        src = values[j0:j1] if f64 else None
+        native.call("fmlx_cell_store", f64, native.ptr(kb), native.ptr(pay), m, j0, starts.ctypes.data, slots, b0,
+                    native.ptr(self.roff), self.rstride, self.rbb, self.cb, native.ptr(src), native.ptr(self.cent),
+                    native.ptr(self.cval), stream)
+        # the largest cell of the run (one host read per build run)
+        cs = self.roff[b0:b0 + slots, :self.rstride - 1:1 << self.rbb]
+        nxt = torch.cat([cs[:, 1:], self.roff[b0:b0 + slots, -1:]], 1)
+        big = int((nxt - cs).max()) if m else 0
+        es = values.element_size()
+        if big > (1 << (32 - self.cb)) or big * es > CELL_LDS_MAX:
+            self._cells_off()
+            return
+        self.cmax = max(self.cmax, big)
+
+    def _cells_off(self) -> None:
+        self.cells, self.rstride, self.cmax = 0, 1, 0
+        self.cent = self.cval = self.roff = self.cpart = self.ccnt = None
+        self.version += 1  # (captured rounds must be re-captured without the cells)
 
     def _transpose_native(self, b0, slots, r0, r1, j0, j1) -> None:
         import numpy as np
@@ -706,7 +824,9 @@ def csc_round(csc: BatchCsc, indptr, idx, val, y, wt, coef, n, d, B, loss, state
                 native.ptr(val), native.ptr(y), native.ptr(wt), native.ptr(coef), n, d, B, loss, native.ptr(state),
                 native.ptr(mult), native.ptr(wl), native.ptr(csc.colptr), native.ptr(csc.erow), native.ptr(csc.evals),
                 native.ptr(fb), int(fuse), max_iter, tol, lr, reg, en, native.ptr(csc.tiles), native.ptr(csc.ntiles),
-                csc.tstride, csc.rb, csc.EL, csc.ET, native.stream_ptr(val.device))
+                csc.tstride, csc.rb, csc.EL, csc.ET, native.ptr(csc.cent), native.ptr(csc.cval), native.ptr(csc.roff),
+                csc.rstride, csc.rbb, getattr(csc, "S", 0), getattr(csc, "CS", 0), getattr(csc, "cb", 0), csc.cells, csc.cmax,
+                native.ptr(csc.cpart), native.ptr(csc.ccnt), native.stream_ptr(val.device))
 
 
 # ---------------------------------------------------------------------------------------------

@@ -83,7 +83,8 @@ _KERNEL_SIGS = {
     "fmlx_glm_csc_round": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int,
                            c_long, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                            c_int, c_double, c_double, c_double, c_double, c_void_p, c_void_p, c_int, c_int, c_int,
-                           c_int, c_void_p],
+                           c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                           c_void_p, c_void_p, c_void_p],
     # sort.hip
     "fmlx_sorted_bounds": [c_void_p, c_long, c_int, c_void_p, c_void_p],
     "fmlx_seg_sort_scratch": ([c_void_p, c_int, c_int, c_int], c_long),
@@ -107,6 +108,12 @@ _KERNEL_SIGS = {
                            c_void_p, c_long, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "fmlx_csc_tile_store": [c_int, c_void_p, c_void_p, c_long, c_long, c_int, c_int, c_void_p, c_void_p, c_void_p,
                             c_void_p],
+    "fmlx_cell_keys": [c_int, c_void_p, c_void_p, c_void_p, c_long, c_long, c_long, c_long, c_int, c_int, c_int, c_int,
+                       c_void_p, c_void_p, c_void_p],
+    "fmlx_cell_rekey": [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p],
+    "fmlx_cell_store": [c_int, c_void_p, c_void_p, c_long, c_long, c_void_p, c_int, c_long, c_void_p, c_int, c_int,
+                        c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "fmlx_cell_bounds": [c_void_p, c_long, c_int, c_void_p, c_int, c_int, c_long, c_int, c_void_p, c_void_p],
     # blas.hip set-up helpers
     "fmlx_fill32": [c_void_p, c_long, ctypes.c_uint, c_void_p],
     "fmlx_csr_batch_bounds": [c_void_p, c_long, c_long, c_long, c_void_p, c_void_p],

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""A/B of the sparse SVC round's backward layout (untiled / row-sorted column tiles of ET entries,
-FMLX_CSC_TILE) and backward grid cap at the svc_sparse
+"""A/B of the sparse SVC round's layouts — backward: untiled / row-sorted column tiles of ET
+entries (FMLX_CSC_TILE); forward: row-group kernel / row-block × column-split cells with S splits
+(FMLX_CSR_CELLS, FMLX_CSR_CELL_SPLITS) — at the svc_sparse
 shard shape (scale 0.125: 6.25M x 1M, 64 nnz/row, batch 100k): steady
 rounds of a warmed trainer, interleaved repeats. One JSON line per (tile, bwd_cap, repeat). (Round 5 also measured a forward taking 2/4/8 rows per
 lane group: 0.0943-0.0977 ms vs 0.0899 for one row; removed.)"""
@@ -38,20 +39,29 @@ def main():
     from flink_ml_amd.ops import glm as gk
 
     trainers = {}
-    for tile, hdiv, spread in ((0, 8, 0), (32768, 8, 0), (32768, 8, 1), (32768, 16, 1)):
+    cfgs = [(0, 8, 0, 0, 11), (32768, 8, 1, 0, 11), (32768, 8, 1, -1, 0), (32768, 8, 1, 10, 11),
+            (32768, 8, 1, 4, 10), (32768, 8, 1, 6, 10)]
+    if len(sys.argv) > 1 and sys.argv[1] == "--layouts":  # (round-5 layout sweep)
+        cfgs = [(0, 8, 0, 0, 11), (32768, 8, 0, 0, 11), (32768, 8, 1, 0, 11), (32768, 16, 1, 0, 11)]
+    if len(sys.argv) > 2 and sys.argv[1] == "--splits":  # e.g. --splits 1 (one config: per-kernel profiles)
+        cfgs = [(32768, 8, 1, int(v), 11) for v in sys.argv[2].split(",")]
+    for tile, hdiv, spread, splits, rbb in cfgs:
         os.environ["FMLX_CSC_TILE"] = str(tile)
         gk.TILE_HEAVY_DIV = hdiv
         gk.TILE_SPREAD = bool(spread)
+        gk.CELLS = splits != 0  # the cell forward with this many column splits (0: row-group forward)
+        gk.CELL_SPLITS = max(0, splits)  # (-1: the automatic choice)
+        gk.CELL_RBB, gk.CELL_RBB_SET = (rbb or 10), rbb > 0  # (0: the automatic choice)
         tr = DeviceGlmTrainer(SGD(max_iter=10 ** 8, learning_rate=0.1, global_batch_size=100_000, tol=0.0),
                               np.zeros(dim), X, y, None, "hinge", use_graph=False)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         tr.csc.ensure(range(tr.csc.P))
         torch.cuda.synchronize()
-        print(json.dumps({"tile": tile, "heavy_div": hdiv, "spread": spread, "EB": tr.csc.EB,
+        print(json.dumps({"tile": tile, "heavy_div": hdiv, "spread": spread, "splits": splits, "S": getattr(tr.csc, "S", 0), "rbb": tr.csc.rbb, "cells": tr.csc.cells, "cmax": tr.csc.cmax, "EB": tr.csc.EB,
                           "tiles_max": int(tr.csc.ntiles.max()) if tr.csc.ET else 0,
                           "build_ms": round((time.perf_counter() - t0) * 1e3, 1), "batches": tr.csc.P}), flush=True)
-        trainers[(tile, hdiv, spread)] = tr
+        trainers[(tile, hdiv, spread, splits, rbb)] = tr
     cases = [(k, 0) for k in trainers]
     for rep in range(2):
         for key, cap in cases:
@@ -63,7 +73,7 @@ def main():
             tr.run_rounds(200)
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) / 200 * 1e3
-            print(json.dumps({"tile": key[0], "heavy_div": key[1], "spread": key[2], "bwd_cap": cap, "rep": rep,
+            print(json.dumps({"tile": key[0], "heavy_div": key[1], "spread": key[2], "splits": key[3], "rbb": key[4], "rep": rep,
                               "ms_per_round": round(ms, 4)}), flush=True)
     lib.fmlx_glm_set_csc_tuning(0, 0)
 

@@ -274,26 +274,100 @@ def test_batch_csc_row_sorted_tiles(vdtype, tile, d, B, monkeypatch):
         assert heavy >= csc.P - 1  # column 0 in every full batch (the last holds 13 rows)
 
 
+@pytest.mark.parametrize("vdtype,d,B,S,rbb", [
+    (torch.float32, 3_001, 1_000, 8, 11), (torch.float64, 3_001, 5_000, 8, 11),  # 3 row blocks (last partial)
+    (torch.float32, 1_000_000, 4_500, 8, 11), (torch.float32, 5, 2_100, 8, 11),  # wide; fewer columns than S
+    (torch.float32, 3_001, 5_000, 1, 11), (torch.float32, 3_001, 5_000, 5, 10),
+])
+def test_batch_csr_forward_cells(vdtype, d, B, S, rbb, monkeypatch):
+    """The forward's cell layout (csc_build.hip cell_keys / sorts / cell_bounds / cell_rekey /
+    cell_store): every batch's entries as row-block × column-split cells, each cell's entries
+    column-sorted (rows ascending within a column), packed (column − s·CS) | row-major rank << cb,
+    with per-(cell, row) offsets — the same (row, column, value) set as the CSR batch, also after
+    storage growth; ``cmax`` is the largest cell."""
+    _need_gpu()
+    from flink_ml_amd.ops import glm as gk
+
+    monkeypatch.setattr(gk, "TILE_MIN_VISITS", 0)
+    monkeypatch.setattr(gk, "CELLS", True)
+    monkeypatch.setattr(gk, "CELL_SPLITS", S)
+    monkeypatch.setattr(gk, "CELL_RBB", rbb)
+    monkeypatch.setattr(gk, "CELL_RBB_SET", True)
+    g = torch.Generator().manual_seed(5)
+    n = 12_345
+    lens = torch.randint(0, 12, (n,), generator=g)
+    lens[B:2 * B] = 0  # an empty batch
+    # rows with unsorted column lists too (CSR order inside a row is kept, not assumed sorted)
+    rows = [torch.randint(0, d, (4 * k + 4,), generator=g).unique()[:k] for k in lens.tolist()]
+    rows = [r[torch.randperm(len(r), generator=g)] if i % 3 == 0 else r for i, r in enumerate(rows)]
+    idx = torch.cat(rows).to(torch.int32)
+    indptr = torch.zeros(n + 1, dtype=torch.int64)
+    indptr[1:] = torch.cumsum(torch.tensor([len(r) for r in rows]), 0)
+    vals = torch.rand(int(indptr[-1]), generator=g, dtype=torch.float64).to(vdtype)
+    csc = gk.BatchCsc.alloc(indptr.cuda(), idx.cuda(), vals.cuda(), n, d, B, max_rounds=2)
+    if gk.DETERMINISTIC:
+        assert csc.cells == 0
+        return
+    S_ = min(S, d)
+    RB = 1 << rbb
+    assert csc.cells == -(-min(B, n) // RB) * S_ and csc.S == S_ and csc.rbb == rbb
+    csc.ensure([0, 1])
+    csc.ensure(range(csc.P))
+    ent = csc.cent.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+    cv = csc.cval.cpu().numpy()
+    roff = csc.roff.cpu().numpy().astype(np.int64)
+    ip = indptr.numpy()
+    big = 0
+    for b in range(csc.P):
+        r0, r1 = b * B, min(n, (b + 1) * B)
+        j0, j1 = int(ip[r0]), int(ip[r1])
+        nrb = -(-(r1 - r0) // RB)
+        o = roff[b]
+        assert o[0] == 0 and np.all(np.diff(o) >= 0) and np.all(o[nrb * S_ * RB:] == j1 - j0)
+        got = []
+        for c in range(nrb * S_):
+            rb, sp = divmod(c, S_)
+            k0, k1 = o[c * RB], o[(c + 1) * RB]
+            big = max(big, k1 - k0)
+            x = ent[j0 + k0:j0 + k1]
+            col = sp * csc.CS + (x & ((1 << csc.cb) - 1))
+            pos = x >> csc.cb
+            assert sorted(pos.tolist()) == list(range(k1 - k0)), "row-major ranks: a permutation"
+            assert np.all(np.diff(col * (1 << 32) + pos) > 0), "column-sorted, rows ascending inside a column"
+            rowof = np.repeat(np.arange(RB), np.diff(o[c * RB:(c + 1) * RB + 1]))  # row of each rank
+            row = rb * RB + rowof[pos]
+            assert np.all(col < min(d, (sp + 1) * csc.CS)) and np.all(row < r1 - r0)
+            got += list(zip(row.tolist(), col.tolist(), cv[j0 + k0:j0 + k1].tolist()))
+        rr = np.repeat(np.arange(r1 - r0), np.diff(ip[r0:r1 + 1]))
+        want = list(zip(rr.tolist(), idx[j0:j1].tolist(), vals[j0:j1].numpy().tolist()))
+        assert sorted(got) == sorted(want), b
+    assert csc.cmax == big
+
+
 @pytest.mark.parametrize("tile", [0, 64, 2048])
 @pytest.mark.parametrize("vdtype", [torch.float32, torch.float64])
-def test_sparse_sgd_tiled_backward_matches_host(tile, vdtype, monkeypatch):
+@pytest.mark.parametrize("cells", [False, True])
+def test_sparse_sgd_tiled_backward_matches_host(tile, vdtype, cells, monkeypatch):
     """Whole fits through the tiled backward (light and heavy tiles; the feedback path is the
-    two-rank test above) against the fp64 host trainer, weighted and not."""
+    two-rank test above) and the cell forward or the row-group forward, against the fp64 host
+    trainer, weighted and not."""
     _need_gpu()
     from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
 
-    n, d = 2100, 800
+    n, d = 5100, 800  # 700-row batches in the forward's 2048-row blocks: partial last blocks
     indptr, idx, vals, dense, y, w = _csr(n, d, 21, max_nnz=60, dtype=vdtype)
     from flink_ml_amd.ops import glm as gk
 
     monkeypatch.setenv("FMLX_CSC_TILE", str(tile))
     monkeypatch.setattr(gk, "TILE_MIN_VISITS", 0)
+    monkeypatch.setattr(gk, "CELLS", cells)
     for wt in (None, w):
-        sgd = SGD(max_iter=9, learning_rate=0.2, global_batch_size=700, tol=1e-9, reg=0.05, elastic_net=0.4)
+        sgd = SGD(max_iter=9, learning_rate=0.2, global_batch_size=2500, tol=1e-9, reg=0.05, elastic_net=0.4)
         ref = TorchGlmTrainer(sgd, np.zeros(d), dense, y, wt, "hinge").fit()
         tr = DeviceGlmTrainer(sgd, np.zeros(d), _sparse_col(indptr, idx, vals, d, "cuda"), y.cuda(),
                               None if wt is None else wt.cuda(), "hinge")
         assert tr.csc is not None and tr.csc.ET == tile
+        assert (tr.csc.cells > 0) == (cells and not gk.DETERMINISTIC)
         got = tr.fit()
         tol = 1e-10 if vdtype == torch.float64 else 1e-5
         assert np.abs(got - ref).max() <= tol * max(1.0, np.abs(ref).max()), (tile, np.abs(got - ref).max())
