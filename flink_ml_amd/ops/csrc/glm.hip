@@ -1379,7 +1379,7 @@ __global__ __launch_bounds__(CELL_THREADS) void glm_csr_cell_fwd_kernel(
     const long* __restrict__ indptr, const uint32_t* __restrict__ cent, const A* __restrict__ cval,
     const int* __restrict__ roff, long rstride, int rbb, int S, int CS, int cb, const A* __restrict__ y,
     const A* __restrict__ wt, const A* __restrict__ coef, long n, long B, int loss, const int* __restrict__ state,
-    A* __restrict__ mult, A* __restrict__ wl, A* __restrict__ partial, int* __restrict__ cnt) {
+    A* __restrict__ mult, A* __restrict__ wl, A* __restrict__ partial, int* __restrict__ cnt, int xcd) {
   const int RB = 1 << rbb;
   extern __shared__ __align__(16) unsigned char cell_lds[];
   A* prod = reinterpret_cast<A*>(cell_lds);  // [the largest cell's entries]
@@ -1392,9 +1392,22 @@ __global__ __launch_bounds__(CELL_THREADS) void glm_csr_cell_fwd_kernel(
   const long start = b * B;
   const long blen = (start + B < n ? start + B : n) - start;
   const int nrb = (int)((blen + RB - 1) >> rbb);
-  const int c = blockIdx.x;
-  if (c >= nrb * S) return;  // (the grid covers the largest batch)
-  const int rb = c / S, sp = c - rb * S;
+  const int ncell = nrb * S;
+  int rb, sp;
+  if (xcd) {
+    // XCD-aware order: block b runs on XCD b mod 8 (round-robin dispatch); give XCD x the cells
+    // of a contiguous split-major range, so its L2 holds the coefficient slices of ≤ 2 splits
+    const int per = (ncell + 7) >> 3;
+    const int g = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (g >= ncell) return;
+    sp = g / nrb;
+    rb = g - sp * nrb;
+  } else {
+    if ((int)blockIdx.x >= ncell) return;  // (the grid covers the largest batch)
+    rb = blockIdx.x / S;
+    sp = blockIdx.x - rb * S;
+  }
+  const int c = rb * S + sp;
   const int tid = threadIdx.x;
   const long base = indptr[start];
   const int* __restrict__ ro = roff + b * rstride + ((long)c << rbb);
@@ -2362,6 +2375,9 @@ FMLX_API void fmlx_glm_set_csc_tuning(int fwd_cap, int bwd_cap) {
 }
 
 // tiled backward: the column tiles of the batches (BatchCsc.tiles) and the packing of erow
+// forward cells in XCD-aware order (default; fmlx_glm_set_cell_xcd(0): launch order) — 64.0 → 62.1 µs
+// per SVC round, profiles/r5/svc_cell_forward_ab.jsonl
+static int g_cell_xcd = 1;
 struct CscTiles {
   const int2* tiles;  // [P][tstride] (start column, first entry) per tile (nullptr: untiled layout)
   const int* ntiles;  // int32 [P]
@@ -2385,7 +2401,7 @@ static void launch_csc_round(const long* indptr, const int* idx, const A* val, c
   if (ti.cent != nullptr) {
     hipLaunchKernelGGL(glm_csr_cell_fwd_kernel<A>, dim3(ti.cells), dim3(CELL_THREADS), (size_t)ti.cmax * sizeof(A),
                        s, indptr, ti.cent, (const A*)ti.cval, ti.roff, (long)ti.rstride, ti.rbb, ti.S, ti.CS, ti.cb, y, wt,
-                       (const A*)coef, n, B, loss, state, mult, wl, (A*)ti.partial, ti.cnt);
+                       (const A*)coef, n, B, loss, state, mult, wl, (A*)ti.partial, ti.cnt, g_cell_xcd);
   } else {
     const long groups = B < n ? B : n;
     long fb_blocks = (groups * G + 255) / 256;  // one row per lane group: the batch in one pass
@@ -2447,6 +2463,8 @@ static int dispatch_csc_round(int G, const long* indptr, const int* idx, const v
 // One sparse SGD round through the per-batch transpose (see glm_csc_bwd_kernel). fuse=1: the
 // backward applies the update + termination (1 GPU); fuse=0: it writes fb[d+2] for the
 // all-reduce and fmlx_glm_update follows.
+FMLX_API void fmlx_glm_set_cell_xcd(int on) { g_cell_xcd = on != 0; }
+
 FMLX_API int fmlx_glm_csc_round(int acc_f64, int G, const long* indptr, const int* idx, const void* val,
                                 const void* y, const void* wt, void* coef, long n, int d, long B, int loss, int* state,
                                 void* mult, void* wl, const int* colptr, const int* erow, const void* eval, void* fb,

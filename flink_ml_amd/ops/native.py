@@ -79,6 +79,7 @@ _KERNEL_SIGS = {
                           c_int, c_void_p, c_void_p, c_void_p],
     "fmlx_glm_csr_predict": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p],
     "fmlx_glm_set_csc_tuning": [c_int, c_int],
+    "fmlx_glm_set_cell_xcd": ([c_int], None),
     "fmlx_glm_wl_elems": [],
     "fmlx_glm_csc_round": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int,
                            c_long, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,

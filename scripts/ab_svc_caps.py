@@ -39,8 +39,8 @@ def main():
     from flink_ml_amd.ops import glm as gk
 
     trainers = {}
-    cfgs = [(0, 8, 0, 0, 11), (32768, 8, 1, 0, 11), (32768, 8, 1, -1, 0), (32768, 8, 1, 10, 11),
-            (32768, 8, 1, 4, 10), (32768, 8, 1, 6, 10)]
+    cfgs = [(32768, 8, 1, 0, 11), (32768, 8, 1, -1, 0), (32768, 8, 1, 10, 11), (32768, 8, 1, 16, 11),
+            (32768, 8, 1, 6, 10)]
     if len(sys.argv) > 1 and sys.argv[1] == "--layouts":  # (round-5 layout sweep)
         cfgs = [(0, 8, 0, 0, 11), (32768, 8, 0, 0, 11), (32768, 8, 1, 0, 11), (32768, 16, 1, 0, 11)]
     if len(sys.argv) > 2 and sys.argv[1] == "--splits":  # e.g. --splits 1 (one config: per-kernel profiles)
@@ -62,20 +62,21 @@ def main():
                           "tiles_max": int(tr.csc.ntiles.max()) if tr.csc.ET else 0,
                           "build_ms": round((time.perf_counter() - t0) * 1e3, 1), "batches": tr.csc.P}), flush=True)
         trainers[(tile, hdiv, spread, splits, rbb)] = tr
-    cases = [(k, 0) for k in trainers]
+    # (the cell trainers twice: blocks in launch order / XCD-aware split-major order)
+    cases = [(k, x) for k in trainers for x in ((0, 1) if trainers[k].csc.cells else (0,))]
     for rep in range(2):
-        for key, cap in cases:
+        for key, xcd in cases:
             tr = trainers[key]
-            lib.fmlx_glm_set_csc_tuning(0, cap)
+            lib.fmlx_glm_set_cell_xcd(xcd)
             tr.run_rounds(20)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             tr.run_rounds(200)
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) / 200 * 1e3
-            print(json.dumps({"tile": key[0], "heavy_div": key[1], "spread": key[2], "splits": key[3], "rbb": key[4], "rep": rep,
+            print(json.dumps({"tile": key[0], "heavy_div": key[1], "spread": key[2], "splits": key[3], "rbb": key[4], "xcd": xcd, "rep": rep,
                               "ms_per_round": round(ms, 4)}), flush=True)
-    lib.fmlx_glm_set_csc_tuning(0, 0)
+    lib.fmlx_glm_set_cell_xcd(0)
 
 
 
