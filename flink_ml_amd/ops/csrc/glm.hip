@@ -1397,8 +1397,10 @@ __global__ __launch_bounds__(CELL_THREADS) void glm_csr_cell_fwd_kernel(
   if (xcd) {
     // XCD-aware order: block b runs on XCD b mod 8 (round-robin dispatch); give XCD x the cells
     // of a contiguous split-major range, so its L2 holds the coefficient slices of ≤ 2 splits
-    const int per = (ncell + 7) >> 3;
-    const int g = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    // (a bijection of [0, grid): XCD x holds the n_x = ⌈(grid − x) / 8⌉ blocks b ≡ x mod 8, so it
+    // starts at Σ_{y<x} n_y = x·⌊grid/8⌋ + min(x, grid mod 8))
+    const int x = (int)(blockIdx.x & 7), q = (int)(gridDim.x >> 3), r = (int)(gridDim.x & 7);
+    const int g = x * q + (x < r ? x : r) + (int)(blockIdx.x >> 3);
     if (g >= ncell) return;
     sp = g / nrb;
     rb = g - sp * nrb;
@@ -2375,7 +2377,7 @@ FMLX_API void fmlx_glm_set_csc_tuning(int fwd_cap, int bwd_cap) {
 }
 
 // tiled backward: the column tiles of the batches (BatchCsc.tiles) and the packing of erow
-// forward cells in XCD-aware order (default; fmlx_glm_set_cell_xcd(0): launch order) — 64.0 → 62.1 µs
+// forward cells in XCD-aware order (default; fmlx_glm_set_cell_xcd(0): launch order) — 63.5 → 61.4 µs
 // per SVC round, profiles/r5/svc_cell_forward_ab.jsonl
 static int g_cell_xcd = 1;
 struct CscTiles {

@@ -346,7 +346,7 @@ def test_batch_csr_forward_cells(vdtype, d, B, S, rbb, monkeypatch):
 
 @pytest.mark.parametrize("tile", [0, 64, 2048])
 @pytest.mark.parametrize("vdtype", [torch.float32, torch.float64])
-@pytest.mark.parametrize("cells", [False, True])
+@pytest.mark.parametrize("cells", [False, True, 5])
 def test_sparse_sgd_tiled_backward_matches_host(tile, vdtype, cells, monkeypatch):
     """Whole fits through the tiled backward (light and heavy tiles; the feedback path is the
     two-rank test above) and the cell forward or the row-group forward, against the fp64 host
@@ -354,20 +354,29 @@ def test_sparse_sgd_tiled_backward_matches_host(tile, vdtype, cells, monkeypatch
     _need_gpu()
     from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
 
-    n, d = 5100, 800  # 700-row batches in the forward's 2048-row blocks: partial last blocks
+    n, d = 5100, 800  # 2000-row batches in 1024-row blocks: partial last blocks, a 1100-row batch
     indptr, idx, vals, dense, y, w = _csr(n, d, 21, max_nnz=60, dtype=vdtype)
     from flink_ml_amd.ops import glm as gk
 
     monkeypatch.setenv("FMLX_CSC_TILE", str(tile))
     monkeypatch.setattr(gk, "TILE_MIN_VISITS", 0)
-    monkeypatch.setattr(gk, "CELLS", cells)
-    for wt in (None, w):
-        sgd = SGD(max_iter=9, learning_rate=0.2, global_batch_size=2500, tol=1e-9, reg=0.05, elastic_net=0.4)
+    monkeypatch.setattr(gk, "CELLS", bool(cells))
+    if cells is not True and cells:
+        monkeypatch.setattr(gk, "CELL_SPLITS", cells)  # 2 row blocks × 5: a grid of 10 (uneven per XCD)
+    from flink_ml_amd.ops import native
+
+    # cells in the default XCD-aware block order, and (odd grid) in launch order
+    for wt, xcd in ((None, 1), (w, 1)) + (((w, 0),) if cells is not True and cells else ()):
+        sgd = SGD(max_iter=9, learning_rate=0.2, global_batch_size=2000, tol=1e-9, reg=0.05, elastic_net=0.4)
         ref = TorchGlmTrainer(sgd, np.zeros(d), dense, y, wt, "hinge").fit()
         tr = DeviceGlmTrainer(sgd, np.zeros(d), _sparse_col(indptr, idx, vals, d, "cuda"), y.cuda(),
                               None if wt is None else wt.cuda(), "hinge")
         assert tr.csc is not None and tr.csc.ET == tile
         assert (tr.csc.cells > 0) == (cells and not gk.DETERMINISTIC)
-        got = tr.fit()
+        native.kernels().fmlx_glm_set_cell_xcd(xcd)
+        try:
+            got = tr.fit()
+        finally:
+            native.kernels().fmlx_glm_set_cell_xcd(1)
         tol = 1e-10 if vdtype == torch.float64 else 1e-5
-        assert np.abs(got - ref).max() <= tol * max(1.0, np.abs(ref).max()), (tile, np.abs(got - ref).max())
+        assert np.abs(got - ref).max() <= tol * max(1.0, np.abs(ref).max()), (tile, xcd, np.abs(got - ref).max())
