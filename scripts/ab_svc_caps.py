@@ -43,6 +43,8 @@ def main():
             (32768, 8, 1, 6, 10)]
     if len(sys.argv) > 1 and sys.argv[1] == "--layouts":  # (round-5 layout sweep)
         cfgs = [(0, 8, 0, 0, 11), (32768, 8, 0, 0, 11), (32768, 8, 1, 0, 11), (32768, 16, 1, 0, 11)]
+    if len(sys.argv) > 1 and sys.argv[1] == "--auto":  # tiles alone vs tiles + cells (automatic shape)
+        cfgs = [(32768, 8, 1, 0, 11), (32768, 8, 1, -1, 0)]
     if len(sys.argv) > 2 and sys.argv[1] == "--splits":  # e.g. --splits 1 (one config: per-kernel profiles)
         cfgs = [(32768, 8, 1, int(v), 11) for v in sys.argv[2].split(",")]
     for tile, hdiv, spread, splits, rbb in cfgs:
