@@ -557,9 +557,17 @@ class DeviceGlmTrainer:
         """Non-blocking termination check: the device state copied to pinned memory at the previous
         check is read if that copy has landed, and a new copy is queued. A stop is seen one check
         interval late at worst — the rounds launched meanwhile are predicated off on the device —
-        and the host never waits for the GPU mid-fit (a blocking check drained the launch queue)."""
+        and the host never waits for the GPU mid-fit (a blocking check drained the launch queue).
+
+        Distributed: every rank must break after the SAME number of launched rounds (a host-issued
+        all-reduce per round, or a captured one, has to find its peers), so the lag is fixed at
+        exactly one interval — the copy queued at the previous check is waited for (it is one
+        interval behind the launch front, so the wait rarely blocks) — instead of depending on
+        each rank's own timing."""
         stopped = False
         ev = getattr(self, "_state_ev", None)
+        if ev is not None and self.distributed:
+            hostsync.wait_event(ev)
         if ev is not None and ev.query():
             st = self._state_host
             stopped = bool(st[6]) if self.defer else not bool(st[1 + (int(st[0]) & 1)])

@@ -119,6 +119,20 @@ def _sign(x):
     return (x > 0) - (x < 0)
 
 
+def _decimal(x: float, d: int, rounding) -> float:
+    """A double rounded at d decimals the way Flink does it: its shortest decimal representation
+    (``BigDecimal.valueOf``) is rounded, under a context wide enough for any double's digits (the
+    default 28 digits raised InvalidOperation for ROUND(1e20, 10))."""
+    from decimal import Decimal, localcontext
+
+    v = Decimal(repr(x))
+    with localcontext() as ctx:
+        ctx.prec = max(28, v.adjusted() + max(d, 0) + 4)
+        if d >= 0:
+            return float(v.quantize(Decimal(1).scaleb(-d), rounding=rounding))
+        return float(v.scaleb(d).quantize(Decimal(1), rounding=rounding).scaleb(-d))
+
+
 def _round(x, d=0):
     """ROUND(x[, d]) as Flink: HALF_UP (ties away from zero) at d decimals (d < 0: tens, hundreds…),
     keeping the input's type — ROUND(INT) is an INT (SQLite's built-in returns REAL). Doubles round
@@ -131,24 +145,25 @@ def _round(x, d=0):
     if isinstance(x, float):
         if x != x or x in (float("inf"), float("-inf")):
             return x
-        return float(Decimal(repr(x)).quantize(Decimal(1).scaleb(-d), rounding=ROUND_HALF_UP)) if d >= 0 else \
-            float(Decimal(repr(x)).scaleb(d).quantize(Decimal(1), rounding=ROUND_HALF_UP).scaleb(-d))
+        return _decimal(x, d, ROUND_HALF_UP)
     if d >= 0:
         return x
     return int(Decimal(x).scaleb(d).quantize(Decimal(1), rounding=ROUND_HALF_UP).scaleb(-d))
 
 
 def _truncate(x, d=0):
-    """TRUNCATE(x[, d]): toward zero at d decimals, the input's type kept (Flink)."""
+    """TRUNCATE(x[, d]): toward zero at d decimals, the input's type kept (Flink). Doubles truncate
+    their shortest decimal representation: TRUNCATE(0.29, 2) = 0.29 (0.29·100 is 28.999… in binary)."""
+    from decimal import ROUND_DOWN
+
     if x is None or d is None:
         return None
     d = int(d)
     if isinstance(x, int):
-        return x if d >= 0 else int(x / 10 ** -d) * 10 ** -d
+        return x if d >= 0 else (1 if x >= 0 else -1) * (abs(x) // 10 ** -d) * 10 ** -d
     if x != x or x in (float("inf"), float("-inf")):
         return x
-    sc = 10.0 ** d
-    return math.trunc(x * sc) / sc
+    return _decimal(x, d, ROUND_DOWN)
 
 
 def _least(*a):

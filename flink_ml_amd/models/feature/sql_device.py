@@ -334,6 +334,65 @@ def java_math(fn, *a):
         return math.inf
 
 
+# |x|·10^d below this: a decimal boundary (ROUND: a half-point; TRUNCATE: a multiple of 10^-d)
+# that lies in x's rounding interval is x's shortest decimal representation itself — the interval
+# (≤ 2^-52·|x| wide, ≤ 1/16 in units of 10^-d) holds no other decimal of d + 1 digits — see
+# decimal_round
+_DEC_EXACT = float(2 ** 48)
+
+
+def _two_product_err(a: torch.Tensor, s: float, p: torch.Tensor) -> torch.Tensor:
+    """a·s − p exactly, for p = fl(a·s) (Dekker's product with Veltkamp splits: every step is an
+    exact fp64 operation; separate elementwise kernels, so nothing is contracted into an fma)."""
+    def split(v):
+        c = v * 134217729.0  # 2^27 + 1
+        hi = c - (c - v)
+        return hi, v - hi
+
+    ah, al = split(a)
+    bh, bl = split(torch.full_like(a, s))
+    return ((ah * bh - p) + ah * bl + al * bh) + al * bl
+
+
+def decimal_round(a: torch.Tensor, d: int, half_up: bool) -> torch.Tensor:
+    """ROUND (half away from zero) / TRUNCATE (toward zero) of doubles at d decimals with Flink's
+    semantics: the SHORTEST decimal representation is rounded (``BigDecimal.valueOf``), not the
+    binary value — ROUND(2.675, 2) = 2.68 and TRUNCATE(0.29, 2) = 0.29, although 2.675·100 and
+    0.29·100 are 267.49999999999997 and 28.999999999999996 in binary.
+
+    Exact elementwise, without decimal strings: with s = 10^d (exact for d <= 22) and y = |x|·s,
+    * a boundary c (TRUNCATE: k/s, ROUND: (2k+1)/(2s), k next to floor(y)) is x's shortest decimal
+      iff the correctly rounded quotient c equals |x| — then the result is decided by c;
+    * otherwise no boundary lies in x's rounding interval, so x and its decimal round alike, and
+      the binary value y + e (e the product's exact error, ``_two_product_err``) decides: its side of
+      a boundary is the sign of (y − boundary) + e, an exact difference plus one rounding.
+    Elements with |x|·s ≥ 2^48 (and d outside 0..22) are left to the host engine (Unsupported)."""
+    if d < 0 or d > 22:
+        raise Unsupported("ROUND / TRUNCATE of a DOUBLE at d < 0 or d > 22")
+    x = a.to(torch.float64)
+    s = float(10 ** d)
+    ax = torch.abs(x)
+    y = ax * s
+    fin = torch.isfinite(x)
+    big = fin & (y >= _DEC_EXACT)
+    if bool(big.any()):
+        raise Unsupported("ROUND / TRUNCATE beyond the exactly decided range")
+    e = _two_product_err(ax, s, y)
+    k = torch.floor(y)
+    if half_up:
+        # the half-point next to y (k − 1/2 is ≥ 1/2 − ulp away); the decimal tie rounds away from zero
+        tie = (2 * k + 1) / (2 * s) == ax
+        side = ((y - k) - 0.5) + e >= 0  # binary value at or above k + 1/2
+        r = torch.where(tie | side, k + 1, k)
+    else:
+        on_k = k / s == ax
+        on_k1 = (k + 1) / s == ax
+        below = (y == k) & (e < 0)  # y rounded up onto k: the binary value is just below it
+        r = torch.where(on_k1, k + 1, torch.where(on_k, k, torch.where(below, k - 1, k)))
+    out = torch.where(fin, torch.copysign(r / s, x), x)
+    return out.to(a.dtype)
+
+
 def _is_int(x) -> bool:
     if isinstance(x, torch.Tensor):
         return not x.dtype.is_floating_point and x.dtype != torch.bool
@@ -526,18 +585,22 @@ class _Eval:
             return torch.pow(a.to(torch.float64) if not a.dtype.is_floating_point else a, b)
         if name == "MOD" and len(args) == 2:
             return self.binary("%", args[0], args[1])
-        if name == "ROUND" and len(args) in (1, 2):
+        if name in ("ROUND", "TRUNCATE") and len(args) in (1, 2):
             a = _num(args[0])
             d = int(args[1]) if len(args) == 2 else 0
             if _is_int(a) and d >= 0:
-                return a  # ROUND(INT) is the INT itself
-            if not _is_float(a):
-                raise Unsupported("ROUND of a non-numeric value")
-            # SQL ROUND is half away from zero (torch.round is half to even)
-            s = 10.0 ** d
+                return a  # ROUND / TRUNCATE of an INT at d >= 0 is the INT itself
             if not isinstance(a, torch.Tensor):
-                return math.copysign(math.floor(abs(a) * s + 0.5) / s, a) if a == a else a
-            return torch.sign(a) * torch.floor(torch.abs(a) * s + 0.5) / s
+                from .misc import _round, _truncate
+
+                return (_round if name == "ROUND" else _truncate)(a, d)
+            if _is_int(a):  # tens, hundreds…: integer arithmetic, ties away from zero
+                p = 10 ** -d
+                m = torch.abs(a) + (p // 2 if name == "ROUND" else 0)
+                return torch.sign(a) * (m // p) * p
+            if not _is_float(a):
+                raise Unsupported(name + " of a non-numeric value")
+            return decimal_round(a, d, name == "ROUND")
         if name == "LOG" and len(args) in (1, 2):  # Flink: LOG(x) = LN(x), LOG(b, x) = LN(x) / LN(b)
             if len(args) == 1:
                 return self.fn("LN", args)
@@ -549,17 +612,6 @@ class _Eval:
             a, b = self.full(a), self.full(b)
             return torch.atan2(a.to(torch.float64) if not a.dtype.is_floating_point else a,
                                b.to(torch.float64) if not b.dtype.is_floating_point else b)
-        if name == "TRUNCATE" and len(args) in (1, 2):  # toward zero at d decimals, the type kept
-            a = _num(args[0])
-            d = int(args[1]) if len(args) == 2 else 0
-            if _is_int(a) and d >= 0:
-                return a
-            if not _is_float(a):
-                raise Unsupported("TRUNCATE of a non-numeric value")
-            sc = 10.0 ** d
-            if not isinstance(a, torch.Tensor):
-                return math.trunc(a * sc) / sc if math.isfinite(a) else a
-            return torch.trunc(a * sc) / sc
         if name in ("PI", "E") and not args:
             return math.pi if name == "PI" else math.e
         if name == "IF" and len(args) == 3:

@@ -164,7 +164,10 @@ def pad_columns(X: torch.Tensor) -> Optional[torch.Tensor]:
     cpl = 1
     while cpl * 64 < nch:
         cpl *= 2
-    if cpl > MAX_CPL and -(-nch // WIDE_WAVES) > 64 * 8:  # neither the one-wave nor the wide kernel
+    # the wide-row kernel only runs where the trainer would pick it (a padded copy for
+    # the GEMV path doubled the partition's HBM for no speedup)
+    wide_ok = not DETERMINISTIC and WIDE_FUSED
+    if cpl > MAX_CPL and (not wide_ok or -(-nch // WIDE_WAVES) > 64 * 8):  # neither fused kernel
         return None
     need = n * dp * X.element_size()
     free, _ = torch.cuda.mem_get_info(X.device)
@@ -173,7 +176,7 @@ def pad_columns(X: torch.Tensor) -> Optional[torch.Tensor]:
     Xp = torch.empty((n, dp), dtype=X.dtype, device=X.device)
     Xp[:, d:].zero_()
     Xp[:, :d].copy_(X)
-    return Xp if pick_layout(Xp) is not None or pick_wide_layout(Xp) is not None else None
+    return Xp if pick_layout(Xp) is not None or wide_ok and pick_wide_layout(Xp) is not None else None
 
 
 def grad_partials(X, y, wt, coef, B: int, loss: int, state, partials, nblocks: int) -> None:

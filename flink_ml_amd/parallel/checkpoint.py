@@ -49,7 +49,15 @@ def _encode(v):
     if v is None or isinstance(v, (bool, int, float, str, bytes)):
         return v
     if isinstance(v, np.ndarray):
-        return {"__np__": torch.from_numpy(np.ascontiguousarray(v)) if v.dtype != object else _encode(v.tolist())}
+        if v.dtype != object:
+            try:
+                return {"__np__": torch.from_numpy(np.ascontiguousarray(v))}
+            except TypeError:  # strings, bytes, datetimes, unsigned widths torch cannot hold
+                if v.dtype.kind in "Mm":  # datetime64 / timedelta64: their int64 ticks
+                    return {"__npt__": v.dtype.str, "shape": list(v.shape),
+                            "ticks": torch.from_numpy(np.ascontiguousarray(v).view(np.int64).reshape(-1))}
+                return {"__npt__": v.dtype.str, "shape": list(v.shape), "data": _encode(v.reshape(-1).tolist())}
+        return {"__np__": _encode(v.tolist())}
     if isinstance(v, dict):
         return {"__dict__": [[_encode(k), _encode(x)] for k, x in v.items()]}
     if isinstance(v, tuple):
@@ -78,6 +86,13 @@ def _decode(v):
     if "__np__" in v:
         x = v["__np__"]
         return x.numpy() if isinstance(x, torch.Tensor) else __import__("numpy").array(_decode(x), dtype=object)
+    if "__npt__" in v:
+        import numpy as np
+
+        dt = np.dtype(v["__npt__"])
+        if "ticks" in v:
+            return v["ticks"].numpy().view(dt).reshape(v["shape"])
+        return np.array(_decode(v["data"]), dtype=dt).reshape(v["shape"])
     if "__tuple__" in v:
         return tuple(_decode(x) for x in v["__tuple__"])
     if "__dict__" in v:

@@ -144,3 +144,21 @@ def test_checkpoint_restore_is_weights_only(tmp_path):
         mgr.save("alg", 4, {"x": Foreign()})
     with pytest.raises(ValueError):
         ck._decode({"__obj__": "os:system", "attrs": {}})
+
+
+def test_checkpoint_round_trips_arrays_torch_cannot_hold(tmp_path):
+    """string / bytes / datetime / uint32 numpy arrays (label or category state) are
+    saved as tagged lists (or int64 ticks) and rebuilt with their dtype."""
+    import numpy as np
+
+    from flink_ml_amd.parallel import checkpoint as ck
+
+    mgr = ck.CheckpointManager(str(tmp_path), 1)
+    st = {"u": np.array([["a", "bc"], ["déf", ""]]), "b": np.array([b"x", b"yz"]),
+          "ts": np.array(["2024-01-02T03:04:05", "NaT"], dtype="datetime64[ns]"),
+          "td": np.array([5, -3], dtype="timedelta64[s]"), "u32": np.array([1, 2 ** 32 - 1], dtype=np.uint32)}
+    mgr.save("alg", 1, st)
+    _, got = mgr.restore("alg")
+    for k, v in st.items():
+        assert got[k].dtype == v.dtype and got[k].shape == v.shape, k
+        np.testing.assert_array_equal(got[k], v)

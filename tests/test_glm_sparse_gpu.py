@@ -380,3 +380,32 @@ def test_sparse_sgd_tiled_backward_matches_host(tile, vdtype, cells, monkeypatch
             native.kernels().fmlx_glm_set_cell_xcd(1)
         tol = 1e-10 if vdtype == torch.float64 else 1e-5
         assert np.abs(got - ref).max() <= tol * max(1.0, np.abs(ref).max()), (tile, xcd, np.abs(got - ref).max())
+
+
+def _tol_stop_worker(rank, world, check_every):
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer
+
+    n, d = 6000, 400
+    indptr, idx, vals, dense, y, w = _csr(n, d, 40 + rank, max_nnz=30, dtype=torch.float32)
+    # tol far above any hinge loss: the iteration stops after its first round, so every launched
+    # round after it is predicated off on the device — but each still issues its host all-reduce,
+    # which only matches its peer's if both ranks break after the same number of launched rounds
+    sgd = SGD(max_iter=60, learning_rate=0.2, global_batch_size=2000, tol=1e9)
+    tr = DeviceGlmTrainer(sgd, np.zeros(d), _sparse_col(indptr, idx, vals, d, "cuda"), y.cuda(), None, "hinge",
+                          check_every=check_every)
+    coef = tr.fit()
+    return coef, tr.rounds_executed(), tr._launched
+
+
+@pytest.mark.parametrize("check_every", [1, 3])
+def test_two_rank_sparse_fit_stops_on_tol_in_lockstep(check_every):
+    """the polled termination check must make every rank break after the same
+    launched round; a rank seeing the stop one interval earlier left its peer's all-reduces
+    unmatched. Two gloo ranks on one GPU, host all-reduce per round (TAIL_FEEDBACK)."""
+    _need_gpu()
+    env = {"FMLX_DEVICE": "cuda:0", "FMLX_XGMI": "0"}
+    res = run_spmd(_tol_stop_worker, 2, check_every, env=env, timeout=300)
+    (c0, r0, l0), (c1, r1, l1) = res
+    assert r0 == r1 == 1
+    assert l0 == l1 < 60
+    assert np.array_equal(c0, c1)

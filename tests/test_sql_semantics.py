@@ -199,3 +199,46 @@ def test_order_by_over_ranks_falls_back():
     t = _mixed()
     with pytest.raises(sql_device.Unsupported):
         sql_device.evaluate("SELECT x FROM __THIS__ ORDER BY x", t, world=2, rank=0)
+
+
+@pytest.mark.parametrize("expr,expected", [
+    ("TRUNCATE(0.29, 2)", 0.29), ("ROUND(2.675, 2)", 2.68), ("ROUND(-2.675, 2)", -2.68), ("ROUND(1.005, 2)", 1.01),
+    ("TRUNCATE(-0.29, 2)", -0.29), ("ROUND(1e20, 10)", 1e20), ("TRUNCATE(1e20, 10)", 1e20),
+    ("TRUNCATE(-17, -1)", -10),
+])
+def test_decimal_rounding_of_doubles_on_both_engines(expr, expected):
+    """Flink rounds a double's shortest decimal form (BigDecimal.valueOf): 0.29·100 and
+    2.675·100 are 28.999… and 267.4999… in binary, yet TRUNCATE(0.29, 2) = 0.29 and
+    ROUND(2.675, 2) = 2.68; ROUND(1e20, 10) is 1e20 (no 28-digit decimal context overflow)."""
+    t = Table({"id": torch.arange(2, dtype=torch.int64)}, num_rows=2)
+    dev, host = _both("SELECT %s AS v FROM __THIS__" % expr, t)
+    for rows in (dev, host):
+        v = rows[0][0]
+        assert type(v) is type(expected) and v == expected, (expr, v)
+
+
+def test_decimal_rounding_of_double_columns_matches_the_host_engine():
+    """The device engine's exact elementwise ROUND / TRUNCATE (decimal boundary test by correctly
+    rounded division + Dekker product error) against the host's Decimal(repr(x)) on values built to
+    sit on decimal boundaries, for d = 0..6; out-of-range magnitudes fall back to the host engine."""
+    import random
+
+    from flink_ml_amd.models.feature.misc import _round, _truncate
+
+    rnd = random.Random(7)
+    vals = [0.29, 2.675, -2.675, 1.005, 0.125, -0.0, 1.15, 2.5, -2.5, 1e-9, 123456.785]
+    for _ in range(4000):
+        q = rnd.randint(-10 ** 7, 10 ** 7)
+        vals.append(q / 10 ** rnd.randint(0, 7) + rnd.choice([0.0, 5e-4, 5e-3, 0.5, 5e-7]))
+        vals.append(rnd.uniform(-1e4, 1e4))
+    x = torch.tensor(vals, dtype=torch.float64)
+    for d in range(7):
+        for half_up, f in ((True, _round), (False, _truncate)):
+            got = sql_device.decimal_round(x, d, half_up).tolist()
+            want = [f(v, d) for v in vals]
+            assert got == want, next((v, g, w) for v, g, w in zip(vals, got, want) if g != w)
+    t = Table({"x": torch.tensor([0.29, 2.675, -1.005], dtype=torch.float64)}, num_rows=3)
+    dev, host = _both("SELECT TRUNCATE(x, 2) AS t, ROUND(x, 2) AS r FROM __THIS__", t)
+    assert dev == host == [(0.29, 0.29), (2.67, 2.68), (-1.0, -1.01)]
+    with pytest.raises(sql_device.Unsupported):
+        sql_device.decimal_round(torch.tensor([1e15]), 3, True)
