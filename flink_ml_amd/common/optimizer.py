@@ -248,10 +248,17 @@ class DeviceGlmTrainer:
         self.wide_fused = self.wide_layout is not None
         self.wide = not self.sparse and self.layout is None and not self.wide_fused
         self._host_round = 0
+        self.bkt = None
         if self.sparse:
             self.scratch = None
             self.nparts = 0
-            if dev.type == "cuda" and self.n > 0 and self._csc_pays(sgd):
+            if dev.type == "cuda" and self.n > 0 and self._bucket_pays(sgd):
+                # each batch visited a few times (the reference's regime): the single-visit round,
+                # nothing built per batch
+                self.bkt = gk.BucketRound.alloc(self.indptr, self.values, self.n, self.d, self.B)
+                if self.bkt is not None:
+                    self.wl = _dzeros(gk.wl_elems(), acc, dev)
+            if self.bkt is None and dev.type == "cuda" and self.n > 0 and self._csc_pays(sgd):
                 # allocated here, batches transposed lazily before the rounds that visit them
                 self.csc = gk.BatchCsc.alloc(self.indptr, self.indices, self.values, self.n, self.d, self.B,
                                              max_rounds=sgd.max_iter)
@@ -335,6 +342,15 @@ class DeviceGlmTrainer:
             self.use_graph = False  # a gloo all-reduce of device tensors cannot be captured
         self.graphs.clear()
 
+    def _bucket_pays(self, sgd: SGD) -> bool:
+        """The single-visit bucket round (no per-batch transpose) for fits that visit each batch
+        fewer than ``gk.TILE_MIN_VISITS`` times; more visits amortise the transposed layout's
+        build (its steady rounds are faster). Not in the deterministic mode (LDS float atomics)."""
+        if gk.DETERMINISTIC or not gk.BUCKETS:
+            return False
+        P = -(-self.n // max(self.B, 1))
+        return sgd.max_iter < gk.TILE_MIN_VISITS * max(P, 1)
+
     def _csc_pays(self, sgd: SGD) -> bool:
         """Whether the per-batch column-major copy pays for itself in this fit (a fit that visits
         each batch fewer than CSC_BUILD_ROUNDS times keeps the atomic-scatter gradient)."""
@@ -353,6 +369,15 @@ class DeviceGlmTrainer:
                 self._launch_round(1, ensure)
             return
         s = self.sgd
+        if self.bkt is not None:
+            gk.bkt_round(self.bkt, self.indptr, self.indices, self.values, self.y, self.w, self.coef, self.n, self.d,
+                         self.B, self.loss, self.state, self.wl, self.feedback, not self.distributed, s.max_iter, s.tol,
+                         s.learning_rate, s.reg, s.elastic_net)
+            if self.distributed:
+                comm.all_reduce_sum(self.feedback)
+                gk.update(self.feedback, self.d, self.coef, self.state, s.max_iter, s.tol, s.learning_rate, s.reg,
+                          s.elastic_net)
+            return
         if self.csc is not None:
             if ensure and not torch.cuda.is_current_stream_capturing():
                 self._ensure_csc(self._launched, 1)
@@ -446,7 +471,7 @@ class DeviceGlmTrainer:
         # everything a round mutates that the next round reads (the sparse path's Σw/Σloss
         # parity slots, the deferred mode's accumulator ring and coefficient ring included) is
         # rewound after the warm-up
-        live = [self.state, self.coef] + ([self.wl] if self.csc is not None else [])
+        live = [self.state, self.coef] + ([self.wl] if self.csc is not None or self.bkt is not None else [])
         if self.defer:
             live += [self.scratch.acc, self.cw, self.scratch.cnt]  # cnt: the dynamic schedule's counters
         snapshot = [t.clone() for t in live]

@@ -121,6 +121,7 @@ def _run(cmd):
 FILE_FLAGS = {"kmeans.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-Wno-inline-asm"],
               # the fused round's ticket atomics: no lane-0 result fix-up (keeps counted vmcnt waits)
               "glm.hip": ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"],
+              "glm_sparse.hip": ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"],
               # MFMA accumulators in arch VGPRs: the AGPR form rotated the DCT's accumulators
               # through VGPRs every k step
               "dct.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}

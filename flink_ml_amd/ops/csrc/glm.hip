@@ -33,90 +33,12 @@
 //    reference's sequential slicing with reset-to-0 (SGD.java:263-268).
 #include "common.h"
 #include "xgmi.h"
+#include "glm_core.h"
+
+FMLX_API void fmlx_glm_sparse_set_trace(void* trace);  // glm_sparse.hip
 
 namespace {
 
-enum { LOSS_LOGISTIC = 0, LOSS_HINGE = 1, LOSS_LSQ = 2, LOSS_FTRL = 3 };
-enum { ST_ROUND = 0, ST_RUN0 = 1, ST_ARRIVE = 3, ST_EXECUTED = 4, ST_ROUND_ALT = 5, ST_DONE = 6 };
-enum { TAIL_PARTIALS = 0, TAIL_FEEDBACK = 1, TAIL_UPDATE = 2, TAIL_XGMI = 3 };
-constexpr int TAIL_GROUP = 32;  // block partials summed per group finisher
-constexpr int TAIL_MAXG = 16;   // groups of the deterministic tail (=> at most 512 blocks)
-constexpr int TAIL_TOP = 64;    // index of the top-level ticket (atomic tail: up to 64 groups)
-
-// fp32 (bf16/fp32 data): one v_exp, one v_log, one v_rcp per row instead of the accurate libm
-// expf/log1pf/division sequences (~100 VALU instructions per row, wave-uniform work that cost
-// 6 µs of the 200 MB round body, measured); fp64 parity mode keeps the accurate path below.
-//   logistic, z = −dot·ys, t = e^(−|z|) ∈ (0, 1]:  softplus(z) = max(z, 0) + log(1 + t),
-//   mult = −ys / (e^(−z) + 1) = −ys · (z > 0 ? 1 : t) / (1 + t)
-__device__ __forceinline__ void loss_and_mult(int loss, float dot, float y, float wt, float& l, float& m) {
-  if (loss == LOSS_LOGISTIC) {
-    const float ys = 2.f * y - 1.f;
-    const float z = -dot * ys;
-    // raw v_exp_f32 / v_log_f32 (base 2): t ∈ (0, 1] and 1 + t ∈ (1, 2] need none of the
-    // denormal range fix-ups of expf/logf; v_rcp_f32 (1 ulp), not the IEEE division sequence
-    const float t = __builtin_amdgcn_exp2f(-fabsf(z) * 1.4426950408889634f);
-    const float r = __builtin_amdgcn_rcpf(1.f + t);
-    l = wt * (fmaxf(z, 0.f) + __builtin_amdgcn_logf(1.f + t) * 0.6931471805599453f);
-    m = wt * (-ys) * (z > 0.f ? r : t * r);
-  } else if (loss == LOSS_HINGE) {
-    const float ys = 2.f * y - 1.f;
-    const float h = 1.f - ys * dot;
-    const bool pos = h > 0.f;
-    l = pos ? wt * h : 0.f;
-    m = pos ? -ys * wt : 0.f;
-  } else if (loss == LOSS_FTRL) {
-    m = __builtin_amdgcn_rcpf(1.f + __expf(-dot)) - y;
-    l = 0.f;
-  } else {
-    const float r = dot - y;
-    l = wt * 0.5f * r * r;
-    m = r * wt;
-  }
-}
-
-template <typename A>
-__device__ __forceinline__ void loss_and_mult(int loss, A dot, A y, A wt, A& l, A& m) {
-  if (loss == LOSS_LOGISTIC) {
-    A ys = (A)2 * y - (A)1;
-    A z = -dot * ys;
-    // wt*log(1+exp(z)), stable softplus
-    A sp = z > (A)0 ? z + log1p(exp(-z)) : log1p(exp(z));
-    l = wt * sp;
-    m = wt * (-ys / (exp(dot * ys) + (A)1));
-  } else if (loss == LOSS_HINGE) {
-    A ys = (A)2 * y - (A)1;
-    A h = (A)1 - ys * dot;
-    if (h > (A)0) { l = wt * h; m = -ys * wt; } else { l = (A)0; m = (A)0; }
-  } else if (loss == LOSS_FTRL) {
-    // OnlineLogisticRegression local gradient (OnlineLogisticRegression.java:344-368, dense
-    // branch): (sigmoid(dot) - label) · x, weight ignored; the weight slot counts rows.
-    m = (A)1 / ((A)1 + exp(-dot)) - y;
-    l = (A)0;
-  } else {
-    A r = dot - y;
-    l = wt * (A)0.5 * r * r;
-    m = r * wt;
-  }
-}
-
-__device__ __forceinline__ bool round_running(const int* st, int& e) {
-  e = st[ST_ROUND];
-  return st[ST_RUN0 + (e & 1)] != 0;
-}
-
-// apply the SGD step + elastic-net regularisation to one coefficient (SGD.java:231-243,
-// RegularizationUtils.java:47-91). The reg loss only feeds the discarded totalLoss slot in the
-// reference, so it is not materialised here.
-template <typename A>
-__device__ __forceinline__ A sgd_apply(A w, A g, A W, A lr, A reg, A en) {
-  if (!(W > (A)0)) return w;
-  w = w - lr / W * g;
-  if (reg == (A)0) return w;
-  if (en == (A)0) return w * ((A)1 - lr * reg);
-  A sg = w > (A)0 ? (A)1 : (w < (A)0 ? (A)-1 : (A)0);
-  if (en == (A)1) return w - lr * en * reg * sg;
-  return w - lr * (en * reg * sg + ((A)1 - en) * reg * w);
-}
 
 // ------------------------------------------------------------------------------------------
 // Fused round tail (after every block wrote its partial row)
@@ -149,33 +71,6 @@ struct GlmTail {
 };
 constexpr int ACC_MAX_REPS = 8;
 
-// Write-through (sc1) hand-off of the partial rows (cdna_hip_programming.md Guideline 16, the
-// sc1 form of the split-K combine): every handed-off value is stored with an agent-scope store
-// (global_store … sc1) and loaded with an agent-scope load (global_load … sc1), so no release
-// fence (an L2 write-back per block: ~20 µs over 512 blocks, measured) and no acquire fence
-// are needed — only the drain before the ticket.
-template <typename A>
-__device__ __forceinline__ void st_agent(A* p, A v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename A>
-__device__ __forceinline__ A ld_agent(const A* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Every wave drains its sc1 stores, lane 0 draws a ticket; the block drawing the last one
-// proceeds (returns true there only).
-__device__ __forceinline__ bool arrive_last(int* cnt, int expected, int* sflag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *sflag = t == expected - 1;
-  }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the ticket
-  return *sflag != 0;
-}
 
 // Replaces this rank's feedback fb[0..stride) (in LDS) by the rank-order sum over all ranks.
 template <typename A>
@@ -1083,23 +978,6 @@ __device__ __forceinline__ A sum_groups(const A* __restrict__ stage1, int ngroup
   return s;
 }
 
-// last-arriving block advances the round state (Guideline 16 counter form).
-__device__ __forceinline__ void arrive_and_advance(int* state, int e, bool cont, int executed_inc) {
-  __syncthreads();
-  // No data is handed between blocks here: every block has already consumed its read of the
-  // state words (its control flow depended on them) before its ticket add, so the last arriver
-  // may overwrite them; the next kernel sees the writes through the kernel boundary.
-  if (threadIdx.x == 0) {
-    const int nblocks = (int)(gridDim.x * gridDim.y);
-    int t = __hip_atomic_fetch_add(&state[ST_ARRIVE], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == nblocks - 1) {
-      state[ST_RUN0 + ((e + 1) & 1)] = cont ? 1 : 0;
-      state[ST_EXECUTED] += executed_inc;
-      state[ST_ROUND] = e + 1;
-      state[ST_ARRIVE] = 0;
-    }
-  }
-}
 
 template <typename A>
 __global__ __launch_bounds__(256) void glm_reduce_update_kernel(
@@ -1209,602 +1087,6 @@ __global__ __launch_bounds__(256) void glm_predict_kernel(const T* __restrict__ 
         raw[2 * r + 1] = -dot;
       } else {
         pred[r] = dot;
-      }
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// CSR (sparse features) gradient — a wave per row, gather dot, atomic scatter of mult·x into
-// a dense gradient (K5 sparse path, for the 1M-feature LinearSVC config).
-// ------------------------------------------------------------------------------------------
-template <typename A>
-__global__ __launch_bounds__(256) void glm_grad_csr_kernel(const long* __restrict__ indptr, const int* __restrict__ idx,
-                                                           const A* __restrict__ val, const A* __restrict__ y,
-                                                           const A* __restrict__ wt, const A* __restrict__ coef, long n,
-                                                           int d, long B, int loss, const int* __restrict__ state,
-                                                           A* __restrict__ grad /* d+2, zeroed */) {
-  int e;
-  if (!round_running(state, e)) return;
-  const long P = (n + B - 1) / B;
-  const long start = (long)(e % P) * B;
-  const long end = start + B < n ? start + B : n;
-  const int lane = threadIdx.x & 63;
-  const long gw = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const long W = ((long)gridDim.x * blockDim.x) >> 6;
-  A wsum = 0, lsum = 0;
-  for (long r = start + gw; r < end; r += W) {
-    const long s0 = indptr[r], s1 = indptr[r + 1];
-    A s = 0;
-    for (long j = s0 + lane; j < s1; j += 64) s += val[j] * coef[idx[j]];
-    s = wave_sum(s);
-    const A yy = y[r];
-    const A ww = wt ? wt[r] : (A)1;
-    A l, m;
-    loss_and_mult(loss, s, yy, ww, l, m);
-    wsum += ww;
-    lsum += l;
-    if (m != (A)0)
-      for (long j = s0 + lane; j < s1; j += 64) atomicAdd(&grad[idx[j]], m * val[j]);
-  }
-  if (lane == 0) {
-    atomicAdd(&grad[d], wsum);
-    atomicAdd(&grad[d + 1], lsum);
-  }
-}
-
-template <typename A>
-__global__ void glm_csr_predict_kernel(const long* __restrict__ indptr, const int* __restrict__ idx,
-                                       const A* __restrict__ val, const A* __restrict__ coef, long n,
-                                       double* __restrict__ dots) {
-  const int lane = threadIdx.x & 63;
-  const long gw = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const long W = ((long)gridDim.x * blockDim.x) >> 6;
-  for (long r = gw; r < n; r += W) {
-    A s = 0;
-    for (long j = indptr[r] + lane; j < indptr[r + 1]; j += 64) s += val[j] * coef[idx[j]];
-    s = wave_sum(s);
-    if (lane == 0) dots[r] = (double)s;
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// Sparse (CSR) SGD round without atomics on the gradient
-// ------------------------------------------------------------------------------------------
-// Batches are the fixed row ranges [b·B, min((b+1)·B, n)) (SGD.java:192-206 slicing), so the
-// transpose of every batch can be built once when the trainer starts (ops/glm.py
-// build_batch_csc): per batch, its non-zeros re-sorted by column with the batch-relative row id,
-// at the SAME offsets as the CSR (batch b's non-zeros are CSR positions [indptr[bB], indptr[bB+B])),
-// plus a dense int32 column pointer [P][d+1]. A round is then two launches:
-//   forward  — a G-lane group per row: gathered dot, loss + multiplier m_r (stored, B floats,
-//              L2-resident), Σweight/Σloss into a parity slot of `wl`;
-//   backward — a thread per column: g_c = Σ m_row·val over the column's batch entries (a
-//              segmented gather, no atomics), then either the SGD update + termination check in
-//              place (1 GPU) or the feedback row for the all-reduce (N GPUs).
-// The 1M-wide scatter of atomicAdds it replaces (glm_grad_csr_kernel) was 472 µs per round on the
-// 100k × 64-nnz batch of the sparse LinearSVC config; the reads here are the batch once in each
-// layout plus one column-pointer row.
-template <int G, typename A>
-__device__ __forceinline__ A group_sum(A v) {
-#pragma unroll
-  for (int off = G / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-
-// Forward: K independent (index, value) slots per lane are loaded before any coefficient gather,
-// so a row costs one dependent step (indptr → entries → coef) instead of a chain per element;
-// entries are streamed non-temporally, which keeps the gathered coefficient vector in L2.
-constexpr int WL_SLOTS = 256;  // Σweight/Σloss accumulator: [2 parities][WL_SLOTS][WL_STRIDE]
-constexpr int WL_STRIDE = 32;  // 128 B apart
-
-template <typename A, int G>
-__global__ __launch_bounds__(256) void glm_csr_fwd_kernel(const long* __restrict__ indptr, const int* __restrict__ idx,
-                                                          const A* __restrict__ val, const A* __restrict__ y,
-                                                          const A* __restrict__ wt, const A* __restrict__ coef, long n,
-                                                          long B, int loss, const int* __restrict__ state,
-                                                          A* __restrict__ mult, A* __restrict__ wl) {
-  constexpr int K = G >= 32 ? 2 : 4;
-  int e;
-  if (!round_running(state, e)) return;
-  const long P = (n + B - 1) / B;
-  const long start = (long)(e % P) * B;
-  const long end = start + B < n ? start + B : n;
-  const int lane = threadIdx.x & (G - 1);
-  const long grp = ((long)blockIdx.x * blockDim.x + threadIdx.x) / G;
-  const long NG = ((long)gridDim.x * blockDim.x) / G;
-  A wsum = 0, lsum = 0;
-  for (long r = start + grp; r < end; r += NG) {
-    const long s0 = indptr[r], s1 = indptr[r + 1];
-    A s = 0;
-    for (long jb = s0; jb < s1; jb += K * G) {
-      int ii[K];
-      A vv[K];
-#pragma unroll
-      for (int t = 0; t < K; ++t) {
-        const long j = jb + lane + t * G;
-        const bool ok = j < s1;
-        const long jj = ok ? j : s0;
-        ii[t] = __builtin_nontemporal_load(idx + jj);
-        const A v = __builtin_nontemporal_load(val + jj);
-        vv[t] = ok ? v : (A)0;
-      }
-#pragma unroll
-      for (int t = 0; t < K; ++t) s += vv[t] * coef[ii[t]];
-    }
-    s = group_sum<G>(s);
-    if (lane == 0) {
-      const A ww = wt ? wt[r] : (A)1;
-      A l, m;
-      loss_and_mult(loss, s, y[r], ww, l, m);
-      mult[r - start] = m;
-      wsum += ww;
-      lsum += l;
-    }
-  }
-  __shared__ A red[2][4];
-  wsum = wave_sum(wsum);
-  lsum = wave_sum(lsum);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { red[0][w] = wsum; red[1][w] = lsum; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    A a0 = 0, a1 = 0;
-    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) { a0 += red[0][i]; a1 += red[1][i]; }
-    // one of WL_SLOTS cache lines per block: same-address float atomics from thousands of
-    // blocks serialise at the coherence point (measured: the single-address version cost more
-    // than the row math); the backward sums the slots in a fixed order
-    A* slot = wl + ((long)(e & 1) * WL_SLOTS + (blockIdx.x & (WL_SLOTS - 1))) * WL_STRIDE;
-    if (a0 != (A)0) atomicAdd(&slot[0], a0);
-    if (a1 != (A)0) atomicAdd(&slot[1], a1);
-  }
-}
-
-// Forward over row-block × column-split cells (BatchCsc cells, csc_build.hip cell_keys … cell_store):
-// cell (rb, s) holds the batch's entries of rows [rb·2^CELL_RBB, …) with columns in [s·CS, (s+1)·CS),
-// stored column-sorted and packed (column − s·CS) | pos << cb, pos = the entry's rank in the cell's
-// row-major order; roff[cell·2^CELL_RBB + r] = first entry of row r of the cell. A block takes a
-// cell: its lanes gather coefficients in column order from one slice (consecutive lanes share
-// cache lines — the one-row-per-lane-group kernel gathers a random line per lane, ~40 µs per 6.4M,
-// profiles/r5/micro_gather_*), write each product into LDS slot pos (plain stores: LDS float
-// atomics cost ~27 µs more per round, profiles/r5/svc_cell_forward_ab.jsonl), then every row sums
-// its slots in order and the cell stores its row partials. The last of a row block's S cells to
-// arrive sums the S partials of every row in split order (deterministic), evaluates loss and
-// multiplier, and adds Σweight / Σloss into the slots.
-constexpr int CELL_THREADS = 1024;
-constexpr int CELL_RBB_MAX = 11;  // rows per row block: 2^rbb ≤ 2^11 (two rows per thread)
-constexpr int CELL_U = 8;
-
-template <typename A>
-__global__ __launch_bounds__(CELL_THREADS) void glm_csr_cell_fwd_kernel(
-    const long* __restrict__ indptr, const uint32_t* __restrict__ cent, const A* __restrict__ cval,
-    const int* __restrict__ roff, long rstride, int rbb, int S, int CS, int cb, const A* __restrict__ y,
-    const A* __restrict__ wt, const A* __restrict__ coef, long n, long B, int loss, const int* __restrict__ state,
-    A* __restrict__ mult, A* __restrict__ wl, A* __restrict__ partial, int* __restrict__ cnt, int xcd) {
-  const int RB = 1 << rbb;
-  extern __shared__ __align__(16) unsigned char cell_lds[];
-  A* prod = reinterpret_cast<A*>(cell_lds);  // [the largest cell's entries]
-  __shared__ A red[2][CELL_THREADS / 64];
-  __shared__ int sflag;
-  int e;
-  if (!round_running(state, e)) return;
-  const long P = (n + B - 1) / B;
-  const long b = (long)(e % P);
-  const long start = b * B;
-  const long blen = (start + B < n ? start + B : n) - start;
-  const int nrb = (int)((blen + RB - 1) >> rbb);
-  const int ncell = nrb * S;
-  int rb, sp;
-  if (xcd) {
-    // XCD-aware order: block b runs on XCD b mod 8 (round-robin dispatch); give XCD x the cells
-    // of a contiguous split-major range, so its L2 holds the coefficient slices of ≤ 2 splits
-    // (a bijection of [0, grid): XCD x holds the n_x = ⌈(grid − x) / 8⌉ blocks b ≡ x mod 8, so it
-    // starts at Σ_{y<x} n_y = x·⌊grid/8⌋ + min(x, grid mod 8))
-    const int x = (int)(blockIdx.x & 7), q = (int)(gridDim.x >> 3), r = (int)(gridDim.x & 7);
-    const int g = x * q + (x < r ? x : r) + (int)(blockIdx.x >> 3);
-    if (g >= ncell) return;
-    sp = g / nrb;
-    rb = g - sp * nrb;
-  } else {
-    if ((int)blockIdx.x >= ncell) return;  // (the grid covers the largest batch)
-    rb = blockIdx.x / S;
-    sp = blockIdx.x - rb * S;
-  }
-  const int c = rb * S + sp;
-  const int tid = threadIdx.x;
-  const long base = indptr[start];
-  const int* __restrict__ ro = roff + b * rstride + ((long)c << rbb);
-  const int k0 = ro[0], k1 = ro[RB];
-  const uint32_t* __restrict__ en = cent + base;
-  const A* __restrict__ ev = cval + base;
-  const A* __restrict__ cs = coef + (long)sp * CS;
-  const uint32_t cmask = (1u << cb) - 1;
-  uint32_t xx[CELL_U];
-  A vv[CELL_U];
-  if (k0 < k1) {  // (an empty cell may sit at the end of the array: nothing to load)
-#pragma unroll
-    for (int u = 0; u < CELL_U; ++u) {
-      const int k = k0 + tid + u * CELL_THREADS;
-      const int kk = k < k1 ? k : k0;
-      xx[u] = __builtin_nontemporal_load(en + kk);
-      vv[u] = __builtin_nontemporal_load(ev + kk);
-    }
-  }
-  for (int kb = k0 + tid; kb < k1; kb += CELL_U * CELL_THREADS) {
-    uint32_t nx[CELL_U];
-    A nv[CELL_U];
-    const int kn = kb + CELL_U * CELL_THREADS;
-    if (kn < k1) {
-#pragma unroll
-      for (int u = 0; u < CELL_U; ++u) {
-        const int k = kn + u * CELL_THREADS;
-        const int kk = k < k1 ? k : kn;
-        nx[u] = __builtin_nontemporal_load(en + kk);
-        nv[u] = __builtin_nontemporal_load(ev + kk);
-      }
-    }
-    // every gather first (lanes past the cell hold its first entry: valid addresses), then the
-    // slot stores — a gather per store would serialise CELL_U memory latencies per step
-    A pp[CELL_U];
-#pragma unroll
-    for (int u = 0; u < CELL_U; ++u) pp[u] = vv[u] * cs[xx[u] & cmask];
-#pragma unroll
-    for (int u = 0; u < CELL_U; ++u)
-      if (kb + u * CELL_THREADS < k1) prod[xx[u] >> cb] = pp[u];
-#pragma unroll
-    for (int u = 0; u < CELL_U; ++u) {
-      xx[u] = nx[u];
-      vv[u] = nv[u];
-    }
-  }
-  const long rb0 = (long)rb << rbb;
-  const int nr = blen - rb0 < RB ? (int)(blen - rb0) : RB;
-  constexpr int RQ = (1 << CELL_RBB_MAX) / CELL_THREADS;
-  int r0s[RQ], r1s[RQ];
-#pragma unroll
-  for (int q = 0; q < RQ; ++q) {  // (row offsets loaded before the barrier)
-    const int r = tid + q * CELL_THREADS;
-    r0s[q] = r < nr ? ro[r] - k0 : 0;
-    r1s[q] = r < nr ? ro[r + 1] - k0 : 0;
-  }
-  __syncthreads();
-  A* __restrict__ mine = partial + (long)c * RB;
-#pragma unroll
-  for (int q = 0; q < RQ; ++q) {
-    const int r = tid + q * CELL_THREADS;
-    A t = 0;
-    for (int j = r0s[q]; j < r1s[q]; ++j) t += prod[j];
-    if (r < nr) st_agent(mine + r, t);
-  }
-  if (!arrive_last(&cnt[rb], S, &sflag)) return;
-  if (tid == 0) st_agent(&cnt[rb], 0);  // every arrival of this launch is in: re-arm for the next
-  A ws = 0, ls = 0;
-  for (int r = tid; r < nr; r += CELL_THREADS) {
-    A dot = 0;
-    for (int q = 0; q < S; ++q) dot += ld_agent(partial + ((long)rb * S + q) * RB + r);
-    const long gr = start + rb0 + r;
-    const A ww = wt ? wt[gr] : (A)1;
-    A l, m;
-    loss_and_mult(loss, dot, y[gr], ww, l, m);
-    mult[rb0 + r] = m;
-    ws += ww;
-    ls += l;
-  }
-  ws = wave_sum(ws);
-  ls = wave_sum(ls);
-  if ((tid & 63) == 0) {
-    red[0][tid >> 6] = ws;
-    red[1][tid >> 6] = ls;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    A a0 = 0, a1 = 0;
-    for (int i = 0; i < CELL_THREADS / 64; ++i) {
-      a0 += red[0][i];
-      a1 += red[1][i];
-    }
-    A* slot = wl + ((long)(e & 1) * WL_SLOTS + (rb & (WL_SLOTS - 1))) * WL_STRIDE;
-    if (a0 != (A)0) atomicAdd(&slot[0], a0);
-    if (a1 != (A)0) atomicAdd(&slot[1], a1);
-  }
-}
-
-// Backward: a block owns 256 consecutive columns, whose batch entries are one contiguous CSC
-// range. The block walks that range coalesced (every thread loads independent entries: row id →
-// multiplier gather → product into LDS), then each thread adds its column's slice of the LDS
-// products in entry order — deterministic, no atomics, no per-column dependent load chains.
-constexpr int CSC_CAP = 4096;  // entries staged per pass (16 KB fp32 / 32 KB fp64)
-
-// Σweight / Σloss of round e: fixed-order sum of the forward's WL_SLOTS slots (all 256 threads)
-template <typename A>
-__device__ __forceinline__ void slot_sums(const A* __restrict__ wl, int e, A& W, A& L) {
-  __shared__ A red[2][4];
-  const bool own = threadIdx.x < WL_SLOTS;  // (blocks of ≥ 256 threads)
-  const A* sl = wl + ((long)(e & 1) * WL_SLOTS + (own ? threadIdx.x : 0)) * WL_STRIDE;
-  const A w0 = wave_sum(own ? sl[0] : (A)0), l0 = wave_sum(own ? sl[1] : (A)0);
-  if ((threadIdx.x & 63) == 0 && own) { red[0][threadIdx.x >> 6] = w0; red[1][threadIdx.x >> 6] = l0; }
-  __syncthreads();
-  W = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-  L = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
-}
-
-template <typename A, bool FUSE>
-__global__ __launch_bounds__(256) void glm_csc_bwd_kernel(const long* __restrict__ indptr,
-                                                          const int* __restrict__ colptr, const int* __restrict__ erow,
-                                                          const A* __restrict__ eval, const A* __restrict__ mult,
-                                                          long n, int d, long B, int* __restrict__ state,
-                                                          A* __restrict__ wl, A* __restrict__ fb, A* __restrict__ coef,
-                                                          int max_iter, A tol, A lr, A reg, A en, int weighted) {
-  __shared__ A prod[CSC_CAP];
-  int e;
-  const bool run = round_running(state, e);
-  // re-arm the other parity's slots (they held the previous round's sums, consumed by now)
-  if (blockIdx.x == 0) {
-    A* o = wl + ((long)((e + 1) & 1) * WL_SLOTS + threadIdx.x) * WL_STRIDE;
-    o[0] = 0;
-    o[1] = 0;
-  }
-  if (!run) {
-    if (FUSE) arrive_and_advance(state, e, false, 0);
-    return;
-  }
-  const long P = (n + B - 1) / B;
-  const long b = (long)(e % P);
-  const long base = indptr[b * B];
-  const int* __restrict__ cp = colptr + b * (long)(d + 1);
-  const int* __restrict__ er = erow + base;
-  const A* __restrict__ ev = eval + base;
-  // Σweight of the round: the batch's row count when unweighted, else the fixed-order sum of the
-  // forward's slots (identical in every block). Σloss only feeds the termination test, which the
-  // last arriving block makes (and block 0 of the feedback path, which exports it).
-  A W, L = 0;
-  if (weighted || (!FUSE && blockIdx.x == 0)) {
-    slot_sums(wl, e, W, L);
-  }
-  if (!weighted) {
-    const long end = (b + 1) * B < n ? (b + 1) * B : n;
-    W = (A)(end - b * B);
-  }
-  for (int cb = blockIdx.x * 256; cb < d; cb += gridDim.x * 256) {
-    const int c = cb + (int)threadIdx.x;
-    const int ce = cb + 256 < d ? cb + 256 : d;
-    const int lo = cp[cb], hi = cp[ce];
-    const int j0 = c < d ? cp[c] : hi, j1 = c < d ? cp[c + 1] : hi;
-    A g = 0;
-    for (int pb = lo; pb < hi; pb += CSC_CAP) {
-      const int top = pb + CSC_CAP < hi ? pb + CSC_CAP : hi;
-      for (int k0 = pb + (int)threadIdx.x; k0 < top; k0 += 4 * 256) {
-        int rr[4];
-        A vv[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int k = k0 + t * 256;
-          const int kk = k < top ? k : k0;
-          rr[t] = __builtin_nontemporal_load(er + kk);
-          vv[t] = __builtin_nontemporal_load(ev + kk);
-        }
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int k = k0 + t * 256;
-          const A p = mult[rr[t]] * vv[t];
-          if (k < top) prod[k - pb] = p;
-        }
-      }
-      __syncthreads();
-      const int a = j0 > pb ? j0 : pb, z = j1 < top ? j1 : top;
-      for (int j = a; j < z; ++j) g += prod[j - pb];
-      __syncthreads();
-    }
-    if (c < d) {
-      if (FUSE)
-        coef[c] = sgd_apply<A>(coef[c], g, W, lr, reg, en);
-      else
-        fb[c] = g;
-    }
-  }
-  if (!FUSE && blockIdx.x == 0 && threadIdx.x == 0) {
-    fb[d] = W;
-    fb[d + 1] = L;
-  }
-  if (FUSE) {
-    __shared__ int last;
-    __syncthreads();
-    if (threadIdx.x == 0)
-      last = __hip_atomic_fetch_add(&state[ST_ARRIVE], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-             (int)gridDim.x - 1;
-    __syncthreads();
-    if (last) {  // every other block has finished its reads of the state words (see arrive_and_advance)
-      A w2;
-      slot_sums(wl, e, w2, L);
-      if (threadIdx.x == 0) {
-        const bool cont = (e + 1 < max_iter) && (L / W > tol);
-        state[ST_RUN0 + ((e + 1) & 1)] = cont ? 1 : 0;
-        state[ST_EXECUTED] += 1;
-        state[ST_ROUND] = e + 1;
-        state[ST_ARRIVE] = 0;
-      }
-    }
-  }
-}
-
-// Tiled backward (BatchCsc tiles, csc_build.hip csc_tiles / csc_tile_keys / csc_tile_store): the
-// batch's columns are cut into tiles of ≤ ET entries (or one heavy column of > EL), and inside a light
-// tile the entries are sorted by ROW, each carrying its slot in the tile's column-ordered range
-// (erow = row | slot << rb). A block takes a tile: the multiplier gathers of consecutive lanes
-// then fall on the same or nearby cache lines (the one-column-block form gathers a random row per
-// lane: measured ~40 µs for 6.4M such 4-byte gathers, the cost scaling with distinct lines per
-// wave instruction), each product goes to its column-ordered LDS slot, and a thread per column
-// sums its slots in entry order — the same per-column order as the untiled kernel, so results
-// are deterministic. A heavy column is a block-strided sum with a fixed-order block reduction.
-constexpr int TILE_THREADS = 1024;
-constexpr int TILE_U = 8;     // entries per thread per gather step
-constexpr int TILE_COLS = 8;  // columns per thread whose pointers are prefetched
-
-template <typename A, bool FUSE>
-__global__ __launch_bounds__(TILE_THREADS) void glm_csc_tile_bwd_kernel(
-    const long* __restrict__ indptr, const int* __restrict__ colptr, const int2* __restrict__ tiles,
-    const int* __restrict__ ntiles, int tstride, const int* __restrict__ erow, const A* __restrict__ eval,
-    const A* __restrict__ mult, long n, int d, long B, int rb, int EL, int* __restrict__ state, A* __restrict__ wl,
-    A* __restrict__ fb, A* __restrict__ coef, int max_iter, A tol, A lr, A reg, A en, int weighted,
-    long long* __restrict__ trace) {
-  extern __shared__ unsigned char tile_smem[];
-  if (trace && threadIdx.x == 0) trace[(long)blockIdx.x * 4] = (long long)__builtin_amdgcn_s_memrealtime();
-  A* prod = reinterpret_cast<A*>(tile_smem);
-  __shared__ A hred[TILE_THREADS / 64];
-  int e;
-  const bool run = round_running(state, e);
-  if (blockIdx.x == 0 && threadIdx.x < WL_SLOTS) {
-    A* o = wl + ((long)((e + 1) & 1) * WL_SLOTS + threadIdx.x) * WL_STRIDE;
-    o[0] = 0;
-    o[1] = 0;
-  }
-  if (!run) {
-    if (FUSE) arrive_and_advance(state, e, false, 0);
-    return;
-  }
-  const long P = (n + B - 1) / B;
-  const long b = (long)(e % P);
-  const long base = indptr[b * B];
-  const int* __restrict__ cp = colptr + b * (long)(d + 1);
-  const int2* __restrict__ tl = tiles + b * (long)tstride;
-  const int nt = ntiles[b];
-  const int* __restrict__ er = erow + base;
-  const A* __restrict__ ev = eval + base;
-  const uint32_t rmask = (1u << rb) - 1;
-  A W, L = 0;
-  if (weighted || (!FUSE && blockIdx.x == 0)) slot_sums(wl, e, W, L);
-  if (!weighted) {
-    const long end = (b + 1) * B < n ? (b + 1) * B : n;
-    W = (A)(end - b * B);
-  }
-  const int tid = threadIdx.x;
-  for (int t = blockIdx.x; t < nt; t += gridDim.x) {
-    const int2 ta = tl[t], tz = tl[t + 1];  // (start column, first entry) of this and the next tile
-    const int c0 = ta.x, c1 = tz.x, k0 = ta.y, k1 = tz.y;
-    if (c1 - c0 == 1 && k1 - k0 > EL) {  // heavy column (block-uniform branch)
-      A g = 0;
-      for (int k = k0 + tid; k < k1; k += TILE_THREADS) {
-        const uint32_t x = (uint32_t)__builtin_nontemporal_load(er + k);
-        g += mult[x & rmask] * __builtin_nontemporal_load(ev + k);
-      }
-      g = wave_sum(g);
-      if ((tid & 63) == 0) hred[tid >> 6] = g;
-      __syncthreads();
-      if (tid == 0) {
-        A s = 0;
-        for (int i = 0; i < TILE_THREADS / 64; ++i) s += hred[i];
-        if (FUSE)
-          coef[c0] = sgd_apply<A>(coef[c0], s, W, lr, reg, en);
-        else
-          fb[c0] = s;
-      }
-      __syncthreads();
-      continue;
-    }
-    // the thread's columns of the tile (c0 + tid + i·TILE_THREADS, i < TILE_COLS): pointers and
-    // coefficients loaded before the gathers, so the column pass after the barrier reads only LDS
-    const bool few = c1 - c0 <= TILE_COLS * TILE_THREADS;  // (block-uniform)
-    int ca[TILE_COLS], cz[TILE_COLS];
-    A cw[TILE_COLS];
-    if (few) {
-#pragma unroll
-      for (int i = 0; i < TILE_COLS; ++i) {
-        const int c = c0 + tid + i * TILE_THREADS;
-        const int cc = c < c1 ? c : c0;
-        ca[i] = cp[cc];
-        cz[i] = c < c1 ? cp[cc + 1] : ca[i];
-        cw[i] = FUSE ? coef[cc] : (A)0;
-      }
-    }
-    constexpr int TU = sizeof(A) == 8 ? TILE_U / 2 : TILE_U;
-    // products into their column-ordered slots: TU entries per thread per step (8; 4 for fp64,
-    // which spilled at 8 under the 1024-thread register budget), the next
-    // step's entries loaded before this step's multiplier gathers (measured against one step of
-    // 32 per thread: 71.0 vs 72.3 µs per round; 8 without the overlap: 71.8)
-    uint32_t xx[TU];
-    A vv[TU];
-    if (k0 < k1) {  // (an empty tile may sit at the end of the array: nothing to load)
-#pragma unroll
-      for (int u = 0; u < TU; ++u) {
-        const int k = k0 + tid + u * TILE_THREADS;
-        const int kk = k < k1 ? k : k0;
-        xx[u] = (uint32_t)__builtin_nontemporal_load(er + kk);
-        vv[u] = __builtin_nontemporal_load(ev + kk);
-      }
-    }
-    for (int kb = k0 + tid; kb < k1; kb += TU * TILE_THREADS) {
-      uint32_t nx[TU];
-      A nv[TU];
-      const int kn = kb + TU * TILE_THREADS;
-      if (kn < k1) {
-#pragma unroll
-        for (int u = 0; u < TU; ++u) {
-          const int k = kn + u * TILE_THREADS;
-          const int kk = k < k1 ? k : kn;
-          nx[u] = (uint32_t)__builtin_nontemporal_load(er + kk);
-          nv[u] = __builtin_nontemporal_load(ev + kk);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < TU; ++u) {
-        const A p = mult[xx[u] & rmask] * vv[u];
-        if (kb + u * TILE_THREADS < k1) prod[xx[u] >> rb] = p;
-      }
-#pragma unroll
-      for (int u = 0; u < TU; ++u) {
-        xx[u] = nx[u];
-        vv[u] = nv[u];
-      }
-    }
-    if (trace && tid == 0) trace[(long)blockIdx.x * 4 + 1] = (long long)__builtin_amdgcn_s_memrealtime();
-    __syncthreads();
-    if (trace && tid == 0) trace[(long)blockIdx.x * 4 + 2] = (long long)__builtin_amdgcn_s_memrealtime();
-    if (few) {
-#pragma unroll
-      for (int i = 0; i < TILE_COLS; ++i) {
-        const int c = c0 + tid + i * TILE_THREADS;
-        A g = 0;
-        for (int j = ca[i] - k0; j < cz[i] - k0; ++j) g += prod[j];
-        if (c < c1) {
-          if (FUSE)
-            coef[c] = sgd_apply<A>(cw[i], g, W, lr, reg, en);
-          else
-            fb[c] = g;
-        }
-      }
-    } else {
-      for (int c = c0 + tid; c < c1; c += TILE_THREADS) {
-        const int a = cp[c] - k0, z = cp[c + 1] - k0;
-        A g = 0;
-        for (int j = a; j < z; ++j) g += prod[j];
-        if (FUSE)
-          coef[c] = sgd_apply<A>(coef[c], g, W, lr, reg, en);
-        else
-          fb[c] = g;
-      }
-    }
-    __syncthreads();
-  }
-  if (!FUSE && blockIdx.x == 0 && tid == 0) {
-    fb[d] = W;
-    fb[d + 1] = L;
-  }
-  if (trace && tid == 0) trace[(long)blockIdx.x * 4 + 3] = (long long)__builtin_amdgcn_s_memrealtime();
-  if (FUSE) {
-    __shared__ int last;
-    __syncthreads();
-    if (tid == 0)
-      last = __hip_atomic_fetch_add(&state[ST_ARRIVE], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-             (int)gridDim.x - 1;
-    __syncthreads();
-    if (last) {
-      A w2;
-      slot_sums(wl, e, w2, L);
-      if (tid == 0) {
-        const bool cont = (e + 1 < max_iter) && (L / W > tol);
-        state[ST_RUN0 + ((e + 1) & 1)] = cont ? 1 : 0;
-        state[ST_EXECUTED] += 1;
-        state[ST_ROUND] = e + 1;
-        state[ST_ARRIVE] = 0;
       }
     }
   }
@@ -1961,8 +1243,6 @@ static int g_nt = -1;
 static int g_acc_reps = 4;  // atomic-tail accumulator replicas (A/B knob, <= ACC_MAX_REPS)
 static int g_ticket2 = 0;   // two-level tickets (A/B knob)
 static long long* g_trace = nullptr;  // per-block timestamps of the next launches (diagnostics)
-constexpr long LDS_PER_CU = 160 * 1024;
-constexpr int NUM_CU = 256;
 
 static int g_dma_depth = 0;  // LDS-DMA row ring depth in steps (0 = 16-byte register loads)
 
@@ -2137,7 +1417,10 @@ FMLX_API int fmlx_glm_set_tuning(long lds_pad, int nt) {
 }
 
 // diagnostics: launches record per-block timestamps into trace[nblocks][4] (null: off)
-FMLX_API void fmlx_glm_set_trace(void* trace) { g_trace = (long long*)trace; }
+FMLX_API void fmlx_glm_set_trace(void* trace) {
+  g_trace = (long long*)trace;
+  fmlx_glm_sparse_set_trace(trace);
+}
 
 // ints of the fused round's counter block: the arrival tickets (TAIL_TOP + 1, padded to 128)
 FMLX_API int fmlx_glm_cnt_elems() { return 128; }
@@ -2351,169 +1634,6 @@ FMLX_API int fmlx_glm_predict(int dtype, int epc, int cpl, const void* X, long l
   return -1;
 }
 
-FMLX_API int fmlx_glm_grad_csr(int acc_f64, const long* indptr, const int* idx, const void* val, const void* y,
-                               const void* wt, const void* coef, long n, int d, long B, int loss, const int* state,
-                               void* grad, void* stream) {
-  hipStream_t s = (hipStream_t)stream;
-  long waves = B < n ? B : n;
-  int blocks = (int)((waves + 3) / 4);
-  if (blocks > 2048) blocks = 2048;
-  if (blocks < 1) blocks = 1;
-  if (acc_f64)
-    hipLaunchKernelGGL(glm_grad_csr_kernel<double>, dim3(blocks), dim3(256), 0, s, indptr, idx, (const double*)val,
-                       (const double*)y, (const double*)wt, (const double*)coef, n, d, B, loss, state, (double*)grad);
-  else
-    hipLaunchKernelGGL(glm_grad_csr_kernel<float>, dim3(blocks), dim3(256), 0, s, indptr, idx, (const float*)val,
-                       (const float*)y, (const float*)wt, (const float*)coef, n, d, B, loss, state, (float*)grad);
-  return (int)hipGetLastError();
-}
-
-static int g_csc_fwd_cap = 65535, g_csc_bwd_cap = 1024, g_csc_tile_cap = 0;  // 0: CUs × tile blocks per CU
-
-FMLX_API void fmlx_glm_set_csc_tuning(int fwd_cap, int bwd_cap) {
-  g_csc_fwd_cap = fwd_cap > 0 ? fwd_cap : 65535;
-  g_csc_bwd_cap = bwd_cap > 0 ? bwd_cap : 1024;
-  g_csc_tile_cap = bwd_cap > 0 ? bwd_cap : 0;
-}
-
-// tiled backward: the column tiles of the batches (BatchCsc.tiles) and the packing of erow
-// forward cells in XCD-aware order (default; fmlx_glm_set_cell_xcd(0): launch order) — 63.5 → 61.4 µs
-// per SVC round, profiles/r5/svc_cell_forward_ab.jsonl
-static int g_cell_xcd = 1;
-struct CscTiles {
-  const int2* tiles;  // [P][tstride] (start column, first entry) per tile (nullptr: untiled layout)
-  const int* ntiles;  // int32 [P]
-  int tstride, rb, EL, ET;  // EL: heavy-column threshold (entries)
-  // row-block × column-split cells of the forward (cent == nullptr: the one-row-per-group forward)
-  const uint32_t* cent;
-  const void* cval;
-  const int* roff;  // [P][rstride] first entry of every (cell, row): cell·2^CELL_RBB + row
-  int rstride, rbb, S, CS, cb, cells;  // cells: grid (cells of the largest batch); rows per block 2^rbb
-  int cmax;         // entries of the largest cell (its LDS slots)
-  void* partial;    // [cells][2^CELL_RBB] row partials
-  int* cnt;         // [row blocks] arrival tickets (zeroed once, re-armed by the finishers)
-};
-FMLX_API int fmlx_glm_wl_elems() { return 2 * WL_SLOTS * WL_STRIDE; }
-
-template <typename A, int G>
-static void launch_csc_round(const long* indptr, const int* idx, const A* val, const A* y, const A* wt, A* coef,
-                             long n, int d, long B, int loss, int* state, A* mult, A* wl, const int* colptr,
-                             const int* erow, const A* eval, A* fb, int fuse, int max_iter, A tol, A lr, A reg, A en,
-                             const CscTiles& ti, hipStream_t s) {
-  if (ti.cent != nullptr) {
-    hipLaunchKernelGGL(glm_csr_cell_fwd_kernel<A>, dim3(ti.cells), dim3(CELL_THREADS), (size_t)ti.cmax * sizeof(A),
-                       s, indptr, ti.cent, (const A*)ti.cval, ti.roff, (long)ti.rstride, ti.rbb, ti.S, ti.CS, ti.cb, y, wt,
-                       (const A*)coef, n, B, loss, state, mult, wl, (A*)ti.partial, ti.cnt, g_cell_xcd);
-  } else {
-    const long groups = B < n ? B : n;
-    long fb_blocks = (groups * G + 255) / 256;  // one row per lane group: the batch in one pass
-    if (fb_blocks > g_csc_fwd_cap) fb_blocks = g_csc_fwd_cap;
-    if (fb_blocks < 1) fb_blocks = 1;
-    hipLaunchKernelGGL((glm_csr_fwd_kernel<A, G>), dim3((int)fb_blocks), dim3(256), 0, s, indptr, idx, val, y, wt,
-                       (const A*)coef, n, B, loss, state, mult, wl);
-  }
-  const int weighted = wt != nullptr;
-  if (ti.tiles != nullptr) {
-    const size_t lds = (size_t)ti.ET * sizeof(A);
-    int per_cu = (int)(LDS_PER_CU / (lds + 2048));
-    per_cu = per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu);  // ≤ 32 waves per CU at 1024 threads
-    int tb = g_csc_tile_cap > 0 ? g_csc_tile_cap : NUM_CU * per_cu;
-    if (tb > ti.tstride) tb = ti.tstride;
-#define FMLX_TILE_BWD(F)                                                                                             \
-  hipLaunchKernelGGL((glm_csc_tile_bwd_kernel<A, F>), dim3(tb), dim3(TILE_THREADS), lds, s, indptr, colptr, ti.tiles, \
-                     ti.ntiles, ti.tstride, erow, eval, (const A*)mult, n, d, B, ti.rb, ti.EL, state, wl, fb, coef,    \
-                     max_iter, tol, lr, reg, en, weighted, g_trace)
-    if (fuse)
-      FMLX_TILE_BWD(true);
-    else
-      FMLX_TILE_BWD(false);
-#undef FMLX_TILE_BWD
-    return;
-  }
-  int bb = (d + 255) / 256;  // grid-strided: each block takes the arrival ticket once
-  if (bb > g_csc_bwd_cap) bb = g_csc_bwd_cap;
-  if (fuse)
-    hipLaunchKernelGGL((glm_csc_bwd_kernel<A, true>), dim3(bb), dim3(256), 0, s, indptr, colptr, erow, eval,
-                       (const A*)mult, n, d, B, state, wl, fb, coef, max_iter, tol, lr, reg, en, weighted);
-  else
-    hipLaunchKernelGGL((glm_csc_bwd_kernel<A, false>), dim3(bb), dim3(256), 0, s, indptr, colptr, erow, eval,
-                       (const A*)mult, n, d, B, state, wl, fb, coef, max_iter, tol, lr, reg, en, weighted);
-}
-
-template <typename A>
-static int dispatch_csc_round(int G, const long* indptr, const int* idx, const void* val, const void* y,
-                              const void* wt, void* coef, long n, int d, long B, int loss, int* state, void* mult,
-                              void* wl, const int* colptr, const int* erow, const void* eval, void* fb, int fuse,
-                              int max_iter, double tol, double lr, double reg, double en, const CscTiles& ti,
-                              hipStream_t s) {
-#define FMLX_CSC(GG)                                                                                                 \
-  launch_csc_round<A, GG>(indptr, idx, (const A*)val, (const A*)y, (const A*)wt, (A*)coef, n, d, B, loss, state,     \
-                          (A*)mult, (A*)wl, colptr, erow, (const A*)eval, (A*)fb, fuse, max_iter, (A)tol, (A)lr,     \
-                          (A)reg, (A)en, ti, s)
-  switch (G) {
-    case 4: FMLX_CSC(4); break;
-    case 8: FMLX_CSC(8); break;
-    case 16: FMLX_CSC(16); break;
-    case 32: FMLX_CSC(32); break;
-    case 64: FMLX_CSC(64); break;
-    default: return -1;
-  }
-#undef FMLX_CSC
-  return (int)hipGetLastError();
-}
-
-// One sparse SGD round through the per-batch transpose (see glm_csc_bwd_kernel). fuse=1: the
-// backward applies the update + termination (1 GPU); fuse=0: it writes fb[d+2] for the
-// all-reduce and fmlx_glm_update follows.
-FMLX_API void fmlx_glm_set_cell_xcd(int on) { g_cell_xcd = on != 0; }
-
-FMLX_API int fmlx_glm_csc_round(int acc_f64, int G, const long* indptr, const int* idx, const void* val,
-                                const void* y, const void* wt, void* coef, long n, int d, long B, int loss, int* state,
-                                void* mult, void* wl, const int* colptr, const int* erow, const void* eval, void* fb,
-                                int fuse, int max_iter, double tol, double lr, double reg, double en,
-                                const int* tiles, const int* ntiles, int tstride, int rb, int EL, int ET,
-                                const uint32_t* cent, const void* cval, const int* roff, int rstride, int rbb, int S,
-                                int CS, int cb, int cells, int cmax, void* partial, int* ccnt, void* stream) {
-  hipStream_t s = (hipStream_t)stream;
-  if (n <= 0 || B <= 0) return -2;
-  const CscTiles ti{reinterpret_cast<const int2*>(tiles), ntiles, tstride, rb, EL, ET, cent, cval, roff, rstride,
-                    rbb, S, CS, cb, cells, cmax, partial, ccnt};
-  if (cent != nullptr) {
-    // (cell ids, packed entries and the row blocks of the largest batch: host-checked sizes)
-    const long lds = (long)cmax * (acc_f64 ? 8 : 4);
-    if (cval == nullptr || roff == nullptr || partial == nullptr || ccnt == nullptr || S < 1 || CS < 1 || cb < 1 ||
-        cb >= 32 || rbb < 1 || rbb > CELL_RBB_MAX || cells < 1 || (long)rstride < ((long)cells << rbb) + 1 ||
-        (long)CS * S < d || cmax < 0 ||
-        cmax > (int)(1u << (32 - cb)) || lds > 150 * 1024)
-      return -5;
-  }
-  if (tiles != nullptr) {
-    const size_t esz = acc_f64 ? 8 : 4;
-    // the packed erow (row | slot << rb) and the LDS slot array of a light tile (< ET entries)
-    if (rb < 1 || ET < 2 || EL < 1 || EL >= ET || tstride < 2 || (size_t)ET * esz > (size_t)LDS_PER_CU - 1024) return -3;
-    if (((long)ET - 1) >> (32 - rb) != 0 || (B - 1) >> rb != 0) return -4;
-  }
-  if (acc_f64)
-    return dispatch_csc_round<double>(G, indptr, idx, val, y, wt, coef, n, d, B, loss, state, mult, wl, colptr, erow,
-                                      eval, fb, fuse, max_iter, tol, lr, reg, en, ti, s);
-  return dispatch_csc_round<float>(G, indptr, idx, val, y, wt, coef, n, d, B, loss, state, mult, wl, colptr, erow,
-                                   eval, fb, fuse, max_iter, tol, lr, reg, en, ti, s);
-}
-
-FMLX_API int fmlx_glm_csr_predict(int acc_f64, const long* indptr, const int* idx, const void* val, const void* coef,
-                                  long n, double* dots, void* stream) {
-  hipStream_t s = (hipStream_t)stream;
-  if (n == 0) return 0;
-  int blocks = (int)((n + 3) / 4);
-  if (blocks > 4096) blocks = 4096;
-  if (acc_f64)
-    hipLaunchKernelGGL(glm_csr_predict_kernel<double>, dim3(blocks), dim3(256), 0, s, indptr, idx, (const double*)val,
-                       (const double*)coef, n, dots);
-  else
-    hipLaunchKernelGGL(glm_csr_predict_kernel<float>, dim3(blocks), dim3(256), 0, s, indptr, idx, (const float*)val,
-                       (const float*)coef, n, dots);
-  return (int)hipGetLastError();
-}
 #endif  // FMLX_ISA_PROBE
 
 FMLX_DEFINE_PRELOAD()

@@ -10,6 +10,7 @@ import os
 import weakref
 from typing import Optional, Tuple
 
+import numpy as np
 import torch
 
 from . import native
@@ -77,7 +78,7 @@ def set_dma(depth: int) -> None:
 def set_trace(buf: Optional[torch.Tensor]) -> None:
     """Diagnostics: fused-round launches write per-block {start, rows done, atomics drained, hw
     id} s_memrealtime stamps (100 MHz) into ``buf`` (int64 [blocks, 4]); None switches off."""
-    native.call("fmlx_glm_set_trace", native.ptr(buf))
+    native.kernels().fmlx_glm_set_trace(native.ptr(buf))
 
 
 def pick_layout(X: torch.Tensor, rounds: bool = True) -> Optional[Tuple[int, int]]:
@@ -391,6 +392,9 @@ TILE_HEAVY_DIV = int(os.environ.get("FMLX_CSC_TILE_HEAVY_DIV", "8"))  # heavy co
 # a fit tiles its batches when it visits each at least this often (the tiling costs about as much
 # as TILE_MIN_VISITS rounds save: ~0.15 ms per 6.4M-entry batch vs ~13 µs per round, svc shape)
 TILE_MIN_VISITS = int(os.environ.get("FMLX_CSC_TILE_MIN_VISITS", "16"))
+# fits visiting each batch fewer than TILE_MIN_VISITS times take the single-visit bucket round
+# (BucketRound) instead of any per-batch transpose; BUCKETS = False: the transposed rounds (tests)
+BUCKETS = True
 TILE_SPREAD = os.environ.get("FMLX_CSC_TILE_SPREAD", "1") == "1"  # tile size from the batch and CU count
 # the forward over row-block × column-split cells (glm.hip glm_csr_cell_fwd_kernel): float atomics
 # in LDS, so off under FMLX_DETERMINISTIC=1 (the one-row-per-lane-group forward is bit-stable)
@@ -830,6 +834,79 @@ def csc_round(csc: BatchCsc, indptr, idx, val, y, wt, coef, n, d, B, loss, state
                 csc.tstride, csc.rb, csc.EL, csc.ET, native.ptr(csc.cent), native.ptr(csc.cval), native.ptr(csc.roff),
                 csc.rstride, csc.rbb, getattr(csc, "S", 0), getattr(csc, "CS", 0), getattr(csc, "cb", 0), csc.cells, csc.cmax,
                 native.ptr(csc.cpart), native.ptr(csc.ccnt), native.stream_ptr(val.device))
+
+
+class BucketRound:
+    """Device buffers of the single-visit sparse round (csrc/glm_sparse.hip glm_bkt_*): per round,
+    the batch's entries are counted per column slice of 2^csb columns, written by the forward into
+    their slice's bucket as (column in slice, m_row·x) and summed per slice in LDS by the backward —
+    nothing is precomputed per batch, so a fit that visits each batch once (the reference's
+    LinearSVC benchmark: SGD.java:263-268 over 100k-row batches) pays no transpose. Buffers: the
+    largest batch's entries (2 + value bytes each), a [d] accumulator for slices summed in several
+    chunks, and O(#slices) counters."""
+
+    CHUNK = 32768  # backward entries per work item (a slice of more is summed in chunks)
+
+    def __init__(self, indptr, values, n: int, d: int, B: int, G: int):
+        lim = np.zeros(3, dtype=np.int32)
+        native.kernels().fmlx_glm_bkt_limits(lim.ctypes.data)
+        nt, _ecap, nb_max = (int(v) for v in lim)
+        dev = values.device
+        es = values.element_size()
+        self.G = G
+        self.d = d
+        # ~256 slices (the backward's parallelism), at most nb_max, slab ≤ 64 KiB of LDS
+        csb = max(6, int(math.ceil(math.log2(max(1.0, d / 256.0)))))
+        csb = min(csb, 14 if es == 4 else 13)
+        self.csb = csb
+        self.nb = -(-d // (1 << csb))
+        if self.nb > nb_max:
+            raise ValueError("too many column slices")
+        nnz, bounds = _batch_bounds(indptr, n, B)
+        most = max(bounds[i + 1] - bounds[i] for i in range(len(bounds) - 1))
+        avg = nnz / max(1, n)
+        # forward rows per block: ~16k entries (4 pieces) — fewer blocks, fewer cursor atomics
+        rb = 1
+        while rb * 2 * max(avg, 1.0) <= 16384 and rb < 2048:
+            rb *= 2
+        self.rb = max(nt // G, rb)
+        self.chunk = self.CHUNK
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        self.bwd_blocks = max(1, min(2 * cus, self.nb + -(-most // self.chunk)))
+        i32 = dict(dtype=torch.int32, device=dev)
+        z = native.zeros((2 * self.nb + 2,), torch.int32, dev)
+        self.cnt, self.done, self.tick = z[:self.nb], z[self.nb:2 * self.nb], z[2 * self.nb:]
+        self.off = torch.empty(self.nb + 1, **i32)
+        self.cur = torch.empty(self.nb, **i32)
+        self.key = torch.empty(max(1, most), dtype=torch.int16, device=dev)
+        self.val = torch.empty(max(1, most), dtype=values.dtype, device=dev)
+        self.acc = native.zeros((d,), values.dtype, dev)
+
+    @staticmethod
+    def alloc(indptr, values, n: int, d: int, B: int):
+        """A BucketRound, or None where the kernels' limits rule it out (too many slices)."""
+        if n <= 0 or B <= 0 or d <= 0 or values.device.type != "cuda":
+            return None
+        avg = float(indptr[-1]) / max(1, n) if not indptr.is_cuda else None
+        if avg is None:
+            nnz, _ = _batch_bounds(indptr, n, B)
+            avg = nnz / max(1, n)
+        try:
+            return BucketRound(indptr, values, n, d, B, BatchCsc.pick_group(avg))
+        except ValueError:
+            return None
+
+
+def bkt_round(bk: BucketRound, indptr, idx, val, y, wt, coef, n, d, B, loss, state, wl, fb, fuse: bool,
+              max_iter, tol, lr, reg, en) -> None:
+    rc = native.kernels().fmlx_glm_bkt_round(
+        int(val.dtype == torch.float64), bk.G, native.ptr(indptr), native.ptr(idx), native.ptr(val), native.ptr(y),
+        native.ptr(wt), native.ptr(coef), n, d, B, loss, native.ptr(state), native.ptr(wl), native.ptr(fb), int(fuse),
+        max_iter, float(tol), float(lr), float(reg), float(en), bk.csb, bk.rb, bk.chunk, native.ptr(bk.cnt),
+        native.ptr(bk.off), native.ptr(bk.cur), native.ptr(bk.tick), native.ptr(bk.done), native.ptr(bk.key),
+        native.ptr(bk.val), native.ptr(bk.acc), bk.bwd_blocks, native.stream_ptr(val.device))
+    if rc != 0:
+        raise RuntimeError("fmlx_glm_bkt_round failed: %d" % rc)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -64,7 +64,7 @@ _KERNEL_SIGS = {
                             c_double, c_double, c_void_p],
     "fmlx_glm_set_tuning": [c_long, c_int],
     "fmlx_glm_set_tail_tuning": [c_int, c_int],
-    "fmlx_glm_set_trace": [c_void_p],
+    "fmlx_glm_set_trace": ([c_void_p], None),
     "fmlx_glm_cnt_elems": [],
     "fmlx_glm_set_dma": [c_int],
     "fmlx_glm_acc_elems": ([c_int], c_long),
@@ -86,6 +86,14 @@ _KERNEL_SIGS = {
                            c_int, c_double, c_double, c_double, c_double, c_void_p, c_void_p, c_int, c_int, c_int,
                            c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                            c_void_p, c_void_p, c_void_p],
+    # glm_sparse.hip: single-visit bucket round
+    "fmlx_glm_bkt_limits": [c_void_p],
+    "fmlx_glm_bkt_set_debug": ([c_int], None),
+    "fmlx_glm_sparse_set_trace": ([c_void_p], None),
+    "fmlx_glm_bkt_round": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int,
+                           c_long, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double, c_double, c_double,
+                           c_double, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                           c_void_p, c_void_p, c_int, c_void_p],
     # sort.hip
     "fmlx_sorted_bounds": [c_void_p, c_long, c_int, c_void_p, c_void_p],
     "fmlx_seg_sort_scratch": ([c_void_p, c_int, c_int, c_int], c_long),

@@ -1,0 +1,48 @@
+"""A/B timing of the single-visit sparse bucket round (glm_sparse.hip glm_bkt_*) on the
+north-star SVC shape (1M columns, 64 nnz per row, 100k-row batches): ms per round of a warmed
+trainer, per kernel through events around each of many rounds, for debug variants that skip parts
+of the forward (1: reservation atomics, 2: the bucket writes, 4: the histogram) — timing only."""
+import json
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+
+
+def main():
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer
+    from flink_ml_amd.ops import glm as gk, native
+    from flink_ml_amd.table import SparseColumn
+
+    dev = torch.device("cuda:0")
+    n, dim, nnz = 1_000_000, 1_000_000, 64
+    g = torch.Generator(device=dev).manual_seed(7)
+    idx = torch.sort(torch.randint(0, dim, (n, nnz), generator=g, device=dev, dtype=torch.int32), dim=1).values
+    indptr = torch.arange(0, (n + 1) * nnz, nnz, dtype=torch.int64, device=dev)
+    vals = torch.rand((n * nnz,), generator=g, device=dev, dtype=torch.float32)
+    X = SparseColumn(indptr, idx.reshape(-1), vals, dim)
+    y = torch.randint(0, 2, (n,), generator=g, device=dev).to(torch.float32)
+    variants = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["0", "1", "2", "4", "7"])]
+    gk.TILE_MIN_VISITS = 10 ** 9
+    for v in variants:
+        native.kernels().fmlx_glm_bkt_set_debug(v)
+        tr = DeviceGlmTrainer(SGD(max_iter=10 ** 8, learning_rate=0.1, global_batch_size=100_000, tol=0.0),
+                              np.zeros(dim), X, y, None, "hinge")
+        assert tr.bkt is not None
+        tr.run_rounds(2 * tr.rounds_per_graph)
+        torch.cuda.synchronize()
+        R = 200
+        t0 = time.perf_counter()
+        tr.run_rounds(R)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1e3 / R
+        print(json.dumps({"dbg": v, "ms_per_round": round(ms, 4), "csb": tr.bkt.csb, "nb": tr.bkt.nb, "rb": tr.bkt.rb,
+                          "G": tr.bkt.G, "bwd_blocks": tr.bkt.bwd_blocks}), flush=True)
+    native.kernels().fmlx_glm_bkt_set_debug(0)
+
+
+if __name__ == "__main__":
+    main()

@@ -170,7 +170,7 @@ def test_bench_timed_region_only_replays(monkeypatch, steps, warmup, R, defer):
     tr = object.__new__(DeviceGlmTrainer)
     tr.use_graph, tr.rounds_per_graph, tr.graphs, tr.timing = True, R, {}, False
     tr.defer, tr.parity = defer, 0
-    tr.csc, tr._launched, tr._short = None, 0, False
+    tr.csc, tr.bkt, tr._launched, tr._short = None, None, 0, False
     log = []
 
     class Graph(_FakeGraph):

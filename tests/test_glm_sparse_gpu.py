@@ -42,10 +42,25 @@ def _sparse_col(indptr, idx, vals, d, device):
     return SparseColumn(indptr.to(device), idx.to(device), vals.to(device), d)
 
 
+def _use_path(monkeypatch, path):
+    """'bucket': the single-visit round (glm_sparse.hip glm_bkt_*, the default for fits visiting
+    each batch < TILE_MIN_VISITS times); 'csc': the transposed rounds."""
+    from flink_ml_amd.ops import glm as gk
+
+    monkeypatch.setattr(gk, "BUCKETS", path == "bucket")
+
+
+def _check_path(tr, path):
+    assert (tr.bkt is not None) == (path == "bucket") and (tr.csc is not None) == (path == "csc")
+
+
+@pytest.mark.parametrize("path", ["bucket", "csc"])
 @pytest.mark.parametrize("graph", [False, True])
-def test_sparse_sgd_transpose_path_matches_host(graph):
+def test_sparse_sgd_transpose_path_matches_host(graph, path, monkeypatch):
     _need_gpu()
     from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
+
+    _use_path(monkeypatch, path)
 
     n, d = 2300, 700
     indptr, idx, vals, dense, y, w = _csr(n, d, 3)
@@ -55,19 +70,22 @@ def test_sparse_sgd_transpose_path_matches_host(graph):
             ref = TorchGlmTrainer(sgd, np.zeros(d), dense, y, w, loss).fit()
             tr = DeviceGlmTrainer(sgd, np.zeros(d), _sparse_col(indptr, idx, vals, d, "cuda"), y.cuda(), w.cuda(),
                                   loss, use_graph=graph)
-            assert tr.csc is not None
+            _check_path(tr, path)
             got = tr.fit()
             assert tr.rounds_executed() == 9
             assert np.allclose(got, ref, atol=1e-10, rtol=1e-10), (loss, reg, en, np.abs(got - ref).max())
 
 
+@pytest.mark.parametrize("path", ["bucket", "csc"])
 @pytest.mark.parametrize("max_nnz", [40, 300])
-def test_sparse_weighted_and_unweighted_rounds_match_host(max_nnz):
+def test_sparse_weighted_and_unweighted_rounds_match_host(max_nnz, path, monkeypatch):
     """Short rows and rows spanning several load steps of a lane group, weighted and unweighted
     (the backward takes Σweight from the row count when unweighted), with tol termination decided
     on the device from the loss the last arriving block sums."""
     _need_gpu()
     from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
+
+    _use_path(monkeypatch, path)
 
     n, d = 1900, 900
     indptr, idx, vals, dense, y, w = _csr(n, d, 11 + max_nnz, max_nnz=max_nnz)
@@ -76,7 +94,7 @@ def test_sparse_weighted_and_unweighted_rounds_match_host(max_nnz):
         ref = TorchGlmTrainer(sgd, np.zeros(d), dense, y, wt, "logistic").fit()
         tr = DeviceGlmTrainer(sgd, np.zeros(d), _sparse_col(indptr, idx, vals, d, "cuda"), y.cuda(),
                               None if wt is None else wt.cuda(), "logistic")
-        assert tr.csc is not None
+        _check_path(tr, path)
         got = tr.fit()
         assert tr.rounds_executed() == 8
         assert np.allclose(got, ref, atol=1e-10, rtol=1e-10), np.abs(got - ref).max()
@@ -98,18 +116,26 @@ def test_sparse_sgd_fp32_transpose_vs_atomic_and_termination(monkeypatch):
     sgd = SGD(max_iter=15, learning_rate=0.5, global_batch_size=1024, tol=1e-9)
     ref = TorchGlmTrainer(sgd, np.zeros(d), dense, y, None, "hinge").fit()
     X = _sparse_col(indptr, idx, vals, d, "cuda")
+    bk = DeviceGlmTrainer(sgd, np.zeros(d), X, y.cuda(), None, "hinge")
+    assert bk.bkt is not None and bk.csc is None
+    got_b = bk.fit()
+    from flink_ml_amd.ops import glm as gk
+
+    monkeypatch.setattr(gk, "BUCKETS", False)
     a = DeviceGlmTrainer(sgd, np.zeros(d), X, y.cuda(), None, "hinge")
     assert a.csc is not None and a.csc.G in (4, 8, 16, 32, 64)
     got = a.fit()
     monkeypatch.setenv("FMLX_CSR_TRANSPOSE", "0")
     b = DeviceGlmTrainer(sgd, np.zeros(d), X, y.cuda(), None, "hinge")
-    assert b.csc is None
+    assert b.csc is None and b.bkt is None
     old = b.fit()
     scale = np.abs(ref).max()
+    assert np.abs(got_b - ref).max() < 1e-5 * scale
     assert np.abs(got - ref).max() < 1e-5 * scale
     assert np.abs(old - ref).max() < 1e-5 * scale
     # tol-based termination is decided on the device from the round's loss sum
     monkeypatch.delenv("FMLX_CSR_TRANSPOSE")
+    monkeypatch.setattr(gk, "BUCKETS", True)
     sgd2 = SGD(max_iter=200, learning_rate=1.0, global_batch_size=5000, tol=0.3)
     r2 = TorchGlmTrainer(sgd2, np.zeros(d), dense, y, None, "logistic")
     c2 = r2.fit()
@@ -119,31 +145,36 @@ def test_sparse_sgd_fp32_transpose_vs_atomic_and_termination(monkeypatch):
     assert np.abs(g2 - c2).max() < 1e-5 * max(1.0, np.abs(c2).max())
 
 
-def _sparse_worker(rank, world):
+def _sparse_worker(rank, world, path):
     import numpy as np
     import torch
 
     from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
+    from flink_ml_amd.ops import glm as gk
+
+    gk.BUCKETS = path == "bucket"
 
     n, d = 1500 + 400 * rank, 300
     indptr, idx, vals, dense, y, w = _csr(n, d, 40 + rank)
     sgd = SGD(max_iter=7, learning_rate=0.1, global_batch_size=900, tol=1e-9, reg=0.05, elastic_net=0.3)
     ref = TorchGlmTrainer(sgd, np.zeros(d), dense, y, w, "hinge").fit()
     tr = DeviceGlmTrainer(sgd, np.zeros(d), _sparse_col(indptr, idx, vals, d, "cuda:0"), y.cuda(), w.cuda(), "hinge")
-    assert tr.csc is not None
-    import os
-
-    assert (tr.csc.ET > 0) == (os.environ.get("FMLX_CSC_TILE_MIN_VISITS") == "0")
+    if path == "bucket":
+        assert tr.bkt is not None and tr.csc is None
+    else:
+        assert tr.csc is not None and (tr.csc.ET > 0) == (path == "tiled")
     got = tr.fit()
     return float(np.abs(got - ref).max()), got.tobytes()
 
 
-@pytest.mark.parametrize("tiled", [False, True])
-def test_sparse_sgd_two_ranks_one_gpu(tiled):
-    """The feedback path (backward writes the gradient row for the all-reduce), untiled and tiled."""
+@pytest.mark.parametrize("path", ["bucket", "untiled", "tiled"])
+def test_sparse_sgd_two_ranks_one_gpu(path):
+    """The feedback path (backward writes the gradient row for the all-reduce): bucket round,
+    untiled and tiled transposed rounds."""
     _need_gpu()
-    env = {"FMLX_DEVICE": "cuda:0", "FMLX_XGMI": "0", "FMLX_CSC_TILE_MIN_VISITS": "0" if tiled else "1000000"}
-    res = run_spmd(_sparse_worker, 2, env=env, timeout=300)
+    env = {"FMLX_DEVICE": "cuda:0", "FMLX_XGMI": "0",
+           "FMLX_CSC_TILE_MIN_VISITS": "0" if path == "tiled" else "1000000"}
+    res = run_spmd(_sparse_worker, 2, path, env=env, timeout=300)
     assert res[0][0] < 1e-10 and res[1][0] < 1e-10
     assert res[0][1] == res[1][1]  # replicas identical
 
@@ -409,3 +440,45 @@ def test_two_rank_sparse_fit_stops_on_tol_in_lockstep(check_every):
     assert r0 == r1 == 1
     assert l0 == l1 < 60
     assert np.array_equal(c0, c1)
+
+
+
+@pytest.mark.parametrize("vdtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("chunk", [32768, 1024])
+def test_bucket_round_skew_pieces_and_chunks_match_host(vdtype, chunk, monkeypatch):
+    """The single-visit bucket round on awkward inputs: most entries in the first column slice
+    (a bucket summed in several chunks through the accumulator: chunk = 1024), rows of up to 300
+    entries (a forward block's entries staged in several LDS pieces), empty rows, a truncated
+    last batch, weighted and not, with elastic net — against the fp64 host trainer."""
+    _need_gpu()
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
+    from flink_ml_amd.ops import glm as gk
+
+    monkeypatch.setattr(gk.BucketRound, "CHUNK", chunk)
+    n, d = 5100, 3000
+    g = torch.Generator().manual_seed(5)
+    counts = torch.randint(0, 301, (n,), generator=g)
+    counts[100:140] = 0
+    indptr = torch.zeros(n + 1, dtype=torch.int64)
+    indptr[1:] = torch.cumsum(counts, 0)
+    rows = []
+    for c in counts.tolist():
+        hot = torch.randperm(64, generator=g)[: c // 2]  # half of every row in columns 0..63
+        cold = 64 + torch.randperm(d - 64, generator=g)[: c - len(hot)]
+        rows.append(torch.sort(torch.cat([hot, cold])).values)
+    idx = torch.cat(rows).to(torch.int32)
+    vals = (torch.rand(len(idx), generator=g, dtype=torch.float64) * 2 - 1).to(vdtype)
+    dense = torch.zeros((n, d), dtype=torch.float64)
+    dense[torch.repeat_interleave(torch.arange(n), counts), idx.long()] = vals.double()
+    y = (dense @ torch.linspace(-1, 1, d, dtype=torch.float64) > 0).double()
+    w = torch.rand(n, generator=g, dtype=torch.float64) + 0.5
+    for wt in (None, w):
+        sgd = SGD(max_iter=7, learning_rate=0.3, global_batch_size=2000, tol=1e-12, reg=0.02, elastic_net=0.3)
+        ref = TorchGlmTrainer(sgd, np.zeros(d), dense, y, wt, "hinge").fit()
+        tr = DeviceGlmTrainer(sgd, np.zeros(d), _sparse_col(indptr, idx, vals, d, "cuda"), y.cuda(),
+                              None if wt is None else wt.cuda(), "hinge")
+        assert tr.bkt is not None and tr.bkt.nb > 1
+        got = tr.fit()
+        assert tr.rounds_executed() == 7
+        tol = 1e-10 if vdtype == torch.float64 else 2e-5
+        assert np.abs(got - ref).max() <= tol * max(1.0, np.abs(ref).max()), np.abs(got - ref).max()

@@ -70,7 +70,7 @@ def _glm_worker(rank, world):
     assert xgmi.collective_path() == "nccl"
     out = {}
     tr, c = _fit_svc_sparse(graph=True)
-    assert tr.distributed and tr.mode == gk.TAIL_FEEDBACK and tr.use_graph and tr.csc is not None
+    assert tr.distributed and tr.mode == gk.TAIL_FEEDBACK and tr.use_graph and tr.bkt is not None
     assert tr.feedback.numel() == 1_000_002  # 4 MB: beyond the xGMI one-shot cap in any case
     assert len(tr.graphs) > 0  # the RCCL all-reduce was captured into hipGraphs and replayed
     out["svc"] = (c, tr.rounds_executed())
