@@ -65,6 +65,47 @@ def timed_region(tr, ctx, warmup: int, steps: int):
     return elapsed, ev0.elapsed_time(ev1) * 1e-3
 
 
+VERIFY_ROUNDS = 3
+VERIFY_RTOL = 1e-4
+
+
+def verify_exchange(make, comm, rounds: int = VERIFY_ROUNDS):
+    """Untimed check that the timed rounds' cross-rank combination computed the right thing
+    (a silent ordering bug of the in-kernel exchange must not yield a confident number).
+
+    Two fresh trainers of the timed configuration run ``rounds`` rounds from the same start with
+    direct launches: ``a`` exactly as timed (in-kernel xGMI exchange, deferred completion when the
+    timed rounds used it), ``b`` on the process group (feedback → RCCL all-reduce → update). Every
+    rank then requires (1) ``a``'s coefficients bitwise identical on all ranks (each applied the same
+    exchanged feedback) and (2) ``a`` ≈ ``b`` (the exchanged feedback equals the process-group sum of
+    the same per-rank partials, up to summation order). Reference: the reference's own payload
+    checks, ``AllReduceImpl.java:118-120,187-188``. Returns (agreed verdict, details)."""
+    a = make()
+    a.use_graph = False
+    a.sgd.max_iter = rounds + 2  # (direct launches read it; the flush round too)
+    a.run_rounds(rounds)
+    a.flush()
+    ca = a.coef[:a.d_model].double().cpu()
+    b = make()
+    b.use_rccl()
+    b.use_graph = False
+    b.sgd.max_iter = rounds + 2
+    b.run_rounds(rounds)
+    b.flush()
+    cb = b.coef[:b.d_model].double().cpu()
+    from flink_ml_amd.parallel.context import get_context
+
+    if os.environ.get("FMLX_BENCH_INJECT_EXCHANGE_ERROR") == str(get_context().rank):
+        ca = ca.clone()
+        ca[0] += 1e-3 * (1.0 + ca.abs().max())  # test hook: a corrupted exchange on this rank
+    replicas = comm.all_gather_tensor(ca)
+    identical = all(torch.equal(replicas[0], c) for c in replicas)
+    scale = max(float(cb.abs().max()), 1e-30)
+    rel = float((ca - cb).abs().max()) / scale
+    ok = comm.all_agree(bool(identical and rel <= VERIFY_RTOL))
+    return ok, {"replicas_identical": identical, "rel_err_vs_process_group": rel}
+
+
 def launch_ranks(n: int, argv, env=None, timeout: float = None) -> int:
     """Starts ``n`` rank processes of this script (``argv``: its arguments) on this node and
     returns the first non-zero exit status (0 if every rank succeeded).
@@ -255,6 +296,36 @@ def main():
     executed = trainer.rounds_executed()
     if executed < args.warmup + args.steps:
         raise SystemExit("SGD terminated early (%d rounds): timing would skip work" % executed)
+    verified, vinfo = None, {}
+    if ctx.is_distributed and world > 1:
+        # the timed replicas must agree bitwise, and the exchange must equal the process-group
+        # sum; otherwise re-time with the system-scope fences, and fail if that disagrees too
+        final = comm.all_gather_tensor(trainer.coef[:trainer.d_model].double().cpu())
+        same = comm.all_agree(all(torch.equal(final[0], c) for c in final))
+        verified, vinfo = verify_exchange(make_trainer, comm)
+        verified = verified and same
+        vinfo["timed_replicas_identical"] = same
+        if not verified and trainer.xg is not None:
+            from flink_ml_amd.parallel import xgmi
+
+            if rank == 0:
+                print("exchange_verified: false (%s); re-timing with FMLX_XGMI_STRICT_FENCE=1" % vinfo,
+                      file=sys.stderr, flush=True)
+            xgmi.set_strict_fence(True)
+            trainer = make_trainer()
+            elapsed, kernel_s = timed_region(trainer, ctx, args.warmup, args.steps)
+            elapsed = comm.all_reduce_scalar(elapsed, "max")
+            kernel_s = comm.all_reduce_scalar(kernel_s, "max")
+            trainer.flush()
+            final = comm.all_gather_tensor(trainer.coef[:trainer.d_model].double().cpu())
+            same = comm.all_agree(all(torch.equal(final[0], c) for c in final))
+            verified, vinfo = verify_exchange(make_trainer, comm)
+            verified = verified and same
+            vinfo.update(timed_replicas_identical=same, strict_fence=True)
+        if not verified:
+            if rank == 0:
+                print(json.dumps({"exchange_verified": False, "detail": vinfo}), flush=True)
+            raise SystemExit("bench.py: the cross-rank exchange disagrees with the process-group all-reduce")
 
     ms = elapsed / args.steps * 1e3
     samples = global_batch * args.steps
@@ -276,6 +347,7 @@ def main():
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None,
+            "exchange_verified": verified,
             "dtype": args.dtype,
             "data": "synthetic (device-generated U[0,1) features, Bernoulli labels; LabeledPointWithWeightGenerator shape)",
             "config": {
@@ -297,6 +369,7 @@ def main():
                 "round": {1: "fused kernel + rccl all-reduce + update", 2: "one fused kernel",
                           3: "one fused kernel with in-kernel xgmi exchange"}[trainer.mode],
                 "hbm_gb_per_s": round(trainer.B * args.dim * X.element_size() / (ms * 1e-3) / 1e9, 1),
+                "exchange_check": vinfo or None,
             },
         }
         print(json.dumps(rec), flush=True)

@@ -49,9 +49,33 @@ def parse_bytes(v: Optional[str]) -> Optional[int]:
     return int(float(m.group(1)) * mult)
 
 
-def hbm_budget() -> Optional[int]:
-    """FMLX_HBM_BUDGET: device bytes a bounded fit may keep resident (None: unlimited)."""
-    return parse_bytes(os.environ.get("FMLX_HBM_BUDGET"))
+# (tests: (free, total) device bytes that stand in for hipMemGetInfo in the default budget)
+_FREE_OVERRIDE: Optional[tuple] = None
+MARGIN_MIN = 4 << 30      # the default budget leaves at least this much of the device free …
+MARGIN_FRAC = 0.10        # … or this fraction of its capacity (kernels' scratch, the trainers' buffers)
+
+
+def hbm_budget(device=None) -> Optional[int]:
+    """Device bytes a bounded fit may keep resident: ``FMLX_HBM_BUDGET`` when set; otherwise, on a
+    GPU, the device's free memory minus a margin (max(4 GiB, 10 % of its capacity)) — so a
+    partition larger than what is free streams by itself, as the reference's data cache spills
+    without being asked (``DataCacheWriter.java:101-107,169-178``), instead of failing to
+    allocate. None (unlimited) without a GPU."""
+    env = parse_bytes(os.environ.get("FMLX_HBM_BUDGET"))
+    if env is not None:
+        return env
+    if _FREE_OVERRIDE is not None:
+        free, total = _FREE_OVERRIDE
+    else:
+        dev = torch.device(device) if device is not None else None
+        if dev is None:
+            from ..config import compute_device
+
+            dev = compute_device()
+        if dev.type != "cuda":
+            return None
+        free, total = torch.cuda.mem_get_info(dev)
+    return max(0, int(free) - max(MARGIN_MIN, int(MARGIN_FRAC * total)))
 
 
 def host_cache_budget() -> int:
@@ -131,16 +155,144 @@ class BatchStore:
             self.cache = None
 
 
+    # (BatchRing interface: byte slots, the bytes of a record, a typed view of a filled slot)
+    def slot_bytes(self) -> int:
+        return self.batch_bytes
+
+    def record_bytes(self, b: int) -> int:
+        return self.rows(b) * self.d * self.es
+
+    def view(self, slot: torch.Tensor, b: int):
+        rows = self.rows(b)
+        return slot[:rows * self.d * self.es].view(self.dtype).view(rows, self.d)
+
+
+def _align(x: int, a: int = 16) -> int:
+    return -(-x // a) * a
+
+
+class SparseBatchStore:
+    """CSR row batches of a host partition (``SparseColumn``) under an HBM budget — the sparse
+    counterpart of ``BatchStore`` (bounded LinearSVC / LR on 1M-wide features): the leading batches
+    that fit stay on the device as ONE CSR (indptr rebased to 0; a batch is an indptr window over
+    the shared indices / values), the others become DataCache records [indptr rebased (rows + 1)
+    int64 | indices int32 | values], streamed through the same ring."""
+
+    def __init__(self, X, B: int, device, budget: Optional[int], ring: int = RING_SLOTS,
+                 host_budget: Optional[int] = None, cache_path: Optional[str] = None,
+                 segment_bytes: Optional[int] = None):
+        ip = X.indptr.to(torch.int64)
+        self.indices_h = X.indices.to(torch.int32)
+        self.values_h = X.values
+        self.size = X.size
+        self.B, self.device = max(1, int(B)), torch.device(device)
+        self.n = len(X)
+        self.dtype = X.values.dtype
+        self.es = X.values.element_size()
+        self.P = max(1, -(-self.n // self.B)) if self.n else 0
+        self.base = int(ip[0]) if self.n else 0
+        self.ip_h = ip - self.base
+        bnd = [int(self.ip_h[min(self.n, b * self.B)]) for b in range(self.P + 1)]
+        self.bounds = bnd
+        self.nnz_max = max([bnd[b + 1] - bnd[b] for b in range(self.P)] + [0])
+        per = [self.record_bytes(b) for b in range(self.P)]
+        if budget is None:
+            R = self.P
+        else:
+            left = budget - ring * self.slot_bytes()
+            R = 0
+            while R < self.P and left >= per[R]:
+                left -= per[R]
+                R += 1
+        self.R = R
+        rows, nz = min(self.n, R * self.B), bnd[R] if self.P else 0
+        self.r_indptr = self.ip_h[:rows + 1].to(self.device)
+        o = self.base
+        self.r_indices = self.indices_h[o:o + nz].to(self.device)
+        self.r_values = self.values_h[o:o + nz].to(self.device)
+        self.cache = None
+        self.recs: List[int] = []
+        self._registered: List[int] = []
+        if R < self.P:
+            kw = {"memory_budget": host_budget if host_budget is not None else host_cache_budget()}
+            if segment_bytes:
+                kw["segment_bytes"] = segment_bytes
+            self.cache = DataCache(path=cache_path, **kw)
+            for b in range(R, self.P):
+                self.recs.append(self.cache.append(self._record(b)))
+            if self.device.type == "cuda":
+                for p, cap in self.cache.memory_segments():
+                    if native.kernels().fmlx_host_register(p, cap) == 0:
+                        self._registered.append(p)
+
+    def _layout(self, rows: int, nz: int):
+        o_idx = _align((rows + 1) * 8)
+        o_val = _align(o_idx + nz * 4)
+        return o_idx, o_val, o_val + nz * self.es
+
+    def _record(self, b: int) -> np.ndarray:
+        r0, rows = b * self.B, self.rows(b)
+        j0, j1 = self.bounds[b], self.bounds[b + 1]
+        o_idx, o_val, total = self._layout(rows, j1 - j0)
+        buf = np.zeros(total, dtype=np.uint8)
+        buf[:(rows + 1) * 8] = (self.ip_h[r0:r0 + rows + 1] - j0).numpy().view(np.uint8)
+        buf[o_idx:o_idx + (j1 - j0) * 4] = self.indices_h[self.base + j0:self.base + j1].numpy().view(np.uint8)
+        v = self.values_h[self.base + j0:self.base + j1].contiguous()
+        buf[o_val:total] = v.view(torch.uint8).numpy()
+        return buf
+
+    def rows(self, b: int) -> int:
+        return min(self.n, (b + 1) * self.B) - b * self.B
+
+    def is_resident(self, b: int) -> bool:
+        return b < self.R
+
+    def resident_view(self, b: int):
+        """(indptr window, indices, values) of a resident batch (absolute offsets)."""
+        r0 = b * self.B
+        return self.r_indptr[r0:r0 + self.rows(b) + 1], self.r_indices, self.r_values
+
+    def record(self, b: int) -> int:
+        return self.recs[b - self.R]
+
+    def slot_bytes(self) -> int:
+        return self._layout(self.B, self.nnz_max)[2]
+
+    def record_bytes(self, b: int) -> int:
+        return self._layout(self.rows(b), self.bounds[b + 1] - self.bounds[b])[2]
+
+    def view(self, slot: torch.Tensor, b: int):
+        rows, nz = self.rows(b), self.bounds[b + 1] - self.bounds[b]
+        o_idx, o_val, total = self._layout(rows, nz)
+        return (slot[:(rows + 1) * 8].view(torch.int64), slot[o_idx:o_idx + nz * 4].view(torch.int32),
+                slot[o_val:total].view(self.dtype))
+
+    def stats(self) -> dict:
+        st = {"batches": self.P, "resident": self.R, "streamed": self.P - self.R, "slot_bytes": self.slot_bytes(),
+              "sparse": True}
+        if self.cache is not None:
+            st.update({"cache_" + k: v for k, v in self.cache.stats().items()})
+        return st
+
+    def close(self) -> None:
+        for p in self._registered:
+            native.kernels().fmlx_host_unregister(p)
+        self._registered = []
+        if self.cache is not None:
+            self.cache.close()
+            self.cache = None
+
+
 class BatchRing:
     """Device slots the non-resident batches are streamed into (see the module docstring)."""
 
-    def __init__(self, store: BatchStore, slots: int = RING_SLOTS):
+    def __init__(self, store, slots: int = RING_SLOTS):
         from ..utils import graphs
 
         self.store = store
         dev = store.device
         self.K = max(2, int(slots))
-        self.slots = [torch.empty((store.B, store.d), dtype=store.dtype, device=dev) for _ in range(self.K)]
+        self.slots = [torch.empty(max(1, store.slot_bytes()), dtype=torch.uint8, device=dev) for _ in range(self.K)]
         self.staging = [None] * self.K  # pinned host buffers for file-segment batches (lazily)
         self.copy_stream = graphs.aux_stream(dev, "ooc-h2d")
         self.copied = [torch.cuda.Event() for _ in range(self.K)]
@@ -150,21 +302,21 @@ class BatchRing:
         self.next = 0
         self.h2d_bytes = 0
 
-    def fetch(self, b: int) -> torch.Tensor:
-        """Slot holding batch ``b``; the current stream waits for its copy."""
+    def fetch(self, b: int):
+        """Batch ``b`` in a device slot (the store's typed view); the current stream waits for its
+        copy."""
         from ..utils import hostsync
 
         st = self.store
         s = self.next
         self.next = (s + 1) % self.K
         slot = self.slots[s]
-        rows = st.rows(b)
-        nbytes = rows * st.d * st.es
+        nbytes = st.record_bytes(b)
         rec = st.record(b)
         src = st.cache.record_ptr(rec)
         if src is None:  # file segment: into this slot's pinned staging buffer first
             if self.staging[s] is None:
-                self.staging[s] = torch.empty(st.batch_bytes, dtype=torch.uint8, pin_memory=True)
+                self.staging[s] = torch.empty(max(1, st.slot_bytes()), dtype=torch.uint8, pin_memory=True)
             if self.used[s]:
                 hostsync.wait_event(self.staged[s])  # its previous copy out of staging is done
             st.cache.read_into(rec, self.staging[s])
@@ -179,7 +331,7 @@ class BatchRing:
         torch.cuda.current_stream(st.device).wait_event(self.copied[s])
         self.used[s] = True
         self._cur = s
-        return slot[:rows]
+        return st.view(slot, b)
 
     def release(self) -> None:
         """The current stream's work that reads the last fetched slot is queued."""
@@ -194,30 +346,51 @@ class StreamedGlmTrainer:
         from ..parallel.context import get_context
         from .optimizer import DeviceGlmTrainer, local_batch_size
 
+        from ..table import SparseColumn
+
         ctx = get_context()
         self.sgd = sgd
         dev = torch.device(device)
         self.device = dev
         B = local_batch_size(sgd.global_batch_size, ctx.rank, ctx.world_size)
-        self.store = BatchStore(X, max(1, B), dev, budget, **store_kw)
+        self.sparse = isinstance(X, SparseColumn)
+        if self.sparse:
+            acc = torch.float64 if X.values.dtype == torch.float64 else torch.float32
+            X = SparseColumn(X.indptr, X.indices, X.values.to(acc), X.size)
+            self.store = SparseBatchStore(X, max(1, B), dev, budget, **store_kw)
+        else:
+            acc = torch.float64 if X.dtype == torch.float64 else torch.float32
+            self.store = BatchStore(X, max(1, B), dev, budget, **store_kw)
         self.ring = BatchRing(self.store) if self.store.R < self.store.P else None
-        acc = torch.float64 if X.dtype == torch.float64 else torch.float32
         self.y = y.to(device=dev, dtype=acc).reshape(-1).contiguous()
         self.w = weight.to(device=dev, dtype=acc).reshape(-1).contiguous() if weight is not None else None
         # the inner trainer owns coefficients, device state, scratch and the fused kernel; it is
         # pointed at one batch per launch (n = that batch's rows, so the kernel's batch is the view)
-        first = self.store.resident_view(0) if self.store.R else self.ring.slots[0]
-        w0 = self.w[:first.shape[0]] if self.w is not None else None
-        # (pad=False: the inner trainer is re-pointed at ring slots of the unpadded width)
-        self.inner = DeviceGlmTrainer(sgd, init_coef, first, self.y[:first.shape[0]], w0, loss, use_graph=False,
-                                      check_every=check_every, pad=False)
+        if self.store.P == 0:
+            first = self.store.resident if not self.sparse else self.store.resident_view(0)
+        elif self.store.R:
+            first = self.store.resident_view(0)
+        else:
+            first = self.store.view(self.ring.slots[0], 0)
+        if self.sparse:
+            ip, ix, vv = first
+            rows0 = int(ip.shape[0]) - 1
+            first = SparseColumn(ip, ix, vv, X.size)
+            # every batch runs the single-visit bucket round, its buffers sized for the largest batch
+            kw = {"bucket_nnz": (max(1, self.store.nnz_max), self.store.bounds[-1] / max(1, self.store.n))}
+        else:
+            rows0 = int(first.shape[0])
+            kw = {"pad": False}  # (the inner trainer is re-pointed at ring slots of the unpadded width)
+        w0 = self.w[:rows0] if self.w is not None else None
+        self.inner = DeviceGlmTrainer(sgd, init_coef, first, self.y[:rows0], w0, loss, use_graph=False,
+                                      check_every=check_every, **kw)
         self.check_every = max(1, int(check_every))
 
     def _round(self, e: int) -> None:
         st, tr = self.store, self.inner
         b = e % st.P if st.P else 0
         if st.P == 0:
-            Xb = st.resident
+            Xb = st.resident if not self.sparse else st.resident_view(0)
             lo = 0
         elif st.is_resident(b):
             Xb = st.resident_view(b)
@@ -225,11 +398,16 @@ class StreamedGlmTrainer:
         else:
             Xb = self.ring.fetch(b)
             lo = b * st.B
-        tr.X = Xb
-        tr.n = Xb.shape[0]
-        tr.y = self.y[lo:lo + Xb.shape[0]]
+        if self.sparse:
+            tr.indptr, tr.indices, tr.values = Xb
+            rows = int(Xb[0].shape[0]) - 1
+        else:
+            tr.X = Xb
+            rows = int(Xb.shape[0])
+        tr.n = rows
+        tr.y = self.y[lo:lo + rows]
         if self.w is not None:
-            tr.w = self.w[lo:lo + Xb.shape[0]]
+            tr.w = self.w[lo:lo + rows]
         tr._launch_round(1)
         tr._launched += 1
         if self.ring is not None and st.P and not st.is_resident(b):
@@ -244,7 +422,7 @@ class StreamedGlmTrainer:
                 if (e + 1) % self.check_every == 0 and self.inner._poll_stopped():
                     break
             self.inner.flush()
-        coef = hostsync.to_host(self.inner.coef).to(torch.float64).numpy()
+        coef = hostsync.to_host(self.inner.coef[:self.inner.d_model]).to(torch.float64).numpy()
         self.inner.check_exchange()
         return coef
 

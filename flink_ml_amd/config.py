@@ -77,19 +77,30 @@ def features_for_compute(table: Table, col: str, allow_sparse: bool = True, exac
     return table.vectors_as_matrix(col, dtype=wide or compute_dtype(), device=dev)
 
 
-def host_features_if_oversized(table: Table, col: str):
-    """A dense host-resident feature column whose compute-dtype bytes exceed ``FMLX_HBM_BUDGET``,
-    converted to the compute dtype but LEFT in host memory, when the compute device is a GPU: the
-    bounded trainers then keep what fits resident and stream the rest (common/outofcore.py).
-    None otherwise (the column goes to the device as usual)."""
+def host_features_if_oversized(table: Table, col: str, allow_sparse: bool = False):
+    """A host-resident feature column too large for the device — dense bytes in the compute dtype
+    (or, with ``allow_sparse``, CSR bytes: indptr + indices + accumulation-dtype values) above the
+    HBM budget (``FMLX_HBM_BUDGET``, else the device's free memory minus a margin) — converted but
+    LEFT in host memory, when the compute device is a GPU: the bounded trainers then keep what
+    fits resident and stream the rest (common/outofcore.py). None otherwise (the column goes to
+    the device as usual)."""
     from .common.outofcore import hbm_budget
 
     dev = compute_device()
-    budget = hbm_budget()
     c = table.column(col)
-    if dev.type != "cuda" or budget is None or not isinstance(c, torch.Tensor) or c.dim() != 2 or c.is_cuda:
+    if dev.type != "cuda":
+        return None
+    if allow_sparse and isinstance(c, SparseColumn) and not c.values.is_cuda:
+        acc = acc_dtype()
+        need = c.indptr.numel() * 8 + c.indices.numel() * (4 + torch.empty(0, dtype=acc).element_size())
+        budget = hbm_budget(dev)
+        if budget is None or need <= budget:
+            return None
+        return c.to(dtype=acc)
+    if not isinstance(c, torch.Tensor) or c.dim() != 2 or c.is_cuda:
         return None
     dt = compute_dtype()
-    if c.shape[0] * c.shape[1] * torch.empty(0, dtype=dt).element_size() <= budget:
+    budget = hbm_budget(dev)
+    if budget is None or c.shape[0] * c.shape[1] * torch.empty(0, dtype=dt).element_size() <= budget:
         return None
     return c.to(dt).contiguous() if c.dtype != dt or not c.is_contiguous() else c

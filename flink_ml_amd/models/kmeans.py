@@ -146,7 +146,7 @@ class KMeans(Estimator, KMeansParams):
             from ..common.outofcore import hbm_budget, streamed_kmeans
 
             cents, weights = streamed_kmeans(Xh, init, self.get(self.MAX_ITER), metric, config.compute_device(),
-                                             hbm_budget())
+                                             hbm_budget(config.compute_device()))
         else:
             cents, weights = kmeans_lloyd(X, init, self.get(self.MAX_ITER), metric)
         model = KMeansModel().set_model_data(kmeans_model_data_table(cents, weights))

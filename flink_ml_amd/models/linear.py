@@ -37,7 +37,7 @@ def extract_training_data(est, table: Table, check_labels=None):
     """(features, labels[n] f64, weights[n] f64 | None) on the compute device — except a dense
     host-resident feature column larger than FMLX_HBM_BUDGET on a GPU, which stays in host memory
     (compute dtype) for the out-of-core trainer (common/outofcore.py)."""
-    X = config.host_features_if_oversized(table, est.get(est.FEATURES_COL))
+    X = config.host_features_if_oversized(table, est.get(est.FEATURES_COL), allow_sparse=True)
     if X is None:
         X = config.features_for_compute(table, est.get(est.FEATURES_COL))
     dev = config.compute_device()

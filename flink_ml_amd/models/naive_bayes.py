@@ -185,7 +185,7 @@ def _label_value_counts_device(X: torch.Tensor, li: torch.Tensor, L: int, dist: 
     features with a table of at most 2^27 cells (the categorical case; value range from the global
     min / max) are counted by one pass of ``cs_hist`` into [d, L, V] and all-reduced as one dense
     table; other values take the sorted-column distinct pass on one rank and the keyed shuffle of
-    ``stats.value_label_counts`` across ranks."""
+    ``catstats.global_value_label_counts`` (native union of the ranks' value lists) across ranks."""
     from ..ops import catstats
 
     n, d = X.shape
@@ -206,17 +206,8 @@ def _label_value_counts_device(X: torch.Tensor, li: torch.Tensor, L: int, dist: 
         slots = [np.nonzero(present[j])[0] for j in range(d)]
         return counts, [(sl + vmin).astype(np.float64) for sl in slots], slots, n_lab.cpu().numpy()
     if dist:
-        vals_t, flat, Vn = value_label_counts(X.to(torch.float64), li, L)
-        Vmax = max(1, int(Vn.max()) if d else 1)
-        counts = np.zeros((d, L, Vmax), dtype=np.float64)
-        off = 0
-        for j in range(d):
-            V = int(Vn[j])
-            counts[j, :, :V] = flat[off:off + V * L].reshape(V, L).T
-            off += V * L
-        n_lab = comm.all_reduce_sum(n_lab)
-        return (counts, [v.cpu().numpy() for v in vals_t], [np.arange(int(Vn[j])) for j in range(d)],
-                n_lab.cpu().numpy())
+        counts, vals, slots = catstats.global_value_label_counts(X, li, L)
+        return counts, vals, slots, comm.all_reduce_sum(n_lab).cpu().numpy()
     counts, vals, slots = catstats.value_label_counts(X, li, L, int_range=None)
     return counts.astype(np.float64), vals, slots, n_lab.cpu().numpy()
 

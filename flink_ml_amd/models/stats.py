@@ -7,8 +7,9 @@ one all-reduce combines them:
   column sum / Σx²; F = MSB / MSW, p = 1 - F_cdf(F; C-1, N-C)  (``ANOVATest.java:120-200``).
 * FValueTest — label/feature moments, then the centred cross-moment (y - ȳ)ᵀ(X - x̄) as one GEMV;
   corr² → F with (1, N-2) dof (``FValueTest.java:150-260``).
-* ChiSqTest — per-feature contingency tables [#values, #labels] counted with one ``bincount``
-  per column; Pearson statistic, dof = (V-1)(L-1), p-value and statistic rounded HALF_UP to 11
+* ChiSqTest — per-feature contingency tables [#values, #labels] (on the GPU: the catstats
+  kernels, across ranks one all-reduce of the table — ``catstats.global_value_label_counts``);
+  Pearson statistic, dof = (V-1)(L-1), p-value and statistic rounded HALF_UP to 11
   decimals like ``ChiSqTest.java:440-455``.
 
 Distribution CDFs come from scipy (commons-math3 in the reference).
@@ -219,17 +220,21 @@ class ChiSqTest(AlgoOperator, _TestParams):
         labels = global_sorted_unique(y)
         L, d = labels.numel(), X.shape[1]
         li = torch.searchsorted(labels, y)
-        if get_world_distributed():
-            # distinct values and contingency counts in one keyed shuffle (no value lists pickled)
-            vals, flat, _ = value_label_counts(X.to(torch.float64), li, L)
-        elif X.is_cuda:
-            # native contingency tables (ops/catstats.py: integer table or sorted-column distinct)
+        if X.is_cuda:
+            # native contingency tables (ops/catstats.py: integer table or sorted-column distinct;
+            # across ranks one all-reduce of the table, after a union of the ranks' value lists)
             from ..ops import catstats
 
-            counts, vals_np, slots = catstats.value_label_counts(X, li, L)
+            if get_world_distributed():
+                counts, vals_np, slots = catstats.global_value_label_counts(X, li.to(torch.int32), L)
+            else:
+                counts, vals_np, slots = catstats.value_label_counts(X, li, L)
             vals = [torch.as_tensor(v) for v in vals_np]
             flat = np.concatenate([counts[j][:, slots[j]].T.reshape(-1) for j in range(d)]).astype(np.float64) \
                 if d else np.zeros(0)
+        elif get_world_distributed():
+            # (CPU ranks) distinct values and contingency counts in one keyed shuffle
+            vals, flat, _ = value_label_counts(X.to(torch.float64), li, L)
         else:
             vals = [torch.unique(X[:, j]) for j in range(d)]
             tables = []

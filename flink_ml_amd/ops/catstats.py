@@ -177,3 +177,69 @@ def value_label_counts(X: torch.Tensor, li: torch.Tensor, L: int,
                 native.stream_ptr(dev))
     c = counts[:d * Vmax * L].reshape(d, Vmax, L).permute(0, 2, 1).cpu().numpy().astype(np.int64)
     return c, [v.cpu().numpy() for v in vals], [np.arange(V) for V in Vn]
+
+
+def global_value_label_counts(X: torch.Tensor, li: torch.Tensor, L: int):
+    """(feature, distinct value, label) counts over ALL ranks on the native kernels — the keyed
+    count of ``ChiSqTest.java:127-155`` / ``NaiveBayes.java:95-103`` without a keyed shuffle:
+
+    * integer features whose [d, L, V] table (value range from the all-reduced min / max) has at
+      most MAX_TABLE cells: one ``int_table`` pass per rank, then ONE all-reduce of the dense table;
+    * otherwise every rank takes its per-column sorted distinct values (``value_label_counts``:
+      radix sort + distinct pass), the ranks' value lists are all-gathered (padded to the longest,
+      the padding repeating a real value of the column) and their union per column is one more
+      ``distinct_codes`` pass; each rank places its local counts at their union slots (a host
+      binary search over the small per-column lists) and one all-reduce sums the tables.
+
+    Returns (counts float64 [d, L, Vmax] numpy, per-feature sorted distinct values (numpy fp64),
+    per-feature slots of those values in the last axis) — the shape ``value_label_counts`` returns
+    on one rank."""
+    from ..parallel import comm
+
+    X = _mat(X)
+    n, d = X.shape
+    dev = X.device
+    mn, mx, non = flags(X) if n else (float("inf"), float("-inf"), False)
+    f = comm.all_reduce(torch.tensor([-mn, mx, float(non)], dtype=torch.float64, device=dev), "max").tolist()
+    mn, mx, non = -f[0], f[1], f[2] != 0.0
+    if not non and mx >= mn and (mx - mn + 1) * L * d <= MAX_TABLE:
+        vmin, V = int(mn), int(mx - mn) + 1
+        cnt = comm.all_reduce_sum(int_table(X, li, L, vmin, V).to(torch.float64)) if n else \
+            comm.all_reduce_sum(torch.zeros((d, L, V), dtype=torch.float64, device=dev))
+        counts = cnt.cpu().numpy()
+        present = counts.sum(1) > 0
+        slots = [np.nonzero(present[j])[0] for j in range(d)]
+        return counts, [(sl + vmin).astype(np.float64) for sl in slots], slots
+    if n:
+        c_loc, vals_loc, slots_loc = value_label_counts(X, li, L, int_range=None)
+    else:
+        c_loc, vals_loc, slots_loc = np.zeros((d, L, 1), np.int64), [np.zeros(0)] * d, [np.zeros(0, np.int64)] * d
+    vl = np.array([len(v) for v in vals_loc], dtype=np.int64)
+    M = int(comm.all_reduce(torch.tensor([int(vl.max()) if d else 0], dtype=torch.int64, device=dev), "max")[0])
+    M = max(M, 1)
+    pad = np.zeros((M, d), dtype=np.float64)
+    for j in range(d):
+        if vl[j]:
+            pad[:vl[j], j] = vals_loc[j]
+    # (the gathered blocks carry each rank's list lengths in a last row)
+    blk = torch.from_numpy(np.concatenate([pad, vl[None, :].astype(np.float64)], 0)).to(dev)
+    gathered = comm.all_gather_tensor(blk)
+    G = torch.stack(gathered)                   # [world, M + 1, d]
+    lens = G[:, M, :].cpu().numpy().astype(np.int64)  # [world, d]
+    vals_g = G[:, :M, :]
+    rows = torch.arange(M, device=dev)[None, :, None]
+    valid = rows < torch.as_tensor(lens, device=dev)[:, None, :]
+    # padding repeats a real value of its column (the first one of the first rank holding one)
+    first_r = np.argmax(lens > 0, axis=0)
+    fill = vals_g[torch.as_tensor(first_r, device=dev), 0, torch.arange(d, device=dev)]
+    U = torch.where(valid, vals_g, fill[None, None, :]).reshape(-1, d)
+    _, union = distinct_codes(U)
+    union = [u.cpu().numpy() if int(lens[:, j].sum()) else np.zeros(0) for j, u in enumerate(union)]
+    Umax = max([1] + [len(u) for u in union])
+    T = np.zeros((d, L, Umax), dtype=np.float64)
+    for j in range(d):
+        if vl[j]:
+            pos = np.searchsorted(union[j], vals_loc[j])
+            T[j][:, pos] = c_loc[j][:, slots_loc[j]]
+    T = comm.all_reduce_sum(torch.from_numpy(T).to(dev)).cpu().numpy()
+    return T, union, [np.arange(len(u)) for u in union]

@@ -617,45 +617,58 @@ __global__ __launch_bounds__(TILE_THREADS) void glm_csc_tile_bwd_kernel(
 // ------------------------------------------------------------------------------------------
 // The reference's LinearSVC benchmark visits every 100k-row batch once (maxIter 20 over 10M rows:
 // SGD.java:263-268), so a column-major copy built per batch (radix passes, ~0.25 ms per 6.4M-entry
-// batch) never pays back. Here a round is three launches over the CSR batch as it stands:
-//   count    — per column slice of 2^csb columns (a "bucket"), the batch's entries: LDS histograms,
-//              one device atomic per (block, bucket); the last block scans them into bucket starts
-//              and reservation cursors;
-//   forward  — a block takes RB rows: a G-lane group per row gathers its dot (as glm_csr_fwd_kernel),
-//              loss + multiplier into LDS, then reserves each bucket's run for the block (ONE
-//              device atomic per (block, bucket)) and writes every entry's (column in slice,
-//              m_row·x) into its bucket, staged through LDS in pieces so that each piece's stores
-//              are bucket-sorted runs (coalesced), not 64 random lines per wave instruction;
+// batch) never pays back. Here a round is four launches over the CSR batch as it stands:
+//   count    — a block per forward block (rb rows): its entries per column slice of 2^csb columns
+//              (a "bucket"), an LDS histogram written as one row of the [blocks][nb] count matrix;
+//   scan     — a block per bucket: the column's exclusive prefix over the forward blocks (each
+//              block's first position inside the bucket) and the bucket's total;
+//   forward  — a block takes its rb rows: a G-lane group per row gathers the dot (as
+//              glm_csr_fwd_kernel), loss + multiplier into LDS; then the block's entries, in
+//              pieces of ECAP staged in LDS and sorted there by bucket, are stored as
+//              (column in slice, m_row·x) runs at their exact bucket positions (coalesced; no
+//              device atomics, deterministic placement);
 //   backward — a block takes a chunk of one bucket (contiguous reads), adds it into an LDS slab of
-//              the slice's gradient (ds_add: no device atomics), then applies the SGD update +
-//              regularisation to the slice (1 GPU) or writes its feedback slice (N GPUs); a bucket
-//              of several chunks sums them through float atomics on whole 256-B rows and the last
-//              chunk (arrival ticket) finishes the slice.
+//              the slice's gradient (ds_add), then applies the SGD update + regularisation to the
+//              slice (1 GPU) or writes its feedback slice (N GPUs); a bucket of several chunks sums
+//              them through float atomics on whole 256-B rows and its last chunk finishes it.
 // A device atomic per ENTRY would run at the scattered-atomic rate (~0.08 TB/s: the 472 µs of
-// glm_grad_csr_kernel); per (block, bucket) there are ~100k of them per round. Float LDS atomics
-// make the last bits depend on arrival order: FMLX_DETERMINISTIC=1 keeps the transposed path.
-constexpr int BK_NT = 1024;     // threads of the three kernels
-constexpr int BK_ECAP = 4096;   // forward: entries staged per piece
-constexpr int BK_EPT = BK_ECAP / BK_NT;
+// glm_grad_csr_kernel). The LDS float atomics make the last bits depend on arrival order:
+// FMLX_DETERMINISTIC=1 keeps the transposed path.
+constexpr int BK_NT = 1024;     // threads of the kernels
+// scatter: 512-thread blocks, entries staged per piece (LDS: a column, a value and a row id each;
+// ≤ 36 KiB, so four blocks share a CU — more independent blocks to overlap each one's chain of
+// bookkeeping loads, scans and stores than two 1024-thread ones)
+constexpr int SC_NT = 512;
+template <typename A>
+constexpr int bk_ecap() {
+  return sizeof(A) == 8 ? 2048 : 3584;
+}
 constexpr int BK_NB_MAX = 1024; // buckets
-constexpr int BK_UNROLL = 8;    // backward: entries in flight per thread
+
+// a bucket entry: one 8-byte store in the scatter, one 8-byte load in the backward (fp64: 16 B)
+template <typename A>
+struct BkRec {
+  uint32_t key;
+  A val;
+};
 
 struct BktArgs {
   int csb, nb;     // slice bits, buckets = ceil(d / 2^csb)
   int rb;          // forward rows per block
   int chunk;       // backward entries per work item
-  int* cnt;        // [nb] zero between rounds (the count finisher re-zeroes it)
-  int* off;        // [nb + 1] bucket starts of the round's batch
-  int* cur;        // [nb] reservation cursors
-  int* tick;       // [2] arrival tickets (zero between rounds)
+  int* cntm;       // [slots][fwd blocks][nb] entries per (forward block, bucket)
+  int* offm;       // [slots][fwd blocks][nb] first position of each forward block inside each bucket
+  int* tot;        // [slots][nb] entries per bucket
+  int slots;       // > 0: the counts of batches 0 … slots − 1 were made once for the fit (slot = batch);
+                   // 0: count + scan run in every round, for its batch (slot 0)
+  long mstride;    // elements of one slot of cntm / offm
   int* done;       // [nb] chunk arrivals of multi-chunk buckets (zero between rounds)
-  uint16_t* key;   // [largest batch nnz] column within the slice
-  void* val;       // [largest batch nnz] m_row · x
+  void* rec;       // [largest batch nnz] BkRec<A>: (column within the slice, m_row · x)
   void* acc;       // [d] zero between rounds: partial slices of multi-chunk buckets
-  int dbg;         // (A/B timing: 1 skip reservation, 2 skip pieces, 4 skip histogram)
 };
 
-// exclusive scan of one int per thread over the block (BK_NT threads); *total = the sum
+// exclusive scan of one int per thread over the block (NT threads); *total = the sum
+template <int NT = BK_NT>
 __device__ __forceinline__ int bk_exscan(int v, int* tmp, int* total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int x = v;
@@ -667,197 +680,227 @@ __device__ __forceinline__ int bk_exscan(int v, int* tmp, int* total) {
   if (lane == 63) tmp[w] = x;
   __syncthreads();
   if (w == 0) {
-    int s = lane < BK_NT / 64 ? tmp[lane] : 0;
+    int s = lane < NT / 64 ? tmp[lane] : 0;
 #pragma unroll
-    for (int o = 1; o < BK_NT / 64; o <<= 1) {
+    for (int o = 1; o < NT / 64; o <<= 1) {
       const int t = __shfl_up(s, o, 64);
       if (lane >= o) s += t;
     }
-    if (lane < BK_NT / 64) tmp[lane] = s;
+    if (lane < NT / 64) tmp[lane] = s;
   }
   __syncthreads();
   const int pre = w ? tmp[w - 1] : 0;
-  *total = tmp[BK_NT / 64 - 1];
+  *total = tmp[NT / 64 - 1];
   __syncthreads();  // (tmp is reused by the next scan)
   return pre + x - v;
 }
 
-template <typename A>
+// exclusive scan of v[0..m) into out[0..m) (LDS or global) by the whole block, each thread a run
+// of consecutive values; returns the total
+template <int NT = BK_NT>
+__device__ __forceinline__ int bk_exscan_array(const int* v, int* out, int m, int* tmp) {
+  const int per = (m + NT - 1) / NT;
+  const int q0 = threadIdx.x * per;
+  int mine = 0;
+  for (int i = 0; i < per; ++i) mine += q0 + i < m ? v[q0 + i] : 0;
+  int total;
+  int run = bk_exscan<NT>(mine, tmp, &total);
+  for (int i = 0; i < per; ++i)
+    if (q0 + i < m) {
+      const int c = v[q0 + i];
+      out[q0 + i] = run;
+      run += c;
+    }
+  return total;
+}
+
+__device__ __forceinline__ bool bk_batch(const int* state, long n, long B, long& start, long& end, int& e) {
+  if (!round_running(state, e)) return false;
+  const long P = (n + B - 1) / B;
+  start = (long)(e % P) * B;
+  end = start + B < n ? start + B : n;
+  return true;
+}
+
+// the count / offset slot of round e's batch
+__device__ __forceinline__ long bk_slot(int e, long n, long B, const BktArgs& k) {
+  const long s = k.slots ? (long)(e % ((n + B - 1) / B)) : 0;
+  return s < k.slots ? s : (k.slots ? k.slots - 1 : 0);  // (host-guarded; never an out-of-range slot)
+}
+
+// count / scan: round e's batch (per-round mode), or batch blockIdx.y (the fit's one-time counts)
+__device__ __forceinline__ bool bk_count_batch(const int* state, long n, long B, const BktArgs& k, long& start,
+                                               long& end, long& slot) {
+  if (k.slots) {
+    slot = blockIdx.y;
+    start = slot * B;
+    end = start + B < n ? start + B : n;
+    return start < n;
+  }
+  int e;
+  slot = 0;
+  return bk_batch(state, n, B, start, end, e);
+}
+
 __global__ __launch_bounds__(BK_NT) void glm_bkt_count_kernel(const long* __restrict__ indptr,
                                                               const int* __restrict__ idx, long n, long B,
                                                               const int* __restrict__ state, BktArgs k) {
   extern __shared__ int bk_hist[];  // [nb]
-  __shared__ int tmp[BK_NT / 64];
-  __shared__ int sflag;
-  int e;
-  if (!round_running(state, e)) return;
-  const long P = (n + B - 1) / B;
-  const long start = (long)(e % P) * B;
-  const long end = start + B < n ? start + B : n;
-  const long j0 = indptr[start], j1 = indptr[end];
+  long start, end, slot;
+  if (!bk_count_batch(state, n, B, k, start, end, slot)) return;
+  const long r0 = start + (long)blockIdx.x * k.rb;
+  if (r0 >= end) return;
+  const long r1 = r0 + k.rb < end ? r0 + k.rb : end;
+  const long j0 = indptr[r0], j1 = indptr[r1];
   for (int i = threadIdx.x; i < k.nb; i += BK_NT) bk_hist[i] = 0;
   __syncthreads();
-  const long stride = (long)gridDim.x * BK_NT;
-  long j = j0 + (long)blockIdx.x * BK_NT + threadIdx.x;
-  for (; j + 3 * stride < j1; j += 4 * stride) {
+  long j = j0 + threadIdx.x;
+  for (; j + 3 * BK_NT < j1; j += 4 * BK_NT) {
     int c[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) c[t] = __builtin_nontemporal_load(idx + j + t * stride);
+    for (int t = 0; t < 4; ++t) c[t] = __builtin_nontemporal_load(idx + j + t * BK_NT);
 #pragma unroll
     for (int t = 0; t < 4; ++t) atomicAdd(&bk_hist[c[t] >> k.csb], 1);
   }
-  for (; j < j1; j += stride) atomicAdd(&bk_hist[__builtin_nontemporal_load(idx + j) >> k.csb], 1);
+  for (; j < j1; j += BK_NT) atomicAdd(&bk_hist[__builtin_nontemporal_load(idx + j) >> k.csb], 1);
   __syncthreads();
-  for (int i = threadIdx.x; i < k.nb; i += BK_NT)
-    if (bk_hist[i]) atomicAdd(&k.cnt[i], bk_hist[i]);
-  if (!arrive_last(&k.tick[0], gridDim.x, &sflag)) return;
-  // the last block: bucket starts (each thread a run of consecutive buckets), counts re-zeroed
-  const int per = (k.nb + BK_NT - 1) / BK_NT;
-  const int b0 = threadIdx.x * per;
+  int* row = k.cntm + slot * k.mstride + (long)blockIdx.x * k.nb;
+  for (int i = threadIdx.x; i < k.nb; i += BK_NT) row[i] = bk_hist[i];
+}
+
+// one block per bucket: the column b of the count matrix → each forward block's first position in
+// the bucket, and the bucket's total
+__global__ __launch_bounds__(BK_NT) void glm_bkt_scan_kernel(long n, long B, const int* __restrict__ state,
+                                                             BktArgs k) {
+  extern __shared__ int bk_col[];  // [forward blocks]
+  __shared__ int tmp[BK_NT / 64];
+  long start, end, slot;
+  if (!bk_count_batch(state, n, B, k, start, end, slot)) return;
+  const int nfb = (int)((end - start + k.rb - 1) / k.rb);
+  const int b = blockIdx.x;
+  const int* cm = k.cntm + slot * k.mstride;
+  int* om = k.offm + slot * k.mstride;
+  for (int f = threadIdx.x; f < nfb; f += BK_NT) bk_col[f] = cm[(long)f * k.nb + b];
+  __syncthreads();
+  const int per = (nfb + BK_NT - 1) / BK_NT;
+  const int q0 = threadIdx.x * per;
   int mine = 0;
-  for (int i = 0; i < per; ++i)
-    if (b0 + i < k.nb) {
-      const int c = __hip_atomic_exchange(&k.cnt[b0 + i], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      bk_hist[b0 + i] = c;
-      mine += c;
-    }
+  for (int i = 0; i < per; ++i) mine += q0 + i < nfb ? bk_col[q0 + i] : 0;
   int total;
   int run = bk_exscan(mine, tmp, &total);
   for (int i = 0; i < per; ++i)
-    if (b0 + i < k.nb) {
-      st_agent(&k.off[b0 + i], run);
-      st_agent(&k.cur[b0 + i], run);
-      run += bk_hist[b0 + i];
+    if (q0 + i < nfb) {
+      om[(long)(q0 + i) * k.nb + b] = run;
+      run += bk_col[q0 + i];
     }
-  if (threadIdx.x == 0) {
-    st_agent(&k.off[k.nb], total);
-    st_agent(&k.tick[0], 0);
-  }
+  if (threadIdx.x == 0) k.tot[slot * k.nb + b] = total;
 }
 
+// scatter: after the row-group forward (glm_csr_fwd_kernel: multipliers into `mult`), a block
+// takes its rb rows and writes their entries (column in slice, m_row·x) at exact bucket positions:
+// the count matrix row gives its per-bucket counts (so the staging offsets need no counting pass)
+// and the scan its first position in each bucket; the entries are staged in LDS bucket-sorted
+// (returning integer atomics on per-bucket cursors, a G-lane group per row: no row search), then
+// stored run by run (coalesced). Blocks of more than ECAP entries (long rows) stage in pieces,
+// finding each entry's row by a binary search over the block's row offsets.
 template <typename A, int G>
-__global__ __launch_bounds__(BK_NT) void glm_bkt_fwd_kernel(const long* __restrict__ indptr,
-                                                            const int* __restrict__ idx, const A* __restrict__ val,
-                                                            const A* __restrict__ y, const A* __restrict__ wt,
-                                                            const A* __restrict__ coef, long n, long B, int loss,
-                                                            const int* __restrict__ state, A* __restrict__ wl,
-                                                            BktArgs k) {
-  constexpr int K = G >= 32 ? 2 : 4;
-  constexpr int NG = BK_NT / G;
+__global__ __launch_bounds__(SC_NT) void glm_bkt_scatter_kernel(const long* __restrict__ indptr,
+                                                                const int* __restrict__ idx,
+                                                                const A* __restrict__ val,
+                                                                const A* __restrict__ mult, long n, long B,
+                                                                const int* __restrict__ state, BktArgs k) {
+  constexpr int BK_ECAP = bk_ecap<A>();
+  constexpr int BK_EPT = BK_ECAP / SC_NT;
   extern __shared__ __align__(16) unsigned char bk_smem[];
-  // [nb] hist | base | lcum | ph | pofs, then rp[rb + 1], mrow[rb], scol[ECAP], sval[ECAP]
-  int* hist = reinterpret_cast<int*>(bk_smem);
-  int* base = hist + k.nb;
-  int* lcum = base + k.nb;
-  int* ph = lcum + k.nb;
+  // [nb] base | ph | pofs, then rp[rb + 1], mrow[rb], scol[ECAP], sval[ECAP], srow[ECAP]
+  int* base = reinterpret_cast<int*>(bk_smem);
+  int* ph = base + k.nb;
   int* pofs = ph + k.nb;
   int* rp = pofs + k.nb;
-  A* mrow = reinterpret_cast<A*>(bk_smem + (((5 * (long)k.nb + k.rb + 1) * 4 + 15) & ~15L));
+  A* mrow = reinterpret_cast<A*>(bk_smem + (((3 * (long)k.nb + k.rb + 1) * 4 + 15) & ~15L));
   int* scol = reinterpret_cast<int*>(mrow + k.rb);
   A* sval = reinterpret_cast<A*>(scol + BK_ECAP);
-  __shared__ int tmp[BK_NT / 64];
-  __shared__ A red[2][BK_NT / 64];
+  uint16_t* srow = reinterpret_cast<uint16_t*>(sval + BK_ECAP);
+  __shared__ int tmp[SC_NT / 64];
+  long start, end;
   int e;
-  if (!round_running(state, e)) return;
-  const long P = (n + B - 1) / B;
-  const long start = (long)(e % P) * B;
-  const long end = start + B < n ? start + B : n;
+  if (!bk_batch(state, n, B, start, end, e)) return;
   const long r0 = start + (long)blockIdx.x * k.rb;
   if (r0 >= end) return;  // (the grid covers the largest batch)
   const int nr = end - r0 < k.rb ? (int)(end - r0) : k.rb;
   const long jb = indptr[r0];
+  const long je = indptr[r0 + nr];
   const int tid = threadIdx.x;
-  for (int i = tid; i < k.nb; i += BK_NT) {
-    hist[i] = 0;
-    lcum[i] = 0;
-  }
-  for (int i = tid; i <= nr; i += BK_NT) rp[i] = (int)(indptr[r0 + i] - jb);
-  __syncthreads();
-  // ---- forward: a G-lane group per row (dot, loss, multiplier) + the block's bucket histogram
-  const int lane = tid & (G - 1), grp = tid / G;
   const int csb = k.csb;
-  A wsum = 0, lsum = 0;
-  for (int q = grp; q < nr; q += NG) {
-    const int s0 = rp[q], s1 = rp[q + 1];
-    A s = 0;
-    for (int jq = s0; jq < s1; jq += K * G) {
-      int ii[K];
-      A vv[K];
-#pragma unroll
-      for (int t = 0; t < K; ++t) {
-        const int j = jq + lane + t * G;
-        const bool ok = j < s1;
-        const long jj = jb + (ok ? j : s0);
-        ii[t] = idx[jj];
-        const A v = val[jj];
-        vv[t] = ok ? v : (A)0;
-      }
-#pragma unroll
-      for (int t = 0; t < K; ++t) s += vv[t] * coef[ii[t]];
-#pragma unroll
-      for (int t = 0; t < K; ++t)
-        if (!(k.dbg & 4) && jq + lane + t * G < s1) atomicAdd(&hist[ii[t] >> csb], 1);
-    }
-    s = group_sum<G>(s);
-    if (lane == 0) {
-      const long r = r0 + q;
-      const A ww = wt ? wt[r] : (A)1;
-      A l, m;
-      loss_and_mult(loss, s, y[r], ww, l, m);
-      mrow[q] = m;
-      wsum += ww;
-      lsum += l;
-    }
-  }
-  wsum = wave_sum(wsum);
-  lsum = wave_sum(lsum);
-  if ((tid & 63) == 0) {
-    red[0][tid >> 6] = wsum;
-    red[1][tid >> 6] = lsum;
-  }
-  __syncthreads();
-  // ---- reserve the block's run in every bucket it touches (one device atomic each)
-  for (int i = tid; i < k.nb; i += BK_NT) {
-    const int c = hist[i];
-    base[i] = c && !(k.dbg & 1) ? atomicAdd(&k.cur[i], c) : 0;
-  }
-  if (tid == 0) {
-    A a0 = 0, a1 = 0;
-    for (int i = 0; i < BK_NT / 64; ++i) {
-      a0 += red[0][i];
-      a1 += red[1][i];
-    }
-    A* slot = wl + ((long)(e & 1) * WL_SLOTS + (blockIdx.x & (WL_SLOTS - 1))) * WL_STRIDE;
-    if (a0 != (A)0) atomicAdd(&slot[0], a0);
-    if (a1 != (A)0) atomicAdd(&slot[1], a1);
-  }
-  __syncthreads();
-  // ---- the block's entries in pieces of ECAP: bucket-sorted in LDS, then stored run by run
-  const int E = rp[nr];
   const uint32_t mask = (1u << csb) - 1;
-  A* bval = reinterpret_cast<A*>(k.val);
-  const int per = (k.nb + BK_NT - 1) / BK_NT;
-  for (int p0 = 0; p0 < ((k.dbg & 2) ? 0 : E); p0 += BK_ECAP) {
+  BkRec<A>* brec = reinterpret_cast<BkRec<A>*>(k.rec);
+  const A* __restrict__ mb = mult + (r0 - start);
+  const int E = (int)(je - jb);
+  const bool one = E <= BK_ECAP;
+  // one piece (the common case): the block's entries are requested first, so their latency runs
+  // under the bookkeeping loads and scans below
+  int col[BK_EPT];
+  A pv[BK_EPT];
+  if (one) {
+#pragma unroll
+    for (int u = 0; u < BK_EPT; ++u) {
+      const int t = tid + u * SC_NT;
+      const long j = jb + (t < E ? t : 0);
+      col[u] = __builtin_nontemporal_load(idx + j);
+      pv[u] = __builtin_nontemporal_load(val + j);
+    }
+  }
+  // this block's first position in every bucket: bucket start (scan of the totals) + its offset
+  const long slot = bk_slot(e, n, B, k);
+  bk_exscan_array<SC_NT>(k.tot + slot * k.nb, base, k.nb, tmp);
+  for (int i = tid; i < k.nb; i += SC_NT) base[i] += k.offm[slot * k.mstride + (long)blockIdx.x * k.nb + i];
+  for (int i = tid; i <= nr; i += SC_NT) rp[i] = (int)(indptr[r0 + i] - jb);
+  for (int i = tid; i < nr; i += SC_NT) mrow[i] = mb[i];
+  __syncthreads();
+  if (one) {
+    // every entry's row id into LDS (a thread per row), staging offsets from the count matrix row;
+    // a returning integer atomic on its bucket's cursor gives each entry its staging slot
+    for (int q = tid; q < nr; q += SC_NT)
+      for (int j = rp[q]; j < rp[q + 1]; ++j) srow[j] = (uint16_t)q;
+    bk_exscan_array<SC_NT>(k.cntm + slot * k.mstride + (long)blockIdx.x * k.nb, pofs, k.nb, tmp);
+    __syncthreads();
+    for (int i = tid; i < k.nb; i += SC_NT) ph[i] = pofs[i];
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < BK_EPT; ++u) {
+      const int t = tid + u * SC_NT;
+      if (t < E) {
+        const int slot = atomicAdd(&ph[col[u] >> csb], 1);
+        scol[slot] = col[u];
+        sval[slot] = pv[u] * mrow[srow[t]];
+      }
+    }
+    __syncthreads();
+    for (int t = tid; t < E; t += SC_NT) {
+      const int c = scol[t];
+      const int bk = c >> csb;
+      const long dst = (long)base[bk] + (t - pofs[bk]);
+      brec[dst] = BkRec<A>{(uint32_t)c & mask, sval[t]};
+    }
+    return;
+  }
+  for (int p0 = 0; p0 < E; p0 += BK_ECAP) {
     const int pe = E - p0 < BK_ECAP ? E - p0 : BK_ECAP;
-    for (int i = tid; i < k.nb; i += BK_NT) ph[i] = 0;
+    for (int i = tid; i < k.nb; i += SC_NT) ph[i] = 0;
     __syncthreads();
     int col[BK_EPT], rk[BK_EPT];
     A pv[BK_EPT];
 #pragma unroll
     for (int u = 0; u < BK_EPT; ++u) {
-      const int t = tid + u * BK_NT;
-      col[u] = 0;
-      pv[u] = 0;
-      rk[u] = 0;
-      if (t < pe) {
-        const int j = p0 + t;
-        col[u] = idx[jb + j];
-        pv[u] = val[jb + j];
-      }
+      const int t = tid + u * SC_NT;
+      const int j = p0 + (t < pe ? t : 0);
+      col[u] = idx[jb + j];
+      pv[u] = val[jb + j];
     }
 #pragma unroll
     for (int u = 0; u < BK_EPT; ++u) {
-      const int t = tid + u * BK_NT;
+      const int t = tid + u * SC_NT;
+      rk[u] = 0;
       if (t < pe) {
         const int j = p0 + t;
         int lo = 0, hi = nr;  // the entry's row: rp[lo] <= j < rp[hi]
@@ -870,22 +913,11 @@ __global__ __launch_bounds__(BK_NT) void glm_bkt_fwd_kernel(const long* __restri
       }
     }
     __syncthreads();
-    {  // piece offsets per bucket
-      const int q0 = tid * per;
-      int mine = 0;
-      for (int i = 0; i < per; ++i) mine += q0 + i < k.nb ? ph[q0 + i] : 0;
-      int total;
-      int run = bk_exscan(mine, tmp, &total);
-      for (int i = 0; i < per; ++i)
-        if (q0 + i < k.nb) {
-          pofs[q0 + i] = run;
-          run += ph[q0 + i];
-        }
-    }
+    bk_exscan_array<SC_NT>(ph, pofs, k.nb, tmp);
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < BK_EPT; ++u) {
-      const int t = tid + u * BK_NT;
+      const int t = tid + u * SC_NT;
       if (t < pe) {
         const int slot = pofs[col[u] >> csb] + rk[u];
         scol[slot] = col[u];
@@ -895,19 +927,24 @@ __global__ __launch_bounds__(BK_NT) void glm_bkt_fwd_kernel(const long* __restri
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < BK_EPT; ++u) {
-      const int t = tid + u * BK_NT;
+      const int t = tid + u * SC_NT;
       if (t < pe) {
         const int c = scol[t];
         const int bk = c >> csb;
-        const long dst = (long)base[bk] + lcum[bk] + (t - pofs[bk]);
-        k.key[dst] = (uint16_t)(c & mask);
-        bval[dst] = sval[t];
+        const long dst = (long)base[bk] + (t - pofs[bk]);
+        brec[dst] = BkRec<A>{(uint32_t)c & mask, sval[t]};
       }
     }
     __syncthreads();
-    for (int i = tid; i < k.nb; i += BK_NT) lcum[i] += ph[i];
+    for (int i = tid; i < k.nb; i += SC_NT) base[i] += ph[i];
     // (the next piece's first barrier orders these updates before their reads)
   }
+}
+
+// backward LDS budget: the chunk's values in column order + one counter per slice column
+template <typename A>
+constexpr int bk_chunk() {
+  return sizeof(A) == 8 ? 16384 : 32768;
 }
 
 template <typename A, bool FUSE>
@@ -915,9 +952,16 @@ __global__ __launch_bounds__(BK_NT) void glm_bkt_bwd_kernel(const long* __restri
                                                             int* __restrict__ state, A* __restrict__ wl,
                                                             A* __restrict__ fb, A* __restrict__ coef, int max_iter,
                                                             A tol, A lr, A reg, A en, int weighted, BktArgs k) {
+  // LDS float atomics run ~7x slower than integer ones on gfx950 (scripts/micro_lds_atomic.hip:
+  // 6.4M ds_add_f32 35 µs, ds_add_u32 5 µs), so a chunk is not summed by float atomics into a
+  // slab: it is counting-sorted by column in LDS (integer histogram, scan, returning integer
+  // atomics for the slots), and each column then sums its slots — no float atomics at all.
   extern __shared__ __align__(16) unsigned char bk_smem[];
-  A* slab = reinterpret_cast<A*>(bk_smem);                     // [2^csb]
-  int* iofs = reinterpret_cast<int*>(slab + (1 << k.csb));      // [nb + 1] first item of each bucket
+  A* sv = reinterpret_cast<A*>(bk_smem);                        // [chunk] values, column-sorted
+  int* cc = reinterpret_cast<int*>(sv + k.chunk);               // [2^csb + 1] column counts → starts
+  int* bst = cc + (1 << k.csb) + 1;                              // [nb + 1] bucket starts
+  int* iofs = bst + k.nb + 1;                                    // [nb + 1] first item of each bucket
+  int* nch = iofs + k.nb + 1;                                    // [nb] items of each bucket
   __shared__ int tmp[BK_NT / 64];
   __shared__ int sflag;
   int e;
@@ -939,70 +983,79 @@ __global__ __launch_bounds__(BK_NT) void glm_bkt_bwd_kernel(const long* __restri
     const long end = (b + 1) * B < n ? (b + 1) * B : n;
     W = (A)(end - b * B);
   }
-  // work items: chunks of `chunk` entries of each bucket (at least one per bucket: every column is
-  // updated, regularisation included)
-  const int per = (k.nb + BK_NT - 1) / BK_NT;
-  {
-    const int q0 = threadIdx.x * per;
-    int mine = 0;
-    for (int i = 0; i < per; ++i)
-      if (q0 + i < k.nb) {
-        const int len = k.off[q0 + i + 1] - k.off[q0 + i];
-        mine += len > k.chunk ? (len + k.chunk - 1) / k.chunk : 1;
-      }
-    int total;
-    int r = bk_exscan(mine, tmp, &total);
-    for (int i = 0; i < per; ++i)
-      if (q0 + i < k.nb) {
-        iofs[q0 + i] = r;
-        const int len = k.off[q0 + i + 1] - k.off[q0 + i];
-        r += len > k.chunk ? (len + k.chunk - 1) / k.chunk : 1;
-      }
-    if (threadIdx.x == 0) iofs[k.nb] = total;
+  // bucket starts, then the work items: chunks of `chunk` entries of each bucket (at least one per
+  // bucket: every column is updated, regularisation included)
+  const int* tot = k.tot + bk_slot(e, n, B, k) * k.nb;
+  bst[k.nb] = bk_exscan_array(tot, bst, k.nb, tmp);
+  for (int i = threadIdx.x; i < k.nb; i += BK_NT) {
+    const int len = tot[i];
+    nch[i] = len > k.chunk ? (len + k.chunk - 1) / k.chunk : 1;
   }
+  __syncthreads();
+  iofs[k.nb] = bk_exscan_array(nch, iofs, k.nb, tmp);
   __syncthreads();
   const int T = iofs[k.nb];
   const int CS = 1 << k.csb;
-  const A* __restrict__ bval = reinterpret_cast<const A*>(k.val);
+  const BkRec<A>* __restrict__ brec = reinterpret_cast<const BkRec<A>*>(k.rec);
   A* acc = reinterpret_cast<A*>(k.acc);
+  constexpr int RPT = bk_chunk<A>() / BK_NT;  // records of a chunk per thread, held in registers
   for (int it = blockIdx.x; it < T; it += gridDim.x) {
     int lo = 0, hi = k.nb;  // iofs[lo] <= it < iofs[hi]
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
       if (iofs[mid] <= it) lo = mid; else hi = mid;
     }
-    const int bk = lo, nch = iofs[bk + 1] - iofs[bk], ch = it - iofs[bk];
-    for (int c = threadIdx.x; c < CS; c += BK_NT) slab[c] = (A)0;
-    __syncthreads();
-    const int bo = k.off[bk], be = k.off[bk + 1];
-    const int k0 = bo + ch * k.chunk;
+    const int bk = lo, nc = nch[bk], ch = it - iofs[bk];
+    for (int c = threadIdx.x; c <= CS; c += BK_NT) cc[c] = 0;
+    const int k0 = bst[bk] + ch * k.chunk;
+    const int be = bst[bk + 1];
     const int k1 = k0 + k.chunk < be ? k0 + k.chunk : be;
-    int q = k0 + threadIdx.x;
-    for (; q + (BK_UNROLL - 1) * BK_NT < k1; q += BK_UNROLL * BK_NT) {
-      uint16_t kk[BK_UNROLL];
-      A vv[BK_UNROLL];
+    // the whole chunk into registers (one 8-byte record load per entry, all in flight at once)
+    uint32_t kk[RPT];
+    A vv[RPT];
 #pragma unroll
-      for (int u = 0; u < BK_UNROLL; ++u) {
-        kk[u] = __builtin_nontemporal_load(k.key + q + u * BK_NT);
-        vv[u] = __builtin_nontemporal_load(bval + q + u * BK_NT);
-      }
-#pragma unroll
-      for (int u = 0; u < BK_UNROLL; ++u) atomicAdd(&slab[kk[u]], vv[u]);
+    for (int u = 0; u < RPT; ++u) {
+      const int q = k0 + (int)threadIdx.x + u * BK_NT;
+      const BkRec<A> r = brec[q < k1 ? q : k0];
+      kk[u] = r.key;
+      vv[u] = r.val;
     }
-    for (; q < k1; q += BK_NT) atomicAdd(&slab[k.key[q]], bval[q]);
+    __syncthreads();  // (the counters are zeroed)
+    // pass 1: column histogram of the chunk
+#pragma unroll
+    for (int u = 0; u < RPT; ++u)
+      if (k0 + (int)threadIdx.x + u * BK_NT < k1) atomicAdd(&cc[kk[u]], 1);
     __syncthreads();
+    // column starts (exclusive scan of the counts; cc[c] becomes the column's slot cursor and the
+    // counts are recovered from the next column's start after the scatter)
+    cc[CS] = bk_exscan_array(cc, cc, CS, tmp);
+    __syncthreads();
+    // pass 2: values into their column's slots
+#pragma unroll
+    for (int u = 0; u < RPT; ++u)
+      if (k0 + (int)threadIdx.x + u * BK_NT < k1) sv[atomicAdd(&cc[kk[u]], 1)] = vv[u];
+    __syncthreads();
+    // column c's slots: [end of c − 1, end of c) (cc[c] is now the end of column c)
     const long c0 = (long)bk << k.csb;
     const int cols = d - c0 < CS ? (int)(d - c0) : CS;
-    if (nch == 1) {
+    if (nc == 1) {
       for (int c = threadIdx.x; c < cols; c += BK_NT) {
+        const int j0 = c ? cc[c - 1] : 0, j1 = cc[c];
+        A g = 0;
+        for (int j = j0; j < j1; ++j) g += sv[j];
         if (FUSE)
-          coef[c0 + c] = sgd_apply<A>(coef[c0 + c], slab[c], W, lr, reg, en);
+          coef[c0 + c] = sgd_apply<A>(coef[c0 + c], g, W, lr, reg, en);
         else
-          fb[c0 + c] = slab[c];
+          fb[c0 + c] = g;
       }
     } else {
-      for (int c = threadIdx.x; c < cols; c += BK_NT) atomicAdd(&acc[c0 + c], slab[c]);
-      if (arrive_last(&k.done[bk], nch, &sflag)) {
+      for (int c = threadIdx.x; c < cols; c += BK_NT) {
+        const int j0 = c ? cc[c - 1] : 0, j1 = cc[c];
+        A g = 0;
+        for (int j = j0; j < j1; ++j) g += sv[j];
+        atomicAdd(&acc[c0 + c], g);
+      }
+      if (arrive_last(&k.done[bk], nc, &sflag)) {
         for (int c = threadIdx.x; c < cols; c += BK_NT) {
           const A g = __hip_atomic_exchange(&acc[c0 + c], (A)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (FUSE)
@@ -1210,31 +1263,43 @@ FMLX_API int fmlx_glm_csr_predict(int acc_f64, const long* indptr, const int* id
 }
 
 // ---- single-visit bucket round (glm_bkt_*) ----
-static int g_bkt_dbg = 0;
-FMLX_API void fmlx_glm_bkt_set_debug(int v) { g_bkt_dbg = v; }
 FMLX_API int fmlx_glm_bkt_limits(int* out) {
   out[0] = BK_NT;
-  out[1] = BK_ECAP;
+  out[1] = bk_ecap<float>();
   out[2] = BK_NB_MAX;
+  out[3] = bk_ecap<double>();
+  out[4] = bk_chunk<float>();
+  out[5] = bk_chunk<double>();
+  out[6] = (int)sizeof(BkRec<float>);
+  out[7] = (int)sizeof(BkRec<double>);
   return 0;
 }
 
 static size_t bkt_fwd_lds(const BktArgs& k, size_t es) {
-  return (((5 * (size_t)k.nb + k.rb + 1) * 4 + 15) & ~(size_t)15) + (size_t)k.rb * es + BK_ECAP * (4 + es);
+  return (((3 * (size_t)k.nb + k.rb + 1) * 4 + 15) & ~(size_t)15) + (size_t)k.rb * es +
+         (size_t)(es == 8 ? bk_ecap<double>() : bk_ecap<float>()) * (4 + es + 2);
 }
 
 template <typename A, int G>
 static void launch_bkt_round(const long* indptr, const int* idx, const A* val, const A* y, const A* wt, A* coef,
-                             long n, int d, long B, int loss, int* state, A* wl, A* fb, int fuse, int max_iter, A tol,
-                             A lr, A reg, A en, const BktArgs& k, int bwd_blocks, hipStream_t s) {
-  hipLaunchKernelGGL(glm_bkt_count_kernel<A>, dim3(NUM_CU), dim3(BK_NT), (size_t)k.nb * 4, s, indptr, idx, n, B,
-                     state, k);
+                             long n, int d, long B, int loss, int* state, A* wl, A* fb, A* mult, int fuse,
+                             int max_iter, A tol, A lr, A reg, A en, const BktArgs& k, int bwd_blocks, hipStream_t s) {
   const long rows = B < n ? B : n;
   const int fblocks = (int)((rows + k.rb - 1) / k.rb);
-  hipLaunchKernelGGL((glm_bkt_fwd_kernel<A, G>), dim3(fblocks), dim3(BK_NT), bkt_fwd_lds(k, sizeof(A)), s, indptr, idx,
-                     val, y, wt, (const A*)coef, n, B, loss, state, wl, k);
-  const size_t blds = ((size_t)1 << k.csb) * sizeof(A) + ((size_t)k.nb + 1) * 4;
+  if (!k.slots) {
+    hipLaunchKernelGGL(glm_bkt_count_kernel, dim3(fblocks), dim3(BK_NT), (size_t)k.nb * 4, s, indptr, idx, n, B,
+                       state, k);
+    hipLaunchKernelGGL(glm_bkt_scan_kernel, dim3(k.nb), dim3(BK_NT), (size_t)fblocks * 4, s, n, B, state, k);
+  }
+  long fw = (rows * G + 255) / 256;  // the row-group forward: one row per lane group
+  if (fw > g_csc_fwd_cap) fw = g_csc_fwd_cap;
+  hipLaunchKernelGGL((glm_csr_fwd_kernel<A, G>), dim3((int)fw), dim3(256), 0, s, indptr, idx, val, y, wt,
+                     (const A*)coef, n, B, loss, state, mult, wl);
+  hipLaunchKernelGGL((glm_bkt_scatter_kernel<A, G>), dim3(fblocks), dim3(SC_NT), bkt_fwd_lds(k, sizeof(A)), s, indptr,
+                     idx, val, (const A*)mult, n, B, state, k);
+  const size_t blds = (size_t)k.chunk * sizeof(A) + (((size_t)1 << k.csb) + 1 + 3 * (size_t)k.nb + 2) * 4;
   const int weighted = wt != nullptr;
+  if (blds > (size_t)LDS_PER_CU) return;  // (fmlx_glm_bkt_round checks it first)
   if (fuse)
     hipLaunchKernelGGL((glm_bkt_bwd_kernel<A, true>), dim3(bwd_blocks), dim3(BK_NT), blds, s, indptr, n, d, B, state,
                        wl, fb, coef, max_iter, tol, lr, reg, en, weighted, k);
@@ -1243,32 +1308,56 @@ static void launch_bkt_round(const long* indptr, const int* idx, const A* val, c
                        wl, fb, coef, max_iter, tol, lr, reg, en, weighted, k);
 }
 
+// The fit's one-time counts: count + scan of batches 0 … slots − 1 of the partition in two launches
+// (grid.y = batch), before its first round; the rounds then run forward + scatter + backward only.
+FMLX_API int fmlx_glm_bkt_count_all(const long* indptr, const int* idx, long n, long B, int csb, int nb, int rb,
+                                    int* cntm, int* offm, int* tot, int slots, long mstride, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n <= 0 || B <= 0 || slots < 1 || nb < 1 || nb > BK_NB_MAX || rb < 1) return -2;
+  const long rows = B < n ? B : n;
+  const long fblocks = (rows + rb - 1) / rb;
+  if (fblocks * 4 > 64 * 1024 || mstride < fblocks * nb || (long)slots * B >= n + B) return -3;
+  const BktArgs k{csb, nb, rb, 0, cntm, offm, tot, slots, mstride, nullptr, nullptr, nullptr};
+  hipLaunchKernelGGL(glm_bkt_count_kernel, dim3((int)fblocks, slots), dim3(BK_NT), (size_t)nb * 4, s, indptr, idx, n, B,
+                     (const int*)nullptr, k);
+  hipLaunchKernelGGL(glm_bkt_scan_kernel, dim3(nb, slots), dim3(BK_NT), (size_t)fblocks * 4, s, n, B,
+                     (const int*)nullptr, k);
+  return (int)hipGetLastError();
+}
+
 // One sparse SGD round through column-slice buckets (see glm_bkt_count_kernel …). fuse=1: the
 // backward applies the update + termination (1 GPU); fuse=0: it writes fb[d+2] for the
 // all-reduce and fmlx_glm_update follows. Host-checked: key/val hold the largest batch's entries,
-// acc[d], cnt/done[nb] and tick[2] are zero, off[nb + 1] and cur[nb] exist.
+// cntm/offm hold [ceil(B / rb)][nb], acc[d] and done[nb] are zero, tot[nb] exists.
 FMLX_API int fmlx_glm_bkt_round(int acc_f64, int G, const long* indptr, const int* idx, const void* val,
                                 const void* y, const void* wt, void* coef, long n, int d, long B, int loss, int* state,
                                 void* wl, void* fb, int fuse, int max_iter, double tol, double lr, double reg,
-                                double en, int csb, int rb, int chunk, int* cnt, int* off, int* cur, int* tick,
-                                int* done, void* key, void* bval, void* acc, int bwd_blocks, void* stream) {
+                                double en, int csb, int rb, int chunk, int* cntm, int* offm, int* tot, int slots,
+                                long mstride, int* done, void* rec, void* acc, void* mult, int bwd_blocks,
+                                void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (n <= 0 || B <= 0 || d <= 0) return -2;
   const size_t es = acc_f64 ? 8 : 4;
   if (csb < 1 || csb > 16 || ((size_t)es << csb) > 64 * 1024) return -3;
   const long nb = ((long)d + (1L << csb) - 1) >> csb;
-  if (nb > BK_NB_MAX || rb < BK_NT / G || rb > 4096 || chunk < BK_NT || bwd_blocks < 1) return -4;
-  const BktArgs k{csb, (int)nb, rb, chunk, cnt, off, cur, tick, done, (uint16_t*)key, bval, acc, g_bkt_dbg};
+  const long rows = B < n ? B : n;
+  const long fblocks = (rows + rb - 1) / rb;
+  if (mult == nullptr || nb > BK_NB_MAX || rb < BK_NT / G || rb > 4096 || chunk < BK_NT || bwd_blocks < 1 || fblocks * 4 > 64 * 1024)
+    return -4;
+  if (chunk > (acc_f64 ? bk_chunk<double>() : bk_chunk<float>()) || csb > 12) return -6;
+  if ((size_t)chunk * es + (((size_t)1 << csb) + 1 + 3 * (size_t)nb + 2) * 4 > (size_t)LDS_PER_CU) return -7;
+  if (slots < 0 || mstride < fblocks * nb) return -8;
+  const BktArgs k{csb, (int)nb, rb, chunk, cntm, offm, tot, slots, mstride, done, rec, acc};
   if (bkt_fwd_lds(k, es) > (size_t)LDS_PER_CU / 2) return -5;
 #define FMLX_BKT(GG)                                                                                                  \
   if (acc_f64)                                                                                                        \
     launch_bkt_round<double, GG>(indptr, idx, (const double*)val, (const double*)y, (const double*)wt, (double*)coef,  \
-                                 n, d, B, loss, state, (double*)wl, (double*)fb, fuse, max_iter, tol, lr, reg, en, k, \
-                                 bwd_blocks, s);                                                                      \
+                                 n, d, B, loss, state, (double*)wl, (double*)fb, (double*)mult, fuse, max_iter, tol,  \
+                                 lr, reg, en, k, bwd_blocks, s);                                                                      \
   else                                                                                                                \
     launch_bkt_round<float, GG>(indptr, idx, (const float*)val, (const float*)y, (const float*)wt, (float*)coef, n, d, \
-                                B, loss, state, (float*)wl, (float*)fb, fuse, max_iter, (float)tol, (float)lr,        \
-                                (float)reg, (float)en, k, bwd_blocks, s);
+                                B, loss, state, (float*)wl, (float*)fb, (float*)mult, fuse, max_iter, (float)tol,     \
+                                (float)lr, (float)reg, (float)en, k, bwd_blocks, s);
   switch (G) {
     case 4: FMLX_BKT(4); break;
     case 8: FMLX_BKT(8); break;

@@ -57,13 +57,16 @@ constexpr int GEN_SIZE = GEN_TS + TS_MAX_BLOCKS;
 // the vmcnt drain + workgroup acquire that suffice while every record word moves with
 // system-scope stores/loads on the uncached buffers. The switch for a first run on a topology
 // where the relaxed hand-off has not been validated (GPU tests run in both modes).
-inline int strict_fence() {
-  static const int v = [] {
+// The host may switch the fences on later (fmlx_xar_set_strict_fence: bench.py after an exchange
+// that failed its verification); a Ctx reads the flag when it is built, i.e. per launch.
+inline int& strict_fence_flag() {
+  static int v = [] {
     const char* e = getenv("FMLX_XGMI_STRICT_FENCE");
     return (e && e[0] == '1') ? 1 : 0;
   }();
   return v;
 }
+inline int strict_fence() { return strict_fence_flag(); }
 
 // Kernel-argument bundle. `peers` is a DEVICE array of `world` buffer pointers (mine at `rank`).
 struct Ctx {

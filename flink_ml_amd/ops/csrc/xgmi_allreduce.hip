@@ -189,6 +189,10 @@ FMLX_API int fmlx_host_flags_alloc(int n, void** host_ptr, void** dev_ptr) {
 }
 // 1 when signal_and_wait uses the system-scope fences (FMLX_XGMI_STRICT_FENCE=1)
 FMLX_API int fmlx_xar_strict_fence() { return xgmi::strict_fence(); }
+FMLX_API int fmlx_xar_set_strict_fence(int on) {
+  xgmi::strict_fence_flag() = on != 0;
+  return 0;
+}
 
 FMLX_API int fmlx_host_flags_free(void* h) { return (int)hipHostFree(h); }
 FMLX_API int fmlx_xar_free(void* p) { return (int)hipFree(p); }

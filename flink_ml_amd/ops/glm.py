@@ -842,69 +842,100 @@ class BucketRound:
     their slice's bucket as (column in slice, m_row·x) and summed per slice in LDS by the backward —
     nothing is precomputed per batch, so a fit that visits each batch once (the reference's
     LinearSVC benchmark: SGD.java:263-268 over 100k-row batches) pays no transpose. Buffers: the
-    largest batch's entries (2 + value bytes each), a [d] accumulator for slices summed in several
-    chunks, and O(#slices) counters."""
+    largest batch's entries (an 8-byte (column, value) record each; fp64 16), a [d] accumulator for slices summed in several
+    chunks, and the [forward blocks][slices] count / offset matrices."""
 
-    CHUNK = 32768  # backward entries per work item (a slice of more is summed in chunks)
+    CHUNK = 32768  # backward entries per work item (a slice of more is summed in chunks; fp64: ≤ 16384)
 
-    def __init__(self, indptr, values, n: int, d: int, B: int, G: int):
-        lim = np.zeros(3, dtype=np.int32)
+    SLOT_BYTES_MAX = 256 << 20  # the one-time counts of a fit's batches: at most this much
+
+    def __init__(self, indptr, values, n: int, d: int, B: int, G: int, most: Optional[int] = None,
+                 avg: Optional[float] = None, batches: int = 0):
+        lim = np.zeros(8, dtype=np.int32)
         native.kernels().fmlx_glm_bkt_limits(lim.ctypes.data)
-        nt, _ecap, nb_max = (int(v) for v in lim)
         dev = values.device
         es = values.element_size()
+        nt, nb_max = int(lim[0]), int(lim[2])
+        _ecap = int(lim[3] if es == 8 else lim[1])
+        chunk_max = int(lim[5] if es == 8 else lim[4])
+        rec_bytes = int(lim[7] if es == 8 else lim[6])
         self.G = G
         self.d = d
-        # ~256 slices (the backward's parallelism), at most nb_max, slab ≤ 64 KiB of LDS
+        # ~256 slices (the backward's parallelism), at most nb_max; ≤ 4096 columns per slice (the
+        # backward's column counters share the LDS with a chunk of values)
         csb = max(6, int(math.ceil(math.log2(max(1.0, d / 256.0)))))
-        csb = min(csb, 14 if es == 4 else 13)
+        csb = min(csb, 12)
         self.csb = csb
         self.nb = -(-d // (1 << csb))
         if self.nb > nb_max:
             raise ValueError("too many column slices")
-        nnz, bounds = _batch_bounds(indptr, n, B)
-        most = max(bounds[i + 1] - bounds[i] for i in range(len(bounds) - 1))
-        avg = nnz / max(1, n)
-        # forward rows per block: ~16k entries (4 pieces) — fewer blocks, fewer cursor atomics
-        rb = 1
-        while rb * 2 * max(avg, 1.0) <= 16384 and rb < 2048:
-            rb *= 2
-        self.rb = max(nt // G, rb)
-        self.chunk = self.CHUNK
+        if most is None:
+            nnz, bounds = _batch_bounds(indptr, n, B)
+            most = max(bounds[i + 1] - bounds[i] for i in range(len(bounds) - 1))
+            avg = nnz / max(1, n)
+        # forward rows per block: one staged piece of ECAP entries on average (a multiple of the
+        # lane groups per block)
+        ng = nt // G
+        self.rb = max(ng, min(4096, int(_ecap / max(avg, 1.0))))
+        self.chunk = min(self.CHUNK, chunk_max)
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
-        self.bwd_blocks = max(1, min(2 * cus, self.nb + -(-most // self.chunk)))
+        # one block per CU at most (the chunk fills its LDS); a block loops over the work items, so a
+        # grid of #slices covers evenly loaded slices with one arrival per block
+        self.bwd_blocks = max(1, min(cus, self.nb))
+        fblocks = -(-max(1, min(B, n)) // self.rb)
+        if fblocks * 4 > 64 * 1024:
+            raise ValueError("batch too long for the bucket round's scan")
+        # batches > 0: the fit visits batches 0 … batches − 1; their per-(block, slice) counts and
+        # offsets are made once, before the first round (count_all), when they fit SLOT_BYTES_MAX;
+        # otherwise every round counts its own batch
+        self.mstride = fblocks * self.nb
+        self.slots = batches if 0 < batches and 2 * batches * self.mstride * 4 <= self.SLOT_BYTES_MAX else 0
+        self.counted = False
         i32 = dict(dtype=torch.int32, device=dev)
-        z = native.zeros((2 * self.nb + 2,), torch.int32, dev)
-        self.cnt, self.done, self.tick = z[:self.nb], z[self.nb:2 * self.nb], z[2 * self.nb:]
-        self.off = torch.empty(self.nb + 1, **i32)
-        self.cur = torch.empty(self.nb, **i32)
-        self.key = torch.empty(max(1, most), dtype=torch.int16, device=dev)
-        self.val = torch.empty(max(1, most), dtype=values.dtype, device=dev)
+        S = max(1, self.slots)
+        self.cntm = torch.empty(S * self.mstride, **i32)
+        self.offm = torch.empty(S * self.mstride, **i32)
+        self.tot = torch.empty(S * self.nb, **i32)
+        self.done = native.zeros((self.nb,), torch.int32, dev)
+        self.rec = torch.empty(max(1, most) * rec_bytes, dtype=torch.uint8, device=dev)
         self.acc = native.zeros((d,), values.dtype, dev)
+        self.mult = torch.empty(max(1, min(B, n)), dtype=values.dtype, device=dev)
+
+    def count_all(self, indptr, idx, n: int, B: int) -> None:
+        """The one-time counts of the fit's batches (no-op per round mode / already made)."""
+        if self.slots and not self.counted:
+            native.call("fmlx_glm_bkt_count_all", native.ptr(indptr), native.ptr(idx), n, B, self.csb, self.nb, self.rb,
+                        native.ptr(self.cntm), native.ptr(self.offm), native.ptr(self.tot), self.slots, self.mstride,
+                        native.stream_ptr(idx.device))
+            self.counted = True
 
     @staticmethod
-    def alloc(indptr, values, n: int, d: int, B: int):
-        """A BucketRound, or None where the kernels' limits rule it out (too many slices)."""
+    def alloc(indptr, values, n: int, d: int, B: int, most: Optional[int] = None, avg: Optional[float] = None,
+              batches: int = 0):
+        """A BucketRound, or None where the kernels' limits rule it out (too many slices).
+        ``most`` / ``avg``: the largest batch's entries and the mean row length, when the caller
+        knows them (the out-of-core trainer points one BucketRound at every streamed batch)."""
         if n <= 0 or B <= 0 or d <= 0 or values.device.type != "cuda":
             return None
-        avg = float(indptr[-1]) / max(1, n) if not indptr.is_cuda else None
         if avg is None:
             nnz, _ = _batch_bounds(indptr, n, B)
             avg = nnz / max(1, n)
         try:
-            return BucketRound(indptr, values, n, d, B, BatchCsc.pick_group(avg))
+            return BucketRound(indptr, values, n, d, B, BatchCsc.pick_group(avg), most=most, avg=avg, batches=batches)
         except ValueError:
             return None
 
 
 def bkt_round(bk: BucketRound, indptr, idx, val, y, wt, coef, n, d, B, loss, state, wl, fb, fuse: bool,
               max_iter, tol, lr, reg, en) -> None:
+    if bk.slots and not bk.counted:
+        raise RuntimeError("BucketRound.count_all must run before the first round")
     rc = native.kernels().fmlx_glm_bkt_round(
         int(val.dtype == torch.float64), bk.G, native.ptr(indptr), native.ptr(idx), native.ptr(val), native.ptr(y),
         native.ptr(wt), native.ptr(coef), n, d, B, loss, native.ptr(state), native.ptr(wl), native.ptr(fb), int(fuse),
-        max_iter, float(tol), float(lr), float(reg), float(en), bk.csb, bk.rb, bk.chunk, native.ptr(bk.cnt),
-        native.ptr(bk.off), native.ptr(bk.cur), native.ptr(bk.tick), native.ptr(bk.done), native.ptr(bk.key),
-        native.ptr(bk.val), native.ptr(bk.acc), bk.bwd_blocks, native.stream_ptr(val.device))
+        max_iter, float(tol), float(lr), float(reg), float(en), bk.csb, bk.rb, bk.chunk, native.ptr(bk.cntm),
+        native.ptr(bk.offm), native.ptr(bk.tot), bk.slots, bk.mstride, native.ptr(bk.done), native.ptr(bk.rec),
+        native.ptr(bk.acc), native.ptr(bk.mult), bk.bwd_blocks, native.stream_ptr(val.device))
     if rc != 0:
         raise RuntimeError("fmlx_glm_bkt_round failed: %d" % rc)
 

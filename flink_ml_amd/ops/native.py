@@ -88,12 +88,13 @@ _KERNEL_SIGS = {
                            c_void_p, c_void_p, c_void_p],
     # glm_sparse.hip: single-visit bucket round
     "fmlx_glm_bkt_limits": [c_void_p],
-    "fmlx_glm_bkt_set_debug": ([c_int], None),
     "fmlx_glm_sparse_set_trace": ([c_void_p], None),
     "fmlx_glm_bkt_round": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int,
                            c_long, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double, c_double, c_double,
-                           c_double, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                           c_void_p, c_void_p, c_int, c_void_p],
+                           c_double, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_long, c_void_p,
+                           c_void_p, c_void_p, c_void_p, c_int, c_void_p],
+    "fmlx_glm_bkt_count_all": [c_void_p, c_void_p, c_long, c_long, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                               c_int, c_long, c_void_p],
     # sort.hip
     "fmlx_sorted_bounds": [c_void_p, c_long, c_int, c_void_p, c_void_p],
     "fmlx_seg_sort_scratch": ([c_void_p, c_int, c_int, c_int], c_long),

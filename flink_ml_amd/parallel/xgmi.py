@@ -58,6 +58,7 @@ native.register_kernel_sigs({
                             c_long, c_void_p],
     "fmlx_xar_twoshot_max": ([], c_long),
     "fmlx_xar_strict_fence": [],
+    "fmlx_xar_set_strict_fence": [c_int],
 })
 
 
@@ -65,6 +66,12 @@ def strict_fence() -> bool:
     """True when the exchange's hand-off uses system-scope release/acquire fences
     (``FMLX_XGMI_STRICT_FENCE=1``, read once per process by the kernel library)."""
     return bool(native.kernels().fmlx_xar_strict_fence())
+
+
+def set_strict_fence(on: bool) -> None:
+    """Switches the system-scope fences on / off for every exchange launched from now on (kernels
+    already captured into hipGraphs keep the mode they were captured with)."""
+    native.kernels().fmlx_xar_set_strict_fence(int(bool(on)))
 
 # polls (each ≈ one xGMI round trip + s_sleep) before a wait gives up: several seconds, far
 # beyond any lockstep drift between ranks, far below a hang

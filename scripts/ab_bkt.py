@@ -1,7 +1,6 @@
 """A/B timing of the single-visit sparse bucket round (glm_sparse.hip glm_bkt_*) on the
 north-star SVC shape (1M columns, 64 nnz per row, 100k-row batches): ms per round of a warmed
-trainer, per kernel through events around each of many rounds, for debug variants that skip parts
-of the forward (1: reservation atomics, 2: the bucket writes, 4: the histogram) — timing only."""
+trainer; argv[1]: comma-separated CHUNK sizes of the backward's work items."""
 import json
 import sys
 import time
@@ -14,7 +13,7 @@ sys.path.insert(0, ".")
 
 def main():
     from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer
-    from flink_ml_amd.ops import glm as gk, native
+    from flink_ml_amd.ops import glm as gk
     from flink_ml_amd.table import SparseColumn
 
     dev = torch.device("cuda:0")
@@ -25,10 +24,10 @@ def main():
     vals = torch.rand((n * nnz,), generator=g, device=dev, dtype=torch.float32)
     X = SparseColumn(indptr, idx.reshape(-1), vals, dim)
     y = torch.randint(0, 2, (n,), generator=g, device=dev).to(torch.float32)
-    variants = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["0", "1", "2", "4", "7"])]
+    variants = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else [str(gk.BucketRound.CHUNK)])]
     gk.TILE_MIN_VISITS = 10 ** 9
     for v in variants:
-        native.kernels().fmlx_glm_bkt_set_debug(v)
+        gk.BucketRound.CHUNK = v
         tr = DeviceGlmTrainer(SGD(max_iter=10 ** 8, learning_rate=0.1, global_batch_size=100_000, tol=0.0),
                               np.zeros(dim), X, y, None, "hinge")
         assert tr.bkt is not None
@@ -39,9 +38,10 @@ def main():
         tr.run_rounds(R)
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) * 1e3 / R
-        print(json.dumps({"dbg": v, "ms_per_round": round(ms, 4), "csb": tr.bkt.csb, "nb": tr.bkt.nb, "rb": tr.bkt.rb,
+        print(json.dumps({"chunk": v, "ms_per_round": round(ms, 4), "csb": tr.bkt.csb, "nb": tr.bkt.nb, "rb": tr.bkt.rb,
                           "G": tr.bkt.G, "bwd_blocks": tr.bkt.bwd_blocks}), flush=True)
-    native.kernels().fmlx_glm_bkt_set_debug(0)
+
+
 
 
 if __name__ == "__main__":

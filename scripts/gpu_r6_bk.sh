@@ -1,0 +1,5 @@
+set -o pipefail
+mkdir -p gpurun_out/r6
+timeout -k 10 600 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_glm_sparse_gpu.py -k "bucket or transpose_path or weighted or two_ranks" > gpurun_out/r6/t_bk.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/r6/t_bk.log; [ $rc -eq 0 ] || { grep -E "^E |FAILED" gpurun_out/r6/t_bk.log | head -20; exit $rc; }
+bash scripts/gpu_r6_abprof.sh 32768

@@ -1,0 +1,67 @@
+"""Host-side profile of one warm whole sparse-SVC fit (north-star shard shape, scale 1/8): where the
+Python / runtime time of trainer set-up, launches and read-back goes (cProfile of the 4th fit),
+plus the device span of each fit and a per-phase wall-clock split."""
+import cProfile
+import io
+import json
+import pstats
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+
+
+def main():
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer
+    from flink_ml_amd.table import SparseColumn
+
+    dev = torch.device("cuda:0")
+    n, dim, nnz = 6_250_000, 1_000_000, 64
+    g = torch.Generator(device=dev).manual_seed(7)
+    idx = torch.empty((n, nnz), dtype=torch.int32, device=dev)
+    for s in range(0, n, 1 << 20):
+        e = min(s + (1 << 20), n)
+        idx[s:e] = torch.sort(torch.randint(0, dim, (e - s, nnz), generator=g, device=dev, dtype=torch.int32),
+                              dim=1).values
+    indptr = torch.arange(0, (n + 1) * nnz, nnz, dtype=torch.int64, device=dev)
+    vals = torch.rand((n * nnz,), generator=g, device=dev, dtype=torch.float32)
+    X = SparseColumn(indptr, idx.reshape(-1), vals, dim)
+    y = torch.randint(0, 2, (n,), generator=g, device=dev).to(torch.float32)
+    torch.cuda.synchronize()
+
+    def fit(phases=None):
+        t0 = time.perf_counter()
+        tr = DeviceGlmTrainer(SGD(max_iter=10, learning_rate=0.1, global_batch_size=100_000, tol=0.0), np.zeros(dim),
+                              X, y, None, "hinge")
+        t1 = time.perf_counter()
+        c = tr.fit()
+        t2 = time.perf_counter()
+        if phases is not None:
+            phases.append({"init_ms": round((t1 - t0) * 1e3, 3), "fit_ms": round((t2 - t1) * 1e3, 3)})
+        return c
+
+    phases = []
+    for _ in range(3):
+        fit(phases)
+    # the constructor alone, 20 times (its host time is GPU-idle time at the start of a fit)
+    pr = cProfile.Profile()
+    sgd = SGD(max_iter=10, learning_rate=0.1, global_batch_size=100_000, tol=0.0)
+    for _ in range(20):
+        pr.enable()
+        tr = DeviceGlmTrainer(sgd, np.zeros(dim), X, y, None, "hinge")
+        pr.disable()
+        del tr
+        torch.cuda.synchronize()
+    for _ in range(3):
+        fit(phases)
+    print(json.dumps({"phases": phases}), flush=True)
+    out = io.StringIO()
+    pstats.Stats(pr, stream=out).sort_stats("tottime").print_stats(40)
+    print(out.getvalue())
+
+
+if __name__ == "__main__":
+    main()

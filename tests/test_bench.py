@@ -271,3 +271,52 @@ def test_bench_world_mismatch_and_rank_failure_exit_nonzero():
     # without --dry-run every CPU rank fails ("needs a GPU"): the launcher reports the failure
     r = _bench_cmd("--gpus", "2", "--steps", "1", "--warmup", "0")
     assert r.returncode != 0 and "needs a GPU" in r.stderr
+
+
+class _FakeVerifyTrainer:
+    """Stands in for DeviceGlmTrainer in bench.verify_exchange: its coefficients after k rounds
+    are a fixed function of k (identical on every rank, as a correct exchange gives)."""
+
+    def __init__(self):
+        import types
+
+        self.sgd = types.SimpleNamespace(max_iter=0)
+        self.use_graph = True
+        self.d_model = 6
+        self.coef = torch.zeros(8)
+        self.rccl = False
+
+    def use_rccl(self):
+        self.rccl = True
+
+    def run_rounds(self, k):
+        self.coef += torch.arange(8, dtype=torch.float32) * 0.25 * k
+
+    def flush(self):
+        pass
+
+
+def _verify_worker(rank, world, inject):
+    import os
+
+    import bench
+    from flink_ml_amd.parallel import comm
+
+    if inject is not None:
+        os.environ["FMLX_BENCH_INJECT_EXCHANGE_ERROR"] = str(inject)
+    ok, info = bench.verify_exchange(_FakeVerifyTrainer, comm)
+    return ok, info["replicas_identical"]
+
+
+@pytest.mark.parametrize("inject", [None, 0, 1])
+def test_bench_verify_exchange_detects_a_corrupted_rank(inject):
+    """after the timed region bench.py requires the ranks' replicas to agree bitwise and
+    the exchange to equal the process-group sum; a corruption on any one rank makes EVERY rank
+    report failure (an agreed verdict), so the run exits non-zero instead of printing a number."""
+    from tests.spmd import run_spmd
+
+    res = run_spmd(_verify_worker, 2, inject, timeout=120)
+    if inject is None:
+        assert res == [(True, True), (True, True)]
+    else:
+        assert [r[0] for r in res] == [False, False] and not res[0][1]

@@ -119,3 +119,46 @@ def test_chisq_and_anova_device_match_cpu(kind):
         anr = [[float(x) for x in r] for r in ANOVATest().set_flatten(True).transform(t)[0].rows()]
     assert got == ref
     np.testing.assert_allclose(np.array(an), np.array(anr), rtol=1e-9)
+
+
+def _shard_table(kind, rank, world):
+    t = _nb_table(kind, n=6_000, d=5)
+    X, y = t.column("features").clone(), t.column("label")
+    if kind == "float":
+        X[4000:, 2] = 9.375  # a value only the last rank's rows hold (the union must add it)
+        X[:50, 3] = -0.0
+    cut = [0, 3_500, 6_000] if world == 2 else [0, 6_000]
+    s, e = cut[rank], cut[rank + 1]
+    return Table({"features": X[s:e], "label": y[s:e]}, num_rows=e - s)
+
+
+def _dist_stats_worker(rank, world, kind):
+    from flink_ml_amd.models import ChiSqTest, NaiveBayes
+    from flink_ml_amd.models import naive_bayes, stats
+
+    def keyed_shuffle(*a, **k):  # the torch.unique / argsort keyed-shuffle path must not run on GPUs
+        raise AssertionError("library-op keyed shuffle on a GPU rank")
+
+    stats.value_label_counts = naive_bayes.value_label_counts = keyed_shuffle
+    t = _shard_table(kind, rank, world)
+    chi = [[float(v) for v in r] for r in ChiSqTest().set_flatten(True).transform(t)[0].rows()]
+    nb = NaiveBayes().set_smoothing(0.5).fit(t).get_model_data()[0].rows()[0]
+    theta = [[sorted(m.items()) for m in row] for row in nb[0]]
+    return chi, theta, list(nb[1].values), list(nb[2].values)
+
+
+@pytest.mark.parametrize("kind", ["int", "float"])
+def test_chisq_and_naive_bayes_two_ranks_match_one(kind):
+    """ChiSqTest / NaiveBayes across ranks on the native contingency kernels — the
+    integer table all-reduced, or (general values) the union of the ranks' sorted distinct lists
+    — equal the one-rank result on the whole data."""
+    _need_gpu()
+    from tests.spmd import run_spmd
+
+    env = {"FMLX_DEVICE": "cuda:0", "FMLX_XGMI": "0"}
+    res = run_spmd(_dist_stats_worker, 2, kind, env=env, timeout=300)
+    (one,) = run_spmd(_dist_stats_worker, 1, kind, env=env, timeout=300)
+    for r in res:
+        assert r[0] == one[0]
+        assert r[1] == one[1] and r[3] == one[3]
+        np.testing.assert_allclose(r[2], one[2], rtol=1e-12)

@@ -146,3 +146,122 @@ def test_kmeans_estimator_with_hbm_budget(monkeypatch):
     np.testing.assert_allclose(np.stack([c.values for c in got[0]]), np.stack([c.values for c in ref[0]]),
                                rtol=1e-5, atol=1e-4)
     np.testing.assert_array_equal(got[1].values, ref[1].values)
+
+
+def _csr_host(n, d, seed, max_nnz=30, dtype=torch.float32):
+    from flink_ml_amd.table import SparseColumn
+
+    g = torch.Generator().manual_seed(seed)
+    counts = torch.randint(0, max_nnz + 1, (n,), generator=g)
+    indptr = torch.zeros(n + 1, dtype=torch.int64)
+    indptr[1:] = torch.cumsum(counts, 0)
+    idx = torch.cat([torch.sort(torch.randperm(d, generator=g)[:c]).values for c in counts.tolist()]).to(torch.int32)
+    vals = torch.rand(len(idx), generator=g, dtype=torch.float64).to(dtype)
+    dense = torch.zeros((n, d), dtype=torch.float64)
+    dense[torch.repeat_interleave(torch.arange(n), counts), idx.long()] = vals.double()
+    y = (dense @ torch.linspace(-1, 1, d, dtype=torch.float64) > 0).double()
+    return SparseColumn(indptr, idx, vals, d), dense, y
+
+
+@pytest.mark.parametrize("budget_batches,host_budget", [(0, None), (2, None), (3, 0), (100, None)])
+def test_sparse_batch_store_roundtrip(tmp_path, budget_batches, host_budget):
+    """CSR batches: the resident prefix (one rebased CSR, batches as indptr windows) and the cached
+    / spilled records [indptr | indices | values] reproduce every batch exactly (VERDICT r5 #5)."""
+    from flink_ml_amd.common.outofcore import SparseBatchStore
+
+    X, _, _ = _csr_host(1003, 50, 4)
+    B = 97
+    probe = SparseBatchStore(X, B, "cpu", None)
+    budget = 3 * probe.slot_bytes() + sum(probe.record_bytes(b) for b in range(min(budget_batches, probe.P)))
+    st = SparseBatchStore(X, B, "cpu", budget, host_budget=host_budget, cache_path=str(tmp_path / "c"),
+                          segment_bytes=4096)
+    assert st.P == 11 and st.R == min(11, budget_batches)
+    if host_budget == 0:
+        assert st.stats()["cache_file_bytes"] > 0
+    for b in range(st.P):
+        r0 = b * B
+        if st.is_resident(b):
+            ip, ix, vv = st.resident_view(b)
+            j0 = int(ip[0])
+            ip = ip - j0
+            ix, vv = ix[j0:j0 + int(ip[-1])], vv[j0:j0 + int(ip[-1])]
+        else:
+            buf = torch.empty(max(1, st.slot_bytes()), dtype=torch.uint8)
+            st.cache.read_into(st.record(b), buf)
+            ip, ix, vv = st.view(buf, b)
+        want_ip = X.indptr[r0:r0 + st.rows(b) + 1] - X.indptr[r0]
+        assert torch.equal(ip, want_ip)
+        j0, j1 = int(X.indptr[r0]), int(X.indptr[r0 + st.rows(b)])
+        assert torch.equal(ix, X.indices[j0:j1]) and torch.equal(vv, X.values[j0:j1])
+    st.close()
+
+
+def test_default_hbm_budget_from_free_memory(monkeypatch):
+    """No FMLX_HBM_BUDGET: the budget is the device's free memory minus max(4 GiB, 10 %) (a test
+    hook stands in for hipMemGetInfo), so an oversized partition streams without being asked."""
+    from flink_ml_amd.common import outofcore
+
+    monkeypatch.delenv("FMLX_HBM_BUDGET", raising=False)
+    monkeypatch.setattr(outofcore, "_FREE_OVERRIDE", (100 << 30, 288 << 30))
+    assert outofcore.hbm_budget() == (100 << 30) - int(0.1 * (288 << 30))
+    monkeypatch.setattr(outofcore, "_FREE_OVERRIDE", (5 << 30, 8 << 30))
+    assert outofcore.hbm_budget() == 1 << 30
+    monkeypatch.setenv("FMLX_HBM_BUDGET", "2G")
+    assert outofcore.hbm_budget() == 2 << 30
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("budget_batches,host_budget", [(0, None), (2, 0)])
+def test_streamed_sparse_sgd_matches_in_hbm(budget_batches, host_budget, tmp_path):
+    """Bounded hinge SGD over CSR batches streamed through the ring (bucket round per batch)
+    against the in-HBM sparse trainer on the same data."""
+    _need_gpu()
+    from flink_ml_amd.common import outofcore
+    from flink_ml_amd.common.optimizer import SGD, DeviceGlmTrainer, TorchGlmTrainer
+
+    n, d, B = 20_011, 3_000, 3_000
+    X, dense, y = _csr_host(n, d, 8)
+    sgd = SGD(max_iter=17, learning_rate=0.5, global_batch_size=B, tol=0.0, reg=0.01, elastic_net=0.5)
+    ref = DeviceGlmTrainer(sgd, np.zeros(d), X.to("cuda"), y.cuda(), None, "hinge").fit()
+    host = TorchGlmTrainer(sgd, np.zeros(d), dense, y, None, "hinge").fit()
+    probe = outofcore.SparseBatchStore(X, B, "cpu", None)
+    budget = outofcore.RING_SLOTS * probe.slot_bytes() + sum(probe.record_bytes(b) for b in range(budget_batches))
+    tr = outofcore.StreamedGlmTrainer(sgd, np.zeros(d), X, y.cuda(), None, "hinge", torch.device("cuda"), budget,
+                                      host_budget=host_budget, cache_path=str(tmp_path / "s"), segment_bytes=1 << 20)
+    assert tr.sparse and tr.store.R == budget_batches and tr.ring is not None and tr.inner.bkt is not None
+    got = tr.fit()
+    assert tr.rounds_executed() == 17 and tr.ring.h2d_bytes > 0
+    tr.close()
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(got, host, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_linear_svc_streams_sparse_by_default_budget(monkeypatch):
+    """LinearSVC on a host CSR column larger than the DEFAULT budget (free memory shrunk through the
+    test hook, no FMLX_HBM_BUDGET): the fit streams by itself and matches the in-HBM fit."""
+    _need_gpu()
+    from flink_ml_amd import Table
+    from flink_ml_amd.common import optimizer, outofcore
+    from flink_ml_amd.models import LinearSVC
+
+    monkeypatch.delenv("FMLX_HBM_BUDGET", raising=False)
+    X, _, y = _csr_host(30_000, 2_000, 12)
+    t = Table({"features": X, "label": y}, num_rows=30_000)
+    est = LinearSVC().set_global_batch_size(4000).set_max_iter(9).set_learning_rate(0.2)
+    ref = est.fit(t).get_model_data()[0].rows()[0][0].values
+    used = []
+    real = outofcore.StreamedGlmTrainer
+
+    class Spy(real):
+        def __init__(self, *a, **k):
+            super().__init__(*a, **k)
+            used.append(self.store.stats())
+
+    monkeypatch.setattr(outofcore, "StreamedGlmTrainer", Spy)
+    need = X.indptr.numel() * 8 + X.indices.numel() * 8
+    monkeypatch.setattr(outofcore, "_FREE_OVERRIDE", (outofcore.MARGIN_MIN + need // 3, 288 << 30))
+    monkeypatch.setattr(outofcore, "MARGIN_FRAC", 0.0)
+    got = est.fit(t).get_model_data()[0].rows()[0][0].values
+    assert used and used[0]["sparse"] and used[0]["streamed"] > 0
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
