@@ -220,14 +220,29 @@ class DeviceGlmTrainer:
         c0 = np.asarray(init_coef, dtype=np.float64)
         if c0.shape[0] < self.d:
             c0 = np.concatenate([c0, np.zeros(self.d - c0.shape[0])])
-        if not np.count_nonzero(c0):  # the usual zero init (1M-wide sparse models): no pageable H2D copy
-            # (count_nonzero: ~10x faster than any() on 1M doubles — host time the GPU idles through)
-            self.coef = _dzeros(c0.shape, acc, dev)
-        else:
-            c0 = torch.from_numpy(np.ascontiguousarray(c0)).to(acc)
-            self.coef = (c0.pin_memory() if dev.type == "cuda" else c0).to(dev, non_blocking=True).contiguous()
         self.B = local_batch_size(sgd.global_batch_size, ctx.rank, ctx.world_size)
-        self.state = _dzeros(8, torch.int32, dev)
+        zero_init = not np.count_nonzero(c0)  # the usual zero init (1M-wide sparse models): no pageable
+        # H2D copy (count_nonzero: ~10x faster than any() on 1M doubles — host time the GPU idles through)
+        self._zb = None
+        if (self.sparse and zero_init and dev.type == "cuda" and self.n > 0
+                and (bucket_nnz is not None or self._bucket_pays(sgd))):
+            # the bucket round's zero-initialised buffers — coefficients, round state, feedback,
+            # Σw/Σloss slots, the rounds' slice counters and accumulator — as ONE allocation and ONE
+            # fill launch (a short fit's GPU idles through every Python-side launch)
+            from ..ops import native
+
+            self._zb = native.zeros_many([((self.d,), acc), ((8,), torch.int32), ((self.d + 2,), acc),
+                                          ((gk.wl_elems(),), acc), ((gk.BucketRound.nb_for(self.d),), torch.int32),
+                                          ((self.d,), acc)], dev)
+            self.coef, self.state, self.feedback = self._zb[:3]
+        else:
+            if zero_init:
+                self.coef = _dzeros(c0.shape, acc, dev)
+            else:
+                c0 = torch.from_numpy(np.ascontiguousarray(c0)).to(acc)
+                self.coef = (c0.pin_memory() if dev.type == "cuda" else c0).to(dev, non_blocking=True).contiguous()
+            self.state = _dzeros(8, torch.int32, dev)
+            self.feedback = _dzeros(self.d + 2, acc, dev)
         # running[0] (a fill kernel: `t[i] = scalar` is a blocking pageable copy)
         if dev.type == "cuda":
             from ..ops import native
@@ -235,7 +250,6 @@ class DeviceGlmTrainer:
             native.fill_i32(self.state[1:2], 1)
         else:
             self.state[1:2].fill_(1)
-        self.feedback = _dzeros(self.d + 2, acc, dev)
         self.distributed = ctx.is_distributed
         self.xg = None
         self.csc = None
@@ -253,22 +267,25 @@ class DeviceGlmTrainer:
         if self.sparse:
             self.scratch = None
             self.nparts = 0
+            zb = self._zb
             if bucket_nnz is not None:
                 # (the out-of-core trainer: one batch at a time, every round on the bucket path;
                 # bucket_nnz = (largest batch's entries, mean row length))
                 self.bkt = gk.BucketRound.alloc(self.indptr, self.values, max(1, self.n), self.d, self.B,
-                                                most=bucket_nnz[0], avg=bucket_nnz[1])
+                                                most=bucket_nnz[0], avg=bucket_nnz[1],
+                                                zero_bufs=None if zb is None else (zb[4], zb[5]))
                 if self.bkt is None:
                     raise ValueError("streamed sparse batches need the bucket round (too many column slices)")
-                self.wl = _dzeros(gk.wl_elems(), acc, dev)
+                self.wl = zb[3] if zb is not None else _dzeros(gk.wl_elems(), acc, dev)
             elif dev.type == "cuda" and self.n > 0 and self._bucket_pays(sgd):
                 # each batch visited a few times (the reference's regime): the single-visit round,
                 # nothing built per batch but the column-slice counts of the visited batches
                 P = -(-self.n // max(self.B, 1))
                 self.bkt = gk.BucketRound.alloc(self.indptr, self.values, self.n, self.d, self.B,
-                                                batches=min(P, sgd.max_iter))
+                                                batches=min(P, sgd.max_iter),
+                                                zero_bufs=None if zb is None else (zb[4], zb[5]))
                 if self.bkt is not None:
-                    self.wl = _dzeros(gk.wl_elems(), acc, dev)
+                    self.wl = zb[3] if zb is not None else _dzeros(gk.wl_elems(), acc, dev)
             if self.bkt is None and dev.type == "cuda" and self.n > 0 and self._csc_pays(sgd):
                 # allocated here, batches transposed lazily before the rounds that visit them
                 self.csc = gk.BatchCsc.alloc(self.indptr, self.indices, self.values, self.n, self.d, self.B,

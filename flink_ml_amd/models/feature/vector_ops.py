@@ -113,9 +113,9 @@ def _dct_matrix(n: int) -> torch.Tensor:
 @rw.register_stage
 class DCT(Transformer, HasInputCol, HasOutputCol):
     """Orthonormal DCT-II / DCT-III (JTransforms ``DoubleDCT_1D`` with scaled=true, DCT.java:103-123)
-    as a product with the basis. K17 on the GPU: f32 rows of n ≤ 128 go through the hand-written
-    f32-MFMA kernel with the basis resident in LDS (``ops/csrc/dct.hip``); fp64 (parity mode),
-    wider rows and the CPU take the same product as a plain GEMM."""
+    as a product with the basis. K17 on the GPU: rows of n ≤ 128 go through the hand-written MFMA
+    kernels with the basis resident in LDS (``ops/csrc/dct.hip``: f32, and f64 in parity mode on
+    the f64 MFMA); wider rows and the CPU take the same product as a plain GEMM."""
 
     JAVA_CLASS_NAME = "org.apache.flink.ml.feature.dct.DCT"
     INVERSE = BooleanParam("inverse", "Whether to perform the inverse DCT (true) or forward DCT (false).", False)
@@ -127,7 +127,7 @@ class DCT(Transformer, HasInputCol, HasOutputCol):
         inv = self.get(self.INVERSE)
         dt = torch.float64 if X.dtype == torch.float64 or X.device.type == "cpu" else torch.float32
         Xd = X.to(dt)
-        if Xd.is_cuda and dt == torch.float32 and 1 <= n <= 128:
+        if Xd.is_cuda and 1 <= n <= 128:
             from ...ops.dct import dct_rows
 
             return [t.with_column(self.get(self.OUTPUT_COL), dct_rows(Xd, inv))]

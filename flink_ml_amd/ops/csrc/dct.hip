@@ -1,6 +1,7 @@
 // DCT-II / DCT-III of every row (reference LIB/feature/dct/DCT.java:103-123,
 // JTransforms DoubleDCT_1D scaled): the orthonormal transform Y = X·Mᵀ (forward) or X = Y·M
-// (inverse) of rows of n ≤ 128 f32 values, on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32).
+// (inverse) of rows of n ≤ 128 f32 values, on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32); fp64
+// rows (parity mode) on v_mfma_f64_16x16x4_f64 (dct_rows_f64_kernel).
 //
 // Even/odd butterfly: the basis rows satisfy M[k][n−1−i] = (−1)^k M[k][i], so with h = ⌈n/2⌉
 //   forward   Y[2k']   = Σ_{i<h} u_i M[2k'][i],     u_i = x_i + x_{n−1−i}  (u_mid = x_mid, n odd)
@@ -222,6 +223,92 @@ __global__ __launch_bounds__(DCT_THREADS) void dct_rows_kernel(const float* __re
   }
 }
 
+// fp64 (parity mode: the reference computes in double, DCT.java:103-123): the same even/odd
+// butterfly and basis layout on v_mfma_f64_16x16x4_f64 — one double per lane per A / B fragment,
+// four per lane of each 16 × 16 accumulator (row 4·q + (lane >> 4), column lane & 15: unlike the
+// f32 16x16x4 form, measured by tests/test_dct_gpu.py). Simpler
+// than the f32 kernel (no tile prefetch under the MFMAs): fp64 rows are the exact-parity path.
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+template <int KS, bool INV>
+__global__ __launch_bounds__(DCT_THREADS) void dct_rows_f64_kernel(const double* __restrict__ X, long rows, int n,
+                                                                   const double* __restrict__ basis,
+                                                                   double* __restrict__ Y) {
+  constexpr int NT = (KS + 3) / 4;
+  constexpr int NT8 = (NT + 1) / 2 * 2;
+  constexpr int BHALF = KS * 64 * NT8;  // doubles of one half basis
+  extern __shared__ __align__(16) double smd[];
+  const DctGeom g = dct_geom(n);
+  double* sb = smd;              // half bases [2][KS][4][16][NT8]
+  double* sx = smd + 2 * BHALF;  // tile [64][S]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int i = tid; i < 2 * BHALF; i += DCT_THREADS) sb[i] = basis[i];
+  const long ntiles = (rows + DCT_ROWS - 1) / DCT_ROWS;
+  const int r = lane & 15, hh = lane >> 4;
+  double* wx = sx + (long)(w * 16) * g.S;
+  for (long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const long row0 = t * DCT_ROWS;
+    const int nrows = rows - row0 < DCT_ROWS ? (int)(rows - row0) : DCT_ROWS;
+    __syncthreads();  // (bases in; the previous tile's rows written out)
+    for (int e = tid; e < DCT_ROWS * n; e += DCT_THREADS) {
+      const int rr = e / n, cc = e - rr * n;
+      sx[rr * g.S + cc] = rr < nrows ? X[(row0 + rr) * n + cc] : 0.0;
+    }
+    __syncthreads();
+    double a1[KS], a2[KS];
+    const double* xr = wx + r * g.S;
+#pragma unroll
+    for (int q = 0; q < KS; ++q) {
+      const int kk = 4 * q + hh;
+      if (!INV) {
+        const double lo = kk < g.h ? xr[kk] : 0.0;
+        const double hi = kk < g.ho ? xr[n - 1 - kk] : 0.0;
+        a1[q] = lo + hi;
+        a2[q] = kk < g.ho ? lo - hi : 0.0;
+      } else {
+        a1[q] = kk < g.h ? xr[2 * kk] : 0.0;
+        a2[q] = kk < g.ho ? xr[2 * kk + 1] : 0.0;
+      }
+    }
+    f64x4 c1[NT], c2[NT];
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+      c1[c] = f64x4{0.0, 0.0, 0.0, 0.0};
+      c2[c] = f64x4{0.0, 0.0, 0.0, 0.0};
+    }
+    const double* b1p = sb + (long)(hh * 16 + r) * NT8;
+#pragma unroll
+    for (int q = 0; q < KS; ++q) {
+#pragma unroll
+      for (int c = 0; c < NT; ++c) {
+        c1[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[q], b1p[(long)q * 64 * NT8 + c], c1[c], 0, 0, 0);
+        c2[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2[q], b1p[BHALF + (long)q * 64 * NT8 + c], c2[c], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+      const int o = 16 * c + r;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        double* yr = wx + (4 * q + hh) * g.S;  // (the f64 accumulator: row 4·q + (lane >> 4))
+        if (!INV) {
+          if (o < g.h) yr[2 * o] = c1[c][q];
+          if (o < g.ho) yr[2 * o + 1] = c2[c][q];
+        } else {
+          if (o < g.h) yr[o] = c1[c][q] + c2[c][q];
+          if (o < g.ho) yr[n - 1 - o] = c1[c][q] - c2[c][q];
+        }
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < nrows * n; e += DCT_THREADS) {
+      const int rr = e / n, cc = e - rr * n;
+      Y[(row0 + rr) * n + cc] = sx[rr * g.S + cc];
+    }
+  }
+}
+
 int g_dct_diag = 0;  // diagnostics (fmlx_dct_set_diag): 1 no MFMAs, 2 no tile loads, 4 no stores
 int g_dct_per_cu = 0;  // blocks per CU (0: as many as the LDS allows, at most 4)
 
@@ -299,6 +386,52 @@ FMLX_API int fmlx_dct_rows(const float* X, long rows, int n, const float* basis,
   }
 #undef FMLX_DCT_CASE
 #undef FMLX_DCT_LAUNCH
+  return (int)hipGetLastError();
+}
+
+// fp64 rows (parity mode): Y = DCT-II / DCT-III of X, both double, basis as fmlx_dct_basis_shape
+// (in double)
+FMLX_API int fmlx_dct_rows_f64(const double* X, long rows, int n, const double* basis, double* Y, int inverse,
+                               int num_cu, void* stream) {
+  if (n < 1 || n > DCT_MAXN) return -1;
+  if (rows <= 0) return 0;
+  const DctGeom g = dct_geom(n);
+  const size_t lds = ((size_t)2 * g.KP * 16 * g.NT8 + (size_t)DCT_ROWS * g.S) * sizeof(double);
+  if (lds > 160 * 1024) return -4;
+  const long ntiles = (rows + DCT_ROWS - 1) / DCT_ROWS;
+  long grid = (long)(num_cu > 0 ? num_cu : 256) * ((160 * 1024) / lds >= 2 ? 2 : 1);
+  if (grid > ntiles) grid = ntiles;
+  hipStream_t s = (hipStream_t)stream;
+#define FMLX_DCT64(KSV)                                                                                        \
+  case KSV:                                                                                                    \
+    if (inverse)                                                                                               \
+      hipLaunchKernelGGL((dct_rows_f64_kernel<KSV, true>), dim3((unsigned)grid), dim3(DCT_THREADS), lds, s, X, \
+                         rows, n, basis, Y);                                                                   \
+    else                                                                                                       \
+      hipLaunchKernelGGL((dct_rows_f64_kernel<KSV, false>), dim3((unsigned)grid), dim3(DCT_THREADS), lds, s, X, \
+                         rows, n, basis, Y);                                                                   \
+    break;
+  switch (g.KP / 4) {
+    FMLX_DCT64(1)
+    FMLX_DCT64(2)
+    FMLX_DCT64(3)
+    FMLX_DCT64(4)
+    FMLX_DCT64(5)
+    FMLX_DCT64(6)
+    FMLX_DCT64(7)
+    FMLX_DCT64(8)
+    FMLX_DCT64(9)
+    FMLX_DCT64(10)
+    FMLX_DCT64(11)
+    FMLX_DCT64(12)
+    FMLX_DCT64(13)
+    FMLX_DCT64(14)
+    FMLX_DCT64(15)
+    FMLX_DCT64(16)
+    default:
+      return -3;
+  }
+#undef FMLX_DCT64
   return (int)hipGetLastError();
 }
 

@@ -742,67 +742,64 @@ __device__ __forceinline__ bool bk_count_batch(const int* state, long n, long B,
   return bk_batch(state, n, B, start, end, e);
 }
 
+// count: a block takes CG consecutive forward blocks (their entries are one contiguous range) and
+// writes their per-bucket counts into the bucket-major count matrix [slot][bucket][forward block]
+constexpr int CG = 8;
 __global__ __launch_bounds__(BK_NT) void glm_bkt_count_kernel(const long* __restrict__ indptr,
                                                               const int* __restrict__ idx, long n, long B,
                                                               const int* __restrict__ state, BktArgs k) {
-  extern __shared__ int bk_hist[];  // [nb]
+  extern __shared__ int bk_hist[];  // [CG][nb]
+  __shared__ long jsub[CG + 1];
   long start, end, slot;
   if (!bk_count_batch(state, n, B, k, start, end, slot)) return;
-  const long r0 = start + (long)blockIdx.x * k.rb;
-  if (r0 >= end) return;
-  const long r1 = r0 + k.rb < end ? r0 + k.rb : end;
-  const long j0 = indptr[r0], j1 = indptr[r1];
-  for (int i = threadIdx.x; i < k.nb; i += BK_NT) bk_hist[i] = 0;
+  const int nfb = (int)((end - start + k.rb - 1) / k.rb);
+  const int f0 = blockIdx.x * CG;
+  if (f0 >= nfb) return;
+  const int ns = nfb - f0 < CG ? nfb - f0 : CG;
+  if (threadIdx.x <= ns) {
+    const long r = start + (long)(f0 + threadIdx.x) * k.rb;
+    jsub[threadIdx.x] = indptr[r < end ? r : end];
+  }
+  for (int i = threadIdx.x; i < ns * k.nb; i += BK_NT) bk_hist[i] = 0;
   __syncthreads();
+  const long j0 = jsub[0], j1 = jsub[ns];
   long j = j0 + threadIdx.x;
+  auto sub_of = [&](long jj) {
+    int q = 0;
+#pragma unroll
+    for (int i = 1; i < CG; ++i) q += (i < ns && jsub[i] <= jj) ? 1 : 0;
+    return q;
+  };
   for (; j + 3 * BK_NT < j1; j += 4 * BK_NT) {
     int c[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) c[t] = __builtin_nontemporal_load(idx + j + t * BK_NT);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) atomicAdd(&bk_hist[c[t] >> k.csb], 1);
+    for (int t = 0; t < 4; ++t) atomicAdd(&bk_hist[sub_of(j + t * BK_NT) * k.nb + (c[t] >> k.csb)], 1);
   }
-  for (; j < j1; j += BK_NT) atomicAdd(&bk_hist[__builtin_nontemporal_load(idx + j) >> k.csb], 1);
+  for (; j < j1; j += BK_NT) atomicAdd(&bk_hist[sub_of(j) * k.nb + (__builtin_nontemporal_load(idx + j) >> k.csb)], 1);
   __syncthreads();
-  int* row = k.cntm + slot * k.mstride + (long)blockIdx.x * k.nb;
-  for (int i = threadIdx.x; i < k.nb; i += BK_NT) row[i] = bk_hist[i];
+  int* cm = k.cntm + slot * k.mstride;
+  for (int i = threadIdx.x; i < ns * k.nb; i += BK_NT) {
+    const int q = i / k.nb, b = i - q * k.nb;
+    cm[(long)b * nfb + f0 + q] = bk_hist[i];
+  }
 }
 
-// one block per bucket: the column b of the count matrix → each forward block's first position in
-// the bucket, and the bucket's total
+// one block per bucket: row b of the (bucket-major) count matrix → each forward block's first
+// position in the bucket, and the bucket's total
 __global__ __launch_bounds__(BK_NT) void glm_bkt_scan_kernel(long n, long B, const int* __restrict__ state,
                                                              BktArgs k) {
-  extern __shared__ int bk_col[];  // [forward blocks]
   __shared__ int tmp[BK_NT / 64];
   long start, end, slot;
   if (!bk_count_batch(state, n, B, k, start, end, slot)) return;
   const int nfb = (int)((end - start + k.rb - 1) / k.rb);
   const int b = blockIdx.x;
-  const int* cm = k.cntm + slot * k.mstride;
-  int* om = k.offm + slot * k.mstride;
-  for (int f = threadIdx.x; f < nfb; f += BK_NT) bk_col[f] = cm[(long)f * k.nb + b];
-  __syncthreads();
-  const int per = (nfb + BK_NT - 1) / BK_NT;
-  const int q0 = threadIdx.x * per;
-  int mine = 0;
-  for (int i = 0; i < per; ++i) mine += q0 + i < nfb ? bk_col[q0 + i] : 0;
-  int total;
-  int run = bk_exscan(mine, tmp, &total);
-  for (int i = 0; i < per; ++i)
-    if (q0 + i < nfb) {
-      om[(long)(q0 + i) * k.nb + b] = run;
-      run += bk_col[q0 + i];
-    }
+  const long row = slot * k.mstride + (long)b * nfb;
+  const int total = bk_exscan_array(k.cntm + row, k.offm + row, nfb, tmp);
   if (threadIdx.x == 0) k.tot[slot * k.nb + b] = total;
 }
 
-// scatter: after the row-group forward (glm_csr_fwd_kernel: multipliers into `mult`), a block
-// takes its rb rows and writes their entries (column in slice, m_row·x) at exact bucket positions:
-// the count matrix row gives its per-bucket counts (so the staging offsets need no counting pass)
-// and the scan its first position in each bucket; the entries are staged in LDS bucket-sorted
-// (returning integer atomics on per-bucket cursors, a G-lane group per row: no row search), then
-// stored run by run (coalesced). Blocks of more than ECAP entries (long rows) stage in pieces,
-// finding each entry's row by a binary search over the block's row offsets.
 template <typename A, int G>
 __global__ __launch_bounds__(SC_NT) void glm_bkt_scatter_kernel(const long* __restrict__ indptr,
                                                                 const int* __restrict__ idx,
@@ -853,7 +850,8 @@ __global__ __launch_bounds__(SC_NT) void glm_bkt_scatter_kernel(const long* __re
   // this block's first position in every bucket: bucket start (scan of the totals) + its offset
   const long slot = bk_slot(e, n, B, k);
   bk_exscan_array<SC_NT>(k.tot + slot * k.nb, base, k.nb, tmp);
-  for (int i = tid; i < k.nb; i += SC_NT) base[i] += k.offm[slot * k.mstride + (long)blockIdx.x * k.nb + i];
+  const int nfb = (int)((end - start + k.rb - 1) / k.rb);
+  for (int i = tid; i < k.nb; i += SC_NT) base[i] += k.offm[slot * k.mstride + (long)i * nfb + blockIdx.x];
   for (int i = tid; i <= nr; i += SC_NT) rp[i] = (int)(indptr[r0 + i] - jb);
   for (int i = tid; i < nr; i += SC_NT) mrow[i] = mb[i];
   __syncthreads();
@@ -862,7 +860,9 @@ __global__ __launch_bounds__(SC_NT) void glm_bkt_scatter_kernel(const long* __re
     // a returning integer atomic on its bucket's cursor gives each entry its staging slot
     for (int q = tid; q < nr; q += SC_NT)
       for (int j = rp[q]; j < rp[q + 1]; ++j) srow[j] = (uint16_t)q;
-    bk_exscan_array<SC_NT>(k.cntm + slot * k.mstride + (long)blockIdx.x * k.nb, pofs, k.nb, tmp);
+    for (int i = tid; i < k.nb; i += SC_NT) ph[i] = k.cntm[slot * k.mstride + (long)i * nfb + blockIdx.x];
+    __syncthreads();
+    bk_exscan_array<SC_NT>(ph, pofs, k.nb, tmp);
     __syncthreads();
     for (int i = tid; i < k.nb; i += SC_NT) ph[i] = pofs[i];
     __syncthreads();
@@ -1287,9 +1287,9 @@ static void launch_bkt_round(const long* indptr, const int* idx, const A* val, c
   const long rows = B < n ? B : n;
   const int fblocks = (int)((rows + k.rb - 1) / k.rb);
   if (!k.slots) {
-    hipLaunchKernelGGL(glm_bkt_count_kernel, dim3(fblocks), dim3(BK_NT), (size_t)k.nb * 4, s, indptr, idx, n, B,
-                       state, k);
-    hipLaunchKernelGGL(glm_bkt_scan_kernel, dim3(k.nb), dim3(BK_NT), (size_t)fblocks * 4, s, n, B, state, k);
+    hipLaunchKernelGGL(glm_bkt_count_kernel, dim3((fblocks + CG - 1) / CG), dim3(BK_NT), (size_t)CG * k.nb * 4, s,
+                       indptr, idx, n, B, state, k);
+    hipLaunchKernelGGL(glm_bkt_scan_kernel, dim3(k.nb), dim3(BK_NT), 0, s, n, B, state, k);
   }
   long fw = (rows * G + 255) / 256;  // the row-group forward: one row per lane group
   if (fw > g_csc_fwd_cap) fw = g_csc_fwd_cap;
@@ -1316,12 +1316,11 @@ FMLX_API int fmlx_glm_bkt_count_all(const long* indptr, const int* idx, long n, 
   if (n <= 0 || B <= 0 || slots < 1 || nb < 1 || nb > BK_NB_MAX || rb < 1) return -2;
   const long rows = B < n ? B : n;
   const long fblocks = (rows + rb - 1) / rb;
-  if (fblocks * 4 > 64 * 1024 || mstride < fblocks * nb || (long)slots * B >= n + B) return -3;
+  if (mstride < fblocks * nb || (long)slots * B >= n + B) return -3;
   const BktArgs k{csb, nb, rb, 0, cntm, offm, tot, slots, mstride, nullptr, nullptr, nullptr};
-  hipLaunchKernelGGL(glm_bkt_count_kernel, dim3((int)fblocks, slots), dim3(BK_NT), (size_t)nb * 4, s, indptr, idx, n, B,
-                     (const int*)nullptr, k);
-  hipLaunchKernelGGL(glm_bkt_scan_kernel, dim3(nb, slots), dim3(BK_NT), (size_t)fblocks * 4, s, n, B,
-                     (const int*)nullptr, k);
+  hipLaunchKernelGGL(glm_bkt_count_kernel, dim3((int)((fblocks + CG - 1) / CG), slots), dim3(BK_NT),
+                     (size_t)CG * nb * 4, s, indptr, idx, n, B, (const int*)nullptr, k);
+  hipLaunchKernelGGL(glm_bkt_scan_kernel, dim3(nb, slots), dim3(BK_NT), 0, s, n, B, (const int*)nullptr, k);
   return (int)hipGetLastError();
 }
 
@@ -1342,7 +1341,7 @@ FMLX_API int fmlx_glm_bkt_round(int acc_f64, int G, const long* indptr, const in
   const long nb = ((long)d + (1L << csb) - 1) >> csb;
   const long rows = B < n ? B : n;
   const long fblocks = (rows + rb - 1) / rb;
-  if (mult == nullptr || nb > BK_NB_MAX || rb < BK_NT / G || rb > 4096 || chunk < BK_NT || bwd_blocks < 1 || fblocks * 4 > 64 * 1024)
+  if (mult == nullptr || nb > BK_NB_MAX || rb < 1 || rb > 4096 || chunk < BK_NT || bwd_blocks < 1)
     return -4;
   if (chunk > (acc_f64 ? bk_chunk<double>() : bk_chunk<float>()) || csb > 12) return -6;
   if ((size_t)chunk * es + (((size_t)1 << csb) + 1 + 3 * (size_t)nb + 2) * 4 > (size_t)LDS_PER_CU) return -7;

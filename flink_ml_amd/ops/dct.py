@@ -14,6 +14,7 @@ from .native import c_int, c_long, c_void_p
 native.register_kernel_sigs({
     "fmlx_dct_basis_shape": [c_int, c_void_p, c_void_p],
     "fmlx_dct_rows": [c_void_p, c_long, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "fmlx_dct_rows_f64": [c_void_p, c_long, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p],
 })
 
 
@@ -39,7 +40,7 @@ def dct_matrix(n: int) -> torch.Tensor:
 
 
 @functools.lru_cache(maxsize=64)
-def _padded_basis(n: int, inverse: bool, device: str) -> torch.Tensor:
+def _padded_basis(n: int, inverse: bool, device: str, dtype: torch.dtype = torch.float32) -> torch.Tensor:
     """Both half bases of the even/odd butterfly as the kernel reads its MFMA B fragments:
     [2][KP/4][4][16][nt8], element [p][q][hh][r][c] = B_p[4q + hh][16c + r] with B_p[kk][o] =
     M[2o + p][kk] (forward: k' = o, i = kk) or M[2kk + p][o] (inverse: k' = kk, i = o)."""
@@ -53,20 +54,21 @@ def _padded_basis(n: int, inverse: bool, device: str) -> torch.Tensor:
     for p in (0, 1):
         rows = M[p::2, :h]  # M[2k' + p][i], i < h
         B = rows.t() if not inverse else rows  # forward: [i][k'];  inverse: [k'][i]
-        P = torch.zeros((KP, 16 * NT8), dtype=torch.float32)
-        P[:B.shape[0], :B.shape[1]] = B.to(torch.float32)
+        P = torch.zeros((KP, 16 * NT8), dtype=dtype)
+        P[:B.shape[0], :B.shape[1]] = B.to(dtype)
         halves.append(P.reshape(KP // 4, 4, NT8, 16).permute(0, 1, 3, 2).contiguous())
     return torch.stack(halves).contiguous().to(device)
 
 
 def dct_rows(X: torch.Tensor, inverse: bool = False) -> torch.Tensor:
-    """DCT of every row of a CUDA f32 matrix [rows, n ≤ 128] (exact-f32 MFMA; one read and one
-    write of the rows)."""
+    """DCT of every row of a CUDA f32 or f64 matrix [rows, n ≤ 128] (exact-f32 / f64 MFMA; one
+    read and one write of the rows)."""
     rows, n = X.shape
     X = X.contiguous()
     Y = torch.empty_like(X)
-    B = _padded_basis(n, bool(inverse), str(X.device))
+    f64 = X.dtype == torch.float64
+    B = _padded_basis(n, bool(inverse), str(X.device), torch.float64 if f64 else torch.float32)
     cus = torch.cuda.get_device_properties(X.device).multi_processor_count
-    native.call("fmlx_dct_rows", native.ptr(X), rows, n, native.ptr(B), native.ptr(Y), int(bool(inverse)), cus,
-                native.stream_ptr(X.device))
+    native.call("fmlx_dct_rows_f64" if f64 else "fmlx_dct_rows", native.ptr(X), rows, n, native.ptr(B), native.ptr(Y),
+                int(bool(inverse)), cus, native.stream_ptr(X.device))
     return Y

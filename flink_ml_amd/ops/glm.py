@@ -850,7 +850,7 @@ class BucketRound:
     SLOT_BYTES_MAX = 256 << 20  # the one-time counts of a fit's batches: at most this much
 
     def __init__(self, indptr, values, n: int, d: int, B: int, G: int, most: Optional[int] = None,
-                 avg: Optional[float] = None, batches: int = 0):
+                 avg: Optional[float] = None, batches: int = 0, zero_bufs=None):
         lim = np.zeros(8, dtype=np.int32)
         native.kernels().fmlx_glm_bkt_limits(lim.ctypes.data)
         dev = values.device
@@ -863,8 +863,7 @@ class BucketRound:
         self.d = d
         # ~256 slices (the backward's parallelism), at most nb_max; ≤ 4096 columns per slice (the
         # backward's column counters share the LDS with a chunk of values)
-        csb = max(6, int(math.ceil(math.log2(max(1.0, d / 256.0)))))
-        csb = min(csb, 12)
+        csb = min(12, max(6, int(math.ceil(math.log2(max(1.0, d / 256.0))))))
         self.csb = csb
         self.nb = -(-d // (1 << csb))
         if self.nb > nb_max:
@@ -875,16 +874,13 @@ class BucketRound:
             avg = nnz / max(1, n)
         # forward rows per block: one staged piece of ECAP entries on average (a multiple of the
         # lane groups per block)
-        ng = nt // G
-        self.rb = max(ng, min(4096, int(_ecap / max(avg, 1.0))))
+        self.rb = max(1, min(4096, int(_ecap / max(avg, 1.0))))
         self.chunk = min(self.CHUNK, chunk_max)
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         # one block per CU at most (the chunk fills its LDS); a block loops over the work items, so a
         # grid of #slices covers evenly loaded slices with one arrival per block
         self.bwd_blocks = max(1, min(cus, self.nb))
         fblocks = -(-max(1, min(B, n)) // self.rb)
-        if fblocks * 4 > 64 * 1024:
-            raise ValueError("batch too long for the bucket round's scan")
         # batches > 0: the fit visits batches 0 … batches − 1; their per-(block, slice) counts and
         # offsets are made once, before the first round (count_all), when they fit SLOT_BYTES_MAX;
         # otherwise every round counts its own batch
@@ -896,9 +892,10 @@ class BucketRound:
         self.cntm = torch.empty(S * self.mstride, **i32)
         self.offm = torch.empty(S * self.mstride, **i32)
         self.tot = torch.empty(S * self.nb, **i32)
-        self.done = native.zeros((self.nb,), torch.int32, dev)
+        # (zero_bufs: the caller's one zero-filled allocation for `done` and `acc`)
+        self.done, self.acc = zero_bufs if zero_bufs is not None else \
+            native.zeros_many([((self.nb,), torch.int32), ((d,), values.dtype)], dev)
         self.rec = torch.empty(max(1, most) * rec_bytes, dtype=torch.uint8, device=dev)
-        self.acc = native.zeros((d,), values.dtype, dev)
         self.mult = torch.empty(max(1, min(B, n)), dtype=values.dtype, device=dev)
 
     def count_all(self, indptr, idx, n: int, B: int) -> None:
@@ -910,8 +907,14 @@ class BucketRound:
             self.counted = True
 
     @staticmethod
+    def nb_for(d: int, es: int = 4) -> int:
+        """Column slices of a BucketRound for width d (the size of its `done` counters)."""
+        csb = min(12, max(6, int(math.ceil(math.log2(max(1.0, d / 256.0))))))
+        return -(-d // (1 << csb))
+
+    @staticmethod
     def alloc(indptr, values, n: int, d: int, B: int, most: Optional[int] = None, avg: Optional[float] = None,
-              batches: int = 0):
+              batches: int = 0, zero_bufs=None):
         """A BucketRound, or None where the kernels' limits rule it out (too many slices).
         ``most`` / ``avg``: the largest batch's entries and the mean row length, when the caller
         knows them (the out-of-core trainer points one BucketRound at every streamed batch)."""
@@ -921,7 +924,8 @@ class BucketRound:
             nnz, _ = _batch_bounds(indptr, n, B)
             avg = nnz / max(1, n)
         try:
-            return BucketRound(indptr, values, n, d, B, BatchCsc.pick_group(avg), most=most, avg=avg, batches=batches)
+            return BucketRound(indptr, values, n, d, B, BatchCsc.pick_group(avg), most=most, avg=avg, batches=batches,
+                               zero_bufs=zero_bufs)
         except ValueError:
             return None
 

@@ -247,6 +247,27 @@ def zeros(shape, dtype, device) -> torch.Tensor:
     return t
 
 
+def zeros_many(specs, device):
+    """Several zero-filled device tensors carved out of ONE allocation with ONE fill launch (each
+    launch from Python costs ~15 µs of host time that a short fit's GPU idles through): ``specs`` =
+    [(shape, dtype), ...] → list of tensors (256-byte aligned views)."""
+    offs, total = [], 0
+    for shape, dtype in specs:
+        n = 1
+        for x in (shape if isinstance(shape, (tuple, list)) else (shape,)):
+            n *= int(x)
+        es = torch.empty(0, dtype=dtype).element_size()
+        offs.append((total, n, dtype, shape))
+        total += -(-max(1, n * es) // 256) * 256
+    blob = zeros((total // 4,), torch.int32, device)
+    raw = blob.view(torch.uint8)
+    out = []
+    for off, n, dtype, shape in offs:
+        es = torch.empty(0, dtype=dtype).element_size()
+        out.append(raw[off:off + n * es].view(dtype).reshape(shape))
+    return out
+
+
 def fill_i32(t: torch.Tensor, value: int) -> torch.Tensor:
     """In-place fill of a contiguous int32 CUDA tensor (library kernel)."""
     call("fmlx_fill32", t.data_ptr(), t.numel(), int(value) & 0xFFFFFFFF, stream_ptr(t.device))
