@@ -171,15 +171,6 @@ class TorchGlmTrainer:
         return self.coef.numpy().copy()
 
 
-# sparse trainer: a batch's column-major copy is built when the fit visits each batch at least
-# CSC_BUILD_ROUNDS times or runs at least CSC_MIN_ITERS rounds. Default 0 (always): at the
-# north-star shape (100k × 64-nnz batches, dim 1M) one atomic-scatter round took 3.3 ms against a
-# 0.09 ms column-major round, so transposing a batch pays off even for a single visit
-# (profiles/r3/svc_sparse_shard_fit_atomic.jsonl)
-CSC_BUILD_ROUNDS = float(os.environ.get("FMLX_CSC_BUILD_ROUNDS", "0"))
-CSC_MIN_ITERS = int(os.environ.get("FMLX_CSC_MIN_ITERS", "64"))
-
-
 class DeviceGlmTrainer:
     """HBM-resident SGD on MI355X via the fused HIP kernels (one process per GPU)."""
 
@@ -286,7 +277,7 @@ class DeviceGlmTrainer:
                                                 zero_bufs=None if zb is None else (zb[4], zb[5]))
                 if self.bkt is not None:
                     self.wl = zb[3] if zb is not None else _dzeros(gk.wl_elems(), acc, dev)
-            if self.bkt is None and dev.type == "cuda" and self.n > 0 and self._csc_pays(sgd):
+            if self.bkt is None and dev.type == "cuda" and self.n > 0:
                 # allocated here, batches transposed lazily before the rounds that visit them
                 self.csc = gk.BatchCsc.alloc(self.indptr, self.indices, self.values, self.n, self.d, self.B,
                                              max_rounds=sgd.max_iter)
@@ -379,12 +370,6 @@ class DeviceGlmTrainer:
         P = -(-self.n // max(self.B, 1))
         return sgd.max_iter < gk.TILE_MIN_VISITS * max(P, 1)
 
-    def _csc_pays(self, sgd: SGD) -> bool:
-        """Whether the per-batch column-major copy pays for itself in this fit (a fit that visits
-        each batch fewer than CSC_BUILD_ROUNDS times keeps the atomic-scatter gradient)."""
-        P = -(-self.n // max(self.B, 1))
-        visits = sgd.max_iter / max(P, 1) if P else 0
-        return visits >= CSC_BUILD_ROUNDS or sgd.max_iter >= CSC_MIN_ITERS
     # -- one round as a fixed launch sequence (capturable) -------------------------------------
     def _launch_round(self, rounds: int = 1, ensure: bool = True) -> None:
         """Launches ``rounds`` consecutive rounds (one host call on the fused dense path,

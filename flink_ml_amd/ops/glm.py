@@ -289,10 +289,11 @@ def grad_csr(indptr, idx, val, y, wt, coef, n, d, B, loss, state, grad) -> None:
 
 
 # sparse rounds through per-batch transposes (csrc/glm.hip glm_csc_bwd_kernel)
-CSC_MAX_BYTES = int(os.environ.get("FMLX_CSC_MAX_BYTES", str(8 << 30)))
-CSC_RUN_MAX = int(os.environ.get("FMLX_CSC_RUN_MAX", "16"))  # consecutive batches transposed per sort
+CSC_MAX_BYTES = 8 << 30  # the column-major copies of a partition: at most this much
+CSC_RUN_MAX = 16  # consecutive batches transposed per sort
+TRANSPOSE = True  # False: the transposed layout is never built (the atomic-scatter fallback; tests)
 # fp32 copies over 11–20 column bits: high-bits pass + bucket-local pass (0: two LSD passes + colptr)
-CSC_BUCKET = os.environ.get("FMLX_CSC_BUCKET", "1") != "0"
+CSC_BUCKET = True
 
 
 SEG_SORT_DIGIT_BITS = 10  # radix.hip RS_MAX_DIGIT_BITS
@@ -383,34 +384,34 @@ def _batch_bounds(indptr: torch.Tensor, n: int, B: int):
 
 
 # the column-major copy's packed payload (column low bits above a 22-bit batch row: no key array
-# out of the high-bits pass); FMLX_CSC_PACK=0 forces the unpacked bucket pass (batches > 2^22 rows
+# out of the high-bits pass); CSC_PACK = False forces the unpacked bucket pass (batches > 2^22 rows
 # take it anyway) — tests cover both
-CSC_PACK = os.environ.get("FMLX_CSC_PACK", "1") == "1"
+CSC_PACK = True
 
 
-TILE_HEAVY_DIV = int(os.environ.get("FMLX_CSC_TILE_HEAVY_DIV", "8"))  # heavy column: > ET / this entries
+TILE_HEAVY_DIV = 8  # heavy column: > ET / this entries
 # a fit tiles its batches when it visits each at least this often (the tiling costs about as much
 # as TILE_MIN_VISITS rounds save: ~0.15 ms per 6.4M-entry batch vs ~13 µs per round, svc shape)
-TILE_MIN_VISITS = int(os.environ.get("FMLX_CSC_TILE_MIN_VISITS", "16"))
+TILE_MIN_VISITS = 16
 # fits visiting each batch fewer than TILE_MIN_VISITS times take the single-visit bucket round
 # (BucketRound) instead of any per-batch transpose; BUCKETS = False: the transposed rounds (tests)
 BUCKETS = True
-TILE_SPREAD = os.environ.get("FMLX_CSC_TILE_SPREAD", "1") == "1"  # tile size from the batch and CU count
+TILE_SPREAD = True  # tile size from the batch and CU count
 # the forward over row-block × column-split cells (glm.hip glm_csr_cell_fwd_kernel): float atomics
 # in LDS, so off under FMLX_DETERMINISTIC=1 (the one-row-per-lane-group forward is bit-stable)
-CELLS = os.environ.get("FMLX_CSR_CELLS", "1") == "1"
-CELL_RBB_SET = "FMLX_CSR_CELL_RBB" in os.environ  # rows per row block 2^this ≤ 2^11 (unset: 10 or 11)
-CELL_RBB = int(os.environ.get("FMLX_CSR_CELL_RBB", "10"))
-CELL_SPLITS = int(os.environ.get("FMLX_CSR_CELL_SPLITS", "0"))  # column slices per row block (0: auto)
+CELLS = True
+CELL_RBB = None  # rows per row block 2^this ≤ 2^11 (None: 10 or 11, by the cell shape rules)
+CELL_SPLITS = 0  # column slices per row block (0: auto)
+CSC_TILE = -1  # light-tile entry capacity of the tiled backward (-1: by dtype, 0: untiled layout)
 CELL_LDS_MAX = 128 * 1024  # LDS slots of the largest cell (bytes; larger: the row-group forward)
 
 
 def csc_tile_entries(B: int, f64: bool) -> int:
     """Entry capacity ET of a light column tile of the tiled backward (0 = untiled layout): the
-    LDS slot array of one block (128 KiB: 32768 fp32 / 16384 fp64 slots by default; FMLX_CSC_TILE
+    LDS slot array of one block (128 KiB: 32768 fp32 / 16384 fp64 slots by default; CSC_TILE
     overrides, 0 disables), bounded so that the packed erow (batch row | slot << row bits) fits
     32 bits."""
-    want = int(os.environ.get("FMLX_CSC_TILE", "-1"))
+    want = int(CSC_TILE)
     if want == 0:
         return 0
     least = 16 if want > 0 else 1024  # (small explicit tiles: tests)
@@ -474,7 +475,7 @@ class BatchCsc:
         # column-sorted per cell, packed (column − s·CS) | row-major rank << cb; roff: first entry
         # of every (cell, row); cmax: entries of the largest built cell (the kernel's LDS slots)
         self.cells = self.cmax = 0
-        self.rbb = max(1, min(11, CELL_RBB))  # (_pick_cells)
+        self.rbb = max(1, min(11, CELL_RBB or 10))  # (_pick_cells)
         self.cent = self.cval = self.roff = self.cpart = self.ccnt = None
         if CELLS and not DETERMINISTIC and values.device.type == "cuda" and self.P and d > 0:
             self._pick_cells(values, bounds, n, d, B)
@@ -491,7 +492,7 @@ class BatchCsc:
         es = values.element_size()
         rows = min(B, n)
         fallback = None
-        for rbb in ((CELL_RBB,) if CELL_RBB_SET else (10, 11)):
+        for rbb in ((CELL_RBB,) if CELL_RBB else (10, 11)):
             nrb = -(-rows // (1 << rbb))
             S = CELL_SPLITS if CELL_SPLITS > 0 else max(1, 2 * cus // nrb)
             while True:
@@ -525,7 +526,7 @@ class BatchCsc:
     def alloc(indptr, indices, values, n: int, d: int, B: int, max_rounds: Optional[int] = None):
         """Checks the size limits and returns an (empty) BatchCsc, or None. ``max_rounds``: the
         rounds the fit can run from round 0 (sizes the first allocation)."""
-        if os.environ.get("FMLX_CSR_TRANSPOSE", "1") == "0" or n <= 0 or B <= 0:
+        if not TRANSPOSE or n <= 0 or B <= 0:
             return None
         P = (n + B - 1) // B
         nnz, bounds = _batch_bounds(indptr, n, B)

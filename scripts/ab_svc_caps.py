@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B of the sparse SVC round's layouts — backward: untiled / row-sorted column tiles of ET
-entries (FMLX_CSC_TILE); forward: row-group kernel / row-block × column-split cells with S splits
-(FMLX_CSR_CELLS, FMLX_CSR_CELL_SPLITS) — at the svc_sparse
+entries (glm.CSC_TILE); forward: row-group kernel / row-block × column-split cells with S splits
+(glm.CELLS, glm.CELL_SPLITS) — at the svc_sparse
 shard shape (scale 0.125: 6.25M x 1M, 64 nnz/row, batch 100k): steady
 rounds of a warmed trainer, interleaved repeats. One JSON line per (tile, bwd_cap, repeat). (Round 5 also measured a forward taking 2/4/8 rows per
 lane group: 0.0943-0.0977 ms vs 0.0899 for one row; removed.)"""
@@ -48,12 +48,12 @@ def main():
     if len(sys.argv) > 2 and sys.argv[1] == "--splits":  # e.g. --splits 1 (one config: per-kernel profiles)
         cfgs = [(32768, 8, 1, int(v), 11) for v in sys.argv[2].split(",")]
     for tile, hdiv, spread, splits, rbb in cfgs:
-        os.environ["FMLX_CSC_TILE"] = str(tile)
+        gk.CSC_TILE = tile
         gk.TILE_HEAVY_DIV = hdiv
         gk.TILE_SPREAD = bool(spread)
         gk.CELLS = splits != 0  # the cell forward with this many column splits (0: row-group forward)
         gk.CELL_SPLITS = max(0, splits)  # (-1: the automatic choice)
-        gk.CELL_RBB, gk.CELL_RBB_SET = (rbb or 10), rbb > 0  # (0: the automatic choice)
+        gk.CELL_RBB = rbb or None  # (0: the automatic choice)
         tr = DeviceGlmTrainer(SGD(max_iter=10 ** 8, learning_rate=0.1, global_batch_size=100_000, tol=0.0),
                               np.zeros(dim), X, y, None, "hinge", use_graph=False)
         torch.cuda.synchronize()

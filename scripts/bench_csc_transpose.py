@@ -2,7 +2,7 @@
 """The sparse trainer's column-major copies alone (ops/glm.py BatchCsc) at the SVC run shape:
 ``--batches`` batches of ``--batch`` rows × ``--nnz`` non-zeros over ``--dim`` columns, one run
 (one sort) per iteration on a fresh BatchCsc — ms per run of batches, for A/Bs and rocprofv3
-passes. ``--lsd`` forces the two-LSD-pass path (FMLX_CSC_BUCKET=0)."""
+passes. ``--lsd`` forces the two-LSD-pass path (glm.CSC_BUCKET = False)."""
 import argparse
 import os
 import statistics

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Steady sparse-SVC rounds at the svc_sparse shard shape (6.25M x 1M, 64 nnz/row, batch 100k)
-for kernel traces / counters: one warmed trainer (every batch transposed; FMLX_CSC_TILE picks the
+for kernel traces / counters: one warmed trainer (every batch transposed; glm.CSC_TILE picks the
 backward layout), then ``--rounds`` rounds.
 
   rocprofv3 --kernel-trace --stats -d gpurun_out/prof -- python3 scripts/prof_svc_round.py

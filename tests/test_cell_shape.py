@@ -24,7 +24,6 @@ def _pick(monkeypatch, n, d, B, nnz, cus=256, es=4, splits=0, rbb=None):
     monkeypatch.setattr(torch.cuda, "get_device_properties",
                         lambda dev: types.SimpleNamespace(multi_processor_count=cus))
     monkeypatch.setattr(gk, "CELL_SPLITS", splits)
-    monkeypatch.setattr(gk, "CELL_RBB_SET", rbb is not None)
     if rbb is not None:
         monkeypatch.setattr(gk, "CELL_RBB", rbb)
     c = gk.BatchCsc.__new__(gk.BatchCsc)

@@ -125,7 +125,7 @@ def test_sparse_sgd_fp32_transpose_vs_atomic_and_termination(monkeypatch):
     a = DeviceGlmTrainer(sgd, np.zeros(d), X, y.cuda(), None, "hinge")
     assert a.csc is not None and a.csc.G in (4, 8, 16, 32, 64)
     got = a.fit()
-    monkeypatch.setenv("FMLX_CSR_TRANSPOSE", "0")
+    monkeypatch.setattr(gk, "TRANSPOSE", False)
     b = DeviceGlmTrainer(sgd, np.zeros(d), X, y.cuda(), None, "hinge")
     assert b.csc is None and b.bkt is None
     old = b.fit()
@@ -134,7 +134,7 @@ def test_sparse_sgd_fp32_transpose_vs_atomic_and_termination(monkeypatch):
     assert np.abs(got - ref).max() < 1e-5 * scale
     assert np.abs(old - ref).max() < 1e-5 * scale
     # tol-based termination is decided on the device from the round's loss sum
-    monkeypatch.delenv("FMLX_CSR_TRANSPOSE")
+    monkeypatch.setattr(gk, "TRANSPOSE", True)
     monkeypatch.setattr(gk, "BUCKETS", True)
     sgd2 = SGD(max_iter=200, learning_rate=1.0, global_batch_size=5000, tol=0.3)
     r2 = TorchGlmTrainer(sgd2, np.zeros(d), dense, y, None, "logistic")
@@ -153,6 +153,7 @@ def _sparse_worker(rank, world, path):
     from flink_ml_amd.ops import glm as gk
 
     gk.BUCKETS = path == "bucket"
+    gk.TILE_MIN_VISITS = 0 if path == "tiled" else 10 ** 6
 
     n, d = 1500 + 400 * rank, 300
     indptr, idx, vals, dense, y, w = _csr(n, d, 40 + rank)
@@ -172,8 +173,7 @@ def test_sparse_sgd_two_ranks_one_gpu(path):
     """The feedback path (backward writes the gradient row for the all-reduce): bucket round,
     untiled and tiled transposed rounds."""
     _need_gpu()
-    env = {"FMLX_DEVICE": "cuda:0", "FMLX_XGMI": "0",
-           "FMLX_CSC_TILE_MIN_VISITS": "0" if path == "tiled" else "1000000"}
+    env = {"FMLX_DEVICE": "cuda:0", "FMLX_XGMI": "0"}
     res = run_spmd(_sparse_worker, 2, path, env=env, timeout=300)
     assert res[0][0] < 1e-10 and res[1][0] < 1e-10
     assert res[0][1] == res[1][1]  # replicas identical
@@ -197,7 +197,7 @@ def test_batch_csc_device_transpose_matches_host(run_max, vdtype, d, B, skew, bu
     _need_gpu()
     from flink_ml_amd.ops import glm as gk
 
-    monkeypatch.setenv("FMLX_CSC_TILE", "0")  # the plain column-major layout (tiles: test below)
+    monkeypatch.setattr(gk, "CSC_TILE", 0)  # the plain column-major layout (tiles: test below)
     monkeypatch.setattr(gk, "CSC_RUN_MAX", run_max)
     monkeypatch.setattr(gk, "CSC_BUCKET", bool(bucket))
     monkeypatch.setattr(gk, "CSC_PACK", bucket != "unpacked")
@@ -285,9 +285,9 @@ def test_batch_csc_row_sorted_tiles(vdtype, tile, d, B, monkeypatch):
     indptr = torch.zeros(n + 1, dtype=torch.int64)
     indptr[1:] = torch.cumsum(torch.tensor([len(r) for r in rows]), 0)
     vals = torch.rand(int(indptr[-1]), generator=g, dtype=torch.float64).to(vdtype)
-    monkeypatch.setenv("FMLX_CSC_TILE", "0")
+    monkeypatch.setattr(gk, "CSC_TILE", 0)
     plain = gk.BatchCsc.build(indptr.cuda(), idx.cuda(), vals.cuda(), n, d, B)
-    monkeypatch.setenv("FMLX_CSC_TILE", str(tile))
+    monkeypatch.setattr(gk, "CSC_TILE", tile)
     monkeypatch.setattr(gk, "TILE_MIN_VISITS", 0)
     csc = gk.BatchCsc.alloc(indptr.cuda(), idx.cuda(), vals.cuda(), n, d, B, max_rounds=3)
     assert csc.ET == (tile if tile > 0 else (16384 if vdtype == torch.float64 else 32768))
@@ -323,7 +323,6 @@ def test_batch_csr_forward_cells(vdtype, d, B, S, rbb, monkeypatch):
     monkeypatch.setattr(gk, "CELLS", True)
     monkeypatch.setattr(gk, "CELL_SPLITS", S)
     monkeypatch.setattr(gk, "CELL_RBB", rbb)
-    monkeypatch.setattr(gk, "CELL_RBB_SET", True)
     g = torch.Generator().manual_seed(5)
     n = 12_345
     lens = torch.randint(0, 12, (n,), generator=g)
@@ -389,7 +388,7 @@ def test_sparse_sgd_tiled_backward_matches_host(tile, vdtype, cells, monkeypatch
     indptr, idx, vals, dense, y, w = _csr(n, d, 21, max_nnz=60, dtype=vdtype)
     from flink_ml_amd.ops import glm as gk
 
-    monkeypatch.setenv("FMLX_CSC_TILE", str(tile))
+    monkeypatch.setattr(gk, "CSC_TILE", tile)
     monkeypatch.setattr(gk, "TILE_MIN_VISITS", 0)
     monkeypatch.setattr(gk, "CELLS", bool(cells))
     if cells is not True and cells:
