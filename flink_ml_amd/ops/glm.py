@@ -837,6 +837,19 @@ def csc_round(csc: BatchCsc, indptr, idx, val, y, wt, coef, n, d, B, loss, state
                 native.ptr(csc.cpart), native.ptr(csc.ccnt), native.stream_ptr(val.device))
 
 
+_BKT_LIMITS = None
+
+
+def _bkt_limits():
+    """The bucket round kernels' compile-time limits (csrc/glm_sparse.hip fmlx_glm_bkt_limits), read once."""
+    global _BKT_LIMITS
+    if _BKT_LIMITS is None:
+        lim = np.zeros(8, dtype=np.int32)
+        native.kernels().fmlx_glm_bkt_limits(lim.ctypes.data)
+        _BKT_LIMITS = lim
+    return _BKT_LIMITS
+
+
 class BucketRound:
     """Device buffers of the single-visit sparse round (csrc/glm_sparse.hip glm_bkt_*): per round,
     the batch's entries are counted per column slice of 2^csb columns, written by the forward into
@@ -852,8 +865,7 @@ class BucketRound:
 
     def __init__(self, indptr, values, n: int, d: int, B: int, G: int, most: Optional[int] = None,
                  avg: Optional[float] = None, batches: int = 0, zero_bufs=None):
-        lim = np.zeros(8, dtype=np.int32)
-        native.kernels().fmlx_glm_bkt_limits(lim.ctypes.data)
+        lim = _bkt_limits()
         dev = values.device
         es = values.element_size()
         nt, nb_max = int(lim[0]), int(lim[2])

@@ -43,7 +43,7 @@ def to_host(t: torch.Tensor) -> torch.Tensor:
     return out
 
 
-WARM_PINNED_BYTES = 64 << 20
+WARM_PINNED_BYTES = 64 << 20  # (plus one block of each smaller power-of-two size, see warm)
 
 
 def warm(device=None) -> None:
@@ -61,3 +61,9 @@ def warm(device=None) -> None:
     buf[:16].copy_(d[:16], non_blocking=True)
     wait_stream(dev)
     del buf, d
+    # torch's caching host allocator keeps freed pinned blocks per power-of-two size and does not
+    # split a larger one for a smaller request: one block of every read-back size up to 64 MiB
+    # (a 1M-wide fp64 coefficient vector is 8 MiB: its first read-back paid a ~1 ms hipHostMalloc
+    # inside the first fit, profiles/r6 svc fit timeline)
+    keep = [torch.empty(1 << b, dtype=torch.uint8, pin_memory=True) for b in range(12, 27)]
+    del keep
