@@ -35,6 +35,9 @@ from ..parallel.context import device_sharers, get_context
 from ..table import SparseColumn
 from ..utils import graphs, hostsync, tracing
 
+# bucket-round fits shorter than this launch their rounds directly instead of capturing hipGraphs
+BKT_GRAPH_MIN_ITERS = 200
+
 
 def _dzeros(shape, dtype, dev) -> torch.Tensor:
     """Zero-filled device buffers of the trainers through the library's own fill kernel (torch's
@@ -225,7 +228,7 @@ class DeviceGlmTrainer:
             from ..ops import native
 
             self._zb = native.zeros_many([((self.d,), acc), ((8,), torch.int32), ((self.d + 2,), acc),
-                                          ((gk.wl_elems(),), acc), ((gk.BucketRound.nb_for(self.d),), torch.int32),
+                                          ((gk.wl_elems(),), acc), ((gk.BucketRound.nb_for(self.d) + 16,), torch.int32),
                                           ((self.d,), acc)], dev)
             self.coef, self.state, self.feedback = self._zb[:3]
         else:
@@ -342,6 +345,7 @@ class DeviceGlmTrainer:
         self.cw = _dzeros((2, self.d), acc, dev) if self.defer else None
         self._flushed = False
         self._short = False  # fit(): too few rounds for hipGraph capture to pay (direct launches)
+        self.bkt_graph_min_iters = BKT_GRAPH_MIN_ITERS
         self.graphs = {}
         self.timing = False
         self.check_every = max(1, int(check_every))
@@ -650,6 +654,11 @@ class DeviceGlmTrainer:
         # a fit shorter than two graphs' worth of rounds launches directly: capture + first replay
         # (~1 ms per graph) would cost more than the launches it saves
         if not self.graphs and self.sgd.max_iter < 2 * self.rounds_per_graph:
+            self._short = True
+        if self.bkt is not None and not self.graphs and self.sgd.max_iter < self.bkt_graph_min_iters:
+            # the bucket round's three launches take less host time than their GPU time
+            # (~0.1 ms at 100k rows); the process's first capture + instantiate costs ~18 ms
+            # (SVC 20-round first fit 22.2 ms with graphs, profiles/r6/INDEX.md)
             self._short = True
         if self.csc is not None:
             # every batch this fit visits in one go: one sort per run of up to CSC_RUN_MAX batches

@@ -995,7 +995,7 @@ __global__ __launch_bounds__(BK_NT) void glm_bkt_bwd_kernel(const long* __restri
   iofs[k.nb] = bk_exscan_array(nch, iofs, k.nb, tmp);
   __syncthreads();
   const int T = iofs[k.nb];
-  const int CS = 1 << k.csb;
+  const int CS = 1 << k.csb;  // ≤ 4 · BK_NT (host-checked csb ≤ 12)
   const BkRec<A>* __restrict__ brec = reinterpret_cast<const BkRec<A>*>(k.rec);
   A* acc = reinterpret_cast<A*>(k.acc);
   constexpr int RPT = bk_chunk<A>() / BK_NT;  // records of a chunk per thread, held in registers
@@ -1007,6 +1007,18 @@ __global__ __launch_bounds__(BK_NT) void glm_bkt_bwd_kernel(const long* __restri
     }
     const int bk = lo, nc = nch[bk], ch = it - iofs[bk];
     for (int c = threadIdx.x; c <= CS; c += BK_NT) cc[c] = 0;
+    // the slice's coefficients this thread updates, requested now (their latency runs under the
+    // chunk's loads and the LDS sort); CS / BK_NT ≤ 4 columns per thread
+    const long c0 = (long)bk << k.csb;
+    const int cols = d - c0 < CS ? (int)(d - c0) : CS;
+    A wold[4];
+    if (FUSE && nc == 1) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = (int)threadIdx.x + u * BK_NT;
+        wold[u] = c < cols ? coef[c0 + c] : (A)0;
+      }
+    }
     const int k0 = bst[bk] + ch * k.chunk;
     const int be = bst[bk + 1];
     const int k1 = k0 + k.chunk < be ? k0 + k.chunk : be;
@@ -1036,15 +1048,16 @@ __global__ __launch_bounds__(BK_NT) void glm_bkt_bwd_kernel(const long* __restri
       if (k0 + (int)threadIdx.x + u * BK_NT < k1) sv[atomicAdd(&cc[kk[u]], 1)] = vv[u];
     __syncthreads();
     // column c's slots: [end of c − 1, end of c) (cc[c] is now the end of column c)
-    const long c0 = (long)bk << k.csb;
-    const int cols = d - c0 < CS ? (int)(d - c0) : CS;
     if (nc == 1) {
-      for (int c = threadIdx.x; c < cols; c += BK_NT) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = (int)threadIdx.x + u * BK_NT;
+        if (c >= cols) break;
         const int j0 = c ? cc[c - 1] : 0, j1 = cc[c];
         A g = 0;
         for (int j = j0; j < j1; ++j) g += sv[j];
         if (FUSE)
-          coef[c0 + c] = sgd_apply<A>(coef[c0 + c], g, W, lr, reg, en);
+          coef[c0 + c] = sgd_apply<A>(wold[u], g, W, lr, reg, en);
         else
           fb[c0 + c] = g;
       }
@@ -1073,11 +1086,23 @@ __global__ __launch_bounds__(BK_NT) void glm_bkt_bwd_kernel(const long* __restri
     fb[d + 1] = L;
   }
   if (FUSE) {
+    // two-level arrival (a single counter serialises every block's ticket, ~11 ns each): the last
+    // block of each group of blocks ≡ g (mod 8) draws a top ticket; the last top one finishes
     __shared__ int last;
     __syncthreads();
-    if (threadIdx.x == 0)
-      last = __hip_atomic_fetch_add(&state[ST_ARRIVE], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-             (int)gridDim.x - 1;
+    if (threadIdx.x == 0) {
+      int* grp = k.done + k.nb;  // [8] group tickets, [8] the top ticket (zero between rounds)
+      const int g = blockIdx.x & 7;
+      const int gs = ((int)gridDim.x - g + 7) >> 3;  // blocks of group g
+      const int ng = gridDim.x < 8 ? (int)gridDim.x : 8;
+      bool top = __hip_atomic_fetch_add(&grp[g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gs - 1;
+      if (top) {
+        st_agent(&grp[g], 0);  // (every block of the group has drawn; re-armed for the next round)
+        top = __hip_atomic_fetch_add(&grp[8], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+        if (top) st_agent(&grp[8], 0);
+      }
+      last = top;
+    }
     __syncthreads();
     if (last) {  // every other block has finished its reads of the state words
       A w2;
@@ -1087,7 +1112,6 @@ __global__ __launch_bounds__(BK_NT) void glm_bkt_bwd_kernel(const long* __restri
         state[ST_RUN0 + ((e + 1) & 1)] = cont ? 1 : 0;
         state[ST_EXECUTED] += 1;
         state[ST_ROUND] = e + 1;
-        state[ST_ARRIVE] = 0;
       }
     }
   }

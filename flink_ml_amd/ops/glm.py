@@ -906,8 +906,9 @@ class BucketRound:
         self.offm = torch.empty(S * self.mstride, **i32)
         self.tot = torch.empty(S * self.nb, **i32)
         # (zero_bufs: the caller's one zero-filled allocation for `done` and `acc`)
+        # done: [nb] chunk arrivals, then the backward's [8] group + [1] top arrival tickets
         self.done, self.acc = zero_bufs if zero_bufs is not None else \
-            native.zeros_many([((self.nb,), torch.int32), ((d,), values.dtype)], dev)
+            native.zeros_many([((self.nb + 16,), torch.int32), ((d,), values.dtype)], dev)
         self.rec = torch.empty(max(1, most) * rec_bytes, dtype=torch.uint8, device=dev)
         self.mult = torch.empty(max(1, min(B, n)), dtype=values.dtype, device=dev)
 
@@ -921,7 +922,7 @@ class BucketRound:
 
     @staticmethod
     def nb_for(d: int, es: int = 4) -> int:
-        """Column slices of a BucketRound for width d (the size of its `done` counters)."""
+        """Column slices of a BucketRound for width d (its `done` counters: this + 16)."""
         csb = min(12, max(6, int(math.ceil(math.log2(max(1.0, d / 256.0))))))
         return -(-d // (1 << csb))
 

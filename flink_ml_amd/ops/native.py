@@ -218,6 +218,13 @@ def _preload(lib) -> None:
             raise RuntimeError("warming the sparse round kernels failed")
         torch.cuda.current_stream().synchronize()
     torch.cuda.get_device_properties(torch.cuda.current_device())  # (first call: runtime queries)
+    # one device segment for torch's caching allocator, freed at once: the trainers' buffers of a
+    # first fit are then carved out of it instead of each new size paying a hipMalloc inside the fit
+    # (a 20-round sparse fit's first allocation took ~15 ms, profiles/r6/INDEX.md)
+    pool = int(os.environ.get("FMLX_DEVICE_POOL_MB", "2048")) << 20
+    if pool > 0:
+        seg = torch.empty(pool, dtype=torch.uint8, device=torch.cuda.current_device())
+        del seg
     PRELOAD_MS = (time.perf_counter() - t0) * 1e3
     PRELOAD_MS = (time.perf_counter() - t0) * 1e3
     PRELOAD_OBJECTS = k

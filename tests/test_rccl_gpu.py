@@ -42,6 +42,7 @@ def _fit_svc_sparse(graph: bool):
     sgd = SGD(max_iter=12, learning_rate=0.1, global_batch_size=4_000, tol=0.0)
     tr = DeviceGlmTrainer(sgd, np.zeros(X.size), X, y.cuda(), None, "hinge", use_graph=graph)
     tr.rounds_per_graph = 4
+    tr.bkt_graph_min_iters = 0  # capture even this short bucket-round fit
     coef = tr.fit()
     return tr, coef
 
