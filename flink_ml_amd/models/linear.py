@@ -81,7 +81,7 @@ def _run_sgd(est, X, y, w, loss: str) -> np.ndarray:
         X = X.reshape(0, d)
     sgd = SGD(est.get(est.MAX_ITER), est.get(est.LEARNING_RATE), est.get(est.GLOBAL_BATCH_SIZE), est.get(est.TOL),
               est.get(est.REG), est.get(est.ELASTIC_NET))
-    return sgd.optimize(np.zeros(d), X, y, w, loss)
+    return sgd.optimize(None, X, y, w, loss)  # (None: the zero initial model, LinearSVC.java:86-97)
 
 
 def _coef_tensor(rows):

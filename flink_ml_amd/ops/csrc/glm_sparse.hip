@@ -617,23 +617,25 @@ __global__ __launch_bounds__(TILE_THREADS) void glm_csc_tile_bwd_kernel(
 // ------------------------------------------------------------------------------------------
 // The reference's LinearSVC benchmark visits every 100k-row batch once (maxIter 20 over 10M rows:
 // SGD.java:263-268), so a column-major copy built per batch (radix passes, ~0.25 ms per 6.4M-entry
-// batch) never pays back. Here a round is four launches over the CSR batch as it stands:
-//   count    — a block per forward block (rb rows): its entries per column slice of 2^csb columns
-//              (a "bucket"), an LDS histogram written as one row of the [blocks][nb] count matrix;
-//   scan     — a block per bucket: the column's exclusive prefix over the forward blocks (each
-//              block's first position inside the bucket) and the bucket's total;
-//   forward  — a block takes its rb rows: a G-lane group per row gathers the dot (as
-//              glm_csr_fwd_kernel), loss + multiplier into LDS; then the block's entries, in
-//              pieces of ECAP staged in LDS and sorted there by bucket, are stored as
-//              (column in slice, m_row·x) runs at their exact bucket positions (coalesced; no
-//              device atomics, deterministic placement);
-//   backward — a block takes a chunk of one bucket (contiguous reads), adds it into an LDS slab of
-//              the slice's gradient (ds_add), then applies the SGD update + regularisation to the
-//              slice (1 GPU) or writes its feedback slice (N GPUs); a bucket of several chunks sums
-//              them through float atomics on whole 256-B rows and its last chunk finishes it.
+// batch) never pays back. Here the fit counts its batches once and a round is two launches over
+// the CSR batch as it stands:
+//   count    — (once per fit, every batch it visits: grid.y = batch) a block per CG forward blocks
+//              of rb rows: their entries per column slice of 2^csb columns (a "bucket"), an LDS
+//              histogram written into the bucket-major [bucket][forward block] count matrix;
+//   scan     — (likewise) a block per bucket: each forward block's first position inside the
+//              bucket and the bucket's total;
+//   forward  — a block takes its rb rows: their entries and gathered coefficients in registers,
+//              the products summed per row in LDS, loss + multiplier per row; then the entries,
+//              sorted by bucket in LDS, are stored as (column in slice, m_row·x) records at their
+//              exact bucket positions (no device atomics, deterministic placement);
+//   backward — a block takes a chunk of one bucket (contiguous reads), counting-sorts it by column
+//              in LDS (integer atomics only) and sums each column's run, then applies the SGD
+//              update + regularisation to the slice (1 GPU) or writes its feedback slice (N GPUs);
+//              a bucket of several chunks sums them through an accumulator row and its last chunk
+//              finishes it.
 // A device atomic per ENTRY would run at the scattered-atomic rate (~0.08 TB/s: the 472 µs of
-// glm_grad_csr_kernel). The LDS float atomics make the last bits depend on arrival order:
-// FMLX_DETERMINISTIC=1 keeps the transposed path.
+// glm_grad_csr_kernel). The multi-chunk accumulator's float atomics make the last bits depend on
+// arrival order: FMLX_DETERMINISTIC=1 keeps the transposed path.
 constexpr int BK_NT = 1024;     // threads of the kernels
 // scatter: 512-thread blocks, entries staged per piece (LDS: a column, a value and a row id each;
 // ≤ 36 KiB, so four blocks share a CU — more independent blocks to overlap each one's chain of
@@ -652,16 +654,19 @@ struct BkRec {
   A val;
 };
 
+
 struct BktArgs {
   int csb, nb;     // slice bits, buckets = ceil(d / 2^csb)
   int rb;          // forward rows per block
   int chunk;       // backward entries per work item
-  int* cntm;       // [slots][fwd blocks][nb] entries per (forward block, bucket)
-  int* offm;       // [slots][fwd blocks][nb] first position of each forward block inside each bucket
+  int* cntm;       // [slots][nb][fwd blocks] entries per (bucket, forward block)
+  int* offm;       // [slots][fwd blocks][nb] each forward block's first record position in each bucket
+  int* lofs;       // [slots][fwd blocks][nb] exclusive prefix over buckets of the block's own counts
   int* tot;        // [slots][nb] entries per bucket
+  int* bst;        // [slots][nb + 1] bucket starts (exclusive prefix of tot; [nb] = the batch's entries)
   int slots;       // > 0: the counts of batches 0 … slots − 1 were made once for the fit (slot = batch);
-                   // 0: count + scan run in every round, for its batch (slot 0)
-  long mstride;    // elements of one slot of cntm / offm
+                   // 0: count + scan + base run in every round, for its batch (slot 0)
+  long mstride;    // elements of one slot of cntm / offm / lofs
   int* done;       // [nb] chunk arrivals of multi-chunk buckets (zero between rounds)
   void* rec;       // [largest batch nnz] BkRec<A>: (column within the slice, m_row · x)
   void* acc;       // [d] zero between rounds: partial slices of multi-chunk buckets
@@ -698,7 +703,7 @@ __device__ __forceinline__ int bk_exscan(int v, int* tmp, int* total) {
 // exclusive scan of v[0..m) into out[0..m) (LDS or global) by the whole block, each thread a run
 // of consecutive values; returns the total
 template <int NT = BK_NT>
-__device__ __forceinline__ int bk_exscan_array(const int* v, int* out, int m, int* tmp) {
+__device__ __forceinline__ int bk_exscan_array(const int* v, int* out, int m, int* tmp, long ostride = 1) {
   const int per = (m + NT - 1) / NT;
   const int q0 = threadIdx.x * per;
   int mine = 0;
@@ -708,7 +713,7 @@ __device__ __forceinline__ int bk_exscan_array(const int* v, int* out, int m, in
   for (int i = 0; i < per; ++i)
     if (q0 + i < m) {
       const int c = v[q0 + i];
-      out[q0 + i] = run;
+      out[(long)(q0 + i) * ostride] = run;
       run += c;
     }
   return total;
@@ -744,6 +749,7 @@ __device__ __forceinline__ bool bk_count_batch(const int* state, long n, long B,
 
 // count: a block takes CG consecutive forward blocks (their entries are one contiguous range) and
 // writes their per-bucket counts into the bucket-major count matrix [slot][bucket][forward block]
+// and each one's exclusive prefix over the buckets (its LDS staging offsets) block-major into lofs
 constexpr int CG = 8;
 __global__ __launch_bounds__(BK_NT) void glm_bkt_count_kernel(const long* __restrict__ indptr,
                                                               const int* __restrict__ idx, long n, long B,
@@ -784,10 +790,34 @@ __global__ __launch_bounds__(BK_NT) void glm_bkt_count_kernel(const long* __rest
     const int q = i / k.nb, b = i - q * k.nb;
     cm[(long)b * nfb + f0 + q] = bk_hist[i];
   }
+  // a wave per forward block: the exclusive prefix of its counts over the buckets (CG ≤ waves)
+  const int w = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  if (w < ns) {
+    const int* h = bk_hist + w * k.nb;
+    int* out = k.lofs + slot * k.mstride + (long)(f0 + w) * k.nb;
+    const int per = (k.nb + 63) >> 6;
+    const int q0 = ln * per;
+    int sum = 0;
+    for (int i = 0; i < per; ++i) sum += q0 + i < k.nb ? h[q0 + i] : 0;
+    int x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(x, o, 64);
+      if (ln >= o) x += t;
+    }
+    int run = x - sum;
+    for (int i = 0; i < per; ++i)
+      if (q0 + i < k.nb) {
+        const int c = h[q0 + i];
+        out[q0 + i] = run;
+        run += c;
+      }
+  }
 }
+static_assert(CG <= BK_NT / 64, "a wave per forward block of a count block");
 
-// one block per bucket: row b of the (bucket-major) count matrix → each forward block's first
-// position in the bucket, and the bucket's total
+// one block per bucket: row b of the (bucket-major) count matrix → each forward block's offset
+// inside the bucket (in place) and the bucket's total
 __global__ __launch_bounds__(BK_NT) void glm_bkt_scan_kernel(long n, long B, const int* __restrict__ state,
                                                              BktArgs k) {
   __shared__ int tmp[BK_NT / 64];
@@ -796,18 +826,57 @@ __global__ __launch_bounds__(BK_NT) void glm_bkt_scan_kernel(long n, long B, con
   const int nfb = (int)((end - start + k.rb - 1) / k.rb);
   const int b = blockIdx.x;
   const long row = slot * k.mstride + (long)b * nfb;
-  const int total = bk_exscan_array(k.cntm + row, k.offm + row, nfb, tmp);
+  const int total = bk_exscan_array(k.cntm + row, k.cntm + row, nfb, tmp);
   if (threadIdx.x == 0) k.tot[slot * k.nb + b] = total;
 }
 
+// bucket starts (exclusive prefix of the totals) into bst; every forward block's offsets plus its
+// bucket's start, transposed through LDS tiles of TBK buckets × TFB blocks into the block-major
+// record positions offm[f][b]: the forward then reads one contiguous row per block
+constexpr int TBK = 32, TFB = 64;
+__global__ __launch_bounds__(BK_NT) void glm_bkt_base_kernel(long n, long B, const int* __restrict__ state,
+                                                             BktArgs k) {
+  extern __shared__ int sb[];  // [nb + 1]
+  __shared__ int tile[TBK][TFB + 1];
+  __shared__ int tmp[BK_NT / 64];
+  long start, end, slot;
+  if (!bk_count_batch(state, n, B, k, start, end, slot)) return;
+  const int nfb = (int)((end - start + k.rb - 1) / k.rb);
+  sb[k.nb] = bk_exscan_array(k.tot + slot * k.nb, sb, k.nb, tmp);
+  __syncthreads();
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i <= k.nb; i += BK_NT) k.bst[slot * (k.nb + 1) + i] = sb[i];
+  const int ntf = (nfb + TFB - 1) / TFB;
+  const int b0 = (int)(blockIdx.x / ntf) * TBK, f0 = (int)(blockIdx.x % ntf) * TFB;
+  const int* cm = k.cntm + slot * k.mstride;
+  for (int i = threadIdx.x; i < TBK * TFB; i += BK_NT) {
+    const int bb = i / TFB, ff = i - bb * TFB;
+    if (b0 + bb < k.nb && f0 + ff < nfb) tile[bb][ff] = cm[(long)(b0 + bb) * nfb + f0 + ff] + sb[b0 + bb];
+  }
+  __syncthreads();
+  int* om = k.offm + slot * k.mstride;
+  for (int i = threadIdx.x; i < TBK * TFB; i += BK_NT) {
+    const int ff = i / TBK, bb = i - ff * TBK;
+    if (b0 + bb < k.nb && f0 + ff < nfb) om[(long)(f0 + ff) * k.nb + b0 + bb] = tile[bb][ff];
+  }
+}
+
+// forward + bucket writes: a block takes its rb rows (one piece of ≤ ECAP entries in the common
+// case, held in registers): the entries and their coefficients are gathered at once, the products
+// staged in LDS and summed per row by G-lane groups, a thread per row turns its dot into the loss and
+// multiplier, then the entries are sorted by bucket in LDS and stored as (column in slice, m·x)
+// records at their exact positions. One read of the batch per round (the separate forward read it
+// a second time: 43 + 38 µs of forward + scatter per 100k × 64 batch, profiles/r6/INDEX.md).
+// (≤ 64 VGPRs: eight waves per SIMD, so four 512-thread blocks share a CU — the LDS allows four;
+// at 70 VGPRs only three fit and the 100k-row batch's 1786 blocks ran in 2.3 waves instead of 1.7)
 template <typename A, int G>
-__global__ __launch_bounds__(SC_NT) void glm_bkt_scatter_kernel(const long* __restrict__ indptr,
-                                                                const int* __restrict__ idx,
-                                                                const A* __restrict__ val,
-                                                                const A* __restrict__ mult, long n, long B,
-                                                                const int* __restrict__ state, BktArgs k) {
+__global__ __launch_bounds__(SC_NT) void glm_bkt_fwd_scatter_kernel(
+    const long* __restrict__ indptr, const int* __restrict__ idx, const A* __restrict__ val, const A* __restrict__ y,
+    const A* __restrict__ wt, const A* __restrict__ coef, long n, long B, int loss, const int* __restrict__ state,
+    A* __restrict__ wl, BktArgs k, long long* __restrict__ trace, long trace_blocks) {
   constexpr int BK_ECAP = bk_ecap<A>();
   constexpr int BK_EPT = BK_ECAP / SC_NT;
+  constexpr int NGRP = SC_NT / G;
   extern __shared__ __align__(16) unsigned char bk_smem[];
   // [nb] base | ph | pofs, then rp[rb + 1], mrow[rb], scol[ECAP], sval[ECAP], srow[ECAP]
   int* base = reinterpret_cast<int*>(bk_smem);
@@ -819,11 +888,17 @@ __global__ __launch_bounds__(SC_NT) void glm_bkt_scatter_kernel(const long* __re
   A* sval = reinterpret_cast<A*>(scol + BK_ECAP);
   uint16_t* srow = reinterpret_cast<uint16_t*>(sval + BK_ECAP);
   __shared__ int tmp[SC_NT / 64];
+  __shared__ A red[2][SC_NT / 64];
   long start, end;
   int e;
   if (!bk_batch(state, n, B, start, end, e)) return;
   const long r0 = start + (long)blockIdx.x * k.rb;
   if (r0 >= end) return;  // (the grid covers the largest batch)
+  // diagnostics (fmlx_glm_bkt_set_trace): phase stamps of each block, 100 MHz
+  long long* tb = trace && blockIdx.x < trace_blocks ? trace + (long)blockIdx.x * 8 : nullptr;
+#define BK_STAMP(p) \
+  if (tb && threadIdx.x == 0) tb[p] = (long long)__builtin_amdgcn_s_memrealtime();
+  BK_STAMP(0)
   const int nr = end - r0 < k.rb ? (int)(end - r0) : k.rb;
   const long jb = indptr[r0];
   const long je = indptr[r0 + nr];
@@ -831,109 +906,154 @@ __global__ __launch_bounds__(SC_NT) void glm_bkt_scatter_kernel(const long* __re
   const int csb = k.csb;
   const uint32_t mask = (1u << csb) - 1;
   BkRec<A>* brec = reinterpret_cast<BkRec<A>*>(k.rec);
-  const A* __restrict__ mb = mult + (r0 - start);
   const int E = (int)(je - jb);
   const bool one = E <= BK_ECAP;
-  // one piece (the common case): the block's entries are requested first, so their latency runs
-  // under the bookkeeping loads and scans below
+  // one piece (the common case): the block's entries are requested first, with the bookkeeping
+  // loads behind them; their coefficients (an L2-resident gather) follow as soon as they land
   int col[BK_EPT];
   A pv[BK_EPT];
   if (one) {
 #pragma unroll
     for (int u = 0; u < BK_EPT; ++u) {
       const int t = tid + u * SC_NT;
-      const long j = jb + (t < E ? t : 0);
-      col[u] = __builtin_nontemporal_load(idx + j);
-      pv[u] = __builtin_nontemporal_load(val + j);
+      col[u] = t < E ? __builtin_nontemporal_load(idx + jb + t) : 0;
+      pv[u] = t < E ? __builtin_nontemporal_load(val + jb + t) : (A)0;
     }
   }
-  // this block's first position in every bucket: bucket start (scan of the totals) + its offset
-  const long slot = bk_slot(e, n, B, k);
-  bk_exscan_array<SC_NT>(k.tot + slot * k.nb, base, k.nb, tmp);
-  const int nfb = (int)((end - start + k.rb - 1) / k.rb);
-  for (int i = tid; i < k.nb; i += SC_NT) base[i] += k.offm[slot * k.mstride + (long)i * nfb + blockIdx.x];
+  // this thread's row (its loss below): label and weight
+  A yv = 0, wv = 1;
+  if (tid < nr) {
+    yv = y[r0 + tid];
+    if (wt) wv = wt[r0 + tid];
+  }
+  // this block's first record position in every bucket and its LDS staging offsets (one
+  // contiguous row each, made once per fit: count / scan / base kernels)
+  const long mo = bk_slot(e, n, B, k) * k.mstride + (long)blockIdx.x * k.nb;
+  for (int i = tid; i < k.nb; i += SC_NT) {
+    base[i] = k.offm[mo + i];
+    const int lo = k.lofs[mo + i];
+    pofs[i] = lo;
+    ph[i] = lo;
+  }
   for (int i = tid; i <= nr; i += SC_NT) rp[i] = (int)(indptr[r0 + i] - jb);
-  for (int i = tid; i < nr; i += SC_NT) mrow[i] = mb[i];
-  __syncthreads();
+  BK_STAMP(6)  // (wave 0's entries and bookkeeping rows have landed)
   if (one) {
-    // every entry's row id into LDS (a thread per row), staging offsets from the count matrix row;
-    // a returning integer atomic on its bucket's cursor gives each entry its staging slot
+    // the products into the staging values (free until the records are staged)
+#pragma unroll
+    for (int u = 0; u < BK_EPT; ++u) {
+      const int t = tid + u * SC_NT;
+      if (t < E) sval[t] = pv[u] * coef[col[u]];
+    }
+  }
+  __syncthreads();
+  BK_STAMP(1)
+  const int lane = tid & (G - 1), grp = tid / G;
+  if (one) {
+    // every entry's row id into LDS (a thread per row; read by the staging after two barriers)
     for (int q = tid; q < nr; q += SC_NT)
       for (int j = rp[q]; j < rp[q + 1]; ++j) srow[j] = (uint16_t)q;
-    for (int i = tid; i < k.nb; i += SC_NT) ph[i] = k.cntm[slot * k.mstride + (long)i * nfb + blockIdx.x];
-    __syncthreads();
-    bk_exscan_array<SC_NT>(ph, pofs, k.nb, tmp);
-    __syncthreads();
-    for (int i = tid; i < k.nb; i += SC_NT) ph[i] = pofs[i];
-    __syncthreads();
+    BK_STAMP(2)
+    // row dots: a G-lane group per row over its staged products
+    for (int q = grp; q < nr; q += NGRP) {
+      A s = 0;
+      for (int j = rp[q] + lane; j < rp[q + 1]; j += G) s += sval[j];
+      s = group_sum<G>(s);
+      if (lane == 0) mrow[q] = s;
+    }
+  } else {
+    // (rows of more than ECAP entries per block) row dots straight from the batch
+    for (int q = grp; q < nr; q += NGRP) {
+      A s = 0;
+      for (int j = rp[q] + lane; j < rp[q + 1]; j += G) s += val[jb + j] * coef[idx[jb + j]];
+      s = group_sum<G>(s);
+      if (lane == 0) mrow[q] = s;
+    }
+  }
+  __syncthreads();
+  // loss + multiplier, a thread per row; Σweight / Σloss of the block into a parity slot of `wl`
+  A wsum = 0, lsum = 0;
+  for (int q = tid; q < nr; q += SC_NT) {
+    const A yy = q == tid ? yv : y[r0 + q];
+    const A ww = q == tid ? wv : (wt ? wt[r0 + q] : (A)1);
+    A l, m;
+    loss_and_mult(loss, mrow[q], yy, ww, l, m);
+    mrow[q] = m;
+    wsum += ww;
+    lsum += l;
+  }
+  wsum = wave_sum(wsum);
+  lsum = wave_sum(lsum);
+  if ((tid & 63) == 0) {
+    red[0][tid >> 6] = wsum;
+    red[1][tid >> 6] = lsum;
+  }
+  __syncthreads();
+  BK_STAMP(3)
+  if (tid == 0) {
+    A a0 = 0, a1 = 0;
+#pragma unroll
+    for (int i = 0; i < SC_NT / 64; ++i) {
+      a0 += red[0][i];
+      a1 += red[1][i];
+    }
+    // one of WL_SLOTS cache lines per block (same-address atomics from every block serialise)
+    A* ws = wl + ((long)(e & 1) * WL_SLOTS + (blockIdx.x & (WL_SLOTS - 1))) * WL_STRIDE;
+    if (a0 != (A)0) atomicAdd(&ws[0], a0);
+    if (a1 != (A)0) atomicAdd(&ws[1], a1);
+  }
+  if (one) {
+    // a returning integer atomic on its bucket's cursor gives each entry its staging slot (the
+    // products' staging values were consumed by the row dots before the last barrier)
 #pragma unroll
     for (int u = 0; u < BK_EPT; ++u) {
       const int t = tid + u * SC_NT;
       if (t < E) {
-        const int slot = atomicAdd(&ph[col[u] >> csb], 1);
-        scol[slot] = col[u];
-        sval[slot] = pv[u] * mrow[srow[t]];
+        const int sl = atomicAdd(&ph[col[u] >> csb], 1);
+        scol[sl] = col[u];
+        sval[sl] = pv[u] * mrow[srow[t]];
       }
     }
     __syncthreads();
+    BK_STAMP(4)
     for (int t = tid; t < E; t += SC_NT) {
       const int c = scol[t];
       const int bk = c >> csb;
       const long dst = (long)base[bk] + (t - pofs[bk]);
       brec[dst] = BkRec<A>{(uint32_t)c & mask, sval[t]};
     }
+    BK_STAMP(5)
     return;
   }
+#undef BK_STAMP
+  // several pieces (rows of more than ECAP entries per block): per piece, pass 1 draws each entry's
+  // rank in its bucket (kept in srow), pass 2 re-reads the entry (L2) and stages it at its slot —
+  // no per-thread arrays across the barriers, so this rare path does not set the kernel's registers
   for (int p0 = 0; p0 < E; p0 += BK_ECAP) {
     const int pe = E - p0 < BK_ECAP ? E - p0 : BK_ECAP;
     for (int i = tid; i < k.nb; i += SC_NT) ph[i] = 0;
     __syncthreads();
-    int col[BK_EPT], rk[BK_EPT];
-    A pv[BK_EPT];
-#pragma unroll
-    for (int u = 0; u < BK_EPT; ++u) {
-      const int t = tid + u * SC_NT;
-      const int j = p0 + (t < pe ? t : 0);
-      col[u] = idx[jb + j];
-      pv[u] = val[jb + j];
-    }
-#pragma unroll
-    for (int u = 0; u < BK_EPT; ++u) {
-      const int t = tid + u * SC_NT;
-      rk[u] = 0;
-      if (t < pe) {
-        const int j = p0 + t;
-        int lo = 0, hi = nr;  // the entry's row: rp[lo] <= j < rp[hi]
-        while (hi - lo > 1) {
-          const int mid = (lo + hi) >> 1;
-          if (rp[mid] <= j) lo = mid; else hi = mid;
-        }
-        pv[u] *= mrow[lo];
-        rk[u] = atomicAdd(&ph[col[u] >> csb], 1);
-      }
-    }
+    for (int t = tid; t < pe; t += SC_NT) srow[t] = (uint16_t)atomicAdd(&ph[idx[jb + p0 + t] >> csb], 1);
     __syncthreads();
     bk_exscan_array<SC_NT>(ph, pofs, k.nb, tmp);
     __syncthreads();
-#pragma unroll
-    for (int u = 0; u < BK_EPT; ++u) {
-      const int t = tid + u * SC_NT;
-      if (t < pe) {
-        const int slot = pofs[col[u] >> csb] + rk[u];
-        scol[slot] = col[u];
-        sval[slot] = pv[u];
+    for (int t = tid; t < pe; t += SC_NT) {
+      const int j = p0 + t;
+      int lo = 0, hi = nr;  // the entry's row: rp[lo] <= j < rp[hi]
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (rp[mid] <= j) lo = mid; else hi = mid;
       }
+      const int c = idx[jb + j];
+      const int sl = pofs[c >> csb] + srow[t];
+      scol[sl] = c;
+      sval[sl] = val[jb + j] * mrow[lo];
     }
     __syncthreads();
-#pragma unroll
-    for (int u = 0; u < BK_EPT; ++u) {
-      const int t = tid + u * SC_NT;
-      if (t < pe) {
-        const int c = scol[t];
-        const int bk = c >> csb;
-        const long dst = (long)base[bk] + (t - pofs[bk]);
-        brec[dst] = BkRec<A>{(uint32_t)c & mask, sval[t]};
-      }
+    for (int t = tid; t < pe; t += SC_NT) {
+      const int c = scol[t];
+      const int bk = c >> csb;
+      const long dst = (long)base[bk] + (t - pofs[bk]);
+      brec[dst] = BkRec<A>{(uint32_t)c & mask, sval[t]};
     }
     __syncthreads();
     for (int i = tid; i < k.nb; i += SC_NT) base[i] += ph[i];
@@ -985,8 +1105,9 @@ __global__ __launch_bounds__(BK_NT) void glm_bkt_bwd_kernel(const long* __restri
   }
   // bucket starts, then the work items: chunks of `chunk` entries of each bucket (at least one per
   // bucket: every column is updated, regularisation included)
-  const int* tot = k.tot + bk_slot(e, n, B, k) * k.nb;
-  bst[k.nb] = bk_exscan_array(tot, bst, k.nb, tmp);
+  const long sl = bk_slot(e, n, B, k);
+  const int* tot = k.tot + sl * k.nb;
+  for (int i = threadIdx.x; i <= k.nb; i += BK_NT) bst[i] = k.bst[sl * (k.nb + 1) + i];
   for (int i = threadIdx.x; i < k.nb; i += BK_NT) {
     const int len = tot[i];
     nch[i] = len > k.chunk ? (len + k.chunk - 1) / k.chunk : 1;
@@ -1121,6 +1242,13 @@ __global__ __launch_bounds__(BK_NT) void glm_bkt_bwd_kernel(const long* __restri
 
 static long long* g_sparse_trace = nullptr;  // per-block timestamps of the tiled backward (diagnostics)
 FMLX_API void fmlx_glm_sparse_set_trace(void* trace) { g_sparse_trace = (long long*)trace; }
+// per-block phase stamps of the bucket forward (8 int64 per block, blocks < `blocks`), or off
+static long long* g_bkt_trace = nullptr;
+static long g_bkt_trace_blocks = 0;
+FMLX_API void fmlx_glm_bkt_set_trace(void* trace, long blocks) {
+  g_bkt_trace = blocks > 0 ? (long long*)trace : nullptr;
+  g_bkt_trace_blocks = blocks > 0 ? blocks : 0;
+}
 
 FMLX_API int fmlx_glm_grad_csr(int acc_f64, const long* indptr, const int* idx, const void* val, const void* y,
                                const void* wt, const void* coef, long n, int d, long B, int loss, const int* state,
@@ -1299,6 +1427,10 @@ FMLX_API int fmlx_glm_bkt_limits(int* out) {
   return 0;
 }
 
+static int bkt_base_blocks(long fblocks, int nb) {
+  return (int)(((fblocks + TFB - 1) / TFB) * ((nb + TBK - 1) / TBK));
+}
+
 static size_t bkt_fwd_lds(const BktArgs& k, size_t es) {
   return (((3 * (size_t)k.nb + k.rb + 1) * 4 + 15) & ~(size_t)15) + (size_t)k.rb * es +
          (size_t)(es == 8 ? bk_ecap<double>() : bk_ecap<float>()) * (4 + es + 2);
@@ -1306,7 +1438,7 @@ static size_t bkt_fwd_lds(const BktArgs& k, size_t es) {
 
 template <typename A, int G>
 static void launch_bkt_round(const long* indptr, const int* idx, const A* val, const A* y, const A* wt, A* coef,
-                             long n, int d, long B, int loss, int* state, A* wl, A* fb, A* mult, int fuse,
+                             long n, int d, long B, int loss, int* state, A* wl, A* fb, int fuse,
                              int max_iter, A tol, A lr, A reg, A en, const BktArgs& k, int bwd_blocks, hipStream_t s) {
   const long rows = B < n ? B : n;
   const int fblocks = (int)((rows + k.rb - 1) / k.rb);
@@ -1314,13 +1446,11 @@ static void launch_bkt_round(const long* indptr, const int* idx, const A* val, c
     hipLaunchKernelGGL(glm_bkt_count_kernel, dim3((fblocks + CG - 1) / CG), dim3(BK_NT), (size_t)CG * k.nb * 4, s,
                        indptr, idx, n, B, state, k);
     hipLaunchKernelGGL(glm_bkt_scan_kernel, dim3(k.nb), dim3(BK_NT), 0, s, n, B, state, k);
+    hipLaunchKernelGGL(glm_bkt_base_kernel, dim3(bkt_base_blocks(fblocks, k.nb)), dim3(BK_NT),
+                       (size_t)(k.nb + 1) * 4, s, n, B, state, k);
   }
-  long fw = (rows * G + 255) / 256;  // the row-group forward: one row per lane group
-  if (fw > g_csc_fwd_cap) fw = g_csc_fwd_cap;
-  hipLaunchKernelGGL((glm_csr_fwd_kernel<A, G>), dim3((int)fw), dim3(256), 0, s, indptr, idx, val, y, wt,
-                     (const A*)coef, n, B, loss, state, mult, wl);
-  hipLaunchKernelGGL((glm_bkt_scatter_kernel<A, G>), dim3(fblocks), dim3(SC_NT), bkt_fwd_lds(k, sizeof(A)), s, indptr,
-                     idx, val, (const A*)mult, n, B, state, k);
+  hipLaunchKernelGGL((glm_bkt_fwd_scatter_kernel<A, G>), dim3(fblocks), dim3(SC_NT), bkt_fwd_lds(k, sizeof(A)), s,
+                     indptr, idx, val, y, wt, (const A*)coef, n, B, loss, state, wl, k, g_bkt_trace, g_bkt_trace_blocks);
   const size_t blds = (size_t)k.chunk * sizeof(A) + (((size_t)1 << k.csb) + 1 + 3 * (size_t)k.nb + 2) * 4;
   const int weighted = wt != nullptr;
   if (blds > (size_t)LDS_PER_CU) return;  // (fmlx_glm_bkt_round checks it first)
@@ -1335,16 +1465,19 @@ static void launch_bkt_round(const long* indptr, const int* idx, const A* val, c
 // The fit's one-time counts: count + scan of batches 0 … slots − 1 of the partition in two launches
 // (grid.y = batch), before its first round; the rounds then run forward + scatter + backward only.
 FMLX_API int fmlx_glm_bkt_count_all(const long* indptr, const int* idx, long n, long B, int csb, int nb, int rb,
-                                    int* cntm, int* offm, int* tot, int slots, long mstride, void* stream) {
+                                    int* cntm, int* offm, int* lofs, int* tot, int* bst, int slots, long mstride,
+                                    void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (n <= 0 || B <= 0 || slots < 1 || nb < 1 || nb > BK_NB_MAX || rb < 1) return -2;
   const long rows = B < n ? B : n;
   const long fblocks = (rows + rb - 1) / rb;
   if (mstride < fblocks * nb || (long)slots * B >= n + B) return -3;
-  const BktArgs k{csb, nb, rb, 0, cntm, offm, tot, slots, mstride, nullptr, nullptr, nullptr};
+  const BktArgs k{csb, nb, rb, 0, cntm, offm, lofs, tot, bst, slots, mstride, nullptr, nullptr, nullptr};
   hipLaunchKernelGGL(glm_bkt_count_kernel, dim3((int)((fblocks + CG - 1) / CG), slots), dim3(BK_NT),
                      (size_t)CG * nb * 4, s, indptr, idx, n, B, (const int*)nullptr, k);
   hipLaunchKernelGGL(glm_bkt_scan_kernel, dim3(nb, slots), dim3(BK_NT), 0, s, n, B, (const int*)nullptr, k);
+  hipLaunchKernelGGL(glm_bkt_base_kernel, dim3(bkt_base_blocks(fblocks, nb), slots), dim3(BK_NT),
+                     (size_t)(nb + 1) * 4, s, n, B, (const int*)nullptr, k);
   return (int)hipGetLastError();
 }
 
@@ -1355,8 +1488,8 @@ FMLX_API int fmlx_glm_bkt_count_all(const long* indptr, const int* idx, long n, 
 FMLX_API int fmlx_glm_bkt_round(int acc_f64, int G, const long* indptr, const int* idx, const void* val,
                                 const void* y, const void* wt, void* coef, long n, int d, long B, int loss, int* state,
                                 void* wl, void* fb, int fuse, int max_iter, double tol, double lr, double reg,
-                                double en, int csb, int rb, int chunk, int* cntm, int* offm, int* tot, int slots,
-                                long mstride, int* done, void* rec, void* acc, void* mult, int bwd_blocks,
+                                double en, int csb, int rb, int chunk, int* cntm, int* offm, int* lofs, int* tot,
+                                int* bst, int slots, long mstride, int* done, void* rec, void* acc, int bwd_blocks,
                                 void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (n <= 0 || B <= 0 || d <= 0) return -2;
@@ -1365,21 +1498,21 @@ FMLX_API int fmlx_glm_bkt_round(int acc_f64, int G, const long* indptr, const in
   const long nb = ((long)d + (1L << csb) - 1) >> csb;
   const long rows = B < n ? B : n;
   const long fblocks = (rows + rb - 1) / rb;
-  if (mult == nullptr || nb > BK_NB_MAX || rb < 1 || rb > 4096 || chunk < BK_NT || bwd_blocks < 1)
+  if (nb > BK_NB_MAX || rb < 1 || rb > 4096 || chunk < BK_NT || bwd_blocks < 1)
     return -4;
   if (chunk > (acc_f64 ? bk_chunk<double>() : bk_chunk<float>()) || csb > 12) return -6;
   if ((size_t)chunk * es + (((size_t)1 << csb) + 1 + 3 * (size_t)nb + 2) * 4 > (size_t)LDS_PER_CU) return -7;
   if (slots < 0 || mstride < fblocks * nb) return -8;
-  const BktArgs k{csb, (int)nb, rb, chunk, cntm, offm, tot, slots, mstride, done, rec, acc};
+  const BktArgs k{csb, (int)nb, rb, chunk, cntm, offm, lofs, tot, bst, slots, mstride, done, rec, acc};
   if (bkt_fwd_lds(k, es) > (size_t)LDS_PER_CU / 2) return -5;
 #define FMLX_BKT(GG)                                                                                                  \
   if (acc_f64)                                                                                                        \
     launch_bkt_round<double, GG>(indptr, idx, (const double*)val, (const double*)y, (const double*)wt, (double*)coef,  \
-                                 n, d, B, loss, state, (double*)wl, (double*)fb, (double*)mult, fuse, max_iter, tol,  \
+                                 n, d, B, loss, state, (double*)wl, (double*)fb, fuse, max_iter, tol,  \
                                  lr, reg, en, k, bwd_blocks, s);                                                                      \
   else                                                                                                                \
     launch_bkt_round<float, GG>(indptr, idx, (const float*)val, (const float*)y, (const float*)wt, (float*)coef, n, d, \
-                                B, loss, state, (float*)wl, (float*)fb, (float*)mult, fuse, max_iter, (float)tol,     \
+                                B, loss, state, (float*)wl, (float*)fb, fuse, max_iter, (float)tol,     \
                                 (float)lr, (float)reg, (float)en, k, bwd_blocks, s);
   switch (G) {
     case 4: FMLX_BKT(4); break;
@@ -1411,15 +1544,18 @@ FMLX_API int fmlx_glm_sparse_warm(void* stream) {
   void* wls = (char*)dstate + 8192;
   const long* ip = (const long*)scratch;
   const int* ix = (const int*)scratch;
-  BktArgs k{12, 1, 1, BK_NT, (int*)scratch, (int*)scratch, (int*)scratch, 0, 1, (int*)scratch, scratch, scratch};
+  int* si = (int*)scratch;
+  BktArgs k{12, 1, 1, BK_NT, si, si, si, si, si, 0, 1, si, scratch, scratch};
   hipLaunchKernelGGL(glm_bkt_count_kernel, dim3(1), dim3(BK_NT), (size_t)CG * 4, s, ip, ix, 1L, 1L, (const int*)st, k);
   hipLaunchKernelGGL(glm_bkt_scan_kernel, dim3(1), dim3(BK_NT), 0, s, 1L, 1L, (const int*)st, k);
+  hipLaunchKernelGGL(glm_bkt_base_kernel, dim3(1), dim3(BK_NT), 8, s, 1L, 1L, (const int*)st, k);
 #define FMLX_WARM(A, GG)                                                                                           \
   hipLaunchKernelGGL((glm_csr_fwd_kernel<A, GG>), dim3(1), dim3(256), 0, s, ip, ix, (const A*)scratch,              \
                      (const A*)scratch, (const A*)nullptr, (const A*)scratch, 1L, 1L, 1, (const int*)st, (A*)scratch, \
                      (A*)scratch);                                                                                 \
-  hipLaunchKernelGGL((glm_bkt_scatter_kernel<A, GG>), dim3(1), dim3(SC_NT), 4096, s, ip, ix, (const A*)scratch,     \
-                     (const A*)scratch, 1L, 1L, (const int*)st, k);
+  hipLaunchKernelGGL((glm_bkt_fwd_scatter_kernel<A, GG>), dim3(1), dim3(SC_NT), 4096, s, ip, ix, (const A*)scratch, \
+                     (const A*)scratch, (const A*)nullptr, (const A*)scratch, 1L, 1L, 1, (const int*)st, (A*)wls, k,      \
+                     (long long*)nullptr, 0L);
   FMLX_WARM(float, 4) FMLX_WARM(float, 8) FMLX_WARM(float, 16) FMLX_WARM(float, 32) FMLX_WARM(float, 64)
   FMLX_WARM(double, 4) FMLX_WARM(double, 8) FMLX_WARM(double, 16) FMLX_WARM(double, 32) FMLX_WARM(double, 64)
 #undef FMLX_WARM

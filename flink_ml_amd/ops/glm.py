@@ -81,6 +81,17 @@ def set_trace(buf: Optional[torch.Tensor]) -> None:
     native.kernels().fmlx_glm_set_trace(native.ptr(buf))
 
 
+def set_bkt_trace(buf: Optional[torch.Tensor]) -> None:
+    """Diagnostics: the bucket round's forward writes per-block phase stamps (s_memrealtime, 100 MHz:
+    entry, bookkeeping loaded, products staged, loss done, records staged, stores issued) into
+    ``buf`` (int64 [blocks, 8]; blocks past its rows write nothing); None switches off."""
+    if buf is None:
+        native.kernels().fmlx_glm_bkt_set_trace(None, 0)
+    else:
+        assert buf.dtype == torch.int64 and buf.dim() == 2 and buf.shape[1] == 8 and buf.is_contiguous()
+        native.kernels().fmlx_glm_bkt_set_trace(native.ptr(buf), int(buf.shape[0]))
+
+
 def pick_layout(X: torch.Tensor, rounds: bool = True) -> Optional[Tuple[int, int]]:
     """(epc, cpl) for the register-resident path, or None if d is too wide / misaligned.
     ``rounds=False``: the prediction kernel's limit (no gradient registers: bf16 up to 8 chunks)."""
@@ -898,26 +909,28 @@ class BucketRound:
         # offsets are made once, before the first round (count_all), when they fit SLOT_BYTES_MAX;
         # otherwise every round counts its own batch
         self.mstride = fblocks * self.nb
-        self.slots = batches if 0 < batches and 2 * batches * self.mstride * 4 <= self.SLOT_BYTES_MAX else 0
+        self.slots = batches if 0 < batches and 3 * batches * self.mstride * 4 <= self.SLOT_BYTES_MAX else 0
         self.counted = False
         i32 = dict(dtype=torch.int32, device=dev)
         S = max(1, self.slots)
-        self.cntm = torch.empty(S * self.mstride, **i32)
-        self.offm = torch.empty(S * self.mstride, **i32)
-        self.tot = torch.empty(S * self.nb, **i32)
+        # one allocation: counts [S][nb][blocks], record offsets and staging offsets [S][blocks][nb],
+        # bucket totals [S][nb] and starts [S][nb + 1]
+        m = S * self.mstride
+        ints = torch.empty(3 * m + S * (2 * self.nb + 1), **i32)
+        self.cntm, self.offm, self.lofs = ints[:m], ints[m:2 * m], ints[2 * m:3 * m]
+        self.tot, self.bst = ints[3 * m:3 * m + S * self.nb], ints[3 * m + S * self.nb:]
         # (zero_bufs: the caller's one zero-filled allocation for `done` and `acc`)
         # done: [nb] chunk arrivals, then the backward's [8] group + [1] top arrival tickets
         self.done, self.acc = zero_bufs if zero_bufs is not None else \
             native.zeros_many([((self.nb + 16,), torch.int32), ((d,), values.dtype)], dev)
         self.rec = torch.empty(max(1, most) * rec_bytes, dtype=torch.uint8, device=dev)
-        self.mult = torch.empty(max(1, min(B, n)), dtype=values.dtype, device=dev)
 
     def count_all(self, indptr, idx, n: int, B: int) -> None:
         """The one-time counts of the fit's batches (no-op per round mode / already made)."""
         if self.slots and not self.counted:
             native.call("fmlx_glm_bkt_count_all", native.ptr(indptr), native.ptr(idx), n, B, self.csb, self.nb, self.rb,
-                        native.ptr(self.cntm), native.ptr(self.offm), native.ptr(self.tot), self.slots, self.mstride,
-                        native.stream_ptr(idx.device))
+                        native.ptr(self.cntm), native.ptr(self.offm), native.ptr(self.lofs), native.ptr(self.tot),
+                        native.ptr(self.bst), self.slots, self.mstride, native.stream_ptr(idx.device))
             self.counted = True
 
     @staticmethod
@@ -952,8 +965,9 @@ def bkt_round(bk: BucketRound, indptr, idx, val, y, wt, coef, n, d, B, loss, sta
         int(val.dtype == torch.float64), bk.G, native.ptr(indptr), native.ptr(idx), native.ptr(val), native.ptr(y),
         native.ptr(wt), native.ptr(coef), n, d, B, loss, native.ptr(state), native.ptr(wl), native.ptr(fb), int(fuse),
         max_iter, float(tol), float(lr), float(reg), float(en), bk.csb, bk.rb, bk.chunk, native.ptr(bk.cntm),
-        native.ptr(bk.offm), native.ptr(bk.tot), bk.slots, bk.mstride, native.ptr(bk.done), native.ptr(bk.rec),
-        native.ptr(bk.acc), native.ptr(bk.mult), bk.bwd_blocks, native.stream_ptr(val.device))
+        native.ptr(bk.offm), native.ptr(bk.lofs), native.ptr(bk.tot), native.ptr(bk.bst), bk.slots, bk.mstride,
+        native.ptr(bk.done), native.ptr(bk.rec),
+        native.ptr(bk.acc), bk.bwd_blocks, native.stream_ptr(val.device))
     if rc != 0:
         raise RuntimeError("fmlx_glm_bkt_round failed: %d" % rc)
 

@@ -91,10 +91,11 @@ _KERNEL_SIGS = {
     "fmlx_glm_sparse_set_trace": ([c_void_p], None),
     "fmlx_glm_bkt_round": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int,
                            c_long, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double, c_double, c_double,
-                           c_double, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_long, c_void_p,
-                           c_void_p, c_void_p, c_void_p, c_int, c_void_p],
+                           c_double, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                           c_long, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
+    "fmlx_glm_bkt_set_trace": ([c_void_p, c_long], None),
     "fmlx_glm_bkt_count_all": [c_void_p, c_void_p, c_long, c_long, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
-                               c_int, c_long, c_void_p],
+                               c_void_p, c_void_p, c_int, c_long, c_void_p],
     # sort.hip
     "fmlx_sorted_bounds": [c_void_p, c_long, c_int, c_void_p, c_void_p],
     "fmlx_seg_sort_scratch": ([c_void_p, c_int, c_int, c_int], c_long),
@@ -220,12 +221,11 @@ def _preload(lib) -> None:
     torch.cuda.get_device_properties(torch.cuda.current_device())  # (first call: runtime queries)
     # one device segment for torch's caching allocator, freed at once: the trainers' buffers of a
     # first fit are then carved out of it instead of each new size paying a hipMalloc inside the fit
-    # (a 20-round sparse fit's first allocation took ~15 ms, profiles/r6/INDEX.md)
+    # (a fresh hipMalloc is tens to hundreds of µs of GPU-idle host time)
     pool = int(os.environ.get("FMLX_DEVICE_POOL_MB", "2048")) << 20
     if pool > 0:
         seg = torch.empty(pool, dtype=torch.uint8, device=torch.cuda.current_device())
         del seg
-    PRELOAD_MS = (time.perf_counter() - t0) * 1e3
     PRELOAD_MS = (time.perf_counter() - t0) * 1e3
     PRELOAD_OBJECTS = k
 

@@ -23,7 +23,7 @@ and results come back on the caller's device.
 """
 from __future__ import annotations
 
-import pickle
+import sys
 from typing import Any, List, Optional, Sequence
 
 import torch
@@ -80,6 +80,8 @@ def check_collectives() -> None:
     """Raises if an earlier one-shot xGMI collective of this process gave up waiting for a peer
     (its output was poisoned with NaN). No device sync: call it after a host sync point so the
     kernels in question have finished."""
+    if "flink_ml_amd.parallel.xgmi" not in sys.modules:
+        return  # no xGMI collective has run in this process (a 1-GPU fit never imports it)
     _xgmi().check()
 
 

@@ -61,14 +61,18 @@ def _timed(ctx, fn):
         prof = cProfile.Profile()
         prof.enable()
     lines = {}
-    if os.environ.get("BENCH_LINETRACE"):  # per-line host time of the trainer constructor (diagnostics)
+    if os.environ.get("BENCH_LINETRACE"):  # per-line host time of the trainer's set-up and fit (diagnostics)
         from flink_ml_amd.common.optimizer import DeviceGlmTrainer
+        from flink_ml_amd.ops import glm as gk
 
-        code = DeviceGlmTrainer.__init__.__code__
+        codes = {f.__code__: f.__qualname__ for f in (DeviceGlmTrainer.__init__, DeviceGlmTrainer.fit,
+                                                     DeviceGlmTrainer._launch_round, gk.BucketRound.__init__,
+                                                     gk.BucketRound.alloc, gk._batch_bounds)}
         last = [None, 0.0]
 
         def tracer(frame, event, arg):
-            if frame.f_code is not code:
+            name = codes.get(frame.f_code)
+            if name is None:
                 return None
 
             sync = os.environ.get("BENCH_LINETRACE") == "sync"  # charge each line its GPU work too
@@ -79,7 +83,7 @@ def _timed(ctx, fn):
                 now = time.perf_counter()
                 if last[0] is not None:
                     lines[last[0]] = lines.get(last[0], 0.0) + now - last[1]
-                last[0] = frame.f_lineno if event == "line" else None
+                last[0] = (name, frame.f_lineno) if event == "line" else None
                 last[1] = time.perf_counter()
                 return local
             return local
@@ -90,8 +94,8 @@ def _timed(ctx, fn):
     torch.cuda.synchronize()
     if lines or os.environ.get("BENCH_LINETRACE"):
         sys.settrace(None)
-        print("constructor lines (ms): %s" % [(ln, round(t * 1e3, 3)) for ln, t in
-                                             sorted(lines.items(), key=lambda kv: -kv[1])[:8]], file=sys.stderr)
+        print("set-up / fit lines (ms): %s" % [("%s:%d" % ln, round(t * 1e3, 3)) for ln, t in
+                                               sorted(lines.items(), key=lambda kv: -kv[1])[:12]], file=sys.stderr)
     if prof is not None:
         import pstats
 
@@ -181,7 +185,7 @@ def run_svc_sparse(a, ctx):
         # the whole fit as the reference's netRuntime counts it: trainer set-up (device copies of
         # the shard's CSR views, the lazy per-batch column-major copies of the visited batches,
         # graph capture when it pays) + maxIter rounds + the coefficient read-back
-        tr = DeviceGlmTrainer(SGD(max_iter=iters, learning_rate=0.1, global_batch_size=gb, tol=0.0), np.zeros(dim),
+        tr = DeviceGlmTrainer(SGD(max_iter=iters, learning_rate=0.1, global_batch_size=gb, tol=0.0), None,
                               X, y, None, "hinge")
         res = tr.fit()
         if os.environ.get("BENCH_KEEP_RESULTS"):
