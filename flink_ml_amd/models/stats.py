@@ -59,9 +59,13 @@ def global_sorted_unique(v: torch.Tensor) -> torch.Tensor:
     if v.is_cuda:
         from ..ops import catstats
 
-        u = catstats.sorted_unique(v).to(v.dtype)  # native histogram / sorted distinct (no library sort)
-    else:
-        u = torch.unique(v)
+        u = catstats.sorted_unique(v)  # native histogram / sorted distinct (no library sort)
+        if get_world_distributed():
+            # the ranks' distinct lists all-gathered and their union taken by the same native
+            # distinct pass (no keyed shuffle, no library sort)
+            u = catstats.sorted_unique(torch.cat([g.to(v.device) for g in comm.all_gather_tensor(u)]))
+        return u.to(v.dtype)
+    u = torch.unique(v)
     if get_world_distributed():
         k, _ = ds.global_distinct(ds.float_keys(u))
         u = torch.sort(ds.keys_to_float(k)).values.to(device=v.device, dtype=v.dtype)

@@ -219,6 +219,15 @@ def _preload(lib) -> None:
             raise RuntimeError("warming the sparse round kernels failed")
         torch.cuda.current_stream().synchronize()
     torch.cuda.get_device_properties(torch.cuda.current_device())  # (first call: runtime queries)
+    # the bucket round's compile-time limits, read here (a first fit paid ~50 µs for the first call
+    # of the entry point); through ``lib``: kernels() holds its lock until this returns
+    import numpy as np
+
+    from . import glm
+
+    lim = np.zeros(8, dtype=np.int32)
+    lib.fmlx_glm_bkt_limits(lim.ctypes.data)
+    glm._BKT_LIMITS = lim
     # one device segment for torch's caching allocator, freed at once: the trainers' buffers of a
     # first fit are then carved out of it instead of each new size paying a hipMalloc inside the fit
     # (a fresh hipMalloc is tens to hundreds of µs of GPU-idle host time)

@@ -65,5 +65,5 @@ def warm(device=None) -> None:
     # split a larger one for a smaller request: one block of every read-back size up to 64 MiB
     # (a 1M-wide fp64 coefficient vector is 8 MiB: its first read-back paid a ~1 ms hipHostMalloc
     # inside the first fit, profiles/r6 svc fit timeline)
-    keep = [torch.empty(1 << b, dtype=torch.uint8, pin_memory=True) for b in range(12, 27)]
+    keep = [torch.empty(1 << b, dtype=torch.uint8, pin_memory=True) for b in range(5, 27)]
     del keep
