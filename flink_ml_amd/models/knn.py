@@ -108,6 +108,19 @@ def knn_predict(Q: torch.Tensor, T: torch.Tensor, tnorm: torch.Tensor, labels: t
                 idx = knn_ops.topk_from_products(G, (q * q).sum(1), tn32, kk)
                 out.append(knn_vote(labels[idx.long()], classes))
             return torch.cat(out) if out else torch.zeros(0, dtype=torch.float64, device=dev)
+    if dev.type == "cuda":
+        from ..ops import knn as knn_ops
+
+        if knn_ops.select_supported(kk, T.shape[0], compute, dev):
+            # k beyond the fused / scan kernels' lists, or fp64 (parity mode): library GEMM per
+            # query block + the radix-select kernel (csrc/knn_select.hip)
+            tnc = tn.contiguous()
+            qb = knn_ops.select_query_block(T.shape[0], Tc.element_size())
+            for s in range(0, Q.shape[0], qb):
+                q = Q[s:s + qb].to(compute)
+                idx = knn_ops.select_topk(torch.mm(q, Tc.t()), (q * q).sum(1), tnc, kk)
+                out.append(knn_vote(labels[idx.long()], classes))
+            return torch.cat(out) if out else torch.zeros(0, dtype=torch.float64, device=dev)
     for s in range(0, Q.shape[0], block):
         q = Q[s:s + block].to(compute)
         qn = (q * q).sum(1)

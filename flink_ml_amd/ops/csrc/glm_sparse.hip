@@ -785,10 +785,11 @@ __global__ __launch_bounds__(BK_NT) void glm_bkt_count_kernel(const long* __rest
   }
   for (; j < j1; j += BK_NT) atomicAdd(&bk_hist[sub_of(j) * k.nb + (__builtin_nontemporal_load(idx + j) >> k.csb)], 1);
   __syncthreads();
+  // (bucket-major: consecutive threads take one bucket's ns consecutive blocks, 32-byte runs)
   int* cm = k.cntm + slot * k.mstride;
   for (int i = threadIdx.x; i < ns * k.nb; i += BK_NT) {
-    const int q = i / k.nb, b = i - q * k.nb;
-    cm[(long)b * nfb + f0 + q] = bk_hist[i];
+    const int b = i / ns, q = i - b * ns;
+    cm[(long)b * nfb + f0 + q] = bk_hist[q * k.nb + b];
   }
   // a wave per forward block: the exclusive prefix of its counts over the buckets (CG ≤ waves)
   const int w = threadIdx.x >> 6, ln = threadIdx.x & 63;

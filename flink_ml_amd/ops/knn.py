@@ -161,3 +161,41 @@ def topk_from_products(G: torch.Tensor, qn: torch.Tensor, tn: torch.Tensor, k: i
     native.call("fmlx_knn_topk", native.ptr(G), G.stride(0), nq, n, S, native.ptr(qn), native.ptr(tn), k,
                 native.ptr(idx), native.ptr(dist), native.ptr(ws_d), native.ptr(ws_i), native.stream_ptr(G.device))
     return (idx, dist) if with_dist else idx
+
+
+# ---- any k, fp32 or fp64: radix selection over a library-GEMM product block (csrc/knn_select.hip)
+native.register_kernel_sigs({
+    "fmlx_knn_select": [c_int, c_void_p, c_long, c_long, c_long, c_void_p, c_void_p, c_int, c_void_p, c_long,
+                        c_void_p],
+})
+SELECT_MAX_K = 8192  # csrc/knn_select.hip SEL_KMAX (the k winners are sorted in LDS)
+SELECT_BLOCK_BYTES = 1 << 30
+
+
+def select_supported(k: int, n: int, dtype, device) -> bool:
+    return (torch.device(device).type == "cuda" and dtype in (torch.float32, torch.float64)
+            and 1 <= k <= SELECT_MAX_K and k <= n < 2 ** 31 - 1)
+
+
+def select_query_block(n: int, es: int) -> int:
+    """Queries per product block: the [block, n] block within SELECT_BLOCK_BYTES."""
+    return int(max(1, min(1 << 16, SELECT_BLOCK_BYTES // max(1, es * n))))
+
+
+def select_topk(G: torch.Tensor, qn: torch.Tensor, tn: torch.Tensor, k: int) -> torch.Tensor:
+    """int32 [nq, k]: the k nearest columns of every row of ``G`` under ``|qn_r + tn_c − 2·G_rc|``,
+    nearest first, ties to the lower column (``KnnModel.java:154-194``) — any k up to
+    SELECT_MAX_K, fp32 or fp64 (one 1024-thread block per row: radix passes, then a sort of the k)."""
+    nq, n = G.shape
+    dt = G.dtype
+    if dt not in (torch.float32, torch.float64) or qn.dtype != dt or tn.dtype != dt:
+        raise TypeError("knn select expects fp32 or fp64 products and norms of one dtype")
+    if G.stride(1) != 1 or qn.numel() != nq or tn.numel() != n or not select_supported(k, n, dt, G.device):
+        raise ValueError("knn select: bad shapes G=%s qn=%s tn=%s k=%d" % (tuple(G.shape), tuple(qn.shape),
+                                                                          tuple(tn.shape), k))
+    qn, tn = qn.contiguous(), tn.contiguous()
+    idx = torch.empty((nq, k), dtype=torch.int32, device=G.device)
+    if nq:
+        native.call("fmlx_knn_select", int(dt == torch.float64), native.ptr(G), G.stride(0), nq, n, native.ptr(qn),
+                    native.ptr(tn), int(k), native.ptr(idx), k, native.stream_ptr(G.device))
+    return idx

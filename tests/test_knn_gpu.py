@@ -184,3 +184,67 @@ def test_knn_model_routes_fused_for_k64():
     ref = knn_vote(lab[ridx], torch.unique(lab))
     assert torch.equal(pred.double(), ref.double())
 
+
+
+# ---- any k, fp32 / fp64: radix selection over the product block (ops/csrc/knn_select.hip)
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("k", [1, 65, 300, 1000, 4099])
+def test_select_topk_exact_vs_fp64(dtype, k):
+    """Integer data: every distance is exact, so the ranking must equal the fp64 stable sort
+    exactly — the many ties going to the lower index (KnnModel.java:154-194), k beyond the
+    fused kernel's 64 up to the whole training set."""
+    from flink_ml_amd.ops import knn as ko
+
+    n = 4099
+    Q, T = _int_data(97, n, 11, seed=k + (7 if dtype == torch.float64 else 0))
+    q, t = Q.to(dtype).cuda(), T.to(dtype).cuda()
+    idx = ko.select_topk(q @ t.t(), (q * q).sum(1), (t * t).sum(1), k)
+    ridx, _ = _ref_fp64(Q, T, k)
+    assert torch.equal(idx.long().cpu(), ridx)
+
+
+def test_select_topk_fp64_random_and_nan():
+    from flink_ml_amd.ops import knn as ko
+
+    g = torch.Generator(device="cpu").manual_seed(13)
+    Q = torch.randn((200, 40), generator=g, dtype=torch.float64)
+    T = torch.randn((50000, 40), generator=g, dtype=torch.float64)
+    tn = (T * T).sum(1)
+    tn[9] = float("nan")                                 # a NaN distance ranks last: never chosen
+    G = Q.cuda() @ T.cuda().t()
+    idx = ko.select_topk(G, (Q * Q).sum(1).cuda(), tn.cuda(), 777)
+    assert not torch.any(idx == 9)
+    tn_ref = tn.clone()
+    tn_ref[9] = float("inf")
+    d2 = ((Q * Q).sum(1)[:, None] + tn_ref[None, :] - 2.0 * G.cpu()).abs()
+    ri = torch.sort(d2, dim=1, stable=True).indices[:, :777]
+    assert torch.equal(idx.long().cpu(), ri)
+
+
+@pytest.mark.parametrize("policy,k", [("fp32", 100), ("fp64", 100), ("fp64", 5)])
+def test_knn_model_large_k_and_fp64_on_select_kernel(policy, k, monkeypatch):
+    """KnnModel beyond the fused kernel's k and in the fp64 parity mode runs the select kernel (no
+    torch top-k) and equals the fp64 reference vote."""
+    from flink_ml_amd import Table
+    from flink_ml_amd.config import dtype_policy
+    from flink_ml_amd.models import Knn
+    from flink_ml_amd.models.knn import knn_vote
+    from flink_ml_amd.ops import knn as ko
+
+    def no_topk(*a, **kw):
+        raise AssertionError("torch.topk on the KNN GPU path")
+
+    monkeypatch.setattr(torch, "topk", no_topk)
+    called = []
+    real = ko.select_topk
+    monkeypatch.setattr(ko, "select_topk", lambda *a: called.append(1) or real(*a))
+    Q, T = _int_data(301, 6000, 150, seed=k)  # D 150 > the fused kernel's 128
+    lab = (T[:, 0] > 0).double() + (T[:, 1] > 0).double()
+    with dtype_policy(policy):
+        model = Knn().set_k(k).fit(Table({"features": T.cuda(), "label": lab.cuda()}))
+        pred = model.transform(Table({"features": Q.cuda()}))[0].column("prediction").cpu()
+    assert called
+    ridx, _ = _ref_fp64(Q, T, k)
+    ref = knn_vote(lab[ridx], torch.unique(lab))
+    assert torch.equal(pred.double(), ref.double())
