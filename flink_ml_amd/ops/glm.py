@@ -914,7 +914,7 @@ class BucketRound:
         self.d = d
         # ~256 slices (the backward's parallelism), at most nb_max; ≤ 4096 columns per slice (the
         # backward's column counters share the LDS with a chunk of values)
-        csb = min(12, max(6, int(math.ceil(math.log2(max(1.0, d / 256.0))))))
+        csb = BucketRound.slice_bits(d)
         self.csb = csb
         self.nb = -(-d // (1 << csb))
         if self.nb > nb_max:
@@ -928,9 +928,10 @@ class BucketRound:
         self.rb = max(1, min(4096, int(_ecap / max(avg, 1.0))))
         self.chunk = min(self.CHUNK, chunk_max)
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
-        # one block per CU at most (the chunk fills its LDS); a block loops over the work items, so a
-        # grid of #slices covers evenly loaded slices with one arrival per block
-        self.bwd_blocks = max(1, min(cus, self.nb))
+        # as many backward blocks as the LDS lets share the CUs (a block loops over the work items,
+        # so a grid of #slices covers evenly loaded slices with one arrival per block)
+        blds = self.chunk * es + ((1 << csb) + 1 + 3 * self.nb + 2) * 4
+        self.bwd_blocks = max(1, min(cus * max(1, (160 << 10) // blds), self.nb))
         fblocks = -(-max(1, min(B, n)) // self.rb)
         # batches > 0: the fit visits batches 0 … batches − 1; their per-(block, slice) counts and
         # offsets are made once, before the first round (count_all), when they fit SLOT_BYTES_MAX;
@@ -960,11 +961,16 @@ class BucketRound:
                         native.ptr(self.bst), self.slots, self.mstride, native.stream_ptr(idx.device))
             self.counted = True
 
+    SLICE_COLS = 256  # columns per slice ≈ d / this, as a power of two in [2^6, 2^12]
+
+    @staticmethod
+    def slice_bits(d: int) -> int:
+        return min(12, max(6, int(math.ceil(math.log2(max(1.0, d / float(BucketRound.SLICE_COLS)))))))
+
     @staticmethod
     def nb_for(d: int, es: int = 4) -> int:
         """Column slices of a BucketRound for width d (its `done` counters: this + 16)."""
-        csb = min(12, max(6, int(math.ceil(math.log2(max(1.0, d / 256.0))))))
-        return -(-d // (1 << csb))
+        return -(-d // (1 << BucketRound.slice_bits(d)))
 
     @staticmethod
     def alloc(indptr, values, n: int, d: int, B: int, most: Optional[int] = None, avg: Optional[float] = None,

@@ -1,6 +1,7 @@
 """A/B timing of the single-visit sparse bucket round (glm_sparse.hip glm_bkt_*) on the
 north-star SVC shape (1M columns, 64 nnz per row, 100k-row batches): ms per round of a warmed
-trainer; argv[1]: comma-separated CHUNK sizes of the backward's work items."""
+trainer; argv[1]: comma-separated variants ``CHUNK`` or ``CHUNK:SLICE_COLS`` (the backward's work-item
+size; the number of column slices ≈ d / SLICE_COLS, rounded to a power-of-two slice width)."""
 import json
 import sys
 import time
@@ -24,10 +25,12 @@ def main():
     vals = torch.rand((n * nnz,), generator=g, device=dev, dtype=torch.float32)
     X = SparseColumn(indptr, idx.reshape(-1), vals, dim)
     y = torch.randint(0, 2, (n,), generator=g, device=dev).to(torch.float32)
-    variants = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else [str(gk.BucketRound.CHUNK)])]
+    variants = [[int(x) for x in v.split(":")] for v in (sys.argv[1].split(",") if len(sys.argv) > 1
+                                                          else [str(gk.BucketRound.CHUNK)])]
     gk.TILE_MIN_VISITS = 10 ** 9
     for v in variants:
-        gk.BucketRound.CHUNK = v
+        gk.BucketRound.CHUNK = v[0]
+        gk.BucketRound.SLICE_COLS = v[1] if len(v) > 1 else 256
         tr = DeviceGlmTrainer(SGD(max_iter=10 ** 8, learning_rate=0.1, global_batch_size=100_000, tol=0.0),
                               np.zeros(dim), X, y, None, "hinge")
         assert tr.bkt is not None
@@ -38,7 +41,7 @@ def main():
         tr.run_rounds(R)
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) * 1e3 / R
-        print(json.dumps({"chunk": v, "ms_per_round": round(ms, 4), "csb": tr.bkt.csb, "nb": tr.bkt.nb, "rb": tr.bkt.rb,
+        print(json.dumps({"chunk": v[0], "slice_cols": gk.BucketRound.SLICE_COLS, "ms_per_round": round(ms, 4), "csb": tr.bkt.csb, "nb": tr.bkt.nb, "rb": tr.bkt.rb,
                           "G": tr.bkt.G, "bwd_blocks": tr.bkt.bwd_blocks}), flush=True)
 
 
