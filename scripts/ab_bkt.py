@@ -3,13 +3,14 @@ north-star SVC shape (1M columns, 64 nnz per row, 100k-row batches): ms per roun
 trainer; argv[1]: comma-separated variants ``CHUNK`` or ``CHUNK:SLICE_COLS`` (the backward's work-item
 size; the number of column slices ≈ d / SLICE_COLS, rounded to a power-of-two slice width)."""
 import json
+import os
 import sys
 import time
 
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
