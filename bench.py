@@ -95,7 +95,9 @@ def verify_exchange(make, comm, rounds: int = VERIFY_ROUNDS):
     cb = b.coef[:b.d_model].double().cpu()
     from flink_ml_amd.parallel.context import get_context
 
-    if os.environ.get("FMLX_BENCH_INJECT_EXCHANGE_ERROR") == str(get_context().rank):
+    me = str(get_context().rank)
+    if os.environ.get("FMLX_BENCH_INJECT_EXCHANGE_ERROR") == me or (
+            os.environ.get("FMLX_BENCH_INJECT_XGMI_ERROR") == me and getattr(a, "xg", None) is not None):
         ca = ca.clone()
         ca[0] += 1e-3 * (1.0 + ca.abs().max())  # test hook: a corrupted exchange on this rank
     replicas = comm.all_gather_tensor(ca)
@@ -322,6 +324,27 @@ def main():
             verified, vinfo = verify_exchange(make_trainer, comm)
             verified = verified and same
             vinfo.update(timed_replicas_identical=same, strict_fence=True)
+        if not verified and trainer.xg is not None:
+            # the in-kernel exchange disagrees even with system-scope fences: time the process-group
+            # path (feedback → RCCL all-reduce → update) instead and report THAT, verified the same
+            # way — never the xGMI number
+            from flink_ml_amd.parallel import xgmi
+
+            if rank == 0:
+                print("exchange_verified: false with the strict fence too (%s); re-timing on the RCCL path"
+                      % vinfo, file=sys.stderr, flush=True)
+            xgmi.disable()
+            trainer = make_trainer()
+            trainer.use_rccl()
+            elapsed, kernel_s = timed_region(trainer, ctx, args.warmup, args.steps)
+            elapsed = comm.all_reduce_scalar(elapsed, "max")
+            kernel_s = comm.all_reduce_scalar(kernel_s, "max")
+            trainer.flush()
+            final = comm.all_gather_tensor(trainer.coef[:trainer.d_model].double().cpu())
+            same = comm.all_agree(all(torch.equal(final[0], c) for c in final))
+            verified, vinfo = verify_exchange(make_trainer, comm)
+            verified = verified and same
+            vinfo.update(timed_replicas_identical=same, xgmi_rejected=True)
         if not verified:
             if rank == 0:
                 print(json.dumps({"exchange_verified": False, "detail": vinfo}), flush=True)
