@@ -30,6 +30,7 @@ _HLIB = None
 # None: not done — no GPU, or FMLX_PRELOAD=0), and the number of code objects
 PRELOAD_MS = None
 PRELOAD_OBJECTS = 0
+PRELOAD_STAGES = {}  # ms per stage of the library load (code objects, pinned blocks, dry launches, pool)
 
 DT_F32, DT_F64, DT_BF16, DT_F16, DT_I32, DT_I64 = 0, 1, 2, 3, 4, 5
 
@@ -207,17 +208,22 @@ def _preload(lib) -> None:
     t0 = time.perf_counter()
     k = fn(torch.cuda.current_stream().cuda_stream)
     PRELOAD_MS = (time.perf_counter() - t0) * 1e3
+    PRELOAD_STAGES["code_objects"] = round(PRELOAD_MS, 2)
     if k < 0:
         raise RuntimeError("preloading the kernel library's code objects failed (%d)" % k)
     from ..utils import hostsync
 
+    t1 = time.perf_counter()
     hostsync.warm(torch.cuda.current_device())  # pinned read-back block + first-use imports
+    PRELOAD_STAGES["pinned_readback"] = round((time.perf_counter() - t1) * 1e3, 2)
+    t1 = time.perf_counter()
     warm = getattr(lib, "fmlx_glm_sparse_warm", None)  # every sparse-round kernel launched once, dry
     if warm is not None:
         warm.argtypes, warm.restype = [c_void_p], c_int
         if warm(torch.cuda.current_stream().cuda_stream) != 0:
             raise RuntimeError("warming the sparse round kernels failed")
         torch.cuda.current_stream().synchronize()
+    PRELOAD_STAGES["sparse_warm_launches"] = round((time.perf_counter() - t1) * 1e3, 2)
     torch.cuda.get_device_properties(torch.cuda.current_device())  # (first call: runtime queries)
     # the bucket round's compile-time limits, read here (a first fit paid ~50 µs for the first call
     # of the entry point); through ``lib``: kernels() holds its lock until this returns
@@ -232,9 +238,11 @@ def _preload(lib) -> None:
     # first fit are then carved out of it instead of each new size paying a hipMalloc inside the fit
     # (a fresh hipMalloc is tens to hundreds of µs of GPU-idle host time)
     pool = int(os.environ.get("FMLX_DEVICE_POOL_MB", "2048")) << 20
+    t1 = time.perf_counter()
     if pool > 0:
         seg = torch.empty(pool, dtype=torch.uint8, device=torch.cuda.current_device())
         del seg
+    PRELOAD_STAGES["device_pool"] = round((time.perf_counter() - t1) * 1e3, 2)
     PRELOAD_MS = (time.perf_counter() - t0) * 1e3
     PRELOAD_OBJECTS = k
 

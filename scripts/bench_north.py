@@ -265,6 +265,7 @@ def run_svc_sparse(a, ctx):
             "whole_fit_device_span_ms": [round(x, 3) for x in spans],
             "library_preload_ms": None if native.PRELOAD_MS is None else round(native.PRELOAD_MS, 2),
             "library_preload_code_objects": native.PRELOAD_OBJECTS,
+            "library_preload_stages_ms": native.PRELOAD_STAGES,
             "whole_fit_max_ms": round(max(samples) * 1e3, 3), "whole_fit_device_alloc_free": mem_deltas, "whole_fit_median_ms": round(sorted(samples)[len(samples) // 2] * 1e3, 3),
             "steady_ms_per_round": round(steady_s * 1e3 / steady, 4),
             "steady_samples_per_s": round(gb * steady / steady_s, 1),
