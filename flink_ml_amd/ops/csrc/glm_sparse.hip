@@ -769,21 +769,51 @@ __global__ __launch_bounds__(BK_NT) void glm_bkt_count_kernel(const long* __rest
   for (int i = threadIdx.x; i < ns * k.nb; i += BK_NT) bk_hist[i] = 0;
   __syncthreads();
   const long j0 = jsub[0], j1 = jsub[ns];
-  long j = j0 + threadIdx.x;
-  auto sub_of = [&](long jj) {
+  // sub-block of an entry from its offset in the range (32-bit: a count block's range is short)
+  int bnd[CG];
+#pragma unroll
+  for (int i = 1; i < CG; ++i) bnd[i] = i < ns ? (int)(jsub[i] - j0) : 0x7fffffff;
+  auto count = [&](long jj, int c) {
+    const int r = (int)(jj - j0);
     int q = 0;
 #pragma unroll
-    for (int i = 1; i < CG; ++i) q += (i < ns && jsub[i] <= jj) ? 1 : 0;
-    return q;
+    for (int i = 1; i < CG; ++i) q += bnd[i] <= r ? 1 : 0;
+    atomicAdd(&bk_hist[q * k.nb + (c >> k.csb)], 1);
   };
-  for (; j + 3 * BK_NT < j1; j += 4 * BK_NT) {
-    int c[4];
+  // the column indices as 16-byte vectors over the 4-aligned middle of the range (two vectors in
+  // flight per thread: 4× the bytes outstanding of scalar loads), scalar head and tail
+  const long a = (j0 + 3) & ~3L, b = j1 & ~3L;
+  if (a >= b) {
+    for (long j = j0 + threadIdx.x; j < j1; j += BK_NT) count(j, __builtin_nontemporal_load(idx + j));
+  } else {
+    if (j0 + (long)threadIdx.x < a) count(j0 + threadIdx.x, __builtin_nontemporal_load(idx + j0 + threadIdx.x));
+    if (b + (long)threadIdx.x < j1) count(b + threadIdx.x, __builtin_nontemporal_load(idx + b + threadIdx.x));
+    typedef int i4_t __attribute__((ext_vector_type(4)));
+    const i4_t* v = reinterpret_cast<const i4_t*>(idx + a);
+    const long nv = (b - a) >> 2;
+    long q = threadIdx.x;
+    for (; q + 1 * BK_NT < nv; q += 2 * BK_NT) {
+      i4_t c[2];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) c[t] = __builtin_nontemporal_load(idx + j + t * BK_NT);
+      for (int t = 0; t < 2; ++t) c[t] = __builtin_nontemporal_load(v + q + t * BK_NT);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) atomicAdd(&bk_hist[sub_of(j + t * BK_NT) * k.nb + (c[t] >> k.csb)], 1);
+      for (int t = 0; t < 2; ++t) {
+        const long jj = a + 4 * (q + t * BK_NT);
+        count(jj, c[t].x);
+        count(jj + 1, c[t].y);
+        count(jj + 2, c[t].z);
+        count(jj + 3, c[t].w);
+      }
+    }
+    for (; q < nv; q += BK_NT) {
+      const i4_t c = __builtin_nontemporal_load(v + q);
+      const long jj = a + 4 * q;
+      count(jj, c.x);
+      count(jj + 1, c.y);
+      count(jj + 2, c.z);
+      count(jj + 3, c.w);
+    }
   }
-  for (; j < j1; j += BK_NT) atomicAdd(&bk_hist[sub_of(j) * k.nb + (__builtin_nontemporal_load(idx + j) >> k.csb)], 1);
   __syncthreads();
   // (bucket-major: consecutive threads take one bucket's ns consecutive blocks, 32-byte runs)
   int* cm = k.cntm + slot * k.mstride;
