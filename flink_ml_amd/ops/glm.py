@@ -881,6 +881,8 @@ def _bkt_limits():
     """The bucket round kernels' compile-time limits (csrc/glm_sparse.hip fmlx_glm_bkt_limits), read once
     (at library load: native._preload)."""
     global _BKT_LIMITS
+    if _BKT_LIMITS is None and native.BKT_LIMITS is not None:
+        _BKT_LIMITS = native.BKT_LIMITS
     if _BKT_LIMITS is None:
         lim = np.zeros(8, dtype=np.int32)
         native.kernels().fmlx_glm_bkt_limits(lim.ctypes.data)

@@ -30,6 +30,7 @@ _HLIB = None
 # None: not done — no GPU, or FMLX_PRELOAD=0), and the number of code objects
 PRELOAD_MS = None
 PRELOAD_OBJECTS = 0
+BKT_LIMITS = None  # the bucket round's compile-time limits (ops/glm.py _bkt_limits), read at load
 PRELOAD_STAGES = {}  # ms per stage of the library load (code objects, pinned blocks, dry launches, pool)
 
 DT_F32, DT_F64, DT_BF16, DT_F16, DT_I32, DT_I64 = 0, 1, 2, 3, 4, 5
@@ -227,13 +228,14 @@ def _preload(lib) -> None:
     torch.cuda.get_device_properties(torch.cuda.current_device())  # (first call: runtime queries)
     # the bucket round's compile-time limits, read here (a first fit paid ~50 µs for the first call
     # of the entry point); through ``lib``: kernels() holds its lock until this returns
+    # (no package import here: a module imported inside this lock could register signatures that
+    # _apply_sigs has already passed)
+    global BKT_LIMITS
     import numpy as np
-
-    from . import glm
 
     lim = np.zeros(8, dtype=np.int32)
     lib.fmlx_glm_bkt_limits(lim.ctypes.data)
-    glm._BKT_LIMITS = lim
+    BKT_LIMITS = lim
     # one device segment for torch's caching allocator, freed at once: the trainers' buffers of a
     # first fit are then carved out of it instead of each new size paying a hipMalloc inside the fit
     # (a fresh hipMalloc is tens to hundreds of µs of GPU-idle host time)
