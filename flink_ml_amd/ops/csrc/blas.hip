@@ -597,10 +597,35 @@ FMLX_API int fmlx_fill32(void* p, long n, unsigned v, void* stream) {
   return (int)hipGetLastError();
 }
 
+// *out = the longest row (out zeroed first by batch_bounds_kernel's launch): a wave max per
+// grid-stride sweep, one 64-bit atomic max per wave
+__global__ __launch_bounds__(256) void row_len_max_kernel(const long* __restrict__ indptr, long n,
+                                                          unsigned long long* __restrict__ out) {
+  unsigned long long m = 0;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const unsigned long long l = (unsigned long long)(indptr[i + 1] - indptr[i]);
+    m = l > m ? l : m;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long t = __shfl_xor(m, o, 64);
+    m = t > m ? t : m;
+  }
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
+}
+
+// out[0] = indptr[n]; out[1 + b] = indptr[min(b·B, n)] for b = 0 … P; out[P + 2] = the longest row
 FMLX_API int fmlx_csr_batch_bounds(const long* indptr, long n, long B, long P, long* out, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
   long b = (P + 2 + 255) / 256;
   if (b > 1024) b = 1024;
-  hipLaunchKernelGGL(batch_bounds_kernel, dim3((unsigned)b), dim3(256), 0, (hipStream_t)stream, indptr, n, B, P, out);
+  hipLaunchKernelGGL(batch_bounds_kernel, dim3((unsigned)b), dim3(256), 0, s, indptr, n, B, P, out);
+  if (hipMemsetAsync(out + P + 2, 0, sizeof(long), s) != hipSuccess) return -1;
+  long r = (n + 255) / 256;
+  if (r > 2048) r = 2048;
+  if (r < 1) r = 1;
+  hipLaunchKernelGGL(row_len_max_kernel, dim3((unsigned)r), dim3(256), 0, s, indptr, n,
+                     (unsigned long long*)(out + P + 2));
   return (int)hipGetLastError();
 }
 

@@ -362,6 +362,7 @@ def seg_sort(keys: torch.Tensor, vals: torch.Tensor, bounds, kbase, key_bits: in
 
 
 _BOUNDS_CACHE = {}  # id(indptr) -> (weak reference, {(n, B, version): (nnz, bounds)})
+_ROW_MAX = {}  # (id(indptr), n, B, version) -> the longest row (filled with the bounds)
 _BOUNDS_PENDING = {}  # id(indptr) -> (weak reference, key, pinned host buffer, completion event)
 
 
@@ -379,15 +380,20 @@ def prefetch_batch_bounds(indptr: torch.Tensor, n: int, B: int) -> None:
     if pend is not None and pend[0]() is indptr and pend[1] == key:
         return
     P = (n + B - 1) // B
-    out = torch.empty(P + 2, dtype=torch.int64, device=indptr.device)
+    out = torch.empty(P + 3, dtype=torch.int64, device=indptr.device)
     native.call("fmlx_csr_batch_bounds", native.ptr(indptr.contiguous()), n, B, P, native.ptr(out),
                 native.stream_ptr(indptr.device))
-    host = torch.empty(P + 2, dtype=torch.int64, pin_memory=True)
+    host = torch.empty(P + 3, dtype=torch.int64, pin_memory=True)
     host.copy_(out, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(indptr.device))
     ref = weakref.ref(indptr, lambda _r, i=id(indptr): _BOUNDS_PENDING.pop(i, None))
     _BOUNDS_PENDING[id(indptr)] = (ref, key, host, ev, out)
+
+
+def batch_row_max(indptr: torch.Tensor, n: int, B: int) -> Optional[int]:
+    """The longest row of the partition, read together with :func:`_batch_bounds` (None before)."""
+    return _ROW_MAX.get((id(indptr), n, B, indptr._version))
 
 
 def _batch_bounds(indptr: torch.Tensor, n: int, B: int):
@@ -400,6 +406,7 @@ def _batch_bounds(indptr: torch.Tensor, n: int, B: int):
         return ent[1][key]
     from ..utils import hostsync
 
+    P = (n + B - 1) // B
     if indptr.is_cuda:
         # one library kernel + one polled copy (no torch index / arange / cat kernels: their code
         # objects load lazily, tens of ms inside the first fit of a process)
@@ -408,10 +415,11 @@ def _batch_bounds(indptr: torch.Tensor, n: int, B: int):
         hostsync.wait_event(ev)
         both = host.tolist()
     else:
-        P = (n + B - 1) // B
         sel = torch.arange(0, P + 1).mul_(B).clamp_(max=n)
-        both = torch.cat([indptr[-1:], indptr[sel]]).tolist()
-    val = (int(both[0]), both[1:])
+        lens = indptr[1:n + 1] - indptr[:n]
+        both = torch.cat([indptr[-1:], indptr[sel], lens.max().reshape(1) if n else indptr[:1] * 0]).tolist()
+    val = (int(both[0]), both[1:P + 2])
+    _ROW_MAX[(id(indptr),) + key] = int(both[P + 2])
     if ent is None or ent[0]() is not indptr:
         ref = weakref.ref(indptr, lambda _r, i=id(indptr): _BOUNDS_CACHE.pop(i, None))
         ent = (ref, {})
@@ -903,6 +911,8 @@ class BucketRound:
 
     SLOT_BYTES_MAX = 256 << 20  # the one-time counts of a fit's batches: at most this much
 
+    RB_HEADROOM = 1.1  # rows per forward block leave this factor of the mean row length free
+
     def __init__(self, indptr, values, n: int, d: int, B: int, G: int, most: Optional[int] = None,
                  avg: Optional[float] = None, batches: int = 0, zero_bufs=None):
         lim = _bkt_limits()
@@ -921,13 +931,18 @@ class BucketRound:
         self.nb = -(-d // (1 << csb))
         if self.nb > nb_max:
             raise ValueError("too many column slices")
+        longest = None
         if most is None:
             nnz, bounds = _batch_bounds(indptr, n, B)
             most = max(bounds[i + 1] - bounds[i] for i in range(len(bounds) - 1))
             avg = nnz / max(1, n)
-        # forward rows per block: one staged piece of ECAP entries on average (a multiple of the
-        # lane groups per block)
-        self.rb = max(1, min(4096, int(_ecap / max(avg, 1.0))))
+            longest = batch_row_max(indptr, n, B)
+        # forward rows per block: one staged piece of ECAP entries — exactly, when every row has the
+        # same length; else with 10 % headroom, so a block whose rows run longer than average rarely
+        # overflows into the multi-piece path (56 rows of Poisson(64) lengths exceed 3584 entries in
+        # half the blocks; their mean exceeding 1.1·64 is a 5-sigma event)
+        uniform = longest is not None and longest <= avg
+        self.rb = max(1, min(4096, int(_ecap / (max(avg, 1.0) * (1.0 if uniform else self.RB_HEADROOM)))))
         self.chunk = min(self.CHUNK, chunk_max)
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         # as many backward blocks as the LDS lets share the CUs (a block loops over the work items,
