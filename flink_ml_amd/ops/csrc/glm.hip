@@ -392,7 +392,8 @@ __device__ bool defer_prologue_xgmi(const GlmTail& tl, A* coef, int* state, int 
       for (;;) {
         v = ld_agent(wflag);
         if ((v >> 1) == e) break;
-        if (++it > 4 * tl.x.spin_limit) {  // the lead never published: stop, and say so
+        if (++it > 4 * tl.x.spin_limit || ((it & 1023) == 0 && xgmi::ld_sys(tl.x.err) != 0)) {
+          // the lead never published (or an exchange already gave up): stop, and say so
           xgmi::st_sys(tl.x.err, 1);
           v = (e << 1) | 1;
           break;

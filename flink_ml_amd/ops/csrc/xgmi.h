@@ -122,7 +122,9 @@ __device__ __forceinline__ bool signal_and_wait(const Ctx& x, long flag_off, int
     const int* f = at<int>(x.peers[threadIdx.x], flag_off) + idx;
     long it = 0;
     while (ld_sys(f) != tag) {
-      if (++it > x.spin_limit) {
+      // (an exchange of this context already gave up: the error word is raised and every result
+      // is discarded — stop after a short poll instead of a full spin limit per call)
+      if (++it > x.spin_limit || ((it & 1023) == 0 && ld_sys(x.err) != 0)) {
         st_sys(x.err, 1);  // plain system-scope store (host memory: no PCIe atomics needed)
         s_timeout = 1;     // any writer, same value
         break;
