@@ -10,13 +10,16 @@
 //     (sqrt is monotone: never applied) and read as its IEEE bits (non-negative: the unsigned
 //     order is the numeric order, NaN last);
 //   * radix passes of 11 bits over the row (LDS histogram with integer atomics, a block scan)
-//     find the k-th smallest key T and how many keys equal to T belong to the result;
+//     narrow down the bin of the k-th smallest key; as soon as the keys of that bin and below fit
+//     the LDS (after one or two passes for continuous data: the top bits are mostly exponent) one
+//     more pass collects them and a bitonic sort by (key, index) ends it. Otherwise the passes run
+//     to the last digit: the k-th smallest key T and how many keys equal to T belong to the result;
 //   * one pass appends every key < T; a second takes the keys equal to T in INDEX order (each
 //     wave owns a contiguous segment, ranks by ballot + mbcnt after a scan of the waves' counts) —
 //     the reference's tie rule;
 //   * the k (key, index) pairs are bitonic-sorted in LDS by (key, index) and written out.
-// The row is re-read once per pass (3 + 2 for fp32, 6 + 2 for fp64); it stays in L2 / the
-// Infinity Cache for the usual query blocks.
+// The row is re-read once per pass (at most 3 + 2 for fp32 / 6 + 2 for fp64); it stays in L2 /
+// the Infinity Cache for the usual query blocks.
 #include "common.h"
 
 #include <math.h>
@@ -72,22 +75,45 @@ __device__ __forceinline__ int sel_exscan(int v, int* tmp, int* total) {
 template <typename A>
 __global__ __launch_bounds__(SEL_NT) void knn_select_kernel(const A* __restrict__ G, long ldg, long n,
                                                             const A* __restrict__ qn, const A* __restrict__ tn,
-                                                            int k, int kp, int* __restrict__ out, long ldo) {
+                                                            int k, int kp, int cap, int* __restrict__ out, long ldo) {
   typedef typename SelKey<A>::U U;
   constexpr int TOTAL = (int)sizeof(U) * 8;
   extern __shared__ __align__(16) unsigned char sel_smem[];
   int* hist = reinterpret_cast<int*>(sel_smem);              // [SEL_NB]
-  U* sk = reinterpret_cast<U*>(hist + SEL_NB);               // [kp] selected keys
-  int* si = reinterpret_cast<int*>(sk + kp);                 // [kp] selected indices
+  U* sk = reinterpret_cast<U*>(hist + SEL_NB);               // [cap] selected keys
+  int* si = reinterpret_cast<int*>(sk + cap);                // [cap] selected indices
   __shared__ int tmp[SEL_NT / 64];
   __shared__ int wcnt[SEL_NT / 64];
-  __shared__ int s_digit, s_rem, s_lt;
+  __shared__ int s_digit, s_rem, s_lt, s_hbin;
   const long row = blockIdx.x;
   const A* __restrict__ g = G + row * ldg;
   const A q = qn[row];
   const int tid = threadIdx.x;
   auto key = [&](long j) -> U { return SelKey<A>::bits(q + tn[j] - (A)2 * g[j]); };
 
+  // bitonic sort of sk/si[0, S) by (key, index), S a power of two; the first k indices out
+  auto sort_and_write = [&](int S) {
+    for (int size = 2; size <= S; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int i = tid; i < S / 2; i += SEL_NT) {
+          const int a = 2 * i - (i & (stride - 1));
+          const int b = a + stride;
+          const bool up = (a & size) == 0;
+          const U ka = sk[a], kb = sk[b];
+          const int ia = si[a], ib = si[b];
+          const bool gt = ka > kb || (ka == kb && ia > ib);
+          if (gt == up) {
+            sk[a] = kb;
+            sk[b] = ka;
+            si[a] = ib;
+            si[b] = ia;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    for (int i = tid; i < k; i += SEL_NT) out[row * ldo + i] = si[i];
+  };
   // ---- radix select: T = the k-th smallest key, rem = how many keys equal to T are taken
   U prefix = 0;
   int rem = k;
@@ -109,11 +135,42 @@ __global__ __launch_bounds__(SEL_NT) void knn_select_kernel(const A* __restrict_
     if (before < rem && rem <= before + h0) {
       s_digit = 2 * tid;
       s_rem = rem - before;
+      s_hbin = h0;
     } else if (before + h0 < rem && rem <= before + h0 + h1) {
       s_digit = 2 * tid + 1;
       s_rem = rem - before - h0;
+      s_hbin = h1;
     }
     __syncthreads();
+    if ((k - s_rem) + s_hbin <= cap) {
+      // the keys whose bits above `lo` are at most the k-th one's — every key below its bin plus
+      // the bin itself — fit the LDS: collect them in one more pass and sort them by (key, index);
+      // the first k are the answer, ties included (the usual case after one or two radix passes)
+      const U top = (prefix >> lo) | (U)s_digit;
+      if (tid == 0) s_lt = 0;
+      __syncthreads();
+      for (long j = tid; j < n; j += SEL_NT) {
+        const U u = key(j);
+        if ((u >> lo) <= top) {
+          const int p = atomicAdd(&s_lt, 1);
+          if (p < cap) {
+            sk[p] = u;
+            si[p] = (int)j;
+          }
+        }
+      }
+      __syncthreads();
+      const int cnt = s_lt < cap ? s_lt : cap;
+      int S = 2;
+      while (S < cnt) S <<= 1;
+      for (int i = cnt + tid; i < S; i += SEL_NT) {
+        sk[i] = ~(U)0;
+        si[i] = 0x7fffffff;
+      }
+      __syncthreads();
+      sort_and_write(S);
+      return;
+    }
     prefix |= (U)s_digit << lo;
     rem = s_rem;
     hi = lo;
@@ -165,26 +222,7 @@ __global__ __launch_bounds__(SEL_NT) void knn_select_kernel(const A* __restrict_
     si[i] = 0x7fffffff;
   }
   __syncthreads();
-  for (int size = 2; size <= kp; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = tid; i < kp / 2; i += SEL_NT) {
-        const int a = 2 * i - (i & (stride - 1));
-        const int b = a + stride;
-        const bool up = (a & size) == 0;
-        const U ka = sk[a], kb = sk[b];
-        const int ia = si[a], ib = si[b];
-        const bool gt = ka > kb || (ka == kb && ia > ib);
-        if (gt == up) {
-          sk[a] = kb;
-          sk[b] = ka;
-          si[a] = ib;
-          si[b] = ia;
-        }
-      }
-      __syncthreads();
-    }
-  }
-  for (int i = tid; i < k; i += SEL_NT) out[row * ldo + i] = si[i];
+  sort_and_write(kp);
 }
 
 }  // namespace
@@ -203,13 +241,14 @@ FMLX_API int fmlx_knn_select(int acc_f64, const void* G, long ldg, long nq, long
   while (kp < k) kp <<= 1;
   if (kp < 2) kp = 2;
   const size_t es = acc_f64 ? 8 : 4;
-  const size_t lds = (size_t)SEL_NB * 4 + (size_t)kp * (es + 4);
+  const int cap = kp > 2048 ? kp : 2048;  // LDS entries: the k winners, or the two-pass candidates
+  const size_t lds = (size_t)SEL_NB * 4 + (size_t)cap * (es + 4);
   if (acc_f64)
     hipLaunchKernelGGL(knn_select_kernel<double>, dim3((unsigned)nq), dim3(SEL_NT), lds, s, (const double*)G, ldg, n,
-                       (const double*)qn, (const double*)tn, k, kp, idx, ldo);
+                       (const double*)qn, (const double*)tn, k, kp, cap, idx, ldo);
   else
     hipLaunchKernelGGL(knn_select_kernel<float>, dim3((unsigned)nq), dim3(SEL_NT), lds, s, (const float*)G, ldg, n,
-                       (const float*)qn, (const float*)tn, k, kp, idx, ldo);
+                       (const float*)qn, (const float*)tn, k, kp, cap, idx, ldo);
   return (int)hipGetLastError();
 }
 

@@ -33,8 +33,12 @@ def main():
                             (10_000, 100_000, 100, 10, torch.float64), (10_000, 100_000, 100, 500, torch.float64),
                             (2_000, 1_000_000, 64, 256, torch.float32)]:
         g = torch.Generator(device=dev).manual_seed(1)
-        Q = torch.randint(-3, 4, (nq, d), generator=g, device=dev).to(dt)
-        T = torch.randint(-3, 4, (n, d), generator=g, device=dev).to(dt)
+        if "--float" in sys.argv:  # continuous data: few ties, the two-pass selection applies
+            Q = torch.randn((nq, d), generator=g, device=dev, dtype=dt)
+            T = torch.randn((n, d), generator=g, device=dev, dtype=dt)
+        else:  # small integers: exact distances, many ties
+            Q = torch.randint(-3, 4, (nq, d), generator=g, device=dev).to(dt)
+            T = torch.randint(-3, 4, (n, d), generator=g, device=dev).to(dt)
         qn, tn = (Q * Q).sum(1), (T * T).sum(1)
         qb = ko.select_query_block(n, Q.element_size())
 
@@ -61,7 +65,8 @@ def main():
             D = (qn[:, None] + tn[None, :] - 2 * Q @ T.t()).abs()
             same = bool(torch.equal(torch.gather(D, 1, a.long()), torch.gather(D, 1, b.long())))
             del D
-        print(json.dumps({"nq": nq, "n": n, "d": d, "k": k, "dtype": str(dt).split(".")[-1],
+        print(json.dumps({"data": "float" if "--float" in sys.argv else "int", "nq": nq, "n": n, "d": d, "k": k,
+                          "dtype": str(dt).split(".")[-1],
                           "select_ms": round(t_ours, 3), "torch_topk_ms": round(t_lib, 3),
                           "same_distances": same}), flush=True)
 
