@@ -248,3 +248,20 @@ def test_knn_model_large_k_and_fp64_on_select_kernel(policy, k, monkeypatch):
     ridx, _ = _ref_fp64(Q, T, k)
     ref = knn_vote(lab[ridx], torch.unique(lab))
     assert torch.equal(pred.double(), ref.double())
+
+
+@pytest.mark.parametrize("k", [1, 300, 2000])
+def test_select_topk_fp32_continuous_fast_path(k):
+    """Continuous fp32 data: the select kernel's collect-and-sort path (the k-th key's bin and all
+    below fit the LDS after a radix pass) must give exactly the stable sort of the same keys."""
+    from flink_ml_amd.ops import knn as ko
+
+    g = torch.Generator(device="cpu").manual_seed(k + 17)
+    Q = torch.randn((64, 24), generator=g)
+    T = torch.randn((20000, 24), generator=g)
+    G = Q.cuda() @ T.cuda().t()
+    qn, tn = (Q * Q).sum(1), (T * T).sum(1)
+    idx = ko.select_topk(G, qn.cuda(), tn.cuda(), k)
+    d2 = ((qn[:, None] + tn[None, :]) - 2.0 * G.cpu()).abs()
+    ri = torch.sort(d2, dim=1, stable=True).indices[:, :k]
+    assert torch.equal(idx.long().cpu(), ri)
