@@ -362,7 +362,7 @@ def seg_sort(keys: torch.Tensor, vals: torch.Tensor, bounds, kbase, key_bits: in
 
 
 _BOUNDS_CACHE = {}  # id(indptr) -> (weak reference, {(n, B, version): (nnz, bounds)})
-_ROW_MAX = {}  # (id(indptr), n, B, version) -> the longest row (filled with the bounds)
+_ROW_MAX = {}  # id(indptr) -> {(n, B, version): the longest row} (filled with the bounds)
 _BOUNDS_PENDING = {}  # id(indptr) -> (weak reference, key, pinned host buffer, completion event)
 
 
@@ -393,7 +393,7 @@ def prefetch_batch_bounds(indptr: torch.Tensor, n: int, B: int) -> None:
 
 def batch_row_max(indptr: torch.Tensor, n: int, B: int) -> Optional[int]:
     """The longest row of the partition, read together with :func:`_batch_bounds` (None before)."""
-    return _ROW_MAX.get((id(indptr), n, B, indptr._version))
+    return _ROW_MAX.get(id(indptr), {}).get((n, B, indptr._version))
 
 
 def _batch_bounds(indptr: torch.Tensor, n: int, B: int):
@@ -419,12 +419,18 @@ def _batch_bounds(indptr: torch.Tensor, n: int, B: int):
         lens = indptr[1:n + 1] - indptr[:n]
         both = torch.cat([indptr[-1:], indptr[sel], lens.max().reshape(1) if n else indptr[:1] * 0]).tolist()
     val = (int(both[0]), both[1:P + 2])
-    _ROW_MAX[(id(indptr),) + key] = int(both[P + 2])
     if ent is None or ent[0]() is not indptr:
-        ref = weakref.ref(indptr, lambda _r, i=id(indptr): _BOUNDS_CACHE.pop(i, None))
+        _ROW_MAX[id(indptr)] = {}
+
+        def _forget(_r, i=id(indptr)):
+            _BOUNDS_CACHE.pop(i, None)
+            _ROW_MAX.pop(i, None)
+
+        ref = weakref.ref(indptr, _forget)
         ent = (ref, {})
         _BOUNDS_CACHE[id(indptr)] = ent
     ent[1][key] = val
+    _ROW_MAX.setdefault(id(indptr), {})[key] = int(both[P + 2])
     return val
 
 
