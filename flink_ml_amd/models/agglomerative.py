@@ -40,9 +40,24 @@ native.register_host_sigs({"fmlx_nnchain": ([ctypes.c_void_p, ctypes.c_int64, ct
                                              ctypes.c_int64)})
 
 
+native.register_kernel_sigs({"fmlx_pairwise_euclid_f64": [ctypes.c_void_p, ctypes.c_long, ctypes.c_int,
+                                                             ctypes.c_long, ctypes.c_void_p, ctypes.c_long,
+                                                             ctypes.c_void_p]})
+
+
 def pairwise_distances(X: torch.Tensor, metric: str) -> torch.Tensor:
-    """Full [n, n] fp64 distance matrix with the reference DistanceMeasure formulas."""
+    """Full [n, n] fp64 distance matrix with the reference DistanceMeasure formulas. Euclidean on
+    the GPU is one library kernel (csrc/blas.hip pairwise_euclid_f64_kernel): a GEMM plus clamp /
+    sqrt passes through torch would also load their code objects lazily, ~60 ms inside the first
+    fit of a process."""
     X = X.to(torch.float64)
+    if metric == "euclidean" and X.device.type == "cuda" and 0 < X.shape[0] <= 16 * 65535:
+        X = X.contiguous()
+        n, d = X.shape
+        out = torch.empty((n, n), dtype=torch.float64, device=X.device)
+        native.call("fmlx_pairwise_euclid_f64", native.ptr(X), n, d, max(d, 1), native.ptr(out), n,
+                    native.stream_ptr(X.device))
+        return out
     if metric == "manhattan":
         return torch.cdist(X, X, p=1)
     sq = (X * X).sum(1)

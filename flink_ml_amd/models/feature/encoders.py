@@ -138,6 +138,16 @@ class OneHotEncoder(Estimator, OneHotEncoderParams):
         maxes = []
         for c in cols:
             x = _numeric_col(t, c)
+            if x.is_cuda and x.numel() and x.dtype in (torch.float32, torch.float64):
+                # one library reduction (min, max, any non-integer / non-finite) answers the checks
+                # for valid input; torch's compare / any kernels would load their code objects
+                # lazily inside the first fit of a process
+                from ...ops import catstats
+
+                mn, mxv, non = catstats.flags(x)
+                if not non and mn >= 0.0 and mxv < 2.0 ** 62:
+                    maxes.append(int(mxv))
+                    continue
             xi = x.to(torch.int64)
             if x.numel() and bool((xi.to(x.dtype) != x).any()):
                 bad = x[xi.to(x.dtype) != x][0].item()

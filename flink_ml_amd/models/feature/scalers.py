@@ -59,8 +59,8 @@ class StandardScalerModel(ModelWithData, StandardScalerParams):
         mean, std = self.model_data_rows()[0]
         X = vector_input(t, self.get(self.INPUT_COL))
         dev = X.values.device if isinstance(X, SparseColumn) else X.device
-        sd = _t(std, dev)
-        scale = torch.where(sd == 0, torch.zeros_like(sd), 1.0 / torch.where(sd == 0, torch.ones_like(sd), sd))
+        sd = _t(std, "cpu")  # [d] scale formed on the host, one copy to the device
+        scale = torch.where(sd == 0, torch.zeros_like(sd), 1.0 / torch.where(sd == 0, torch.ones_like(sd), sd)).to(dev)
         with_mean, with_std = self.get(self.WITH_MEAN), self.get(self.WITH_STD)
         if isinstance(X, SparseColumn) and not with_mean:
             out = sparse_map_values(X, lambda v, i: v * scale[i]) if with_std else X
@@ -80,9 +80,11 @@ class StandardScaler(Estimator, StandardScalerParams):
         n = s["count"]
         if n == 0:
             raise RuntimeError("The training set is empty.")
-        mean = s["sum"] / n
+        # the [d] finalisation on the host (same IEEE fp64 ops): on the device each of these small
+        # elementwise ops loads its torch code object at first use (~70 ms each in a fresh process)
+        mean = s["sum"].cpu() / n
         if n > 1:
-            std = torch.sqrt((s["sumsq"] - n * mean * mean) / (n - 1))
+            std = torch.sqrt((s["sumsq"].cpu() - n * mean * mean) / (n - 1))
         else:
             std = torch.zeros_like(mean)
         m = StandardScalerModel().set_model_data(
@@ -116,11 +118,12 @@ class MinMaxScalerModel(ModelWithData, MinMaxScalerParams):
         mn, mx = self.model_data_rows()[0]
         X = dense_input(t, self.get(self.INPUT_COL))
         lo, hi = self.get(self.MIN), self.get(self.MAX)
-        mnv, mxv = _t(mn, X.device), _t(mx, X.device)
+        mnv, mxv = _t(mn, "cpu"), _t(mx, "cpu")  # [d] scale / offset formed on the host
         const = (mnv - mxv).abs() < 1.0e-5
         rng = torch.where(const, torch.ones_like(mnv), mxv - mnv)
         scale = torch.where(const, torch.zeros_like(mnv), (hi - lo) / rng)
         offset = torch.where(const, torch.full_like(mnv, (hi + lo) / 2), lo - mnv * scale)
+        scale, offset = scale.to(X.device), offset.to(X.device)
         return [t.with_column(self.get(self.OUTPUT_COL), fo.affine_cols(X, None, scale, offset))]
 
 
@@ -157,8 +160,8 @@ class MaxAbsScalerModel(ModelWithData, HasInputCol, HasOutputCol):
         (mx,) = self.model_data_rows()[0]
         X = vector_input(t, self.get(self.INPUT_COL))
         dev = X.values.device if isinstance(X, SparseColumn) else X.device
-        m = _t(mx, dev)
-        scale = torch.where(m != 0, 1.0 / torch.where(m != 0, m, torch.ones_like(m)), torch.ones_like(m))
+        m = _t(mx, "cpu")  # [d] scale formed on the host
+        scale = torch.where(m != 0, 1.0 / torch.where(m != 0, m, torch.ones_like(m)), torch.ones_like(m)).to(dev)
         if isinstance(X, SparseColumn):
             out = sparse_map_values(X, lambda v, i: v * scale[i])
         else:
@@ -180,8 +183,10 @@ class MaxAbsScaler(Estimator, HasInputCol, HasOutputCol):
                 mx = mx.scatter_reduce(0, X.indices.long(), X.values.to(torch.float64).abs(), "amax")
         else:
             st = fo.column_stats(X)
-            mx = torch.maximum(st["max"].abs(), st["min"].abs()) if X.shape[0] else torch.zeros(
-                X.shape[1], dtype=torch.float64, device=X.device)
+            # (the [d] max-abs on the host: a device torch.maximum / abs would load their code
+            # objects at first use, ~100 ms in a fresh process)
+            mx = torch.maximum(st["max"].cpu().abs(), st["min"].cpu().abs()) if X.shape[0] else torch.zeros(
+                X.shape[1], dtype=torch.float64)
         mx = comm.all_reduce(mx.clone(), "max")
         m = MaxAbsScalerModel().set_model_data(MaxAbsScalerModel.make_model_data_table([(dense_vec(mx),)]))
         rw_update(m, self)
@@ -237,8 +242,8 @@ class RobustScalerModel(ModelWithData, RobustScalerModelParams):
         X = dense_input(t, self.get(self.INPUT_COL))
         if X.shape[0] and X.shape[1] != med.size():
             raise ValueError("Number of features must be %d but got %d." % (med.size(), X.shape[1]))
-        r = _t(rng, X.device)
-        scale = torch.where(r == 0, torch.zeros_like(r), 1.0 / torch.where(r == 0, torch.ones_like(r), r))
+        r = _t(rng, "cpu")  # [d] scale formed on the host
+        scale = torch.where(r == 0, torch.zeros_like(r), 1.0 / torch.where(r == 0, torch.ones_like(r), r)).to(X.device)
         out = fo.affine_cols(X, _t(med, X.device) if self.get(self.WITH_CENTERING) else None,
                              scale if self.get(self.WITH_SCALING) else None)
         return [t.with_column(self.get(self.OUTPUT_COL), out)]
@@ -308,8 +313,9 @@ class VarianceThresholdSelector(Estimator, VarianceThresholdSelectorParams):
         n = s["count"]
         if n == 0:
             raise RuntimeError("The training set is empty.")
-        var = s["sumsq"] / n - (s["sum"] / n) * (s["sum"] / n)
-        idx = torch.nonzero(var > self.get(self.VARIANCE_THRESHOLD)).reshape(-1).cpu().tolist()
+        sm, sq = s["sum"].cpu(), s["sumsq"].cpu()  # [d] on the host (no first-use torch kernel loads)
+        var = sq / n - (sm / n) * (sm / n)
+        idx = torch.nonzero(var > self.get(self.VARIANCE_THRESHOLD)).reshape(-1).tolist()
         m = VarianceThresholdSelectorModel().set_model_data(
             VarianceThresholdSelectorModel.make_model_data_table([(int(s["sum"].shape[0]), idx)]))
         rw_update(m, self)

@@ -25,7 +25,7 @@ from ...common.param import (HasCategoricalCols, HasInputCol, HasInputCols, HasN
 from ...io import read_write as rw
 from ...io import serialization as ser
 from ...linalg.vectors import DenseVector, SparseVector, Vector
-from ...ops import hashing
+from ...ops import hashing, native
 from ...param.param import (BooleanParam, FloatParam, IntParam, ParamValidators, StringArrayParam, StringParam)
 from ...parallel import comm
 from ...parallel import datastream as ds
@@ -299,6 +299,42 @@ def _per_string_arrays(t: Table, col: str, fn, native_kind: str = "", batched=No
     return StringArrayColumn(off, vflat[voff[codes[rid]] + local] if total else vflat[:0], vocab)
 
 
+TF_ROWS_MAX_LEN = 32  # longest document the per-row device count takes (csrc/hash.hip fmlx_tf_rows)
+native.register_kernel_sigs({
+    "fmlx_tf_rows": [native.c_void_p, native.c_void_p, native.c_int, native.c_long, native.c_int, native.c_int,
+                     native.c_void_p, native.c_void_p, native.c_void_p, native.c_void_p, native.c_void_p, native.c_int,
+                     native.c_void_p],
+})
+
+
+def _tf_rows(off: torch.Tensor, idx: torch.Tensor, n: int, maxlen: int, binary: bool, nf: int):
+    """HashingTF's per-document bucket counts on the GPU with one thread per document (the
+    document's buckets sorted and counted in registers, csrc/hash.hip tf_rows_kernel) — instead of
+    a sort-unique over all (document, bucket) keys. None when not on the GPU or a document is
+    longer than ``maxlen`` (<= TF_ROWS_MAX_LEN): the caller takes the general path."""
+    if idx.device.type != "cuda" or n == 0 or maxlen > TF_ROWS_MAX_LEN or TF_ROWS_MAX_LEN <= 0:
+        return None
+    dev = idx.device
+    off = off.to(dev, torch.int64).contiguous()
+    if idx.dtype not in (torch.int32, torch.int64):
+        idx = idx.to(torch.int64)
+    idx = idx.contiguous()
+    key64, stream = int(idx.dtype == torch.int64), native.stream_ptr(dev)
+    indptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    native.call("fmlx_tf_rows", native.ptr(off), native.ptr(idx) if idx.numel() else None, key64, n, maxlen, 0,
+                native.ptr(indptr[1:]), native.ptr(flag), None, None, None, int(binary), stream)
+    if int(flag.item()):
+        return None
+    indptr[1:] = torch.cumsum(indptr[1:], 0)
+    nnz = int(indptr[-1])
+    oi = torch.empty(nnz, dtype=torch.int32, device=dev)
+    ov = torch.empty(nnz, dtype=torch.float64, device=dev)
+    native.call("fmlx_tf_rows", native.ptr(off), native.ptr(idx) if idx.numel() else None, key64, n, maxlen, 1,
+                None, None, native.ptr(indptr), native.ptr(oi), native.ptr(ov), int(binary), stream)
+    return SparseColumn(indptr, oi, ov, nf)
+
+
 def _count_csr(rows: torch.Tensor, idx: torch.Tensor, n: int, width: int):
     """Per-row term counts of (row, index) pairs as one sort-unique → (indptr, indices, counts)."""
     keys, cnt = torch.unique(rows * width + idx, return_counts=True)
@@ -487,6 +523,9 @@ class HashingTF(Transformer, HasInputCol, HasOutputCol, HasNumFeatures):
             # hash each distinct string once, then gather the buckets by code on the device
             vb = hashing.non_negative_mod(hashing.hash_strings(dc.vocab), nf).astype(np.int64)
             idx = torch.from_numpy(vb).to(dc.device)[dc.codes.long()]
+            got = _tf_rows(dc.offsets, idx, len(dc), TF_ROWS_MAX_LEN, binary, nf)
+            if got is not None:
+                return [t.with_column(self.get(self.OUTPUT_COL), got)]
             indptr, ind, cnt, _ = _count_csr(dc.row_ids(), idx, len(dc), nf)
             vals = torch.ones_like(cnt, dtype=torch.float64) if binary else cnt.to(torch.float64)
             return [t.with_column(self.get(self.OUTPUT_COL), SparseColumn(indptr, ind.to(torch.int32), vals, nf))]
@@ -507,8 +546,13 @@ class HashingTF(Transformer, HasInputCol, HasOutputCol, HasNumFeatures):
             h = hashing.hash_strings(flat) if all_str else np.array([hashing.hash_object(x) for x in flat],
                                                                     dtype=np.int32)
             idx = torch.from_numpy(hashing.non_negative_mod(h, nf).astype(np.int64)).to(dev)
-        # term counts per document as one sort-unique over (doc, bucket) keys -> CSR column
         n = len(lens)
+        if n and max(lens) <= TF_ROWS_MAX_LEN:
+            off = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)).to(dev)
+            got = _tf_rows(off, idx, n, max(lens), binary, nf)
+            if got is not None:
+                return [t.with_column(self.get(self.OUTPUT_COL), got)]
+        # term counts per document as one sort-unique over (doc, bucket) keys -> CSR column
         doc = torch.repeat_interleave(torch.arange(n, device=dev), torch.tensor(lens, dtype=torch.int64, device=dev))
         keys, cnt = torch.unique(doc * nf + idx, return_counts=True)
         rows = torch.div(keys, nf, rounding_mode="floor")
@@ -520,6 +564,13 @@ class HashingTF(Transformer, HasInputCol, HasOutputCol, HasNumFeatures):
 
 
 # ------------------------------------------------------------------------------------ FeatureHasher
+FH_ROWS_MAX_COLS = 16  # input columns the per-row device assembly takes (csrc/hash.hip fmlx_fh_rows)
+native.register_kernel_sigs({
+    "fmlx_fh_rows": [native.c_void_p, native.c_int, native.c_long, native.c_int, native.c_void_p, native.c_void_p,
+                     native.c_void_p, native.c_void_p, native.c_void_p],
+})
+
+
 @rw.register_stage
 class FeatureHasher(Transformer, HasInputCols, HasOutputCol, HasCategoricalCols, HasNumFeatures):
     JAVA_CLASS_NAME = "org.apache.flink.ml.feature.featurehasher.FeatureHasher"
@@ -548,6 +599,10 @@ class FeatureHasher(Transformer, HasInputCols, HasOutputCol, HasCategoricalCols,
             return np.mod(h, nf)
 
         n = t.num_rows
+        if (dev.type == "cuda" and n and 0 < len(ins) <= FH_ROWS_MAX_COLS
+                and all(isinstance(t.column(c), torch.Tensor) for c in ins)):
+            out = self._device_rows(t, ins, is_cat, bucket, nf, dev, n)
+            return [t.with_column(self.get(self.OUTPUT_COL), out)]
         rows_l, idx_l, val_l = [], [], []
         ar = torch.arange(n, device=dev)
         for c in [c for c in ins if not is_cat(c)]:
@@ -607,6 +662,45 @@ class FeatureHasher(Transformer, HasInputCols, HasOutputCol, HasCategoricalCols,
         indptr[1:] = torch.cumsum(torch.bincount(urows, minlength=n), 0)
         col_out = SparseColumn(indptr, (ukeys - urows * nf).to(torch.int32), sums, nf)
         return [t.with_column(self.get(self.OUTPUT_COL), col_out)]
+
+    @staticmethod
+    def _device_rows(t, ins, is_cat, bucket, nf, dev, n):
+        """Every input a tensor on the GPU: each row's (index, value) pairs — numeric columns
+        (constant index, the value), categorical ones (the murmur3 of "col=value", 1.0) — go to
+        one kernel (csrc/hash.hip fh_rows_kernel) that sorts and merges them per row in registers,
+        instead of a sort-unique + index_add over all n·W pairs."""
+        keep, desc = [], []
+        for c in [c for c in ins if not is_cat(c)]:
+            x = t.column(c).to(dev, torch.float64).contiguous()
+            keep.append(x)
+            desc.append((0, x.data_ptr(), 2, int(bucket([c])[0])))
+        for c in [c for c in ins if is_cat(c)]:
+            col = t.column(c)
+            if col.dtype.is_floating_point:
+                # Double.toString + murmur3 of every value on the device (csrc/javastr.hip)
+                h = hashing.hash_prefixed_doubles_device(c + "=", col.detach().to(dev))
+                keep.append(h)
+                desc.append((h.data_ptr(), 0, 1, nf))
+            else:
+                u, inv = torch.unique(col, return_inverse=True)
+                names = (["true" if v else "false" for v in u.tolist()] if col.dtype == torch.bool
+                         else [str(int(v)) for v in u.tolist()])
+                lut = torch.from_numpy(bucket(c + "=" + x for x in names)).to(dev)
+                ix = lut[inv.to(dev)].contiguous()
+                keep.append(ix)
+                desc.append((ix.data_ptr(), 0, 3, 0))
+        d = torch.tensor(desc, dtype=torch.int64).to(dev)
+        W, stream = len(desc), native.stream_ptr(dev)
+        indptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        native.call("fmlx_fh_rows", native.ptr(d), W, n, 0, native.ptr(indptr[1:]), None, None, None, stream)
+        indptr[1:] = torch.cumsum(indptr[1:], 0)
+        nnz = int(indptr[-1])
+        oi = torch.empty(nnz, dtype=torch.int32, device=dev)
+        ov = torch.empty(nnz, dtype=torch.float64, device=dev)
+        native.call("fmlx_fh_rows", native.ptr(d), W, n, 1, None, native.ptr(indptr), native.ptr(oi), native.ptr(ov),
+                    stream)
+        del keep
+        return SparseColumn(indptr, oi, ov, nf)
 
 
 # ------------------------------------------------------------------------------------ CountVectorizer
@@ -827,10 +921,11 @@ class IDF(Estimator, IDFModelParams):
         n = int(comm.all_reduce_scalar(float(n), "sum"))
         if n == 0:
             raise RuntimeError("The training set is empty.")
+        df = df.cpu()  # the [d] finalisation on the host (no first-use torch kernel loads on the GPU)
         keep = df >= self.get(self.MIN_DOC_FREQ)
         idf = torch.where(keep, torch.log((n + 1) / (df + 1)), torch.zeros_like(df))
         dfl = torch.where(keep, df, torch.zeros_like(df)).to(torch.int64)
         m = IDFModel().set_model_data(IDFModel.make_model_data_table(
-            [(DenseVector(idf.cpu().numpy()), dfl.cpu().tolist(), n)]))
+            [(DenseVector(idf.numpy()), dfl.tolist(), n)]))
         rw_update(m, self)
         return m

@@ -14,7 +14,7 @@ from typing import List
 import numpy as np
 import torch
 
-from ...ops import blas
+from ...ops import blas, native
 
 from ...api.stage import Transformer
 from ...common.param import HasHandleInvalid, HasInputCol, HasInputCols, HasOutputCol, HasOutputCols
@@ -67,6 +67,25 @@ class Binarizer(Transformer, HasInputCols, HasOutputCols):
 
 
 # ------------------------------------------------------------------------------------ Bucketizer
+native.register_kernel_sigs({"fmlx_bucketize": [native.c_void_p, native.c_long, native.c_void_p, native.c_int,
+                                                 native.c_int, native.c_void_p, native.c_void_p, native.c_void_p,
+                                                 native.c_void_p]})
+
+
+def _bucketize_device(x: torch.Tensor, s: torch.Tensor, keep: bool, want_mask: bool):
+    """(bucket index f64, invalid mask u8 or None when every value is valid) of a device column in
+    one kernel pass (csrc/colstats.hip bucketize_kernel)."""
+    x = x.contiguous()
+    n, dev = x.shape[0], x.device
+    out = torch.empty(n, dtype=torch.float64, device=dev)
+    inv = torch.empty(n, dtype=torch.uint8, device=dev) if want_mask else None
+    ninv = torch.zeros(1, dtype=torch.int32, device=dev)
+    if n:
+        native.call("fmlx_bucketize", native.ptr(x), n, native.ptr(s), len(s), int(keep), native.ptr(out),
+                    native.ptr(inv) if inv is not None else None, native.ptr(ninv), native.stream_ptr(dev))
+    return out, (inv if inv is not None else True) if int(ninv.item()) else None
+
+
 @rw.register_stage
 class Bucketizer(Transformer, HasInputCols, HasOutputCols, HasHandleInvalid):
     JAVA_CLASS_NAME = "org.apache.flink.ml.feature.bucketizer.Bucketizer"
@@ -84,6 +103,17 @@ class Bucketizer(Transformer, HasInputCols, HasOutputCols, HasHandleInvalid):
             dev = col.device if isinstance(col, torch.Tensor) else torch.device("cpu")
             x = t.scalars(c, dtype=torch.float64, device=dev)
             s = torch.tensor(sp, dtype=torch.float64, device=dev)
+            if dev.type == "cuda" and len(s):
+                idx, invalid = _bucketize_device(x, s, hi == self.KEEP_INVALID, hi == self.SKIP_INVALID)
+                if invalid is not None:  # (some invalid value)
+                    if hi == self.ERROR_INVALID:
+                        raise RuntimeError(
+                            "The input contains invalid value. See handleInvalid parameter for more options.")
+                    if hi == self.SKIP_INVALID:
+                        inv_cpu = invalid.cpu().to(torch.bool)
+                        keep_rows = ~inv_cpu if keep_rows is None else keep_rows & ~inv_cpu
+                res[o] = idx
+                continue
             pos = torch.searchsorted(s, x, right=False)  # first index with s[idx] >= x
             exact = (pos < len(s)) & (s[torch.clamp(pos, max=len(s) - 1)] == x)
             idx = torch.where(exact, torch.where(pos == len(s) - 1, pos - 1, pos), pos - 1).to(torch.float64)

@@ -212,6 +212,18 @@ def _label_value_counts_device(X: torch.Tensor, li: torch.Tensor, L: int, dist: 
     return counts.astype(np.float64), vals, slots, n_lab.cpu().numpy()
 
 
+def _labels_integral(y: torch.Tensor) -> bool:
+    """No label with a fractional part (NaN counts as one, ±inf does not: y != round(y)). On the
+    GPU one library reduction answers it for finite labels (torch's compare / round / any kernels
+    load their code objects lazily: ~16 ms inside the first fit of a process)."""
+    if y.is_cuda:
+        from ..ops import catstats
+
+        if not catstats.flags(y)[2]:
+            return True
+    return not bool((y != torch.round(y)).any())
+
+
 @rw.register_stage
 class NaiveBayes(Estimator, NaiveBayesParams):
     JAVA_CLASS_NAME = "org.apache.flink.ml.classification.naivebayes.NaiveBayes"
@@ -226,7 +238,7 @@ class NaiveBayes(Estimator, NaiveBayesParams):
             raise ValueError("Feature vectors should be of equal length.")
         # on the GPU the stored dtype stays (the contingency kernels read f32 or f64 themselves)
         X, y = features_and_labels(t, self.get(self.FEATURES_COL), self.get(self.LABEL_COL), keep_dtype=True)
-        if bool((y != torch.round(y)).any()):
+        if not _labels_integral(y):
             raise ValueError("Label value should be indexed number.")
         s = self.get(self.SMOOTHING)
         dist = get_world_distributed()

@@ -133,4 +133,60 @@ FMLX_API int fmlx_affine_cols(int dtype, int out_dtype, const void* X, long ld, 
   return -1;
 }
 
+// ---- Bucketizer (Bucketizer.java:118-143 with Bucketizer's binarySearch semantics): one pass
+// per column instead of searchsorted + ~10 elementwise torch passes. For split points s[0..m):
+// pos = the first index with s[pos] >= x; an exact hit maps to pos (the last split to m − 2),
+// anything else to pos − 1; NaN and values outside [s[0], s[m−1]] are invalid — counted in
+// *ninv, flagged in inv[] (when given) and, with keep_invalid, mapped to bucket m − 1. The splits
+// stay in LDS (m <= BKZ_LDS) or are read from global memory.
+namespace {
+constexpr int BKZ_LDS = 4096;
+__global__ __launch_bounds__(256) void bucketize_kernel(const double* __restrict__ x, long n,
+                                                        const double* __restrict__ sp, int m, int keep_invalid,
+                                                        double* __restrict__ out, unsigned char* __restrict__ inv,
+                                                        int* __restrict__ ninv) {
+  __shared__ double ls[BKZ_LDS];
+  const bool in_lds = m <= BKZ_LDS;
+  if (in_lds)
+    for (int i = threadIdx.x; i < m; i += blockDim.x) ls[i] = sp[i];
+  __syncthreads();
+  const double* s = in_lds ? ls : sp;
+  int bad = 0;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const double v = x[i];
+    int lo = 0, hi = m;  // lower bound: first s[pos] >= v (NaN: no s[mid] < v holds -> 0; flagged below)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (s[mid] < v)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    const int pos = lo;
+    const bool exact = pos < m && s[pos] == v;
+    const bool invalid = v != v || (!exact && (pos == 0 || pos == m));
+    double b = exact ? (double)(pos == m - 1 ? pos - 1 : pos) : (double)(pos - 1);
+    if (invalid && keep_invalid) b = (double)(m - 1);
+    out[i] = b;
+    if (inv) inv[i] = invalid ? 1 : 0;
+    bad += invalid ? 1 : 0;
+  }
+  // per-wave sum, one vector atomic per wave with invalid values
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) bad += __shfl_xor(bad, o, 64);
+  if ((threadIdx.x & 63) == 0 && bad) atomicAdd(ninv, bad);
+}
+}  // namespace
+
+FMLX_API int fmlx_bucketize(const double* x, long n, const double* splits, int m, int keep_invalid, double* out,
+                            unsigned char* inv, int* ninv, void* stream) {
+  if (n <= 0) return 0;
+  if (x == nullptr || splits == nullptr || m < 1 || out == nullptr || ninv == nullptr) return -1;
+  const long want = (n + 255) / 256;
+  const int blocks = (int)(want < 8192 ? want : 8192);
+  hipLaunchKernelGGL(bucketize_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, n, splits, m, keep_invalid,
+                     out, inv, ninv);
+  return (int)hipGetLastError();
+}
+
 FMLX_DEFINE_PRELOAD()

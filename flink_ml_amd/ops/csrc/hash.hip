@@ -44,7 +44,202 @@ __global__ __launch_bounds__(256) void murmur3_chars_kernel(const uint16_t* __re
     }
   }
 }
+
+// ---- FeatureHasher row assembly: W (index, value) pairs per row -> the row's sparse vector
+// (reference FeatureHasher.HashFunction.map, FeatureHasher.java:118-141 + updateMap :184-194: a
+// TreeMap<Integer, Double> that stores the first value of an index as it is and adds the later
+// ones in column order). One thread per row: the W pairs are sorted by index in registers with an
+// odd-even transposition network (adjacent swaps on strictly greater keys: stable, so equal
+// indices keep their column order) and merged by a left-to-right sum. Phase 0 writes the row's
+// distinct count to cnt[r]; phase 1 (after the host's scan into indptr) writes the entries.
+// Group g of desc[W][4] = {index ptr, value ptr (0: 1.0), mode, const}; mode 0 = int32 final
+// indices, 1 = raw int32 Java hashes (floorMod(Math.abs(h), const)), 2 = the constant index
+// `const`, 3 = int64 final indices.
+template <int WP>
+__global__ __launch_bounds__(256) void fh_rows_kernel(const long long* __restrict__ desc, int W, long n, int phase,
+                                                      long long* __restrict__ cnt, const long long* __restrict__ indptr,
+                                                      int* __restrict__ oi, double* __restrict__ ov) {
+  constexpr int PAD = 0x7fffffff;
+  for (long r = (long)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (long)gridDim.x * blockDim.x) {
+    int key[WP];
+    double val[WP];
+#pragma unroll
+    for (int g = 0; g < WP; ++g) {
+      key[g] = PAD;
+      val[g] = 0.0;
+      if (g < W) {
+        const long long* d = desc + 4 * g;
+        const int mode = (int)d[2];
+        if (mode == 2) {
+          key[g] = (int)d[3];
+        } else if (mode == 3) {
+          key[g] = (int)reinterpret_cast<const long long*>(d[0])[r];
+        } else {
+          const int h = reinterpret_cast<const int*>(d[0])[r];
+          if (mode == 1) {
+            const int m = (int)d[3];
+            const int a = h == (int)0x80000000 ? h : (h < 0 ? -h : h);  // Math.abs(Integer.MIN_VALUE) < 0
+            const int q = a % m;
+            key[g] = q < 0 ? q + m : q;
+          } else {
+            key[g] = h;
+          }
+        }
+        val[g] = d[1] ? reinterpret_cast<const double*>(d[1])[r] : 1.0;
+      }
+    }
+#pragma unroll
+    for (int pass = 0; pass < WP; ++pass) {
+#pragma unroll
+      for (int i = pass & 1; i + 1 < WP; i += 2) {
+        if (key[i] > key[i + 1]) {
+          const int tk = key[i];
+          key[i] = key[i + 1];
+          key[i + 1] = tk;
+          const double tv = val[i];
+          val[i] = val[i + 1];
+          val[i + 1] = tv;
+        }
+      }
+    }
+    if (phase == 0) {
+      long long c = 0;
+#pragma unroll
+      for (int i = 0; i < WP; ++i) c += (i < W && (i == 0 || key[i] != key[i - 1])) ? 1 : 0;
+      cnt[r] = c;
+    } else {
+      long long p = indptr[r];
+      int prev = key[0];
+      double acc = val[0];
+#pragma unroll
+      for (int i = 1; i < WP; ++i) {
+        if (i < W) {
+          if (key[i] != prev) {
+            oi[p] = prev;
+            ov[p] = acc;
+            ++p;
+            prev = key[i];
+            acc = val[i];
+          } else {
+            acc += val[i];
+          }
+        }
+      }
+      oi[p] = prev;
+      ov[p] = acc;
+    }
+  }
+}
+
+// ---- HashingTF per-document term counts: CSR rows of bucket indices (int64 or int32) -> each
+// row's ascending distinct indices with their counts (HashingTF.java:101-125's per-row map).
+// One thread per row, the row sorted in registers as above; a row longer than WP raises *flag
+// (phase 0) and the host takes the general path.
+template <int WP>
+__global__ __launch_bounds__(256) void tf_rows_kernel(const long long* __restrict__ off, const void* __restrict__ keys,
+                                                      int key64, long n, int phase, long long* __restrict__ cnt,
+                                                      int* __restrict__ flag, const long long* __restrict__ indptr,
+                                                      int* __restrict__ oi, double* __restrict__ ov, int binary) {
+  constexpr int PAD = 0x7fffffff;
+  for (long r = (long)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (long)gridDim.x * blockDim.x) {
+    const long long b = off[r];
+    const int L = (int)(off[r + 1] - b);
+    if (L > WP) {
+      if (phase == 0) {
+        *flag = 1;
+        cnt[r] = 0;
+      }
+      continue;
+    }
+    int key[WP];
+#pragma unroll
+    for (int i = 0; i < WP; ++i)
+      key[i] = i < L ? (key64 ? (int)reinterpret_cast<const long long*>(keys)[b + i]
+                               : reinterpret_cast<const int*>(keys)[b + i])
+                     : PAD;
+#pragma unroll
+    for (int pass = 0; pass < WP; ++pass) {
+#pragma unroll
+      for (int i = pass & 1; i + 1 < WP; i += 2) {
+        const int lo = min(key[i], key[i + 1]), hi = max(key[i], key[i + 1]);
+        key[i] = lo;
+        key[i + 1] = hi;
+      }
+    }
+    if (phase == 0) {
+      long long c = 0;
+#pragma unroll
+      for (int i = 0; i < WP; ++i) c += (i < L && (i == 0 || key[i] != key[i - 1])) ? 1 : 0;
+      cnt[r] = c;
+    } else if (L > 0) {
+      long long p = indptr[r];
+      int prev = key[0];
+      double c = 1.0;
+#pragma unroll
+      for (int i = 1; i < WP; ++i) {
+        if (i < L) {
+          if (key[i] != prev) {
+            oi[p] = prev;
+            ov[p] = binary ? 1.0 : c;
+            ++p;
+            prev = key[i];
+            c = 1.0;
+          } else {
+            c += 1.0;
+          }
+        }
+      }
+      oi[p] = prev;
+      ov[p] = binary ? 1.0 : c;
+    }
+  }
+}
 }  // namespace
+
+// off: int64 [n+1] row offsets; keys int64 (key64) or int32 bucket indices in [0, 2^31 − 1).
+// Phase 0: cnt[n] = distinct per row, *flag = 1 if a row exceeds 32 entries; phase 1: entries.
+FMLX_API int fmlx_tf_rows(const long long* off, const void* keys, int key64, long n, int maxlen, int phase,
+                          long long* cnt, int* flag, const long long* indptr, int* oi, double* ov, int binary,
+                          void* stream) {
+  if (n <= 0) return 0;
+  if (off == nullptr || (phase == 0 && (cnt == nullptr || flag == nullptr)) ||
+      (phase != 0 && (indptr == nullptr || oi == nullptr || ov == nullptr)))
+    return -1;
+  long want = (n + 255) / 256;
+  const int blocks = (int)(want < 16384 ? want : 16384);
+  hipStream_t s = (hipStream_t)stream;
+  if (maxlen <= 8)
+    hipLaunchKernelGGL(tf_rows_kernel<8>, dim3(blocks), dim3(256), 0, s, off, keys, key64, n, phase, cnt, flag, indptr,
+                       oi, ov, binary);
+  else if (maxlen <= 16)
+    hipLaunchKernelGGL(tf_rows_kernel<16>, dim3(blocks), dim3(256), 0, s, off, keys, key64, n, phase, cnt, flag,
+                       indptr, oi, ov, binary);
+  else
+    hipLaunchKernelGGL(tf_rows_kernel<32>, dim3(blocks), dim3(256), 0, s, off, keys, key64, n, phase, cnt, flag,
+                       indptr, oi, ov, binary);
+  return (int)hipGetLastError();
+}
+
+FMLX_API int fmlx_fh_rows_wmax() { return 16; }
+
+// desc: device int64 [W][4] (see fh_rows_kernel); phase 0 -> cnt[n], phase 1 -> oi / ov at indptr
+FMLX_API int fmlx_fh_rows(const long long* desc, int W, long n, int phase, long long* cnt, const long long* indptr,
+                          int* oi, double* ov, void* stream) {
+  if (n <= 0) return 0;
+  if (W < 1 || W > 16 || desc == nullptr || (phase == 0 && cnt == nullptr) ||
+      (phase != 0 && (indptr == nullptr || oi == nullptr || ov == nullptr)))
+    return -1;
+  long want = (n + 255) / 256;
+  const int blocks = (int)(want < 16384 ? want : 16384);
+  hipStream_t s = (hipStream_t)stream;
+  if (W <= 4)
+    hipLaunchKernelGGL(fh_rows_kernel<4>, dim3(blocks), dim3(256), 0, s, desc, W, n, phase, cnt, indptr, oi, ov);
+  else if (W <= 8)
+    hipLaunchKernelGGL(fh_rows_kernel<8>, dim3(blocks), dim3(256), 0, s, desc, W, n, phase, cnt, indptr, oi, ov);
+  else
+    hipLaunchKernelGGL(fh_rows_kernel<16>, dim3(blocks), dim3(256), 0, s, desc, W, n, phase, cnt, indptr, oi, ov);
+  return (int)hipGetLastError();
+}
 
 FMLX_API int fmlx_murmur3_chars_device(const void* units, const long* offsets, long n, int mod, int mode,
                                        int* hash_out, int* index_out, void* stream) {

@@ -102,14 +102,19 @@ class CentroidBuffers:
         self._pack = None
 
     def set(self, centroids: torch.Tensor) -> None:
-        c = centroids.to(device=self.cent.device, dtype=self.cent.dtype)
+        # the k x D representations are formed on the host and copied over once (a fit's initial
+        # centroids come from the host anyway): on the device the norm / pow / scatter ops would
+        # each load their torch code object at first use, ~10-40 ms apiece in a fresh process
+        c = torch.as_tensor(centroids).detach().to(device="cpu", dtype=self.cent.dtype)
+        cb = c.to(torch.bfloat16)
+        Cb = torch.zeros((self.kpad, self.DP), dtype=torch.bfloat16)
+        Cb[: self.k, : self.D] = -2 * cb  # the MFMA assign consumes −2·c (exact in bf16)
+        nb = torch.full((self.kpad,), float("inf"), dtype=torch.float32)
+        nb[: self.k] = (cb.float() * cb.float()).sum(1)
         self.cent.copy_(c)
         self.cnorm.copy_(torch.linalg.vector_norm(c.to(torch.float64), dim=1).to(self.cent.dtype))
-        cb = c.to(torch.bfloat16)
-        self.Cb.zero_()
-        self.Cb[: self.k, : self.D] = -2 * cb  # the MFMA assign consumes −2·c (exact in bf16)
-        self.cnorm_b.fill_(float("inf"))
-        self.cnorm_b[: self.k] = (cb.float() ** 2).sum(1)
+        self.Cb.copy_(Cb)
+        self.cnorm_b.copy_(nb)
         self._pack = None
 
     def fp32_pack(self):

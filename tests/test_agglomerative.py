@@ -113,3 +113,36 @@ def test_distributed_window_all():
     for f, p in rows:
         g.setdefault(p, set()).add(f)
     assert sorted(map(frozenset, g.values()), key=sorted) == _exp([(1, 1), (1, 0), (4, 1.5), (4, 0)], [(1, 4), (4, 4)])
+
+
+@pytest.mark.gpu
+def test_pairwise_euclid_kernel_matches_torch():
+    """csrc/blas.hip pairwise_euclid_f64_kernel against the fp64 torch formula: symmetric, zero
+    diagonal, tile edges (n not a multiple of 16, d not a multiple of 16)."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from flink_ml_amd.models.agglomerative import pairwise_distances
+
+    g = torch.Generator().manual_seed(4)
+    for n, d in ((1, 3), (17, 5), (1000, 100), (333, 37)):
+        X = torch.randn(n, d, generator=g, dtype=torch.float64)
+        D = pairwise_distances(X.cuda(), "euclidean").cpu()
+        sq = (X * X).sum(1)
+        ref = torch.sqrt(torch.clamp(sq[:, None] + sq[None, :] - 2.0 * X @ X.t(), min=0.0))
+        # off the diagonal (the torch formula's diagonal is sqrt of a rounding residue, up to ~1e-6;
+        # the kernel's is exactly 0, checked below)
+        off = ~torch.eye(n, dtype=torch.bool)
+        torch.testing.assert_close(D[off], ref[off], rtol=1e-12, atol=1e-9)
+        assert torch.equal(D, D.t()) and bool((torch.diagonal(D) == 0).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", [k for k in MERGE if k[1] == "euclidean"])
+def test_merge_info_gpu(key):
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    link, metric = key
+    t = Table({"features": torch.tensor(PTS, dtype=torch.float64).cuda()}, num_rows=len(PTS))
+    mi = AgglomerativeClustering().set_linkage(link).set_distance_measure(metric).set_compute_full_tree(True) \
+        .transform(t)[1]
+    np.testing.assert_allclose(mi.get_list("distance"), MERGE[key], atol=1e-7)

@@ -83,6 +83,33 @@ def test_hashing_tf_device():
     assert out[0] == Vectors.sparse(262144, [67564, 89917, 113827, 131486, 228971], [1.0] * 5)
 
 
+@pytest.mark.parametrize("binary", [False, True])
+def test_hashing_tf_rows_kernel_matches_general_path(binary):
+    """The per-document device count (csrc/hash.hip tf_rows_kernel) against the general
+    sort-unique path: repeated terms, empty documents, colliding buckets (small numFeatures),
+    and a document longer than TF_ROWS_MAX_LEN (the whole column falls back)."""
+    from flink_ml_amd.models import HashingTF
+    from flink_ml_amd.models.feature import text
+
+    rng = np.random.default_rng(5)
+    vocab = ["w%d" % i for i in range(40)] + ["ünï", ""]
+    docs = [[vocab[j] for j in rng.integers(0, len(vocab), rng.integers(0, 20))] for _ in range(3000)]
+    for extra in ([], [["w1"] * 40]):
+        t = Table.from_rows([(d,) for d in docs + extra], ["input"])
+        for nf in (7, 262144):
+            tf = HashingTF().set_num_features(nf).set_binary(binary)
+            got = tf.transform(t)[0].column("output")
+            saved = text.TF_ROWS_MAX_LEN
+            text.TF_ROWS_MAX_LEN = 0
+            try:
+                ref = tf.transform(t)[0].column("output")
+            finally:
+                text.TF_ROWS_MAX_LEN = saved
+            assert torch.equal(got.indptr.cpu(), ref.indptr.cpu())
+            assert torch.equal(got.indices.cpu().long(), ref.indices.cpu().long())
+            assert torch.equal(got.values.cpu(), ref.values.cpu())
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.bfloat16])
 @pytest.mark.parametrize("shape,G", [((100000, 100), 10), ((3000, 300), 1), ((777, 5), 32)])
 def test_group_colstats_kernel(dtype, shape, G):
@@ -137,3 +164,37 @@ def test_radix_hist_kernel_multi_quantile(dtype, d):
     dev = column_quantiles(X.cuda(), ps, 0.001).cpu()
     host = column_quantiles(X, ps, 0.001)
     assert torch.equal(dev, host)
+
+
+@pytest.mark.parametrize("handle", ["keep", "skip", "error"])
+def test_bucketizer_kernel_matches_cpu(handle):
+    """csrc/colstats.hip bucketize_kernel against the CPU searchsorted path: exact hits on every
+    split (the last one maps to the last bucket), NaN and out-of-range values, infinite splits,
+    and a split array too long for the LDS copy."""
+    from flink_ml_amd.models import Bucketizer
+
+    rng = np.random.default_rng(2)
+    long_sp = np.sort(rng.normal(size=5000)).tolist()
+    sp = [[-0.5, 0.0, 0.5, 1.0], [float("-inf"), -1.0, 1.0, float("inf")], long_sp]
+    cols = {}
+    for i, s in enumerate(sp):
+        v = rng.normal(size=20000)
+        fin = [x for x in s if np.isfinite(x)]
+        v[:len(fin)] = fin
+        if handle == "error":  # every value inside the splits' range
+            v = np.clip(v, s[0], s[-1])
+        else:
+            v[-7:] = [np.nan, -5.0, 5.0, -0.0, np.inf, -np.inf, 0.25]
+        cols["c%d" % i] = v
+    bz = Bucketizer().set_input_cols(*cols).set_output_cols(*["o%d" % i for i in range(3)]) \
+        .set_splits_array(sp).set_handle_invalid(handle)
+    ref = bz.transform(Table({k: torch.from_numpy(v) for k, v in cols.items()}, num_rows=20000))[0]
+    got = bz.transform(Table({k: torch.from_numpy(v).cuda() for k, v in cols.items()}, num_rows=20000))[0]
+    assert got.num_rows == ref.num_rows
+    for i in range(3):
+        assert got.column("o%d" % i).is_cuda
+        assert torch.equal(got.column("o%d" % i).cpu(), ref.column("o%d" % i).cpu())
+    if handle == "error":
+        bad = Table({"c0": torch.tensor([0.1, float("nan")], dtype=torch.float64).cuda()}, num_rows=2)
+        with pytest.raises(RuntimeError, match="invalid value"):
+            Bucketizer().set_input_cols("c0").set_output_cols("o").set_splits_array([sp[0]]).transform(bad)

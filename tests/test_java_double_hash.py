@@ -146,3 +146,67 @@ def test_feature_hasher_device_categorical_matches_host():
     gpu = fh.transform(Table({"a": torch.from_numpy(x).cuda(), "b": torch.from_numpy(y).cuda()}))[0].column("o")
     cpu = fh.transform(Table({"a": torch.from_numpy(x), "b": torch.from_numpy(y)}))[0].column("o")
     assert torch.equal(gpu.indices.cpu(), cpu.indices.cpu()) and torch.equal(gpu.indptr.cpu(), cpu.indptr.cpu())
+
+
+def _treemap_rows(cols, cats, nf):
+    """The reference's per-row TreeMap (FeatureHasher.java:118-141, updateMap :184-194) in Python:
+    numeric columns first, then categorical, the first value of an index stored as is."""
+
+    def idx(h):
+        h = int(h)
+        a = h if h == -(1 << 31) else abs(h)
+        return a % nf
+
+    names = list(cols)
+    num = [c for c in names if c not in cats]
+    n = len(cols[names[0]])
+    hnum = {c: idx(hashing.hash_strings([c])[0]) for c in num}
+    hcat = {c: hashing.hash_prefixed_doubles(c + "=", np.asarray(cols[c], dtype=np.float64)) for c in cats}
+    rows = []
+    for r in range(n):
+        m = {}
+        for c in num:
+            k = hnum[c]
+            m[k] = m[k] + float(cols[c][r]) if k in m else float(cols[c][r])
+        for c in cats:
+            k = idx(hcat[c][r])
+            m[k] = m[k] + 1.0 if k in m else 1.0
+        rows.append(sorted(m.items()))
+    return rows
+
+
+@pytest.mark.gpu
+def test_feature_hasher_device_rows_match_treemap():
+    """The per-row device assembly (csrc/hash.hip fh_rows_kernel) against the reference TreeMap
+    semantics, exactly — a small numFeatures forces collisions between numeric and categorical
+    features, -0.0 must survive as a first value — and against the general sort-unique path."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from flink_ml_amd import Table
+    from flink_ml_amd.models import FeatureHasher
+    from flink_ml_amd.models.feature import text
+
+    rng = np.random.default_rng(11)
+    n = 3000
+    cols = {"f0": rng.normal(size=n), "f1": rng.integers(0, 5, n).astype(np.float64), "f2": rng.normal(size=n),
+            "f3": rng.integers(0, 9, n).astype(np.float64), "f4": rng.normal(size=n)}
+    cols["f0"][:50] = -0.0
+    cats = ["f1", "f3"]
+    for nf in (3, 7, 1000):
+        fh = FeatureHasher().set_input_cols(*cols).set_categorical_cols(*cats).set_output_col("o").set_num_features(nf)
+        tab = Table({c: torch.from_numpy(v).cuda() for c, v in cols.items()})
+        got = fh.transform(tab)[0].column("o")
+        ip, ix, vv = got.indptr.cpu().numpy(), got.indices.cpu().numpy(), got.values.cpu().numpy()
+        want = _treemap_rows(cols, cats, nf)
+        for r in range(n):
+            row = list(zip(ix[ip[r]:ip[r + 1]].tolist(), vv[ip[r]:ip[r + 1]].tolist()))
+            assert [k for k, _ in row] == [k for k, _ in want[r]], (nf, r)
+            assert all(struct.pack("<d", a) == struct.pack("<d", b) for (_, a), (_, b) in zip(row, want[r])), (nf, r)
+        saved = text.FH_ROWS_MAX_COLS
+        text.FH_ROWS_MAX_COLS = 0  # the general path on the same device tensors
+        try:
+            gen = fh.transform(tab)[0].column("o")
+        finally:
+            text.FH_ROWS_MAX_COLS = saved
+        assert torch.equal(gen.indptr.cpu(), got.indptr.cpu()) and torch.equal(gen.indices.cpu(), got.indices.cpu())
+        torch.testing.assert_close(gen.values.cpu(), got.values.cpu(), rtol=1e-12, atol=1e-12)
