@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--pattern", default=None)
     ap.add_argument("--max-values", type=int, default=1_000_000)
     ap.add_argument("--min-ms", type=float, default=10.0)
+    ap.add_argument("--warm", action="store_true", help="run each config once first (warm op profile)")
     a = ap.parse_args()
     from flink_ml_amd.bench import runner
 
@@ -59,6 +60,8 @@ def main():
         if name == "version" or (rx and not rx.match(name)):
             continue
         spec = runner._cap_values(spec, a.max_values)
+        if a.warm:
+            runner.run_benchmark(name, spec)
         m = OpTimer(a.min_ms)
         t0 = time.perf_counter()
         try:
