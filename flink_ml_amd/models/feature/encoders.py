@@ -32,6 +32,7 @@ from ...io import read_write as rw
 from ...io import serialization as ser
 from ...linalg.vectors import DenseVector, SparseVector, Vector
 from ...ops import features as fo
+from ...ops import native
 from ...param.param import BooleanParam, FloatParam, IntParam, ParamValidators, StringParam
 from ...parallel import comm
 from ...parallel import datastream as ds
@@ -786,6 +787,21 @@ def _is_missing(x: torch.Tensor, missing: float) -> torch.Tensor:
     return torch.isnan(x) if math.isnan(missing) else (x == missing)
 
 
+native.register_kernel_sigs({"fmlx_masked_sum_f64": [native.c_void_p, native.c_long, native.c_double, native.c_int,
+                                                      native.c_void_p, native.c_void_p, native.c_void_p]})
+
+
+def _valid_sum_count(x: torch.Tensor, missing: float):
+    """[sum, count] of a device column's entries that are neither NaN nor ``missing`` — one pass
+    of csrc/colstats.hip masked_sum_kernel (no filtered copy of the column)."""
+    x = x.contiguous()
+    buf = torch.empty(2 * 1024 + 2, dtype=torch.float64, device=x.device)
+    native.call("fmlx_masked_sum_f64", native.ptr(x) if x.numel() else None, x.numel(), float(missing),
+                int(math.isnan(missing)), native.ptr(buf), native.ptr(buf[2048:]), native.stream_ptr(x.device))
+    s, c = buf[2048:].cpu().tolist()
+    return [s, c]
+
+
 @rw.register_stage
 class ImputerModel(ModelWithData, ImputerModelParams):
     """``ImputerModel.java``: null / missingValue entries -> per-column surrogate (output double).
@@ -835,10 +851,14 @@ class Imputer(Estimator, ImputerParams):
         xs = []
         for c in cols:
             x = _numeric_col(t, c).to(torch.float64)
+            if strategy == self.MEAN and x.is_cuda:
+                xs.append(x)  # (masked in the sum kernel below)
+                continue
             xs.append(x[~(torch.isnan(x) | _is_missing(x, missing))])
         sur: Dict[str, float] = {}
         if strategy == self.MEAN:
-            st = torch.tensor([[float(x.sum()), float(x.numel())] for x in xs], dtype=torch.float64)
+            st = torch.tensor([_valid_sum_count(x, missing) if x.is_cuda else [float(x.sum()), float(x.numel())]
+                               for x in xs], dtype=torch.float64)
             if dist:
                 st = comm.all_reduce_sum(st)
             if st[0, 1] <= 0:

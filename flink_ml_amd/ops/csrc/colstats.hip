@@ -189,4 +189,75 @@ FMLX_API int fmlx_bucketize(const double* x, long n, const double* splits, int m
   return (int)hipGetLastError();
 }
 
+// ---- Imputer mean strategy (Imputer.java:140-170): sum and count of the values that are neither
+// NaN nor missingValue, without materialising the filtered column. Block partials in a fixed
+// order, then one block folds them in block order: deterministic run to run.
+namespace {
+constexpr int MSUM_BLOCKS = 1024;
+__device__ __forceinline__ void block_sum2(double& a, double& b, double* sh) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[w] = a;
+    sh[nw + w] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    a = 0.0;
+    b = 0.0;
+    for (int i = 0; i < nw; ++i) {
+      a += sh[i];
+      b += sh[nw + i];
+    }
+  }
+}
+__global__ __launch_bounds__(256) void masked_sum_kernel(const double* __restrict__ x, long n, double missing,
+                                                         int miss_nan, double* __restrict__ part) {
+  __shared__ double sh[8];
+  double s = 0.0, c = 0.0;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const double v = x[i];
+    const bool skip = v != v || (!miss_nan && v == missing);
+    s += skip ? 0.0 : v;
+    c += skip ? 0.0 : 1.0;
+  }
+  block_sum2(s, c, sh);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = s;
+    part[2 * blockIdx.x + 1] = c;
+  }
+}
+__global__ __launch_bounds__(256) void fold_pairs_kernel(const double* __restrict__ part, int np, double* __restrict__ out) {
+  __shared__ double sh[8];
+  double s = 0.0, c = 0.0;
+  for (int i = threadIdx.x; i < np; i += blockDim.x) {
+    s += part[2 * i];
+    c += part[2 * i + 1];
+  }
+  block_sum2(s, c, sh);
+  if (threadIdx.x == 0) {
+    out[0] = s;
+    out[1] = c;
+  }
+}
+}  // namespace
+
+// out[2] = (sum, count) of x's entries that are not NaN and (unless miss_nan) != missing;
+// part: scratch of 2 * 1024 doubles
+FMLX_API int fmlx_masked_sum_f64(const double* x, long n, double missing, int miss_nan, double* part, double* out,
+                                 void* stream) {
+  if (x == nullptr && n > 0) return -1;
+  if (part == nullptr || out == nullptr) return -1;
+  const long want = (n + 255) / 256;
+  const int blocks = (int)(want < 1 ? 1 : (want < MSUM_BLOCKS ? want : MSUM_BLOCKS));
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(masked_sum_kernel, dim3(blocks), dim3(256), 0, st, x, n, missing, miss_nan, part);
+  hipLaunchKernelGGL(fold_pairs_kernel, dim3(1), dim3(256), 0, st, part, blocks, out);
+  return (int)hipGetLastError();
+}
+
 FMLX_DEFINE_PRELOAD()

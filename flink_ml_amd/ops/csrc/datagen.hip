@@ -195,7 +195,37 @@ __global__ __launch_bounds__(256) void reservoir_final_kernel(unsigned long long
     if (slot < k) atomicMax(&out[slot], (int)i);
   }
 }
+
+// the stream positions that can hold a rejected draw (u_p + p >= 2^31 − k − 1, see
+// reservoir_sample_device), compacted in ANY order through one counter: they are a tiny fraction
+// of the stream (≈ npos² / 2^32) and the host orders them before its sequential scan
+__global__ __launch_bounds__(256) void reservoir_cand_kernel(const int* __restrict__ u, long npos, long thr, long cap,
+                                                             int* __restrict__ cp, int* __restrict__ cu,
+                                                             unsigned long long* __restrict__ cnt) {
+  for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < npos; p += (long)gridDim.x * blockDim.x) {
+    const int v = u[p];
+    if ((long)v + p >= thr) {
+      const unsigned long long at = atomicAdd(cnt, 1ull);
+      if ((long)at < cap) {
+        cp[at] = (int)p;
+        cu[at] = v;
+      }
+    }
+  }
+}
 }  // namespace
+
+// cnt: one u64, zeroed by the caller; entries past cap are counted but not stored
+FMLX_API int fmlx_reservoir_candidates(const int* u, long npos, int k, long cap, int* cp, int* cu,
+                                       unsigned long long* cnt, void* stream) {
+  if (npos <= 0) return 0;
+  if (u == nullptr || cnt == nullptr || cap < 0 || (cap > 0 && (cp == nullptr || cu == nullptr))) return -1;
+  const long want = (npos + 255) / 256;
+  const int blocks = (int)(want < 8192 ? want : 8192);
+  hipLaunchKernelGGL(reservoir_cand_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, u, npos,
+                     (1L << 31) - (long)k - 1, cap, cp, cu, cnt);
+  return (int)hipGetLastError();
+}
 
 // out: int32[k], preset to 0 .. k − 1 (the reservoir's initial fill)
 FMLX_API int fmlx_reservoir_final(unsigned long long seed, long end, int k, const long* rej, long nrej, int* out,

@@ -212,6 +212,7 @@ def java_rows(seed: int, n: int, ops: Sequence[int], nvec: int, device=None, vec
 native.register_kernel_sigs({
     "fmlx_java_next31": [native.c_ulonglong, native.c_ulonglong, c_long, c_void_p, c_void_p],
     "fmlx_reservoir_final": [native.c_ulonglong, c_long, c_int, c_void_p, c_long, c_void_p, c_void_p],
+    "fmlx_reservoir_candidates": [c_void_p, c_long, c_int, c_long, c_void_p, c_void_p, c_void_p, c_void_p],
 })
 _host_sigs_done = False
 
@@ -244,6 +245,27 @@ def next31_stream(seed: int, start: int, count: int, device) -> torch.Tensor:
     return out
 
 
+RESERVOIR_CAND_HOST_SORT_MAX = 1 << 16  # candidates ordered on the host after the compaction kernel
+
+
+def _reservoir_candidates(u: torch.Tensor, npos: int, k: int):
+    """[positions | values] of the stream's candidate positions in position order (int32 [2, c],
+    host), from the unordered compaction kernel plus a host sort; None when there are more than
+    RESERVOIR_CAND_HOST_SORT_MAX (the caller takes the ordered torch path)."""
+    cap = RESERVOIR_CAND_HOST_SORT_MAX
+    buf = torch.empty(2 * cap + 2, dtype=torch.int32, device=u.device)  # cp | cu | u64 counter
+    buf[2 * cap:].zero_()
+    native.call("fmlx_reservoir_candidates", native.ptr(u), npos, k, cap, native.ptr(buf), native.ptr(buf[cap:]),
+                native.ptr(buf[2 * cap:]), native.stream_ptr(u.device))
+    h = buf.cpu().numpy()
+    c = int(h[2 * cap:].view(np.uint64)[0])
+    if c > cap:
+        return None
+    cp, cu = h[:c], h[cap:cap + c]
+    order = np.argsort(cp, kind="stable")
+    return np.stack([cp[order], cu[order]])
+
+
 def reservoir_sample_device(n: int, k: int, seed: int, device) -> torch.Tensor:
     """Positions ``SamplingOperator`` keeps (a java.util.Random(seed) reservoir of size k over n
     elements), in reservoir-slot order — bit-exact with the sequential sampler
@@ -270,11 +292,13 @@ def reservoir_sample_device(n: int, k: int, seed: int, device) -> torch.Tensor:
         u = next31_stream(seed, 0, npos, dev)
         # position p can only hold a rejected draw if u_p ≥ 2^31 − b for its bound b ≤ p + k + 1
         # (b shrinks with the rejections before p): ≈ half as many candidates as u ≥ 2^31 − n
-        pos = torch.arange(npos, dtype=torch.int64, device=dev)
-        cand = torch.nonzero(u.to(torch.int64) + pos >= (1 << 31) - k - 1).view(-1)
-        del pos
-        both = torch.stack([cand.to(torch.int32), u[cand]])  # one D2H copy of [positions | values]
-        both = both.cpu().numpy()
+        both = _reservoir_candidates(u, npos, k) if dev.type == "cuda" else None
+        if both is None:
+            pos = torch.arange(npos, dtype=torch.int64, device=dev)
+            cand = torch.nonzero(u.to(torch.int64) + pos >= (1 << 31) - k - 1).view(-1)
+            del pos
+            both = torch.stack([cand.to(torch.int32), u[cand]])  # one D2H copy of [positions | values]
+            both = both.cpu().numpy()
         cand_p, cand_u = np.ascontiguousarray(both[0]), np.ascontiguousarray(both[1])
         rej = np.zeros(max(len(cand_p), 1), dtype=np.int64)
         done = np.zeros(1, dtype=np.int32)

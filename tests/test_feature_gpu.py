@@ -198,3 +198,26 @@ def test_bucketizer_kernel_matches_cpu(handle):
         bad = Table({"c0": torch.tensor([0.1, float("nan")], dtype=torch.float64).cuda()}, num_rows=2)
         with pytest.raises(RuntimeError, match="invalid value"):
             Bucketizer().set_input_cols("c0").set_output_cols("o").set_splits_array([sp[0]]).transform(bad)
+
+
+@pytest.mark.parametrize("missing", [float("nan"), -1.0])
+def test_imputer_mean_kernel_matches_cpu(missing):
+    """csrc/colstats.hip masked_sum_kernel (Imputer mean without a filtered copy) against the CPU
+    path: NaNs and missingValue entries skipped, an all-missing column raises on both."""
+    from flink_ml_amd.models import Imputer
+
+    rng = np.random.default_rng(8)
+    cols = {}
+    for i in range(3):
+        v = rng.normal(size=300_001) * (i + 1)
+        v[rng.integers(0, v.size, 5000)] = np.nan
+        v[rng.integers(0, v.size, 5000)] = -1.0
+        cols["f%d" % i] = v
+    imp = Imputer().set_input_cols(*cols).set_output_cols("a", "b", "c").set_missing_value(missing)
+    ref = imp.fit(Table({k: torch.from_numpy(v) for k, v in cols.items()}, num_rows=300_001)).get_model_data()[0]
+    got = imp.fit(Table({k: torch.from_numpy(v).cuda() for k, v in cols.items()}, num_rows=300_001)) \
+        .get_model_data()[0]
+    r, g = ref.get_list(ref.column_names[0])[0], got.get_list(got.column_names[0])[0]
+    assert set(r) == set(g)
+    for k in r:
+        assert abs(r[k] - g[k]) <= 1e-12 * max(1.0, abs(r[k])), (k, r[k], g[k])

@@ -28,7 +28,9 @@ def test_next31_stream_offsets():
 def test_device_reservoir_on_gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    for n, k, seed in ((3_000_000, 1024, 1), (100_000, 10, 7)):
+    # (the candidate compaction kernel + host order up to 65536 candidates, ≈ n² / 2^32: the
+    # 100k / 300k / 1M cases; 3M takes the ordered torch path)
+    for n, k, seed in ((3_000_000, 1024, 1), (100_000, 10, 7), (300_000, 65536, 9), (1_000_000, 10, 2)):
         assert torch.equal(datagen.next31_stream(seed, 17, 5000, "cuda").cpu(), datagen.next31_stream(seed, 17, 5000, "cpu"))
         got = datagen.reservoir_sample_device(n, k, seed, "cuda").cpu().numpy()
         assert np.array_equal(got, reservoir_sample_indices(n, k, seed))
