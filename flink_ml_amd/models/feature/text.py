@@ -392,6 +392,43 @@ class RegexTokenizer(Transformer, HasInputCol, HasOutputCol):
         return [t.with_column(self.get(self.OUTPUT_COL), out)]
 
 
+NGRAM_DENSE_MAX = 1 << 26  # possible grams (V^n) up to which NGram uses the presence-table kernels
+native.register_kernel_sigs({
+    "fmlx_ngram_codes": [native.c_void_p, native.c_void_p, native.c_long, native.c_int, native.c_long, native.c_int,
+                         native.c_void_p, native.c_void_p, native.c_void_p, native.c_void_p, native.c_void_p,
+                         native.c_void_p],
+})
+
+
+def _ngram_device(dc, n: int, V: int) -> StringArrayColumn:
+    """NGram on a device dictionary column with few possible grams (V^n <= NGRAM_DENSE_MAX): a
+    presence table and its prefix sum replace the sort-unique of all grams (csrc/hash.hip
+    ngram_mark_kernel / ngram_emit_kernel); the distinct grams come out sorted, as before."""
+    dev = dc.codes.device
+    codes = dc.codes.to(torch.int32).contiguous()
+    off = dc.offsets.to(dev, torch.int64).contiguous()
+    nd, G, stream = len(dc), V ** n, native.stream_ptr(dev)
+    present = torch.zeros(G, dtype=torch.uint8, device=dev)
+    noff = torch.zeros(nd + 1, dtype=torch.int64, device=dev)
+    native.call("fmlx_ngram_codes", native.ptr(codes) if codes.numel() else None, native.ptr(off), nd, n, V, 0,
+                native.ptr(present), native.ptr(noff[1:]), None, None, None, stream)
+    noff[1:] = torch.cumsum(noff[1:], 0)
+    rank = torch.cumsum(present, 0, dtype=torch.int32)
+    total = int(noff[-1])
+    out = torch.empty(total, dtype=torch.int32, device=dev)
+    if total:
+        native.call("fmlx_ngram_codes", native.ptr(codes), native.ptr(off), nd, n, V, 1, None, None, native.ptr(rank),
+                    native.ptr(noff), native.ptr(out), stream)
+    u = torch.nonzero(present).view(-1).cpu().numpy()
+    digits = []
+    for _ in range(n):
+        digits.append(u % V)
+        u = u // V
+    words = dc.vocab
+    vocab = [" ".join(words[digits[n - 1 - j][i]] for j in range(n)) for i in range(len(digits[0]))]
+    return StringArrayColumn(noff, out, vocab)
+
+
 @rw.register_stage
 class NGram(Transformer, HasInputCol, HasOutputCol):
     JAVA_CLASS_NAME = "org.apache.flink.ml.feature.ngram.NGram"
@@ -405,6 +442,9 @@ class NGram(Transformer, HasInputCol, HasOutputCol):
         if dc is not None and all(isinstance(w, str) for w in dc.vocab) and V > 0 and (V + 1) ** n < (1 << 62):
             # grams as base-V integers over consecutive codes of a row, dictionary-encoded again;
             # only the distinct grams are joined into strings on the host
+            if dc.codes.is_cuda and V ** n <= NGRAM_DENSE_MAX:
+                out = _ngram_device(dc, n, V)
+                return [t.with_column(self.get(self.OUTPUT_COL), out)]
             codes = dc.codes.long()
             N = codes.shape[0]
             pos = torch.arange(N, device=codes.device)
@@ -769,6 +809,29 @@ class CountVectorizerModel(ModelWithData, CountVectorizerModelParams):
 # segmented sort (equal-length documents), else one global unique of (doc, term) keys
 DF_BITMAP_MAX = 1 << 32
 DF_SEGMENTED_SORT = True
+CV_TFDF_MAX_V = 4096  # dictionary sizes the one-pass tf / df kernel takes (csrc/hash.hip cv_tfdf_kernel)
+native.register_kernel_sigs({
+    "fmlx_cv_tfdf": [native.c_void_p, native.c_void_p, native.c_long, native.c_int, native.c_void_p, native.c_void_p,
+                     native.c_void_p, native.c_void_p],
+})
+
+
+def _cv_counts_device(dc, tab, V: int, N: int):
+    """(vocabulary table in first-seen order, [tf, df] per term, first positions) of a device
+    dictionary column in one kernel pass over its codes (csrc/hash.hip cv_tfdf_kernel); the [V]
+    results are ordered on the host."""
+    dev = dc.codes.device
+    codes = dc.codes if dc.codes.dtype == torch.int32 else dc.codes.to(torch.int32)
+    off = dc.offsets.to(dev, torch.int64).contiguous()
+    out = torch.zeros(3 * V, dtype=torch.int64, device=dev)  # tf | df | first
+    out[2 * V:] = N
+    native.call("fmlx_cv_tfdf", native.ptr(codes.contiguous()), native.ptr(off), len(dc), V, native.ptr(out),
+                native.ptr(out[V:]), native.ptr(out[2 * V:]), native.stream_ptr(dev))
+    h = out.cpu().numpy().reshape(3, V)
+    present = np.nonzero(h[0] > 0)[0]
+    present = present[np.argsort(h[2][present], kind="stable")]  # first-seen order
+    sums = np.stack([h[0][present], h[1][present]], 1).astype(np.float64)
+    return tab.take(present), sums, h[2][present].copy()
 
 
 @rw.register_stage
@@ -789,42 +852,45 @@ class CountVectorizer(Estimator, CountVectorizerParams):
             # term and document frequencies per distinct string from the codes on the device; the
             # first-occurrence order (it decides HashMap bucket-collision order) via a scatter-min
             V = len(dc.vocab)
-            codes = dc.codes.long()
-            N, nd = codes.shape[0], len(dc)
-            tf_t = torch.bincount(codes, minlength=V)
-            lens = dc.offsets[1:] - dc.offsets[:-1]
-            L = int(lens[0]) if nd else 0
-            if nd * V <= DF_BITMAP_MAX:  # (doc, term) presence bitmap: a scatter instead of a sort
-                pres = torch.zeros(nd * V, dtype=torch.bool, device=codes.device)
-                pres[dc.row_ids() * V + codes] = True
-                df_t = pres.view(nd, V).sum(0)
-                del pres
-            elif 0 < L <= 4096 and DF_SEGMENTED_SORT and bool((lens == L).all()):
-                # equal-length documents: sort each document's codes (a segmented sort along
-                # dim 1), count every term once per document
-                S = torch.sort(dc.codes.view(nd, L), dim=1).values
-                first_in_doc = torch.ones_like(S, dtype=torch.bool)
-                first_in_doc[:, 1:] = S[:, 1:] != S[:, :-1]
-                df_t = torch.bincount(S[first_in_doc].long(), minlength=V)
-                del S, first_in_doc
+            N, nd = dc.codes.shape[0], len(dc)
+            if dc.codes.is_cuda and 0 < V <= CV_TFDF_MAX_V and N < (1 << 32) and nd:
+                tab, sums, firsts = _cv_counts_device(dc, tab, V, N)
             else:
-                df_t = torch.bincount(torch.unique(dc.row_ids() * V + codes) % V, minlength=V)
-            present = torch.nonzero(tf_t > 0).reshape(-1)
-            # first occurrences over a geometrically growing prefix: every term usually shows up
-            # early, so the scatter-min does not run over (and contend on) all N codes
-            first = torch.full((V,), N, dtype=torch.int64, device=codes.device)
-            s0, step = 0, 1 << 20
-            while s0 < N:
-                e0 = min(N, s0 + step)
-                first.scatter_reduce_(0, codes[s0:e0], torch.arange(s0, e0, device=codes.device), reduce="amin")
-                if not bool((first[present] == N).any()):
-                    break
-                s0, step = e0, step * 4
-            present = present[torch.argsort(first[present])]  # first-seen order, sorted on the device
-            pres_h = present.cpu().numpy()
-            tab = tab.take(pres_h)
-            sums = torch.stack([tf_t[present], df_t[present]], 1).cpu().numpy().astype(np.float64)
-            firsts = first[present].cpu().numpy()
+                codes = dc.codes.long()
+                tf_t = torch.bincount(codes, minlength=V)
+                lens = dc.offsets[1:] - dc.offsets[:-1]
+                L = int(lens[0]) if nd else 0
+                if nd * V <= DF_BITMAP_MAX:  # (doc, term) presence bitmap: a scatter instead of a sort
+                    pres = torch.zeros(nd * V, dtype=torch.bool, device=codes.device)
+                    pres[dc.row_ids() * V + codes] = True
+                    df_t = pres.view(nd, V).sum(0)
+                    del pres
+                elif 0 < L <= 4096 and DF_SEGMENTED_SORT and bool((lens == L).all()):
+                    # equal-length documents: sort each document's codes (a segmented sort along
+                    # dim 1), count every term once per document
+                    S = torch.sort(dc.codes.view(nd, L), dim=1).values
+                    first_in_doc = torch.ones_like(S, dtype=torch.bool)
+                    first_in_doc[:, 1:] = S[:, 1:] != S[:, :-1]
+                    df_t = torch.bincount(S[first_in_doc].long(), minlength=V)
+                    del S, first_in_doc
+                else:
+                    df_t = torch.bincount(torch.unique(dc.row_ids() * V + codes) % V, minlength=V)
+                present = torch.nonzero(tf_t > 0).reshape(-1)
+                # first occurrences over a geometrically growing prefix: every term usually shows up
+                # early, so the scatter-min does not run over (and contend on) all N codes
+                first = torch.full((V,), N, dtype=torch.int64, device=codes.device)
+                s0, step = 0, 1 << 20
+                while s0 < N:
+                    e0 = min(N, s0 + step)
+                    first.scatter_reduce_(0, codes[s0:e0], torch.arange(s0, e0, device=codes.device), reduce="amin")
+                    if not bool((first[present] == N).any()):
+                        break
+                    s0, step = e0, step * 4
+                present = present[torch.argsort(first[present])]  # first-seen order, sorted on the device
+                pres_h = present.cpu().numpy()
+                tab = tab.take(pres_h)
+                sums = torch.stack([tf_t[present], df_t[present]], 1).cpu().numpy().astype(np.float64)
+                firsts = first[present].cpu().numpy()
             ndocs = len(dc)
         else:
             docs = _strings_col(inputs[0], self.get(self.INPUT_COL))

@@ -257,6 +257,60 @@ FMLX_API int fmlx_java_int_draws(unsigned long long seed, unsigned long long sta
   return (int)hipGetLastError();
 }
 
+// ---- rare-rejection compaction of the int draws: the rejected positions (ok == 0) compacted in
+// any order through one counter (the host sorts the few of them), then every accepted draw copied
+// to its final place: output i reads source i + #{j : q_j <= i} with q_j = p_j − j for the sorted
+// rejected positions p_j (a binary search) — one read and one write per draw instead of a boolean
+// mask index (a prefix sum over the whole stream).
+namespace {
+__global__ __launch_bounds__(256) void zero_positions_kernel(const unsigned char* __restrict__ ok, long n, long cap,
+                                                             long long* __restrict__ pos,
+                                                             unsigned long long* __restrict__ cnt) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    if (ok[i] == 0) {
+      const unsigned long long at = atomicAdd(cnt, 1ull);
+      if ((long)at < cap) pos[at] = i;
+    }
+  }
+}
+__global__ __launch_bounds__(256) void remove_positions_kernel(const int* __restrict__ src, const long long* __restrict__ q,
+                                                               int nq, int* __restrict__ dst, long nout) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nout; i += (long)gridDim.x * blockDim.x) {
+    int lo = 0, hi = nq;  // #{j : q_j <= i}
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (q[mid] <= i)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    dst[i] = src[i + lo];
+  }
+}
+}  // namespace
+
+// pos: int64 [cap]; cnt: one u64 zeroed by the caller (counts past cap too)
+FMLX_API int fmlx_u8_zero_positions(const unsigned char* ok, long n, long cap, long long* pos, unsigned long long* cnt,
+                                    void* stream) {
+  if (n <= 0) return 0;
+  if (ok == nullptr || cnt == nullptr || (cap > 0 && pos == nullptr)) return -1;
+  const long want = (n + 255) / 256;
+  const int blocks = (int)(want < 8192 ? want : 8192);
+  hipLaunchKernelGGL(zero_positions_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, ok, n, cap, pos, cnt);
+  return (int)hipGetLastError();
+}
+
+// q: int64 [nq] non-decreasing (sorted rejected positions minus their rank); src holds at least
+// nout + nq entries
+FMLX_API int fmlx_remove_positions_i32(const int* src, const long long* q, int nq, int* dst, long nout, void* stream) {
+  if (nout <= 0) return 0;
+  if (src == nullptr || dst == nullptr || nq < 0 || (nq > 0 && q == nullptr)) return -1;
+  const long want = (nout + 255) / 256;
+  const int blocks = (int)(want < 16384 ? want : 16384);
+  hipLaunchKernelGGL(remove_positions_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, src, q, nq, dst, nout);
+  return (int)hipGetLastError();
+}
+
 FMLX_API int fmlx_java_rows(int vec_dtype, unsigned long long seed, unsigned long long start_draw, long row0,
                             long nrows, const int* ops, const int* slot_off, int nslots, int nvec, int draws_per_row,
                             void* vec, double* scal, unsigned long long* first_reject, void* stream) {

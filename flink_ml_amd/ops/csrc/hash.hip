@@ -194,7 +194,126 @@ __global__ __launch_bounds__(256) void tf_rows_kernel(const long long* __restric
     }
   }
 }
+
+// ---- CountVectorizer term / document frequencies and first occurrences in one pass over the
+// dictionary codes (CountVectorizer.java:151-204: per document a term counts once toward df and
+// every time toward tf; the first-seen order decides the vocabulary order). A wave per document,
+// per-block LDS histograms (integer atomics), a per-wave presence bitmap of V bits: the lane whose
+// atomicOr first sets a term's bit in this document counts its df; the wave clears its bitmap
+// after the document. Block results go out with one global atomic per non-zero term.
+constexpr int CV_VMAX = 4096;
+__global__ __launch_bounds__(256) void cv_tfdf_kernel(const int* __restrict__ codes, const long long* __restrict__ off,
+                                                      long nd, int V, long docs_per_block,
+                                                      unsigned long long* __restrict__ tf,
+                                                      unsigned long long* __restrict__ df,
+                                                      unsigned long long* __restrict__ first) {
+  __shared__ unsigned tfl[CV_VMAX];
+  __shared__ unsigned dfl[CV_VMAX];
+  __shared__ unsigned fl[CV_VMAX];
+  __shared__ unsigned bm[4][CV_VMAX / 32];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int words = (V + 31) >> 5;
+  for (int i = threadIdx.x; i < V; i += blockDim.x) {
+    tfl[i] = 0u;
+    dfl[i] = 0u;
+    fl[i] = 0xffffffffu;
+  }
+  for (int i = lane; i < words; i += 64) bm[w][i] = 0u;
+  __syncthreads();
+  const long d0 = (long)blockIdx.x * docs_per_block;
+  const long d1 = d0 + docs_per_block < nd ? d0 + docs_per_block : nd;
+  const long long base = d0 < nd ? off[d0] : 0;
+  for (long d = d0 + w; d < d1; d += 4) {
+    const long long b = off[d], e = off[d + 1];
+    for (long long j = b + lane; j < e; j += 64) {
+      const int c = codes[j];
+      atomicAdd(&tfl[c], 1u);
+      atomicMin(&fl[c], (unsigned)(j - base));
+      const unsigned bit = 1u << (c & 31);
+      if ((atomicOr(&bm[w][c >> 5], bit) & bit) == 0u) atomicAdd(&dfl[c], 1u);
+    }
+    for (int i = lane; i < words; i += 64) bm[w][i] = 0u;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < V; i += blockDim.x) {
+    if (tfl[i]) {
+      atomicAdd(&tf[i], (unsigned long long)tfl[i]);
+      atomicAdd(&df[i], (unsigned long long)dfl[i]);
+      atomicMin(&first[i], (unsigned long long)base + fl[i]);
+    }
+  }
+}
+
+// ---- NGram over dictionary codes (NGram.java:81-100): a row of L codes yields max(0, L − n + 1)
+// grams, each the base-V number of n consecutive codes. Mark pass: one thread per row writes its
+// gram count and sets present[g] (a byte per possible gram, V^n small; racing writers store the
+// same 1). After the host's scans (row offsets, inclusive gram ranks) the emit pass writes every
+// gram's rank — its index in the sorted distinct grams — at its final place.
+__global__ __launch_bounds__(256) void ngram_mark_kernel(const int* __restrict__ codes, const long long* __restrict__ off,
+                                                         long nd, int n, long long V, unsigned char* __restrict__ present,
+                                                         long long* __restrict__ cnt) {
+  for (long r = (long)blockIdx.x * blockDim.x + threadIdx.x; r < nd; r += (long)gridDim.x * blockDim.x) {
+    const long long b = off[r];
+    const long long c = off[r + 1] - b - n + 1;
+    cnt[r] = c > 0 ? c : 0;
+    for (long long t = 0; t < c; ++t) {
+      long long g = 0;
+      for (int j = 0; j < n; ++j) g = g * V + codes[b + t + j];
+      present[g] = 1;
+    }
+  }
+}
+__global__ __launch_bounds__(256) void ngram_emit_kernel(const int* __restrict__ codes, const long long* __restrict__ off,
+                                                         long nd, int n, long long V, const int* __restrict__ rank,
+                                                         const long long* __restrict__ noff, int* __restrict__ out) {
+  for (long r = (long)blockIdx.x * blockDim.x + threadIdx.x; r < nd; r += (long)gridDim.x * blockDim.x) {
+    const long long b = off[r];
+    const long long c = off[r + 1] - b - n + 1;
+    const long long o = noff[r];
+    for (long long t = 0; t < c; ++t) {
+      long long g = 0;
+      for (int j = 0; j < n; ++j) g = g * V + codes[b + t + j];
+      out[o + t] = rank[g] - 1;
+    }
+  }
+}
 }  // namespace
+
+// phase 0: present (u8 [V^n], zeroed by the caller) and cnt (int64 [nd]); phase 1: out at noff
+// from the inclusive ranks (int32 [V^n])
+FMLX_API int fmlx_ngram_codes(const int* codes, const long long* off, long nd, int n, long long V, int phase,
+                              unsigned char* present, long long* cnt, const int* rank, const long long* noff, int* out,
+                              void* stream) {
+  if (nd <= 0) return 0;
+  if (off == nullptr || n < 1 || V < 1 || (phase == 0 && (present == nullptr || cnt == nullptr)) ||
+      (phase != 0 && (rank == nullptr || noff == nullptr || out == nullptr)))
+    return -1;
+  const long want = (nd + 255) / 256;
+  const int blocks = (int)(want < 16384 ? want : 16384);
+  hipStream_t s = (hipStream_t)stream;
+  if (phase == 0)
+    hipLaunchKernelGGL(ngram_mark_kernel, dim3(blocks), dim3(256), 0, s, codes, off, nd, n, V, present, cnt);
+  else
+    hipLaunchKernelGGL(ngram_emit_kernel, dim3(blocks), dim3(256), 0, s, codes, off, nd, n, V, rank, noff, out);
+  return (int)hipGetLastError();
+}
+
+FMLX_API int fmlx_cv_vmax() { return CV_VMAX; }
+
+// codes int32 [N] in [0, V), off int64 [nd+1]; tf / df zeroed and first filled with N by the
+// caller (u64 [V] each). A block's codes must span < 2^32 positions.
+FMLX_API int fmlx_cv_tfdf(const int* codes, const long long* off, long nd, int V, unsigned long long* tf,
+                          unsigned long long* df, unsigned long long* first, void* stream) {
+  if (nd <= 0) return 0;
+  if (V < 1 || V > CV_VMAX || off == nullptr || tf == nullptr || df == nullptr || first == nullptr) return -1;
+  long blocks = 2048;
+  if (blocks > (nd + 3) / 4) blocks = (nd + 3) / 4;
+  const long per = (nd + blocks - 1) / blocks;
+  blocks = (nd + per - 1) / per;
+  hipLaunchKernelGGL(cv_tfdf_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, codes, off, nd, V, per,
+                     tf, df, first);
+  return (int)hipGetLastError();
+}
 
 // off: int64 [n+1] row offsets; keys int64 (key64) or int32 bucket indices in [0, 2^31 − 1).
 // Phase 0: cnt[n] = distinct per row, *flag = 1 if a row exceeds 32 entries; phase 1: entries.

@@ -24,6 +24,8 @@ _MASK = (1 << 48) - 1
 
 native.register_kernel_sigs({
     "fmlx_java_int_draws": [native.c_ulonglong, native.c_ulonglong, c_long, c_int, c_void_p, c_void_p, c_void_p],
+    "fmlx_u8_zero_positions": [c_void_p, c_long, c_long, c_void_p, c_void_p, c_void_p],
+    "fmlx_remove_positions_i32": [c_void_p, c_void_p, c_int, c_void_p, c_long, c_void_p],
     "fmlx_java_rows": [c_int, native.c_ulonglong, native.c_ulonglong, c_long, c_long, c_void_p, c_void_p, c_int, c_int,
                        c_int, c_void_p, c_void_p, c_void_p, c_void_p],
 })
@@ -118,6 +120,28 @@ def _cpu_rows(x0: int, start: int, n: int, ops, nvec, vec: np.ndarray, scal: np.
     return int(bad[0]) if bad.size else -1
 
 
+INT_DRAWS_REJECT_CAP = 1 << 16  # rejected draws per window the positional compaction takes
+
+
+def _compact_accepted(r: torch.Tensor, ok: torch.Tensor, count: int, rem: int, dst: torch.Tensor):
+    """Copies the first min(rem, accepted) accepted draws of ``r`` to ``dst`` with the
+    rare-rejection kernels (csrc/datagen.hip); returns how many, or None when the window holds more
+    than INT_DRAWS_REJECT_CAP rejections (the caller takes the boolean-mask path)."""
+    dev, cap = r.device, INT_DRAWS_REJECT_CAP
+    buf = torch.zeros(cap + 1, dtype=torch.int64, device=dev)  # positions | counter
+    stream = native.stream_ptr(dev)
+    native.call("fmlx_u8_zero_positions", native.ptr(ok), count, cap, native.ptr(buf), native.ptr(buf[cap:]), stream)
+    h = buf.cpu().numpy()
+    nrej = int(h[cap])
+    if nrej > cap:
+        return None
+    rej = np.sort(h[:nrej])
+    take = min(rem, count - nrej)
+    q = torch.from_numpy(rej - np.arange(nrej, dtype=np.int64)).to(dev) if nrej else buf[:1]
+    native.call("fmlx_remove_positions_i32", native.ptr(r), native.ptr(q), nrej, native.ptr(dst), take, stream)
+    return take
+
+
 def java_uniform_int_rows(seed: int, n: int, k: int, bound: int, device) -> torch.Tensor:
     """[n, k] int32 of ``k`` successive ``Random.nextInt(bound)`` per row (rows back to back in one
     ``java.util.Random(seed)`` stream), on the device for any bound: raw draws and their rejection
@@ -135,9 +159,11 @@ def java_uniform_int_rows(seed: int, n: int, k: int, bound: int, device) -> torc
         r = torch.empty(count, dtype=torch.int32, device=device)
         ok = torch.empty(count, dtype=torch.uint8, device=device)
         native.call("fmlx_java_int_draws", x0, pos, count, bound, native.ptr(r), native.ptr(ok), native.stream_ptr(device))
-        acc = r[ok.bool()]
-        take = min(rem, acc.numel())
-        out[got:got + take] = acc[:take]
+        take = _compact_accepted(r, ok, count, rem, out[got:]) if r.is_cuda else None
+        if take is None:
+            acc = r[ok.bool()]
+            take = min(rem, acc.numel())
+            out[got:got + take] = acc[:take]
         if take == rem:
             break
         got += take

@@ -212,7 +212,8 @@ def test_bench_timed_region_only_replays(monkeypatch, steps, warmup, R, defer):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("bound,k,n", [(1_000_000, 100, 3000), ((1 << 30) + 3, 3, 5000), (100, 10, 20000), (7, 1, 999)])
+@pytest.mark.parametrize("bound,k,n", [(1_000_000, 100, 3000), ((1 << 30) + 3, 3, 5000), (100, 10, 20000), (7, 1, 999),
+                                       ((1 << 30) + 3, 3, 100_000)])  # (the last: > 65536 rejections, mask path)
 def test_java_uniform_int_rows_gpu_matches_sequential(bound, k, n):
     """Every draw nextInt(b) with one non-power-of-two b: the compacted parallel draws equal the
     sequential java.util.Random rejection loop (bound 2^30+3 rejects ~half of all draws)."""

@@ -221,3 +221,78 @@ def test_imputer_mean_kernel_matches_cpu(missing):
     assert set(r) == set(g)
     for k in r:
         assert abs(r[k] - g[k]) <= 1e-12 * max(1.0, abs(r[k])), (k, r[k], g[k])
+
+
+def test_count_vectorizer_tfdf_kernel():
+    """csrc/hash.hip cv_tfdf_kernel against numpy per-term tf / df / first position, and the fitted
+    vocabulary against the torch path (skewed term frequencies, empty and repeated-term
+    documents, unused dictionary entries), with and without minDF / maxDF."""
+    from flink_ml_amd.models import CountVectorizer
+    from flink_ml_amd.models.feature import text
+    from flink_ml_amd.table import StringArrayColumn
+
+    rng = np.random.default_rng(6)
+    V, nd = 300, 20000
+    vocab = ["t%03d" % i for i in range(V)]
+    lens = rng.integers(0, 40, nd)
+    codes = np.minimum(rng.zipf(1.3, int(lens.sum())) - 1, V - 10).astype(np.int32)  # last 9 unused
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    col = StringArrayColumn(torch.from_numpy(off).cuda(), torch.from_numpy(codes).cuda(), vocab)
+    from flink_ml_amd.utils.strtable import StrTable
+
+    tab, sums, firsts = text._cv_counts_device(col, StrTable.from_strings(vocab), V, len(codes))
+    tf = np.bincount(codes, minlength=V)
+    df = np.zeros(V, dtype=np.int64)
+    for d in range(nd):
+        df[np.unique(codes[off[d]:off[d + 1]])] += 1
+    first = np.full(V, len(codes))
+    for p in range(len(codes) - 1, -1, -1):
+        first[codes[p]] = p
+    present = np.nonzero(tf)[0]
+    present = present[np.argsort(first[present], kind="stable")]
+    assert tab.take_strings(np.arange(len(tab))) == [vocab[i] for i in present]
+    np.testing.assert_array_equal(sums[:, 0], tf[present])
+    np.testing.assert_array_equal(sums[:, 1], df[present])
+    np.testing.assert_array_equal(firsts, first[present])
+    t = Table({"input": col}, num_rows=nd)
+    for kw in ({}, {"min_df": 3.0, "max_df": 0.5}):
+        cv = CountVectorizer().set_vocabulary_size(50)
+        if kw:
+            cv = cv.set_min_df(kw["min_df"]).set_max_df(kw["max_df"])
+        got = cv.fit(t).get_model_data()[0].get_list("vocabulary")[0]
+        saved = text.CV_TFDF_MAX_V
+        text.CV_TFDF_MAX_V = 0
+        try:
+            ref = cv.fit(t).get_model_data()[0].get_list("vocabulary")[0]
+        finally:
+            text.CV_TFDF_MAX_V = saved
+        assert list(got) == list(ref)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_ngram_presence_kernels_match_sort_path(n):
+    """csrc/hash.hip ngram_mark_kernel / ngram_emit_kernel against the sort-unique path on the same
+    device column: rows shorter than n (no grams), empty rows, repeated grams."""
+    from flink_ml_amd.models import NGram
+    from flink_ml_amd.models.feature import text
+    from flink_ml_amd.table import StringArrayColumn
+
+    rng = np.random.default_rng(n)
+    vocab = ["a", "bb", "c c", "ü", "e"]
+    lens = rng.integers(0, 6, 5000)
+    codes = rng.integers(0, len(vocab), int(lens.sum())).astype(np.int32)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    col = StringArrayColumn(torch.from_numpy(off).cuda(), torch.from_numpy(codes).cuda(), vocab)
+    t = Table({"input": col}, num_rows=len(lens))
+    ng = NGram().set_n(n)
+    got = ng.transform(t)[0].column("output")
+    saved = text.NGRAM_DENSE_MAX
+    text.NGRAM_DENSE_MAX = 0
+    try:
+        ref = ng.transform(t)[0].column("output")
+    finally:
+        text.NGRAM_DENSE_MAX = saved
+    assert list(got.vocab) == list(ref.vocab)
+    assert torch.equal(got.offsets.cpu(), ref.offsets.cpu())
+    assert torch.equal(got.codes.cpu().long(), ref.codes.cpu().long())
+    assert [list(r) for r in got][:50] == [list(r) for r in ref][:50]
