@@ -74,12 +74,12 @@ class InputDataGenerator(DataGenerator):
         return ctx.rank, ctx.world_size, task_rows(self.get(self.NUM_VALUES), ctx.rank, ctx.world_size), \
             task_seed(self.get_seed(), ctx.rank)
 
-    def _rows(self, ops, nvec, vec_dtype=None):
+    def _rows(self, ops, nvec, vec_dtype=None, int_codes=False):
         _, _, n, seed = self._task()
         dev = config.compute_device()
         if vec_dtype is None:
             vec_dtype = torch.float64 if dev.type == "cpu" else config.compute_dtype()
-        return java_rows(seed, n, ops, nvec, device=dev, vec_dtype=vec_dtype)
+        return java_rows(seed, n, ops, nvec, device=dev, vec_dtype=vec_dtype, int_codes=int_codes)
 
 
 @rw.register_stage
@@ -149,7 +149,7 @@ class RandomStringGenerator(InputDataGenerator, HasNumDistinctValues):
     def get_data(self):
         names = self.get(self.COL_NAMES)
         k = len(names[0])
-        _, sc = self._rows([self.get(self.NUM_DISTINCT_VALUES)] * k, 0)
+        _, sc = self._rows([self.get(self.NUM_DISTINCT_VALUES)] * k, 0, int_codes=True)
         vocab = [str(i) for i in range(self.get(self.NUM_DISTINCT_VALUES))]
         # dictionary-encoded, device-resident strings (rows materialise as str on demand)
         return [Table({c: StringColumn(sc[:, i].contiguous().to(torch.int32), vocab) for i, c in enumerate(names[0])},
@@ -163,7 +163,7 @@ class RandomStringArrayGenerator(InputDataGenerator, HasNumDistinctValues, HasAr
     def get_data(self):
         names = self.get(self.COL_NAMES)
         k, a = len(names[0]), self.get(self.ARRAY_SIZE)
-        _, sc = self._rows([self.get(self.NUM_DISTINCT_VALUES)] * (k * a), 0)
+        _, sc = self._rows([self.get(self.NUM_DISTINCT_VALUES)] * (k * a), 0, int_codes=True)
         codes = sc.reshape(sc.shape[0], k, a)
         vocab = [str(i) for i in range(self.get(self.NUM_DISTINCT_VALUES))]
         # dictionary-encoded, device-resident string arrays (rows materialise as lists on demand)

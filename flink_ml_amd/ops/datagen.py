@@ -171,8 +171,11 @@ def java_uniform_int_rows(seed: int, n: int, k: int, bound: int, device) -> torc
     return out.view(n, k)
 
 
-def java_rows(seed: int, n: int, ops: Sequence[int], nvec: int, device=None, vec_dtype=torch.float64):
-    """Rows of one generator task: (vec [n, nvec] in ``vec_dtype``, scalars [n, len(ops)-nvec] fp64)."""
+def java_rows(seed: int, n: int, ops: Sequence[int], nvec: int, device=None, vec_dtype=torch.float64,
+              int_codes: bool = False):
+    """Rows of one generator task: (vec [n, nvec] in ``vec_dtype``, scalars [n, len(ops)-nvec] fp64).
+    ``int_codes``: scalars that are all nextInt(b) draws of one bound may come back as int32 (the
+    string generators' dictionary codes: no fp64 round trip of the whole draw stream)."""
     device = torch.device(device) if device is not None else torch.device("cpu")
     ops = [int(o) for o in ops]
     if nvec == 0 and ops and len(set(ops)) == 1 and ops[0] > 0 and ops[0] & (ops[0] - 1) != 0 and n > 0:
@@ -180,7 +183,7 @@ def java_rows(seed: int, n: int, ops: Sequence[int], nvec: int, device=None, vec
         # device, or run the sequential Random on the host (native) — no per-rejection restarts
         if device.type == "cuda":
             codes = java_uniform_int_rows(seed, n, len(ops), ops[0], device)
-            return torch.empty((n, 0), dtype=vec_dtype, device=device), codes.to(torch.float64)
+            return torch.empty((n, 0), dtype=vec_dtype, device=device), codes if int_codes else codes.to(torch.float64)
         import ctypes
 
         native.register_host_sigs({"fmlx_java_next_ints": [ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
@@ -188,7 +191,7 @@ def java_rows(seed: int, n: int, ops: Sequence[int], nvec: int, device=None, vec
         out = np.empty(n * len(ops), dtype=np.int32)
         native.host().fmlx_java_next_ints(int(seed), out.size, int(ops[0]), out.ctypes.data)
         return (torch.empty((n, 0), dtype=vec_dtype),
-                torch.from_numpy(out.reshape(n, len(ops)).astype(np.float64)))
+                torch.from_numpy(out.reshape(n, len(ops)) if int_codes else out.reshape(n, len(ops)).astype(np.float64)))
     ns = len(ops) - nvec
     dpr = _draws_per_row(ops)
     x0 = scramble(seed)

@@ -106,17 +106,20 @@ def _unsigned_to_value(u: torch.Tensor, nbits: int) -> torch.Tensor:
     return bits.to(torch.int32).view(torch.float32)
 
 
-def kth_smallest_device(X: torch.Tensor, ks: torch.Tensor, distributed: bool = False) -> torch.Tensor:
+def kth_smallest_device(X: torch.Tensor, ks, distributed: bool = False, nq: int = 0) -> torch.Tensor:
     """k-th smallest (1-based ``ks`` [Q, d], Q <= 4) of every column of a GPU matrix, NaNs skipped,
     by the ``radixselect.hip`` histogram kernel: 4 (fp32) / 8 (fp64) passes of 8-bit digits for
-    all Q ranks at once; per pass only the [Q, d, 256] histogram is all-reduced."""
+    all Q ranks at once; per pass only the [Q, d, 256] histogram is all-reduced. ``ks`` may also be
+    a function of the columns' (global) non-NaN counts — the top digit's histogram, which every
+    rank target shares — returning the ranks (``nq`` of them): no separate counting pass."""
     if X.dtype not in (torch.float32, torch.float64):
         X = X.to(torch.float32)
     if X.stride(1) != 1:
         X = X.contiguous()
     n, d = X.shape
-    Q = ks.shape[0]
-    assert 1 <= Q <= _MAXQ and ks.shape[1] == d
+    rank_fn = ks if callable(ks) else None
+    Q = nq if rank_fn is not None else ks.shape[0]
+    assert 1 <= Q <= _MAXQ and (rank_fn is not None or ks.shape[1] == d)
     nbits = 64 if X.dtype == torch.float64 else 32
     dev = X.device
     groups = (d + 15) // 16
@@ -126,15 +129,21 @@ def kth_smallest_device(X: torch.Tensor, ks: torch.Tensor, distributed: bool = F
     part = torch.empty(chunks * Q * d * 256, dtype=torch.int32, device=dev)
     hist = torch.empty((Q, d, 256), dtype=torch.int64, device=dev)
     prefix = torch.zeros((Q, d), dtype=torch.int64, device=dev)
-    kk = ks.to(device=dev, dtype=torch.int64).clone()
+    kk = None if rank_fn is not None else ks.to(device=dev, dtype=torch.int64).clone()
     for i, shift in enumerate(range(nbits - 8, -1, -8)):
         # the top digit's histogram is the same for every rank target: count it once
         q_eff = 1 if i == 0 else Q
         native.call("fmlx_radix_hist", native.dtype_code(X.dtype), native.ptr(X), X.stride(0), n, d,
                     native.ptr(prefix), q_eff, shift, int(i == 0), chunks, native.ptr(part), native.ptr(hist),
                     native.stream_ptr(dev))
-        h = hist[:1].expand(Q, d, 256) if i == 0 else hist
-        h = comm.all_reduce_sum(h.contiguous()) if distributed else h
+        if i == 0:
+            h = comm.all_reduce_sum(hist[:1].contiguous()) if distributed else hist[:1]
+            if rank_fn is not None:
+                kk = rank_fn(h[0].sum(-1)).to(device=dev, dtype=torch.int64).clone()
+                assert kk.shape == (Q, d)
+            h = h.expand(Q, d, 256)
+        else:
+            h = comm.all_reduce_sum(hist.contiguous()) if distributed else hist
         cum = torch.cumsum(h, dim=2)
         sel = torch.clamp(torch.searchsorted(cum, kk[..., None]).squeeze(-1), max=255)
         before = torch.where(sel > 0, cum.gather(2, torch.clamp(sel - 1, min=0)[..., None]).squeeze(-1),
@@ -146,6 +155,14 @@ def kth_smallest_device(X: torch.Tensor, ks: torch.Tensor, distributed: bool = F
 
 def column_quantiles(X: torch.Tensor, ps: Sequence[float], rel_err: float, distributed: bool = False) -> torch.Tensor:
     """[len(ps), d] quantiles of every column (NaNs ignored), exact and rank-local."""
+    if X.device.type == "cuda" and 0 < len(ps) <= _MAXQ and X.dim() == 2 and X.shape[1] > 0:
+        # the non-NaN counts come from the select's first (top-digit) histogram
+        def ranks_of(counts):
+            if bool((counts == 0).any()):
+                raise RuntimeError("Cannot query percentiles without any records inserted.")
+            return torch.stack(quantile_ranks(counts, ps, rel_err))
+
+        return kth_smallest_device(X, ranks_of, distributed, nq=len(ps)).to(torch.float64)
     valid = ~torch.isnan(X)
     counts = valid.sum(0).to(torch.int64)
     if distributed:

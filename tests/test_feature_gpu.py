@@ -164,6 +164,10 @@ def test_radix_hist_kernel_multi_quantile(dtype, d):
     dev = column_quantiles(X.cuda(), ps, 0.001).cpu()
     host = column_quantiles(X, ps, 0.001)
     assert torch.equal(dev, host)
+    Xn = X.clone()
+    Xn[:, 0] = float("nan")  # (the counts come from the select's first histogram on the device)
+    with pytest.raises(RuntimeError, match="without any records"):
+        column_quantiles(Xn.cuda(), ps, 0.001)
 
 
 @pytest.mark.parametrize("handle", ["keep", "skip", "error"])
