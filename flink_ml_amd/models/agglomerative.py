@@ -42,7 +42,28 @@ native.register_host_sigs({"fmlx_nnchain": ([ctypes.c_void_p, ctypes.c_int64, ct
 
 native.register_kernel_sigs({"fmlx_pairwise_euclid_f64": [ctypes.c_void_p, ctypes.c_long, ctypes.c_int,
                                                              ctypes.c_long, ctypes.c_void_p, ctypes.c_long,
-                                                             ctypes.c_void_p]})
+                                                             ctypes.c_int, ctypes.c_void_p]})
+
+
+def _euclid_device(X: torch.Tensor, condensed: bool) -> torch.Tensor:
+    X = X.contiguous()
+    n, d = X.shape
+    out = torch.empty(n * (n - 1) // 2 if condensed else (n, n), dtype=torch.float64, device=X.device)
+    if out.numel():
+        native.call("fmlx_pairwise_euclid_f64", native.ptr(X), n, d, max(d, 1), native.ptr(out), n, int(condensed),
+                    native.stream_ptr(X.device))
+    return out
+
+
+def condensed_distances(X: torch.Tensor, metric: str) -> np.ndarray:
+    """The upper triangle of the distance matrix, row by row (what the NN-chain core reads), on
+    the host. Euclidean on the GPU writes it directly (half the copy, no index pass)."""
+    X = X.to(torch.float64)
+    n = X.shape[0]
+    if metric == "euclidean" and X.device.type == "cuda" and 1 < n <= 16 * 65535:
+        return _euclid_device(X, True).cpu().numpy()
+    pair = pairwise_distances(X, metric).cpu().numpy()
+    return np.ascontiguousarray(pair[np.triu_indices(n, 1)], dtype=np.float64)
 
 
 def pairwise_distances(X: torch.Tensor, metric: str) -> torch.Tensor:
@@ -52,12 +73,7 @@ def pairwise_distances(X: torch.Tensor, metric: str) -> torch.Tensor:
     fit of a process."""
     X = X.to(torch.float64)
     if metric == "euclidean" and X.device.type == "cuda" and 0 < X.shape[0] <= 16 * 65535:
-        X = X.contiguous()
-        n, d = X.shape
-        out = torch.empty((n, n), dtype=torch.float64, device=X.device)
-        native.call("fmlx_pairwise_euclid_f64", native.ptr(X), n, d, max(d, 1), native.ptr(out), n,
-                    native.stream_ptr(X.device))
-        return out
+        return _euclid_device(X, False)
     if metric == "manhattan":
         return torch.cdist(X, X, p=1)
     sq = (X * X).sum(1)
@@ -71,8 +87,9 @@ def pairwise_distances(X: torch.Tensor, metric: str) -> torch.Tensor:
 
 
 def nn_chain(pair: np.ndarray, n: int, linkage: str):
-    """Merges (a, b, merged, dist) in discovery order and node sizes via the native core."""
-    cond = np.ascontiguousarray(pair[np.triu_indices(n, 1)], dtype=np.float64)
+    """Merges (a, b, merged, dist) in discovery order and node sizes via the native core. ``pair``
+    is the full [n, n] matrix or its condensed upper triangle."""
+    cond = np.ascontiguousarray(pair if pair.ndim == 1 else pair[np.triu_indices(n, 1)], dtype=np.float64)
     m = max(n - 1, 0)
     a = np.zeros(m, dtype=np.int64)
     b = np.zeros(m, dtype=np.int64)
@@ -133,7 +150,7 @@ class AgglomerativeClustering(AlgoOperator, AgglomerativeClusteringParams):
         dev = config.compute_device()
         X = c.to_dense(torch.float64, device=dev) if isinstance(c, SparseColumn) else \
             config.features_for_compute(t, self.get(self.FEATURES_COL), allow_sparse=False).to(dev, torch.float64)
-        pair = pairwise_distances(X, self.get(self.DISTANCE_MEASURE)).cpu().numpy()
+        pair = condensed_distances(X, self.get(self.DISTANCE_MEASURE))
         a, b, merged, dist, sizes = nn_chain(pair, n, self.get(self.LINKAGE))
         order = np.argsort(dist, kind="stable")
         chain = [[int(a[i]), int(b[i]), int(merged[i]), float(dist[i])] for i in order]

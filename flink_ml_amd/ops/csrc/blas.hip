@@ -662,7 +662,9 @@ FMLX_API int fmlx_preload_all(void* stream) {
 // elementwise passes.
 namespace {
 __global__ __launch_bounds__(256) void pairwise_euclid_f64_kernel(const double* __restrict__ X, long n, int d,
-                                                                  long ldx, double* __restrict__ out, long ldo) {
+                                                                  long ldx, double* __restrict__ out, long ldo,
+                                                                  int condensed) {
+  if (condensed && (long)blockIdx.x * 16 + 15 <= (long)blockIdx.y * 16) return;  // tile below the diagonal
   __shared__ double As[16][17];
   __shared__ double Bs[16][17];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
@@ -684,16 +686,23 @@ __global__ __launch_bounds__(256) void pairwise_euclid_f64_kernel(const double* 
     __syncthreads();
   }
   const long i = i0 + ty, j = j0 + tx;
-  if (i < n && j < n) out[i * ldo + j] = sqrt(fmax(0.0, si + sj - 2.0 * dot));
+  if (i >= n || j >= n) return;
+  const double v = sqrt(fmax(0.0, si + sj - 2.0 * dot));
+  if (!condensed)
+    out[i * ldo + j] = v;
+  else if (i < j)  // row-major upper triangle without the diagonal (scipy's condensed order)
+    out[i * n - i * (i + 1) / 2 + (j - i - 1)] = v;
 }
 }  // namespace
 
-FMLX_API int fmlx_pairwise_euclid_f64(const double* X, long n, int d, long ldx, double* out, long ldo, void* stream) {
+// condensed != 0: out holds n(n−1)/2 entries, the upper triangle row by row (ldo ignored)
+FMLX_API int fmlx_pairwise_euclid_f64(const double* X, long n, int d, long ldx, double* out, long ldo, int condensed,
+                                      void* stream) {
   if (n <= 0) return 0;
-  if (X == nullptr || out == nullptr || d < 0 || ldx < d || ldo < n || (n + 15) / 16 > 65535) return -1;
+  if (X == nullptr || out == nullptr || d < 0 || ldx < d || (!condensed && ldo < n) || (n + 15) / 16 > 65535) return -1;
   const unsigned nb = (unsigned)((n + 15) / 16);
   hipLaunchKernelGGL(pairwise_euclid_f64_kernel, dim3(nb, nb), dim3(256), 0, (hipStream_t)stream, X, n, d, ldx, out,
-                     ldo);
+                     ldo, condensed);
   return (int)hipGetLastError();
 }
 

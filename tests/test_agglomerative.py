@@ -121,7 +121,7 @@ def test_pairwise_euclid_kernel_matches_torch():
     diagonal, tile edges (n not a multiple of 16, d not a multiple of 16)."""
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
-    from flink_ml_amd.models.agglomerative import pairwise_distances
+    from flink_ml_amd.models.agglomerative import condensed_distances, pairwise_distances
 
     g = torch.Generator().manual_seed(4)
     for n, d in ((1, 3), (17, 5), (1000, 100), (333, 37)):
@@ -134,6 +134,8 @@ def test_pairwise_euclid_kernel_matches_torch():
         off = ~torch.eye(n, dtype=torch.bool)
         torch.testing.assert_close(D[off], ref[off], rtol=1e-12, atol=1e-9)
         assert torch.equal(D, D.t()) and bool((torch.diagonal(D) == 0).all())
+        cond = condensed_distances(X.cuda(), "euclidean")  # the kernel's condensed mode
+        np.testing.assert_array_equal(cond, D.numpy()[np.triu_indices(n, 1)])
 
 
 @pytest.mark.gpu
