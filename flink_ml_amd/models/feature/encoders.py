@@ -579,7 +579,16 @@ class VectorIndexer(Estimator, VectorIndexerParams):
         # more local distinct values already rules it out (agreed by one all-reduce)
         stats = torch.zeros(d + 2, dtype=torch.float64)
         stats[d], stats[d + 1] = float(n), float(d)
-        if n:
+        bounded = None
+        if n and X.is_cuda and d:
+            # how many distinct values, up to maxCategories + 1: an early-exit hash-set pass
+            # (catstats.hip small_distinct_kernel) instead of sorting every column
+            from ...ops import catstats
+
+            bounded = catstats.bounded_distinct_counts(X, max_cat)
+            if bounded is not None:
+                stats[:d] = torch.from_numpy(bounded.astype(np.float64))
+        if n and bounded is None:
             S, _ = torch.sort(X, dim=0)
             stats[:d] = (1 + (S[1:] != S[:-1]).sum(0)).to(torch.float64).cpu()
         if dist:

@@ -27,6 +27,8 @@ native.register_kernel_sigs({
     "fmlx_cs_distinct": [c_void_p, c_void_p, c_long, c_int, c_int, c_void_p, c_long, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p],
     "fmlx_cs_chist": [c_void_p, c_long, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
+    "fmlx_cs_small_distinct": [c_void_p, c_long, c_long, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                               c_void_p],
 })
 
 # integer tables up to this many cells are counted directly (value range × labels × features)
@@ -59,6 +61,34 @@ def flags(X: torch.Tensor) -> Tuple[float, float, bool]:
                 native.ptr(out), native.stream_ptr(dev))
     mn, mx, non = out.cpu().tolist()
     return mn, mx, non != 0.0
+
+
+SMALL_DISTINCT_TABLE_MAX = 2048  # LDS hash-set slots (csrc/catstats.hip small_distinct_kernel)
+
+
+def bounded_distinct_counts(X: torch.Tensor, cap: int):
+    """Per column of a device fp64 matrix: the number of distinct values (NaN one value, −0 == +0)
+    when it is at most ``cap``, else cap + 1 — one early-exit hash-set pass (a continuous column
+    stops after a few hundred rows). None when cap is too large for the LDS table."""
+    X = _mat(X)
+    if X.dtype != torch.float64:
+        X = X.to(torch.float64)
+    if X.stride(1) != 1:
+        X = X.contiguous()
+    n, d = X.shape
+    S = 1
+    while S < 2 * cap + 256:
+        S <<= 1
+    if cap < 1 or S > SMALL_DISTINCT_TABLE_MAX or d > 65535:
+        return None
+    dev = X.device
+    gtab = torch.full((d * S,), -1, dtype=torch.int64, device=dev)
+    ints = torch.zeros(2 * d, dtype=torch.int32, device=dev)  # counts | overflow flags
+    if n and d:
+        native.call("fmlx_cs_small_distinct", native.ptr(X), X.stride(0), n, d, int(cap), S, native.ptr(gtab),
+                    native.ptr(ints), native.ptr(ints[d:]), native.stream_ptr(dev))
+    h = ints.cpu().numpy()
+    return np.where(h[d:] != 0, cap + 1, h[:d]).astype(np.int64)
 
 
 def int_hist(v: torch.Tensor, lo: int, R: int) -> torch.Tensor:

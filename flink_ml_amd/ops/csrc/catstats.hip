@@ -563,4 +563,102 @@ FMLX_API int fmlx_cs_chist(const int* codes, long n, int nc, const long* coloff,
   return (int)hipGetLastError();
 }
 
+// ---- bounded distinct counts per column (VectorIndexer.java:96-106: a column is categorical when
+// it holds at most maxCategories distinct values). Only "how many, up to cap" is needed: per
+// (row chunk, column) block an LDS hash set of 64-bit keys (NaN canonical, −0 folded into +0 — the
+// keys of the later keyed distinct), merged into one global set per column; a column whose count
+// passes cap raises its flag and every block drops it at the next check, so a continuous column
+// costs a few hundred rows instead of a full sort. Probing is bounded by the table size.
+namespace {
+constexpr unsigned long long SD_EMPTY = ~0ull;  // a NaN payload the key canonicalisation never yields
+constexpr int SD_MAXCAP = 1024;
+__device__ __forceinline__ unsigned long long sd_key(double v) {
+  if (v != v) return 0x7ff8000000000000ull;
+  return (unsigned long long)__double_as_longlong(v + 0.0);
+}
+__device__ __forceinline__ unsigned sd_hash(unsigned long long k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  return (unsigned)k;
+}
+// 0 = present already, 1 = inserted, 2 = table full
+__device__ __forceinline__ int sd_insert(unsigned long long* tab, int S, unsigned long long k) {
+  unsigned h = sd_hash(k) & (unsigned)(S - 1);
+  for (int t = 0; t < S; ++t) {
+    const unsigned long long old = atomicCAS(&tab[h], SD_EMPTY, k);
+    if (old == SD_EMPTY) return 1;
+    if (old == k) return 0;
+    h = (h + 1) & (unsigned)(S - 1);
+  }
+  return 2;
+}
+__global__ __launch_bounds__(256) void small_distinct_kernel(const double* __restrict__ X, long ld, long n, int d,
+                                                             long rows_per_block, int cap, int S,
+                                                             unsigned long long* __restrict__ gtab,
+                                                             int* __restrict__ gcnt, int* __restrict__ over) {
+  __shared__ unsigned long long tab[2 * SD_MAXCAP + 512];
+  __shared__ int cnt, stop;
+  const int c = blockIdx.y;
+  for (int i = threadIdx.x; i < S; i += blockDim.x) tab[i] = SD_EMPTY;
+  if (threadIdx.x == 0) {
+    cnt = 0;
+    stop = 0;
+  }
+  __syncthreads();
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  const long r1 = r0 + rows_per_block < n ? r0 + rows_per_block : n;
+  volatile int* vover = over;
+  volatile int* vstop = &stop;
+  for (long base = r0; base < r1; base += 256 * 16) {
+    if (threadIdx.x == 0 && vover[c]) stop = 1;
+    __syncthreads();
+    if (stop) break;
+    for (int u = 0; u < 16; ++u) {
+      if (*vstop) break;  // (no inserts past the overflow: a full table would cost S probes each)
+      const long r = base + (long)u * 256 + threadIdx.x;
+      if (r < r1) {
+        const int res = sd_insert(tab, S, sd_key(X[r * ld + c]));
+        if (res == 2 || (res == 1 && atomicAdd(&cnt, 1) + 1 > cap)) {
+          stop = 1;
+          atomicOr(&over[c], 1);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  if (stop || vover[c]) return;
+  // merge into the column's global set
+  unsigned long long* gt = gtab + (long)c * S;
+  for (int i = threadIdx.x; i < S; i += blockDim.x) {
+    const unsigned long long k = tab[i];
+    if (k == SD_EMPTY) continue;
+    const int res = sd_insert(gt, S, k);
+    if (res == 2 || (res == 1 && atomicAdd(&gcnt[c], 1) + 1 > cap)) atomicOr(&over[c], 1);
+  }
+}
+}  // namespace
+
+FMLX_API int fmlx_cs_small_distinct_maxcap() { return SD_MAXCAP; }
+
+// X f64 [n, d] (row stride ld); cap <= 1024. gtab u64 [d][S] filled with ~0, gcnt / over int [d]
+// zeroed by the caller, S = the power of two >= 2·cap + 256 (passed in, checked). Afterwards a
+// column holds gcnt distinct values, or more than cap if over != 0.
+FMLX_API int fmlx_cs_small_distinct(const double* X, long ld, long n, int d, int cap, int S, unsigned long long* gtab,
+                                    int* gcnt, int* over, void* stream) {
+  if (n <= 0 || d <= 0) return 0;
+  if (X == nullptr || cap < 1 || cap > SD_MAXCAP || S < 2 * cap + 256 || S > 2 * SD_MAXCAP + 512 || (S & (S - 1)) ||
+      d > 65535 || gtab == nullptr || gcnt == nullptr || over == nullptr)
+    return -1;
+  long want = 2048 / d + 1;
+  long chunks = (n + 4095) / 4096;
+  if (chunks > want) chunks = want;
+  const long rpb = (n + chunks - 1) / chunks;
+  chunks = (n + rpb - 1) / rpb;
+  hipLaunchKernelGGL(small_distinct_kernel, dim3((unsigned)chunks, (unsigned)d), dim3(256), 0, (hipStream_t)stream, X,
+                     ld, n, d, rpb, cap, S, gtab, gcnt, over);
+  return (int)hipGetLastError();
+}
+
 FMLX_DEFINE_PRELOAD()

@@ -300,3 +300,29 @@ def test_ngram_presence_kernels_match_sort_path(n):
     assert torch.equal(got.offsets.cpu(), ref.offsets.cpu())
     assert torch.equal(got.codes.cpu().long(), ref.codes.cpu().long())
     assert [list(r) for r in got][:50] == [list(r) for r in ref][:50]
+
+
+def test_bounded_distinct_counts_kernel():
+    """csrc/catstats.hip small_distinct_kernel: exact counts up to cap (merged over many row
+    chunks), cap + 1 beyond it (early exit), NaN one value and −0 == +0; VectorIndexer on the GPU
+    picks the same categorical columns and maps as on the CPU."""
+    from flink_ml_amd.models import VectorIndexer
+    from flink_ml_amd.ops import catstats
+
+    rng = np.random.default_rng(12)
+    n, cap = 300_000, 20
+    cols = [rng.integers(0, 5, n), rng.integers(0, cap, n), rng.integers(0, cap + 1, n), rng.normal(size=n),
+            rng.integers(0, 3, n).astype(np.float64)]
+    X = np.stack([np.asarray(c, dtype=np.float64) for c in cols], 1)
+    X[::7, 4] = np.nan
+    X[::5, 0] = -0.0  # -0 == +0 (0 is among the values)
+    got = catstats.bounded_distinct_counts(torch.from_numpy(X).cuda(), cap)
+    assert got.tolist() == [5, 20, 21, 21, 4]
+    Xc = X[:, :3]
+    t_cpu = Table({"input": torch.from_numpy(Xc)}, num_rows=n)
+    t_gpu = Table({"input": torch.from_numpy(Xc).cuda()}, num_rows=n)
+    vi = VectorIndexer().set_max_categories(cap)
+    m_cpu = vi.fit(t_cpu).get_model_data()[0]
+    m_gpu = vi.fit(t_gpu).get_model_data()[0]
+    name = m_cpu.column_names[0]
+    assert m_cpu.get_list(name) == m_gpu.get_list(name)
