@@ -205,8 +205,16 @@ def _string_counts_table(t: Table, col: str):
         except TypeError:
             raise RuntimeError("The input column only supports string and numeric type.") from None
         # counts and first occurrences per vocabulary entry by code on the device
-        codes = c.codes.to(config.compute_device()).long()
         V = len(c.vocab)
+        from ...ops import catstats
+
+        got = catstats.code_counts_first(c.codes.to(config.compute_device()), V)
+        if got is not None:  # one kernel pass; the [V] results ordered on the host
+            cnt_h, first_h = got
+            present = np.nonzero(cnt_h > 0)[0]
+            present = present[np.argsort(first_h[present], kind="stable")]
+            return tab.take(present), cnt_h[present], first_h[present]
+        codes = c.codes.to(config.compute_device()).long()
         cnt = torch.bincount(codes, minlength=V)
         first = first_occurrence(codes, V)
         present = torch.nonzero(cnt > 0).reshape(-1)

@@ -63,6 +63,35 @@ def flags(X: torch.Tensor) -> Tuple[float, float, bool]:
     return mn, mx, non != 0.0
 
 
+native.register_kernel_sigs({
+    "fmlx_cv_tfdf": [c_void_p, c_void_p, c_long, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+})
+CODE_COUNTS_MAX_V = 4096  # dictionary sizes of the one-pass count kernel (csrc/hash.hip cv_tfdf_kernel)
+CODE_COUNTS_SEG = 4096  # codes per pseudo-document (the kernel's unit of work per wave)
+
+
+def code_counts_first(codes: torch.Tensor, V: int):
+    """(count, first position) per dictionary code in [0, V) of a device int32 code column, host
+    int64 arrays, in one pass of the CountVectorizer tf kernel over fixed-size segments (the
+    column cut into pseudo-documents; their document frequencies are not used). None when V is
+    beyond the kernel's LDS tables."""
+    n = codes.shape[0]
+    if not codes.is_cuda or V < 1 or V > CODE_COUNTS_MAX_V or n >= (1 << 32):
+        return None
+    dev = codes.device
+    codes = codes.to(torch.int32).contiguous()
+    seg = CODE_COUNTS_SEG
+    nd = max(1, -(-n // seg))
+    off = torch.from_numpy(np.minimum(np.arange(nd + 1, dtype=np.int64) * seg, n)).to(dev)
+    out = torch.zeros(3 * V, dtype=torch.int64, device=dev)  # count | (unused) | first
+    out[2 * V:] = n
+    if n:
+        native.call("fmlx_cv_tfdf", native.ptr(codes), native.ptr(off), nd, V, native.ptr(out), native.ptr(out[V:]),
+                    native.ptr(out[2 * V:]), native.stream_ptr(dev))
+    h = out.cpu().numpy().reshape(3, V)
+    return h[0], h[2]
+
+
 SMALL_DISTINCT_TABLE_MAX = 2048  # LDS hash-set slots (csrc/catstats.hip small_distinct_kernel)
 
 

@@ -326,3 +326,28 @@ def test_bounded_distinct_counts_kernel():
     m_gpu = vi.fit(t_gpu).get_model_data()[0]
     name = m_cpu.column_names[0]
     assert m_cpu.get_list(name) == m_gpu.get_list(name)
+
+
+@pytest.mark.parametrize("order", ["arbitrary", "frequencyDesc", "alphabetAsc"])
+def test_string_indexer_code_counts_kernel(order):
+    """StringIndexer on a device dictionary column (counts and first positions from the one-pass
+    code-count kernel over pseudo-documents) against the same strings as a host list column;
+    unused dictionary entries, a column longer than one segment."""
+    from flink_ml_amd.models import StringIndexer
+    from flink_ml_amd.ops import catstats
+    from flink_ml_amd.table import StringColumn
+
+    rng = np.random.default_rng(4)
+    vocab = ["s%02d" % i for i in range(60)]
+    codes = np.minimum(rng.zipf(1.5, 50_000) - 1, 49).astype(np.int32)  # entries 50..59 unused
+    cnt, first = catstats.code_counts_first(torch.from_numpy(codes).cuda(), len(vocab))
+    np.testing.assert_array_equal(cnt, np.bincount(codes, minlength=len(vocab)))
+    ref_first = np.full(len(vocab), len(codes))
+    for p in range(len(codes) - 1, -1, -1):
+        ref_first[codes[p]] = p
+    np.testing.assert_array_equal(first, ref_first)
+    si = StringIndexer().set_input_cols("s").set_output_cols("o").set_string_order_type(order)
+    dev = si.fit(Table({"s": StringColumn(torch.from_numpy(codes).cuda(), vocab)}, num_rows=len(codes)))
+    host = si.fit(Table({"s": [vocab[c] for c in codes]}, num_rows=len(codes)))
+    a, b = dev.get_model_data()[0], host.get_model_data()[0]
+    assert a.get_list(a.column_names[0]) == b.get_list(b.column_names[0])
