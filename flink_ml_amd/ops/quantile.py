@@ -129,28 +129,34 @@ def kth_smallest_device(X: torch.Tensor, ks, distributed: bool = False, nq: int 
     part = torch.empty(chunks * Q * d * 256, dtype=torch.int32, device=dev)
     hist = torch.empty((Q, d, 256), dtype=torch.int64, device=dev)
     prefix = torch.zeros((Q, d), dtype=torch.int64, device=dev)
-    kk = None if rank_fn is not None else ks.to(device=dev, dtype=torch.int64).clone()
+    # the per-pass digit choice runs on the host over the small [Q, d, 256] histogram (integer
+    # exact; on the device its cumsum / searchsorted / gather kernels would each load a torch code
+    # object at first use): one histogram copy down and one prefix copy up per pass
+    prefix_h = torch.zeros((Q, d), dtype=torch.int64)
+    kk = None if rank_fn is not None else ks.to(device="cpu", dtype=torch.int64).clone()
     for i, shift in enumerate(range(nbits - 8, -1, -8)):
         # the top digit's histogram is the same for every rank target: count it once
         q_eff = 1 if i == 0 else Q
+        if i:
+            prefix.copy_(prefix_h)
         native.call("fmlx_radix_hist", native.dtype_code(X.dtype), native.ptr(X), X.stride(0), n, d,
                     native.ptr(prefix), q_eff, shift, int(i == 0), chunks, native.ptr(part), native.ptr(hist),
                     native.stream_ptr(dev))
         if i == 0:
-            h = comm.all_reduce_sum(hist[:1].contiguous()) if distributed else hist[:1]
+            h = (comm.all_reduce_sum(hist[:1].contiguous()) if distributed else hist[:1]).cpu()
             if rank_fn is not None:
-                kk = rank_fn(h[0].sum(-1)).to(device=dev, dtype=torch.int64).clone()
+                kk = rank_fn(h[0].sum(-1)).to(device="cpu", dtype=torch.int64).clone()
                 assert kk.shape == (Q, d)
             h = h.expand(Q, d, 256)
         else:
-            h = comm.all_reduce_sum(hist.contiguous()) if distributed else hist
+            h = (comm.all_reduce_sum(hist.contiguous()) if distributed else hist).cpu()
         cum = torch.cumsum(h, dim=2)
         sel = torch.clamp(torch.searchsorted(cum, kk[..., None]).squeeze(-1), max=255)
         before = torch.where(sel > 0, cum.gather(2, torch.clamp(sel - 1, min=0)[..., None]).squeeze(-1),
                              torch.zeros_like(kk))
         kk = kk - before
-        prefix = (prefix << 8) | sel
-    return _unsigned_to_value(prefix, nbits)
+        prefix_h = (prefix_h << 8) | sel
+    return _unsigned_to_value(prefix_h, nbits).to(dev)
 
 
 def column_quantiles(X: torch.Tensor, ps: Sequence[float], rel_err: float, distributed: bool = False) -> torch.Tensor:
