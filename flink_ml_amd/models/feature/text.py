@@ -419,7 +419,8 @@ def _ngram_device(dc, n: int, V: int) -> StringArrayColumn:
     if total:
         native.call("fmlx_ngram_codes", native.ptr(codes), native.ptr(off), nd, n, V, 1, None, None, native.ptr(rank),
                     native.ptr(noff), native.ptr(out), stream)
-    u = torch.nonzero(present).view(-1).cpu().numpy()
+    # (a small table is read back whole: cheaper than a device nonzero, and no torch kernel to load)
+    u = np.nonzero(present.cpu().numpy())[0] if G <= (1 << 22) else torch.nonzero(present).view(-1).cpu().numpy()
     digits = []
     for _ in range(n):
         digits.append(u % V)
