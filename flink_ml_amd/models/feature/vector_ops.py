@@ -66,6 +66,14 @@ class Binarizer(Transformer, HasInputCols, HasOutputCols):
         return [t.with_columns(res)]
 
 
+def _no_nan_device(x: torch.Tensor) -> bool:
+    """No NaN in a device column: the valid count of the masked-sum kernel (csrc/colstats.hip)
+    equals the length — one pass, no torch isnan / any kernels."""
+    from .encoders import _valid_sum_count
+
+    return int(_valid_sum_count(x.to(torch.float64), float("nan"))[1]) == x.shape[0]
+
+
 # ------------------------------------------------------------------------------------ Bucketizer
 native.register_kernel_sigs({"fmlx_bucketize": [native.c_void_p, native.c_long, native.c_void_p, native.c_int,
                                                  native.c_int, native.c_void_p, native.c_void_p, native.c_void_p,
@@ -295,6 +303,7 @@ class VectorAssembler(Transformer, HasInputCols, HasOutputCol, HasHandleInvalid)
         fast = all(isinstance(t.column(c), torch.Tensor) for c in cols)
         if fast:
             parts, ok = [], torch.ones(t.num_rows, dtype=torch.bool, device=t.column(cols[0]).device)
+            filtered = False
             for c, sz in zip(cols, sizes):
                 col = t.column(c).to(torch.float64)
                 col = col[:, None] if col.dim() == 1 else col
@@ -304,9 +313,11 @@ class VectorAssembler(Transformer, HasInputCols, HasOutputCol, HasHandleInvalid)
                                            "not meet with expected. Expected size: %d, actual size: %d."
                                            % (sz, col.shape[1]))
                     ok &= False  # skip: every row of a fixed-width column has the wrong size
-                if col.shape[1] == 1 and not keep:
+                    filtered = True
+                if col.shape[1] == 1 and not keep and not (col.is_cuda and _no_nan_device(col[:, 0])):
                     nan = torch.isnan(col[:, 0])
                     if bool(nan.any()):
+                        filtered = True
                         if hi == self.ERROR_INVALID:
                             raise RuntimeError("Vector assembler failed with exception : Encountered NaN while "
                                                "assembling a row with handleInvalid = 'error'.")
@@ -314,7 +325,7 @@ class VectorAssembler(Transformer, HasInputCols, HasOutputCol, HasHandleInvalid)
                 parts.append(col)
             out = torch.cat(parts, dim=1)
             res = t.with_column(self.get(self.OUTPUT_COL), out)
-            return [res if bool(ok.all()) else res.filter(ok.cpu())]
+            return [res if not filtered or bool(ok.all()) else res.filter(ok.cpu())]
         lists = [t.get_list(c) for c in cols]
         outs, keep_rows = [], []
         for r in range(t.num_rows):

@@ -351,3 +351,28 @@ def test_string_indexer_code_counts_kernel(order):
     host = si.fit(Table({"s": [vocab[c] for c in codes]}, num_rows=len(codes)))
     a, b = dev.get_model_data()[0], host.get_model_data()[0]
     assert a.get_list(a.column_names[0]) == b.get_list(b.column_names[0])
+
+
+@pytest.mark.parametrize("handle", ["skip", "error", "keep"])
+def test_vector_assembler_device_nan_check(handle):
+    """VectorAssembler on device columns: the NaN check through the masked-sum kernel (no NaN:
+    nothing filtered) and the torch mask path when a NaN is present, as on the CPU."""
+    from flink_ml_amd.models import VectorAssembler
+
+    rng = np.random.default_rng(9)
+    a, b = rng.normal(size=1000), rng.normal(size=(1000, 3))
+    va = VectorAssembler().set_input_cols("a", "b").set_output_col("o").set_input_sizes(1, 3) \
+        .set_handle_invalid(handle)
+    for with_nan in (False, True):
+        a2 = a.copy()
+        if with_nan:
+            a2[17] = np.nan
+        tg = Table({"a": torch.from_numpy(a2).cuda(), "b": torch.from_numpy(b).cuda()}, num_rows=1000)
+        tc = Table({"a": torch.from_numpy(a2), "b": torch.from_numpy(b)}, num_rows=1000)
+        if with_nan and handle == "error":
+            with pytest.raises(RuntimeError, match="NaN"):
+                va.transform(tg)
+            continue
+        g, c = va.transform(tg)[0], va.transform(tc)[0]
+        assert g.num_rows == c.num_rows == (999 if with_nan and handle == "skip" else 1000)
+        torch.testing.assert_close(g.column("o").cpu(), c.column("o").cpu(), rtol=0, atol=0, equal_nan=True)
